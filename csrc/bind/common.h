@@ -1,0 +1,21 @@
+// Shared helpers for the torch-facing binding TUs.
+#pragma once
+#include <c10/hip/HIPStream.h>
+#include <pybind11/numpy.h>
+#include <pybind11/stl.h>
+#include <torch/extension.h>
+
+namespace py = pybind11;
+
+#define IA_CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define IA_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define IA_CHECK_F32(t) TORCH_CHECK((t).scalar_type() == torch::kFloat32, #t " must be float32")
+#define IA_CHECK_GPU_F32(t) \
+  IA_CHECK_CUDA(t);         \
+  IA_CHECK_CONTIG(t);       \
+  IA_CHECK_F32(t)
+
+inline hipStream_t ia_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void register_envs(py::module& m);
+void register_kernels(py::module& m);

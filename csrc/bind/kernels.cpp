@@ -1,0 +1,95 @@
+// Torch-facing wrappers for the HIP kernels (tensor checks -> raw pointers).
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+#define IA_HIP_CHECK(expr)                                                            \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    TORCH_CHECK(_e == hipSuccess, "HIP error in " #expr ": ", hipGetErrorString(_e)); \
+  } while (0)
+
+ia::MLPDesc make_desc(const std::vector<torch::Tensor>& Ws, const std::vector<torch::Tensor>& bs, int64_t hidden_act,
+                      int64_t out_act, const c10::optional<torch::Tensor>& mean, const c10::optional<torch::Tensor>& var,
+                      double eps, double clip) {
+  TORCH_CHECK(!Ws.empty() && Ws.size() <= (size_t)ia::kMaxLayers, "1..4 layers supported");
+  TORCH_CHECK(Ws.size() == bs.size(), "one bias per weight");
+  ia::MLPDesc d{};
+  d.n_layers = (int)Ws.size();
+  d.hidden_act = (int)hidden_act;
+  d.out_act = (int)out_act;
+  d.dims[0] = (int)Ws[0].size(1);
+  for (size_t l = 0; l < Ws.size(); ++l) {
+    IA_CHECK_GPU_F32(Ws[l]);
+    IA_CHECK_GPU_F32(bs[l]);
+    TORCH_CHECK(Ws[l].dim() == 2 && Ws[l].size(1) == d.dims[l], "layer ", l, " input dim mismatch");
+    TORCH_CHECK(bs[l].numel() == Ws[l].size(0), "bias size mismatch");
+    d.dims[l + 1] = (int)Ws[l].size(0);
+    d.W[l] = Ws[l].data_ptr<float>();
+    d.b[l] = bs[l].data_ptr<float>();
+  }
+  for (int l = 0; l <= d.n_layers; ++l) TORCH_CHECK(d.dims[l] <= ia::kMaxDim, "tmlp width limit is 128");
+  if (mean.has_value() && mean->defined()) {
+    IA_CHECK_GPU_F32(*mean);
+    IA_CHECK_GPU_F32(*var);
+    TORCH_CHECK(mean->numel() == d.dims[0] && var->numel() == d.dims[0], "norm stats size mismatch");
+    d.norm_mean = mean->data_ptr<float>();
+    d.norm_var = var->data_ptr<float>();
+  }
+  d.norm_eps = (float)eps;
+  d.norm_clip = (float)clip;
+  return d;
+}
+
+torch::Tensor tmlp_forward(torch::Tensor x, std::vector<torch::Tensor> Ws, std::vector<torch::Tensor> bs,
+                           int64_t hidden_act, int64_t out_act, c10::optional<torch::Tensor> mean,
+                           c10::optional<torch::Tensor> var, double eps, double clip) {
+  IA_CHECK_GPU_F32(x);
+  TORCH_CHECK(x.dim() == 2, "x must be [B, D]");
+  auto d = make_desc(Ws, bs, hidden_act, out_act, mean, var, eps, clip);
+  TORCH_CHECK(x.size(1) == d.dims[0], "input dim mismatch");
+  auto y = torch::empty({x.size(0), d.dims[d.n_layers]}, x.options());
+  IA_HIP_CHECK(ia::tmlp_forward(d, x.data_ptr<float>(), (int)x.size(0), y.data_ptr<float>(), ia_stream()));
+  return y;
+}
+
+// Returns (dx or None, [dW...], [db...]).
+py::tuple tmlp_backward(torch::Tensor x, torch::Tensor dy, std::vector<torch::Tensor> Ws, std::vector<torch::Tensor> bs,
+                        int64_t hidden_act, int64_t out_act, c10::optional<torch::Tensor> mean,
+                        c10::optional<torch::Tensor> var, double eps, double clip, bool need_dx) {
+  IA_CHECK_GPU_F32(x);
+  IA_CHECK_GPU_F32(dy);
+  auto d = make_desc(Ws, bs, hidden_act, out_act, mean, var, eps, clip);
+  const int B = (int)x.size(0);
+  TORCH_CHECK(dy.size(0) == B && dy.size(1) == d.dims[d.n_layers], "dy shape mismatch");
+  ia::MLPGrads g{};
+  std::vector<torch::Tensor> dWs, dbs;
+  for (int l = 0; l < d.n_layers; ++l) {
+    dWs.push_back(torch::empty_like(Ws[l]));
+    dbs.push_back(torch::empty_like(bs[l]));
+    g.dW[l] = dWs.back().data_ptr<float>();
+    g.db[l] = dbs.back().data_ptr<float>();
+  }
+  g.accumulate = 0;
+  torch::Tensor dx;
+  if (need_dx) dx = torch::empty_like(x);
+  const size_t slab_n = ia::tmlp_slab_floats(d, B);
+  torch::Tensor slab;
+  if (slab_n) slab = torch::empty({(int64_t)slab_n}, x.options());
+  IA_HIP_CHECK(ia::tmlp_backward(d, x.data_ptr<float>(), dy.data_ptr<float>(), B, need_dx ? dx.data_ptr<float>() : nullptr,
+                                 g, slab_n ? slab.data_ptr<float>() : nullptr, ia_stream()));
+  py::object dxo = need_dx ? py::cast(dx) : py::none();
+  return py::make_tuple(dxo, dWs, dbs);
+}
+
+}  // namespace
+
+void register_kernels(py::module& m) {
+  m.def("tmlp_forward", &tmlp_forward, py::arg("x"), py::arg("weights"), py::arg("biases"), py::arg("hidden_act"),
+        py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
+        py::arg("norm_eps") = 1e-5, py::arg("norm_clip") = 0.0);
+  m.def("tmlp_backward", &tmlp_backward, py::arg("x"), py::arg("dy"), py::arg("weights"), py::arg("biases"),
+        py::arg("hidden_act"), py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
+        py::arg("norm_eps") = 1e-5, py::arg("norm_clip") = 0.0, py::arg("need_dx") = false);
+}

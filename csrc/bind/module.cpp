@@ -1,0 +1,9 @@
+// imitation_amd._C — module definition.
+#include "common.h"
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "imitation_amd native runtime + HIP/CDNA4 kernels (gfx950)";
+  m.attr("arch") = "gfx950";
+  register_envs(m);
+  register_kernels(m);
+}

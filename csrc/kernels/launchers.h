@@ -1,0 +1,21 @@
+// Host launch entry points of every HIP kernel (raw pointers + stream only, so
+// that the torch-facing binding TUs never include device code and the kernel
+// TUs never include torch headers).  All launchers are graph-capture safe: no
+// allocation, no synchronisation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ia/tmlp.h"
+
+namespace ia {
+
+// ---- tmlp.hip: fused tiny-MLP
+int tmlp_waves_for(const MLPDesc& d);
+size_t tmlp_slab_floats(const MLPDesc& d, int B);
+hipError_t tmlp_forward(const MLPDesc& d, const float* X, int B, float* Y, hipStream_t s);
+hipError_t tmlp_backward(const MLPDesc& d, const float* X, const float* dY, int B, float* dX, const MLPGrads& g,
+                         float* slab, hipStream_t s);
+
+}  // namespace ia
