@@ -83,6 +83,25 @@ py::tuple tmlp_backward(torch::Tensor x, torch::Tensor dy, std::vector<torch::Te
   return py::make_tuple(dxo, dWs, dbs);
 }
 
+py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch::Tensor last_val, torch::Tensor dones,
+              double gamma, double lam) {
+  IA_CHECK_GPU_F32(rew);
+  IA_CHECK_GPU_F32(val);
+  IA_CHECK_GPU_F32(starts);
+  IA_CHECK_GPU_F32(last_val);
+  IA_CHECK_GPU_F32(dones);
+  TORCH_CHECK(rew.dim() == 2, "rewards must be [T, N]");
+  const int T = (int)rew.size(0), N = (int)rew.size(1);
+  TORCH_CHECK(val.sizes() == rew.sizes() && starts.sizes() == rew.sizes(), "shape mismatch");
+  TORCH_CHECK(last_val.numel() == N && dones.numel() == N, "bootstrap shape mismatch");
+  auto adv = torch::empty_like(rew);
+  auto ret = torch::empty_like(rew);
+  IA_HIP_CHECK(ia::gae_launch(rew.data_ptr<float>(), val.data_ptr<float>(), starts.data_ptr<float>(),
+                              last_val.data_ptr<float>(), dones.data_ptr<float>(), T, N, (float)gamma, (float)lam,
+                              adv.data_ptr<float>(), ret.data_ptr<float>(), ia_stream()));
+  return py::make_tuple(adv, ret);
+}
+
 }  // namespace
 
 void register_kernels(py::module& m) {
@@ -92,4 +111,6 @@ void register_kernels(py::module& m) {
   m.def("tmlp_backward", &tmlp_backward, py::arg("x"), py::arg("dy"), py::arg("weights"), py::arg("biases"),
         py::arg("hidden_act"), py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
         py::arg("norm_eps") = 1e-5, py::arg("norm_clip") = 0.0, py::arg("need_dx") = false);
+  m.def("gae", &gae, py::arg("rewards"), py::arg("values"), py::arg("episode_starts"), py::arg("last_values"),
+        py::arg("dones"), py::arg("gamma"), py::arg("lam"));
 }

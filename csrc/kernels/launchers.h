@@ -18,4 +18,8 @@ hipError_t tmlp_forward(const MLPDesc& d, const float* X, int B, float* Y, hipSt
 hipError_t tmlp_backward(const MLPDesc& d, const float* X, const float* dY, int B, float* dX, const MLPGrads& g,
                          float* slab, hipStream_t s);
 
+// ---- rl.hip: GAE scan over [T, N]
+hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
+                      int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);
+
 }  // namespace ia

@@ -495,6 +495,11 @@ class NativeVecEnv(VecEnv):
         seeds = super().seed(seed)
         return seeds
 
+    def seed_envs(self, seeds: Sequence[int]) -> None:
+        """Reseed env i with ``seeds[i]`` immediately (per-env non-sequential seeds)."""
+        assert len(seeds) == self.num_envs
+        self._impl.seed([int(s) for s in seeds])
+
     def reset(self):
         if any(s is not None for s in self._seeds):
             self._impl.seed([int(s) if s is not None else int(np.random.randint(0, 2**31 - 1)) for s in self._seeds])

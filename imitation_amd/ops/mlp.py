@@ -1,0 +1,161 @@
+"""Fused tiny-MLP op (``csrc/kernels/tmlp.hip``) with autograd.
+
+One launch evaluates a whole ``[norm] -> Linear -> act -> ... -> Linear -> out_act``
+stack for every row of the batch on MFMA (bf16 operands, fp32 accumulation);
+the backward launch recomputes the forward tile in LDS and emits dW/db (and
+dX when needed) with a deterministic block-order reduction.
+
+Replaces the per-layer PyTorch launches of ``build_mlp`` stacks used by the
+reference's reward nets and SB3 policy heads
+(``src/imitation/util/networks.py:204-283``, ``src/imitation/rewards/reward_nets.py:441-457``).
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+ACT_CODES = {"identity": 0, "relu": 1, "tanh": 2, "leaky_relu": 3, "sigmoid": 4}
+
+
+def act_code(module_or_name) -> Optional[int]:
+    """Activation code for a module / name, or None if the kernel cannot fuse it."""
+    import torch.nn as nn
+
+    if module_or_name is None:
+        return 0
+    if isinstance(module_or_name, str):
+        return ACT_CODES.get(module_or_name)
+    m = module_or_name
+    if isinstance(m, type):
+        try:
+            m = m()
+        except TypeError:
+            return None
+    if isinstance(m, nn.Identity):
+        return 0
+    if isinstance(m, nn.ReLU):
+        return 1
+    if isinstance(m, nn.Tanh):
+        return 2
+    if isinstance(m, nn.LeakyReLU) and abs(m.negative_slope - 0.01) < 1e-12:
+        return 3
+    if isinstance(m, nn.Sigmoid):
+        return 4
+    return None
+
+
+def _act(code: int, x: torch.Tensor) -> torch.Tensor:
+    if code == 1:
+        return F.relu(x)
+    if code == 2:
+        return torch.tanh(x)
+    if code == 3:
+        return F.leaky_relu(x, 0.01)
+    if code == 4:
+        return torch.sigmoid(x)
+    return x
+
+
+def tmlp_reference(
+    x: torch.Tensor,
+    weights: Sequence[torch.Tensor],
+    biases: Sequence[torch.Tensor],
+    hidden_act: int,
+    out_act: int = 0,
+    norm_mean: Optional[torch.Tensor] = None,
+    norm_var: Optional[torch.Tensor] = None,
+    norm_eps: float = 1e-5,
+) -> torch.Tensor:
+    """Plain PyTorch fp32 reference of the fused MLP (the kernel's numerics oracle)."""
+    h = x
+    if norm_mean is not None:
+        h = (h - norm_mean) / torch.sqrt(norm_var + norm_eps)
+    n = len(weights)
+    for i, (w, b) in enumerate(zip(weights, biases)):
+        h = F.linear(h, w, b)
+        h = _act(out_act if i == n - 1 else hidden_act, h)
+    return h
+
+
+class _TMLPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, hidden_act, out_act, mean, var, eps, *params):
+        from imitation_amd.ops import native
+
+        C = native()
+        ws: List[torch.Tensor] = [p.contiguous() for p in params[0::2]]
+        bs: List[torch.Tensor] = [p.contiguous() for p in params[1::2]]
+        xc = x.contiguous()
+        y = C.tmlp_forward(xc, ws, bs, int(hidden_act), int(out_act), mean, var, float(eps), 0.0)
+        ctx.hidden_act, ctx.out_act, ctx.eps = int(hidden_act), int(out_act), float(eps)
+        ctx.has_norm = mean is not None
+        ctx.n_layers = len(ws)
+        saved = [xc] + ws + bs
+        if mean is not None:
+            saved += [mean, var]
+        ctx.save_for_backward(*saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from imitation_amd.ops import native
+
+        C = native()
+        saved = ctx.saved_tensors
+        L = ctx.n_layers
+        x = saved[0]
+        ws = list(saved[1 : 1 + L])
+        bs = list(saved[1 + L : 1 + 2 * L])
+        mean = var = None
+        if ctx.has_norm:
+            mean, var = saved[1 + 2 * L], saved[2 + 2 * L]
+        need_dx = bool(ctx.needs_input_grad[0])
+        dx, dws, dbs = C.tmlp_backward(
+            x, dy.contiguous(), ws, bs, ctx.hidden_act, ctx.out_act, mean, var, ctx.eps, 0.0, need_dx
+        )
+        grads = []
+        for dw, db in zip(dws, dbs):
+            grads += [dw, db]
+        return (dx, None, None, None, None, None, *grads)
+
+
+def kernel_supports(dims: Sequence[int]) -> bool:
+    return 1 <= len(dims) - 1 <= 4 and max(dims) <= 128
+
+
+def tmlp(
+    x: torch.Tensor,
+    weights: Sequence[torch.Tensor],
+    biases: Sequence[torch.Tensor],
+    hidden_act: int,
+    out_act: int = 0,
+    norm_mean: Optional[torch.Tensor] = None,
+    norm_var: Optional[torch.Tensor] = None,
+    norm_eps: float = 1e-5,
+) -> torch.Tensor:
+    """Fused MLP forward (differentiable w.r.t. ``x`` and every weight / bias).
+
+    GPU fp32 tensors go through the HIP kernel; everything else through
+    :func:`tmlp_reference`.
+    """
+    from imitation_amd.ops import use_kernel
+
+    dims = [weights[0].shape[1]] + [w.shape[0] for w in weights]
+    if (
+        use_kernel(x)
+        and x.dtype == torch.float32
+        and x.dim() == 2
+        and kernel_supports(dims)
+        and all(w.dtype == torch.float32 for w in weights)
+    ):
+        if norm_mean is not None:
+            norm_mean = norm_mean.detach().float().contiguous()
+            norm_var = norm_var.detach().float().contiguous()
+        params = []
+        for w, b in zip(weights, biases):
+            params += [w, b]
+        return _TMLPFn.apply(x, hidden_act, out_act, norm_mean, norm_var, norm_eps, *params)
+    return tmlp_reference(x, weights, biases, hidden_act, out_act, norm_mean, norm_var, norm_eps)

@@ -1,0 +1,219 @@
+"""Device-resident RL buffers (SB3 ``buffers`` surface).
+
+* :class:`RolloutBuffer` -- on-policy storage ``[n_steps, n_envs, ...]`` kept on
+  the training device (SB3 keeps it in host numpy and re-uploads every
+  minibatch); GAE runs as one HIP kernel (``imitation_amd.ops.rl.gae``).
+* :class:`ReplayBuffer` -- off-policy ring buffer ``[capacity, n_envs, ...]`` on
+  the device with uniform with-replacement sampling by device-side index gather
+  (SURVEY §2.3 K23). Sized by bytes, it can use a large share of the 288 GB HBM.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, Generator, List, NamedTuple, Optional, Union
+
+import numpy as np
+import torch as th
+
+from imitation_amd.envs import spaces
+from imitation_amd.rl.preprocessing import get_action_dim, get_obs_shape
+
+
+class RolloutBufferSamples(NamedTuple):
+    observations: th.Tensor
+    actions: th.Tensor
+    old_values: th.Tensor
+    old_log_prob: th.Tensor
+    advantages: th.Tensor
+    returns: th.Tensor
+
+
+class ReplayBufferSamples(NamedTuple):
+    observations: th.Tensor
+    actions: th.Tensor
+    next_observations: th.Tensor
+    dones: th.Tensor
+    rewards: th.Tensor
+
+
+def _torch_dtype(space: spaces.Space):
+    if isinstance(space, spaces.Box):
+        return th.uint8 if space.dtype == np.uint8 else th.float32
+    if isinstance(space, (spaces.Discrete, spaces.MultiDiscrete)):
+        return th.int64
+    return th.float32
+
+
+def _to_t(x, device, dtype=None) -> th.Tensor:
+    if isinstance(x, th.Tensor):
+        return x.to(device=device, dtype=dtype if dtype is not None else x.dtype)
+    return th.as_tensor(np.asarray(x), device=device, dtype=dtype)
+
+
+class BaseBuffer:
+    def __init__(self, buffer_size: int, observation_space: spaces.Space, action_space: spaces.Space,
+                 device: Union[th.device, str] = "auto", n_envs: int = 1):
+        from imitation_amd.rl.policies import get_device
+
+        self.buffer_size = buffer_size
+        self.observation_space = observation_space
+        self.action_space = action_space
+        self.obs_shape = get_obs_shape(observation_space)
+        self.action_dim = get_action_dim(action_space)
+        self.pos = 0
+        self.full = False
+        self.device = get_device(device)
+        self.n_envs = n_envs
+
+    def size(self) -> int:
+        return self.buffer_size if self.full else self.pos
+
+    def reset(self) -> None:
+        self.pos = 0
+        self.full = False
+
+    def to_torch(self, array, copy: bool = True) -> th.Tensor:
+        if isinstance(array, th.Tensor):
+            return array.to(self.device)
+        return th.tensor(array, device=self.device) if copy else th.as_tensor(array, device=self.device)
+
+
+class RolloutBuffer(BaseBuffer):
+    def __init__(self, buffer_size: int, observation_space: spaces.Space, action_space: spaces.Space,
+                 device: Union[th.device, str] = "auto", gae_lambda: float = 1, gamma: float = 0.99, n_envs: int = 1):
+        super().__init__(buffer_size, observation_space, action_space, device, n_envs=n_envs)
+        self.gae_lambda = gae_lambda
+        self.gamma = gamma
+        self.generator_ready = False
+        self.reset()
+
+    def reset(self) -> None:
+        T, N, dev = self.buffer_size, self.n_envs, self.device
+        self.observations = th.zeros((T, N, *self.obs_shape), dtype=_torch_dtype(self.observation_space), device=dev)
+        act_dtype = th.int64 if isinstance(self.action_space, (spaces.Discrete, spaces.MultiDiscrete)) else th.float32
+        self.actions = th.zeros((T, N, self.action_dim), dtype=act_dtype, device=dev)
+        self.rewards = th.zeros((T, N), dtype=th.float32, device=dev)
+        self.returns = th.zeros((T, N), dtype=th.float32, device=dev)
+        self.episode_starts = th.zeros((T, N), dtype=th.float32, device=dev)
+        self.values = th.zeros((T, N), dtype=th.float32, device=dev)
+        self.log_probs = th.zeros((T, N), dtype=th.float32, device=dev)
+        self.advantages = th.zeros((T, N), dtype=th.float32, device=dev)
+        self.generator_ready = False
+        super().reset()
+
+    def compute_returns_and_advantage(self, last_values: th.Tensor, dones) -> None:
+        from imitation_amd.ops import rl as rl_ops
+
+        last_values = last_values.reshape(-1).float().to(self.device)
+        dones_t = _to_t(dones, self.device, th.float32).reshape(-1)
+        self.advantages, self.returns = rl_ops.gae(
+            self.rewards, self.values, self.episode_starts, last_values, dones_t, self.gamma, self.gae_lambda
+        )
+
+    def add(self, obs, action, reward, episode_start, value: th.Tensor, log_prob: th.Tensor) -> None:
+        if len(log_prob.shape) == 0:
+            log_prob = log_prob.reshape(-1, 1)
+        if isinstance(self.observation_space, spaces.Discrete):
+            obs = _to_t(obs, self.device).reshape((self.n_envs, *self.obs_shape))
+        self.observations[self.pos].copy_(_to_t(obs, self.device, self.observations.dtype).reshape(self.observations[self.pos].shape))
+        self.actions[self.pos].copy_(_to_t(action, self.device, self.actions.dtype).reshape((self.n_envs, self.action_dim)))
+        self.rewards[self.pos].copy_(_to_t(reward, self.device, th.float32).reshape(-1))
+        self.episode_starts[self.pos].copy_(_to_t(episode_start, self.device, th.float32).reshape(-1))
+        self.values[self.pos].copy_(value.detach().reshape(-1).float())
+        self.log_probs[self.pos].copy_(log_prob.detach().reshape(-1).float())
+        self.pos += 1
+        if self.pos == self.buffer_size:
+            self.full = True
+
+    def _flat(self):
+        T, N = self.buffer_size, self.n_envs
+        return dict(
+            observations=self.observations.reshape(T * N, *self.obs_shape),
+            actions=self.actions.reshape(T * N, self.action_dim),
+            values=self.values.reshape(-1),
+            log_probs=self.log_probs.reshape(-1),
+            advantages=self.advantages.reshape(-1),
+            returns=self.returns.reshape(-1),
+        )
+
+    def get(self, batch_size: Optional[int] = None, generator: Optional[th.Generator] = None) -> Generator[RolloutBufferSamples, None, None]:
+        assert self.full, ""
+        total = self.buffer_size * self.n_envs
+        indices = th.randperm(total, device=self.device, generator=generator)
+        flat = self._flat()
+        if batch_size is None:
+            batch_size = total
+        start = 0
+        while start < total:
+            yield self._get_samples(flat, indices[start : start + batch_size])
+            start += batch_size
+
+    def _get_samples(self, flat, idx: th.Tensor) -> RolloutBufferSamples:
+        acts = flat["actions"][idx]
+        if isinstance(self.action_space, spaces.Discrete):
+            acts = acts.reshape(-1)
+        return RolloutBufferSamples(
+            flat["observations"][idx], acts, flat["values"][idx], flat["log_probs"][idx], flat["advantages"][idx], flat["returns"][idx]
+        )
+
+
+class ReplayBuffer(BaseBuffer):
+    """Off-policy ring buffer on the device (SB3 ``ReplayBuffer`` semantics incl. timeout handling)."""
+
+    def __init__(self, buffer_size: int, observation_space: spaces.Space, action_space: spaces.Space,
+                 device: Union[th.device, str] = "auto", n_envs: int = 1, optimize_memory_usage: bool = False,
+                 handle_timeout_termination: bool = True):
+        super().__init__(buffer_size, observation_space, action_space, device, n_envs=n_envs)
+        self.buffer_size = max(buffer_size // n_envs, 1)
+        self.optimize_memory_usage = optimize_memory_usage
+        self.handle_timeout_termination = handle_timeout_termination
+        S, N, dev = self.buffer_size, self.n_envs, self.device
+        odt = _torch_dtype(observation_space)
+        self.observations = th.zeros((S, N, *self.obs_shape), dtype=odt, device=dev)
+        self.next_observations = th.zeros((S, N, *self.obs_shape), dtype=odt, device=dev)
+        adt = th.int64 if isinstance(action_space, (spaces.Discrete, spaces.MultiDiscrete)) else th.float32
+        self.actions = th.zeros((S, N, self.action_dim), dtype=adt, device=dev)
+        self.rewards = th.zeros((S, N), dtype=th.float32, device=dev)
+        self.dones = th.zeros((S, N), dtype=th.float32, device=dev)
+        self.timeouts = th.zeros((S, N), dtype=th.float32, device=dev)
+
+    def add(self, obs, next_obs, action, reward, done, infos: List[Dict[str, Any]]) -> None:
+        p = self.pos
+        self.observations[p].copy_(_to_t(obs, self.device, self.observations.dtype).reshape(self.observations[p].shape))
+        self.next_observations[p].copy_(_to_t(next_obs, self.device, self.next_observations.dtype).reshape(self.observations[p].shape))
+        self.actions[p].copy_(_to_t(action, self.device, self.actions.dtype).reshape((self.n_envs, self.action_dim)))
+        self.rewards[p].copy_(_to_t(reward, self.device, th.float32).reshape(-1))
+        self.dones[p].copy_(_to_t(done, self.device, th.float32).reshape(-1))
+        if self.handle_timeout_termination:
+            self.timeouts[p].copy_(
+                th.tensor([float(info.get("TimeLimit.truncated", False)) for info in infos], device=self.device)
+            )
+        self.pos += 1
+        if self.pos == self.buffer_size:
+            self.full = True
+            self.pos = 0
+
+    def sample(self, batch_size: int, env=None) -> ReplayBufferSamples:
+        upper = self.buffer_size if self.full else self.pos
+        batch_inds = th.randint(0, upper, (batch_size,), device=self.device)
+        return self._get_samples(batch_inds, env=env)
+
+    def _get_samples(self, batch_inds: th.Tensor, env=None) -> ReplayBufferSamples:
+        env_inds = th.randint(0, self.n_envs, (len(batch_inds),), device=self.device)
+        obs = self.observations[batch_inds, env_inds]
+        next_obs = self.next_observations[batch_inds, env_inds]
+        if env is not None and hasattr(env, "normalize_obs"):
+            obs = self.to_torch(env.normalize_obs(obs.cpu().numpy()))
+            next_obs = self.to_torch(env.normalize_obs(next_obs.cpu().numpy()))
+        acts = self.actions[batch_inds, env_inds]
+        dones = (self.dones[batch_inds, env_inds] * (1 - self.timeouts[batch_inds, env_inds])).reshape(-1, 1)
+        rews = self.rewards[batch_inds, env_inds].reshape(-1, 1)
+        if env is not None and hasattr(env, "normalize_reward"):
+            rews = self.to_torch(env.normalize_reward(rews.cpu().numpy())).float()
+        return ReplayBufferSamples(
+            observations=obs.float() if obs.dtype != th.uint8 else obs,
+            actions=acts,
+            next_observations=next_obs.float() if next_obs.dtype != th.uint8 else next_obs,
+            dones=dones,
+            rewards=rews,
+        )
