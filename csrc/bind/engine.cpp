@@ -1,0 +1,180 @@
+// Torch-facing bindings of the device engine kernels (rollout, PPO update).
+// Arguments arrive as a Python dict of tensors / numbers, so the engine's Python
+// side (imitation_amd/engine/*.py) owns the layout and this file only validates
+// devices/dtypes and forwards raw pointers.
+#include "common.h"
+#include "launchers.h"
+#include "vec_env.h"
+
+namespace {
+
+#define IA_HIP_CHECK2(expr)                                                           \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    TORCH_CHECK(_e == hipSuccess, "HIP error in " #expr ": ", hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename T>
+T* tptr(const py::dict& d, const char* k, bool optional = false) {
+  if (!d.contains(k) || d[k].is_none()) {
+    TORCH_CHECK(optional, "engine arg missing: ", k);
+    return nullptr;
+  }
+  auto t = d[k].cast<torch::Tensor>();
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "engine arg ", k, " must be a contiguous GPU tensor");
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+int ival(const py::dict& d, const char* k, int def = 0) { return d.contains(k) ? d[k].cast<int>() : def; }
+double fval(const py::dict& d, const char* k, double def = 0.0) { return d.contains(k) ? d[k].cast<double>() : def; }
+
+ia::WaveMLP wave_mlp(const py::dict& d) {
+  ia::WaveMLP m{};
+  auto Ws = d["W"].cast<std::vector<torch::Tensor>>();
+  auto bs = d["b"].cast<std::vector<torch::Tensor>>();
+  TORCH_CHECK(!Ws.empty() && Ws.size() <= (size_t)ia::kWaveMaxLayers, "1..4 layers");
+  m.n_layers = (int)Ws.size();
+  m.dims[0] = (int)Ws[0].size(1);
+  for (size_t l = 0; l < Ws.size(); ++l) {
+    TORCH_CHECK(Ws[l].is_cuda() && Ws[l].is_contiguous() && Ws[l].scalar_type() == torch::kFloat32, "W");
+    m.dims[l + 1] = (int)Ws[l].size(0);
+    TORCH_CHECK(m.dims[l + 1] <= ia::kWaveMaxDim && m.dims[l] <= ia::kWaveMaxDim, "engine MLP width <= 64");
+    m.W[l] = Ws[l].data_ptr<float>();
+    m.b[l] = bs[l].data_ptr<float>();
+  }
+  m.hidden_act = d["hidden_act"].cast<int>();
+  m.out_act = d["out_act"].cast<int>();
+  m.norm_mean = tptr<const float>(d, "norm_mean", true);
+  m.norm_var = tptr<const float>(d, "norm_var", true);
+  m.norm_eps = (float)fval(d, "norm_eps", 1e-5);
+  return m;
+}
+
+void rollout(py::dict d) {
+  ia::RolloutArgs a{};
+  std::string env = d["env"].cast<std::string>();
+  int ms = 0;
+  TORCH_CHECK(ia::make_env_params(env, &a.P, &ms), "unknown native env ", env);
+  TORCH_CHECK(a.P.kind != ia::ENV_PONG, "image envs are not supported by the device rollout");
+  a.max_steps = ival(d, "max_steps", ms);
+  a.T = ival(d, "T");
+  a.N = ival(d, "N");
+  a.gamma = (float)fval(d, "gamma", 0.99);
+  a.seed = (uint64_t)d["seed"].cast<long long>();
+  a.step0 = d["step0"].cast<long long>();
+  a.state = tptr<float>(d, "state");
+  a.rng = tptr<uint64_t>(d, "rng");
+  a.elapsed = tptr<int>(d, "elapsed");
+  a.ep_ret = tptr<float>(d, "ep_ret");
+  a.cur_obs = tptr<float>(d, "cur_obs");
+  a.cur_start = tptr<float>(d, "cur_start");
+  a.pi = wave_mlp(d["pi"].cast<py::dict>());
+  a.vf = wave_mlp(d["vf"].cast<py::dict>());
+  a.log_std = tptr<const float>(d, "log_std", true);
+  a.act_low = tptr<const float>(d, "act_low", true);
+  a.act_high = tptr<const float>(d, "act_high", true);
+  a.n_actions = ival(d, "n_actions", 0);
+  a.rew_enabled = ival(d, "rew_enabled", 0);
+  if (a.rew_enabled) {
+    a.rew = wave_mlp(d["rew"].cast<py::dict>());
+    a.use_state = ival(d, "use_state", 1);
+    a.use_action = ival(d, "use_action", 1);
+    a.use_next_state = ival(d, "use_next_state", 0);
+    a.use_done = ival(d, "use_done", 0);
+    a.rew_transform = ival(d, "rew_transform", 0);
+  }
+  TORCH_CHECK(a.P.obs_dim <= ia::kEngineMaxObs, "obs dim too large for the device rollout");
+  a.obs_buf = tptr<float>(d, "obs_buf");
+  a.act_raw = tptr<float>(d, "act_raw");
+  a.act_env = tptr<float>(d, "act_env");
+  a.logp = tptr<float>(d, "logp");
+  a.values = tptr<float>(d, "values");
+  a.rewards = tptr<float>(d, "rewards");
+  a.env_rew = tptr<float>(d, "env_rew");
+  a.starts = tptr<float>(d, "starts");
+  a.dones = tptr<float>(d, "dones");
+  a.next_obs = tptr<float>(d, "next_obs");
+  a.ep_ret_out = tptr<float>(d, "ep_ret_out");
+  a.last_values = tptr<float>(d, "last_values");
+  IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
+}
+
+void ppo_update(py::dict d) {
+  ia::PPOArgs a{};
+  a.D = ival(d, "D");
+  a.A = ival(d, "A");
+  a.discrete = ival(d, "discrete");
+  auto pid = d["pi_dims"].cast<std::vector<int>>();
+  auto vid = d["vf_dims"].cast<std::vector<int>>();
+  TORCH_CHECK(pid.size() >= 2 && pid.size() <= (size_t)ia::kWaveMaxLayers + 1, "pi dims");
+  TORCH_CHECK(vid.size() >= 2 && vid.size() <= (size_t)ia::kWaveMaxLayers + 1, "vf dims");
+  a.n_pi = (int)pid.size() - 1;
+  a.n_vf = (int)vid.size() - 1;
+  for (size_t i = 0; i < pid.size(); ++i) a.pi_dims[i] = pid[i];
+  for (size_t i = 0; i < vid.size(); ++i) a.vf_dims[i] = vid[i];
+  auto pw = d["pi_w_off"].cast<std::vector<int>>();
+  auto pb = d["pi_b_off"].cast<std::vector<int>>();
+  auto vw = d["vf_w_off"].cast<std::vector<int>>();
+  auto vb = d["vf_b_off"].cast<std::vector<int>>();
+  for (int l = 0; l < a.n_pi; ++l) { a.pi_w_off[l] = pw[l]; a.pi_b_off[l] = pb[l]; }
+  for (int l = 0; l < a.n_vf; ++l) { a.vf_w_off[l] = vw[l]; a.vf_b_off[l] = vb[l]; }
+  a.log_std_off = ival(d, "log_std_off", -1);
+  a.hidden_act = ival(d, "hidden_act");
+  a.params = tptr<float>(d, "params");
+  a.grads = tptr<float>(d, "grads");
+  a.exp_avg = tptr<float>(d, "exp_avg");
+  a.exp_avg_sq = tptr<float>(d, "exp_avg_sq");
+  a.n_params = ival(d, "n_params");
+  a.has_norm = ival(d, "has_norm");
+  a.norm_mean = tptr<float>(d, "norm_mean", true);
+  a.norm_var = tptr<float>(d, "norm_var", true);
+  a.norm_count = tptr<float>(d, "norm_count", true);
+  a.norm_eps = (float)fval(d, "norm_eps", 1e-5);
+  a.obs = tptr<const float>(d, "obs");
+  a.acts = tptr<const float>(d, "acts");
+  a.old_logp = tptr<const float>(d, "old_logp");
+  a.adv = tptr<const float>(d, "adv");
+  a.returns = tptr<const float>(d, "returns");
+  a.perm = tptr<const int>(d, "perm");
+  a.rows = ival(d, "rows");
+  a.batch = ival(d, "batch");
+  a.n_epochs = ival(d, "n_epochs");
+  a.clip_range = (float)fval(d, "clip_range");
+  a.ent_coef = (float)fval(d, "ent_coef");
+  a.vf_coef = (float)fval(d, "vf_coef");
+  a.max_grad_norm = (float)fval(d, "max_grad_norm");
+  a.lr = (float)fval(d, "lr");
+  a.beta1 = (float)fval(d, "beta1", 0.9);
+  a.beta2 = (float)fval(d, "beta2", 0.999);
+  a.adam_eps = (float)fval(d, "adam_eps", 1e-5);
+  a.normalize_advantage = ival(d, "normalize_advantage", 1);
+  a.adam_step = tptr<float>(d, "adam_step");
+  a.stats = tptr<float>(d, "stats");
+  a.mode = ival(d, "mode", 0);
+  a.mb_index = ival(d, "mb_index", 0);
+  TORCH_CHECK(a.D <= 64, "obs dim <= 64");
+  IA_HIP_CHECK2(ia::ppo_launch(a, ia_stream()));
+}
+
+size_t ppo_lds(py::dict d) {
+  ia::PPOArgs a{};
+  a.D = ival(d, "D");
+  a.A = ival(d, "A");
+  a.discrete = ival(d, "discrete");
+  auto pid = d["pi_dims"].cast<std::vector<int>>();
+  auto vid = d["vf_dims"].cast<std::vector<int>>();
+  a.n_pi = (int)pid.size() - 1;
+  a.n_vf = (int)vid.size() - 1;
+  for (size_t i = 0; i < pid.size(); ++i) a.pi_dims[i] = pid[i];
+  for (size_t i = 0; i < vid.size(); ++i) a.vf_dims[i] = vid[i];
+  a.batch = ival(d, "batch");
+  return ia::ppo_lds_bytes(a);
+}
+
+}  // namespace
+
+void register_engine(py::module& m) {
+  m.def("engine_rollout", &rollout, "T-step device rollout (policy + env + learned reward) for N envs");
+  m.def("engine_ppo_update", &ppo_update, "persistent PPO update / DP minibatch grads / apply");
+  m.def("engine_ppo_lds", &ppo_lds, "LDS bytes the PPO kernel needs for a configuration");
+}

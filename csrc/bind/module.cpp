@@ -6,4 +6,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("arch") = "gfx950";
   register_envs(m);
   register_kernels(m);
+  register_engine(m);
 }

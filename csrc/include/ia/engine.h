@@ -1,0 +1,117 @@
+// Device-resident training engine: argument blocks shared by the HIP kernels
+// (csrc/kernels/engine.hip, ppo.hip) and their host launchers / bindings.
+//
+// The engine keeps a whole adversarial-imitation round on the GPU (SURVEY §7.4
+// items 2-3): env state, policy / value / reward nets, rollout buffer, GAE, the
+// PPO update and the generator replay buffer never leave HBM.
+#pragma once
+#include <stdint.h>
+
+#include "ia/common.h"
+#include "ia/envs.h"
+
+namespace ia {
+
+constexpr int kWaveMaxLayers = 4;
+constexpr int kWaveMaxDim = 64;  // one lane per unit
+constexpr int kEngineMaxObs = 64;
+
+// An MLP evaluated by ONE wave (lane j = unit j), used per env inside the rollout kernel.
+struct WaveMLP {
+  int n_layers;
+  int dims[kWaveMaxLayers + 1];
+  int hidden_act;
+  int out_act;
+  const float* W[kWaveMaxLayers];  // [dout][din] row-major (nn.Linear layout)
+  const float* b[kWaveMaxLayers];
+  const float* norm_mean;  // optional input RunningNorm (eval mode)
+  const float* norm_var;
+  float norm_eps;
+};
+
+enum RewardTransform : int { REW_RAW = 0, REW_SOFTPLUS = 1 };
+
+struct RolloutArgs {
+  EnvParams P;
+  int max_steps;  // TimeLimit horizon
+  int T;          // steps per env this call
+  int N;          // envs
+  float gamma;    // for TimeLimit-truncation bootstrap (SB3 collect_rollouts)
+  uint64_t seed;  // action-sampling stream
+  long long step0;  // global step counter (decorrelates calls)
+  // persistent env state (device)
+  float* state;      // [N][state_dim]
+  uint64_t* rng;     // [N]
+  int* elapsed;      // [N]
+  float* ep_ret;     // [N] running env return (Monitor)
+  float* cur_obs;    // [N][D]  (policy's _last_obs)
+  float* cur_start;  // [N]     (_last_episode_starts)
+  // policy
+  WaveMLP pi, vf;
+  const float* log_std;  // [A] (Gaussian) or nullptr (Categorical)
+  const float* act_low;  // [A] Box bounds for clipping
+  const float* act_high;
+  int n_actions;  // >0: Categorical over n_actions
+  // learned reward (GAIL / AIRL reward_train); rew_enabled==0 -> env reward
+  int rew_enabled;
+  WaveMLP rew;
+  int use_state, use_action, use_next_state, use_done;
+  int rew_transform;
+  // outputs, [T][N] (+ trailing feature dim)
+  float* obs_buf;
+  float* act_raw;   // sampled (unclipped) action, PPO buffer
+  float* act_env;   // action given to the env (clipped), replay buffer / reward
+  float* logp;
+  float* values;
+  float* rewards;   // learned reward (+ γ V(terminal) on truncation)
+  float* env_rew;
+  float* starts;
+  float* dones;
+  float* next_obs;  // terminal obs on done
+  float* ep_ret_out;  // episode return where done
+  float* last_values;  // [N]
+};
+
+// One PPO update (all epochs x minibatches) in one persistent workgroup.
+struct PPOArgs {
+  int D, A;             // obs dim, action dim (Gaussian) / n_actions (Categorical)
+  int discrete;
+  int n_pi, n_vf;       // layer counts (incl. head)
+  int pi_dims[kWaveMaxLayers + 1];
+  int vf_dims[kWaveMaxLayers + 1];
+  int hidden_act;
+  // flat parameter / grad / Adam state vectors; layout = torch module order
+  float* params;
+  float* grads;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int n_params;
+  int pi_w_off[kWaveMaxLayers], pi_b_off[kWaveMaxLayers];
+  int vf_w_off[kWaveMaxLayers], vf_b_off[kWaveMaxLayers];
+  int log_std_off;  // -1 if none
+  // features RunningNorm (train mode: stats updated from each minibatch)
+  float* norm_mean;
+  float* norm_var;
+  float* norm_count;  // float counter (exact up to 2^24)
+  float norm_eps;
+  int has_norm;
+  // data: flat rollout [rows]
+  const float* obs;
+  const float* acts;
+  const float* old_logp;
+  const float* adv;
+  const float* returns;
+  const int* perm;  // [n_epochs][rows]
+  int rows, batch, n_epochs;
+  // hyper-parameters
+  float clip_range, ent_coef, vf_coef, max_grad_norm;
+  float lr, beta1, beta2, adam_eps;
+  int normalize_advantage;
+  float* adam_step;  // running step count (float)
+  // diagnostics [5]: entropy_loss, pg_loss, value_loss, clip_fraction, approx_kl (sums over minibatches)
+  float* stats;
+  int mode;  // 0: full persistent update; 1: one minibatch -> grads only; 2: apply clip+Adam from grads
+  int mb_index;  // minibatch index for mode 1 (epoch * n_mb + mb)
+};
+
+}  // namespace ia

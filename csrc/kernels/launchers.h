@@ -7,6 +7,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "ia/engine.h"
 #include "ia/tmlp.h"
 
 namespace ia {
@@ -21,5 +22,13 @@ hipError_t tmlp_backward(const MLPDesc& d, const float* X, const float* dY, int 
 // ---- rl.hip: GAE scan over [T, N]
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
                       int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);
+
+// ---- engine.hip: device-resident rollout (policy + env + learned reward)
+size_t rollout_lds_bytes(const RolloutArgs& a);
+hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s);
+
+// ---- ppo.hip: persistent PPO update
+size_t ppo_lds_bytes(const PPOArgs& a);
+hipError_t ppo_launch(const PPOArgs& a, hipStream_t s);
 
 }  // namespace ia

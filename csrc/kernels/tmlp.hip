@@ -239,6 +239,7 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
       }
     }
     // G = dZ_l . W_l (rows x in) -> dZ_{l-1} = G * act'(H_l), or dX for l == 0
+    __syncthreads();
     if (l > 0 || dX != nullptr) {
       const int K = pad32(dout), ldw = ld_for_k(dout);
       const int act_prev = l > 0 ? layer_act(d, l - 1) : ACT_IDENTITY;

@@ -1,0 +1,475 @@
+"""Device-resident adversarial imitation (GAIL / AIRL-ready) -- the MI355X fast path.
+
+Same algorithm, hyper-parameters and public surface as
+:class:`imitation_amd.algorithms.adversarial.gail.GAIL` (reference
+``src/imitation/algorithms/adversarial/{common,gail}.py``), but a training round
+never leaves the GPU:
+
+=====================  ==========================================================
+reference (host loop)  this engine
+=====================  ==========================================================
+SB3 collect_rollouts:  ``engine_rollout`` -- ONE kernel runs n_steps x n_envs of
+policy fwd, VecEnv     policy sampling, env physics (native model), learned
+pipes, reward wrapper  reward ``softplus(D(s,a))``, TimeLimit bootstrap; buffers
+numpy<->device copies  are written straight into HBM
+RolloutBuffer GAE      ``gae`` kernel (one lane per env)
+(python loop)
+PPO.train              ``engine_ppo_update`` -- ONE persistent workgroup runs all
+(~10 launches / mb)    epochs x minibatches (fp32 MFMA, params in LDS, Adam in L2)
+BufferingWrapper +     device replay ring, same FIFO content as the reference's
+ReplayBuffer (numpy)   flatten-then-store order
+train_disc             fused MLP fwd/bwd kernels + device demo sampler
+=====================  ==========================================================
+
+Data parallel: each rank runs its own envs; the PPO update switches to the
+per-minibatch kernel pair with an RCCL all-reduce of the normaliser moments and
+of the flat gradient between them (synchronous DP == large-batch SGD), and the
+discriminator averages its gradient bucket once per update.
+
+Eligibility (checked in :func:`supports`): native vector env (non-image), an
+on-policy :class:`~imitation_amd.rl.ppo.PPO` with an MLP actor-critic (widths ≤ 64,
+≤ 4 layers, minibatch ≤ 128 and a multiple of 16), and an MLP
+``BasicRewardNet`` (optionally inside ``NormalizedRewardNet``). Anything else
+should use the host-loop trainers.
+"""
+
+from __future__ import annotations
+
+import time
+from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+import torch as th
+from torch import nn
+
+from imitation_amd import ops
+from imitation_amd.algorithms.adversarial import common
+from imitation_amd.algorithms.adversarial.gail import GAIL
+from imitation_amd.data import buffer as buffer_mod
+from imitation_amd.data import types
+from imitation_amd.envs import spaces
+from imitation_amd.envs.vec_env import NativeVecEnv, VecEnvWrapper
+from imitation_amd.ops import rl as rl_ops
+from imitation_amd.ops.mlp import act_code
+from imitation_amd.parallel import dist as pdist
+from imitation_amd.rewards import reward_nets
+from imitation_amd.rl.policies import ActorCriticPolicy
+from imitation_amd.rl.ppo import PPO
+from imitation_amd.util import networks
+
+
+def _unwrap_native(venv) -> Optional[NativeVecEnv]:
+    e = venv
+    while e is not None:
+        if isinstance(e, NativeVecEnv):
+            return e
+        e = getattr(e, "venv", None)
+    return None
+
+
+def _mlp_layers(seq: nn.Sequential) -> Tuple[Optional[networks.BaseNorm], List[nn.Linear], int, int]:
+    """(input norm, linears, hidden act code, out act code) of a build_mlp / trunk Sequential."""
+    norm = None
+    lins: List[nn.Linear] = []
+    acts: List[int] = []
+    for m in seq:
+        if isinstance(m, networks.BaseNorm):
+            norm = m
+        elif isinstance(m, nn.Linear):
+            lins.append(m)
+            acts.append(0)
+        elif isinstance(m, (nn.Flatten, networks.SqueezeLayer, nn.Dropout)):
+            continue
+        else:
+            c = act_code(m)
+            if c is None:
+                raise ValueError(f"engine cannot fuse activation {m}")
+            acts[-1] = c
+    hidden = acts[0] if len(acts) > 1 else 0
+    return norm, lins, hidden, acts[-1] if acts else 0
+
+
+def _policy_nets(policy: ActorCriticPolicy):
+    fe = policy.features_extractor
+    norm = getattr(fe, "normalize", None)
+    pi_trunk = list(policy.mlp_extractor.policy_net)
+    vf_trunk = list(policy.mlp_extractor.value_net)
+
+    def trunk(mods):
+        lins, act = [], 0
+        for m in mods:
+            if isinstance(m, nn.Linear):
+                lins.append(m)
+            else:
+                c = act_code(m)
+                if c is None:
+                    raise ValueError(f"engine cannot fuse activation {m}")
+                act = c
+        return lins, act
+
+    pl, pa = trunk(pi_trunk)
+    vl, va = trunk(vf_trunk)
+    if pl and vl and pa != va:
+        raise ValueError("actor and critic trunks must share the activation")
+    return norm, pl + [policy.action_net], vl + [policy.value_net], pa or va
+
+
+def supports(venv, gen_algo, reward_net) -> Tuple[bool, str]:
+    if not th.cuda.is_available():
+        return False, "no GPU"
+    nat = _unwrap_native(venv)
+    if nat is None:
+        return False, "env is not a native vector env"
+    if nat._is_image:
+        return False, "image observations"
+    if not isinstance(gen_algo, PPO):
+        return False, "generator is not PPO"
+    pol = gen_algo.policy
+    if type(pol).__name__.startswith("Homogenous") or not isinstance(pol, ActorCriticPolicy):
+        return False, "policy is not a plain ActorCriticPolicy"
+    if not pol.share_features_extractor:
+        return False, "separate features extractors"
+    try:
+        norm, pl, vl, act = _policy_nets(pol)
+    except ValueError as e:
+        return False, str(e)
+    dims = [pol.features_dim] + [l.out_features for l in pl]
+    if max(dims) > 64 or len(pl) > 4 or len(vl) > 4:
+        return False, "policy too wide / deep for the engine"
+    if gen_algo.batch_size % 16 != 0 or gen_algo.batch_size > 128:
+        return False, "minibatch must be a multiple of 16 and <= 128"
+    if (gen_algo.n_steps * gen_algo.n_envs) % gen_algo.batch_size != 0:
+        return False, "rollout size not a multiple of the minibatch"
+    if gen_algo.clip_range_vf is not None or gen_algo.target_kl is not None:
+        return False, "clip_range_vf / target_kl not supported by the engine"
+    base = reward_net.base if isinstance(reward_net, reward_nets.NormalizedRewardNet) else reward_net
+    if not isinstance(base, reward_nets.BasicRewardNet):
+        return False, "reward net is not a BasicRewardNet"
+    return True, ""
+
+
+class _FlatParams:
+    """Re-point a list of parameters at views of one flat fp32 device buffer."""
+
+    def __init__(self, params: Sequence[nn.Parameter]):
+        self.params = list(params)
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.flat = th.zeros(n, device=dev, dtype=th.float32)
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.flat[off : off + p.numel()].copy_(p.detach().reshape(-1))
+            self.offsets.append(off)
+            p.data = self.flat[off : off + p.numel()].view_as(p)
+            off += p.numel()
+        self.n = n
+
+    def offset(self, p: nn.Parameter) -> int:
+        for q, o in zip(self.params, self.offsets):
+            if q is p:
+                return o
+        raise KeyError("parameter not in flat buffer")
+
+
+class DeviceGAIL(GAIL):
+    """GAIL whose generator rounds run entirely on the GPU (see module docstring)."""
+
+    def __init__(self, *, demonstrations, demo_batch_size: int, venv, gen_algo: PPO, reward_net: reward_nets.RewardNet, **kwargs):
+        ok, why = supports(venv, gen_algo, reward_net)
+        if not ok:
+            raise ValueError(f"DeviceGAIL not applicable: {why}; use algorithms.adversarial.gail.GAIL")
+        super().__init__(demonstrations=demonstrations, demo_batch_size=demo_batch_size, venv=venv, gen_algo=gen_algo,
+                         reward_net=reward_net, **kwargs)
+        self._native = _unwrap_native(venv)
+        self._C = ops.native()
+        self._dev = gen_algo.device
+        self._setup_engine()
+
+    # ------------------------------------------------------------------ setup
+    def _setup_engine(self) -> None:
+        dev = self._dev
+        algo: PPO = self.gen_algo
+        pol: ActorCriticPolicy = algo.policy
+        nat = self._native
+        self.N = nat.num_envs
+        self.T = algo.n_steps
+        self.D = int(np.prod(nat.observation_space.shape))
+        self.discrete = isinstance(nat.action_space, spaces.Discrete)
+        self.A = int(nat.action_space.n) if self.discrete else int(np.prod(nat.action_space.shape))
+        # env state -> device
+        obs0 = nat.reset()
+        st = nat.get_state()
+        self.state = th.as_tensor(st["state"], device=dev).float().contiguous()
+        self.rng = th.as_tensor(st["rng"].astype(np.int64), device=dev).contiguous()
+        self.elapsed = th.as_tensor(st["elapsed"].astype(np.int32), device=dev).contiguous()
+        self.ep_ret = th.zeros(self.N, device=dev)
+        self.cur_obs = th.as_tensor(np.asarray(obs0, np.float32), device=dev).reshape(self.N, self.D).contiguous()
+        self.cur_start = th.ones(self.N, device=dev)
+        self.max_steps = int(nat.max_episode_steps)
+        # policy parameters -> one flat buffer (module params become views)
+        norm, pl, vl, hid = _policy_nets(pol)
+        self.pol_norm = norm
+        self.pi_layers, self.vf_layers, self.hidden_act = pl, vl, hid
+        plist: List[nn.Parameter] = []
+        for l in pl + vl:
+            plist += [l.weight, l.bias]
+        self.has_log_std = hasattr(pol, "log_std") and not self.discrete
+        if self.has_log_std:
+            plist.append(pol.log_std)
+        self.flat = _FlatParams(plist)
+        self.grads = th.zeros_like(self.flat.flat)
+        self.exp_avg = th.zeros_like(self.flat.flat)
+        self.exp_avg_sq = th.zeros_like(self.flat.flat)
+        self.adam_step = th.zeros(1, device=dev)
+        if norm is not None:
+            self.norm_count = norm.count.detach().float().reshape(1).clone()
+        else:
+            self.norm_count = None
+        if self.discrete:
+            self.act_low = self.act_high = None
+        else:
+            self.act_low = th.as_tensor(nat.action_space.low.reshape(-1), device=dev).float()
+            self.act_high = th.as_tensor(nat.action_space.high.reshape(-1), device=dev).float()
+        # rollout buffers [T, N, ...]
+        T, N, D = self.T, self.N, self.D
+        Aw = 1 if self.discrete else self.A
+        z = lambda *s: th.zeros(*s, device=dev)
+        self.buf = dict(obs_buf=z(T, N, D), act_raw=z(T, N, Aw), act_env=z(T, N, Aw), logp=z(T, N), values=z(T, N),
+                        rewards=z(T, N), env_rew=z(T, N), starts=z(T, N), dones=z(T, N), next_obs=z(T, N, D),
+                        ep_ret_out=z(T, N), last_values=z(N))
+        self.stats = z(5)
+        self._seed = int(np.random.randint(0, 2**62)) ^ (pdist.rank() * 0x9E3779B97F4A7C15 & ((1 << 62) - 1))
+        self._step0 = 0
+        cap = self._gen_replay_buffer.capacity
+        obs_dt = th.float32
+        act_shape = () if self.discrete else (self.A,)
+        self._gen_dev = buffer_mod.DeviceBuffer(
+            cap, {"obs": (D,), "acts": act_shape, "next_obs": (D,), "dones": ()},
+            {"obs": obs_dt, "acts": th.int64 if self.discrete else th.float32, "next_obs": obs_dt, "dones": th.bool}, dev)
+        self._ppo_static = self._ppo_args_static()
+        self._ep_lens_running = np.zeros(self.N, dtype=np.int64)
+
+    def _wave_mlp(self, lins: Sequence[nn.Linear], hidden_act: int, out_act: int, norm=None) -> Dict[str, Any]:
+        d: Dict[str, Any] = dict(W=[l.weight.detach() for l in lins], b=[l.bias.detach() for l in lins],
+                                 hidden_act=int(hidden_act), out_act=int(out_act))
+        if norm is not None:
+            d.update(norm_mean=norm.running_mean.detach().float().contiguous(),
+                     norm_var=norm.running_var.detach().float().contiguous(), norm_eps=float(norm.eps))
+        return d
+
+    def _reward_spec(self) -> Dict[str, Any]:
+        base = self._reward_net.base if isinstance(self._reward_net, reward_nets.NormalizedRewardNet) else self._reward_net
+        rnorm, rl, rh, ro = _mlp_layers(base.mlp)
+        spec = dict(rew=self._wave_mlp(rl, rh, ro, rnorm), use_state=int(base.use_state), use_action=int(base.use_action),
+                    use_next_state=int(base.use_next_state), use_done=int(base.use_done))
+        return spec
+
+    def _ppo_args_static(self) -> Dict[str, Any]:
+        algo: PPO = self.gen_algo
+        fp = self.flat
+        pi_dims = [self.D] + [l.out_features for l in self.pi_layers]
+        vf_dims = [self.D] + [l.out_features for l in self.vf_layers]
+        d = dict(D=self.D, A=self.A, discrete=int(self.discrete), pi_dims=pi_dims, vf_dims=vf_dims,
+                 pi_w_off=[fp.offset(l.weight) for l in self.pi_layers], pi_b_off=[fp.offset(l.bias) for l in self.pi_layers],
+                 vf_w_off=[fp.offset(l.weight) for l in self.vf_layers], vf_b_off=[fp.offset(l.bias) for l in self.vf_layers],
+                 log_std_off=fp.offset(self.gen_algo.policy.log_std) if self.has_log_std else -1,
+                 hidden_act=int(self.hidden_act), params=fp.flat, grads=self.grads, exp_avg=self.exp_avg,
+                 exp_avg_sq=self.exp_avg_sq, n_params=fp.n, has_norm=int(self.pol_norm is not None),
+                 rows=self.T * self.N, batch=int(algo.batch_size), n_epochs=int(algo.n_epochs),
+                 ent_coef=float(algo.ent_coef), vf_coef=float(algo.vf_coef), max_grad_norm=float(algo.max_grad_norm),
+                 normalize_advantage=int(algo.normalize_advantage), adam_step=self.adam_step, stats=self.stats)
+        opt = algo.policy.optimizer
+        g = opt.param_groups[0]
+        d.update(beta1=float(g.get("betas", (0.9, 0.999))[0]), beta2=float(g.get("betas", (0.9, 0.999))[1]),
+                 adam_eps=float(g.get("eps", 1e-8)))
+        if self.pol_norm is not None:
+            d.update(norm_mean=self.pol_norm.running_mean, norm_var=self.pol_norm.running_var, norm_count=self.norm_count,
+                     norm_eps=float(self.pol_norm.eps))
+        lds = self._C.engine_ppo_lds(d)
+        if lds > 150 * 1024:
+            raise ValueError(f"PPO engine needs {lds} B of LDS (> 150 KiB)")
+        return d
+
+    # ------------------------------------------------------------------ one generator round
+    def _rollout(self) -> None:
+        algo: PPO = self.gen_algo
+        pol = algo.policy
+        args = dict(env=self._native.env_id, max_steps=self.max_steps, T=self.T, N=self.N, gamma=float(algo.gamma),
+                    seed=int(self._seed), step0=int(self._step0), state=self.state, rng=self.rng, elapsed=self.elapsed,
+                    ep_ret=self.ep_ret, cur_obs=self.cur_obs, cur_start=self.cur_start,
+                    pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
+                    vf=self._wave_mlp(self.vf_layers, self.hidden_act, 0, self.pol_norm),
+                    log_std=pol.log_std.detach() if self.has_log_std else None, act_low=self.act_low,
+                    act_high=self.act_high, n_actions=self.A if self.discrete else 0)
+        if self.debug_use_ground_truth:
+            args.update(rew_enabled=0)
+        else:
+            args.update(rew_enabled=1, rew_transform=1, **self._reward_spec())
+        args.update(self.buf)
+        self._C.engine_rollout(args)
+        self._step0 += self.T
+
+    def _ppo_update(self) -> None:
+        algo: PPO = self.gen_algo
+        rows = self.T * self.N
+        algo._update_current_progress_remaining(algo.num_timesteps, algo._total_timesteps or algo.num_timesteps)
+        lr = float(algo.lr_schedule(algo._current_progress_remaining))
+        clip = float(algo.clip_range(algo._current_progress_remaining))
+        perm = th.stack([th.randperm(rows, device=self._dev) for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
+        adv, ret = rl_ops.gae(self.buf["rewards"], self.buf["values"], self.buf["starts"], self.buf["last_values"],
+                              self.cur_start, float(algo.gamma), float(algo.gae_lambda))
+        obs = self.buf["obs_buf"].reshape(rows, self.D)
+        acts = self.buf["act_raw"].reshape(rows, -1)
+        d = dict(self._ppo_static)
+        d.update(obs=obs, acts=acts, old_logp=self.buf["logp"].reshape(rows), adv=adv.reshape(rows).contiguous(),
+                 returns=ret.reshape(rows).contiguous(), perm=perm, clip_range=clip, lr=lr)
+        self.stats.zero_()
+        if pdist.world_size() == 1:
+            d["mode"] = 0
+            self._C.engine_ppo_update(d)
+        else:
+            n_mb = rows // algo.batch_size
+            B = algo.batch_size
+            for it in range(algo.n_epochs * n_mb):
+                e, mb = divmod(it, n_mb)
+                if self.pol_norm is not None:
+                    idx = perm[e, mb * B : (mb + 1) * B].long()
+                    self._dp_norm_update(obs.index_select(0, idx))
+                d["mode"] = 1
+                d["mb_index"] = it
+                self._C.engine_ppo_update(d)
+                pdist.allreduce_grads_flat(self.grads)
+                d["mode"] = 2
+                self._C.engine_ppo_update(d)
+        if self.pol_norm is not None:
+            self.pol_norm.count.copy_(self.norm_count.to(self.pol_norm.count.dtype).reshape(()))
+        algo._n_updates += algo.n_epochs
+        self._last_ppo_info = (rows, algo.n_epochs * (rows // algo.batch_size))
+
+    def _dp_norm_update(self, batch: th.Tensor) -> None:
+        """RunningNorm.update_stats with all-reduced moments (the kernel is told not to update)."""
+        norm = self.pol_norm
+        mean, var, cnt = pdist.allreduce_moments(batch)
+        c0 = self.norm_count
+        tot = c0 + cnt
+        delta = mean - norm.running_mean
+        norm.running_mean.add_(delta * cnt / tot)
+        rv = norm.running_var * c0 + var * cnt + delta.square() * c0 * cnt / tot
+        norm.running_var.copy_(rv / tot)
+        self.norm_count.add_(cnt)
+
+    def _store_generator_samples(self) -> None:
+        """Replay-buffer content identical to BufferingWrapper -> flatten -> FIFO store."""
+        dones = self.buf["dones"].to("cpu", non_blocking=False).numpy().astype(bool)  # [T, N] (one sync / round)
+        T, N = dones.shape
+        finished: List[Tuple[int, int, int, int]] = []  # (end_t, env, start_t, len)
+        partial: List[Tuple[int, int, int]] = []
+        seg_start = np.zeros(N, dtype=np.int64)
+        ep_lens = []
+        for t in range(T):
+            for n in np.flatnonzero(dones[t]):
+                finished.append((t, n, int(seg_start[n]), t - int(seg_start[n]) + 1))
+                ep_lens.append(int(self._ep_lens_running[n] + t - seg_start[n] + 1))
+                self._ep_lens_running[n] = 0
+                seg_start[n] = t + 1
+        for n in range(N):
+            if seg_start[n] < T:
+                partial.append((n, int(seg_start[n]), T - int(seg_start[n])))
+                self._ep_lens_running[n] += T - seg_start[n]
+        order = []
+        for (t, n, s, ln) in finished:
+            order.extend(((np.arange(s, t + 1)) * N + n).tolist())
+        for (n, s, ln) in partial:
+            order.extend(((np.arange(s, T)) * N + n).tolist())
+        order = np.asarray(order, dtype=np.int64)
+        cap = self._gen_dev.capacity
+        keep = th.as_tensor(order[-cap:], device=self._dev)
+        rows = T * N
+        acts = self.buf["act_env"].reshape(rows, -1)
+        if self.discrete:
+            acts = acts.reshape(rows).long()
+        self._gen_dev.store({
+            "obs": self.buf["obs_buf"].reshape(rows, self.D).index_select(0, keep),
+            "acts": acts.index_select(0, keep),
+            "next_obs": self.buf["next_obs"].reshape(rows, self.D).index_select(0, keep),
+            "dones": self.buf["dones"].reshape(rows).index_select(0, keep).bool(),
+        })
+        local_lens = list(ep_lens)
+        if pdist.world_size() > 1:
+            ep_lens = [l for part in pdist.all_gather_object(ep_lens) for l in part]
+        self._check_fixed_horizon(ep_lens)
+        # Monitor-style episode stats for the generator logger
+        if finished:
+            ep_ret = self.buf["ep_ret_out"].cpu().numpy()
+            algo = self.gen_algo
+            if algo.ep_info_buffer is None:
+                import collections
+
+                algo.ep_info_buffer = collections.deque(maxlen=algo._stats_window_size)
+            for (t, n, s, ln), l_full in zip(finished, local_lens):
+                algo.ep_info_buffer.append({"r": float(ep_ret[t, n]), "l": int(l_full), "t": 0.0})
+
+    def _gen_sample(self, batch_size: int) -> Dict[str, th.Tensor]:
+        if self._gen_dev.size() == 0:
+            raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
+        return self._gen_dev.sample(batch_size)
+
+    def train_gen(self, total_timesteps: Optional[int] = None, learn_kwargs: Optional[Mapping] = None) -> None:
+        """One (or more) device rounds: rollout -> GAE -> PPO update -> replay store."""
+        if total_timesteps is None:
+            total_timesteps = self.gen_train_timesteps
+        algo: PPO = self.gen_algo
+        n_rounds = max(1, total_timesteps // (self.T * self.N))
+        with self.logger.accumulate_means("gen"):
+            for _ in range(n_rounds):
+                if algo._total_timesteps < algo.num_timesteps + self.T * self.N:
+                    algo._total_timesteps = algo.num_timesteps + self.T * self.N
+                self._rollout()
+                algo.num_timesteps += self.T * self.N
+                self._ppo_update()
+                self._store_generator_samples()
+                self._global_step += 1
+            self._log_gen()
+
+    def _log_gen(self) -> None:
+        algo = self.gen_algo
+        s = (self.stats / max(1, self._last_ppo_info[1])).tolist()
+        lg = self.logger
+        lg.record("train/entropy_loss", s[0])
+        lg.record("train/policy_gradient_loss", s[1])
+        lg.record("train/value_loss", s[2])
+        lg.record("train/clip_fraction", s[3])
+        lg.record("train/approx_kl", s[4])
+        lg.record("train/n_updates", algo._n_updates)
+        lg.record("time/total_timesteps", algo.num_timesteps)
+        if algo.ep_info_buffer:
+            lg.record("rollout/ep_rew_mean", float(np.mean([e["r"] for e in algo.ep_info_buffer])))
+            lg.record("rollout/ep_len_mean", float(np.mean([e["l"] for e in algo.ep_info_buffer])))
+
+    def sync_env_to_host(self) -> None:
+        """Copy the device env state back into the native host env (e.g. before host-side evaluation)."""
+        self._native.set_state({"state": self.state.cpu().numpy(), "rng": self.rng.cpu().numpy(),
+                                "elapsed": self.elapsed.cpu().numpy().astype(np.int64)})
+
+
+def smoke_round(device) -> None:
+    """Tiny end-to-end device round (used by ``__graft_entry__.smoke``)."""
+    from imitation_amd.data import rollout as rollout_mod
+    from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
+    from imitation_amd.util import logger as imit_logger
+    from imitation_amd.util.util import make_vec_env
+
+    rng = np.random.default_rng(0)
+    venv = make_vec_env("seals/HalfCheetah-v1", rng=rng, n_envs=8)
+    demo_env = make_vec_env("seals/HalfCheetah-v1", rng=np.random.default_rng(1), n_envs=4)
+    demos = rollout_mod.flatten_trajectories(
+        rollout_mod.generate_trajectories(None, demo_env, rollout_mod.make_min_timesteps(2048), rng=rng))
+    gen = PPO(FeedForward32Policy, venv, n_steps=64, batch_size=64, n_epochs=2, device=device,
+              policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+    rn = reward_nets.BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=networks.RunningNorm)
+    tr = DeviceGAIL(demonstrations=demos, demo_batch_size=256, venv=venv, gen_algo=gen, reward_net=rn,
+                    n_disc_updates_per_round=2, custom_logger=imit_logger.configure("/tmp/ia_smoke", format_strs=[]))
+    tr.train(2 * 64 * 8)
+    th.cuda.synchronize()
+    assert all(th.isfinite(p).all() for p in gen.policy.parameters())

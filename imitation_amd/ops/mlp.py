@@ -59,6 +59,18 @@ def _act(code: int, x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+class _RoundBF16(torch.autograd.Function):
+    """Round values to bf16 in the forward pass, identity gradient (straight-through)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 def tmlp_reference(
     x: torch.Tensor,
     weights: Sequence[torch.Tensor],
@@ -68,14 +80,22 @@ def tmlp_reference(
     norm_mean: Optional[torch.Tensor] = None,
     norm_var: Optional[torch.Tensor] = None,
     norm_eps: float = 1e-5,
+    emulate_bf16_operands: bool = False,
 ) -> torch.Tensor:
-    """Plain PyTorch fp32 reference of the fused MLP (the kernel's numerics oracle)."""
+    """Plain PyTorch fp32 reference of the fused MLP (the kernel's numerics oracle).
+
+    ``emulate_bf16_operands`` rounds every MFMA operand (normalised input, weights,
+    hidden activations) to bf16 while keeping fp32 accumulation -- exactly the
+    kernel's operand precision -- so that piecewise activations (ReLU) take the same
+    branch as the kernel and gradients can be compared tightly.
+    """
+    rnd = _RoundBF16.apply if emulate_bf16_operands else (lambda t: t)
     h = x
     if norm_mean is not None:
         h = (h - norm_mean) / torch.sqrt(norm_var + norm_eps)
     n = len(weights)
     for i, (w, b) in enumerate(zip(weights, biases)):
-        h = F.linear(h, w, b)
+        h = F.linear(rnd(h), rnd(w), b)
         h = _act(out_act if i == n - 1 else hidden_act, h)
     return h
 

@@ -207,6 +207,17 @@ def allreduce_grads(params: Iterable[torch.nn.Parameter]) -> None:
         off += n
 
 
+def allreduce_grads_flat(flat: torch.Tensor) -> None:
+    """Mean all-reduce of one flat gradient vector in place (one collective)."""
+    if world_size() <= 1:
+        return
+    flat.mul_(1.0 / world_size())
+    buf = _comm_device(flat)
+    tdist.all_reduce(buf)
+    if buf is not flat:
+        flat.copy_(buf)
+
+
 def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
     """Broadcast all parameters and buffers from ``src`` (one flat message per dtype)."""
     if world_size() <= 1:

@@ -1,0 +1,152 @@
+"""Device engine kernels vs host/PyTorch references (GPU only)."""
+
+import os
+
+import numpy as np
+import pytest
+import torch as th
+
+gpu = pytest.mark.gpu
+
+
+def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epochs=2, seed=0, discrete=False):
+    from imitation_amd.data import rollout
+    from imitation_amd.engine.gail import DeviceGAIL
+    from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
+    from imitation_amd.rewards.reward_nets import BasicRewardNet, NormalizedRewardNet
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.util import logger
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    th.manual_seed(seed)
+    np.random.seed(seed)
+    rng = np.random.default_rng(seed)
+    venv = make_vec_env(env_id, rng=rng, n_envs=n_envs)
+    demo_env = make_vec_env(env_id, rng=np.random.default_rng(7), n_envs=4)
+    demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
+    gen = PPO(FeedForward32Policy, venv, n_steps=n_steps, batch_size=batch, n_epochs=n_epochs, device="cuda", seed=seed,
+              ent_coef=0.01, policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+    rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
+    tr = DeviceGAIL(demonstrations=demos, demo_batch_size=256, venv=venv, gen_algo=gen, reward_net=rn,
+                    n_disc_updates_per_round=1, custom_logger=logger.configure("/tmp/ia_test_engine", format_strs=[]))
+    return tr, venv, gen, rn
+
+
+@gpu
+def test_rollout_matches_host_env_policy_and_reward():
+    from imitation_amd.envs.vec_env import NativeVecEnv
+
+    tr, venv, gen, rn = _setup()
+    nat = tr._native
+    st0 = {k: v.copy() for k, v in nat.get_state().items()}
+    obs0 = tr.cur_obs.cpu().numpy().copy()
+    tr._rollout()
+    th.cuda.synchronize()
+    b = {k: v.cpu().numpy() for k, v in tr.buf.items()}
+    T, N = b["dones"].shape
+    # 1) env: replay the device's env actions on the host runtime
+    nat.set_state(st0)
+    obs = obs0
+    for t in range(T):
+        np.testing.assert_allclose(b["obs_buf"][t], obs, rtol=2e-3, atol=2e-3)
+        o, r, d, infos = nat.step(b["act_env"][t])
+        np.testing.assert_allclose(b["env_rew"][t], r, rtol=2e-3, atol=2e-3)
+        assert (b["dones"][t] > 0.5).tolist() == d.tolist()
+        nxt = np.stack([infos[i]["terminal_observation"] if d[i] else o[i] for i in range(N)])
+        np.testing.assert_allclose(b["next_obs"][t], nxt, rtol=2e-3, atol=2e-3)
+        obs = o
+    # 2) policy log-prob / value of the stored samples (fp32 torch reference)
+    os.environ["IMITATION_AMD_FUSED"] = "0"
+    try:
+        pol = gen.policy
+        pol.set_training_mode(False)
+        with th.no_grad():
+            o_t = th.as_tensor(b["obs_buf"].reshape(T * N, -1), device="cuda")
+            a_t = th.as_tensor(b["act_raw"].reshape(T * N, -1), device="cuda")
+            v, lp, _ = pol.evaluate_actions(o_t, a_t)
+        np.testing.assert_allclose(lp.cpu().numpy(), b["logp"].reshape(-1), rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(v.cpu().numpy().reshape(-1), b["values"].reshape(-1), rtol=1e-4, atol=1e-4)
+        # 3) learned reward = GAIL reward_train on (s, a_env, s', done) (+ bootstrap only on truncation)
+        rew = tr.reward_train.predict(b["obs_buf"].reshape(T * N, -1), b["act_env"].reshape(T * N, -1),
+                                      b["next_obs"].reshape(T * N, -1), b["dones"].reshape(-1) > 0.5)
+        np.testing.assert_allclose(rew, b["rewards"].reshape(-1), rtol=1e-4, atol=1e-4)
+    finally:
+        os.environ.pop("IMITATION_AMD_FUSED", None)
+
+
+def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, norm_count):
+    """PyTorch fp32 PPO update with a fixed permutation (SB3 semantics)."""
+    import torch.nn.functional as F
+
+    pol = gen.policy
+    pol.set_training_mode(True)
+    params = list(pol.parameters())
+    opt = th.optim.Adam(params, lr=lr, eps=1e-5)
+    B = gen.batch_size
+    rows = obs.shape[0]
+    for e in range(perm.shape[0]):
+        for mb in range(rows // B):
+            idx = perm[e, mb * B:(mb + 1) * B].long()
+            v, lp, ent = pol.evaluate_actions(obs[idx], acts[idx])
+            v = v.flatten()
+            a = adv[idx]
+            a = (a - a.mean()) / (a.std() + 1e-8)
+            ratio = th.exp(lp - old_logp[idx])
+            pl = -th.min(a * ratio, a * th.clamp(ratio, 1 - clip, 1 + clip)).mean()
+            vl = F.mse_loss(ret[idx], v)
+            el = -th.mean(ent)
+            loss = pl + gen.ent_coef * el + gen.vf_coef * vl
+            opt.zero_grad()
+            loss.backward()
+            th.nn.utils.clip_grad_norm_(params, gen.max_grad_norm)
+            opt.step()
+
+
+@gpu
+def test_ppo_kernel_matches_torch_reference():
+    tr, venv, gen, rn = _setup(n_envs=4, n_steps=32, batch=64, n_epochs=2)
+    tr._rollout()
+    pol = gen.policy
+    norm = pol.features_extractor.normalize
+    p0 = [p.detach().clone() for p in pol.parameters()]
+    n0 = (norm.running_mean.clone(), norm.running_var.clone(), norm.count.clone())
+    # device update with a known permutation
+    rows = tr.T * tr.N
+    th.manual_seed(123)
+    tr._ppo_update()
+    p_dev = [p.detach().clone() for p in pol.parameters()]
+    mean_dev, var_dev = norm.running_mean.clone(), norm.running_var.clone()
+    # reference: restore and replay with the same permutation
+    th.manual_seed(123)
+    perm = th.stack([th.randperm(rows, device="cuda") for _ in range(gen.n_epochs)])
+    with th.no_grad():
+        for p, q in zip(pol.parameters(), p0):
+            p.copy_(q)
+        norm.running_mean.copy_(n0[0]); norm.running_var.copy_(n0[1]); norm.count.copy_(n0[2])
+    from imitation_amd.ops import rl as rl_ops
+
+    adv, ret = rl_ops.gae_reference(*(x.cpu() for x in (tr.buf["rewards"], tr.buf["values"], tr.buf["starts"], tr.buf["last_values"], tr.cur_start)), gen.gamma, gen.gae_lambda)
+    os.environ["IMITATION_AMD_FUSED"] = "0"
+    try:
+        _torch_ppo_reference(gen, tr.buf["obs_buf"].reshape(rows, -1), tr.buf["act_raw"].reshape(rows, -1),
+                             tr.buf["logp"].reshape(rows), adv.reshape(rows).cuda(), ret.reshape(rows).cuda(), perm,
+                             clip=float(gen.clip_range(1.0)), lr=float(gen.lr_schedule(1.0)), norm_count=None)
+    finally:
+        os.environ.pop("IMITATION_AMD_FUSED", None)
+    th.testing.assert_close(norm.running_mean, mean_dev, rtol=1e-5, atol=1e-5)
+    th.testing.assert_close(norm.running_var, var_dev, rtol=1e-4, atol=1e-5)
+    for q_ref, q_dev in zip(pol.parameters(), p_dev):
+        th.testing.assert_close(q_ref.detach(), q_dev, rtol=2e-3, atol=2e-4)
+
+
+@gpu
+def test_device_gail_rounds_run_and_learn_something():
+    tr, venv, gen, rn = _setup(n_envs=8, n_steps=64, batch=64, n_epochs=2)
+    before = [p.detach().clone() for p in gen.policy.parameters()]
+    tr.train(3 * tr.gen_train_timesteps)
+    th.cuda.synchronize()
+    after = list(gen.policy.parameters())
+    assert any(not th.equal(a, b) for a, b in zip(after, before))
+    assert all(th.isfinite(p).all() for p in after)
+    assert tr._gen_dev.size() > 0

@@ -54,17 +54,22 @@ def test_tmlp_forward_backward_matches_fp32(dims, act, B, norm):
     wr = [w.detach().clone().requires_grad_(True) for w in ws]
     br = [b.detach().clone().requires_grad_(True) for b in bs]
     xr = x.detach().clone().requires_grad_(True)
-    yr = mlp_ops.tmlp_reference(xr, wr, br, act, 0, mean, var)
+    yr = mlp_ops.tmlp_reference(xr, wr, br, act, 0, mean, var, emulate_bf16_operands=True)
     scale = yr.abs().max().item() + 1e-3
     # bf16 operands, fp32 accumulation: relative error ~ 2^-8 per layer
     assert (y - yr).abs().max().item() <= 3e-2 * scale
     gy = th.randn_like(y)
     (y * gy).sum().backward()
     (yr * gy).sum().backward()
-    for a, b in list(zip(ws, wr)) + list(zip(bs, br)) + [(x, xr)]:
-        err = (a.grad - b.grad).abs().max().item()
-        ref = b.grad.abs().max().item() + 1e-3
-        assert err <= 5e-2 * ref, (err, ref)
+    # per layer, errors are measured against the layer's largest gradient entry (a bias
+    # gradient is a sum over the batch and may cancel to ~0 while its terms do not)
+    for l in range(len(ws)):
+        ref = max(wr[l].grad.abs().max().item(), br[l].grad.abs().max().item()) + 1e-3
+        for a, b in ((ws[l], wr[l]), (bs[l], br[l])):
+            err = (a.grad - b.grad).abs().max().item()
+            assert err <= 3e-2 * ref, (l, err, ref)
+    err = (x.grad - xr.grad).abs().max().item()
+    assert err <= 3e-2 * (xr.grad.abs().max().item() + 1e-3)
 
 
 @gpu
