@@ -1,0 +1,317 @@
+"""Behavioural cloning (reference: ``src/imitation/algorithms/bc.py``).
+
+Loss ``-mean log π(a|s) - w_ent·H + w_l2·½‖θ‖²`` (``bc.py:94-156``), gradient
+accumulation over ``batch_size / minibatch_size`` minibatches (``:482-510``),
+epoch/batch iteration with end-of-epoch callbacks (``:36-77``), periodic rollout
+statistics (``:171-201``) and the ``bc/*`` metric keys (``:204-247``).
+
+:class:`MultiBC` (fork addition, ``bc.py:512-776``) concatenates the per-agent
+slices ``observation_overide(i, obs)`` / ``action_overide(i, acts)`` along the
+batch axis -- i.e. the agents are folded into the GEMM M dimension and the whole
+homogeneous team is one fused forward/backward.
+
+MI355X: policy heads are fused MFMA MLP kernels; minibatches come from the
+vectorised transitions loader; under data parallelism the accumulated gradient is
+averaged across ranks with one bucketed all-reduce right before ``optimizer.step``
+(hook point SURVEY §2.4: ``bc.py:464-466``).
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import itertools
+from typing import Any, Callable, Dict, Iterable, Iterator, Mapping, Optional, Tuple, Type, Union
+
+import numpy as np
+import torch as th
+
+from imitation_amd.algorithms import base as algo_base
+from imitation_amd.data import rollout, types
+from imitation_amd.envs import spaces
+from imitation_amd.parallel import dist as pdist
+from imitation_amd.policies import base as policy_base
+from imitation_amd.rl import torch_layers
+from imitation_amd.rl.policies import ActorCriticPolicy, get_device
+from imitation_amd.util import logger as imit_logger
+from imitation_amd.util import util
+
+
+@dataclasses.dataclass(frozen=True)
+class BatchIteratorWithEpochEndCallback:
+    """Loops through batches from a batch loader and calls a callback after every epoch."""
+
+    batch_loader: Iterable[types.TransitionMapping]
+    n_epochs: Optional[int]
+    n_batches: Optional[int]
+    on_epoch_end: Optional[Callable[[int], None]]
+
+    def __post_init__(self) -> None:
+        both = self.n_epochs is not None and self.n_batches is not None
+        neither = self.n_epochs is None and self.n_batches is None
+        if both or neither:
+            raise ValueError("Must provide exactly one of `n_epochs` and `n_batches` arguments.")
+
+    def __iter__(self) -> Iterator[types.TransitionMapping]:
+        def batch_iterator() -> Iterator[types.TransitionMapping]:
+            for epoch_num in itertools.islice(itertools.count(), self.n_epochs):
+                yielded = False
+                for batch in self.batch_loader:
+                    yield batch
+                    yielded = True
+                if not yielded:
+                    raise AssertionError(f"Data loader returned no data during epoch {epoch_num} -- did it reset correctly?")
+                if self.on_epoch_end is not None:
+                    self.on_epoch_end(epoch_num)
+
+        return itertools.islice(batch_iterator(), self.n_batches)
+
+
+@dataclasses.dataclass(frozen=True)
+class BCTrainingMetrics:
+    """Container for the different components of behavior cloning loss."""
+
+    neglogp: th.Tensor
+    entropy: Optional[th.Tensor]
+    ent_loss: th.Tensor
+    prob_true_act: th.Tensor
+    l2_norm: th.Tensor
+    l2_loss: th.Tensor
+    loss: th.Tensor
+
+
+@dataclasses.dataclass(frozen=True)
+class BehaviorCloningLossCalculator:
+    """Functor to compute the loss used in Behavior Cloning."""
+
+    ent_weight: float
+    l2_weight: float
+
+    def __call__(self, policy: ActorCriticPolicy, obs, acts) -> BCTrainingMetrics:
+        tensor_obs = types.map_maybe_dict(util.safe_to_tensor, types.maybe_unwrap_dictobs(obs))
+        acts = util.safe_to_tensor(acts)
+        _, log_prob, entropy = policy.evaluate_actions(tensor_obs, acts)
+        prob_true_act = th.exp(log_prob).mean()
+        log_prob = log_prob.mean()
+        entropy = entropy.mean() if entropy is not None else None
+        params = [w for w in policy.parameters()]
+        l2_norm = th.stack([th.sum(th.square(w)) for w in params]).sum() / 2 if params else th.zeros(())
+        ent_loss = -self.ent_weight * (entropy if entropy is not None else th.zeros(1, device=log_prob.device))
+        neglogp = -log_prob
+        l2_loss = self.l2_weight * l2_norm
+        loss = neglogp + ent_loss + l2_loss
+        return BCTrainingMetrics(neglogp=neglogp, entropy=entropy, ent_loss=ent_loss, prob_true_act=prob_true_act,
+                                 l2_norm=l2_norm, l2_loss=l2_loss, loss=loss)
+
+
+def enumerate_batches(batch_it: Iterable[types.TransitionMapping]) -> Iterable[Tuple[Tuple[int, int, int], types.TransitionMapping]]:
+    """Prepends batch stats before the batches of a batch iterator."""
+    num_samples_so_far = 0
+    for num_batches, batch in enumerate(batch_it):
+        batch_size = len(batch["obs"])
+        num_samples_so_far += batch_size
+        yield (num_batches, batch_size, num_samples_so_far), batch
+
+
+@dataclasses.dataclass(frozen=True)
+class RolloutStatsComputer:
+    """Computes statistics about rollouts (for logging during BC)."""
+
+    venv: Optional[Any]
+    n_episodes: int
+
+    def __call__(self, policy, rng: np.random.Generator) -> Mapping[str, float]:
+        if self.venv is not None and self.n_episodes > 0:
+            trajs = rollout.generate_trajectories(policy, self.venv, rollout.make_min_episodes(self.n_episodes), rng=rng)
+            return rollout.rollout_stats(trajs)
+        return dict()
+
+
+class BCLogger:
+    """Utility class to help logging information relevant to Behavior Cloning."""
+
+    def __init__(self, logger: imit_logger.HierarchicalLogger):
+        self._logger = logger
+        self._tensorboard_step = 0
+        self._current_epoch = 0
+
+    def reset_tensorboard_steps(self):
+        self._tensorboard_step = 0
+
+    def log_epoch(self, epoch_number):
+        self._current_epoch = epoch_number
+
+    def log_batch(self, batch_num: int, batch_size: int, num_samples_so_far: int, training_metrics: BCTrainingMetrics,
+                  rollout_stats: Mapping[str, float]):
+        self._logger.record("batch_size", batch_size)
+        self._logger.record("bc/epoch", self._current_epoch)
+        self._logger.record("bc/batch", batch_num)
+        self._logger.record("bc/samples_so_far", num_samples_so_far)
+        vals = {k: v for k, v in training_metrics.__dict__.items()}
+        tens = [v.detach().reshape(-1)[0] for v in vals.values() if v is not None]
+        host = th.stack(tens).tolist() if tens else []
+        it = iter(host)
+        for k, v in vals.items():
+            self._logger.record(f"bc/{k}", float(next(it)) if v is not None else None)
+        for k, v in rollout_stats.items():
+            if "return" in k and "monitor" not in k:
+                self._logger.record("rollout/" + k, v)
+        self._logger.dump(self._tensorboard_step)
+        self._tensorboard_step += 1
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        del state["_logger"]
+        return state
+
+
+def reconstruct_policy(policy_path: str, device: Union[th.device, str] = "auto") -> ActorCriticPolicy:
+    """Reconstruct a saved policy (``util.save_policy`` / ``final.th``). The file is our own output."""
+    policy = th.load(policy_path, map_location=get_device(device), weights_only=False)
+    assert isinstance(policy, ActorCriticPolicy)
+    return policy
+
+
+class _BCBase(algo_base.DemonstrationAlgorithm):
+    """Shared training loop of BC and MultiBC."""
+
+    def _init_common(self, batch_size, minibatch_size, demonstrations, custom_logger):
+        self._demo_data_loader: Optional[Iterable[types.TransitionMapping]] = None
+        self.batch_size = batch_size
+        self.minibatch_size = minibatch_size or batch_size
+        if self.batch_size % self.minibatch_size != 0:  # pragma: no cover
+            raise ValueError("Batch size must be a multiple of minibatch size.")
+        algo_base.DemonstrationAlgorithm.__init__(self, demonstrations=demonstrations, custom_logger=custom_logger)
+        self._bc_logger = BCLogger(self.logger)
+
+    def _init_optimizer(self, optimizer_cls, optimizer_kwargs, ent_weight, l2_weight):
+        if optimizer_kwargs and "weight_decay" in optimizer_kwargs:  # pragma: no cover
+            raise ValueError("Use the parameter l2_weight instead of weight_decay.")
+        self.optimizer = optimizer_cls(self.policy.parameters(), **(optimizer_kwargs or {}))
+        self.loss_calculator = BehaviorCloningLossCalculator(ent_weight, l2_weight)
+        pdist.broadcast_module(self._policy)
+        self._grad_bucket = pdist.GradBucket(self.policy.parameters()) if pdist.world_size() > 1 else None
+
+    @property
+    def policy(self) -> ActorCriticPolicy:
+        return self._policy
+
+    def set_demonstrations(self, demonstrations: algo_base.AnyTransitions) -> None:
+        self._demo_data_loader = algo_base.make_data_loader(demonstrations, self.minibatch_size)
+
+    def _prepare_batch(self, batch) -> Tuple[Any, th.Tensor]:
+        obs = types.map_maybe_dict(lambda x: util.safe_to_tensor(x, device=self.policy.device), types.maybe_unwrap_dictobs(batch["obs"]))
+        acts = util.safe_to_tensor(batch["acts"], device=self.policy.device)
+        return obs, acts
+
+    def _zero_grad(self):
+        self.optimizer.zero_grad(set_to_none=self._grad_bucket is None)
+        if self._grad_bucket is not None:
+            self._grad_bucket.zero()
+
+    def train(self, *, n_epochs: Optional[int] = None, n_batches: Optional[int] = None,
+              on_epoch_end: Optional[Callable[[], None]] = None, on_batch_end: Optional[Callable[[], None]] = None,
+              log_interval: int = 500, log_rollouts_venv=None, log_rollouts_n_episodes: int = 5,
+              progress_bar: bool = True, reset_tensorboard: bool = False):
+        """Train with supervised learning for ``n_epochs`` epochs or ``n_batches`` batches."""
+        if reset_tensorboard:
+            self._bc_logger.reset_tensorboard_steps()
+        self._bc_logger.log_epoch(0)
+        compute_rollout_stats = RolloutStatsComputer(log_rollouts_venv, log_rollouts_n_episodes)
+
+        def _on_epoch_end(epoch_number: int):
+            self._bc_logger.log_epoch(epoch_number + 1)
+            if on_epoch_end is not None:
+                on_epoch_end()
+
+        mini_per_batch = self.batch_size // self.minibatch_size
+        n_minibatches = n_batches * mini_per_batch if n_batches is not None else None
+        assert self._demo_data_loader is not None
+        demonstration_batches = BatchIteratorWithEpochEndCallback(self._demo_data_loader, n_epochs, n_minibatches, _on_epoch_end)
+        batches_with_stats = enumerate_batches(demonstration_batches)
+        state: Dict[str, Any] = {}
+
+        def process_batch():
+            if self._grad_bucket is not None:
+                self._grad_bucket.allreduce()
+            self.optimizer.step()
+            self._zero_grad()
+            if state["batch_num"] % log_interval == 0:
+                rollout_stats = compute_rollout_stats(self.policy, self.rng)
+                self._bc_logger.log_batch(state["batch_num"], state["minibatch_size"], state["num_samples_so_far"],
+                                          state["metrics"], rollout_stats)
+            if on_batch_end is not None:
+                on_batch_end()
+
+        self._zero_grad()
+        num_samples_so_far = 0
+        for (batch_num, minibatch_size, num_samples_so_far), batch in batches_with_stats:
+            obs, acts = self._prepare_batch(batch)
+            metrics = self.loss_calculator(self.policy, obs, acts)
+            loss = metrics.loss * minibatch_size / self.batch_size
+            loss.backward()
+            batch_num = batch_num * self.minibatch_size // self.batch_size
+            state.update(batch_num=batch_num, minibatch_size=minibatch_size, num_samples_so_far=num_samples_so_far, metrics=metrics)
+            if num_samples_so_far % self.batch_size == 0:
+                process_batch()
+        if num_samples_so_far % self.batch_size != 0 and state:
+            state["batch_num"] += 1
+            process_batch()
+
+
+class BC(_BCBase):
+    """Behavioral cloning (BC): supervised learning of the expert's actions."""
+
+    def __init__(self, *, observation_space: spaces.Space, action_space: spaces.Space, rng: np.random.Generator,
+                 policy: Optional[ActorCriticPolicy] = None, demonstrations: Optional[algo_base.AnyTransitions] = None,
+                 batch_size: int = 32, minibatch_size: Optional[int] = None,
+                 optimizer_cls: Type[th.optim.Optimizer] = th.optim.Adam, optimizer_kwargs: Optional[Mapping[str, Any]] = None,
+                 ent_weight: float = 1e-3, l2_weight: float = 0.0, device: Union[str, th.device] = "auto",
+                 custom_logger: Optional[imit_logger.HierarchicalLogger] = None):
+        self._init_common(batch_size, minibatch_size, demonstrations, custom_logger)
+        self.action_space = action_space
+        self.observation_space = observation_space
+        self.rng = rng
+        if policy is None:
+            extractor = torch_layers.CombinedExtractor if isinstance(observation_space, spaces.Dict) else torch_layers.FlattenExtractor
+            policy = policy_base.FeedForward32Policy(observation_space=observation_space, action_space=action_space,
+                                                     lr_schedule=lambda _: th.finfo(th.float32).max,
+                                                     features_extractor_class=extractor)
+        self._policy = policy.to(get_device(device))
+        assert self.policy.observation_space == self.observation_space
+        assert self.policy.action_space == self.action_space
+        self._init_optimizer(optimizer_cls, optimizer_kwargs, ent_weight, l2_weight)
+
+
+class MultiBC(_BCBase):
+    """BC for N parameter-shared homogeneous agents (fork addition, ``bc.py:512-776``)."""
+
+    def __init__(self, *, single_agent_observation_space, single_agent_action_space, observation_overide, action_overide,
+                 num_agents, rng: np.random.Generator, policy: Optional[ActorCriticPolicy] = None,
+                 demonstrations: Optional[algo_base.AnyTransitions] = None, batch_size: int = 32,
+                 minibatch_size: Optional[int] = None, optimizer_cls: Type[th.optim.Optimizer] = th.optim.Adam,
+                 optimizer_kwargs: Optional[Mapping[str, Any]] = None, ent_weight: float = 1e-3, l2_weight: float = 0.0,
+                 device: Union[str, th.device] = "auto", custom_logger: Optional[imit_logger.HierarchicalLogger] = None):
+        self._init_common(batch_size, minibatch_size, demonstrations, custom_logger)
+        self.action_space = single_agent_action_space
+        self.observation_space = single_agent_observation_space
+        self.observation_overide = observation_overide
+        self.action_overide = action_overide
+        self.num_agents = num_agents
+        self.rng = rng
+        if policy is None:
+            extractor = torch_layers.CombinedExtractor if isinstance(single_agent_observation_space, spaces.Dict) else torch_layers.FlattenExtractor
+            policy = policy_base.HomogenousFeedForward32Policy(
+                observation_space=self.observation_space, action_space=self.action_space,
+                observation_overide=self.observation_overide, action_overide=self.action_overide,
+                num_agents=self.num_agents, lr_schedule=lambda _: th.finfo(th.float32).max,
+                features_extractor_class=extractor)
+        self._policy = policy.to(get_device(device))
+        assert self.policy.observation_space == self.observation_space
+        assert self.policy.action_space == self.action_space
+        self._init_optimizer(optimizer_cls, optimizer_kwargs, ent_weight, l2_weight)
+
+    def _prepare_batch(self, batch):
+        obs_all, acts_all = super()._prepare_batch(batch)
+        obs = th.cat([self.observation_overide(i, obs_all) for i in range(self.num_agents)])
+        acts = th.cat([self.action_overide(i, acts_all) for i in range(self.num_agents)])
+        return obs, acts

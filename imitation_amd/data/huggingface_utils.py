@@ -1,0 +1,132 @@
+"""HuggingFace ``datasets`` adapter for trajectories (reference: ``src/imitation/data/huggingface_utils.py``).
+
+Columns: ``obs`` [T+1, ...], ``acts`` [T, ...], ``infos`` (one JSON string per
+step), ``terminal``, optional ``rews``. ``jsonpickle`` is not
+installed here; :func:`encode_info` / :func:`decode_info` implement the subset of
+its wire format that trajectory infos use (plain JSON values, ``py/tuple``,
+numpy arrays as ``py/object: numpy.ndarray``), so files are interchangeable for
+plain-dict infos.
+"""
+
+from __future__ import annotations
+
+import json
+from typing import Any, Dict, Iterable, Optional, Sequence, cast
+
+import datasets
+import numpy as np
+
+from imitation_amd.data import types
+
+
+def _to_jsonable(v: Any) -> Any:
+    if isinstance(v, dict):
+        return {str(k): _to_jsonable(x) for k, x in v.items()}
+    if isinstance(v, tuple):
+        return {"py/tuple": [_to_jsonable(x) for x in v]}
+    if isinstance(v, list):
+        return [_to_jsonable(x) for x in v]
+    if isinstance(v, np.ndarray):
+        return {"py/object": "numpy.ndarray", "dtype": str(v.dtype), "shape": list(v.shape),
+                "values": _to_jsonable(v.reshape(-1).tolist())}
+    if isinstance(v, (np.bool_,)):
+        return bool(v)
+    if isinstance(v, np.integer):
+        return int(v)
+    if isinstance(v, np.floating):
+        return float(v)
+    if isinstance(v, float) and (np.isnan(v) or np.isinf(v)):
+        return {"py/float": repr(v)}
+    return v
+
+
+def _from_jsonable(v: Any) -> Any:
+    if isinstance(v, dict):
+        if "py/tuple" in v:
+            return tuple(_from_jsonable(x) for x in v["py/tuple"])
+        if v.get("py/object") == "numpy.ndarray" and "values" in v:
+            arr = np.asarray(_from_jsonable(v["values"]), dtype=v.get("dtype", None))
+            return arr.reshape(v.get("shape", arr.shape))
+        if "py/float" in v:
+            return float(v["py/float"])
+        return {k: _from_jsonable(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_from_jsonable(x) for x in v]
+    return v
+
+
+def encode_info(info: Dict[str, Any]) -> str:
+    return json.dumps(_to_jsonable(info))
+
+
+def decode_info(s: str) -> Any:
+    return _from_jsonable(json.loads(s))
+
+
+class TrajectoryDatasetSequence(Sequence[types.Trajectory]):
+    """A sequence of trajectories lazily backed by a HuggingFace dataset."""
+
+    def __init__(self, dataset: datasets.Dataset):
+        def numpy_transform(batch):
+            return {key: np.asarray(val) if key != "infos" else val for key, val in batch.items()}
+
+        self._dataset = dataset.with_transform(numpy_transform)
+        self._trajectory_class = types.TrajectoryWithRew if "rews" in dataset.features else types.Trajectory
+
+    def __len__(self) -> int:
+        return len(self._dataset)
+
+    def __getitem__(self, idx):
+        if isinstance(idx, slice):
+            return [self[i] for i in range(*idx.indices(len(self)))]
+        kwargs = self._dataset[idx]
+        kwargs["infos"] = _LazyDecodedList(kwargs["infos"])
+        return self._trajectory_class(**kwargs)
+
+    @property
+    def dataset(self):
+        return self._dataset.with_transform(None)
+
+
+class _LazyDecodedList(Sequence[Any]):
+    """A list of JSON-encoded infos decoded on access (and cached)."""
+
+    def __init__(self, encoded_list: Sequence[str]):
+        self._encoded_list = encoded_list
+        self._decoded_cache: Dict[int, Any] = {}
+
+    def __len__(self):
+        return len(self._encoded_list)
+
+    def __getitem__(self, idx):
+        if isinstance(idx, slice):
+            return [self[i] for i in range(*idx.indices(len(self)))]
+        if idx < 0:
+            idx += len(self)
+        if idx not in self._decoded_cache:
+            self._decoded_cache[idx] = decode_info(self._encoded_list[idx])
+        return self._decoded_cache[idx]
+
+
+def trajectories_to_dict(trajectories: Sequence[types.Trajectory]) -> Dict[str, Sequence[Any]]:
+    has_reward = [isinstance(t, types.TrajectoryWithRew) for t in trajectories]
+    all_rew = all(has_reward)
+    if not all_rew and any(has_reward):
+        raise ValueError("Some trajectories have rewards but not all")
+    if any(isinstance(t.obs, types.DictObs) for t in trajectories):
+        raise ValueError("DictObs are not currently supported")
+    d: Dict[str, Sequence[Any]] = dict(
+        obs=[t.obs for t in trajectories],
+        acts=[t.acts for t in trajectories],
+        infos=[[encode_info(i) for i in (t.infos if t.infos is not None else [{}] * len(t))] for t in trajectories],
+        terminal=[t.terminal for t in trajectories],
+    )
+    if all_rew:
+        d["rews"] = [cast(types.TrajectoryWithRew, t).rews for t in trajectories]
+    return d
+
+
+def trajectories_to_dataset(trajectories: Sequence[types.Trajectory], info: Optional[datasets.DatasetInfo] = None) -> datasets.Dataset:
+    if isinstance(trajectories, TrajectoryDatasetSequence):
+        return trajectories.dataset
+    return datasets.Dataset.from_dict(trajectories_to_dict(trajectories), info=info)
