@@ -96,6 +96,7 @@ void rollout(py::dict d) {
   a.next_obs = tptr<float>(d, "next_obs");
   a.ep_ret_out = tptr<float>(d, "ep_ret_out");
   a.last_values = tptr<float>(d, "last_values");
+  a.prof = tptr<unsigned long long>(d, "prof", true);
   IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
 }
 
@@ -152,6 +153,7 @@ void ppo_update(py::dict d) {
   a.stats = tptr<float>(d, "stats");
   a.mode = ival(d, "mode", 0);
   a.mb_index = ival(d, "mb_index", 0);
+  a.prof = tptr<unsigned long long>(d, "prof", true);
   TORCH_CHECK(a.D <= 64, "obs dim <= 64");
   IA_HIP_CHECK2(ia::ppo_launch(a, ia_stream()));
 }

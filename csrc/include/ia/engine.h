@@ -70,6 +70,7 @@ struct RolloutArgs {
   float* next_obs;  // terminal obs on done
   float* ep_ret_out;  // episode return where done
   float* last_values;  // [N]
+  unsigned long long* prof;  // optional [N][4] cycle counters: policy, env, reward, other
 };
 
 // One PPO update (all epochs x minibatches) in one persistent workgroup.
@@ -112,6 +113,7 @@ struct PPOArgs {
   float* stats;
   int mode;  // 0: full persistent update; 1: one minibatch -> grads only; 2: apply clip+Adam from grads
   int mb_index;  // minibatch index for mode 1 (epoch * n_mb + mb)
+  unsigned long long* prof;  // optional [10] cycle counters per phase
 };
 
 }  // namespace ia

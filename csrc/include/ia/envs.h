@@ -21,6 +21,20 @@
 
 #include "ia/rng.h"
 
+// Transcendentals of the env models: full-precision libm on the host runtime, the
+// hardware fast paths (v_exp_f32 / v_sin_f32 based) inside the device rollout,
+// where the serial per-env chain is the latency bottleneck. Results agree to
+// ~1e-6 relative per call; tests compare host vs device trajectories with a tolerance.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define IA_EXPF(x) __expf(x)
+#define IA_SINF(x) __sinf(x)
+#define IA_COSF(x) __cosf(x)
+#else
+#define IA_EXPF(x) expf(x)
+#define IA_SINF(x) sinf(x)
+#define IA_COSF(x) cosf(x)
+#endif
+
 namespace ia {
 
 enum EnvKind : int {
@@ -216,7 +230,7 @@ IA_HD void loco_obs(const LocoParams& p, const float* s, float* o) {
 }
 
 IA_HD float stance(float q) {  // smooth contact indicator: foot on ground when q < 0
-  return 1.0f / (1.0f + expf(8.0f * q));
+  return 1.0f / (1.0f + IA_EXPF(8.0f * q));
 }
 
 IA_HD float loco_step(const LocoParams& p, float* s, const float* a_in) {
@@ -236,7 +250,7 @@ IA_HD float loco_step(const LocoParams& p, float* s, const float* a_in) {
     for (int j = 0; j < p.nj; ++j) {
       float q = qpos[jq + j], qd = qvel[jv + j];
       // actuated, damped, spring-loaded hinge with a gravity-like nonlinearity
-      float qdd = p.gear[j] * a[j] - p.stiff[j] * q - p.damp[j] * qd - 2.0f * sinf(q);
+      float qdd = p.gear[j] * a[j] - p.stiff[j] * q - p.damp[j] * qd - 2.0f * IA_SINF(q);
       qvel[jv + j] = qd + p.dt * qdd;
       float st = stance(q);
       // a stance foot sweeping backwards (qd < 0) pushes the body forward
@@ -254,7 +268,7 @@ IA_HD float loco_step(const LocoParams& p, float* s, const float* a_in) {
     }
     if (p.nv_root > 2) {  // pitch: torsional spring driven by joint torques
       float th = qpos[2], vth = qvel[2];
-      float th_dd = -15.f * sinf(th) - 3.f * vth + pitch_torque;
+      float th_dd = -15.f * IA_SINF(th) - 3.f * vth + pitch_torque;
       qvel[2] = vth + p.dt * th_dd;
     }
     for (int i = 3; i < p.nv_root; ++i) {  // extra root dofs: damped, weakly driven

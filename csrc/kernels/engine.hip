@@ -24,35 +24,50 @@
 namespace ia {
 namespace {
 
-constexpr int kW = 64;  // transposed-weight row stride (one slot per lane)
+constexpr int kW = 64;  // one weight slot per lane
 
+// LDS pointers typed address_space(3) (32-bit, ds_read/ds_write).
+typedef __attribute__((address_space(3))) float lf;
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f32v4 lf4;
+
+__host__ __device__ __forceinline__ int ceil8(int x) { return (x + 7) & ~7; }
+
+// Weight image of one layer: [ceil8(din)/4][64 lanes][4 k] so lane j fetches the
+// weights of 4 consecutive inputs of unit j with one ds_read_b128; zero-padded.
 struct LdsMLP {
   int n_layers;
   int dims[kWaveMaxLayers + 1];
   int hidden_act, out_act;
-  float* WT[kWaveMaxLayers];  // [din][kW]
-  float* b[kWaveMaxLayers];   // [kW]
-  float* mean;                // [kW] or null
-  float* rstd;                // [kW]
+  lf* WT[kWaveMaxLayers];
+  lf* b[kWaveMaxLayers];  // [kW]
+  lf* mean;               // [kW] or null
+  lf* rstd;               // [kW]
 };
 
-__device__ float* load_mlp(const WaveMLP& m, LdsMLP& out, float* lds) {
+__device__ __forceinline__ int wt_index(int k, int j) { return ((k >> 2) * kW + j) * 4 + (k & 3); }
+
+__device__ lf* load_mlp(const WaveMLP& m, LdsMLP& out, lf* lds) {
   out.n_layers = m.n_layers;
   out.hidden_act = m.hidden_act;
   out.out_act = m.out_act;
-  for (int l = 0; l <= m.n_layers; ++l) out.dims[l] = m.dims[l];
+#pragma unroll
+  for (int l = 0; l <= kWaveMaxLayers; ++l) out.dims[l] = l <= m.n_layers ? m.dims[l] : 0;
   const int lane = threadIdx.x;
-  for (int l = 0; l < m.n_layers; ++l) {
-    const int din = m.dims[l], dout = m.dims[l + 1];
-    out.WT[l] = lds;
-    for (int e = lane; e < din * kW; e += 64) {
-      const int k = e / kW, j = e - k * kW;
-      lds[e] = j < dout ? m.W[l][j * din + k] : 0.f;
+#pragma unroll
+  for (int l = 0; l < kWaveMaxLayers; ++l) {
+    if (l < m.n_layers) {
+      const int din = m.dims[l], dout = m.dims[l + 1], dp = ceil8(din);
+      out.WT[l] = lds;
+      for (int k = 0; k < dp; ++k) lds[wt_index(k, lane)] = (lane < dout && k < din) ? m.W[l][lane * din + k] : 0.f;
+      lds += dp * kW;
+      out.b[l] = lds;
+      lds[lane] = lane < dout ? m.b[l][lane] : 0.f;
+      lds += kW;
+    } else {
+      out.WT[l] = nullptr;
+      out.b[l] = nullptr;
     }
-    lds += din * kW;
-    out.b[l] = lds;
-    lds[lane] = lane < dout ? m.b[l][lane] : 0.f;
-    lds += kW;
   }
   if (m.norm_mean) {
     out.mean = lds;
@@ -72,26 +87,159 @@ __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
+// acc_j += sum_k W[j][k] * x_k, x_k = readlane(h, k) (k uniform), 8 inputs per step:
+// both 16-byte weight fetches are issued before the FMA chain.
+__device__ __forceinline__ float layer_dot(const lf* WT, int din, float h, float acc) {
+  const lf4* w4 = (const lf4*)WT + threadIdx.x;
+  const int dp = ceil8(din);
+  for (int k = 0; k < dp; k += 8) {
+    const f32v4 w0 = w4[(k >> 2) * kW], w1 = w4[((k >> 2) + 1) * kW];
+    acc = fmaf(w0.x, bcast(h, k + 0), acc);
+    acc = fmaf(w0.y, bcast(h, k + 1), acc);
+    acc = fmaf(w0.z, bcast(h, k + 2), acc);
+    acc = fmaf(w0.w, bcast(h, k + 3), acc);
+    acc = fmaf(w1.x, bcast(h, k + 4), acc);
+    acc = fmaf(w1.y, bcast(h, k + 5), acc);
+    acc = fmaf(w1.z, bcast(h, k + 6), acc);
+    acc = fmaf(w1.w, bcast(h, k + 7), acc);
+  }
+  return acc;
+}
+
+// Fast tanh for the rollout policy/reward nets (|err| ~1e-7 abs).
+__device__ __forceinline__ float act_fast(int act, float x) {
+  if (act == ACT_TANH) {
+    const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
+    return 1.f - 2.f / (e + 1.f);
+  }
+  return apply_act(act, x);
+}
+
 // Lane j of x holds input feature j (j < dims[0]); returns lane j = output unit j.
+// Inputs beyond dims[0] must be zero (padded weight rows multiply them).
 __device__ float wave_mlp(const LdsMLP& m, float x) {
   const int lane = threadIdx.x;
   float h = x;
   if (m.mean) h = lane < m.dims[0] ? (h - m.mean[lane]) * m.rstd[lane] : 0.f;
-  for (int l = 0; l < m.n_layers; ++l) {
-    const int din = m.dims[l];
-    const float* WT = m.WT[l];
-    float acc = m.b[l][lane];
-    int k = 0;
-    for (; k + 4 <= din; k += 4) {
-      const float x0 = bcast(h, k), x1 = bcast(h, k + 1), x2 = bcast(h, k + 2), x3 = bcast(h, k + 3);
-      acc = fmaf(WT[(k + 0) * kW + lane], x0, acc);
-      acc = fmaf(WT[(k + 1) * kW + lane], x1, acc);
-      acc = fmaf(WT[(k + 2) * kW + lane], x2, acc);
-      acc = fmaf(WT[(k + 3) * kW + lane], x3, acc);
+#pragma unroll
+  for (int l = 0; l < kWaveMaxLayers; ++l) {
+    if (l < m.n_layers) {
+      const float acc = layer_dot(m.WT[l], m.dims[l], h, m.b[l][lane]);
+      const int act = l == m.n_layers - 1 ? m.out_act : m.hidden_act;
+      h = lane < m.dims[l + 1] ? act_fast(act, acc) : 0.f;
     }
-    for (; k < din; ++k) acc = fmaf(WT[k * kW + lane], bcast(h, k), acc);
-    const int act = l == m.n_layers - 1 ? m.out_act : m.hidden_act;
-    h = lane < m.dims[l + 1] ? apply_act(act, acc) : 0.f;
+  }
+  return h;
+}
+
+// Actor and critic evaluated together: lanes [0,32) = actor units, [32,64) = critic
+// units (both nets <= 32 wide, same depth, shared input normaliser). Halves the
+// serial k-loop of the two per-step policy evaluations.
+struct PairMLP {
+  int n_layers;
+  int din[kWaveMaxLayers];  // max(din_pi, din_vf) per layer
+  int dpi[kWaveMaxLayers + 1], dvf[kWaveMaxLayers + 1];
+  int hidden_act;
+  lf* WT[kWaveMaxLayers];
+  lf* b[kWaveMaxLayers];  // [64]
+  lf* mean;
+  lf* rstd;
+};
+
+__device__ bool pair_ok(const WaveMLP& pi, const WaveMLP& vf) {
+  if (pi.n_layers != vf.n_layers || pi.dims[0] != vf.dims[0] || pi.hidden_act != vf.hidden_act) return false;
+  for (int l = 0; l <= pi.n_layers; ++l)
+    if (pi.dims[l] > 32 || vf.dims[l] > 32) return false;
+  return true;
+}
+
+__host__ __device__ inline int pair_lds_floats(const WaveMLP& pi, const WaveMLP& vf) {
+  int f = 0;
+  for (int l = 0; l < pi.n_layers; ++l) {
+    const int din = pi.dims[l] > vf.dims[l] ? pi.dims[l] : vf.dims[l];
+    f += ceil8(din) * kW + kW;
+  }
+  return f + (pi.norm_mean ? 2 * kW : 0);
+}
+
+__device__ lf* load_pair(const WaveMLP& pi, const WaveMLP& vf, PairMLP& out, lf* lds) {
+  const int lane = threadIdx.x;
+  out.n_layers = pi.n_layers;
+  out.hidden_act = pi.hidden_act;
+#pragma unroll
+  for (int l = 0; l <= kWaveMaxLayers; ++l) {
+    out.dpi[l] = l <= pi.n_layers ? pi.dims[l] : 0;
+    out.dvf[l] = l <= vf.n_layers ? vf.dims[l] : 0;
+  }
+  const bool hi = lane >= 32;
+  const int j = hi ? lane - 32 : lane;
+#pragma unroll
+  for (int l = 0; l < kWaveMaxLayers; ++l) {
+    if (l < pi.n_layers) {
+      const int dp = pi.dims[l], dv = vf.dims[l], din = dp > dv ? dp : dv;
+      const int op = pi.dims[l + 1], ov = vf.dims[l + 1];
+      out.din[l] = din;
+      out.WT[l] = lds;
+      for (int k = 0; k < ceil8(din); ++k) {
+        float v = 0.f;
+        if (!hi && j < op && k < dp) v = pi.W[l][j * dp + k];
+        if (hi && j < ov && k < dv) v = vf.W[l][j * dv + k];
+        lds[wt_index(k, lane)] = v;
+      }
+      lds += ceil8(din) * kW;
+      out.b[l] = lds;
+      lds[lane] = !hi ? (j < op ? pi.b[l][j] : 0.f) : (j < ov ? vf.b[l][j] : 0.f);
+      lds += kW;
+    } else {
+      out.din[l] = 0;
+      out.WT[l] = nullptr;
+      out.b[l] = nullptr;
+    }
+  }
+  if (pi.norm_mean) {
+    out.mean = lds;
+    out.rstd = lds + kW;
+    const int d0 = pi.dims[0];
+    lds[lane] = lane < d0 ? pi.norm_mean[lane] : 0.f;
+    lds[kW + lane] = lane < d0 ? rsqrtf(pi.norm_var[lane] + pi.norm_eps) : 1.f;
+    lds += 2 * kW;
+  } else {
+    out.mean = nullptr;
+    out.rstd = nullptr;
+  }
+  return lds;
+}
+
+// x: lane k < dims[0] holds feature k. Returns lane j<dpi[L]: actor output j; lane 32: value.
+__device__ float pair_mlp(const PairMLP& m, float x) {
+  const int lane = threadIdx.x;
+  const bool hi = lane >= 32;
+  float h = x;
+  if (m.mean) h = lane < m.dpi[0] ? (h - m.mean[lane]) * m.rstd[lane] : 0.f;
+#pragma unroll
+  for (int l = 0; l < kWaveMaxLayers; ++l) {
+    if (l < m.n_layers) {
+      float acc = m.b[l][lane];
+      if (l == 0) {
+        acc = layer_dot(m.WT[l], m.din[l], h, acc);
+      } else {  // actor lanes read actor units (lanes k), critic lanes read critic units (32 + k)
+        const lf4* w4 = (const lf4*)m.WT[l] + lane;
+        const int dp = ceil8(m.din[l]);
+        for (int k = 0; k < dp; k += 8) {
+          const f32v4 w0 = w4[(k >> 2) * kW], w1 = w4[((k >> 2) + 1) * kW];
+          const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float lo = bcast(h, k + u), up = bcast(h, 32 + k + u);
+            acc = fmaf(wv[u], hi ? up : lo, acc);
+          }
+        }
+      }
+      const bool last = l == m.n_layers - 1;
+      const int dout = hi ? m.dvf[l + 1] : m.dpi[l + 1];
+      const int j = hi ? lane - 32 : lane;
+      h = j < dout ? (last ? acc : act_fast(m.hidden_act, acc)) : 0.f;
+    }
   }
   return h;
 }
@@ -107,6 +255,94 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Locomotion model stepped by the whole wave: joint j on lane j, root dynamics
+// computed redundantly (uniformly) by every lane, cross-joint sums taken with
+// readlane in joint order (the host runtime's summation order). Same equations as
+// ia::loco_step (csrc/include/ia/envs.h); the serial per-joint chain of the host
+// version is what made the env step the longest part of a rollout step.
+__device__ float loco_step_wave(const LocoParams& p, float* s, const float* a_in) {
+  const int lane = threadIdx.x;
+  const int nq = loco_nq(p), nj = p.nj, jq = p.nq_root, jv = p.nv_root;
+  const bool jl = lane < nj;
+  const float a = jl ? fminf(fmaxf(a_in[lane], -1.f), 1.f) : 0.f;
+  float q = jl ? s[jq + lane] : 0.f;
+  float qd = jl ? s[nq + jv + lane] : 0.f;
+  const float gear = jl ? p.gear[lane] : 0.f, stiff = jl ? p.stiff[lane] : 0.f;
+  const float damp = jl ? p.damp[lane] : 0.f, tc = jl ? p.thrust[lane] : 0.f;
+  float ctrl = 0.f, pitch = 0.f;
+  for (int j = 0; j < nj; ++j) {
+    const float aj = bcast(a, j);
+    ctrl += aj * aj;
+    pitch += p.pitch_coupling[j] * aj;
+  }
+  float rq[8], rv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    rq[i] = i < p.nq_root ? s[i] : 0.f;
+    rv[i] = i < p.nv_root ? s[nq + i] : 0.f;
+  }
+  const float x_before = rq[0];
+  const float dt = p.dt;
+  for (int sub = 0; sub < p.frame_skip; ++sub) {
+    const float qdd = gear * a - stiff * q - damp * qd - 2.0f * IA_SINF(q);
+    const float st = stance(q);
+    const float th_j = jl ? tc * st * fmaxf(-qd, 0.f) : 0.f;
+    qd = qd + dt * qdd;
+    float thrust = 0.f, lift = 0.f;
+    for (int j = 0; j < nj; ++j) {
+      thrust += bcast(th_j, j);
+      lift += bcast(st, j);
+    }
+    const float vx = rv[0];
+    rv[0] = vx + dt * (thrust - p.drag * vx * (1.0f + fabsf(vx)));
+    if (p.nv_root > 1) rv[1] = rv[1] + dt * (-20.f * rq[1] - 4.f * rv[1] + 0.5f * (lift / (float)nj - 0.5f));
+    if (p.nv_root > 2) rv[2] = rv[2] + dt * (-15.f * IA_SINF(rq[2]) - 3.f * rv[2] + pitch);
+#pragma unroll
+    for (int i = 3; i < 8; ++i)
+      if (i < p.nv_root) rv[i] = rv[i] * (1.f - 2.f * dt) + dt * 0.1f * pitch;
+    rq[0] += dt * rv[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+      if (i < p.nq_root) {
+        const int vi = i < p.nv_root ? i : (i % p.nv_root);
+        float v = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v = u == vi ? rv[u] : v;
+        rq[i] += dt * v * (i < p.nv_root ? 1.f : 0.1f);
+      }
+    }
+    float qn = q + dt * qd;
+    if (qn > 1.2f) { qn = 1.2f; if (qd > 0) qd = 0.f; }
+    if (qn < -1.2f) { qn = -1.2f; if (qd < 0) qd = 0.f; }
+    q = qn;
+  }
+  __syncthreads();
+  if (jl) {
+    s[jq + lane] = q;
+    s[nq + jv + lane] = qd;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < p.nq_root) s[i] = rq[i];
+      if (i < p.nv_root) s[nq + i] = rv[i];
+    }
+  }
+  __syncthreads();
+  const float dt_total = dt * p.frame_skip;
+  return p.fwd_weight * (rq[0] - x_before) / dt_total + p.healthy_reward - p.ctrl_cost * ctrl;
+}
+
+// Observation of a locomotion state, one feature per lane.
+__device__ float loco_obs_lane(const LocoParams& p, const float* s) {
+  const int lane = threadIdx.x;
+  const int nq = loco_nq(p), nv = loco_nv(p);
+  const int npos = nq - p.obs_skip;
+  if (lane < npos) return s[p.obs_skip + lane];
+  if (lane < npos + nv) return s[nq + lane - npos];
+  return 0.f;
+}
+
 __device__ __forceinline__ uint64_t hash3(uint64_t a, uint64_t b, uint64_t c) {
   uint64_t s = a ^ (0x9E3779B97F4A7C15ull * (b + 1)) ^ (0xC2B2AE3D27D4EB4Full * (c + 1));
   splitmix64(s);
@@ -114,7 +350,8 @@ __device__ __forceinline__ uint64_t hash3(uint64_t a, uint64_t b, uint64_t c) {
 }
 
 __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  extern __shared__ __attribute__((aligned(16))) float lds_raw[];
+  lf* lds = (lf*)lds_raw;
   const int n = blockIdx.x;
   const int lane = threadIdx.x;
   const EnvParams& P = a.P;
@@ -122,11 +359,16 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
   const int A = a.n_actions > 0 ? 1 : P.act_dim;
   const int S = state_size(P);
   LdsMLP pi, vf, rw;
-  float* p = lds;
+  PairMLP pv;
+  lf* p = lds;
+  const bool paired = pair_ok(a.pi, a.vf);
+  if (paired) p = load_pair(a.pi, a.vf, pv, p);
   p = load_mlp(a.pi, pi, p);
   p = load_mlp(a.vf, vf, p);
   if (a.rew_enabled) p = load_mlp(a.rew, rw, p);
-  float* st = p;       // [kMaxState]
+  // env state / obs / action scratch stays a generic pointer: the shared host/device
+  // env code (ia/envs.h) takes float*
+  float* st = (float*)p;       // [kMaxState]
   float* ob = st + kMaxState;  // [kEngineMaxObs]
   float* act = ob + kEngineMaxObs;  // [kWaveMaxDim]
   for (int i = lane; i < S; i += 64) st[i] = a.state[(size_t)n * S + i];
@@ -140,13 +382,22 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
   const float lstd = (a.log_std && lane < A) ? a.log_std[lane] : 0.f;
   const float half_log2pi = 0.91893853320467274f;
 
+  unsigned long long c_pol = 0, c_env = 0, c_rew = 0, c_all0 = clock64(), c0 = 0;
   for (int t = 0; t < a.T; ++t) {
     const size_t row = (size_t)t * a.N + n;
+    c0 = clock64();
     if (lane < D) a.obs_buf[row * D + lane] = o;
     if (lane == 0) a.starts[row] = start;
     // ---- policy + value
-    const float head = wave_mlp(pi, o);
-    const float value = bcast(wave_mlp(vf, o), 0);
+    float head, value;
+    if (paired) {
+      const float out = pair_mlp(pv, o);
+      head = out;
+      value = bcast(out, 32);
+    } else {
+      head = wave_mlp(pi, o);
+      value = bcast(wave_mlp(vf, o), 0);
+    }
     const uint64_t key = hash3(a.seed, (uint64_t)n, (uint64_t)(a.step0 + t));
     float a_raw, a_env, logp;
     if (a.n_actions > 0) {
@@ -185,21 +436,31 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
       act[lane] = a_env;
     }
     // ---- env step (lane 0), SB3 auto-reset + TimeLimit + Monitor
+    c_pol += clock64() - c0;
+    c0 = clock64();
     __syncthreads();
     int term = 0;
     float r_env = 0.f;
-    if (lane == 0) {
-      r_env = env_step(P, st, act, &term, rng);
-      env_obs(P, st, ob);
+    float o_next;  // terminal obs when done
+    if (P.kind == ENV_LOCO) {
+      r_env = loco_step_wave(P.loco, st, act);
+      o_next = loco_obs_lane(P.loco, st);
+    } else {
+      if (lane == 0) {
+        r_env = env_step(P, st, act, &term, rng);
+        env_obs(P, st, ob);
+      }
+      __syncthreads();
+      term = __builtin_amdgcn_readfirstlane(term);
+      r_env = bcast(r_env, 0);
+      o_next = lane < D ? ob[lane] : 0.f;
     }
-    __syncthreads();
-    term = __builtin_amdgcn_readfirstlane(term);
-    r_env = bcast(r_env, 0);
     elapsed += 1;
     ep_ret += r_env;
     const bool trunc = !term && elapsed >= a.max_steps;
     const bool done = term || trunc;
-    const float o_next = lane < D ? ob[lane] : 0.f;  // terminal obs when done
+    c_env += clock64() - c0;
+    c0 = clock64();
     // ---- learned reward R(s, a, s', d)
     float r = r_env;
     if (a.rew_enabled) {
@@ -228,6 +489,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
       float logit = bcast(wave_mlp(rw, x), 0);
       r = a.rew_transform == REW_SOFTPLUS ? (logit > 0.f ? logit + log1pf(expf(-logit)) : log1pf(expf(logit))) : logit;
     }
+    c_rew += clock64() - c0;
     if (trunc) {  // SB3: bootstrap the value of the truncated terminal obs into the reward
       r += a.gamma * bcast(wave_mlp(vf, o_next), 0);
     }
@@ -270,11 +532,17 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
   rng = (uint64_t)__builtin_amdgcn_readfirstlane((int)(rng & 0xffffffffu)) |
         ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(rng >> 32)) << 32);
   if (lane == 0) a.rng[n] = rng;
+  if (a.prof && lane == 0) {
+    a.prof[n * 4 + 0] = c_pol;
+    a.prof[n * 4 + 1] = c_env;
+    a.prof[n * 4 + 2] = c_rew;
+    a.prof[n * 4 + 3] = clock64() - c_all0;
+  }
 }
 
 int mlp_lds_floats(const WaveMLP& m) {
   int f = 0;
-  for (int l = 0; l < m.n_layers; ++l) f += m.dims[l] * kW + kW;
+  for (int l = 0; l < m.n_layers; ++l) f += ceil8(m.dims[l]) * kW + kW;
   if (m.norm_mean) f += 2 * kW;
   return f;
 }
@@ -283,6 +551,7 @@ int mlp_lds_floats(const WaveMLP& m) {
 
 size_t rollout_lds_bytes(const RolloutArgs& a) {
   int f = mlp_lds_floats(a.pi) + mlp_lds_floats(a.vf) + (a.rew_enabled ? mlp_lds_floats(a.rew) : 0);
+  if (a.pi.n_layers == a.vf.n_layers) f += pair_lds_floats(a.pi, a.vf);  // paired image
   f += kMaxState + kEngineMaxObs + kWaveMaxDim;
   return (size_t)f * sizeof(float);
 }

@@ -1,0 +1,309 @@
+"""DAgger (reference: ``src/imitation/algorithms/dagger.py``).
+
+Rounds of: collect with a β-mixture of expert and learner actions (the expert's
+action is always the one recorded), save each finished episode as a demo file,
+retrain BC on the union of all rounds' demos. Beta schedules (``dagger.py:28-96``),
+:class:`InteractiveTrajectoryCollector` (``:151-287``), :class:`DAggerTrainer`
+(``:294-552``, checkpoint/resume via ``save_trainer`` / :func:`reconstruct_trainer`),
+:class:`SimpleDAggerTrainer` (``:555-697``).
+
+Demo files use the same HF-dataset-directory format and ``round-XYZ/dagger-demo-*.npz``
+naming as the reference.
+"""
+
+from __future__ import annotations
+
+import abc
+import logging
+import os
+import pathlib
+import uuid
+from typing import Any, Callable, List, Mapping, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch as th
+
+from imitation_amd.algorithms import base, bc
+from imitation_amd.data import rollout, serialize, types
+from imitation_amd.envs.vec_env import VecEnvWrapper
+from imitation_amd.rl.base import check_for_correct_spaces
+from imitation_amd.rl.policies import get_device
+from imitation_amd.util import logger as imit_logger
+from imitation_amd.util import util
+
+
+class BetaSchedule(abc.ABC):
+    """Computes beta (% of time demonstration action used) from training round."""
+
+    @abc.abstractmethod
+    def __call__(self, round_num: int) -> float:
+        """Beta for round ``round_num``."""
+
+
+class LinearBetaSchedule(BetaSchedule):
+    """Linearly-decreasing schedule for beta (1 -> 0 over ``rampdown_rounds``)."""
+
+    def __init__(self, rampdown_rounds: int) -> None:
+        self.rampdown_rounds = rampdown_rounds
+
+    def __call__(self, round_num: int) -> float:
+        assert round_num >= 0
+        return min(1, max(0, (self.rampdown_rounds - round_num) / self.rampdown_rounds))
+
+
+class ExponentialBetaSchedule(BetaSchedule):
+    """Exponentially decaying schedule for beta."""
+
+    def __init__(self, decay_probability: float):
+        if not (0 < decay_probability <= 1):
+            raise ValueError("decay_probability lies outside the range (0, 1].")
+        self.decay_probability = decay_probability
+
+    def __call__(self, round_num: int) -> float:
+        assert round_num >= 0
+        return self.decay_probability**round_num
+
+
+def reconstruct_trainer(scratch_dir: types.AnyPath, venv, custom_logger: Optional[imit_logger.HierarchicalLogger] = None,
+                        device: Union[th.device, str] = "auto") -> "DAggerTrainer":
+    """Reconstruct a trainer from ``scratch_dir/checkpoint-latest.pt`` (a file this framework wrote)."""
+    custom_logger = custom_logger or imit_logger.configure()
+    checkpoint_path = util.parse_path(scratch_dir) / "checkpoint-latest.pt"
+    trainer = th.load(checkpoint_path, map_location=get_device(device), weights_only=False)
+    trainer.venv = venv
+    trainer._logger = custom_logger
+    return trainer
+
+
+def _save_dagger_demo(trajectory: types.Trajectory, trajectory_index: int, save_dir: types.AnyPath, rng: np.random.Generator,
+                      prefix: str = "") -> None:
+    save_dir = util.parse_path(save_dir)
+    assert isinstance(trajectory, types.Trajectory)
+    actual_prefix = f"{prefix}-" if prefix else ""
+    randbits = int.from_bytes(rng.bytes(16), "big")
+    random_uuid = uuid.UUID(int=randbits, version=4).hex
+    npz_path = save_dir / f"{actual_prefix}dagger-demo-{trajectory_index}-{random_uuid}.npz"
+    assert not npz_path.exists(), "The following DAgger demonstration path already exists: {0}".format(npz_path)
+    serialize.save(npz_path, [trajectory])
+    logging.info(f"Saved demo at '{npz_path}'")
+
+
+class InteractiveTrajectoryCollector(VecEnvWrapper):
+    """VecEnv wrapper that mixes in learner actions with prob 1-β and records expert demos."""
+
+    def __init__(self, venv, get_robot_acts: Callable[[np.ndarray], np.ndarray], beta: float, save_dir: types.AnyPath,
+                 rng: np.random.Generator) -> None:
+        super().__init__(venv)
+        self.get_robot_acts = get_robot_acts
+        assert 0 <= beta <= 1
+        self.beta = beta
+        self.traj_accum: Optional[rollout.TrajectoryAccumulator] = None
+        self.save_dir = save_dir
+        self._last_obs: Optional[np.ndarray] = None
+        self._done_before = True
+        self._is_reset = False
+        self._last_user_actions: Optional[np.ndarray] = None
+        self.rng = rng
+
+    def seed(self, seed: Optional[int] = None) -> List[Optional[int]]:
+        self.rng = np.random.default_rng(seed=seed)
+        return list(self.venv.seed(seed))
+
+    def reset(self) -> np.ndarray:
+        self.traj_accum = rollout.TrajectoryAccumulator()
+        obs = self.venv.reset()
+        assert isinstance(obs, np.ndarray)
+        for i, ob in enumerate(obs):
+            self.traj_accum.add_step({"obs": ob}, key=i)
+        self._last_obs = obs
+        self._is_reset = True
+        self._last_user_actions = None
+        return obs
+
+    def step_async(self, actions: np.ndarray) -> None:
+        assert self._is_reset, "call .reset() before .step()"
+        assert self._last_obs is not None
+        actual_acts = np.array(actions)
+        mask = self.rng.uniform(0, 1, size=(self.num_envs,)) > self.beta
+        if np.sum(mask) != 0:
+            actual_acts[mask] = self.get_robot_acts(self._last_obs[mask])
+        self._last_user_actions = actions
+        self.venv.step_async(actual_acts)
+
+    def step_wait(self):
+        next_obs, rews, dones, infos = self.venv.step_wait()
+        assert isinstance(next_obs, np.ndarray)
+        assert self.traj_accum is not None
+        assert self._last_user_actions is not None
+        self._last_obs = next_obs
+        fresh = self.traj_accum.add_steps_and_auto_finish(obs=next_obs, acts=self._last_user_actions, rews=rews,
+                                                          infos=infos, dones=dones)
+        for traj_index, traj in enumerate(fresh):
+            _save_dagger_demo(traj, traj_index, self.save_dir, self.rng)
+        return next_obs, rews, dones, infos
+
+
+class NeedsDemosException(Exception):
+    """Signals demos need to be collected for current round before continuing."""
+
+
+class DAggerTrainer(base.BaseImitationAlgorithm):
+    """DAgger training class with low-level API suitable for interactive human feedback."""
+
+    DEFAULT_N_EPOCHS: int = 4
+
+    def __init__(self, *, venv, scratch_dir: types.AnyPath, rng: np.random.Generator,
+                 beta_schedule: Optional[Callable[[int], float]] = None, bc_trainer: bc.BC,
+                 custom_logger: Optional[imit_logger.HierarchicalLogger] = None):
+        super().__init__(custom_logger=custom_logger)
+        if beta_schedule is None:
+            beta_schedule = LinearBetaSchedule(15)
+        self.beta_schedule = beta_schedule
+        self.scratch_dir = util.parse_path(scratch_dir)
+        self.venv = venv
+        self.round_num = 0
+        self._last_loaded_round = -1
+        self._all_demos: List[types.Trajectory] = []
+        self.rng = rng
+        try:
+            check_for_correct_spaces(self.venv, bc_trainer.observation_space, bc_trainer.action_space)
+        except ValueError as e:
+            UserWarning(e)
+        self.bc_trainer = bc_trainer
+        self.bc_trainer.logger = self.logger
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        del d["venv"]
+        del d["_logger"]
+        return d
+
+    @property
+    def logger(self) -> imit_logger.HierarchicalLogger:
+        return super().logger
+
+    @logger.setter
+    def logger(self, value: imit_logger.HierarchicalLogger) -> None:
+        self._logger = value
+        self.bc_trainer.logger = value
+
+    @property
+    def policy(self):
+        return self.bc_trainer.policy
+
+    @property
+    def batch_size(self) -> int:
+        return self.bc_trainer.batch_size
+
+    def _load_all_demos(self) -> Tuple[types.Transitions, List[int]]:
+        num_demos_by_round = []
+        for round_num in range(self._last_loaded_round + 1, self.round_num + 1):
+            round_dir = self._demo_dir_path_for_round(round_num)
+            demo_paths = self._get_demo_paths(round_dir)
+            self._all_demos.extend(serialize.load(p)[0] for p in demo_paths)
+            num_demos_by_round.append(len(demo_paths))
+        logging.info(f"Loaded {len(self._all_demos)} total")
+        return rollout.flatten_trajectories(self._all_demos), num_demos_by_round
+
+    def _get_demo_paths(self, round_dir: pathlib.Path) -> List[pathlib.Path]:
+        filenames = sorted(os.listdir(round_dir))
+        return [round_dir / f for f in filenames if f.endswith(".npz")]
+
+    def _demo_dir_path_for_round(self, round_num: Optional[int] = None) -> pathlib.Path:
+        if round_num is None:
+            round_num = self.round_num
+        return self.scratch_dir / "demos" / f"round-{round_num:03d}"
+
+    def _try_load_demos(self) -> None:
+        demo_dir = self._demo_dir_path_for_round()
+        demo_paths = self._get_demo_paths(demo_dir) if demo_dir.is_dir() else []
+        if len(demo_paths) == 0:
+            raise NeedsDemosException(
+                f"No demos found for round {self.round_num} in dir '{demo_dir}'. "
+                f"Maybe you need to collect some demos? See .create_trajectory_collector()"
+            )
+        if self._last_loaded_round < self.round_num:
+            transitions, num_demos = self._load_all_demos()
+            logging.info(f"Loaded {sum(num_demos)} new demos from {len(num_demos)} rounds")
+            if len(transitions) < self.batch_size:
+                raise ValueError(
+                    f"Not enough transitions to form a single batch: self.batch_size={self.batch_size} > "
+                    f"len(transitions)={len(transitions)}"
+                )
+            loader = base.TransitionsBatchLoader(transitions, self.batch_size, shuffle=True, drop_last=True,
+                                                 seed=int(self.rng.integers(0, 2**31 - 1)))
+            self.bc_trainer.set_demonstrations(loader)
+            self._last_loaded_round = self.round_num
+
+    def extend_and_update(self, bc_train_kwargs: Optional[Mapping[str, Any]] = None) -> int:
+        """Load new demos, train BC on all demos, advance the round counter."""
+        bc_train_kwargs = {} if bc_train_kwargs is None else dict(bc_train_kwargs)
+        if "log_rollouts_venv" not in bc_train_kwargs:
+            bc_train_kwargs["log_rollouts_venv"] = self.venv
+        if "n_epochs" not in bc_train_kwargs and "n_batches" not in bc_train_kwargs:
+            bc_train_kwargs["n_epochs"] = self.DEFAULT_N_EPOCHS
+        logging.info("Loading demonstrations")
+        self._try_load_demos()
+        logging.info(f"Training at round {self.round_num}")
+        self.bc_trainer.train(**bc_train_kwargs)
+        self.round_num += 1
+        logging.info(f"New round number is {self.round_num}")
+        return self.round_num
+
+    def create_trajectory_collector(self) -> InteractiveTrajectoryCollector:
+        save_dir = self._demo_dir_path_for_round()
+        beta = self.beta_schedule(self.round_num)
+        return InteractiveTrajectoryCollector(venv=self.venv, get_robot_acts=lambda acts: self.bc_trainer.policy.predict(acts)[0],
+                                              beta=beta, save_dir=save_dir, rng=self.rng)
+
+    def save_trainer(self) -> Tuple[pathlib.Path, pathlib.Path]:
+        """Save ``checkpoint-{round}.pt`` / ``checkpoint-latest.pt`` and the policy files."""
+        self.scratch_dir.mkdir(parents=True, exist_ok=True)
+        checkpoint_paths = [self.scratch_dir / f"checkpoint-{self.round_num:03d}.pt", self.scratch_dir / "checkpoint-latest.pt"]
+        for p in checkpoint_paths:
+            th.save(self, p)
+        policy_paths = [self.scratch_dir / f"policy-{self.round_num:03d}.pt", self.scratch_dir / "policy-latest.pt"]
+        for p in policy_paths:
+            util.save_policy(self.policy, p)
+        return checkpoint_paths[0], policy_paths[0]
+
+
+class SimpleDAggerTrainer(DAggerTrainer):
+    """Simpler subclass of DAggerTrainer for training with synthetic feedback."""
+
+    def __init__(self, *, venv, scratch_dir: types.AnyPath, expert_policy, rng: np.random.Generator,
+                 expert_trajs: Optional[Sequence[types.Trajectory]] = None, **dagger_trainer_kwargs):
+        super().__init__(venv=venv, scratch_dir=scratch_dir, rng=rng, **dagger_trainer_kwargs)
+        self.expert_policy = expert_policy
+        if expert_policy.observation_space != self.venv.observation_space:
+            raise ValueError("Mismatched observation space between expert_policy and venv")
+        if expert_policy.action_space != self.venv.action_space:
+            raise ValueError("Mismatched action space between expert_policy and venv")
+        if expert_trajs is not None:
+            for traj_index, traj in enumerate(expert_trajs):
+                _save_dagger_demo(traj, traj_index, self._demo_dir_path_for_round(), self.rng, prefix="initial_data")
+
+    def train(self, total_timesteps: int, *, rollout_round_min_episodes: int = 3, rollout_round_min_timesteps: int = 500,
+              bc_train_kwargs: Optional[dict] = None) -> None:
+        """Train the DAgger agent until at least ``total_timesteps`` environment steps have been collected."""
+        total_timestep_count = 0
+        round_num = 0
+        while total_timestep_count < total_timesteps:
+            collector = self.create_trajectory_collector()
+            round_episode_count = 0
+            round_timestep_count = 0
+            sample_until = rollout.make_sample_until(min_timesteps=max(rollout_round_min_timesteps, self.batch_size),
+                                                     min_episodes=rollout_round_min_episodes)
+            trajectories = rollout.generate_trajectories(policy=self.expert_policy, venv=collector, sample_until=sample_until,
+                                                         deterministic_policy=True, rng=collector.rng)
+            for traj in trajectories:
+                self._logger.record_mean("dagger/mean_episode_reward", np.sum(traj.rews))
+                round_timestep_count += len(traj)
+                total_timestep_count += len(traj)
+            round_episode_count += len(trajectories)
+            self._logger.record("dagger/total_timesteps", total_timestep_count)
+            self._logger.record("dagger/round_num", round_num)
+            self._logger.record("dagger/round_episode_count", round_episode_count)
+            self._logger.record("dagger/round_timestep_count", round_timestep_count)
+            self.extend_and_update(bc_train_kwargs)
+            round_num += 1

@@ -70,6 +70,10 @@ class TabularModelPOMDP(core.Env):
         return self.n_states
 
     @property
+    def action_dim(self) -> int:
+        return self.n_actions
+
+    @property
     def obs_dim(self) -> int:
         return self.observation_matrix.shape[1]
 
@@ -234,3 +238,19 @@ class CliffWorld(TabularModelPOMDP):
         init[to_id(height - 1, 0)] = 1.0
         super().__init__(transition_matrix=T, observation_matrix=O, reward_matrix=R, horizon=horizon, initial_state_dist=init)
         self.width, self.height = width, height
+
+
+class ExposePOMDPStateWrapper(core.Wrapper):
+    """Observe the latent state index instead of the observation vector (seals ``ExposePOMDPStateWrapper``)."""
+
+    def __init__(self, env: TabularModelPOMDP):
+        super().__init__(env)
+        self.observation_space = env.unwrapped.state_space
+
+    def reset(self, *, seed=None, options=None):
+        _, info = self.env.reset(seed=seed, options=options)
+        return self.env.unwrapped.state, info
+
+    def step(self, action):
+        _, rew, term, trunc, info = self.env.step(action)
+        return self.env.unwrapped.state, rew, term, trunc, info

@@ -182,8 +182,8 @@ class ReplayBuffer(BaseBuffer):
         self.observations[p].copy_(_to_t(obs, self.device, self.observations.dtype).reshape(self.observations[p].shape))
         self.next_observations[p].copy_(_to_t(next_obs, self.device, self.next_observations.dtype).reshape(self.observations[p].shape))
         self.actions[p].copy_(_to_t(action, self.device, self.actions.dtype).reshape((self.n_envs, self.action_dim)))
-        self.rewards[p].copy_(_to_t(reward, self.device, th.float32).reshape(-1))
-        self.dones[p].copy_(_to_t(done, self.device, th.float32).reshape(-1))
+        self.rewards[p].copy_(_to_t(reward, self.device, th.float32).reshape(-1).expand(self.n_envs))
+        self.dones[p].copy_(_to_t(done, self.device, th.float32).reshape(-1).expand(self.n_envs))
         if self.handle_timeout_termination:
             self.timeouts[p].copy_(
                 th.tensor([float(info.get("TimeLimit.truncated", False)) for info in infos], device=self.device)
@@ -192,6 +192,22 @@ class ReplayBuffer(BaseBuffer):
         if self.pos == self.buffer_size:
             self.full = True
             self.pos = 0
+
+    def extend(self, obs, next_obs, action, reward, done) -> None:
+        """Bulk-append ``n`` single-env transitions (``n_envs == 1``) with one device copy per field."""
+        assert self.n_envs == 1
+        obs = _to_t(obs, self.device, self.observations.dtype)
+        n = obs.shape[0]
+        idx = (th.arange(n, device=self.device) + self.pos) % self.buffer_size
+        self.observations[idx, 0] = obs.reshape((n, *self.obs_shape))
+        self.next_observations[idx, 0] = _to_t(next_obs, self.device, self.next_observations.dtype).reshape((n, *self.obs_shape))
+        self.actions[idx, 0] = _to_t(action, self.device, self.actions.dtype).reshape((n, self.action_dim))
+        self.rewards[idx, 0] = _to_t(reward, self.device, th.float32).reshape(-1).expand(n)
+        self.dones[idx, 0] = _to_t(done, self.device, th.float32).reshape(-1).expand(n)
+        self.timeouts[idx, 0] = 0.0
+        if self.pos + n >= self.buffer_size:
+            self.full = True
+        self.pos = (self.pos + n) % self.buffer_size
 
     def sample(self, batch_size: int, env=None) -> ReplayBufferSamples:
         upper = self.buffer_size if self.full else self.pos
