@@ -82,7 +82,7 @@ __device__ __forceinline__ float wsum(float v) {
 // [actor layers][critic layers] each {W,b | gW,gb | mW,mb | vW,vb}, then
 // H0 | actor H1..HL | critic H1..HL | dZ actor | dZ critic | raw | acts | rowv | ls | norm | red
 struct Lay {
-  lf *W, *b, *gW, *gb, *mW, *mb, *vW, *vb;
+  lf *W, *b, *gW, *gb;
   int din, dout, n, w_off, b_off;
 };
 
@@ -91,18 +91,28 @@ __device__ __forceinline__ const int* dims_of(const PPOArgs& a) { return Q ? a.v
 template <int Q>
 __device__ __forceinline__ int nl_of(const PPOArgs& a) { return Q ? a.n_vf : a.n_pi; }
 
+// floats of all padded parameter images (actor layers then critic layers)
+__host__ __device__ inline int param_floats(const PPOArgs& a) {
+  int f = 0;
+  for (int l = 0; l < kL; ++l) {
+    if (l < a.n_pi) f += layer_floats(a.pi_dims[l], a.pi_dims[l + 1]);
+    if (l < a.n_vf) f += layer_floats(a.vf_dims[l], a.vf_dims[l + 1]);
+  }
+  return f;
+}
+
 template <int Q>
 __device__ __forceinline__ Lay lay(lf* lds, const PPOArgs& a, int li) {
   int off = 0;
   if (Q == 1) {
 #pragma unroll
     for (int l = 0; l < kL; ++l)
-      if (l < a.n_pi) off += 4 * layer_floats(a.pi_dims[l], a.pi_dims[l + 1]);
+      if (l < a.n_pi) off += layer_floats(a.pi_dims[l], a.pi_dims[l + 1]);
   }
   const int* d = dims_of<Q>(a);
 #pragma unroll
   for (int l = 0; l < kL; ++l)
-    if (l < li) off += 4 * layer_floats(d[l], d[l + 1]);
+    if (l < li) off += layer_floats(d[l], d[l + 1]);
   Lay y;
   y.din = d[li];
   y.dout = d[li + 1];
@@ -110,25 +120,14 @@ __device__ __forceinline__ Lay lay(lf* lds, const PPOArgs& a, int li) {
   const int sw = p16(y.dout) * ldp(y.din);
   y.W = lds + off;
   y.b = y.W + sw;
-  y.gW = y.W + y.n;
+  y.gW = y.W + param_floats(a);  // gradient image region mirrors the parameter region
   y.gb = y.gW + sw;
-  y.mW = y.gW + y.n;
-  y.mb = y.mW + sw;
-  y.vW = y.mW + y.n;
-  y.vb = y.vW + sw;
   y.w_off = Q ? a.vf_w_off[li] : a.pi_w_off[li];
   y.b_off = Q ? a.vf_b_off[li] : a.pi_b_off[li];
   return y;
 }
 
-__host__ __device__ inline int param_floats(const PPOArgs& a) {
-  int f = 0;
-  for (int l = 0; l < kL; ++l) {
-    if (l < a.n_pi) f += 4 * layer_floats(a.pi_dims[l], a.pi_dims[l + 1]);
-    if (l < a.n_vf) f += 4 * layer_floats(a.vf_dims[l], a.vf_dims[l + 1]);
-  }
-  return f;
-}
+
 __host__ __device__ inline int max_dim(const PPOArgs& a) {
   int m = a.D;
   for (int l = 0; l <= kL; ++l) {
@@ -163,7 +162,7 @@ struct Bufs {
 __device__ __forceinline__ Bufs bufs(lf* lds, const PPOArgs& a) {
   Bufs b;
   b.img = img_floats(a);
-  lf* p = lds + param_floats(a);
+  lf* p = lds + 2 * param_floats(a);  // Wall | Gall
   b.H0 = p; p += b.img;
   b.Ha = p; p += a.n_pi * b.img;
   b.Hc = p; p += a.n_vf * b.img;
@@ -178,7 +177,7 @@ __device__ __forceinline__ Bufs bufs(lf* lds, const PPOArgs& a) {
   return b;
 }
 __host__ __device__ inline int total_floats(const PPOArgs& a) {
-  return param_floats(a) + img_floats(a) * (1 + a.n_pi + a.n_vf) + 2 * dz_floats(a) + kMaxB * a.D +
+  return 2 * param_floats(a) + img_floats(a) * (1 + a.n_pi + a.n_vf) + 2 * dz_floats(a) + kMaxB * a.D +
          kMaxB * (a.discrete ? 1 : a.A) + 6 * kMaxB + 64 + 132 + 32 + 2 * kL * 8;
 }
 
@@ -188,7 +187,7 @@ __device__ __forceinline__ lf* Hq(const Bufs& b, int l) {
 }
 
 // flat (torch layout) <-> padded image
-__device__ void img_load(lf* img, lf* bimg, const float* flat, const Lay& y) {
+__device__ __forceinline__ void img_load(lf* img, lf* bimg, const float* flat, const Lay& y) {
   const int ld = ldp(y.din), R = p16(y.dout);
   for (int e = threadIdx.x; e < R * ld; e += kThreads) {
     const int o = e / ld, i = e - o * ld;
@@ -196,10 +195,10 @@ __device__ void img_load(lf* img, lf* bimg, const float* flat, const Lay& y) {
   }
   for (int o = threadIdx.x; o < R; o += kThreads) bimg[o] = o < y.dout ? flat[y.b_off + o] : 0.f;
 }
-__device__ void img_zero(lf* img, int n) {
+__device__ __forceinline__ void img_zero(lf* img, int n) {
   for (int e = threadIdx.x; e < n; e += kThreads) img[e] = 0.f;
 }
-__device__ void img_store(const lf* img, const lf* bimg, float* flat, const Lay& y) {
+__device__ __forceinline__ void img_store(const lf* img, const lf* bimg, float* flat, const Lay& y) {
   const int ld = ldp(y.din);
   for (int e = threadIdx.x; e < y.dout * y.din; e += kThreads) {
     const int o = e / y.din, i = e - o * y.din;
@@ -248,13 +247,13 @@ __device__ __forceinline__ void write_lt(li32* tab, lf* lds, const PPOArgs& a, c
       r[LT_HIN] = (int)(Hq<Q>(bf, li) - lds);
       r[LT_HOUT] = (int)(Hq<Q>(bf, li + 1) - lds);
       r[LT_DZIN] = (int)((li == L - 1 ? (Q ? bf.dZc : bf.dZa) : Hq<Q>(bf, li + 2)) - lds);
-      r[LT_N] = y.n;
+      r[LT_N] = param_floats(a);
     }
   }
 }
 
 // gw: wave index within the net's group (0..3).
-__device__ void fwd_stage(lf* lds, const LT& t, int B, int gw) {
+__device__ __forceinline__ void fwd_stage(lf* lds, const LT& t, int B, int gw) {
   const int lane = threadIdx.x & 63;
   const lf* W = lds + t.off;
   const lf* bias = W + p16(t.dout) * ldp(t.din);
@@ -282,11 +281,11 @@ __device__ void fwd_stage(lf* lds, const LT& t, int B, int gw) {
 // `lower`, dZ of the layer below. dZ of this layer lives in the head dZ image or in
 // place in H[li+2]; dZ of the layer below is written in place into H[li+1] (free:
 // its last reader was the previous backward stage).
-__device__ void bwd_stage(lf* lds, const LT& t, int B, int gw, bool lower, int hidden_act) {
+__device__ __forceinline__ void bwd_stage(lf* lds, const LT& t, int B, int gw, bool lower, int hidden_act) {
   const int lane = threadIdx.x & 63;
   const lf* W = lds + t.off;
   const int sw = p16(t.dout) * ldp(t.din);
-  lf* gW = lds + t.off + t.n;
+  lf* gW = lds + t.off + t.n;  // t.n = size of the parameter region
   lf* gb = gW + sw;
   const int ldi = ldp(t.din), ldo = ldp(t.dout);
   const lf* dz = lds + t.dzin;
@@ -377,7 +376,7 @@ __device__ __forceinline__ void stage_rows(const PPOArgs& a, const Bufs& bf, con
 }
 
 // normaliser update + advantage normalisation + normalised input image H0
-__device__ void prepare_minibatch(const PPOArgs& a, const Bufs& bf, bool update_norm) {
+__device__ __forceinline__ void prepare_minibatch(const PPOArgs& a, const Bufs& bf, bool update_norm) {
   const int B = a.batch, D = a.D;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   lf* nmean = bf.norm;
@@ -423,7 +422,7 @@ __device__ void prepare_minibatch(const PPOArgs& a, const Bufs& bf, bool update_
 // ---------------------------------------------------------------- losses (one wave each)
 // Actor head -> dZa, log-std gradient, statistics. Runs on wave 0 only: B <= 64 rows,
 // one row per lane, every row reduction is a wave shuffle.
-__device__ void policy_loss(const PPOArgs& a, const Bufs& bf, int dout) {
+__device__ __forceinline__ void policy_loss(const PPOArgs& a, const Bufs& bf, int dout) {
   const int B = a.batch;
   const int lane = threadIdx.x & 63;
   const int ldo = ldp(dout);
@@ -507,7 +506,7 @@ __device__ void policy_loss(const PPOArgs& a, const Bufs& bf, int dout) {
   }
 }
 
-__device__ void value_loss(const PPOArgs& a, const Bufs& bf) {
+__device__ __forceinline__ void value_loss(const PPOArgs& a, const Bufs& bf) {
   const int B = a.batch;
   const int lane = threadIdx.x & 63;
   const lf* v = Hq<1>(bf, a.n_vf);
@@ -522,15 +521,20 @@ __device__ void value_loss(const PPOArgs& a, const Bufs& bf) {
 }
 
 // ---------------------------------------------------------------- clip_grad_norm_ + Adam
-__device__ void clip_and_adam(lf* lds, const li32* tab, const PPOArgs& a, const Bufs& bf, float step, bool has_ls) {
+// Adam moments live in registers for the whole launch: thread t owns parameter-image
+// elements t, t + kThreads, ... (kSlots of them) of the concatenated Wall/Gall
+// regions, so the elementwise update touches LDS only for W and G.
+template <int kSlots>
+__device__ __forceinline__ void clip_and_adam(lf* lds, const PPOArgs& a, const Bufs& bf, float step, bool has_ls, float (&m)[kSlots],
+                              float (&v)[kSlots]) {
+  const int n_all = param_floats(a);
+  lf* W = lds;
+  const lf* G = lds + n_all;
   float ss = 0.f;
-  for (int q = 0; q < 2; ++q) {
-    const int L = q ? a.n_vf : a.n_pi;
-    for (int li = 0; li < L; ++li) {
-      const LT t = load_lt(tab, q * kL + li);
-      const lf* g = lds + t.off + t.n;
-      for (int e = threadIdx.x; e < t.n; e += kThreads) ss += g[e] * g[e];
-    }
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) {
+    const int e = threadIdx.x + j * kThreads;
+    if (e < n_all) ss += G[e] * G[e];
   }
   if (has_ls && threadIdx.x < a.A) ss += bf.ls[16 + threadIdx.x] * bf.ls[16 + threadIdx.x];
   ss = wsum(ss);
@@ -545,37 +549,64 @@ __device__ void clip_and_adam(lf* lds, const li32* tab, const PPOArgs& a, const 
   const float bc2s = sqrtf(1.f - powf(a.beta2, step));
   const float step_size = a.lr / bc1;
   const float b1 = a.beta1, b2 = a.beta2, eps = a.adam_eps;
-  for (int q = 0; q < 2; ++q) {
-    const int L = q ? a.n_vf : a.n_pi;
-    for (int li = 0; li < L; ++li) {
-      const LT t = load_lt(tab, q * kL + li);
-      lf* W = lds + t.off;  // W,b / gW,gb / mW,mb / vW,vb: four contiguous images of t.n floats
-      lf* G = W + t.n;
-      lf* M = G + t.n;
-      lf* V = M + t.n;
-      for (int e = threadIdx.x; e < t.n; e += kThreads) {
-        const float g = G[e] * coef;
-        const float m = b1 * M[e] + (1.f - b1) * g;
-        const float v = b2 * V[e] + (1.f - b2) * g * g;
-        M[e] = m;
-        V[e] = v;
-        W[e] -= step_size * m / (sqrtf(v) / bc2s + eps);
-      }
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) {
+    const int e = threadIdx.x + j * kThreads;
+    if (e < n_all) {
+      const float g = G[e] * coef;
+      m[j] = b1 * m[j] + (1.f - b1) * g;
+      v[j] = b2 * v[j] + (1.f - b2) * g * g;
+      W[e] -= step_size * m[j] / (sqrtf(v[j]) / bc2s + eps);
     }
   }
   if (has_ls && threadIdx.x < a.A) {
     lf* ls = bf.ls;
     const int k = threadIdx.x;
     const float g = ls[16 + k] * coef;
-    const float m = b1 * ls[32 + k] + (1.f - b1) * g;
-    const float v = b2 * ls[48 + k] + (1.f - b2) * g * g;
-    ls[32 + k] = m;
-    ls[48 + k] = v;
-    ls[k] -= step_size * m / (sqrtf(v) / bc2s + eps);
+    const float mm = b1 * ls[32 + k] + (1.f - b1) * g;
+    const float vv = b2 * ls[48 + k] + (1.f - b2) * g * g;
+    ls[32 + k] = mm;
+    ls[48 + k] = vv;
+    ls[k] -= step_size * mm / (sqrtf(vv) / bc2s + eps);
   }
   __syncthreads();
 }
 
+// Moments: global flat vector <-> registers, staged through the gradient region.
+template <int kSlots>
+__device__ __forceinline__ void moments_in(lf* lds, const PPOArgs& a, const float* flat, float (&r)[kSlots]) {
+  const int n_all = param_floats(a);
+#pragma unroll
+  for (int li = 0; li < kL; ++li) {
+    if (li < a.n_pi) { const Lay y = lay<0>(lds, a, li); img_load(y.gW, y.gb, flat, y); }
+    if (li < a.n_vf) { const Lay y = lay<1>(lds, a, li); img_load(y.gW, y.gb, flat, y); }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) {
+    const int e = threadIdx.x + j * kThreads;
+    r[j] = e < n_all ? lds[n_all + e] : 0.f;
+  }
+  __syncthreads();
+}
+template <int kSlots>
+__device__ __forceinline__ void moments_out(lf* lds, const PPOArgs& a, float* flat, const float (&r)[kSlots]) {
+  const int n_all = param_floats(a);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) {
+    const int e = threadIdx.x + j * kThreads;
+    if (e < n_all) lds[n_all + e] = r[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int li = 0; li < kL; ++li) {
+    if (li < a.n_pi) { const Lay y = lay<0>(lds, a, li); img_store(y.gW, y.gb, flat, y); }
+    if (li < a.n_vf) { const Lay y = lay<1>(lds, a, li); img_store(y.gW, y.gb, flat, y); }
+  }
+}
+
+template <int kSlots>
 __global__ __launch_bounds__(kThreads) void ppo_kernel(PPOArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* lds = (lf*)lds_raw;
@@ -586,23 +617,28 @@ __global__ __launch_bounds__(kThreads) void ppo_kernel(PPOArgs a) {
   const bool has_ls = a.log_std_off >= 0 && !a.discrete;
   const bool need_moments = a.mode != 1;
 
+  float mom1[kSlots], mom2[kSlots];
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) mom1[j] = mom2[j] = 0.f;
+  if (need_moments) {
+    moments_in(lds, a, a.exp_avg, mom1);
+    moments_in(lds, a, a.exp_avg_sq, mom2);
+  }
 #pragma unroll
   for (int li = 0; li < kL; ++li) {
     if (li < a.n_pi) {
       const Lay y = lay<0>(lds, a, li);
       img_load(y.W, y.b, a.params, y);
-      if (need_moments) { img_load(y.mW, y.mb, a.exp_avg, y); img_load(y.vW, y.vb, a.exp_avg_sq, y); }
       if (a.mode == 2) img_load(y.gW, y.gb, a.grads, y);
-      else img_zero(y.gW, y.n);  // padding must stay zero; backward overwrites the rest
     }
     if (li < a.n_vf) {
       const Lay y = lay<1>(lds, a, li);
       img_load(y.W, y.b, a.params, y);
-      if (need_moments) { img_load(y.mW, y.mb, a.exp_avg, y); img_load(y.vW, y.vb, a.exp_avg_sq, y); }
       if (a.mode == 2) img_load(y.gW, y.gb, a.grads, y);
-      else img_zero(y.gW, y.n);
     }
   }
+  // gradient padding must stay zero (backward only writes the valid entries)
+  if (a.mode != 2) img_zero(lds + param_floats(a), param_floats(a));
   if (threadIdx.x == 0) write_lt<0>(tab, lds, a, bf);
   if (threadIdx.x == 64) write_lt<1>(tab, lds, a, bf);
   if (threadIdx.x < 16) {
@@ -667,14 +703,14 @@ __global__ __launch_bounds__(kThreads) void ppo_kernel(PPOArgs a) {
     IA_PROF(4)
     if (a.mode == 0) {
       step += 1.f;
-      clip_and_adam(lds, tab, a, bf, step, has_ls);
+      clip_and_adam<kSlots>(lds, a, bf, step, has_ls, mom1, mom2);
     }
     IA_PROF(5)
 #undef IA_PROF
   }
   if (a.mode == 2) {
     step += 1.f;
-    clip_and_adam(lds, tab, a, bf, step, has_ls);
+    clip_and_adam<kSlots>(lds, a, bf, step, has_ls, mom1, mom2);
   }
   __syncthreads();
 #pragma unroll
@@ -682,13 +718,17 @@ __global__ __launch_bounds__(kThreads) void ppo_kernel(PPOArgs a) {
     if (li < a.n_pi) {
       const Lay y = lay<0>(lds, a, li);
       if (a.mode == 1) img_store(y.gW, y.gb, a.grads, y);
-      else { img_store(y.W, y.b, a.params, y); img_store(y.mW, y.mb, a.exp_avg, y); img_store(y.vW, y.vb, a.exp_avg_sq, y); }
+      else img_store(y.W, y.b, a.params, y);
     }
     if (li < a.n_vf) {
       const Lay y = lay<1>(lds, a, li);
       if (a.mode == 1) img_store(y.gW, y.gb, a.grads, y);
-      else { img_store(y.W, y.b, a.params, y); img_store(y.mW, y.mb, a.exp_avg, y); img_store(y.vW, y.vb, a.exp_avg_sq, y); }
+      else img_store(y.W, y.b, a.params, y);
     }
+  }
+  if (need_moments) {
+    moments_out(lds, a, a.exp_avg, mom1);
+    moments_out(lds, a, a.exp_avg_sq, mom2);
   }
   if (threadIdx.x < a.A && has_ls) {
     const int k = threadIdx.x;
@@ -723,7 +763,11 @@ hipError_t ppo_launch(const PPOArgs& a, hipStream_t s) {
   if (a.batch % 16 != 0 || a.batch > kMaxB || a.rows % a.batch != 0 || a.D > 64 || a.A > 16) return hipErrorInvalidValue;
   const size_t lds = ppo_lds_bytes(a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ppo_kernel, dim3(1), dim3(kThreads), lds, s, a);
+  const int slots = (param_floats(a) + kThreads - 1) / kThreads;
+  if (slots <= 8) hipLaunchKernelGGL(ppo_kernel<8>, dim3(1), dim3(kThreads), lds, s, a);
+  else if (slots <= 16) hipLaunchKernelGGL(ppo_kernel<16>, dim3(1), dim3(kThreads), lds, s, a);
+  else if (slots <= 32) hipLaunchKernelGGL(ppo_kernel<32>, dim3(1), dim3(kThreads), lds, s, a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -92,10 +92,10 @@ class _DeviceDemoSampler:
         if self.n < batch_size:
             raise ValueError(f"Number of transitions in `demonstrations` {self.n} is smaller than batch size {batch_size}.")
         self.data = {
-            "obs": th.as_tensor(np.asarray(transitions.obs), device=self.device),
-            "acts": th.as_tensor(np.asarray(transitions.acts), device=self.device),
-            "next_obs": th.as_tensor(np.asarray(transitions.next_obs), device=self.device),
-            "dones": th.as_tensor(np.asarray(transitions.dones), device=self.device),
+            "obs": th.as_tensor(np.array(transitions.obs), device=self.device),
+            "acts": th.as_tensor(np.array(transitions.acts), device=self.device),
+            "next_obs": th.as_tensor(np.array(transitions.next_obs), device=self.device),
+            "dones": th.as_tensor(np.array(transitions.dones), device=self.device),
         }
         self._gen = th.Generator(device=self.device)
         self._gen.manual_seed(int(seed if seed is not None else np.random.randint(0, 2**31 - 1)) + 104729 * pdist.rank())

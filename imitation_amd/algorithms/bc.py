@@ -165,8 +165,10 @@ class BCLogger:
 
 
 def reconstruct_policy(policy_path: str, device: Union[th.device, str] = "auto") -> ActorCriticPolicy:
-    """Reconstruct a saved policy (``util.save_policy`` / ``final.th``). The file is our own output."""
-    policy = th.load(policy_path, map_location=get_device(device), weights_only=False)
+    """Reconstruct a saved policy (``util.save_policy`` / ``final.th``; weights_only load)."""
+    from imitation_amd.rl.policies import load_policy_file
+
+    policy = load_policy_file(policy_path, device=device)
     assert isinstance(policy, ActorCriticPolicy)
     return policy
 

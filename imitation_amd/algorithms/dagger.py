@@ -14,16 +14,18 @@ naming as the reference.
 from __future__ import annotations
 
 import abc
+import json
 import logging
 import os
 import pathlib
 import uuid
-from typing import Any, Callable, List, Mapping, Optional, Sequence, Tuple, Union
+from typing import Any, Callable, Dict, List, Mapping, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch as th
 
 from imitation_amd.algorithms import base, bc
+from imitation_amd.rl import save_util
 from imitation_amd.data import rollout, serialize, types
 from imitation_amd.envs.vec_env import VecEnvWrapper
 from imitation_amd.rl.base import check_for_correct_spaces
@@ -64,14 +66,58 @@ class ExponentialBetaSchedule(BetaSchedule):
         return self.decay_probability**round_num
 
 
+def _schedule_to_json(schedule) -> Dict[str, Any]:
+    if isinstance(schedule, LinearBetaSchedule):
+        return {"type": "linear", "rampdown_rounds": schedule.rampdown_rounds}
+    if isinstance(schedule, ExponentialBetaSchedule):
+        return {"type": "exponential", "decay_probability": schedule.decay_probability}
+    logging.warning("custom beta schedule %r is not serializable; a reloaded trainer uses the default", schedule)
+    return {"type": "default"}
+
+
+def _schedule_from_json(d: Mapping[str, Any]):
+    if d["type"] == "linear":
+        return LinearBetaSchedule(d["rampdown_rounds"])
+    if d["type"] == "exponential":
+        return ExponentialBetaSchedule(d["decay_probability"])
+    return None
+
+
 def reconstruct_trainer(scratch_dir: types.AnyPath, venv, custom_logger: Optional[imit_logger.HierarchicalLogger] = None,
                         device: Union[th.device, str] = "auto") -> "DAggerTrainer":
-    """Reconstruct a trainer from ``scratch_dir/checkpoint-latest.pt`` (a file this framework wrote)."""
+    """Rebuild a trainer from ``scratch_dir/checkpoint-latest.pt`` (reference: dagger.py reconstruct_trainer).
+
+    Checkpoints are tensor/JSON-only (``torch.load(weights_only=True)``): trainer
+    metadata as JSON, the BC policy and optimizer state dicts, and for
+    :class:`SimpleDAggerTrainer` the expert policy. Demonstrations are re-read from
+    ``scratch_dir/demos`` on the next update.
+    """
+    from imitation_amd.rl.policies import load_policy_file
+
     custom_logger = custom_logger or imit_logger.configure()
-    checkpoint_path = util.parse_path(scratch_dir) / "checkpoint-latest.pt"
-    trainer = th.load(checkpoint_path, map_location=get_device(device), weights_only=False)
-    trainer.venv = venv
-    trainer._logger = custom_logger
+    scratch_dir = util.parse_path(scratch_dir)
+    ckpt = th.load(scratch_dir / "checkpoint-latest.pt", map_location=get_device(device), weights_only=True)
+    meta = json.loads(ckpt["meta"])
+    policy_path = scratch_dir / "policy-latest.pt"
+    policy = load_policy_file(policy_path, device=device)
+    opt_cls = save_util._resolve_class(meta["bc"]["optimizer_cls"])
+    bc_trainer = bc.BC(observation_space=policy.observation_space, action_space=policy.action_space,
+                       rng=np.random.default_rng(), policy=policy, demonstrations=None,
+                       batch_size=meta["bc"]["batch_size"], minibatch_size=meta["bc"]["minibatch_size"],
+                       optimizer_cls=opt_cls, optimizer_kwargs=meta["bc"]["optimizer_kwargs"],
+                       ent_weight=meta["bc"]["ent_weight"], l2_weight=meta["bc"]["l2_weight"],
+                       custom_logger=custom_logger)
+    bc_trainer.optimizer.load_state_dict(ckpt["optimizer"])
+    rng = np.random.default_rng()
+    rng.bit_generator.state = meta["rng_state"]
+    kwargs = dict(venv=venv, scratch_dir=scratch_dir, rng=rng, beta_schedule=_schedule_from_json(meta["beta_schedule"]),
+                  bc_trainer=bc_trainer, custom_logger=custom_logger)
+    if meta["class"] == "SimpleDAggerTrainer":
+        expert = load_policy_file(scratch_dir / "expert-policy.pt", device=device)
+        trainer: DAggerTrainer = SimpleDAggerTrainer(expert_policy=expert, **kwargs)
+    else:
+        trainer = DAggerTrainer(**kwargs)
+    trainer.round_num = meta["round_num"]
     return trainer
 
 
@@ -257,14 +303,35 @@ class DAggerTrainer(base.BaseImitationAlgorithm):
                                               beta=beta, save_dir=save_dir, rng=self.rng)
 
     def save_trainer(self) -> Tuple[pathlib.Path, pathlib.Path]:
-        """Save ``checkpoint-{round}.pt`` / ``checkpoint-latest.pt`` and the policy files."""
+        """Save ``checkpoint-{round}.pt`` / ``checkpoint-latest.pt`` and ``policy-{round}.pt`` /
+        ``policy-latest.pt`` (tensor/JSON-only files; see :func:`reconstruct_trainer`)."""
         self.scratch_dir.mkdir(parents=True, exist_ok=True)
+        bct = self.bc_trainer
+        opt_cls = type(bct.optimizer)
+        meta = {
+            "class": type(self).__name__,
+            "round_num": self.round_num,
+            "beta_schedule": _schedule_to_json(self.beta_schedule),
+            "rng_state": self.rng.bit_generator.state,
+            "bc": {
+                "batch_size": bct.batch_size,
+                "minibatch_size": bct.minibatch_size,
+                "optimizer_cls": f"{opt_cls.__module__}:{opt_cls.__qualname__}",
+                "optimizer_kwargs": {k: v for k, v in bct.optimizer.defaults.items()
+                                     if k in ("lr", "eps", "amsgrad", "momentum", "alpha")},
+                "ent_weight": bct.loss_calculator.ent_weight,
+                "l2_weight": bct.loss_calculator.l2_weight,
+            },
+        }
+        ckpt = {"format": "imitation_amd.dagger.v1", "meta": json.dumps(meta), "optimizer": bct.optimizer.state_dict()}
         checkpoint_paths = [self.scratch_dir / f"checkpoint-{self.round_num:03d}.pt", self.scratch_dir / "checkpoint-latest.pt"]
         for p in checkpoint_paths:
-            th.save(self, p)
+            th.save(ckpt, p)
         policy_paths = [self.scratch_dir / f"policy-{self.round_num:03d}.pt", self.scratch_dir / "policy-latest.pt"]
         for p in policy_paths:
             util.save_policy(self.policy, p)
+        if hasattr(self, "expert_policy") and hasattr(self.expert_policy, "save"):
+            self.expert_policy.save(self.scratch_dir / "expert-policy.pt")
         return checkpoint_paths[0], policy_paths[0]
 
 

@@ -61,6 +61,12 @@ def _log_kernel_norm(kernel: str, h: float, d: int) -> float:
         factor = _log_sn(d - 1) + math.lgamma(d)
     elif kernel == "linear":
         factor = _log_vn(d) - math.log(d + 1.0)
+    elif kernel == "cosine":
+        acc, tmp = 0.0, 2.0 / math.pi
+        for k in range(1, d + 1, 2):
+            acc += tmp
+            tmp *= -(d - k) * (d - k - 1) * (2.0 / math.pi) ** 2
+        factor = math.log(acc) + _log_sn(d - 1)
     else:
         raise ValueError(f"unsupported kernel {kernel}")
     return -factor - d * math.log(h)
@@ -102,6 +108,8 @@ class DeviceKDE:
                     k = (1 - r * r).clamp_min(0)
                 elif self.kernel == "linear":
                     k = (1 - r).clamp_min(0)
+                elif self.kernel == "cosine":
+                    k = th.where(r < 1, th.cos(0.5 * math.pi * r), th.zeros_like(r))
                 else:
                     raise ValueError(self.kernel)
                 logk = th.log(k)

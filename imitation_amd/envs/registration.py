@@ -56,4 +56,9 @@ for _id, _steps in _NATIVE_IDS.items():
     core.register(_id, entry_point=functools.partial(_make_native, _id), max_episode_steps=_steps, native_id=_id)
 
 core.register("seals/RandomTransition-v0", entry_point=tabular.RandomTransitionEnv)
+core.register(
+    "seals/Random-v0",
+    entry_point=functools.partial(tabular.RandomTransitionEnv, n_states=16, n_actions=3, branch_factor=2, horizon=20,
+                                  random_obs=True, obs_dim=5, generator_seed=42),
+)
 core.register("seals/CliffWorld-v0", entry_point=tabular.CliffWorld)

@@ -67,8 +67,22 @@ class Box(Space):
             shape = low_a.shape if low_a.shape else high_a.shape
         shape = tuple(int(s) for s in shape)
         super().__init__(shape, dtype, seed)
-        self.low = np.broadcast_to(np.asarray(low, dtype=dtype), shape).copy()
-        self.high = np.broadcast_to(np.asarray(high, dtype=dtype), shape).copy()
+
+        def _cast(v, fill):
+            v = np.asarray(v, dtype=np.float64) if not np.issubdtype(np.asarray(v).dtype, np.integer) else np.asarray(v)
+            if np.issubdtype(dtype, np.integer) and v.dtype.kind == "f":
+                info = np.iinfo(dtype)  # unbounded integer boxes clamp to the dtype range (as gymnasium)
+                v = np.broadcast_to(v, shape)
+                out = np.zeros(shape, dtype=dtype)
+                fin = np.isfinite(v)
+                out[fin] = v[fin].astype(dtype)
+                out[np.isposinf(v)] = info.max
+                out[np.isneginf(v)] = info.min
+                return out
+            return np.broadcast_to(v.astype(dtype), shape).copy()
+
+        self.low = _cast(low, -np.inf)
+        self.high = _cast(high, np.inf)
 
     @property
     def bounded_below(self):

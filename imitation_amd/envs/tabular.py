@@ -54,8 +54,12 @@ class TabularModelPOMDP(core.Env):
         self._n_actions_taken: Optional[int] = None
 
     @property
-    def horizon(self) -> int:
+    def horizon(self) -> Optional[int]:
         return self._horizon
+
+    @horizon.setter
+    def horizon(self, h: Optional[int]) -> None:
+        self._horizon = None if h is None else int(h)
 
     @property
     def n_states(self) -> int:
@@ -115,7 +119,7 @@ class TabularModelPOMDP(core.Env):
         self._cur_state = new
         rew = self.reward_fn(old, int(action), new)
         self._n_actions_taken += 1
-        done = self._n_actions_taken >= self._horizon
+        done = self._horizon is not None and self._n_actions_taken >= self._horizon
         return self.obs_from_state(new), rew, False, done, {"old_state": old, "new_state": new}
 
 
@@ -134,7 +138,7 @@ class TabularModelMDP(TabularModelPOMDP):
 
 
 def make_random_trans_mat(n_states: int, n_actions: int, max_branch_factor: int, rand_state: np.random.Generator) -> np.ndarray:
-    out = np.zeros((n_states, n_actions, n_states), dtype=np.float32)
+    out = np.zeros((n_states, n_actions, n_states), dtype=np.float64)
     for s in range(n_states):
         for a in range(n_actions):
             succ = rand_state.choice(n_states, size=(max_branch_factor,), replace=False)
@@ -178,7 +182,7 @@ class RandomTransitionEnv(TabularModelPOMDP):
         rng = np.random.default_rng(generator_seed)
         obs_mat = make_obs_mat(n_states, random_obs, obs_dim, rng)
         trans = make_random_trans_mat(n_states, n_actions, branch_factor, rng)
-        init = make_random_state_dist(n_states, n_states, rng)
+        init = make_random_state_dist(branch_factor, n_states, rng)
         weights = rng.normal(0, 1, (obs_mat.shape[-1],))
         reward = obs_mat @ weights
         super().__init__(

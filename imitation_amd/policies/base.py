@@ -82,9 +82,18 @@ class HomogenousActorCriticPolicy(policies.ActorCriticPolicy):
 
     @classmethod
     def load(cls, observation_overide, action_overide, num_agents, path: str, device: Union[th.device, str] = "auto"):
+        import json
+
+        from imitation_amd.rl import save_util
+
         device = get_device(device)
-        saved = th.load(path, map_location=device, weights_only=False)
-        model = cls(observation_overide, action_overide, num_agents, **saved["data"])
+        saved = th.load(path, map_location=device, weights_only=True)
+        data = save_util._decode(json.loads(saved["data"])) if isinstance(saved.get("data"), str) else saved["data"]
+        for k in ("observation_overide", "action_overide", "num_agents"):
+            data.pop(k, None)
+        data["lr_schedule"] = lambda _: 0.0
+        data = {k: v for k, v in data.items() if v is not None}
+        model = cls(observation_overide, action_overide, num_agents, **data)
         model.load_state_dict(saved["state_dict"])
         model.to(device)
         return model

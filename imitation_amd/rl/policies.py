@@ -26,6 +26,8 @@ import pathlib
 import warnings
 from typing import Any, Dict, List, Optional, Tuple, Type, Union
 
+import json
+
 import numpy as np
 import torch as th
 from torch import nn
@@ -158,16 +160,25 @@ class BaseModel(nn.Module):
         return th.device("cpu")
 
     def save(self, path) -> None:
-        th.save({"state_dict": self.state_dict(), "data": self._get_constructor_parameters(), "class": type(self).__name__}, path)
+        """Save as a tensor-only file: state dict + JSON constructor parameters + class path.
+
+        Loadable with ``torch.load(weights_only=True)`` -- nothing is unpickled on load.
+        """
+        from imitation_amd.rl import save_util
+
+        th.save(
+            {
+                "format": "imitation_amd.policy.v1",
+                "class": f"{type(self).__module__}:{type(self).__qualname__}",
+                "data": json.dumps(save_util._encode(self._get_constructor_parameters())),
+                "state_dict": self.state_dict(),
+            },
+            path,
+        )
 
     @classmethod
     def load(cls, path, device: Union[th.device, str] = "auto"):
-        device = get_device(device)
-        saved = th.load(path, map_location=device, weights_only=False)
-        model = cls(**saved["data"])
-        model.load_state_dict(saved["state_dict"])
-        model.to(device)
-        return model
+        return load_policy_file(path, device=device, expected_cls=cls)
 
     def load_from_vector(self, vector: np.ndarray) -> None:
         th.nn.utils.vector_to_parameters(th.as_tensor(vector, dtype=th.float, device=self.device), self.parameters())
@@ -557,3 +568,52 @@ class MultiInputActorCriticPolicy(ActorCriticPolicy):
 MlpPolicy = ActorCriticPolicy
 CnnPolicy = ActorCriticCnnPolicy
 MultiInputPolicy = MultiInputActorCriticPolicy
+
+
+def load_policy_file(path, device: Union[th.device, str] = "auto", expected_cls=None):
+    """Load a policy written by :meth:`BaseModel.save` (tensor-only file, ``weights_only=True``).
+
+    The class is resolved by import path and restricted to this package. Classes whose
+    ``__init__`` pins some constructor arguments (e.g. ``FeedForward32Policy``) are
+    rebuilt through the nearest base ``__init__`` that accepts the saved arguments.
+    """
+    from imitation_amd.rl import save_util
+
+    device = get_device(device)
+    saved = th.load(path, map_location=device, weights_only=True)
+    if not isinstance(saved, dict) or saved.get("format") != "imitation_amd.policy.v1":
+        raise ValueError(f"{path} is not a policy file written by imitation_amd")
+    cls_path = saved["class"]
+    if not cls_path.startswith("imitation_amd."):
+        raise ValueError(f"refusing to construct class outside imitation_amd: {cls_path}")
+    pcls = save_util._resolve_class(cls_path)
+    if expected_cls is not None and not issubclass(pcls, expected_cls):
+        raise TypeError(f"{path} holds a {pcls.__name__}, not a {expected_cls.__name__}")
+    data = save_util._decode(json.loads(saved["data"]))
+    if "lr_schedule" in data or issubclass(pcls, ActorCriticPolicy):
+        data["lr_schedule"] = _constant_zero
+    data = {k: v for k, v in data.items() if v is not None or k in ("net_arch",)}
+    try:
+        model = pcls(**data)
+    except TypeError:
+        model = None
+        for base in pcls.__mro__[1:]:
+            if base is object or not issubclass(base, BaseModel):
+                continue
+            try:
+                obj = pcls.__new__(pcls)
+                base.__init__(obj, **data)
+                model = obj
+                break
+            except TypeError:
+                continue
+        if model is None:
+            raise
+    model.load_state_dict(saved["state_dict"])
+    model.to(device)
+    return model
+
+
+def _constant_zero(_progress: float) -> float:
+    return 0.0
+

@@ -84,10 +84,6 @@ def _space_from_sb3_json(d: Dict[str, Any]) -> Optional[spaces.Space]:
             high = np.full(shape, high.item())
         low = low.reshape(shape)
         high = high.reshape(shape)
-        if np.issubdtype(dt, np.floating):
-            fi = np.finfo(dt)
-            low = np.where(np.abs(low) >= fi.max * 0.999, -np.inf, low)
-            high = np.where(np.abs(high) >= fi.max * 0.999, np.inf, high)
         return spaces.Box(low.astype(dt), high.astype(dt), shape, dt)
     if "MultiDiscrete" in t:
         return spaces.MultiDiscrete(_parse_np_repr(d["nvec"], np.int64))

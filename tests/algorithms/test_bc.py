@@ -1,0 +1,100 @@
+"""Behavioral cloning (reference: tests/algorithms/test_bc.py)."""
+
+import numpy as np
+import pytest
+import torch as th
+
+from imitation_amd.algorithms import bc
+from imitation_amd.data import rollout, types
+from imitation_amd.policies import base as policy_base
+from imitation_amd.testing import reward_improvement
+from imitation_amd.util import util
+
+
+@pytest.fixture
+def expert_transitions(cartpole_expert_trajectories):
+    return rollout.flatten_trajectories(cartpole_expert_trajectories[:10])
+
+
+@pytest.mark.parametrize("data_kind", ["transitions", "trajectories", "data_loader", "dict_iter"])
+def test_bc_accepts_demonstration_kinds(data_kind, cartpole_venv, cartpole_expert_trajectories, expert_transitions, rng,
+                                        custom_logger):
+    if data_kind == "transitions":
+        demos = expert_transitions
+    elif data_kind == "trajectories":
+        demos = cartpole_expert_trajectories[:3]
+    elif data_kind == "data_loader":
+        demos = th.utils.data.DataLoader(expert_transitions, batch_size=32, shuffle=True, drop_last=True,
+                                         collate_fn=types.transitions_collate_fn)
+    else:
+        demos = [types.transitions_collate_fn([expert_transitions[i] for i in range(j, j + 32)]) for j in range(0, 320, 32)]
+    trainer = bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+                    rng=rng, demonstrations=demos, batch_size=32, custom_logger=custom_logger)
+    trainer.train(n_batches=5)
+
+
+def test_bc_train_requires_exactly_one_duration(cartpole_venv, expert_transitions, rng):
+    trainer = bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+                    rng=rng, demonstrations=expert_transitions, batch_size=32)
+    with pytest.raises(ValueError):
+        trainer.train(n_epochs=1, n_batches=1)
+    with pytest.raises(ValueError):
+        trainer.train()
+
+
+def test_bc_improves_policy(cartpole_venv, cartpole_expert_trajectories, rng):
+    """BC on CartPole expert data improves returns significantly (reference test_bc.py:200-232)."""
+    trainer = bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+                    rng=rng, demonstrations=rollout.flatten_trajectories(cartpole_expert_trajectories), batch_size=64)
+    before = rollout.rollout(trainer.policy, cartpole_venv, rollout.make_min_episodes(15), rng=rng, deterministic_policy=True)
+    trainer.train(n_epochs=3)
+    after = rollout.rollout(trainer.policy, cartpole_venv, rollout.make_min_episodes(15), rng=rng, deterministic_policy=True)
+    old = [t.rews.sum() for t in before]
+    new = [t.rews.sum() for t in after]
+    assert reward_improvement.mean_reward_improved_by(old, new, 50)
+    assert reward_improvement.is_significant_reward_improvement(old, new, p_value=0.05)
+
+
+def test_gradient_accumulation_matches_large_batch(cartpole_venv, expert_transitions):
+    """minibatch_size accumulation == one big batch (reference test_bc.py:235-283)."""
+    batch_size, mini = 64, 16
+    trainers = []
+    for mb in (batch_size, mini):
+        th.manual_seed(0)
+        pol = policy_base.FeedForward32Policy(observation_space=cartpole_venv.observation_space,
+                                              action_space=cartpole_venv.action_space,
+                                              lr_schedule=lambda _: th.finfo(th.float32).max)
+        trainers.append(bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+                              rng=np.random.default_rng(0), policy=pol, demonstrations=None, batch_size=batch_size,
+                              minibatch_size=mb, optimizer_kwargs=dict(lr=1e-3)))
+    # identical data stream for both
+    data = [types.transitions_collate_fn([expert_transitions[i] for i in range(j, j + batch_size)])
+            for j in range(0, 4 * batch_size, batch_size)]
+    trainers[0].set_demonstrations(data)
+    small = []
+    for d in data:
+        for k in range(0, batch_size, mini):
+            small.append({key: (v[k:k + mini] if not isinstance(v, list) else v[k:k + mini]) for key, v in d.items()})
+    trainers[1].set_demonstrations(small)
+    trainers[0].train(n_batches=4)
+    trainers[1].train(n_batches=4)
+    for p1, p2 in zip(trainers[0].policy.parameters(), trainers[1].policy.parameters()):
+        np.testing.assert_allclose(p1.detach().numpy(), p2.detach().numpy(), atol=1e-5, rtol=1e-4)
+
+
+def test_bc_policy_save_load(tmp_path, cartpole_venv, expert_transitions, rng):
+    trainer = bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+                    rng=rng, demonstrations=expert_transitions, batch_size=32)
+    trainer.train(n_batches=3)
+    path = tmp_path / "policy.pt"
+    util.save_policy(trainer.policy, path) if hasattr(util, "save_policy") else trainer.save_policy(path)
+    pol = bc.reconstruct_policy(str(path), device="cpu")
+    obs = np.asarray(expert_transitions.obs[:20])
+    a1, _ = trainer.policy.predict(obs, deterministic=True)
+    a2, _ = pol.predict(obs, deterministic=True)
+    np.testing.assert_array_equal(a1, a2)
+
+
+def test_bc_loss_calculator_values():
+    calc = bc.BehaviorCloningLossCalculator(ent_weight=1e-3, l2_weight=0.0)
+    assert calc.ent_weight == 1e-3

@@ -1,0 +1,197 @@
+"""MCE IRL and tabular environments (reference: tests/algorithms/test_mce_irl.py)."""
+
+import numpy as np
+import pytest
+import torch as th
+
+from imitation_amd.algorithms import base
+from imitation_amd.algorithms.mce_irl import MCEIRL, TabularPolicy, mce_occupancy_measures, mce_partition_fh
+from imitation_amd.data import rollout
+from imitation_amd.envs import core, spaces, tabular
+from imitation_amd.envs.vec_env import DummyVecEnv
+from imitation_amd.rewards import reward_nets
+from imitation_amd.util.util import tensor_iter_norm
+
+
+@pytest.fixture
+def random_mdp():
+    return tabular.RandomTransitionEnv(n_states=5, n_actions=3, branch_factor=2, horizon=10, random_obs=False,
+                                       obs_dim=None, generator_seed=42)
+
+
+def make_reward_net(env):
+    return reward_nets.BasicRewardNet(env.observation_space, env.action_space, use_action=False, use_next_state=False,
+                                      use_done=False, hid_sizes=[])
+
+
+def _rollouts(env, n=10, seed=None):
+    rv = []
+    for _ in range(n):
+        obs, _ = env.reset(seed=seed)
+        if seed is not None:
+            env.action_space.seed(seed)
+        traj, done = [obs], False
+        while not done:
+            obs, rew, term, trunc, _ = env.step(env.action_space.sample())
+            done = term or trunc
+            traj.append((obs, rew))
+        rv.append(traj)
+    return rv
+
+
+def test_random_mdp():
+    for i in range(3):
+        n_states, n_actions, branch = 4 * (i + 3), i + 2, i + 1
+        if branch == 1:
+            n_actions = min(n_states, max(n_actions, 4))
+        horizon = 5 * (i + 1)
+        random_obs = (i % 2) == 0
+        obs_dim = (i * 3 + 4) ** 2 + i
+        mdp = tabular.RandomTransitionEnv(n_states=n_states, n_actions=n_actions, branch_factor=branch, horizon=horizon,
+                                          random_obs=random_obs, obs_dim=obs_dim if random_obs else None, generator_seed=i)
+        assert mdp.transition_matrix.shape == (n_states, n_actions, n_states)
+        assert np.allclose(1, mdp.transition_matrix.sum(-1)) and np.all(mdp.transition_matrix >= 0)
+        assert mdp.observation_matrix.shape[0] == n_states and mdp.observation_matrix.ndim == 2
+        assert mdp.reward_matrix.shape == (n_states,) and mdp.horizon == horizon
+        assert np.allclose(1, mdp.initial_state_dist.sum()) and np.sum(mdp.initial_state_dist > 0) == branch
+        assert len(set(map(str, _rollouts(mdp, 100)))) > 1
+        assert len(set(map(str, _rollouts(mdp, 100, seed=42)))) == 1
+
+
+def test_infinite_horizon_error(random_mdp, rng):
+    random_mdp.horizon = None
+    with pytest.raises(ValueError, match="Only finite-horizon.*"):
+        mce_partition_fh(random_mdp)
+    with pytest.raises(ValueError, match="Only finite-horizon.*"):
+        mce_occupancy_measures(random_mdp)
+    with pytest.raises(ValueError, match="Only finite-horizon.*"):
+        MCEIRL(None, random_mdp, make_reward_net(random_mdp), rng)
+
+
+@pytest.mark.parametrize("discount", [0.0, 0.5, 0.9, 0.99, 1.0])
+def test_policy_om_random_mdp(discount):
+    mdp = core.make("seals/Random-v0").unwrapped
+    V, Q, pi = mce_partition_fh(mdp, discount=discount)
+    assert np.all(np.isfinite(V)) and np.all(np.isfinite(Q)) and np.all(np.isfinite(pi))
+    assert np.all(pi >= 0) and np.allclose(pi.sum(-1), 1)
+    Dt, D = mce_occupancy_measures(mdp, pi=pi, discount=discount)
+    assert len(Dt) == mdp.horizon + 1 and np.all(np.isfinite(D)) and np.any(D > 0)
+    expected = mdp.horizon + 1.0 if discount == 1.0 else (1 - discount ** (mdp.horizon + 1)) / (1 - discount)
+    assert np.allclose(D.sum(), expected)
+
+
+class ReasonablePOMDP(tabular.TabularModelPOMDP):
+    """5-state MDP where actions 0/2 are good, action 1 leads to a very bad state."""
+
+    def __init__(self):
+        obs = np.array([[3, -5, -1, -1, -4, 5, 3, 0], [4, -4, 2, 2, -4, -1, -2, -2], [3, -1, 5, -1, 0, 2, -5, 2],
+                        [-5, -1, 4, 1, 4, 1, 5, 3], [2, -5, 1, -5, 1, 4, 4, -3]], dtype=np.float32)
+        T = np.zeros((5, 3, 5))
+        T[0, 0, [1, 2]] = [0.9, 0.1]
+        T[0, 1, 3] = 1
+        T[0, 2, [1, 2]] = [0.1, 0.9]
+        for s in (1, 2):
+            T[s, 0, [3, 4]] = [0.05, 0.95]
+            T[s, 1, 3] = 1
+            T[s, 2, 4] = 1
+        T[3, :, 4] = 1
+        T[4, :, 0] = 1
+        R = np.array([1, 2, 2, -20, 1], dtype=np.float64)
+        super().__init__(transition_matrix=T, observation_matrix=obs, reward_matrix=R, horizon=20,
+                         initial_state_dist=np.array([1.0, 0, 0, 0, 0]))
+
+
+@pytest.mark.parametrize("discount", [0.0, 0.99, 1.0])
+def test_policy_om_reasonable_pomdp(discount):
+    pomdp = ReasonablePOMDP()
+    V, Q, pi = mce_partition_fh(pomdp, discount=discount)
+    Dt, D = mce_occupancy_measures(pomdp, pi=pi, discount=discount)
+    for x in (V, Q, pi, Dt, D):
+        assert np.all(np.isfinite(x))
+    assert np.allclose(pi[:19, 0, 0], pi[:19, 0, 2])
+    if discount > 0:
+        assert np.all(pi[:19, 0, 0] > 2 * pi[:19, 0, 1])
+    assert np.allclose(pi[:5, 3:5], 1 / 3.0)
+    assert np.allclose(pi[:19, 1, :], pi[:19, 2, :])
+    if discount > 0:
+        assert np.all(pi[:19, 1, 2] > pi[:19, 1, 0]) and np.all(pi[:19, 1, 0] > pi[:19, 1, 1])
+    assert np.allclose(Dt[0], pomdp.initial_state_dist)
+
+
+def test_tabular_policy(rng):
+    pi = np.stack([np.eye(2), 1 - np.eye(2)])
+    tab = TabularPolicy(state_space=spaces.Discrete(2), action_space=spaces.Discrete(2), pi=pi, rng=rng)
+    states = np.array([0, 1, 1, 0, 1])
+    actions, ts = tab.predict(states)
+    np.testing.assert_array_equal(states, actions)
+    np.testing.assert_equal(ts[0], 1)
+    actions, ts = tab.predict(states, ts, np.zeros(5, bool))
+    np.testing.assert_array_equal(1 - states, actions)
+    np.testing.assert_equal(ts[0], 2)
+    actions, ts = tab.predict(states, ts, np.ones(5, bool))
+    np.testing.assert_array_equal(states, actions)
+    mask = (1 - states).astype(bool)
+    actions, ts = tab.predict(states, ts, mask)
+    np.testing.assert_array_equal(np.zeros(5), actions)
+    np.testing.assert_equal(ts[0], 2 - mask.astype(int))
+
+
+def test_tabular_policy_randomness(rng):
+    pi = np.array([[[0.5, 0.5], [0.9, 0.1]]])
+    tab = TabularPolicy(state_space=spaces.Discrete(2), action_space=spaces.Discrete(2), pi=pi, rng=rng)
+    assert 0.45 <= np.mean(tab.predict(np.zeros(1000, int))[0]) <= 0.55
+    assert 0.05 <= np.mean(tab.predict(np.ones(1000, int))[0]) <= 0.15
+    np.testing.assert_equal(tab.predict(np.ones(1000, int), deterministic=True)[0], 0)
+
+
+def test_tabular_policy_rollouts(rng):
+    mdp = ReasonablePOMDP()
+    venv = DummyVecEnv([lambda: tabular.ExposePOMDPStateWrapper(mdp)])
+    sub = np.stack([np.eye(3)] * 5, axis=1)
+    pi = np.repeat(sub, (mdp.horizon + 2) // 3, axis=0)
+    tab = TabularPolicy(state_space=spaces.Discrete(5), action_space=spaces.Discrete(3), pi=pi, rng=rng)
+    trajs = rollout.generate_trajectories(tab, venv, sample_until=rollout.make_min_episodes(1), rng=rng)
+    exposed = pi[:, 0, :].nonzero()[1]
+    assert (trajs[0].acts == exposed[: len(trajs[0].acts)]).all()
+
+
+def test_mce_irl_demo_formats(rng, random_mdp):
+    venv = DummyVecEnv([lambda: tabular.ExposePOMDPStateWrapper(random_mdp)])
+    trajs = rollout.generate_trajectories(policy=None, venv=venv, sample_until=rollout.make_min_timesteps(100), rng=rng)
+    demos = {
+        "trajs": trajs,
+        "trans": rollout.flatten_trajectories(trajs),
+        "data_loader": base.make_data_loader(trajs, batch_size=32, data_loader_kwargs=dict(drop_last=False)),
+    }
+    final = {}
+    for kind, demo in demos.items():
+        with th.random.fork_rng():
+            th.random.manual_seed(715298)
+            mce = MCEIRL(demo, random_mdp, make_reward_net(random_mdp), linf_eps=1e-3, rng=rng)
+            assert np.allclose(mce.demo_state_om.sum(), random_mdp.horizon + 1)
+            final[kind] = mce.train(max_iter=5)
+            assert tensor_iter_norm(mce.reward_net.parameters()) < 1000
+    for k, cts in final.items():
+        assert np.allclose(cts, final["trajs"], atol=1e-3, rtol=1e-3), k
+
+
+@pytest.mark.parametrize("hid", [[], [32, 32]])
+@pytest.mark.parametrize("discount", [0.0, 0.99, 1.0])
+def test_mce_irl_reasonable_mdp(hid, discount, rng):
+    with th.random.fork_rng():
+        th.random.manual_seed(715298)
+        mdp = ReasonablePOMDP()
+        mdp.reset(seed=715298)
+        V, Q, pi = mce_partition_fh(mdp, discount=discount)
+        Dt, D = mce_occupancy_measures(mdp, pi=pi, discount=discount)
+        rn = reward_nets.BasicRewardNet(mdp.observation_space, mdp.action_space, use_action=False, use_next_state=False,
+                                        use_done=False, hid_sizes=hid)
+        mce = MCEIRL(D, mdp, rn, linf_eps=1e-3, discount=discount, rng=rng)
+        final = mce.train()
+        assert np.allclose(final, D, atol=1e-3, rtol=1e-3)
+        assert tensor_iter_norm(rn.parameters()) < 1000
+        venv = DummyVecEnv([lambda: tabular.ExposePOMDPStateWrapper(mdp)])
+        trajs = rollout.generate_trajectories(mce.policy, venv, sample_until=rollout.make_min_episodes(5), rng=rng)
+        stats = rollout.rollout_stats(trajs)
+        if discount > 0.0:
+            assert stats["return_mean"] >= 15

@@ -47,9 +47,11 @@ def device():
 
 @pytest.fixture(params=[1, 4])
 def cartpole_venv(request, rng):
+    from imitation_amd.data.wrappers import RolloutInfoWrapper
     from imitation_amd.util.util import make_vec_env
 
-    return make_vec_env("CartPole-v1", rng=rng, n_envs=request.param)
+    return make_vec_env("seals/CartPole-v0", rng=rng, n_envs=request.param,
+                        post_wrappers=[lambda e, _: RolloutInfoWrapper(e)])
 
 
 @pytest.fixture
@@ -57,3 +59,59 @@ def custom_logger(tmp_path):
     from imitation_amd.util import logger
 
     return logger.configure(str(tmp_path))
+
+
+TESTDATA = os.path.join(ROOT, "tests", "testdata")
+CARTPOLE_EXPERT_ZIP = os.path.join(TESTDATA, "expert_models", "cartpole_0", "policies", "final", "model.zip")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def local_expert_hub(tmp_path_factory):
+    """A local stand-in for the HF hub holding the checked-in CartPole expert
+    (the reference pulls ``HumanCompatibleAI/ppo-<env>`` from the network)."""
+    hub = tmp_path_factory.mktemp("hub")
+    for env_name in ("seals-CartPole-v0", "CartPole-v1", "CartPole-v0"):
+        d = hub / "HumanCompatibleAI" / f"ppo-{env_name}"
+        d.mkdir(parents=True)
+        os.symlink(CARTPOLE_EXPERT_ZIP, d / "model.zip")
+    old = os.environ.get("IMITATION_AMD_HUB")
+    os.environ["IMITATION_AMD_HUB"] = str(hub)
+    yield hub
+    if old is None:
+        os.environ.pop("IMITATION_AMD_HUB", None)
+    else:
+        os.environ["IMITATION_AMD_HUB"] = old
+
+
+@pytest.fixture(scope="session")
+def expert_cache_dir(tmp_path_factory):
+    return tmp_path_factory.mktemp("experts")
+
+
+@pytest.fixture
+def cartpole_expert_trajectories(expert_cache_dir):
+    from imitation_amd.testing.expert_trajectories import lazy_generate_expert_trajectories
+
+    return lazy_generate_expert_trajectories(expert_cache_dir, "seals/CartPole-v0", 60, np.random.default_rng(0))
+
+
+@pytest.fixture
+def cartpole_expert_policy(cartpole_venv):
+    from imitation_amd.policies import serialize
+
+    return serialize.load_policy("ppo-huggingface", cartpole_venv, env_name="seals/CartPole-v0")
+
+
+@pytest.fixture
+def pendulum_expert_trajectories():
+    from imitation_amd.data import serialize
+
+    return serialize.load_with_rewards(os.path.join(TESTDATA, "expert_models", "pendulum_0", "rollouts", "final.npz"))
+
+
+@pytest.fixture
+def pendulum_venv(rng):
+    from imitation_amd.data.wrappers import RolloutInfoWrapper
+    from imitation_amd.util.util import make_vec_env
+
+    return make_vec_env("Pendulum-v1", rng=rng, n_envs=4, post_wrappers=[lambda e, _: RolloutInfoWrapper(e)])
