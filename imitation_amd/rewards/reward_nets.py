@@ -31,9 +31,10 @@ from torch import nn
 from imitation_amd.envs import spaces
 from imitation_amd.rl import preprocessing
 from imitation_amd.util import networks, util
+from imitation_amd.util.module_spec import SpecRecorded
 
 
-class RewardNet(nn.Module, abc.ABC):
+class RewardNet(SpecRecorded, nn.Module, abc.ABC):
     """Minimal abstract reward network: implement ``forward(state, action, next_state, done)``."""
 
     def __init__(self, observation_space: spaces.Space, action_space: spaces.Space, normalize_images: bool = True):
@@ -296,7 +297,7 @@ class ShapedRewardNet(ForwardWrapper):
         return final
 
 
-class BasicPotentialMLP(nn.Module):
+class BasicPotentialMLP(SpecRecorded, nn.Module):
     """Potential Φ(s) as a flat MLP."""
 
     def __init__(self, observation_space: spaces.Space, hid_sizes: Iterable[int], **kwargs):
@@ -308,7 +309,7 @@ class BasicPotentialMLP(nn.Module):
         return self._potential_net(state)
 
 
-class BasicPotentialCNN(nn.Module):
+class BasicPotentialCNN(SpecRecorded, nn.Module):
     """Potential Φ(s) as a CNN over image observations."""
 
     def __init__(self, observation_space: spaces.Space, hid_sizes: Iterable[int], hwc_format: bool = True, **kwargs):

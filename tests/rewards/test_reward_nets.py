@@ -1,0 +1,125 @@
+"""Reward nets, wrappers and serialization (reference: tests/rewards/test_reward_nets.py)."""
+
+import numpy as np
+import pytest
+import torch as th
+
+from imitation_amd.envs import spaces
+from imitation_amd.rewards import reward_nets, serialize
+from imitation_amd.testing import reward_nets as testing_reward_nets
+from imitation_amd.util import networks
+
+OBS = spaces.Box(-1, 1, (4,))
+ACT = spaces.Discrete(3)
+
+
+def _batch(n=10, seed=0):
+    r = np.random.default_rng(seed)
+    obs = r.uniform(-1, 1, (n, 4)).astype(np.float32)
+    return obs, r.integers(0, 3, n), r.uniform(-1, 1, (n, 4)).astype(np.float32), r.random(n) < 0.2
+
+
+MAKERS = {
+    "basic": lambda: reward_nets.BasicRewardNet(OBS, ACT),
+    "basic_norm": lambda: reward_nets.BasicRewardNet(OBS, ACT, normalize_input_layer=networks.RunningNorm),
+    "shaped": lambda: reward_nets.BasicShapedRewardNet(OBS, ACT),
+    "normalized": lambda: reward_nets.NormalizedRewardNet(reward_nets.BasicRewardNet(OBS, ACT), networks.RunningNorm),
+    "normalized_shaped": lambda: reward_nets.NormalizedRewardNet(reward_nets.BasicShapedRewardNet(OBS, ACT), networks.RunningNorm),
+    "ensemble_std": lambda: reward_nets.AddSTDRewardWrapper(testing_reward_nets.make_ensemble(OBS, ACT, 3), default_alpha=0.1),
+    "normalized_ensemble_std": lambda: reward_nets.NormalizedRewardNet(
+        reward_nets.AddSTDRewardWrapper(testing_reward_nets.make_ensemble(OBS, ACT, 2)), networks.RunningNorm),
+}
+
+
+@pytest.mark.parametrize("name", list(MAKERS))
+def test_serialize_identity(name, tmp_path):
+    net = MAKERS[name]()
+    b = _batch()
+    path = tmp_path / "net.pt"
+    serialize.save_reward_net(net, path)
+    loaded = serialize.load_reward_net(path)
+    assert type(loaded) is type(net)
+    np.testing.assert_allclose(net.predict(*b), loaded.predict(*b), rtol=1e-6)
+
+
+@pytest.mark.parametrize(
+    "name,key",
+    [("shaped", "RewardNet_shaped"), ("shaped", "RewardNet_unshaped"), ("normalized", "RewardNet_normalized"),
+     ("normalized", "RewardNet_unnormalized"), ("ensemble_std", "RewardNet_std_added"),
+     ("normalized_ensemble_std", "RewardNet_std_added"), ("basic", "zero")],
+)
+def test_load_reward_registry(name, key, tmp_path):
+    net = MAKERS[name]()
+    path = tmp_path / "net.pt"
+    serialize.save_reward_net(net, path)
+    fn = serialize.load_reward(key, str(path), None)
+    b = _batch()
+    out = fn(*b)
+    assert out.shape == (10,)
+    if key == "RewardNet_unshaped":
+        np.testing.assert_allclose(out, net.base.predict(*b), rtol=1e-6)
+    if key == "RewardNet_unnormalized":
+        np.testing.assert_allclose(out, net.base.predict(*b), rtol=1e-6)
+    if key == "zero":
+        assert np.all(out == 0)
+
+
+def test_wrong_wrapper_structure_raises(tmp_path):
+    serialize.save_reward_net(MAKERS["basic"](), tmp_path / "n.pt")
+    with pytest.raises(TypeError, match="Wrapper structure should match"):
+        serialize.load_reward("RewardNet_shaped", str(tmp_path / "n.pt"), None)
+
+
+def test_shaping_formula():
+    base = reward_nets.BasicRewardNet(OBS, ACT)
+    pot = reward_nets.BasicPotentialMLP(OBS, hid_sizes=[8])
+    shaped = reward_nets.ShapedRewardNet(base, pot, discount_factor=0.9)
+    s, a, ns, d = shaped.preprocess(*_batch())
+    expect = base(s, a, ns, d) + 0.9 * (1 - d) * pot(ns).flatten() - pot(s).flatten()
+    th.testing.assert_close(shaped(s, a, ns, d), expect)
+
+
+def test_normalized_reward_net_stats():
+    net = MAKERS["normalized"]()
+    b = _batch(200)
+    for _ in range(20):
+        net.predict_processed(*b)
+    out = net.predict_processed(*b, update_stats=False)
+    assert abs(out.mean()) < 0.1 and abs(out.std() - 1) < 0.2
+
+
+def test_ensemble_moments():
+    ens = testing_reward_nets.make_ensemble(OBS, ACT, 4)
+    b = _batch()
+    all_r = ens.predict_processed_all(*b)
+    mean, var = ens.predict_reward_moments(*b)
+    np.testing.assert_allclose(mean, all_r.mean(-1), rtol=1e-6)
+    np.testing.assert_allclose(var, all_r.var(-1, ddof=1), rtol=1e-5)
+    with pytest.raises(ValueError):
+        reward_nets.RewardEnsemble(OBS, ACT, [reward_nets.BasicRewardNet(OBS, ACT)])
+
+
+def test_add_std_requires_variance():
+    with pytest.raises(TypeError):
+        reward_nets.AddSTDRewardWrapper(reward_nets.BasicRewardNet(OBS, ACT))
+
+
+def test_forward_wrapper_on_predict_processed_raises():
+    with pytest.raises(ValueError):
+        reward_nets.ShapedRewardNet(MAKERS["normalized"](), lambda x: x.sum(1), 0.9)
+
+
+def test_mock_reward_net():
+    m = testing_reward_nets.MockRewardNet(OBS, ACT, value=2.5)
+    np.testing.assert_allclose(m.predict(*_batch()), 2.5)
+
+
+def test_cnn_reward_net_shapes():
+    img = spaces.Box(0, 255, (16, 16, 3), dtype=np.uint8)
+    for kw in (dict(use_action=True, use_done=False), dict(use_action=True, use_done=True), dict(use_action=False, use_done=True)):
+        net = reward_nets.CnnRewardNet(img, ACT, hid_channels=(4, 4), **kw)
+        obs = np.random.randint(0, 255, (5, 16, 16, 3), dtype=np.uint8)
+        out = net.predict(obs, np.array([0, 1, 2, 0, 1]), obs, np.array([0, 1, 0, 0, 1], bool))
+        assert out.shape == (5,)
+    with pytest.raises(ValueError):
+        reward_nets.CnnRewardNet(OBS, ACT)
