@@ -102,9 +102,41 @@ py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch:
   return py::make_tuple(adv, ret);
 }
 
+// Returns (probs [P], losses [P], coef [P]).
+py::tuple pref_loss_fwd(torch::Tensor r1, torch::Tensor r2, torch::Tensor prefs, double discount, double threshold,
+                        double noise) {
+  IA_CHECK_GPU_F32(r1);
+  IA_CHECK_GPU_F32(r2);
+  IA_CHECK_GPU_F32(prefs);
+  TORCH_CHECK(r1.dim() == 2 && r1.sizes() == r2.sizes(), "r1/r2 must be [P, L] of equal shape");
+  const int P = (int)r1.size(0), L = (int)r1.size(1);
+  TORCH_CHECK(prefs.numel() == P, "one preference per pair");
+  auto probs = torch::empty({P}, r1.options());
+  auto losses = torch::empty({P}, r1.options());
+  auto coef = torch::empty({P}, r1.options());
+  IA_HIP_CHECK(ia::pref_loss_fwd(r1.data_ptr<float>(), r2.data_ptr<float>(), prefs.data_ptr<float>(), P, L,
+                                 (float)discount, (float)threshold, (float)noise, probs.data_ptr<float>(),
+                                 losses.data_ptr<float>(), coef.data_ptr<float>(), ia_stream()));
+  return py::make_tuple(probs, losses, coef);
+}
+
+py::tuple pref_loss_bwd(torch::Tensor coef, torch::Tensor gout, int64_t L, double discount) {
+  IA_CHECK_GPU_F32(coef);
+  IA_CHECK_GPU_F32(gout);
+  const int P = (int)coef.numel();
+  auto d1 = torch::empty({P, L}, coef.options());
+  auto d2 = torch::empty({P, L}, coef.options());
+  IA_HIP_CHECK(ia::pref_loss_bwd(coef.data_ptr<float>(), gout.data_ptr<float>(), P, (int)L, (float)discount,
+                                 d1.data_ptr<float>(), d2.data_ptr<float>(), ia_stream()));
+  return py::make_tuple(d1, d2);
+}
+
 }  // namespace
 
 void register_kernels(py::module& m) {
+  m.def("pref_loss_fwd", &pref_loss_fwd, py::arg("r1"), py::arg("r2"), py::arg("prefs"), py::arg("discount"),
+        py::arg("threshold"), py::arg("noise"));
+  m.def("pref_loss_bwd", &pref_loss_bwd, py::arg("coef"), py::arg("gout"), py::arg("L"), py::arg("discount"));
   m.def("tmlp_forward", &tmlp_forward, py::arg("x"), py::arg("weights"), py::arg("biases"), py::arg("hidden_act"),
         py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
         py::arg("norm_eps") = 1e-5, py::arg("norm_clip") = 0.0);

@@ -23,6 +23,12 @@ hipError_t tmlp_backward(const MLPDesc& d, const float* X, const float* dY, int 
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
                       int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);
 
+// ---- pref.hip: Bradley-Terry preference loss over fragment pairs
+hipError_t pref_loss_fwd(const float* r1, const float* r2, const float* prefs, int P, int L, float discount,
+                         float threshold, float noise, float* probs, float* losses, float* coef, hipStream_t s);
+hipError_t pref_loss_bwd(const float* coef, const float* gout, int P, int L, float discount, float* d1, float* d2,
+                         hipStream_t s);
+
 // ---- engine.hip: device-resident rollout (policy + env + learned reward)
 size_t rollout_lds_bytes(const RolloutArgs& a);
 hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s);

@@ -116,3 +116,25 @@ def test_native_extension_is_loaded_on_gpu():
     C = _native.load()
     assert C.arch == "gfx950"
     assert ops.use_kernel(th.zeros(1, device="cuda"))
+
+
+@gpu
+@pytest.mark.parametrize("P,L,discount,noise,thr", [(32, 50, 1.0, 0.0, 50.0), (7, 3, 0.9, 0.1, 2.0), (200, 130, 0.99, 0.0, 50.0)])
+def test_preference_kernel_matches_reference(P, L, discount, noise, thr):
+    from imitation_amd.ops import preference as pref_ops
+
+    g = th.Generator().manual_seed(P + L)
+    r1 = th.randn(P, L, generator=g)
+    r2 = th.randn(P, L, generator=g)
+    prefs = (th.rand(P, generator=g) > 0.5).float()
+    prefs[::5] = 0.5
+    a1, a2 = r1.clone().requires_grad_(), r2.clone().requires_grad_()
+    loss_r, probs_r = pref_ops.bradley_terry_reference(a1, a2, prefs, discount, thr, noise)
+    loss_r.backward()
+    b1, b2 = r1.cuda().requires_grad_(), r2.cuda().requires_grad_()
+    loss, probs = pref_ops.bradley_terry(b1, b2, prefs.cuda(), discount, thr, noise)
+    (3.0 * loss).backward()
+    th.testing.assert_close(loss.cpu(), loss_r.detach(), rtol=1e-5, atol=1e-6)
+    th.testing.assert_close(probs.cpu(), probs_r.detach(), rtol=1e-5, atol=1e-6)
+    th.testing.assert_close(b1.grad.cpu(), 3.0 * a1.grad, rtol=1e-4, atol=1e-7)
+    th.testing.assert_close(b2.grad.cpu(), 3.0 * a2.grad, rtol=1e-4, atol=1e-7)
