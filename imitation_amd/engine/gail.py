@@ -136,8 +136,8 @@ def supports(venv, gen_algo, reward_net) -> Tuple[bool, str]:
     dims = [pol.features_dim] + [l.out_features for l in pl]
     if max(dims) > 64 or len(pl) > 4 or len(vl) > 4:
         return False, "policy too wide / deep for the engine"
-    if gen_algo.batch_size % 16 != 0 or gen_algo.batch_size > 128:
-        return False, "minibatch must be a multiple of 16 and <= 128"
+    if gen_algo.batch_size % 16 != 0 or gen_algo.batch_size > 64:
+        return False, "minibatch must be a multiple of 16 and <= 64"
     if (gen_algo.n_steps * gen_algo.n_envs) % gen_algo.batch_size != 0:
         return False, "rollout size not a multiple of the minibatch"
     if gen_algo.clip_range_vf is not None or gen_algo.target_kl is not None:

@@ -55,18 +55,28 @@ def env_name_to_hub(env_name: str) -> str:
     return env_name.replace("/", "-")
 
 
+_BUNDLED_HUB = pathlib.Path(__file__).resolve().parents[2] / "experts"
+
+
 def hub_dir() -> pathlib.Path:
     return pathlib.Path(os.environ.get("IMITATION_AMD_HUB", os.path.expanduser("~/.cache/imitation_amd/hub")))
 
 
+def hub_dirs():
+    """Search order: ``$IMITATION_AMD_HUB`` (or ``~/.cache/imitation_amd/hub``), then the
+    experts bundled in the repository (``experts/``: the CartPole expert of the test data)."""
+    return [hub_dir(), _BUNDLED_HUB]
+
+
 def resolve_hub_model(algo_name: str, env_name: str, organization: str = "HumanCompatibleAI") -> pathlib.Path:
     model_name = f"{algo_name}-{env_name_to_hub(env_name)}"
-    root = hub_dir() / organization / model_name
-    for cand in (root / f"{model_name}.zip", root / "model.zip", hub_dir() / f"{model_name}.zip"):
-        if cand.exists():
-            return cand
+    for hub in hub_dirs():
+        root = hub / organization / model_name
+        for cand in (root / f"{model_name}.zip", root / "model.zip", hub / f"{model_name}.zip"):
+            if cand.exists():
+                return cand
     raise FileNotFoundError(
-        f"No local copy of hub model {organization}/{model_name} under {hub_dir()} "
+        f"No local copy of hub model {organization}/{model_name} under {[str(h) for h in hub_dirs()]} "
         "(training nodes have no network access; place the model.zip there or set IMITATION_AMD_HUB)."
     )
 

@@ -1,0 +1,129 @@
+"""Run many configurations of another experiment in parallel (reference:
+src/imitation/scripts/parallel.py, which drives Ray Tune).
+
+Trials are expanded from ``search_space`` (see ``scripts.tune``) and executed in a
+local process pool, one process per trial (``spawn``), each attaching a
+FileStorageObserver under ``{local_dir}/{run_name}/sacred``. On a multi-GPU node,
+``resources_per_trial={"gpu": k}`` pins every trial to its own k GPUs through
+``HIP_VISIBLE_DEVICES`` so up to ``num_gpus // k`` trials run concurrently.
+"""
+
+from __future__ import annotations
+
+import collections.abc
+import concurrent.futures as cf
+import copy
+import importlib
+import multiprocessing as mp
+import os
+import pathlib
+from typing import Any, Dict, List, Mapping, Sequence
+
+import numpy as np
+
+from imitation_amd.scripts import tune
+from imitation_amd.scripts.config.parallel import parallel_ex
+from imitation_amd.scripts.config_engine import FileStorageObserver, recursive_update
+
+EXPERIMENTS = {
+    "train_rl": ("imitation_amd.scripts.train_rl", "train_rl_ex"),
+    "train_adversarial": ("imitation_amd.scripts.train_adversarial", "train_adversarial_ex"),
+    "train_imitation": ("imitation_amd.scripts.train_imitation", "train_imitation_ex"),
+    "train_preference_comparisons": ("imitation_amd.scripts.train_preference_comparisons",
+                                     "train_preference_comparisons_ex"),
+    "eval_policy": ("imitation_amd.scripts.eval_policy", "eval_policy_ex"),
+}
+
+
+def _get_experiment(name: str):
+    mod, attr = EXPERIMENTS[name]
+    return getattr(importlib.import_module(mod), attr)
+
+
+def _num_gpus() -> int:
+    try:
+        import torch
+
+        return torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        return 0
+
+
+def _run_trial(ex_name: str, run_kwargs: Dict[str, Any], observer_dir: str, run_name: str, gpus: str = "") -> Dict[str, Any]:
+    if gpus:
+        os.environ["HIP_VISIBLE_DEVICES"] = gpus
+    ex = _get_experiment(ex_name)
+    ex.observers = [FileStorageObserver(observer_dir)]
+    ex.path = ex.path  # keep experiment name
+    run = ex.run(command_name=run_kwargs.get("command_name"), named_configs=run_kwargs.get("named_configs", []),
+                 config_updates=run_kwargs.get("config_updates", {}))
+    result = run.result
+    return {"result": result, "config_updates": run_kwargs.get("config_updates", {}),
+            "named_configs": run_kwargs.get("named_configs", []), "status": run.status}
+
+
+def _metric(result: Any, key: str = "imit_stats/monitor_return_mean") -> float:
+    cur = result
+    for part in key.split("/"):
+        if isinstance(cur, Mapping) and part in cur:
+            cur = cur[part]
+        else:
+            alt = result.get("monitor_return_mean", result.get("return_mean")) if isinstance(result, Mapping) else None
+            return float("nan") if alt is None else float(alt)
+    return float(cur)
+
+
+@parallel_ex.main
+def parallel(sacred_ex_name: str, run_name: str, num_samples: int, search_space: Mapping[str, Any],
+             base_named_configs: Sequence[str], base_config_updates: Mapping[str, Any],
+             resources_per_trial: Mapping[str, Any], init_kwargs: Mapping[str, Any], repeat: int,
+             experiment_checkpoint_path: str, tune_run_kwargs: Dict[str, Any], local_dir: str) -> List[Dict[str, Any]]:
+    """Returns one record per trial: its search-space sample, status and result."""
+    if not isinstance(base_named_configs, collections.abc.Sequence):
+        raise TypeError("base_named_configs must be a Sequence")
+    if not isinstance(base_config_updates, collections.abc.Mapping):
+        raise TypeError("base_config_updates must be a Mapping")
+    del init_kwargs, experiment_checkpoint_path
+    rng = np.random.default_rng(tune_run_kwargs.get("seed", 0))
+    samples = tune.generate_trials(search_space, int(num_samples), rng)
+    trials = []
+    for s in samples:
+        for rep in range(int(repeat)):
+            updates = recursive_update(copy.deepcopy(dict(base_config_updates)), s.get("config_updates") or {})
+            if repeat > 1:
+                updates.setdefault("seed", int(rng.integers(0, 2**31 - 1)))
+            trials.append(dict(command_name=s.get("command_name"),
+                               named_configs=list(base_named_configs) + list(s.get("named_configs") or []),
+                               config_updates=updates, sample=s))
+    observer_dir = str(pathlib.Path(tune_run_kwargs.get("local_dir", local_dir)) / run_name / "sacred")
+    gpus_per_trial = int(resources_per_trial.get("gpu", 0) or 0)
+    n_gpus = _num_gpus()
+    if gpus_per_trial > 0 and n_gpus >= gpus_per_trial:
+        slots = [",".join(str(g) for g in range(i, i + gpus_per_trial)) for i in range(0, n_gpus - gpus_per_trial + 1,
+                                                                                      gpus_per_trial)]
+    else:
+        slots = [""]
+    max_conc = int(tune_run_kwargs.get("max_concurrent_trials", len(slots) if slots != [""] else 1))
+    records: List[Dict[str, Any]] = []
+    if max_conc <= 1:
+        for t in trials:
+            records.append(_run_trial(sacred_ex_name, t, observer_dir, run_name, slots[0]))
+    else:
+        ctx = mp.get_context("spawn")
+        with cf.ProcessPoolExecutor(max_workers=max_conc, mp_context=ctx) as pool:
+            futs = [pool.submit(_run_trial, sacred_ex_name, t, observer_dir, run_name, slots[i % len(slots)])
+                    for i, t in enumerate(trials)]
+            records = [f.result() for f in futs]
+    for r, t in zip(records, trials):
+        r["sample"] = t["sample"]
+        r["metric"] = _metric(r["result"]) if r["status"] == "COMPLETED" else float("nan")
+    return records
+
+
+def main_console(argv=None):
+    parallel_ex.observers.append(FileStorageObserver(pathlib.Path.cwd() / "output" / "sacred" / "parallel"))
+    return parallel_ex.run_commandline(argv)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main_console()

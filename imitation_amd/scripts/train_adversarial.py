@@ -1,0 +1,137 @@
+"""Train GAIL or AIRL (reference: src/imitation/scripts/train_adversarial.py).
+
+    python -m imitation_amd.scripts.train_adversarial gail with seals_half_cheetah
+    python -m imitation_amd.scripts.train_adversarial airl with seals_cartpole fast
+
+``engine=auto`` (default) runs GAIL through the device engine
+(``imitation_amd.engine.gail.DeviceGAIL``: rollout, learned reward, PPO update and
+discriminator all on the GPU) whenever the configuration is one it supports, and
+otherwise through the reference-structured host loop. ``engine=host`` forces the
+host loop. Distributed: launch with ``torchrun --nproc-per-node N`` -- every rank
+trains on its own envs and data shard; gradients are all-reduced over RCCL.
+"""
+
+from __future__ import annotations
+
+import functools
+import logging
+import pathlib
+from typing import Any, Mapping, Optional, Type
+
+from imitation_amd.algorithms.adversarial import airl as airl_algo
+from imitation_amd.algorithms.adversarial import common
+from imitation_amd.algorithms.adversarial import gail as gail_algo
+from imitation_amd.data import rollout
+from imitation_amd.parallel import dist as pdist
+from imitation_amd.policies import serialize
+from imitation_amd.rewards import serialize as reward_serialize
+from imitation_amd.scripts.config.train_adversarial import train_adversarial_ex
+from imitation_amd.scripts.config_engine import FileStorageObserver, get_by_dotted_path, print_config
+from imitation_amd.scripts.ingredients import demonstrations, environment
+from imitation_amd.scripts.ingredients import logging as logging_ingredient
+from imitation_amd.scripts.ingredients import policy_evaluation, reward, rl
+
+logger = logging.getLogger("imitation_amd.scripts.train_adversarial")
+
+
+def save(trainer: common.AdversarialTrainer, save_path: pathlib.Path) -> None:
+    """Discriminator (train/test reward nets, pickle-free) and generator (model.zip)."""
+    if not pdist.is_main():
+        return
+    save_path.mkdir(parents=True, exist_ok=True)
+    reward_serialize.save_reward_net(trainer.reward_train, save_path / "reward_train.pt")
+    reward_serialize.save_reward_net(trainer.reward_test, save_path / "reward_test.pt")
+    serialize.save_stable_model(save_path / "gen_policy", trainer.gen_algo)
+
+
+def _add_hook(ingredient) -> None:
+    """Merge ``<ingredient>.algorithm_specific[<command>]`` into the ingredient's config."""
+
+    @ingredient.config_hook
+    def hook(config, command_name, logger):
+        path = "" if ingredient.path == "train_adversarial" else ingredient.config_path
+        cfg = get_by_dotted_path(config, path) if path else config
+        return dict((cfg or {}).get("algorithm_specific", {}).get(command_name, {}))
+
+    @ingredient.config
+    def dummy_config():
+        algorithm_specific = {}
+
+
+for _ing in [train_adversarial_ex, *train_adversarial_ex._all_ingredients()]:
+    _add_hook(_ing)
+
+
+def _make_trainer(algo_cls, engine: str, **kwargs) -> common.AdversarialTrainer:
+    if algo_cls is gail_algo.GAIL and engine in ("auto", "device"):
+        from imitation_amd.engine.gail import DeviceGAIL, supports
+
+        ok, why = supports(kwargs["venv"], kwargs["gen_algo"], kwargs["reward_net"])
+        if ok:
+            try:
+                trainer = DeviceGAIL(**kwargs)
+                logger.info("Using the device engine (DeviceGAIL)")
+                return trainer
+            except ValueError as e:  # e.g. nets too large for the persistent PPO kernel's LDS
+                why = str(e)
+        if engine == "device":
+            raise ValueError(f"engine=device requested but unsupported: {why}")
+        logger.info(f"Device engine not applicable ({why}); using the host loop")
+    return algo_cls(**kwargs)
+
+
+@train_adversarial_ex.capture
+def train_adversarial(_run, show_config: bool, algo_cls: Type[common.AdversarialTrainer],
+                      algorithm_kwargs: Mapping[str, Any], total_timesteps: int, checkpoint_interval: int,
+                      agent_path: Optional[str], engine: str = "auto") -> Mapping[str, Mapping[str, float]]:
+    """Checkpoints go to ``{log_dir}/checkpoints/{round|final}/{reward_train,reward_test}.pt`` and ``gen_policy/``."""
+    total_timesteps = int(total_timesteps)
+    checkpoint_interval = int(checkpoint_interval)
+    pdist.init()
+    if show_config:
+        print_config(_run)
+    custom_logger, log_dir = logging_ingredient.setup_logging()
+    expert_trajs = demonstrations.get_expert_trajectories()
+    with environment.make_venv() as venv:
+        reward_net = reward.make_reward_net(venv)
+        relabel_reward_fn = functools.partial(reward_net.predict_processed, update_stats=False)
+        if agent_path is None:
+            gen_algo = rl.make_rl_algo(venv, relabel_reward_fn=relabel_reward_fn)
+        else:
+            gen_algo = rl.load_rl_algo_from_path(agent_path=agent_path, venv=venv, relabel_reward_fn=relabel_reward_fn)
+        logger.info(f"Using '{algo_cls}' algorithm")
+        algorithm_kwargs = {k: v for k, v in dict(algorithm_kwargs).items() if k not in ("shared", "airl", "gail")}
+        trainer = _make_trainer(algo_cls, engine, venv=venv, demonstrations=expert_trajs, gen_algo=gen_algo,
+                                log_dir=log_dir, reward_net=reward_net, custom_logger=custom_logger, **algorithm_kwargs)
+
+        def callback(round_num: int, /) -> None:
+            if checkpoint_interval > 0 and round_num % checkpoint_interval == 0:
+                save(trainer, log_dir / "checkpoints" / f"{round_num:05d}")
+
+        trainer.train(total_timesteps, callback)
+        imit_stats = policy_evaluation.eval_policy(trainer.policy, trainer.venv_train)
+    if checkpoint_interval >= 0:
+        save(trainer, log_dir / "checkpoints" / "final")
+    return {"imit_stats": imit_stats, "expert_stats": rollout.rollout_stats(expert_trajs)}
+
+
+@train_adversarial_ex.command
+def gail():
+    """Generative Adversarial Imitation Learning."""
+    return train_adversarial(algo_cls=gail_algo.GAIL)
+
+
+@train_adversarial_ex.command
+def airl():
+    """Adversarial Inverse Reinforcement Learning."""
+    return train_adversarial(algo_cls=airl_algo.AIRL)
+
+
+def main_console(argv=None):
+    observer = FileStorageObserver(pathlib.Path.cwd() / "output" / "sacred" / "train_adversarial")
+    train_adversarial_ex.observers.append(observer)
+    return train_adversarial_ex.run_commandline(argv)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main_console()

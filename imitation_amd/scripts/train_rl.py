@@ -1,0 +1,73 @@
+"""Train a policy with RL, optionally on a learned reward (reference: src/imitation/scripts/train_rl.py).
+
+Checkpoints: ``{log_dir}/policies/{step|final}/model.zip``, rollouts ``{log_dir}/rollouts/final.npz``
+(an HF dataset directory, like the reference's ``data.serialize.save``).
+"""
+
+from __future__ import annotations
+
+import logging
+import pathlib
+import warnings
+from typing import Any, Mapping, Optional
+
+import numpy as np
+
+from imitation_amd.data import rollout, serialize as data_serialize, wrappers
+from imitation_amd.envs.vec_env import VecNormalize
+from imitation_amd.policies import serialize as policies_serialize
+from imitation_amd.rewards.reward_wrapper import RewardVecEnvWrapper
+from imitation_amd.rewards.serialize import load_reward
+from imitation_amd.rl import callbacks
+from imitation_amd.scripts.config.train_rl import train_rl_ex
+from imitation_amd.scripts.config_engine import FileStorageObserver
+from imitation_amd.scripts.ingredients import environment
+from imitation_amd.scripts.ingredients import logging as logging_ingredient
+from imitation_amd.scripts.ingredients import policy_evaluation, rl
+
+
+@train_rl_ex.main
+def train_rl(*, total_timesteps: int, normalize_reward: bool, normalize_kwargs: dict, reward_type: Optional[str],
+             reward_path: Optional[str], load_reward_kwargs: Optional[Mapping[str, Any]], rollout_save_final: bool,
+             rollout_save_n_timesteps: Optional[int], rollout_save_n_episodes: Optional[int], policy_save_interval: int,
+             policy_save_final: bool, agent_path: Optional[str], _rnd: np.random.Generator) -> Mapping[str, float]:
+    """Train an RL expert; returns ``rollout_stats`` of the final policy."""
+    custom_logger, log_dir = logging_ingredient.setup_logging()
+    rollout_dir = log_dir / "rollouts"
+    policy_dir = log_dir / "policies"
+    rollout_dir.mkdir(parents=True, exist_ok=True)
+    policy_dir.mkdir(parents=True, exist_ok=True)
+    with environment.make_venv(post_wrappers=[lambda env, idx: wrappers.RolloutInfoWrapper(env)]) as venv:
+        callback_objs = []
+        if reward_type is not None:
+            reward_fn = load_reward(reward_type, reward_path, venv, **(load_reward_kwargs or {}))
+            venv = RewardVecEnvWrapper(venv, reward_fn)
+            callback_objs.append(venv.make_log_callback())
+            logging.info(f"Wrapped env in reward {reward_type} from {reward_path}.")
+        if normalize_reward:
+            venv = VecNormalize(venv, norm_obs=False, **normalize_kwargs)
+            if reward_type == "RewardNet_normalized":
+                warnings.warn("Applying normalization to already normalized reward function. Consider setting "
+                              "normalize_reward as False", RuntimeWarning)
+        if policy_save_interval > 0:
+            callback_objs.append(callbacks.EveryNTimesteps(policy_save_interval,
+                                                           policies_serialize.SavePolicyCallback(policy_dir)))
+        callback = callbacks.CallbackList(callback_objs)
+        algo = rl.make_rl_algo(venv) if agent_path is None else rl.load_rl_algo_from_path(agent_path=agent_path, venv=venv)
+        algo.set_logger(custom_logger)
+        algo.learn(total_timesteps, callback=callback)
+        if rollout_save_final:
+            sample_until = rollout.make_sample_until(rollout_save_n_timesteps, rollout_save_n_episodes)
+            data_serialize.save(rollout_dir / "final.npz", rollout.rollout(algo, algo.get_env(), sample_until, rng=_rnd))
+        if policy_save_final:
+            policies_serialize.save_stable_model(policy_dir / "final", algo)
+        return policy_evaluation.eval_policy(algo, venv)
+
+
+def main_console(argv=None):
+    train_rl_ex.observers.append(FileStorageObserver(pathlib.Path.cwd() / "output" / "sacred" / "train_rl"))
+    return train_rl_ex.run_commandline(argv)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main_console()
