@@ -360,6 +360,7 @@ class Experiment(Ingredient):
 
     def run(self, command_name: Optional[str] = None, config_updates: Optional[Mapping] = None,
             named_configs: Sequence[str] = (), options: Optional[Mapping] = None) -> "Run":
+        options = dict(options or {})
         command_name = command_name or self.default_command
         if command_name is None:
             raise ValueError("No command given and no default (@main) command defined.")
@@ -372,6 +373,8 @@ class Experiment(Ingredient):
             raise KeyError(f"Unknown command {command_name!r}; available: {sorted(self._all_commands())}")
         observers = list(self.observers)
         run = Run(self, command_name, config, named_configs, config_updates or {}, observers)
+        if options.get("name"):
+            run.experiment_info["name"] = options["name"]
         run(self._all_commands()[command_name])
         return run
 
@@ -392,7 +395,7 @@ class Experiment(Ingredient):
             return None
         if opts.get("print_config") and command != "print_config":
             print_config_dict(self.resolve_config(named, updates, command))
-        return self.run(command, updates, named)
+        return self.run(command, updates, named, options=opts)
 
     def help_text(self) -> str:
         lines = [f"{self.path} commands:"]

@@ -96,26 +96,33 @@ def parallel(sacred_ex_name: str, run_name: str, num_samples: int, search_space:
                                named_configs=list(base_named_configs) + list(s.get("named_configs") or []),
                                config_updates=updates, sample=s))
     observer_dir = str(pathlib.Path(tune_run_kwargs.get("local_dir", local_dir)) / run_name / "sacred")
+    records = run_trials(sacred_ex_name, trials, observer_dir, run_name, resources_per_trial,
+                         tune_run_kwargs.get("max_concurrent_trials"))
+    for r, t in zip(records, trials):
+        r["sample"] = t["sample"]
+    return records
+
+
+def run_trials(ex_name: str, trials: List[Dict[str, Any]], observer_dir: str, run_name: str,
+               resources_per_trial: Mapping[str, Any], max_concurrent: Any = None) -> List[Dict[str, Any]]:
+    """Run ``trials`` (dicts of command_name / named_configs / config_updates) of experiment ``ex_name``."""
     gpus_per_trial = int(resources_per_trial.get("gpu", 0) or 0)
     n_gpus = _num_gpus()
     if gpus_per_trial > 0 and n_gpus >= gpus_per_trial:
-        slots = [",".join(str(g) for g in range(i, i + gpus_per_trial)) for i in range(0, n_gpus - gpus_per_trial + 1,
-                                                                                      gpus_per_trial)]
+        slots = [",".join(str(g) for g in range(i, i + gpus_per_trial))
+                 for i in range(0, n_gpus - gpus_per_trial + 1, gpus_per_trial)]
     else:
         slots = [""]
-    max_conc = int(tune_run_kwargs.get("max_concurrent_trials", len(slots) if slots != [""] else 1))
-    records: List[Dict[str, Any]] = []
+    max_conc = int(max_concurrent if max_concurrent is not None else (len(slots) if slots != [""] else 1))
     if max_conc <= 1:
-        for t in trials:
-            records.append(_run_trial(sacred_ex_name, t, observer_dir, run_name, slots[0]))
+        records = [_run_trial(ex_name, t, observer_dir, run_name, slots[0]) for t in trials]
     else:
         ctx = mp.get_context("spawn")
         with cf.ProcessPoolExecutor(max_workers=max_conc, mp_context=ctx) as pool:
-            futs = [pool.submit(_run_trial, sacred_ex_name, t, observer_dir, run_name, slots[i % len(slots)])
+            futs = [pool.submit(_run_trial, ex_name, t, observer_dir, run_name, slots[i % len(slots)])
                     for i, t in enumerate(trials)]
             records = [f.result() for f in futs]
-    for r, t in zip(records, trials):
-        r["sample"] = t["sample"]
+    for r in records:
         r["metric"] = _metric(r["result"]) if r["status"] == "COMPLETED" else float("nan")
     return records
 
