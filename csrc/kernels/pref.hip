@@ -43,15 +43,17 @@ __global__ __launch_bounds__(256) void pref_fwd_kernel(const float* __restrict__
   if (lane == 0) {
     const bool inside = diff >= -threshold && diff <= threshold;
     const float d = fminf(fmaxf(diff, -threshold), threshold);
-    const float pm = 1.f / (1.f + expf(d));
+    const float ed = expf(d);
+    const float pm = 1.f / (1.f + ed);
     const float p = noise * 0.5f + (1.f - noise) * pm;
     const float y = prefs[i];
     const float lp = fmaxf(logf(p), -100.f), l1p = fmaxf(logf(1.f - p), -100.f);
     losses[i] = -(y * lp + (1.f - y) * l1p);
     probs[i] = p;
-    // torch BCE backward: (p - y) / max(p (1 - p), 1e-12); dp/ddiff = -(1-noise) pm (1-pm)
+    // torch BCE backward: (p - y) / max(p (1 - p), 1e-12). dpm/ddiff is formed like autograd
+    // does for 1/(1+e^d): -pm^2 e^d (NOT -pm (1 - pm): 1 - pm rounds to 0 once pm ~ 1 in fp32).
     const float dl_dp = (p - y) / fmaxf(p * (1.f - p), 1e-12f);
-    coef[i] = inside ? dl_dp * (-(1.f - noise) * pm * (1.f - pm)) : 0.f;
+    coef[i] = inside ? dl_dp * ((1.f - noise) * -(pm * pm) * ed) : 0.f;
   }
 }
 

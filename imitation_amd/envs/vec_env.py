@@ -578,8 +578,11 @@ def native_spaces(env_id: str, impl=None) -> Tuple[spaces.Space, spaces.Space]:
         od = impl.obs_dim()
         if env_id.startswith("Pendulum"):
             obs_space = spaces.Box(np.array([-1, -1, -8], np.float32), np.array([1, 1, 8], np.float32))
-        elif env_id.startswith("CartPole") or env_id == "seals/CartPole-v0":
+        elif env_id.startswith("CartPole"):
             hi = np.array([4.8, np.finfo(np.float32).max, 0.41887903, np.finfo(np.float32).max], np.float32)
+            obs_space = spaces.Box(-hi, hi)
+        elif env_id == "seals/CartPole-v0":  # seals: fixed horizon, no termination -> unbounded box
+            hi = np.full(4, np.finfo(np.float32).max, np.float32)
             obs_space = spaces.Box(-hi, hi)
         elif "MountainCar" in env_id:
             obs_space = spaces.Box(np.array([-1.2, -0.07], np.float32), np.array([0.6, 0.07], np.float32))

@@ -11,6 +11,8 @@ env steps; the global count is ``num_timesteps * world_size``.
 
 from __future__ import annotations
 
+import warnings
+
 import collections
 import pathlib
 import sys
@@ -336,6 +338,14 @@ class BaseAlgorithm:
             raise ValueError("archive lacks decodable observation/action spaces")
         if env is not None:
             env = cls._wrap_env(env, data.get("verbose", 0))
+            if (isinstance(obs_space, spaces.Box) and isinstance(env.observation_space, spaces.Box)
+                    and obs_space != env.observation_space and obs_space.shape == env.observation_space.shape
+                    and obs_space.dtype == env.observation_space.dtype):
+                # Same layout, different declared bounds (e.g. a gymnasium CartPole expert on the
+                # unbounded seals CartPole): the network is unaffected by the bounds, so adopt the env's.
+                warnings.warn(f"Observation-space bounds of the archive {obs_space} differ from the env's "
+                              f"{env.observation_space}; using the env's.")
+                obs_space = env.observation_space
             check_for_correct_spaces(env, obs_space, act_space)
         policy_class = data.get("policy_class")
         if not isinstance(policy_class, type):

@@ -1,0 +1,118 @@
+"""HierarchicalLogger semantics (reference: tests/util/test_logger.py)."""
+
+import csv
+import json
+import os.path as osp
+from collections import defaultdict
+
+import pytest
+
+from imitation_amd.util import logger
+
+
+def _csv(path):
+    out = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            for k, v in row.items():
+                out[k].append(float(v) if v != "" else "")
+    return dict(out)
+
+
+def _json(path):
+    lines = [json.loads(l) for l in open(path)]
+    keys = set().union(*lines)
+    return {k: [l.get(k, "") for l in lines] for k in keys}
+
+
+def test_no_accum(tmp_path):
+    h = logger.configure(str(tmp_path), ["csv", "json"])
+    h.record("A", -1)
+    h.record("A", 1)  # overwrites, not averaged
+    h.record("B", 1)
+    h.dump()
+    h.record("A", 2)
+    h.dump()
+    h.record("B", 3)
+    h.dump()
+    expect = {"A": [1, 2, ""], "B": [1, "", 3]}
+    assert _csv(tmp_path / "progress.csv") == expect
+    assert _json(tmp_path / "progress.json") == expect
+
+
+def test_unknown_format():
+    with pytest.raises(ValueError, match="Unknown format specified"):
+        logger.make_output_format("txt", "log_dir")
+
+
+def test_reentry_fails(tmp_path):
+    h = logger.configure(str(tmp_path))
+    with h.accumulate_means("foo"):
+        with pytest.raises(RuntimeError, match="Nested"):
+            with h.accumulate_means("bar"):
+                pass
+
+
+def test_name_to_value_means(tmp_path):
+    h = logger.configure(str(tmp_path))
+    with h.accumulate_means("foo"):
+        h.record("A", 1)
+        assert h.name_to_value["raw/foo/A"] == 1
+        h.record("B", 10)
+        h.dump()
+        h.record("B", 20)
+    assert h.name_to_value["mean/foo/A"] == 1
+    assert h.name_to_value["mean/foo/B"] == 15 and h.name_to_count["mean/foo/B"] == 2
+    h.dump()
+    assert len(h.name_to_value) == 0
+
+
+def test_hard(tmp_path):
+    h = logger.configure(str(tmp_path))
+    h.record("no_context", 1)
+    with h.accumulate_means("disc"):
+        h.record("C", 2)
+        h.record("D", 2)
+        h.dump()
+        h.record("C", 4)
+        h.dump()
+    with h.accumulate_means("gen"):
+        h.record("E", 2)
+        h.dump()
+        h.record("E", 0)
+        h.dump()
+    with h.accumulate_means("disc"):
+        h.record("C", 3)
+        h.dump()
+    h.dump()
+    assert _csv(tmp_path / "progress.csv") == {"mean/gen/E": [1], "mean/disc/C": [3], "mean/disc/D": [2], "no_context": [1]}
+    assert _csv(tmp_path / "raw" / "gen" / "progress.csv") == {"raw/gen/E": [2, 0]}
+    assert _csv(tmp_path / "raw" / "disc" / "progress.csv") == {"raw/disc/C": [2, 4, 3], "raw/disc/D": [2, "", ""]}
+
+
+def test_prefixes(tmp_path):
+    h = logger.configure(str(tmp_path))
+    with h.add_accumulate_prefix("foo"), h.accumulate_means("bar"):
+        h.record("A", 1)
+        h.dump()
+    with h.accumulate_means("blat"), h.add_key_prefix("k"):
+        h.record("C", 3)
+        h.dump()
+    h.dump()
+    assert _csv(tmp_path / "progress.csv") == {"mean/foo/bar/A": [1], "mean/blat/k/C": [3]}
+    assert _csv(tmp_path / "raw" / "foo" / "bar" / "progress.csv") == {"raw/foo/bar/A": [1]}
+    with pytest.raises(RuntimeError):
+        with h.accumulate_means("x"), h.add_accumulate_prefix("y"):
+            pass
+    with pytest.raises(RuntimeError):
+        with h.add_key_prefix("z"):
+            pass
+
+
+def test_tensorboard_event_file(tmp_path):
+    h = logger.configure(str(tmp_path), ["tensorboard"])
+    h.record("x", 1.5)
+    h.dump(step=3)
+    h.close()
+    files = list(tmp_path.glob("events.out.tfevents.*"))
+    assert files and files[0].stat().st_size > 0

@@ -1,0 +1,65 @@
+"""Normalisation layers and MLP/CNN builders (reference: tests/util/test_networks.py)."""
+
+import numpy as np
+import pytest
+import torch as th
+
+from imitation_amd.util import networks
+
+
+@pytest.mark.parametrize("cls", [networks.RunningNorm, networks.EMANorm])
+def test_norm_identity_at_init(cls):
+    n = cls(3)
+    x = th.randn(10, 3)
+    with networks.evaluating(n):
+        th.testing.assert_close(n(x), x / np.sqrt(1 + n.eps), rtol=1e-5, atol=1e-6)
+
+
+def test_running_norm_matches_distribution():
+    th.manual_seed(0)
+    n = networks.RunningNorm(2)
+    data = th.randn(5000, 2) * th.tensor([2.0, 0.5]) + th.tensor([1.0, -3.0])
+    with networks.training(n):
+        for b in data.split(100):
+            n(b)
+    th.testing.assert_close(n.running_mean, data.mean(0), rtol=1e-4, atol=1e-4)
+    th.testing.assert_close(n.running_var, data.var(0, unbiased=False), rtol=1e-3, atol=1e-3)
+    assert int(n.count) == 5000
+
+
+def test_running_norm_eval_does_not_update():
+    n = networks.RunningNorm(2)
+    with networks.evaluating(n):
+        n(th.randn(10, 2) + 5)
+    assert th.all(n.running_mean == 0)
+
+
+@pytest.mark.parametrize("decay", [0.5, 0.99])
+def test_ema_norm_converges(decay):
+    th.manual_seed(1)
+    n = networks.EMANorm(1, decay=decay)
+    with networks.training(n):
+        for _ in range(300):
+            n(th.randn(64, 1) * 3 + 2)
+    assert abs(float(n.running_mean) - 2) < 0.5 and abs(float(n.running_var) - 9) < 3
+
+
+def test_ema_norm_validation():
+    with pytest.raises(ValueError):
+        networks.EMANorm(1, decay=1.5)
+
+
+def test_build_mlp_shapes_and_names():
+    m = networks.build_mlp(in_size=4, hid_sizes=(8, 8), out_size=2, name="foo", normalize_input_layer=networks.RunningNorm)
+    assert m(th.randn(5, 4)).shape == (5, 2)
+    names = [n for n, _ in m.named_children()]
+    assert names[0].startswith("foo_normalize_input") and "foo_dense0" in names
+    sq = networks.build_mlp(in_size=3, hid_sizes=(4,), squeeze_output=True)
+    assert sq(th.randn(6, 3)).shape == (6,)
+    with pytest.raises(ValueError):
+        networks.build_mlp(in_size=3, hid_sizes=(4,), out_size=2, squeeze_output=True)
+
+
+def test_build_cnn_shapes():
+    c = networks.build_cnn(in_channels=3, hid_channels=(4, 8), out_size=5)
+    assert c(th.randn(2, 3, 16, 16)).shape == (2, 5)
