@@ -50,10 +50,19 @@ __global__ __launch_bounds__(256) void pref_fwd_kernel(const float* __restrict__
     const float lp = fmaxf(logf(p), -100.f), l1p = fmaxf(logf(1.f - p), -100.f);
     losses[i] = -(y * lp + (1.f - y) * l1p);
     probs[i] = p;
-    // torch BCE backward: (p - y) / max(p (1 - p), 1e-12). dpm/ddiff is formed like autograd
-    // does for 1/(1+e^d): -pm^2 e^d (NOT -pm (1 - pm): 1 - pm rounds to 0 once pm ~ 1 in fp32).
-    const float dl_dp = (p - y) / fmaxf(p * (1.f - p), 1e-12f);
-    coef[i] = inside ? dl_dp * ((1.f - noise) * -(pm * pm) * ed) : 0.f;
+    // noise == 0: dloss/ddiff = y - pm exactly. torch's BCE backward, (p - y) / max(p (1 - p), 1e-12)
+    // times dp/ddiff, agrees with this while p stays away from 0/1 and is noise once it
+    // saturates (1 - p rounds to 0 in fp32 past |diff| ~ 17; the 1e-12 clamp past ~ 27).
+    // noise > 0 keeps p inside [noise/2, 1 - noise/2], where the chain rule is well conditioned;
+    // dpm/ddiff = -pm^2 e^d avoids the cancellation in pm (1 - pm).
+    float c;
+    if (noise == 0.f) {
+      c = y - pm;
+    } else {
+      const float dl_dp = (p - y) / fmaxf(p * (1.f - p), 1e-12f);
+      c = dl_dp * ((1.f - noise) * -(pm * pm) * ed);
+    }
+    coef[i] = inside ? c : 0.f;
   }
 }
 

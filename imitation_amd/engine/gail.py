@@ -313,6 +313,11 @@ class DeviceGAIL(GAIL):
     def _ppo_update(self) -> None:
         algo: PPO = self.gen_algo
         rows = self.T * self.N
+        if self.pol_norm is not None:
+            # the policy normaliser may also have been updated outside the engine (the
+            # discriminator's log-prob pass runs the policy in training mode, as the
+            # reference does): the kernel continues from the module's own count
+            self.norm_count.copy_(self.pol_norm.count.reshape(1))
         algo._update_current_progress_remaining(algo.num_timesteps, algo._total_timesteps or algo.num_timesteps)
         lr = float(algo.lr_schedule(algo._current_progress_remaining))
         clip = float(algo.clip_range(algo._current_progress_remaining))
@@ -446,6 +451,33 @@ class DeviceGAIL(GAIL):
         if algo.ep_info_buffer:
             lg.record("rollout/ep_rew_mean", float(np.mean([e["r"] for e in algo.ep_info_buffer])))
             lg.record("rollout/ep_len_mean", float(np.mean([e["l"] for e in algo.ep_info_buffer])))
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    _ENGINE_TENSORS = ("exp_avg", "exp_avg_sq", "adam_step", "state", "rng", "elapsed", "ep_ret", "cur_obs", "cur_start")
+
+    def engine_state(self) -> Dict[str, Any]:
+        """Device-engine state not covered by module ``state_dict``s (used by
+        :mod:`imitation_amd.utils.checkpoint`); parameters live in the policy modules."""
+        st: Dict[str, Any] = {k: getattr(self, k).detach().cpu().clone() for k in self._ENGINE_TENSORS}
+        if self.norm_count is not None:
+            st["norm_count"] = self.norm_count.cpu().clone()
+        st.update(step0=int(self._step0), seed=int(self._seed), ep_lens_running=th.as_tensor(self._ep_lens_running),
+                  gen_dev={k: v.cpu().clone() for k, v in self._gen_dev._arrays.items()},
+                  gen_dev_idx=int(self._gen_dev._idx), gen_dev_n=int(self._gen_dev._n_data))
+        return st
+
+    def load_engine_state(self, st: Dict[str, Any]) -> None:
+        with th.no_grad():
+            for k in self._ENGINE_TENSORS:
+                getattr(self, k).copy_(st[k].to(self._dev))
+            if self.norm_count is not None and "norm_count" in st:
+                self.norm_count.copy_(st["norm_count"].to(self._dev))
+            for k, v in st["gen_dev"].items():
+                self._gen_dev._arrays[k].copy_(v.to(self._dev))
+        self._step0, self._seed = st["step0"], st["seed"]
+        self._ep_lens_running = st["ep_lens_running"].numpy().copy()
+        self._gen_dev._idx, self._gen_dev._n_data = st["gen_dev_idx"], st["gen_dev_n"]
+        self.sync_env_to_host()
 
     def sync_env_to_host(self) -> None:
         """Copy the device env state back into the native host env (e.g. before host-side evaluation)."""

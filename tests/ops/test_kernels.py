@@ -124,8 +124,10 @@ def test_preference_kernel_matches_reference(P, L, discount, noise, thr):
     from imitation_amd.ops import preference as pref_ops
 
     g = th.Generator().manual_seed(P + L)
-    r1 = th.randn(P, L, generator=g)
-    r2 = th.randn(P, L, generator=g)
+    # scale so |diff| stays O(1): torch's BCE backward is ill-conditioned once p saturates
+    # (see test_preference_kernel_saturated_grad for that regime).
+    r1 = th.randn(P, L, generator=g) * (1.5 / L**0.5)
+    r2 = th.randn(P, L, generator=g) * (1.5 / L**0.5)
     prefs = (th.rand(P, generator=g) > 0.5).float()
     prefs[::5] = 0.5
     a1, a2 = r1.clone().requires_grad_(), r2.clone().requires_grad_()
@@ -138,3 +140,27 @@ def test_preference_kernel_matches_reference(P, L, discount, noise, thr):
     th.testing.assert_close(probs.cpu(), probs_r.detach(), rtol=1e-5, atol=1e-6)
     th.testing.assert_close(b1.grad.cpu(), 3.0 * a1.grad, rtol=1e-4, atol=1e-7)
     th.testing.assert_close(b2.grad.cpu(), 3.0 * a2.grad, rtol=1e-4, atol=1e-7)
+
+
+@gpu
+def test_preference_kernel_saturated_grad():
+    """Past |diff| ~ 17 fp32 autograd of BCE(sigmoid) degenerates; the kernel returns the exact
+    derivative dloss/ddiff = y - p (float64 oracle) for noise == 0."""
+    from imitation_amd.ops import preference as pref_ops
+
+    g = th.Generator().manual_seed(3)
+    P, L, thr = 64, 50, 50.0
+    r1 = th.randn(P, L, generator=g) * 4.0
+    r2 = th.randn(P, L, generator=g) * 4.0
+    prefs = (th.rand(P, generator=g) > 0.5).float()
+    b1, b2 = r1.cuda().requires_grad_(), r2.cuda().requires_grad_()
+    loss, probs = pref_ops.bradley_terry(b1, b2, prefs.cuda(), 1.0, thr, 0.0)
+    loss.backward()
+    d = (r2.double() - r1.double()).sum(-1)
+    inside = (d.abs() <= thr).double()
+    pm = 1.0 / (1.0 + d.clamp(-thr, thr).exp())
+    expect = ((prefs.double() - pm) * inside / P)[:, None].expand(P, L)
+    assert th.isfinite(b2.grad).all()
+    th.testing.assert_close(b2.grad.cpu().double(), expect, rtol=1e-4, atol=1e-6)
+    th.testing.assert_close(b1.grad.cpu().double(), -expect, rtol=1e-4, atol=1e-6)
+    th.testing.assert_close(probs.cpu().double(), pm, rtol=1e-4, atol=1e-6)
