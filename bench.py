@@ -38,8 +38,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--engine", choices=["device", "host"], default=os.environ.get("IA_BENCH_ENGINE", "device"))
-    p.add_argument("--env", default="seals/HalfCheetah-v1")
+    p.add_argument("--engine", choices=["auto", "device", "host"], default=os.environ.get("IA_BENCH_ENGINE", "auto"))
+    p.add_argument("--env", default="HalfCheetah-v4")
+    p.add_argument("--eval-episodes", type=int, default=8, help="final eval return (after timing); 0 = skip")
     p.add_argument("--n-envs", type=int, default=8)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--profile-dir", default=None)
@@ -57,49 +58,22 @@ def main():
 
     rank, world = pdist.init()
     if th.cuda.is_available():
-        th.cuda.set_device(pdist.local_rank())
-        device = th.device("cuda", pdist.local_rank())
+        dev_idx = pdist.local_rank() % th.cuda.device_count()  # == local rank on a full node
+        th.cuda.set_device(dev_idx)
+        device = th.device("cuda", dev_idx)
     else:
         device = th.device("cpu")
     th.manual_seed(args.seed + rank)
     np.random.seed(args.seed + rank)
 
-    from imitation_amd.data import rollout
-    from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
-    from imitation_amd.rewards.reward_nets import BasicRewardNet, NormalizedRewardNet
-    from imitation_amd.rl.ppo import PPO
-    from imitation_amd.util import logger as imit_logger
-    from imitation_amd.util.networks import RunningNorm
-    from imitation_amd.util.util import make_vec_env
+    from imitation_amd import models
 
-    rng = np.random.default_rng(args.seed + 1000 * rank)
-    venv = make_vec_env(args.env, rng=rng, n_envs=args.n_envs)
-    # synthetic demonstrations: random-policy trajectories of the same env (>= demo batch)
-    demo_env = make_vec_env(args.env, rng=np.random.default_rng(12345), n_envs=16)
-    demos = rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(16384), rng=np.random.default_rng(0))
-    transitions = rollout.flatten_trajectories(demos)
-
-    rl_kwargs = dict(batch_size=64, clip_range=0.1, ent_coef=3.992371122209408e-6, gae_lambda=0.95, gamma=0.95,
-                     learning_rate=0.00026250519057717037, max_grad_norm=0.8, n_epochs=5, vf_coef=0.11483689492120866)
-    policy_kwargs = dict(features_extractor_class=NormalizeFeaturesExtractor,
-                         features_extractor_kwargs=dict(normalize_class=RunningNorm))
-    n_steps = 4096 // args.n_envs
-    gen = PPO(FeedForward32Policy, venv, n_steps=n_steps, policy_kwargs=policy_kwargs, device=device, seed=args.seed, **rl_kwargs)
-    reward_net = NormalizedRewardNet(
-        BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm
-    )
-    log = imit_logger.configure(os.path.join("/tmp", f"ia_bench_{os.getpid()}"), format_strs=[])
-    algo_kwargs = dict(demo_batch_size=8192, gen_replay_buffer_capacity=512, n_disc_updates_per_round=8)
-    if args.engine == "device":
-        from imitation_amd.engine.gail import DeviceGAIL
-
-        trainer = DeviceGAIL(demonstrations=transitions, venv=venv, gen_algo=gen, reward_net=reward_net,
-                             custom_logger=log, **algo_kwargs)
-    else:
-        from imitation_amd.algorithms.adversarial.gail import GAIL
-
-        trainer = GAIL(demonstrations=transitions, venv=venv, gen_algo=gen, reward_net=reward_net, custom_logger=log,
-                       **algo_kwargs)
+    # the reference's tuned gail_seals_half_cheetah config (imitation_amd/models/recipes.py)
+    built = models.build("gail_halfcheetah", device=device, n_envs=args.n_envs, engine=args.engine, seed=args.seed,
+                         rank=rank, env_id=args.env, log_dir=os.path.join("/tmp", f"ia_bench_{os.getpid()}"))
+    trainer, venv = built.trainer, built.venv
+    engine = built.extras["engine"]
+    n_steps = trainer.gen_algo.n_steps
     steps_per_round = trainer.gen_train_timesteps
 
     def one_round():
@@ -120,9 +94,17 @@ def main():
     dt = pdist.allreduce_scalars([dt], op="max")[0]
     total_steps = steps_per_round * args.steps * world
     value = total_steps / dt
+    eval_return = None
+    if args.eval_episodes > 0:  # outside the timed region: mean return of the trained generator
+        from imitation_amd.rl.evaluation import evaluate_policy
+
+        if hasattr(trainer, "sync_env_to_host"):
+            trainer.sync_env_to_host()
+        mean_r, _ = evaluate_policy(trainer.gen_algo.policy, venv, n_eval_episodes=args.eval_episodes)
+        eval_return = round(float(pdist.allreduce_scalars([float(mean_r)], op="sum")[0]) / world, 3)
     if rank == 0:
         out = {
-            "metric": "env-steps/sec (whole node), GAIL seals/HalfCheetah-v1-shaped, PPO generator, 8 envs/GPU",
+            "metric": "env-steps/sec (whole node) + final eval return, GAIL HalfCheetah-v4 at 1/2/4/8 MI355X",
             "value": round(value, 2),
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -133,13 +115,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
             "dtype": "bf16",
-            "data": "synthetic (HalfCheetah-shaped native env, random-policy demos, random-init nets)",
+            "final_eval_return": eval_return,
+            "data": "synthetic (native HalfCheetah-v4-shaped env, random-policy demos, random-init nets)",
             "config": {
                 "model": "GAIL: FeedForward32Policy[32,32]+RunningNorm / BasicRewardNet(32,32)+RunningNorm",
                 "global_batch": 4096 * world,
                 "seq_len": n_steps,
                 "parallelism": f"dp{world}",
-                "engine": args.engine,
+                "engine": engine,
                 "env": args.env,
             },
         }

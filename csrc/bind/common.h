@@ -20,3 +20,4 @@ inline hipStream_t ia_stream() { return c10::hip::getCurrentHIPStream().stream()
 void register_envs(py::module& m);
 void register_kernels(py::module& m);
 void register_engine(py::module& m);
+void register_disc(py::module& m);

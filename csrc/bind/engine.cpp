@@ -155,7 +155,35 @@ void ppo_update(py::dict d) {
   a.mb_index = ival(d, "mb_index", 0);
   a.prof = tptr<unsigned long long>(d, "prof", true);
   TORCH_CHECK(a.D <= 64, "obs dim <= 64");
+  ia::PPORcGeo geo;
+  size_t rc_lds = 0;
+  if (a.mode == 0 && ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, rc_lds)) {
+    auto ws = torch::empty({(int64_t)ia::ppo_rc_workspace_floats(a)},
+                           torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, c10::hip::current_device()));
+    IA_HIP_CHECK2(ia::ppo_rc_launch(a, ws.data_ptr<float>(), ia_stream()));
+    return;
+  }
   IA_HIP_CHECK2(ia::ppo_launch(a, ia_stream()));
+}
+
+// Which kernel engine_ppo_update(mode 0) runs for this configuration: "rc" or "lds".
+std::string ppo_path(py::dict d) {
+  ia::PPOArgs a{};
+  a.D = ival(d, "D");
+  a.A = ival(d, "A");
+  a.discrete = ival(d, "discrete");
+  auto pid = d["pi_dims"].cast<std::vector<int>>();
+  auto vid = d["vf_dims"].cast<std::vector<int>>();
+  a.n_pi = (int)pid.size() - 1;
+  a.n_vf = (int)vid.size() - 1;
+  for (size_t i = 0; i < pid.size(); ++i) a.pi_dims[i] = pid[i];
+  for (size_t i = 0; i < vid.size(); ++i) a.vf_dims[i] = vid[i];
+  a.batch = ival(d, "batch");
+  a.rows = ival(d, "rows");
+  a.log_std_off = ival(d, "log_std_off", -1);
+  ia::PPORcGeo geo;
+  size_t lds = 0;
+  return (ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, lds)) ? "rc" : "lds";
 }
 
 size_t ppo_lds(py::dict d) {
@@ -178,5 +206,6 @@ size_t ppo_lds(py::dict d) {
 void register_engine(py::module& m) {
   m.def("engine_rollout", &rollout, "T-step device rollout (policy + env + learned reward) for N envs");
   m.def("engine_ppo_update", &ppo_update, "persistent PPO update / DP minibatch grads / apply");
+  m.def("engine_ppo_path", &ppo_path, "kernel used by engine_ppo_update mode 0 (rc | lds)");
   m.def("engine_ppo_lds", &ppo_lds, "LDS bytes the PPO kernel needs for a configuration");
 }

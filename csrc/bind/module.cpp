@@ -7,4 +7,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_envs(m);
   register_kernels(m);
   register_engine(m);
+  register_disc(m);
 }

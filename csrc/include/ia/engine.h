@@ -116,4 +116,21 @@ struct PPOArgs {
   unsigned long long* prof;  // optional [10] cycle counters per phase
 };
 
+// Geometry + workspace of the register-chained PPO kernel (ppo_rc.hip), planned on the host.
+constexpr int kMaxRcItems = 32;
+struct PPORcGeo {
+  int din[2][kWaveMaxLayers], dout[2][kWaveMaxLayers];
+  int w_off[2][kWaveMaxLayers], ldw[2][kWaveMaxLayers], b_off[2][kWaveMaxLayers];
+  int h_off[2][kWaveMaxLayers], ldh[2][kWaveMaxLayers];
+  int z_off[2][kWaveMaxLayers], ldz[2][kWaveMaxLayers], db_off[2][kWaveMaxLayers];
+  int ls_off, lsp_off, nm_off, red_off, param_lds;
+  int n_items;
+  int items[kMaxRcItems];  // q | layer << 1 | kind << 3 (0 W tile, 1 bias, 2 log_std) | out tile << 5 | in tile << 9
+  int dp;                  // padded obs row stride of xraw
+  float* xraw;             // [K][64][dp] gathered raw observations
+  float* acts;             // [K][64][16]
+  float* rowd;             // [K][64][4] old_logp, normalised advantage, return
+  float* mom;              // [K][128] per-minibatch obs mean / var
+};
+
 }  // namespace ia

@@ -34,6 +34,17 @@ struct MLPGrads {
   int accumulate;  // 1: add into existing grads, 0: overwrite
 };
 
+// Discriminator loss fused into the backward pass (GAIL/AIRL train_disc): the MLP output
+// is the logit z of "expert"; rows [0, n_expert) are expert (label 1), the rest generator
+// (label 0). dL/dz = (sigmoid(z) - y) * scale, and per-block sums of the statistics the
+// reference logs (common.py compute_train_stats) go to stats_slab[block][kDiscStats].
+constexpr int kDiscStats = 8;  // loss, correct, gen_pred, exp_correct, gen_correct, entropy, -, -
+struct DiscLoss {
+  int n_expert;
+  float scale;
+  float* stats_slab;
+};
+
 struct TmlpPlan {
   int rows;       // rows per block = 16 * waves
   int waves;

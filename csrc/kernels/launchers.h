@@ -19,6 +19,57 @@ hipError_t tmlp_forward(const MLPDesc& d, const float* X, int B, float* Y, hipSt
 hipError_t tmlp_backward(const MLPDesc& d, const float* X, const float* dY, int B, float* dX, const MLPGrads& g,
                          float* slab, hipStream_t s);
 
+// Fused discriminator loss on top of the backward kernel (kDisc): writes the gradient
+// slab [nblk][n_params] (flat order W0, b0, W1, b1, ...) and stats slab [nblk][kDiscStats].
+int tmlp_disc_blocks(const MLPDesc& d, int B);
+hipError_t tmlp_disc_fwd_bwd(const MLPDesc& d, const float* X, int B, const DiscLoss& dl, float* slab, hipStream_t s);
+
+// ---- disc.hip: fused discriminator update
+struct DiscGatherArgs {
+  int mb;  // rows per side: X holds 2*mb rows, expert first
+  int din, obs_dim, act_width;
+  int use_state, use_action, use_next_state, use_done;
+  int act_discrete;
+  const int64_t* e_idx;
+  const int64_t* g_idx;
+  const float *e_obs, *e_next_obs, *e_acts;
+  const int64_t* e_acts_i;
+  const bool* e_dones;
+  const float *g_obs, *g_next_obs, *g_acts;
+  const int64_t* g_acts_i;
+  const bool* g_dones;
+  const float* shift;  // per-column shift for the moment sums (running mean) or null
+  float* X;            // [2*mb][din]
+  float* partials;     // [nblk][2][din]
+};
+struct DiscNormArgs {
+  int mode;  // 0: reduce partials + merge; 1: reduce partials -> sums only; 2: merge from sums
+  int mb, din, nblk;
+  double* sums;  // [2][din] (modes 1, 2)
+  int n_total;   // rows behind sums (mode 2: all DP ranks)
+  const float* partials;
+  const float* shift;
+  float *rew_mean, *rew_var;
+  int* rew_count;
+  int pol_cols;
+  float *pol_mean, *pol_var;
+  int* pol_count;
+};
+struct DiscAdamArgs {
+  int n_params, nblk, stats_nblk;
+  int reduce, adam;  // reduce slab -> grad; apply Adam (from reduced or from grads[])
+  const float* slab;
+  const float* stats_slab;
+  float* stats_out;  // [kDiscStats] or null
+  float* grads;
+  float *params, *exp_avg, *exp_avg_sq;
+  float beta1, beta2, eps, weight_decay, step_size, bc2_sqrt;
+};
+int disc_gather_blocks(int mb);
+hipError_t disc_gather(const DiscGatherArgs& a, hipStream_t s);
+hipError_t disc_norm(const DiscNormArgs& a, hipStream_t s);
+hipError_t disc_adam(const DiscAdamArgs& a, hipStream_t s);
+
 // ---- rl.hip: GAE scan over [T, N]
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
                       int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);
@@ -32,6 +83,11 @@ hipError_t pref_loss_bwd(const float* coef, const float* gout, int P, int L, flo
 // ---- engine.hip: device-resident rollout (policy + env + learned reward)
 size_t rollout_lds_bytes(const RolloutArgs& a);
 hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s);
+
+// ---- ppo_rc.hip: register-chained single-rank PPO update (falls back to ppo.hip)
+bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes);
+size_t ppo_rc_workspace_floats(const PPOArgs& a);
+hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s);
 
 // ---- ppo.hip: persistent PPO update
 size_t ppo_lds_bytes(const PPOArgs& a);

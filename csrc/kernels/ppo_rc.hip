@@ -1,0 +1,794 @@
+// Register-chained PPO update (single rank, mode 0): the fast path of engine_ppo_update.
+//
+// Same semantics as ppo.hip (SB3 PPO.train: RunningNorm train-mode update per
+// minibatch, advantage normalisation, clipped surrogate + entropy + value loss,
+// clip_grad_norm_, Adam; reference call chain common.py train_gen -> PPO.learn ->
+// PPO.train) but laid out so that a minibatch needs three workgroup barriers instead
+// of one per layer and stage:
+//
+// * The MLPs run in the TRANSPOSED formulation C[out][row] = W . H^T on
+//   v_mfma_f32_16x16x4_f32 (exact fp32). A lane's accumulator then holds outputs
+//   4*(lane>>4)+q of row lane&15, and with the K (input-feature) order permuted as
+//   f(s, kk) = 16*(s>>2) + 4*kk + (s&3) those four registers ARE the B operand of the
+//   next layer's MFMA steps -- activations never leave registers between layers, and
+//   each wave (16 rows of one net) runs forward, loss and the dX backward chain with
+//   no barrier. Weights are read from LDS as float4 (forward) / float (W^T backward).
+// * Row-data preparation is hoisted out of the sequential loop: ppo_rc_prep_kernel
+//   gathers every minibatch of every epoch in parallel (perm is known up front),
+//   normalises advantages per minibatch and computes each minibatch's observation
+//   moments; the kernel only Chan-merges those moments (one lane per feature) one
+//   minibatch ahead.
+// * dW (K = rows) needs rows along K, i.e. a transpose: layer inputs and dZ are
+//   stored row-major in LDS once, then every wave computes whole dW tiles over all
+//   rows for the parameter "items" it owns. The owner keeps that tile's gradient and
+//   Adam moments in registers, so after the grad-norm reduction Adam updates W in
+//   LDS in place -- there is no gradient image at all.
+//
+// barriers / minibatch: [fwd+loss+bwd chain] B1 [dW items, |g|^2] B2 [clip, Adam] B3
+#include <hip/hip_runtime.h>
+
+#include "ia/engine.h"
+#include "launchers.h"
+
+namespace ia {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) float lf;
+typedef __attribute__((address_space(3))) f4 lf4;
+
+constexpr int kThreads = 512;
+constexpr int kWaves = 8;
+constexpr int kT = 2;      // max 16-wide tiles of a hidden layer (width <= 32)
+constexpr int kItems = 4;  // max parameter items owned per wave
+constexpr int kL = kWaveMaxLayers;
+
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ float act_fn(int act, float x) {
+  switch (act) {
+    case 1: return fmaxf(x, 0.f);
+    case 2: return tanhf(x);
+    case 3: return x > 0.f ? x : 0.01f * x;
+    case 4: return 1.f / (1.f + expf(-x));
+    default: return x;
+  }
+}
+__device__ __forceinline__ float act_grad(int act, float y) {
+  switch (act) {
+    case 1: return y > 0.f ? 1.f : 0.f;
+    case 2: return 1.f - y * y;
+    case 3: return y > 0.f ? 1.f : 0.01f;
+    case 4: return y * (1.f - y);
+    default: return 1.f;
+  }
+}
+__device__ __forceinline__ float sum16(float v) {  // over the 16 rows (lanes with equal lane>>4)
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+__device__ __forceinline__ float sum_kk(float v) {  // over the 4 lane groups of one row
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+__device__ __forceinline__ float max_kk(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16));
+  v = fmaxf(v, __shfl_xor(v, 32));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Geometry of one net layer in the LDS images (all offsets in floats, uniform).
+struct LG {
+  int din, dout, w, ldw, b, h, ldh, z, ldz, db;
+};
+__device__ __forceinline__ LG lg(const PPORcGeo& g, int q, int l) {
+  LG r;
+  r.din = rfl(g.din[q][l]);
+  r.dout = rfl(g.dout[q][l]);
+  r.w = rfl(g.w_off[q][l]);
+  r.ldw = rfl(g.ldw[q][l]);
+  r.b = rfl(g.b_off[q][l]);
+  r.h = rfl(g.h_off[q][l]);
+  r.ldh = rfl(g.ldh[q][l]);
+  r.z = rfl(g.z_off[q][l]);
+  r.ldz = rfl(g.ldz[q][l]);
+  r.db = rfl(g.db_off[q][l]);
+  return r;
+}
+
+// ---------------------------------------------------------------- prep (parallel over minibatches)
+// One wave per minibatch k = epoch * n_mb + mb, one lane per row.
+__global__ __launch_bounds__(64) void ppo_rc_prep_kernel(PPOArgs a, PPORcGeo g) {
+  const int k = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int B = a.batch, D = a.D;
+  const int n_mb = a.rows / B;
+  const int e = k / n_mb, mb = k - e * n_mb;
+  const bool ok = lane < B;
+  const int idx = ok ? a.perm[(size_t)e * a.rows + (size_t)mb * B + lane] : 0;
+  float* xr = g.xraw + ((size_t)k * 64 + lane) * g.dp;
+  for (int c = 0; c < g.dp; ++c) {
+    const float v = (ok && c < D) ? a.obs[(size_t)idx * D + c] : 0.f;
+    if (ok) xr[c] = v;
+    if (c < D && a.has_norm) {
+      const float m = wave_sum(v) / (float)B;
+      const float d = ok ? v - m : 0.f;
+      const float var = wave_sum(d * d) / (float)B;
+      if (lane == 0) {
+        g.mom[(size_t)k * 128 + c] = m;
+        g.mom[(size_t)k * 128 + 64 + c] = var;
+      }
+    }
+  }
+  float* ac = g.acts + ((size_t)k * 64 + lane) * 16;
+  for (int j = 0; j < 16; ++j) {
+    float v = 0.f;
+    if (ok) {
+      if (a.discrete) v = j == 0 ? a.acts[idx] : 0.f;
+      else v = j < a.A ? a.acts[(size_t)idx * a.A + j] : 0.f;
+      ac[j] = v;
+    }
+  }
+  float adv = ok ? a.adv[idx] : 0.f;
+  if (a.normalize_advantage && B > 1) {
+    const float m = wave_sum(adv) / (float)B;
+    const float d = ok ? adv - m : 0.f;
+    const float sd = sqrtf(wave_sum(d * d) / (float)(B - 1));
+    adv = d / (sd + 1e-8f);
+  }
+  if (ok) {
+    f4 rd = {a.old_logp[idx], adv, a.returns[idx], 0.f};
+    *reinterpret_cast<f4*>(g.rowd + ((size_t)k * 64 + lane) * 4) = rd;
+  }
+}
+
+// ---------------------------------------------------------------- main kernel
+struct Rows {  // one minibatch's rows for this lane, prefetched a minibatch ahead
+  float x[16];  // raw obs: feature 4s + kk of row lane&15 (s < S0)
+  f4 act;       // actions 4kk..4kk+3 (Gaussian) / act index in .x (discrete)
+  f4 rd;        // old_logp, adv_n, return
+};
+
+__device__ __forceinline__ void load_rows(const PPORcGeo& g, int k, int row, int kk, int s0, Rows& r) {
+  const float* xr = g.xraw + ((size_t)k * 64 + row) * g.dp;
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    if (s < s0) r.x[s] = xr[4 * s + kk];
+  const float* ac = g.acts + ((size_t)k * 64 + row) * 16;
+  r.act = *reinterpret_cast<const f4*>(ac + 4 * kk);
+  r.rd = *reinterpret_cast<const f4*>(g.rowd + ((size_t)k * 64 + row) * 4);
+}
+
+__global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) {
+  extern __shared__ __attribute__((aligned(16))) float lds_raw[];
+  lf* L = (lf*)lds_raw;
+  const int tid = threadIdx.x;
+  const int w = rfl(tid >> 6), lane = tid & 63;
+  const int r16 = lane & 15, kk = lane >> 4;
+  const int q = w >> 2;   // 0 actor, 1 critic
+  const int gw = w & 3;   // row tile
+  const int B = a.batch;
+  const int RT = B / 16;
+  const bool rows_wave = gw < RT;
+  const int nl = q == 0 ? a.n_pi : a.n_vf;
+  const int D = a.D, A = a.A;
+  const int s0 = (D + 3) / 4;
+  const bool gauss = !a.discrete;
+  const bool has_ls = gauss && a.log_std_off >= 0;
+  const int n_mb = a.rows / B;
+  const int K = a.n_epochs * n_mb;
+  const float invB = 1.f / (float)B;
+  const float c_half_log2pi = 0.91893853320467274f;
+
+  // ---- parameters -> LDS images (padding zero), Adam moments -> owner registers
+  for (int i = tid; i < g.param_lds; i += kThreads) L[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+      if (l >= (qq == 0 ? a.n_pi : a.n_vf)) continue;
+      const LG y = lg(g, qq, l);
+      const int wo = qq == 0 ? a.pi_w_off[l] : a.vf_w_off[l];
+      const int bo = qq == 0 ? a.pi_b_off[l] : a.vf_b_off[l];
+      for (int i = tid; i < y.dout * y.din; i += kThreads) {
+        const int o = i / y.din, c = i - o * y.din;
+        L[y.w + o * y.ldw + c] = a.params[wo + i];
+      }
+      for (int i = tid; i < y.dout; i += kThreads) L[y.b + i] = a.params[bo + i];
+    }
+  }
+  if (tid < 16) L[g.ls_off + tid] = (has_ls && tid < A) ? a.params[a.log_std_off + tid] : 0.f;
+  // normaliser running state (double-buffered per-minibatch mean / rstd)
+  // (owned by wave 7, one lane per feature)
+  const int nc = tid - (kThreads - 64);
+  const bool norm_lane = a.has_norm && nc >= 0 && nc < D;
+  float run_m = 0.f, run_v = 1.f, run_c = 0.f;
+  if (norm_lane) {
+    run_m = a.norm_mean[nc];
+    run_v = a.norm_var[nc];
+    run_c = a.norm_count[0];
+  }
+  // owned items: gradient / moments registers
+  const int n_items = rfl(g.n_items);
+  float gm[kItems][4], gv[kItems][4], gg[kItems][4];
+#pragma unroll
+  for (int it = 0; it < kItems; ++it) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gm[it][j] = gv[it][j] = gg[it][j] = 0.f;
+    const int id = w + it * kWaves;
+    if (id < n_items) {
+      const int desc = rfl(g.items[id]);
+      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+      if (kind == 0) {
+        const int din = g.din[iq][il], dout = g.dout[iq][il];
+        const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
+        const int in = 16 * tb + r16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int o = 16 * ta + 4 * kk + j;
+          if (o < dout && in < din) {
+            gm[it][j] = a.exp_avg[wo + o * din + in];
+            gv[it][j] = a.exp_avg_sq[wo + o * din + in];
+          }
+        }
+      } else if (kind == 1) {
+        const int dout = g.dout[iq][il];
+        const int bo = iq == 0 ? a.pi_b_off[il] : a.vf_b_off[il];
+        if (lane < dout) {
+          gm[it][0] = a.exp_avg[bo + lane];
+          gv[it][0] = a.exp_avg_sq[bo + lane];
+        }
+      } else if (has_ls && lane < A) {
+        gm[it][0] = a.exp_avg[a.log_std_off + lane];
+        gv[it][0] = a.exp_avg_sq[a.log_std_off + lane];
+      }
+    }
+  }
+  // stats accumulators (per lane; one lane per row contributes)
+  float st_ent = 0.f, st_pg = 0.f, st_vl = 0.f, st_cf = 0.f, st_kl = 0.f;
+  float step = a.adam_step[0];
+  float b1t = powf(a.beta1, step), b2t = powf(a.beta2, step);
+  const int hid_act = a.hidden_act;
+  // first minibatch norm stats
+  if (norm_lane && K > 0) {
+    const float m = g.mom[nc], v = g.mom[64 + nc], n = (float)B;
+    const float tot = run_c + n, delta = m - run_m;
+    run_m += delta * n / tot;
+    run_v = (run_v * run_c + v * n + delta * delta * run_c * n / tot) / tot;
+    run_c = tot;
+    L[g.nm_off + nc] = run_m;
+    L[g.nm_off + 64 + nc] = rsqrtf(run_v + a.norm_eps);
+  }
+  Rows cur;
+  const int row = 16 * gw + r16;
+  if (rows_wave && K > 0) load_rows(g, 0, row, kk, s0, cur);
+  unsigned long long prof[3] = {0, 0, 0};
+  __syncthreads();
+
+  for (int k = 0; k < K; ++k) {
+    unsigned long long t0 = a.prof ? clock64() : 0;
+    const int nb = (k & 1) * 128;  // norm buffer of minibatch k
+    Rows nxt;
+    if (rows_wave && k + 1 < K) load_rows(g, k + 1, row, kk, s0, nxt);
+    // Chan merge for minibatch k+1 (one lane per feature, wave 7)
+    if (norm_lane && k + 1 < K) {
+      const int c = nc;
+      {
+        const float m = g.mom[(size_t)(k + 1) * 128 + c], v = g.mom[(size_t)(k + 1) * 128 + 64 + c], n = (float)B;
+        const float tot = run_c + n, delta = m - run_m;
+        run_m += delta * n / tot;
+        run_v = (run_v * run_c + v * n + delta * delta * run_c * n / tot) / tot;
+        run_c = tot;
+        L[g.nm_off + (128 - nb) + c] = run_m;
+        L[g.nm_off + (128 - nb) + 64 + c] = rsqrtf(run_v + a.norm_eps);
+      }
+    }
+    if (rows_wave) {
+      // ---------------- normalised input: B operand of layer 0 (natural K order 4s + kk)
+      float xb[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        xb[s] = 0.f;
+        if (s < s0) {
+          const int c = 4 * s + kk;
+          float v = cur.x[s];
+          if (a.has_norm) v = (v - L[g.nm_off + nb + (c < D ? c : 0)]) * L[g.nm_off + nb + 64 + (c < D ? c : 0)];
+          xb[s] = c < D ? v : 0.f;
+        }
+      }
+      if (q == 0) {  // shared layer-0 input image
+        const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          if (s < s0) L[h0 + row * ld0 + 4 * s + kk] = xb[s];
+      }
+      // ---------------- forward (registers)
+      f4 hreg[kL - 1][kT];  // outputs of hidden layers (C layout), kept for act'
+      f4 head = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int l = 0; l < kL; ++l) {
+        if (l >= nl) continue;
+        const LG y = lg(g, q, l);
+        const bool last = l == nl - 1;
+        const int tout = (y.dout + 15) >> 4;
+        f4 acc[kT];
+#pragma unroll
+        for (int t = 0; t < kT; ++t) {
+          acc[t] = {0.f, 0.f, 0.f, 0.f};
+          if (t >= tout) continue;
+          const lf* wr = L + y.w + (16 * t + r16) * y.ldw;
+          if (l == 0) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+              if (s < s0) acc[t] = mfma(wr[4 * s + kk], xb[s], acc[t]);
+          } else {
+            const int tin = (y.din + 15) >> 4;
+#pragma unroll
+            for (int h = 0; h < kT; ++h) {
+              if (h >= tin) continue;
+              const f4 w4 = *(const lf4*)(wr + 16 * h + 4 * kk);
+              acc[t] = mfma(w4.x, hreg[l - 1][h].x, acc[t]);
+              acc[t] = mfma(w4.y, hreg[l - 1][h].y, acc[t]);
+              acc[t] = mfma(w4.z, hreg[l - 1][h].z, acc[t]);
+              acc[t] = mfma(w4.w, hreg[l - 1][h].w, acc[t]);
+            }
+          }
+          const int o0 = 16 * t + 4 * kk;
+          const f4 bb = *(const lf4*)(L + y.b + o0);
+          f4 v;
+          v.x = acc[t].x + bb.x;
+          v.y = acc[t].y + bb.y;
+          v.z = acc[t].z + bb.z;
+          v.w = acc[t].w + bb.w;
+          if (!last) {
+            v.x = o0 + 0 < y.dout ? act_fn(hid_act, v.x) : 0.f;
+            v.y = o0 + 1 < y.dout ? act_fn(hid_act, v.y) : 0.f;
+            v.z = o0 + 2 < y.dout ? act_fn(hid_act, v.z) : 0.f;
+            v.w = o0 + 3 < y.dout ? act_fn(hid_act, v.w) : 0.f;
+            if (l < kL - 1) {
+              hreg[l][t] = v;
+              // input image of layer l + 1 (for its dW)
+              const LG yn = lg(g, q, l + 1);
+              *(lf4*)(L + yn.h + row * yn.ldh + o0) = v;
+            }
+          } else if (t == 0) {
+            head = v;
+          }
+        }
+      }
+      // ---------------- loss -> dZ of the head (C layout, tile 0)
+      f4 dz = {0.f, 0.f, 0.f, 0.f};
+      const LG yh = lg(g, q, nl - 1);
+      if (q == 0) {
+        const float ao[4] = {cur.act.x, cur.act.y, cur.act.z, cur.act.w};
+        const float hv[4] = {head.x, head.y, head.z, head.w};
+        float dzv[4] = {0.f, 0.f, 0.f, 0.f};
+        const float old_lp = cur.rd.x, adv = cur.rd.y;
+        float logp, ent_row = 0.f;
+        int act_row = 0;
+        float pk[4] = {0.f, 0.f, 0.f, 0.f}, lpk[4] = {0.f, 0.f, 0.f, 0.f};
+        float zs[4] = {0.f, 0.f, 0.f, 0.f}, isd[4] = {0.f, 0.f, 0.f, 0.f};
+        if (gauss) {
+          float part = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int o = 4 * kk + j;
+            if (o < A) {
+              const float lsv = L[g.ls_off + o];
+              isd[j] = expf(-lsv);
+              zs[j] = (ao[j] - hv[j]) * isd[j];
+              part += -0.5f * zs[j] * zs[j] - lsv - c_half_log2pi;
+            }
+          }
+          logp = sum_kk(part);
+        } else {
+          const int n = yh.dout;
+          float mx = -INFINITY;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (4 * kk + j < n) mx = fmaxf(mx, hv[j]);
+          mx = max_kk(mx);
+          float zsum = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (4 * kk + j < n) zsum += expf(hv[j] - mx);
+          const float lz = logf(sum_kk(zsum));
+          act_row = __shfl((int)cur.act.x, r16);  // lane group 0 holds the action index
+          float sel = 0.f, ent = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int o = 4 * kk + j;
+            if (o < n) {
+              lpk[j] = hv[j] - mx - lz;
+              pk[j] = expf(lpk[j]);
+              ent -= pk[j] * lpk[j];
+              if (o == act_row) sel = lpk[j];
+            }
+          }
+          logp = sum_kk(sel);
+          ent_row = sum_kk(ent);
+        }
+        const float lr_ = logp - old_lp;
+        const float ratio = expf(lr_);
+        const float lo = 1.f - a.clip_range, hi = 1.f + a.clip_range;
+        const float pl1 = adv * ratio, pl2 = adv * fminf(fmaxf(ratio, lo), hi);
+        float c1, c2;  // torch.min routes the gradient to the smaller operand, half each on ties
+        if (pl1 < pl2) { c1 = 1.f; c2 = 0.f; } else if (pl2 < pl1) { c1 = 0.f; c2 = 1.f; } else { c1 = 0.5f; c2 = 0.5f; }
+        const float inside = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float dlogp = -invB * (c1 * adv + c2 * adv * inside) * ratio;
+        if (gauss) {
+          float lsp[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int o = 4 * kk + j;
+            dzv[j] = o < A ? dlogp * zs[j] * isd[j] : 0.f;
+            lsp[j] = o < A ? dlogp * (zs[j] * zs[j] - 1.f) : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float s = sum16(lsp[j]);
+            if (r16 == 0) L[g.lsp_off + gw * 16 + 4 * kk + j] = s;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int o = 4 * kk + j;
+            dzv[j] = o < yh.dout ? dlogp * ((o == act_row ? 1.f : 0.f) - pk[j]) -
+                                       a.ent_coef * invB * (-pk[j] * (lpk[j] + ent_row))
+                                 : 0.f;
+          }
+        }
+        dz = {dzv[0], dzv[1], dzv[2], dzv[3]};
+        if (kk == 0) {
+          st_pg += -fminf(pl1, pl2);
+          st_cf += fabsf(ratio - 1.f) > a.clip_range ? 1.f : 0.f;
+          st_kl += (ratio - 1.f) - lr_;
+          if (!gauss) st_ent += -ent_row;
+        }
+      } else {
+        float d = 0.f;
+        if (kk == 0) {
+          d = head.x - cur.rd.z;
+          st_vl += d * d;
+        }
+        dz = {kk == 0 ? a.vf_coef * 2.f * d * invB : 0.f, 0.f, 0.f, 0.f};
+      }
+      // ---------------- backward chain: store dZ_l, bias partials, dZ_{l-1} = W_l^T dZ_l * act'
+      f4 dzc[kT];
+      dzc[0] = dz;
+#pragma unroll
+      for (int t = 1; t < kT; ++t) dzc[t] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int l = kL - 1; l >= 0; --l) {
+        if (l >= nl) continue;
+        const LG y = lg(g, q, l);
+        const int tout = (y.dout + 15) >> 4;
+#pragma unroll
+        for (int u = 0; u < kT; ++u) {
+          if (u >= tout) continue;
+          *(lf4*)(L + y.z + row * y.ldz + 16 * u + 4 * kk) = dzc[u];
+          const float s0v = sum16(dzc[u].x), s1v = sum16(dzc[u].y), s2v = sum16(dzc[u].z), s3v = sum16(dzc[u].w);
+          if (r16 == 0) {
+            const f4 sv = {s0v, s1v, s2v, s3v};
+            *(lf4*)(L + y.db + gw * 64 + 16 * u + 4 * kk) = sv;
+          }
+        }
+        if (l == 0) break;
+        const int tin = (y.din + 15) >> 4;
+        f4 nd[kT];
+#pragma unroll
+        for (int u = 0; u < kT; ++u) {
+          nd[u] = {0.f, 0.f, 0.f, 0.f};
+          if (u >= tin) continue;
+          f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int tt = 0; tt < kT; ++tt) {
+            if (tt >= tout) continue;
+            const lf* wc = L + y.w + (16 * tt + 4 * kk) * y.ldw + 16 * u + r16;
+            acc = mfma(wc[0], dzc[tt].x, acc);
+            acc = mfma(wc[y.ldw], dzc[tt].y, acc);
+            acc = mfma(wc[2 * y.ldw], dzc[tt].z, acc);
+            acc = mfma(wc[3 * y.ldw], dzc[tt].w, acc);
+          }
+          const f4 hv = hreg[l > 0 ? l - 1 : 0][u];
+          nd[u].x = acc.x * act_grad(hid_act, hv.x);
+          nd[u].y = acc.y * act_grad(hid_act, hv.y);
+          nd[u].z = acc.z * act_grad(hid_act, hv.z);
+          nd[u].w = acc.w * act_grad(hid_act, hv.w);
+        }
+#pragma unroll
+        for (int u = 0; u < kT; ++u) dzc[u] = nd[u];
+      }
+    }
+    __syncthreads();  // B1: H / dZ images, bias and log-std partials complete
+    unsigned long long t1 = a.prof ? clock64() : 0;
+
+    // ---------------- dW / db / dlog_std for the owned items; |g|^2 partial
+    float ss = 0.f;
+#pragma unroll
+    for (int it = 0; it < kItems; ++it) {
+      const int id = w + it * kWaves;
+      if (id >= n_items) continue;
+      const int desc = rfl(g.items[id]);
+      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+      const LG y = lg(g, iq, il);
+      if (kind == 0) {
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        const lf* zp = L + y.z + kk * y.ldz + 16 * ta + r16;
+        const lf* hp = L + y.h + kk * y.ldh + 16 * tb + r16;
+        for (int s = 0; s < B / 4; ++s) acc = mfma(zp[4 * s * y.ldz], hp[4 * s * y.ldh], acc);
+        const int in = 16 * tb + r16;
+        const float av[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int o = 16 * ta + 4 * kk + j;
+          const float gval = (o < y.dout && in < y.din) ? av[j] : 0.f;
+          gg[it][j] = gval;
+          ss += gval * gval;
+        }
+      } else if (kind == 1) {
+        float gval = 0.f;
+        if (lane < y.dout)
+          for (int r = 0; r < RT; ++r) gval += L[y.db + r * 64 + lane];
+        gg[it][0] = gval;
+        ss += gval * gval;
+      } else {
+        float gval = 0.f;
+        if (has_ls && lane < A) {
+          for (int r = 0; r < RT; ++r) gval += L[g.lsp_off + r * 16 + lane];
+          gval -= a.ent_coef;
+        }
+        gg[it][0] = gval;
+        ss += gval * gval;
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) L[g.red_off + w] = ss;
+    // Gaussian entropy loss uses log_std before this minibatch's update
+    if (gauss && tid == 0) {
+      float sl = 0.f;
+      for (int j = 0; j < A; ++j) sl += has_ls ? L[g.ls_off + j] : 0.f;
+      st_ent += -(sl + A * (0.5f + c_half_log2pi));
+    }
+    __syncthreads();  // B2: all gradients formed
+    unsigned long long t2 = a.prof ? clock64() : 0;
+
+    // ---------------- clip_grad_norm_ + Adam on the owned items (W/b/log_std in LDS)
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) tot += L[g.red_off + i];
+    const float coef = fminf(1.f, a.max_grad_norm / (sqrtf(tot) + 1e-6f));
+    step += 1.f;
+    b1t *= a.beta1;
+    b2t *= a.beta2;
+    const float step_size = a.lr / (1.f - b1t);
+    const float bc2s = sqrtf(1.f - b2t);
+    const float b1 = a.beta1, b2 = a.beta2, eps = a.adam_eps;
+#pragma unroll
+    for (int it = 0; it < kItems; ++it) {
+      const int id = w + it * kWaves;
+      if (id >= n_items) continue;
+      const int desc = rfl(g.items[id]);
+      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+      const LG y = lg(g, iq, il);
+      if (kind == 0) {
+        const int in = 16 * tb + r16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int o = 16 * ta + 4 * kk + j;
+          if (o < y.dout && in < y.din) {
+            const float gval = gg[it][j] * coef;
+            gm[it][j] = b1 * gm[it][j] + (1.f - b1) * gval;
+            gv[it][j] = b2 * gv[it][j] + (1.f - b2) * gval * gval;
+            L[y.w + o * y.ldw + in] -= step_size * gm[it][j] / (sqrtf(gv[it][j]) / bc2s + eps);
+          }
+        }
+      } else {
+        const bool ok = kind == 1 ? lane < y.dout : (has_ls && lane < A);
+        if (ok) {
+          const float gval = gg[it][0] * coef;
+          gm[it][0] = b1 * gm[it][0] + (1.f - b1) * gval;
+          gv[it][0] = b2 * gv[it][0] + (1.f - b2) * gval * gval;
+          const int p = kind == 1 ? y.b + lane : g.ls_off + lane;
+          L[p] -= step_size * gm[it][0] / (sqrtf(gv[it][0]) / bc2s + eps);
+        }
+      }
+    }
+    if (rows_wave) cur = nxt;
+    __syncthreads();  // B3: parameters updated
+    if (a.prof) {
+      const unsigned long long t3 = clock64();
+      prof[0] += t1 - t0;
+      prof[1] += t2 - t1;
+      prof[2] += t3 - t2;
+    }
+  }
+
+  // ---- write back: params (from LDS), moments (owners), log_std, normaliser, stats
+#pragma unroll
+  for (int qq = 0; qq < 2; ++qq) {
+#pragma unroll
+    for (int l = 0; l < kL; ++l) {
+      if (l >= (qq == 0 ? a.n_pi : a.n_vf)) continue;
+      const LG y = lg(g, qq, l);
+      const int wo = qq == 0 ? a.pi_w_off[l] : a.vf_w_off[l];
+      const int bo = qq == 0 ? a.pi_b_off[l] : a.vf_b_off[l];
+      for (int i = tid; i < y.dout * y.din; i += kThreads) {
+        const int o = i / y.din, c = i - o * y.din;
+        a.params[wo + i] = L[y.w + o * y.ldw + c];
+      }
+      for (int i = tid; i < y.dout; i += kThreads) a.params[bo + i] = L[y.b + i];
+    }
+  }
+  if (has_ls && tid < A) a.params[a.log_std_off + tid] = L[g.ls_off + tid];
+#pragma unroll
+  for (int it = 0; it < kItems; ++it) {
+    const int id = w + it * kWaves;
+    if (id >= n_items) continue;
+    const int desc = rfl(g.items[id]);
+    const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+    if (kind == 0) {
+      const int din = g.din[iq][il], dout = g.dout[iq][il];
+      const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
+      const int in = 16 * tb + r16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = 16 * ta + 4 * kk + j;
+        if (o < dout && in < din) {
+          a.exp_avg[wo + o * din + in] = gm[it][j];
+          a.exp_avg_sq[wo + o * din + in] = gv[it][j];
+        }
+      }
+    } else if (kind == 1) {
+      const int dout = g.dout[iq][il];
+      const int bo = iq == 0 ? a.pi_b_off[il] : a.vf_b_off[il];
+      if (lane < dout) {
+        a.exp_avg[bo + lane] = gm[it][0];
+        a.exp_avg_sq[bo + lane] = gv[it][0];
+      }
+    } else if (has_ls && lane < A) {
+      a.exp_avg[a.log_std_off + lane] = gm[it][0];
+      a.exp_avg_sq[a.log_std_off + lane] = gv[it][0];
+    }
+  }
+  if (norm_lane && K > 0) {
+    a.norm_mean[nc] = run_m;
+    a.norm_var[nc] = run_v;
+    if (nc == 0) a.norm_count[0] = run_c;
+  }
+  // stats: [entropy_loss, pg_loss, value_loss, clip_fraction, approx_kl], sums of minibatch means
+  const float vals[5] = {st_ent, st_pg, st_vl, st_cf, st_kl};
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const float v = wave_sum(vals[i]);
+    if (lane == 0) L[g.red_off + 8 + w * 5 + i] = v;
+  }
+  __syncthreads();
+  if (tid < 5) {
+    float s = 0.f;
+    for (int i = 0; i < kWaves; ++i) s += L[g.red_off + 8 + i * 5 + tid];
+    if (!(tid == 0 && gauss)) s *= invB;  // per-row sums -> sums of minibatch means
+    a.stats[tid] += s;
+  }
+  if (tid == 0) a.adam_step[0] = step;
+  if (a.prof && tid == 0) {
+    a.prof[0] += prof[0];
+    a.prof[1] += prof[1];
+    a.prof[2] += prof[2];
+  }
+}
+
+}  // namespace
+
+// Host planning: LDS images + parameter items. Returns false if the configuration is
+// outside the fast path (falls back to ppo.hip).
+bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
+  g = PPORcGeo{};
+  if (a.batch % 16 != 0 || a.batch > 64 || a.rows % a.batch != 0 || a.D > 64 || a.A > 16) return false;
+  if (a.n_pi < 1 || a.n_vf < 1 || a.n_pi > kL || a.n_vf > kL) return false;
+  const int* dims[2] = {a.pi_dims, a.vf_dims};
+  const int nls[2] = {a.n_pi, a.n_vf};
+  int off = 0;
+  auto take = [&](int n) {
+    const int o = off;
+    off += (n + 3) & ~3;
+    return o;
+  };
+  // parameter images first (zeroed at kernel start)
+  for (int q = 0; q < 2; ++q) {
+    for (int l = 0; l < nls[q]; ++l) {
+      const int din = dims[q][l], dout = dims[q][l + 1];
+      const bool last = l == nls[q] - 1;
+      if (!last && dout > 16 * kT) return false;
+      if (last && dout > 16) return false;
+      if (l > 0 && din > 16 * kT) return false;
+      g.din[q][l] = din;
+      g.dout[q][l] = dout;
+      const int ip = l == 0 ? ((din + 3) & ~3) : ((din + 15) & ~15);
+      const int op = (dout + 15) & ~15;
+      g.ldw[q][l] = (l == 0 ? ((din + 15) & ~15) : ip) + 4;
+      g.w_off[q][l] = take(op * g.ldw[q][l]);
+      g.b_off[q][l] = take(op);
+    }
+  }
+  g.ls_off = take(16);
+  g.param_lds = off;
+  // activation images: layer-0 input shared by both nets
+  const int ld0 = ((a.D + 15) & ~15) + 4;
+  const int h0 = take(64 * ld0);
+  for (int q = 0; q < 2; ++q) {
+    for (int l = 0; l < nls[q]; ++l) {
+      if (l == 0) {
+        g.h_off[q][0] = h0;
+        g.ldh[q][0] = ld0;
+      } else {
+        g.ldh[q][l] = ((g.din[q][l] + 15) & ~15) + 4;
+        g.h_off[q][l] = take(64 * g.ldh[q][l]);
+      }
+      g.ldz[q][l] = ((g.dout[q][l] + 15) & ~15) + 4;
+      g.z_off[q][l] = take(64 * g.ldz[q][l]);
+      g.db_off[q][l] = take(4 * 64);
+    }
+  }
+  g.lsp_off = take(4 * 16);
+  g.nm_off = take(256);
+  g.red_off = take(8 + 8 * 5);
+  lds_bytes = (size_t)off * 4;
+  if (lds_bytes > 160 * 1024) return false;
+  // items: dW tiles, biases, log_std
+  int n = 0;
+  for (int q = 0; q < 2; ++q) {
+    for (int l = 0; l < nls[q]; ++l) {
+      const int to = (g.dout[q][l] + 15) / 16, ti = (g.din[q][l] + 15) / 16;
+      for (int ta = 0; ta < to; ++ta)
+        for (int tb = 0; tb < ti; ++tb) {
+          if (n >= kMaxRcItems) return false;
+          g.items[n++] = q | (l << 1) | (0 << 3) | (ta << 5) | (tb << 9);
+        }
+      if (n >= kMaxRcItems) return false;
+      g.items[n++] = q | (l << 1) | (1 << 3);
+    }
+  }
+  if (!a.discrete && a.log_std_off >= 0) {
+    if (n >= kMaxRcItems) return false;
+    g.items[n++] = 2 << 3;
+  }
+  g.n_items = n;
+  if ((n + kWaves - 1) / kWaves > kItems) return false;
+  g.dp = (a.D + 3) & ~3;
+  return true;
+}
+
+size_t ppo_rc_workspace_floats(const PPOArgs& a) {
+  const size_t K = (size_t)a.n_epochs * (a.rows / a.batch);
+  const size_t dp = (a.D + 3) & ~3;
+  return K * 64 * (dp + 16 + 4) + K * 128;
+}
+
+hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
+  PPORcGeo g;
+  size_t lds = 0;
+  if (!ppo_rc_plan(a, g, lds)) return hipErrorInvalidValue;
+  const size_t K = (size_t)a.n_epochs * (a.rows / a.batch);
+  g.xraw = workspace;
+  g.acts = g.xraw + K * 64 * g.dp;
+  g.rowd = g.acts + K * 64 * 16;
+  g.mom = g.rowd + K * 64 * 4;
+  if (K == 0) return hipSuccess;
+  hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64), 0, s, a, g);
+  hipLaunchKernelGGL(ppo_rc_kernel, dim3(1), dim3(kThreads), lds, s, a, g);
+  return hipGetLastError();
+}
+
+}  // namespace ia

@@ -111,11 +111,21 @@ __device__ __forceinline__ float wave_colsum(float s) {
   return s;
 }
 
-template <int NW>
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// kDisc: dY is not read; it is formed from the logits and labels (see DiscLoss) and the
+// block's loss statistics are written next to its gradient slab row.
+template <int NW, bool kDisc>
 __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p, const float* __restrict__ X,
                                                            const float* __restrict__ dY, int B, float* __restrict__ dX,
-                                                           MLPGrads g, float* __restrict__ slab) {
+                                                           MLPGrads g, float* __restrict__ slab, DiscLoss dl) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float disc_st[NW][kDiscStats];
+  float st[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int L = d.n_layers;
   char* q = smem;
   bf16* Wb = reinterpret_cast<bf16*>(q);
@@ -140,7 +150,7 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
   const int row0 = blockIdx.x * p.rows;
   const int w = wave_id();
   const int ROWS = p.rows;
-  const bool direct = gridDim.x == 1;
+  const bool direct = !kDisc && gridDim.x == 1;
   float* slab_row = direct ? nullptr : slab + (size_t)blockIdx.x * p.n_params;
 
   lds_zero(smem, p.bwd_lds);
@@ -172,7 +182,25 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
           Hs[l + 1][r * p.ld_h + col] = to_bf16(h);
         } else {
           const int gr = row0 + r;
-          float dy = (gr < B && col < dout) ? dY[(size_t)gr * dout + col] : 0.f;
+          float dy;
+          if constexpr (kDisc) {
+            dy = 0.f;
+            if (gr < B && col == 0) {
+              const float y = gr < dl.n_expert ? 1.f : 0.f;
+              const float sg = 1.f / (1.f + expf(-h));
+              const float sp = fmaxf(h, 0.f) + log1pf(expf(-fabsf(h)));  // softplus(z)
+              dy = (sg - y) * dl.scale;
+              const bool gen_pred = h < 0.f, gen_true = y == 0.f, correct = gen_pred == gen_true;
+              st[0] += sp - h * y;  // BCE-with-logits
+              st[1] += correct ? 1.f : 0.f;
+              st[2] += gen_pred ? 1.f : 0.f;
+              st[3] += (!gen_true && correct) ? 1.f : 0.f;
+              st[4] += (gen_true && correct) ? 1.f : 0.f;
+              st[5] += sp - h * sg;  // entropy of Bernoulli(sigmoid(z))
+            }
+          } else {
+            dy = (gr < B && col < dout) ? dY[(size_t)gr * dout + col] : 0.f;
+          }
           float dz = dy * act_grad_from_out(act, h);
           dzv[i] = dz;
           colsum += dz;
@@ -187,6 +215,21 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
         colsum = wave_colsum(colsum);
         if (lane_id() < 16) dbs[(0 * NW + w) * p.dmax_pad + col] = colsum;
       }
+    }
+  }
+
+  if constexpr (kDisc) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const float v = wave_sum64(st[k]);
+      if (lane_id() == 0) disc_st[w][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kDiscStats) {
+      float v = 0.f;
+      if (threadIdx.x < 6)
+        for (int ww = 0; ww < NW; ++ww) v += disc_st[ww][threadIdx.x];
+      dl.stats_slab[(size_t)blockIdx.x * kDiscStats + threadIdx.x] = v;
     }
   }
 
@@ -312,6 +355,27 @@ __global__ void tmlp_grad_reduce_kernel(const float* __restrict__ slab, int nblk
 
 }  // namespace
 
+int tmlp_disc_blocks(const MLPDesc& d, int B) {
+  const TmlpPlan p = plan_tmlp(d, tmlp_waves_for(d));
+  return (B + p.rows - 1) / p.rows;
+}
+
+hipError_t tmlp_disc_fwd_bwd(const MLPDesc& d, const float* X, int B, const DiscLoss& dl, float* slab, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (d.dims[d.n_layers] != 1 || d.out_act != ACT_IDENTITY) return hipErrorInvalidValue;
+  const int nw = tmlp_waves_for(d);
+  TmlpPlan p = plan_tmlp(d, nw);
+  const int nblk = (B + p.rows - 1) / p.rows;
+  const MLPGrads g{};
+  if (nw == 4)
+    hipLaunchKernelGGL((tmlp_bwd_kernel<4, true>), dim3(nblk), dim3(256), p.bwd_lds, s, d, p, X, nullptr, B, nullptr, g,
+                       slab, dl);
+  else
+    hipLaunchKernelGGL((tmlp_bwd_kernel<2, true>), dim3(nblk), dim3(128), p.bwd_lds, s, d, p, X, nullptr, B, nullptr, g,
+                       slab, dl);
+  return hipGetLastError();
+}
+
 int tmlp_waves_for(const MLPDesc& d) {
   TmlpPlan p4 = plan_tmlp(d, 4);
   return p4.bwd_lds <= 160 * 1024 ? 4 : 2;
@@ -344,10 +408,11 @@ hipError_t tmlp_backward(const MLPDesc& d, const float* X, const float* dY, int 
   TmlpPlan p = plan_tmlp(d, nw);
   const int nblk = (B + p.rows - 1) / p.rows;
   if (nblk > 1 && slab == nullptr) return hipErrorInvalidValue;
+  const DiscLoss none{};
   if (nw == 4)
-    hipLaunchKernelGGL(tmlp_bwd_kernel<4>, dim3(nblk), dim3(256), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab);
+    hipLaunchKernelGGL((tmlp_bwd_kernel<4, false>), dim3(nblk), dim3(256), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab, none);
   else
-    hipLaunchKernelGGL(tmlp_bwd_kernel<2>, dim3(nblk), dim3(128), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab);
+    hipLaunchKernelGGL((tmlp_bwd_kernel<2, false>), dim3(nblk), dim3(128), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab, none);
   if (nblk > 1) {
     hipLaunchKernelGGL(tmlp_grad_reduce_kernel, dim3((p.n_params + 255) / 256), dim3(256), 0, s, slab, nblk, p, d, g);
   }

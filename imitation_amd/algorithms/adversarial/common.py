@@ -25,7 +25,7 @@ from __future__ import annotations
 import abc
 import dataclasses
 import logging
-from typing import Callable, Dict, Iterable, Iterator, Mapping, Optional, Type
+from typing import Callable, Dict, Iterable, Iterator, Mapping, Optional, Sequence, Type
 
 import numpy as np
 import torch as th
@@ -41,6 +41,29 @@ from imitation_amd.rl import base as rl_base
 from imitation_amd.rl import distributions
 from imitation_amd.rl.policies import ActorCriticPolicy
 from imitation_amd.util import logger, networks, util
+
+
+def train_stats_from_sums(vec: Sequence[float], n_labels: float) -> Mapping[str, float]:
+    """Statistics dict from ``[loss, acc, n_generated, n_gen_pred, n_exp_correct,
+    n_gen_correct, entropy]`` (shared by the host path and the fused device update)."""
+    loss, acc, n_generated, n_gen_pred, n_exp_correct, n_gen_correct, entropy = vec
+    n_expert = n_labels - n_generated
+    pct_expert = n_expert / n_labels if n_labels > 0 else float("NaN")
+    n_expert_pred = int(n_labels - n_gen_pred)
+    pct_expert_pred = n_expert_pred / n_labels if n_labels > 0 else float("NaN")
+    expert_acc = float("NaN") if n_expert < 1 else n_exp_correct / n_expert
+    generated_acc = n_gen_correct / float(max(1, n_generated))
+    return {
+        "disc_loss": float(loss),
+        "disc_acc": float(acc),
+        "disc_acc_expert": float(expert_acc),
+        "disc_acc_gen": float(generated_acc),
+        "disc_entropy": float(entropy),
+        "disc_proportion_expert_true": float(pct_expert),
+        "disc_proportion_expert_pred": float(pct_expert_pred),
+        "n_expert": float(n_expert),
+        "n_generated": float(n_generated),
+    }
 
 
 def compute_train_stats(disc_logits_expert_is_high: th.Tensor, labels_expert_is_one: th.Tensor, disc_loss: th.Tensor) -> Mapping[str, float]:
@@ -62,24 +85,7 @@ def compute_train_stats(disc_logits_expert_is_high: th.Tensor, labels_expert_is_
             th.sum(th.logical_and(gen_true, correct).float()),
             th.mean(ent),
         ]).tolist()
-    loss, acc, n_generated, n_gen_pred, n_exp_correct, n_gen_correct, entropy = vec
-    n_expert = n_labels - n_generated
-    pct_expert = n_expert / n_labels if n_labels > 0 else float("NaN")
-    n_expert_pred = int(n_labels - n_gen_pred)
-    pct_expert_pred = n_expert_pred / n_labels if n_labels > 0 else float("NaN")
-    expert_acc = float("NaN") if n_expert < 1 else n_exp_correct / n_expert
-    generated_acc = n_gen_correct / float(max(1, n_generated))
-    return {
-        "disc_loss": float(loss),
-        "disc_acc": float(acc),
-        "disc_acc_expert": float(expert_acc),
-        "disc_acc_gen": float(generated_acc),
-        "disc_entropy": float(entropy),
-        "disc_proportion_expert_true": float(pct_expert),
-        "disc_proportion_expert_pred": float(pct_expert_pred),
-        "n_expert": float(n_expert),
-        "n_generated": float(n_generated),
-    }
+    return train_stats_from_sums(vec, n_labels)
 
 
 class _DeviceDemoSampler:
@@ -102,12 +108,17 @@ class _DeviceDemoSampler:
         self._perm = None
         self._pos = 0
 
-    def __next__(self) -> Dict[str, th.Tensor]:
+    def next_indices(self) -> th.Tensor:
+        """Row indices of the next batch (a contiguous slice of the epoch permutation)."""
         if self._perm is None or self._pos + self.batch_size > self.n:
             self._perm = th.randperm(self.n, device=self.device, generator=self._gen)
             self._pos = 0
         idx = self._perm[self._pos : self._pos + self.batch_size]
         self._pos += self.batch_size
+        return idx
+
+    def __next__(self) -> Dict[str, th.Tensor]:
+        idx = self.next_indices()
         return {k: v.index_select(0, idx) for k, v in self.data.items()}
 
     def __iter__(self):

@@ -185,6 +185,7 @@ class DeviceGAIL(GAIL):
         self._C = ops.native()
         self._dev = gen_algo.device
         self._setup_engine()
+        self._setup_fused_disc()
 
     # ------------------------------------------------------------------ setup
     def _setup_engine(self) -> None:
@@ -451,6 +452,201 @@ class DeviceGAIL(GAIL):
         if algo.ep_info_buffer:
             lg.record("rollout/ep_rew_mean", float(np.mean([e["r"] for e in algo.ep_info_buffer])))
             lg.record("rollout/ep_len_mean", float(np.mean([e["l"] for e in algo.ep_info_buffer])))
+
+    # ------------------------------------------------------------------ fused discriminator update
+    def _fused_disc_check(self) -> Tuple[bool, str]:
+        if type(self).logits_expert_is_high is not GAIL.logits_expert_is_high:
+            return False, "custom discriminator logits"
+        opt = self._disc_opt
+        if type(opt) is not th.optim.Adam or len(opt.param_groups) != 1:
+            return False, "discriminator optimizer is not a single-group torch.optim.Adam"
+        g = opt.param_groups[0]
+        if any(g.get(k) for k in ("amsgrad", "maximize", "capturable", "differentiable", "decoupled_weight_decay")):
+            return False, "Adam variant not fused"
+        if self._init_tensorboard:
+            return False, "tensorboard summaries need per-step logits"
+        if not isinstance(self._endless_expert_iterator, common._DeviceDemoSampler):
+            return False, "demonstrations are not a flat device transitions set"
+        base = self._reward_net.base if isinstance(self._reward_net, reward_nets.NormalizedRewardNet) else self._reward_net
+        try:
+            norm, lins, _, out_act = _mlp_layers(base.mlp)
+        except ValueError as e:
+            return False, str(e)
+        if norm is not None and type(norm) is not networks.RunningNorm:
+            return False, "reward-net input normaliser is not RunningNorm"
+        if out_act != 0 or lins[-1].out_features != 1 or len(lins) > 4:
+            return False, "reward MLP shape"
+        if max([lins[0].in_features] + [l.out_features for l in lins]) > 128:
+            return False, "reward MLP wider than 128"
+        mlp_params = {id(p) for l in lins for p in (l.weight, l.bias)}
+        if {id(p) for p in self._reward_net.parameters()} != mlp_params:
+            return False, "reward net has parameters outside its MLP"
+        if self.pol_norm is not None and (type(self.pol_norm) is not networks.RunningNorm or not base.use_state):
+            return False, "policy normaliser"
+        return True, ""
+
+    def _setup_fused_disc(self) -> None:
+        ok, why = self._fused_disc_check()
+        self._fused_disc = ok
+        self._fused_disc_why = why
+        if not ok:
+            return
+        dev = self._dev
+        base = self._reward_net.base if isinstance(self._reward_net, reward_nets.NormalizedRewardNet) else self._reward_net
+        norm, lins, hid, _ = _mlp_layers(base.mlp)
+        self._rnorm = norm
+        plist: List[nn.Parameter] = []
+        for l in lins:
+            plist += [l.weight, l.bias]
+        self._rflat = _FlatParams(plist)
+        n = self._rflat.n
+        self._r_m = th.zeros(n, device=dev)
+        self._r_v = th.zeros(n, device=dev)
+        self._adopt_disc_opt_state()
+        sampler = self._endless_expert_iterator
+        ed = sampler.data
+        ed["obs"] = ed["obs"].float().contiguous()
+        ed["next_obs"] = ed["next_obs"].float().contiguous()
+        ed["acts"] = (ed["acts"].long() if self.discrete else ed["acts"].float()).reshape(ed["acts"].shape[0], -1)
+        ed["acts"] = ed["acts"].reshape(-1).contiguous() if self.discrete else ed["acts"].contiguous()
+        ed["dones"] = ed["dones"].bool().contiguous()
+        gd = self._gen_dev._arrays
+        B, mb = self.demo_batch_size, self.demo_minibatch_size
+        dims = [lins[0].in_features] + [l.out_features for l in lins]
+        gblk, fblk, n_params = self._C.disc_plan_sizes(dims, mb)
+        assert n_params == n, (n_params, n)
+        n_mb = B // mb
+        z = lambda *sh, dt=th.float32: th.zeros(*sh, device=dev, dtype=dt)  # noqa: E731
+        self._disc_ws = dict(X=z(2 * mb, dims[0]), partials=z(gblk * 2 * dims[0]), slab=z(n_mb * fblk * n),
+                             stats_slab=z(n_mb * fblk * 8), grads=z(n), sums=z(2 * dims[0], dt=th.float64))
+        self._disc_stats = z(max(1, self.n_disc_updates_per_round), 8)
+        g = self._disc_opt.param_groups[0]
+        d = dict(batch=B, minibatch=mb, W=[l.weight for l in lins], b=[l.bias for l in lins], hidden_act=int(hid),
+                 rew_mean=norm.running_mean if norm is not None else None,
+                 rew_var=norm.running_var if norm is not None else None,
+                 rew_count=norm.count if norm is not None else None, rew_eps=float(norm.eps) if norm is not None else 1e-5,
+                 obs_dim=self.D, act_width=self.A, use_state=int(base.use_state), use_action=int(base.use_action),
+                 use_next_state=int(base.use_next_state), use_done=int(base.use_done), act_discrete=int(self.discrete),
+                 e_obs=ed["obs"], e_next_obs=ed["next_obs"], e_acts=ed["acts"], e_dones=ed["dones"],
+                 g_obs=gd["obs"], g_next_obs=gd["next_obs"], g_acts=gd["acts"], g_dones=gd["dones"],
+                 pol_mean=self.pol_norm.running_mean if self.pol_norm is not None else None,
+                 pol_var=self.pol_norm.running_var if self.pol_norm is not None else None,
+                 pol_count=self.pol_norm.count if self.pol_norm is not None else None,
+                 params=self._rflat.flat, exp_avg=self._r_m, exp_avg_sq=self._r_v,
+                 beta1=float(g["betas"][0]), beta2=float(g["betas"][1]), eps=float(g["eps"]),
+                 weight_decay=float(g.get("weight_decay", 0.0)), **self._disc_ws)
+        self._disc_plan = self._C.DiscPlan(d)
+
+    def _adopt_disc_opt_state(self) -> None:
+        """Make the torch Adam state of every reward parameter a view of the flat moment
+        buffers the fused kernel updates (copying in any state the optimizer already has,
+        e.g. after ``load_state_dict``), so both update paths and checkpoints agree."""
+        opt = self._disc_opt
+        for p, off in zip(self._rflat.params, self._rflat.offsets):
+            k = p.numel()
+            m = self._r_m[off : off + k].view_as(p)
+            v = self._r_v[off : off + k].view_as(p)
+            st = opt.state.get(p)
+            if st and st.get("exp_avg") is not None and st["exp_avg"].data_ptr() == m.data_ptr() \
+                    and st["exp_avg_sq"].data_ptr() == v.data_ptr():
+                continue
+            step = th.tensor(0.0)
+            if st:
+                with th.no_grad():
+                    m.copy_(st["exp_avg"])
+                    v.copy_(st["exp_avg_sq"])
+                step = st["step"] if isinstance(st["step"], th.Tensor) else th.tensor(float(st["step"]))
+            else:
+                m.zero_()
+                v.zero_()
+            opt.state[p] = {"step": step, "exp_avg": m, "exp_avg_sq": v}
+
+    def _fused_disc_update(self, slot: int) -> None:
+        """One discriminator optimizer step (== AdversarialTrainer.train_disc) with no host sync."""
+        if self._gen_dev.size() == 0:
+            raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
+        opt = self._disc_opt
+        self._adopt_disc_opt_state()
+        g = opt.param_groups[0]
+        t = float(opt.state[self._rflat.params[0]]["step"]) + 1.0
+        beta1, beta2 = g["betas"]
+        lr = float(g["lr"])
+        step_size = lr / (1.0 - beta1**t)
+        bc2_sqrt = (1.0 - beta2**t) ** 0.5
+        B, mb = self.demo_batch_size, self.demo_minibatch_size
+        e_idx = self._endless_expert_iterator.next_indices()
+        g_idx = th.randint(0, self._gen_dev.size(), (B,), device=self._dev)
+        merge_rew = self._rnorm is not None and self._rnorm.training
+        merge_pol = self.pol_norm is not None and self.pol_norm.training
+        plan = self._disc_plan
+        stats_out = self._disc_stats[slot]
+        if pdist.world_size() == 1:
+            plan.update(e_idx, g_idx, step_size, bc2_sqrt, merge_rew, merge_pol, stats_out)
+        else:
+            world = pdist.world_size()
+            for k in range(B // mb):
+                plan.gather(k, e_idx, g_idx)
+                if merge_rew or merge_pol:
+                    if pdist.norm_sync_active():
+                        plan.norm(1, 0, merge_rew, merge_pol)
+                        pdist.allreduce_sum_(self._disc_ws["sums"])
+                        plan.norm(2, 2 * mb * world, merge_rew, merge_pol)
+                    else:
+                        plan.norm(0, 0, merge_rew, merge_pol)
+                plan.fwd_bwd(k)
+            plan.adam(1, 0, 0.0, 1.0, stats_out)
+            pdist.allreduce_grads_flat(self._disc_ws["grads"])
+            plan.adam(0, 1, step_size, bc2_sqrt, None)
+        for p in self._rflat.params:
+            opt.state[p]["step"] += 1
+        self._disc_step += 1
+
+    def _disc_stats_dict(self, v: Sequence[float]) -> Mapping[str, float]:
+        B, mb = self.demo_batch_size, self.demo_minibatch_size
+        rows = 2 * mb
+        return common.train_stats_from_sums(
+            [v[0] / rows * (mb / B), v[1] / rows, float(mb), v[2], v[3], v[4], v[5] / rows], float(rows))
+
+    def _record_disc(self, stats: Mapping[str, float], disc_step: int) -> None:
+        self.logger.record("global_step", self._global_step)
+        for k, v in stats.items():
+            self.logger.record(k, v)
+        self.logger.dump(disc_step)
+
+    def train_disc(self, *, expert_samples: Optional[Mapping] = None, gen_samples: Optional[Mapping] = None) -> Mapping[str, float]:
+        if not self._fused_disc or expert_samples is not None or gen_samples is not None:
+            return super().train_disc(expert_samples=expert_samples, gen_samples=gen_samples)
+        with self.logger.accumulate_means("disc"):
+            self._fused_disc_update(0)
+            stats = self._disc_stats_dict(self._disc_stats[0].tolist())
+            self._record_disc(stats, self._disc_step)
+        return stats
+
+    def train(self, total_timesteps: int, callback=None) -> None:
+        """Rounds of device generator training + fused discriminator updates; the
+        discriminator statistics of a round are fetched with one host sync and logged
+        per update exactly as the reference's ``train_disc`` does."""
+        if not self._fused_disc:
+            return super().train(total_timesteps, callback)
+        n_rounds = total_timesteps // self.gen_train_timesteps
+        assert n_rounds >= 1, (
+            f"No updates (need at least {self.gen_train_timesteps} timesteps, have only total_timesteps={total_timesteps})!")
+        n = self.n_disc_updates_per_round
+        for r in range(n_rounds):
+            self.train_gen(self.gen_train_timesteps)
+            steps = []
+            with networks.training(self.reward_train):
+                for i in range(n):
+                    self._fused_disc_update(i)
+                    steps.append(self._disc_step)
+            if n:
+                vals = self._disc_stats[:n].tolist()
+                for i in range(n):
+                    with self.logger.accumulate_means("disc"):
+                        self._record_disc(self._disc_stats_dict(vals[i]), steps[i])
+            if callback:
+                callback(r)
+            self.logger.dump(self._global_step)
 
     # ------------------------------------------------------------------ checkpoint / resume
     _ENGINE_TENSORS = ("exp_avg", "exp_avg_sq", "adam_step", "state", "rng", "elapsed", "ep_ret", "cur_obs", "cur_start")

@@ -63,7 +63,9 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> Tuple[int, 
     if ws <= 1:
         return 0, 1
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # IMITATION_AMD_DIST_BACKEND=gloo lets several ranks share one GPU (rehearsal of the
+        # multi-GPU path on a single card; RCCL refuses two ranks on one device)
+        backend = os.environ.get("IMITATION_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend == "nccl":
         torch.cuda.set_device(local_rank())
@@ -205,6 +207,16 @@ def allreduce_grads(params: Iterable[torch.nn.Parameter]) -> None:
         n = p.grad.numel()
         p.grad.copy_(flat[off : off + n].view_as(p.grad))
         off += n
+
+
+def allreduce_sum_(t: torch.Tensor) -> None:
+    """Sum all-reduce of ``t`` in place (one collective; no-op on one rank)."""
+    if world_size() <= 1:
+        return
+    buf = _comm_device(t)
+    tdist.all_reduce(buf)
+    if buf is not t:
+        t.copy_(buf)
 
 
 def allreduce_grads_flat(flat: torch.Tensor) -> None:

@@ -104,8 +104,12 @@ def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, nor
 
 
 @gpu
-def test_ppo_kernel_matches_torch_reference():
-    tr, venv, gen, rn = _setup(n_envs=4, n_steps=32, batch=64, n_epochs=2)
+@pytest.mark.parametrize("env_id,allow_rc", [("seals/HalfCheetah-v1", 1), ("seals/HalfCheetah-v1", 0),
+                                             ("seals/CartPole-v0", 1), ("seals/CartPole-v0", 0)])
+def test_ppo_kernel_matches_torch_reference(env_id, allow_rc):
+    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=4, n_steps=32, batch=64, n_epochs=2)
+    tr._ppo_static["allow_rc"] = allow_rc
+    assert tr._C.engine_ppo_path(tr._ppo_static) == ("rc" if allow_rc else "lds")
     tr._rollout()
     pol = gen.policy
     norm = pol.features_extractor.normalize
@@ -150,3 +154,118 @@ def test_device_gail_rounds_run_and_learn_something():
     assert any(not th.equal(a, b) for a, b in zip(after, before))
     assert all(th.isfinite(p).all() for p in after)
     assert tr._gen_dev.size() > 0
+
+
+def _disc_reference(tr, e_idx, g_idx, mb_rows):
+    """fp32 PyTorch reference of one fused discriminator minibatch: norm updates + BCE grads
+    (MFMA operands emulated in bf16 so ReLU branches agree)."""
+    import copy
+
+    import torch.nn.functional as F
+
+    from imitation_amd.engine.gail import _mlp_layers
+    from imitation_amd.ops.mlp import tmlp_reference
+
+    base = tr._reward_net.base
+    norm, lins, hid, _ = _mlp_layers(base.mlp)
+    rnorm = copy.deepcopy(norm)
+    pnorm = copy.deepcopy(tr.pol_norm)
+    ed, gd = tr._endless_expert_iterator.data, tr._gen_dev._arrays
+    obs = th.cat([ed["obs"][e_idx], gd["obs"][g_idx]])
+    acts = th.cat([ed["acts"][e_idx], gd["acts"][g_idx]])
+    x = th.cat([obs, acts], 1)
+    pnorm.update_stats(obs)
+    rnorm.update_stats(x)
+    Ws = [l.weight.detach().clone().requires_grad_() for l in lins]
+    bs = [l.bias.detach().clone().requires_grad_() for l in lins]
+    logits = tmlp_reference(x, Ws, bs, hid, 0, rnorm.running_mean, rnorm.running_var, rnorm.eps,
+                            emulate_bf16_operands=True).reshape(-1)
+    labels = th.cat([th.ones(mb_rows // 2), th.zeros(mb_rows // 2)]).cuda()
+    loss = F.binary_cross_entropy_with_logits(logits, labels) * (tr.demo_minibatch_size / tr.demo_batch_size)
+    loss.backward()
+    grads = th.cat([t.grad.reshape(-1) for pair in zip(Ws, bs) for t in pair])
+    return rnorm, pnorm, grads, logits.detach(), loss.detach()
+
+
+@gpu
+def test_fused_disc_grads_and_norms_match_reference():
+    tr, venv, gen, rn = _setup(n_envs=8, n_steps=32, batch=64)
+    assert tr._fused_disc, tr._fused_disc_why
+    tr.train_gen()
+    th.cuda.synchronize()
+    B = tr.demo_batch_size
+    e_idx = th.randperm(len(tr._endless_expert_iterator.data["obs"]), device="cuda")[:B].contiguous()
+    g_idx = th.randint(0, tr._gen_dev.size(), (B,), device="cuda")
+    rnorm, pnorm, grads_ref, logits, loss = _disc_reference(tr, e_idx, g_idx, 2 * B)
+    plan = tr._disc_plan
+    stats = th.zeros(8, device="cuda")
+    plan.gather(0, e_idx, g_idx)
+    plan.norm(0, 0, True, True)
+    plan.fwd_bwd(0)
+    plan.adam(1, 0, 0.0, 1.0, stats)
+    th.cuda.synchronize()
+    norm = tr._rnorm
+    th.testing.assert_close(norm.running_mean, rnorm.running_mean, rtol=1e-5, atol=1e-5)
+    th.testing.assert_close(norm.running_var, rnorm.running_var, rtol=1e-4, atol=1e-5)
+    assert int(norm.count) == int(rnorm.count)
+    th.testing.assert_close(tr.pol_norm.running_mean, pnorm.running_mean, rtol=1e-5, atol=1e-5)
+    th.testing.assert_close(tr.pol_norm.running_var, pnorm.running_var, rtol=1e-4, atol=1e-5)
+    assert int(tr.pol_norm.count) == int(pnorm.count)
+    g = tr._disc_ws["grads"]
+    # backward MFMA operands (dZ, H) are bf16 as well: elementwise error ~1e-3 of the largest grad
+    th.testing.assert_close(g, grads_ref, rtol=2e-2, atol=1.5e-3 * float(grads_ref.abs().max()))
+    assert float(th.nn.functional.cosine_similarity(g, grads_ref, dim=0)) > 0.9999
+    s = tr._disc_stats_dict(stats.tolist())
+    from imitation_amd.algorithms.adversarial.common import compute_train_stats
+
+    labels = th.cat([th.ones(B), th.zeros(B)]).long().cuda()
+    ref = compute_train_stats(logits, labels, loss)
+    for k in ("disc_loss", "disc_entropy"):
+        assert abs(s[k] - ref[k]) < 2e-3 * max(1.0, abs(ref[k])), (k, s[k], ref[k])
+    for k in ("disc_acc", "disc_acc_expert", "disc_acc_gen", "disc_proportion_expert_pred"):
+        assert abs(s[k] - ref[k]) < 0.02, (k, s[k], ref[k])  # a few near-zero logits may flip sign in bf16
+    assert s["n_expert"] == ref["n_expert"] and s["n_generated"] == ref["n_generated"]
+
+
+@gpu
+def test_fused_disc_adam_matches_torch_adam():
+    tr, venv, gen, rn = _setup(n_envs=8, n_steps=32, batch=64)
+    assert tr._fused_disc
+    params = tr._rflat.params
+    clones = [p.detach().clone().requires_grad_() for p in params]
+    opt = th.optim.Adam(clones, **{k: v for k, v in tr._disc_opt.defaults.items()
+                                   if k in ("lr", "betas", "eps", "weight_decay")})
+    g = tr._disc_ws["grads"]
+    for step in range(1, 4):
+        gr = th.randn(g.numel(), device="cuda") * 0.1
+        g.copy_(gr)
+        off = 0
+        for c in clones:
+            c.grad = gr[off : off + c.numel()].view_as(c).clone()
+            off += c.numel()
+        opt.step()
+        b1, b2 = tr._disc_opt.defaults["betas"]
+        lr = tr._disc_opt.defaults["lr"]
+        tr._disc_plan.adam(0, 1, lr / (1 - b1**step), (1 - b2**step) ** 0.5, None)
+    th.cuda.synchronize()
+    for p, c in zip(params, clones):
+        th.testing.assert_close(p.detach(), c.detach(), rtol=1e-6, atol=1e-7)
+
+
+@gpu
+def test_fused_disc_train_logs_and_matches_generic_path_shape():
+    tr, venv, gen, rn = _setup(n_envs=8, n_steps=32, batch=64)
+    assert tr._fused_disc
+    before = [p.detach().clone() for p in rn.parameters()]
+    tr.train(2 * tr.gen_train_timesteps)
+    stats = tr.train_disc()
+    assert set(stats) >= {"disc_loss", "disc_acc", "disc_entropy", "n_expert", "n_generated"}
+    assert all(np.isfinite(v) for k, v in stats.items() if k != "disc_acc_expert")
+    assert stats["n_expert"] == stats["n_generated"] == tr.demo_minibatch_size
+    assert any(not th.equal(a, b) for a, b in zip(before, rn.parameters()))
+    st = tr._disc_opt.state[tr._rflat.params[0]]
+    assert float(st["step"]) == tr._disc_step == 3
+    # the generic (autograd + torch Adam) path shares the same optimizer state
+    tr.train_disc(expert_samples=next(tr._endless_expert_iterator), gen_samples=tr._gen_sample(tr.demo_batch_size))
+    assert float(tr._disc_opt.state[tr._rflat.params[0]]["step"]) == 4
+    assert tr._disc_opt.state[tr._rflat.params[0]]["exp_avg"].data_ptr() == tr._r_m.data_ptr()

@@ -18,9 +18,14 @@ for i in range(3):
     th.cuda.synchronize(); t = time.perf_counter(); tr._rollout(); th.cuda.synchronize(); dt = time.perf_counter() - t
     p = prof.cpu().numpy().astype(np.float64)
     print(f'rollout {dt*1e3:.2f} ms; cycles/step per env: policy {p[:,0].mean()/512:.0f} env {p[:,1].mean()/512:.0f} reward {p[:,2].mean()/512:.0f} total {p[:,3].mean()/512:.0f}', flush=True)
-for i in range(3):
-    pprof.zero_()
-    th.cuda.synchronize(); t = time.perf_counter(); tr._ppo_update(); th.cuda.synchronize(); dt = time.perf_counter() - t
-    pp = pprof.cpu().numpy() / 320
-    print(f'ppo update {dt*1e3:.2f} ms; cycles/minibatch: ' + ' '.join(f'{n}={v:.0f}' for n, v in zip(['rows','prep','fwd','loss','bwd','adam'], pp)), flush=True)
+for allow_rc in (1, 0):
+    tr._ppo_static['allow_rc'] = allow_rc
+    path = tr._C.engine_ppo_path(tr._ppo_static)
+    names = ['fwd+loss+bwd', 'dW', 'adam'] if path == 'rc' else ['rows', 'prep', 'fwd', 'loss', 'bwd', 'adam']
+    for i in range(3):
+        pprof.zero_()
+        th.cuda.synchronize(); t = time.perf_counter(); tr._ppo_update(); th.cuda.synchronize(); dt = time.perf_counter() - t
+        pp = pprof.cpu().numpy() / 320
+        print(f'ppo update [{path}] {dt*1e3:.2f} ms; cycles/minibatch: ' + ' '.join(f'{n}={v:.0f}' for n, v in zip(names, pp)), flush=True)
+tr._ppo_static['allow_rc'] = 1
 tr._ep_lens_running[:] = 0
