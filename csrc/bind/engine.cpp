@@ -154,6 +154,7 @@ void ppo_update(py::dict d) {
   a.mode = ival(d, "mode", 0);
   a.mb_index = ival(d, "mb_index", 0);
   a.prof = tptr<unsigned long long>(d, "prof", true);
+  a.rc_gmax = ival(d, "rc_gmax", 0);
   TORCH_CHECK(a.D <= 64, "obs dim <= 64");
   ia::PPORcGeo geo;
   size_t rc_lds = 0;
@@ -181,9 +182,12 @@ std::string ppo_path(py::dict d) {
   a.batch = ival(d, "batch");
   a.rows = ival(d, "rows");
   a.log_std_off = ival(d, "log_std_off", -1);
+  a.rc_gmax = ival(d, "rc_gmax", 0);
   ia::PPORcGeo geo;
   size_t lds = 0;
-  return (ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, lds)) ? "rc" : "lds";
+  if (ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, lds))
+    return "rc:g" + std::to_string(geo.G) + "x" + std::to_string(geo.nch) + "x" + std::to_string(geo.cw) + ":kt" + std::to_string(geo.kt);
+  return "lds";
 }
 
 size_t ppo_lds(py::dict d) {

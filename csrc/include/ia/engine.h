@@ -114,10 +114,12 @@ struct PPOArgs {
   int mode;  // 0: full persistent update; 1: one minibatch -> grads only; 2: apply clip+Adam from grads
   int mb_index;  // minibatch index for mode 1 (epoch * n_mb + mb)
   unsigned long long* prof;  // optional [10] cycle counters per phase
+  int rc_gmax;   // mode 0 fast path: max cooperating workgroups per minibatch (0 = default 8)
 };
 
 // Geometry + workspace of the register-chained PPO kernel (ppo_rc.hip), planned on the host.
-constexpr int kMaxRcItems = 32;
+constexpr int kMaxRcItems = 64;
+constexpr int kMaxRcGroups = 16;
 struct PPORcGeo {
   int din[2][kWaveMaxLayers], dout[2][kWaveMaxLayers];
   int w_off[2][kWaveMaxLayers], ldw[2][kWaveMaxLayers], b_off[2][kWaveMaxLayers];
@@ -127,10 +129,16 @@ struct PPORcGeo {
   int n_items;
   int items[kMaxRcItems];  // q | layer << 1 | kind << 3 (0 W tile, 1 bias, 2 log_std) | out tile << 5 | in tile << 9
   int dp;                  // padded obs row stride of xraw
-  float* xraw;             // [K][64][dp] gathered raw observations
-  float* acts;             // [K][64][16]
-  float* rowd;             // [K][64][4] old_logp, normalised advantage, return
+  int kt;                  // 16-wide tiles per hidden layer (2: width <= 32, 4: width <= 64)
+  int cw;                  // rows per chunk (one fwd/bwd pass of a workgroup)
+  int nch;                 // chunks per workgroup per minibatch
+  int G;                   // cooperating workgroups per minibatch (minibatch = G * nch * cw rows)
+  float* xraw;             // [K][G*nch][64][dp] gathered raw observations (one 64-row slot per chunk)
+  float* acts;             // [K][G*nch][64][16]
+  float* rowd;             // [K][G*nch][64][4] old_logp, normalised advantage, return
   float* mom;              // [K][128] per-minibatch obs mean / var
+  float* slab;             // [2][G][n_items][256] per-workgroup gradient partials (G > 1)
+  unsigned* sync;          // [0] arrival counter, [1] timeout flag (zeroed per launch)
 };
 
 }  // namespace ia

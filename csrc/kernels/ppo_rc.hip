@@ -1,4 +1,4 @@
-// Register-chained PPO update (single rank, mode 0): the fast path of engine_ppo_update.
+// Register-chained PPO update (mode 0): the fast path of engine_ppo_update.
 //
 // Same semantics as ppo.hip (SB3 PPO.train: RunningNorm train-mode update per
 // minibatch, advantage normalisation, clipped surrogate + entropy + value loss,
@@ -24,7 +24,18 @@
 //   Adam moments in registers, so after the grad-norm reduction Adam updates W in
 //   LDS in place -- there is no gradient image at all.
 //
-// barriers / minibatch: [fwd+loss+bwd chain] B1 [dW items, |g|^2] B2 [clip, Adam] B3
+// Large minibatches (AIRL-Hopper's 512 rows, or the data-parallel replicated update
+// whose minibatch is world x the per-rank one) are split over G cooperating
+// workgroups, each running nch chunks of cw rows and accumulating its dW partials in
+// the owner registers. The G partials are exchanged through a double-buffered slab
+// with the placement-independent sc1 hand-off (sc1 stores, every storing wave's
+// vmcnt(0), a workgroup barrier, one agent-scope arrival per workgroup, sc1 poll,
+// sc1 loads -- MI355X_MICROARCH "Workgroup dispatch ... & inter-workgroup
+// visibility", row 1) and summed in workgroup order, so every workgroup applies the
+// bit-identical update to its own LDS copy of the parameters; there is one grid-wide
+// wait per minibatch and no parameter broadcast. The spin is bounded (timeout flag).
+//
+// barriers / minibatch: [fwd+loss+bwd chain] B1 [dW items] (exchange) [|g|^2] B2 [clip, Adam] B3
 #include <hip/hip_runtime.h>
 
 #include "ia/engine.h"
@@ -39,8 +50,6 @@ typedef __attribute__((address_space(3))) f4 lf4;
 
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
-constexpr int kT = 2;      // max 16-wide tiles of a hidden layer (width <= 32)
-constexpr int kItems = 4;  // max parameter items owned per wave
 constexpr int kL = kWaveMaxLayers;
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
@@ -87,6 +96,13 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// sc1 (L1-bypassing, agent-coherent) 4-B accesses for the cross-workgroup hand-off.
+__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_sc1(float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ unsigned ld_sc1u(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Geometry of one net layer in the LDS images (all offsets in floats, uniform).
 struct LG {
   int din, dout, w, ldw, b, h, ldh, z, ldz, db;
@@ -107,68 +123,134 @@ __device__ __forceinline__ LG lg(const PPORcGeo& g, int q, int l) {
 }
 
 // ---------------------------------------------------------------- prep (parallel over minibatches)
-// One wave per minibatch k = epoch * n_mb + mb, one lane per row.
-__global__ __launch_bounds__(64) void ppo_rc_prep_kernel(PPOArgs a, PPORcGeo g) {
+// One workgroup per minibatch k = epoch * n_mb + mb, one wave per chunk (looping when the
+// minibatch has more chunks than waves), one lane per row. Minibatch statistics (obs
+// moments, advantage mean / std) are exact two-pass reductions over all its rows.
+constexpr int kPrepWaves = 16;
+
+__device__ __forceinline__ int prep_idx(const PPOArgs& a, const PPORcGeo& g, int e, int mb, int c, int lane) {
+  const int Bg = g.G * g.nch * g.cw;
+  return a.perm[(size_t)e * a.rows + (size_t)mb * Bg + (size_t)c * g.cw + lane];
+}
+
+__global__ __launch_bounds__(64 * kPrepWaves) void ppo_rc_prep_kernel(PPOArgs a, PPORcGeo g) {
+  __shared__ float red[kPrepWaves][64];
+  __shared__ float stat[2][64];
+  __shared__ float adv_stat[2];
+  __shared__ float red_a[kPrepWaves];
   const int k = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int B = a.batch, D = a.D;
-  const int n_mb = a.rows / B;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int CH = g.G * g.nch, cw = g.cw, Bg = CH * cw, D = a.D;
+  const int n_mb = a.rows / Bg;
   const int e = k / n_mb, mb = k - e * n_mb;
-  const bool ok = lane < B;
-  const int idx = ok ? a.perm[(size_t)e * a.rows + (size_t)mb * B + lane] : 0;
-  float* xr = g.xraw + ((size_t)k * 64 + lane) * g.dp;
-  for (int c = 0; c < g.dp; ++c) {
-    const float v = (ok && c < D) ? a.obs[(size_t)idx * D + c] : 0.f;
-    if (ok) xr[c] = v;
-    if (c < D && a.has_norm) {
-      const float m = wave_sum(v) / (float)B;
-      const float d = ok ? v - m : 0.f;
-      const float var = wave_sum(d * d) / (float)B;
-      if (lane == 0) {
-        g.mom[(size_t)k * 128 + c] = m;
-        g.mom[(size_t)k * 128 + 64 + c] = var;
+  const bool ok = lane < cw;
+  // ---- pass 1: gather, feature sums, advantage sum
+  float fs = 0.f, as = 0.f;  // lane c: this wave's sum of feature c; as: advantage sum (lane 0)
+  for (int c = wv; c < CH; c += nw) {
+    const int idx = ok ? prep_idx(a, g, e, mb, c, lane) : 0;
+    const size_t slot = (size_t)k * CH + c;
+    float* xr = g.xraw + (slot * 64 + lane) * g.dp;
+    for (int f = 0; f < g.dp; ++f) {
+      const float v = (ok && f < D) ? a.obs[(size_t)idx * D + f] : 0.f;
+      if (ok) xr[f] = v;
+      if (f < D && a.has_norm) {
+        const float s = wave_sum(v);
+        if (lane == f) fs += s;
       }
     }
+    float* ac = g.acts + (slot * 64 + lane) * 16;
+    for (int j = 0; j < 16; ++j) {
+      if (ok) {
+        float v = 0.f;
+        if (a.discrete) v = j == 0 ? a.acts[idx] : 0.f;
+        else v = j < a.A ? a.acts[(size_t)idx * a.A + j] : 0.f;
+        ac[j] = v;
+      }
+    }
+    as += wave_sum(ok ? a.adv[idx] : 0.f);
   }
-  float* ac = g.acts + ((size_t)k * 64 + lane) * 16;
-  for (int j = 0; j < 16; ++j) {
-    float v = 0.f;
-    if (ok) {
-      if (a.discrete) v = j == 0 ? a.acts[idx] : 0.f;
-      else v = j < a.A ? a.acts[(size_t)idx * a.A + j] : 0.f;
-      ac[j] = v;
+  red[wv][lane] = fs;
+  if (lane == 0) red_a[wv] = as;
+  __syncthreads();
+  if (wv == 0) {
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += red[i][lane];
+    stat[0][lane] = s / (float)Bg;
+    if (lane == 0) {
+      float t = 0.f;
+      for (int i = 0; i < nw; ++i) t += red_a[i];
+      adv_stat[0] = t / (float)Bg;
     }
   }
-  float adv = ok ? a.adv[idx] : 0.f;
-  if (a.normalize_advantage && B > 1) {
-    const float m = wave_sum(adv) / (float)B;
-    const float d = ok ? adv - m : 0.f;
-    const float sd = sqrtf(wave_sum(d * d) / (float)(B - 1));
-    adv = d / (sd + 1e-8f);
+  __syncthreads();
+  const float am = adv_stat[0];
+  // ---- pass 2: centred second moments
+  float fv = 0.f, av = 0.f;
+  for (int c = wv; c < CH; c += nw) {
+    const int idx = ok ? prep_idx(a, g, e, mb, c, lane) : 0;
+    if (a.has_norm) {
+      for (int f = 0; f < D; ++f) {
+        const float v = ok ? a.obs[(size_t)idx * D + f] : 0.f;
+        const float d = ok ? v - stat[0][f] : 0.f;
+        const float s = wave_sum(d * d);
+        if (lane == f) fv += s;
+      }
+    }
+    const float d = ok ? a.adv[idx] - am : 0.f;
+    av += wave_sum(d * d);
   }
-  if (ok) {
+  __syncthreads();
+  red[wv][lane] = fv;
+  __syncthreads();
+  if (wv == 0) {
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += red[i][lane];
+    stat[1][lane] = s / (float)Bg;
+  }
+  __syncthreads();
+  if (lane == 0) red_a[wv] = av;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += red_a[i];
+    adv_stat[1] = sqrtf(s / (float)(Bg > 1 ? Bg - 1 : 1));
+  }
+  __syncthreads();
+  if (a.has_norm && threadIdx.x < D) {
+    g.mom[(size_t)k * 128 + threadIdx.x] = stat[0][threadIdx.x];
+    g.mom[(size_t)k * 128 + 64 + threadIdx.x] = stat[1][threadIdx.x];
+  }
+  const float sd = adv_stat[1];
+  // ---- pass 3: per-row (old_logp, normalised advantage, return)
+  for (int c = wv; c < CH; c += nw) {
+    if (!ok) continue;
+    const int idx = prep_idx(a, g, e, mb, c, lane);
+    float adv = a.adv[idx];
+    if (a.normalize_advantage && Bg > 1) adv = (adv - am) / (sd + 1e-8f);
+    const size_t slot = (size_t)k * CH + c;
     f4 rd = {a.old_logp[idx], adv, a.returns[idx], 0.f};
-    *reinterpret_cast<f4*>(g.rowd + ((size_t)k * 64 + lane) * 4) = rd;
+    *reinterpret_cast<f4*>(g.rowd + (slot * 64 + lane) * 4) = rd;
   }
 }
 
 // ---------------------------------------------------------------- main kernel
-struct Rows {  // one minibatch's rows for this lane, prefetched a minibatch ahead
+struct Rows {  // one chunk's rows for this lane, prefetched a chunk ahead
   float x[16];  // raw obs: feature 4s + kk of row lane&15 (s < S0)
   f4 act;       // actions 4kk..4kk+3 (Gaussian) / act index in .x (discrete)
   f4 rd;        // old_logp, adv_n, return
 };
 
-__device__ __forceinline__ void load_rows(const PPORcGeo& g, int k, int row, int kk, int s0, Rows& r) {
-  const float* xr = g.xraw + ((size_t)k * 64 + row) * g.dp;
+__device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int row, int kk, int s0, Rows& r) {
+  const float* xr = g.xraw + (slot * 64 + row) * g.dp;
 #pragma unroll
   for (int s = 0; s < 16; ++s)
     if (s < s0) r.x[s] = xr[4 * s + kk];
-  const float* ac = g.acts + ((size_t)k * 64 + row) * 16;
+  const float* ac = g.acts + (slot * 64 + row) * 16;
   r.act = *reinterpret_cast<const f4*>(ac + 4 * kk);
-  r.rd = *reinterpret_cast<const f4*>(g.rowd + ((size_t)k * 64 + row) * 4);
+  r.rd = *reinterpret_cast<const f4*>(g.rowd + (slot * 64 + row) * 4);
 }
 
+template <int KT, int KI>
 __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* L = (lf*)lds_raw;
@@ -177,18 +259,22 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   const int r16 = lane & 15, kk = lane >> 4;
   const int q = w >> 2;   // 0 actor, 1 critic
   const int gw = w & 3;   // row tile
-  const int B = a.batch;
-  const int RT = B / 16;
+  const int grp = blockIdx.x;
+  const int G = g.G, nch = g.nch, cw = g.cw;
+  const int CH = G * nch;
+  const int Bg = CH * cw;  // minibatch rows
+  const int RT = cw / 16;
   const bool rows_wave = gw < RT;
   const int nl = q == 0 ? a.n_pi : a.n_vf;
   const int D = a.D, A = a.A;
   const int s0 = (D + 3) / 4;
   const bool gauss = !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
-  const int n_mb = a.rows / B;
+  const int n_mb = a.rows / Bg;
   const int K = a.n_epochs * n_mb;
-  const float invB = 1.f / (float)B;
+  const float invB = 1.f / (float)Bg;
   const float c_half_log2pi = 0.91893853320467274f;
+  const int n_items = rfl(g.n_items);
 
   // ---- parameters -> LDS images (padding zero), Adam moments -> owner registers
   for (int i = tid; i < g.param_lds; i += kThreads) L[i] = 0.f;
@@ -220,10 +306,9 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     run_c = a.norm_count[0];
   }
   // owned items: gradient / moments registers
-  const int n_items = rfl(g.n_items);
-  float gm[kItems][4], gv[kItems][4], gg[kItems][4];
+  float gm[KI][4], gv[KI][4], gg[KI][4];
 #pragma unroll
-  for (int it = 0; it < kItems; ++it) {
+  for (int it = 0; it < KI; ++it) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) gm[it][j] = gv[it][j] = gg[it][j] = 0.f;
     const int id = w + it * kWaves;
@@ -262,7 +347,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   const int hid_act = a.hidden_act;
   // first minibatch norm stats
   if (norm_lane && K > 0) {
-    const float m = g.mom[nc], v = g.mom[64 + nc], n = (float)B;
+    const float m = g.mom[nc], v = g.mom[64 + nc], n = (float)Bg;
     const float tot = run_c + n, delta = m - run_m;
     run_m += delta * n / tot;
     run_v = (run_v * run_c + v * n + delta * delta * run_c * n / tot) / tot;
@@ -272,20 +357,29 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   }
   Rows cur;
   const int row = 16 * gw + r16;
-  if (rows_wave && K > 0) load_rows(g, 0, row, kk, s0, cur);
+  // chunk unit u = k * nch + ch -> prep slot k * CH + grp * nch + ch
+  auto slot_of = [&](int u) -> size_t { return (size_t)(u / nch) * CH + (size_t)grp * nch + (u % nch); };
+  if (rows_wave && K > 0) load_rows(g, slot_of(0), row, kk, s0, cur);
   unsigned long long prof[3] = {0, 0, 0};
+  unsigned* arrive = g.sync;
+  unsigned* tflag = g.sync + 1;
   __syncthreads();
 
   for (int k = 0; k < K; ++k) {
     unsigned long long t0 = a.prof ? clock64() : 0;
     const int nb = (k & 1) * 128;  // norm buffer of minibatch k
-    Rows nxt;
-    if (rows_wave && k + 1 < K) load_rows(g, k + 1, row, kk, s0, nxt);
-    // Chan merge for minibatch k+1 (one lane per feature, wave 7)
-    if (norm_lane && k + 1 < K) {
-      const int c = nc;
-      {
-        const float m = g.mom[(size_t)(k + 1) * 128 + c], v = g.mom[(size_t)(k + 1) * 128 + 64 + c], n = (float)B;
+#pragma unroll
+    for (int it = 0; it < KI; ++it)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gg[it][j] = 0.f;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int u = k * nch + ch;
+      Rows nxt;
+      if (rows_wave && u + 1 < K * nch) load_rows(g, slot_of(u + 1), row, kk, s0, nxt);
+      // Chan merge for minibatch k+1 (one lane per feature, wave 7)
+      if (ch == 0 && norm_lane && k + 1 < K) {
+        const int c = nc;
+        const float m = g.mom[(size_t)(k + 1) * 128 + c], v = g.mom[(size_t)(k + 1) * 128 + 64 + c], n = (float)Bg;
         const float tot = run_c + n, delta = m - run_m;
         run_m += delta * n / tot;
         run_v = (run_v * run_c + v * n + delta * delta * run_c * n / tot) / tot;
@@ -293,270 +387,318 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         L[g.nm_off + (128 - nb) + c] = run_m;
         L[g.nm_off + (128 - nb) + 64 + c] = rsqrtf(run_v + a.norm_eps);
       }
-    }
-    if (rows_wave) {
-      // ---------------- normalised input: B operand of layer 0 (natural K order 4s + kk)
-      float xb[16];
+      if (rows_wave) {
+        // ---------------- normalised input: B operand of layer 0 (natural K order 4s + kk)
+        float xb[16];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        xb[s] = 0.f;
-        if (s < s0) {
-          const int c = 4 * s + kk;
-          float v = cur.x[s];
-          if (a.has_norm) v = (v - L[g.nm_off + nb + (c < D ? c : 0)]) * L[g.nm_off + nb + 64 + (c < D ? c : 0)];
-          xb[s] = c < D ? v : 0.f;
+        for (int s = 0; s < 16; ++s) {
+          xb[s] = 0.f;
+          if (s < s0) {
+            const int c = 4 * s + kk;
+            float v = cur.x[s];
+            if (a.has_norm) v = (v - L[g.nm_off + nb + (c < D ? c : 0)]) * L[g.nm_off + nb + 64 + (c < D ? c : 0)];
+            xb[s] = c < D ? v : 0.f;
+          }
         }
-      }
-      if (q == 0) {  // shared layer-0 input image
-        const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
+        if (q == 0) {  // shared layer-0 input image
+          const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
 #pragma unroll
-        for (int s = 0; s < 16; ++s)
-          if (s < s0) L[h0 + row * ld0 + 4 * s + kk] = xb[s];
-      }
-      // ---------------- forward (registers)
-      f4 hreg[kL - 1][kT];  // outputs of hidden layers (C layout), kept for act'
-      f4 head = {0.f, 0.f, 0.f, 0.f};
+          for (int s = 0; s < 16; ++s)
+            if (s < s0) L[h0 + row * ld0 + 4 * s + kk] = xb[s];
+        }
+        // ---------------- forward (registers)
+        f4 hreg[kL - 1][KT];  // outputs of hidden layers (C layout), kept for act'
+        f4 head = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int l = 0; l < kL; ++l) {
-        if (l >= nl) continue;
-        const LG y = lg(g, q, l);
-        const bool last = l == nl - 1;
-        const int tout = (y.dout + 15) >> 4;
-        f4 acc[kT];
+        for (int l = 0; l < kL; ++l) {
+          if (l >= nl) continue;
+          const LG y = lg(g, q, l);
+          const bool last = l == nl - 1;
+          const int tout = (y.dout + 15) >> 4;
+          f4 acc[KT];
 #pragma unroll
-        for (int t = 0; t < kT; ++t) {
-          acc[t] = {0.f, 0.f, 0.f, 0.f};
-          if (t >= tout) continue;
-          const lf* wr = L + y.w + (16 * t + r16) * y.ldw;
-          if (l == 0) {
+          for (int t = 0; t < KT; ++t) {
+            acc[t] = {0.f, 0.f, 0.f, 0.f};
+            if (t >= tout) continue;
+            const lf* wr = L + y.w + (16 * t + r16) * y.ldw;
+            if (l == 0) {
 #pragma unroll
-            for (int s = 0; s < 16; ++s)
-              if (s < s0) acc[t] = mfma(wr[4 * s + kk], xb[s], acc[t]);
+              for (int s = 0; s < 16; ++s)
+                if (s < s0) acc[t] = mfma(wr[4 * s + kk], xb[s], acc[t]);
+            } else {
+              const int tin = (y.din + 15) >> 4;
+#pragma unroll
+              for (int h = 0; h < KT; ++h) {
+                if (h >= tin) continue;
+                const f4 w4 = *(const lf4*)(wr + 16 * h + 4 * kk);
+                acc[t] = mfma(w4.x, hreg[l - 1][h].x, acc[t]);
+                acc[t] = mfma(w4.y, hreg[l - 1][h].y, acc[t]);
+                acc[t] = mfma(w4.z, hreg[l - 1][h].z, acc[t]);
+                acc[t] = mfma(w4.w, hreg[l - 1][h].w, acc[t]);
+              }
+            }
+            const int o0 = 16 * t + 4 * kk;
+            const f4 bb = *(const lf4*)(L + y.b + o0);
+            f4 v;
+            v.x = acc[t].x + bb.x;
+            v.y = acc[t].y + bb.y;
+            v.z = acc[t].z + bb.z;
+            v.w = acc[t].w + bb.w;
+            if (!last) {
+              v.x = o0 + 0 < y.dout ? act_fn(hid_act, v.x) : 0.f;
+              v.y = o0 + 1 < y.dout ? act_fn(hid_act, v.y) : 0.f;
+              v.z = o0 + 2 < y.dout ? act_fn(hid_act, v.z) : 0.f;
+              v.w = o0 + 3 < y.dout ? act_fn(hid_act, v.w) : 0.f;
+              if (l < kL - 1) {
+                hreg[l][t] = v;
+                // input image of layer l + 1 (for its dW)
+                const LG yn = lg(g, q, l + 1);
+                *(lf4*)(L + yn.h + row * yn.ldh + o0) = v;
+              }
+            } else if (t == 0) {
+              head = v;
+            }
+          }
+        }
+        // ---------------- loss -> dZ of the head (C layout, tile 0)
+        f4 dz = {0.f, 0.f, 0.f, 0.f};
+        const LG yh = lg(g, q, nl - 1);
+        if (q == 0) {
+          const float ao[4] = {cur.act.x, cur.act.y, cur.act.z, cur.act.w};
+          const float hv[4] = {head.x, head.y, head.z, head.w};
+          float dzv[4] = {0.f, 0.f, 0.f, 0.f};
+          const float old_lp = cur.rd.x, adv = cur.rd.y;
+          float logp, ent_row = 0.f;
+          int act_row = 0;
+          float pk[4] = {0.f, 0.f, 0.f, 0.f}, lpk[4] = {0.f, 0.f, 0.f, 0.f};
+          float zs[4] = {0.f, 0.f, 0.f, 0.f}, isd[4] = {0.f, 0.f, 0.f, 0.f};
+          if (gauss) {
+            float part = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int o = 4 * kk + j;
+              if (o < A) {
+                const float lsv = L[g.ls_off + o];
+                isd[j] = expf(-lsv);
+                zs[j] = (ao[j] - hv[j]) * isd[j];
+                part += -0.5f * zs[j] * zs[j] - lsv - c_half_log2pi;
+              }
+            }
+            logp = sum_kk(part);
           } else {
-            const int tin = (y.din + 15) >> 4;
+            const int n = yh.dout;
+            float mx = -INFINITY;
 #pragma unroll
-            for (int h = 0; h < kT; ++h) {
-              if (h >= tin) continue;
-              const f4 w4 = *(const lf4*)(wr + 16 * h + 4 * kk);
-              acc[t] = mfma(w4.x, hreg[l - 1][h].x, acc[t]);
-              acc[t] = mfma(w4.y, hreg[l - 1][h].y, acc[t]);
-              acc[t] = mfma(w4.z, hreg[l - 1][h].z, acc[t]);
-              acc[t] = mfma(w4.w, hreg[l - 1][h].w, acc[t]);
+            for (int j = 0; j < 4; ++j)
+              if (4 * kk + j < n) mx = fmaxf(mx, hv[j]);
+            mx = max_kk(mx);
+            float zsum = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (4 * kk + j < n) zsum += expf(hv[j] - mx);
+            const float lz = logf(sum_kk(zsum));
+            act_row = __shfl((int)cur.act.x, r16);  // lane group 0 holds the action index
+            float sel = 0.f, ent = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int o = 4 * kk + j;
+              if (o < n) {
+                lpk[j] = hv[j] - mx - lz;
+                pk[j] = expf(lpk[j]);
+                ent -= pk[j] * lpk[j];
+                if (o == act_row) sel = lpk[j];
+              }
+            }
+            logp = sum_kk(sel);
+            ent_row = sum_kk(ent);
+          }
+          const float lr_ = logp - old_lp;
+          const float ratio = expf(lr_);
+          const float lo = 1.f - a.clip_range, hi = 1.f + a.clip_range;
+          const float pl1 = adv * ratio, pl2 = adv * fminf(fmaxf(ratio, lo), hi);
+          float c1, c2;  // torch.min routes the gradient to the smaller operand, half each on ties
+          if (pl1 < pl2) { c1 = 1.f; c2 = 0.f; } else if (pl2 < pl1) { c1 = 0.f; c2 = 1.f; } else { c1 = 0.5f; c2 = 0.5f; }
+          const float inside = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+          const float dlogp = -invB * (c1 * adv + c2 * adv * inside) * ratio;
+          if (gauss) {
+            float lsp[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int o = 4 * kk + j;
+              dzv[j] = o < A ? dlogp * zs[j] * isd[j] : 0.f;
+              lsp[j] = o < A ? dlogp * (zs[j] * zs[j] - 1.f) : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float s = sum16(lsp[j]);
+              if (r16 == 0) L[g.lsp_off + gw * 16 + 4 * kk + j] = s;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int o = 4 * kk + j;
+              dzv[j] = o < yh.dout ? dlogp * ((o == act_row ? 1.f : 0.f) - pk[j]) -
+                                         a.ent_coef * invB * (-pk[j] * (lpk[j] + ent_row))
+                                   : 0.f;
             }
           }
-          const int o0 = 16 * t + 4 * kk;
-          const f4 bb = *(const lf4*)(L + y.b + o0);
-          f4 v;
-          v.x = acc[t].x + bb.x;
-          v.y = acc[t].y + bb.y;
-          v.z = acc[t].z + bb.z;
-          v.w = acc[t].w + bb.w;
-          if (!last) {
-            v.x = o0 + 0 < y.dout ? act_fn(hid_act, v.x) : 0.f;
-            v.y = o0 + 1 < y.dout ? act_fn(hid_act, v.y) : 0.f;
-            v.z = o0 + 2 < y.dout ? act_fn(hid_act, v.z) : 0.f;
-            v.w = o0 + 3 < y.dout ? act_fn(hid_act, v.w) : 0.f;
-            if (l < kL - 1) {
-              hreg[l][t] = v;
-              // input image of layer l + 1 (for its dW)
-              const LG yn = lg(g, q, l + 1);
-              *(lf4*)(L + yn.h + row * yn.ldh + o0) = v;
-            }
-          } else if (t == 0) {
-            head = v;
-          }
-        }
-      }
-      // ---------------- loss -> dZ of the head (C layout, tile 0)
-      f4 dz = {0.f, 0.f, 0.f, 0.f};
-      const LG yh = lg(g, q, nl - 1);
-      if (q == 0) {
-        const float ao[4] = {cur.act.x, cur.act.y, cur.act.z, cur.act.w};
-        const float hv[4] = {head.x, head.y, head.z, head.w};
-        float dzv[4] = {0.f, 0.f, 0.f, 0.f};
-        const float old_lp = cur.rd.x, adv = cur.rd.y;
-        float logp, ent_row = 0.f;
-        int act_row = 0;
-        float pk[4] = {0.f, 0.f, 0.f, 0.f}, lpk[4] = {0.f, 0.f, 0.f, 0.f};
-        float zs[4] = {0.f, 0.f, 0.f, 0.f}, isd[4] = {0.f, 0.f, 0.f, 0.f};
-        if (gauss) {
-          float part = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int o = 4 * kk + j;
-            if (o < A) {
-              const float lsv = L[g.ls_off + o];
-              isd[j] = expf(-lsv);
-              zs[j] = (ao[j] - hv[j]) * isd[j];
-              part += -0.5f * zs[j] * zs[j] - lsv - c_half_log2pi;
-            }
-          }
-          logp = sum_kk(part);
-        } else {
-          const int n = yh.dout;
-          float mx = -INFINITY;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (4 * kk + j < n) mx = fmaxf(mx, hv[j]);
-          mx = max_kk(mx);
-          float zsum = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (4 * kk + j < n) zsum += expf(hv[j] - mx);
-          const float lz = logf(sum_kk(zsum));
-          act_row = __shfl((int)cur.act.x, r16);  // lane group 0 holds the action index
-          float sel = 0.f, ent = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int o = 4 * kk + j;
-            if (o < n) {
-              lpk[j] = hv[j] - mx - lz;
-              pk[j] = expf(lpk[j]);
-              ent -= pk[j] * lpk[j];
-              if (o == act_row) sel = lpk[j];
-            }
-          }
-          logp = sum_kk(sel);
-          ent_row = sum_kk(ent);
-        }
-        const float lr_ = logp - old_lp;
-        const float ratio = expf(lr_);
-        const float lo = 1.f - a.clip_range, hi = 1.f + a.clip_range;
-        const float pl1 = adv * ratio, pl2 = adv * fminf(fmaxf(ratio, lo), hi);
-        float c1, c2;  // torch.min routes the gradient to the smaller operand, half each on ties
-        if (pl1 < pl2) { c1 = 1.f; c2 = 0.f; } else if (pl2 < pl1) { c1 = 0.f; c2 = 1.f; } else { c1 = 0.5f; c2 = 0.5f; }
-        const float inside = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-        const float dlogp = -invB * (c1 * adv + c2 * adv * inside) * ratio;
-        if (gauss) {
-          float lsp[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int o = 4 * kk + j;
-            dzv[j] = o < A ? dlogp * zs[j] * isd[j] : 0.f;
-            lsp[j] = o < A ? dlogp * (zs[j] * zs[j] - 1.f) : 0.f;
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float s = sum16(lsp[j]);
-            if (r16 == 0) L[g.lsp_off + gw * 16 + 4 * kk + j] = s;
+          dz = {dzv[0], dzv[1], dzv[2], dzv[3]};
+          if (kk == 0) {
+            st_pg += -fminf(pl1, pl2);
+            st_cf += fabsf(ratio - 1.f) > a.clip_range ? 1.f : 0.f;
+            st_kl += (ratio - 1.f) - lr_;
+            if (!gauss) st_ent += -ent_row;
           }
         } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int o = 4 * kk + j;
-            dzv[j] = o < yh.dout ? dlogp * ((o == act_row ? 1.f : 0.f) - pk[j]) -
-                                       a.ent_coef * invB * (-pk[j] * (lpk[j] + ent_row))
-                                 : 0.f;
+          float d = 0.f;
+          if (kk == 0) {
+            d = head.x - cur.rd.z;
+            st_vl += d * d;
           }
+          dz = {kk == 0 ? a.vf_coef * 2.f * d * invB : 0.f, 0.f, 0.f, 0.f};
         }
-        dz = {dzv[0], dzv[1], dzv[2], dzv[3]};
-        if (kk == 0) {
-          st_pg += -fminf(pl1, pl2);
-          st_cf += fabsf(ratio - 1.f) > a.clip_range ? 1.f : 0.f;
-          st_kl += (ratio - 1.f) - lr_;
-          if (!gauss) st_ent += -ent_row;
+        // ---------------- backward chain: store dZ_l, bias partials, dZ_{l-1} = W_l^T dZ_l * act'
+        f4 dzc[KT];
+        dzc[0] = dz;
+#pragma unroll
+        for (int t = 1; t < KT; ++t) dzc[t] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int l = kL - 1; l >= 0; --l) {
+          if (l >= nl) continue;
+          const LG y = lg(g, q, l);
+          const int tout = (y.dout + 15) >> 4;
+#pragma unroll
+          for (int u2 = 0; u2 < KT; ++u2) {
+            if (u2 >= tout) continue;
+            *(lf4*)(L + y.z + row * y.ldz + 16 * u2 + 4 * kk) = dzc[u2];
+            const float s0v = sum16(dzc[u2].x), s1v = sum16(dzc[u2].y), s2v = sum16(dzc[u2].z), s3v = sum16(dzc[u2].w);
+            if (r16 == 0) {
+              const f4 sv = {s0v, s1v, s2v, s3v};
+              *(lf4*)(L + y.db + gw * 64 + 16 * u2 + 4 * kk) = sv;
+            }
+          }
+          if (l == 0) break;
+          const int tin = (y.din + 15) >> 4;
+          f4 nd[KT];
+#pragma unroll
+          for (int u2 = 0; u2 < KT; ++u2) {
+            nd[u2] = {0.f, 0.f, 0.f, 0.f};
+            if (u2 >= tin) continue;
+            f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int tt = 0; tt < KT; ++tt) {
+              if (tt >= tout) continue;
+              const lf* wc = L + y.w + (16 * tt + 4 * kk) * y.ldw + 16 * u2 + r16;
+              acc = mfma(wc[0], dzc[tt].x, acc);
+              acc = mfma(wc[y.ldw], dzc[tt].y, acc);
+              acc = mfma(wc[2 * y.ldw], dzc[tt].z, acc);
+              acc = mfma(wc[3 * y.ldw], dzc[tt].w, acc);
+            }
+            const f4 hv = hreg[l > 0 ? l - 1 : 0][u2];
+            nd[u2].x = acc.x * act_grad(hid_act, hv.x);
+            nd[u2].y = acc.y * act_grad(hid_act, hv.y);
+            nd[u2].z = acc.z * act_grad(hid_act, hv.z);
+            nd[u2].w = acc.w * act_grad(hid_act, hv.w);
+          }
+#pragma unroll
+          for (int u2 = 0; u2 < KT; ++u2) dzc[u2] = nd[u2];
         }
-      } else {
-        float d = 0.f;
-        if (kk == 0) {
-          d = head.x - cur.rd.z;
-          st_vl += d * d;
-        }
-        dz = {kk == 0 ? a.vf_coef * 2.f * d * invB : 0.f, 0.f, 0.f, 0.f};
       }
-      // ---------------- backward chain: store dZ_l, bias partials, dZ_{l-1} = W_l^T dZ_l * act'
-      f4 dzc[kT];
-      dzc[0] = dz;
+      __syncthreads();  // B1: H / dZ images, bias and log-std partials of this chunk complete
+
+      // ---------------- dW / db / dlog_std partials of this chunk for the owned items
 #pragma unroll
-      for (int t = 1; t < kT; ++t) dzc[t] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int l = kL - 1; l >= 0; --l) {
-        if (l >= nl) continue;
-        const LG y = lg(g, q, l);
-        const int tout = (y.dout + 15) >> 4;
-#pragma unroll
-        for (int u = 0; u < kT; ++u) {
-          if (u >= tout) continue;
-          *(lf4*)(L + y.z + row * y.ldz + 16 * u + 4 * kk) = dzc[u];
-          const float s0v = sum16(dzc[u].x), s1v = sum16(dzc[u].y), s2v = sum16(dzc[u].z), s3v = sum16(dzc[u].w);
-          if (r16 == 0) {
-            const f4 sv = {s0v, s1v, s2v, s3v};
-            *(lf4*)(L + y.db + gw * 64 + 16 * u + 4 * kk) = sv;
-          }
-        }
-        if (l == 0) break;
-        const int tin = (y.din + 15) >> 4;
-        f4 nd[kT];
-#pragma unroll
-        for (int u = 0; u < kT; ++u) {
-          nd[u] = {0.f, 0.f, 0.f, 0.f};
-          if (u >= tin) continue;
+      for (int it = 0; it < KI; ++it) {
+        const int id = w + it * kWaves;
+        if (id >= n_items) continue;
+        const int desc = rfl(g.items[id]);
+        const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+        const LG y = lg(g, iq, il);
+        if (kind == 0) {
           f4 acc = {0.f, 0.f, 0.f, 0.f};
+          const lf* zp = L + y.z + kk * y.ldz + 16 * ta + r16;
+          const lf* hp = L + y.h + kk * y.ldh + 16 * tb + r16;
+          for (int s = 0; s < cw / 4; ++s) acc = mfma(zp[4 * s * y.ldz], hp[4 * s * y.ldh], acc);
+          const int in = 16 * tb + r16;
+          const float av[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
-          for (int tt = 0; tt < kT; ++tt) {
-            if (tt >= tout) continue;
-            const lf* wc = L + y.w + (16 * tt + 4 * kk) * y.ldw + 16 * u + r16;
-            acc = mfma(wc[0], dzc[tt].x, acc);
-            acc = mfma(wc[y.ldw], dzc[tt].y, acc);
-            acc = mfma(wc[2 * y.ldw], dzc[tt].z, acc);
-            acc = mfma(wc[3 * y.ldw], dzc[tt].w, acc);
+          for (int j = 0; j < 4; ++j) {
+            const int o = 16 * ta + 4 * kk + j;
+            gg[it][j] += (o < y.dout && in < y.din) ? av[j] : 0.f;
           }
-          const f4 hv = hreg[l > 0 ? l - 1 : 0][u];
-          nd[u].x = acc.x * act_grad(hid_act, hv.x);
-          nd[u].y = acc.y * act_grad(hid_act, hv.y);
-          nd[u].z = acc.z * act_grad(hid_act, hv.z);
-          nd[u].w = acc.w * act_grad(hid_act, hv.w);
+        } else if (kind == 1) {
+          float gval = 0.f;
+          if (lane < y.dout)
+            for (int r = 0; r < RT; ++r) gval += L[y.db + r * 64 + lane];
+          gg[it][0] += gval;
+        } else {
+          float gval = 0.f;
+          if (has_ls && lane < A)
+            for (int r = 0; r < RT; ++r) gval += L[g.lsp_off + r * 16 + lane];
+          gg[it][0] += gval;
         }
-#pragma unroll
-        for (int u = 0; u < kT; ++u) dzc[u] = nd[u];
       }
+      if (rows_wave) cur = nxt;
+      if (ch + 1 < nch) __syncthreads();  // images are rewritten by the next chunk
     }
-    __syncthreads();  // B1: H / dZ images, bias and log-std partials complete
     unsigned long long t1 = a.prof ? clock64() : 0;
 
-    // ---------------- dW / db / dlog_std for the owned items; |g|^2 partial
+    // ---------------- cross-workgroup exchange of the partials (G > 1)
+    if (G > 1) {
+      float* slab = g.slab + (size_t)(k & 1) * G * n_items * 256;
+#pragma unroll
+      for (int it = 0; it < KI; ++it) {
+        const int id = w + it * kWaves;
+        if (id >= n_items) continue;
+        float* p = slab + ((size_t)grp * n_items + id) * 256 + lane * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st_sc1(p + j, gg[it][j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        atomicAdd(arrive, 1u);
+        const unsigned target = (unsigned)G * (unsigned)(k + 1);
+        unsigned spins = 0;
+        while (ld_sc1u(arrive) < target) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 22) || ld_sc1u(tflag) != 0u) {
+            atomicOr(tflag, 1u);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < KI; ++it) {
+        const int id = w + it * kWaves;
+        if (id >= n_items) continue;
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int gi = 0; gi < G; ++gi) {
+          float* p = slab + ((size_t)gi * n_items + id) * 256 + lane * 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[j] += ld_sc1(p + j);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gg[it][j] = s[j];
+      }
+    }
+    // entropy term of log_std (d(-ent_coef * H)/d log_std = -ent_coef), once per minibatch; |g|^2
     float ss = 0.f;
 #pragma unroll
-    for (int it = 0; it < kItems; ++it) {
+    for (int it = 0; it < KI; ++it) {
       const int id = w + it * kWaves;
       if (id >= n_items) continue;
       const int desc = rfl(g.items[id]);
-      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-      const LG y = lg(g, iq, il);
-      if (kind == 0) {
-        f4 acc = {0.f, 0.f, 0.f, 0.f};
-        const lf* zp = L + y.z + kk * y.ldz + 16 * ta + r16;
-        const lf* hp = L + y.h + kk * y.ldh + 16 * tb + r16;
-        for (int s = 0; s < B / 4; ++s) acc = mfma(zp[4 * s * y.ldz], hp[4 * s * y.ldh], acc);
-        const int in = 16 * tb + r16;
-        const float av[4] = {acc.x, acc.y, acc.z, acc.w};
+      const int kind = (desc >> 3) & 3;
+      if (kind == 2 && has_ls && lane < A) gg[it][0] -= a.ent_coef;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int o = 16 * ta + 4 * kk + j;
-          const float gval = (o < y.dout && in < y.din) ? av[j] : 0.f;
-          gg[it][j] = gval;
-          ss += gval * gval;
-        }
-      } else if (kind == 1) {
-        float gval = 0.f;
-        if (lane < y.dout)
-          for (int r = 0; r < RT; ++r) gval += L[y.db + r * 64 + lane];
-        gg[it][0] = gval;
-        ss += gval * gval;
-      } else {
-        float gval = 0.f;
-        if (has_ls && lane < A) {
-          for (int r = 0; r < RT; ++r) gval += L[g.lsp_off + r * 16 + lane];
-          gval -= a.ent_coef;
-        }
-        gg[it][0] = gval;
-        ss += gval * gval;
-      }
+      for (int j = 0; j < 4; ++j) ss += gg[it][j] * gg[it][j];
     }
     ss = wave_sum(ss);
     if (lane == 0) L[g.red_off + w] = ss;
     // Gaussian entropy loss uses log_std before this minibatch's update
-    if (gauss && tid == 0) {
+    if (gauss && tid == 0 && grp == 0) {
       float sl = 0.f;
       for (int j = 0; j < A; ++j) sl += has_ls ? L[g.ls_off + j] : 0.f;
       st_ent += -(sl + A * (0.5f + c_half_log2pi));
@@ -576,7 +718,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     const float bc2s = sqrtf(1.f - b2t);
     const float b1 = a.beta1, b2 = a.beta2, eps = a.adam_eps;
 #pragma unroll
-    for (int it = 0; it < kItems; ++it) {
+    for (int it = 0; it < KI; ++it) {
       const int id = w + it * kWaves;
       if (id >= n_items) continue;
       const int desc = rfl(g.items[id]);
@@ -605,7 +747,6 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         }
       }
     }
-    if (rows_wave) cur = nxt;
     __syncthreads();  // B3: parameters updated
     if (a.prof) {
       const unsigned long long t3 = clock64();
@@ -615,7 +756,24 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     }
   }
 
-  // ---- write back: params (from LDS), moments (owners), log_std, normaliser, stats
+  // ---- stats (every workgroup: its rows); sums of minibatch means
+  const float vals[5] = {st_ent, st_pg, st_vl, st_cf, st_kl};
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const float v = wave_sum(vals[i]);
+    if (lane == 0) L[g.red_off + 8 + w * 5 + i] = v;
+  }
+  __syncthreads();
+  if (tid < 5) {
+    float s = 0.f;
+    for (int i = 0; i < kWaves; ++i) s += L[g.red_off + 8 + i * 5 + tid];
+    if (!(tid == 0 && gauss)) s *= invB;  // per-row sums -> sums of minibatch means
+    if (G > 1) atomicAdd(a.stats + tid, s);
+    else a.stats[tid] += s;
+  }
+  if (grp != 0) return;  // every workgroup holds the identical model: one writes it back
+
+  // ---- write back: params (from LDS), moments (owners), log_std, normaliser
 #pragma unroll
   for (int qq = 0; qq < 2; ++qq) {
 #pragma unroll
@@ -633,7 +791,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   }
   if (has_ls && tid < A) a.params[a.log_std_off + tid] = L[g.ls_off + tid];
 #pragma unroll
-  for (int it = 0; it < kItems; ++it) {
+  for (int it = 0; it < KI; ++it) {
     const int id = w + it * kWaves;
     if (id >= n_items) continue;
     const int desc = rfl(g.items[id]);
@@ -667,20 +825,6 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     a.norm_var[nc] = run_v;
     if (nc == 0) a.norm_count[0] = run_c;
   }
-  // stats: [entropy_loss, pg_loss, value_loss, clip_fraction, approx_kl], sums of minibatch means
-  const float vals[5] = {st_ent, st_pg, st_vl, st_cf, st_kl};
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const float v = wave_sum(vals[i]);
-    if (lane == 0) L[g.red_off + 8 + w * 5 + i] = v;
-  }
-  __syncthreads();
-  if (tid < 5) {
-    float s = 0.f;
-    for (int i = 0; i < kWaves; ++i) s += L[g.red_off + 8 + i * 5 + tid];
-    if (!(tid == 0 && gauss)) s *= invB;  // per-row sums -> sums of minibatch means
-    a.stats[tid] += s;
-  }
   if (tid == 0) a.adam_step[0] = step;
   if (a.prof && tid == 0) {
     a.prof[0] += prof[0];
@@ -689,16 +833,41 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   }
 }
 
+constexpr int items_per_wave(int kt) { return kt == 2 ? 4 : 8; }
+
 }  // namespace
 
-// Host planning: LDS images + parameter items. Returns false if the configuration is
-// outside the fast path (falls back to ppo.hip).
+// Host planning: LDS images + parameter items + workgroup split. Returns false if the
+// configuration is outside the fast path (falls back to ppo.hip).
 bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g = PPORcGeo{};
-  if (a.batch % 16 != 0 || a.batch > 64 || a.rows % a.batch != 0 || a.D > 64 || a.A > 16) return false;
+  if (a.batch % 16 != 0 || a.batch <= 0 || a.rows % a.batch != 0 || a.D > 64 || a.A > 16) return false;
   if (a.n_pi < 1 || a.n_vf < 1 || a.n_pi > kL || a.n_vf > kL) return false;
   const int* dims[2] = {a.pi_dims, a.vf_dims};
   const int nls[2] = {a.n_pi, a.n_vf};
+  int wmax = 0;
+  for (int q = 0; q < 2; ++q)
+    for (int l = 0; l + 1 < nls[q]; ++l) wmax = dims[q][l + 1] > wmax ? dims[q][l + 1] : wmax;
+  if (wmax > 64) return false;
+  g.kt = wmax <= 32 ? 2 : 4;
+  const int KT = g.kt;
+  // workgroup split: chunks of cw rows (64 for narrow nets, 32 for 64-wide ones: LDS)
+  int cw = KT == 2 ? 64 : 32;
+  if (a.batch < cw) cw = a.batch;
+  if (a.batch % cw != 0) {
+    cw = 16;
+  }
+  const int chunks = a.batch / cw;
+  const int gmax = a.rc_gmax > 0 ? (a.rc_gmax < kMaxRcGroups ? a.rc_gmax : kMaxRcGroups) : 8;
+  int G = 1;
+  for (int c = gmax; c >= 1; --c)
+    if (chunks % c == 0) {
+      G = c;
+      break;
+    }
+  g.cw = cw;
+  g.G = G;
+  g.nch = chunks / G;
   int off = 0;
   auto take = [&](int n) {
     const int o = off;
@@ -710,9 +879,9 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     for (int l = 0; l < nls[q]; ++l) {
       const int din = dims[q][l], dout = dims[q][l + 1];
       const bool last = l == nls[q] - 1;
-      if (!last && dout > 16 * kT) return false;
+      if (!last && dout > 16 * KT) return false;
       if (last && dout > 16) return false;
-      if (l > 0 && din > 16 * kT) return false;
+      if (l > 0 && din > 16 * KT) return false;
       g.din[q][l] = din;
       g.dout[q][l] = dout;
       const int ip = l == 0 ? ((din + 3) & ~3) : ((din + 15) & ~15);
@@ -724,9 +893,9 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   }
   g.ls_off = take(16);
   g.param_lds = off;
-  // activation images: layer-0 input shared by both nets
+  // activation images (cw rows): layer-0 input shared by both nets
   const int ld0 = ((a.D + 15) & ~15) + 4;
-  const int h0 = take(64 * ld0);
+  const int h0 = take(cw * ld0);
   for (int q = 0; q < 2; ++q) {
     for (int l = 0; l < nls[q]; ++l) {
       if (l == 0) {
@@ -734,10 +903,10 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
         g.ldh[q][0] = ld0;
       } else {
         g.ldh[q][l] = ((g.din[q][l] + 15) & ~15) + 4;
-        g.h_off[q][l] = take(64 * g.ldh[q][l]);
+        g.h_off[q][l] = take(cw * g.ldh[q][l]);
       }
       g.ldz[q][l] = ((g.dout[q][l] + 15) & ~15) + 4;
-      g.z_off[q][l] = take(64 * g.ldz[q][l]);
+      g.z_off[q][l] = take(cw * g.ldz[q][l]);
       g.db_off[q][l] = take(4 * 64);
     }
   }
@@ -765,15 +934,18 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     g.items[n++] = 2 << 3;
   }
   g.n_items = n;
-  if ((n + kWaves - 1) / kWaves > kItems) return false;
+  if ((n + kWaves - 1) / kWaves > items_per_wave(KT)) return false;
   g.dp = (a.D + 3) & ~3;
   return true;
 }
 
 size_t ppo_rc_workspace_floats(const PPOArgs& a) {
+  PPORcGeo g;
+  size_t lds = 0;
+  if (!ppo_rc_plan(a, g, lds)) return 0;
   const size_t K = (size_t)a.n_epochs * (a.rows / a.batch);
-  const size_t dp = (a.D + 3) & ~3;
-  return K * 64 * (dp + 16 + 4) + K * 128;
+  const size_t slots = K * g.G * g.nch;
+  return slots * 64 * (g.dp + 16 + 4) + K * 128 + 2 * (size_t)g.G * g.n_items * 256 + 64;
 }
 
 hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
@@ -781,13 +953,26 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   size_t lds = 0;
   if (!ppo_rc_plan(a, g, lds)) return hipErrorInvalidValue;
   const size_t K = (size_t)a.n_epochs * (a.rows / a.batch);
+  const size_t slots = K * g.G * g.nch;
   g.xraw = workspace;
-  g.acts = g.xraw + K * 64 * g.dp;
-  g.rowd = g.acts + K * 64 * 16;
-  g.mom = g.rowd + K * 64 * 4;
+  g.acts = g.xraw + slots * 64 * g.dp;
+  g.rowd = g.acts + slots * 64 * 16;
+  g.mom = g.rowd + slots * 64 * 4;
+  g.slab = g.mom + K * 128;
+  g.sync = reinterpret_cast<unsigned*>(g.slab + 2 * (size_t)g.G * g.n_items * 256);
   if (K == 0) return hipSuccess;
-  hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64), 0, s, a, g);
-  hipLaunchKernelGGL(ppo_rc_kernel, dim3(1), dim3(kThreads), lds, s, a, g);
+  hipError_t e = hipMemsetAsync(g.sync, 0, 64 * sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  const int CH = g.G * g.nch;
+  const int prep_waves = CH < kPrepWaves ? CH : kPrepWaves;
+  hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64 * prep_waves), 0, s, a, g);
+  // > 80 KiB of LDS keeps the cooperating workgroups one per CU (the measured condition of
+  // the sc1 hand-off); all G <= 16 of them are co-resident on an otherwise idle GPU
+  const size_t lds_launch = g.G > 1 && lds < 96 * 1024 ? 96 * 1024 : lds;
+  if (g.kt == 2)
+    hipLaunchKernelGGL((ppo_rc_kernel<2, 4>), dim3(g.G), dim3(kThreads), lds_launch, s, a, g);
+  else
+    hipLaunchKernelGGL((ppo_rc_kernel<4, 8>), dim3(g.G), dim3(kThreads), lds_launch, s, a, g);
   return hipGetLastError();
 }
 

@@ -136,16 +136,31 @@ def supports(venv, gen_algo, reward_net) -> Tuple[bool, str]:
     dims = [pol.features_dim] + [l.out_features for l in pl]
     if max(dims) > 64 or len(pl) > 4 or len(vl) > 4:
         return False, "policy too wide / deep for the engine"
-    if gen_algo.batch_size % 16 != 0 or gen_algo.batch_size > 64:
-        return False, "minibatch must be a multiple of 16 and <= 64"
+    if gen_algo.batch_size % 16 != 0:
+        return False, "minibatch must be a multiple of 16"
     if (gen_algo.n_steps * gen_algo.n_envs) % gen_algo.batch_size != 0:
         return False, "rollout size not a multiple of the minibatch"
+    if gen_algo.batch_size > 64 and not ppo_path(pol, nat, gen_algo.batch_size,
+                                                 gen_algo.n_steps * gen_algo.n_envs).startswith("rc"):
+        return False, "minibatch > 64 needs the register-chained PPO kernel, which rejects this policy"
     if gen_algo.clip_range_vf is not None or gen_algo.target_kl is not None:
         return False, "clip_range_vf / target_kl not supported by the engine"
     base = reward_net.base if isinstance(reward_net, reward_nets.NormalizedRewardNet) else reward_net
     if not isinstance(base, reward_nets.BasicRewardNet):
         return False, "reward net is not a BasicRewardNet"
     return True, ""
+
+
+def ppo_path(pol: ActorCriticPolicy, nat, batch: int, rows: int, rc_gmax: int = 0) -> str:
+    """Which PPO kernel the engine would run (``"rc:g<G>x<nch>x<cw>:kt<KT>"`` or ``"lds"``)."""
+    norm, pl, vl, _ = _policy_nets(pol)
+    discrete = isinstance(nat.action_space, spaces.Discrete)
+    D = int(np.prod(nat.observation_space.shape))
+    A = int(nat.action_space.n) if discrete else int(np.prod(nat.action_space.shape))
+    d = dict(D=D, A=A, discrete=int(discrete), pi_dims=[D] + [l.out_features for l in pl],
+             vf_dims=[D] + [l.out_features for l in vl], batch=int(batch), rows=int(rows),
+             log_std_off=0 if (hasattr(pol, "log_std") and not discrete) else -1, rc_gmax=int(rc_gmax))
+    return ops.native().engine_ppo_path(d)
 
 
 class _FlatParams:
@@ -185,6 +200,7 @@ class DeviceGAIL(GAIL):
         self._C = ops.native()
         self._dev = gen_algo.device
         self._setup_engine()
+        self._setup_dp()
         self._setup_fused_disc()
 
     # ------------------------------------------------------------------ setup
@@ -287,9 +303,10 @@ class DeviceGAIL(GAIL):
         if self.pol_norm is not None:
             d.update(norm_mean=self.pol_norm.running_mean, norm_var=self.pol_norm.running_var, norm_count=self.norm_count,
                      norm_eps=float(self.pol_norm.eps))
-        lds = self._C.engine_ppo_lds(d)
-        if lds > 150 * 1024:
-            raise ValueError(f"PPO engine needs {lds} B of LDS (> 150 KiB)")
+        if not self._C.engine_ppo_path(d).startswith("rc"):
+            lds = self._C.engine_ppo_lds(d) if d["batch"] <= 64 else 1 << 30
+            if lds > 150 * 1024:
+                raise ValueError(f"PPO engine needs {lds} B of LDS (> 150 KiB)")
         return d
 
     # ------------------------------------------------------------------ one generator round
@@ -322,19 +339,26 @@ class DeviceGAIL(GAIL):
         algo._update_current_progress_remaining(algo.num_timesteps, algo._total_timesteps or algo.num_timesteps)
         lr = float(algo.lr_schedule(algo._current_progress_remaining))
         clip = float(algo.clip_range(algo._current_progress_remaining))
-        perm = th.stack([th.randperm(rows, device=self._dev) for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
         adv, ret = rl_ops.gae(self.buf["rewards"], self.buf["values"], self.buf["starts"], self.buf["last_values"],
                               self.cur_start, float(algo.gamma), float(algo.gae_lambda))
         obs = self.buf["obs_buf"].reshape(rows, self.D)
         acts = self.buf["act_raw"].reshape(rows, -1)
+        old_logp = self.buf["logp"].reshape(rows)
+        adv = adv.reshape(rows).contiguous()
+        ret = ret.reshape(rows).contiguous()
         d = dict(self._ppo_static)
-        d.update(obs=obs, acts=acts, old_logp=self.buf["logp"].reshape(rows), adv=adv.reshape(rows).contiguous(),
-                 returns=ret.reshape(rows).contiguous(), perm=perm, clip_range=clip, lr=lr)
+        d.update(clip_range=clip, lr=lr)
         self.stats.zero_()
-        if pdist.world_size() == 1:
-            d["mode"] = 0
+        world = pdist.world_size()
+        if world == 1:
+            perm = th.stack([th.randperm(rows, device=self._dev) for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
+            d.update(obs=obs, acts=acts, old_logp=old_logp, adv=adv, returns=ret, perm=perm, mode=0)
             self._C.engine_ppo_update(d)
+        elif self._dp_replicated:
+            self._ppo_update_replicated(d, obs, acts, old_logp, adv, ret)
         else:
+            perm = th.stack([th.randperm(rows, device=self._dev) for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
+            d.update(obs=obs, acts=acts, old_logp=old_logp, adv=adv, returns=ret, perm=perm)
             n_mb = rows // algo.batch_size
             B = algo.batch_size
             for it in range(algo.n_epochs * n_mb):
@@ -352,6 +376,53 @@ class DeviceGAIL(GAIL):
             self.pol_norm.count.copy_(self.norm_count.to(self.pol_norm.count.dtype).reshape(()))
         algo._n_updates += algo.n_epochs
         self._last_ppo_info = (rows, algo.n_epochs * (rows // algo.batch_size))
+
+    def _setup_dp(self) -> None:
+        """Data-parallel PPO plan. With the register-chained kernel available for the global
+        minibatch (world x batch rows), every rank all-gathers the round's rollout rows
+        (ONE collective of rows x (D + A + 3) floats) and runs the identical, deterministic
+        update over the global batch -- exactly synchronous DP (averaged minibatch gradients,
+        global advantage / normaliser statistics), with no per-minibatch collective. The
+        minibatch permutation comes from a generator seeded identically on every rank.
+        Otherwise the per-minibatch grad/all-reduce/apply kernels are used."""
+        world = pdist.world_size()
+        self._dp_replicated = False
+        if world <= 1:
+            return
+        algo: PPO = self.gen_algo
+        rows = self.T * self.N
+        path = ppo_path(algo.policy, self._native, algo.batch_size * world, rows * world)
+        self._dp_replicated = path.startswith("rc")
+        seed = int(pdist.broadcast_object(int(np.random.randint(0, 2**31 - 1))))
+        self._perm_gen = th.Generator(device=self._dev)
+        self._perm_gen.manual_seed(seed)
+        Aw = 1 if self.discrete else self.A
+        self._dp_cols = (self.D, Aw)
+        self._dp_pack = th.zeros(rows, self.D + Aw + 3, device=self._dev)
+        self._dp_global = th.zeros(world * rows, self.D + Aw + 3, device=self._dev)
+
+    def _ppo_update_replicated(self, d: Dict[str, Any], obs, acts, old_logp, adv, ret) -> None:
+        algo: PPO = self.gen_algo
+        world = pdist.world_size()
+        rows = obs.shape[0]
+        D, Aw = self._dp_cols
+        pk = self._dp_pack
+        pk[:, :D] = obs
+        pk[:, D : D + Aw] = acts
+        pk[:, D + Aw] = old_logp
+        pk[:, D + Aw + 1] = adv
+        pk[:, D + Aw + 2] = ret
+        pdist.all_gather_flat(self._dp_global, pk)
+        gl = self._dp_global
+        rows_g = world * rows
+        perm = th.stack([th.randperm(rows_g, device=self._dev, generator=self._perm_gen)
+                         for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
+        d.update(obs=gl[:, :D].contiguous(), acts=gl[:, D : D + Aw].contiguous(),
+                 old_logp=gl[:, D + Aw].contiguous(), adv=gl[:, D + Aw + 1].contiguous(),
+                 returns=gl[:, D + Aw + 2].contiguous(), perm=perm, rows=rows_g, batch=algo.batch_size * world,
+                 mode=0, allow_rc=1)
+        self._C.engine_ppo_update(d)
+        # stats are sums over the global minibatches; every rank holds the same model
 
     def _dp_norm_update(self, batch: th.Tensor) -> None:
         """RunningNorm.update_stats with all-reduced moments (the kernel is told not to update)."""

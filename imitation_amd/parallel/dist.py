@@ -273,6 +273,20 @@ def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts).to(x.device)
 
 
+def all_gather_flat(out: torch.Tensor, x: torch.Tensor) -> None:
+    """Equal-size all-gather of ``x`` into ``out`` (``[world * n, ...]``, rank order), one collective."""
+    if world_size() <= 1:
+        out.copy_(x.reshape(out.shape))
+        return
+    if tdist.get_backend() == "nccl":
+        tdist.all_gather_into_tensor(out, x.contiguous())
+        return
+    xc = _comm_device(x.contiguous())
+    parts = [torch.empty_like(xc) for _ in range(world_size())]
+    tdist.all_gather(parts, xc)
+    out.copy_(torch.cat(parts).to(out.device).reshape(out.shape))
+
+
 def all_gather_object(obj) -> list:
     if world_size() <= 1:
         return [obj]

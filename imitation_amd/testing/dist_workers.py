@@ -71,3 +71,69 @@ def ppo_dp_worker(rank, world, seed):
                 policy_kwargs=dict(net_arch=[16]))
     model.learn(128)
     return [p.detach().numpy().copy() for p in model.policy.parameters()]
+
+
+def device_gail_dp_worker(rank, world, seed, batch):
+    """Replicated data-parallel device PPO update on ``cuda:0`` (ranks share the card over gloo).
+
+    Returns this rank's updated policy parameters and, on rank 0, the max deviation from
+    the fp32 PyTorch reference run on the all-gathered rows with the global minibatch."""
+    import os
+
+    from imitation_amd.data import rollout
+    from imitation_amd.engine.gail import DeviceGAIL
+    from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
+    from imitation_amd.rewards.reward_nets import BasicRewardNet, NormalizedRewardNet
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.testing.ppo_reference import torch_ppo_reference
+    from imitation_amd.util import logger
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    th.manual_seed(seed + rank)
+    np.random.seed(seed + rank)
+    rng = np.random.default_rng(seed + rank)
+    venv = make_vec_env("seals/HalfCheetah-v1", rng=rng, n_envs=4)
+    demo_env = make_vec_env("seals/HalfCheetah-v1", rng=np.random.default_rng(7), n_envs=4)
+    demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(512), rng=rng))
+    gen = PPO(FeedForward32Policy, venv, n_steps=32, batch_size=batch, n_epochs=2, device="cuda", seed=seed,
+              ent_coef=0.01, policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+    rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
+    tr = DeviceGAIL(demonstrations=demos, demo_batch_size=128, venv=venv, gen_algo=gen, reward_net=rn,
+                    n_disc_updates_per_round=1, custom_logger=logger.configure(f"/tmp/ia_dp_dev_{rank}", format_strs=[]))
+    assert tr._dp_replicated, "replicated DP path not selected"
+    tr._rollout()
+    pol = gen.policy
+    norm = pol.features_extractor.normalize
+    p0 = [p.detach().clone() for p in pol.parameters()]
+    n0 = (norm.running_mean.clone(), norm.running_var.clone(), norm.count.clone())
+    gen_state = tr._perm_gen.get_state()
+    tr._ppo_update()
+    th.cuda.synchronize()
+    out = {"params": [p.detach().cpu().numpy().copy() for p in pol.parameters()],
+           "norm": (norm.running_mean.cpu().numpy().copy(), norm.running_var.cpu().numpy().copy())}
+    if rank == 0:
+        gl = tr._dp_global
+        D, Aw = tr._dp_cols
+        rows_g = gl.shape[0]
+        g = th.Generator(device="cuda")
+        g.set_state(gen_state)
+        perm = th.stack([th.randperm(rows_g, device="cuda", generator=g) for _ in range(gen.n_epochs)])
+        p_dev = [p.detach().clone() for p in pol.parameters()]
+        with th.no_grad():
+            for p, q in zip(pol.parameters(), p0):
+                p.copy_(q)
+            norm.running_mean.copy_(n0[0]); norm.running_var.copy_(n0[1]); norm.count.copy_(n0[2])
+        from imitation_amd.parallel import dist as pdist
+
+        os.environ["IMITATION_AMD_FUSED"] = "0"
+        try:
+            with pdist.no_norm_sync():  # rank-local reference: no collectives
+                torch_ppo_reference(gen, gl[:, :D], gl[:, D:D + Aw], gl[:, D + Aw], gl[:, D + Aw + 1], gl[:, D + Aw + 2],
+                                    perm, clip=float(gen.clip_range(1.0)), lr=float(gen.lr_schedule(1.0)),
+                                    batch=batch * world)
+        finally:
+            os.environ.pop("IMITATION_AMD_FUSED", None)
+        out["max_dev"] = max(float((q.detach() - r).abs().max()) for q, r in zip(pol.parameters(), p_dev))
+        out["max_ref"] = max(float(q.detach().abs().max()) for q in pol.parameters())
+    return out

@@ -9,7 +9,8 @@ import torch as th
 gpu = pytest.mark.gpu
 
 
-def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epochs=2, seed=0, discrete=False):
+def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epochs=2, seed=0, discrete=False,
+           net_arch=None):
     from imitation_amd.data import rollout
     from imitation_amd.engine.gail import DeviceGAIL
     from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
@@ -25,8 +26,15 @@ def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epoc
     venv = make_vec_env(env_id, rng=rng, n_envs=n_envs)
     demo_env = make_vec_env(env_id, rng=np.random.default_rng(7), n_envs=4)
     demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
-    gen = PPO(FeedForward32Policy, venv, n_steps=n_steps, batch_size=batch, n_epochs=n_epochs, device="cuda", seed=seed,
-              ent_coef=0.01, policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+    from imitation_amd.rl.policies import ActorCriticPolicy
+
+    pk = dict(features_extractor_class=NormalizeFeaturesExtractor)
+    policy_cls = FeedForward32Policy
+    if net_arch is not None:
+        pk["net_arch"] = net_arch
+        policy_cls = ActorCriticPolicy
+    gen = PPO(policy_cls, venv, n_steps=n_steps, batch_size=batch, n_epochs=n_epochs, device="cuda", seed=seed,
+              ent_coef=0.01, policy_kwargs=pk)
     rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
     tr = DeviceGAIL(demonstrations=demos, demo_batch_size=256, venv=venv, gen_algo=gen, reward_net=rn,
                     n_disc_updates_per_round=1, custom_logger=logger.configure("/tmp/ia_test_engine", format_strs=[]))
@@ -75,41 +83,33 @@ def test_rollout_matches_host_env_policy_and_reward():
         os.environ.pop("IMITATION_AMD_FUSED", None)
 
 
-def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, norm_count):
-    """PyTorch fp32 PPO update with a fixed permutation (SB3 semantics)."""
-    import torch.nn.functional as F
+def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, norm_count=None):
+    from imitation_amd.testing.ppo_reference import torch_ppo_reference
 
-    pol = gen.policy
-    pol.set_training_mode(True)
-    params = list(pol.parameters())
-    opt = th.optim.Adam(params, lr=lr, eps=1e-5)
-    B = gen.batch_size
-    rows = obs.shape[0]
-    for e in range(perm.shape[0]):
-        for mb in range(rows // B):
-            idx = perm[e, mb * B:(mb + 1) * B].long()
-            v, lp, ent = pol.evaluate_actions(obs[idx], acts[idx])
-            v = v.flatten()
-            a = adv[idx]
-            a = (a - a.mean()) / (a.std() + 1e-8)
-            ratio = th.exp(lp - old_logp[idx])
-            pl = -th.min(a * ratio, a * th.clamp(ratio, 1 - clip, 1 + clip)).mean()
-            vl = F.mse_loss(ret[idx], v)
-            el = -th.mean(ent)
-            loss = pl + gen.ent_coef * el + gen.vf_coef * vl
-            opt.zero_grad()
-            loss.backward()
-            th.nn.utils.clip_grad_norm_(params, gen.max_grad_norm)
-            opt.step()
+    torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr)
 
 
 @gpu
-@pytest.mark.parametrize("env_id,allow_rc", [("seals/HalfCheetah-v1", 1), ("seals/HalfCheetah-v1", 0),
-                                             ("seals/CartPole-v0", 1), ("seals/CartPole-v0", 0)])
-def test_ppo_kernel_matches_torch_reference(env_id, allow_rc):
-    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=4, n_steps=32, batch=64, n_epochs=2)
+@pytest.mark.parametrize("env_id,allow_rc,batch,gmax,net_arch,path", [
+    ("seals/HalfCheetah-v1", 1, 64, 0, None, "rc:g1x1x64:kt2"),
+    ("seals/HalfCheetah-v1", 0, 64, 0, None, "lds"),
+    ("seals/CartPole-v0", 1, 64, 0, None, "rc:g1x1x64:kt2"),
+    ("seals/CartPole-v0", 0, 64, 0, None, "lds"),
+    # cooperating workgroups (sc1 partial exchange) and multi-chunk workgroups
+    ("seals/HalfCheetah-v1", 1, 128, 0, None, "rc:g2x1x64:kt2"),
+    ("seals/HalfCheetah-v1", 1, 128, 1, None, "rc:g1x2x64:kt2"),
+    ("seals/HalfCheetah-v1", 1, 256, 2, None, "rc:g2x2x64:kt2"),
+    ("seals/CartPole-v0", 1, 256, 0, None, "rc:g4x1x64:kt2"),
+    # 64-wide nets (AIRL-Hopper MlpPolicy [64, 64]): 32-row chunks
+    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64]), "rc:g2x1x32:kt4"),
+    ("seals/Hopper-v1", 1, 256, 4, dict(pi=[64, 64], vf=[64, 64]), "rc:g4x2x32:kt4"),
+])
+def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_arch, path):
+    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=8 if batch > 64 else 4, n_steps=32, batch=batch, n_epochs=2,
+                               net_arch=net_arch)
     tr._ppo_static["allow_rc"] = allow_rc
-    assert tr._C.engine_ppo_path(tr._ppo_static) == ("rc" if allow_rc else "lds")
+    tr._ppo_static["rc_gmax"] = gmax
+    assert tr._C.engine_ppo_path(tr._ppo_static) == path
     tr._rollout()
     pol = gen.policy
     norm = pol.features_extractor.normalize

@@ -72,3 +72,17 @@ def test_ppo_ranks_stay_in_sync():
     out = run_ranks(W.ppo_dp_worker, 2, 3)
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_device_gail_replicated_dp_matches_large_batch(world, monkeypatch):
+    """world ranks share one GPU over gloo: after one device PPO round every rank holds the
+    bit-identical model, equal to the fp32 reference over the gathered rows (minibatch world x 64)."""
+    monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
+    out = run_ranks(W.device_gail_dp_worker, world, 5, 64, timeout=240)
+    for r in range(1, world):
+        for a, b in zip(out[0]["params"], out[r]["params"]):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(out[0]["norm"][0], out[r]["norm"][0])
+    assert out[0]["max_dev"] < 2e-3 * max(1.0, out[0]["max_ref"]), out[0]["max_dev"]
