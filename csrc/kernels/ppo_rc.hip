@@ -96,9 +96,21 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// sc1 (L1-bypassing, agent-coherent) 4-B accesses for the cross-workgroup hand-off.
-__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_sc1(float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// sc1 (L1-bypassing, agent-coherent) accesses for the cross-workgroup hand-off. The
+// 16-B forms are inline asm so that a lane can issue all G partial loads back to back
+// (relaxed atomic loads are 4-B and get serialised by the compiler); the results are
+// tied to the explicit vmcnt(0) wait through "+v" operands so no use moves above it.
+__device__ __forceinline__ void st_sc1_x4(float* p, f4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ f4 ld_sc1_x4(const float* p) {
+  f4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void wait_vm4(f4& a, f4& b, f4& c, f4& d) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
 __device__ __forceinline__ unsigned ld_sc1u(unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -650,9 +662,8 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       for (int it = 0; it < KI; ++it) {
         const int id = w + it * kWaves;
         if (id >= n_items) continue;
-        float* p = slab + ((size_t)grp * n_items + id) * 256 + lane * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) st_sc1(p + j, gg[it][j]);
+        const f4 v = {gg[it][0], gg[it][1], gg[it][2], gg[it][3]};
+        st_sc1_x4(slab + ((size_t)grp * n_items + id) * 256 + lane * 4, v);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -661,7 +672,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         const unsigned target = (unsigned)G * (unsigned)(k + 1);
         unsigned spins = 0;
         while (ld_sc1u(arrive) < target) {
-          __builtin_amdgcn_s_sleep(2);
+          __builtin_amdgcn_s_sleep(1);
           if (++spins > (1u << 22) || ld_sc1u(tflag) != 0u) {
             atomicOr(tflag, 1u);
             break;
@@ -673,14 +684,24 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       for (int it = 0; it < KI; ++it) {
         const int id = w + it * kWaves;
         if (id >= n_items) continue;
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int gi = 0; gi < G; ++gi) {
-          float* p = slab + ((size_t)gi * n_items + id) * 256 + lane * 4;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) s[j] += ld_sc1(p + j);
+        f4 s = {0.f, 0.f, 0.f, 0.f};
+        const float* p = slab + (size_t)id * 256 + lane * 4;
+        const size_t gs = (size_t)n_items * 256;
+        for (int gi = 0; gi < G; gi += 4) {  // G is 1, 2, 4, 8 or 16 .. any count: tail lanes read group 0
+          f4 v0 = ld_sc1_x4(p + (size_t)gi * gs);
+          f4 v1 = ld_sc1_x4(p + (size_t)(gi + 1 < G ? gi + 1 : 0) * gs);
+          f4 v2 = ld_sc1_x4(p + (size_t)(gi + 2 < G ? gi + 2 : 0) * gs);
+          f4 v3 = ld_sc1_x4(p + (size_t)(gi + 3 < G ? gi + 3 : 0) * gs);
+          wait_vm4(v0, v1, v2, v3);
+          s += v0;
+          if (gi + 1 < G) s += v1;
+          if (gi + 2 < G) s += v2;
+          if (gi + 3 < G) s += v3;
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gg[it][j] = s[j];
+        gg[it][0] = s.x;
+        gg[it][1] = s.y;
+        gg[it][2] = s.z;
+        gg[it][3] = s.w;
       }
     }
     // entropy term of log_std (d(-ent_coef * H)/d log_std = -ent_coef), once per minibatch; |g|^2
