@@ -21,3 +21,4 @@ void register_envs(py::module& m);
 void register_kernels(py::module& m);
 void register_engine(py::module& m);
 void register_disc(py::module& m);
+void register_conv(py::module& m);

@@ -8,4 +8,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_kernels(m);
   register_engine(m);
   register_disc(m);
+  register_conv(m);
 }

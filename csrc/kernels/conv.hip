@@ -1,0 +1,417 @@
+// NHWC implicit-GEMM convolutions on CDNA4 MFMA (bf16 operands, fp32 accumulate) for the
+// NatureCNN trunk of the Atari policies (SB3 NatureCNN used via the reference's
+// `cnn_policy`, scripts/ingredients/policy.py:48-50; DAgger-Pong, BASELINE config 4) and
+// the reward CNNs (reward_nets.py:535-600 via util/networks.py:286-357 build_cnn).
+//
+// Frames arrive channel-last from the native Atari env ([B, 84, 84, 4]), so every kernel
+// works on NHWC and the GEMM contraction index k = (kh, kw, c) has c fastest: for a fixed
+// kh the KW*C taps of a row are CONTIGUOUS in memory. One MFMA operand fragment is 8
+// consecutive k (v_mfma_f32_16x16x32_bf16: lane l holds A[m = l&15][k = 8*(l>>4) + j]),
+// i.e. one 16-byte (bf16) / 32-byte (fp32) load straight from the activation tensor -- the
+// forward and the data-gradient kernels need no LDS staging and no barrier at all:
+//
+//   conv_fwd    Y[m][n]  = act(sum_k X(m, k) W[n][k] + b[n])            m = (b, oh, ow)
+//   conv_dgrad  dZp[p][c] = [Xp > 0] * sum_{tap, n} dZ(p, tap)[n] Wt[c][tap][n]   p = (b, ih, iw)
+//                (the stride-S taps that do not hit p are skipped per wave with a ballot)
+//   conv_wgrad  dW[n][k] = sum_m dZ[m][n] X(m, k),  db[n] = sum_m dZ[m][n]
+//                (contraction over m needs m-contiguous operands: 32-row chunks of dZ and
+//                of the im2col rows are staged transposed in LDS; each block reduces a
+//                contiguous m range into fp32 partials, conv_reduce sums them in block
+//                order -- deterministic, no atomics)
+//
+// dZ = dY * [Y > 0] (ReLU of the layer's own output) is formed on load when relu_out is
+// set, so no separate mask kernel runs.
+#include <hip/hip_runtime.h>
+
+#include "ia/mfma.h"
+#include "launchers.h"
+
+namespace ia {
+namespace {
+
+constexpr int kLdT = 40;  // LDS row stride (bf16) of the transposed 32-row chunks: 80 B
+
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
+  return z;
+}
+
+// 8 consecutive input elements -> bf16x8 (scaled)
+__device__ __forceinline__ bf16x8 load8(const bf16* p, float) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ bf16x8 load8(const float* p, float s) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  bf16x8 v;
+  v[0] = (bf16)(a.x * s); v[1] = (bf16)(a.y * s); v[2] = (bf16)(a.z * s); v[3] = (bf16)(a.w * s);
+  v[4] = (bf16)(b.x * s); v[5] = (bf16)(b.y * s); v[6] = (bf16)(b.z * s); v[7] = (bf16)(b.w * s);
+  return v;
+}
+__device__ __forceinline__ bf16x8 load8(const uint8_t* p, float s) {
+  const uint32_t a = *reinterpret_cast<const uint32_t*>(p);
+  const uint32_t b = *reinterpret_cast<const uint32_t*>(p + 4);
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = (bf16)((float)((a >> (8 * j)) & 0xffu) * s);
+    v[4 + j] = (bf16)((float)((b >> (8 * j)) & 0xffu) * s);
+  }
+  return v;
+}
+
+// dZ fragment of 8 consecutive channels: dY * [Y > 0] when relu_out
+__device__ __forceinline__ bf16x8 load_dz8(const bf16* dY, const bf16* Y, size_t off, int relu_out) {
+  bf16x8 d = *reinterpret_cast<const bf16x8*>(dY + off);
+  if (relu_out) {
+    const bf16x8 y = *reinterpret_cast<const bf16x8*>(Y + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!((float)y[j] > 0.f)) d[j] = (bf16)0.f;
+  }
+  return d;
+}
+
+// ------------------------------------------------------------------ forward
+template <typename TIn, int NT>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X, const bf16* __restrict__ Wb,
+                                                       const float* __restrict__ bias, bf16* __restrict__ Y, ConvGeo g,
+                                                       float in_scale, int relu) {
+  const int l = threadIdx.x & 63;
+  const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  const int OHW = g.OH * g.OW;
+  const int M = g.B * OHW;
+  if (m0 >= M) return;
+  const int K = g.KH * g.KW * g.C;
+  const int rowlen = g.KW * g.C;
+  const int r = l & 15, kq = (l >> 4) * 8;
+  const int m = m0 + r;
+  const bool mv = m < M;
+  const int mm = mv ? m : M - 1;
+  const int b = mm / OHW, pix = mm - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
+  const TIn* xb = X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C;
+  const size_t xrow = (size_t)g.W * g.C;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = zero4();
+  const bf16* wr = Wb + (size_t)r * K + kq;
+#pragma unroll 2
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    const int k = k0 + kq;
+    const int kh = k / rowlen, off = k - kh * rowlen;
+    bf16x8 av = load8(xb + kh * xrow + off, in_scale);
+    if (!mv) av = zero8();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * K + k0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
+    }
+  }
+  const int col = l & 15;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n = t * 16 + col;
+    const float bb = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + 4 * (l >> 4) + i;
+      if (row < M) {
+        float v = acc[t][i] + bb;
+        if (relu) v = fmaxf(v, 0.f);
+        Y[(size_t)row * g.N + n] = (bf16)v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ data gradient
+template <int CT>
+__global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
+                                                         const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
+                                                         bf16* __restrict__ dZp, ConvGeo g, int relu_out, int relu_in) {
+  const int l = threadIdx.x & 63;
+  const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  const int HW = g.H * g.W;
+  const int P = g.B * HW;
+  if (p0 >= P) return;
+  const int Kp = g.KH * g.KW * g.N;
+  const int r = l & 15, kq = (l >> 4) * 8;
+  const int p = p0 + r;
+  const bool pv = p < P;
+  const int pp = pv ? p : P - 1;
+  const int b = pp / HW, pix = pp - b * HW, ih = pix / g.W, iw = pix - ih * g.W;
+  f32x4 acc[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) acc[t] = zero4();
+  const bf16* wr = Wt + (size_t)r * Kp + kq;
+  for (int k0 = 0; k0 < Kp; k0 += 32) {
+    const int tap = k0 / g.N, n0 = k0 - tap * g.N;
+    const int kh = tap / g.KW, kw = tap - kh * g.KW;
+    const int ohn = ih - kh, own = iw - kw;
+    const int oh = ohn / g.S, ow = own / g.S;
+    const bool valid = pv && ohn >= 0 && own >= 0 && oh * g.S == ohn && ow * g.S == own && oh < g.OH && ow < g.OW;
+    if (__ballot(valid) == 0ull) continue;  // this tap misses all 16 pixels of the tile
+    bf16x8 av = zero8();
+    if (valid) av = load_dz8(dY, Y, ((size_t)(b * g.OH + oh) * g.OW + ow) * g.N + n0 + kq, relu_out);
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * Kp + k0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
+    }
+  }
+  const int col = l & 15;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int c = t * 16 + col;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = p0 + 4 * (l >> 4) + i;
+      if (row < P) {
+        float v = acc[t][i];
+        if (relu_in && !((float)Xp[(size_t)row * g.C + c] > 0.f)) v = 0.f;
+        dZp[(size_t)row * g.C + c] = (bf16)v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ weight gradient (partials)
+// 512 threads; wave w owns output tiles t = w + 8 i (t = nt * KT + kt), TPW >= ceil(NT*KT/8).
+template <typename TIn, int NT, int TPW>
+__global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__ X, const bf16* __restrict__ dY,
+                                                         const bf16* __restrict__ Y, float* __restrict__ slab, ConvGeo g,
+                                                         float in_scale, int relu_out, int m_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int K = g.KH * g.KW * g.C;
+  bf16* At = reinterpret_cast<bf16*>(smem);  // [K][kLdT]   im2col chunk, m contiguous
+  bf16* Zt = At + (size_t)K * kLdT;          // [N][kLdT]   dZ chunk, m contiguous
+  const int OHW = g.OH * g.OW;
+  const int M = g.B * OHW;
+  const int N = g.N;
+  const int KT = K / 16;
+  const int n_tiles = NT * KT;
+  const int rowlen = g.KW * g.C;
+  const size_t xrow = (size_t)g.W * g.C;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int mb = blockIdx.x * m_per_block;
+  const int me = min(M, mb + m_per_block);
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc[i] = zero4();
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // bias partials of the (n, m_local) items this thread stages
+  for (int c0 = mb; c0 < me; c0 += 32) {
+    // stage the im2col chunk transposed: item (k-group kg, m_local)
+    for (int it = threadIdx.x; it < (K / 8) * 32; it += 512) {
+      const int ml = it & 31, kg = it >> 5;
+      const int m = c0 + ml;
+      bf16x8 v = zero8();
+      if (m < me) {
+        const int b = m / OHW, pix = m - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
+        const int k = kg * 8, kh = k / rowlen, off = k - kh * rowlen;
+        v = load8(X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C + kh * xrow + off, in_scale);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) At[(size_t)(kg * 8 + j) * kLdT + ml] = v[j];
+    }
+    // stage dZ transposed: item (n, m_local)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int it = threadIdx.x + 512 * j;
+      if (it < N * 32) {
+        const int ml = it & 31, n = it >> 5;
+        const int m = c0 + ml;
+        float z = 0.f;
+        if (m < me) {
+          z = (float)dY[(size_t)m * N + n];
+          if (relu_out && !((float)Y[(size_t)m * N + n] > 0.f)) z = 0.f;
+        }
+        const bf16 zb = (bf16)z;
+        Zt[n * kLdT + ml] = zb;
+        bsum[j] += (float)zb;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const int t = w + 8 * i;
+      if (t < n_tiles) {
+        const int nt = t / KT, kt = t - nt * KT;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Zt + (nt * 16 + (l & 15)) * kLdT + (l >> 4) * 8);
+        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(At + (size_t)(kt * 16 + (l & 15)) * kLdT + (l >> 4) * 8);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[i], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // partial dW [N][K] then db [N] of this block
+  float* out = slab + (size_t)blockIdx.x * ((size_t)N * K + N);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = w + 8 * i;
+    if (t < n_tiles) {
+      const int nt = t / KT, kt = t - nt * KT;
+      const int k = kt * 16 + (l & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[(size_t)(nt * 16 + 4 * (l >> 4) + q) * K + k] = acc[i][q];
+    }
+  }
+  // bias: the 32 m_local items of one n are 32 consecutive threads (half a wave)
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float v = bsum[j];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 16);
+    const int it = threadIdx.x + 512 * j;
+    if ((threadIdx.x & 31) == 0 && it < N * 32) red[it >> 5] = v;
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < N; n += 512) out[(size_t)N * K + n] = red[n];
+}
+
+__global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restrict__ slab, int nblk, int len,
+                                                          float* __restrict__ dW, float* __restrict__ db, int nk) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += slab[(size_t)b * len + i];
+  if (i < nk) dW[i] = s;
+  else if (db) db[i - nk] = s;
+}
+
+template <typename TIn>
+hipError_t launch_fwd(const TIn* X, const bf16* Wb, const float* bias, bf16* Y, const ConvGeo& g, float scale, int relu,
+                      hipStream_t s) {
+  const int M = g.B * g.OH * g.OW;
+  const dim3 grid((M + 63) / 64), block(256);
+  switch (g.N / 16) {
+    case 1: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 1>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
+    case 2: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 2>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
+    case 4: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 4>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <typename TIn, int NT>
+hipError_t launch_wgrad_nt(const TIn* X, const bf16* dY, const bf16* Y, float* slab, const ConvGeo& g, float scale,
+                           int relu_out, int nblk, int mpb, hipStream_t s) {
+  const int K = g.KH * g.KW * g.C;
+  const int tiles = NT * (K / 16);
+  const size_t lds = ((size_t)K * kLdT + (size_t)g.N * kLdT) * sizeof(bf16);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const int tpw = (tiles + 7) / 8;
+  if (tpw <= 4)
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 4>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+  else if (tpw <= 8)
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 8>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+  else if (tpw <= 12)
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 12>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+  else if (tpw <= 18)
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 18>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+template <typename TIn>
+hipError_t launch_wgrad(const TIn* X, const bf16* dY, const bf16* Y, float* slab, float* dW, float* db, const ConvGeo& g,
+                        float scale, int relu_out, hipStream_t s) {
+  const int M = g.B * g.OH * g.OW;
+  int nblk = 0, mpb = 0;
+  conv_wgrad_blocks(g, &nblk, &mpb);
+  hipError_t e;
+  switch (g.N / 16) {
+    case 1: e = launch_wgrad_nt<TIn, 1>(X, dY, Y, slab, g, scale, relu_out, nblk, mpb, s); break;
+    case 2: e = launch_wgrad_nt<TIn, 2>(X, dY, Y, slab, g, scale, relu_out, nblk, mpb, s); break;
+    case 4: e = launch_wgrad_nt<TIn, 4>(X, dY, Y, slab, g, scale, relu_out, nblk, mpb, s); break;
+    default: return hipErrorInvalidValue;
+  }
+  if (e != hipSuccess) return e;
+  (void)M;
+  const int K = g.KH * g.KW * g.C;
+  const int len = g.N * K + g.N;
+  hipLaunchKernelGGL(conv_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, s, slab, nblk, len, dW, db, g.N * K);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool conv_geo_ok(const ConvGeo& g) {
+  const int K = g.KH * g.KW * g.C;
+  if (g.B <= 0 || g.OH <= 0 || g.OW <= 0) return false;
+  if ((g.OH - 1) * g.S + g.KH > g.H || (g.OW - 1) * g.S + g.KW > g.W) return false;
+  if (K % 32 != 0 || (g.KW * g.C) % 8 != 0) return false;
+  if (g.N % 16 != 0 || g.N > 64) return false;
+  return true;
+}
+
+void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* mpb) {
+  const int M = g.B * g.OH * g.OW;
+  const int chunks = (M + 31) / 32;
+  const int K = g.KH * g.KW * g.C;
+  // fp32 partial traffic (nblk x N x K) vs parallelism: fewer blocks for the big-K layers
+  const int cap = K * g.N >= 16384 ? 64 : 128;
+  int b = chunks < cap ? chunks : cap;
+  const int cpb = (chunks + b - 1) / b;
+  b = (chunks + cpb - 1) / cpb;
+  *nblk = b;
+  *mpb = cpb * 32;
+}
+
+size_t conv_wgrad_slab_floats(const ConvGeo& g) {
+  int nblk = 0, mpb = 0;
+  conv_wgrad_blocks(g, &nblk, &mpb);
+  const int K = g.KH * g.KW * g.C;
+  return (size_t)nblk * ((size_t)g.N * K + g.N);
+}
+
+hipError_t conv_forward(int in_kind, const void* X, const void* Wb, const float* bias, void* Y, const ConvGeo& g,
+                        float in_scale, int relu, hipStream_t s) {
+  if (!conv_geo_ok(g)) return hipErrorInvalidValue;
+  const bf16* w = static_cast<const bf16*>(Wb);
+  bf16* y = static_cast<bf16*>(Y);
+  switch (in_kind) {
+    case 0: return launch_fwd(static_cast<const float*>(X), w, bias, y, g, in_scale, relu, s);
+    case 1: return launch_fwd(static_cast<const bf16*>(X), w, bias, y, g, in_scale, relu, s);
+    case 2: return launch_fwd(static_cast<const uint8_t*>(X), w, bias, y, g, in_scale, relu, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y, float* slab, float* dW, float* db,
+                      const ConvGeo& g, float in_scale, int relu_out, hipStream_t s) {
+  if (!conv_geo_ok(g)) return hipErrorInvalidValue;
+  const bf16* dy = static_cast<const bf16*>(dY);
+  const bf16* y = static_cast<const bf16*>(Y);
+  switch (in_kind) {
+    case 0: return launch_wgrad(static_cast<const float*>(X), dy, y, slab, dW, db, g, in_scale, relu_out, s);
+    case 1: return launch_wgrad(static_cast<const bf16*>(X), dy, y, slab, dW, db, g, in_scale, relu_out, s);
+    case 2: return launch_wgrad(static_cast<const uint8_t*>(X), dy, y, slab, dW, db, g, in_scale, relu_out, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
+                      int relu_out, int relu_in, hipStream_t s) {
+  if (!conv_geo_ok(g) || g.N % 32 != 0 || g.C % 16 != 0 || g.C > 64) return hipErrorInvalidValue;
+  const int P = g.B * g.H * g.W;
+  const dim3 grid((P + 63) / 64), block(256);
+  const bf16* dy = static_cast<const bf16*>(dY);
+  const bf16* y = static_cast<const bf16*>(Y);
+  const bf16* wt = static_cast<const bf16*>(Wt);
+  const bf16* xp = static_cast<const bf16*>(Xp);
+  bf16* dz = static_cast<bf16*>(dZp);
+  switch (g.C / 16) {
+    case 1: hipLaunchKernelGGL((conv_dgrad_kernel<1>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); break;
+    case 2: hipLaunchKernelGGL((conv_dgrad_kernel<2>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); break;
+    case 4: hipLaunchKernelGGL((conv_dgrad_kernel<4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace ia

@@ -93,4 +93,23 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s);
 size_t ppo_lds_bytes(const PPOArgs& a);
 hipError_t ppo_launch(const PPOArgs& a, hipStream_t s);
 
+// ---- conv.hip: NHWC implicit-GEMM convolutions (NatureCNN / reward CNN), bf16 MFMA
+struct ConvGeo {
+  int B, H, W, C;  // input NHWC
+  int KH, KW, S;   // kernel, stride (valid padding)
+  int OH, OW, N;   // output NHWC
+};
+bool conv_geo_ok(const ConvGeo& g);
+void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* m_per_block);
+size_t conv_wgrad_slab_floats(const ConvGeo& g);
+// in_kind: 0 fp32, 1 bf16, 2 uint8 input; weights bf16 [N][KH][KW][C]; Y bf16 [B*OH*OW][N]
+hipError_t conv_forward(int in_kind, const void* X, const void* Wb, const float* bias, void* Y, const ConvGeo& g,
+                        float in_scale, int relu, hipStream_t s);
+// dW fp32 [N][KH][KW][C], db fp32 [N] (may be null); slab of conv_wgrad_slab_floats
+hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y, float* slab, float* dW, float* db,
+                      const ConvGeo& g, float in_scale, int relu_out, hipStream_t s);
+// dZp bf16 [B*H*W][C] = [Xp > 0] * conv^T(dY * [Y > 0]); Wt bf16 [C][KH][KW][N]
+hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
+                      int relu_out, int relu_in, hipStream_t s);
+
 }  // namespace ia

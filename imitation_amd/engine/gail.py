@@ -473,8 +473,10 @@ class DeviceGAIL(GAIL):
             "dones": self.buf["dones"].reshape(rows).index_select(0, keep).bool(),
         })
         local_lens = list(ep_lens)
-        if pdist.world_size() > 1:
-            ep_lens = [l for part in pdist.all_gather_object(ep_lens) for l in part]
+        if pdist.world_size() > 1 and not self.allow_variable_horizon:
+            # global horizon set == {global min, global max}: one 2-float MIN all-reduce
+            lo, neg_hi = pdist.allreduce_scalars([min(ep_lens, default=2**31), -max(ep_lens, default=-1)], op="min")
+            ep_lens = [] if lo > -neg_hi else sorted({int(lo), int(-neg_hi)})
         self._check_fixed_horizon(ep_lens)
         # Monitor-style episode stats for the generator logger
         if finished:

@@ -1,0 +1,109 @@
+"""Conv+ReLU stacks on the NHWC implicit-GEMM HIP kernels (``csrc/kernels/conv.hip``).
+
+The NatureCNN trunk of the Atari policies (SB3 ``NatureCNN``, selected by the
+reference's ``cnn_policy`` named config, ``src/imitation/scripts/ingredients/policy.py:48-50``;
+DAgger-Pong in BASELINE.json) is three valid-padding conv+ReLU layers. ``conv_stack``
+runs them as one autograd node:
+
+* forward: one MFMA kernel per layer (bias + ReLU fused), activations kept NHWC bf16;
+* backward: per layer one weight-gradient kernel (+ a deterministic block reduction)
+  and, below the top layer, one data-gradient kernel whose epilogue applies the
+  previous layer's ReLU mask -- no separate mask / transpose / im2col launches.
+
+Numerics: bf16 operands, fp32 accumulation (weights are fp32 module parameters,
+rounded to bf16 per call). ``conv_stack_reference`` is the fp32 PyTorch oracle.
+"""
+
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from imitation_amd import ops
+
+
+def conv_stack_reference(x_nhwc: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor],
+                         strides: Sequence[int], in_scale: float = 1.0) -> torch.Tensor:
+    """fp32 reference: NHWC in, NHWC out (ReLU after every layer)."""
+    x = x_nhwc.float().permute(0, 3, 1, 2) * in_scale
+    for w, b, s in zip(weights, biases, strides):
+        x = F.relu(F.conv2d(x, w, b, stride=s))
+    return x.permute(0, 2, 3, 1)
+
+
+def supported(x_shape, weights: Sequence[torch.Tensor], strides: Sequence[int]) -> bool:
+    """Whether the kernel path covers this stack (valid padding, channel/tile constraints)."""
+    if len(x_shape) != 4:
+        return False
+    _, H, W, C = x_shape
+    for i, (w, s) in enumerate(zip(weights, strides)):
+        N, Cw, KH, KW = w.shape
+        if Cw != C or N % 16 != 0 or N > 64 or (KH * KW * C) % 32 != 0 or (KW * C) % 8 != 0:
+            return False
+        if i > 0 and (C % 16 != 0 or C > 64):
+            return False
+        if i + 1 < len(weights) and N % 32 != 0:  # dgrad of the next layer walks taps in 32-wide k-steps
+            return False
+        OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+        if OH <= 0 or OW <= 0:
+            return False
+        H, W, C = OH, OW, N
+    return True
+
+
+class _ConvStack(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, in_scale, strides, *params):
+        C = ops.native()
+        ws, bs = params[0::2], params[1::2]
+        acts: List[torch.Tensor] = []
+        h = x
+        for i, (w, b, s) in enumerate(zip(ws, bs, strides)):
+            wb = w.detach().permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+            h = C.conv_fwd(h, wb, b.detach().float().contiguous(), int(s), float(in_scale) if i == 0 else 1.0, True)
+            acts.append(h)
+        ctx.save_for_backward(x, *ws, *acts)
+        ctx.in_scale = float(in_scale)
+        ctx.strides = tuple(int(s) for s in strides)
+        ctx.n = len(ws)
+        return h.float()
+
+    @staticmethod
+    def backward(ctx, gy):
+        C = ops.native()
+        n = ctx.n
+        saved = ctx.saved_tensors
+        x, ws, acts = saved[0], saved[1 : 1 + n], saved[1 + n :]
+        grads = [None] * (2 * n)
+        dz = gy.contiguous().to(torch.bfloat16)
+        for i in range(n - 1, -1, -1):
+            w, s = ws[i], ctx.strides[i]
+            N, Cin, KH, KW = w.shape
+            inp = x if i == 0 else acts[i - 1]
+            top = i == n - 1  # only the top layer's ReLU mask is still pending on dz
+            scale = ctx.in_scale if i == 0 else 1.0
+            dW, db = C.conv_wgrad(inp, dz, acts[i], int(KH), int(KW), int(s), scale, top)
+            grads[2 * i] = dW.permute(0, 3, 1, 2).contiguous().to(w.dtype)
+            grads[2 * i + 1] = db
+            if i > 0:
+                wt = w.detach().permute(1, 2, 3, 0).contiguous().to(torch.bfloat16)
+                dz = C.conv_dgrad(dz, acts[i], wt, acts[i - 1], int(s), top, True)
+        return (None, None, None, *grads)
+
+
+def conv_stack(x_nhwc: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor],
+               strides: Sequence[int], in_scale: float = 1.0) -> torch.Tensor:
+    """ReLU(conv) x len(weights) over an NHWC input; returns fp32 NHWC.
+
+    GPU tensors run the HIP kernels (raising if the extension is missing); CPU tensors
+    and ``IMITATION_AMD_FUSED=0`` use :func:`conv_stack_reference`. The input gets no
+    gradient (it is observation data).
+    """
+    if not ops.use_kernel(x_nhwc) or not supported(tuple(x_nhwc.shape), weights, strides):
+        return conv_stack_reference(x_nhwc, weights, biases, strides, in_scale)
+    params = []
+    for w, b in zip(weights, biases):
+        params += [w, b]
+    return _ConvStack.apply(x_nhwc.contiguous(), float(in_scale), tuple(int(s) for s in strides), *params)

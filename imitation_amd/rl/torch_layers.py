@@ -65,12 +65,15 @@ class NatureCNN(BaseFeaturesExtractor):
         self.linear = nn.Sequential(nn.Linear(n_flatten, features_dim), nn.ReLU())
 
     def forward(self, observations: th.Tensor) -> th.Tensor:
-        x = observations
-        if self.channels_last_input:
-            x = x.permute(0, 3, 1, 2)
-        if x.is_cuda:
-            x = x.contiguous(memory_format=th.channels_last)
-        return self.linear(self.cnn(x))
+        # conv trunk: NHWC implicit-GEMM MFMA kernels on GPU (ops/conv.py, csrc/kernels/conv.hip),
+        # fp32 reference on CPU; the module keeps SB3's state-dict layout (cnn.{0,2,4}, linear.0)
+        from imitation_amd.ops import conv as conv_ops
+
+        x = observations if self.channels_last_input else observations.permute(0, 2, 3, 1)
+        convs = [m for m in self.cnn if isinstance(m, nn.Conv2d)]
+        y = conv_ops.conv_stack(x, [c.weight for c in convs], [c.bias for c in convs], [c.stride[0] for c in convs])
+        y = y.permute(0, 3, 1, 2).reshape(y.shape[0], -1)  # nn.Flatten order (C, H, W)
+        return self.linear(y)
 
 
 class CombinedExtractor(BaseFeaturesExtractor):

@@ -1,0 +1,134 @@
+"""NHWC conv-stack kernels (csrc/kernels/conv.hip) vs the fp32 PyTorch reference."""
+
+import numpy as np
+import pytest
+import torch as th
+
+from imitation_amd.ops import conv as conv_ops
+
+NATURE = [((32, 4, 8, 8), 4), ((64, 32, 4, 4), 2), ((64, 64, 3, 3), 1)]
+
+
+def _params(seed, layers=NATURE, device="cpu"):
+    g = th.Generator().manual_seed(seed)
+    ws, bs, ss = [], [], []
+    for shape, s in layers:
+        fan_in = shape[1] * shape[2] * shape[3]
+        ws.append((th.randn(shape, generator=g) * (2.0 / fan_in) ** 0.5).to(device).requires_grad_(True))
+        bs.append((0.05 * th.randn(shape[0], generator=g)).to(device).requires_grad_(True))
+        ss.append(s)
+    return ws, bs, ss
+
+
+def test_supported_shapes():
+    ws, _, ss = _params(0)
+    assert conv_ops.supported((2, 84, 84, 4), ws, ss)
+    assert not conv_ops.supported((2, 84, 84, 3), [th.zeros(32, 3, 3, 3)], [1])  # K = 27 not a multiple of 32
+    assert not conv_ops.supported((2, 84, 84, 3), ws, ss)  # channel mismatch
+    assert not conv_ops.supported((2, 84, 84, 4), [th.zeros(24, 4, 8, 8)], [4])  # N % 16
+
+
+def test_cpu_path_is_reference():
+    ws, bs, ss = _params(1)
+    x = th.rand(2, 84, 84, 4)
+    y = conv_ops.conv_stack(x, ws, bs, ss)
+    assert y.shape == (2, 7, 7, 64)
+    th.testing.assert_close(y, conv_ops.conv_stack_reference(x, ws, bs, ss))
+
+
+def test_nature_cnn_matches_sequential_on_cpu():
+    from imitation_amd.envs import spaces
+    from imitation_amd.rl.torch_layers import NatureCNN
+
+    space = spaces.Box(0, 255, (84, 84, 4), np.uint8)
+    th.manual_seed(0)
+    net = NatureCNN(space)
+    x = th.rand(3, 84, 84, 4)
+    ref = net.linear(net.cnn(x.permute(0, 3, 1, 2)))
+    th.testing.assert_close(net(x), ref, rtol=1e-5, atol=1e-5)
+
+
+def _bf(t):
+    return t.to(th.bfloat16).float()
+
+
+def _bf16_emulated(x, ws, bs, ss, gy):
+    """fp32 PyTorch with the kernels' bf16 rounding points (operands, stored activations, dZ):
+    isolates kernel errors from the bf16 precision choice itself."""
+    import torch.nn.functional as F
+    from torch.nn import grad as nng
+
+    h, inputs, acts = _bf(x.permute(0, 3, 1, 2)), [], []
+    for w, b, s in zip(ws, bs, ss):
+        inputs.append(h)
+        h = _bf(F.relu(F.conv2d(h, _bf(w), b, stride=s)))
+        acts.append(h)
+    dz = _bf(gy.permute(0, 3, 1, 2)) * (acts[-1] > 0)
+    gws, gbs = [None] * len(ws), [None] * len(ws)
+    for i in range(len(ws) - 1, -1, -1):
+        dzb = _bf(dz)
+        gws[i] = nng.conv2d_weight(inputs[i], ws[i].shape, dzb, stride=ss[i])
+        gbs[i] = dzb.sum((0, 2, 3))
+        if i > 0:
+            dz = _bf(nng.conv2d_input(inputs[i].shape, _bf(ws[i]), dzb, stride=ss[i]) * (acts[i - 1] > 0))
+    return acts[-1].permute(0, 2, 3, 1), gws + gbs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 3, 16, 64])
+def test_conv_stack_forward_backward_matches_reference(B):
+    ws, bs, ss = _params(2, device="cuda")
+    x = th.rand(B, 84, 84, 4, device="cuda")
+    y = conv_ops.conv_stack(x, ws, bs, ss)
+    ref = conv_ops.conv_stack_reference(x, ws, bs, ss).detach()
+    assert y.shape == ref.shape == (B, 7, 7, 64)
+    gy = th.randn_like(ref)
+    grads = th.autograd.grad((y * gy).sum(), ws + bs)
+    ref_grads = th.autograd.grad((conv_ops.conv_stack_reference(x, ws, bs, ss) * gy).sum(), ws + bs)
+    with th.no_grad():
+        ye, emu = _bf16_emulated(x, [w.detach() for w in ws], [b.detach() for b in bs], ss, gy)
+    # exact w.r.t. the bf16 rounding points
+    assert float((y - ye).norm() / ye.norm()) < 2e-3
+    for g, e in zip(grads, emu):
+        assert g.shape == e.shape
+        assert float((g - e).norm() / (e.norm() + 1e-12)) < 1e-2
+    # and close to fp32: the forward to bf16 precision; gradients of a random-sign loss are
+    # dominated by the few ReLU masks that flip under bf16 (cancelling sums), so cosine
+    assert float((y - ref).norm() / ref.norm()) < 1e-2
+    for g, r in zip(grads, ref_grads):
+        cos = float((g * r).sum() / (g.norm() * r.norm() + 1e-12))
+        assert cos > 0.99, cos
+
+
+@pytest.mark.gpu
+def test_conv_kernels_loaded_and_deterministic():
+    from imitation_amd import ops
+
+    C = ops.native()
+    assert hasattr(C, "conv_fwd") and hasattr(C, "conv_wgrad") and hasattr(C, "conv_dgrad")
+    ws, bs, ss = _params(3, device="cuda")
+    x = th.rand(8, 84, 84, 4, device="cuda")
+    out = []
+    for _ in range(2):
+        y = conv_ops.conv_stack(x, ws, bs, ss)
+        out.append(th.autograd.grad(y.square().sum(), ws))
+    for a, b in zip(*out):
+        assert th.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_nature_cnn_policy_bc_step_on_gpu():
+    """ActorCriticCnnPolicy (NatureCNN on the HIP kernels) evaluate_actions + backward on Pong frames."""
+    from imitation_amd.envs import spaces
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+
+    obs_space = spaces.Box(0, 255, (84, 84, 4), np.uint8)
+    act_space = spaces.Discrete(6)
+    pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
+    obs = th.randint(0, 256, (32, 84, 84, 4), device="cuda", dtype=th.uint8)
+    acts = th.randint(0, 6, (32,), device="cuda")
+    _, logp, ent = pol.evaluate_actions(obs, acts)
+    loss = -logp.mean() - 1e-3 * ent.mean()
+    loss.backward()
+    g = [p.grad for p in pol.features_extractor.cnn.parameters()]
+    assert all(x is not None and th.isfinite(x).all() and float(x.abs().sum()) > 0 for x in g)

@@ -1,0 +1,51 @@
+"""Time the replicated data-parallel PPO update of the GAIL-HalfCheetah bench config on ONE GPU.
+
+At world size W every rank runs the register-chained kernel over the all-gathered rows
+(W x 4096) with minibatch W x 64 (G = W cooperating workgroups): emulated here with
+8W envs x 512 steps and batch 64W. Prints ms per PPO update for W = 1, 2, 4, 8.
+"""
+import sys
+import time
+
+import numpy as np
+import torch as th
+
+sys.path.insert(0, ".")
+
+
+def main():
+    from imitation_amd.data import rollout
+    from imitation_amd.engine.gail import DeviceGAIL
+    from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
+    from imitation_amd.rewards.reward_nets import BasicRewardNet, NormalizedRewardNet
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.util import logger
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    for W in (1, 2, 4, 8):
+        rng = np.random.default_rng(0)
+        venv = make_vec_env("seals/HalfCheetah-v1", rng=rng, n_envs=8 * W)
+        demo_env = make_vec_env("seals/HalfCheetah-v1", rng=np.random.default_rng(7), n_envs=4)
+        demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
+        gen = PPO(FeedForward32Policy, venv, n_steps=512, batch_size=64 * W, n_epochs=5, device="cuda",
+                  policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+        rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
+        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, venv=venv, gen_algo=gen, reward_net=rn,
+                        n_disc_updates_per_round=1, custom_logger=logger.configure("/tmp/ia_probe", format_strs=[]))
+        path = tr._C.engine_ppo_path(tr._ppo_static)
+        tr._rollout()
+        for _ in range(2):
+            tr._ppo_update()
+        th.cuda.synchronize()
+        n = 5
+        t0 = time.perf_counter()
+        for _ in range(n):
+            tr._ppo_update()
+        th.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        print(f"W={W} path={path} rows={tr.T * tr.N} batch={64 * W}: ppo update {1e3 * dt:.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
