@@ -12,7 +12,8 @@
 //
 //   conv_fwd    Y[m][n]  = act(sum_k X(m, k) W[n][k] + b[n])            m = (b, oh, ow)
 //   conv_dgrad  dZp[p][c] = [Xp > 0] * sum_{tap, n} dZ(p, tap)[n] Wt[c][tap][n]   p = (b, ih, iw)
-//                (the stride-S taps that do not hit p are skipped per wave with a ballot)
+//                (tiles hold pixels of one stride phase, which only the KH*KW/S^2 taps of that
+//                phase reach; border misses are skipped per wave with a ballot)
 //   conv_wgrad  dW[n][k] = sum_m dZ[m][n] X(m, k),  db[n] = sum_m dZ[m][n]
 //                (contraction over m needs m-contiguous operands: 32-row chunks of dZ and
 //                of the im2col rows are staged transposed in LDS; each block reduces a
@@ -125,52 +126,70 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
 }
 
 // ------------------------------------------------------------------ data gradient
+// Pixels are grouped by stride phase (ih % S, iw % S) (blockIdx.y): every pixel of a phase
+// is hit by the same kh = ph (mod S), kw = pw (mod S) taps, so a tile only walks those
+// (1/S^2 of KH*KW) and only the image border still masks rows.
 template <int CT>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
                                                          const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
                                                          bf16* __restrict__ dZp, ConvGeo g, int relu_out, int relu_in) {
   const int l = threadIdx.x & 63;
+  const int ph = blockIdx.y / g.S, pw = blockIdx.y - ph * g.S;
+  const int Hc = (g.H - ph + g.S - 1) / g.S, Wc = (g.W - pw + g.S - 1) / g.S;
+  const int HWc = Hc * Wc;
+  const int P = g.B * HWc;  // pixels of this phase
   const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-  const int HW = g.H * g.W;
-  const int P = g.B * HW;
   if (p0 >= P) return;
   const int Kp = g.KH * g.KW * g.N;
   const int r = l & 15, kq = (l >> 4) * 8;
+  auto pix_of = [&](int q, int& b, int& ih, int& iw) {
+    b = q / HWc;
+    const int rem = q - b * HWc, i = rem / Wc, j = rem - i * Wc;
+    ih = ph + g.S * i;
+    iw = pw + g.S * j;
+  };
   const int p = p0 + r;
   const bool pv = p < P;
-  const int pp = pv ? p : P - 1;
-  const int b = pp / HW, pix = pp - b * HW, ih = pix / g.W, iw = pix - ih * g.W;
+  int b, ih, iw;
+  pix_of(pv ? p : P - 1, b, ih, iw);
   f32x4 acc[CT];
 #pragma unroll
   for (int t = 0; t < CT; ++t) acc[t] = zero4();
   const bf16* wr = Wt + (size_t)r * Kp + kq;
-  for (int k0 = 0; k0 < Kp; k0 += 32) {
-    const int tap = k0 / g.N, n0 = k0 - tap * g.N;
-    const int kh = tap / g.KW, kw = tap - kh * g.KW;
-    const int ohn = ih - kh, own = iw - kw;
-    const int oh = ohn / g.S, ow = own / g.S;
-    const bool valid = pv && ohn >= 0 && own >= 0 && oh * g.S == ohn && ow * g.S == own && oh < g.OH && ow < g.OW;
-    if (__ballot(valid) == 0ull) continue;  // this tap misses all 16 pixels of the tile
-    bf16x8 av = zero8();
-    if (valid) av = load_dz8(dY, Y, ((size_t)(b * g.OH + oh) * g.OW + ow) * g.N + n0 + kq, relu_out);
+  for (int kh = ph; kh < g.KH; kh += g.S) {
+    const int oh = (ih - kh) / g.S;
+    const bool hv = ih >= kh && oh < g.OH;
+    for (int kw = pw; kw < g.KW; kw += g.S) {
+      const int ow = (iw - kw) / g.S;
+      const bool valid = pv && hv && iw >= kw && ow < g.OW;
+      if (__ballot(valid) == 0ull) continue;  // this tap misses all 16 pixels of the tile (border)
+      const size_t dzoff = ((size_t)(b * g.OH + oh) * g.OW + ow) * g.N + kq;
+      const int kbase = (kh * g.KW + kw) * g.N;
+      for (int n0 = 0; n0 < g.N; n0 += 32) {
+        bf16x8 av = zero8();
+        if (valid) av = load_dz8(dY, Y, dzoff + n0, relu_out);
 #pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * Kp + k0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
+        for (int t = 0; t < CT; ++t) {
+          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * Kp + kbase + n0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
+        }
+      }
     }
   }
   const int col = l & 15;
 #pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int c = t * 16 + col;
+  for (int i = 0; i < 4; ++i) {
+    const int q = p0 + 4 * (l >> 4) + i;
+    if (q >= P) continue;
+    int bb, hh, ww;
+    pix_of(q, bb, hh, ww);
+    const size_t row = ((size_t)bb * g.H + hh) * g.W + ww;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = p0 + 4 * (l >> 4) + i;
-      if (row < P) {
-        float v = acc[t][i];
-        if (relu_in && !((float)Xp[(size_t)row * g.C + c] > 0.f)) v = 0.f;
-        dZp[(size_t)row * g.C + c] = (bf16)v;
-      }
+    for (int t = 0; t < CT; ++t) {
+      const int c = t * 16 + col;
+      float v = acc[t][i];
+      if (relu_in && !((float)Xp[row * g.C + c] > 0.f)) v = 0.f;
+      dZp[row * g.C + c] = (bf16)v;
     }
   }
 }
@@ -354,7 +373,7 @@ void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* mpb) {
   const int chunks = (M + 31) / 32;
   const int K = g.KH * g.KW * g.C;
   // fp32 partial traffic (nblk x N x K) vs parallelism: fewer blocks for the big-K layers
-  const int cap = K * g.N >= 16384 ? 64 : 128;
+  const int cap = 256;  // one block per CU; fp32 partial traffic is nblk x N x K
   int b = chunks < cap ? chunks : cap;
   const int cpb = (chunks + b - 1) / b;
   b = (chunks + cpb - 1) / cpb;
@@ -398,8 +417,9 @@ hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y,
 hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
                       int relu_out, int relu_in, hipStream_t s) {
   if (!conv_geo_ok(g) || g.N % 32 != 0 || g.C % 16 != 0 || g.C > 64) return hipErrorInvalidValue;
-  const int P = g.B * g.H * g.W;
-  const dim3 grid((P + 63) / 64), block(256);
+  const int Hc = (g.H + g.S - 1) / g.S, Wc = (g.W + g.S - 1) / g.S;  // largest phase
+  const int P = g.B * Hc * Wc;
+  const dim3 grid((P + 63) / 64, g.S * g.S), block(256);
   const bf16* dy = static_cast<const bf16*>(dY);
   const bf16* y = static_cast<const bf16*>(Y);
   const bf16* wt = static_cast<const bf16*>(Wt);

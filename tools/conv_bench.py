@@ -8,7 +8,9 @@ import time
 import torch as th
 import torch.nn.functional as F
 
-sys.path.insert(0, ".")
+import os  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from imitation_amd.ops import conv as conv_ops  # noqa: E402
 
 LAYERS = [((32, 4, 8, 8), 4), ((64, 32, 4, 4), 2), ((64, 64, 3, 3), 1)]

@@ -5,8 +5,10 @@ import torch as th
 import torch.nn.functional as F
 from torch.nn import grad as nng
 
-sys.path.insert(0, ".")
-sys.path.insert(0, "tests/ops")
+import os  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "ops"))
 from imitation_amd.ops import conv as conv_ops  # noqa: E402
 from test_conv import _params  # noqa: E402
 

@@ -10,7 +10,9 @@ import time
 import numpy as np
 import torch as th
 
-sys.path.insert(0, ".")
+import os  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
