@@ -374,3 +374,4 @@ class SimpleDAggerTrainer(DAggerTrainer):
             self._logger.record("dagger/round_timestep_count", round_timestep_count)
             self.extend_and_update(bc_train_kwargs)
             round_num += 1
+        self.last_train_timesteps = total_timestep_count

@@ -115,7 +115,10 @@ class _TMLPFn(torch.autograd.Function):
         ctx.n_layers = len(ws)
         saved = [xc] + ws + bs
         if mean is not None:
-            saved += [mean, var]
+            # snapshot: a train-mode RunningNorm updates these buffers in place on its next
+            # call (e.g. the potential net of a shaped reward on s and then on s')
+            mv = torch.stack([mean, var])
+            saved += [mv[0], mv[1]]
         ctx.save_for_backward(*saved)
         return y
 
