@@ -42,12 +42,13 @@ def _to_jsonable(v: Any) -> Any:
 
 def _from_jsonable(v: Any) -> Any:
     if isinstance(v, dict):
-        if "py/tuple" in v:
+        # tags are only honoured in the exact form the encoder writes them
+        if len(v) == 1 and isinstance(v.get("py/tuple"), list):
             return tuple(_from_jsonable(x) for x in v["py/tuple"])
         if v.get("py/object") == "numpy.ndarray" and "values" in v:
             arr = np.asarray(_from_jsonable(v["values"]), dtype=v.get("dtype", None))
             return arr.reshape(v.get("shape", arr.shape))
-        if "py/float" in v:
+        if len(v) == 1 and isinstance(v.get("py/float"), str):
             return float(v["py/float"])
         return {k: _from_jsonable(x) for k, x in v.items()}
     if isinstance(v, list):
@@ -63,6 +64,31 @@ def decode_info(s: str) -> Any:
     return _from_jsonable(json.loads(s))
 
 
+def _list_scalar_to_numpy(val) -> np.ndarray:
+    """Rectangular nested Arrow list value -> ndarray straight from the Arrow buffers.
+
+    The datasets formatters materialise nested lists as Python objects first (minutes for
+    a few thousand 84x84x4 frames); flattening the child arrays level by level is a
+    buffer copy."""
+    import pyarrow as pa
+
+    arr = val.values
+    shape = [len(arr)]
+    while pa.types.is_list(arr.type) or pa.types.is_large_list(arr.type) or pa.types.is_fixed_size_list(arr.type):
+        if len(arr) == 0:
+            break
+        if pa.types.is_fixed_size_list(arr.type):
+            n = arr.type.list_size
+        else:
+            lens = arr.value_lengths().to_numpy(zero_copy_only=False)
+            n = int(lens[0])
+            if not (lens == n).all():
+                raise ValueError("ragged nested list")
+        shape.append(n)
+        arr = arr.flatten()
+    return arr.to_numpy(zero_copy_only=False).reshape(shape)
+
+
 class TrajectoryDatasetSequence(Sequence[types.Trajectory]):
     """A sequence of trajectories lazily backed by a HuggingFace dataset."""
 
@@ -70,16 +96,38 @@ class TrajectoryDatasetSequence(Sequence[types.Trajectory]):
         def numpy_transform(batch):
             return {key: np.asarray(val) if key != "infos" else val for key, val in batch.items()}
 
+        self._raw = dataset
         self._dataset = dataset.with_transform(numpy_transform)
         self._trajectory_class = types.TrajectoryWithRew if "rews" in dataset.features else types.Trajectory
+        # Arrow fast path for array columns (no index mapping: row i of the table == item i)
+        self._table = dataset.data.table if getattr(dataset, "_indices", None) is None else None
 
     def __len__(self) -> int:
         return len(self._dataset)
 
+    def _row_fast(self, idx: int) -> Dict[str, Any]:
+        t = self._table
+        out: Dict[str, Any] = {}
+        for key in ("obs", "acts", "rews"):
+            if key in t.column_names:
+                out[key] = _list_scalar_to_numpy(t.column(key)[idx])
+        out["terminal"] = bool(t.column("terminal")[idx].as_py())
+        out["infos"] = t.column("infos")[idx].as_py()
+        return out
+
     def __getitem__(self, idx):
         if isinstance(idx, slice):
             return [self[i] for i in range(*idx.indices(len(self)))]
-        kwargs = self._dataset[idx]
+        kwargs = None
+        if self._table is not None:
+            if idx < 0:
+                idx += len(self)
+            try:
+                kwargs = self._row_fast(int(idx))
+            except (ValueError, KeyError, TypeError):
+                kwargs = None
+        if kwargs is None:
+            kwargs = self._dataset[idx]
         kwargs["infos"] = _LazyDecodedList(kwargs["infos"])
         return self._trajectory_class(**kwargs)
 
