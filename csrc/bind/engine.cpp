@@ -82,7 +82,16 @@ void rollout(py::dict d) {
     a.use_next_state = ival(d, "use_next_state", 0);
     a.use_done = ival(d, "use_done", 0);
     a.rew_transform = ival(d, "rew_transform", 0);
+    a.shaped = ival(d, "shaped", 0);
+    if (a.shaped) {
+      a.pot = wave_mlp(d["pot"].cast<py::dict>());
+      a.shaping_gamma = (float)fval(d, "shaping_gamma", 0.99);
+      TORCH_CHECK(a.pot.dims[0] == ival(d, "obs_dim_check", a.pot.dims[0]), "potential input dim");
+    }
   }
+  a.rew_raw = tptr<float>(d, "rew_raw", true);
+  a.boot = tptr<float>(d, "boot", true);
+  TORCH_CHECK((a.rew_raw == nullptr) == (a.boot == nullptr), "rew_raw and boot go together");
   TORCH_CHECK(a.P.obs_dim <= ia::kEngineMaxObs, "obs dim too large for the device rollout");
   a.obs_buf = tptr<float>(d, "obs_buf");
   a.act_raw = tptr<float>(d, "act_raw");
@@ -98,6 +107,21 @@ void rollout(py::dict d) {
   a.last_values = tptr<float>(d, "last_values");
   a.prof = tptr<unsigned long long>(d, "prof", true);
   IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
+}
+
+void reward_outnorm(py::dict d) {
+  ia::OutNormArgs a{};
+  a.T = ival(d, "T");
+  a.N = ival(d, "N");
+  a.rew_raw = tptr<const float>(d, "rew_raw");
+  a.boot = tptr<const float>(d, "boot");
+  a.rewards = tptr<float>(d, "rewards");
+  a.mean = tptr<float>(d, "mean");
+  a.var = tptr<float>(d, "var");
+  a.count = tptr<float>(d, "count");
+  a.eps = (float)fval(d, "eps", 1e-5);
+  a.step_stats = tptr<const float>(d, "step_stats", true);
+  IA_HIP_CHECK2(ia::reward_outnorm_launch(a, ia_stream()));
 }
 
 void ppo_update(py::dict d) {
@@ -209,6 +233,7 @@ size_t ppo_lds(py::dict d) {
 
 void register_engine(py::module& m) {
   m.def("engine_rollout", &rollout, "T-step device rollout (policy + env + learned reward) for N envs");
+  m.def("engine_reward_outnorm", &reward_outnorm, "NormalizedRewardNet output normalisation over a rollout");
   m.def("engine_ppo_update", &ppo_update, "persistent PPO update / DP minibatch grads / apply");
   m.def("engine_ppo_path", &ppo_path, "kernel used by engine_ppo_update mode 0 (rc | lds)");
   m.def("engine_ppo_lds", &ppo_lds, "LDS bytes the PPO kernel needs for a configuration");

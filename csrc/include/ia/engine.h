@@ -57,6 +57,14 @@ struct RolloutArgs {
   WaveMLP rew;
   int use_state, use_action, use_next_state, use_done;
   int rew_transform;
+  // AIRL ShapedRewardNet: r = base(s,a,s',d) + shaping_gamma * (1 - d) * pot(s') - pot(s)
+  int shaped;
+  WaveMLP pot;
+  float shaping_gamma;
+  // when set: the learned reward (pre output-normalisation) and the TimeLimit bootstrap term
+  // are also stored separately, for reward_outnorm (NormalizedRewardNet.predict_processed)
+  float* rew_raw;  // [T][N]
+  float* boot;     // [T][N]
   // outputs, [T][N] (+ trailing feature dim)
   float* obs_buf;
   float* act_raw;   // sampled (unclipped) action, PPO buffer
@@ -71,6 +79,22 @@ struct RolloutArgs {
   float* ep_ret_out;  // episode return where done
   float* last_values;  // [N]
   unsigned long long* prof;  // optional [N][4] cycle counters: policy, env, reward, other
+};
+
+// NormalizedRewardNet output normalisation over a rollout, step by step in env order:
+// rewards[t][n] = (rew_raw[t][n] - mean) / sqrt(var + eps) + boot[t][n], then the running
+// (mean, var, count) are Chan-merged with step t's batch moments (over the N envs, or the
+// global ones given in step_stats[t] = (count, mean, biased var) under data parallelism).
+struct OutNormArgs {
+  int T, N;
+  const float* rew_raw;
+  const float* boot;
+  float* rewards;
+  float* mean;   // [1] running state, updated in place
+  float* var;    // [1]
+  float* count;  // [1] (float)
+  float eps;
+  const float* step_stats;  // [T][3] or nullptr
 };
 
 // One PPO update (all epochs x minibatches) in one persistent workgroup.

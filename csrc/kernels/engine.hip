@@ -366,6 +366,8 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
   p = load_mlp(a.pi, pi, p);
   p = load_mlp(a.vf, vf, p);
   if (a.rew_enabled) p = load_mlp(a.rew, rw, p);
+  LdsMLP pt;
+  if (a.rew_enabled && a.shaped) p = load_mlp(a.pot, pt, p);
   // env state / obs / action scratch stays a generic pointer: the shared host/device
   // env code (ia/envs.h) takes float*
   float* st = (float*)p;       // [kMaxState]
@@ -488,11 +490,22 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
       if (a.use_done) { if (lane == off) x = done ? 1.f : 0.f; off += 1; }
       float logit = bcast(wave_mlp(rw, x), 0);
       r = a.rew_transform == REW_SOFTPLUS ? (logit > 0.f ? logit + log1pf(expf(-logit)) : log1pf(expf(logit))) : logit;
+      if (a.shaped) {  // AIRL potential shaping (reward_nets.py ShapedRewardNet.forward)
+        const float phi_s = bcast(wave_mlp(pt, lane < D ? o : 0.f), 0);
+        const float phi_n = done ? 0.f : bcast(wave_mlp(pt, lane < D ? o_next : 0.f), 0);
+        r += a.shaping_gamma * phi_n - phi_s;
+      }
     }
     c_rew += clock64() - c0;
+    float bt = 0.f;
     if (trunc) {  // SB3: bootstrap the value of the truncated terminal obs into the reward
-      r += a.gamma * bcast(wave_mlp(vf, o_next), 0);
+      bt = a.gamma * bcast(wave_mlp(vf, o_next), 0);
     }
+    if (a.rew_raw && lane == 0) {
+      a.rew_raw[row] = r;
+      a.boot[row] = bt;
+    }
+    r += bt;
     if (lane == 0) {
       a.logp[row] = logp;
       a.values[row] = value;
@@ -549,8 +562,49 @@ int mlp_lds_floats(const WaveMLP& m) {
 
 }  // namespace
 
+// NormalizedRewardNet output normalisation (see OutNormArgs): one wave, sequential in t.
+__global__ __launch_bounds__(64) void reward_outnorm_kernel(OutNormArgs a) {
+  const int lane = threadIdx.x;
+  float mean = a.mean[0], var = a.var[0], cnt = a.count[0];
+  for (int t = 0; t < a.T; ++t) {
+    const float rstd = 1.f / sqrtf(var + a.eps);
+    float s = 0.f;
+    for (int n = lane; n < a.N; n += 64) {
+      const size_t i = (size_t)t * a.N + n;
+      const float x = a.rew_raw[i];
+      a.rewards[i] = (x - mean) * rstd + a.boot[i];
+      s += x;
+    }
+    float bm, bv, bn;
+    if (a.step_stats) {
+      bn = a.step_stats[3 * t];
+      bm = a.step_stats[3 * t + 1];
+      bv = a.step_stats[3 * t + 2];
+    } else {
+      bn = (float)a.N;
+      bm = wave_sum(s) / bn;
+      float q = 0.f;
+      for (int n = lane; n < a.N; n += 64) {
+        const float d = a.rew_raw[(size_t)t * a.N + n] - bm;
+        q += d * d;
+      }
+      bv = wave_sum(q) / bn;
+    }
+    const float delta = bm - mean, tot = cnt + bn;
+    mean += delta * bn / tot;
+    var = (var * cnt + bv * bn + delta * delta * cnt * bn / tot) / tot;
+    cnt = tot;
+  }
+  if (lane == 0) {
+    a.mean[0] = mean;
+    a.var[0] = var;
+    a.count[0] = cnt;
+  }
+}
+
 size_t rollout_lds_bytes(const RolloutArgs& a) {
   int f = mlp_lds_floats(a.pi) + mlp_lds_floats(a.vf) + (a.rew_enabled ? mlp_lds_floats(a.rew) : 0);
+  if (a.rew_enabled && a.shaped) f += mlp_lds_floats(a.pot);
   if (a.pi.n_layers == a.vf.n_layers) f += pair_lds_floats(a.pi, a.vf);  // paired image
   f += kMaxState + kEngineMaxObs + kWaveMaxDim;
   return (size_t)f * sizeof(float);
@@ -561,6 +615,12 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   const size_t lds = rollout_lds_bytes(a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rollout_kernel, dim3(a.N), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t reward_outnorm_launch(const OutNormArgs& a, hipStream_t s) {
+  if (a.T <= 0 || a.N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reward_outnorm_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -269,3 +269,80 @@ def test_fused_disc_train_logs_and_matches_generic_path_shape():
     tr.train_disc(expert_samples=next(tr._endless_expert_iterator), gen_samples=tr._gen_sample(tr.demo_batch_size))
     assert float(tr._disc_opt.state[tr._rflat.params[0]]["step"]) == 4
     assert tr._disc_opt.state[tr._rflat.params[0]]["exp_avg"].data_ptr() == tr._r_m.data_ptr()
+
+
+def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True):
+    from imitation_amd.data import rollout
+    from imitation_amd.engine.airl import DeviceAIRL
+    from imitation_amd.policies.base import NormalizeFeaturesExtractor
+    from imitation_amd.rewards.reward_nets import BasicShapedRewardNet, NormalizedRewardNet
+    from imitation_amd.rl.policies import ActorCriticPolicy
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.util import logger
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    th.manual_seed(seed)
+    np.random.seed(seed)
+    rng = np.random.default_rng(seed)
+    venv = make_vec_env("seals/Hopper-v1", rng=rng, n_envs=n_envs)
+    demo_env = make_vec_env("seals/Hopper-v1", rng=np.random.default_rng(7), n_envs=4)
+    demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
+    gen = PPO(ActorCriticPolicy, venv, n_steps=n_steps, batch_size=batch, n_epochs=2, device="cuda", seed=seed,
+              policy_kwargs=dict(net_arch=dict(pi=[64, 64], vf=[64, 64]), activation_fn=th.nn.ReLU,
+                                 features_extractor_class=NormalizeFeaturesExtractor))
+    rn = BasicShapedRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
+    if normalize_output:
+        rn = NormalizedRewardNet(rn, RunningNorm)
+    tr = DeviceAIRL(demonstrations=demos, demo_batch_size=256, venv=venv, gen_algo=gen, reward_net=rn,
+                    n_disc_updates_per_round=2, custom_logger=logger.configure("/tmp/ia_test_airl", format_strs=[]))
+    return tr, venv, gen, rn
+
+
+@gpu
+@pytest.mark.parametrize("normalize_output", [True, False])
+def test_device_airl_rollout_reward_matches_reward_train(normalize_output):
+    """Shaped reward (+ output normalisation replayed step by step) == AIRL.reward_train.predict_processed."""
+    import copy
+
+    tr, venv, gen, rn = _setup_airl(normalize_output=normalize_output)
+    # give the reward nets non-trivial normaliser state first
+    tr.train(tr.gen_train_timesteps)
+    host = copy.deepcopy(rn)
+    tr._rollout()
+    th.cuda.synchronize()
+    b = {k: v.cpu().numpy() for k, v in tr.buf.items()}
+    T, N = b["dones"].shape
+    boot = tr._boot.cpu().numpy() if normalize_output else None
+    exp = []
+    os.environ["IMITATION_AMD_FUSED"] = "0"  # fp32 PyTorch reference (the fused MLP op is bf16)
+    try:
+        for t in range(T):
+            r = host.predict_processed(b["obs_buf"][t], b["act_env"][t], b["next_obs"][t], b["dones"][t] > 0.5)
+            exp.append(r)
+    finally:
+        os.environ.pop("IMITATION_AMD_FUSED", None)
+    exp = np.stack(exp)
+    got = b["rewards"] - (boot if normalize_output else 0.0)
+    if not normalize_output:  # bootstrap only where truncated: compare on the other rows
+        mask = ~((b["dones"] > 0.5))
+        np.testing.assert_allclose(got[mask], exp[mask], rtol=2e-3, atol=2e-3)
+    else:
+        np.testing.assert_allclose(got, exp, rtol=2e-3, atol=2e-3)
+        onorm = rn.normalize_output_layer
+        th.testing.assert_close(onorm.running_mean.cpu(), host.normalize_output_layer.running_mean.cpu(), rtol=1e-4, atol=1e-5)
+        th.testing.assert_close(onorm.running_var.cpu(), host.normalize_output_layer.running_var.cpu(), rtol=1e-4, atol=1e-5)
+        assert int(onorm.count) == int(host.normalize_output_layer.count)
+
+
+@gpu
+def test_device_airl_rounds_train():
+    tr, venv, gen, rn = _setup_airl(n_envs=8, n_steps=128, batch=256)
+    assert tr._C.engine_ppo_path(tr._ppo_static).startswith("rc:")
+    p0 = [p.detach().clone() for p in gen.policy.parameters()]
+    r0 = [p.detach().clone() for p in rn.parameters()]
+    tr.train(3 * tr.gen_train_timesteps)
+    th.cuda.synchronize()
+    assert all(th.isfinite(p).all() for p in list(gen.policy.parameters()) + list(rn.parameters()))
+    assert any(not th.equal(a, b) for a, b in zip(p0, gen.policy.parameters()))
+    assert any(not th.equal(a, b) for a, b in zip(r0, rn.parameters()))
