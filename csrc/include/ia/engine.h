@@ -150,6 +150,7 @@ struct PPORcGeo {
   int h_off[2][kWaveMaxLayers], ldh[2][kWaveMaxLayers];
   int z_off[2][kWaveMaxLayers], ldz[2][kWaveMaxLayers], db_off[2][kWaveMaxLayers];
   int ls_off, lsp_off, nm_off, red_off, param_lds;
+  int zero_off;  // 64 floats of zeros (never written): operand of the padding dW items
   int n_items;
   int items[kMaxRcItems];  // q | layer << 1 | kind << 3 (0 W tile, 1 bias, 2 log_std) | out tile << 5 | in tile << 9
   int dp;                  // padded obs row stride of xraw

@@ -55,10 +55,17 @@ constexpr int kL = kWaveMaxLayers;
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// tanh as 1 - 2 / (exp(2x) + 1) on v_exp_f32 / v_rcp_f32 (abs error ~1e-7; saturates
+// correctly at +-inf) instead of the branchy libm tanhf
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
+  return 1.f - 2.f * __frcp_rn(e + 1.f);
+}
+
 __device__ __forceinline__ float act_fn(int act, float x) {
   switch (act) {
     case 1: return fmaxf(x, 0.f);
-    case 2: return tanhf(x);
+    case 2: return tanh_fast(x);
     case 3: return x > 0.f ? x : 0.01f * x;
     case 4: return 1.f / (1.f + expf(-x));
     default: return x;
@@ -262,7 +269,10 @@ __device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int ro
   r.rd = *reinterpret_cast<const f4*>(g.rowd + (slot * 64 + row) * 4);
 }
 
-template <int KT, int KI>
+// Shape specialisation: S0T (16-wide input k-steps / 4), NLT (layers per net), ACTT (hidden
+// activation), HWT (hidden width) fold the per-layer loop bounds, tile counts and the
+// activation switch at compile time; 0 / -1 = read them at run time (generic build).
+template <int KT, int KI, int S0T, int NLT, int ACTT, int HWT, int CWT>
 __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* L = (lf*)lds_raw;
@@ -272,14 +282,14 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   const int q = w >> 2;   // 0 actor, 1 critic
   const int gw = w & 3;   // row tile
   const int grp = blockIdx.x;
-  const int G = g.G, nch = g.nch, cw = g.cw;
+  const int G = g.G, nch = g.nch, cw = CWT > 0 ? CWT : g.cw;
   const int CH = G * nch;
   const int Bg = CH * cw;  // minibatch rows
   const int RT = cw / 16;
   const bool rows_wave = gw < RT;
-  const int nl = q == 0 ? a.n_pi : a.n_vf;
+  const int nl = NLT > 0 ? NLT : (q == 0 ? a.n_pi : a.n_vf);
   const int D = a.D, A = a.A;
-  const int s0 = (D + 3) / 4;
+  const int s0 = S0T > 0 ? S0T : (D + 3) / 4;
   const bool gauss = !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
   const int n_mb = a.rows / Bg;
@@ -356,7 +366,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   float st_ent = 0.f, st_pg = 0.f, st_vl = 0.f, st_cf = 0.f, st_kl = 0.f;
   float step = a.adam_step[0];
   float b1t = powf(a.beta1, step), b2t = powf(a.beta2, step);
-  const int hid_act = a.hidden_act;
+  const int hid_act = ACTT >= 0 ? ACTT : a.hidden_act;
   // first minibatch norm stats
   if (norm_lane && K > 0) {
     const float m = g.mom[nc], v = g.mom[64 + nc], n = (float)Bg;
@@ -367,12 +377,42 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     L[g.nm_off + nc] = run_m;
     L[g.nm_off + 64 + nc] = rsqrtf(run_v + a.norm_eps);
   }
+  // dW item operands (LDS offsets of this lane's dZ / H columns; padding items read zeros)
+  int izo[KI], izs[KI], iho[KI], ihs[KI], imask[KI];
+#pragma unroll
+  for (int it = 0; it < KI; ++it) {
+    const int id = w + it * kWaves;
+    izo[it] = iho[it] = g.zero_off + r16;
+    izs[it] = ihs[it] = 0;
+    imask[it] = 0;
+    if (id < n_items) {
+      const int desc = rfl(g.items[id]);
+      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+      if (kind == 0) {
+        const LG y = lg(g, iq, il);
+        izo[it] = y.z + kk * y.ldz + 16 * ta + r16;
+        iho[it] = y.h + kk * y.ldh + 16 * tb + r16;
+        izs[it] = 4 * y.ldz;
+        ihs[it] = 4 * y.ldh;
+        const int in = 16 * tb + r16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (16 * ta + 4 * kk + j < y.dout && in < y.din) imask[it] |= 1 << j;
+      }
+    }
+  }
+  float pre_m = 0.f, pre_v = 0.f;  // moments of the next minibatch to merge
+  if (norm_lane && K > 1) {
+    pre_m = g.mom[128 + nc];
+    pre_v = g.mom[128 + 64 + nc];
+  }
   Rows cur;
   const int row = 16 * gw + r16;
   // chunk unit u = k * nch + ch -> prep slot k * CH + grp * nch + ch
   auto slot_of = [&](int u) -> size_t { return (size_t)(u / nch) * CH + (size_t)grp * nch + (u % nch); };
   if (rows_wave && K > 0) load_rows(g, slot_of(0), row, kk, s0, cur);
   unsigned long long prof[3] = {0, 0, 0};
+  unsigned long long wprof[4] = {0, 0, 0, 0};  // this wave: rows/x, forward, loss, backward chain
   unsigned* arrive = g.sync;
   unsigned* tflag = g.sync + 1;
   __syncthreads();
@@ -388,17 +428,17 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       const int u = k * nch + ch;
       Rows nxt;
       if (rows_wave && u + 1 < K * nch) load_rows(g, slot_of(u + 1), row, kk, s0, nxt);
-      // Chan merge for minibatch k+1 (one lane per feature, wave 7)
-      if (ch == 0 && norm_lane && k + 1 < K) {
-        const int c = nc;
-        const float m = g.mom[(size_t)(k + 1) * 128 + c], v = g.mom[(size_t)(k + 1) * 128 + 64 + c], n = (float)Bg;
-        const float tot = run_c + n, delta = m - run_m;
-        run_m += delta * n / tot;
-        run_v = (run_v * run_c + v * n + delta * delta * run_c * n / tot) / tot;
-        run_c = tot;
-        L[g.nm_off + (128 - nb) + c] = run_m;
-        L[g.nm_off + (128 - nb) + 64 + c] = rsqrtf(run_v + a.norm_eps);
+      // moments of minibatch k+1 (prefetched one minibatch earlier) -> registers; issue k+2
+      float mom_m = 0.f, mom_v = 0.f;
+      if (ch == 0 && norm_lane) {
+        mom_m = pre_m;
+        mom_v = pre_v;
+        if (k + 2 < K) {
+          pre_m = g.mom[(size_t)(k + 2) * 128 + nc];
+          pre_v = g.mom[(size_t)(k + 2) * 128 + 64 + nc];
+        }
       }
+      unsigned long long c0 = a.prof ? clock64() : 0;
       if (rows_wave) {
         // ---------------- normalised input: B operand of layer 0 (natural K order 4s + kk)
         float xb[16];
@@ -418,6 +458,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           for (int s = 0; s < 16; ++s)
             if (s < s0) L[h0 + row * ld0 + 4 * s + kk] = xb[s];
         }
+        unsigned long long c1 = a.prof ? clock64() : 0;
         // ---------------- forward (registers)
         f4 hreg[kL - 1][KT];  // outputs of hidden layers (C layout), kept for act'
         f4 head = {0.f, 0.f, 0.f, 0.f};
@@ -426,7 +467,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           if (l >= nl) continue;
           const LG y = lg(g, q, l);
           const bool last = l == nl - 1;
-          const int tout = (y.dout + 15) >> 4;
+          const int tout = (HWT > 0 && !last) ? HWT / 16 : ((y.dout + 15) >> 4);
           f4 acc[KT];
 #pragma unroll
           for (int t = 0; t < KT; ++t) {
@@ -438,7 +479,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
               for (int s = 0; s < 16; ++s)
                 if (s < s0) acc[t] = mfma(wr[4 * s + kk], xb[s], acc[t]);
             } else {
-              const int tin = (y.din + 15) >> 4;
+              const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
 #pragma unroll
               for (int h = 0; h < KT; ++h) {
                 if (h >= tin) continue;
@@ -457,10 +498,10 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
             v.z = acc[t].z + bb.z;
             v.w = acc[t].w + bb.w;
             if (!last) {
-              v.x = o0 + 0 < y.dout ? act_fn(hid_act, v.x) : 0.f;
-              v.y = o0 + 1 < y.dout ? act_fn(hid_act, v.y) : 0.f;
-              v.z = o0 + 2 < y.dout ? act_fn(hid_act, v.z) : 0.f;
-              v.w = o0 + 3 < y.dout ? act_fn(hid_act, v.w) : 0.f;
+              v.x = (HWT > 0 || o0 + 0 < y.dout) ? act_fn(hid_act, v.x) : 0.f;
+              v.y = (HWT > 0 || o0 + 1 < y.dout) ? act_fn(hid_act, v.y) : 0.f;
+              v.z = (HWT > 0 || o0 + 2 < y.dout) ? act_fn(hid_act, v.z) : 0.f;
+              v.w = (HWT > 0 || o0 + 3 < y.dout) ? act_fn(hid_act, v.w) : 0.f;
               if (l < kL - 1) {
                 hreg[l][t] = v;
                 // input image of layer l + 1 (for its dW)
@@ -472,6 +513,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
             }
           }
         }
+        unsigned long long c2 = a.prof ? clock64() : 0;
         // ---------------- loss -> dZ of the head (C layout, tile 0)
         f4 dz = {0.f, 0.f, 0.f, 0.f};
         const LG yh = lg(g, q, nl - 1);
@@ -569,6 +611,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           }
           dz = {kk == 0 ? a.vf_coef * 2.f * d * invB : 0.f, 0.f, 0.f, 0.f};
         }
+        unsigned long long c3 = a.prof ? clock64() : 0;
         // ---------------- backward chain: store dZ_l, bias partials, dZ_{l-1} = W_l^T dZ_l * act'
         f4 dzc[KT];
         dzc[0] = dz;
@@ -578,7 +621,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         for (int l = kL - 1; l >= 0; --l) {
           if (l >= nl) continue;
           const LG y = lg(g, q, l);
-          const int tout = (y.dout + 15) >> 4;
+          const int tout = (HWT > 0 && l != nl - 1) ? HWT / 16 : ((y.dout + 15) >> 4);
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) {
             if (u2 >= tout) continue;
@@ -590,7 +633,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
             }
           }
           if (l == 0) break;
-          const int tin = (y.din + 15) >> 4;
+          const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
           f4 nd[KT];
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) {
@@ -615,8 +658,26 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) dzc[u2] = nd[u2];
         }
+        if (a.prof) {
+          const unsigned long long c4 = clock64();
+          wprof[0] += c1 - c0;
+          wprof[1] += c2 - c1;
+          wprof[2] += c3 - c2;
+          wprof[3] += c4 - c3;
+        }
       }
       __syncthreads();  // B1: H / dZ images, bias and log-std partials of this chunk complete
+      // Chan merge for minibatch k+1 (one lane per feature, wave 7), off the chain's critical
+      // path; minibatch k reads the other half of the double-buffered normaliser image
+      if (ch == 0 && norm_lane && k + 1 < K) {
+        const float n = (float)Bg;
+        const float tot = run_c + n, delta = mom_m - run_m;
+        run_m += delta * n / tot;
+        run_v = (run_v * run_c + mom_v * n + delta * delta * run_c * n / tot) / tot;
+        run_c = tot;
+        L[g.nm_off + (128 - nb) + nc] = run_m;
+        L[g.nm_off + (128 - nb) + 64 + nc] = rsqrtf(run_v + a.norm_eps);
+      }
 
       // ---------------- dW / db / dlog_std partials of this chunk for the owned items
 #pragma unroll
@@ -624,21 +685,19 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         const int id = w + it * kWaves;
         if (id >= n_items) continue;
         const int desc = rfl(g.items[id]);
-        const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-        const LG y = lg(g, iq, il);
+        const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3;
         if (kind == 0) {
           f4 acc = {0.f, 0.f, 0.f, 0.f};
-          const lf* zp = L + y.z + kk * y.ldz + 16 * ta + r16;
-          const lf* hp = L + y.h + kk * y.ldh + 16 * tb + r16;
-          for (int s = 0; s < cw / 4; ++s) acc = mfma(zp[4 * s * y.ldz], hp[4 * s * y.ldh], acc);
-          const int in = 16 * tb + r16;
-          const float av[4] = {acc.x, acc.y, acc.z, acc.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int o = 16 * ta + 4 * kk + j;
-            gg[it][j] += (o < y.dout && in < y.din) ? av[j] : 0.f;
-          }
+          const lf* zp = L + izo[it];
+          const lf* hp = L + iho[it];
+#pragma unroll 4
+          for (int s = 0; s < cw / 4; ++s) acc = mfma(zp[s * izs[it]], hp[s * ihs[it]], acc);
+          gg[it][0] += (imask[it] & 1) ? acc.x : 0.f;
+          gg[it][1] += (imask[it] & 2) ? acc.y : 0.f;
+          gg[it][2] += (imask[it] & 4) ? acc.z : 0.f;
+          gg[it][3] += (imask[it] & 8) ? acc.w : 0.f;
         } else if (kind == 1) {
+          const LG y = lg(g, iq, il);
           float gval = 0.f;
           if (lane < y.dout)
             for (int r = 0; r < RT; ++r) gval += L[y.db + r * 64 + lane];
@@ -852,6 +911,9 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     a.prof[1] += prof[1];
     a.prof[2] += prof[2];
   }
+  if (a.prof && lane == 0 && (w == 0 || w == 4)) {  // actor / critic row tile 0
+    for (int i = 0; i < 4; ++i) a.prof[3 + (w == 4 ? 4 : 0) + i] += wprof[i];
+  }
 }
 
 constexpr int items_per_wave(int kt) { return kt == 2 ? 4 : 8; }
@@ -913,6 +975,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     }
   }
   g.ls_off = take(16);
+  g.zero_off = take(64);
   g.param_lds = off;
   // activation images (cw rows): layer-0 input shared by both nets
   const int ld0 = ((a.D + 15) & ~15) + 4;
@@ -990,10 +1053,24 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   // > 80 KiB of LDS keeps the cooperating workgroups one per CU (the measured condition of
   // the sc1 hand-off); all G <= 16 of them are co-resident on an otherwise idle GPU
   const size_t lds_launch = g.G > 1 && lds < 96 * 1024 ? 96 * 1024 : lds;
-  if (g.kt == 2)
-    hipLaunchKernelGGL((ppo_rc_kernel<2, 4>), dim3(g.G), dim3(kThreads), lds_launch, s, a, g);
+  // shape-specialised builds for the headline configs, generic otherwise
+  int hw = a.pi_dims[1];
+  bool uniform = a.n_pi == 3 && a.n_vf == 3;
+  for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
+  const int s0 = (a.D + 3) / 4;
+  const dim3 grid(g.G), block(kThreads);
+#define IA_RC(KT, KI, S0, NL, ACT, HW, CW) hipLaunchKernelGGL((ppo_rc_kernel<KT, KI, S0, NL, ACT, HW, CW>), grid, block, lds_launch, s, a, g)
+  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64)
+    IA_RC(2, 4, 5, 3, 2, 32, 64);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
+  else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32)
+    IA_RC(4, 8, 3, 3, 1, 64, 32);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
+  else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64)
+    IA_RC(2, 4, 1, 3, 2, 32, 64);  // CartPole FeedForward32Policy
+  else if (g.kt == 2)
+    IA_RC(2, 4, 0, 0, -1, 0, 0);
   else
-    hipLaunchKernelGGL((ppo_rc_kernel<4, 8>), dim3(g.G), dim3(kThreads), lds_launch, s, a, g);
+    IA_RC(4, 8, 0, 0, -1, 0, 0);
+#undef IA_RC
   return hipGetLastError();
 }
 

@@ -1,9 +1,9 @@
-import sys, time, numpy as np, torch as th
-sys.path.insert(0, '.')
+import os, sys, time, numpy as np, torch as th
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tests.engine.test_device_engine import _setup
 tr, venv, gen, rn = _setup(n_envs=8, n_steps=512, batch=64, n_epochs=5)
 prof = th.zeros(8, 4, dtype=th.int64, device='cuda')
-pprof = th.zeros(10, dtype=th.int64, device='cuda')
+pprof = th.zeros(16, dtype=th.int64, device='cuda')
 orig = tr._C.engine_rollout
 orig2 = tr._C.engine_ppo_update
 def wrapped(d):
@@ -21,11 +21,13 @@ for i in range(3):
 for allow_rc in (1, 0):
     tr._ppo_static['allow_rc'] = allow_rc
     path = tr._C.engine_ppo_path(tr._ppo_static)
-    names = ['fwd+loss+bwd', 'dW', 'adam'] if path == 'rc' else ['rows', 'prep', 'fwd', 'loss', 'bwd', 'adam']
+    names = ['fwd+loss+bwd', 'dW+exchange', 'adam'] if path.startswith('rc') else ['rows', 'prep', 'fwd', 'loss', 'bwd', 'adam']
     for i in range(3):
         pprof.zero_()
         th.cuda.synchronize(); t = time.perf_counter(); tr._ppo_update(); th.cuda.synchronize(); dt = time.perf_counter() - t
         pp = pprof.cpu().numpy() / 320
         print(f'ppo update [{path}] {dt*1e3:.2f} ms; cycles/minibatch: ' + ' '.join(f'{n}={v:.0f}' for n, v in zip(names, pp)), flush=True)
+        if path.startswith('rc'):
+            print('   actor wave: rows %.0f fwd %.0f loss %.0f bwd %.0f | critic wave: rows %.0f fwd %.0f loss %.0f bwd %.0f' % tuple(pp[3:11]), flush=True)
 tr._ppo_static['allow_rc'] = 1
 tr._ep_lens_running[:] = 0
