@@ -98,65 +98,95 @@ __device__ __forceinline__ void chan_merge(float* rmean, float* rvar, int count,
   rvar[c] = v / tot;
 }
 
-__global__ __launch_bounds__(128) void disc_norm_kernel(DiscNormArgs a) {
-  const int c = threadIdx.x;
+// 1024 threads = 8 block-phases x 128 columns: phase p sums partial blocks p, p+8, ... in
+// order, then the 8 phase sums are added in phase order (fixed order: deterministic).
+constexpr int kNormPhases = 8;
+
+__global__ __launch_bounds__(128 * kNormPhases) void disc_norm_kernel(DiscNormArgs a) {
+  __shared__ double red[kNormPhases][2][128];
+  const int c = threadIdx.x & 127, ph = threadIdx.x >> 7;
   const int n = a.mode == 2 ? a.n_total : 2 * a.mb;
   const int rc = a.rew_count ? *a.rew_count : 0;
   const int pc = a.pol_count ? *a.pol_count : 0;
-  if (c < a.din) {
+  if (a.mode != 2) {
+    double s1 = 0.0, s2 = 0.0;
+    if (c < a.din)
+      for (int b = ph; b < a.nblk; b += kNormPhases) {
+        const float* p = a.partials + (size_t)b * 2 * a.din;
+        s1 += (double)p[c];
+        s2 += (double)p[a.din + c];
+      }
+    red[ph][0][c] = s1;
+    red[ph][1][c] = s2;
+    __syncthreads();
+  }
+  if (ph == 0 && c < a.din) {
     double S1 = 0.0, S2 = 0.0;
     if (a.mode == 2) {
       S1 = a.sums[c];
       S2 = a.sums[a.din + c];
     } else {
-      for (int b = 0; b < a.nblk; ++b) {
-        const float* p = a.partials + (size_t)b * 2 * a.din;
-        S1 += (double)p[c];
-        S2 += (double)p[a.din + c];
+      for (int q = 0; q < kNormPhases; ++q) {
+        S1 += red[q][0][c];
+        S2 += red[q][1][c];
       }
     }
     if (a.mode == 1) {
       a.sums[c] = S1;
       a.sums[a.din + c] = S2;
-      return;
+    } else {
+      const double shift = a.shift ? (double)a.shift[c] : 0.0;
+      const double m = S1 / n;
+      double var = S2 / n - m * m;
+      if (var < 0.0) var = 0.0;
+      const float bmean = (float)(shift + m), bvar = (float)var;
+      if (a.rew_mean) chan_merge(a.rew_mean, a.rew_var, rc, c, bmean, bvar, n);
+      if (a.pol_mean && c < a.pol_cols) chan_merge(a.pol_mean, a.pol_var, pc, c, bmean, bvar, n);
     }
-    const double shift = a.shift ? (double)a.shift[c] : 0.0;
-    const double m = S1 / n;
-    double var = S2 / n - m * m;
-    if (var < 0.0) var = 0.0;
-    const float bmean = (float)(shift + m), bvar = (float)var;
-    if (a.rew_mean) chan_merge(a.rew_mean, a.rew_var, rc, c, bmean, bvar, n);
-    if (a.pol_mean && c < a.pol_cols) chan_merge(a.pol_mean, a.pol_var, pc, c, bmean, bvar, n);
   }
   if (a.mode == 1) return;
   __syncthreads();
-  if (c == 0) {
+  if (threadIdx.x == 0) {
     if (a.rew_count) *a.rew_count = rc + n;
     if (a.pol_count) *a.pol_count = pc + n;
   }
 }
 
-// grid: ceil(n_params / 64) blocks of 256 = 4 block-phases x 64 params.
-__global__ __launch_bounds__(256) void disc_adam_kernel(DiscAdamArgs a) {
-  __shared__ float red[4][64];
+// grid: ceil(n_params / 64) blocks of 1024 = 16 block-phases x 64 params (fixed-order
+// reduction of the gradient slab: phase q sums slab blocks q, q+16, ...; phases in order).
+constexpr int kAdamPhases = 16;
+
+__global__ __launch_bounds__(64 * kAdamPhases) void disc_adam_kernel(DiscAdamArgs a) {
+  __shared__ float red[kAdamPhases][64];
+  __shared__ float sred[kAdamPhases][kDiscStats];
   const int pl = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + pl;
   float s = 0.f;
   if (a.reduce && e < a.n_params)
-    for (int b = ph; b < a.nblk; b += 4) s += a.slab[(size_t)b * a.n_params + e];
+    for (int b = ph; b < a.nblk; b += kAdamPhases) s += a.slab[(size_t)b * a.n_params + e];
   red[ph][pl] = s;
-  // loss statistics of this (last) minibatch: block 0, threads 64..71 (phase 1)
-  if (a.reduce && blockIdx.x == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + kDiscStats && a.stats_out) {
-    const int k = threadIdx.x - 64;
+  // loss statistics of this (last) minibatch: block 0, lanes 0..kDiscStats-1 of every phase
+  const bool do_stats = a.reduce && blockIdx.x == 0 && a.stats_out;
+  if (do_stats && pl < kDiscStats) {
     float t = 0.f;
-    for (int b = 0; b < a.stats_nblk; ++b) t += a.stats_slab[(size_t)b * kDiscStats + k];
-    a.stats_out[k] = t;
+    for (int b = ph; b < a.stats_nblk; b += kAdamPhases) t += a.stats_slab[(size_t)b * kDiscStats + pl];
+    sred[ph][pl] = t;
   }
   __syncthreads();
+  if (do_stats && threadIdx.x < kDiscStats) {
+    float t = 0.f;
+    for (int q = 0; q < kAdamPhases; ++q) t += sred[q][threadIdx.x];
+    a.stats_out[threadIdx.x] = t;
+  }
+  if (ph == 0 && e < a.n_params) {
+    float acc = 0.f;
+    for (int q = 0; q < kAdamPhases; ++q) acc += red[q][pl];
+    red[0][pl] = acc;
+  }
   if (ph != 0 || e >= a.n_params) return;
   float g;
   if (a.reduce) {
-    g = (red[0][pl] + red[1][pl]) + (red[2][pl] + red[3][pl]);
+    g = red[0][pl];
     if (!a.adam) {
       a.grads[e] = g;
       return;
@@ -189,12 +219,12 @@ hipError_t disc_gather(const DiscGatherArgs& a, hipStream_t s) {
 
 hipError_t disc_norm(const DiscNormArgs& a, hipStream_t s) {
   if (a.din > 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(disc_norm_kernel, dim3(1), dim3(128), 0, s, a);
+  hipLaunchKernelGGL(disc_norm_kernel, dim3(1), dim3(128 * kNormPhases), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t disc_adam(const DiscAdamArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(disc_adam_kernel, dim3((a.n_params + 63) / 64), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(disc_adam_kernel, dim3((a.n_params + 63) / 64), dim3(64 * kAdamPhases), 0, s, a);
   return hipGetLastError();
 }
 

@@ -463,9 +463,27 @@ class DeviceEngineMixin:
         norm.running_var.copy_(rv / tot)
         self.norm_count.add_(cnt)
 
+    def _stage_rollout_to_host(self):
+        """Async D2H copy of (dones, episode returns) into pinned buffers; returns the event
+        that marks them ready."""
+        if not hasattr(self, "_host_stage"):
+            self._host_stage = th.empty(2, self.T, self.N, pin_memory=True)
+        self._host_stage[0].copy_(self.buf["dones"], non_blocking=True)
+        self._host_stage[1].copy_(self.buf["ep_ret_out"], non_blocking=True)
+        ev = th.cuda.Event()
+        ev.record()
+        self._host_staged = True
+        return ev
+
     def _store_generator_samples(self) -> None:
         """Replay-buffer content identical to BufferingWrapper -> flatten -> FIFO store."""
-        dones = self.buf["dones"].to("cpu", non_blocking=False).numpy().astype(bool)  # [T, N] (one sync / round)
+        if getattr(self, "_host_staged", False):
+            dones = self._host_stage[0].numpy().astype(bool)
+            ep_ret_host = self._host_stage[1].numpy()
+            self._host_staged = False
+        else:
+            dones = self.buf["dones"].to("cpu", non_blocking=False).numpy().astype(bool)  # [T, N] (one sync / round)
+            ep_ret_host = None
         T, N = dones.shape
         finished: List[Tuple[int, int, int, int]] = []  # (end_t, env, start_t, len)
         partial: List[Tuple[int, int, int]] = []
@@ -507,7 +525,7 @@ class DeviceEngineMixin:
         self._check_fixed_horizon(ep_lens)
         # Monitor-style episode stats for the generator logger
         if finished:
-            ep_ret = self.buf["ep_ret_out"].cpu().numpy()
+            ep_ret = ep_ret_host if ep_ret_host is not None else self.buf["ep_ret_out"].cpu().numpy()
             algo = self.gen_algo
             if algo.ep_info_buffer is None:
                 import collections
@@ -532,8 +550,12 @@ class DeviceEngineMixin:
                 if algo._total_timesteps < algo.num_timesteps + self.T * self.N:
                     algo._total_timesteps = algo.num_timesteps + self.T * self.N
                 self._rollout()
+                # episode bookkeeping needs dones / returns on the host: copy them right after
+                # the rollout and let the CPU work while the PPO kernel runs
+                ready = self._stage_rollout_to_host()
                 algo.num_timesteps += self.T * self.N
                 self._ppo_update()
+                ready.synchronize()
                 self._store_generator_samples()
                 self._global_step += 1
             self._log_gen()
