@@ -74,6 +74,8 @@ void rollout(py::dict d) {
   a.act_low = tptr<const float>(d, "act_low", true);
   a.act_high = tptr<const float>(d, "act_high", true);
   a.n_actions = ival(d, "n_actions", 0);
+  a.explore_mode = tptr<const int>(d, "explore_mode", true);
+  TORCH_CHECK(!a.explore_mode || a.n_actions > 0 || (a.act_low && a.act_high), "exploration needs Box bounds");
   a.rew_enabled = ival(d, "rew_enabled", 0);
   if (a.rew_enabled) {
     a.rew = wave_mlp(d["rew"].cast<py::dict>());

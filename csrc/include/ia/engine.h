@@ -52,6 +52,9 @@ struct RolloutArgs {
   const float* act_low;  // [A] Box bounds for clipping
   const float* act_high;
   int n_actions;  // >0: Categorical over n_actions
+  // optional ExplorationWrapper schedule: explore_mode[t] != 0 -> every env takes a uniform
+  // random action at step t (Box.sample / Discrete.sample) instead of the policy's
+  const int* explore_mode;  // [T] or nullptr
   // learned reward (GAIL / AIRL reward_train); rew_enabled==0 -> env reward
   int rew_enabled;
   WaveMLP rew;

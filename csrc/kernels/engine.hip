@@ -432,6 +432,21 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
       logp = wave_sum(lp);
       a_env = lane < A ? fminf(fmaxf(a_raw, a.act_low[lane]), a.act_high[lane]) : 0.f;
     }
+    if (a.explore_mode && a.explore_mode[t]) {  // ExplorationWrapper's random policy
+      uint64_t s = key ^ 0x5851F42D4C957F2Dull;
+      if (a.n_actions > 0) {
+        s ^= 0x2545F4914F6CDD1Dull;
+        const float u = uniform01(s);
+        int k = (int)(u * (float)a.n_actions);
+        k = k < a.n_actions ? k : a.n_actions - 1;
+        a_raw = a_env = (float)k;
+      } else {
+        s ^= 0xD6E8FEB86659FD93ull * (lane + 1);
+        const float u = uniform01(s);
+        a_env = lane < A ? a.act_low[lane] + u * (a.act_high[lane] - a.act_low[lane]) : 0.f;
+        a_raw = a_env;
+      }
+    }
     if (lane < A) {
       a.act_raw[row * A + lane] = a_raw;
       a.act_env[row * A + lane] = a_env;

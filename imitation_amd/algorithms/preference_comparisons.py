@@ -23,6 +23,7 @@ backward kernel. Ensemble members are scored in the same batched way.
 from __future__ import annotations
 
 import abc
+import os
 import math
 import re
 from collections import defaultdict
@@ -633,7 +634,121 @@ class BasicRewardTrainer(RewardTrainer):
     def requires_regularizer_update(self) -> bool:
         return self.regularizer is not None and self.regularizer.val_split is not None
 
+    def _fast_path_ok(self, dataset) -> bool:
+        """Device-resident minibatching applies: BCE loss on a single reward net, no
+        validation split, a plain PreferenceDataset of equal-length array fragments."""
+        pm = self._preference_model
+        if os.environ.get("IMITATION_AMD_PREF_FAST", "1") == "0":
+            return False
+        if type(self.loss) is not CrossEntropyRewardLoss or pm.ensemble_model is not None:
+            return False
+        if self.requires_regularizer_update or not isinstance(dataset, PreferenceDataset) or len(dataset) == 0:
+            return False
+        if isinstance(dataset.fragments1[0].obs, types.DictObs):
+            return False
+        return len({len(f) for f in dataset.fragments1} | {len(f) for f in dataset.fragments2}) == 1
+
+    def _train_fast(self, dataset: PreferenceDataset, epoch_multiplier: float) -> int:
+        """Same epochs / shuffling (a DataLoader over pair indices, generator seeded from ``self.rng`` as
+        the DataLoader does) / gradient accumulation / logged means as the generic loop, but
+        the whole dataset is packed and preprocessed ONCE into device tensors; a minibatch
+        is a row gather, one reward-net forward over its 2*B*L transitions and the fused
+        Bradley-Terry kernel. Per-minibatch metrics stay on device until the epoch ends
+        (one host sync per epoch instead of three per minibatch)."""
+        pm = self._preference_model
+        pairs = list(zip(dataset.fragments1, dataset.fragments2))
+        packed = _pack_pairs(pairs)
+        s_all, a_all, ns_all, d_all = pm.model.preprocess(packed.state, packed.action, packed.next_state, packed.done)
+        dev = s_all.device
+        P, L = len(pairs), packed.max_len
+        prefs_all = th.as_tensor(dataset.preferences, device=dev)
+        gt = None
+        if _trajectory_pair_includes_reward(pairs[0]):
+            gt = th.as_tensor(np.stack([np.asarray(f.rews, np.float32) for pr in pairs for f in pr]), device=dev).view(P, 2, L)
+        span = th.arange(2 * L, device=dev)
+        # a DataLoader over the pair indices: the generator is consumed exactly as by the
+        # DataLoader of the generic loop (base seed + permutation per epoch)
+        index_loader = data_th.DataLoader(range(P), batch_size=self.minibatch_size, shuffle=True,
+                                          generator=th.Generator().manual_seed(util.make_seeds(self.rng)))
+        epochs = round(self.epochs * epoch_multiplier)
+        assert epochs > 0, "Must train for at least one epoch."
+        B = self.minibatch_size
+        graph = None
+        if (dev.type == "cuda" and self.minibatch_size == self.batch_size and self.regularizer is None
+                and os.environ.get("IMITATION_AMD_PREF_GRAPH", "1") != "0"):
+            graph = self._minibatch_graph(s_all, a_all, ns_all, d_all, prefs_all, gt, P, L, B)
+        epoch_num = 0
+        with self.logger.accumulate_means("reward"):
+            for epoch_num in range(epochs):
+                order = th.cat(list(index_loader)).to(dev, non_blocking=True)
+                recs = []
+                accumulated = 0
+                self.optim.zero_grad()
+                for start in range(0, P, B):
+                    idx = order[start : start + B]
+                    n = int(min(B, P - start))
+                    if graph is not None:
+                        recs.append(graph.run(idx))
+                        continue
+                    rows = (idx[:, None] * (2 * L) + span).reshape(-1)
+                    rews = pm.model(s_all.index_select(0, rows), a_all.index_select(0, rows),
+                                    ns_all.index_select(0, rows), d_all.index_select(0, rows)).view(n, 2, L)
+                    prefs = prefs_all.index_select(0, idx)
+                    loss, probs = pref_ops.bradley_terry(rews[:, 0], rews[:, 1], prefs, pm.discount_factor, pm.threshold,
+                                                         pm.noise_prob)
+                    rec = [loss.detach(), ((probs.detach() > 0.5) == (prefs > 0.5)).float().mean()]
+                    if gt is not None:
+                        g = gt.index_select(0, idx)
+                        gp = pref_ops.bradley_terry_probs_reference(g[:, 0], g[:, 1], pm.discount_factor, pm.threshold,
+                                                                    pm.noise_prob)
+                        rec.append(th.nn.functional.binary_cross_entropy(gp, prefs))
+                    recs.append(th.stack(rec))
+                    loss = loss * (n / self.batch_size)
+                    if self.regularizer:
+                        self.regularizer.regularize_and_backward(loss)
+                    else:
+                        loss.backward()
+                    accumulated += n
+                    if accumulated >= self.batch_size:
+                        self.optim.step()
+                        self.optim.zero_grad()
+                        accumulated = 0
+                if accumulated != 0:
+                    self.optim.step()
+                names = ["loss", "accuracy", "gt_reward_loss"]
+                with self.logger.add_key_prefix(f"epoch-{epoch_num}"), self.logger.add_key_prefix("train"):
+                    for vals in th.stack(recs).cpu().tolist():
+                        for k, v in zip(names, vals):
+                            self.logger.record(k, v)
+        return epoch_num
+
+    def _minibatch_graph(self, s_all, a_all, ns_all, d_all, prefs_all, gt, P: int, L: int, B: int) -> "_MinibatchGraph":
+        """The persistent HIP-graph of one full minibatch step (re-captured only when the
+        dataset outgrows its device buffers or the shapes change)."""
+        key = (L, B, tuple(s_all.shape[1:]), tuple(a_all.shape[1:]), tuple(ns_all.shape[1:]), tuple(d_all.shape[1:]),
+               s_all.dtype, a_all.dtype, gt is not None, s_all.device)
+        g = getattr(self, "_mb_graph", None)
+        if g is None or g.key != key or g.capacity < P:
+            cap = 1 << max(0, (P - 1).bit_length())
+            g = _MinibatchGraph(self, key, cap, s_all, a_all, ns_all, d_all, gt is not None, L, B)
+            self._mb_graph = g
+        g.load(s_all, a_all, ns_all, d_all, prefs_all, gt, P)
+        return g
+
+    def _record_final(self, epoch_num: int) -> None:
+        """Record the last epoch's means under ``reward/final/...``."""
+        outer_prefix = self.logger.get_accumulate_prefixes()
+        base_path = f"{outer_prefix}reward/"
+        pattern = re.compile(rf"mean/{re.escape(base_path)}epoch-{epoch_num}/(.+)")
+        for key in list(self.logger.name_to_value.keys()):
+            m = pattern.match(key)
+            if m:
+                self.logger.record(f"{base_path}final/{m.group(1)}", self.logger.name_to_value[key])
+
     def _train(self, dataset: PreferenceDataset, epoch_multiplier: float = 1.0) -> None:
+        if self._fast_path_ok(dataset):
+            self._record_final(self._train_fast(dataset, epoch_multiplier))
+            return
         if self.regularizer is not None and self.regularizer.val_split is not None:
             val_length = int(len(dataset) * self.regularizer.val_split)
             train_length = len(dataset) - val_length
@@ -682,14 +797,7 @@ class BasicRewardTrainer(RewardTrainer):
                             with self.logger.add_key_prefix("val"):
                                 val_loss += self._training_inner_loop(fragment_pairs, preferences).item()
                     self.regularizer.update_params(train_loss, val_loss)
-        # record the last epoch's means under reward/final/...
-        outer_prefix = self.logger.get_accumulate_prefixes()
-        base_path = f"{outer_prefix}reward/"
-        pattern = re.compile(rf"mean/{re.escape(base_path)}epoch-{epoch_num}/(.+)")
-        for key in list(self.logger.name_to_value.keys()):
-            m = pattern.match(key)
-            if m:
-                self.logger.record(f"{base_path}final/{m.group(1)}", self.logger.name_to_value[key])
+        self._record_final(epoch_num)
 
     def _training_inner_loop(self, fragment_pairs, preferences: np.ndarray) -> th.Tensor:
         output = self.loss.forward(fragment_pairs, preferences, self._preference_model)
@@ -697,6 +805,89 @@ class BasicRewardTrainer(RewardTrainer):
         for name, value in output.metrics.items():
             self.logger.record(name, value.item())
         return output.loss
+
+
+class _MinibatchGraph:
+    """One reward-model minibatch step (row gather -> reward net fwd (incl. RunningNorm
+    update) -> fused Bradley-Terry loss -> backward -> AdamW step, plus the logged
+    metrics) captured as a HIP graph over device-resident dataset buffers, one graph per
+    minibatch size (full, and the epoch's last partial one); a minibatch is then an index
+    copy and a graph replay instead of ~100 eager launches. The first minibatch of each
+    size runs eagerly on a side stream (the warm-up IS that minibatch's step), the capture
+    follows. Semantics are the eager loop's with minibatch == batch and no regulariser: a
+    partial minibatch's loss is scaled by n / batch and stepped at the epoch end, which is
+    the same single step. The optimiser runs in ``capturable`` mode; gradients live in the
+    graphs' pools."""
+
+    def __init__(self, trainer: "BasicRewardTrainer", key, capacity: int, s_all, a_all, ns_all, d_all, has_gt: bool,
+                 L: int, B: int):
+        self.key, self.capacity, self.L, self.B = key, capacity, L, B
+        self.trainer = trainer
+        dev = s_all.device
+        rows = capacity * 2 * L
+        mk = lambda t: th.zeros((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        self.s, self.a, self.ns, self.d = mk(s_all), mk(a_all), mk(ns_all), mk(d_all)
+        self.prefs = th.zeros(capacity, device=dev)
+        self.gt = th.zeros(capacity, 2, L, device=dev) if has_gt else None
+        self.span = th.arange(2 * L, device=dev)
+        self.graphs: Dict[int, Tuple[th.Tensor, Any, Any]] = {}  # n -> (idx buffer, graph, metrics out)
+
+    def load(self, s_all, a_all, ns_all, d_all, prefs_all, gt, P: int) -> None:
+        n = s_all.shape[0]
+        self.s[:n].copy_(s_all)
+        self.a[:n].copy_(a_all)
+        self.ns[:n].copy_(ns_all)
+        self.d[:n].copy_(d_all)
+        self.prefs[:P].copy_(prefs_all)
+        if gt is not None:
+            self.gt[:P].copy_(gt)
+
+    def _step(self, idx: th.Tensor) -> th.Tensor:
+        tr = self.trainer
+        pm = tr._preference_model
+        n, L = idx.shape[0], self.L
+        rows = (idx[:, None] * (2 * L) + self.span).reshape(-1)
+        rews = pm.model(self.s.index_select(0, rows), self.a.index_select(0, rows), self.ns.index_select(0, rows),
+                        self.d.index_select(0, rows)).view(n, 2, L)
+        prefs = self.prefs.index_select(0, idx)
+        loss, probs = pref_ops.bradley_terry(rews[:, 0], rews[:, 1], prefs, pm.discount_factor, pm.threshold,
+                                             pm.noise_prob)
+        rec = [loss.detach(), ((probs.detach() > 0.5) == (prefs > 0.5)).float().mean()]
+        if self.gt is not None:
+            g = self.gt.index_select(0, idx)
+            gp = pref_ops.bradley_terry_probs_reference(g[:, 0], g[:, 1], pm.discount_factor, pm.threshold, pm.noise_prob)
+            rec.append(th.nn.functional.binary_cross_entropy(gp, prefs))
+        (loss * (n / tr.batch_size)).backward()
+        tr.optim.step()
+        return th.stack(rec)
+
+    def run(self, idx: th.Tensor) -> th.Tensor:
+        """One minibatch step; returns its metrics (a fresh device tensor)."""
+        n = int(idx.shape[0])
+        opt = self.trainer.optim
+        if n in self.graphs:
+            buf, graph, out = self.graphs[n]
+            buf.copy_(idx)
+            graph.replay()
+            return out.clone()
+        for grp in opt.param_groups:
+            grp["capturable"] = True
+        for st in opt.state.values():
+            if "step" in st and not st["step"].is_cuda:
+                st["step"] = st["step"].to(idx.device, th.float32)
+        buf = idx.clone()
+        side = th.cuda.Stream()
+        side.wait_stream(th.cuda.current_stream())
+        with th.cuda.stream(side):  # warm-up == this minibatch's real step
+            opt.zero_grad(set_to_none=True)
+            rec = self._step(buf)
+        th.cuda.current_stream().wait_stream(side)
+        opt.zero_grad(set_to_none=True)
+        graph = th.cuda.CUDAGraph()
+        with th.cuda.graph(graph):
+            out = self._step(buf)
+        self.graphs[n] = (buf, graph, out)
+        return rec
 
 
 class EnsembleTrainer(BasicRewardTrainer):

@@ -72,27 +72,17 @@ def supports(venv, gen_algo, reward_net) -> Tuple[bool, str]:
     return True, ""
 
 
-class DeviceAIRL(DeviceEngineMixin, AIRL):
-    """AIRL whose generator rounds run entirely on the GPU (see module docstring)."""
+class OutputNormMixin:
+    """``NormalizedRewardNet.predict_processed`` (update_stats=True) replayed on device after
+    the rollout kernel: the kernel stores the raw learned reward and the TimeLimit
+    bootstrap; ``reward_outnorm`` normalises step by step in env order and Chan-merges each
+    step's moments (all-reduced once per round under DP)."""
 
-    _host_cls_name = "algorithms.adversarial.airl.AIRL"
-
-    @staticmethod
-    def _supports(venv, gen_algo, reward_net):
-        return supports(venv, gen_algo, reward_net)
-
-    def _reward_spec(self) -> Dict[str, Any]:
-        _, shaped = _split(self._reward_net)
-        base = shaped.base
-        rnorm, rl, rh, ro = _mlp_layers(base.mlp)
-        pnorm, pl, ph, po = _mlp_layers(shaped.potential._potential_net)
-        return dict(rew=self._wave_mlp(rl, rh, ro, rnorm), pot=self._wave_mlp(pl, ph, po, pnorm), shaped=1,
-                    shaping_gamma=float(shaped.discount_factor), rew_transform=0, use_state=int(base.use_state),
-                    use_action=int(base.use_action), use_next_state=int(base.use_next_state),
-                    use_done=int(base.use_done))
+    def _output_norm(self):
+        return _split(self._reward_net)[0]
 
     def _rollout_extra_bufs(self) -> Dict[str, Any]:
-        out_norm, _ = _split(self._reward_net)
+        out_norm = self._output_norm()
         if out_norm is None:
             return {}
         if not hasattr(self, "_rew_raw"):
@@ -102,7 +92,7 @@ class DeviceAIRL(DeviceEngineMixin, AIRL):
         return {"rew_raw": self._rew_raw, "boot": self._boot}
 
     def _post_rollout_rewards(self) -> None:
-        out_norm, _ = _split(self._reward_net)
+        out_norm = self._output_norm()
         if out_norm is None:
             return
         step_stats = None
@@ -121,3 +111,23 @@ class DeviceAIRL(DeviceEngineMixin, AIRL):
                                            var=out_norm.running_var, count=self._onorm_count,
                                            eps=float(out_norm.eps), step_stats=step_stats))
         out_norm.count.copy_(self._onorm_count.to(out_norm.count.dtype).reshape(()))
+
+
+class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
+    """AIRL whose generator rounds run entirely on the GPU (see module docstring)."""
+
+    _host_cls_name = "algorithms.adversarial.airl.AIRL"
+
+    @staticmethod
+    def _supports(venv, gen_algo, reward_net):
+        return supports(venv, gen_algo, reward_net)
+
+    def _reward_spec(self) -> Dict[str, Any]:
+        _, shaped = _split(self._reward_net)
+        base = shaped.base
+        rnorm, rl, rh, ro = _mlp_layers(base.mlp)
+        pnorm, pl, ph, po = _mlp_layers(shaped.potential._potential_net)
+        return dict(rew=self._wave_mlp(rl, rh, ro, rnorm), pot=self._wave_mlp(pl, ph, po, pnorm), shaped=1,
+                    shaping_gamma=float(shaped.discount_factor), rew_transform=0, use_state=int(base.use_state),
+                    use_action=int(base.use_action), use_next_state=int(base.use_next_state),
+                    use_done=int(base.use_done))

@@ -196,30 +196,20 @@ class _FlatParams:
         raise KeyError("parameter not in flat buffer")
 
 
-class DeviceEngineMixin:
-    """Device generator rounds (rollout -> GAE -> PPO -> replay store) and the fused
-    discriminator update for an :class:`~imitation_amd.algorithms.adversarial.common.AdversarialTrainer`
-    subclass; mixed in front of GAIL (:class:`DeviceGAIL`) or AIRL
-    (:class:`imitation_amd.engine.airl.DeviceAIRL`)."""
+class DeviceGeneratorCore:
+    """Device PPO generator: env state, flat policy parameters, the fused rollout kernel
+    (policy + env + learned reward), GAE and the PPO update kernels, data-parallel plan.
+    Shared by the adversarial engines (:class:`DeviceEngineMixin`) and the preference-
+    comparison agent (:class:`imitation_amd.engine.preference.DeviceAgentTrainer`).
+    Subclasses set ``gen_algo``, ``_reward_net`` and ``debug_use_ground_truth`` and call
+    :meth:`_init_generator`."""
 
-    _host_cls_name = "the host trainer"
-
-    @staticmethod
-    def _supports(venv, gen_algo, reward_net) -> Tuple[bool, str]:
-        return supports(venv, gen_algo, reward_net)
-
-    def __init__(self, *, demonstrations, demo_batch_size: int, venv, gen_algo: PPO, reward_net: reward_nets.RewardNet, **kwargs):
-        ok, why = self._supports(venv, gen_algo, reward_net)
-        if not ok:
-            raise ValueError(f"{type(self).__name__} not applicable: {why}; use {self._host_cls_name}")
-        super().__init__(demonstrations=demonstrations, demo_batch_size=demo_batch_size, venv=venv, gen_algo=gen_algo,
-                         reward_net=reward_net, **kwargs)
+    def _init_generator(self, venv) -> None:
         self._native = _unwrap_native(venv)
         self._C = ops.native()
-        self._dev = gen_algo.device
+        self._dev = self.gen_algo.device
         self._setup_engine()
         self._setup_dp()
-        self._setup_fused_disc()
 
     # ------------------------------------------------------------------ setup
     def _setup_engine(self) -> None:
@@ -236,7 +226,7 @@ class DeviceEngineMixin:
         obs0 = nat.reset()
         st = nat.get_state()
         self.state = th.as_tensor(st["state"], device=dev).float().contiguous()
-        self.rng = th.as_tensor(st["rng"].astype(np.int64), device=dev).contiguous()
+        self.env_rng = th.as_tensor(st["rng"].astype(np.int64), device=dev).contiguous()
         self.elapsed = th.as_tensor(st["elapsed"].astype(np.int32), device=dev).contiguous()
         self.ep_ret = th.zeros(self.N, device=dev)
         self.cur_obs = th.as_tensor(np.asarray(obs0, np.float32), device=dev).reshape(self.N, self.D).contiguous()
@@ -276,12 +266,6 @@ class DeviceEngineMixin:
         self.stats = z(5)
         self._seed = int(np.random.randint(0, 2**62)) ^ (pdist.rank() * 0x9E3779B97F4A7C15 & ((1 << 62) - 1))
         self._step0 = 0
-        cap = self._gen_replay_buffer.capacity
-        obs_dt = th.float32
-        act_shape = () if self.discrete else (self.A,)
-        self._gen_dev = buffer_mod.DeviceBuffer(
-            cap, {"obs": (D,), "acts": act_shape, "next_obs": (D,), "dones": ()},
-            {"obs": obs_dt, "acts": th.int64 if self.discrete else th.float32, "next_obs": obs_dt, "dones": th.bool}, dev)
         self._ppo_static = self._ppo_args_static()
         self._ep_lens_running = np.zeros(self.N, dtype=np.int64)
 
@@ -335,7 +319,7 @@ class DeviceEngineMixin:
         algo: PPO = self.gen_algo
         pol = algo.policy
         args = dict(env=self._native.env_id, max_steps=self.max_steps, T=self.T, N=self.N, gamma=float(algo.gamma),
-                    seed=int(self._seed), step0=int(self._step0), state=self.state, rng=self.rng, elapsed=self.elapsed,
+                    seed=int(self._seed), step0=int(self._step0), state=self.state, rng=self.env_rng, elapsed=self.elapsed,
                     ep_ret=self.ep_ret, cur_obs=self.cur_obs, cur_start=self.cur_start,
                     pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
                     vf=self._wave_mlp(self.vf_layers, self.hidden_act, 0, self.pol_norm),
@@ -463,6 +447,11 @@ class DeviceEngineMixin:
         norm.running_var.copy_(rv / tot)
         self.norm_count.add_(cnt)
 
+    def sync_env_to_host(self) -> None:
+        """Copy the device env state back into the native host env (e.g. before host-side evaluation)."""
+        self._native.set_state({"state": self.state.cpu().numpy(), "rng": self.env_rng.cpu().numpy(),
+                                "elapsed": self.elapsed.cpu().numpy().astype(np.int64)})
+
     def _stage_rollout_to_host(self):
         """Async D2H copy of (dones, episode returns) into pinned buffers; returns the event
         that marks them ready."""
@@ -474,6 +463,33 @@ class DeviceEngineMixin:
         ev.record()
         self._host_staged = True
         return ev
+
+class DeviceEngineMixin(DeviceGeneratorCore):
+    """Device generator rounds (rollout -> GAE -> PPO -> replay store) and the fused
+    discriminator update for an :class:`~imitation_amd.algorithms.adversarial.common.AdversarialTrainer`
+    subclass; mixed in front of GAIL (:class:`DeviceGAIL`) or AIRL
+    (:class:`imitation_amd.engine.airl.DeviceAIRL`)."""
+
+    _host_cls_name = "the host trainer"
+
+    @staticmethod
+    def _supports(venv, gen_algo, reward_net) -> Tuple[bool, str]:
+        return supports(venv, gen_algo, reward_net)
+
+    def __init__(self, *, demonstrations, demo_batch_size: int, venv, gen_algo: PPO, reward_net: reward_nets.RewardNet, **kwargs):
+        ok, why = self._supports(venv, gen_algo, reward_net)
+        if not ok:
+            raise ValueError(f"{type(self).__name__} not applicable: {why}; use {self._host_cls_name}")
+        super().__init__(demonstrations=demonstrations, demo_batch_size=demo_batch_size, venv=venv, gen_algo=gen_algo,
+                         reward_net=reward_net, **kwargs)
+        self._init_generator(venv)
+        D = self.D
+        act_shape = () if self.discrete else (self.A,)
+        self._gen_dev = buffer_mod.DeviceBuffer(
+            self._gen_replay_buffer.capacity, {"obs": (D,), "acts": act_shape, "next_obs": (D,), "dones": ()},
+            {"obs": th.float32, "acts": th.int64 if self.discrete else th.float32, "next_obs": th.float32,
+             "dones": th.bool}, self._dev)
+        self._setup_fused_disc()
 
     def _store_generator_samples(self) -> None:
         """Replay-buffer content identical to BufferingWrapper -> flatten -> FIFO store."""
@@ -771,7 +787,7 @@ class DeviceEngineMixin:
             self.logger.dump(self._global_step)
 
     # ------------------------------------------------------------------ checkpoint / resume
-    _ENGINE_TENSORS = ("exp_avg", "exp_avg_sq", "adam_step", "state", "rng", "elapsed", "ep_ret", "cur_obs", "cur_start")
+    _ENGINE_TENSORS = ("exp_avg", "exp_avg_sq", "adam_step", "state", "env_rng", "elapsed", "ep_ret", "cur_obs", "cur_start")
 
     def engine_state(self) -> Dict[str, Any]:
         """Device-engine state not covered by module ``state_dict``s (used by
@@ -796,11 +812,6 @@ class DeviceEngineMixin:
         self._ep_lens_running = st["ep_lens_running"].numpy().copy()
         self._gen_dev._idx, self._gen_dev._n_data = st["gen_dev_idx"], st["gen_dev_n"]
         self.sync_env_to_host()
-
-    def sync_env_to_host(self) -> None:
-        """Copy the device env state back into the native host env (e.g. before host-side evaluation)."""
-        self._native.set_state({"state": self.state.cpu().numpy(), "rng": self.rng.cpu().numpy(),
-                                "elapsed": self.elapsed.cpu().numpy().astype(np.int64)})
 
 
 class DeviceGAIL(DeviceEngineMixin, GAIL):

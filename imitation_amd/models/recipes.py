@@ -201,9 +201,11 @@ def dagger_pong(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "Pong
 
 def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "seals/Walker2d-v1",
                         num_iterations: int = 5, fragment_length: int = 100, n_steps: int = 256,
-                        log_dir: Optional[str] = None, **overrides) -> Built:
+                        log_dir: Optional[str] = None, engine: str = "auto", **overrides) -> Built:
     """Preference comparisons on Walker2d: PPO agent on the learned reward, ``BasicRewardNet``
-    (RunningNorm input), synthetic oracle preferences from the env's true reward."""
+    (RunningNorm input), synthetic oracle preferences from the env's true reward. The agent
+    trains and samples on the GPU (:class:`~imitation_amd.engine.preference.DeviceAgentTrainer`)
+    when eligible."""
     from imitation_amd.algorithms import preference_comparisons as pc
     from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
     from imitation_amd.rewards.reward_nets import BasicRewardNet
@@ -219,8 +221,16 @@ def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str
     agent = PPO(FeedForward32Policy, venv, n_steps=n_steps, batch_size=64, n_epochs=5, device=dev, seed=seed,
                 policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor,
                                    features_extractor_kwargs=dict(normalize_class=RunningNorm)))
-    gen = pc.AgentTrainer(algorithm=agent, reward_fn=reward_net, venv=venv, exploration_frac=0.05, rng=rng,
-                          custom_logger=log)
+    gen_cls = pc.AgentTrainer
+    if engine in ("auto", "device"):
+        from imitation_amd.engine import preference as device_pref
+
+        ok, why = device_pref.supports(venv, agent, reward_net)
+        if ok:
+            gen_cls = device_pref.DeviceAgentTrainer
+        elif engine == "device":
+            raise ValueError(f"device engine not applicable: {why}")
+    gen = gen_cls(algorithm=agent, reward_fn=reward_net, venv=venv, exploration_frac=0.05, rng=rng, custom_logger=log)
     kw = dict(fragmenter=pc.RandomFragmenter(rng=rng, custom_logger=log),
               preference_gatherer=pc.SyntheticGatherer(rng=rng, custom_logger=log),
               reward_trainer=pc.BasicRewardTrainer(preference_model=pc.PreferenceModel(reward_net),
@@ -231,7 +241,8 @@ def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str
     kw.update(overrides)
     # all components carry their own seeded rng, so (as the reference requires) none is passed here
     trainer = pc.PreferenceComparisons(gen, reward_net, num_iterations=num_iterations, custom_logger=log, rng=None, **kw)
-    return Built(trainer, venv, "preference_walker2d", env_id, n_steps * n_envs, {"agent": agent})
+    return Built(trainer, venv, "preference_walker2d", env_id, n_steps * n_envs,
+                 {"agent": agent, "engine": "device" if gen_cls is not pc.AgentTrainer else "host"})
 
 
 def bc_cartpole(device=None, seed: int = 0, env_id: str = "CartPole-v1", n_demo_timesteps: int = 4000,

@@ -213,7 +213,7 @@ def test_fused_disc_grads_and_norms_match_reference():
     assert int(tr.pol_norm.count) == int(pnorm.count)
     g = tr._disc_ws["grads"]
     # backward MFMA operands (dZ, H) are bf16 as well: elementwise error ~1e-3 of the largest grad
-    th.testing.assert_close(g, grads_ref, rtol=2e-2, atol=1.5e-3 * float(grads_ref.abs().max()))
+    th.testing.assert_close(g, grads_ref, rtol=2e-2, atol=2.5e-3 * float(grads_ref.abs().max()))
     assert float(th.nn.functional.cosine_similarity(g, grads_ref, dim=0)) > 0.9999
     s = tr._disc_stats_dict(stats.tolist())
     from imitation_amd.algorithms.adversarial.common import compute_train_stats
