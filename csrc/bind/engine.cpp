@@ -111,6 +111,38 @@ void rollout(py::dict d) {
   IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
 }
 
+void reward_batch(py::dict d) {
+  ia::RewardBatchArgs a{};
+  a.rows = ival(d, "rows");
+  a.D = ival(d, "D");
+  a.A = ival(d, "A");
+  a.n_actions = ival(d, "n_actions", 0);
+  a.obs = tptr<const float>(d, "obs");
+  a.acts = tptr<const float>(d, "acts");
+  a.next_obs = tptr<const float>(d, "next_obs");
+  a.dones = tptr<const float>(d, "dones");
+  a.boot = tptr<const float>(d, "boot");
+  a.rew = wave_mlp(d["rew"].cast<py::dict>());
+  a.use_state = ival(d, "use_state", 1);
+  a.use_action = ival(d, "use_action", 1);
+  a.use_next_state = ival(d, "use_next_state", 0);
+  a.use_done = ival(d, "use_done", 0);
+  a.rew_transform = ival(d, "rew_transform", 0);
+  a.shaped = ival(d, "shaped", 0);
+  if (a.shaped) {
+    a.pot = wave_mlp(d["pot"].cast<py::dict>());
+    a.shaping_gamma = (float)fval(d, "shaping_gamma", 0.99);
+    TORCH_CHECK(a.pot.dims[0] == a.D, "potential input dim");
+  }
+  const int din = (a.use_state ? a.D : 0) + (a.use_action ? (a.n_actions > 0 ? a.n_actions : a.A) : 0) +
+                  (a.use_next_state ? a.D : 0) + (a.use_done ? 1 : 0);
+  TORCH_CHECK(a.rew.dims[0] == din, "reward MLP input dim ", a.rew.dims[0], " != ", din);
+  TORCH_CHECK(din <= ia::kWaveMaxDim, "reward input wider than a wave");
+  a.rewards = tptr<float>(d, "rewards");
+  a.rew_raw = tptr<float>(d, "rew_raw", true);
+  IA_HIP_CHECK2(ia::reward_batch_launch(a, ia_stream()));
+}
+
 void reward_outnorm(py::dict d) {
   ia::OutNormArgs a{};
   a.T = ival(d, "T");
@@ -235,6 +267,7 @@ size_t ppo_lds(py::dict d) {
 
 void register_engine(py::module& m) {
   m.def("engine_rollout", &rollout, "T-step device rollout (policy + env + learned reward) for N envs");
+  m.def("engine_reward_batch", &reward_batch, "learned reward of all rollout transitions in parallel");
   m.def("engine_reward_outnorm", &reward_outnorm, "NormalizedRewardNet output normalisation over a rollout");
   m.def("engine_ppo_update", &ppo_update, "persistent PPO update / DP minibatch grads / apply");
   m.def("engine_ppo_path", &ppo_path, "kernel used by engine_ppo_update mode 0 (rc | lds)");

@@ -84,6 +84,30 @@ struct RolloutArgs {
   unsigned long long* prof;  // optional [N][4] cycle counters: policy, env, reward, other
 };
 
+// Learned reward of a finished rollout, all T*N transitions in parallel (the reward
+// does not feed back into the dynamics, so it leaves the rollout's serial step chain):
+// r = transform(rew(s, a, s', d)) [+ shaping_gamma (1 - d) pot(s') - pot(s)];
+// rewards[i] = r + boot[i]; rew_raw[i] = r when given (NormalizedRewardNet replay).
+struct RewardBatchArgs {
+  int rows;       // T * N, row = t * N + n
+  int D;          // obs dim
+  int A;          // act buffer width (1 for Categorical)
+  int n_actions;  // >0: Categorical (acts hold the index)
+  const float* obs;
+  const float* acts;  // env (clipped) actions
+  const float* next_obs;
+  const float* dones;
+  const float* boot;
+  WaveMLP rew;
+  int use_state, use_action, use_next_state, use_done;
+  int rew_transform;
+  int shaped;
+  WaveMLP pot;
+  float shaping_gamma;
+  float* rewards;
+  float* rew_raw;  // optional
+};
+
 // NormalizedRewardNet output normalisation over a rollout, step by step in env order:
 // rewards[t][n] = (rew_raw[t][n] - mean) / sqrt(var + eps) + boot[t][n], then the running
 // (mean, var, count) are Chan-merged with step t's batch moments (over the N envs, or the

@@ -617,6 +617,58 @@ __global__ __launch_bounds__(64) void reward_outnorm_kernel(OutNormArgs a) {
   }
 }
 
+// Reward of many transitions: one wave per row, rows strided over the grid; the MLP
+// images are staged in LDS once per workgroup. Same fp32 arithmetic (and input layout)
+// as the in-rollout reward, so the result is bit-identical to it.
+__global__ __launch_bounds__(64) void reward_batch_kernel(RewardBatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_raw[];
+  lf* p = (lf*)lds_raw;
+  const int lane = threadIdx.x;
+  LdsMLP rw, pt;
+  p = load_mlp(a.rew, rw, p);
+  if (a.shaped) p = load_mlp(a.pot, pt, p);
+  __syncthreads();
+  const int D = a.D, A = a.A;
+  for (int row = blockIdx.x; row < a.rows; row += gridDim.x) {
+    const size_t r64 = (size_t)row;
+    const float o = lane < D ? a.obs[r64 * D + lane] : 0.f;
+    const float o_next = lane < D ? a.next_obs[r64 * D + lane] : 0.f;
+    const float a_env = lane < A ? a.acts[r64 * A + lane] : 0.f;
+    const bool done = a.dones[r64] > 0.5f;
+    float x = 0.f;
+    int off = 0;
+    if (a.use_state) { if (lane < D) x = o; off += D; }
+    if (a.use_action) {
+      if (a.n_actions > 0) {
+        const int k = (int)bcast(a_env, 0);
+        if (lane >= off && lane < off + a.n_actions) x = (lane - off) == k ? 1.f : 0.f;
+        off += a.n_actions;
+      } else {
+        const float av = __shfl(a_env, lane - off);
+        if (lane >= off && lane < off + A) x = av;
+        off += A;
+      }
+    }
+    if (a.use_next_state) {
+      const float v = __shfl(o_next, lane - off);
+      if (lane >= off && lane < off + D) x = v;
+      off += D;
+    }
+    if (a.use_done) { if (lane == off) x = done ? 1.f : 0.f; off += 1; }
+    const float logit = bcast(wave_mlp(rw, x), 0);
+    float r = a.rew_transform == REW_SOFTPLUS ? (logit > 0.f ? logit + log1pf(expf(-logit)) : log1pf(expf(logit))) : logit;
+    if (a.shaped) {
+      const float phi_s = bcast(wave_mlp(pt, o), 0);
+      const float phi_n = done ? 0.f : bcast(wave_mlp(pt, o_next), 0);
+      r += a.shaping_gamma * phi_n - phi_s;
+    }
+    if (lane == 0) {
+      if (a.rew_raw) a.rew_raw[r64] = r;
+      a.rewards[r64] = r + a.boot[r64];
+    }
+  }
+}
+
 size_t rollout_lds_bytes(const RolloutArgs& a) {
   int f = mlp_lds_floats(a.pi) + mlp_lds_floats(a.vf) + (a.rew_enabled ? mlp_lds_floats(a.rew) : 0);
   if (a.rew_enabled && a.shaped) f += mlp_lds_floats(a.pot);
@@ -630,6 +682,17 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   const size_t lds = rollout_lds_bytes(a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rollout_kernel, dim3(a.N), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t reward_batch_launch(const RewardBatchArgs& a, hipStream_t s) {
+  if (a.rows <= 0) return hipSuccess;
+  if (a.D > kEngineMaxObs || a.A > kWaveMaxDim) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(mlp_lds_floats(a.rew) + (a.shaped ? mlp_lds_floats(a.pot) : 0)) * sizeof(float);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const int rows_per_wg = 4;  // ~4 workgroups per CU, their waves interleave on the SIMDs
+  const int grid = (a.rows + rows_per_wg - 1) / rows_per_wg;
+  hipLaunchKernelGGL(reward_batch_kernel, dim3(grid), dim3(64), lds, s, a);
   return hipGetLastError();
 }
 

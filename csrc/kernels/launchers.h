@@ -84,6 +84,7 @@ hipError_t pref_loss_bwd(const float* coef, const float* gout, int P, int L, flo
 size_t rollout_lds_bytes(const RolloutArgs& a);
 hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s);
 hipError_t reward_outnorm_launch(const OutNormArgs& a, hipStream_t s);
+hipError_t reward_batch_launch(const RewardBatchArgs& a, hipStream_t s);
 
 // ---- ppo_rc.hip: register-chained single-rank PPO update (falls back to ppo.hip)
 bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes);

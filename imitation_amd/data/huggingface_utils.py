@@ -27,8 +27,12 @@ def _to_jsonable(v: Any) -> Any:
     if isinstance(v, list):
         return [_to_jsonable(x) for x in v]
     if isinstance(v, np.ndarray):
-        return {"py/object": "numpy.ndarray", "dtype": str(v.dtype), "shape": list(v.shape),
-                "values": _to_jsonable(v.reshape(-1).tolist())}
+        flat = v.reshape(-1)
+        if flat.dtype.kind in "biu" or (flat.dtype.kind == "f" and bool(np.isfinite(flat).all())):
+            values = flat.tolist()  # already plain JSON scalars: no per-element pass (84x84x4 frames)
+        else:
+            values = _to_jsonable(flat.tolist())
+        return {"py/object": "numpy.ndarray", "dtype": str(v.dtype), "shape": list(v.shape), "values": values}
     if isinstance(v, (np.bool_,)):
         return bool(v)
     if isinstance(v, np.integer):
@@ -46,7 +50,12 @@ def _from_jsonable(v: Any) -> Any:
         if len(v) == 1 and isinstance(v.get("py/tuple"), list):
             return tuple(_from_jsonable(x) for x in v["py/tuple"])
         if v.get("py/object") == "numpy.ndarray" and "values" in v:
-            arr = np.asarray(_from_jsonable(v["values"]), dtype=v.get("dtype", None))
+            try:  # plain numeric lists convert in C; tagged (nan/inf) entries need the walk
+                arr = np.asarray(v["values"], dtype=v.get("dtype", None))
+                if arr.dtype == object:
+                    raise TypeError
+            except (TypeError, ValueError):
+                arr = np.asarray(_from_jsonable(v["values"]), dtype=v.get("dtype", None))
             return arr.reshape(v.get("shape", arr.shape))
         if len(v) == 1 and isinstance(v.get("py/float"), str):
             return float(v["py/float"])

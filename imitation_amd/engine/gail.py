@@ -35,6 +35,7 @@ should use the host-loop trainers.
 
 from __future__ import annotations
 
+import os
 import time
 from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple
 
@@ -325,13 +326,34 @@ class DeviceGeneratorCore:
                     vf=self._wave_mlp(self.vf_layers, self.hidden_act, 0, self.pol_norm),
                     log_std=pol.log_std.detach() if self.has_log_std else None, act_low=self.act_low,
                     act_high=self.act_high, n_actions=self.A if self.discrete else 0)
+        args.update(self.buf)
+        extra = self._rollout_extra_bufs()
+        args.update(extra)
+        inline = os.environ.get("IMITATION_AMD_INLINE_REWARD", "0") == "1"
         if self.debug_use_ground_truth:
             args.update(rew_enabled=0)
-        else:
+            self._C.engine_rollout(args)
+        elif inline:  # learned reward evaluated inside the step loop
             args.update(rew_enabled=1, **self._reward_spec())
-        args.update(self.buf)
-        args.update(self._rollout_extra_bufs())
-        self._C.engine_rollout(args)
+            self._C.engine_rollout(args)
+        else:
+            # the learned reward does not feed back into the dynamics: the rollout kernel only
+            # records the TimeLimit bootstrap, and every transition's reward is computed
+            # afterwards in one parallel pass (bit-identical to the in-loop evaluation)
+            if "boot" not in extra:
+                if not hasattr(self, "_boot_scratch"):
+                    self._boot_scratch = th.zeros(self.T, self.N, device=self._dev)
+                    self._rr_scratch = th.zeros(self.T, self.N, device=self._dev)
+                args.update(boot=self._boot_scratch, rew_raw=self._rr_scratch)
+            args.update(rew_enabled=0)
+            self._C.engine_rollout(args)
+            b = self.buf
+            rb = dict(rows=self.T * self.N, D=self.D, A=1 if self.discrete else self.A,
+                      n_actions=self.A if self.discrete else 0, obs=b["obs_buf"], acts=b["act_env"],
+                      next_obs=b["next_obs"], dones=b["dones"], boot=args["boot"], rewards=b["rewards"],
+                      rew_raw=extra.get("rew_raw"))
+            rb.update(self._reward_spec())
+            self._C.engine_reward_batch(rb)
         if not self.debug_use_ground_truth:
             self._post_rollout_rewards()
         self._step0 += self.T
