@@ -33,6 +33,7 @@ from imitation_amd.policies import base as policy_base
 from imitation_amd.rl import torch_layers
 from imitation_amd.rl.policies import ActorCriticPolicy, get_device
 from imitation_amd.util import logger as imit_logger
+from imitation_amd.utils import graphs
 from imitation_amd.util import util
 
 
@@ -205,6 +206,25 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         acts = util.safe_to_tensor(batch["acts"], device=self.policy.device)
         return obs, acts
 
+    def _graphed_step(self) -> Optional[graphs.GraphedTrainStep]:
+        """HIP-graph minibatch step when it has the eager loop's semantics: GPU policy, no
+        gradient accumulation (minibatch == batch), no DP gradient bucket, an optimiser with
+        a capturable mode. Disabled with ``IMITATION_AMD_BC_GRAPH=0``."""
+        if (self.minibatch_size != self.batch_size or self._grad_bucket is not None
+                or not graphs.graphs_enabled(self.policy.device, "IMITATION_AMD_BC_GRAPH")
+                or not graphs.supports_capture(self.optimizer)):
+            return None
+        g = getattr(self, "_graph_step", None)
+        if g is None or g.optimizer is not self.optimizer:
+            def step(obs, acts):
+                metrics = self.loss_calculator(self.policy, obs, acts)
+                metrics.loss.backward()
+                self.optimizer.step()
+                return metrics
+
+            g = self._graph_step = graphs.GraphedTrainStep(step, self.optimizer)
+        return g
+
     def _zero_grad(self):
         self.optimizer.zero_grad(set_to_none=self._grad_bucket is None)
         if self._grad_bucket is not None:
@@ -232,11 +252,12 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         batches_with_stats = enumerate_batches(demonstration_batches)
         state: Dict[str, Any] = {}
 
-        def process_batch():
-            if self._grad_bucket is not None:
-                self._grad_bucket.allreduce()
-            self.optimizer.step()
-            self._zero_grad()
+        def process_batch(stepped: bool = False):
+            if not stepped:
+                if self._grad_bucket is not None:
+                    self._grad_bucket.allreduce()
+                self.optimizer.step()
+                self._zero_grad()
             if state["batch_num"] % log_interval == 0:
                 rollout_stats = compute_rollout_stats(self.policy, self.rng)
                 self._bc_logger.log_batch(state["batch_num"], state["minibatch_size"], state["num_samples_so_far"],
@@ -245,9 +266,20 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
                 on_batch_end()
 
         self._zero_grad()
+        graphed = self._graphed_step()
         num_samples_so_far = 0
         for (batch_num, minibatch_size, num_samples_so_far), batch in batches_with_stats:
             obs, acts = self._prepare_batch(batch)
+            if graphed is not None and isinstance(obs, th.Tensor) and minibatch_size == self.batch_size:
+                # whole minibatch step (fwd + bwd + optimizer) as one HIP-graph replay
+                metrics = graphed(obs, acts)
+                batch_num = batch_num * self.minibatch_size // self.batch_size
+                state.update(batch_num=batch_num, minibatch_size=minibatch_size, num_samples_so_far=num_samples_so_far,
+                             metrics=metrics)
+                process_batch(stepped=True)
+                continue
+            if graphed is not None and graphed.n_captures:
+                self._zero_grad()  # p.grad still holds the last replay's gradients
             metrics = self.loss_calculator(self.policy, obs, acts)
             loss = metrics.loss * minibatch_size / self.batch_size
             loss.backward()

@@ -98,3 +98,38 @@ def test_bc_policy_save_load(tmp_path, cartpole_venv, expert_transitions, rng):
 def test_bc_loss_calculator_values():
     calc = bc.BehaviorCloningLossCalculator(ent_weight=1e-3, l2_weight=0.0)
     assert calc.ent_weight == 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env_id", ["CartPole-v1", "PongNoFrameskip-v4"])
+def test_bc_graph_replay_matches_eager(monkeypatch, env_id):
+    """The HIP-graph BC step (utils/graphs.GraphedTrainStep) == the eager step: same
+    parameters after several batches and the same logged metrics (both with the
+    capturable Adam arithmetic)."""
+    import torch as th
+
+    from imitation_amd.algorithms import bc as bc_mod
+    from imitation_amd.data import rollout
+    from imitation_amd.util import logger as imit_logger
+    from imitation_amd.util.util import make_vec_env
+
+    venv = make_vec_env(env_id, rng=np.random.default_rng(0), n_envs=2)
+    trajs = rollout.generate_trajectories(None, venv, rollout.make_min_timesteps(300), rng=np.random.default_rng(1))
+    demos = rollout.flatten_trajectories(trajs)
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IMITATION_AMD_BC_GRAPH", mode)
+        th.manual_seed(0)
+        np.random.seed(0)  # the demo loader's shuffling seed comes from the global numpy RNG
+        log = imit_logger.configure(format_strs=[])
+        tr = bc_mod.BC(observation_space=venv.observation_space, action_space=venv.action_space,
+                       rng=np.random.default_rng(2), demonstrations=demos, batch_size=32, device="cuda",
+                       custom_logger=log)
+        for g in tr.optimizer.param_groups:
+            g["capturable"] = True
+        tr.train(n_batches=6, log_interval=2, progress_bar=False)
+        g = getattr(tr, "_graph_step", None)
+        assert (g is not None and g.n_replays == 5) == (mode == "1")
+        out.append([p.detach().clone() for p in tr.policy.parameters()])
+    for a, b in zip(*out):
+        th.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
