@@ -83,6 +83,17 @@ __device__ lf* load_mlp(const WaveMLP& m, LdsMLP& out, lf* lds) {
   return lds;
 }
 
+// The rollout / reward kernels run ONE wave per workgroup: lanes exchange data through
+// LDS, and a wave's LDS accesses complete in issue order, so a wavefront-scope fence (a
+// compiler ordering point) replaces __syncthreads(). The workgroup-scope release of
+// __syncthreads() would also wait for every outstanding global store of the step
+// (vmcnt(0)) -- an L2 round trip on the serial step chain.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
@@ -260,15 +271,31 @@ __device__ __forceinline__ float wave_max(float v) {
 // readlane in joint order (the host runtime's summation order). Same equations as
 // ia::loco_step (csrc/include/ia/envs.h); the serial per-joint chain of the host
 // version is what made the env step the longest part of a rollout step.
-__device__ float loco_step_wave(const LocoParams& p, float* s, const float* a_in) {
+// Per-lane joint constants, loaded once per kernel (a lane-indexed kernarg read is a
+// vector memory load; inside the step it would wait behind the step's global stores).
+struct LocoLane {
+  float gear, stiff, damp, thrust;
+};
+
+__device__ LocoLane loco_lane(const LocoParams& p) {
+  const int lane = threadIdx.x;
+  const bool jl = lane < p.nj;
+  return {jl ? p.gear[lane] : 0.f, jl ? p.stiff[lane] : 0.f, jl ? p.damp[lane] : 0.f, jl ? p.thrust[lane] : 0.f};
+}
+
+// The env state / action scratch live in LDS: accessed through LDS-typed pointers
+// (ds_read / ds_write, lgkmcnt) rather than generic ones -- a flat access waits on vmcnt,
+// i.e. behind every global store the step has issued (gfx9 counts stores in vmcnt).
+__device__ float loco_step_wave(const LocoParams& p, const LocoLane& ll, float* s_gen, const float* a_gen) {
+  lf* s = (lf*)s_gen;
+  const lf* a_in = (const lf*)a_gen;
   const int lane = threadIdx.x;
   const int nq = loco_nq(p), nj = p.nj, jq = p.nq_root, jv = p.nv_root;
   const bool jl = lane < nj;
   const float a = jl ? fminf(fmaxf(a_in[lane], -1.f), 1.f) : 0.f;
   float q = jl ? s[jq + lane] : 0.f;
   float qd = jl ? s[nq + jv + lane] : 0.f;
-  const float gear = jl ? p.gear[lane] : 0.f, stiff = jl ? p.stiff[lane] : 0.f;
-  const float damp = jl ? p.damp[lane] : 0.f, tc = jl ? p.thrust[lane] : 0.f;
+  const float gear = ll.gear, stiff = ll.stiff, damp = ll.damp, tc = ll.thrust;
   float ctrl = 0.f, pitch = 0.f;
   for (int j = 0; j < nj; ++j) {
     const float aj = bcast(a, j);
@@ -316,7 +343,7 @@ __device__ float loco_step_wave(const LocoParams& p, float* s, const float* a_in
     if (qn < -1.2f) { qn = -1.2f; if (qd < 0) qd = 0.f; }
     q = qn;
   }
-  __syncthreads();
+  wave_sync();
   if (jl) {
     s[jq + lane] = q;
     s[nq + jv + lane] = qd;
@@ -328,13 +355,14 @@ __device__ float loco_step_wave(const LocoParams& p, float* s, const float* a_in
       if (i < p.nv_root) s[nq + i] = rv[i];
     }
   }
-  __syncthreads();
+  wave_sync();
   const float dt_total = dt * p.frame_skip;
   return p.fwd_weight * (rq[0] - x_before) / dt_total + p.healthy_reward - p.ctrl_cost * ctrl;
 }
 
 // Observation of a locomotion state, one feature per lane.
-__device__ float loco_obs_lane(const LocoParams& p, const float* s) {
+__device__ float loco_obs_lane(const LocoParams& p, const float* s_gen) {
+  const lf* s = (const lf*)s_gen;
   const int lane = threadIdx.x;
   const int nq = loco_nq(p), nv = loco_nv(p);
   const int npos = nq - p.obs_skip;
@@ -374,8 +402,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
   float* ob = st + kMaxState;  // [kEngineMaxObs]
   float* act = ob + kEngineMaxObs;  // [kWaveMaxDim]
   for (int i = lane; i < S; i += 64) st[i] = a.state[(size_t)n * S + i];
-  __syncthreads();
+  wave_sync();
 
+  const LocoLane ll = P.kind == ENV_LOCO ? loco_lane(P.loco) : LocoLane{0.f, 0.f, 0.f, 0.f};
   float o = lane < D ? a.cur_obs[(size_t)n * D + lane] : 0.f;
   float start = a.cur_start[n];
   uint64_t rng = a.rng[n];
@@ -450,24 +479,24 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
     if (lane < A) {
       a.act_raw[row * A + lane] = a_raw;
       a.act_env[row * A + lane] = a_env;
-      act[lane] = a_env;
+      ((lf*)act)[lane] = a_env;
     }
     // ---- env step (lane 0), SB3 auto-reset + TimeLimit + Monitor
     c_pol += clock64() - c0;
     c0 = clock64();
-    __syncthreads();
+    wave_sync();
     int term = 0;
     float r_env = 0.f;
     float o_next;  // terminal obs when done
     if (P.kind == ENV_LOCO) {
-      r_env = loco_step_wave(P.loco, st, act);
+      r_env = loco_step_wave(P.loco, ll, st, act);
       o_next = loco_obs_lane(P.loco, st);
     } else {
       if (lane == 0) {
         r_env = env_step(P, st, act, &term, rng);
         env_obs(P, st, ob);
       }
-      __syncthreads();
+      wave_sync();
       term = __builtin_amdgcn_readfirstlane(term);
       r_env = bcast(r_env, 0);
       o_next = lane < D ? ob[lane] : 0.f;
@@ -531,12 +560,12 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
     }
     if (lane < D) a.next_obs[row * D + lane] = o_next;
     if (done) {
-      __syncthreads();
+      wave_sync();
       if (lane == 0) {
         env_reset(P, st, rng);
         env_obs(P, st, ob);
       }
-      __syncthreads();
+      wave_sync();
       elapsed = 0;
       ep_ret = 0.f;
       o = lane < D ? ob[lane] : 0.f;
@@ -547,7 +576,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(RolloutArgs a) {
   }
   // bootstrap value of the final observation
   const float lastv = bcast(wave_mlp(vf, o), 0);
-  __syncthreads();
+  wave_sync();
   for (int i = lane; i < S; i += 64) a.state[(size_t)n * S + i] = st[i];
   if (lane < D) a.cur_obs[(size_t)n * D + lane] = o;
   if (lane == 0) {
@@ -627,7 +656,7 @@ __global__ __launch_bounds__(64) void reward_batch_kernel(RewardBatchArgs a) {
   LdsMLP rw, pt;
   p = load_mlp(a.rew, rw, p);
   if (a.shaped) p = load_mlp(a.pot, pt, p);
-  __syncthreads();
+  wave_sync();
   const int D = a.D, A = a.A;
   for (int row = blockIdx.x; row < a.rows; row += gridDim.x) {
     const size_t r64 = (size_t)row;

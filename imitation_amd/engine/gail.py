@@ -9,9 +9,11 @@ never leaves the GPU:
 reference (host loop)  this engine
 =====================  ==========================================================
 SB3 collect_rollouts:  ``engine_rollout`` -- ONE kernel runs n_steps x n_envs of
-policy fwd, VecEnv     policy sampling, env physics (native model), learned
-pipes, reward wrapper  reward ``softplus(D(s,a))``, TimeLimit bootstrap; buffers
-numpy<->device copies  are written straight into HBM
+policy fwd, VecEnv     policy sampling, env physics (native model) and the
+pipes, reward wrapper  TimeLimit bootstrap; buffers are written straight into
+numpy<->device copies  HBM. The learned reward ``softplus(D(s,a))`` does not feed
+                       back into the dynamics: ``engine_reward_batch`` computes it
+                       for all T x N transitions in one parallel pass afterwards
 RolloutBuffer GAE      ``gae`` kernel (one lane per env)
 (python loop)
 PPO.train              ``engine_ppo_update`` -- ONE persistent workgroup runs all
