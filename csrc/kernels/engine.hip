@@ -331,11 +331,15 @@ __device__ float loco_step_wave(const LocoParams& p, const LocoLane& ll, float* 
 #pragma unroll
     for (int i = 1; i < 8; ++i) {
       if (i < p.nq_root) {
-        const int vi = i < p.nv_root ? i : (i % p.nv_root);
-        float v = 0.f;
+        if (i < p.nv_root) {  // (uniform branch) static register index: no select chain
+          rq[i] += dt * rv[i] * 1.f;
+        } else {  // free-joint quaternion slots (3D bodies only)
+          const int vi = i % p.nv_root;
+          float v = 0.f;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v = u == vi ? rv[u] : v;
-        rq[i] += dt * v * (i < p.nv_root ? 1.f : 0.1f);
+          for (int u = 0; u < 8; ++u) v = u == vi ? rv[u] : v;
+          rq[i] += dt * v * 0.1f;
+        }
       }
     }
     float qn = q + dt * qd;
