@@ -27,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,13 +52,63 @@ def parse():
 BASELINE_VALUE = None  # the reference publishes no throughput number
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N rank processes (one per GPU, RCCL) and
+    return the worst exit code. Runs before anything touches the GPU (counting devices
+    does not initialise HIP), so the children are fresh processes, not exec'd images.
+    ``IMITATION_AMD_DIST_BACKEND=gloo`` rehearses the multi-rank path with every rank on
+    one device (or on the CPU)."""
+    backend = os.environ.get("IMITATION_AMD_DIST_BACKEND", "nccl")
+    if backend != "gloo":
+        import torch as th
+
+        have = th.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have} "
+                  f"(set IMITATION_AMD_DIST_BACKEND=gloo to rehearse on fewer devices)", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in pending:  # one rank died: the others would block in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc if rc >= 0 else 1
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     import torch as th
 
     from imitation_amd.parallel import dist as pdist
 
     rank, world = pdist.init()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        sys.exit(2)
     if th.cuda.is_available():
         dev_idx = pdist.local_rank() % th.cuda.device_count()  # == local rank on a full node
         th.cuda.set_device(dev_idx)
@@ -90,8 +142,9 @@ def main():
     if device.type == "cuda":
         th.cuda.synchronize()
     pdist.barrier()
-    dt = time.perf_counter() - t0
-    dt = pdist.allreduce_scalars([dt], op="max")[0]
+    dt_local = time.perf_counter() - t0
+    per_rank = [round(1000.0 * x / args.steps, 3) for x in pdist.all_gather_object(dt_local)]
+    dt = pdist.allreduce_scalars([dt_local], op="max")[0]
     total_steps = steps_per_round * args.steps * world
     value = total_steps / dt
     eval_return = None
@@ -114,8 +167,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
-            "dtype": "bf16",
+            # rollout + PPO run exact fp32 (MFMA f32), the discriminator bf16 MFMA operands
+            "dtype": "mixed (fp32 policy/PPO, bf16 discriminator)",
             "final_eval_return": eval_return,
+            "per_rank_ms_per_step": per_rank,
             "data": "synthetic (native HalfCheetah-v4-shaped env, random-policy demos, random-init nets)",
             "config": {
                 "model": "GAIL: FeedForward32Policy[32,32]+RunningNorm / BasicRewardNet(32,32)+RunningNorm",

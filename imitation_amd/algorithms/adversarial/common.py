@@ -34,7 +34,6 @@ from torch.nn import functional as F
 from imitation_amd.algorithms import base
 from imitation_amd.data import buffer, rollout, types, wrappers
 from imitation_amd.envs import spaces
-from imitation_amd.ops import losses as loss_ops
 from imitation_amd.parallel import dist as pdist
 from imitation_amd.rewards import reward_nets, reward_wrapper
 from imitation_amd.rl import base as rl_base
@@ -248,7 +247,7 @@ class AdversarialTrainer(base.DemonstrationAlgorithm[types.Transitions]):
                 disc_logits = self.logits_expert_is_high(
                     batch["state"], batch["action"], batch["next_state"], batch["done"], batch["log_policy_act_prob"]
                 )
-                loss = loss_ops.bce_with_logits(disc_logits, batch["labels_expert_is_one"].float())
+                loss = F.binary_cross_entropy_with_logits(disc_logits, batch["labels_expert_is_one"].float())
                 assert len(batch["state"]) == 2 * self.demo_minibatch_size
                 loss = loss * (self.demo_minibatch_size / self.demo_batch_size)
                 loss.backward()

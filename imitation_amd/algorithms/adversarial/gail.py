@@ -13,7 +13,6 @@ import torch as th
 
 from imitation_amd.algorithms import base
 from imitation_amd.algorithms.adversarial import common
-from imitation_amd.ops import losses as loss_ops
 from imitation_amd.rewards import reward_nets
 
 
@@ -26,7 +25,7 @@ class RewardNetFromDiscriminatorLogit(reward_nets.RewardNet):
 
     def forward(self, state: th.Tensor, action: th.Tensor, next_state: th.Tensor, done: th.Tensor) -> th.Tensor:
         logits = self.base.forward(state, action, next_state, done)
-        return loss_ops.neg_logsigmoid_neg(logits)
+        return th.nn.functional.softplus(logits)  # -log(1 - sigmoid(logits))
 
 
 class GAIL(common.AdversarialTrainer):

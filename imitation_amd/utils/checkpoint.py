@@ -368,9 +368,14 @@ def save_checkpoint(trainer, path: str, meta: Optional[Dict[str, Any]] = None) -
         m.update(meta or {})
         with open(os.path.join(tmp, META_FILE), "w") as f:
             json.dump(m, f, indent=2, sort_keys=True)
-        if os.path.exists(path):
-            shutil.rmtree(path)
+        old = None
+        if os.path.exists(path):  # move the previous copy aside: `path` is never missing
+            old = tempfile.mkdtemp(prefix=".ckpt-old-", dir=parent)
+            os.rmdir(old)
+            os.replace(path, old)
         os.replace(tmp, path)
+        if old is not None:
+            shutil.rmtree(old, ignore_errors=True)
     except BaseException:
         shutil.rmtree(tmp, ignore_errors=True)
         raise
@@ -437,8 +442,25 @@ class CheckpointManager:
         s = self.list()
         return s[-1] if s else None
 
+    def agreed_step(self) -> Optional[int]:
+        """Newest step that EVERY rank has saved (MIN over ranks of each rank's latest, then
+        checked present everywhere): a rank that died between the others' saves must not
+        make the replicas restore different steps."""
+        from imitation_amd.parallel import dist as pdist
+
+        mine = self.list()
+        if pdist.world_size() <= 1:
+            return mine[-1] if mine else None
+        lo = int(pdist.allreduce_scalars([float(mine[-1]) if mine else -1.0], op="min")[0])
+        if lo < 0:
+            return None
+        have = pdist.allreduce_scalars([1.0 if lo in mine else 0.0], op="min")[0]
+        if have < 1.0:
+            raise RuntimeError(f"checkpoint step {lo} is missing on some rank; cannot restore consistently")
+        return lo
+
     def restore_latest(self, trainer) -> int:
-        step = self.latest()
+        step = self.agreed_step()
         if step is None:
             return 0
         load_checkpoint(trainer, self._rank_dir(step))

@@ -75,3 +75,15 @@ def test_dagger_pong_builds(tmp_path):
     assert isinstance(b.trainer, SimpleDAggerTrainer)
     assert isinstance(b.trainer.bc_trainer.policy.features_extractor, NatureCNN)
     assert b.venv.observation_space.shape == (84, 84, 4)
+
+
+def test_dp_ranks_get_independent_env_streams(tmp_path):
+    """PPO(seed=...) re-seeds the env with the shared seed; the recipe re-seeds per rank so
+    the weak-scaled DP batch is made of independent rollouts."""
+    obs = []
+    for rank in (0, 1, 1):
+        b = models.build("gail_halfcheetah", n_demo_timesteps=1024, engine="host", rank=rank,
+                         log_dir=str(tmp_path / str(rank)))
+        obs.append(np.asarray(b.venv.reset()))
+    assert not np.allclose(obs[0], obs[1])
+    np.testing.assert_array_equal(obs[1], obs[2])  # still deterministic per rank
