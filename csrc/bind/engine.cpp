@@ -59,7 +59,6 @@ void rollout(py::dict d) {
   a.max_steps = ival(d, "max_steps", ms);
   a.T = ival(d, "T");
   a.N = ival(d, "N");
-  a.gamma = (float)fval(d, "gamma", 0.99);
   a.seed = (uint64_t)d["seed"].cast<long long>();
   a.step0 = d["step0"].cast<long long>();
   a.state = tptr<float>(d, "state");
@@ -69,13 +68,53 @@ void rollout(py::dict d) {
   a.cur_obs = tptr<float>(d, "cur_obs");
   a.cur_start = tptr<float>(d, "cur_start");
   a.pi = wave_mlp(d["pi"].cast<py::dict>());
-  a.vf = wave_mlp(d["vf"].cast<py::dict>());
   a.log_std = tptr<const float>(d, "log_std", true);
   a.act_low = tptr<const float>(d, "act_low", true);
   a.act_high = tptr<const float>(d, "act_high", true);
   a.n_actions = ival(d, "n_actions", 0);
+  TORCH_CHECK(a.n_actions > 0 || (a.act_low && a.act_high && a.log_std), "Gaussian policy needs log_std and Box bounds");
+  TORCH_CHECK(a.n_actions <= 64, "Categorical over more than 64 actions");
+  TORCH_CHECK(a.pi.dims[0] == a.P.obs_dim, "actor input dim != obs dim");
+  TORCH_CHECK(a.pi.dims[a.pi.n_layers] == (a.n_actions > 0 ? a.n_actions : a.P.act_dim), "actor head width");
   a.explore_mode = tptr<const int>(d, "explore_mode", true);
-  TORCH_CHECK(!a.explore_mode || a.n_actions > 0 || (a.act_low && a.act_high), "exploration needs Box bounds");
+  TORCH_CHECK(a.P.obs_dim <= ia::kEngineMaxObs, "obs dim too large for the device rollout");
+  a.obs_buf = tptr<float>(d, "obs_buf");
+  a.act_raw = tptr<float>(d, "act_raw");
+  a.act_env = tptr<float>(d, "act_env");
+  a.env_rew = tptr<float>(d, "env_rew");
+  a.starts = tptr<float>(d, "starts");
+  a.dones = tptr<float>(d, "dones");
+  a.trunc = tptr<float>(d, "trunc");
+  a.next_obs = tptr<float>(d, "next_obs");
+  a.ep_ret_out = tptr<float>(d, "ep_ret_out");
+  IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
+}
+
+void rollout_post(py::dict d) {
+  ia::RolloutPostArgs a{};
+  a.T = ival(d, "T");
+  a.N = ival(d, "N");
+  a.D = ival(d, "D");
+  a.A = ival(d, "A");
+  a.n_actions = ival(d, "n_actions", 0);
+  a.gamma = (float)fval(d, "gamma", 0.99);
+  a.obs = tptr<const float>(d, "obs_buf");
+  a.act_raw = tptr<const float>(d, "act_raw");
+  a.act_env = tptr<const float>(d, "act_env");
+  a.next_obs = tptr<const float>(d, "next_obs");
+  a.dones = tptr<const float>(d, "dones");
+  a.trunc = tptr<const float>(d, "trunc");
+  a.env_rew = tptr<const float>(d, "env_rew");
+  a.cur_obs = tptr<const float>(d, "cur_obs");
+  a.vf = wave_mlp(d["vf"].cast<py::dict>());
+  TORCH_CHECK(a.vf.dims[0] == a.D && a.vf.dims[a.vf.n_layers] == 1, "critic shape");
+  a.logp = tptr<float>(d, "logp", true);
+  if (a.logp) {
+    a.pi = wave_mlp(d["pi"].cast<py::dict>());
+    TORCH_CHECK(a.pi.dims[0] == a.D, "actor input dim");
+    a.log_std = tptr<const float>(d, "log_std", true);
+    TORCH_CHECK(a.n_actions > 0 || a.log_std, "Gaussian log-prob needs log_std");
+  }
   a.rew_enabled = ival(d, "rew_enabled", 0);
   if (a.rew_enabled) {
     a.rew = wave_mlp(d["rew"].cast<py::dict>());
@@ -88,59 +127,19 @@ void rollout(py::dict d) {
     if (a.shaped) {
       a.pot = wave_mlp(d["pot"].cast<py::dict>());
       a.shaping_gamma = (float)fval(d, "shaping_gamma", 0.99);
-      TORCH_CHECK(a.pot.dims[0] == ival(d, "obs_dim_check", a.pot.dims[0]), "potential input dim");
+      TORCH_CHECK(a.pot.dims[0] == a.D, "potential input dim");
     }
+    const int din = (a.use_state ? a.D : 0) + (a.use_action ? (a.n_actions > 0 ? a.n_actions : a.A) : 0) +
+                    (a.use_next_state ? a.D : 0) + (a.use_done ? 1 : 0);
+    TORCH_CHECK(a.rew.dims[0] == din, "reward MLP input dim ", a.rew.dims[0], " != ", din);
+    TORCH_CHECK(din <= ia::kWaveMaxDim, "reward input wider than a wave");
   }
-  a.rew_raw = tptr<float>(d, "rew_raw", true);
-  a.boot = tptr<float>(d, "boot", true);
-  TORCH_CHECK((a.rew_raw == nullptr) == (a.boot == nullptr), "rew_raw and boot go together");
-  TORCH_CHECK(a.P.obs_dim <= ia::kEngineMaxObs, "obs dim too large for the device rollout");
-  a.obs_buf = tptr<float>(d, "obs_buf");
-  a.act_raw = tptr<float>(d, "act_raw");
-  a.act_env = tptr<float>(d, "act_env");
-  a.logp = tptr<float>(d, "logp");
   a.values = tptr<float>(d, "values");
-  a.rewards = tptr<float>(d, "rewards");
-  a.env_rew = tptr<float>(d, "env_rew");
-  a.starts = tptr<float>(d, "starts");
-  a.dones = tptr<float>(d, "dones");
-  a.next_obs = tptr<float>(d, "next_obs");
-  a.ep_ret_out = tptr<float>(d, "ep_ret_out");
-  a.last_values = tptr<float>(d, "last_values");
-  a.prof = tptr<unsigned long long>(d, "prof", true);
-  IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
-}
-
-void reward_batch(py::dict d) {
-  ia::RewardBatchArgs a{};
-  a.rows = ival(d, "rows");
-  a.D = ival(d, "D");
-  a.A = ival(d, "A");
-  a.n_actions = ival(d, "n_actions", 0);
-  a.obs = tptr<const float>(d, "obs");
-  a.acts = tptr<const float>(d, "acts");
-  a.next_obs = tptr<const float>(d, "next_obs");
-  a.dones = tptr<const float>(d, "dones");
-  a.boot = tptr<const float>(d, "boot");
-  a.rew = wave_mlp(d["rew"].cast<py::dict>());
-  a.use_state = ival(d, "use_state", 1);
-  a.use_action = ival(d, "use_action", 1);
-  a.use_next_state = ival(d, "use_next_state", 0);
-  a.use_done = ival(d, "use_done", 0);
-  a.rew_transform = ival(d, "rew_transform", 0);
-  a.shaped = ival(d, "shaped", 0);
-  if (a.shaped) {
-    a.pot = wave_mlp(d["pot"].cast<py::dict>());
-    a.shaping_gamma = (float)fval(d, "shaping_gamma", 0.99);
-    TORCH_CHECK(a.pot.dims[0] == a.D, "potential input dim");
-  }
-  const int din = (a.use_state ? a.D : 0) + (a.use_action ? (a.n_actions > 0 ? a.n_actions : a.A) : 0) +
-                  (a.use_next_state ? a.D : 0) + (a.use_done ? 1 : 0);
-  TORCH_CHECK(a.rew.dims[0] == din, "reward MLP input dim ", a.rew.dims[0], " != ", din);
-  TORCH_CHECK(din <= ia::kWaveMaxDim, "reward input wider than a wave");
+  a.boot = tptr<float>(d, "boot");
   a.rewards = tptr<float>(d, "rewards");
   a.rew_raw = tptr<float>(d, "rew_raw", true);
-  IA_HIP_CHECK2(ia::reward_batch_launch(a, ia_stream()));
+  a.last_values = tptr<float>(d, "last_values");
+  IA_HIP_CHECK2(ia::rollout_post_launch(a, ia_stream()));
 }
 
 void reward_outnorm(py::dict d) {
@@ -266,8 +265,9 @@ size_t ppo_lds(py::dict d) {
 }  // namespace
 
 void register_engine(py::module& m) {
-  m.def("engine_rollout", &rollout, "T-step device rollout (policy + env + learned reward) for N envs");
-  m.def("engine_reward_batch", &reward_batch, "learned reward of all rollout transitions in parallel");
+  m.def("engine_rollout", &rollout, "T-step device rollout (actor sampling + env) for N envs");
+  m.def("engine_rollout_post", &rollout_post,
+        "values, log-probs, TimeLimit bootstrap and learned reward of a rollout, all transitions in parallel");
   m.def("engine_reward_outnorm", &reward_outnorm, "NormalizedRewardNet output normalisation over a rollout");
   m.def("engine_ppo_update", &ppo_update, "persistent PPO update / DP minibatch grads / apply");
   m.def("engine_ppo_path", &ppo_path, "kernel used by engine_ppo_update mode 0 (rc | lds)");

@@ -31,12 +31,12 @@ struct WaveMLP {
 
 enum RewardTransform : int { REW_RAW = 0, REW_SOFTPLUS = 1 };
 
+// Serial part of a device rollout (rollout.hip): actor sampling + env physics.
 struct RolloutArgs {
   EnvParams P;
   int max_steps;  // TimeLimit horizon
   int T;          // steps per env this call
   int N;          // envs
-  float gamma;    // for TimeLimit-truncation bootstrap (SB3 collect_rollouts)
   uint64_t seed;  // action-sampling stream
   long long step0;  // global step counter (decorrelates calls)
   // persistent env state (device)
@@ -46,8 +46,8 @@ struct RolloutArgs {
   float* ep_ret;     // [N] running env return (Monitor)
   float* cur_obs;    // [N][D]  (policy's _last_obs)
   float* cur_start;  // [N]     (_last_episode_starts)
-  // policy
-  WaveMLP pi, vf;
+  // actor: trunk + action head, input RunningNorm (eval mode) in pi.norm_*
+  WaveMLP pi;
   const float* log_std;  // [A] (Gaussian) or nullptr (Categorical)
   const float* act_low;  // [A] Box bounds for clipping
   const float* act_high;
@@ -55,57 +55,51 @@ struct RolloutArgs {
   // optional ExplorationWrapper schedule: explore_mode[t] != 0 -> every env takes a uniform
   // random action at step t (Box.sample / Discrete.sample) instead of the policy's
   const int* explore_mode;  // [T] or nullptr
-  // learned reward (GAIL / AIRL reward_train); rew_enabled==0 -> env reward
-  int rew_enabled;
-  WaveMLP rew;
-  int use_state, use_action, use_next_state, use_done;
-  int rew_transform;
-  // AIRL ShapedRewardNet: r = base(s,a,s',d) + shaping_gamma * (1 - d) * pot(s') - pot(s)
-  int shaped;
-  WaveMLP pot;
-  float shaping_gamma;
-  // when set: the learned reward (pre output-normalisation) and the TimeLimit bootstrap term
-  // are also stored separately, for reward_outnorm (NormalizedRewardNet.predict_processed)
-  float* rew_raw;  // [T][N]
-  float* boot;     // [T][N]
   // outputs, [T][N] (+ trailing feature dim)
   float* obs_buf;
   float* act_raw;   // sampled (unclipped) action, PPO buffer
   float* act_env;   // action given to the env (clipped), replay buffer / reward
-  float* logp;
-  float* values;
-  float* rewards;   // learned reward (+ γ V(terminal) on truncation)
   float* env_rew;
   float* starts;
   float* dones;
+  float* trunc;     // 1 where the episode was cut by the TimeLimit (not terminated)
   float* next_obs;  // terminal obs on done
   float* ep_ret_out;  // episode return where done
-  float* last_values;  // [N]
-  unsigned long long* prof;  // optional [N][4] cycle counters: policy, env, reward, other
 };
 
-// Learned reward of a finished rollout, all T*N transitions in parallel (the reward
-// does not feed back into the dynamics, so it leaves the rollout's serial step chain):
-// r = transform(rew(s, a, s', d)) [+ shaping_gamma (1 - d) pot(s') - pot(s)];
-// rewards[i] = r + boot[i]; rew_raw[i] = r when given (NormalizedRewardNet replay).
-struct RewardBatchArgs {
-  int rows;       // T * N, row = t * N + n
+// Parallel part (engine.hip): per transition V(s), log pi(a|s), the TimeLimit bootstrap
+// boot = gamma V(s') on truncation, and the reward
+// rewards = (rew_enabled ? R(s, a, s', d) [+ shaping] : env_rew) + boot; rows T*N .. T*N+N
+// give last_values = V(cur_obs). rew_raw (optional) keeps R before output normalisation.
+struct RolloutPostArgs {
+  int T, N;
   int D;          // obs dim
   int A;          // act buffer width (1 for Categorical)
   int n_actions;  // >0: Categorical (acts hold the index)
+  float gamma;
   const float* obs;
-  const float* acts;  // env (clipped) actions
+  const float* act_raw;
+  const float* act_env;
   const float* next_obs;
   const float* dones;
-  const float* boot;
+  const float* trunc;
+  const float* env_rew;
+  const float* cur_obs;
+  WaveMLP pi, vf;
+  const float* log_std;
+  int rew_enabled;
   WaveMLP rew;
   int use_state, use_action, use_next_state, use_done;
   int rew_transform;
   int shaped;
   WaveMLP pot;
   float shaping_gamma;
+  float* values;
+  float* logp;  // nullptr: skip the actor (sampling-only rollouts)
+  float* boot;
   float* rewards;
-  float* rew_raw;  // optional
+  float* rew_raw;
+  float* last_values;
 };
 
 // NormalizedRewardNet output normalisation over a rollout, step by step in env order:

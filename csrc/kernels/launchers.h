@@ -80,11 +80,14 @@ hipError_t pref_loss_fwd(const float* r1, const float* r2, const float* prefs, i
 hipError_t pref_loss_bwd(const float* coef, const float* gout, int P, int L, float discount, float* d1, float* d2,
                          hipStream_t s);
 
-// ---- engine.hip: device-resident rollout (policy + env + learned reward)
+// ---- rollout.hip / engine.hip: device-resident rollout (serial actor + env chain, then the
+// parallel value / log-prob / bootstrap / learned-reward pass)
+bool rollout_split_form(const WaveMLP& m);
 size_t rollout_lds_bytes(const RolloutArgs& a);
 hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s);
+size_t rollout_post_lds_bytes(const RolloutPostArgs& a);
+hipError_t rollout_post_launch(const RolloutPostArgs& a, hipStream_t s);
 hipError_t reward_outnorm_launch(const OutNormArgs& a, hipStream_t s);
-hipError_t reward_batch_launch(const RewardBatchArgs& a, hipStream_t s);
 
 // ---- ppo_rc.hip: register-chained single-rank PPO update (falls back to ppo.hip)
 bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes);

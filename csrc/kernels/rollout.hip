@@ -1,0 +1,466 @@
+// Device rollout, serial part: T steps of actor sampling + env physics for N envs in
+// ONE launch (replaces the reference's per-step host loop: SB3 collect_rollouts ->
+// policy.forward -> VecEnv.step over pipes -> RewardVecEnvWrapper).
+//
+// Only what the NEXT step depends on stays on the serial chain: the actor mean /
+// logits, the sampled action and the env step. Everything a step merely records --
+// value estimate, log-prob, TimeLimit bootstrap, learned reward -- is recomputed for
+// all T x N transitions at once by rollout_post_kernel (engine.hip), and the sampling
+// noise of a whole chunk of steps is drawn up front by all 64 lanes into LDS.
+//
+// Mapping: one wave64 per env, one env per workgroup (no inter-wave sync at all).
+// Actor layer l, "split" form (every width <= 32): lane (h, j) = (lane >> 5, lane & 31)
+// owns unit j and half h of the K (input) range, its weights live in VGPRs, the layer
+// input is broadcast from a 64-float LDS vector with ds_read_b128 (every lane of a
+// half reads the same address), and the two half sums meet through
+// v_permlane32_swap. Widths up to 64 use the "full" form (lane = unit, whole K).
+// The locomotion model keeps its state in registers: joint j on lane j, the root
+// coordinates uniform in every lane, cross-joint sums by DPP quad/row butterflies.
+// No loop iteration waits on global memory: inputs are LDS, outputs are fire-and-
+// forget stores.
+#include <hip/hip_runtime.h>
+
+#include "ia/engine.h"
+#include "ia/envs.h"
+#include "ia/wave.h"
+#include "launchers.h"
+
+namespace ia {
+namespace {
+
+constexpr int kNoiseFloats = 4096;  // per chunk of steps (16 KiB)
+
+// Split form: weights in VGPRs, lane (h, j) holds W[j][k0 + i], i < 16.
+// Full form:  weights in LDS, image [din/4][64 lanes][4 k] (one ds_read_b128 per 4 inputs).
+template <bool SPLIT>
+struct Actor {
+  static constexpr int KH = SPLIT ? 16 : 1;
+  float w[kWaveMaxLayers][KH];
+  const lf* wt[kWaveMaxLayers];  // full form
+  float bias[kWaveMaxLayers];
+  int k0[kWaveMaxLayers];  // first input of this lane's slice (uniform per half)
+  int ng[kWaveMaxLayers];  // groups of 4 inputs (uniform)
+  int dout[kWaveMaxLayers];
+  int n_layers, hidden_act;
+};
+
+__host__ __device__ __forceinline__ int split_kh(int din) { return ((din + 1) / 2 + 3) & ~3; }
+__host__ __device__ __forceinline__ int full_lds_floats(const WaveMLP& m) {
+  int f = 0;
+  for (int l = 0; l < m.n_layers; ++l) f += ((m.dims[l] + 3) & ~3) * 64;
+  return f;
+}
+
+template <bool SPLIT>
+__device__ void load_actor(const WaveMLP& m, Actor<SPLIT>& r, lf* wlds) {
+  const int lane = threadIdx.x;
+  const int h = SPLIT ? (lane >> 5) : 0;
+  const int j = SPLIT ? (lane & 31) : lane;
+  r.n_layers = m.n_layers;
+  r.hidden_act = m.hidden_act;
+#pragma unroll
+  for (int l = 0; l < kWaveMaxLayers; ++l) {
+    const bool on = l < m.n_layers;
+    const int din = on ? m.dims[l] : 0, dout = on ? m.dims[l + 1] : 0;
+    const int kh = SPLIT ? split_kh(din) : ((din + 3) & ~3);
+    const int k0 = h ? kh : 0;
+    r.k0[l] = k0;
+    r.ng[l] = kh >> 2;
+    r.dout[l] = dout;
+    if (SPLIT) {
+      const int kend = h ? din : kh;
+#pragma unroll
+      for (int i = 0; i < Actor<SPLIT>::KH; ++i) {
+        const int k = k0 + i;
+        r.w[l][i] = (on && j < dout && k < kend && k < din) ? m.W[l][j * din + k] : 0.f;
+      }
+    } else {
+      r.wt[l] = wlds;
+      if (on) {
+        for (int k = 0; k < kh; ++k) wlds[((k >> 2) * 64 + lane) * 4 + (k & 3)] = (j < dout && k < din) ? m.W[l][j * din + k] : 0.f;
+        wlds += kh * 64;
+      }
+    }
+    r.bias[l] = (on && j < dout && h == 0) ? m.b[l][j] : 0.f;
+  }
+}
+
+// x (the normalised observation) is already in xb[0 .. 64) (zero padded). Returns, in
+// lane j < dout of the last layer (both halves in split form), the actor output j.
+template <bool SPLIT>
+__device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
+  const int lane = threadIdx.x;
+  const int j = SPLIT ? (lane & 31) : lane;
+  const lf4* x4 = (const lf4*)xb;
+  float h = 0.f;
+#pragma unroll
+  for (int l = 0; l < kWaveMaxLayers; ++l) {
+    if (l < r.n_layers) {
+      const lf4* src = x4 + (r.k0[l] >> 2);
+      float acc0 = r.bias[l], acc1 = 0.f;
+      if (SPLIT) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (g < r.ng[l]) {
+            const f32v4 v = src[g];
+            acc0 = fmaf(r.w[l][4 * g + 0], v.x, acc0);
+            acc1 = fmaf(r.w[l][4 * g + 1], v.y, acc1);
+            acc0 = fmaf(r.w[l][4 * g + 2], v.z, acc0);
+            acc1 = fmaf(r.w[l][4 * g + 3], v.w, acc1);
+          }
+        }
+      } else {
+        const lf4* w4 = (const lf4*)r.wt[l] + lane;
+        for (int g = 0; g < r.ng[l]; ++g) {
+          const f32v4 v = src[g], w = w4[g * 64];
+          acc0 = fmaf(w.x, v.x, acc0);
+          acc1 = fmaf(w.y, v.y, acc1);
+          acc0 = fmaf(w.z, v.z, acc0);
+          acc1 = fmaf(w.w, v.w, acc1);
+        }
+      }
+      float acc = acc0 + acc1;
+      if (SPLIT) acc = add_halves(acc);
+      const bool last = l == r.n_layers - 1;
+      h = j < r.dout[l] ? (last ? acc : act_fast(r.hidden_act, acc)) : 0.f;
+      if (!last) {
+        wave_sync();  // every lane has read this layer's input
+        if (lane < (SPLIT ? 32 : 64)) xb[lane] = h;
+        wave_sync();
+      }
+    }
+  }
+  return h;
+}
+
+// Generic (non-locomotion) envs step on lane 0 out of line, so their code does not
+// share the register budget of the kernel's step loop.
+__device__ __noinline__ float env_step_lane0(const EnvParams& P, float* s, const float* action, int* term, uint64_t* rng) {
+  return env_step(P, s, action, term, *rng);
+}
+__device__ __noinline__ void env_reset_lane0(const EnvParams& P, float* s, float* o, uint64_t* rng) {
+  env_reset(P, s, *rng);
+  env_obs(P, s, o);
+}
+
+// ---------------------------------------------------------------- locomotion, state in registers
+struct LocoRegs {
+  float q, qd;          // joint lane state (lane < nj)
+  float rq[8], rv[8];   // root coordinates (uniform)
+  float gear, stiff, damp, thrust, pcoup;  // per-joint-lane constants
+};
+
+__device__ void loco_load(const LocoParams& p, const lf* s, LocoRegs& L) {
+  const int lane = threadIdx.x, nq = loco_nq(p);
+  const bool jl = lane < p.nj;
+  L.q = jl ? s[p.nq_root + lane] : 0.f;
+  L.qd = jl ? s[nq + p.nv_root + lane] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    L.rq[i] = i < p.nq_root ? s[i] : 0.f;
+    L.rv[i] = i < p.nv_root ? s[nq + i] : 0.f;
+  }
+}
+
+__device__ void loco_store(const LocoParams& p, const LocoRegs& L, lf* s) {
+  const int lane = threadIdx.x, nq = loco_nq(p);
+  if (lane < p.nj) {
+    s[p.nq_root + lane] = L.q;
+    s[nq + p.nv_root + lane] = L.qd;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < p.nq_root) s[i] = L.rq[i];
+      if (i < p.nv_root) s[nq + i] = L.rv[i];
+    }
+  }
+}
+
+// Observation [qpos[obs_skip:], qvel] in lane layout, through the LDS scratch sb.
+__device__ float loco_obs(const LocoParams& p, const LocoRegs& L, lf* sb) {
+  const int lane = threadIdx.x;
+  const int npr = p.nq_root - p.obs_skip, nj = p.nj;
+  float rqi = 0.f, rvi = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    rqi = (lane + p.obs_skip) == i ? L.rq[i] : rqi;
+    rvi = lane == i ? L.rv[i] : rvi;
+  }
+  wave_sync();
+  if (lane < npr) sb[lane] = rqi;
+  if (lane < nj) {
+    sb[npr + lane] = L.q;
+    sb[npr + nj + p.nv_root + lane] = L.qd;
+  }
+  if (lane < p.nv_root) sb[npr + nj + lane] = rvi;
+  wave_sync();
+  const int D = npr + nj + p.nv_root + nj;
+  return lane < D ? sb[lane] : 0.f;
+}
+
+// ia::loco_step (envs.h) with the joint loops spread over lanes; a = clipped action of
+// joint lane j (0 elsewhere). Returns the step reward (uniform).
+__device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
+  const int lane = threadIdx.x;
+  const bool jl = lane < p.nj;
+  const float a = jl ? fminf(fmaxf(a_in, -1.f), 1.f) : 0.f;
+  const float ctrl = sum_lanes8(a * a);
+  const float pitch = sum_lanes8(L.pcoup * a);
+  const float x_before = L.rq[0];
+  const float dt = p.dt;
+  const float inv_nj = 1.f / (float)p.nj;
+  float q = L.q, qd = L.qd;
+  for (int sub = 0; sub < p.frame_skip; ++sub) {
+    const float qdd = L.gear * a - L.stiff * q - L.damp * qd - 2.0f * __sinf(q);
+    const float st = jl ? stance(q) : 0.f;
+    const float th_j = L.thrust * st * fmaxf(-qd, 0.f);
+    qd = qd + dt * qdd;
+    const float thrust = sum_lanes8(th_j);
+    const float lift = sum_lanes8(st);
+    const float vx = L.rv[0];
+    L.rv[0] = vx + dt * (thrust - p.drag * vx * (1.0f + fabsf(vx)));
+    if (p.nv_root > 1) L.rv[1] = L.rv[1] + dt * (-20.f * L.rq[1] - 4.f * L.rv[1] + 0.5f * (lift * inv_nj - 0.5f));
+    if (p.nv_root > 2) L.rv[2] = L.rv[2] + dt * (-15.f * __sinf(L.rq[2]) - 3.f * L.rv[2] + pitch);
+#pragma unroll
+    for (int i = 3; i < 8; ++i)
+      if (i < p.nv_root) L.rv[i] = L.rv[i] * (1.f - 2.f * dt) + dt * 0.1f * pitch;
+    L.rq[0] += dt * L.rv[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+      if (i < p.nq_root) {
+        if (i < p.nv_root) {
+          L.rq[i] += dt * L.rv[i] * 1.f;
+        } else {  // free-joint quaternion slots (3D bodies only)
+          const int vi = i % p.nv_root;
+          float v = 0.f;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v = u == vi ? L.rv[u] : v;
+          L.rq[i] += dt * v * 0.1f;
+        }
+      }
+    }
+    float qn = q + dt * qd;
+    if (qn > 1.2f) { qn = 1.2f; if (qd > 0) qd = 0.f; }
+    if (qn < -1.2f) { qn = -1.2f; if (qd < 0) qd = 0.f; }
+    q = qn;
+  }
+  L.q = jl ? q : 0.f;
+  L.qd = jl ? qd : 0.f;
+  const float dt_total = dt * p.frame_skip;
+  return p.fwd_weight * (L.rq[0] - x_before) / dt_total + p.healthy_reward - p.ctrl_cost * ctrl;
+}
+
+template <bool SPLIT, bool LOCO>
+__global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_raw[];
+  lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
+  lf* sb = xb + 64;            // [64] observation scratch
+  lf* st = sb + 64;            // [kMaxState] env state (generic envs, resets)
+  lf* act = st + kMaxState;    // [64]
+  lf* noise = act + 64;        // [kNoiseFloats]
+  li* explore = (li*)(noise + kNoiseFloats);  // [chunk]
+  lf* wlds = (lf*)(explore + ((a.T + 3) & ~3)); // full-form actor weights (16-B aligned)
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x;
+  const EnvParams& P = a.P;
+  const int D = P.obs_dim;
+  const bool discrete = a.n_actions > 0;
+  const int A = discrete ? 1 : P.act_dim;
+  const int AW = discrete ? a.n_actions : P.act_dim;  // noise values per step
+  const int S = state_size(P);
+  constexpr bool loco = LOCO;
+
+  Actor<SPLIT> ar;
+  load_actor<SPLIT>(a.pi, ar, wlds);
+  const float nmean = (a.pi.norm_mean && lane < D) ? a.pi.norm_mean[lane] : 0.f;
+  const float nrstd = (a.pi.norm_mean && lane < D) ? rsqrtf(a.pi.norm_var[lane] + a.pi.norm_eps) : 1.f;
+  const float lstd = (!discrete && a.log_std && lane < A) ? a.log_std[lane] : 0.f;
+  const float sd = expf(lstd);
+  const float lo = (!discrete && a.act_low && lane < A) ? a.act_low[lane] : 0.f;
+  const float hi = (!discrete && a.act_high && lane < A) ? a.act_high[lane] : 0.f;
+
+  for (int i = lane; i < S; i += 64) st[i] = a.state[(size_t)n * S + i];
+  xb[lane] = 0.f;
+  LocoRegs L{};
+  if (loco) {
+    const LocoParams& p = P.loco;
+    const bool jl = lane < p.nj;
+    L.gear = jl ? p.gear[lane] : 0.f;
+    L.stiff = jl ? p.stiff[lane] : 0.f;
+    L.damp = jl ? p.damp[lane] : 0.f;
+    L.thrust = jl ? p.thrust[lane] : 0.f;
+    L.pcoup = jl ? p.pitch_coupling[lane] : 0.f;
+  }
+  wave_sync();
+  if (loco) loco_load(P.loco, st, L);
+
+  float o = lane < D ? a.cur_obs[(size_t)n * D + lane] : 0.f;
+  float start = a.cur_start[n];
+  uint64_t rng = a.rng[n];
+  int elapsed = a.elapsed[n];
+  float ep_ret = a.ep_ret[n];
+  const int chunk = AW > 0 ? max(1, min(a.T, kNoiseFloats / AW)) : a.T;
+
+  for (int t0 = 0; t0 < a.T; t0 += chunk) {
+    const int tc = min(chunk, a.T - t0);
+    // ---- this chunk's sampling noise, all lanes in parallel (off the step chain)
+    wave_sync();
+    for (int e = lane; e < tc * AW; e += 64) {
+      const int tr = e / AW, k = e - tr * AW;
+      const uint64_t key = hash3(a.seed, (uint64_t)n, (uint64_t)(a.step0 + t0 + tr));
+      uint64_t s = key ^ (kLaneTweak * (uint64_t)(k + 1));
+      float v;
+      if (discrete) {  // Gumbel-max: argmax(logits + G) ~ Categorical(softmax(logits))
+        const float u = fmaxf(uniform01(s), 1e-12f);
+        v = -logf(-logf(u));
+      } else {
+        v = normal01(s);
+      }
+      noise[e] = v;
+    }
+    for (int e = lane; e < tc; e += 64) explore[e] = a.explore_mode ? a.explore_mode[t0 + e] : 0;
+    wave_sync();
+
+    for (int tr = 0; tr < tc; ++tr) {
+      const int t = t0 + tr;
+      const size_t row = (size_t)t * a.N + n;
+      if (lane < D) a.obs_buf[row * D + lane] = o;
+      if (lane == 0) a.starts[row] = start;
+      // ---- actor
+      xb[lane] = lane < D ? (o - nmean) * nrstd : 0.f;
+      wave_sync();
+      const float head = actor_forward<SPLIT>(ar, xb);
+      float a_raw, a_env;
+      if (discrete) {
+        const float g = lane < a.n_actions ? head + noise[tr * AW + lane] : -INFINITY;
+        const float mx = wave_max(g);
+        const unsigned long long m = __ballot(g == mx && lane < a.n_actions);
+        const int k = m ? __builtin_ctzll(m) : a.n_actions - 1;
+        a_raw = a_env = (float)k;
+      } else {
+        a_raw = lane < A ? head + sd * noise[tr * AW + lane] : 0.f;
+        a_env = lane < A ? fminf(fmaxf(a_raw, lo), hi) : 0.f;
+      }
+      if (explore[tr]) {  // ExplorationWrapper's random policy (uniform branch)
+        const uint64_t key = hash3(a.seed, (uint64_t)n, (uint64_t)(a.step0 + t));
+        uint64_t s = key ^ kExploreTweak;
+        if (discrete) {
+          s ^= kExploreDiscreteTweak;
+          const float u = uniform01(s);
+          int k = (int)(u * (float)a.n_actions);
+          k = k < a.n_actions ? k : a.n_actions - 1;
+          a_raw = a_env = (float)k;
+        } else {
+          s ^= kLaneTweak * (uint64_t)(lane + 1);
+          const float u = uniform01(s);
+          a_env = lane < A ? lo + u * (hi - lo) : 0.f;
+          a_raw = a_env;
+        }
+      }
+      if (lane < A) {
+        a.act_raw[row * A + lane] = a_raw;
+        a.act_env[row * A + lane] = a_env;
+      }
+      // ---- env step + SB3 auto-reset, TimeLimit, Monitor
+      int term = 0;
+      float r_env;
+      float o_next;
+      if (loco) {
+        r_env = loco_step_regs(P.loco, L, a_env);
+        o_next = loco_obs(P.loco, L, sb);
+      } else {
+        if (lane < A) act[lane] = a_env;
+        wave_sync();
+        if (lane == 0) {
+          r_env = env_step_lane0(P, (float*)st, (const float*)act, &term, &rng);
+          env_obs(P, (const float*)st, (float*)sb);
+        }
+        wave_sync();
+        term = __builtin_amdgcn_readfirstlane(term);
+        r_env = bcast(r_env, 0);
+        o_next = lane < D ? sb[lane] : 0.f;
+      }
+      elapsed += 1;
+      ep_ret += r_env;
+      const bool trunc = !term && elapsed >= a.max_steps;
+      const bool done = term || trunc;
+      if (lane < D) a.next_obs[row * D + lane] = o_next;
+      if (lane == 0) {
+        a.env_rew[row] = r_env;
+        a.dones[row] = done ? 1.f : 0.f;
+        a.trunc[row] = trunc ? 1.f : 0.f;
+        a.ep_ret_out[row] = done ? ep_ret : 0.f;
+      }
+      if (done) {
+        if (loco) loco_store(P.loco, L, st);
+        wave_sync();
+        if (lane == 0) {
+          if (loco) loco_reset(P.loco, (float*)st, rng);
+          else env_reset_lane0(P, (float*)st, (float*)sb, &rng);
+        }
+        wave_sync();
+        if (loco) {
+          loco_load(P.loco, st, L);
+          o = loco_obs(P.loco, L, sb);
+        } else {
+          o = lane < D ? sb[lane] : 0.f;
+        }
+        elapsed = 0;
+        ep_ret = 0.f;
+      } else {
+        o = o_next;
+      }
+      start = done ? 1.f : 0.f;
+    }
+  }
+  if (loco) loco_store(P.loco, L, st);
+  wave_sync();
+  for (int i = lane; i < S; i += 64) a.state[(size_t)n * S + i] = st[i];
+  if (lane < D) a.cur_obs[(size_t)n * D + lane] = o;
+  if (lane == 0) {
+    a.cur_start[n] = start;
+    a.elapsed[n] = elapsed;
+    a.ep_ret[n] = ep_ret;
+  }
+  // lane 0's rng advanced inside env_step / env_reset; persist it
+  rng = (uint64_t)__builtin_amdgcn_readfirstlane((int)(rng & 0xffffffffu)) |
+        ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(rng >> 32)) << 32);
+  if (lane == 0) a.rng[n] = rng;
+}
+
+}  // namespace
+
+bool rollout_split_form(const WaveMLP& m) {
+  for (int l = 0; l <= m.n_layers; ++l)
+    if (m.dims[l] > 32) return false;
+  return true;
+}
+
+size_t rollout_lds_bytes(const RolloutArgs& a) {
+  const size_t full = rollout_split_form(a.pi) ? 0 : (size_t)full_lds_floats(a.pi);
+  return (size_t)(64 + 64 + kMaxState + 64 + kNoiseFloats + full) * sizeof(float) + (size_t)((a.T + 3) & ~3) * sizeof(int);
+}
+
+hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
+  if (a.T <= 0 || a.N <= 0) return hipSuccess;
+  if (a.P.obs_dim > 64 || a.pi.n_layers < 1 || a.pi.n_layers > kWaveMaxLayers) return hipErrorInvalidValue;
+  for (int l = 0; l <= a.pi.n_layers; ++l)
+    if (a.pi.dims[l] > 64 || a.pi.dims[l] < 1) return hipErrorInvalidValue;
+  if (a.pi.dims[0] != a.P.obs_dim) return hipErrorInvalidValue;
+  if (a.n_actions > 64 || (a.P.kind == ENV_LOCO && a.P.loco.nj > 8)) return hipErrorInvalidValue;
+  const size_t lds = rollout_lds_bytes(a);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const bool split = rollout_split_form(a.pi), loco = a.P.kind == ENV_LOCO;
+  if (split && loco)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, true>), dim3(a.N), dim3(64), lds, s, a);
+  else if (split)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, false>), dim3(a.N), dim3(64), lds, s, a);
+  else if (loco)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, true>), dim3(a.N), dim3(64), lds, s, a);
+  else
+    hipLaunchKernelGGL((rollout_chain_kernel<false, false>), dim3(a.N), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ia

@@ -87,9 +87,8 @@ class OutputNormMixin:
             return {}
         if not hasattr(self, "_rew_raw"):
             self._rew_raw = th.zeros(self.T, self.N, device=self._dev)
-            self._boot = th.zeros(self.T, self.N, device=self._dev)
             self._onorm_count = th.zeros(1, device=self._dev)
-        return {"rew_raw": self._rew_raw, "boot": self._boot}
+        return {"rew_raw": self._rew_raw}
 
     def _post_rollout_rewards(self) -> None:
         out_norm = self._output_norm()

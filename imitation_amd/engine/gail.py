@@ -264,8 +264,9 @@ class DeviceGeneratorCore:
         Aw = 1 if self.discrete else self.A
         z = lambda *s: th.zeros(*s, device=dev)
         self.buf = dict(obs_buf=z(T, N, D), act_raw=z(T, N, Aw), act_env=z(T, N, Aw), logp=z(T, N), values=z(T, N),
-                        rewards=z(T, N), env_rew=z(T, N), starts=z(T, N), dones=z(T, N), next_obs=z(T, N, D),
-                        ep_ret_out=z(T, N), last_values=z(N))
+                        rewards=z(T, N), env_rew=z(T, N), starts=z(T, N), dones=z(T, N), trunc=z(T, N), boot=z(T, N),
+                        next_obs=z(T, N, D), ep_ret_out=z(T, N), last_values=z(N))
+        self._boot = self.buf["boot"]
         self.stats = z(5)
         self._seed = int(np.random.randint(0, 2**62)) ^ (pdist.rank() * 0x9E3779B97F4A7C15 & ((1 << 62) - 1))
         self._step0 = 0
@@ -318,47 +319,49 @@ class DeviceGeneratorCore:
         return d
 
     # ------------------------------------------------------------------ one generator round
-    def _rollout(self) -> None:
+    _CHAIN_OUT = ("obs_buf", "act_raw", "act_env", "env_rew", "starts", "dones", "trunc", "next_obs", "ep_ret_out")
+
+    def _launch_chain(self, explore_mode: Optional[th.Tensor] = None) -> None:
+        """The serial part of a rollout (rollout.hip): T steps of actor sampling + env
+        physics per env, nothing else on the step chain."""
         algo: PPO = self.gen_algo
         pol = algo.policy
-        args = dict(env=self._native.env_id, max_steps=self.max_steps, T=self.T, N=self.N, gamma=float(algo.gamma),
-                    seed=int(self._seed), step0=int(self._step0), state=self.state, rng=self.env_rng, elapsed=self.elapsed,
-                    ep_ret=self.ep_ret, cur_obs=self.cur_obs, cur_start=self.cur_start,
+        args = dict(env=self._native.env_id, max_steps=self.max_steps, T=self.T, N=self.N, seed=int(self._seed),
+                    step0=int(self._step0), state=self.state, rng=self.env_rng, elapsed=self.elapsed, ep_ret=self.ep_ret,
+                    cur_obs=self.cur_obs, cur_start=self.cur_start,
                     pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
-                    vf=self._wave_mlp(self.vf_layers, self.hidden_act, 0, self.pol_norm),
                     log_std=pol.log_std.detach() if self.has_log_std else None, act_low=self.act_low,
-                    act_high=self.act_high, n_actions=self.A if self.discrete else 0)
-        args.update(self.buf)
-        extra = self._rollout_extra_bufs()
-        args.update(extra)
-        inline = os.environ.get("IMITATION_AMD_INLINE_REWARD", "0") == "1"
-        if self.debug_use_ground_truth:
-            args.update(rew_enabled=0)
-            self._C.engine_rollout(args)
-        elif inline:  # learned reward evaluated inside the step loop
-            args.update(rew_enabled=1, **self._reward_spec())
-            self._C.engine_rollout(args)
-        else:
-            # the learned reward does not feed back into the dynamics: the rollout kernel only
-            # records the TimeLimit bootstrap, and every transition's reward is computed
-            # afterwards in one parallel pass (bit-identical to the in-loop evaluation)
-            if "boot" not in extra:
-                if not hasattr(self, "_boot_scratch"):
-                    self._boot_scratch = th.zeros(self.T, self.N, device=self._dev)
-                    self._rr_scratch = th.zeros(self.T, self.N, device=self._dev)
-                args.update(boot=self._boot_scratch, rew_raw=self._rr_scratch)
-            args.update(rew_enabled=0)
-            self._C.engine_rollout(args)
-            b = self.buf
-            rb = dict(rows=self.T * self.N, D=self.D, A=1 if self.discrete else self.A,
-                      n_actions=self.A if self.discrete else 0, obs=b["obs_buf"], acts=b["act_env"],
-                      next_obs=b["next_obs"], dones=b["dones"], boot=args["boot"], rewards=b["rewards"],
-                      rew_raw=extra.get("rew_raw"))
-            rb.update(self._reward_spec())
-            self._C.engine_reward_batch(rb)
-        if not self.debug_use_ground_truth:
-            self._post_rollout_rewards()
+                    act_high=self.act_high, n_actions=self.A if self.discrete else 0, explore_mode=explore_mode)
+        args.update({k: self.buf[k] for k in self._CHAIN_OUT})
+        self._C.engine_rollout(args)
         self._step0 += self.T
+
+    def _launch_post(self, reward: bool) -> None:
+        """The parallel part (engine.hip): V(s), log-probs, TimeLimit bootstrap and the learned
+        reward of all T x N transitions, V of the final observations."""
+        algo: PPO = self.gen_algo
+        pol = algo.policy
+        b = self.buf
+        d = dict(T=self.T, N=self.N, D=self.D, A=1 if self.discrete else self.A, n_actions=self.A if self.discrete else 0,
+                 gamma=float(algo.gamma), cur_obs=self.cur_obs,
+                 pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
+                 vf=self._wave_mlp(self.vf_layers, self.hidden_act, 0, self.pol_norm),
+                 log_std=pol.log_std.detach() if self.has_log_std else None, rew_enabled=int(reward))
+        d.update({k: b[k] for k in ("obs_buf", "act_raw", "act_env", "next_obs", "dones", "trunc", "env_rew", "values",
+                                    "logp", "boot", "rewards", "last_values")})
+        if reward:
+            d.update(self._reward_spec())
+            d.update(self._rollout_extra_bufs())
+        self._C.engine_rollout_post(d)
+
+    def _rollout(self) -> None:
+        """One training rollout: chain -> parallel pass (-> AIRL output normalisation). The
+        learned reward does not feed back into the dynamics, so it leaves the step chain."""
+        self._launch_chain()
+        reward = not self.debug_use_ground_truth
+        self._launch_post(reward)
+        if reward:
+            self._post_rollout_rewards()
 
     def _rollout_extra_bufs(self) -> Dict[str, Any]:
         return {}

@@ -96,7 +96,6 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
         self._explore_random = ew.current_policy == ew._random_policy
         T, N = self.T, self.N
         self._rew_raw = th.zeros(T, N, device=self._dev)
-        self._boot = th.zeros(T, N, device=self._dev)
         self._onorm_count = th.zeros(1, device=self._dev)
         self._explore_dev = th.zeros(T, dtype=th.int32, device=self._dev)
         Aw = 1 if self.discrete else self.A
@@ -117,20 +116,13 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
                     use_next_state=int(base.use_next_state), use_done=int(base.use_done), rew_transform=0)
 
     def _rollout_extra_bufs(self) -> Dict[str, Any]:
-        return {"rew_raw": self._rew_raw, "boot": self._boot}
+        return {"rew_raw": self._rew_raw}
 
     def _sample_rollout(self, explore: bool) -> None:
         """One rollout-kernel round of the current (stochastic) policy without the learned
-        reward -- ``generate_trajectories`` / ExplorationWrapper sampling."""
-        algo = self.gen_algo
-        pol = algo.policy
-        args = dict(env=self._native.env_id, max_steps=self.max_steps, T=self.T, N=self.N, gamma=float(algo.gamma),
-                    seed=int(self._seed), step0=int(self._step0), state=self.state, rng=self.env_rng, elapsed=self.elapsed,
-                    ep_ret=self.ep_ret, cur_obs=self.cur_obs, cur_start=self.cur_start,
-                    pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
-                    vf=self._wave_mlp(self.vf_layers, self.hidden_act, 0, self.pol_norm),
-                    log_std=pol.log_std.detach() if self.has_log_std else None, act_low=self.act_low,
-                    act_high=self.act_high, n_actions=self.A if self.discrete else 0, rew_enabled=0)
+        reward -- ``generate_trajectories`` / ExplorationWrapper sampling. Only the serial
+        chain runs: values, log-probs and rewards are not needed for sampling."""
+        explore_mode = None
         if explore:
             sched = np.zeros(self.T, dtype=np.int32)
             for t in range(self.T):  # ExplorationWrapper.__call__: act, then maybe switch
@@ -138,10 +130,8 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
                 if self.rng.random() < self.switch_prob:
                     self._explore_random = bool(self.rng.random() < self.random_prob)
             self._explore_dev.copy_(th.from_numpy(sched))
-            args["explore_mode"] = self._explore_dev
-        args.update(self.buf)
-        self._C.engine_rollout(args)
-        self._step0 += self.T
+            explore_mode = self._explore_dev
+        self._launch_chain(explore_mode)
 
     def _stage(self) -> th.cuda.Event:
         """Pack the round's trajectory columns on device, one async D2H into pinned memory."""

@@ -346,32 +346,3 @@ def test_device_airl_rounds_train():
     assert all(th.isfinite(p).all() for p in list(gen.policy.parameters()) + list(rn.parameters()))
     assert any(not th.equal(a, b) for a, b in zip(p0, gen.policy.parameters()))
     assert any(not th.equal(a, b) for a, b in zip(r0, rn.parameters()))
-
-
-@gpu
-@pytest.mark.parametrize("algo", ["gail", "airl"])
-def test_batched_reward_pass_matches_inline_reward(monkeypatch, algo):
-    """The post-rollout parallel reward pass (engine_reward_batch) gives exactly the rewards
-    of the in-loop evaluation (same env trajectory, same fp32 arithmetic)."""
-    if algo == "gail":
-        tr, venv, gen, rn = _setup()
-    else:
-        tr, _, _, _ = _setup_airl(normalize_output=True)
-    st = {k: getattr(tr, k).clone() for k in ("state", "env_rng", "elapsed", "ep_ret", "cur_obs", "cur_start")}
-    out = []
-    for inline in ("1", "0"):
-        monkeypatch.setenv("IMITATION_AMD_INLINE_REWARD", inline)
-        for k, v in st.items():
-            getattr(tr, k).copy_(v)
-        step0 = tr._step0
-        onorm = getattr(tr, "_output_norm", lambda: None)()
-        saved = {k: v.clone() for k, v in onorm.state_dict().items()} if onorm is not None else None
-        tr._rollout()
-        th.cuda.synchronize()
-        out.append({k: tr.buf[k].clone() for k in ("rewards", "obs_buf", "dones")})
-        tr._step0 = step0
-        if saved is not None:
-            onorm.load_state_dict(saved)
-    a, b = out
-    assert th.equal(a["obs_buf"], b["obs_buf"]) and th.equal(a["dones"], b["dones"])
-    th.testing.assert_close(a["rewards"], b["rewards"], rtol=0, atol=0)
