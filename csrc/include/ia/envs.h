@@ -29,7 +29,9 @@
 #define IA_EXPF(x) __expf(x)
 #define IA_SINF(x) __sinf(x)
 #define IA_COSF(x) __cosf(x)
+#define IA_RCPF(x) __frcp_rn(x)
 #else
+#define IA_RCPF(x) (1.0f / (x))
 #define IA_EXPF(x) expf(x)
 #define IA_SINF(x) sinf(x)
 #define IA_COSF(x) cosf(x)
@@ -230,7 +232,7 @@ IA_HD void loco_obs(const LocoParams& p, const float* s, float* o) {
 }
 
 IA_HD float stance(float q) {  // smooth contact indicator: foot on ground when q < 0
-  return 1.0f / (1.0f + IA_EXPF(8.0f * q));
+  return IA_RCPF(1.0f + IA_EXPF(8.0f * q));
 }
 
 IA_HD float loco_step(const LocoParams& p, float* s, const float* a_in) {

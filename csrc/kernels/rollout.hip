@@ -85,9 +85,28 @@ __device__ void load_actor(const WaveMLP& m, Actor<SPLIT>& r, lf* wlds) {
   }
 }
 
+// Hidden activation: compile-time for the common tanh / relu nets, runtime otherwise.
+template <int HACT>
+__device__ __forceinline__ float hidden_act(int act, float x) {
+  if (HACT == ACT_TANH) return act_fast(ACT_TANH, x);
+  if (HACT == ACT_RELU) return fmaxf(x, 0.f);
+  return act_fast(act, x);
+}
+
+// Keep a loop-invariant value in a VGPR: one wave per SIMD has registers to spare, while
+// the kernel's uniform values otherwise overflow the SGPR file and get spilled to VGPR
+// lanes (one v_readlane per use inside the step loop).
+template <typename T>
+__device__ __forceinline__ T pin(T x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // x (the normalised observation) is already in xb[0 .. 64) (zero padded). Returns, in
 // lane j < dout of the last layer (both halves in split form), the actor output j.
-template <bool SPLIT>
+// The split form always runs 4 groups of 4 inputs (zero weights pad the short layers):
+// 4 extra FMAs on the 17-input layer instead of uniform branches around every group.
+template <bool SPLIT, int HACT>
 __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
   const int lane = threadIdx.x;
   const int j = SPLIT ? (lane & 31) : lane;
@@ -101,13 +120,11 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
       if (SPLIT) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          if (g < r.ng[l]) {
-            const f32v4 v = src[g];
-            acc0 = fmaf(r.w[l][4 * g + 0], v.x, acc0);
-            acc1 = fmaf(r.w[l][4 * g + 1], v.y, acc1);
-            acc0 = fmaf(r.w[l][4 * g + 2], v.z, acc0);
-            acc1 = fmaf(r.w[l][4 * g + 3], v.w, acc1);
-          }
+          const f32v4 v = src[g];
+          acc0 = fmaf(r.w[l][4 * g + 0], v.x, acc0);
+          acc1 = fmaf(r.w[l][4 * g + 1], v.y, acc1);
+          acc0 = fmaf(r.w[l][4 * g + 2], v.z, acc0);
+          acc1 = fmaf(r.w[l][4 * g + 3], v.w, acc1);
         }
       } else {
         const lf4* w4 = (const lf4*)r.wt[l] + lane;
@@ -122,7 +139,7 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
       float acc = acc0 + acc1;
       if (SPLIT) acc = add_halves(acc);
       const bool last = l == r.n_layers - 1;
-      h = j < r.dout[l] ? (last ? acc : act_fast(r.hidden_act, acc)) : 0.f;
+      h = j < r.dout[l] ? (last ? acc : hidden_act<HACT>(r.hidden_act, acc)) : 0.f;
       if (!last) {
         wave_sync();  // every lane has read this layer's input
         if (lane < (SPLIT ? 32 : 64)) xb[lane] = h;
@@ -144,10 +161,14 @@ __device__ __noinline__ void env_reset_lane0(const EnvParams& P, float* s, float
 }
 
 // ---------------------------------------------------------------- locomotion, state in registers
+// ENV template values of the chain kernel.
+enum ChainEnv : int { CE_GENERIC = 0, CE_LOCO = 1, CE_LOCO3 = 2 /* planar root: nq_root == nv_root == 3 */ };
+
 struct LocoRegs {
   float q, qd;          // joint lane state (lane < nj)
   float rq[8], rv[8];   // root coordinates (uniform)
   float gear, stiff, damp, thrust, pcoup;  // per-joint-lane constants
+  float dt, drag, fwd_weight, healthy, ctrl_cost, inv_nj, inv_dt_total;
 };
 
 __device__ void loco_load(const LocoParams& p, const lf* s, LocoRegs& L) {
@@ -178,12 +199,15 @@ __device__ void loco_store(const LocoParams& p, const LocoRegs& L, lf* s) {
 }
 
 // Observation [qpos[obs_skip:], qvel] in lane layout, through the LDS scratch sb.
+template <int ENV>
 __device__ float loco_obs(const LocoParams& p, const LocoRegs& L, lf* sb) {
   const int lane = threadIdx.x;
-  const int npr = p.nq_root - p.obs_skip, nj = p.nj;
+  const int nr = ENV == CE_LOCO3 ? 3 : 8;
+  const int nqr = ENV == CE_LOCO3 ? 3 : p.nq_root, nvr = ENV == CE_LOCO3 ? 3 : p.nv_root;
+  const int npr = nqr - p.obs_skip, nj = p.nj;
   float rqi = 0.f, rvi = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < nr; ++i) {
     rqi = (lane + p.obs_skip) == i ? L.rq[i] : rqi;
     rvi = lane == i ? L.rv[i] : rvi;
   }
@@ -191,16 +215,17 @@ __device__ float loco_obs(const LocoParams& p, const LocoRegs& L, lf* sb) {
   if (lane < npr) sb[lane] = rqi;
   if (lane < nj) {
     sb[npr + lane] = L.q;
-    sb[npr + nj + p.nv_root + lane] = L.qd;
+    sb[npr + nj + nvr + lane] = L.qd;
   }
-  if (lane < p.nv_root) sb[npr + nj + lane] = rvi;
+  if (lane < nvr) sb[npr + nj + lane] = rvi;
   wave_sync();
-  const int D = npr + nj + p.nv_root + nj;
+  const int D = npr + nj + nvr + nj;
   return lane < D ? sb[lane] : 0.f;
 }
 
-// ia::loco_step (envs.h) with the joint loops spread over lanes; a = clipped action of
-// joint lane j (0 elsewhere). Returns the step reward (uniform).
+// ia::loco_step (envs.h) with the joint loops spread over lanes; a_in = action of joint
+// lane j. Returns the step reward (uniform).
+template <int ENV>
 __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
   const int lane = threadIdx.x;
   const bool jl = lane < p.nj;
@@ -208,8 +233,7 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
   const float ctrl = sum_lanes8(a * a);
   const float pitch = sum_lanes8(L.pcoup * a);
   const float x_before = L.rq[0];
-  const float dt = p.dt;
-  const float inv_nj = 1.f / (float)p.nj;
+  const float dt = L.dt;
   float q = L.q, qd = L.qd;
   for (int sub = 0; sub < p.frame_skip; ++sub) {
     const float qdd = L.gear * a - L.stiff * q - L.damp * qd - 2.0f * __sinf(q);
@@ -219,24 +243,32 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
     const float thrust = sum_lanes8(th_j);
     const float lift = sum_lanes8(st);
     const float vx = L.rv[0];
-    L.rv[0] = vx + dt * (thrust - p.drag * vx * (1.0f + fabsf(vx)));
-    if (p.nv_root > 1) L.rv[1] = L.rv[1] + dt * (-20.f * L.rq[1] - 4.f * L.rv[1] + 0.5f * (lift * inv_nj - 0.5f));
-    if (p.nv_root > 2) L.rv[2] = L.rv[2] + dt * (-15.f * __sinf(L.rq[2]) - 3.f * L.rv[2] + pitch);
+    L.rv[0] = vx + dt * (thrust - L.drag * vx * (1.0f + fabsf(vx)));
+    if (ENV == CE_LOCO3) {
+      L.rv[1] = L.rv[1] + dt * (-20.f * L.rq[1] - 4.f * L.rv[1] + 0.5f * (lift * L.inv_nj - 0.5f));
+      L.rv[2] = L.rv[2] + dt * (-15.f * __sinf(L.rq[2]) - 3.f * L.rv[2] + pitch);
+      L.rq[0] += dt * L.rv[0];
+      L.rq[1] += dt * L.rv[1] * 1.f;
+      L.rq[2] += dt * L.rv[2] * 1.f;
+    } else {
+      if (p.nv_root > 1) L.rv[1] = L.rv[1] + dt * (-20.f * L.rq[1] - 4.f * L.rv[1] + 0.5f * (lift * L.inv_nj - 0.5f));
+      if (p.nv_root > 2) L.rv[2] = L.rv[2] + dt * (-15.f * __sinf(L.rq[2]) - 3.f * L.rv[2] + pitch);
 #pragma unroll
-    for (int i = 3; i < 8; ++i)
-      if (i < p.nv_root) L.rv[i] = L.rv[i] * (1.f - 2.f * dt) + dt * 0.1f * pitch;
-    L.rq[0] += dt * L.rv[0];
+      for (int i = 3; i < 8; ++i)
+        if (i < p.nv_root) L.rv[i] = L.rv[i] * (1.f - 2.f * dt) + dt * 0.1f * pitch;
+      L.rq[0] += dt * L.rv[0];
 #pragma unroll
-    for (int i = 1; i < 8; ++i) {
-      if (i < p.nq_root) {
-        if (i < p.nv_root) {
-          L.rq[i] += dt * L.rv[i] * 1.f;
-        } else {  // free-joint quaternion slots (3D bodies only)
-          const int vi = i % p.nv_root;
-          float v = 0.f;
+      for (int i = 1; i < 8; ++i) {
+        if (i < p.nq_root) {
+          if (i < p.nv_root) {
+            L.rq[i] += dt * L.rv[i] * 1.f;
+          } else {  // free-joint quaternion slots (3D bodies only)
+            const int vi = i % p.nv_root;
+            float v = 0.f;
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v = u == vi ? L.rv[u] : v;
-          L.rq[i] += dt * v * 0.1f;
+            for (int u = 0; u < 8; ++u) v = u == vi ? L.rv[u] : v;
+            L.rq[i] += dt * v * 0.1f;
+          }
         }
       }
     }
@@ -247,11 +279,23 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
   }
   L.q = jl ? q : 0.f;
   L.qd = jl ? qd : 0.f;
-  const float dt_total = dt * p.frame_skip;
-  return p.fwd_weight * (L.rq[0] - x_before) / dt_total + p.healthy_reward - p.ctrl_cost * ctrl;
+  return L.fwd_weight * (L.rq[0] - x_before) * L.inv_dt_total + L.healthy - L.ctrl_cost * ctrl;
 }
 
-template <bool SPLIT, bool LOCO>
+// Per-lane output cursors (VGPRs, advanced by one step per iteration): the per-step
+// stores need no scalar base registers, and the five per-env scalars of a step go out
+// as ONE store (lane 0 env reward, 1 done, 2 truncation, 3 finished-episode return,
+// 4 episode start).
+struct Cursors {
+  float* obs;
+  float* next_obs;
+  float* act_raw;
+  float* act_env;
+  float* sc;
+  int vec_step, act_step, sc_step;
+};
+
+template <bool SPLIT, int ENV, int HACT>
 __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
@@ -259,7 +303,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   lf* st = sb + 64;            // [kMaxState] env state (generic envs, resets)
   lf* act = st + kMaxState;    // [64]
   lf* noise = act + 64;        // [kNoiseFloats]
-  li* explore = (li*)(noise + kNoiseFloats);  // [chunk]
+  li* explore = (li*)(noise + kNoiseFloats);  // [T]
   lf* wlds = (lf*)(explore + ((a.T + 3) & ~3)); // full-form actor weights (16-B aligned)
   const int n = blockIdx.x;
   const int lane = threadIdx.x;
@@ -269,16 +313,16 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   const int A = discrete ? 1 : P.act_dim;
   const int AW = discrete ? a.n_actions : P.act_dim;  // noise values per step
   const int S = state_size(P);
-  constexpr bool loco = LOCO;
+  constexpr bool loco = ENV != CE_GENERIC;
 
   Actor<SPLIT> ar;
   load_actor<SPLIT>(a.pi, ar, wlds);
-  const float nmean = (a.pi.norm_mean && lane < D) ? a.pi.norm_mean[lane] : 0.f;
-  const float nrstd = (a.pi.norm_mean && lane < D) ? rsqrtf(a.pi.norm_var[lane] + a.pi.norm_eps) : 1.f;
+  const float nmean = pin((a.pi.norm_mean && lane < D) ? a.pi.norm_mean[lane] : 0.f);
+  const float nrstd = pin((a.pi.norm_mean && lane < D) ? rsqrtf(a.pi.norm_var[lane] + a.pi.norm_eps) : 1.f);
   const float lstd = (!discrete && a.log_std && lane < A) ? a.log_std[lane] : 0.f;
-  const float sd = expf(lstd);
-  const float lo = (!discrete && a.act_low && lane < A) ? a.act_low[lane] : 0.f;
-  const float hi = (!discrete && a.act_high && lane < A) ? a.act_high[lane] : 0.f;
+  const float sd = pin(expf(lstd));
+  const float lo = pin((!discrete && a.act_low && lane < A) ? a.act_low[lane] : 0.f);
+  const float hi = pin((!discrete && a.act_high && lane < A) ? a.act_high[lane] : 0.f);
 
   for (int i = lane; i < S; i += 64) st[i] = a.state[(size_t)n * S + i];
   xb[lane] = 0.f;
@@ -286,14 +330,34 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   if (loco) {
     const LocoParams& p = P.loco;
     const bool jl = lane < p.nj;
-    L.gear = jl ? p.gear[lane] : 0.f;
-    L.stiff = jl ? p.stiff[lane] : 0.f;
-    L.damp = jl ? p.damp[lane] : 0.f;
-    L.thrust = jl ? p.thrust[lane] : 0.f;
-    L.pcoup = jl ? p.pitch_coupling[lane] : 0.f;
+    L.gear = pin(jl ? p.gear[lane] : 0.f);
+    L.stiff = pin(jl ? p.stiff[lane] : 0.f);
+    L.damp = pin(jl ? p.damp[lane] : 0.f);
+    L.thrust = pin(jl ? p.thrust[lane] : 0.f);
+    L.pcoup = pin(jl ? p.pitch_coupling[lane] : 0.f);
+    L.dt = pin(p.dt);
+    L.drag = pin(p.drag);
+    L.fwd_weight = pin(p.fwd_weight);
+    L.healthy = pin(p.healthy_reward);
+    L.ctrl_cost = pin(p.ctrl_cost);
+    L.inv_nj = pin(1.f / (float)p.nj);
+    L.inv_dt_total = pin(1.f / (p.dt * (float)p.frame_skip));
   }
   wave_sync();
   if (loco) loco_load(P.loco, st, L);
+
+  Cursors c;
+  c.vec_step = a.N * D;
+  c.act_step = a.N * A;
+  c.sc_step = a.N;
+  c.obs = pin(a.obs_buf + (size_t)n * D + (lane < D ? lane : 0));
+  c.next_obs = pin(a.next_obs + (size_t)n * D + (lane < D ? lane : 0));
+  c.act_raw = pin(a.act_raw + (size_t)n * A + (lane < A ? lane : 0));
+  c.act_env = pin(a.act_env + (size_t)n * A + (lane < A ? lane : 0));
+  {
+    float* b = lane == 0 ? a.env_rew : lane == 1 ? a.dones : lane == 2 ? a.trunc : lane == 3 ? a.ep_ret_out : a.starts;
+    c.sc = pin(b + n);
+  }
 
   float o = lane < D ? a.cur_obs[(size_t)n * D + lane] : 0.f;
   float start = a.cur_start[n];
@@ -301,6 +365,8 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   int elapsed = a.elapsed[n];
   float ep_ret = a.ep_ret[n];
   const int chunk = AW > 0 ? max(1, min(a.T, kNoiseFloats / AW)) : a.T;
+  const bool has_explore = a.explore_mode != nullptr;
+  const int max_steps = a.max_steps;
 
   for (int t0 = 0; t0 < a.T; t0 += chunk) {
     const int tc = min(chunk, a.T - t0);
@@ -319,31 +385,30 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       }
       noise[e] = v;
     }
-    for (int e = lane; e < tc; e += 64) explore[e] = a.explore_mode ? a.explore_mode[t0 + e] : 0;
+    if (has_explore)
+      for (int e = lane; e < tc; e += 64) explore[e] = a.explore_mode[t0 + e];
     wave_sync();
 
-    for (int tr = 0; tr < tc; ++tr) {
-      const int t = t0 + tr;
-      const size_t row = (size_t)t * a.N + n;
-      if (lane < D) a.obs_buf[row * D + lane] = o;
-      if (lane == 0) a.starts[row] = start;
+    const lf* nz = noise + (lane < AW ? lane : 0);
+    for (int tr = 0; tr < tc; ++tr, nz += AW) {
+      if (lane < D) *c.obs = o;
       // ---- actor
       xb[lane] = lane < D ? (o - nmean) * nrstd : 0.f;
       wave_sync();
-      const float head = actor_forward<SPLIT>(ar, xb);
+      const float head = actor_forward<SPLIT, HACT>(ar, xb);
       float a_raw, a_env;
       if (discrete) {
-        const float g = lane < a.n_actions ? head + noise[tr * AW + lane] : -INFINITY;
+        const float g = lane < a.n_actions ? head + *nz : -INFINITY;
         const float mx = wave_max(g);
         const unsigned long long m = __ballot(g == mx && lane < a.n_actions);
         const int k = m ? __builtin_ctzll(m) : a.n_actions - 1;
         a_raw = a_env = (float)k;
       } else {
-        a_raw = lane < A ? head + sd * noise[tr * AW + lane] : 0.f;
-        a_env = lane < A ? fminf(fmaxf(a_raw, lo), hi) : 0.f;
+        a_raw = head + sd * *nz;
+        a_env = fminf(fmaxf(a_raw, lo), hi);
       }
-      if (explore[tr]) {  // ExplorationWrapper's random policy (uniform branch)
-        const uint64_t key = hash3(a.seed, (uint64_t)n, (uint64_t)(a.step0 + t));
+      if (has_explore && explore[tr]) {  // ExplorationWrapper's random policy (uniform branch)
+        const uint64_t key = hash3(a.seed, (uint64_t)n, (uint64_t)(a.step0 + t0 + tr));
         uint64_t s = key ^ kExploreTweak;
         if (discrete) {
           s ^= kExploreDiscreteTweak;
@@ -354,21 +419,21 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
         } else {
           s ^= kLaneTweak * (uint64_t)(lane + 1);
           const float u = uniform01(s);
-          a_env = lane < A ? lo + u * (hi - lo) : 0.f;
+          a_env = lo + u * (hi - lo);
           a_raw = a_env;
         }
       }
       if (lane < A) {
-        a.act_raw[row * A + lane] = a_raw;
-        a.act_env[row * A + lane] = a_env;
+        *c.act_raw = a_raw;
+        *c.act_env = a_env;
       }
       // ---- env step + SB3 auto-reset, TimeLimit, Monitor
       int term = 0;
       float r_env;
       float o_next;
       if (loco) {
-        r_env = loco_step_regs(P.loco, L, a_env);
-        o_next = loco_obs(P.loco, L, sb);
+        r_env = loco_step_regs<ENV>(P.loco, L, a_env);
+        o_next = loco_obs<ENV>(P.loco, L, sb);
       } else {
         if (lane < A) act[lane] = a_env;
         wave_sync();
@@ -383,17 +448,20 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       }
       elapsed += 1;
       ep_ret += r_env;
-      const bool trunc = !term && elapsed >= a.max_steps;
+      const bool trunc = !term && elapsed >= max_steps;
       const bool done = term || trunc;
-      if (lane < D) a.next_obs[row * D + lane] = o_next;
-      if (lane == 0) {
-        a.env_rew[row] = r_env;
-        a.dones[row] = done ? 1.f : 0.f;
-        a.trunc[row] = trunc ? 1.f : 0.f;
-        a.ep_ret_out[row] = done ? ep_ret : 0.f;
+      if (lane < D) *c.next_obs = o_next;
+      if (lane < 5) {
+        const float v = lane == 0 ? r_env : lane == 1 ? (done ? 1.f : 0.f) : lane == 2 ? (trunc ? 1.f : 0.f)
+                      : lane == 3 ? (done ? ep_ret : 0.f) : start;
+        *c.sc = v;
       }
+      c.obs += c.vec_step;
+      c.next_obs += c.vec_step;
+      c.act_raw += c.act_step;
+      c.act_env += c.act_step;
+      c.sc += c.sc_step;
       if (done) {
-        if (loco) loco_store(P.loco, L, st);
         wave_sync();
         if (lane == 0) {
           if (loco) loco_reset(P.loco, (float*)st, rng);
@@ -402,7 +470,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
         wave_sync();
         if (loco) {
           loco_load(P.loco, st, L);
-          o = loco_obs(P.loco, L, sb);
+          o = loco_obs<ENV>(P.loco, L, sb);
         } else {
           o = lane < D ? sb[lane] : 0.f;
         }
@@ -451,15 +519,27 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   if (a.n_actions > 64 || (a.P.kind == ENV_LOCO && a.P.loco.nj > 8)) return hipErrorInvalidValue;
   const size_t lds = rollout_lds_bytes(a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const bool split = rollout_split_form(a.pi), loco = a.P.kind == ENV_LOCO;
-  if (split && loco)
-    hipLaunchKernelGGL((rollout_chain_kernel<true, true>), dim3(a.N), dim3(64), lds, s, a);
+  const bool split = rollout_split_form(a.pi);
+  const LocoParams& p = a.P.loco;
+  const int env = a.P.kind != ENV_LOCO ? CE_GENERIC : (p.nq_root == 3 && p.nv_root == 3) ? CE_LOCO3 : CE_LOCO;
+  const int act = a.pi.n_layers > 1 ? a.pi.hidden_act : ACT_IDENTITY;
+  const dim3 g(a.N), b(64);
+  if (split && env == CE_LOCO3 && act == ACT_TANH)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH>), g, b, lds, s, a);
+  else if (split && env == CE_LOCO3 && act == ACT_RELU)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_RELU>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_TANH)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_TANH>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_RELU)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_RELU>), g, b, lds, s, a);
+  else if (split && env == CE_GENERIC)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_GENERIC, -1>), g, b, lds, s, a);
+  else if (!split && env == CE_GENERIC)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_GENERIC, -1>), g, b, lds, s, a);
   else if (split)
-    hipLaunchKernelGGL((rollout_chain_kernel<true, false>), dim3(a.N), dim3(64), lds, s, a);
-  else if (loco)
-    hipLaunchKernelGGL((rollout_chain_kernel<false, true>), dim3(a.N), dim3(64), lds, s, a);
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO, -1>), g, b, lds, s, a);
   else
-    hipLaunchKernelGGL((rollout_chain_kernel<false, false>), dim3(a.N), dim3(64), lds, s, a);
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO, -1>), g, b, lds, s, a);
   return hipGetLastError();
 }
 
