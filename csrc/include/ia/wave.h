@@ -31,16 +31,6 @@ __device__ __forceinline__ float bcast(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
 
 // DPP lane moves (bound_ctrl: out-of-row sources read 0).
 template <int CTRL>
@@ -57,12 +47,50 @@ __device__ __forceinline__ float sum_lanes8(float v) {
   return bcast(v, 7);
 }
 
+// Sum over the 16 lanes of each DPP row, result in every lane of the row: pair and quad
+// butterflies (quad_perm), then row_half_mirror (quad 0 <-> quad 1 of each 8-lane half)
+// and row_mirror (half 0 <-> half 1). Four v_add_f32_dpp, no LDS traffic (a __shfl_xor
+// butterfly is four ds_bpermute round trips).
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
+  return v;
+}
+
+// Lane i <-> lane i ^ 16 (gfx950 v_permlane16_swap: odd rows of the first operand trade
+// places with even rows of the second); returns own + partner / max(own, partner).
+__device__ __forceinline__ float add_rows16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max_rows16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_halves(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 // Lane i <-> lane i ^ 32 (gfx950 v_permlane32_swap: lanes 32-63 of the first operand
 // trade places with lanes 0-31 of the second); returns own + partner in every lane.
 __device__ __forceinline__ float add_halves(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+
+// Whole-wave sum / max in every lane: DPP row reduction, then the two cross-row swaps.
+__device__ __forceinline__ float wave_sum(float v) { return add_halves(add_rows16(row_sum16(v))); }
+__device__ __forceinline__ float wave_max(float v) { return max_halves(max_rows16(row_max16(v))); }
 
 // tanh as 1 - 2 / (exp(2x) + 1) on v_exp_f32 / v_rcp_f32 (|err| ~1e-7 abs).
 __device__ __forceinline__ float act_fast(int act, float x) {

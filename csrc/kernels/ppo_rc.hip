@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ia/engine.h"
+#include "ia/wave.h"
 #include "launchers.h"
 
 namespace ia {
@@ -80,28 +81,12 @@ __device__ __forceinline__ float act_grad(int act, float y) {
     default: return 1.f;
   }
 }
-__device__ __forceinline__ float sum16(float v) {  // over the 16 rows (lanes with equal lane>>4)
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
-  return v;
-}
-__device__ __forceinline__ float sum_kk(float v) {  // over the 4 lane groups of one row
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
-}
-__device__ __forceinline__ float max_kk(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16));
-  v = fmaxf(v, __shfl_xor(v, 32));
-  return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+// Row / lane-group reductions without LDS round trips (ia/wave.h): sum16 over the 16 rows
+// of an MFMA tile (lanes with equal lane >> 4), sum_kk / max_kk over the 4 lane groups
+// of one row (lanes r, r + 16, r + 32, r + 48).
+__device__ __forceinline__ float sum16(float v) { return row_sum16(v); }
+__device__ __forceinline__ float sum_kk(float v) { return add_halves(add_rows16(v)); }
+__device__ __forceinline__ float max_kk(float v) { return max_halves(max_rows16(v)); }
 
 // sc1 (L1-bypassing, agent-coherent) accesses for the cross-workgroup hand-off. The
 // 16-B forms are inline asm so that a lane can issue all G partial loads back to back
@@ -401,6 +386,35 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       }
     }
   }
+  // loop-invariant item bookkeeping (kind, bias-partial source, Adam targets), computed once
+  // instead of re-reading the descriptors and layer geometry every minibatch
+  int ikind[KI], ib_off[KI], ib_ok[KI], paddr[KI][4];
+#pragma unroll
+  for (int it = 0; it < KI; ++it) {
+    const int id = w + it * kWaves;
+    ikind[it] = -1;
+    ib_off[it] = 0;
+    ib_ok[it] = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) paddr[it][j] = -1;
+    if (id >= n_items) continue;
+    const int desc = rfl(g.items[id]);
+    const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+    const LG y = lg(g, iq, il);
+    ikind[it] = kind;
+    if (kind == 0) {
+      const int in = 16 * tb + r16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = 16 * ta + 4 * kk + j;
+        if (o < y.dout && in < y.din) paddr[it][j] = y.w + o * y.ldw + in;
+      }
+    } else {
+      ib_off[it] = kind == 1 ? y.db : g.lsp_off;
+      ib_ok[it] = kind == 1 ? (lane < y.dout) : (has_ls && lane < A);
+      if (ib_ok[it]) paddr[it][0] = kind == 1 ? y.b + lane : g.ls_off + lane;
+    }
+  }
   float pre_m = 0.f, pre_v = 0.f;  // moments of the next minibatch to merge
   if (norm_lane && K > 1) {
     pre_m = g.mom[128 + nc];
@@ -682,11 +696,8 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       // ---------------- dW / db / dlog_std partials of this chunk for the owned items
 #pragma unroll
       for (int it = 0; it < KI; ++it) {
-        const int id = w + it * kWaves;
-        if (id >= n_items) continue;
-        const int desc = rfl(g.items[id]);
-        const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3;
-        if (kind == 0) {
+        if (ikind[it] < 0) continue;
+        if (ikind[it] == 0) {
           f4 acc = {0.f, 0.f, 0.f, 0.f};
           const lf* zp = L + izo[it];
           const lf* hp = L + iho[it];
@@ -696,16 +707,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           gg[it][1] += (imask[it] & 2) ? acc.y : 0.f;
           gg[it][2] += (imask[it] & 4) ? acc.z : 0.f;
           gg[it][3] += (imask[it] & 8) ? acc.w : 0.f;
-        } else if (kind == 1) {
-          const LG y = lg(g, iq, il);
+        } else {  // bias (row-tile partials of dZ) / log_std (partials of the Gaussian term)
+          const int stride = ikind[it] == 1 ? 64 : 16;
           float gval = 0.f;
-          if (lane < y.dout)
-            for (int r = 0; r < RT; ++r) gval += L[y.db + r * 64 + lane];
-          gg[it][0] += gval;
-        } else {
-          float gval = 0.f;
-          if (has_ls && lane < A)
-            for (int r = 0; r < RT; ++r) gval += L[g.lsp_off + r * 16 + lane];
+          if (ib_ok[it])
+            for (int r = 0; r < RT; ++r) gval += L[ib_off[it] + r * stride + lane];
           gg[it][0] += gval;
         }
       }
@@ -767,11 +773,8 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     float ss = 0.f;
 #pragma unroll
     for (int it = 0; it < KI; ++it) {
-      const int id = w + it * kWaves;
-      if (id >= n_items) continue;
-      const int desc = rfl(g.items[id]);
-      const int kind = (desc >> 3) & 3;
-      if (kind == 2 && has_ls && lane < A) gg[it][0] -= a.ent_coef;
+      if (ikind[it] < 0) continue;
+      if (ikind[it] == 2 && ib_ok[it]) gg[it][0] -= a.ent_coef;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ss += gg[it][j] * gg[it][j];
     }
@@ -795,36 +798,26 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     b1t *= a.beta1;
     b2t *= a.beta2;
     const float step_size = a.lr / (1.f - b1t);
-    const float bc2s = sqrtf(1.f - b2t);
+    const float inv_bc2s = 1.f / sqrtf(1.f - b2t);
     const float b1 = a.beta1, b2 = a.beta2, eps = a.adam_eps;
+    // torch Adam: p -= step_size * m / (sqrt(v) / sqrt(1 - b2^t) + eps), on v_sqrt / v_rcp
+    // (~1 ulp each). All of this wave's parameter reads are issued before any write
+    // (the items never alias), so the LDS read latency is paid once, not per element.
+    float pval[KI][4];
+#pragma unroll
+    for (int it = 0; it < KI; ++it)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pval[it][j] = paddr[it][j] >= 0 ? L[paddr[it][j]] : 0.f;
 #pragma unroll
     for (int it = 0; it < KI; ++it) {
-      const int id = w + it * kWaves;
-      if (id >= n_items) continue;
-      const int desc = rfl(g.items[id]);
-      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-      const LG y = lg(g, iq, il);
-      if (kind == 0) {
-        const int in = 16 * tb + r16;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int o = 16 * ta + 4 * kk + j;
-          if (o < y.dout && in < y.din) {
-            const float gval = gg[it][j] * coef;
-            gm[it][j] = b1 * gm[it][j] + (1.f - b1) * gval;
-            gv[it][j] = b2 * gv[it][j] + (1.f - b2) * gval * gval;
-            L[y.w + o * y.ldw + in] -= step_size * gm[it][j] / (sqrtf(gv[it][j]) / bc2s + eps);
-          }
-        }
-      } else {
-        const bool ok = kind == 1 ? lane < y.dout : (has_ls && lane < A);
-        if (ok) {
-          const float gval = gg[it][0] * coef;
-          gm[it][0] = b1 * gm[it][0] + (1.f - b1) * gval;
-          gv[it][0] = b2 * gv[it][0] + (1.f - b2) * gval * gval;
-          const int p = kind == 1 ? y.b + lane : g.ls_off + lane;
-          L[p] -= step_size * gm[it][0] / (sqrtf(gv[it][0]) / bc2s + eps);
-        }
+      for (int j = 0; j < 4; ++j) {
+        if (paddr[it][j] < 0) continue;
+        const float gval = gg[it][j] * coef;
+        gm[it][j] = b1 * gm[it][j] + (1.f - b1) * gval;
+        gv[it][j] = b2 * gv[it][j] + (1.f - b2) * gval * gval;
+        const float denom = __builtin_amdgcn_sqrtf(gv[it][j]) * inv_bc2s + eps;
+        L[paddr[it][j]] = pval[it][j] - step_size * gm[it][j] * __builtin_amdgcn_rcpf(denom);
       }
     }
     __syncthreads();  // B3: parameters updated
