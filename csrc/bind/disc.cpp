@@ -142,6 +142,23 @@ class DiscPlan {
   }
 
   int n_params() const { return n_params_; }
+  int n_minibatches() const { return n_mb_; }
+  int pol_cols() const { return n_.pol_cols; }
+  // [slots, 2 * pol_cols + 1] float32 record buffer for deferred policy-norm merges
+  void set_pol_defer(torch::Tensor t) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32 && t.dim() == 2 &&
+                    t.size(1) == 2 * n_.pol_cols + 1,
+                "pol_defer must be a contiguous float32 GPU tensor [slots, 2 * pol_cols + 1]");
+    defer_ = t;
+    defer_slots_ = (int)t.size(0);
+  }
+  // apply slots [0, n_slots) of the deferred records to the policy RunningNorm, in order
+  void pol_norm_merge(int n_slots) {
+    TORCH_CHECK(defer_.defined() && n_slots <= defer_slots_, "pol_norm_merge: bad slot count");
+    TORCH_CHECK(n_.pol_mean && n_.pol_count, "plan has no policy norm");
+    IA_HIP_CHECK3(ia::pol_norm_merge(n_.pol_mean, n_.pol_var, n_.pol_count, defer_.data_ptr<float>(), n_slots,
+                                     n_.pol_cols, ia_stream()));
+  }
 
   // One minibatch: gather + (local) moments + norm merge, or DP split via `sums`.
   void gather(int k, torch::Tensor e_idx, torch::Tensor g_idx) {
@@ -153,8 +170,15 @@ class DiscPlan {
     IA_HIP_CHECK3(ia::disc_gather(g, ia_stream()));
   }
   // merge_rew / merge_pol: whether each RunningNorm is in training mode (updates its stats)
-  void norm(int mode, int n_total, bool merge_rew, bool merge_pol) {
+  // pol_defer_slot >= 0: the policy-norm merge is recorded into slot k of the buffer set by
+  // set_pol_defer (applied later by pol_norm_merge) instead of done in place
+  void norm(int mode, int n_total, bool merge_rew, bool merge_pol, int pol_defer_slot = -1) {
     ia::DiscNormArgs n = n_;
+    n.pol_defer = nullptr;
+    if (merge_pol && pol_defer_slot >= 0) {
+      TORCH_CHECK(defer_.defined() && pol_defer_slot < defer_slots_, "pol_defer slot ", pol_defer_slot, " out of range");
+      n.pol_defer = defer_.data_ptr<float>() + (size_t)pol_defer_slot * (2 * n_.pol_cols + 1);
+    }
     n.mode = mode;
     n.n_total = n_total;
     if (!merge_rew) {
@@ -190,10 +214,10 @@ class DiscPlan {
   }
   // Whole single-rank update: all minibatches + Adam, 3 launches per minibatch + 1.
   void update(torch::Tensor e_idx, torch::Tensor g_idx, double step_size, double bc2_sqrt, bool merge_rew, bool merge_pol,
-              c10::optional<torch::Tensor> stats_out) {
+              c10::optional<torch::Tensor> stats_out, int pol_defer_base = -1) {
     for (int k = 0; k < n_mb_; ++k) {
       gather(k, e_idx, g_idx);
-      if (merge_rew || merge_pol) norm(0, 0, merge_rew, merge_pol);
+      if (merge_rew || merge_pol) norm(0, 0, merge_rew, merge_pol, pol_defer_base < 0 ? -1 : pol_defer_base + k);
       fwd_bwd(k);
     }
     adam(1, 1, step_size, bc2_sqrt, stats_out);
@@ -205,6 +229,8 @@ class DiscPlan {
                 "indices must be int64 GPU tensors of >= batch entries");
   }
   std::vector<torch::Tensor> held_;
+  torch::Tensor defer_;
+  int defer_slots_ = 0;
   ia::MLPDesc desc_{};
   ia::DiscGatherArgs g_{};
   ia::DiscNormArgs n_{};
@@ -232,11 +258,16 @@ void register_disc(py::module& m) {
       .def(py::init<py::dict>())
       .def_property_readonly("n_params", &DiscPlan::n_params)
       .def("gather", &DiscPlan::gather)
-      .def("norm", &DiscPlan::norm, py::arg("mode"), py::arg("n_total"), py::arg("merge_rew"), py::arg("merge_pol"))
+      .def_property_readonly("n_minibatches", &DiscPlan::n_minibatches)
+      .def_property_readonly("pol_cols", &DiscPlan::pol_cols)
+      .def("set_pol_defer", &DiscPlan::set_pol_defer)
+      .def("pol_norm_merge", &DiscPlan::pol_norm_merge, py::arg("n_slots"))
+      .def("norm", &DiscPlan::norm, py::arg("mode"), py::arg("n_total"), py::arg("merge_rew"), py::arg("merge_pol"),
+           py::arg("pol_defer_slot") = -1)
       .def("fwd_bwd", &DiscPlan::fwd_bwd)
       .def("adam", &DiscPlan::adam, py::arg("reduce"), py::arg("do_adam"), py::arg("step_size"), py::arg("bc2_sqrt"),
            py::arg("stats_out") = py::none())
       .def("update", &DiscPlan::update, py::arg("e_idx"), py::arg("g_idx"), py::arg("step_size"), py::arg("bc2_sqrt"),
-           py::arg("merge_rew"), py::arg("merge_pol"), py::arg("stats_out") = py::none());
+           py::arg("merge_rew"), py::arg("merge_pol"), py::arg("stats_out") = py::none(), py::arg("pol_defer_base") = -1);
   m.def("disc_plan_sizes", &disc_plan_sizes, py::arg("dims"), py::arg("minibatch"));
 }

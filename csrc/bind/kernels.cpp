@@ -102,6 +102,15 @@ py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch:
   return py::make_tuple(adv, ret);
 }
 
+// [E, n] int32: row e is a pseudo-random permutation of 0..n-1 keyed by (seed, e).
+torch::Tensor random_permutations(int64_t E, int64_t n, int64_t seed, torch::Device device) {
+  TORCH_CHECK(device.is_cuda(), "random_permutations runs on the GPU");
+  TORCH_CHECK(E >= 0 && n >= 0 && n <= (1ll << 30), "bad permutation shape");
+  auto out = torch::empty({E, n}, torch::TensorOptions().dtype(torch::kInt32).device(device));
+  IA_HIP_CHECK(ia::perm_feistel((int)E, (int)n, (uint64_t)seed, out.data_ptr<int>(), ia_stream()));
+  return out;
+}
+
 // Returns (probs [P], losses [P], coef [P]).
 py::tuple pref_loss_fwd(torch::Tensor r1, torch::Tensor r2, torch::Tensor prefs, double discount, double threshold,
                         double noise) {
@@ -145,4 +154,5 @@ void register_kernels(py::module& m) {
         py::arg("norm_eps") = 1e-5, py::arg("norm_clip") = 0.0, py::arg("need_dx") = false);
   m.def("gae", &gae, py::arg("rewards"), py::arg("values"), py::arg("episode_starts"), py::arg("last_values"),
         py::arg("dones"), py::arg("gamma"), py::arg("lam"));
+  m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
 }

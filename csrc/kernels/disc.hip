@@ -141,15 +141,38 @@ __global__ __launch_bounds__(128 * kNormPhases) void disc_norm_kernel(DiscNormAr
       if (var < 0.0) var = 0.0;
       const float bmean = (float)(shift + m), bvar = (float)var;
       if (a.rew_mean) chan_merge(a.rew_mean, a.rew_var, rc, c, bmean, bvar, n);
-      if (a.pol_mean && c < a.pol_cols) chan_merge(a.pol_mean, a.pol_var, pc, c, bmean, bvar, n);
+      if (a.pol_defer && c < a.pol_cols) {
+        a.pol_defer[c] = bmean;
+        a.pol_defer[a.pol_cols + c] = bvar;
+        if (c == 0) a.pol_defer[2 * a.pol_cols] = (float)n;
+      } else if (a.pol_mean && c < a.pol_cols) {
+        chan_merge(a.pol_mean, a.pol_var, pc, c, bmean, bvar, n);
+      }
     }
   }
   if (a.mode == 1) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     if (a.rew_count) *a.rew_count = rc + n;
-    if (a.pol_count) *a.pol_count = pc + n;
+    if (a.pol_count && !a.pol_defer) *a.pol_count = pc + n;
   }
+}
+
+// One thread per column; slots merged in order (the policy RunningNorm side effect of
+// the discriminator batches, deferred so that those updates can run concurrently with
+// the PPO update that also merges into this norm).
+__global__ __launch_bounds__(128) void pol_norm_merge_kernel(float* mean, float* var, int* count, const float* defer,
+                                                             int n_slots, int cols) {
+  const int c = threadIdx.x;
+  int cnt = *count;
+  for (int k = 0; k < n_slots; ++k) {
+    const float* d = defer + (size_t)k * (2 * cols + 1);
+    const int n = (int)d[2 * cols];
+    if (c < cols) chan_merge(mean, var, cnt, c, d[c], d[cols + c], n);
+    cnt += n;
+  }
+  __syncthreads();
+  if (c == 0) *count = cnt;
 }
 
 // grid: ceil(n_params / 64) blocks of 1024 = 16 block-phases x 64 params (fixed-order
@@ -220,6 +243,14 @@ hipError_t disc_gather(const DiscGatherArgs& a, hipStream_t s) {
 hipError_t disc_norm(const DiscNormArgs& a, hipStream_t s) {
   if (a.din > 128) return hipErrorInvalidValue;
   hipLaunchKernelGGL(disc_norm_kernel, dim3(1), dim3(128 * kNormPhases), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t pol_norm_merge(float* mean, float* var, int* count, const float* defer, int n_slots, int cols,
+                          hipStream_t s) {
+  if (n_slots <= 0) return hipSuccess;
+  if (cols > 128 || cols <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pol_norm_merge_kernel, dim3(1), dim3(128), 0, s, mean, var, count, defer, n_slots, cols);
   return hipGetLastError();
 }
 

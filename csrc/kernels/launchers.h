@@ -54,6 +54,9 @@ struct DiscNormArgs {
   int pol_cols;
   float *pol_mean, *pol_var;
   int* pol_count;
+  // non-null: record this batch's (mean[pol_cols], var[pol_cols], n) here instead of
+  // merging into pol_mean / pol_var (applied later, in order, by pol_norm_merge)
+  float* pol_defer;
 };
 struct DiscAdamArgs {
   int n_params, nblk, stats_nblk;
@@ -69,10 +72,16 @@ int disc_gather_blocks(int mb);
 hipError_t disc_gather(const DiscGatherArgs& a, hipStream_t s);
 hipError_t disc_norm(const DiscNormArgs& a, hipStream_t s);
 hipError_t disc_adam(const DiscAdamArgs& a, hipStream_t s);
+// Chan-merge n_slots deferred batch records ([slot][2 * cols + 1]) into a RunningNorm, in
+// slot order (bitwise the merges disc_norm would have done in place).
+hipError_t pol_norm_merge(float* mean, float* var, int* count, const float* defer, int n_slots, int cols,
+                          hipStream_t s);
 
 // ---- rl.hip: GAE scan over [T, N]
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
                       int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);
+// E keyed pseudo-random permutations of [0, n) (Feistel + cycle walking), out [E, n] int32
+hipError_t perm_feistel(int E, int n, uint64_t seed, int* out, hipStream_t s);
 
 // ---- pref.hip: Bradley-Terry preference loss over fragment pairs
 hipError_t pref_loss_fwd(const float* r1, const float* r2, const float* prefs, int P, int L, float discount,

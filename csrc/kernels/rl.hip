@@ -1,11 +1,23 @@
-// RL update kernels: GAE scan.
+// RL update kernels: GAE as a parallel affine scan, and keyed pseudo-random
+// permutations for the PPO minibatch order.
 //
 // GAE(gamma, lambda) over [T, N] rollouts (SB3 RolloutBuffer semantics; the
-// reference reaches it through SB3 PPO).  Each block
-// owns 64 envs; its 256 threads stage a 64-step time chunk of rewards / values /
-// episode_starts into LDS with coalesced loads (row t of the chunk is 64
-// consecutive envs), then one wave scans the chunk backwards with the carry in a
-// register, and the chunk's advantages/returns are written back coalesced.
+// reference reaches it through SB3 PPO). The backward
+// recurrence  a_t = delta_t + c_t * a_{t+1},  c_t = gamma * lambda * (1 - start_{t+1}),
+// is a composition of affine maps, so instead of one lane walking all T steps of an
+// env (T dependent FMAs: 87 us for the 512-step GAIL round) each env gets one wave:
+// lane l owns the contiguous steps [l*L, (l+1)*L), folds them into one map (C, D)
+// with zero carry-in, a 6-step suffix scan across the 64 lanes composes the maps of
+// all later chunks, and each lane replays its chunk with the exact carry-in. Fixed
+// association order: deterministic, and within a few ulp of the serial loop.
+//
+// Minibatch permutations: SB3 draws np.random.permutation per epoch; the engine used
+// torch.randperm (a device radix sort, ~40 us per epoch on the round's critical
+// path). Here every index is mapped through a 4-round keyed Feistel network on the
+// next even bit width >= log2(n) with cycle walking back into [0, n) -- a bijection,
+// so each epoch's row order is a permutation, computed in one pass with no sort and
+// no scratch. Keys come from splitmix64(seed, epoch), so DP replicas given the same
+// seed produce the same order.
 #include <hip/hip_runtime.h>
 
 #include "launchers.h"
@@ -13,65 +25,108 @@
 namespace ia {
 namespace {
 
-constexpr int kEnvs = 64;
-constexpr int kChunk = 64;
+constexpr int kGaeWaves = 4;
 
-__global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
-                                                  const float* __restrict__ starts, const float* __restrict__ last_val,
-                                                  const float* __restrict__ dones, int T, int N, float gamma, float lam,
-                                                  float* __restrict__ adv, float* __restrict__ ret) {
-  __shared__ float sr[kChunk][kEnvs + 1];
-  __shared__ float sv[kChunk + 1][kEnvs + 1];  // row kChunk = values of the step after the chunk
-  __shared__ float ss[kChunk + 1][kEnvs + 1];
-  __shared__ float sa[kChunk][kEnvs + 1];
-  const int env0 = blockIdx.x * kEnvs;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int env = env0 + lane;
-  float carry = 0.f;
-  for (int t1 = T; t1 > 0; t1 -= kChunk) {
-    const int t0 = t1 - kChunk > 0 ? t1 - kChunk : 0;
-    const int len = t1 - t0;
-    __syncthreads();
-    for (int e = tid; e < (len + 1) * kEnvs; e += blockDim.x) {
-      const int r = e / kEnvs, c = e - r * kEnvs;
-      const int t = t0 + r, n = env0 + c;
-      const bool ok = n < N;
-      if (r < len) {
-        sr[r][c] = ok ? rew[(size_t)t * N + n] : 0.f;
-        sv[r][c] = ok ? val[(size_t)t * N + n] : 0.f;
-        ss[r][c] = ok ? starts[(size_t)t * N + n] : 0.f;
-      } else {  // boundary row: next step's value / start flag, or the bootstrap
-        if (t < T) {
-          sv[r][c] = ok ? val[(size_t)t * N + n] : 0.f;
-          ss[r][c] = ok ? starts[(size_t)t * N + n] : 0.f;
-        } else {
-          sv[r][c] = ok ? last_val[n] : 0.f;
-          ss[r][c] = ok ? dones[n] : 0.f;  // "next non-terminal" = 1 - dones at the end
-        }
-      }
+__global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* __restrict__ rew,
+                                                                  const float* __restrict__ val,
+                                                                  const float* __restrict__ starts,
+                                                                  const float* __restrict__ last_val,
+                                                                  const float* __restrict__ dones, int T, int N,
+                                                                  float gamma, float lam, float* __restrict__ adv,
+                                                                  float* __restrict__ ret) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * kGaeWaves + (threadIdx.x >> 6);
+  if (n >= N) return;  // whole wave exits together
+  const int L = (T + 63) >> 6;
+  const int t0 = lane * L;
+  const int t1 = t0 + L < T ? t0 + L : T;
+  const float gl = gamma * lam;
+  // fold this lane's chunk: a(t0) = D + C * a(t1)
+  float C = 1.f, D = 0.f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    const size_t o = (size_t)t * N + n;
+    float nv, nnt;
+    if (t + 1 < T) {
+      nv = val[o + N];
+      nnt = 1.f - starts[o + N];
+    } else {
+      nv = last_val[n];
+      nnt = 1.f - dones[n];
     }
-    __syncthreads();
-    if (tid < 64) {
-      for (int r = len - 1; r >= 0; --r) {
-        const float nnt = 1.f - ss[r + 1][lane];
-        const float delta = sr[r][lane] + gamma * sv[r + 1][lane] * nnt - sv[r][lane];
-        carry = delta + gamma * lam * nnt * carry;
-        sa[r][lane] = carry;
-      }
-    }
-    __syncthreads();
-    for (int e = tid; e < len * kEnvs; e += blockDim.x) {
-      const int r = e / kEnvs, c = e - r * kEnvs;
-      const int n = env0 + c;
-      if (n < N) {
-        const size_t o = (size_t)(t0 + r) * N + n;
-        adv[o] = sa[r][c];
-        ret[o] = sa[r][c] + sv[r][c];
-      }
+    const float delta = rew[o] + gamma * nv * nnt - val[o];
+    const float c = gl * nnt;
+    D = delta + c * D;
+    C = c * C;
+  }
+  // inclusive suffix scan of the maps over lanes l..63: (C, D)_l o (C, D)_{l+k}
+  float SC = C, SD = D;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const float oc = __shfl_down(SC, k, 64);
+    const float od = __shfl_down(SD, k, 64);
+    if (lane + k < 64) {
+      SD = SD + SC * od;
+      SC = SC * oc;
     }
   }
-  (void)env;
+  // carry into this chunk = a(t1) = suffix value of lane + 1 (zero past the end)
+  float a = __shfl_down(SD, 1, 64);
+  if (lane == 63) a = 0.f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    const size_t o = (size_t)t * N + n;
+    float nv, nnt;
+    if (t + 1 < T) {
+      nv = val[o + N];
+      nnt = 1.f - starts[o + N];
+    } else {
+      nv = last_val[n];
+      nnt = 1.f - dones[n];
+    }
+    const float v = val[o];
+    const float delta = rew[o] + gamma * nv * nnt - v;
+    a = delta + gl * nnt * a;
+    adv[o] = a;
+    ret[o] = a + v;
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// grid (ceil(n / 256), E); one thread per (epoch, index)
+__global__ __launch_bounds__(256) void perm_feistel_kernel(int n, int half_bits, uint64_t seed, int* __restrict__ out) {
+  const int e = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k01 = splitmix64(seed ^ (0xA24BAED4963EE407ull * (uint64_t)(e + 1)));
+  const uint64_t k23 = splitmix64(k01);
+  const uint32_t key[4] = {(uint32_t)k01, (uint32_t)(k01 >> 32), (uint32_t)k23, (uint32_t)(k23 >> 32)};
+  const uint32_t mask = (1u << half_bits) - 1u;
+  uint32_t x = (uint32_t)i;
+  do {  // cycle walking: the domain is < 4n, so this ends after < 4 rounds on average
+    uint32_t Lh = x >> half_bits, Rh = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t f = mix32(Rh ^ key[r]) & mask;
+      const uint32_t nl = Rh;
+      Rh = Lh ^ f;
+      Lh = nl;
+    }
+    x = (Lh << half_bits) | Rh;
+  } while (x >= (uint32_t)n);
+  out[(size_t)e * n + i] = (int)x;
 }
 
 }  // namespace
@@ -79,9 +134,18 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew,
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
                       int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s) {
   if (T <= 0 || N <= 0) return hipSuccess;
-  const int nblk = (N + kEnvs - 1) / kEnvs;
-  hipLaunchKernelGGL(gae_kernel, dim3(nblk), dim3(256), 0, s, rew, val, starts, last_val, dones, T, N, gamma, lam, adv,
-                     ret);
+  const int nblk = (N + kGaeWaves - 1) / kGaeWaves;
+  hipLaunchKernelGGL(gae_scan_kernel, dim3(nblk), dim3(64 * kGaeWaves), 0, s, rew, val, starts, last_val, dones, T, N,
+                     gamma, lam, adv, ret);
+  return hipGetLastError();
+}
+
+hipError_t perm_feistel(int E, int n, uint64_t seed, int* out, hipStream_t s) {
+  if (E <= 0 || n <= 0) return hipSuccess;
+  if (n > (1 << 30)) return hipErrorInvalidValue;
+  int bits = 2;
+  while ((1ll << bits) < (long long)n) bits += 2;
+  hipLaunchKernelGGL(perm_feistel_kernel, dim3((n + 255) / 256, E), dim3(256), 0, s, n, bits / 2, seed, out);
   return hipGetLastError();
 }
 

@@ -270,6 +270,7 @@ class DeviceGeneratorCore:
         self.stats = z(5)
         self._seed = int(np.random.randint(0, 2**62)) ^ (pdist.rank() * 0x9E3779B97F4A7C15 & ((1 << 62) - 1))
         self._step0 = 0
+        self._perm_round = 0
         self._ppo_static = self._ppo_args_static()
         self._ep_lens_running = np.zeros(self.N, dtype=np.int64)
 
@@ -389,13 +390,13 @@ class DeviceGeneratorCore:
         self.stats.zero_()
         world = pdist.world_size()
         if world == 1:
-            perm = th.stack([th.randperm(rows, device=self._dev) for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
+            perm = self._epoch_perms(rows, self._seed)
             d.update(obs=obs, acts=acts, old_logp=old_logp, adv=adv, returns=ret, perm=perm, mode=0)
             self._C.engine_ppo_update(d)
         elif self._dp_replicated:
             self._ppo_update_replicated(d, obs, acts, old_logp, adv, ret)
         else:
-            perm = th.stack([th.randperm(rows, device=self._dev) for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
+            perm = self._epoch_perms(rows, self._seed)
             d.update(obs=obs, acts=acts, old_logp=old_logp, adv=adv, returns=ret, perm=perm)
             n_mb = rows // algo.batch_size
             B = algo.batch_size
@@ -431,9 +432,7 @@ class DeviceGeneratorCore:
         rows = self.T * self.N
         path = ppo_path(algo.policy, self._native, algo.batch_size * world, rows * world)
         self._dp_replicated = path.startswith("rc")
-        seed = int(pdist.broadcast_object(int(np.random.randint(0, 2**31 - 1))))
-        self._perm_gen = th.Generator(device=self._dev)
-        self._perm_gen.manual_seed(seed)
+        self._dp_perm_seed = int(pdist.broadcast_object(int(np.random.randint(0, 2**62))))
         Aw = 1 if self.discrete else self.A
         self._dp_cols = (self.D, Aw)
         self._dp_pack = th.zeros(rows, self.D + Aw + 3, device=self._dev)
@@ -453,14 +452,21 @@ class DeviceGeneratorCore:
         pdist.all_gather_flat(self._dp_global, pk)
         gl = self._dp_global
         rows_g = world * rows
-        perm = th.stack([th.randperm(rows_g, device=self._dev, generator=self._perm_gen)
-                         for _ in range(algo.n_epochs)]).to(th.int32).contiguous()
+        perm = self._epoch_perms(rows_g, self._dp_perm_seed)
         d.update(obs=gl[:, :D].contiguous(), acts=gl[:, D : D + Aw].contiguous(),
                  old_logp=gl[:, D + Aw].contiguous(), adv=gl[:, D + Aw + 1].contiguous(),
                  returns=gl[:, D + Aw + 2].contiguous(), perm=perm, rows=rows_g, batch=algo.batch_size * world,
                  mode=0, allow_rc=1)
         self._C.engine_ppo_update(d)
         # stats are sums over the global minibatches; every rank holds the same model
+
+    def _epoch_perms(self, rows: int, base_seed: int) -> th.Tensor:
+        """``[n_epochs, rows]`` int32 minibatch orders of this update: one ``perm_feistel``
+        launch keyed by (base seed, update counter) -- replicas that share the base seed
+        (replicated DP) draw identical orders, and the counter is checkpointed."""
+        self._perm_round += 1
+        key = (int(base_seed) * 0x9E3779B97F4A7C15 + self._perm_round) & ((1 << 64) - 1)
+        return rl_ops.random_permutations(self.gen_algo.n_epochs, rows, key, self._dev)
 
     def _dp_norm_update(self, batch: th.Tensor) -> None:
         """RunningNorm.update_stats with all-reduced moments (the kernel is told not to update)."""
@@ -603,9 +609,11 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 self._global_step += 1
             self._log_gen()
 
-    def _log_gen(self) -> None:
+    def _log_gen(self, stats: Optional[th.Tensor] = None) -> None:
+        """Record the PPO update's statistics (``stats``: an already-fetched host copy)."""
         algo = self.gen_algo
-        s = (self.stats / max(1, self._last_ppo_info[1])).tolist()
+        src = self.stats if stats is None else stats
+        s = (src / max(1, self._last_ppo_info[1])).tolist()
         lg = self.logger
         lg.record("train/entropy_loss", s[0])
         lg.record("train/policy_gradient_loss", s[1])
@@ -701,6 +709,24 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                  beta1=float(g["betas"][0]), beta2=float(g["betas"][1]), eps=float(g["eps"]),
                  weight_decay=float(g.get("weight_decay", 0.0)), **self._disc_ws)
         self._disc_plan = self._C.DiscPlan(d)
+        # Overlap (see train()): the round's discriminator updates run on a side stream
+        # concurrently with its PPO update. They only read the expert set, the replay ring
+        # and the reward net; their one write the PPO kernel also makes -- the policy
+        # RunningNorm merge of the disc batch (GAIL's log-prob side effect) -- is recorded
+        # per minibatch and applied in order after PPO, so the result is bitwise that of
+        # the serial order.
+        self._overlap_disc = os.environ.get("IMITATION_AMD_DISC_OVERLAP", "1") != "0"
+        self._side_stream = th.cuda.Stream(device=dev) if self._overlap_disc else None
+        self._pol_defer_buf = None
+        if self._overlap_disc and self.pol_norm is not None and self._disc_plan.pol_cols > 0:
+            self._ensure_pol_defer(max(1, self.n_disc_updates_per_round))
+        self._disc_stats_host = th.zeros(max(1, self.n_disc_updates_per_round), 8, pin_memory=True)
+
+    def _ensure_pol_defer(self, n_updates: int) -> None:
+        slots = n_updates * self._disc_plan.n_minibatches
+        if self._pol_defer_buf is None or self._pol_defer_buf.shape[0] < slots:
+            self._pol_defer_buf = th.zeros(slots, 2 * self._disc_plan.pol_cols + 1, device=self._dev)
+            self._disc_plan.set_pol_defer(self._pol_defer_buf)
 
     def _adopt_disc_opt_state(self) -> None:
         """Make the torch Adam state of every reward parameter a view of the flat moment
@@ -726,8 +752,10 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 v.zero_()
             opt.state[p] = {"step": step, "exp_avg": m, "exp_avg_sq": v}
 
-    def _fused_disc_update(self, slot: int) -> None:
-        """One discriminator optimizer step (== AdversarialTrainer.train_disc) with no host sync."""
+    def _fused_disc_update(self, slot: int, defer_pol: bool = False) -> None:
+        """One discriminator optimizer step (== AdversarialTrainer.train_disc) with no host sync.
+        ``defer_pol``: record the policy-norm merges in slots ``slot * n_minibatches + k`` of
+        the deferred-merge buffer instead of applying them (see :meth:`train`)."""
         if self._gen_dev.size() == 0:
             raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
         opt = self._disc_opt
@@ -745,19 +773,21 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         merge_pol = self.pol_norm is not None and self.pol_norm.training
         plan = self._disc_plan
         stats_out = self._disc_stats[slot]
+        base = slot * plan.n_minibatches if (defer_pol and merge_pol) else -1
         if pdist.world_size() == 1:
-            plan.update(e_idx, g_idx, step_size, bc2_sqrt, merge_rew, merge_pol, stats_out)
+            plan.update(e_idx, g_idx, step_size, bc2_sqrt, merge_rew, merge_pol, stats_out, base)
         else:
             world = pdist.world_size()
             for k in range(B // mb):
                 plan.gather(k, e_idx, g_idx)
                 if merge_rew or merge_pol:
+                    ds = base + k if base >= 0 else -1
                     if pdist.norm_sync_active():
                         plan.norm(1, 0, merge_rew, merge_pol)
                         pdist.allreduce_sum_(self._disc_ws["sums"])
-                        plan.norm(2, 2 * mb * world, merge_rew, merge_pol)
+                        plan.norm(2, 2 * mb * world, merge_rew, merge_pol, ds)
                     else:
-                        plan.norm(0, 0, merge_rew, merge_pol)
+                        plan.norm(0, 0, merge_rew, merge_pol, ds)
                 plan.fwd_bwd(k)
             plan.adam(1, 0, 0.0, 1.0, stats_out)
             pdist.allreduce_grads_flat(self._disc_ws["grads"])
@@ -797,21 +827,96 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         assert n_rounds >= 1, (
             f"No updates (need at least {self.gen_train_timesteps} timesteps, have only total_timesteps={total_timesteps})!")
         n = self.n_disc_updates_per_round
+        if n > self._disc_stats.shape[0]:
+            self._disc_stats = th.zeros(n, 8, device=self._dev)
+            self._disc_stats_host = th.zeros(n, 8, pin_memory=True)
+        overlap = self._overlap_disc and n > 0 and self.gen_train_timesteps == self.T * self.N
+        nxt = None
         for r in range(n_rounds):
-            self.train_gen(self.gen_train_timesteps)
-            steps = []
-            with networks.training(self.reward_train):
-                for i in range(n):
-                    self._fused_disc_update(i)
-                    steps.append(self._disc_step)
+            if overlap:
+                # without a callback nothing observes the state between rounds, so the next
+                # rollout is enqueued before this round's logging
+                steps, nxt = self._overlapped_round(n, nxt, launch_next=callback is None and r + 1 < n_rounds)
+                vals = self._disc_stats_host[:n].tolist()
+            else:
+                self.train_gen(self.gen_train_timesteps)
+                steps = []
+                with networks.training(self.reward_train):
+                    for i in range(n):
+                        self._fused_disc_update(i)
+                        steps.append(self._disc_step)
+                vals = self._disc_stats[:n].tolist() if n else []
             if n:
-                vals = self._disc_stats[:n].tolist()
                 for i in range(n):
                     with self.logger.accumulate_means("disc"):
                         self._record_disc(self._disc_stats_dict(vals[i]), steps[i])
             if callback:
                 callback(r)
             self.logger.dump(self._global_step)
+
+    def _launch_rollout(self) -> th.cuda.Event:
+        """Enqueue one rollout (chain + post pass) and the async copy of its dones / returns to
+        pinned host memory; returns the event that marks both done."""
+        self._rollout()
+        return self._stage_rollout_to_host()
+
+    def _overlapped_round(self, n: int, ready: Optional[th.cuda.Event] = None,
+                          launch_next: bool = False) -> Tuple[List[int], Optional[th.cuda.Event]]:
+        """One GAIL round with its ``n`` discriminator updates on the side stream, concurrent
+        with the PPO update (the round's rewards were already computed from the previous
+        discriminator, so nothing PPO reads changes).
+
+        ``ready``: the round's rollout was already enqueued (by the previous call) and this
+        is its staging event. ``launch_next``: enqueue the next round's rollout behind this
+        round's PPO + deferred merges BEFORE waiting for PPO on the host, so the GPU never
+        idles while the host logs. Returns (disc steps, next round's staging event); the
+        disc stats are in ``_disc_stats_host`` when this returns."""
+        algo: PPO = self.gen_algo
+        main = th.cuda.current_stream(self._dev)
+        side = self._side_stream
+        pol_merge = self.pol_norm is not None and self.pol_norm.training
+        defer = pol_merge and self._pol_defer_buf is not None
+        if defer:
+            self._ensure_pol_defer(n)
+        serial = pol_merge and not defer  # the disc would write the norm PPO is using
+        if not hasattr(self, "_ppo_stats_host"):
+            self._ppo_stats_host = th.zeros(self.stats.numel(), pin_memory=True)
+        steps: List[int] = []
+        nxt = None
+        with self.logger.accumulate_means("gen"):
+            if algo._total_timesteps < algo.num_timesteps + self.T * self.N:
+                algo._total_timesteps = algo.num_timesteps + self.T * self.N
+            if ready is None:
+                ready = self._launch_rollout()
+            algo.num_timesteps += self.T * self.N
+            self._ppo_update()
+            self._ppo_stats_host.copy_(self.stats, non_blocking=True)
+            ppo_done = th.cuda.Event()
+            ppo_done.record(main)
+            ready.synchronize()
+            if serial:
+                side.wait_stream(main)
+            else:
+                side.wait_event(ready)
+            with th.cuda.stream(side):
+                self._store_generator_samples()
+                with networks.training(self.reward_train):
+                    for i in range(n):
+                        self._fused_disc_update(i, defer_pol=defer)
+                        steps.append(self._disc_step)
+                self._disc_stats_host[:n].copy_(self._disc_stats[:n], non_blocking=True)
+                disc_done = th.cuda.Event()
+                disc_done.record(side)
+            main.wait_event(disc_done)
+            if defer:
+                self._disc_plan.pol_norm_merge(n * self._disc_plan.n_minibatches)
+            self._global_step += 1
+            if launch_next:
+                nxt = self._launch_rollout()
+            ppo_done.synchronize()
+            self._log_gen(self._ppo_stats_host)
+        disc_done.synchronize()
+        return steps, nxt
 
     # ------------------------------------------------------------------ checkpoint / resume
     _ENGINE_TENSORS = ("exp_avg", "exp_avg_sq", "adam_step", "state", "env_rng", "elapsed", "ep_ret", "cur_obs", "cur_start")
@@ -822,7 +927,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         st: Dict[str, Any] = {k: getattr(self, k).detach().cpu().clone() for k in self._ENGINE_TENSORS}
         if self.norm_count is not None:
             st["norm_count"] = self.norm_count.cpu().clone()
-        st.update(step0=int(self._step0), seed=int(self._seed), ep_lens_running=th.as_tensor(self._ep_lens_running),
+        st.update(step0=int(self._step0), seed=int(self._seed), perm_round=int(self._perm_round), ep_lens_running=th.as_tensor(self._ep_lens_running),
                   gen_dev={k: v.cpu().clone() for k, v in self._gen_dev._arrays.items()},
                   gen_dev_idx=int(self._gen_dev._idx), gen_dev_n=int(self._gen_dev._n_data))
         return st
@@ -836,6 +941,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             for k, v in st["gen_dev"].items():
                 self._gen_dev._arrays[k].copy_(v.to(self._dev))
         self._step0, self._seed = st["step0"], st["seed"]
+        self._perm_round = int(st.get("perm_round", 0))
         self._ep_lens_running = st["ep_lens_running"].numpy().copy()
         self._gen_dev._idx, self._gen_dev._n_data = st["gen_dev_idx"], st["gen_dev_n"]
         self.sync_env_to_host()

@@ -2,7 +2,9 @@
 
 ``gae`` replaces SB3's host-side reversed Python loop over ``n_steps``
 (``RolloutBuffer.compute_returns_and_advantage``): the HIP
-kernel runs one lane per env and scans time backwards in registers.
+kernel gives each env one wave and runs the backward recurrence as a parallel affine
+scan over 64 time chunks. ``random_permutations`` produces the PPO epochs' minibatch
+orders without a sort (keyed Feistel bijections).
 """
 
 from __future__ import annotations
@@ -45,3 +47,68 @@ def gae(rewards, values, episode_starts, last_values, dones, gamma: float, lam: 
             float(lam),
         )
     return gae_reference(rewards, values, episode_starts, last_values, dones, gamma, lam)
+
+
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def _mix32(x):
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    return x ^ (x >> 16)
+
+
+def random_permutations_reference(E: int, n: int, seed: int):
+    """Host (numpy) twin of the ``perm_feistel`` kernel (csrc/kernels/rl.hip): row ``e`` of
+    the ``[E, n]`` int32 result is the keyed 4-round Feistel permutation of ``0..n-1``
+    with cycle walking. Bit-identical to the GPU kernel for the same ``seed``."""
+    import numpy as np
+
+    seed &= _M64
+    bits = 2
+    while (1 << bits) < n:
+        bits += 2
+    h = bits // 2
+    mask = np.uint64((1 << h) - 1)
+    out = np.empty((E, n), dtype=np.int32)
+    for e in range(E):
+        k01 = _splitmix64(seed ^ ((0xA24BAED4963EE407 * (e + 1)) & _M64))
+        k23 = _splitmix64(k01)
+        keys = [k01 & 0xFFFFFFFF, k01 >> 32, k23 & 0xFFFFFFFF, k23 >> 32]
+        x = np.arange(n, dtype=np.uint64)
+        todo = np.ones(n, dtype=bool)
+        res = np.empty(n, dtype=np.uint64)
+        while todo.any():
+            lh, rh = x >> np.uint64(h), x & mask
+            for k in keys:
+                f = _mix32(rh ^ np.uint64(k)) & mask
+                lh, rh = rh, lh ^ f
+            x = (lh << np.uint64(h)) | rh
+            done = todo & (x < np.uint64(n))
+            res[done] = x[done]
+            todo &= ~done
+        out[e] = res.astype(np.int32)
+    return out
+
+
+def random_permutations(E: int, n: int, seed: int, device) -> torch.Tensor:
+    """``[E, n]`` int32 minibatch orders (one permutation of the rows per epoch), keyed by
+    ``seed``; replaces ``torch.randperm`` per epoch (a device radix sort) with one
+    ``perm_feistel`` launch. Same values on the GPU kernel and the numpy fallback."""
+    from imitation_amd.ops import native
+
+    device = torch.device(device)
+    seed = int(seed) & _M64
+    if device.type == "cuda":
+        s = seed - (1 << 64) if seed >= (1 << 63) else seed  # int64 two's complement for the binding
+        return native().random_permutations(int(E), int(n), s, device)
+    return torch.from_numpy(random_permutations_reference(E, n, seed))

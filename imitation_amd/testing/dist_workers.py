@@ -107,7 +107,7 @@ def device_gail_dp_worker(rank, world, seed, batch):
     norm = pol.features_extractor.normalize
     p0 = [p.detach().clone() for p in pol.parameters()]
     n0 = (norm.running_mean.clone(), norm.running_var.clone(), norm.count.clone())
-    gen_state = tr._perm_gen.get_state()
+    perm_round = tr._perm_round
     tr._ppo_update()
     th.cuda.synchronize()
     out = {"params": [p.detach().cpu().numpy().copy() for p in pol.parameters()],
@@ -116,9 +116,8 @@ def device_gail_dp_worker(rank, world, seed, batch):
         gl = tr._dp_global
         D, Aw = tr._dp_cols
         rows_g = gl.shape[0]
-        g = th.Generator(device="cuda")
-        g.set_state(gen_state)
-        perm = th.stack([th.randperm(rows_g, device="cuda", generator=g) for _ in range(gen.n_epochs)])
+        tr._perm_round = perm_round  # replay the update's minibatch orders
+        perm = tr._epoch_perms(rows_g, tr._dp_perm_seed).long()
         p_dev = [p.detach().clone() for p in pol.parameters()]
         with th.no_grad():
             for p, q in zip(pol.parameters(), p0):

@@ -25,6 +25,7 @@ def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epoc
     rng = np.random.default_rng(seed)
     venv = make_vec_env(env_id, rng=rng, n_envs=n_envs)
     demo_env = make_vec_env(env_id, rng=np.random.default_rng(7), n_envs=4)
+    demo_env.action_space.seed(7)  # random-policy demos: reproducible across setups
     demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
     from imitation_amd.rl.policies import ActorCriticPolicy
 
@@ -117,13 +118,13 @@ def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_a
     n0 = (norm.running_mean.clone(), norm.running_var.clone(), norm.count.clone())
     # device update with a known permutation
     rows = tr.T * tr.N
-    th.manual_seed(123)
+    perm_round = tr._perm_round
     tr._ppo_update()
     p_dev = [p.detach().clone() for p in pol.parameters()]
     mean_dev, var_dev = norm.running_mean.clone(), norm.running_var.clone()
     # reference: restore and replay with the same permutation
-    th.manual_seed(123)
-    perm = th.stack([th.randperm(rows, device="cuda") for _ in range(gen.n_epochs)])
+    tr._perm_round = perm_round
+    perm = tr._epoch_perms(rows, tr._seed).long()
     with th.no_grad():
         for p, q in zip(pol.parameters(), p0):
             p.copy_(q)
@@ -154,6 +155,40 @@ def test_device_gail_rounds_run_and_learn_something():
     assert any(not th.equal(a, b) for a, b in zip(after, before))
     assert all(th.isfinite(p).all() for p in after)
     assert tr._gen_dev.size() > 0
+
+
+@gpu
+def test_disc_overlap_is_bitwise_the_serial_order(monkeypatch):
+    """Discriminator updates on the side stream, concurrent with PPO, with the policy-norm
+    merges deferred: parameters, Adam moments and both RunningNorms equal the serial run."""
+    names = None
+    runs = []
+    modes = os.environ.get("IA_OVERLAP_MODES", "serial,deferred-same-stream,overlap").split(",")
+    for mode in modes:
+        monkeypatch.setenv("IMITATION_AMD_DISC_OVERLAP", "0" if mode == "serial" else "1")
+        tr, venv, gen, rn = _setup(n_envs=8, n_steps=64, batch=64, n_epochs=2)
+        if mode == "deferred-same-stream":
+            tr._side_stream = th.cuda.current_stream()
+        tr.n_disc_updates_per_round = 3
+        tr.train(3 * tr.gen_train_timesteps)
+        th.cuda.synchronize()
+        pn = tr.pol_norm
+        named = [(f"policy.{k}", v) for k, v in gen.policy.named_parameters()] + \
+                [(f"reward.{k}", v) for k, v in rn.named_parameters()] + \
+                [("pol_mean", pn.running_mean), ("pol_var", pn.running_var), ("pol_count", pn.count),
+                 ("disc_m", tr._r_m), ("disc_v", tr._r_v), ("rew_mean", tr._rnorm.running_mean),
+                 ("rew_count", tr._rnorm.count)]
+        names = [k for k, _ in named]
+        runs.append([v.detach().cpu().clone() for _, v in named])
+        assert tr._disc_step == 9
+    bad = []
+    for i, k in enumerate(names):
+        for j in range(1, len(modes)):
+            if not th.equal(runs[0][i], runs[j][i]):
+                bad.append((k, j, float((runs[0][i].double() - runs[j][i].double()).abs().max())))
+    for b in bad:
+        print("DIFF", *b)
+    assert not bad
 
 
 def _disc_reference(tr, e_idx, g_idx, mb_rows):

@@ -110,6 +110,16 @@ def test_gae_kernel_matches_reference(T, N):
 
 
 @gpu
+@pytest.mark.parametrize("E,n", [(5, 4096), (3, 1), (2, 3), (4, 1000), (5, 32768), (1, 70001)])
+def test_perm_feistel_kernel_matches_host_twin(E, n):
+    got = rl_ops.random_permutations(E, n, 0xDEADBEEF12345, "cuda").cpu().numpy()
+    want = rl_ops.random_permutations_reference(E, n, 0xDEADBEEF12345)
+    np.testing.assert_array_equal(got, want)
+    for row in got:
+        assert np.array_equal(np.sort(row), np.arange(n))
+
+
+@gpu
 def test_native_extension_is_loaded_on_gpu():
     from imitation_amd import _native
 

@@ -1,0 +1,29 @@
+"""CPU checks of the host twins of the RL kernels (csrc/kernels/rl.hip)."""
+
+import numpy as np
+import pytest
+
+from imitation_amd.ops import rl as rl_ops
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 64, 1000, 4096])
+def test_feistel_rows_are_permutations(n):
+    p = rl_ops.random_permutations_reference(4, n, 1234)
+    assert p.shape == (4, n) and p.dtype == np.int32
+    for row in p:
+        assert np.array_equal(np.sort(row), np.arange(n))
+    if n >= 64:
+        assert not np.array_equal(p[0], p[1])  # epochs draw different orders
+
+
+def test_feistel_keyed_and_roughly_uniform():
+    a = rl_ops.random_permutations_reference(1, 4096, 1)
+    b = rl_ops.random_permutations_reference(1, 4096, 2)
+    assert not np.array_equal(a, b)
+    np.testing.assert_array_equal(a, rl_ops.random_permutations_reference(1, 4096, 1))
+    # where index 0 lands over many keys: ~uniform over 16 buckets
+    pos = np.array([int(np.flatnonzero(rl_ops.random_permutations_reference(1, 256, s)[0] == 0)[0]) for s in range(800)])
+    counts = np.bincount(pos // 16, minlength=16)
+    assert counts.min() > 20 and counts.max() < 80
+    # displacement is not concentrated near the identity
+    assert np.mean(np.abs(a[0] - np.arange(4096))) > 1000
