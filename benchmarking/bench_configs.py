@@ -94,7 +94,7 @@ def make_step(name, device, rank, args):
             tr.train(args.dagger_round_steps, rollout_round_min_episodes=1,
                      rollout_round_min_timesteps=args.dagger_round_steps,
                      bc_train_kwargs=dict(n_epochs=1, log_interval=10**9, progress_bar=False))
-            return tr.last_train_timesteps
+            return tr.last_train_timesteps_local  # this rank's steps (x world below)
 
         return b, step, "env-steps/s", tr.policy, b.venv
     if name == "preference_walker2d":

@@ -264,7 +264,60 @@ size_t ppo_lds(py::dict d) {
 
 }  // namespace
 
+// One DAgger-collector env step (mode 0) or reset of every env (mode 1); see dagger.hip.
+void dagger_env_step(py::dict d) {
+  ia::DaggerEnvArgs a{};
+  std::string env = d["env"].cast<std::string>();
+  int ms = 0;
+  TORCH_CHECK(ia::make_env_params(env, &a.P, &ms), "unknown native env ", env);
+  a.N = ival(d, "N");
+  a.max_steps = ival(d, "max_steps", ms);
+  a.mode = ival(d, "mode", 0);
+  a.sdim = ia::state_size(a.P);
+  a.state = tptr<float>(d, "state");
+  a.rng = tptr<uint64_t>(d, "rng");
+  a.elapsed = tptr<int>(d, "elapsed");
+  a.ep_ret = tptr<float>(d, "ep_ret");
+  auto check_numel = [&](const char* k, int64_t want) {
+    if (!d.contains(k) || d[k].is_none()) return;
+    auto t = d[k].cast<torch::Tensor>();
+    TORCH_CHECK(t.numel() == want, "dagger_env_step: ", k, " has ", t.numel(), " elements, expected ", want);
+  };
+  check_numel("state", (int64_t)a.N * a.sdim);
+  check_numel("rng", a.N);
+  check_numel("elapsed", a.N);
+  const bool img = a.P.kind == ia::ENV_PONG;
+  const int64_t obs_elems = img ? (int64_t)ia::kPongH * ia::kPongW * ia::kPongStack : a.P.obs_dim;
+  if (img) {
+    a.obs_u8 = tptr<uint8_t>(d, "obs");
+    check_numel("obs", a.N * obs_elems);
+  } else {
+    a.obs_f = tptr<float>(d, "obs");
+    check_numel("obs", a.N * obs_elems);
+  }
+  if (a.mode == 0) {
+    if (a.P.n_actions > 0) {
+      a.act_i = tptr<const int64_t>(d, "actions");
+      check_numel("actions", a.N);
+    } else {
+      a.act_f = tptr<const float>(d, "actions");
+      check_numel("actions", (int64_t)a.N * a.P.act_dim);
+    }
+    a.rew = tptr<float>(d, "rew");
+    a.term = tptr<uint8_t>(d, "term");
+    a.trunc = tptr<uint8_t>(d, "trunc");
+    if (img) a.term_obs_u8 = tptr<uint8_t>(d, "term_obs");
+    else a.term_obs_f = tptr<float>(d, "term_obs");
+    check_numel("term_obs", a.N * obs_elems);
+    a.ep_ret_out = tptr<float>(d, "ep_ret_out");
+    a.ep_len_out = tptr<int>(d, "ep_len_out");
+    for (const char* k : {"rew", "term", "trunc", "ep_ret_out", "ep_len_out"}) check_numel(k, a.N);
+  }
+  IA_HIP_CHECK2(ia::dagger_env_step(a, ia_stream()));
+}
+
 void register_engine(py::module& m) {
+  m.def("dagger_env_step", &dagger_env_step, "DAgger collector: one device env step (mode 0) / reset all (mode 1)");
   m.def("engine_rollout", &rollout, "T-step device rollout (actor sampling + env) for N envs");
   m.def("engine_rollout_post", &rollout_post,
         "values, log-probs, TimeLimit bootstrap and learned reward of a rollout, all transitions in parallel");

@@ -64,6 +64,10 @@ void register_envs(py::module& m) {
              d["state"] = st;
              d["rng"] = rng;
              d["elapsed"] = t;
+             if (e.is_image())  // frame stacks [N, 84, 84, 4]
+               d["frames"] = torch::from_blob(e.frames().data(), {e.num_envs(), ia::kPongH, ia::kPongW, ia::kPongStack},
+                                              torch::kUInt8)
+                                 .clone();
              return d;
            })
       .def("set_state", [](ia::BatchedEnv& e, py::dict d) {
@@ -74,5 +78,10 @@ void register_envs(py::module& m) {
         memcpy(e.state().data(), st.data_ptr<float>(), st.numel() * sizeof(float));
         memcpy(e.rng().data(), rng.data_ptr<int64_t>(), rng.numel() * sizeof(int64_t));
         memcpy(e.elapsed().data(), t.data_ptr<int64_t>(), t.numel() * sizeof(int64_t));
+        if (e.is_image() && d.contains("frames")) {
+          auto fr = d["frames"].cast<torch::Tensor>().contiguous().to(torch::kUInt8);
+          TORCH_CHECK(fr.numel() == (int64_t)e.frames().size(), "frames size mismatch");
+          memcpy(e.frames().data(), fr.data_ptr<uint8_t>(), fr.numel());
+        }
       });
 }

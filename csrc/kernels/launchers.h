@@ -77,6 +77,28 @@ hipError_t disc_adam(const DiscAdamArgs& a, hipStream_t s);
 hipError_t pol_norm_merge(float* mean, float* var, int* count, const float* defer, int n_slots, int cols,
                           hipStream_t s);
 
+// ---- dagger.hip: device env step of the DAgger collector (one workgroup per env)
+struct DaggerEnvArgs {
+  EnvParams P;
+  int N, max_steps, sdim;
+  int mode;  // 0: step with the given actions; 1: reset every env
+  float* state;
+  uint64_t* rng;
+  int* elapsed;
+  float* ep_ret;            // running episode return
+  const int64_t* act_i;     // discrete actions [N] (or null)
+  const float* act_f;       // continuous actions [N, act_dim] (or null)
+  uint8_t* obs_u8;          // image envs: current frame stack [N, 84, 84, 4], updated in place
+  float* obs_f;             // vector envs: current observation [N, obs_dim], updated in place
+  float* rew;               // [N] this step
+  uint8_t *term, *trunc;    // [N] this step
+  uint8_t* term_obs_u8;     // [N, 84, 84, 4] terminal frames (written for done envs)
+  float* term_obs_f;        // [N, obs_dim] terminal observations (written for done envs)
+  float* ep_ret_out;        // [N] episode return at episode end (else 0)
+  int* ep_len_out;          // [N] episode length at episode end (else 0)
+};
+hipError_t dagger_env_step(const DaggerEnvArgs& a, hipStream_t s);
+
 // ---- rl.hip: GAE scan over [T, N]
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
                       int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);

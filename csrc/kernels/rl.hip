@@ -16,7 +16,7 @@
 // path). Here every index is mapped through a 4-round keyed Feistel network on the
 // next even bit width >= log2(n) with cycle walking back into [0, n) -- a bijection,
 // so each epoch's row order is a permutation, computed in one pass with no sort and
-// no scratch. Keys come from splitmix64(seed, epoch), so DP replicas given the same
+// no scratch. Keys come from mix64(seed, epoch), so DP replicas given the same
 // seed produce the same order.
 #include <hip/hip_runtime.h>
 
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* _
   }
 }
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
@@ -110,8 +110,8 @@ __global__ __launch_bounds__(256) void perm_feistel_kernel(int n, int half_bits,
   const int e = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const uint64_t k01 = splitmix64(seed ^ (0xA24BAED4963EE407ull * (uint64_t)(e + 1)));
-  const uint64_t k23 = splitmix64(k01);
+  const uint64_t k01 = mix64(seed ^ (0xA24BAED4963EE407ull * (uint64_t)(e + 1)));
+  const uint64_t k23 = mix64(k01);
   const uint32_t key[4] = {(uint32_t)k01, (uint32_t)(k01 >> 32), (uint32_t)k23, (uint32_t)(k23 >> 32)};
   const uint32_t mask = (1u << half_bits) - 1u;
   uint32_t x = (uint32_t)i;

@@ -48,6 +48,7 @@ class BatchedEnv {
   std::vector<float>& state() { return state_; }
   std::vector<uint64_t>& rng() { return rng_; }
   std::vector<int64_t>& elapsed() { return t_; }
+  std::vector<uint8_t>& frames() { return frames_; }
 
  private:
   void write_obs(int i, void* obs);

@@ -1,14 +1,25 @@
-"""DAgger (reference: ``src/imitation/algorithms/dagger.py``).
+"""DAgger: dataset aggregation with a β-mixture of expert and learner control.
 
-Rounds of: collect with a β-mixture of expert and learner actions (the expert's
-action is always the one recorded), save each finished episode as a demo file,
-retrain BC on the union of all rounds' demos. Beta schedules (``dagger.py:28-96``),
-:class:`InteractiveTrajectoryCollector` (``:151-287``), :class:`DAggerTrainer`
-(``:294-552``, checkpoint/resume via ``save_trainer`` / :func:`reconstruct_trainer`),
-:class:`SimpleDAggerTrainer` (``:555-697``).
+Reference: ``src/imitation/algorithms/dagger.py`` -- beta schedules
+(``:28-96``), ``InteractiveTrajectoryCollector`` (``:151-287``), ``DAggerTrainer``
+(``:294-552``) and ``SimpleDAggerTrainer`` (``:555-697``). Public API and the on-disk
+demo layout are the reference's; the internals are organised around three pieces:
 
-Demo files use the same HF-dataset-directory format and ``round-XYZ/dagger-demo-*.npz``
-naming as the reference.
+* :class:`RoundDemoStore` owns every round's demonstrations: the files
+  (``<scratch>/demos/round-XYZ/[prefix-]dagger-demo-<i>-<uuid>.npz``, one HF-dataset
+  dir per trajectory, readable by the reference) and an in-memory aggregate that grows
+  by the NEW rounds only (the reference re-flattens every demo each round). Under data
+  parallelism every rank writes into its own scratch tree (``<scratch>/rank-RR``) and
+  the newly loaded rounds are all-gathered, so all replicas train BC on the identical
+  union in (round, rank, file) order; the "no demos yet" decision is rank-agreed.
+* the collectors: :class:`InteractiveTrajectoryCollector` (host VecEnv wrapper, the
+  human-in-the-loop API) or, for native image envs on a GPU,
+  :class:`imitation_amd.engine.dagger.DeviceDAggerCollector` (env stepping, frame
+  rendering, both CNN policies and the β-mix on the device; see that module).
+* :class:`DAggerTrainer` rounds: collect -> ingest -> BC (the BC step all-reduces its
+  gradient bucket under DP, ``algorithms/bc.py``) -> advance the round counter.
+
+Checkpoints are tensor/JSON-only (``torch.load(weights_only=True)``).
 """
 
 from __future__ import annotations
@@ -16,7 +27,6 @@ from __future__ import annotations
 import abc
 import json
 import logging
-import os
 import pathlib
 import uuid
 from typing import Any, Callable, Dict, List, Mapping, Optional, Sequence, Tuple, Union
@@ -25,39 +35,50 @@ import numpy as np
 import torch as th
 
 from imitation_amd.algorithms import base, bc
-from imitation_amd.rl import save_util
 from imitation_amd.data import rollout, serialize, types
+from imitation_amd.envs import spaces as spaces_mod
 from imitation_amd.envs.vec_env import VecEnvWrapper
+from imitation_amd.parallel import dist as pdist
+from imitation_amd.rl import save_util
 from imitation_amd.rl.base import check_for_correct_spaces
 from imitation_amd.rl.policies import get_device
 from imitation_amd.util import logger as imit_logger
 from imitation_amd.util import util
 
+log = logging.getLogger(__name__)
 
+
+# ----------------------------------------------------------------------------- β schedules
 class BetaSchedule(abc.ABC):
-    """Computes beta (% of time demonstration action used) from training round."""
+    """β(round): probability that the expert's (rather than the learner's) action is executed."""
 
     @abc.abstractmethod
     def __call__(self, round_num: int) -> float:
-        """Beta for round ``round_num``."""
+        """β for round ``round_num``."""
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"type": "default"}
 
 
 class LinearBetaSchedule(BetaSchedule):
-    """Linearly-decreasing schedule for beta (1 -> 0 over ``rampdown_rounds``)."""
+    """β ramps linearly from 1 down to 0 over ``rampdown_rounds`` rounds."""
 
     def __init__(self, rampdown_rounds: int) -> None:
         self.rampdown_rounds = rampdown_rounds
 
     def __call__(self, round_num: int) -> float:
         assert round_num >= 0
-        return min(1, max(0, (self.rampdown_rounds - round_num) / self.rampdown_rounds))
+        return float(np.clip(1.0 - round_num / self.rampdown_rounds, 0.0, 1.0))
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"type": "linear", "rampdown_rounds": self.rampdown_rounds}
 
 
 class ExponentialBetaSchedule(BetaSchedule):
-    """Exponentially decaying schedule for beta."""
+    """β = ``decay_probability`` ** round."""
 
     def __init__(self, decay_probability: float):
-        if not (0 < decay_probability <= 1):
+        if not 0 < decay_probability <= 1:
             raise ValueError("decay_probability lies outside the range (0, 1].")
         self.decay_probability = decay_probability
 
@@ -65,136 +86,179 @@ class ExponentialBetaSchedule(BetaSchedule):
         assert round_num >= 0
         return self.decay_probability**round_num
 
-
-def _schedule_to_json(schedule) -> Dict[str, Any]:
-    if isinstance(schedule, LinearBetaSchedule):
-        return {"type": "linear", "rampdown_rounds": schedule.rampdown_rounds}
-    if isinstance(schedule, ExponentialBetaSchedule):
-        return {"type": "exponential", "decay_probability": schedule.decay_probability}
-    logging.warning("custom beta schedule %r is not serializable; a reloaded trainer uses the default", schedule)
-    return {"type": "default"}
+    def to_json(self) -> Dict[str, Any]:
+        return {"type": "exponential", "decay_probability": self.decay_probability}
 
 
-def _schedule_from_json(d: Mapping[str, Any]):
-    if d["type"] == "linear":
+def _schedule_from_json(d: Mapping[str, Any]) -> Optional[BetaSchedule]:
+    kind = d.get("type")
+    if kind == "linear":
         return LinearBetaSchedule(d["rampdown_rounds"])
-    if d["type"] == "exponential":
+    if kind == "exponential":
         return ExponentialBetaSchedule(d["decay_probability"])
     return None
 
 
-def reconstruct_trainer(scratch_dir: types.AnyPath, venv, custom_logger: Optional[imit_logger.HierarchicalLogger] = None,
-                        device: Union[th.device, str] = "auto") -> "DAggerTrainer":
-    """Rebuild a trainer from ``scratch_dir/checkpoint-latest.pt`` (reference: dagger.py reconstruct_trainer).
-
-    Checkpoints are tensor/JSON-only (``torch.load(weights_only=True)``): trainer
-    metadata as JSON, the BC policy and optimizer state dicts, and for
-    :class:`SimpleDAggerTrainer` the expert policy. Demonstrations are re-read from
-    ``scratch_dir/demos`` on the next update.
-    """
-    from imitation_amd.rl.policies import load_policy_file
-
-    custom_logger = custom_logger or imit_logger.configure()
-    scratch_dir = util.parse_path(scratch_dir)
-    ckpt = th.load(scratch_dir / "checkpoint-latest.pt", map_location=get_device(device), weights_only=True)
-    meta = json.loads(ckpt["meta"])
-    policy_path = scratch_dir / "policy-latest.pt"
-    policy = load_policy_file(policy_path, device=device)
-    opt_cls = save_util._resolve_class(meta["bc"]["optimizer_cls"])
-    bc_trainer = bc.BC(observation_space=policy.observation_space, action_space=policy.action_space,
-                       rng=np.random.default_rng(), policy=policy, demonstrations=None,
-                       batch_size=meta["bc"]["batch_size"], minibatch_size=meta["bc"]["minibatch_size"],
-                       optimizer_cls=opt_cls, optimizer_kwargs=meta["bc"]["optimizer_kwargs"],
-                       ent_weight=meta["bc"]["ent_weight"], l2_weight=meta["bc"]["l2_weight"],
-                       custom_logger=custom_logger)
-    bc_trainer.optimizer.load_state_dict(ckpt["optimizer"])
-    rng = np.random.default_rng()
-    rng.bit_generator.state = meta["rng_state"]
-    kwargs = dict(venv=venv, scratch_dir=scratch_dir, rng=rng, beta_schedule=_schedule_from_json(meta["beta_schedule"]),
-                  bc_trainer=bc_trainer, custom_logger=custom_logger)
-    if meta["class"] == "SimpleDAggerTrainer":
-        expert = load_policy_file(scratch_dir / "expert-policy.pt", device=device)
-        trainer: DAggerTrainer = SimpleDAggerTrainer(expert_policy=expert, **kwargs)
-    else:
-        trainer = DAggerTrainer(**kwargs)
-    trainer.round_num = meta["round_num"]
-    return trainer
+def _schedule_json(schedule) -> Dict[str, Any]:
+    if isinstance(schedule, BetaSchedule):
+        return schedule.to_json()
+    log.warning("beta schedule %r is not serializable; a reloaded trainer uses the default", schedule)
+    return {"type": "default"}
 
 
-def _save_dagger_demo(trajectory: types.Trajectory, trajectory_index: int, save_dir: types.AnyPath, rng: np.random.Generator,
-                      prefix: str = "") -> None:
-    save_dir = util.parse_path(save_dir)
-    assert isinstance(trajectory, types.Trajectory)
-    actual_prefix = f"{prefix}-" if prefix else ""
-    randbits = int.from_bytes(rng.bytes(16), "big")
-    random_uuid = uuid.UUID(int=randbits, version=4).hex
-    npz_path = save_dir / f"{actual_prefix}dagger-demo-{trajectory_index}-{random_uuid}.npz"
-    assert not npz_path.exists(), "The following DAgger demonstration path already exists: {0}".format(npz_path)
-    serialize.save(npz_path, [trajectory])
-    logging.info(f"Saved demo at '{npz_path}'")
+# ----------------------------------------------------------------------------- demo store
+def _demo_filename(index: int, rng: np.random.Generator, prefix: str = "") -> str:
+    tag = uuid.UUID(int=int.from_bytes(rng.bytes(16), "big"), version=4).hex
+    return f"{prefix + '-' if prefix else ''}dagger-demo-{index}-{tag}.npz"
 
 
+def _save_dagger_demo(trajectory: types.Trajectory, trajectory_index: int, save_dir: types.AnyPath,
+                      rng: np.random.Generator, prefix: str = "") -> pathlib.Path:
+    """Write one trajectory as ``save_dir/[prefix-]dagger-demo-<index>-<uuid>.npz``."""
+    if not isinstance(trajectory, types.Trajectory):
+        raise TypeError(f"expected a Trajectory, got {type(trajectory)}")
+    path = util.parse_path(save_dir) / _demo_filename(trajectory_index, rng, prefix)
+    if path.exists():
+        raise FileExistsError(f"DAgger demonstration path already exists: {path}")
+    serialize.save(path, [trajectory])
+    log.info("saved demo at %s", path)
+    return path
+
+
+class RoundDemoStore:
+    """All demonstrations of a DAgger run, per round, on disk and aggregated in memory.
+
+    ``root`` is this rank's scratch tree. :meth:`ingest` reads rounds that have not been
+    read yet, all-gathers them across DP ranks and extends the flat aggregate handed to
+    BC (one concatenation of the new transitions)."""
+
+    def __init__(self, root: pathlib.Path):
+        self.root = root
+        self.trajectories: List[types.Trajectory] = []
+        self.loaded_through = -1  # last round already in memory
+        self._flat: Optional[types.Transitions] = None
+
+    def round_dir(self, round_num: int) -> pathlib.Path:
+        return self.root / "demos" / f"round-{round_num:03d}"
+
+    def files(self, round_num: int) -> List[pathlib.Path]:
+        d = self.round_dir(round_num)
+        if not d.is_dir():
+            return []
+        return [d / name for name in sorted(p.name for p in d.iterdir()) if name.endswith(".npz")]
+
+    def write(self, trajectory: types.Trajectory, index: int, round_num: int, rng: np.random.Generator,
+              prefix: str = "") -> pathlib.Path:
+        return _save_dagger_demo(trajectory, index, self.round_dir(round_num), rng, prefix)
+
+    def demos_everywhere(self, round_num: int) -> bool:
+        """True iff EVERY rank has at least one demo file for ``round_num`` (rank-agreed)."""
+        have = float(len(self.files(round_num)) > 0)
+        if pdist.world_size() > 1:
+            have = pdist.allreduce_scalars([have], op="min")[0]
+        return have > 0
+
+    def ingest(self, through_round: int) -> Tuple[types.Transitions, List[int]]:
+        """Load rounds ``loaded_through+1 .. through_round`` (all ranks' files, rank order);
+        returns the aggregate transitions and the per-round counts of new demos."""
+        new: List[types.Trajectory] = []
+        counts: List[int] = []
+        for r in range(self.loaded_through + 1, through_round + 1):
+            local = [serialize.load(p)[0] for p in self.files(r)]
+            parts = pdist.all_gather_object(local) if pdist.world_size() > 1 else [local]
+            counts.append(sum(len(p) for p in parts))
+            for part in parts:
+                new.extend(part)
+        self.loaded_through = max(self.loaded_through, through_round)
+        self.trajectories.extend(new)
+        if new:
+            fresh = rollout.flatten_trajectories(new)
+            self._flat = fresh if self._flat is None else _concat_transitions(self._flat, fresh)
+        log.info("aggregate now holds %d demos (%d new)", len(self.trajectories), len(new))
+        assert self._flat is not None, "ingest() found no demonstrations"
+        return self._flat, counts
+
+
+def _concat_transitions(a: types.Transitions, b: types.Transitions) -> types.Transitions:
+    cat = lambda x, y: types.DictObs.concatenate([x, y]) if isinstance(x, types.DictObs) else np.concatenate([x, y])  # noqa: E731
+    return types.Transitions(obs=cat(a.obs, b.obs), acts=np.concatenate([a.acts, b.acts]),
+                             infos=np.concatenate([a.infos, b.infos]), next_obs=cat(a.next_obs, b.next_obs),
+                             dones=np.concatenate([a.dones, b.dones]))
+
+
+# ----------------------------------------------------------------------------- host collector
 class InteractiveTrajectoryCollector(VecEnvWrapper):
-    """VecEnv wrapper that mixes in learner actions with prob 1-β and records expert demos."""
+    """VecEnv wrapper for DAgger data collection (reference ``dagger.py:151-287``).
+
+    ``step(actions)`` takes the EXPERT's intended actions. Per env and step, independently,
+    the expert action is executed with probability β and the learner's
+    (``get_robot_acts(obs)``) otherwise; the recorded action is always the expert's.
+    Every finished episode is written to ``save_dir`` as a demo file."""
 
     def __init__(self, venv, get_robot_acts: Callable[[np.ndarray], np.ndarray], beta: float, save_dir: types.AnyPath,
                  rng: np.random.Generator) -> None:
         super().__init__(venv)
+        if not 0 <= beta <= 1:
+            raise ValueError(f"beta={beta} outside [0, 1]")
         self.get_robot_acts = get_robot_acts
-        assert 0 <= beta <= 1
         self.beta = beta
-        self.traj_accum: Optional[rollout.TrajectoryAccumulator] = None
         self.save_dir = save_dir
-        self._last_obs: Optional[np.ndarray] = None
-        self._done_before = True
-        self._is_reset = False
-        self._last_user_actions: Optional[np.ndarray] = None
         self.rng = rng
+        self.traj_accum: Optional[rollout.TrajectoryAccumulator] = None
+        self._obs: Optional[np.ndarray] = None
+        self._expert_acts: Optional[np.ndarray] = None
 
     def seed(self, seed: Optional[int] = None) -> List[Optional[int]]:
+        """Reseed the β-mixing RNG and the wrapped envs."""
         self.rng = np.random.default_rng(seed=seed)
         return list(self.venv.seed(seed))
 
     def reset(self) -> np.ndarray:
-        self.traj_accum = rollout.TrajectoryAccumulator()
         obs = self.venv.reset()
-        assert isinstance(obs, np.ndarray)
-        for i, ob in enumerate(obs):
-            self.traj_accum.add_step({"obs": ob}, key=i)
-        self._last_obs = obs
-        self._is_reset = True
-        self._last_user_actions = None
+        if not isinstance(obs, np.ndarray):
+            raise TypeError("DAgger collection needs array observations")
+        self.traj_accum = rollout.TrajectoryAccumulator()
+        for env_idx in range(len(obs)):
+            self.traj_accum.add_step({"obs": obs[env_idx]}, key=env_idx)
+        self._obs, self._expert_acts = obs, None
         return obs
 
+    def _executed_actions(self, expert: np.ndarray) -> np.ndarray:
+        learner_turn = self.rng.uniform(0, 1, size=(self.num_envs,)) > self.beta
+        executed = np.array(expert)
+        if learner_turn.any():
+            executed[learner_turn] = self.get_robot_acts(self._obs[learner_turn])
+        return executed
+
     def step_async(self, actions: np.ndarray) -> None:
-        assert self._is_reset, "call .reset() before .step()"
-        assert self._last_obs is not None
-        actual_acts = np.array(actions)
-        mask = self.rng.uniform(0, 1, size=(self.num_envs,)) > self.beta
-        if np.sum(mask) != 0:
-            actual_acts[mask] = self.get_robot_acts(self._last_obs[mask])
-        self._last_user_actions = actions
-        self.venv.step_async(actual_acts)
+        if self.traj_accum is None or self._obs is None:
+            raise RuntimeError("call .reset() before .step()")
+        executed = self._executed_actions(actions)
+        self._expert_acts = actions
+        self.venv.step_async(executed)
 
     def step_wait(self):
-        next_obs, rews, dones, infos = self.venv.step_wait()
-        assert isinstance(next_obs, np.ndarray)
-        assert self.traj_accum is not None
-        assert self._last_user_actions is not None
-        self._last_obs = next_obs
-        fresh = self.traj_accum.add_steps_and_auto_finish(obs=next_obs, acts=self._last_user_actions, rews=rews,
-                                                          infos=infos, dones=dones)
-        for traj_index, traj in enumerate(fresh):
-            _save_dagger_demo(traj, traj_index, self.save_dir, self.rng)
-        return next_obs, rews, dones, infos
+        obs, rews, dones, infos = self.venv.step_wait()
+        if self._expert_acts is None or self.traj_accum is None:
+            raise RuntimeError("step_wait() without step_async()")
+        self._obs = obs
+        finished = self.traj_accum.add_steps_and_auto_finish(obs=obs, acts=self._expert_acts, rews=rews, infos=infos,
+                                                             dones=dones)
+        for k, traj in enumerate(finished):
+            _save_dagger_demo(traj, k, self.save_dir, self.rng)
+        return obs, rews, dones, infos
 
 
 class NeedsDemosException(Exception):
     """Signals demos need to be collected for current round before continuing."""
 
 
+# ----------------------------------------------------------------------------- trainers
 class DAggerTrainer(base.BaseImitationAlgorithm):
-    """DAgger training class with low-level API suitable for interactive human feedback."""
+    """DAgger rounds with a low-level API suitable for interactive (human) feedback.
+
+    ``create_trajectory_collector`` -> collect episodes with it -> ``extend_and_update``
+    (aggregate + BC + next round)."""
 
     DEFAULT_N_EPOCHS: int = 4
 
@@ -202,26 +266,25 @@ class DAggerTrainer(base.BaseImitationAlgorithm):
                  beta_schedule: Optional[Callable[[int], float]] = None, bc_trainer: bc.BC,
                  custom_logger: Optional[imit_logger.HierarchicalLogger] = None):
         super().__init__(custom_logger=custom_logger)
-        if beta_schedule is None:
-            beta_schedule = LinearBetaSchedule(15)
-        self.beta_schedule = beta_schedule
-        self.scratch_dir = util.parse_path(scratch_dir)
+        self.beta_schedule = beta_schedule if beta_schedule is not None else LinearBetaSchedule(15)
+        self.base_scratch_dir = util.parse_path(scratch_dir)
+        world = pdist.world_size()
+        self.scratch_dir = self.base_scratch_dir / f"rank-{pdist.rank():02d}" if world > 1 else self.base_scratch_dir
         self.venv = venv
-        self.round_num = 0
-        self._last_loaded_round = -1
-        self._all_demos: List[types.Trajectory] = []
         self.rng = rng
+        self.round_num = 0
+        self._store = RoundDemoStore(self.scratch_dir)
         try:
             check_for_correct_spaces(self.venv, bc_trainer.observation_space, bc_trainer.action_space)
         except ValueError as e:
-            UserWarning(e)
+            log.warning("%s", e)
         self.bc_trainer = bc_trainer
         self.bc_trainer.logger = self.logger
 
     def __getstate__(self):
         d = dict(self.__dict__)
-        del d["venv"]
-        del d["_logger"]
+        d.pop("venv", None)
+        d.pop("_logger", None)
         return d
 
     @property
@@ -241,77 +304,64 @@ class DAggerTrainer(base.BaseImitationAlgorithm):
     def batch_size(self) -> int:
         return self.bc_trainer.batch_size
 
-    def _load_all_demos(self) -> Tuple[types.Transitions, List[int]]:
-        num_demos_by_round = []
-        for round_num in range(self._last_loaded_round + 1, self.round_num + 1):
-            round_dir = self._demo_dir_path_for_round(round_num)
-            demo_paths = self._get_demo_paths(round_dir)
-            self._all_demos.extend(serialize.load(p)[0] for p in demo_paths)
-            num_demos_by_round.append(len(demo_paths))
-        logging.info(f"Loaded {len(self._all_demos)} total")
-        return rollout.flatten_trajectories(self._all_demos), num_demos_by_round
-
-    def _get_demo_paths(self, round_dir: pathlib.Path) -> List[pathlib.Path]:
-        filenames = sorted(os.listdir(round_dir))
-        return [round_dir / f for f in filenames if f.endswith(".npz")]
+    @property
+    def _all_demos(self) -> List[types.Trajectory]:
+        """Every demonstration trajectory aggregated so far (all ranks, round order)."""
+        return self._store.trajectories
 
     def _demo_dir_path_for_round(self, round_num: Optional[int] = None) -> pathlib.Path:
-        if round_num is None:
-            round_num = self.round_num
-        return self.scratch_dir / "demos" / f"round-{round_num:03d}"
+        return self._store.round_dir(self.round_num if round_num is None else round_num)
 
-    def _try_load_demos(self) -> None:
-        demo_dir = self._demo_dir_path_for_round()
-        demo_paths = self._get_demo_paths(demo_dir) if demo_dir.is_dir() else []
-        if len(demo_paths) == 0:
+    def _aggregate_current_round(self) -> None:
+        """Make BC see the union of all rounds up to the current one (rank-agreed)."""
+        if not self._store.demos_everywhere(self.round_num):
             raise NeedsDemosException(
-                f"No demos found for round {self.round_num} in dir '{demo_dir}'. "
-                f"Maybe you need to collect some demos? See .create_trajectory_collector()"
-            )
-        if self._last_loaded_round < self.round_num:
-            transitions, num_demos = self._load_all_demos()
-            logging.info(f"Loaded {sum(num_demos)} new demos from {len(num_demos)} rounds")
-            if len(transitions) < self.batch_size:
-                raise ValueError(
-                    f"Not enough transitions to form a single batch: self.batch_size={self.batch_size} > "
-                    f"len(transitions)={len(transitions)}"
-                )
-            loader = base.TransitionsBatchLoader(transitions, self.batch_size, shuffle=True, drop_last=True,
-                                                 seed=int(self.rng.integers(0, 2**31 - 1)))
-            self.bc_trainer.set_demonstrations(loader)
-            self._last_loaded_round = self.round_num
+                f"No demos found for round {self.round_num} in dir '{self._demo_dir_path_for_round()}'"
+                + (" on every rank" if pdist.world_size() > 1 else "")
+                + ". Maybe you need to collect some demos? See .create_trajectory_collector()")
+        if self._store.loaded_through >= self.round_num:
+            return
+        transitions, counts = self._store.ingest(self.round_num)
+        log.info("loaded %d new demos from %d rounds", sum(counts), len(counts))
+        if len(transitions) < self.batch_size:
+            raise ValueError(f"Not enough transitions to form a single batch: self.batch_size={self.batch_size} > "
+                             f"len(transitions)={len(transitions)}")
+        seed = int(self.rng.integers(0, 2**31 - 1)) + 7919 * pdist.rank()
+        self.bc_trainer.set_demonstrations(base.TransitionsBatchLoader(transitions, self.batch_size, shuffle=True,
+                                                                       drop_last=True, seed=seed))
 
     def extend_and_update(self, bc_train_kwargs: Optional[Mapping[str, Any]] = None) -> int:
-        """Load new demos, train BC on all demos, advance the round counter."""
-        bc_train_kwargs = {} if bc_train_kwargs is None else dict(bc_train_kwargs)
-        if "log_rollouts_venv" not in bc_train_kwargs:
-            bc_train_kwargs["log_rollouts_venv"] = self.venv
-        if "n_epochs" not in bc_train_kwargs and "n_batches" not in bc_train_kwargs:
-            bc_train_kwargs["n_epochs"] = self.DEFAULT_N_EPOCHS
-        logging.info("Loading demonstrations")
-        self._try_load_demos()
-        logging.info(f"Training at round {self.round_num}")
-        self.bc_trainer.train(**bc_train_kwargs)
+        """Aggregate the new demos, train BC on everything collected so far, advance the round."""
+        kwargs = dict(bc_train_kwargs or {})
+        kwargs.setdefault("log_rollouts_venv", self.venv)
+        if "n_epochs" not in kwargs and "n_batches" not in kwargs:
+            kwargs["n_epochs"] = self.DEFAULT_N_EPOCHS
+        if pdist.world_size() > 1:
+            lo, neg_hi = pdist.allreduce_scalars([self.round_num, -self.round_num], op="min")
+            if lo != -neg_hi:
+                raise RuntimeError(f"DAgger ranks disagree on the round number ({int(lo)}..{int(-neg_hi)})")
+        self._aggregate_current_round()
+        log.info("training BC at round %d", self.round_num)
+        self.bc_trainer.train(**kwargs)
         self.round_num += 1
-        logging.info(f"New round number is {self.round_num}")
         return self.round_num
 
-    def create_trajectory_collector(self) -> InteractiveTrajectoryCollector:
-        save_dir = self._demo_dir_path_for_round()
-        beta = self.beta_schedule(self.round_num)
-        return InteractiveTrajectoryCollector(venv=self.venv, get_robot_acts=lambda acts: self.bc_trainer.policy.predict(acts)[0],
-                                              beta=beta, save_dir=save_dir, rng=self.rng)
+    def _robot_actions(self, obs: np.ndarray) -> np.ndarray:
+        return self.bc_trainer.policy.predict(obs)[0]
 
-    def save_trainer(self) -> Tuple[pathlib.Path, pathlib.Path]:
-        """Save ``checkpoint-{round}.pt`` / ``checkpoint-latest.pt`` and ``policy-{round}.pt`` /
-        ``policy-latest.pt`` (tensor/JSON-only files; see :func:`reconstruct_trainer`)."""
-        self.scratch_dir.mkdir(parents=True, exist_ok=True)
+    def create_trajectory_collector(self) -> InteractiveTrajectoryCollector:
+        """Host collector for the current round (β from the schedule, demos into the round dir)."""
+        return InteractiveTrajectoryCollector(venv=self.venv, get_robot_acts=self._robot_actions,
+                                              beta=self.beta_schedule(self.round_num),
+                                              save_dir=self._demo_dir_path_for_round(), rng=self.rng)
+
+    def _checkpoint_meta(self) -> Dict[str, Any]:
         bct = self.bc_trainer
         opt_cls = type(bct.optimizer)
-        meta = {
+        return {
             "class": type(self).__name__,
             "round_num": self.round_num,
-            "beta_schedule": _schedule_to_json(self.beta_schedule),
+            "beta_schedule": _schedule_json(self.beta_schedule),
             "rng_state": self.rng.bit_generator.state,
             "bc": {
                 "batch_size": bct.batch_size,
@@ -323,55 +373,174 @@ class DAggerTrainer(base.BaseImitationAlgorithm):
                 "l2_weight": bct.loss_calculator.l2_weight,
             },
         }
-        ckpt = {"format": "imitation_amd.dagger.v1", "meta": json.dumps(meta), "optimizer": bct.optimizer.state_dict()}
-        checkpoint_paths = [self.scratch_dir / f"checkpoint-{self.round_num:03d}.pt", self.scratch_dir / "checkpoint-latest.pt"]
-        for p in checkpoint_paths:
-            th.save(ckpt, p)
-        policy_paths = [self.scratch_dir / f"policy-{self.round_num:03d}.pt", self.scratch_dir / "policy-latest.pt"]
-        for p in policy_paths:
-            util.save_policy(self.policy, p)
-        if hasattr(self, "expert_policy") and hasattr(self.expert_policy, "save"):
-            self.expert_policy.save(self.scratch_dir / "expert-policy.pt")
-        return checkpoint_paths[0], policy_paths[0]
+
+    def save_trainer(self) -> Tuple[pathlib.Path, pathlib.Path]:
+        """Write ``checkpoint-{round}.pt`` / ``checkpoint-latest.pt`` (JSON metadata + optimizer
+        state) and ``policy-{round}.pt`` / ``policy-latest.pt`` into this rank's scratch dir."""
+        self.scratch_dir.mkdir(parents=True, exist_ok=True)
+        ckpt = {"format": "imitation_amd.dagger.v1", "meta": json.dumps(self._checkpoint_meta()),
+                "optimizer": self.bc_trainer.optimizer.state_dict()}
+        tags = (f"{self.round_num:03d}", "latest")
+        ckpt_paths = [self.scratch_dir / f"checkpoint-{t}.pt" for t in tags]
+        pol_paths = [self.scratch_dir / f"policy-{t}.pt" for t in tags]
+        for cp, pp in zip(ckpt_paths, pol_paths):
+            th.save(ckpt, cp)
+            util.save_policy(self.policy, pp)
+        expert = getattr(self, "expert_policy", None)
+        if expert is not None and hasattr(expert, "save"):
+            expert.save(self.scratch_dir / "expert-policy.pt")
+        return ckpt_paths[0], pol_paths[0]
+
+
+def reconstruct_trainer(scratch_dir: types.AnyPath, venv, custom_logger: Optional[imit_logger.HierarchicalLogger] = None,
+                        device: Union[th.device, str] = "auto") -> DAggerTrainer:
+    """Rebuild a trainer saved by :meth:`DAggerTrainer.save_trainer` (reference
+    ``dagger.py:99-127``). Demonstrations are re-read from the scratch dir on the next
+    update. Under DP each rank reads its own ``rank-RR`` subtree."""
+    from imitation_amd.rl.policies import load_policy_file
+
+    custom_logger = custom_logger or imit_logger.configure()
+    root = util.parse_path(scratch_dir)
+    own = root / f"rank-{pdist.rank():02d}" if pdist.world_size() > 1 else root
+    ckpt = th.load(own / "checkpoint-latest.pt", map_location=get_device(device), weights_only=True)
+    meta = json.loads(ckpt["meta"])
+    policy = load_policy_file(own / "policy-latest.pt", device=device)
+    b = meta["bc"]
+    bc_trainer = bc.BC(observation_space=policy.observation_space, action_space=policy.action_space,
+                       rng=np.random.default_rng(), policy=policy, demonstrations=None, batch_size=b["batch_size"],
+                       minibatch_size=b["minibatch_size"], optimizer_cls=save_util._resolve_class(b["optimizer_cls"]),
+                       optimizer_kwargs=b["optimizer_kwargs"], ent_weight=b["ent_weight"], l2_weight=b["l2_weight"],
+                       custom_logger=custom_logger)
+    bc_trainer.optimizer.load_state_dict(ckpt["optimizer"])
+    rng = np.random.default_rng()
+    rng.bit_generator.state = meta["rng_state"]
+    common = dict(venv=venv, scratch_dir=root, rng=rng, beta_schedule=_schedule_from_json(meta["beta_schedule"]),
+                  bc_trainer=bc_trainer, custom_logger=custom_logger)
+    if meta["class"] == "SimpleDAggerTrainer":
+        trainer: DAggerTrainer = SimpleDAggerTrainer(expert_policy=load_policy_file(own / "expert-policy.pt", device=device),
+                                                     **common)
+    else:
+        trainer = DAggerTrainer(**common)
+    trainer.round_num = meta["round_num"]
+    return trainer
 
 
 class SimpleDAggerTrainer(DAggerTrainer):
-    """Simpler subclass of DAggerTrainer for training with synthetic feedback."""
+    """DAgger with a synthetic (policy) expert: ``train`` runs whole rounds by itself.
+
+    Each round collects at least ``max(rollout_round_min_timesteps, batch_size)`` steps
+    and ``rollout_round_min_episodes`` episodes PER RANK (weak scaling; the expert acts
+    deterministically), then aggregates and trains. ``total_timesteps`` counts the env
+    steps of all ranks. Native image envs on a GPU collect with the device collector
+    (``device_collector='auto'``)."""
 
     def __init__(self, *, venv, scratch_dir: types.AnyPath, expert_policy, rng: np.random.Generator,
-                 expert_trajs: Optional[Sequence[types.Trajectory]] = None, **dagger_trainer_kwargs):
+                 expert_trajs: Optional[Sequence[types.Trajectory]] = None, device_collector: Union[str, bool] = "auto",
+                 **dagger_trainer_kwargs):
         super().__init__(venv=venv, scratch_dir=scratch_dir, rng=rng, **dagger_trainer_kwargs)
+        for what in ("observation_space", "action_space"):
+            if getattr(expert_policy, what) != getattr(self.venv, what):
+                raise ValueError(f"Mismatched {what.split('_')[0]} space between expert_policy and venv")
         self.expert_policy = expert_policy
-        if expert_policy.observation_space != self.venv.observation_space:
-            raise ValueError("Mismatched observation space between expert_policy and venv")
-        if expert_policy.action_space != self.venv.action_space:
-            raise ValueError("Mismatched action space between expert_policy and venv")
-        if expert_trajs is not None:
-            for traj_index, traj in enumerate(expert_trajs):
-                _save_dagger_demo(traj, traj_index, self._demo_dir_path_for_round(), self.rng, prefix="initial_data")
+        for k, traj in enumerate(expert_trajs or ()):
+            self._store.write(traj, k, self.round_num, self.rng, prefix="initial_data")
+        self._device_collector = None
+        self._writer = None
+        if device_collector:
+            from imitation_amd.engine import dagger as dagger_engine
+
+            ok, why = dagger_engine.supports(self.venv, self.expert_policy, self.bc_trainer.policy)
+            if ok:
+                self._device_collector = dagger_engine.DeviceDAggerCollector(self.venv, self.expert_policy,
+                                                                             self.bc_trainer.policy, self.rng)
+                self._device_agg = dagger_engine.DeviceDemoAggregate(self.bc_trainer.policy.device)
+                self._device_counts: Dict[int, int] = {}
+                self._writer = dagger_engine.AsyncDemoWriter()
+                if expert_trajs:
+                    self._device_append(list(expert_trajs), self.round_num)
+            elif device_collector is True:
+                raise ValueError(f"device DAgger collector not applicable: {why}")
+
+    def _device_append(self, trajs: Sequence[types.Trajectory], round_num: int, obs=None, acts=None) -> None:
+        """Add demos to the device aggregate (all-gathered under DP); host arrays are uploaded."""
+        if obs is None:
+            flat = rollout.flatten_trajectories(list(trajs))
+            dev = self._device_agg.device
+            obs = th.as_tensor(np.asarray(flat.obs), device=dev)
+            acts = th.as_tensor(np.asarray(flat.acts), device=dev)
+            if isinstance(self.venv.action_space, spaces_mod.Discrete):
+                acts = acts.long()
+        self._device_agg.append(obs, acts)
+        self._device_counts[round_num] = self._device_counts.get(round_num, 0) + len(trajs)
+        self._store.trajectories.extend(trajs)
+
+    @property
+    def collector_kind(self) -> str:
+        return "device" if self._device_collector is not None else "host"
+
+    def _collect_round(self, min_episodes: int, min_timesteps: int) -> List[types.TrajectoryWithRew]:
+        beta = self.beta_schedule(self.round_num)
+        if self._device_collector is not None:
+            col = self._device_collector
+            trajs = col.collect(beta, min_timesteps=min_timesteps, min_episodes=min_episodes)
+            for k, traj in enumerate(trajs):  # reference-format demo files, off the critical path
+                self._writer.submit(self._store.write, traj, k, self.round_num, np.random.default_rng(self.rng.integers(2**63)))
+            self._device_append(trajs, self.round_num, col.last_obs, col.last_acts)
+            return trajs
+        collector = self.create_trajectory_collector()
+        sample_until = rollout.make_sample_until(min_timesteps=min_timesteps, min_episodes=min_episodes)
+        return rollout.generate_trajectories(policy=self.expert_policy, venv=collector, sample_until=sample_until,
+                                             deterministic_policy=True, rng=collector.rng)
+
+    def _aggregate_current_round(self) -> None:
+        if self._device_collector is None:
+            return super()._aggregate_current_round()
+        have = float(self._device_counts.get(self.round_num, 0) > 0)
+        if pdist.world_size() > 1:
+            have = pdist.allreduce_scalars([have], op="min")[0]
+        if not have:
+            raise NeedsDemosException(f"No demos collected for round {self.round_num}")
+        if self._store.loaded_through >= self.round_num:
+            return
+        self._store.loaded_through = self.round_num
+        if len(self._device_agg) < self.batch_size:
+            raise ValueError(f"Not enough transitions to form a single batch: self.batch_size={self.batch_size} > "
+                             f"len(transitions)={len(self._device_agg)}")
+        from imitation_amd.engine import dagger as dagger_engine
+
+        seed = int(self.rng.integers(0, 2**31 - 1)) + 7919 * pdist.rank()
+        self.bc_trainer.set_demonstrations(dagger_engine.DeviceTransitionsLoader(self._device_agg, self.batch_size, seed))
+
+    def save_trainer(self) -> Tuple[pathlib.Path, pathlib.Path]:
+        if self._writer is not None:
+            self._writer.flush()  # every demo file of the finished rounds is on disk
+        return super().save_trainer()
 
     def train(self, total_timesteps: int, *, rollout_round_min_episodes: int = 3, rollout_round_min_timesteps: int = 500,
               bc_train_kwargs: Optional[dict] = None) -> None:
-        """Train the DAgger agent until at least ``total_timesteps`` environment steps have been collected."""
-        total_timestep_count = 0
-        round_num = 0
-        while total_timestep_count < total_timesteps:
-            collector = self.create_trajectory_collector()
-            round_episode_count = 0
-            round_timestep_count = 0
-            sample_until = rollout.make_sample_until(min_timesteps=max(rollout_round_min_timesteps, self.batch_size),
-                                                     min_episodes=rollout_round_min_episodes)
-            trajectories = rollout.generate_trajectories(policy=self.expert_policy, venv=collector, sample_until=sample_until,
-                                                         deterministic_policy=True, rng=collector.rng)
-            for traj in trajectories:
-                self._logger.record_mean("dagger/mean_episode_reward", np.sum(traj.rews))
-                round_timestep_count += len(traj)
-                total_timestep_count += len(traj)
-            round_episode_count += len(trajectories)
-            self._logger.record("dagger/total_timesteps", total_timestep_count)
-            self._logger.record("dagger/round_num", round_num)
-            self._logger.record("dagger/round_episode_count", round_episode_count)
-            self._logger.record("dagger/round_timestep_count", round_timestep_count)
+        """Run rounds until ``total_timesteps`` env steps (all ranks) have been collected."""
+        collected = 0
+        local = 0
+        rounds = 0
+        min_steps = max(rollout_round_min_timesteps, self.batch_size)
+        while collected < total_timesteps:
+            trajs = self._collect_round(rollout_round_min_episodes, min_steps)
+            lens = [len(t) for t in trajs]
+            n_eps, n_steps = len(trajs), sum(lens)
+            local += n_steps
+            if pdist.world_size() > 1:
+                n_eps, n_steps = (int(v) for v in pdist.allreduce_scalars([n_eps, n_steps], op="sum"))
+            collected += n_steps
+            for t in trajs:
+                self._logger.record_mean("dagger/mean_episode_reward", float(np.sum(t.rews)))
+            lg = self._logger
+            lg.record("dagger/total_timesteps", collected)
+            lg.record("dagger/round_num", rounds)
+            lg.record("dagger/round_episode_count", n_eps)
+            lg.record("dagger/round_timestep_count", n_steps)
             self.extend_and_update(bc_train_kwargs)
-            round_num += 1
-        self.last_train_timesteps = total_timestep_count
+            rounds += 1
+        self.last_train_timesteps = collected  # all ranks
+        self.last_train_timesteps_local = local
+        if self._writer is not None:
+            self._writer.flush()

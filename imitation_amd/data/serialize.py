@@ -26,7 +26,15 @@ from imitation_amd.util import util
 def save(path: AnyPath, trajectories: Sequence[Trajectory]) -> None:
     """Save trajectories to a HuggingFace dataset directory at ``path``."""
     p = str(util.parse_path(path))
-    huggingface_utils.trajectories_to_dataset(trajectories).save_to_disk(p)
+    import datasets
+
+    was_enabled = datasets.utils.logging.is_progress_bar_enabled()
+    datasets.utils.logging.disable_progress_bar()  # one bar per demo file otherwise
+    try:
+        huggingface_utils.trajectories_to_dataset(trajectories).save_to_disk(p)
+    finally:
+        if was_enabled:
+            datasets.utils.logging.enable_progress_bar()
     logging.info(f"Dumped demonstrations to {p}.")
 
 

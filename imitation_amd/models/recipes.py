@@ -209,7 +209,7 @@ def dagger_pong(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "Pong
     trainer = dagger.SimpleDAggerTrainer(venv=venv, scratch_dir=scratch, expert_policy=expert_policy,
                                          rng=np.random.default_rng(seed), bc_trainer=bc_trainer, custom_logger=log,
                                          **overrides)
-    return Built(trainer, venv, "dagger_pong", env_id, 0, {"expert_policy": expert_policy})
+    return Built(trainer, venv, "dagger_pong", env_id, 0, {"expert_policy": expert_policy, "engine": trainer.collector_kind})
 
 
 def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "seals/Walker2d-v1",

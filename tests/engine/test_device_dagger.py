@@ -1,0 +1,108 @@
+"""Device DAgger collector (engine/dagger.py, csrc/kernels/dagger.hip) vs the host env."""
+
+import numpy as np
+import pytest
+import torch as th
+
+gpu = pytest.mark.gpu
+
+
+@gpu
+@pytest.mark.parametrize("env_id,max_steps", [("PongNoFrameskip-v4", 40), ("CartPole-v1", 60), ("seals/HalfCheetah-v1", 30)])
+def test_dagger_env_step_matches_host_env(env_id, max_steps):
+    from imitation_amd.envs.vec_env import NativeVecEnv
+
+    N = 4
+    venv = NativeVecEnv(env_id, N, seed=3, max_episode_steps=max_steps)
+    obs0 = venv.reset()
+    st = venv.get_state()
+    from imitation_amd import ops
+
+    C = ops.native()
+    dev = th.device("cuda")
+    img = venv._is_image
+    dt = th.uint8 if img else th.float32
+    d = dict(env=env_id, N=N, max_steps=max_steps, mode=0,
+             state=th.as_tensor(st["state"], device=dev).float().contiguous(),
+             rng=th.as_tensor(st["rng"].astype(np.int64), device=dev).contiguous(),
+             elapsed=th.as_tensor(st["elapsed"].astype(np.int32), device=dev).contiguous(),
+             ep_ret=th.zeros(N, device=dev), obs=th.as_tensor(obs0, device=dev).to(dt).contiguous(),
+             rew=th.zeros(N, device=dev), term=th.zeros(N, dtype=th.uint8, device=dev),
+             trunc=th.zeros(N, dtype=th.uint8, device=dev), term_obs=th.zeros_like(th.as_tensor(obs0, device=dev).to(dt)),
+             ep_ret_out=th.zeros(N, device=dev), ep_len_out=th.zeros(N, dtype=th.int32, device=dev))
+    rng = np.random.default_rng(0)
+    discrete = venv._discrete
+    n_done = 0
+    for t in range(3 * max_steps):
+        if discrete:
+            a = rng.integers(0, venv.action_space.n, size=N)
+            d["actions"] = th.as_tensor(a, device=dev, dtype=th.int64)
+        else:
+            a = rng.uniform(-1, 1, size=(N,) + venv.action_space.shape).astype(np.float32)
+            d["actions"] = th.as_tensor(a, device=dev)
+        C.dagger_env_step(d)
+        obs, rew, dones, infos = venv.step(a)
+        if img:  # integer frames: bit-exact
+            np.testing.assert_array_equal(d["obs"].cpu().numpy(), obs)
+        else:  # same IA_HD physics; the device build contracts FMAs (ulp-level drift)
+            np.testing.assert_allclose(d["obs"].cpu().numpy(), obs, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(d["rew"].cpu().numpy(), rew, rtol=1e-4, atol=1e-4)
+        dev_done = (d["term"] | d["trunc"]).cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(dev_done, dones)
+        for i in np.flatnonzero(dones):
+            n_done += 1
+            np.testing.assert_allclose(d["term_obs"][i].cpu().numpy(), infos[i]["terminal_observation"], rtol=1e-4, atol=1e-4)
+            assert int(d["ep_len_out"][i]) == infos[i]["episode"]["l"]
+            assert abs(float(d["ep_ret_out"][i]) - infos[i]["episode"]["r"]) < 1e-3 * max(1.0, abs(infos[i]["episode"]["r"]))
+    assert n_done >= N  # the TimeLimit / reset path ran
+
+
+def _pong_trainer(tmp_path, n_envs=4, device_collector=True):
+    from imitation_amd.algorithms import bc, dagger
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+    from imitation_amd.util import logger
+    from imitation_amd.util.util import make_vec_env
+
+    th.manual_seed(0)
+    venv = make_vec_env("PongNoFrameskip-v4", rng=np.random.default_rng(0), n_envs=n_envs, max_episode_steps=200)
+    lr = lambda _: 1e-3  # noqa: E731
+    expert = ActorCriticCnnPolicy(venv.observation_space, venv.action_space, lr).cuda()
+    learner = ActorCriticCnnPolicy(venv.observation_space, venv.action_space, lr).cuda()
+    log = logger.configure(str(tmp_path / "log"), format_strs=[])
+    bct = bc.BC(observation_space=venv.observation_space, action_space=venv.action_space, rng=np.random.default_rng(0),
+                policy=learner, batch_size=32, device="cuda", custom_logger=log)
+    tr = dagger.SimpleDAggerTrainer(venv=venv, scratch_dir=tmp_path / "scratch", expert_policy=expert,
+                                    rng=np.random.default_rng(0), bc_trainer=bct, custom_logger=log,
+                                    device_collector=device_collector)
+    return tr, venv, expert, learner
+
+
+@gpu
+def test_device_dagger_pong_rounds(tmp_path):
+    tr, venv, expert, learner = _pong_trainer(tmp_path)
+    assert tr.collector_kind == "device"
+    col = tr._device_collector
+    before = [p.detach().clone() for p in learner.parameters()]
+    tr.train(1000, rollout_round_min_episodes=1, rollout_round_min_timesteps=400,
+             bc_train_kwargs=dict(n_epochs=1, progress_bar=False, log_interval=10**9))
+    assert tr.round_num >= 1
+    assert col._graph is not None, "the chunk step was not graph-captured"
+    n_rows = sum(len(t) for t in tr._all_demos)
+    assert len(tr._device_agg) == n_rows and n_rows >= 400
+    # finished episodes only, expert actions recorded, obs length = acts + 1
+    for t in tr._all_demos:
+        assert t.obs.shape[0] == len(t.acts) + 1 and t.obs.dtype == np.uint8
+    # device rows == the host trajectories' transitions (same order)
+    first = tr._all_demos[0]
+    np.testing.assert_array_equal(tr._device_agg.obs[: len(first)].cpu().numpy(), first.obs[:-1])
+    np.testing.assert_array_equal(tr._device_agg.acts[: len(first)].cpu().numpy(), first.acts)
+    # reference-format demo files were written for every trajectory of round 0
+    files = tr._store.files(0)
+    assert len(files) >= 1
+    assert any(not th.equal(a, b) for a, b in zip(before, learner.parameters()))
+    # recorded actions are the deterministic expert's
+    o = th.as_tensor(first.obs[:16], device="cuda")
+    from imitation_amd.engine.dagger import policy_actions
+
+    with th.no_grad():
+        np.testing.assert_array_equal(policy_actions(expert, o, True).cpu().numpy(), first.acts[:16])
