@@ -110,9 +110,70 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, to
   return dz;
 }
 
+// h fp32 [B, NH] = relu(x [B, K] . w [NH, K]^T + b); x, w bf16
+torch::Tensor cnn_fc(torch::Tensor x, torch::Tensor w, torch::Tensor b) {
+  IA_CHECK_CUDA(x);
+  IA_CHECK_CONTIG(x);
+  IA_CHECK_CUDA(w);
+  IA_CHECK_CONTIG(w);
+  IA_CHECK_GPU_F32(b);
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16, "x, w must be bf16");
+  const int B = (int)x.size(0);
+  const int64_t K = x.numel() / std::max<int64_t>(1, B);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K, "w must be [NH, K] with K = x.numel() / B");
+  const int NH = (int)w.size(0);
+  TORCH_CHECK(b.numel() == NH && K % 32 == 0 && NH % 16 == 0, "cnn_fc: K % 32, NH % 16, bias [NH]");
+  auto h = torch::empty({B, NH}, x.options().dtype(torch::kFloat32));
+  IA_HIP_CHECK3(ia::cnn_fc(x.data_ptr(), w.data_ptr(), b.data_ptr<float>(), h.data_ptr<float>(), B, (int)K, NH, ia_stream()));
+  return h;
+}
+
+// Action head + choice (+ beta-mix); see cnn_infer.hip. All outputs are preallocated int64 [B].
+void cnn_head(torch::Tensor h, torch::Tensor w2, torch::Tensor b2, int64_t mode, int64_t seed,
+              c10::optional<torch::Tensor> counter, torch::Tensor out, c10::optional<torch::Tensor> rec_out,
+              c10::optional<torch::Tensor> mix_expert, c10::optional<torch::Tensor> beta,
+              c10::optional<torch::Tensor> exec_out) {
+  IA_CHECK_GPU_F32(h);
+  IA_CHECK_GPU_F32(w2);
+  IA_CHECK_GPU_F32(b2);
+  ia::CnnHeadArgs a{};
+  a.B = (int)h.size(0);
+  a.NH = (int)h.size(1);
+  a.A = (int)w2.size(0);
+  TORCH_CHECK(w2.dim() == 2 && w2.size(1) == a.NH && b2.numel() == a.A, "head shapes");
+  auto i64 = [&](const torch::Tensor& t, const char* k) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kInt64 && t.numel() == a.B, k,
+                " must be a contiguous int64 GPU tensor of B elements");
+    return t.data_ptr<int64_t>();
+  };
+  a.h = h.data_ptr<float>();
+  a.W2 = w2.data_ptr<float>();
+  a.b2 = b2.data_ptr<float>();
+  a.mode = (int)mode;
+  a.seed = (uint64_t)seed;
+  if (counter.has_value() && counter->defined()) {
+    TORCH_CHECK(counter->is_cuda() && counter->scalar_type() == torch::kInt64 && counter->numel() == 1, "counter");
+    a.counter = reinterpret_cast<uint64_t*>(counter->data_ptr<int64_t>());
+  }
+  a.out = i64(out, "out");
+  if (rec_out.has_value() && rec_out->defined()) a.rec_out = i64(*rec_out, "rec_out");
+  if (exec_out.has_value() && exec_out->defined()) {
+    TORCH_CHECK(mix_expert.has_value() && beta.has_value(), "exec_out needs mix_expert and beta");
+    a.exec_out = i64(*exec_out, "exec_out");
+    a.mix_expert = i64(*mix_expert, "mix_expert");
+    IA_CHECK_GPU_F32(*beta);
+    a.beta = beta->data_ptr<float>();
+  }
+  IA_HIP_CHECK3(ia::cnn_head(a, ia_stream()));
+}
+
 }  // namespace
 
 void register_conv(py::module& m) {
+  m.def("cnn_fc", &cnn_fc, "NatureCNN actor FC: relu(x . w^T + b), bf16 MFMA", py::arg("x"), py::arg("w"), py::arg("b"));
+  m.def("cnn_head", &cnn_head, "actor head + argmax / Gumbel sample (+ beta mix)", py::arg("h"), py::arg("w2"),
+        py::arg("b2"), py::arg("mode"), py::arg("seed"), py::arg("counter"), py::arg("out"), py::arg("rec_out") = py::none(),
+        py::arg("mix_expert") = py::none(), py::arg("beta") = py::none(), py::arg("exec_out") = py::none());
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv + bias + ReLU (bf16 MFMA)", py::arg("x"), py::arg("wb"),
         py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true);
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)");

@@ -312,6 +312,10 @@ void dagger_env_step(py::dict d) {
     a.ep_ret_out = tptr<float>(d, "ep_ret_out");
     a.ep_len_out = tptr<int>(d, "ep_len_out");
     for (const char* k : {"rew", "term", "trunc", "ep_ret_out", "ep_len_out"}) check_numel(k, a.N);
+    if (d.contains("obs_rec") && !d["obs_rec"].is_none()) {
+      a.obs_rec = img ? (void*)tptr<uint8_t>(d, "obs_rec") : (void*)tptr<float>(d, "obs_rec");
+      check_numel("obs_rec", a.N * obs_elems);
+    }
   }
   IA_HIP_CHECK2(ia::dagger_env_step(a, ia_stream()));
 }

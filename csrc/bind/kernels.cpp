@@ -102,6 +102,34 @@ py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch:
   return py::make_tuple(adv, ret);
 }
 
+// One fused Adam / AdamW step over flat fp32 buffers (ops/optim.py FusedAdam).
+void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg, torch::Tensor exp_avg_sq,
+               torch::Tensor step, double lr, double beta1, double beta2, double eps, double weight_decay, bool decoupled,
+               bool maximize, bool zero_grad) {
+  for (auto* t : {&params, &grads, &exp_avg, &exp_avg_sq}) {
+    IA_CHECK_GPU_F32(*t);
+    TORCH_CHECK(t->numel() == params.numel(), "flat Adam buffers must have equal sizes");
+  }
+  IA_CHECK_GPU_F32(step);
+  TORCH_CHECK(step.numel() == 1, "step must be a 1-element device tensor");
+  ia::AdamArgs a{};
+  a.params = params.data_ptr<float>();
+  a.grads = grads.data_ptr<float>();
+  a.exp_avg = exp_avg.data_ptr<float>();
+  a.exp_avg_sq = exp_avg_sq.data_ptr<float>();
+  a.step = step.data_ptr<float>();
+  a.n = params.numel();
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.decoupled = decoupled ? 1 : 0;
+  a.maximize = maximize ? 1 : 0;
+  a.zero_grad = zero_grad ? 1 : 0;
+  IA_HIP_CHECK(ia::adam_flat(a, ia_stream()));
+}
+
 // [E, n] int32: row e is a pseudo-random permutation of 0..n-1 keyed by (seed, e).
 torch::Tensor random_permutations(int64_t E, int64_t n, int64_t seed, torch::Device device) {
   TORCH_CHECK(device.is_cuda(), "random_permutations runs on the GPU");
@@ -154,5 +182,8 @@ void register_kernels(py::module& m) {
         py::arg("norm_eps") = 1e-5, py::arg("norm_clip") = 0.0, py::arg("need_dx") = false);
   m.def("gae", &gae, py::arg("rewards"), py::arg("values"), py::arg("episode_starts"), py::arg("last_values"),
         py::arg("dones"), py::arg("gamma"), py::arg("lam"));
+  m.def("adam_flat", &adam_flat, py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"),
+        py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
+        py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"));
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
 }

@@ -84,6 +84,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
   const int M = g.B * OHW;
   if (m0 >= M) return;
   const int K = g.KH * g.KW * g.C;
+  const int n_base = blockIdx.y * 16 * NT;  // split-N grids (small batches): this block's channels
   const int rowlen = g.KW * g.C;
   const int r = l & 15, kq = (l >> 4) * 8;
   const int m = m0 + r;
@@ -95,8 +96,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = zero4();
-  const bf16* wr = Wb + (size_t)r * K + kq;
-#pragma unroll 2
+  const bf16* wr = Wb + (size_t)(n_base + r) * K + kq;
+#pragma unroll 4
   for (int k0 = 0; k0 < K; k0 += 32) {
     const int k = k0 + kq;
     const int kh = k / rowlen, off = k - kh * rowlen;
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
   const int col = l & 15;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int n = t * 16 + col;
+    const int n = n_base + t * 16 + col;
     const float bb = bias ? bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -291,12 +292,22 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
   for (int n = threadIdx.x; n < N; n += 512) out[(size_t)N * K + n] = red[n];
 }
 
+// Fixed-order sum of the wgrad block partials: 4 independent accumulators (blocks b with
+// b % 4 == j) keep 4 loads in flight per thread, combined in a fixed order at the end.
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restrict__ slab, int nblk, int len,
                                                           float* __restrict__ dW, float* __restrict__ db, int nk) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += slab[(size_t)b * len + i];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = 0;
+  for (; b + 3 < nblk; b += 4) {
+    s0 += slab[(size_t)b * len + i];
+    s1 += slab[(size_t)(b + 1) * len + i];
+    s2 += slab[(size_t)(b + 2) * len + i];
+    s3 += slab[(size_t)(b + 3) * len + i];
+  }
+  for (; b < nblk; ++b) s0 += slab[(size_t)b * len + i];
+  const float s = (s0 + s1) + (s2 + s3);
   if (i < nk) dW[i] = s;
   else if (db) db[i - nk] = s;
 }
@@ -305,7 +316,15 @@ template <typename TIn>
 hipError_t launch_fwd(const TIn* X, const bf16* Wb, const float* bias, bf16* Y, const ConvGeo& g, float scale, int relu,
                       hipStream_t s) {
   const int M = g.B * g.OH * g.OW;
-  const dim3 grid((M + 63) / 64), block(256);
+  const dim3 block(256);
+  if ((M + 63) / 64 < 96) {
+    // small batches (policy inference): one 16-channel slice per block row, so the grid has
+    // N/16 x as many waves to hide the operand-load latency of the K loop
+    const dim3 grid((M + 63) / 64, g.N / 16);
+    hipLaunchKernelGGL((conv_fwd_kernel<TIn, 1>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu);
+    return hipGetLastError();
+  }
+  const dim3 grid((M + 63) / 64);
   switch (g.N / 16) {
     case 1: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 1>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
     case 2: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 2>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
@@ -372,8 +391,11 @@ void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* mpb) {
   const int M = g.B * g.OH * g.OW;
   const int chunks = (M + 31) / 32;
   const int K = g.KH * g.KW * g.C;
-  // fp32 partial traffic (nblk x N x K) vs parallelism: fewer blocks for the big-K layers
-  const int cap = 256;  // one block per CU; fp32 partial traffic is nblk x N x K
+  // fp32 partial traffic (nblk x N x K, written then re-read by conv_reduce) vs parallelism:
+  // ~1M partial floats per layer at most (the 256-block cap moved 24 MB per NatureCNN BC step)
+  const int len = g.N * K + g.N;
+  int cap = (1 << 20) / len;
+  cap = cap < 16 ? 16 : (cap > 256 ? 256 : cap);
   int b = chunks < cap ? chunks : cap;
   const int cpb = (chunks + b - 1) / b;
   b = (chunks + cpb - 1) / cpb;

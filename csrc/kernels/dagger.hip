@@ -23,13 +23,16 @@
 namespace ia {
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 1024;  // 7056 pixels: ~7 per thread
 constexpr int kPix = kPongH * kPongW;
 
-__device__ __forceinline__ void render(const float* s, uint32_t* frame, bool reset_stack) {
+// rec (optional): receives the stack as it was before this render
+__device__ __forceinline__ void render(const float* s, uint32_t* frame, bool reset_stack, uint32_t* rec = nullptr) {
   for (int p = threadIdx.x; p < kPix; p += kThreads) {
     const uint32_t v = pong_pixel(s, p / kPongW, p % kPongW);
-    frame[p] = reset_stack ? v * 0x01010101u : ((frame[p] >> 8) | (v << 24));
+    const uint32_t old = frame[p];
+    if (rec) rec[p] = old;
+    frame[p] = reset_stack ? v * 0x01010101u : ((old >> 8) | (v << 24));
   }
 }
 
@@ -76,6 +79,8 @@ __global__ __launch_bounds__(kThreads) void dagger_env_kernel(DaggerEnvArgs a) {
     for (int k = 0; k < a.sdim; ++k) s_state[k] = st[k];
     if (!img) {
       float* o = a.obs_f + (size_t)n * a.P.obs_dim;
+      if (a.obs_rec)
+        for (int k = 0; k < a.P.obs_dim; ++k) static_cast<float*>(a.obs_rec)[(size_t)n * a.P.obs_dim + k] = o[k];
       env_obs(a.P, st, o);
       if (done) {
         for (int k = 0; k < a.P.obs_dim; ++k) a.term_obs_f[(size_t)n * a.P.obs_dim + k] = o[k];
@@ -92,7 +97,8 @@ __global__ __launch_bounds__(kThreads) void dagger_env_kernel(DaggerEnvArgs a) {
   }
   __syncthreads();
   if (!img) return;
-  render(s_state, frame, false);  // the post-step frame
+  uint32_t* rec = a.obs_rec ? static_cast<uint32_t*>(a.obs_rec) + (size_t)n * kPix : nullptr;
+  render(s_state, frame, false, rec);  // the post-step frame (pre-step stack -> rec)
   if (s_done) {
     __syncthreads();
     uint32_t* tobs = reinterpret_cast<uint32_t*>(a.term_obs_u8 + (size_t)n * kPix * kPongStack);

@@ -96,8 +96,38 @@ struct DaggerEnvArgs {
   float* term_obs_f;        // [N, obs_dim] terminal observations (written for done envs)
   float* ep_ret_out;        // [N] episode return at episode end (else 0)
   int* ep_len_out;          // [N] episode length at episode end (else 0)
+  void* obs_rec;            // optional: the pre-step observation is copied here ([N, obs...])
 };
 hipError_t dagger_env_step(const DaggerEnvArgs& a, hipStream_t s);
+
+// ---- cnn_infer.hip: NatureCNN actor tail for the DAgger collector
+// h[B][NH] = relu(X[B][K] . W[NH][K]^T + bias), X / W bf16 (K % 32 == 0, NH % 16 == 0)
+hipError_t cnn_fc(const void* X, const void* W, const float* bias, float* H, int B, int K, int NH, hipStream_t s);
+struct CnnHeadArgs {
+  const float *h, *W2, *b2;  // h [B, NH], W2 [A, NH], b2 [A]
+  int B, NH, A;
+  int mode;                  // 0: argmax; 1: Gumbel-max sample
+  uint64_t seed;
+  uint64_t* counter;         // device call counter (advanced by one per launch), or null
+  int64_t* out;              // [B] chosen action
+  int64_t* rec_out;          // optional second copy of the action (record slot)
+  const int64_t* mix_expert; // optional: expert actions for the beta-mix
+  const float* beta;         // device scalar (with mix_expert)
+  int64_t* exec_out;         // optional: executed action (u > beta ? own : expert)
+};
+hipError_t cnn_head(const CnnHeadArgs& a, hipStream_t s);
+
+// ---- optim.hip: fused Adam / AdamW over a flat fp32 buffer
+struct AdamArgs {
+  float *params, *grads, *exp_avg, *exp_avg_sq;
+  const float* step;  // device step counter, already incremented for this step
+  int64_t n;
+  float lr, beta1, beta2, eps, weight_decay;
+  int decoupled;  // AdamW: p *= 1 - lr * wd
+  int maximize;
+  int zero_grad;  // clear the gradient after reading it
+};
+hipError_t adam_flat(const AdamArgs& a, hipStream_t s);
 
 // ---- rl.hip: GAE scan over [T, N]
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,

@@ -1,0 +1,66 @@
+// Fused Adam / AdamW over one flat fp32 parameter buffer (imitation_amd/ops/optim.py).
+//
+// torch.optim.Adam(capturable, foreach) spends ~8 multi-tensor launches per step on a
+// model's parameter list (BC on NatureCNN: ~110 us of a ~1 ms graphed minibatch); the
+// reference optimisers are th.optim.Adam (bc.py:284, common.py:123) and AdamW
+// (preference_comparisons.py:1192). Here every parameter of a group lives in one
+// contiguous buffer, so a step is ONE elementwise launch: 4 floats per thread, the
+// bias corrections from the device step counter (graph-capturable), and the gradient
+// slot cleared in the same pass (the next backward accumulates into a zeroed bucket).
+#include <hip/hip_runtime.h>
+
+#include "launchers.h"
+
+namespace ia {
+namespace {
+
+__device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, const AdamArgs& a, float step_size,
+                                         float bc2_sqrt) {
+  float gr = a.maximize ? -g : g;
+  if (a.weight_decay != 0.f) {
+    if (a.decoupled) p *= 1.f - a.lr * a.weight_decay;
+    else gr += a.weight_decay * p;
+  }
+  m += (1.f - a.beta1) * (gr - m);
+  v = v * a.beta2 + (1.f - a.beta2) * gr * gr;
+  const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+  p -= step_size * (m / denom);
+  if (a.zero_grad) g = 0.f;
+}
+
+__global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
+  const float t = *a.step;
+  const float bc1 = 1.f - powf(a.beta1, t);
+  const float bc2_sqrt = sqrtf(1.f - powf(a.beta2, t));
+  const float step_size = a.lr / bc1;
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 + 3 < a.n) {
+    float4 p = *reinterpret_cast<float4*>(a.params + i4);
+    float4 g = *reinterpret_cast<float4*>(a.grads + i4);
+    float4 m = *reinterpret_cast<float4*>(a.exp_avg + i4);
+    float4 v = *reinterpret_cast<float4*>(a.exp_avg_sq + i4);
+    adam_one(p.x, g.x, m.x, v.x, a, step_size, bc2_sqrt);
+    adam_one(p.y, g.y, m.y, v.y, a, step_size, bc2_sqrt);
+    adam_one(p.z, g.z, m.z, v.z, a, step_size, bc2_sqrt);
+    adam_one(p.w, g.w, m.w, v.w, a, step_size, bc2_sqrt);
+    *reinterpret_cast<float4*>(a.params + i4) = p;
+    if (a.zero_grad) *reinterpret_cast<float4*>(a.grads + i4) = g;
+    *reinterpret_cast<float4*>(a.exp_avg + i4) = m;
+    *reinterpret_cast<float4*>(a.exp_avg_sq + i4) = v;
+  } else {
+    for (int64_t i = i4; i < a.n; ++i) adam_one(a.params[i], a.grads[i], a.exp_avg[i], a.exp_avg_sq[i], a, step_size, bc2_sqrt);
+  }
+}
+
+}  // namespace
+
+hipError_t adam_flat(const AdamArgs& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  if (((uintptr_t)a.params | (uintptr_t)a.grads | (uintptr_t)a.exp_avg | (uintptr_t)a.exp_avg_sq) & 15)
+    return hipErrorInvalidValue;  // float4 access needs 16-B aligned buffers
+  const int64_t threads = (a.n + 3) / 4;
+  hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ia

@@ -455,7 +455,12 @@ class SimpleDAggerTrainer(DAggerTrainer):
                                                                              self.bc_trainer.policy, self.rng)
                 self._device_agg = dagger_engine.DeviceDemoAggregate(self.bc_trainer.policy.device)
                 self._device_counts: Dict[int, int] = {}
+                # demo files are persisted in the background (flushed by save_trainer /
+                # flush_demos and at interpreter exit); BC trains from the device aggregate
                 self._writer = dagger_engine.AsyncDemoWriter()
+                import atexit
+
+                atexit.register(self._writer.close)
                 if expert_trajs:
                     self._device_append(list(expert_trajs), self.round_num)
             elif device_collector is True:
@@ -511,6 +516,11 @@ class SimpleDAggerTrainer(DAggerTrainer):
         seed = int(self.rng.integers(0, 2**31 - 1)) + 7919 * pdist.rank()
         self.bc_trainer.set_demonstrations(dagger_engine.DeviceTransitionsLoader(self._device_agg, self.batch_size, seed))
 
+    def flush_demos(self) -> None:
+        """Block until every collected demonstration is on disk (device collector only)."""
+        if self._writer is not None:
+            self._writer.flush()
+
     def save_trainer(self) -> Tuple[pathlib.Path, pathlib.Path]:
         if self._writer is not None:
             self._writer.flush()  # every demo file of the finished rounds is on disk
@@ -542,5 +552,3 @@ class SimpleDAggerTrainer(DAggerTrainer):
             rounds += 1
         self.last_train_timesteps = collected  # all ranks
         self.last_train_timesteps_local = local
-        if self._writer is not None:
-            self._writer.flush()

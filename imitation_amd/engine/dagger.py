@@ -98,6 +98,76 @@ def policy_actions(policy: ActorCriticPolicy, obs: th.Tensor, deterministic: boo
     return th.max(th.min(a, high), low)
 
 
+class CnnActor:
+    """Graph-static inference of a NatureCNN :class:`ActorCriticPolicy` with discrete actions
+    (the DAgger-Pong expert and learner): three ``conv_fwd`` launches straight on the uint8
+    frames (``in_scale`` = 1/255 replaces the float preprocessing), ``cnn_fc`` and the
+    ``cnn_head`` action choice (csrc/kernels/cnn_infer.hip). The bf16 NHWC conv weights and
+    the (h, w, c)-ordered FC weight are persistent copies refreshed by :meth:`refresh`
+    (call it whenever the module's weights changed); biases and the head are read live."""
+
+    def __init__(self, policy: ActorCriticPolicy, obs_shape: Sequence[int]):
+        from torch import nn
+
+        self.policy = policy
+        fe = policy.features_extractor
+        self.convs = [m for m in fe.cnn if isinstance(m, nn.Conv2d)]
+        self.fc = fe.linear[0]
+        self.head = policy.action_net
+        H, W, C = obs_shape
+        self.strides = [int(c.stride[0]) for c in self.convs]
+        for c in self.convs:
+            H, W, C = (H - c.kernel_size[0]) // c.stride[0] + 1, (W - c.kernel_size[1]) // c.stride[1] + 1, c.out_channels
+        self.out_hwc = (H, W, C)
+        dev = policy.device
+        self.wb = [th.empty(c.out_channels, c.kernel_size[0], c.kernel_size[1], c.in_channels, dtype=th.bfloat16, device=dev)
+                   for c in self.convs]
+        self.fc_w = th.empty(self.fc.out_features, self.fc.in_features, dtype=th.bfloat16, device=dev)
+        self.refresh()
+
+    @staticmethod
+    def applicable(policy: ActorCriticPolicy, obs_shape: Sequence[int]) -> bool:
+        from torch import nn
+
+        from imitation_amd.ops import conv as conv_ops
+        from imitation_amd.rl.torch_layers import NatureCNN
+
+        fe = policy.features_extractor
+        if not isinstance(fe, NatureCNN) or not fe.channels_last_input or not policy.share_features_extractor:
+            return False
+        if not policy.normalize_images or len(list(policy.mlp_extractor.policy_net)) != 0:
+            return False
+        if not isinstance(policy.action_space, spaces.Discrete) or int(policy.action_space.n) > 64:
+            return False
+        mods = list(fe.cnn)
+        convs = [m for m in mods if isinstance(m, nn.Conv2d)]
+        if any(c.padding not in (0, (0, 0)) or c.stride[0] != c.stride[1] or c.dilation not in (1, (1, 1)) or c.groups != 1
+               for c in convs):
+            return False
+        if [type(m) for m in mods] != [nn.Conv2d, nn.ReLU] * len(convs) + [nn.Flatten]:
+            return False
+        lin = list(fe.linear)
+        if len(lin) != 2 or not isinstance(lin[0], nn.Linear) or not isinstance(lin[1], nn.ReLU):
+            return False
+        if lin[0].in_features % 32 or lin[0].out_features % 16:
+            return False
+        return conv_ops.supported((1,) + tuple(obs_shape), [c.weight for c in convs], [c.stride[0] for c in convs])
+
+    @th.no_grad()
+    def refresh(self) -> None:
+        for wb, c in zip(self.wb, self.convs):
+            wb.copy_(c.weight.permute(0, 2, 3, 1))
+        H, W, C = self.out_hwc
+        self.fc_w.copy_(self.fc.weight.view(self.fc.out_features, C, H, W).permute(0, 2, 3, 1).reshape(self.fc.out_features, -1))
+
+    def hidden(self, obs_u8: th.Tensor) -> th.Tensor:
+        C = ops.native()
+        x = obs_u8
+        for i, (wb, c, s) in enumerate(zip(self.wb, self.convs, self.strides)):
+            x = C.conv_fwd(x, wb, c.bias, s, 1.0 / 255.0 if i == 0 else 1.0, True)
+        return C.cnn_fc(x.reshape(x.shape[0], -1), self.fc_w, self.fc.bias)
+
+
 class DeviceDemoAggregate:
     """Flat device-resident (obs, acts) of every aggregated DAgger demonstration, grown by
     capacity doubling; under DP each append is all-gathered so replicas hold the same rows
@@ -231,33 +301,60 @@ class DeviceDAggerCollector:
         self.elapsed = th.as_tensor(st["elapsed"].astype(np.int32), device=dev).contiguous()
         self.ep_ret = th.zeros(N, device=dev)
         self.obs = th.zeros((N,) + self.obs_shape, dtype=odt, device=dev)
-        # one chunk of step records (graph-static)
-        self.c_obs = th.zeros((K, N) + self.obs_shape, dtype=odt, device=dev)
-        self.c_term_obs = th.zeros((K, N) + self.obs_shape, dtype=odt, device=dev)
-        self.c_acts = th.zeros((K, N) + self.act_shape, dtype=adt, device=dev)
-        self.c_rew = th.zeros(K, N, device=dev)
-        self.c_term = th.zeros(K, N, dtype=th.uint8, device=dev)
-        self.c_trunc = th.zeros(K, N, dtype=th.uint8, device=dev)
-        self.c_ep_ret = th.zeros(K, N, device=dev)
-        self.c_ep_len = th.zeros(K, N, dtype=th.int32, device=dev)
+        # two sets of chunk step records (graph-static; double-buffered so the host reads one
+        # chunk's done flags while the next chunk runs)
+        def chunk_set():
+            return dict(obs=th.zeros((K, N) + self.obs_shape, dtype=odt, device=dev),
+                        term_obs=th.zeros((K, N) + self.obs_shape, dtype=odt, device=dev),
+                        acts=th.zeros((K, N) + self.act_shape, dtype=adt, device=dev), rew=th.zeros(K, N, device=dev),
+                        term=th.zeros(K, N, dtype=th.uint8, device=dev), trunc=th.zeros(K, N, dtype=th.uint8, device=dev),
+                        ep_ret=th.zeros(K, N, device=dev), ep_len=th.zeros(K, N, dtype=th.int32, device=dev),
+                        flags=th.zeros(2, K, N, dtype=th.uint8, pin_memory=True), graph=None, ready=None)
+
+        self._sets = [chunk_set(), chunk_set()]
+        self._rec: Dict[str, th.Tensor] = {}
         self._beta = th.ones((), device=dev)
-        self._host_flags = th.zeros(2, K, N, dtype=th.uint8, pin_memory=True)
-        self._graph = None
+        # fused CNN actors (both policies NatureCNN + Discrete): 11 launches per step instead of ~60
+        self.cnn = (self.img and self.discrete and CnnActor.applicable(expert_policy, self.obs_shape)
+                    and CnnActor.applicable(learner_policy, self.obs_shape)
+                    and os.environ.get("IMITATION_AMD_DAGGER_CNN", "1") != "0")
+        if self.cnn:
+            self._actors = (CnnActor(expert_policy, self.obs_shape), CnnActor(learner_policy, self.obs_shape))
+            self._a_exp = th.zeros(N, dtype=th.int64, device=dev)
+            self._a_rob = th.zeros(N, dtype=th.int64, device=dev)
+            self._a_exec = th.zeros(N, dtype=th.int64, device=dev)
+            self._head_ctr = th.zeros(1, dtype=th.int64, device=dev)
+            self._head_seed = int(rng.integers(0, 2**62))
         self._max_steps = int(self.nat.max_episode_steps)
         self.last_obs: Optional[th.Tensor] = None
         self.last_acts: Optional[th.Tensor] = None
         self.steps_collected = 0
 
     # -------------------------------------------------------------- device steps
-    def _env_args(self, mode: int, k: int = 0, actions: Optional[th.Tensor] = None) -> Dict:
+    def _env_args(self, mode: int, k: int = 0, actions: Optional[th.Tensor] = None, b: Optional[Dict] = None) -> Dict:
         d = dict(env=self.nat.env_id, N=self.N, max_steps=self._max_steps, mode=mode, state=self.state, rng=self.env_rng,
                  elapsed=self.elapsed, ep_ret=self.ep_ret, obs=self.obs)
         if mode == 0:
-            d.update(actions=actions, rew=self.c_rew[k], term=self.c_term[k], trunc=self.c_trunc[k],
-                     term_obs=self.c_term_obs[k], ep_ret_out=self.c_ep_ret[k], ep_len_out=self.c_ep_len[k])
+            d.update(actions=actions, rew=b["rew"][k], term=b["term"][k], trunc=b["trunc"][k], term_obs=b["term_obs"][k],
+                     ep_ret_out=b["ep_ret"][k], ep_len_out=b["ep_len"][k])
         return d
 
-    def _step(self, k: int) -> None:
+    def _step_cnn(self, k: int, b: Dict) -> None:
+        C = self._C
+        ea, la = self._actors
+        h_e = ea.hidden(self.obs)
+        C.cnn_head(h_e, self.expert.action_net.weight, self.expert.action_net.bias, 0, 0, None, self._a_exp,
+                   rec_out=b["acts"][k])
+        h_l = la.hidden(self.obs)
+        C.cnn_head(h_l, self.learner.action_net.weight, self.learner.action_net.bias, 1, self._head_seed, self._head_ctr,
+                   self._a_rob, mix_expert=self._a_exp, beta=self._beta, exec_out=self._a_exec)
+        d = self._env_args(0, k, self._a_exec, b)
+        d["obs_rec"] = b["obs"][k]
+        C.dagger_env_step(d)
+
+    def _step(self, k: int, b: Dict) -> None:
+        if self.cnn:
+            return self._step_cnn(k, b)
         obs = self.obs
         with th.no_grad():
             a_exp = policy_actions(self.expert, obs, True)
@@ -266,33 +363,62 @@ class DeviceDAggerCollector:
         if not self.discrete:
             learner_turn = learner_turn.reshape((self.N,) + (1,) * len(self.act_shape))
         a_exec = th.where(learner_turn, a_rob.to(a_exp.dtype), a_exp)
-        self.c_obs[k].copy_(obs)
-        self.c_acts[k].copy_(a_exp.reshape(self.c_acts[k].shape))
-        self._C.dagger_env_step(self._env_args(0, k, a_exec.contiguous() if self.discrete else a_exec.float().contiguous()))
+        b["obs"][k].copy_(obs)
+        b["acts"][k].copy_(a_exp.reshape(b["acts"][k].shape))
+        self._C.dagger_env_step(self._env_args(0, k, a_exec.contiguous() if self.discrete else a_exec.float().contiguous(), b))
 
-    def _run_chunk(self) -> None:
+    def _run_chunk(self, b: Dict) -> None:
         if not self.use_graph:
             for k in range(self.chunk):
-                self._step(k)
+                self._step(k, b)
             return
-        if self._graph is None:
-            # the first chunk runs eagerly (also the allocator warm-up); later chunks replay
+        if b["graph"] is None:
+            # the first chunk of each buffer set runs eagerly (also the allocator warm-up);
+            # later chunks replay
             for k in range(self.chunk):
-                self._step(k)
+                self._step(k, b)
             g = th.cuda.CUDAGraph()
             try:
                 # capture only: nothing in this block executes until replay()
                 with th.cuda.graph(g):
                     for k in range(self.chunk):
-                        self._step(k)
-                self._graph = g
+                        self._step(k, b)
+                b["graph"] = g
             except RuntimeError as e:  # e.g. an op that syncs: stay eager
                 import logging
 
                 logging.getLogger(__name__).warning("DAgger step graph capture failed (%s); stepping eagerly", e)
                 self.use_graph = False
             return
-        self._graph.replay()
+        b["graph"].replay()
+
+    def _record(self, i: int, b: Dict) -> None:
+        """Enqueue: chunk ``i``'s records -> the round buffers (grown by doubling), its done
+        flags -> pinned host memory, and the event marking both."""
+        K = self.chunk
+        need = (i + 1) * K
+        keys = ("obs", "term_obs", "acts", "rew")
+        cap = self._rec["obs"].shape[0] if self._rec else 0
+        if need > cap:
+            new_cap = max(need, 2 * cap, 8 * K)
+            for key in keys:
+                src = b[key]
+                t = th.empty((new_cap,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+                if cap:
+                    t[: i * K].copy_(self._rec[key][: i * K])
+                self._rec[key] = t
+        for key in keys:
+            self._rec[key][i * K : need].copy_(b[key])
+        b["flags"][0].copy_(b["term"], non_blocking=True)
+        b["flags"][1].copy_(b["trunc"], non_blocking=True)
+        ev = th.cuda.Event()
+        ev.record()
+        b["ready"] = ev
+
+    def _launch(self, i: int) -> None:
+        b = self._sets[i % 2]
+        self._run_chunk(b)
+        self._record(i, b)
 
     def reset(self) -> None:
         self._C.dagger_env_step(self._env_args(1))
@@ -302,30 +428,25 @@ class DeviceDAggerCollector:
         """One round with the reference's ``generate_trajectories`` stopping rule."""
         dev, N, K = self.device, self.N, self.chunk
         self._beta.fill_(float(beta))
+        if self.cnn:
+            for actor in self._actors:
+                actor.refresh()  # the learner changed since the last round
         self.reset()
-        rec_obs: List[th.Tensor] = []  # per chunk [K, N, ...] copies
-        rec_term: List[th.Tensor] = []
-        rec_acts: List[th.Tensor] = []
-        rec_rew: List[th.Tensor] = []
         active = np.ones(N, dtype=bool)
         start = np.zeros(N, dtype=np.int64)
         finished: List[Tuple[int, int, int]] = []  # (env, first step, last step)
         n_steps_done = 0
-        t_base = 0
         satisfied = False
-        while active.any():
-            self._run_chunk()
-            rec_obs.append(self.c_obs.clone())
-            rec_term.append(self.c_term_obs.clone())
-            rec_acts.append(self.c_acts.clone())
-            rec_rew.append(self.c_rew.clone())
-            self._host_flags[0].copy_(self.c_term, non_blocking=True)
-            self._host_flags[1].copy_(self.c_trunc, non_blocking=True)
-            th.cuda.current_stream(dev).synchronize()
-            done_chunk = (self._host_flags[0].numpy() | self._host_flags[1].numpy()).astype(bool)
+        i = 0
+        self._launch(0)
+        while True:
+            # keep the next chunk running while the host reads this one's flags
+            self._launch(i + 1)
+            b = self._sets[i % 2]
+            b["ready"].synchronize()
+            done_chunk = (b["flags"][0].numpy() | b["flags"][1].numpy()).astype(bool)
+            t_base = i * K
             for k in range(K):
-                if not active.any():
-                    break
                 t = t_base + k
                 dones = done_chunk[k] & active
                 for n in np.flatnonzero(dones):
@@ -336,12 +457,14 @@ class DeviceDAggerCollector:
                     satisfied = len(finished) >= min_episodes and n_steps_done >= min_timesteps
                 if satisfied:
                     active &= ~dones
-            t_base += K
+                if not active.any():
+                    break
+            i += 1
+            if not active.any():
+                break
+        t_base = i * K  # chunks whose steps count (the speculative next one is discarded)
         self.steps_collected = t_base * N
-        obs_all = th.cat(rec_obs)  # [T, N, ...]
-        term_all = th.cat(rec_term)
-        acts_all = th.cat(rec_acts)
-        rew_all = th.cat(rec_rew)
+        obs_all, term_all, acts_all, rew_all = (self._rec[k] for k in ("obs", "term_obs", "acts", "rew"))  # [T, N, ...]
         # flat row indices (t * N + n) of every finished episode, in finishing order
         rows = np.concatenate([np.arange(s, e + 1) * N + n for (n, s, e) in finished]) if finished else np.zeros(0, np.int64)
         ends = np.asarray([e * N + n for (n, s, e) in finished], dtype=np.int64)

@@ -1,0 +1,187 @@
+"""Fused flat-buffer Adam / AdamW (SURVEY §2.2 "fused optimizer step", K26).
+
+The reference trains with ``th.optim.Adam`` (BC ``bc.py:284``, discriminator
+``common.py:123``) and ``th.optim.AdamW`` (preference reward ``preference_comparisons.py:1192``).
+PyTorch's capturable foreach Adam is ~8 multi-tensor launches per step; for the KB-MB
+models here those launches ARE the optimizer's cost. :class:`FusedAdam` re-points every
+parameter of a group at a view of ONE contiguous fp32 buffer (and every ``.grad`` at a
+view of one gradient buffer, which is also the natural DP all-reduce bucket), so a step
+is one device step-counter increment plus one ``adam_flat`` launch
+(csrc/kernels/optim.hip) that also clears the gradient it consumed. Everything lives on
+the device, so the step is HIP-graph capturable.
+
+On the CPU the same update runs as plain torch ops (numerics tests compare both against
+``th.optim.Adam`` / ``AdamW``). ``state_dict`` has torch's per-parameter layout
+(``step`` / ``exp_avg`` / ``exp_avg_sq``), so checkpoints interchange with torch Adam.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, Iterable, List, Optional
+
+import torch as th
+
+
+class FusedAdam(th.optim.Optimizer):
+    """Adam (``decoupled_weight_decay=False``) or AdamW over flat per-group buffers."""
+
+    def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, amsgrad: bool = False, *, maximize: bool = False,
+                 decoupled_weight_decay: bool = False, capturable: bool = True, foreach: Optional[bool] = None,
+                 differentiable: bool = False, fused: Optional[bool] = None):
+        if amsgrad:
+            raise ValueError("FusedAdam does not implement amsgrad")
+        if differentiable:
+            raise ValueError("FusedAdam is not differentiable")
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=maximize,
+                        decoupled_weight_decay=decoupled_weight_decay, capturable=True)
+        super().__init__(params, defaults)
+        self._flat: List[Dict[str, Any]] = []
+        for group in self.param_groups:
+            self._flat.append(self._pack_group(group))
+
+    # ------------------------------------------------------------------ layout
+    def _pack_group(self, group) -> Dict[str, Any]:
+        ps = [p for p in group["params"]]
+        if not ps:
+            return {"params": [], "n": 0}
+        dev = ps[0].device
+        if any(p.device != dev or p.dtype != th.float32 for p in ps):
+            raise ValueError("FusedAdam needs fp32 parameters on one device")
+        n = sum(p.numel() for p in ps)
+        pad = (-n) % 4  # float4 kernel access
+        flat = th.zeros(n + pad, device=dev)
+        grad = th.zeros(n + pad, device=dev)
+        m = th.zeros(n + pad, device=dev)
+        v = th.zeros(n + pad, device=dev)
+        step = th.zeros(1, device=dev)
+        views = []
+        off = 0
+        for p in ps:
+            k = p.numel()
+            flat[off : off + k].copy_(p.detach().reshape(-1))
+            if p.grad is not None:
+                grad[off : off + k].copy_(p.grad.detach().reshape(-1))
+            p.data = flat[off : off + k].view_as(p)
+            gv = grad[off : off + k].view_as(p)
+            p.grad = gv
+            views.append((off, k, gv))
+            self.state[p] = {"step": step, "exp_avg": m[off : off + k].view_as(p), "exp_avg_sq": v[off : off + k].view_as(p)}
+            off += k
+        return {"params": ps, "flat": flat, "grad": grad, "m": m, "v": v, "step": step, "views": views, "n": n}
+
+    @property
+    def flat_grads(self) -> List[th.Tensor]:
+        """The gradient bucket of every group (what a DP all-reduce should reduce)."""
+        return [f["grad"] for f in self._flat if f["n"]]
+
+    def _bind_grads(self, f: Dict[str, Any]) -> None:
+        """Re-point ``.grad`` at the bucket views if something replaced them (e.g. a module's
+        ``zero_grad()`` set them to None or autograd installed a fresh tensor)."""
+        for p, (off, k, gv) in zip(f["params"], f["views"]):
+            g = p.grad
+            if g is None:
+                gv.zero_()
+            elif g.data_ptr() != gv.data_ptr():
+                gv.copy_(g)
+            else:
+                continue
+            p.grad = gv
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """Zero the gradient buckets; ``.grad`` stays bound to them (``set_to_none`` is moot)."""
+        for f in self._flat:
+            if f["n"]:
+                f["grad"].zero_()
+                self._bind_grads(f)
+
+    # ------------------------------------------------------------------ step
+    @th.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with th.enable_grad():
+                loss = closure()
+        from imitation_amd import ops
+
+        for group, f in zip(self.param_groups, self._flat):
+            if not f["n"]:
+                continue
+            self._bind_grads(f)
+            b1, b2 = group["betas"]
+            f["step"].add_(1.0)
+            if f["flat"].is_cuda and ops.use_kernel(f["flat"]):
+                ops.native().adam_flat(f["flat"], f["grad"], f["m"], f["v"], f["step"], float(group["lr"]), float(b1),
+                                       float(b2), float(group["eps"]), float(group["weight_decay"]),
+                                       bool(group["decoupled_weight_decay"]), bool(group["maximize"]), True)
+            else:
+                self._step_reference(group, f)
+        return loss
+
+    @staticmethod
+    def _step_reference(group, f) -> None:
+        """Same update as the kernel, in torch ops (CPU / fallback)."""
+        p, g, m, v = f["flat"], f["grad"], f["m"], f["v"]
+        b1, b2 = group["betas"]
+        lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]
+        t = f["step"]
+        gr = -g if group["maximize"] else g.clone()
+        if wd != 0.0:
+            if group["decoupled_weight_decay"]:
+                p.mul_(1.0 - lr * wd)
+            else:
+                gr.add_(p, alpha=wd)
+        m.lerp_(gr, 1.0 - b1)
+        v.mul_(b2).addcmul_(gr, gr, value=1.0 - b2)
+        step_size = lr / (1.0 - b1**t)
+        denom = v.sqrt() / th.sqrt(1.0 - b2**t) + eps
+        p.sub_(step_size * (m / denom))
+        g.zero_()
+
+    # ------------------------------------------------------------------ checkpoints
+    def load_state_dict(self, state_dict: Dict[str, Any]) -> None:
+        """Load a torch-Adam-layout state and copy it into the flat buffers (the loaded
+        tensors would otherwise replace the views)."""
+        super().load_state_dict(state_dict)
+        for group, f in zip(self.param_groups, self._flat):
+            for key in ("lr", "eps", "weight_decay", "maximize"):
+                group.setdefault(key, self.defaults[key])
+            group["betas"] = tuple(group["betas"])
+            group.setdefault("decoupled_weight_decay", self.defaults["decoupled_weight_decay"])
+            if not f["n"]:
+                continue
+            steps = []
+            with th.no_grad():
+                for p, (off, k, _) in zip(f["params"], f["views"]):
+                    st = self.state.get(p, {})
+                    if "exp_avg" in st:
+                        f["m"][off : off + k].copy_(st["exp_avg"].reshape(-1))
+                        f["v"][off : off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                        steps.append(float(st["step"]))
+                    self.state[p] = {"step": f["step"], "exp_avg": f["m"][off : off + k].view_as(p),
+                                     "exp_avg_sq": f["v"][off : off + k].view_as(p)}
+                f["step"].fill_(max(steps) if steps else 0.0)
+
+
+class FusedAdamW(FusedAdam):
+    """AdamW (decoupled weight decay, default 1e-2 like ``th.optim.AdamW``)."""
+
+    def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, amsgrad: bool = False, **kwargs):
+        kwargs.pop("decoupled_weight_decay", None)
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
+                         decoupled_weight_decay=True, **kwargs)
+
+
+def fused_for(optimizer_cls, device) -> Optional[type]:
+    """The fused replacement of ``optimizer_cls`` on ``device`` (None = keep the given class).
+    Exactly ``th.optim.Adam`` / ``th.optim.AdamW`` on a GPU, unless ``IMITATION_AMD_FUSED_ADAM=0``."""
+    import os
+
+    if th.device(device).type != "cuda" or os.environ.get("IMITATION_AMD_FUSED_ADAM", "1") == "0":
+        return None
+    if optimizer_cls is th.optim.Adam:
+        return FusedAdam
+    if optimizer_cls is th.optim.AdamW:
+        return FusedAdamW
+    return None

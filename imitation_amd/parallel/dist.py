@@ -190,6 +190,30 @@ class GradBucket:
             self.flat.copy_(buf)
 
 
+class FlatGradBucket:
+    """DP bucket over an optimizer that already keeps its gradients in flat buffers
+    (:class:`imitation_amd.ops.optim.FusedAdam`): one mean all-reduce per buffer, no
+    re-pointing of ``.grad``."""
+
+    def __init__(self, optimizer):
+        self.optimizer = optimizer
+
+    def bind(self) -> None:
+        for f in getattr(self.optimizer, "_flat", []):
+            if f["n"]:
+                self.optimizer._bind_grads(f)
+
+    def zero(self) -> None:
+        self.optimizer.zero_grad()
+
+    def allreduce(self) -> None:
+        if world_size() <= 1:
+            return
+        self.bind()
+        for flat in self.optimizer.flat_grads:
+            allreduce_grads_flat(flat)
+
+
 def allreduce_grads(params: Iterable[torch.nn.Parameter]) -> None:
     """One-shot mean all-reduce of ``.grad`` over ranks (pack -> 1 collective -> unpack)."""
     if world_size() <= 1:

@@ -54,3 +54,25 @@ def test_pickle_refused(tmp_path):
     p.write_bytes(b"\x80\x04N.")
     with pytest.raises(Exception):
         serialize.load(p)
+
+
+def test_arrow_native_dataset_equals_from_dict(tmp_path):
+    """The zero-copy nested-Arrow build has from_dict's exact features and content."""
+    import datasets
+
+    from imitation_amd.data import huggingface_utils as hu
+
+    rng = np.random.default_rng(0)
+    for obs_shape, act_shape, with_rew in [((84, 84, 4), (), True), ((5,), (3,), False), ((2, 3), (), True)]:
+        trajs = []
+        for L in (7, 3):
+            obs = (rng.integers(0, 255, (L + 1,) + obs_shape, dtype=np.uint8) if len(obs_shape) == 3
+                   else rng.standard_normal((L + 1,) + obs_shape).astype(np.float32))
+            acts = rng.integers(0, 6, L) if act_shape == () else rng.standard_normal((L,) + act_shape).astype(np.float32)
+            kw = dict(obs=obs, acts=acts, infos=[{"k": i} for i in range(L)], terminal=bool(L % 2))
+            trajs.append(types.TrajectoryWithRew(rews=rng.standard_normal(L).astype(np.float32), **kw) if with_rew
+                         else types.Trajectory(**kw))
+        fast = hu._fast_dataset(trajs, None)
+        slow = datasets.Dataset.from_dict(hu.trajectories_to_dict(trajs))
+        assert fast is not None and fast.features == slow.features
+        assert fast.data.table.equals(slow.data.table.cast(fast.data.table.schema))

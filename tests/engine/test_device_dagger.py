@@ -86,7 +86,7 @@ def test_device_dagger_pong_rounds(tmp_path):
     tr.train(1000, rollout_round_min_episodes=1, rollout_round_min_timesteps=400,
              bc_train_kwargs=dict(n_epochs=1, progress_bar=False, log_interval=10**9))
     assert tr.round_num >= 1
-    assert col._graph is not None, "the chunk step was not graph-captured"
+    assert all(b["graph"] is not None for b in col._sets), "the chunk steps were not graph-captured"
     n_rows = sum(len(t) for t in tr._all_demos)
     assert len(tr._device_agg) == n_rows and n_rows >= 400
     # finished episodes only, expert actions recorded, obs length = acts + 1
@@ -97,6 +97,7 @@ def test_device_dagger_pong_rounds(tmp_path):
     np.testing.assert_array_equal(tr._device_agg.obs[: len(first)].cpu().numpy(), first.obs[:-1])
     np.testing.assert_array_equal(tr._device_agg.acts[: len(first)].cpu().numpy(), first.acts)
     # reference-format demo files were written for every trajectory of round 0
+    tr.flush_demos()
     files = tr._store.files(0)
     assert len(files) >= 1
     assert any(not th.equal(a, b) for a, b in zip(before, learner.parameters()))
@@ -106,3 +107,44 @@ def test_device_dagger_pong_rounds(tmp_path):
 
     with th.no_grad():
         np.testing.assert_array_equal(policy_actions(expert, o, True).cpu().numpy(), first.acts[:16])
+
+
+@gpu
+def test_cnn_actor_matches_policy():
+    """Fused NatureCNN inference (conv_fwd x3 + cnn_fc + cnn_head) == policy argmax; Gumbel
+    samples follow the policy's action probabilities."""
+    from imitation_amd import ops
+    from imitation_amd.engine.dagger import CnnActor
+    from imitation_amd.envs.vec_env import native_spaces
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+
+    obs_space, act_space = native_spaces("PongNoFrameskip-v4")
+    th.manual_seed(0)
+    pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
+    assert CnnActor.applicable(pol, obs_space.shape)
+    actor = CnnActor(pol, obs_space.shape)
+    B = 64
+    x = th.randint(0, 255, (B, 84, 84, 4), dtype=th.uint8, device="cuda")
+    with th.no_grad():
+        feats = pol.extract_features(x)
+        logits = pol.action_net(feats)
+        h = actor.hidden(x)
+    th.testing.assert_close(h, feats, rtol=3e-2, atol=3e-2 * float(feats.abs().max()))
+    C = ops.native()
+    out = th.zeros(B, dtype=th.int64, device="cuda")
+    C.cnn_head(h, pol.action_net.weight, pol.action_net.bias, 0, 0, None, out)
+    ref = (h @ pol.action_net.weight.T + pol.action_net.bias).argmax(-1)
+    assert th.equal(out, ref)
+    agree = (out == logits.argmax(-1)).float().mean().item()
+    assert agree > 0.9, agree  # bf16 convs: near-ties may flip
+    # Gumbel-max sampling frequencies ~ softmax(logits) for one row, counter advances per call
+    ctr = th.zeros(1, dtype=th.int64, device="cuda")
+    hrow = h[:1].expand(B, -1).contiguous()
+    counts = th.zeros(act_space.n, device="cuda")
+    for _ in range(200):
+        C.cnn_head(hrow, pol.action_net.weight, pol.action_net.bias, 1, 123, ctr, out)
+        counts += th.bincount(out, minlength=act_space.n).float()
+    assert int(ctr.item()) == 200
+    p = th.softmax(hrow[0] @ pol.action_net.weight.T + pol.action_net.bias, -1)
+    freq = counts / counts.sum()
+    assert float((freq - p).abs().max()) < 0.02

@@ -1,0 +1,110 @@
+"""FusedAdam / FusedAdamW (ops/optim.py, csrc/kernels/optim.hip) vs torch.optim.Adam / AdamW."""
+
+import pytest
+import torch as th
+
+from imitation_amd.ops import optim as optim_ops
+
+
+def _nets(device, seed=0):
+    th.manual_seed(seed)
+    a = th.nn.Sequential(th.nn.Linear(7, 13), th.nn.Tanh(), th.nn.Linear(13, 3)).to(device)
+    b = th.nn.Sequential(th.nn.Linear(7, 13), th.nn.Tanh(), th.nn.Linear(13, 3)).to(device)
+    b.load_state_dict(a.state_dict())
+    return a, b
+
+
+def _run(device, fused_cls, torch_cls, steps=6, **kw):
+    a, b = _nets(device)
+    oa = fused_cls(a.parameters(), **kw)
+    ob = torch_cls(b.parameters(), **kw)
+    g = th.Generator().manual_seed(1)
+    for _ in range(steps):
+        x = th.randn(16, 7, generator=g).to(device)
+        for net, opt in ((a, oa), (b, ob)):
+            opt.zero_grad()
+            net(x).square().mean().backward()
+            opt.step()
+    return a, b, oa, ob
+
+
+@pytest.mark.parametrize("kw", [dict(lr=1e-2), dict(lr=3e-3, weight_decay=0.1), dict(lr=1e-2, betas=(0.8, 0.99), eps=1e-6),
+                                dict(lr=1e-2, maximize=True)])
+def test_fused_adam_matches_torch_cpu(kw):
+    a, b, oa, ob = _run("cpu", optim_ops.FusedAdam, th.optim.Adam, **kw)
+    for p, q in zip(a.parameters(), b.parameters()):
+        th.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_adamw_matches_torch_cpu():
+    a, b, oa, ob = _run("cpu", optim_ops.FusedAdamW, th.optim.AdamW, lr=1e-2, weight_decay=0.05)
+    for p, q in zip(a.parameters(), b.parameters()):
+        th.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_adam_state_dict_roundtrip_with_torch_adam():
+    a, b, oa, ob = _run("cpu", optim_ops.FusedAdam, th.optim.Adam, lr=1e-2)
+    c, _ = _nets("cpu")
+    c.load_state_dict(b.state_dict())
+    oc = optim_ops.FusedAdam(c.parameters(), lr=1e-2)
+    oc.load_state_dict(ob.state_dict())  # torch Adam state -> flat buffers
+    x = th.randn(4, 7)
+    for net, opt in ((b, ob), (c, oc)):
+        opt.zero_grad()
+        net(x).sum().backward()
+        opt.step()
+    for p, q in zip(b.parameters(), c.parameters()):
+        th.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    assert float(oc.state[next(iter(c.parameters()))]["step"]) == 7.0
+
+
+def test_grads_stay_bound_after_module_zero_grad():
+    a, _ = _nets("cpu")
+    opt = optim_ops.FusedAdam(a.parameters(), lr=1e-2)
+    a.zero_grad()  # nn.Module sets .grad = None
+    a(th.randn(3, 7)).sum().backward()
+    opt.step()  # re-binds and consumes the fresh grads
+    assert all(p.grad is not None and float(p.grad.abs().sum()) == 0.0 for p in a.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls,tcls,kw", [(optim_ops.FusedAdam, th.optim.Adam, dict(lr=1e-2, weight_decay=0.01)),
+                                         (optim_ops.FusedAdamW, th.optim.AdamW, dict(lr=1e-2, weight_decay=0.05))])
+def test_fused_adam_kernel_matches_torch(cls, tcls, kw):
+    a, b, oa, ob = _run("cuda", cls, tcls, steps=8, **kw)
+    for p, q in zip(a.parameters(), b.parameters()):
+        th.testing.assert_close(p, q, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.gpu
+def test_fused_adam_graph_captured_bc_step_matches_eager():
+    """BC on the GPU picks FusedAdam; the graphed minibatch step equals the eager one."""
+    import os
+
+    import numpy as np
+
+    from imitation_amd.algorithms import bc
+    from imitation_amd.envs import spaces
+    from imitation_amd.util import logger
+
+    obs_space = spaces.Box(-1, 1, (5,))
+    act_space = spaces.Discrete(3)
+    rng = np.random.default_rng(0)
+    obs = rng.standard_normal((256, 5)).astype(np.float32)
+    acts = rng.integers(0, 3, 256)
+    from imitation_amd.data import types
+
+    demos = types.TransitionsMinimal(obs=obs, acts=acts, infos=np.array([{}] * 256))
+    res = []
+    for graph in ("1", "0"):
+        os.environ["IMITATION_AMD_BC_GRAPH"] = graph
+        th.manual_seed(0)
+        t = bc.BC(observation_space=obs_space, action_space=act_space, rng=np.random.default_rng(0), demonstrations=demos,
+                  batch_size=32, device="cuda", custom_logger=logger.configure("/tmp/ia_fa", format_strs=[]))
+        t._demo_data_loader._rng = np.random.default_rng(5)
+        assert isinstance(t.optimizer, optim_ops.FusedAdam)
+        t.train(n_batches=20, progress_bar=False, log_interval=10**9)
+        res.append([p.detach().cpu().clone() for p in t.policy.parameters()])
+    os.environ.pop("IMITATION_AMD_BC_GRAPH", None)
+    for p, q in zip(*res):
+        th.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)

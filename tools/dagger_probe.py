@@ -33,14 +33,14 @@ def main():
         n_b = len(tr._device_agg) // tr.batch_size
         print(f"round {r}: collect {1e3*(t1-t0):.1f} ms ({col.steps_collected} env steps, {steps} kept, "
               f"{1e6*(t1-t0)/max(1,col.steps_collected/col.N):.1f} us/step) aggregate {1e3*(t2-t1):.1f} ms "
-              f"bc {1e3*(t3-t2):.1f} ms ({n_b} batches, {1e3*(t3-t2)/max(1,n_b):.3f} ms/batch) graph={col._graph is not None}",
+              f"bc {1e3*(t3-t2):.1f} ms ({n_b} batches, {1e3*(t3-t2)/max(1,n_b):.3f} ms/batch) graph={col._sets[0]['graph'] is not None}",
               flush=True)
     tr._writer.flush()
     # chunk replay alone
     th.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(20):
-        col._run_chunk()
+        col._run_chunk(col._sets[0])
     th.cuda.synchronize()
     print(f"chunk replay: {1e3*(time.perf_counter()-t0)/20:.3f} ms per {col.chunk} steps", flush=True)
 
