@@ -98,11 +98,16 @@ def make_step(name, device, rank, args):
 
         return b, step, "env-steps/s", tr.policy, b.venv
     if name == "preference_walker2d":
-        b = models.build(name, device=device, seed=args.seed, num_iterations=1)
+        # the reference schedule (5 iterations over 1e6 steps, 5000 comparisons); warm-up
+        # steps run the initial iteration (initial comparisons x epoch multiplier 200), each
+        # timed step is one later iteration: agent training (200K env steps) + sampling,
+        # fragmenting, preference gathering and 3 reward epochs over the growing dataset
+        b = models.build(name, device=device, seed=args.seed)
         tr = b.trainer
+        it = tr.train_iter(b.extras["total_timesteps"], total_comparisons=args.pref_comparisons)
 
         def step():
-            tr.train(b.env_steps_per_round, total_comparisons=args.pref_comparisons)
+            next(it)
             return b.env_steps_per_round
 
         return b, step, "env-steps/s", b.extras["agent"].policy, b.venv
@@ -147,7 +152,7 @@ def main():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--device", default=None)
     p.add_argument("--dagger-round-steps", type=int, default=2048)
-    p.add_argument("--pref-comparisons", type=int, default=64)
+    p.add_argument("--pref-comparisons", type=int, default=5000)
     p.add_argument("--out", default=None, help="append JSON lines to this file (rank 0)")
     args = p.parse_args()
     import torch as th

@@ -213,15 +213,25 @@ def dagger_pong(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "Pong
 
 
 def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "seals/Walker2d-v1",
-                        num_iterations: int = 5, fragment_length: int = 100, n_steps: int = 256,
-                        log_dir: Optional[str] = None, engine: str = "auto", **overrides) -> Built:
-    """Preference comparisons on Walker2d: PPO agent on the learned reward, ``BasicRewardNet``
-    (RunningNorm input), synthetic oracle preferences from the env's true reward. The agent
-    trains and samples on the GPU (:class:`~imitation_amd.engine.preference.DeviceAgentTrainer`)
-    when eligible."""
+                        num_iterations: int = 5, fragment_length: int = 100, total_timesteps: int = 1_000_000,
+                        n_steps: Optional[int] = None, log_dir: Optional[str] = None, engine: str = "auto",
+                        **overrides) -> Built:
+    """Preference comparisons on Walker2d with the reference's ``seals_walker`` named config
+    (``scripts/config/train_preference_comparisons.py:179-203`` + ``train_defaults``):
+    MlpPolicy pi/vf [64, 64] ReLU with the policy ingredient's NormalizeFeaturesExtractor,
+    PPO rl batch 8192 (n_steps = 8192 / n_envs), minibatch 128, 20 epochs, clip 0.4,
+    ent 1.306e-4, gae_lambda 0.92, gamma 0.98, lr 1.386e-4, max_grad_norm 0.6, vf 0.617;
+    ``BasicRewardNet`` (RunningNorm input), reward trainer 3 epochs (batch 32, AdamW 1e-3),
+    fragment length 100, 5 iterations over 1e6 timesteps, hyperbolic query schedule,
+    ``initial_comparison_frac`` 0.1 and the library-default ``initial_epoch_multiplier`` 200,
+    no exploration (``n_steps`` overrides the rollout length for quick tests). The agent trains and samples on the GPU
+    (:class:`~imitation_amd.engine.preference.DeviceAgentTrainer`) when eligible."""
+    from torch import nn
+
     from imitation_amd.algorithms import preference_comparisons as pc
-    from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
+    from imitation_amd.policies.base import NormalizeFeaturesExtractor
     from imitation_amd.rewards.reward_nets import BasicRewardNet
+    from imitation_amd.rl.policies import ActorCriticPolicy
     from imitation_amd.rl.ppo import PPO
     from imitation_amd.util.networks import RunningNorm
     from imitation_amd.util.util import make_vec_env
@@ -231,8 +241,11 @@ def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str
     venv = make_vec_env(env_id, rng=rng, n_envs=n_envs)
     log = _logger(log_dir)
     reward_net = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm).to(dev)
-    agent = PPO(FeedForward32Policy, venv, n_steps=n_steps, batch_size=64, n_epochs=5, device=dev, seed=seed,
-                policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor,
+    agent = PPO(ActorCriticPolicy, venv, n_steps=n_steps or 8192 // n_envs, batch_size=128, n_epochs=20, clip_range=0.4,
+                ent_coef=0.00013057334805552262, gae_lambda=0.92, gamma=0.98, learning_rate=0.000138575372312869,
+                max_grad_norm=0.6, vf_coef=0.6167177795726859, device=dev, seed=seed,
+                policy_kwargs=dict(activation_fn=nn.ReLU, net_arch=dict(pi=[64, 64], vf=[64, 64]),
+                                   features_extractor_class=NormalizeFeaturesExtractor,
                                    features_extractor_kwargs=dict(normalize_class=RunningNorm)))
     gen_cls = pc.AgentTrainer
     if engine in ("auto", "device"):
@@ -243,19 +256,20 @@ def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str
             gen_cls = device_pref.DeviceAgentTrainer
         elif engine == "device":
             raise ValueError(f"device engine not applicable: {why}")
-    gen = gen_cls(algorithm=agent, reward_fn=reward_net, venv=venv, exploration_frac=0.05, rng=rng, custom_logger=log)
-    kw = dict(fragmenter=pc.RandomFragmenter(rng=rng, custom_logger=log),
+    gen = gen_cls(algorithm=agent, reward_fn=reward_net, venv=venv, exploration_frac=0.0, rng=rng, custom_logger=log)
+    kw = dict(fragmenter=pc.RandomFragmenter(rng=rng, custom_logger=log, warning_threshold=0),
               preference_gatherer=pc.SyntheticGatherer(rng=rng, custom_logger=log),
               reward_trainer=pc.BasicRewardTrainer(preference_model=pc.PreferenceModel(reward_net),
                                                    loss=pc.CrossEntropyRewardLoss(), rng=rng, epochs=3,
                                                    custom_logger=log),
               fragment_length=fragment_length, transition_oversampling=1, initial_comparison_frac=0.1,
-              allow_variable_horizon=False, initial_epoch_multiplier=4, query_schedule="hyperbolic")
+              allow_variable_horizon=False, initial_epoch_multiplier=200.0, query_schedule="hyperbolic")
     kw.update(overrides)
     # all components carry their own seeded rng, so (as the reference requires) none is passed here
     trainer = pc.PreferenceComparisons(gen, reward_net, num_iterations=num_iterations, custom_logger=log, rng=None, **kw)
-    return Built(trainer, venv, "preference_walker2d", env_id, n_steps * n_envs,
-                 {"agent": agent, "engine": "device" if gen_cls is not pc.AgentTrainer else "host"})
+    return Built(trainer, venv, "preference_walker2d", env_id, total_timesteps // num_iterations,
+                 {"agent": agent, "engine": "device" if gen_cls is not pc.AgentTrainer else "host",
+                  "total_timesteps": total_timesteps})
 
 
 def bc_cartpole(device=None, seed: int = 0, env_id: str = "CartPole-v1", n_demo_timesteps: int = 4000,

@@ -136,3 +136,82 @@ def device_gail_dp_worker(rank, world, seed, batch):
         out["max_dev"] = max(float((q.detach() - r).abs().max()) for q, r in zip(pol.parameters(), p_dev))
         out["max_ref"] = max(float(q.detach().abs().max()) for q in pol.parameters())
     return out
+
+
+def _pref_dataset(P: int, L: int, seed: int):
+    from imitation_amd.algorithms import preference_comparisons as pc
+    from imitation_amd.data import types
+
+    rng = np.random.default_rng(seed)
+
+    def frag():
+        return types.TrajectoryWithRew(obs=rng.standard_normal((L + 1, 5)).astype(np.float32),
+                                       acts=rng.standard_normal((L, 2)).astype(np.float32), infos=None, terminal=False,
+                                       rews=rng.standard_normal(L).astype(np.float32))
+
+    ds = pc.PreferenceDataset()
+    pairs = [(frag(), frag()) for _ in range(P)]
+    ds.push(pairs, rng.uniform(0, 1, P).astype(np.float32))
+    return ds
+
+
+def pref_reward_dp_worker(rank, world, P, L, mb, epochs, seed):
+    """BasicRewardTrainer on a replicated preference dataset; returns the trained parameters."""
+    import torch as th
+
+    from imitation_amd.algorithms import preference_comparisons as pc
+    from imitation_amd.envs import spaces
+    from imitation_amd.rewards.reward_nets import BasicRewardNet
+    from imitation_amd.util import logger
+    from imitation_amd.util.networks import RunningNorm
+
+    th.manual_seed(seed)
+    net = BasicRewardNet(spaces.Box(-1, 1, (5,)), spaces.Box(-1, 1, (2,)), normalize_input_layer=RunningNorm)
+    tr = pc.BasicRewardTrainer(pc.PreferenceModel(net), pc.CrossEntropyRewardLoss(), rng=np.random.default_rng(seed),
+                               batch_size=mb, epochs=epochs, lr=1e-2,
+                               custom_logger=logger.configure(f"/tmp/ia_pref_dp_{rank}", format_strs=[]))
+    ds = _pref_dataset(P, L, seed)
+    assert tr._fast_path_ok(ds)
+    tr.train(ds)
+    norm = net.mlp.normalize_input if hasattr(net.mlp, "normalize_input") else None
+    out = [p.detach().numpy().copy() for p in net.parameters()]
+    out += [b.detach().numpy().copy() for b in net.buffers()]
+    return out
+
+
+def pref_gather_worker(rank, world, seed):
+    """PreferenceComparisons under DP: every replica pushes the same all-gathered pairs."""
+    from imitation_amd.algorithms import preference_comparisons as pc
+
+    rng = np.random.default_rng(seed + rank)
+    ds = _pref_dataset(3 + rank, 4, seed + rank)
+    frags, prefs = pc._all_gather_pairs(list(zip(ds.fragments1, ds.fragments2)), ds.preferences)
+    return [f[0].obs.sum() for f in frags], prefs.tolist()
+
+
+def dagger_dp_worker(rank, world, scratch, seed):
+    """SimpleDAggerTrainer under DP (host collector, gloo): per-rank scratch trees, the
+    all-gathered demo union, identical BC replicas."""
+    import os
+
+    import torch as th
+
+    from imitation_amd.algorithms import bc, dagger
+    from imitation_amd.policies.base import ZeroPolicy
+    from imitation_amd.util import logger
+    from imitation_amd.util.util import make_vec_env
+
+    th.manual_seed(seed)
+    venv = make_vec_env("seals/CartPole-v0", rng=np.random.default_rng(seed + rank), n_envs=2)
+    log = logger.configure(os.path.join(scratch, f"log{rank}"), format_strs=[])
+    bct = bc.BC(observation_space=venv.observation_space, action_space=venv.action_space,
+                rng=np.random.default_rng(seed + rank), batch_size=16, custom_logger=log)
+    expert = ZeroPolicy(venv.observation_space, venv.action_space)
+    tr = dagger.SimpleDAggerTrainer(venv=venv, scratch_dir=scratch, expert_policy=expert, rng=np.random.default_rng(seed + rank),
+                                    bc_trainer=bct, custom_logger=log)
+    tr.train(1000 * world, rollout_round_min_episodes=1, rollout_round_min_timesteps=500,
+             bc_train_kwargs=dict(n_batches=8, progress_bar=False))
+    local_files = sum(len(tr._store.files(r)) for r in range(tr.round_num))
+    return dict(params=[p.detach().numpy().copy() for p in tr.policy.parameters()], round_num=tr.round_num,
+                n_demos=len(tr._all_demos), local_files=local_files, scratch=str(tr.scratch_dir),
+                last=tr.last_train_timesteps, local=tr.last_train_timesteps_local)
