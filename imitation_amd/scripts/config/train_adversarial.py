@@ -26,7 +26,7 @@ def defaults():
     algorithm_specific = {}  # algorithm_specific[<command>] is merged into the config
     checkpoint_interval = 0  # rounds between checkpoints (<0 disables)
     agent_path = None  # warm-start generator from this model
-    engine = "auto"  # "device": whole GAIL round on the GPU (csrc/kernels/engine.hip); "host": reference loop
+    engine = "auto"  # "device": whole GAIL / AIRL round on the GPU (engine/{gail,airl}.py); "host": reference loop
 
 
 @train_adversarial_ex.config

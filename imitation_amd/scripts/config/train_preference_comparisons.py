@@ -15,6 +15,7 @@ MUJOCO_SHARED_LOCALS = dict(rl=dict(rl_kwargs=dict(ent_coef=0.1)))
 
 @train_preference_comparisons_ex.config
 def train_defaults():
+    engine = "auto"  # "device": agent rollouts + PPO on the GPU (engine/preference.py); "host": AgentTrainer
     fragment_length = 100  # timesteps per fragment used for comparisons
     total_timesteps = int(1e6)
     total_comparisons = 5000

@@ -62,22 +62,44 @@ for _ing in [train_adversarial_ex, *train_adversarial_ex._all_ingredients()]:
     _add_hook(_ing)
 
 
-def _make_trainer(algo_cls, engine: str, **kwargs) -> common.AdversarialTrainer:
-    if algo_cls is gail_algo.GAIL and engine in ("auto", "device"):
-        from imitation_amd.engine.gail import DeviceGAIL, supports
+def _device_engine(algo_cls):
+    """(device trainer class, eligibility check) of a host algorithm class, or None."""
+    if algo_cls is gail_algo.GAIL:
+        from imitation_amd.engine import gail as eng
 
+        return eng.DeviceGAIL, eng.supports
+    if algo_cls is airl_algo.AIRL:
+        from imitation_amd.engine import airl as eng
+
+        return eng.DeviceAIRL, eng.supports
+    return None
+
+
+def _make_trainer(algo_cls, engine: str, **kwargs) -> common.AdversarialTrainer:
+    """The device engine (``DeviceGAIL`` / ``DeviceAIRL``: fused rollout + PPO + discriminator
+    kernels) when ``engine`` is ``auto``/``device`` and the configuration is eligible, else the
+    host-loop trainer. ``engine=device`` fails loudly when it is not eligible. The choice is
+    recorded as ``trainer.engine_kind``."""
+    dev = _device_engine(algo_cls) if engine in ("auto", "device") else None
+    why = "no device engine for this algorithm" if dev is None else ""
+    if dev is not None:
+        cls, supports = dev
         ok, why = supports(kwargs["venv"], kwargs["gen_algo"], kwargs["reward_net"])
         if ok:
             try:
-                trainer = DeviceGAIL(**kwargs)
-                logger.info("Using the device engine (DeviceGAIL)")
+                trainer = cls(**kwargs)
+                trainer.engine_kind = "device"
+                logger.info(f"Using the device engine ({cls.__name__})")
                 return trainer
             except ValueError as e:  # e.g. nets too large for the persistent PPO kernel's LDS
                 why = str(e)
-        if engine == "device":
-            raise ValueError(f"engine=device requested but unsupported: {why}")
+    if engine == "device":
+        raise ValueError(f"engine=device requested but unsupported: {why}")
+    if engine != "host":
         logger.info(f"Device engine not applicable ({why}); using the host loop")
-    return algo_cls(**kwargs)
+    trainer = algo_cls(**kwargs)
+    trainer.engine_kind = "host"
+    return trainer
 
 
 @train_adversarial_ex.capture
@@ -112,7 +134,7 @@ def train_adversarial(_run, show_config: bool, algo_cls: Type[common.Adversarial
         imit_stats = policy_evaluation.eval_policy(trainer.policy, trainer.venv_train)
     if checkpoint_interval >= 0:
         save(trainer, log_dir / "checkpoints" / "final")
-    return {"imit_stats": imit_stats, "expert_stats": rollout.rollout_stats(expert_trajs)}
+    return {"imit_stats": imit_stats, "expert_stats": rollout.rollout_stats(expert_trajs), "engine": trainer.engine_kind}
 
 
 @train_adversarial_ex.command
