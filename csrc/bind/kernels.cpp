@@ -83,6 +83,94 @@ py::tuple tmlp_backward(torch::Tensor x, torch::Tensor dy, std::vector<torch::Te
   return py::make_tuple(dxo, dWs, dbs);
 }
 
+// Grouped (ensemble) descriptor: Ws[l] [G, out, in], bs[l] [G, out], mean / var [G, din];
+// x is [B, din] (shared by every group) or [G, B, din].
+ia::MLPDesc make_group_desc(const torch::Tensor& x, const std::vector<torch::Tensor>& Ws, const std::vector<torch::Tensor>& bs,
+                            int64_t hidden_act, int64_t out_act, const c10::optional<torch::Tensor>& mean,
+                            const c10::optional<torch::Tensor>& var, double eps, int* B_out) {
+  TORCH_CHECK(!Ws.empty() && Ws.size() <= (size_t)ia::kMaxLayers && Ws.size() == bs.size(), "1..4 layers");
+  const int64_t G = Ws[0].size(0);
+  ia::MLPDesc d{};
+  d.n_layers = (int)Ws.size();
+  d.hidden_act = (int)hidden_act;
+  d.out_act = (int)out_act;
+  d.dims[0] = (int)Ws[0].size(2);
+  d.groups = (int)G;
+  for (size_t l = 0; l < Ws.size(); ++l) {
+    IA_CHECK_GPU_F32(Ws[l]);
+    IA_CHECK_GPU_F32(bs[l]);
+    TORCH_CHECK(Ws[l].dim() == 3 && Ws[l].size(0) == G && Ws[l].size(2) == d.dims[l], "layer ", l, " must be [G, out, in]");
+    TORCH_CHECK(bs[l].dim() == 2 && bs[l].size(0) == G && bs[l].size(1) == Ws[l].size(1), "bias ", l, " must be [G, out]");
+    d.dims[l + 1] = (int)Ws[l].size(1);
+    d.W[l] = Ws[l].data_ptr<float>();
+    d.b[l] = bs[l].data_ptr<float>();
+    d.gs_w[l] = Ws[l].size(1) * Ws[l].size(2);
+    d.gs_b[l] = Ws[l].size(1);
+  }
+  for (int l = 0; l <= d.n_layers; ++l) TORCH_CHECK(d.dims[l] <= ia::kMaxDim, "tmlp width limit is 128");
+  if (mean.has_value() && mean->defined()) {
+    IA_CHECK_GPU_F32(*mean);
+    IA_CHECK_GPU_F32(*var);
+    TORCH_CHECK(mean->numel() == G * d.dims[0] && var->numel() == G * d.dims[0], "norm stats must be [G, din]");
+    d.norm_mean = mean->data_ptr<float>();
+    d.norm_var = var->data_ptr<float>();
+    d.gs_norm = d.dims[0];
+  }
+  d.norm_eps = (float)eps;
+  IA_CHECK_GPU_F32(x);
+  if (x.dim() == 2) {
+    TORCH_CHECK(x.size(1) == d.dims[0], "input dim mismatch");
+    *B_out = (int)x.size(0);
+    d.gs_x = 0;
+  } else {
+    TORCH_CHECK(x.dim() == 3 && x.size(0) == G && x.size(2) == d.dims[0], "x must be [B, din] or [G, B, din]");
+    *B_out = (int)x.size(1);
+    d.gs_x = x.size(1) * x.size(2);
+  }
+  d.gs_y = (int64_t)(*B_out) * d.dims[d.n_layers];
+  return d;
+}
+
+// y [G, B, out]: every ensemble member's MLP in ONE launch (grid.y = member)
+torch::Tensor tmlp_forward_grouped(torch::Tensor x, std::vector<torch::Tensor> Ws, std::vector<torch::Tensor> bs,
+                                   int64_t hidden_act, int64_t out_act, c10::optional<torch::Tensor> mean,
+                                   c10::optional<torch::Tensor> var, double eps) {
+  int B = 0;
+  auto d = make_group_desc(x, Ws, bs, hidden_act, out_act, mean, var, eps, &B);
+  auto y = torch::empty({(int64_t)d.groups, B, d.dims[d.n_layers]}, x.options());
+  IA_HIP_CHECK(ia::tmlp_forward(d, x.data_ptr<float>(), B, y.data_ptr<float>(), ia_stream()));
+  return y;
+}
+
+// (dx [G, B, din] or None, [dW [G, out, in]...], [db [G, out]...]) for dy [G, B, out]
+py::tuple tmlp_backward_grouped(torch::Tensor x, torch::Tensor dy, std::vector<torch::Tensor> Ws, std::vector<torch::Tensor> bs,
+                                int64_t hidden_act, int64_t out_act, c10::optional<torch::Tensor> mean,
+                                c10::optional<torch::Tensor> var, double eps, bool need_dx) {
+  int B = 0;
+  auto d = make_group_desc(x, Ws, bs, hidden_act, out_act, mean, var, eps, &B);
+  const int64_t G = d.groups;
+  IA_CHECK_GPU_F32(dy);
+  TORCH_CHECK(dy.dim() == 3 && dy.size(0) == G && dy.size(1) == B && dy.size(2) == d.dims[d.n_layers], "dy must be [G, B, out]");
+  TORCH_CHECK(!need_dx || d.gs_x != 0, "dx of a shared input is not produced");
+  ia::MLPGrads g{};
+  std::vector<torch::Tensor> dWs, dbs;
+  for (int l = 0; l < d.n_layers; ++l) {
+    dWs.push_back(torch::empty_like(Ws[l]));
+    dbs.push_back(torch::empty_like(bs[l]));
+    g.dW[l] = dWs.back().data_ptr<float>();
+    g.db[l] = dbs.back().data_ptr<float>();
+  }
+  torch::Tensor dx;
+  if (need_dx) dx = torch::empty_like(x);
+  const size_t slab_n = ia::tmlp_slab_floats(d, B);
+  torch::Tensor slab;
+  if (slab_n) slab = torch::empty({(int64_t)(slab_n * G)}, x.options());
+  IA_HIP_CHECK(ia::tmlp_backward(d, x.data_ptr<float>(), dy.data_ptr<float>(), B, need_dx ? dx.data_ptr<float>() : nullptr, g,
+                                 slab_n ? slab.data_ptr<float>() : nullptr, ia_stream()));
+  py::object dxo = need_dx ? py::cast(dx) : py::none();
+  return py::make_tuple(dxo, dWs, dbs);
+}
+
 py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch::Tensor last_val, torch::Tensor dones,
               double gamma, double lam) {
   IA_CHECK_GPU_F32(rew);
@@ -180,6 +268,12 @@ void register_kernels(py::module& m) {
   m.def("tmlp_backward", &tmlp_backward, py::arg("x"), py::arg("dy"), py::arg("weights"), py::arg("biases"),
         py::arg("hidden_act"), py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
         py::arg("norm_eps") = 1e-5, py::arg("norm_clip") = 0.0, py::arg("need_dx") = false);
+  m.def("tmlp_forward_grouped", &tmlp_forward_grouped, py::arg("x"), py::arg("weights"), py::arg("biases"),
+        py::arg("hidden_act"), py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
+        py::arg("norm_eps") = 1e-5);
+  m.def("tmlp_backward_grouped", &tmlp_backward_grouped, py::arg("x"), py::arg("dy"), py::arg("weights"), py::arg("biases"),
+        py::arg("hidden_act"), py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
+        py::arg("norm_eps") = 1e-5, py::arg("need_dx") = false);
   m.def("gae", &gae, py::arg("rewards"), py::arg("values"), py::arg("episode_starts"), py::arg("last_values"),
         py::arg("dones"), py::arg("gamma"), py::arg("lam"));
   m.def("adam_flat", &adam_flat, py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"),

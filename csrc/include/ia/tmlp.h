@@ -26,6 +26,11 @@ struct MLPDesc {
   const float* norm_var;
   float norm_eps;
   float norm_clip;  // >0: clamp normalised input to [-clip, clip]
+  // Grouped launches (reward ensembles): blockIdx.y = group g reads W_l + g * gs_w[l],
+  // b_l + g * gs_b[l], norm + g * gs_norm, X + g * gs_x and writes Y + g * gs_y (strides in
+  // floats; 0 = shared by every group, e.g. one input batch for all members).
+  int groups;
+  long long gs_w[kMaxLayers], gs_b[kMaxLayers], gs_norm, gs_x, gs_y;
 };
 
 struct MLPGrads {

@@ -25,6 +25,7 @@ __device__ void stage_input(bf16* H, int ld, const float* __restrict__ X, int B,
   const int din = d.dims[0];
   const int kp = pad32(din);
   const int n = rows * kp;
+  const long long go = (long long)blockIdx.y * d.gs_norm;
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
     const int r = e / kp, c = e - r * kp;
     const int gr = row0 + r;
@@ -32,7 +33,7 @@ __device__ void stage_input(bf16* H, int ld, const float* __restrict__ X, int B,
     if (gr < B && c < din) {
       v = X[(size_t)gr * din + c];
       if (d.norm_mean) {
-        v = (v - d.norm_mean[c]) * rsqrtf(d.norm_var[c] + d.norm_eps);
+        v = (v - d.norm_mean[go + c]) * rsqrtf(d.norm_var[go + c] + d.norm_eps);
         if (d.norm_clip > 0.f) v = fminf(fmaxf(v, -d.norm_clip), d.norm_clip);
       }
     }
@@ -66,6 +67,9 @@ __global__ __launch_bounds__(64 * NW) void tmlp_fwd_kernel(MLPDesc d, TmlpPlan p
   bf16* H1 = reinterpret_cast<bf16*>(smem + p.w_bytes + p.h_bytes);
   const int row0 = blockIdx.x * p.rows;
   const int w = wave_id();
+  const long long grp = blockIdx.y;
+  X += grp * d.gs_x;
+  Y += grp * d.gs_y;
   lds_zero(smem, p.fwd_lds);
   __syncthreads();
   stage_input(H0, p.ld_h, X, B, row0, p.rows, d);
@@ -74,14 +78,14 @@ __global__ __launch_bounds__(64 * NW) void tmlp_fwd_kernel(MLPDesc d, TmlpPlan p
   for (int l = 0; l < d.n_layers; ++l) {
     const int din = d.dims[l], dout = d.dims[l + 1];
     __syncthreads();
-    stage_w(Wb, d.W[l], dout, din, false);
+    stage_w(Wb, d.W[l] + grp * d.gs_w[l], dout, din, false);
     __syncthreads();
     const int K = pad32(din), ldw = ld_for_k(din);
     const bool last = l == d.n_layers - 1;
     const int act = layer_act(d, l);
     const int ntiles = last ? pad16(dout) / 16 : pad32(dout) / 16;
     const bf16* A = Hin + w * 16 * p.ld_h;
-    const float* __restrict__ bias = d.b[l];
+    const float* __restrict__ bias = d.b[l] + grp * d.gs_b[l];
     for (int nt = 0; nt < ntiles; ++nt) {
       f32x4 acc = mma_16x16(A, p.ld_h, Wb + nt * 16 * ldw, ldw, K, zero4());
       const int col = nt * 16 + acc_col();
@@ -151,7 +155,11 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
   const int w = wave_id();
   const int ROWS = p.rows;
   const bool direct = !kDisc && gridDim.x == 1;
-  float* slab_row = direct ? nullptr : slab + (size_t)blockIdx.x * p.n_params;
+  const long long grp = blockIdx.y;  // grouped launch: this group's inputs / params / grads
+  X += grp * d.gs_x;
+  if (dY) dY += grp * d.gs_y;
+  if (dX) dX += grp * d.gs_x;
+  float* slab_row = direct ? nullptr : slab + ((size_t)grp * gridDim.x + blockIdx.x) * p.n_params;
 
   lds_zero(smem, p.bwd_lds);
   __syncthreads();
@@ -161,7 +169,7 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
   for (int l = 0; l < L; ++l) {
     const int din = d.dims[l], dout = d.dims[l + 1];
     __syncthreads();
-    stage_w(Wb, d.W[l], dout, din, false);
+    stage_w(Wb, d.W[l] + grp * d.gs_w[l], dout, din, false);
     __syncthreads();
     const int K = pad32(din), ldw = ld_for_k(din);
     const int act = layer_act(d, l);
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
     for (int nt = 0; nt < ntiles; ++nt) {
       f32x4 acc = mma_16x16(A, p.ld_h, Wb + nt * 16 * ldw, ldw, K, zero4());
       const int col = nt * 16 + acc_col();
-      const float bv = col < dout ? d.b[l][col] : 0.f;
+      const float bv = col < dout ? d.b[l][grp * d.gs_b[l] + col] : 0.f;
       float colsum = 0.f;
       float dzv[4];
 #pragma unroll
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
         HT[i * p.ld_ht + r] = Hs[l][r * p.ld_h + i];
       }
     }
-    if (l > 0 || dX != nullptr) stage_w(Wb, d.W[l], dout, din, true);
+    if (l > 0 || dX != nullptr) stage_w(Wb, d.W[l] + grp * d.gs_w[l], dout, din, true);
     __syncthreads();
 
     // db_l: reduce wave partials
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
       float s = 0.f;
       for (int ww = 0; ww < NW; ++ww) s += dbs[(z * NW + ww) * p.dmax_pad + c];
       if (direct) {
-        float* dst = g.db[l] + c;
+        float* dst = g.db[l] + grp * d.gs_b[l] + c;
         *dst = g.accumulate ? *dst + s : s;
       } else {
         slab_row[p.param_off[2 * l + 1] + c] = s;
@@ -272,7 +280,7 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
           const int o = tm * 16 + acc_row(i);
           if (o < dout && in < din) {
             if (direct) {
-              float* dst = g.dW[l] + o * din + in;
+              float* dst = g.dW[l] + grp * d.gs_w[l] + o * din + in;
               *dst = g.accumulate ? *dst + acc[i] : acc[i];
             } else {
               slab_row[p.param_off[2 * l] + o * din + in] = acc[i];
@@ -315,9 +323,10 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
             if (gr < B && col < din) {
               float gx = acc[i];
               if (d.norm_mean) {
-                const float sc = rsqrtf(d.norm_var[col] + d.norm_eps);
+                const long long go = grp * d.gs_norm;
+                const float sc = rsqrtf(d.norm_var[go + col] + d.norm_eps);
                 if (d.norm_clip > 0.f) {
-                  const float xn = (X[(size_t)gr * din + col] - d.norm_mean[col]) * sc;
+                  const float xn = (X[(size_t)gr * din + col] - d.norm_mean[go + col]) * sc;
                   if (xn <= -d.norm_clip || xn >= d.norm_clip) gx = 0.f;
                 }
                 gx *= sc;
@@ -336,17 +345,19 @@ __global__ __launch_bounds__(64 * NW) void tmlp_bwd_kernel(MLPDesc d, TmlpPlan p
 __global__ void tmlp_grad_reduce_kernel(const float* __restrict__ slab, int nblk, TmlpPlan p, MLPDesc d, MLPGrads g) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= p.n_params) return;
+  const long long grp = blockIdx.y;
+  slab += (size_t)grp * nblk * p.n_params;
   float s = 0.f;
   for (int b = 0; b < nblk; ++b) s += slab[(size_t)b * p.n_params + e];
   // locate parameter tensor
   for (int l = d.n_layers - 1; l >= 0; --l) {
     if (e >= p.param_off[2 * l + 1]) {
-      float* dst = g.db[l] + (e - p.param_off[2 * l + 1]);
+      float* dst = g.db[l] + grp * d.gs_b[l] + (e - p.param_off[2 * l + 1]);
       *dst = g.accumulate ? *dst + s : s;
       return;
     }
     if (e >= p.param_off[2 * l]) {
-      float* dst = g.dW[l] + (e - p.param_off[2 * l]);
+      float* dst = g.dW[l] + grp * d.gs_w[l] + (e - p.param_off[2 * l]);
       *dst = g.accumulate ? *dst + s : s;
       return;
     }
@@ -394,10 +405,11 @@ hipError_t tmlp_forward(const MLPDesc& d, const float* X, int B, float* Y, hipSt
   TmlpPlan p = plan_tmlp(d, 4);
   if (p.fwd_lds > 160 * 1024) p = plan_tmlp(d, 2);
   const int nblk = (B + p.rows - 1) / p.rows;
+  const unsigned G = d.groups > 1 ? (unsigned)d.groups : 1u;
   if (p.waves == 4)
-    hipLaunchKernelGGL(tmlp_fwd_kernel<4>, dim3(nblk), dim3(256), p.fwd_lds, s, d, p, X, B, Y);
+    hipLaunchKernelGGL(tmlp_fwd_kernel<4>, dim3(nblk, G), dim3(256), p.fwd_lds, s, d, p, X, B, Y);
   else
-    hipLaunchKernelGGL(tmlp_fwd_kernel<2>, dim3(nblk), dim3(128), p.fwd_lds, s, d, p, X, B, Y);
+    hipLaunchKernelGGL(tmlp_fwd_kernel<2>, dim3(nblk, G), dim3(128), p.fwd_lds, s, d, p, X, B, Y);
   return hipGetLastError();
 }
 
@@ -409,12 +421,15 @@ hipError_t tmlp_backward(const MLPDesc& d, const float* X, const float* dY, int 
   const int nblk = (B + p.rows - 1) / p.rows;
   if (nblk > 1 && slab == nullptr) return hipErrorInvalidValue;
   const DiscLoss none{};
+  const unsigned G = d.groups > 1 ? (unsigned)d.groups : 1u;
   if (nw == 4)
-    hipLaunchKernelGGL((tmlp_bwd_kernel<4, false>), dim3(nblk), dim3(256), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab, none);
+    hipLaunchKernelGGL((tmlp_bwd_kernel<4, false>), dim3(nblk, G), dim3(256), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab,
+                       none);
   else
-    hipLaunchKernelGGL((tmlp_bwd_kernel<2, false>), dim3(nblk), dim3(128), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab, none);
+    hipLaunchKernelGGL((tmlp_bwd_kernel<2, false>), dim3(nblk, G), dim3(128), p.bwd_lds, s, d, p, X, dY, B, dX, g, slab,
+                       none);
   if (nblk > 1) {
-    hipLaunchKernelGGL(tmlp_grad_reduce_kernel, dim3((p.n_params + 255) / 256), dim3(256), 0, s, slab, nblk, p, d, g);
+    hipLaunchKernelGGL(tmlp_grad_reduce_kernel, dim3((p.n_params + 255) / 256, G), dim3(256), 0, s, slab, nblk, p, d, g);
   }
   return hipGetLastError();
 }

@@ -950,13 +950,128 @@ class EnsembleTrainer(BasicRewardTrainer):
         for t in getattr(self, "member_trainers", []):
             t.logger = custom_logger
 
-    def _train(self, dataset: PreferenceDataset, epoch_multiplier: float = 1.0) -> None:
-        sampler = data_th.RandomSampler(dataset, replacement=True, num_samples=len(dataset),
+    def _batched_ok(self, dataset) -> bool:
+        """All members train in one grouped step when they stack (identical BasicRewardNet
+        MLPs) and the member trainers would take their fast path; ``IMITATION_AMD_ENSEMBLE_BATCHED=0``
+        keeps the reference's member-by-member loop."""
+        if os.environ.get("IMITATION_AMD_ENSEMBLE_BATCHED", "1") == "0":
+            return False
+        ens = self._preference_model.ensemble_model
+        if ens is None or ens.stack() is None or type(self.loss) is not CrossEntropyRewardLoss:
+            return False
+        if self.regularizer is not None or not isinstance(dataset, PreferenceDataset) or len(dataset) == 0:
+            return False
+        if isinstance(dataset.fragments1[0].obs, types.DictObs):
+            return False
+        return len({len(f) for f in dataset.fragments1} | {len(f) for f in dataset.fragments2}) == 1
+
+    def _stack_optimizer(self, stack):
+        """One (Fused)AdamW over the stacked member parameters (== M independent AdamWs)."""
+        if getattr(self, "_stack_opt", None) is None:
+            params = [t.clone().requires_grad_(True) for t in stack.gather_params()]
+            lr = self.member_trainers[0].optim.defaults["lr"]
+            cls = optim_ops.fused_for(th.optim.AdamW, params[0].device) or th.optim.AdamW
+            self._stack_params = params
+            self._stack_opt = cls(params, lr=lr)
+        return self._stack_params, self._stack_opt
+
+    def _train_batched(self, dataset: PreferenceDataset, epoch_multiplier: float) -> None:
+        """The reference's bagged member training (same bootstrap bags, per-member epoch
+        orders and accumulation, from the same rng draws) with every minibatch of ALL members
+        as one grouped forward/backward (``ops.tmlp_grouped``) and one optimizer step."""
+        pm = self._preference_model
+        ens = pm.ensemble_model
+        st = ens.stack()
+        M = ens.num_members
+        params, opt = self._stack_optimizer(st)
+        with th.no_grad():
+            for t, g in zip(params, st.gather_params()):
+                t.copy_(g)  # members may have changed since the last call (e.g. a checkpoint load)
+        norm = st.gather_norm()
+        pairs = list(zip(dataset.fragments1, dataset.fragments2))
+        packed = _pack_pairs(pairs)
+        s_all, a_all, ns_all, d_all = ens.preprocess(packed.state, packed.action, packed.next_state, packed.done)
+        x_all = st.features(s_all, a_all, ns_all, d_all)
+        dev = x_all.device
+        P, L = len(pairs), packed.max_len
+        prefs_all = th.as_tensor(dataset.preferences, device=dev)
+        gt = None
+        if _trajectory_pair_includes_reward(pairs[0]):
+            gt = th.as_tensor(np.stack([np.asarray(f.rews, np.float32) for pr in pairs for f in pr]), device=dev).view(P, 2, L)
+        # rng draws in the reference's order: the bagging sampler, then each member trainer's
+        # DataLoader seed
+        sampler = data_th.RandomSampler(range(P), replacement=True, num_samples=P,
                                         generator=th.Generator().manual_seed(util.make_seeds(self.rng)))
-        for idx, trainer in enumerate(self.member_trainers):
-            bagging = data_th.Subset(dataset, list(sampler))
-            with self.logger.add_accumulate_prefix(f"member-{idx}"):
-                trainer.train(bagging, epoch_multiplier=epoch_multiplier)
+        bags = th.as_tensor([list(sampler) for _ in range(M)], device=dev)  # [M, P]
+        loaders = [data_th.DataLoader(range(P), batch_size=self.minibatch_size, shuffle=True,
+                                      generator=th.Generator().manual_seed(t._shuffle_seed())) for t in self.member_trainers]
+        epochs = round(self.epochs * epoch_multiplier)
+        assert epochs > 0, "Must train for at least one epoch."
+        B = self.minibatch_size
+        span = th.arange(2 * L, device=dev)
+        recs_by_epoch = []
+        import contextlib
+
+        sync = pdist.no_norm_sync() if pdist.world_size() > 1 else contextlib.nullcontext()  # replicated compute
+        with sync:
+            for _ in range(epochs):
+                orders = th.stack([th.cat(list(ld)) for ld in loaders]).to(dev)  # [M, P] positions in each bag
+                recs = []
+                accumulated = 0
+                opt.zero_grad()
+                for start in range(0, P, B):
+                    n = int(min(B, P - start))
+                    idx = bags.gather(1, orders[:, start : start + n])  # [M, n] pair indices
+                    rows = (idx[..., None] * (2 * L) + span).reshape(M, -1)
+                    x = x_all[rows]  # [M, n*2L, din]
+                    if norm is not None:
+                        st.update_norm(norm, x)
+                    rews = st.forward(x, params, norm).view(M * n, 2, L)
+                    prefs = prefs_all[idx].reshape(-1)
+                    loss, probs = pref_ops.bradley_terry(rews[:, 0], rews[:, 1], prefs, pm.discount_factor, pm.threshold,
+                                                         pm.noise_prob)
+                    # sum of the members' minibatch means, each scaled like its own trainer's
+                    (loss * M * (n / self.batch_size)).backward()
+                    with th.no_grad():
+                        p2 = probs.detach().view(M, n).clamp(1e-7, 1 - 1e-7)
+                        y = prefs.view(M, n)
+                        rec = [-(y * p2.log() + (1 - y) * (1 - p2).log()).mean(1), ((p2 > 0.5) == (y > 0.5)).float().mean(1)]
+                        if gt is not None:
+                            g = gt[idx.reshape(-1)]
+                            gp = pref_ops.bradley_terry_probs_reference(g[:, 0], g[:, 1], pm.discount_factor, pm.threshold,
+                                                                        pm.noise_prob).view(M, n).clamp(1e-7, 1 - 1e-7)
+                            rec.append(-(y * gp.log() + (1 - y) * (1 - gp).log()).mean(1))
+                        recs.append(th.stack(rec, 1))  # [M, n_metrics]
+                    accumulated += n
+                    if accumulated >= self.batch_size:
+                        opt.step()
+                        opt.zero_grad()
+                        accumulated = 0
+                if accumulated != 0:
+                    opt.step()
+                recs_by_epoch.append(th.stack(recs, 1).cpu())  # [M, n_minibatches, n_metrics]
+        st.scatter(params, norm)
+        names = ["loss", "accuracy", "gt_reward_loss"]
+        for m, trainer in enumerate(self.member_trainers):
+            with self.logger.add_accumulate_prefix(f"member-{m}"):
+                with self.logger.accumulate_means("reward"):
+                    for e, recs in enumerate(recs_by_epoch):
+                        with self.logger.add_key_prefix(f"epoch-{e}"), self.logger.add_key_prefix("train"):
+                            for vals in recs[m].tolist():
+                                for k, v in zip(names, vals):
+                                    self.logger.record(k, v)
+                trainer._record_final(epochs - 1)
+
+    def _train(self, dataset: PreferenceDataset, epoch_multiplier: float = 1.0) -> None:
+        if self._batched_ok(dataset):
+            self._train_batched(dataset, epoch_multiplier)
+        else:
+            sampler = data_th.RandomSampler(dataset, replacement=True, num_samples=len(dataset),
+                                            generator=th.Generator().manual_seed(util.make_seeds(self.rng)))
+            for idx, trainer in enumerate(self.member_trainers):
+                bagging = data_th.Subset(dataset, list(sampler))
+                with self.logger.add_accumulate_prefix(f"member-{idx}"):
+                    trainer.train(bagging, epoch_multiplier=epoch_multiplier)
         metrics = defaultdict(list)
         for key in list(self.logger.name_to_value.keys()):
             if re.match(r"member-(\d+)/reward/(.+)", key) and "final" in key:

@@ -52,6 +52,18 @@ def _split(reward_net) -> Tuple[Any, Any]:
     return None, reward_net
 
 
+def _ensemble_of(reward_fn) -> Tuple[Optional[reward_nets.RewardEnsemble], Optional[float]]:
+    """(stackable RewardEnsemble, std coefficient) behind ``reward_fn`` or (None, None):
+    a bare ensemble rewards its member mean, ``AddSTDRewardWrapper`` mean + alpha * std."""
+    alpha = 0.0
+    ens = reward_fn
+    if isinstance(reward_fn, reward_nets.AddSTDRewardWrapper):
+        ens, alpha = reward_fn.base, float(reward_fn.default_alpha)
+    if isinstance(ens, reward_nets.RewardEnsemble) and ens.stack() is not None:
+        return ens, alpha
+    return None, None
+
+
 def supports(venv, algorithm, reward_fn) -> Tuple[bool, str]:
     """Whether :class:`DeviceAgentTrainer` can run this agent (reason when not)."""
     ok, why = supports_generator(venv, algorithm)
@@ -59,6 +71,11 @@ def supports(venv, algorithm, reward_fn) -> Tuple[bool, str]:
         return ok, why
     if not isinstance(reward_fn, reward_nets.RewardNet):
         return False, "reward_fn is not a RewardNet"
+    ens, _ = _ensemble_of(reward_fn)
+    if ens is not None:
+        return (True, "") if ens.device.type == "cuda" else (False, "ensemble not on the GPU")
+    if isinstance(reward_fn, (reward_nets.RewardEnsemble, reward_nets.AddSTDRewardWrapper)):
+        return False, "ensemble members do not stack (not identical BasicRewardNet MLPs)"
     out_norm, base = _split(reward_fn)
     if out_norm is not None and type(out_norm) is not networks.RunningNorm:
         return False, "output normaliser is not RunningNorm"
@@ -108,6 +125,28 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
         self._wrapped_ret = np.zeros(N, dtype=np.float64)
 
     # ------------------------------------------------------------------ kernels
+    def _rollout(self) -> None:
+        """Single reward nets run inside the post pass; an ensemble (active selection,
+        ``AddSTDRewardWrapper``) is scored afterwards for all T x N transitions with ONE
+        grouped launch over its stacked members, then mean (+ alpha * unbiased std)."""
+        ens, alpha = _ensemble_of(self._reward_net)
+        if ens is None or self.debug_use_ground_truth:
+            return super()._rollout()
+        self._launch_chain()
+        self._launch_post(False)  # values, log-probs, TimeLimit bootstrap
+        b = self.buf
+        T, N = self.T, self.N
+        st = ens.stack()
+        flat = lambda t: t.reshape(T * N, -1)  # noqa: E731
+        acts = b["act_env"].reshape(T * N) if self.discrete else flat(b["act_env"])
+        with th.no_grad():
+            s, a, ns, d = ens.members[0].preprocess(flat(b["obs_buf"]), acts, flat(b["next_obs"]), b["dones"].reshape(-1))
+            r_all = st.forward(st.features(s, a, ns, d), st.gather_params(), st.gather_norm())  # [M, T*N]
+            r = r_all.mean(0)
+            if alpha:
+                r = r + alpha * r_all.var(0, unbiased=True).sqrt()
+            b["rewards"].copy_(r.view(T, N) + self._boot)
+
     def _reward_spec(self) -> Dict[str, Any]:
         """``reward_net.predict_processed``: the base MLP's raw output (eval-mode input norm)."""
         _, base = _split(self._reward_net)

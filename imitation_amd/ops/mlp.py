@@ -182,3 +182,79 @@ def tmlp(
             params += [w, b]
         return _TMLPFn.apply(x, hidden_act, out_act, norm_mean, norm_var, norm_eps, *params)
     return tmlp_reference(x, weights, biases, hidden_act, out_act, norm_mean, norm_var, norm_eps)
+
+
+# ----------------------------------------------------------------------------- grouped (ensembles)
+def tmlp_grouped_reference(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor],
+                           hidden_act: int, out_act: int = 0, norm_mean: Optional[torch.Tensor] = None,
+                           norm_var: Optional[torch.Tensor] = None, norm_eps: float = 1e-5) -> torch.Tensor:
+    """fp32 reference of :func:`tmlp_grouped`: ``x`` [B, din] (shared) or [G, B, din];
+    ``weights[l]`` [G, out, in], ``biases[l]`` [G, out], norm stats [G, din] -> [G, B, out]."""
+    G = weights[0].shape[0]
+    h = x.unsqueeze(0).expand(G, -1, -1) if x.dim() == 2 else x
+    if norm_mean is not None:
+        h = (h - norm_mean[:, None, :]) / torch.sqrt(norm_var[:, None, :] + norm_eps)
+    n = len(weights)
+    for i, (w, b) in enumerate(zip(weights, biases)):
+        h = torch.baddbmm(b[:, None, :], h, w.transpose(1, 2))
+        h = _act(out_act if i == n - 1 else hidden_act, h)
+    return h
+
+
+class _TMLPGroupedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, hidden_act, out_act, mean, var, eps, *params):
+        from imitation_amd.ops import native
+
+        C = native()
+        ws = [p.contiguous() for p in params[0::2]]
+        bs = [p.contiguous() for p in params[1::2]]
+        xc = x.contiguous()
+        y = C.tmlp_forward_grouped(xc, ws, bs, int(hidden_act), int(out_act), mean, var, float(eps))
+        ctx.cfg = (int(hidden_act), int(out_act), float(eps), mean is not None, len(ws))
+        saved = [xc] + ws + bs
+        if mean is not None:
+            mv = torch.stack([mean, var])  # snapshot (a train-mode norm updates in place later)
+            saved += [mv[0], mv[1]]
+        ctx.save_for_backward(*saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from imitation_amd.ops import native
+
+        hidden_act, out_act, eps, has_norm, L = ctx.cfg
+        saved = ctx.saved_tensors
+        x, ws, bs = saved[0], list(saved[1 : 1 + L]), list(saved[1 + L : 1 + 2 * L])
+        mean = var = None
+        if has_norm:
+            mean, var = saved[1 + 2 * L], saved[2 + 2 * L]
+        need_dx = bool(ctx.needs_input_grad[0]) and x.dim() == 3
+        dx, dws, dbs = native().tmlp_backward_grouped(x, dy.contiguous(), ws, bs, hidden_act, out_act, mean, var, eps,
+                                                      need_dx)
+        grads = []
+        for dw, db in zip(dws, dbs):
+            grads += [dw, db]
+        return (dx, None, None, None, None, None, *grads)
+
+
+def tmlp_grouped(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor], hidden_act: int,
+                 out_act: int = 0, norm_mean: Optional[torch.Tensor] = None, norm_var: Optional[torch.Tensor] = None,
+                 norm_eps: float = 1e-5) -> torch.Tensor:
+    """G structurally identical MLPs (an ensemble) in ONE launch: ``grid.y`` = member, each
+    with its own stacked weights / biases / input-norm statistics; ``x`` is shared
+    ([B, din]) or per member ([G, B, din]). Differentiable w.r.t. the stacked parameters
+    (and a per-member ``x``). GPU fp32 -> HIP kernel (csrc/kernels/tmlp.hip), else the
+    batched-matmul reference."""
+    from imitation_amd.ops import use_kernel
+
+    dims = [weights[0].shape[2]] + [w.shape[1] for w in weights]
+    if use_kernel(x) and x.dtype == torch.float32 and kernel_supports(dims) and all(w.dtype == torch.float32 for w in weights):
+        if norm_mean is not None:
+            norm_mean = norm_mean.detach().float().contiguous()
+            norm_var = norm_var.detach().float().contiguous()
+        params = []
+        for w, b in zip(weights, biases):
+            params += [w, b]
+        return _TMLPGroupedFn.apply(x, hidden_act, out_act, norm_mean, norm_var, norm_eps, *params)
+    return tmlp_grouped_reference(x, weights, biases, hidden_act, out_act, norm_mean, norm_var, norm_eps)

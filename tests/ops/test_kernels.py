@@ -174,3 +174,39 @@ def test_preference_kernel_saturated_grad():
     th.testing.assert_close(b2.grad.cpu().double(), expect, rtol=1e-4, atol=1e-6)
     th.testing.assert_close(b1.grad.cpu().double(), -expect, rtol=1e-4, atol=1e-6)
     th.testing.assert_close(probs.cpu().double(), pm, rtol=1e-4, atol=1e-6)
+
+
+@gpu
+@pytest.mark.parametrize("dims,act,B,shared", [([23, 32, 32, 1], 1, 3000, True), ([23, 32, 32, 1], 1, 700, False),
+                                                ([17, 64, 64, 3], 2, 97, False), ([11, 32, 1], 1, 16, True)])
+def test_tmlp_grouped_matches_per_member_reference(dims, act, B, shared):
+    """Grouped launch (grid.y = member; ensembles) == each member's fp32 bf16-emulated reference,
+    forward and backward (parameter grads, per-member input grads)."""
+    dev = th.device("cuda")
+    G = 5
+    members = [_mk_mlp(dims, dev) for _ in range(G)]
+    Ws = [th.stack([m[0][l] for m in members]).detach().requires_grad_(True) for l in range(len(dims) - 1)]
+    bs = [th.stack([m[1][l] for m in members]).detach().requires_grad_(True) for l in range(len(dims) - 1)]
+    mean = th.randn(G, dims[0], device=dev) * 0.3
+    var = th.rand(G, dims[0], device=dev) + 0.5
+    x = th.randn(B, dims[0], device=dev) if shared else th.randn(G, B, dims[0], device=dev)
+    x.requires_grad_(not shared)
+    y = mlp_ops.tmlp_grouped(x, Ws, bs, act, 0, mean, var)
+    assert y.shape == (G, B, dims[-1])
+    gy = th.randn_like(y)
+    (y * gy).sum().backward()
+    for g in range(G):
+        wr = [W[g].detach().clone().requires_grad_(True) for W in Ws]
+        br = [b[g].detach().clone().requires_grad_(True) for b in bs]
+        xr = (x if shared else x[g]).detach().clone().requires_grad_(True)
+        yr = mlp_ops.tmlp_reference(xr, wr, br, act, 0, mean[g], var[g], emulate_bf16_operands=True)
+        scale = yr.abs().max().item() + 1e-3
+        assert (y[g] - yr).abs().max().item() <= 3e-2 * scale, g
+        (yr * gy[g]).sum().backward()
+        for l in range(len(wr)):
+            ref = max(wr[l].grad.abs().max().item(), br[l].grad.abs().max().item()) + 1e-3
+            assert (Ws[l].grad[g] - wr[l].grad).abs().max().item() <= 3e-2 * ref, (g, l)
+            assert (bs[l].grad[g] - br[l].grad).abs().max().item() <= 3e-2 * ref, (g, l)
+        if not shared:
+            refx = xr.grad.abs().max().item() + 1e-3
+            assert (x.grad[g] - xr.grad).abs().max().item() <= 3e-2 * refx, g
