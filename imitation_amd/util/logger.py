@@ -1,130 +1,166 @@
-"""Hierarchical logger (reference: ``src/imitation/util/logger.py``; SURVEY §5.5).
+"""Hierarchical logger (reference: ``src/imitation/util/logger.py``; SURVEY C20, §5.5).
 
-``HierarchicalLogger.accumulate_means(name)`` routes ``record`` calls to a cached
-sub-logger under ``<dir>/raw/<prefixes>/<name>`` (key ``raw/.../key``) while
-``record_mean``-ing them into the root logger under ``mean/.../key``
-(``logger.py:290-315``). Nested contexts raise; ``add_accumulate_prefix`` only
-outside, ``add_key_prefix`` only inside the context (``:161-217``).
+Same observable behaviour as the reference's ``HierarchicalLogger``: inside
+``accumulate_means(name)`` every ``record(key, v)`` is written to a per-scope sub-logger
+as ``raw/<accumulate prefixes>/<name>/<key prefixes>/<key>`` (output files under
+``<dir>/raw/<prefixes>/<name>/``) and averaged into the root logger as
+``mean/<...same path...>/<key>``; outside a scope ``record`` goes to the root.
+``add_accumulate_prefix`` is only legal outside a scope, ``add_key_prefix`` only inside,
+and scopes do not nest.
 
-Distributed runs: only rank 0 writes files/stdout (other ranks get a logger
-with no output formats), so metric keys and on-disk layout match the reference.
+Organisation here: the active scope is one :class:`_Scope` value (name, sub-logger, key
+prefixes) instead of parallel mutable fields, sub-loggers come from a
+:class:`_SubLoggerCache` keyed by their directory, and key paths are built by one helper.
+Data parallel runs: only rank 0 writes (other ranks get loggers without output formats),
+so metric keys and the on-disk layout are independent of the world size.
 """
 
 from __future__ import annotations
 
 import contextlib
+import dataclasses
 import datetime
 import os
 import pathlib
 import sys
 import tempfile
-from typing import Any, Dict, Generator, List, Optional, Sequence, Tuple
+from typing import Dict, Iterator, List, Optional, Sequence
 
 from imitation_amd.rl import logger as sb_logger
 
+DEFAULT_FORMATS = ("stdout", "log", "csv")
+
 
 def make_output_format(_format: str, log_dir: str, log_suffix: str = "", max_length: int = 50) -> sb_logger.KVWriter:
+    """One SB3-style writer; ``stdout`` / ``log`` use a wider key column than SB3's default."""
     os.makedirs(log_dir, exist_ok=True)
-    if _format == "stdout":
-        return sb_logger.HumanOutputFormat(sys.stdout, max_length=max_length)
-    if _format == "log":
-        return sb_logger.HumanOutputFormat(os.path.join(log_dir, f"log{log_suffix}.txt"), max_length=max_length)
+    if _format in ("stdout", "log"):
+        target = sys.stdout if _format == "stdout" else os.path.join(log_dir, f"log{log_suffix}.txt")
+        return sb_logger.HumanOutputFormat(target, max_length=max_length)
     return sb_logger.make_output_format(_format, log_dir, log_suffix)
 
 
-def _build_output_formats(folder: pathlib.Path, format_strs: Sequence[str]) -> Sequence[sb_logger.KVWriter]:
+def _build_output_formats(folder: pathlib.Path, format_strs: Sequence[str]) -> List[sb_logger.KVWriter]:
     folder.mkdir(parents=True, exist_ok=True)
-    out: List[sb_logger.KVWriter] = []
-    for f in format_strs:
-        if f == "wandb":
-            out.append(WandbOutputFormat())
-        else:
-            out.append(make_output_format(f, str(folder)))
-    return out
+    return [WandbOutputFormat() if f == "wandb" else make_output_format(f, str(folder)) for f in format_strs]
+
+
+def _key(kind: str, accumulate: Sequence[str], name: str, key_prefixes: Sequence[str], key: str) -> str:
+    return "/".join([kind, *accumulate, name, *key_prefixes, key])
+
+
+@dataclasses.dataclass
+class _Scope:
+    """The active ``accumulate_means`` context."""
+
+    name: str
+    subdir: str
+    logger: sb_logger.Logger
+    key_prefixes: List[str] = dataclasses.field(default_factory=list)
+
+
+class _SubLoggerCache:
+    """Sub-loggers of the ``raw/...`` scopes, created on first use and kept for reuse."""
+
+    def __init__(self, root_dir: Optional[str], format_strs: Sequence[str]):
+        self.root_dir = root_dir
+        self.format_strs = list(format_strs)
+        self.loggers: Dict[str, sb_logger.Logger] = {}
+
+    def get(self, subdir: str) -> sb_logger.Logger:
+        lg = self.loggers.get(subdir)
+        if lg is None:
+            assert self.root_dir is not None
+            folder = pathlib.Path(self.root_dir) / "raw" / subdir
+            folder.mkdir(exist_ok=True, parents=True)
+            lg = sb_logger.Logger(str(folder), _build_output_formats(folder, self.format_strs))
+            self.loggers[subdir] = lg
+        return lg
+
+    def close(self) -> None:
+        for lg in self.loggers.values():
+            lg.close()
 
 
 class HierarchicalLogger(sb_logger.Logger):
-    """Logger with ``accumulate_means`` sub-logger contexts (see module docstring)."""
+    """SB3 logger with ``accumulate_means`` scopes (module docstring)."""
 
-    def __init__(self, default_logger: sb_logger.Logger, format_strs: Sequence[str] = ("stdout", "log", "csv")):
+    def __init__(self, default_logger: sb_logger.Logger, format_strs: Sequence[str] = DEFAULT_FORMATS):
         self.default_logger = default_logger
-        self.current_logger: Optional[sb_logger.Logger] = None
-        self._cached_loggers: Dict[str, sb_logger.Logger] = {}
-        self._accumulate_prefixes: List[str] = []
-        self._key_prefixes: List[str] = []
-        self._subdir: Optional[str] = None
-        self._name: Optional[str] = None
         self.format_strs = format_strs
-        super().__init__(folder=self.default_logger.dir, output_formats=[])
+        self._subloggers = _SubLoggerCache(default_logger.dir, format_strs)
+        self._accumulate_prefixes: List[str] = []
+        self._scope: Optional[_Scope] = None
+        super().__init__(folder=default_logger.dir, output_formats=[])
+        self._sync_maps()
 
-    def _update_name_to_maps(self) -> None:
-        self.name_to_value = self._logger.name_to_value
-        self.name_to_count = self._logger.name_to_count
-        self.name_to_excluded = self._logger.name_to_excluded
+    # ------------------------------------------------------------------ scope state
+    @property
+    def current_logger(self) -> Optional[sb_logger.Logger]:
+        return self._scope.logger if self._scope is not None else None
 
+    @property
+    def _logger(self) -> sb_logger.Logger:
+        return self._scope.logger if self._scope is not None else self.default_logger
+
+    def _sync_maps(self) -> None:
+        """``name_to_*`` are those of whichever logger is active (as in the reference)."""
+        lg = self._logger
+        self.name_to_value, self.name_to_count, self.name_to_excluded = lg.name_to_value, lg.name_to_count, lg.name_to_excluded
+
+    # ------------------------------------------------------------------ prefixes / scopes
     @contextlib.contextmanager
-    def add_accumulate_prefix(self, prefix: str) -> Generator[None, None, None]:
-        if self.current_logger is not None:
+    def add_accumulate_prefix(self, prefix: str) -> Iterator[None]:
+        """Prefix the scope path of every ``accumulate_means`` opened inside (outside scopes only)."""
+        if self._scope is not None:
             raise RuntimeError("Cannot add prefix when accumulate_means context is already active.")
+        self._accumulate_prefixes.append(prefix)
         try:
-            self._accumulate_prefixes.append(prefix)
             yield
         finally:
             self._accumulate_prefixes.pop()
 
     def get_accumulate_prefixes(self) -> str:
-        prefixes = "/".join(self._accumulate_prefixes)
-        return prefixes + "/" if prefixes else ""
+        joined = "/".join(self._accumulate_prefixes)
+        return joined + "/" if joined else ""
 
     @contextlib.contextmanager
-    def add_key_prefix(self, prefix: str) -> Generator[None, None, None]:
-        if self.current_logger is None:
+    def add_key_prefix(self, prefix: str) -> Iterator[None]:
+        """Prefix the keys recorded inside the active scope."""
+        if self._scope is None:
             raise RuntimeError("Cannot add key prefix when accumulate_means context is not active.")
+        self._scope.key_prefixes.append(prefix)
         try:
-            self._key_prefixes.append(prefix)
             yield
         finally:
-            self._key_prefixes.pop()
+            self._scope.key_prefixes.pop()
 
     @contextlib.contextmanager
-    def accumulate_means(self, name: str) -> Generator[None, None, None]:
-        if self.current_logger is not None:
+    def accumulate_means(self, name: str) -> Iterator[None]:
+        """Route records to the ``raw/.../name`` sub-logger and their means to the root."""
+        if self._scope is not None:
             raise RuntimeError("Nested `accumulate_means` context")
         subdir = os.path.join(*self._accumulate_prefixes, name)
-        if subdir in self._cached_loggers:
-            logger = self._cached_loggers[subdir]
-        else:
-            assert self.default_logger.dir is not None
-            folder = pathlib.Path(self.default_logger.dir) / "raw" / subdir
-            folder.mkdir(exist_ok=True, parents=True)
-            fmts = _build_output_formats(folder, self.format_strs)
-            logger = sb_logger.Logger(str(folder), list(fmts))
-            self._cached_loggers[subdir] = logger
+        self._scope = _Scope(name=name, subdir=subdir, logger=self._subloggers.get(subdir))
+        self._sync_maps()
         try:
-            self.current_logger = logger
-            self._subdir = subdir
-            self._name = name
-            self._update_name_to_maps()
             yield
         finally:
-            self.current_logger = None
-            self._subdir = None
-            self._name = None
-            self._update_name_to_maps()
+            self._scope = None
+            self._sync_maps()
 
+    # ------------------------------------------------------------------ recording
     def record(self, key, val, exclude=None):
-        if self.current_logger is not None:
-            assert self._subdir is not None
-            raw_key = "/".join(["raw", *self._accumulate_prefixes, self._name, *self._key_prefixes, key])
-            self.current_logger.record(raw_key, val, exclude)
-            mean_key = "/".join(["mean", *self._accumulate_prefixes, self._name, *self._key_prefixes, key])
-            self.default_logger.record_mean(mean_key, val, exclude)
-        else:
+        scope = self._scope
+        if scope is None:
             self.default_logger.record(key, val, exclude)
+            return
+        scope.logger.record(_key("raw", self._accumulate_prefixes, scope.name, scope.key_prefixes, key), val, exclude)
+        self.default_logger.record_mean(_key("mean", self._accumulate_prefixes, scope.name, scope.key_prefixes, key), val,
+                                        exclude)
 
-    @property
-    def _logger(self):
-        return self.current_logger if self.current_logger is not None else self.default_logger
+    def record_mean(self, key, val, exclude=None):
+        self.default_logger.record_mean(key, val, exclude)
 
     def dump(self, step=0):
         self._logger.dump(step)
@@ -138,17 +174,17 @@ class HierarchicalLogger(sb_logger.Logger):
     def set_level(self, level: int) -> None:
         self.default_logger.set_level(level)
 
-    def record_mean(self, key, val, exclude=None):
-        self.default_logger.record_mean(key, val, exclude)
-
     def close(self):
         self.default_logger.close()
-        for logger in self._cached_loggers.values():
-            logger.close()
+        self._subloggers.close()
+
+    @property
+    def _cached_loggers(self) -> Dict[str, sb_logger.Logger]:
+        return self._subloggers.loggers
 
 
 class WandbOutputFormat(sb_logger.KVWriter):
-    """Weights & Biases writer (requires ``wandb``, which is optional)."""
+    """Weights & Biases writer (``wandb`` is optional and not installed here)."""
 
     def __init__(self):
         try:
@@ -160,33 +196,28 @@ class WandbOutputFormat(sb_logger.KVWriter):
         self.wandb_module = wandb
 
     def write(self, key_values, key_excluded, step=0):  # pragma: no cover - needs wandb
-        for (key, value), (key_ex, excluded) in zip(sorted(key_values.items()), sorted(key_excluded.items())):
-            assert key == key_ex
-            if excluded is not None and "wandb" in excluded:
-                continue
-            self.wandb_module.log({key: value}, step=step)
+        payload = {k: v for k, v in sorted(key_values.items())
+                   if not (key_excluded.get(k) is not None and "wandb" in key_excluded[k])}
+        for k, v in payload.items():
+            self.wandb_module.log({k: v}, step=step)
         self.wandb_module.log({}, commit=True)
 
     def close(self) -> None:  # pragma: no cover
         self.wandb_module.finish()
 
 
+def _default_folder() -> str:
+    stamp = datetime.datetime.now().strftime("imitation-%Y-%m-%d-%H-%M-%S-%f")
+    return os.path.join(tempfile.gettempdir(), stamp)
+
+
 def configure(folder=None, format_strs: Optional[Sequence[str]] = None) -> HierarchicalLogger:
-    """Configure a :class:`HierarchicalLogger` (library default formats stdout/log/csv)."""
-    if folder is None:
-        tempdir = tempfile.gettempdir()
-        now = datetime.datetime.now()
-        timestamp = now.strftime("imitation-%Y-%m-%d-%H-%M-%S-%f")
-        folder = os.path.join(tempdir, timestamp)
-    folder = str(folder)
-    if format_strs is None:
-        format_strs = ["stdout", "log", "csv"]
+    """A :class:`HierarchicalLogger` writing to ``folder`` (a fresh temp dir by default) with
+    ``format_strs`` (library default stdout/log/csv); DP ranks other than 0 write nothing."""
     from imitation_amd.parallel import dist as pdist
 
+    folder = str(folder) if folder is not None else _default_folder()
+    formats = list(DEFAULT_FORMATS if format_strs is None else format_strs)
     if pdist.rank() != 0:
-        # Non-zero DP ranks keep the API but write nothing.
-        default_logger = sb_logger.Logger(folder, [])
-        return HierarchicalLogger(default_logger, [])
-    output_formats = _build_output_formats(pathlib.Path(folder), format_strs)
-    default_logger = sb_logger.Logger(folder, list(output_formats))
-    return HierarchicalLogger(default_logger, format_strs)
+        return HierarchicalLogger(sb_logger.Logger(folder, []), [])
+    return HierarchicalLogger(sb_logger.Logger(folder, _build_output_formats(pathlib.Path(folder), formats)), formats)
