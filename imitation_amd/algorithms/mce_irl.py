@@ -118,21 +118,23 @@ class TabularPolicy(BasePolicy):
         raise NotImplementedError("Should never be called.")  # pragma: no cover
 
     def predict(self, observation, state=None, episode_start=None, deterministic: bool = False):
-        if state is None:
-            timesteps = np.zeros(len(observation), dtype=int)
-        else:
+        """Actions for a batch of states from the time-indexed policy table; ``state`` carries
+        each env's timestep (starts at 0, reset where ``episode_start``)."""
+        obs = np.asarray(observation)
+        t = np.zeros(len(obs), dtype=int) if state is None else np.asarray(state[0])
+        if state is not None:
             assert len(state) == 1
-            timesteps = state[0]
-        assert len(timesteps) == len(observation), "timestep and obs batch size differ"
+        assert len(t) == len(obs), "timestep and obs batch size differ"
         if episode_start is not None:
-            timesteps[episode_start] = 0
-        actions: List[int] = []
-        for obs, t in zip(observation, timesteps):
-            assert self.observation_space.contains(obs), "illegal state"
-            dist = self.pi[t, obs, :]
-            actions.append(int(dist.argmax()) if deterministic else self.rng.choice(len(dist), p=dist))
-        timesteps += 1
-        return np.array(actions), (timesteps,)
+            t[np.asarray(episode_start, dtype=bool)] = 0
+        assert all(self.observation_space.contains(o) for o in obs), "illegal state"
+        probs = self.pi[t, obs]  # [B, A] gathered in one indexing op
+        if deterministic:
+            acts = probs.argmax(axis=1)
+        else:  # inverse-CDF sampling per row, one uniform draw each
+            u = self.rng.random(len(obs))[:, None]
+            acts = np.minimum((probs.cumsum(axis=1) < u).sum(axis=1), probs.shape[1] - 1)
+        return acts.astype(int), (t + 1,)
 
 
 MCEDemonstrations = Union[np.ndarray, base.AnyTransitions]
@@ -164,33 +166,30 @@ class MCEIRL(base.DemonstrationAlgorithm[types.TransitionsMinimal]):
         self._policy = TabularPolicy(state_space=self.env.state_space, action_space=self.env.action_space, pi=uniform_pi, rng=self.rng)
 
     def _set_demo_from_trajectories(self, trajs: Iterable[types.Trajectory]) -> None:
-        self.demo_state_om = np.zeros((self.env.state_dim,))
-        num_demos = 0
+        """Discounted state visitation counts averaged over demonstrations (one bincount
+        per trajectory with weights ``discount ** t``)."""
+        S = self.env.state_dim
+        om = np.zeros(S)
+        n = 0
         for traj in trajs:
-            cum_discount = 1.0
-            for obs in types.assert_not_dictobs(traj.obs):
-                self.demo_state_om[obs] += cum_discount
-                cum_discount *= self.discount
-            num_demos += 1
-        self.demo_state_om /= num_demos
+            states = np.asarray(types.assert_not_dictobs(traj.obs)).astype(int).reshape(-1)
+            om += np.bincount(states, weights=self.discount ** np.arange(len(states)), minlength=S)
+            n += 1
+        self.demo_state_om = om / n
 
     def _set_demo_from_obs(self, obses: np.ndarray, dones: Optional[np.ndarray], next_obses: Optional[np.ndarray]) -> None:
-        self.demo_state_om = np.zeros((self.env.state_dim,))
-        for obs in obses:
-            if isinstance(obs, th.Tensor):
-                obs = obs.item()
-            self.demo_state_om[obs] += 1.0
+        """Undiscounted visitation counts of transition data (terminal next-states included),
+        rescaled to a horizon-``H`` trajectory's total mass ``H + 1``."""
+        S = self.env.state_dim
+        as_int = lambda a: np.asarray(a.cpu() if isinstance(a, th.Tensor) else a).astype(int).reshape(-1)  # noqa: E731
+        om = np.bincount(as_int(obses), minlength=S).astype(float)
         if dones is not None and next_obses is not None:
-            for done, obs in zip(dones, next_obses):
-                if isinstance(done, th.Tensor):
-                    done = done.item()
-                    obs = obs.item()
-                if done:
-                    self.demo_state_om[obs] += 1.0
+            done = np.asarray(dones.cpu() if isinstance(dones, th.Tensor) else dones).astype(bool).reshape(-1)
+            om += np.bincount(as_int(next_obses)[done], minlength=S)
         else:
             warnings.warn("Training MCEIRL with transitions that lack next observation."
                           "This will result in systematically wrong occupancy measure estimates.")
-        self.demo_state_om *= (self.env.horizon + 1) / self.demo_state_om.sum()
+        self.demo_state_om = om * (self.env.horizon + 1) / om.sum()
 
     def set_demonstrations(self, demonstrations: MCEDemonstrations) -> None:
         if isinstance(demonstrations, np.ndarray):

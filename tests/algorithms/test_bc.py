@@ -133,3 +133,41 @@ def test_bc_graph_replay_matches_eager(monkeypatch, env_id):
         out.append([p.detach().clone() for p in tr.policy.parameters()])
     for a, b in zip(*out):
         th.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_multibc_trains_on_agent_concatenated_batches():
+    """MultiBC (fork addition, reference bc.py:512-776): every minibatch is the agents' slices
+    concatenated along the batch axis (bc.py:758-759) -- its loss equals BC's loss on that
+    concatenation -- and training learns a per-agent rule shared by both agents."""
+    import torch as th
+
+    from imitation_amd.algorithms import bc
+    from imitation_amd.data import types
+    from imitation_amd.envs import spaces
+    from imitation_amd.util import logger
+
+    rng = np.random.default_rng(0)
+    d, n_agents, N = 3, 2, 512
+    obs = rng.standard_normal((N, d * n_agents)).astype(np.float32)
+    acts = np.stack([(obs[:, d * i] > 0).astype(np.int64) for i in range(n_agents)], axis=1)  # action = sign of feature 0
+    obs_over = lambda i, o: o[:, d * i: d * i + d]  # noqa: E731
+    act_over = lambda i, a: a[:, i]  # noqa: E731
+    demos = types.TransitionsMinimal(obs=obs, acts=acts, infos=np.array([{}] * N))
+    th.manual_seed(0)
+    trainer = bc.MultiBC(single_agent_observation_space=spaces.Box(-10, 10, (d,)), single_agent_action_space=spaces.Discrete(2),
+                         observation_overide=obs_over, action_overide=act_over, num_agents=n_agents,
+                         rng=np.random.default_rng(0), demonstrations=demos, batch_size=64,
+                         optimizer_kwargs=dict(lr=3e-3), custom_logger=logger.configure(format_strs=[]))
+    batch = {"obs": obs[:8], "acts": th.as_tensor(acts[:8])}
+    o_cat, a_cat = trainer._prepare_batch(batch)
+    assert o_cat.shape == (16, d) and a_cat.shape == (16,)
+    np.testing.assert_array_equal(o_cat.numpy(), np.concatenate([obs[:8, :d], obs[:8, d:]]))
+    np.testing.assert_array_equal(a_cat.numpy(), np.concatenate([acts[:8, 0], acts[:8, 1]]))
+    m1 = trainer.loss_calculator(trainer.policy, o_cat, a_cat)
+    m2 = trainer.loss_calculator(trainer.policy, th.as_tensor(np.concatenate([obs[:8, :d], obs[:8, d:]])),
+                                 th.as_tensor(np.concatenate([acts[:8, 0], acts[:8, 1]])))
+    th.testing.assert_close(m1.loss, m2.loss)
+    trainer.train(n_epochs=15, progress_bar=False, log_interval=10**9)
+    pred, _ = trainer.policy.predict(obs, deterministic=True)
+    assert pred.shape == (N, n_agents)
+    assert (pred == acts).mean() > 0.9
