@@ -81,7 +81,7 @@ def load(path: AnyPath, allow_pickle: bool = False) -> Sequence[Trajectory]:
     import pickle
 
     with open(path, "rb") as f:  # pragma: no cover - explicit opt-in only
-        data = pickle.load(f)
+        data = pickle.load(f)  # noqa: pickle -- explicit allow_pickle=True opt-in
     warnings.warn("Loading old pickle version of Trajectories", DeprecationWarning)
     return data
 

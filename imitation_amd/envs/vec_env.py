@@ -344,7 +344,7 @@ class _CloudpickleWrapper:
         return cloudpickle.dumps(self.fn)
 
     def __setstate__(self, state):
-        self.fn = cloudpickle.loads(state)
+        self.fn = cloudpickle.loads(state)  # noqa: pickle -- our own env factories, parent -> worker
 
     def __call__(self):
         return self.fn()
