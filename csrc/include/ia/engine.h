@@ -173,6 +173,7 @@ struct PPORcGeo {
   int ls_off, lsp_off, nm_off, red_off, param_lds;
   int zero_off;  // 64 floats of zeros (never written): operand of the padding dW items
   int n_items;
+  int n_witems;            // items [0, n_witems) are dW tiles
   int items[kMaxRcItems];  // q | layer << 1 | kind << 3 (0 W tile, 1 bias, 2 log_std) | out tile << 5 | in tile << 9
   int dp;                  // padded obs row stride of xraw
   int kt;                  // 16-wide tiles per hidden layer (2: width <= 32, 4: width <= 64)

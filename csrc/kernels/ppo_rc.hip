@@ -19,8 +19,11 @@
 //   moments; the kernel only Chan-merges those moments (one lane per feature) one
 //   minibatch ahead.
 // * dW (K = rows) needs rows along K, i.e. a transpose: layer inputs and dZ are
-//   stored row-major in LDS once, then every wave computes whole dW tiles over all
-//   rows for the parameter "items" it owns. The owner keeps that tile's gradient and
+//   stored K-major in LDS once ([column][permuted row], row r at (r & 3) * cw/4 + r / 4,
+//   so the rows 4s + kk that lane group kk feeds to MFMA step s are contiguous and one
+//   ds_read_b128 serves four steps), then every wave computes whole dW tiles over all
+//   rows for the parameter "items" it owns -- all of its weight tiles interleaved, so
+//   their MFMA chains hide each other's latency. The owner keeps that tile's gradient and
 //   Adam moments in registers, so after the grad-norm reduction Adam updates W in
 //   LDS in place -- there is no gradient image at all.
 //
@@ -254,6 +257,48 @@ __device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int ro
   r.rd = *reinterpret_cast<const f4*>(g.rowd + (slot * 64 + row) * 4);
 }
 
+// dW tiles of this wave's N weight items over one chunk (K = cw rows): acc[i] = dZ^T H for
+// item i. Operand columns are K-major (see header), so each lane reads 4 MFMA steps per
+// 16-byte LDS load; the N accumulation chains are interleaved step by step.
+template <int N, int CWT>
+__device__ __forceinline__ void dw_tiles(const lf* L, const int* izo, const int* iho, int cw, f4* acc) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc[i] = {0.f, 0.f, 0.f, 0.f};
+  const int ng = (CWT > 0 ? CWT : cw) >> 4;
+#pragma unroll
+  for (int gi = 0; gi < (CWT > 0 ? CWT / 16 : 4); ++gi) {
+    if (CWT == 0 && gi >= ng) break;
+    f4 z[N], h[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      z[i] = *(const lf4*)(L + izo[i] + 4 * gi);
+      h[i] = *(const lf4*)(L + iho[i] + 4 * gi);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      acc[i] = mfma(z[i].x, h[i].x, acc[i]);
+      acc[i] = mfma(z[i].y, h[i].y, acc[i]);
+      acc[i] = mfma(z[i].z, h[i].z, acc[i]);
+      acc[i] = mfma(z[i].w, h[i].w, acc[i]);
+    }
+  }
+}
+
+template <int KI, int CWT>
+__device__ __forceinline__ void dw_tiles_n(const lf* L, const int* izo, const int* iho, int cw, int n, f4* acc) {
+  switch (n) {
+    case 1: dw_tiles<1, CWT>(L, izo, iho, cw, acc); break;
+    case 2: dw_tiles<(KI >= 2 ? 2 : 1), CWT>(L, izo, iho, cw, acc); break;
+    case 3: dw_tiles<(KI >= 3 ? 3 : 1), CWT>(L, izo, iho, cw, acc); break;
+    case 4: dw_tiles<(KI >= 4 ? 4 : 1), CWT>(L, izo, iho, cw, acc); break;
+    case 5: dw_tiles<(KI >= 5 ? 5 : 1), CWT>(L, izo, iho, cw, acc); break;
+    case 6: dw_tiles<(KI >= 6 ? 6 : 1), CWT>(L, izo, iho, cw, acc); break;
+    case 7: dw_tiles<(KI >= 7 ? 7 : 1), CWT>(L, izo, iho, cw, acc); break;
+    case 8: dw_tiles<(KI >= 8 ? 8 : 1), CWT>(L, izo, iho, cw, acc); break;
+    default: break;
+  }
+}
+
 // Shape specialisation: S0T (16-wide input k-steps / 4), NLT (layers per net), ACTT (hidden
 // activation), HWT (hidden width) fold the per-layer loop bounds, tile counts and the
 // activation switch at compile time; 0 / -1 = read them at run time (generic build).
@@ -363,22 +408,23 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     L[g.nm_off + 64 + nc] = rsqrtf(run_v + a.norm_eps);
   }
   // dW item operands (LDS offsets of this lane's dZ / H columns; padding items read zeros)
-  int izo[KI], izs[KI], iho[KI], ihs[KI], imask[KI];
+  // (weight items are ids [0, n_witems): this wave's are its first nwi slots)
+  const int n_witems = rfl(g.n_witems);
+  const int nwi = n_witems > w ? min(KI, (n_witems - w + kWaves - 1) / kWaves) : 0;
+  const int rq = cw / 4;  // K-major image: row r at (r & 3) * rq + (r >> 2)
+  int izo[KI], iho[KI], imask[KI];
 #pragma unroll
   for (int it = 0; it < KI; ++it) {
     const int id = w + it * kWaves;
-    izo[it] = iho[it] = g.zero_off + r16;
-    izs[it] = ihs[it] = 0;
+    izo[it] = iho[it] = g.zero_off;
     imask[it] = 0;
     if (id < n_items) {
       const int desc = rfl(g.items[id]);
       const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
       if (kind == 0) {
         const LG y = lg(g, iq, il);
-        izo[it] = y.z + kk * y.ldz + 16 * ta + r16;
-        iho[it] = y.h + kk * y.ldh + 16 * tb + r16;
-        izs[it] = 4 * y.ldz;
-        ihs[it] = 4 * y.ldh;
+        izo[it] = y.z + (16 * ta + r16) * y.ldz + kk * rq;
+        iho[it] = y.h + (16 * tb + r16) * y.ldh + kk * rq;
         const int in = 16 * tb + r16;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -422,10 +468,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   }
   Rows cur;
   const int row = 16 * gw + r16;
+  const int rp = (row & 3) * rq + (row >> 2);  // this lane's row in the K-major images
   // chunk unit u = k * nch + ch -> prep slot k * CH + grp * nch + ch
   auto slot_of = [&](int u) -> size_t { return (size_t)(u / nch) * CH + (size_t)grp * nch + (u % nch); };
   if (rows_wave && K > 0) load_rows(g, slot_of(0), row, kk, s0, cur);
-  unsigned long long prof[3] = {0, 0, 0};
+  unsigned long long prof[5] = {0, 0, 0, 0, 0};  // chunk, exchange+|g|^2, clip+Adam; wave 0: B1 wait, dW items
   unsigned long long wprof[4] = {0, 0, 0, 0};  // this wave: rows/x, forward, loss, backward chain
   unsigned* arrive = g.sync;
   unsigned* tflag = g.sync + 1;
@@ -470,7 +517,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
 #pragma unroll
           for (int s = 0; s < 16; ++s)
-            if (s < s0) L[h0 + row * ld0 + 4 * s + kk] = xb[s];
+            if (s < s0) L[h0 + (4 * s + kk) * ld0 + rp] = xb[s];
         }
         unsigned long long c1 = a.prof ? clock64() : 0;
         // ---------------- forward (registers)
@@ -520,7 +567,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
                 hreg[l][t] = v;
                 // input image of layer l + 1 (for its dW)
                 const LG yn = lg(g, q, l + 1);
-                *(lf4*)(L + yn.h + row * yn.ldh + o0) = v;
+                lf* hp = L + yn.h + o0 * yn.ldh + rp;
+                hp[0] = v.x;
+                hp[yn.ldh] = v.y;
+                hp[2 * yn.ldh] = v.z;
+                hp[3 * yn.ldh] = v.w;
               }
             } else if (t == 0) {
               head = v;
@@ -639,7 +690,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) {
             if (u2 >= tout) continue;
-            *(lf4*)(L + y.z + row * y.ldz + 16 * u2 + 4 * kk) = dzc[u2];
+            lf* zp = L + y.z + (16 * u2 + 4 * kk) * y.ldz + rp;
+            zp[0] = dzc[u2].x;
+            zp[y.ldz] = dzc[u2].y;
+            zp[2 * y.ldz] = dzc[u2].z;
+            zp[3 * y.ldz] = dzc[u2].w;
             const float s0v = sum16(dzc[u2].x), s1v = sum16(dzc[u2].y), s2v = sum16(dzc[u2].z), s3v = sum16(dzc[u2].w);
             if (r16 == 0) {
               const f4 sv = {s0v, s1v, s2v, s3v};
@@ -680,7 +735,9 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           wprof[3] += c4 - c3;
         }
       }
+      const unsigned long long cb0 = a.prof ? clock64() : 0;
       __syncthreads();  // B1: H / dZ images, bias and log-std partials of this chunk complete
+      const unsigned long long cb1 = a.prof ? clock64() : 0;
       // Chan merge for minibatch k+1 (one lane per feature, wave 7), off the chain's critical
       // path; minibatch k reads the other half of the double-buffered normaliser image
       if (ch == 0 && norm_lane && k + 1 < K) {
@@ -694,26 +751,32 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       }
 
       // ---------------- dW / db / dlog_std partials of this chunk for the owned items
+      {
+        f4 acc[KI];
+        dw_tiles_n<KI, CWT>(L, izo, iho, cw, nwi, acc);
+#pragma unroll
+        for (int it = 0; it < KI; ++it) {
+          if (it >= nwi) continue;
+          gg[it][0] += (imask[it] & 1) ? acc[it].x : 0.f;
+          gg[it][1] += (imask[it] & 2) ? acc[it].y : 0.f;
+          gg[it][2] += (imask[it] & 4) ? acc[it].z : 0.f;
+          gg[it][3] += (imask[it] & 8) ? acc[it].w : 0.f;
+        }
+      }
 #pragma unroll
       for (int it = 0; it < KI; ++it) {
-        if (ikind[it] < 0) continue;
-        if (ikind[it] == 0) {
-          f4 acc = {0.f, 0.f, 0.f, 0.f};
-          const lf* zp = L + izo[it];
-          const lf* hp = L + iho[it];
-#pragma unroll 4
-          for (int s = 0; s < cw / 4; ++s) acc = mfma(zp[s * izs[it]], hp[s * ihs[it]], acc);
-          gg[it][0] += (imask[it] & 1) ? acc.x : 0.f;
-          gg[it][1] += (imask[it] & 2) ? acc.y : 0.f;
-          gg[it][2] += (imask[it] & 4) ? acc.z : 0.f;
-          gg[it][3] += (imask[it] & 8) ? acc.w : 0.f;
-        } else {  // bias (row-tile partials of dZ) / log_std (partials of the Gaussian term)
+        if (ikind[it] <= 0) continue;
+        {  // bias (row-tile partials of dZ) / log_std (partials of the Gaussian term)
           const int stride = ikind[it] == 1 ? 64 : 16;
           float gval = 0.f;
           if (ib_ok[it])
             for (int r = 0; r < RT; ++r) gval += L[ib_off[it] + r * stride + lane];
           gg[it][0] += gval;
         }
+      }
+      if (a.prof) {
+        prof[3] += cb1 - cb0;
+        prof[4] += clock64() - cb1;
       }
       if (rows_wave) cur = nxt;
       if (ch + 1 < nch) __syncthreads();  // images are rewritten by the next chunk
@@ -903,6 +966,8 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     a.prof[0] += prof[0];
     a.prof[1] += prof[1];
     a.prof[2] += prof[2];
+    a.prof[11] += prof[3];
+    a.prof[12] += prof[4];
   }
   if (a.prof && lane == 0 && (w == 0 || w == 4)) {  // actor / critic row tile 0
     for (int i = 0; i < 4; ++i) a.prof[3 + (w == 4 ? 4 : 0) + i] += wprof[i];
@@ -970,20 +1035,21 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.ls_off = take(16);
   g.zero_off = take(64);
   g.param_lds = off;
-  // activation images (cw rows): layer-0 input shared by both nets
-  const int ld0 = ((a.D + 15) & ~15) + 4;
-  const int h0 = take(cw * ld0);
+  // activation images, K-major: [column (16-padded)][cw rows + 4] (the +4 keeps the
+  // 16 lanes of one b128 read on distinct banks); layer-0 input shared by both nets
+  const int ldr = cw + 4;
+  const int h0 = take(((a.D + 15) & ~15) * ldr);
   for (int q = 0; q < 2; ++q) {
     for (int l = 0; l < nls[q]; ++l) {
       if (l == 0) {
         g.h_off[q][0] = h0;
-        g.ldh[q][0] = ld0;
+        g.ldh[q][0] = ldr;
       } else {
-        g.ldh[q][l] = ((g.din[q][l] + 15) & ~15) + 4;
-        g.h_off[q][l] = take(cw * g.ldh[q][l]);
+        g.ldh[q][l] = ldr;
+        g.h_off[q][l] = take(((g.din[q][l] + 15) & ~15) * ldr);
       }
-      g.ldz[q][l] = ((g.dout[q][l] + 15) & ~15) + 4;
-      g.z_off[q][l] = take(cw * g.ldz[q][l]);
+      g.ldz[q][l] = ldr;
+      g.z_off[q][l] = take(((g.dout[q][l] + 15) & ~15) * ldr);
       g.db_off[q][l] = take(4 * 64);
     }
   }
@@ -992,7 +1058,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.red_off = take(8 + 8 * 5);
   lds_bytes = (size_t)off * 4;
   if (lds_bytes > 160 * 1024) return false;
-  // items: dW tiles, biases, log_std
+  // items: dW tiles first (ids [0, n_witems): a wave's weight items are its first slots),
+  // then biases, then log_std
   int n = 0;
   for (int q = 0; q < 2; ++q) {
     for (int l = 0; l < nls[q]; ++l) {
@@ -1002,6 +1069,11 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
           if (n >= kMaxRcItems) return false;
           g.items[n++] = q | (l << 1) | (0 << 3) | (ta << 5) | (tb << 9);
         }
+    }
+  }
+  g.n_witems = n;
+  for (int q = 0; q < 2; ++q) {
+    for (int l = 0; l < nls[q]; ++l) {
       if (n >= kMaxRcItems) return false;
       g.items[n++] = q | (l << 1) | (1 << 3);
     }

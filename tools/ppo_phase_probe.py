@@ -40,6 +40,7 @@ def main():
     names = ["chunk(fwd+loss+bwd+dW)", "exchange+|g|^2", "clip+adam"]
     for i, nm in enumerate(names):
         print(f"{nm:>26s}: {p[i] / K:9.0f} cycles/minibatch", flush=True)
+    print(f"wave 0: B1 wait {p[11] / K:.0f} dW items {p[12] / K:.0f}", flush=True)
     for w, base in (("actor", 3), ("critic", 7)):
         parts = ["rows/x", "forward", "loss", "bwd chain"]
         print(w, " ".join(f"{parts[i]}={p[base + i] / K:.0f}" for i in range(4)), flush=True)

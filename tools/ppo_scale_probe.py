@@ -47,6 +47,13 @@ def main():
         th.cuda.synchronize()
         dt = (time.perf_counter() - t0) / n
         print(f"W={W} path={path} rows={tr.T * tr.N} batch={64 * W}: ppo update {1e3 * dt:.3f} ms", flush=True)
+        prof = th.zeros(16, dtype=th.int64, device="cuda")
+        tr._ppo_static["prof"] = prof
+        tr._ppo_update()
+        th.cuda.synchronize()
+        p = prof.cpu().numpy().astype(np.float64) / tr._last_ppo_info[1]
+        print(f"    cycles/minibatch (workgroup 0): chunk {p[0]:.0f} exchange+|g|^2 {p[1]:.0f} clip+adam {p[2]:.0f} | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f}", flush=True)
+        tr._ppo_static.pop("prof")
 
 
 if __name__ == "__main__":
