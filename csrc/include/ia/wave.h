@@ -92,11 +92,12 @@ __device__ __forceinline__ float add_halves(float v) {
 __device__ __forceinline__ float wave_sum(float v) { return add_halves(add_rows16(row_sum16(v))); }
 __device__ __forceinline__ float wave_max(float v) { return max_halves(max_rows16(row_max16(v))); }
 
-// tanh as 1 - 2 / (exp(2x) + 1) on v_exp_f32 / v_rcp_f32 (|err| ~1e-7 abs).
+// tanh as 1 - 2 / (exp(2x) + 1) on v_exp_f32 / v_rcp_f32 (|err| ~2e-7 abs; the hardware
+// reciprocal, not the ~11-instruction IEEE divide sequence)
 __device__ __forceinline__ float act_fast(int act, float x) {
   if (act == ACT_TANH) {
     const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
-    return 1.f - 2.f * __frcp_rn(e + 1.f);
+    return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
   }
   return apply_act(act, x);
 }

@@ -59,11 +59,11 @@ constexpr int kL = kWaveMaxLayers;
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// tanh as 1 - 2 / (exp(2x) + 1) on v_exp_f32 / v_rcp_f32 (abs error ~1e-7; saturates
+// tanh as 1 - 2 / (exp(2x) + 1) on v_exp_f32 / v_rcp_f32 (abs error ~2e-7; saturates
 // correctly at +-inf) instead of the branchy libm tanhf
 __device__ __forceinline__ float tanh_fast(float x) {
   const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
-  return 1.f - 2.f * __frcp_rn(e + 1.f);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);  // v_rcp_f32 (1 ulp), not the IEEE divide sequence
 }
 
 __device__ __forceinline__ float act_fn(int act, float x) {
@@ -330,6 +330,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 
   // ---- parameters -> LDS images (padding zero), Adam moments -> owner registers
   for (int i = tid; i < g.param_lds; i += kThreads) L[i] = 0.f;
+  for (int i = tid; i < 256; i += kThreads) L[g.nm_off + i] = 0.f;  // padding features stay 0
   __syncthreads();
 #pragma unroll
   for (int qq = 0; qq < 2; ++qq) {
@@ -502,16 +503,21 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       unsigned long long c0 = a.prof ? clock64() : 0;
       if (rows_wave) {
         // ---------------- normalised input: B operand of layer 0 (natural K order 4s + kk)
+        // (padding features: raw value 0 from the prep kernel, normaliser image entries 0)
         float xb[16];
+        {
+          float nmv[16], nrv[16];
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          xb[s] = 0.f;
-          if (s < s0) {
-            const int c = 4 * s + kk;
-            float v = cur.x[s];
-            if (a.has_norm) v = (v - L[g.nm_off + nb + (c < D ? c : 0)]) * L[g.nm_off + nb + 64 + (c < D ? c : 0)];
-            xb[s] = c < D ? v : 0.f;
+          for (int s = 0; s < 16; ++s) {
+            nmv[s] = 0.f;
+            nrv[s] = 1.f;
+            if (s < s0 && a.has_norm) {
+              nmv[s] = L[g.nm_off + nb + 4 * s + kk];
+              nrv[s] = L[g.nm_off + nb + 64 + 4 * s + kk];
+            }
           }
+#pragma unroll
+          for (int s = 0; s < 16; ++s) xb[s] = s < s0 ? (cur.x[s] - nmv[s]) * nrv[s] : 0.f;
         }
         if (q == 0) {  // shared layer-0 input image
           const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
@@ -528,19 +534,30 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           if (l >= nl) continue;
           const LG y = lg(g, q, l);
           const bool last = l == nl - 1;
-          const int tout = (HWT > 0 && !last) ? HWT / 16 : ((y.dout + 15) >> 4);
+          const int tout = last ? 1 : (HWT > 0 ? HWT / 16 : ((y.dout + 15) >> 4));  // head: dout <= 16
+          // all of the layer's weight operands are read first, then the output tiles'
+          // MFMA chains run interleaved (same accumulation order per tile as one chain)
           f4 acc[KT];
 #pragma unroll
-          for (int t = 0; t < KT; ++t) {
-            acc[t] = {0.f, 0.f, 0.f, 0.f};
-            if (t >= tout) continue;
-            const lf* wr = L + y.w + (16 * t + r16) * y.ldw;
-            if (l == 0) {
+          for (int t = 0; t < KT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
+          if (l == 0) {
+            float w0[KT][16];
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
 #pragma unroll
               for (int s = 0; s < 16; ++s)
-                if (s < s0) acc[t] = mfma(wr[4 * s + kk], xb[s], acc[t]);
-            } else {
-              const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
+                if (t < tout && s < s0) w0[t][s] = L[y.w + (16 * t + r16) * y.ldw + 4 * s + kk];
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+#pragma unroll
+              for (int t = 0; t < KT; ++t)
+                if (t < tout && s < s0) acc[t] = mfma(w0[t][s], xb[s], acc[t]);
+          } else if constexpr (KT > 2) {  // 64-wide: one tile at a time (register budget)
+            const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
+#pragma unroll
+            for (int t = 0; t < KT; ++t) {
+              if (t >= tout) continue;
+              const lf* wr = L + y.w + (16 * t + r16) * y.ldw;
 #pragma unroll
               for (int h = 0; h < KT; ++h) {
                 if (h >= tin) continue;
@@ -551,6 +568,29 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
                 acc[t] = mfma(w4.w, hreg[l - 1][h].w, acc[t]);
               }
             }
+          } else {
+            const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
+            f4 w4[KT][KT];
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+#pragma unroll
+              for (int h = 0; h < KT; ++h)
+                if (t < tout && h < tin) w4[t][h] = *(const lf4*)(L + y.w + (16 * t + r16) * y.ldw + 16 * h + 4 * kk);
+#pragma unroll
+            for (int h = 0; h < KT; ++h) {
+#pragma unroll
+              for (int t = 0; t < KT; ++t) {
+                if (t >= tout || h >= tin) continue;
+                acc[t] = mfma(w4[t][h].x, hreg[l - 1][h].x, acc[t]);
+                acc[t] = mfma(w4[t][h].y, hreg[l - 1][h].y, acc[t]);
+                acc[t] = mfma(w4[t][h].z, hreg[l - 1][h].z, acc[t]);
+                acc[t] = mfma(w4[t][h].w, hreg[l - 1][h].w, acc[t]);
+              }
+            }
+          }
+#pragma unroll
+          for (int t = 0; t < KT; ++t) {
+            if (t >= tout) continue;
             const int o0 = 16 * t + 4 * kk;
             const f4 bb = *(const lf4*)(L + y.b + o0);
             f4 v;
@@ -593,11 +633,12 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           float zs[4] = {0.f, 0.f, 0.f, 0.f}, isd[4] = {0.f, 0.f, 0.f, 0.f};
           if (gauss) {
             float part = 0.f;
+            const f4 ls4 = *(const lf4*)(L + g.ls_off + 4 * kk);  // entries >= A are 0
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int o = 4 * kk + j;
               if (o < A) {
-                const float lsv = L[g.ls_off + o];
+                const float lsv = ls4[j];
                 isd[j] = expf(-lsv);
                 zs[j] = (ao[j] - hv[j]) * isd[j];
                 part += -0.5f * zs[j] * zs[j] - lsv - c_half_log2pi;
@@ -686,7 +727,21 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         for (int l = kL - 1; l >= 0; --l) {
           if (l >= nl) continue;
           const LG y = lg(g, q, l);
-          const int tout = (HWT > 0 && l != nl - 1) ? HWT / 16 : ((y.dout + 15) >> 4);
+          const int tout = l == nl - 1 ? 1 : (HWT > 0 ? HWT / 16 : ((y.dout + 15) >> 4));
+          const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
+          // W_l^T operands (W[16 tt + 4 kk + j][16 u2 + r16]) read before this layer's
+          // image stores, so the loads are not ordered behind them
+          constexpr int KW = KT > 2 ? 1 : KT;  // 64-wide: W^T read per tile below (register budget)
+          float wt[KW][KW][4];
+          if (KT <= 2 && l > 0) {
+#pragma unroll
+            for (int u2 = 0; u2 < KT; ++u2)
+#pragma unroll
+              for (int tt = 0; tt < KT; ++tt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  if (u2 < tin && tt < tout) wt[u2 % KW][tt % KW][j] = L[y.w + (16 * tt + 4 * kk + j) * y.ldw + 16 * u2 + r16];
+          }
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) {
             if (u2 >= tout) continue;
@@ -702,22 +757,39 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
             }
           }
           if (l == 0) break;
-          const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
+          // the input tiles' chains interleaved (per tile: tt, j ascending as one chain)
+          f4 accb[KT];
+#pragma unroll
+          for (int u2 = 0; u2 < KT; ++u2) accb[u2] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (KT <= 2) {
+#pragma unroll
+            for (int tt = 0; tt < KT; ++tt)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int u2 = 0; u2 < KT; ++u2)
+                  if (u2 < tin && tt < tout) accb[u2] = mfma(wt[u2 % KW][tt % KW][j], dzc[tt][j], accb[u2]);
+          } else {
+#pragma unroll
+            for (int u2 = 0; u2 < KT; ++u2) {
+              if (u2 >= tin) continue;
+#pragma unroll
+              for (int tt = 0; tt < KT; ++tt) {
+                if (tt >= tout) continue;
+                const lf* wc = L + y.w + (16 * tt + 4 * kk) * y.ldw + 16 * u2 + r16;
+                accb[u2] = mfma(wc[0], dzc[tt].x, accb[u2]);
+                accb[u2] = mfma(wc[y.ldw], dzc[tt].y, accb[u2]);
+                accb[u2] = mfma(wc[2 * y.ldw], dzc[tt].z, accb[u2]);
+                accb[u2] = mfma(wc[3 * y.ldw], dzc[tt].w, accb[u2]);
+              }
+            }
+          }
           f4 nd[KT];
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) {
             nd[u2] = {0.f, 0.f, 0.f, 0.f};
             if (u2 >= tin) continue;
-            f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int tt = 0; tt < KT; ++tt) {
-              if (tt >= tout) continue;
-              const lf* wc = L + y.w + (16 * tt + 4 * kk) * y.ldw + 16 * u2 + r16;
-              acc = mfma(wc[0], dzc[tt].x, acc);
-              acc = mfma(wc[y.ldw], dzc[tt].y, acc);
-              acc = mfma(wc[2 * y.ldw], dzc[tt].z, acc);
-              acc = mfma(wc[3 * y.ldw], dzc[tt].w, acc);
-            }
+            const f4 acc = accb[u2];
             const f4 hv = hreg[l > 0 ? l - 1 : 0][u2];
             nd[u2].x = acc.x * act_grad(hid_act, hv.x);
             nd[u2].y = acc.y * act_grad(hid_act, hv.y);
