@@ -172,6 +172,8 @@ struct PPORcGeo {
   int z_off[2][kWaveMaxLayers], ldz[2][kWaveMaxLayers], db_off[2][kWaveMaxLayers];
   int ls_off, lsp_off, nm_off, red_off, param_lds;
   int zero_off;  // 64 floats of zeros (never written): operand of the padding dW items
+  int trash_off;   // 64 floats: Adam target of padding elements
+  int lds_floats;  // whole image size (zeroed at kernel start)
   int n_items;
   int n_witems;            // items [0, n_witems) are dW tiles
   int items[kMaxRcItems];  // q | layer << 1 | kind << 3 (0 W tile, 1 bias, 2 log_std) | out tile << 5 | in tile << 9

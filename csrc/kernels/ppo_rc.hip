@@ -329,8 +329,10 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   const int n_items = rfl(g.n_items);
 
   // ---- parameters -> LDS images (padding zero), Adam moments -> owner registers
-  for (int i = tid; i < g.param_lds; i += kThreads) L[i] = 0.f;
-  for (int i = tid; i < 256; i += kThreads) L[g.nm_off + i] = 0.f;  // padding features stay 0
+  // Zero ALL of the LDS images once: padding entries (weight rows / columns past the layer
+  // dims, unwritten input-image columns, normaliser entries of padding features) then stay
+  // exactly 0, so padded dW / bias entries come out 0 without per-lane masks.
+  for (int i = tid; i < g.lds_floats; i += kThreads) L[i] = 0.f;
   __syncthreads();
 #pragma unroll
   for (int qq = 0; qq < 2; ++qq) {
@@ -413,12 +415,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   const int n_witems = rfl(g.n_witems);
   const int nwi = n_witems > w ? min(KI, (n_witems - w + kWaves - 1) / kWaves) : 0;
   const int rq = cw / 4;  // K-major image: row r at (r & 3) * rq + (r >> 2)
-  int izo[KI], iho[KI], imask[KI];
+  int izo[KI], iho[KI];
 #pragma unroll
   for (int it = 0; it < KI; ++it) {
     const int id = w + it * kWaves;
     izo[it] = iho[it] = g.zero_off;
-    imask[it] = 0;
     if (id < n_items) {
       const int desc = rfl(g.items[id]);
       const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
@@ -426,24 +427,23 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         const LG y = lg(g, iq, il);
         izo[it] = y.z + (16 * ta + r16) * y.ldz + kk * rq;
         iho[it] = y.h + (16 * tb + r16) * y.ldh + kk * rq;
-        const int in = 16 * tb + r16;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (16 * ta + 4 * kk + j < y.dout && in < y.din) imask[it] |= 1 << j;
       }
     }
   }
   // loop-invariant item bookkeeping (kind, bias-partial source, Adam targets), computed once
   // instead of re-reading the descriptors and layer geometry every minibatch
-  int ikind[KI], ib_off[KI], ib_ok[KI], paddr[KI][4];
+  // paddr: LDS address of each owned element; padding elements point at a 64-float trash
+  // row (Adam then runs branch-free: their gradient and moments stay 0)
+  int ikind[KI], ib_off[KI], paddr[KI][4];
+  float ib_okf[KI];  // 1 for lanes holding a real bias / log_std element
 #pragma unroll
   for (int it = 0; it < KI; ++it) {
     const int id = w + it * kWaves;
     ikind[it] = -1;
     ib_off[it] = 0;
-    ib_ok[it] = 0;
+    ib_okf[it] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) paddr[it][j] = -1;
+    for (int j = 0; j < 4; ++j) paddr[it][j] = g.trash_off + lane;
     if (id >= n_items) continue;
     const int desc = rfl(g.items[id]);
     const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
@@ -458,8 +458,9 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       }
     } else {
       ib_off[it] = kind == 1 ? y.db : g.lsp_off;
-      ib_ok[it] = kind == 1 ? (lane < y.dout) : (has_ls && lane < A);
-      if (ib_ok[it]) paddr[it][0] = kind == 1 ? y.b + lane : g.ls_off + lane;
+      const bool ok = kind == 1 ? (lane < y.dout) : (has_ls && lane < A);
+      ib_okf[it] = ok ? 1.f : 0.f;
+      if (ok) paddr[it][0] = kind == 1 ? y.b + lane : g.ls_off + lane;
     }
   }
   float pre_m = 0.f, pre_v = 0.f;  // moments of the next minibatch to merge
@@ -829,10 +830,10 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 #pragma unroll
         for (int it = 0; it < KI; ++it) {
           if (it >= nwi) continue;
-          gg[it][0] += (imask[it] & 1) ? acc[it].x : 0.f;
-          gg[it][1] += (imask[it] & 2) ? acc[it].y : 0.f;
-          gg[it][2] += (imask[it] & 4) ? acc[it].z : 0.f;
-          gg[it][3] += (imask[it] & 8) ? acc[it].w : 0.f;
+          gg[it][0] += acc[it].x;  // padding entries are exactly 0 (zeroed images)
+          gg[it][1] += acc[it].y;
+          gg[it][2] += acc[it].z;
+          gg[it][3] += acc[it].w;
         }
       }
 #pragma unroll
@@ -840,10 +841,9 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         if (ikind[it] <= 0) continue;
         {  // bias (row-tile partials of dZ) / log_std (partials of the Gaussian term)
           const int stride = ikind[it] == 1 ? 64 : 16;
-          float gval = 0.f;
-          if (ib_ok[it])
-            for (int r = 0; r < RT; ++r) gval += L[ib_off[it] + r * stride + lane];
-          gg[it][0] += gval;
+          float gval = 0.f;  // (lanes past the vector read finite neighbours, masked by ib_okf)
+          for (int r = 0; r < RT; ++r) gval += L[ib_off[it] + r * stride + lane];
+          gg[it][0] += gval * ib_okf[it];
         }
       }
       if (a.prof) {
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 #pragma unroll
     for (int it = 0; it < KI; ++it) {
       if (ikind[it] < 0) continue;
-      if (ikind[it] == 2 && ib_ok[it]) gg[it][0] -= a.ent_coef;
+      if (ikind[it] == 2) gg[it][0] -= a.ent_coef * ib_okf[it];
 #pragma unroll
       for (int j = 0; j < 4; ++j) ss += gg[it][j] * gg[it][j];
     }
@@ -942,12 +942,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 #pragma unroll
     for (int it = 0; it < KI; ++it)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pval[it][j] = paddr[it][j] >= 0 ? L[paddr[it][j]] : 0.f;
+      for (int j = 0; j < 4; ++j) pval[it][j] = L[paddr[it][j]];
 #pragma unroll
     for (int it = 0; it < KI; ++it) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (paddr[it][j] < 0) continue;
         const float gval = gg[it][j] * coef;
         gm[it][j] = b1 * gm[it][j] + (1.f - b1) * gval;
         gv[it][j] = b2 * gv[it][j] + (1.f - b2) * gval * gval;
@@ -1128,6 +1127,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.lsp_off = take(4 * 16);
   g.nm_off = take(256);
   g.red_off = take(8 + 8 * 5);
+  g.trash_off = take(64);
+  g.lds_floats = off;
   lds_bytes = (size_t)off * 4;
   if (lds_bytes > 160 * 1024) return false;
   // items: dW tiles first (ids [0, n_witems): a wave's weight items are its first slots),
