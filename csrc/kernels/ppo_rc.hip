@@ -302,7 +302,8 @@ __device__ __forceinline__ void dw_tiles_n(const lf* L, const int* izo, const in
 // Shape specialisation: S0T (16-wide input k-steps / 4), NLT (layers per net), ACTT (hidden
 // activation), HWT (hidden width) fold the per-layer loop bounds, tile counts and the
 // activation switch at compile time; 0 / -1 = read them at run time (generic build).
-template <int KT, int KI, int S0T, int NLT, int ACTT, int HWT, int CWT>
+// DT: action head (0 Gaussian, 1 categorical, -1 read at run time).
+template <int KT, int KI, int S0T, int NLT, int ACTT, int HWT, int CWT, int DT>
 __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* L = (lf*)lds_raw;
@@ -320,8 +321,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   const int nl = NLT > 0 ? NLT : (q == 0 ? a.n_pi : a.n_vf);
   const int D = a.D, A = a.A;
   const int s0 = S0T > 0 ? S0T : (D + 3) / 4;
-  const bool gauss = !a.discrete;
+  const bool gauss = DT >= 0 ? DT == 0 : !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
+  float am[4];  // action-slot masks of this lane group (Gaussian head)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) am[j] = 4 * (lane >> 4) + j < a.A ? 1.f : 0.f;
   const int n_mb = a.rows / Bg;
   const int K = a.n_epochs * n_mb;
   const float invB = 1.f / (float)Bg;
@@ -633,17 +637,17 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           float pk[4] = {0.f, 0.f, 0.f, 0.f}, lpk[4] = {0.f, 0.f, 0.f, 0.f};
           float zs[4] = {0.f, 0.f, 0.f, 0.f}, isd[4] = {0.f, 0.f, 0.f, 0.f};
           if (gauss) {
+            // branch-free over the 4 action slots of this lane group: padding slots have
+            // log_std 0, action 0 and mean 0 (zero weight rows), so zs = 0 there and only the
+            // constant term needs the slot mask am[j]
             float part = 0.f;
-            const f4 ls4 = *(const lf4*)(L + g.ls_off + 4 * kk);  // entries >= A are 0
+            const f4 ls4 = *(const lf4*)(L + g.ls_off + 4 * kk);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const int o = 4 * kk + j;
-              if (o < A) {
-                const float lsv = ls4[j];
-                isd[j] = expf(-lsv);
-                zs[j] = (ao[j] - hv[j]) * isd[j];
-                part += -0.5f * zs[j] * zs[j] - lsv - c_half_log2pi;
-              }
+              const float lsv = ls4[j];
+              isd[j] = __expf(-lsv);
+              zs[j] = (ao[j] - hv[j]) * isd[j];
+              part += am[j] * (-0.5f * zs[j] * zs[j] - lsv - c_half_log2pi);
             }
             logp = sum_kk(part);
           } else {
@@ -686,8 +690,8 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int o = 4 * kk + j;
-              dzv[j] = o < A ? dlogp * zs[j] * isd[j] : 0.f;
-              lsp[j] = o < A ? dlogp * (zs[j] * zs[j] - 1.f) : 0.f;
+              dzv[j] = dlogp * zs[j] * isd[j];
+              lsp[j] = am[j] * dlogp * (zs[j] * zs[j] - 1.f);
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1197,17 +1201,18 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
   const int s0 = (a.D + 3) / 4;
   const dim3 grid(g.G), block(kThreads);
-#define IA_RC(KT, KI, S0, NL, ACT, HW, CW) hipLaunchKernelGGL((ppo_rc_kernel<KT, KI, S0, NL, ACT, HW, CW>), grid, block, lds_launch, s, a, g)
-  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64)
-    IA_RC(2, 4, 5, 3, 2, 32, 64);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
-  else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32)
-    IA_RC(4, 8, 3, 3, 1, 64, 32);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
-  else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64)
-    IA_RC(2, 4, 1, 3, 2, 32, 64);  // CartPole FeedForward32Policy
+#define IA_RC(KT, KI, S0, NL, ACT, HW, CW, DT) \
+  hipLaunchKernelGGL((ppo_rc_kernel<KT, KI, S0, NL, ACT, HW, CW, DT>), grid, block, lds_launch, s, a, g)
+  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete)
+    IA_RC(2, 4, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
+  else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)
+    IA_RC(4, 8, 3, 3, 1, 64, 32, 0);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
+  else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && a.discrete)
+    IA_RC(2, 4, 1, 3, 2, 32, 64, 1);  // CartPole FeedForward32Policy
   else if (g.kt == 2)
-    IA_RC(2, 4, 0, 0, -1, 0, 0);
+    IA_RC(2, 4, 0, 0, -1, 0, 0, -1);
   else
-    IA_RC(4, 8, 0, 0, -1, 0, 0);
+    IA_RC(4, 8, 0, 0, -1, 0, 0, -1);
 #undef IA_RC
   return hipGetLastError();
 }
