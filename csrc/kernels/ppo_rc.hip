@@ -106,6 +106,10 @@ __device__ __forceinline__ f4 ld_sc1_x4(const float* p) {
 __device__ __forceinline__ void wait_vm4(f4& a, f4& b, f4& c, f4& d) {
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
 }
+__device__ __forceinline__ void wait_vm8(f4 (&v)[8]) {
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])::"memory");
+}
 __device__ __forceinline__ unsigned ld_sc1u(unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -255,6 +259,42 @@ __device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int ro
   const float* ac = g.acts + (slot * 64 + row) * 16;
   r.act = *reinterpret_cast<const f4*>(ac + 4 * kk);
   r.rd = *reinterpret_cast<const f4*>(g.rowd + (slot * 64 + row) * 4);
+}
+
+// Sum of the G workgroups' partials of this wave's items, in group order, 8 sc1 loads in
+// flight per lane and ONE wait per batch of IB = 8 / G items (a load round trip is ~1.2K
+// cycles; a wait per item and 4 groups made the loads the exchange's dominant cost).
+template <int GT, int KI>
+__device__ __forceinline__ void exchange_sum(const float* slab, int n_items, int w, int lane, float (&gg)[KI][4]) {
+  constexpr int IB0 = 8 / GT;
+  constexpr int IB = IB0 < KI ? IB0 : KI;
+#pragma unroll
+  for (int i0 = 0; i0 < KI; i0 += IB) {
+    f4 v[8];
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int it = i0 + i;
+      const int id = w + it * kWaves;
+      const bool ok = it < KI && id < n_items;
+#pragma unroll
+      for (int gi = 0; gi < GT; ++gi) v[i * GT + gi] = ld_sc1_x4(slab + ((size_t)gi * n_items + (ok ? id : w)) * 256 + lane * 4);
+    }
+#pragma unroll
+    for (int e = IB * GT; e < 8; ++e) v[e] = v[0];
+    wait_vm8(v);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int it = i0 + i;
+      if (it >= KI || w + it * kWaves >= n_items) continue;
+      f4 sacc = v[i * GT];
+#pragma unroll
+      for (int gi = 1; gi < GT; ++gi) sacc += v[i * GT + gi];
+      gg[it][0] = sacc.x;
+      gg[it][1] = sacc.y;
+      gg[it][2] = sacc.z;
+      gg[it][3] = sacc.w;
+    }
+  }
 }
 
 // dW tiles of this wave's N weight items over one chunk (K = cw rows): acc[i] = dZ^T H for
@@ -478,8 +518,12 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   // chunk unit u = k * nch + ch -> prep slot k * CH + grp * nch + ch
   auto slot_of = [&](int u) -> size_t { return (size_t)(u / nch) * CH + (size_t)grp * nch + (u % nch); };
   if (rows_wave && K > 0) load_rows(g, slot_of(0), row, kk, s0, cur);
-  unsigned long long prof[5] = {0, 0, 0, 0, 0};  // chunk, exchange+|g|^2, clip+Adam; wave 0: B1 wait, dW items
-  unsigned long long wprof[4] = {0, 0, 0, 0};  // this wave: rows/x, forward, loss, backward chain
+  // cycle counters (a.prof): accumulated in LDS by one lane, so that they hold no registers
+  // across the minibatch loop. [0..2] chunk, exchange + |g|^2, clip + Adam (wave 0);
+  // [3..6] / [7..10] actor / critic row tile 0: rows/x, forward, loss, backward chain;
+  // [11] wave 0 B1 wait, [12] dW items; [13..15] exchange: publish, arrival, loads
+  __shared__ unsigned long long sprof[16];
+  if (tid < 16) sprof[tid] = 0;
   unsigned* arrive = g.sync;
   unsigned* tflag = g.sync + 1;
   __syncthreads();
@@ -804,12 +848,13 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) dzc[u2] = nd[u2];
         }
-        if (a.prof) {
+        if (a.prof && lane == 0 && (w == 0 || w == 4)) {
           const unsigned long long c4 = clock64();
-          wprof[0] += c1 - c0;
-          wprof[1] += c2 - c1;
-          wprof[2] += c3 - c2;
-          wprof[3] += c4 - c3;
+          const int pb = w == 4 ? 7 : 3;
+          sprof[pb + 0] += c1 - c0;
+          sprof[pb + 1] += c2 - c1;
+          sprof[pb + 2] += c3 - c2;
+          sprof[pb + 3] += c4 - c3;
         }
       }
       const unsigned long long cb0 = a.prof ? clock64() : 0;
@@ -850,9 +895,9 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           gg[it][0] += gval * ib_okf[it];
         }
       }
-      if (a.prof) {
-        prof[3] += cb1 - cb0;
-        prof[4] += clock64() - cb1;
+      if (a.prof && tid == 0) {
+        sprof[11] += cb1 - cb0;
+        sprof[12] += clock64() - cb1;
       }
       if (rows_wave) cur = nxt;
       if (ch + 1 < nch) __syncthreads();  // images are rewritten by the next chunk
@@ -869,8 +914,10 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         const f4 v = {gg[it][0], gg[it][1], gg[it][2], gg[it][3]};
         st_sc1_x4(slab + ((size_t)grp * n_items + id) * 256 + lane * 4, v);
       }
+      const unsigned long long e0 = a.prof ? clock64() : 0;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      const unsigned long long e1 = a.prof ? clock64() : 0;
       if (tid == 0) {
         atomicAdd(arrive, 1u);
         const unsigned target = (unsigned)G * (unsigned)(k + 1);
@@ -884,6 +931,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         }
       }
       __syncthreads();
+      const unsigned long long e2 = a.prof ? clock64() : 0;
+      if (G == 2) exchange_sum<2, KI>(slab, n_items, w, lane, gg);
+      else if (G == 4) exchange_sum<4, KI>(slab, n_items, w, lane, gg);
+      else if (G == 8) exchange_sum<8, KI>(slab, n_items, w, lane, gg);
+      else
 #pragma unroll
       for (int it = 0; it < KI; ++it) {
         const int id = w + it * kWaves;
@@ -906,6 +958,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
         gg[it][1] = s.y;
         gg[it][2] = s.z;
         gg[it][3] = s.w;
+      }
+      if (a.prof && tid == 0) {
+        sprof[13] += e1 - e0;
+        sprof[14] += e2 - e1;
+        sprof[15] += clock64() - e2;
       }
     }
     // entropy term of log_std (d(-ent_coef * H)/d log_std = -ent_coef), once per minibatch; |g|^2
@@ -959,11 +1016,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       }
     }
     __syncthreads();  // B3: parameters updated
-    if (a.prof) {
+    if (a.prof && tid == 0) {
       const unsigned long long t3 = clock64();
-      prof[0] += t1 - t0;
-      prof[1] += t2 - t1;
-      prof[2] += t3 - t2;
+      sprof[0] += t1 - t0;
+      sprof[1] += t2 - t1;
+      sprof[2] += t3 - t2;
     }
   }
 
@@ -1037,16 +1094,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     if (nc == 0) a.norm_count[0] = run_c;
   }
   if (tid == 0) a.adam_step[0] = step;
-  if (a.prof && tid == 0) {
-    a.prof[0] += prof[0];
-    a.prof[1] += prof[1];
-    a.prof[2] += prof[2];
-    a.prof[11] += prof[3];
-    a.prof[12] += prof[4];
-  }
-  if (a.prof && lane == 0 && (w == 0 || w == 4)) {  // actor / critic row tile 0
-    for (int i = 0; i < 4; ++i) a.prof[3 + (w == 4 ? 4 : 0) + i] += wprof[i];
-  }
+  if (a.prof && tid < 16) a.prof[tid] += sprof[tid];  // (stats barrier above orders the LDS)
 }
 
 constexpr int items_per_wave(int kt) { return kt == 2 ? 4 : 8; }

@@ -31,6 +31,11 @@ def main():
         tr._ppo_update()
     th.cuda.synchronize()
     print(f"ppo update {1e3 * (time.perf_counter() - t0) / n:.3f} ms (no counters)", flush=True)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        tr._rollout()
+    th.cuda.synchronize()
+    print(f"rollout {1e3 * (time.perf_counter() - t0) / n:.3f} ms (unchanged kernel: box-speed reference)", flush=True)
     prof = th.zeros(16, dtype=th.int64, device="cuda")
     tr._ppo_static["prof"] = prof
     tr._ppo_update()

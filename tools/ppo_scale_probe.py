@@ -52,7 +52,8 @@ def main():
         tr._ppo_update()
         th.cuda.synchronize()
         p = prof.cpu().numpy().astype(np.float64) / tr._last_ppo_info[1]
-        print(f"    cycles/minibatch (workgroup 0): chunk {p[0]:.0f} exchange+|g|^2 {p[1]:.0f} clip+adam {p[2]:.0f} | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f}", flush=True)
+        print(f"    cycles/minibatch (workgroup 0): chunk {p[0]:.0f} exchange+|g|^2 {p[1]:.0f} clip+adam {p[2]:.0f} | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f}"
+              f" | exchange: publish {p[13]:.0f} arrival {p[14]:.0f} loads {p[15]:.0f}", flush=True)
         tr._ppo_static.pop("prof")
 
 
