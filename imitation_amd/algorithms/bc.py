@@ -129,6 +129,8 @@ class RolloutStatsComputer:
     n_episodes: int
 
     def __call__(self, policy, rng: np.random.Generator) -> Mapping[str, float]:
+        if self.venv is not None and self.n_episodes > 0 and hasattr(self.venv, "device_rollout_stats"):
+            return self.venv.device_rollout_stats(policy, self.n_episodes)  # e.g. DAgger's device collector
         if self.venv is not None and self.n_episodes > 0:
             trajs = rollout.generate_trajectories(policy, self.venv, rollout.make_min_episodes(self.n_episodes), rng=rng)
             return rollout.rollout_stats(trajs)

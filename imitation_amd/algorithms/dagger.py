@@ -330,10 +330,14 @@ class DAggerTrainer(base.BaseImitationAlgorithm):
         self.bc_trainer.set_demonstrations(base.TransitionsBatchLoader(transitions, self.batch_size, shuffle=True,
                                                                        drop_last=True, seed=seed))
 
+    def _log_rollouts_venv(self):
+        """Where BC's rollout statistics run by default (the reference: ``self.venv``)."""
+        return self.venv
+
     def extend_and_update(self, bc_train_kwargs: Optional[Mapping[str, Any]] = None) -> int:
         """Aggregate the new demos, train BC on everything collected so far, advance the round."""
         kwargs = dict(bc_train_kwargs or {})
-        kwargs.setdefault("log_rollouts_venv", self.venv)
+        kwargs.setdefault("log_rollouts_venv", self._log_rollouts_venv())
         if "n_epochs" not in kwargs and "n_batches" not in kwargs:
             kwargs["n_epochs"] = self.DEFAULT_N_EPOCHS
         if pdist.world_size() > 1:
@@ -478,6 +482,15 @@ class SimpleDAggerTrainer(DAggerTrainer):
         self._device_agg.append(obs, acts)
         self._device_counts[round_num] = self._device_counts.get(round_num, 0) + len(trajs)
         self._store.trajectories.extend(trajs)
+
+    def _log_rollouts_venv(self):
+        """With the device collector, BC's rollout statistics run on the device as well
+        (same stopping rule and keys as the host rollouts over ``self.venv``)."""
+        if self._device_collector is not None:
+            from imitation_amd.engine import dagger as dagger_engine
+
+            return dagger_engine.DeviceStatsVenv(self._device_collector)
+        return self.venv
 
     @property
     def collector_kind(self) -> str:

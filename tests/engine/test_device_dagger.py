@@ -148,3 +148,25 @@ def test_cnn_actor_matches_policy():
     p = th.softmax(hrow[0] @ pol.action_net.weight.T + pol.action_net.bias, -1)
     freq = counts / counts.sum()
     assert float((freq - p).abs().max()) < 0.02
+
+
+@gpu
+def test_device_rollout_stats_match_host_keys(tmp_path):
+    """BC's rollout statistics through the device collector: same keys and stopping rule as
+    the host rollouts over the venv (TimeLimit 200: every env finishes at step 200)."""
+    from imitation_amd.algorithms import bc
+
+    tr, venv, expert, learner = _pong_trainer(tmp_path)
+    dev_venv = tr._log_rollouts_venv()
+    assert hasattr(dev_venv, "device_rollout_stats")
+    s_dev = bc.RolloutStatsComputer(dev_venv, 2)(learner, np.random.default_rng(0))
+    s_host = bc.RolloutStatsComputer(venv, 2)(learner, np.random.default_rng(0))
+    assert set(s_dev) == set(s_host)
+    assert s_dev["n_traj"] == s_host["n_traj"] == venv.num_envs
+    assert s_dev["len_mean"] == s_host["len_mean"] == 200
+    assert s_dev["monitor_return_mean"] == s_dev["return_mean"]
+    assert -21 <= s_dev["return_min"] <= s_dev["return_max"] <= 21
+    # a DAgger round still collects normally after the stats rollout
+    tr.train(400, rollout_round_min_episodes=1, rollout_round_min_timesteps=400,
+             bc_train_kwargs=dict(n_epochs=1, progress_bar=False, log_interval=10**9))
+    assert tr.round_num >= 1

@@ -36,6 +36,20 @@ def main():
               f"bc {1e3*(t3-t2):.1f} ms ({n_b} batches, {1e3*(t3-t2)/max(1,n_b):.3f} ms/batch) graph={col._sets[0]['graph'] is not None}",
               flush=True)
     tr._writer.flush()
+    # the bench step (SimpleDAggerTrainer.train, one round), profiled by cProfile on the host
+    import cProfile
+    import pstats
+    for r in range(2):
+        th.cuda.synchronize()
+        t0 = time.perf_counter()
+        pr = cProfile.Profile()
+        pr.enable()
+        tr.train(2048, rollout_round_min_episodes=1, rollout_round_min_timesteps=2048, bc_train_kwargs=kw)
+        th.cuda.synchronize()
+        pr.disable()
+        dt = time.perf_counter() - t0
+        print(f"train step {r}: {1e3*dt:.1f} ms, {tr.last_train_timesteps_local} steps -> {tr.last_train_timesteps_local/dt:.0f} env-steps/s", flush=True)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(25)
     # chunk replay alone
     th.cuda.synchronize()
     t0 = time.perf_counter()
