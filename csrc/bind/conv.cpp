@@ -20,7 +20,7 @@ int in_kind(const torch::Tensor& x) {
   return -1;
 }
 
-ia::ConvGeo geo(const torch::Tensor& x, int64_t N, int64_t KH, int64_t KW, int64_t S) {
+ia::ConvGeo geo(const torch::Tensor& x, int64_t N, int64_t KH, int64_t KW, int64_t S, int64_t P = 0) {
   TORCH_CHECK(x.dim() == 4, "x must be NHWC [B, H, W, C]");
   ia::ConvGeo g{};
   g.B = (int)x.size(0);
@@ -30,23 +30,36 @@ ia::ConvGeo geo(const torch::Tensor& x, int64_t N, int64_t KH, int64_t KW, int64
   g.KH = (int)KH;
   g.KW = (int)KW;
   g.S = (int)S;
-  g.OH = (g.H - g.KH) / g.S + 1;
-  g.OW = (g.W - g.KW) / g.S + 1;
+  g.P = (int)P;
+  g.OH = (g.H + 2 * g.P - g.KH) / g.S + 1;
+  g.OW = (g.W + 2 * g.P - g.KW) / g.S + 1;
   g.N = (int)N;
-  TORCH_CHECK(ia::conv_geo_ok(g), "conv geometry outside the kernel (K % 32, KW*C % 8, N in {16,32,48,64})");
+  g.Kp = (g.KH * g.KW * g.C + 31) & ~31;
+  TORCH_CHECK(ia::conv_geo_ok(g),
+              "conv geometry outside the kernel (valid: KW*C % 8; padded / K % 32 != 0: C % 8, stride 1; N in {16,32,48,64})");
   return g;
+}
+
+// [N, KH, KW, C] -> [N, Kp] with zero columns past K (no copy when K == Kp)
+torch::Tensor pad_k(const torch::Tensor& w, int Kp) {
+  const int64_t N = w.size(0), K = w.numel() / N;
+  if (K == Kp) return w;
+  auto out = torch::zeros({N, (int64_t)Kp}, w.options());
+  out.narrow(1, 0, K).copy_(w.reshape({N, K}));
+  return out;
 }
 
 // x NHWC, wb bf16 [N][KH][KW][C] -> y bf16 [B, OH, OW, N]
 torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor wb, c10::optional<torch::Tensor> bias, int64_t stride,
-                       double in_scale, bool relu) {
+                       double in_scale, bool relu, int64_t pad) {
   IA_CHECK_CUDA(x);
   IA_CHECK_CONTIG(x);
   IA_CHECK_CUDA(wb);
   IA_CHECK_CONTIG(wb);
   TORCH_CHECK(wb.scalar_type() == torch::kBFloat16 && wb.dim() == 4, "wb must be bf16 [N, KH, KW, C]");
-  auto g = geo(x, wb.size(0), wb.size(1), wb.size(2), stride);
+  auto g = geo(x, wb.size(0), wb.size(1), wb.size(2), stride, pad);
   TORCH_CHECK(wb.size(3) == g.C, "channel mismatch");
+  auto wk = pad_k(wb, g.Kp);
   const float* b = nullptr;
   if (bias.has_value() && bias->defined()) {
     IA_CHECK_GPU_F32(*bias);
@@ -54,20 +67,20 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor wb, c10::optional<torch::T
     b = bias->data_ptr<float>();
   }
   auto y = torch::empty({g.B, g.OH, g.OW, g.N}, x.options().dtype(torch::kBFloat16));
-  IA_HIP_CHECK3(ia::conv_forward(in_kind(x), x.data_ptr(), wb.data_ptr(), b, y.data_ptr(), g, (float)in_scale, relu ? 1 : 0,
+  IA_HIP_CHECK3(ia::conv_forward(in_kind(x), x.data_ptr(), wk.data_ptr(), b, y.data_ptr(), g, (float)in_scale, relu ? 1 : 0,
                                  ia_stream()));
   return y;
 }
 
 // (dW fp32 [N][KH][KW][C], db fp32 [N]); dZ = dy * [y > 0] if relu_out
 py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t KH, int64_t KW, int64_t stride,
-                     double in_scale, bool relu_out) {
+                     double in_scale, bool relu_out, int64_t pad) {
   IA_CHECK_CUDA(x);
   IA_CHECK_CONTIG(x);
   IA_CHECK_CUDA(dy);
   IA_CHECK_CONTIG(dy);
   TORCH_CHECK(dy.scalar_type() == torch::kBFloat16, "dy must be bf16 NHWC");
-  auto g = geo(x, dy.size(3), KH, KW, stride);
+  auto g = geo(x, dy.size(3), KH, KW, stride, pad);
   TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.OH && dy.size(2) == g.OW, "dy shape");
   if (relu_out) {
     IA_CHECK_CUDA(y);
@@ -76,17 +89,19 @@ py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t
   }
   auto f32 = x.options().dtype(torch::kFloat32);
   auto slab = torch::empty({(int64_t)ia::conv_wgrad_slab_floats(g)}, f32);
-  auto dW = torch::empty({g.N, g.KH, g.KW, g.C}, f32);
+  auto dWp = torch::empty({g.N, g.Kp}, f32);
   auto db = torch::empty({g.N}, f32);
   IA_HIP_CHECK3(ia::conv_wgrad(in_kind(x), x.data_ptr(), dy.data_ptr(), relu_out ? y.data_ptr() : nullptr,
-                               slab.data_ptr<float>(), dW.data_ptr<float>(), db.data_ptr<float>(), g, (float)in_scale,
+                               slab.data_ptr<float>(), dWp.data_ptr<float>(), db.data_ptr<float>(), g, (float)in_scale,
                                relu_out ? 1 : 0, ia_stream()));
+  const int64_t K = (int64_t)g.KH * g.KW * g.C;
+  auto dW = (K == g.Kp ? dWp : dWp.narrow(1, 0, K).contiguous()).view({g.N, g.KH, g.KW, g.C});
   return py::make_tuple(dW, db);
 }
 
 // dZp bf16 [B, H, W, C] = [xp > 0] * conv^T(dy * [y > 0]); wt bf16 [C][KH][KW][N]
 torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, torch::Tensor xp, int64_t stride,
-                         bool relu_out, bool relu_in) {
+                         bool relu_out, bool relu_in, int64_t pad) {
   IA_CHECK_CUDA(dy);
   IA_CHECK_CONTIG(dy);
   IA_CHECK_CUDA(wt);
@@ -96,7 +111,7 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, to
   TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && wt.scalar_type() == torch::kBFloat16 &&
                   xp.scalar_type() == torch::kBFloat16, "dy, wt, xp must be bf16");
   TORCH_CHECK(wt.dim() == 4, "wt must be [C, KH, KW, N]");
-  auto g = geo(xp, dy.size(3), wt.size(1), wt.size(2), stride);
+  auto g = geo(xp, dy.size(3), wt.size(1), wt.size(2), stride, pad);
   TORCH_CHECK(wt.size(0) == g.C && wt.size(3) == g.N, "wt shape");
   TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.OH && dy.size(2) == g.OW, "dy shape");
   if (relu_out) {
@@ -175,7 +190,10 @@ void register_conv(py::module& m) {
         py::arg("b2"), py::arg("mode"), py::arg("seed"), py::arg("counter"), py::arg("out"), py::arg("rec_out") = py::none(),
         py::arg("mix_expert") = py::none(), py::arg("beta") = py::none(), py::arg("exec_out") = py::none());
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv + bias + ReLU (bf16 MFMA)", py::arg("x"), py::arg("wb"),
-        py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true);
-  m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)");
-  m.def("conv_dgrad", &conv_dgrad, "NHWC conv data gradient with fused ReLU masks");
+        py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0);
+  m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)", py::arg("x"),
+        py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
+        py::arg("relu_out"), py::arg("pad") = 0);
+  m.def("conv_dgrad", &conv_dgrad, "NHWC conv data gradient with fused ReLU masks", py::arg("dy"), py::arg("y"),
+        py::arg("wt"), py::arg("xp"), py::arg("stride"), py::arg("relu_out"), py::arg("relu_in"), py::arg("pad") = 0);
 }

@@ -22,6 +22,12 @@
 //
 // dZ = dY * [Y > 0] (ReLU of the layer's own output) is formed on load when relu_out is
 // set, so no separate mask kernel runs.
+//
+// Zero padding (g.P > 0: the reward CNNs' 3x3 stride-1 "same" convs, reward_nets.py:535-600
+// / networks.py:286-357) needs C % 8 == 0, so a fragment's 8 consecutive k = (kh, kw, c..c+7)
+// stay inside one tap: the fragment is loaded if that tap's input pixel is inside the image
+// and is zero otherwise. K = KH*KW*C is padded to Kp (a multiple of 32) with zero weight
+// columns; fragments past K read as zero too.
 #include <hip/hip_runtime.h>
 
 #include "ia/mfma.h"
@@ -30,7 +36,16 @@
 namespace ia {
 namespace {
 
-constexpr int kLdT = 40;  // LDS row stride (bf16) of the transposed 32-row chunks: 80 B
+// rows per wgrad chunk: 128 (or 64 where the chunk's LDS images would not fit) once a layer
+// has at least kWgradBigM GEMM rows, else 32
+constexpr int kWgradBigM = 1 << 16;
+__host__ __device__ __forceinline__ int wgrad_chunk(const ConvGeo& g) {
+  if (g.B * g.OH * g.OW < kWgradBigM) return 32;
+  const int rows = g.Kp + g.N;  // LDS image rows (bf16)
+  if (rows * (128 + 8) * 2 <= 160 * 1024) return 128;
+  if (rows * (64 + 8) * 2 <= 160 * 1024) return 64;
+  return 32;
+}
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -74,7 +89,18 @@ __device__ __forceinline__ bf16x8 load_dz8(const bf16* dY, const bf16* Y, size_t
 }
 
 // ------------------------------------------------------------------ forward
-template <typename TIn, int NT>
+// tap-checked fragment of a padded conv: 8 consecutive k at k (k % 8 == 0, C % 8 == 0)
+template <typename TIn>
+__device__ __forceinline__ bf16x8 load8_pad(const TIn* X, const ConvGeo& g, int b, int oh, int ow, int k, bool mv,
+                                            float in_scale) {
+  const int tap = k / g.C, c = k - tap * g.C;
+  const int kh = tap / g.KW, kw = tap - kh * g.KW;
+  const int ih = oh * g.S - g.P + kh, iw = ow * g.S - g.P + kw;
+  if (!mv || kh >= g.KH || (unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero8();
+  return load8(X + ((size_t)(b * g.H + ih) * g.W + iw) * g.C + c, in_scale);
+}
+
+template <typename TIn, int NT, bool PADDED = false>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X, const bf16* __restrict__ Wb,
                                                        const float* __restrict__ bias, bf16* __restrict__ Y, ConvGeo g,
                                                        float in_scale, int relu) {
@@ -83,7 +109,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
   const int OHW = g.OH * g.OW;
   const int M = g.B * OHW;
   if (m0 >= M) return;
-  const int K = g.KH * g.KW * g.C;
+  const int K = g.Kp;
   const int n_base = blockIdx.y * 16 * NT;  // split-N grids (small batches): this block's channels
   const int rowlen = g.KW * g.C;
   const int r = l & 15, kq = (l >> 4) * 8;
@@ -91,7 +117,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
   const bool mv = m < M;
   const int mm = mv ? m : M - 1;
   const int b = mm / OHW, pix = mm - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
-  const TIn* xb = X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C;
+  const TIn* xb = PADDED ? X : X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C;
   const size_t xrow = (size_t)g.W * g.C;
   f32x4 acc[NT];
 #pragma unroll
@@ -100,9 +126,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
 #pragma unroll 4
   for (int k0 = 0; k0 < K; k0 += 32) {
     const int k = k0 + kq;
-    const int kh = k / rowlen, off = k - kh * rowlen;
-    bf16x8 av = load8(xb + kh * xrow + off, in_scale);
-    if (!mv) av = zero8();
+    bf16x8 av;
+    if constexpr (PADDED) {
+      av = load8_pad(X, g, b, oh, ow, k, mv, in_scale);
+    } else {
+      const int kh = k / rowlen, off = k - kh * rowlen;
+      av = load8(xb + kh * xrow + off, in_scale);
+      if (!mv) av = zero8();
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * K + k0);
@@ -157,12 +188,15 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict_
 #pragma unroll
   for (int t = 0; t < CT; ++t) acc[t] = zero4();
   const bf16* wr = Wt + (size_t)r * Kp + kq;
+  // (padded convs are stride 1: one phase, every tap; output pixel (ih + P - kh, iw + P - kw))
   for (int kh = ph; kh < g.KH; kh += g.S) {
-    const int oh = (ih - kh) / g.S;
-    const bool hv = ih >= kh && oh < g.OH;
+    const int th = ih + g.P - kh;
+    const int oh = th / g.S;
+    const bool hv = th >= 0 && oh < g.OH;
     for (int kw = pw; kw < g.KW; kw += g.S) {
-      const int ow = (iw - kw) / g.S;
-      const bool valid = pv && hv && iw >= kw && ow < g.OW;
+      const int tw = iw + g.P - kw;
+      const int ow = tw / g.S;
+      const bool valid = pv && hv && tw >= 0 && ow < g.OW;
       if (__ballot(valid) == 0ull) continue;  // this tap misses all 16 pixels of the tile (border)
       const size_t dzoff = ((size_t)(b * g.OH + oh) * g.OW + ow) * g.N + kq;
       const int kbase = (kh * g.KW + kw) * g.N;
@@ -197,68 +231,85 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict_
 
 // ------------------------------------------------------------------ weight gradient (partials)
 // 512 threads; wave w owns output tiles t = w + 8 i (t = nt * KT + kt), TPW >= ceil(NT*KT/8).
-template <typename TIn, int NT, int TPW>
+// Each block reduces a contiguous m range in chunks of CH rows staged transposed in LDS
+// (row stride CH + 8 bf16): the im2col rows as 8-k fragments, dZ as 8-channel fragments
+// (one 16-byte load per (row, 8 channels)); every tile then runs CH/32 MFMA k-steps per
+// chunk. CH = 128 for large M (4x the MFMA work per barrier pair and per load round trip),
+// 32 for the small BC batches, where more blocks matter more.
+template <typename TIn, int NT, int TPW, int CH>
 __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__ X, const bf16* __restrict__ dY,
                                                          const bf16* __restrict__ Y, float* __restrict__ slab, ConvGeo g,
                                                          float in_scale, int relu_out, int m_per_block) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int K = g.KH * g.KW * g.C;
-  bf16* At = reinterpret_cast<bf16*>(smem);  // [K][kLdT]   im2col chunk, m contiguous
-  bf16* Zt = At + (size_t)K * kLdT;          // [N][kLdT]   dZ chunk, m contiguous
+  constexpr int LD = CH + 8;
+  const int K = g.Kp;
+  bf16* At = reinterpret_cast<bf16*>(smem);  // [K][LD]   im2col chunk, m contiguous
+  bf16* Zt = At + (size_t)K * LD;            // [N][LD]   dZ chunk, m contiguous
   const int OHW = g.OH * g.OW;
-  const int M = g.B * OHW;
   const int N = g.N;
   const int KT = K / 16;
   const int n_tiles = NT * KT;
   const int rowlen = g.KW * g.C;
   const size_t xrow = (size_t)g.W * g.C;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const bool tap_checked = g.P > 0 || g.Kp != g.KH * g.KW * g.C;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
   const int mb = blockIdx.x * m_per_block;
-  const int me = min(M, mb + m_per_block);
+  const int me = min(g.B * OHW, mb + m_per_block);
   f32x4 acc[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) acc[i] = zero4();
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // bias partials of the (n, m_local) items this thread stages
-  for (int c0 = mb; c0 < me; c0 += 32) {
-    // stage the im2col chunk transposed: item (k-group kg, m_local)
-    for (int it = threadIdx.x; it < (K / 8) * 32; it += 512) {
-      const int ml = it & 31, kg = it >> 5;
+  float bsum = 0.f;  // bias partial of channel tid (tid < N)
+  for (int c0 = mb; c0 < me; c0 += CH) {
+    // im2col fragments (k-group kg, row ml), transposed
+    for (int it = tid; it < (K / 8) * CH; it += 512) {
+      const int ml = it % CH, kg = it / CH;
       const int m = c0 + ml;
       bf16x8 v = zero8();
       if (m < me) {
         const int b = m / OHW, pix = m - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
-        const int k = kg * 8, kh = k / rowlen, off = k - kh * rowlen;
-        v = load8(X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C + kh * xrow + off, in_scale);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) At[(size_t)(kg * 8 + j) * kLdT + ml] = v[j];
-    }
-    // stage dZ transposed: item (n, m_local)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int it = threadIdx.x + 512 * j;
-      if (it < N * 32) {
-        const int ml = it & 31, n = it >> 5;
-        const int m = c0 + ml;
-        float z = 0.f;
-        if (m < me) {
-          z = (float)dY[(size_t)m * N + n];
-          if (relu_out && !((float)Y[(size_t)m * N + n] > 0.f)) z = 0.f;
+        if (tap_checked) {
+          v = load8_pad(X, g, b, oh, ow, kg * 8, true, in_scale);
+        } else {
+          const int k = kg * 8, kh = k / rowlen, off = k - kh * rowlen;
+          v = load8(X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C + kh * xrow + off, in_scale);
         }
-        const bf16 zb = (bf16)z;
-        Zt[n * kLdT + ml] = zb;
-        bsum[j] += (float)zb;
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) At[(size_t)(kg * 8 + j) * LD + ml] = v[j];
+    }
+    // dZ fragments (8 channels ng, row ml): dY * [Y > 0] when relu_out, transposed
+    for (int it = tid; it < (N / 8) * CH; it += 512) {
+      const int ml = it % CH, ng = it / CH;
+      const int m = c0 + ml;
+      bf16x8 z = zero8();
+      if (m < me) z = load_dz8(dY, Y, (size_t)m * N + ng * 8, relu_out);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Zt[(ng * 8 + j) * LD + ml] = z[j];
     }
     __syncthreads();
+    if (tid < N) {
+      const bf16x8* zr = reinterpret_cast<const bf16x8*>(Zt + tid * LD);
+#pragma unroll
+      for (int q = 0; q < CH / 8; ++q) {
+        const bf16x8 z = zr[q];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum += (float)z[j];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int t = w + 8 * i;
       if (t < n_tiles) {
         const int nt = t / KT, kt = t - nt * KT;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Zt + (nt * 16 + (l & 15)) * kLdT + (l >> 4) * 8);
-        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(At + (size_t)(kt * 16 + (l & 15)) * kLdT + (l >> 4) * 8);
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[i], 0, 0, 0);
+        const bf16* za = Zt + (nt * 16 + (l & 15)) * LD + (l >> 4) * 8;
+        const bf16* xa = At + (size_t)(kt * 16 + (l & 15)) * LD + (l >> 4) * 8;
+#pragma unroll
+        for (int s = 0; s < CH / 32; ++s) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(za + s * 32);
+          const bf16x8 bb = *reinterpret_cast<const bf16x8*>(xa + s * 32);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc[i], 0, 0, 0);
+        }
       }
     }
     __syncthreads();
@@ -275,21 +326,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
       for (int q = 0; q < 4; ++q) out[(size_t)(nt * 16 + 4 * (l >> 4) + q) * K + k] = acc[i][q];
     }
   }
-  // bias: the 32 m_local items of one n are 32 consecutive threads (half a wave)
-  float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float v = bsum[j];
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 4);
-    v += __shfl_xor(v, 8);
-    v += __shfl_xor(v, 16);
-    const int it = threadIdx.x + 512 * j;
-    if ((threadIdx.x & 31) == 0 && it < N * 32) red[it >> 5] = v;
-  }
-  __syncthreads();
-  for (int n = threadIdx.x; n < N; n += 512) out[(size_t)N * K + n] = red[n];
+  if (tid < N) out[(size_t)N * K + tid] = bsum;
 }
 
 // Fixed-order sum of the wgrad block partials: 4 independent accumulators (blocks b with
@@ -317,6 +354,16 @@ hipError_t launch_fwd(const TIn* X, const bf16* Wb, const float* bias, bf16* Y, 
                       hipStream_t s) {
   const int M = g.B * g.OH * g.OW;
   const dim3 block(256);
+  if (g.P > 0 || g.Kp != g.KH * g.KW * g.C) {
+    const dim3 grid((M + 63) / 64);
+    switch (g.N / 16) {
+      case 1: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 1, true>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
+      case 2: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 2, true>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
+      case 4: hipLaunchKernelGGL((conv_fwd_kernel<TIn, 4, true>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if ((M + 63) / 64 < 96) {
     // small batches (policy inference): one 16-channel slice per block row, so the grid has
     // N/16 x as many waves to hide the operand-load latency of the K loop
@@ -334,25 +381,36 @@ hipError_t launch_fwd(const TIn* X, const bf16* Wb, const float* bias, bf16* Y, 
   return hipGetLastError();
 }
 
-template <typename TIn, int NT>
-hipError_t launch_wgrad_nt(const TIn* X, const bf16* dY, const bf16* Y, float* slab, const ConvGeo& g, float scale,
+template <typename TIn, int NT, int CH>
+hipError_t launch_wgrad_ch(const TIn* X, const bf16* dY, const bf16* Y, float* slab, const ConvGeo& g, float scale,
                            int relu_out, int nblk, int mpb, hipStream_t s) {
-  const int K = g.KH * g.KW * g.C;
+  const int K = g.Kp;
   const int tiles = NT * (K / 16);
-  const size_t lds = ((size_t)K * kLdT + (size_t)g.N * kLdT) * sizeof(bf16);
+  const size_t lds = ((size_t)K + (size_t)g.N) * (CH + 8) * sizeof(bf16);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int tpw = (tiles + 7) / 8;
+  const dim3 grid(nblk), block(512);
   if (tpw <= 4)
-    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 4>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 4, CH>), grid, block, lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
   else if (tpw <= 8)
-    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 8>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 8, CH>), grid, block, lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
   else if (tpw <= 12)
-    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 12>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 12, CH>), grid, block, lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
   else if (tpw <= 18)
-    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 18>), dim3(nblk), dim3(512), lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
+    hipLaunchKernelGGL((conv_wgrad_kernel<TIn, NT, 18, CH>), grid, block, lds, s, X, dY, Y, slab, g, scale, relu_out, mpb);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+template <typename TIn, int NT>
+hipError_t launch_wgrad_nt(const TIn* X, const bf16* dY, const bf16* Y, float* slab, const ConvGeo& g, float scale,
+                           int relu_out, int nblk, int mpb, hipStream_t s) {
+  switch (wgrad_chunk(g)) {
+    case 128: return launch_wgrad_ch<TIn, NT, 128>(X, dY, Y, slab, g, scale, relu_out, nblk, mpb, s);
+    case 64: return launch_wgrad_ch<TIn, NT, 64>(X, dY, Y, slab, g, scale, relu_out, nblk, mpb, s);
+    default: return launch_wgrad_ch<TIn, NT, 32>(X, dY, Y, slab, g, scale, relu_out, nblk, mpb, s);
+  }
 }
 
 template <typename TIn>
@@ -370,7 +428,7 @@ hipError_t launch_wgrad(const TIn* X, const bf16* dY, const bf16* Y, float* slab
   }
   if (e != hipSuccess) return e;
   (void)M;
-  const int K = g.KH * g.KW * g.C;
+  const int K = g.Kp;
   const int len = g.N * K + g.N;
   hipLaunchKernelGGL(conv_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, s, slab, nblk, len, dW, db, g.N * K);
   return hipGetLastError();
@@ -380,33 +438,43 @@ hipError_t launch_wgrad(const TIn* X, const bf16* dY, const bf16* Y, float* slab
 
 bool conv_geo_ok(const ConvGeo& g) {
   const int K = g.KH * g.KW * g.C;
-  if (g.B <= 0 || g.OH <= 0 || g.OW <= 0) return false;
-  if ((g.OH - 1) * g.S + g.KH > g.H || (g.OW - 1) * g.S + g.KW > g.W) return false;
-  if (K % 32 != 0 || (g.KW * g.C) % 8 != 0) return false;
+  if (g.B <= 0 || g.OH <= 0 || g.OW <= 0 || g.P < 0) return false;
+  if ((g.OH - 1) * g.S + g.KH > g.H + 2 * g.P || (g.OW - 1) * g.S + g.KW > g.W + 2 * g.P) return false;
+  if (g.Kp != ((K + 31) & ~31)) return false;
+  if (g.P > 0 || g.Kp != K) {  // tap-checked path
+    if (g.C % 8 != 0 || g.S != 1) return false;
+  } else if ((g.KW * g.C) % 8 != 0) {
+    return false;
+  }
   if (g.N % 16 != 0 || g.N > 64) return false;
   return true;
 }
 
 void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* mpb) {
   const int M = g.B * g.OH * g.OW;
-  const int chunks = (M + 31) / 32;
-  const int K = g.KH * g.KW * g.C;
+  const int CH = wgrad_chunk(g);
+  const int chunks = (M + CH - 1) / CH;
+  const int K = g.Kp;
   // fp32 partial traffic (nblk x N x K, written then re-read by conv_reduce) vs parallelism:
-  // ~1M partial floats per layer at most (the 256-block cap moved 24 MB per NatureCNN BC step)
+  // small layers (BC batches) ~1M partial floats at most (the 256-block cap moved 24 MB per
+  // NatureCNN BC step); large ones (>= 64K rows, e.g. full-resolution reward CNN batches,
+  // where the m loop is the cost) up to 8M floats and 512 blocks -- 2 per CU
   const int len = g.N * K + g.N;
-  int cap = (1 << 20) / len;
-  cap = cap < 16 ? 16 : (cap > 256 ? 256 : cap);
+  const bool big = CH > 32;
+  int cap = (big ? (8 << 20) : (1 << 20)) / len;
+  const int hi = big ? 512 : 256;
+  cap = cap < 16 ? 16 : (cap > hi ? hi : cap);
   int b = chunks < cap ? chunks : cap;
   const int cpb = (chunks + b - 1) / b;
   b = (chunks + cpb - 1) / cpb;
   *nblk = b;
-  *mpb = cpb * 32;
+  *mpb = cpb * CH;
 }
 
 size_t conv_wgrad_slab_floats(const ConvGeo& g) {
   int nblk = 0, mpb = 0;
   conv_wgrad_blocks(g, &nblk, &mpb);
-  const int K = g.KH * g.KW * g.C;
+  const int K = g.Kp;
   return (size_t)nblk * ((size_t)g.N * K + g.N);
 }
 

@@ -162,8 +162,10 @@ hipError_t ppo_launch(const PPOArgs& a, hipStream_t s);
 // ---- conv.hip: NHWC implicit-GEMM convolutions (NatureCNN / reward CNN), bf16 MFMA
 struct ConvGeo {
   int B, H, W, C;  // input NHWC
-  int KH, KW, S;   // kernel, stride (valid padding)
+  int KH, KW, S;   // kernel, stride
   int OH, OW, N;   // output NHWC
+  int P;           // zero padding (symmetric; > 0 only for stride 1 with C % 8 == 0)
+  int Kp;          // GEMM K = KH*KW*C rounded up to 32; weights [N][Kp] zero-padded
 };
 bool conv_geo_ok(const ConvGeo& g);
 void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* m_per_block);

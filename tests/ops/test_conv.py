@@ -23,7 +23,12 @@ def _params(seed, layers=NATURE, device="cpu"):
 def test_supported_shapes():
     ws, _, ss = _params(0)
     assert conv_ops.supported((2, 84, 84, 4), ws, ss)
-    assert not conv_ops.supported((2, 84, 84, 3), [th.zeros(32, 3, 3, 3)], [1])  # K = 27 not a multiple of 32
+    # K = 27: the tap-checked path (input channels zero-padded to 8) needs stride 1
+    assert conv_ops.supported((2, 84, 84, 3), [th.zeros(32, 3, 3, 3)], [1])
+    assert not conv_ops.supported((2, 84, 84, 3), [th.zeros(32, 3, 3, 3)], [2])
+    # reward CNN: 3x3 'same' padding, stride 1 only
+    assert conv_ops.supported((2, 84, 84, 4), [th.zeros(32, 4, 3, 3), th.zeros(32, 32, 3, 3)], [1, 1], [1, 1])
+    assert not conv_ops.supported((2, 84, 84, 4), [th.zeros(32, 4, 3, 3)], [2], [1])
     assert not conv_ops.supported((2, 84, 84, 3), ws, ss)  # channel mismatch
     assert not conv_ops.supported((2, 84, 84, 4), [th.zeros(24, 4, 8, 8)], [4])  # N % 16
 
@@ -52,25 +57,26 @@ def _bf(t):
     return t.to(th.bfloat16).float()
 
 
-def _bf16_emulated(x, ws, bs, ss, gy):
+def _bf16_emulated(x, ws, bs, ss, gy, pads=None):
     """fp32 PyTorch with the kernels' bf16 rounding points (operands, stored activations, dZ):
     isolates kernel errors from the bf16 precision choice itself."""
     import torch.nn.functional as F
     from torch.nn import grad as nng
 
+    pads = list(pads) if pads is not None else [0] * len(ws)
     h, inputs, acts = _bf(x.permute(0, 3, 1, 2)), [], []
-    for w, b, s in zip(ws, bs, ss):
+    for w, b, s, p in zip(ws, bs, ss, pads):
         inputs.append(h)
-        h = _bf(F.relu(F.conv2d(h, _bf(w), b, stride=s)))
+        h = _bf(F.relu(F.conv2d(h, _bf(w), b, stride=s, padding=p)))
         acts.append(h)
     dz = _bf(gy.permute(0, 3, 1, 2)) * (acts[-1] > 0)
     gws, gbs = [None] * len(ws), [None] * len(ws)
     for i in range(len(ws) - 1, -1, -1):
         dzb = _bf(dz)
-        gws[i] = nng.conv2d_weight(inputs[i], ws[i].shape, dzb, stride=ss[i])
+        gws[i] = nng.conv2d_weight(inputs[i], ws[i].shape, dzb, stride=ss[i], padding=pads[i])
         gbs[i] = dzb.sum((0, 2, 3))
         if i > 0:
-            dz = _bf(nng.conv2d_input(inputs[i].shape, _bf(ws[i]), dzb, stride=ss[i]) * (acts[i - 1] > 0))
+            dz = _bf(nng.conv2d_input(inputs[i].shape, _bf(ws[i]), dzb, stride=ss[i], padding=pads[i]) * (acts[i - 1] > 0))
     return acts[-1].permute(0, 2, 3, 1), gws + gbs
 
 
@@ -132,3 +138,35 @@ def test_nature_cnn_policy_bc_step_on_gpu():
     loss.backward()
     g = [p.grad for p in pol.features_extractor.cnn.parameters()]
     assert all(x is not None and th.isfinite(x).all() and float(x.abs().sum()) > 0 for x in g)
+
+
+REWARD_CNN = [((32, 4, 3, 3), 1), ((32, 32, 3, 3), 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,B,H,W", [(4, 6, 20, 17), (8, 2, 84, 84), (3, 5, 9, 11)])
+def test_same_padding_stack_matches_reference(cin, B, H, W):
+    """Reward-CNN stacks (3x3 stride-1 'same' conv + ReLU x2, reward_nets.py CnnRewardNet /
+    BasicPotentialCNN) on the padded kernels: exact w.r.t. the bf16 rounding points, and
+    close to fp32 F.conv2d (cosine for the gradients, as above)."""
+    layers = [((32, cin, 3, 3), 1), ((32, 32, 3, 3), 1)]
+    ws, bs, ss = _params(5, layers, device="cuda")
+    pads = [1, 1]
+    x = th.rand(B, H, W, cin, device="cuda")
+    assert conv_ops.supported(tuple(x.shape), ws, ss, pads)
+    y = conv_ops.conv_stack(x, ws, bs, ss, 1.0, pads)
+    ref = conv_ops.conv_stack_reference(x, ws, bs, ss, 1.0, pads).detach()
+    assert y.shape == ref.shape == (B, H, W, 32)
+    gy = th.randn_like(ref)
+    grads = th.autograd.grad((y * gy).sum(), ws + bs)
+    ref_grads = th.autograd.grad((conv_ops.conv_stack_reference(x, ws, bs, ss, 1.0, pads) * gy).sum(), ws + bs)
+    with th.no_grad():
+        ye, emu = _bf16_emulated(x, [w.detach() for w in ws], [b.detach() for b in bs], ss, gy, pads)
+    assert float((y - ye).norm() / ye.norm()) < 2e-3
+    for g, e in zip(grads, emu):
+        assert g.shape == e.shape
+        assert float((g - e).norm() / (e.norm() + 1e-12)) < 1e-2
+    assert float((y - ref).norm() / ref.norm()) < 1e-2
+    for g, r in zip(grads, ref_grads):
+        cos = float((g * r).sum() / (g.norm() * r.norm() + 1e-12))
+        assert cos > 0.99, cos

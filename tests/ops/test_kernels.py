@@ -210,3 +210,35 @@ def test_tmlp_grouped_matches_per_member_reference(dims, act, B, shared):
         if not shared:
             refx = xr.grad.abs().max().item() + 1e-3
             assert (x.grad[g] - xr.grad).abs().max().item() <= 3e-2 * refx, g
+
+
+@gpu
+def test_reward_cnn_fused_forward_matches_modules():
+    """CnnRewardNet / BasicPotentialCNN (build_cnn's CNN module) on the HIP conv path ==
+    the same modules run layer by layer, forward and parameter gradients."""
+    from imitation_amd.envs import spaces
+    from imitation_amd.rewards.reward_nets import BasicPotentialCNN, CnnRewardNet
+
+    th.manual_seed(0)
+    obs_space = spaces.Box(0, 255, (84, 84, 4), np.uint8)
+    act_space = spaces.Discrete(6)
+    net = CnnRewardNet(obs_space, act_space).cuda()
+    pot = BasicPotentialCNN(obs_space, hid_sizes=(32, 32)).cuda()
+    assert net.cnn._fused_plan() is not None and pot._potential_net._fused_plan() is not None
+    B = 8
+    s = th.rand(B, 84, 84, 4, device="cuda")
+    a = th.nn.functional.one_hot(th.randint(0, 6, (B,), device="cuda"), 6).float()
+    d = th.zeros(B, device="cuda")
+    for mod, fn in ((net, lambda: net(s, a, s, d)), (pot, lambda: pot(s))):
+        out = fn()
+        g_fused = th.autograd.grad(out.sum(), list(mod.parameters()))
+        seq = net.cnn if mod is net else pot._potential_net
+        seq._fused_plan = lambda: None  # the module-by-module path
+        try:
+            ref = fn()
+            g_ref = th.autograd.grad(ref.sum(), list(mod.parameters()))
+        finally:
+            del seq._fused_plan
+        assert th.allclose(out, ref, atol=2e-2, rtol=2e-2), (out - ref).abs().max()
+        for x1, x2 in zip(g_fused, g_ref):
+            assert (x1 - x2).norm() <= 3e-2 * x2.norm() + 1e-6

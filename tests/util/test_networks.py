@@ -63,3 +63,20 @@ def test_build_mlp_shapes_and_names():
 def test_build_cnn_shapes():
     c = networks.build_cnn(in_channels=3, hid_channels=(4, 8), out_size=5)
     assert c(th.randn(2, 3, 16, 16)).shape == (2, 5)
+
+
+def test_build_cnn_fused_plan():
+    """build_cnn returns the CNN module (same layer names) whose conv stack plan is
+    recognised for the HIP path; activations other than ReLU / active dropout opt out."""
+    c = networks.build_cnn(in_channels=4, hid_channels=(32, 32), out_size=1, squeeze_output=True)
+    assert isinstance(c, th.nn.Sequential) and isinstance(c, networks.CNN)
+    assert [k for k in c.state_dict()][:2] == ["conv0.weight", "conv0.bias"]
+    plan = c._fused_plan()
+    assert plan is not None and plan["pads"] == [1, 1] and plan["squeeze"]
+    x = th.randn(3, 4, 12, 12)
+    assert c(x).shape == (3,)  # CPU: modules as given
+    assert networks.build_cnn(in_channels=4, hid_channels=(8,), activation=th.nn.Tanh)._fused_plan() is None
+    d = networks.build_cnn(in_channels=4, hid_channels=(8,), dropout_prob=0.5)
+    assert d._fused_plan() is None
+    d.eval()
+    assert d._fused_plan() is not None
