@@ -38,7 +38,7 @@ namespace {
 
 // rows per wgrad chunk: 128 (or 64 where the chunk's LDS images would not fit) once a layer
 // has at least kWgradBigM GEMM rows, else 32
-constexpr int kWgradBigM = 1 << 16;
+constexpr int kWgradBigM = 1 << 14;
 __host__ __device__ __forceinline__ int wgrad_chunk(const ConvGeo& g) {
   if (g.B * g.OH * g.OW < kWgradBigM) return 32;
   const int rows = g.Kp + g.N;  // LDS image rows (bf16)
@@ -100,12 +100,14 @@ __device__ __forceinline__ bf16x8 load8_pad(const TIn* X, const ConvGeo& g, int 
   return load8(X + ((size_t)(b * g.H + ih) * g.W + iw) * g.C + c, in_scale);
 }
 
-template <typename TIn, int NT, bool PADDED = false>
+// RT row tiles (16 output pixels each) per wave share every weight fragment: at large M the
+// per-wave weight re-reads from L2, not the MFMAs, set the forward's time.
+template <typename TIn, int NT, bool PADDED = false, int RT = 1>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X, const bf16* __restrict__ Wb,
                                                        const float* __restrict__ bias, bf16* __restrict__ Y, ConvGeo g,
                                                        float in_scale, int relu) {
   const int l = threadIdx.x & 63;
-  const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * RT;
   const int OHW = g.OH * g.OW;
   const int M = g.B * OHW;
   if (m0 >= M) return;
@@ -113,31 +115,54 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
   const int n_base = blockIdx.y * 16 * NT;  // split-N grids (small batches): this block's channels
   const int rowlen = g.KW * g.C;
   const int r = l & 15, kq = (l >> 4) * 8;
-  const int m = m0 + r;
-  const bool mv = m < M;
-  const int mm = mv ? m : M - 1;
-  const int b = mm / OHW, pix = mm - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
-  const TIn* xb = PADDED ? X : X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C;
   const size_t xrow = (size_t)g.W * g.C;
-  f32x4 acc[NT];
+  int rb[RT], roh[RT], row_[RT];
+  bool rmv[RT];
+  const TIn* xb[RT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = zero4();
+  for (int ri = 0; ri < RT; ++ri) {
+    const int m = m0 + ri * 16 + r;
+    rmv[ri] = m < M;
+    const int mm = rmv[ri] ? m : M - 1;
+    const int b = mm / OHW, pix = mm - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
+    rb[ri] = b;
+    roh[ri] = oh;
+    row_[ri] = ow;
+    xb[ri] = PADDED ? X : X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C;
+  }
+  f32x4 acc[RT][NT];
+#pragma unroll
+  for (int ri = 0; ri < RT; ++ri)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[ri][t] = zero4();
   const bf16* wr = Wb + (size_t)(n_base + r) * K + kq;
-#pragma unroll 4
+#pragma unroll 2
   for (int k0 = 0; k0 < K; k0 += 32) {
     const int k = k0 + kq;
-    bf16x8 av;
+    bf16x8 bv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bv[t] = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * K + k0);
+    int tap_c = 0, tap_kh = 0, tap_kw = 0;
     if constexpr (PADDED) {
-      av = load8_pad(X, g, b, oh, ow, k, mv, in_scale);
-    } else {
-      const int kh = k / rowlen, off = k - kh * rowlen;
-      av = load8(xb + kh * xrow + off, in_scale);
-      if (!mv) av = zero8();
+      const int tap = k / g.C;
+      tap_c = k - tap * g.C;
+      tap_kh = tap / g.KW;
+      tap_kw = tap - tap_kh * g.KW;
     }
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * K + k0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
+    for (int ri = 0; ri < RT; ++ri) {
+      bf16x8 av;
+      if constexpr (PADDED) {
+        const int ih = roh[ri] * g.S - g.P + tap_kh, iw = row_[ri] * g.S - g.P + tap_kw;
+        const bool ok = rmv[ri] && tap_kh < g.KH && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        av = ok ? load8(X + ((size_t)(rb[ri] * g.H + ih) * g.W + iw) * g.C + tap_c, in_scale) : zero8();
+      } else {
+        const int kh = k / rowlen, off = k - kh * rowlen;
+        av = load8(xb[ri] + kh * xrow + off, in_scale);
+        if (!rmv[ri]) av = zero8();
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[ri][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[t], acc[ri][t], 0, 0, 0);
     }
   }
   const int col = l & 15;
@@ -146,12 +171,15 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
     const int n = n_base + t * 16 + col;
     const float bb = bias ? bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = m0 + 4 * (l >> 4) + i;
-      if (row < M) {
-        float v = acc[t][i] + bb;
-        if (relu) v = fmaxf(v, 0.f);
-        Y[(size_t)row * g.N + n] = (bf16)v;
+    for (int ri = 0; ri < RT; ++ri) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + ri * 16 + 4 * (l >> 4) + i;
+        if (row < M) {
+          float v = acc[ri][t][i] + bb;
+          if (relu) v = fmaxf(v, 0.f);
+          Y[(size_t)row * g.N + n] = (bf16)v;
+        }
       }
     }
   }
@@ -161,7 +189,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
 // Pixels are grouped by stride phase (ih % S, iw % S) (blockIdx.y): every pixel of a phase
 // is hit by the same kh = ph (mod S), kw = pw (mod S) taps, so a tile only walks those
 // (1/S^2 of KH*KW) and only the image border still masks rows.
-template <int CT>
+template <int CT, int RT = 1>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
                                                          const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
                                                          bf16* __restrict__ dZp, ConvGeo g, int relu_out, int relu_in) {
@@ -170,7 +198,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict_
   const int Hc = (g.H - ph + g.S - 1) / g.S, Wc = (g.W - pw + g.S - 1) / g.S;
   const int HWc = Hc * Wc;
   const int P = g.B * HWc;  // pixels of this phase
-  const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * RT;
   if (p0 >= P) return;
   const int Kp = g.KH * g.KW * g.N;
   const int r = l & 15, kq = (l >> 4) * 8;
@@ -180,51 +208,67 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict_
     ih = ph + g.S * i;
     iw = pw + g.S * j;
   };
-  const int p = p0 + r;
-  const bool pv = p < P;
-  int b, ih, iw;
-  pix_of(pv ? p : P - 1, b, ih, iw);
-  f32x4 acc[CT];
+  int pb[RT], pih[RT], piw[RT];
+  bool pv[RT];
 #pragma unroll
-  for (int t = 0; t < CT; ++t) acc[t] = zero4();
+  for (int ri = 0; ri < RT; ++ri) {
+    const int p = p0 + ri * 16 + r;
+    pv[ri] = p < P;
+    pix_of(pv[ri] ? p : P - 1, pb[ri], pih[ri], piw[ri]);
+  }
+  f32x4 acc[RT][CT];
+#pragma unroll
+  for (int ri = 0; ri < RT; ++ri)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[ri][t] = zero4();
   const bf16* wr = Wt + (size_t)r * Kp + kq;
   // (padded convs are stride 1: one phase, every tap; output pixel (ih + P - kh, iw + P - kw))
   for (int kh = ph; kh < g.KH; kh += g.S) {
-    const int th = ih + g.P - kh;
-    const int oh = th / g.S;
-    const bool hv = th >= 0 && oh < g.OH;
     for (int kw = pw; kw < g.KW; kw += g.S) {
-      const int tw = iw + g.P - kw;
-      const int ow = tw / g.S;
-      const bool valid = pv && hv && tw >= 0 && ow < g.OW;
-      if (__ballot(valid) == 0ull) continue;  // this tap misses all 16 pixels of the tile (border)
-      const size_t dzoff = ((size_t)(b * g.OH + oh) * g.OW + ow) * g.N + kq;
+      bool valid[RT];
+      size_t dzoff[RT];
+      bool any = false;
+#pragma unroll
+      for (int ri = 0; ri < RT; ++ri) {
+        const int th = pih[ri] + g.P - kh, tw = piw[ri] + g.P - kw;
+        const int oh = th / g.S, ow = tw / g.S;
+        valid[ri] = pv[ri] && th >= 0 && oh < g.OH && tw >= 0 && ow < g.OW;
+        dzoff[ri] = valid[ri] ? ((size_t)(pb[ri] * g.OH + oh) * g.OW + ow) * g.N + kq : 0;
+        any |= __ballot(valid[ri]) != 0ull;
+      }
+      if (!any) continue;  // this tap misses every pixel of the wave's tiles (border)
       const int kbase = (kh * g.KW + kw) * g.N;
       for (int n0 = 0; n0 < g.N; n0 += 32) {
-        bf16x8 av = zero8();
-        if (valid) av = load_dz8(dY, Y, dzoff + n0, relu_out);
+        bf16x8 bv[CT];
 #pragma unroll
-        for (int t = 0; t < CT; ++t) {
-          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * Kp + kbase + n0);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[t], 0, 0, 0);
+        for (int t = 0; t < CT; ++t) bv[t] = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * Kp + kbase + n0);
+#pragma unroll
+        for (int ri = 0; ri < RT; ++ri) {
+          bf16x8 av = zero8();
+          if (valid[ri]) av = load_dz8(dY, Y, dzoff[ri] + n0, relu_out);
+#pragma unroll
+          for (int t = 0; t < CT; ++t) acc[ri][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[t], acc[ri][t], 0, 0, 0);
         }
       }
     }
   }
   const int col = l & 15;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = p0 + 4 * (l >> 4) + i;
-    if (q >= P) continue;
-    int bb, hh, ww;
-    pix_of(q, bb, hh, ww);
-    const size_t row = ((size_t)bb * g.H + hh) * g.W + ww;
+  for (int ri = 0; ri < RT; ++ri) {
 #pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const int c = t * 16 + col;
-      float v = acc[t][i];
-      if (relu_in && !((float)Xp[row * g.C + c] > 0.f)) v = 0.f;
-      dZp[row * g.C + c] = (bf16)v;
+    for (int i = 0; i < 4; ++i) {
+      const int q = p0 + ri * 16 + 4 * (l >> 4) + i;
+      if (q >= P) continue;
+      int bb, hh, ww;
+      pix_of(q, bb, hh, ww);
+      const size_t row = ((size_t)bb * g.H + hh) * g.W + ww;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int c = t * 16 + col;
+        float v = acc[ri][t][i];
+        if (relu_in && !((float)Xp[row * g.C + c] > 0.f)) v = 0.f;
+        dZp[row * g.C + c] = (bf16)v;
+      }
     }
   }
 }
@@ -354,6 +398,21 @@ hipError_t launch_fwd(const TIn* X, const bf16* Wb, const float* bias, bf16* Y, 
                       hipStream_t s) {
   const int M = g.B * g.OH * g.OW;
   const dim3 block(256);
+  if (M >= (1 << 16)) {  // large M: 4 row tiles per wave
+    const dim3 grid((M + 255) / 256);
+    const bool pad = g.P > 0 || g.Kp != g.KH * g.KW * g.C;
+#define IA_FWD4(NT)                                                                                                   \
+  if (pad) hipLaunchKernelGGL((conv_fwd_kernel<TIn, NT, true, 4>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu); \
+  else hipLaunchKernelGGL((conv_fwd_kernel<TIn, NT, false, 4>), grid, block, 0, s, X, Wb, bias, Y, g, scale, relu)
+    switch (g.N / 16) {
+      case 1: IA_FWD4(1); break;
+      case 2: IA_FWD4(2); break;
+      case 4: IA_FWD4(4); break;
+      default: return hipErrorInvalidValue;
+    }
+#undef IA_FWD4
+    return hipGetLastError();
+  }
   if (g.P > 0 || g.Kp != g.KH * g.KW * g.C) {
     const dim3 grid((M + 63) / 64);
     switch (g.N / 16) {
@@ -509,18 +568,23 @@ hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void*
   if (!conv_geo_ok(g) || g.N % 32 != 0 || g.C % 16 != 0 || g.C > 64) return hipErrorInvalidValue;
   const int Hc = (g.H + g.S - 1) / g.S, Wc = (g.W + g.S - 1) / g.S;  // largest phase
   const int P = g.B * Hc * Wc;
-  const dim3 grid((P + 63) / 64, g.S * g.S), block(256);
+  const bool big = P >= (1 << 16);  // large M: 4 pixel tiles per wave share the weight fragments
+  const dim3 grid(big ? (P + 255) / 256 : (P + 63) / 64, g.S * g.S), block(256);
   const bf16* dy = static_cast<const bf16*>(dY);
   const bf16* y = static_cast<const bf16*>(Y);
   const bf16* wt = static_cast<const bf16*>(Wt);
   const bf16* xp = static_cast<const bf16*>(Xp);
   bf16* dz = static_cast<bf16*>(dZp);
+#define IA_DG(CT)                                                                                                     \
+  if (big) hipLaunchKernelGGL((conv_dgrad_kernel<CT, 4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); \
+  else hipLaunchKernelGGL((conv_dgrad_kernel<CT, 1>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in)
   switch (g.C / 16) {
-    case 1: hipLaunchKernelGGL((conv_dgrad_kernel<1>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); break;
-    case 2: hipLaunchKernelGGL((conv_dgrad_kernel<2>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); break;
-    case 4: hipLaunchKernelGGL((conv_dgrad_kernel<4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); break;
+    case 1: IA_DG(1); break;
+    case 2: IA_DG(2); break;
+    case 4: IA_DG(4); break;
     default: return hipErrorInvalidValue;
   }
+#undef IA_DG
   return hipGetLastError();
 }
 
