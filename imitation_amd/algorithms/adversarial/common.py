@@ -67,15 +67,21 @@ def train_stats_from_sums(vec: Sequence[float], n_labels: float) -> Mapping[str,
 
 def compute_train_stats(disc_logits_expert_is_high: th.Tensor, labels_expert_is_one: th.Tensor, disc_loss: th.Tensor) -> Mapping[str, float]:
     """Discriminator statistics (``common.py:27-92``), reduced on-device, one host sync."""
+    vec = train_stats_vec(disc_logits_expert_is_high, labels_expert_is_one, disc_loss).tolist()
+    return train_stats_from_sums(vec, float(len(labels_expert_is_one)))
+
+
+def train_stats_vec(disc_logits_expert_is_high: th.Tensor, labels_expert_is_one: th.Tensor, disc_loss: th.Tensor) -> th.Tensor:
+    """The device-side sums behind :func:`compute_train_stats` (no host sync):
+    [loss, accuracy, #gen labels, #gen predictions, #expert correct, #gen correct, entropy]."""
     with th.no_grad():
         logits = disc_logits_expert_is_high.float()
         gen_pred = logits < 0
         gen_true = labels_expert_is_one == 0
         exp_true = th.logical_not(gen_true)
-        n_labels = float(len(labels_expert_is_one))
         correct = th.eq(gen_pred, gen_true)
         ent = F.binary_cross_entropy_with_logits(logits, th.sigmoid(logits), reduction="none")
-        vec = th.stack([
+        return th.stack([
             th.mean(disc_loss.float()),
             th.mean(correct.float()),
             th.sum(gen_true.float()),
@@ -83,8 +89,7 @@ def compute_train_stats(disc_logits_expert_is_high: th.Tensor, labels_expert_is_
             th.sum(th.logical_and(exp_true, correct).float()),
             th.sum(th.logical_and(gen_true, correct).float()),
             th.mean(ent),
-        ]).tolist()
-    return train_stats_from_sums(vec, n_labels)
+        ])
 
 
 class _DeviceDemoSampler:

@@ -817,11 +817,80 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             self._record_disc(stats, self._disc_step)
         return stats
 
+    # ------------------------------------------------------------------ graphed generic discriminator update
+    def _graphed_disc_ok(self) -> bool:
+        """The generic (autograd) discriminator step -- e.g. AIRL's shaped reward net, which
+        the fused kernels do not cover -- as one HIP-graph replay per update: single
+        process (no gradient all-reduce / norm collectives), a capturable optimiser, the
+        device demo sampler, and no per-step tensorboard summaries (a host sync)."""
+        from imitation_amd.utils import graphs
+
+        return (not self._fused_disc and pdist.world_size() == 1 and self._disc_bucket is None
+                and graphs.graphs_enabled(self._dev, "IMITATION_AMD_DISC_GRAPH")
+                and graphs.supports_capture(self._disc_opt) and not self._init_tensorboard
+                and isinstance(self._endless_expert_iterator, common._DeviceDemoSampler))
+
+    def _generic_disc_fn(self, e_obs, e_acts, e_next, e_dones, g_idx) -> th.Tensor:
+        """``AdversarialTrainer.train_disc``'s minibatch losses, backward and optimiser step
+        over device batches (expert rows given, generator rows gathered from the device replay
+        buffer by ``g_idx``); returns the last minibatch's statistics sums (device)."""
+        import torch.nn.functional as F
+
+        ga = self._gen_dev._arrays
+        gen = {k: ga[k].index_select(0, g_idx) for k in ("obs", "acts", "next_obs", "dones")}
+        ex = {"obs": e_obs, "acts": e_acts, "next_obs": e_next, "dones": e_dones}
+        for batch in self._make_disc_train_batches(gen_samples=gen, expert_samples=ex):
+            logits = self.logits_expert_is_high(batch["state"], batch["action"], batch["next_state"], batch["done"],
+                                                batch["log_policy_act_prob"])
+            loss = F.binary_cross_entropy_with_logits(logits, batch["labels_expert_is_one"].float())
+            loss = loss * (self.demo_minibatch_size / self.demo_batch_size)
+            loss.backward()
+        self._disc_opt.step()
+        return common.train_stats_vec(logits, batch["labels_expert_is_one"], loss)
+
+    def _graphed_disc_update(self, slot: int) -> None:
+        from imitation_amd.utils import graphs
+
+        if self._gen_dev.size() == 0:
+            raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
+        if getattr(self, "_disc_graph", None) is None:
+            self._disc_graph = graphs.GraphedTrainStep(self._generic_disc_fn, self._disc_opt)
+        ex = self._next_expert_batch()
+        g_idx = th.randint(0, self._gen_dev.size(), (self.demo_batch_size,), device=self._dev)
+        out = self._disc_graph(ex["obs"], ex["acts"], ex["next_obs"], ex["dones"], g_idx)
+        self._disc_stats_gen[slot].copy_(out)
+        self._disc_step += 1
+
+    def _train_graphed_generic(self, total_timesteps: int, callback=None) -> None:
+        n_rounds = total_timesteps // self.gen_train_timesteps
+        assert n_rounds >= 1, (
+            f"No updates (need at least {self.gen_train_timesteps} timesteps, have only total_timesteps={total_timesteps})!")
+        n = self.n_disc_updates_per_round
+        if getattr(self, "_disc_stats_gen", None) is None or self._disc_stats_gen.shape[0] < n:
+            self._disc_stats_gen = th.zeros(max(n, 1), 7, device=self._dev)
+        rows = float(2 * self.demo_minibatch_size)
+        for r in range(n_rounds):
+            self.train_gen(self.gen_train_timesteps)
+            steps = []
+            with networks.training(self.reward_train):
+                for i in range(n):
+                    self._graphed_disc_update(i)
+                    steps.append(self._disc_step)
+            vals = self._disc_stats_gen[:n].tolist() if n else []  # one host sync per round
+            for i in range(n):
+                with self.logger.accumulate_means("disc"):
+                    self._record_disc(common.train_stats_from_sums(vals[i], rows), steps[i])
+            if callback:
+                callback(r)
+            self.logger.dump(self._global_step)
+
     def train(self, total_timesteps: int, callback=None) -> None:
         """Rounds of device generator training + fused discriminator updates; the
         discriminator statistics of a round are fetched with one host sync and logged
         per update exactly as the reference's ``train_disc`` does."""
         if not self._fused_disc:
+            if self._graphed_disc_ok():
+                return self._train_graphed_generic(total_timesteps, callback)
             return super().train(total_timesteps, callback)
         n_rounds = total_timesteps // self.gen_train_timesteps
         assert n_rounds >= 1, (

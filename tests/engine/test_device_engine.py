@@ -322,6 +322,7 @@ def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True):
     rng = np.random.default_rng(seed)
     venv = make_vec_env("seals/Hopper-v1", rng=rng, n_envs=n_envs)
     demo_env = make_vec_env("seals/Hopper-v1", rng=np.random.default_rng(7), n_envs=4)
+    demo_env.action_space.seed(7)  # the random demo policy samples from the action space
     demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
     gen = PPO(ActorCriticPolicy, venv, n_steps=n_steps, batch_size=batch, n_epochs=2, device="cuda", seed=seed,
               policy_kwargs=dict(net_arch=dict(pi=[64, 64], vf=[64, 64]), activation_fn=th.nn.ReLU,
@@ -381,3 +382,39 @@ def test_device_airl_rounds_train():
     assert all(th.isfinite(p).all() for p in list(gen.policy.parameters()) + list(rn.parameters()))
     assert any(not th.equal(a, b) for a, b in zip(p0, gen.policy.parameters()))
     assert any(not th.equal(a, b) for a, b in zip(r0, rn.parameters()))
+
+
+@gpu
+def test_device_airl_graphed_disc_matches_eager():
+    """The generic discriminator update as a HIP-graph replay (AIRL's shaped reward net):
+    same reward-net parameters and logged statistics as the eager autograd updates
+    (IMITATION_AMD_DISC_GRAPH=0), over rounds where the graph is captured then replayed."""
+    def run(graph: bool):
+        os.environ["IMITATION_AMD_DISC_GRAPH"] = "1" if graph else "0"
+        try:
+            tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=3)
+            assert tr._graphed_disc_ok() == graph
+            recs = []
+            if graph:
+                orig = tr._record_disc
+                tr._record_disc = lambda stats, step: (recs.append((step, dict(stats))), orig(stats, step))
+            else:  # the host loop logs inside train_disc, which returns the same statistics
+                orig_td = tr.train_disc
+                tr.train_disc = lambda **kw: (lambda st: (recs.append((tr._disc_step, dict(st))), st)[1])(orig_td(**kw))
+            tr.train(3 * tr.gen_train_timesteps)
+            th.cuda.synchronize()
+            if graph:
+                assert tr._disc_graph.n_captures == 1 and tr._disc_graph.n_replays == 3 * 2 - 1
+            return [p.detach().cpu().clone() for p in rn.parameters()], recs
+        finally:
+            os.environ.pop("IMITATION_AMD_DISC_GRAPH", None)
+
+    p_g, rec_g = run(True)
+    p_e, rec_e = run(False)
+    assert [s for s, _ in rec_g] == [s for s, _ in rec_e]
+    for a, b in zip(p_g, p_e):
+        th.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    for (_, a), (_, b) in zip(rec_g, rec_e):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert abs(a[k] - b[k]) <= 1e-3 * max(1.0, abs(b[k])), (k, a[k], b[k])
