@@ -72,7 +72,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor wb, c10::optional<torch::T
   return y;
 }
 
-// (dW fp32 [N][KH][KW][C], db fp32 [N]); dZ = dy * [y > 0] if relu_out
+// (dW fp32 [N][C][KH][KW] (torch layout), db fp32 [N]); dZ = dy * [y > 0] if relu_out
 py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t KH, int64_t KW, int64_t stride,
                      double in_scale, bool relu_out, int64_t pad) {
   IA_CHECK_CUDA(x);
@@ -89,13 +89,11 @@ py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t
   }
   auto f32 = x.options().dtype(torch::kFloat32);
   auto slab = torch::empty({(int64_t)ia::conv_wgrad_slab_floats(g)}, f32);
-  auto dWp = torch::empty({g.N, g.Kp}, f32);
+  auto dW = torch::empty({g.N, g.C, g.KH, g.KW}, f32);  // torch layout, written by the reduction
   auto db = torch::empty({g.N}, f32);
   IA_HIP_CHECK3(ia::conv_wgrad(in_kind(x), x.data_ptr(), dy.data_ptr(), relu_out ? y.data_ptr() : nullptr,
-                               slab.data_ptr<float>(), dWp.data_ptr<float>(), db.data_ptr<float>(), g, (float)in_scale,
+                               slab.data_ptr<float>(), dW.data_ptr<float>(), db.data_ptr<float>(), g, (float)in_scale,
                                relu_out ? 1 : 0, ia_stream()));
-  const int64_t K = (int64_t)g.KH * g.KW * g.C;
-  auto dW = (K == g.Kp ? dWp : dWp.narrow(1, 0, K).contiguous()).view({g.N, g.KH, g.KW, g.C});
   return py::make_tuple(dW, db);
 }
 
@@ -123,6 +121,36 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, to
   IA_HIP_CHECK3(ia::conv_dgrad(dy.data_ptr(), relu_out ? y.data_ptr() : nullptr, wt.data_ptr(), xp.data_ptr(),
                                dz.data_ptr(), g, relu_out ? 1 : 0, relu_in ? 1 : 0, ia_stream()));
   return dz;
+}
+
+// fp32 conv weights [N, C, KH, KW] -> (bf16 [N, KH, KW, C] each, bf16 [C, KH, KW, N] where want_t)
+py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> want_t) {
+  TORCH_CHECK(ws.size() == want_t.size() && (int)ws.size() <= ia::kMaxPack, "conv_pack_weights: layer count");
+  ia::ConvPackArgs a{};
+  a.n = (int)ws.size();
+  std::vector<torch::Tensor> wbs, wts;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    auto& w = ws[i];
+    IA_CHECK_GPU_F32(w);
+    IA_CHECK_CONTIG(w);
+    TORCH_CHECK(w.dim() == 4, "conv weight must be [N, C, KH, KW]");
+    const int64_t N = w.size(0), C = w.size(1), KH = w.size(2), KW = w.size(3);
+    auto wb = torch::empty({N, KH, KW, C}, w.options().dtype(torch::kBFloat16));
+    torch::Tensor wt;
+    if (want_t[i]) wt = torch::empty({C, KH, KW, N}, w.options().dtype(torch::kBFloat16));
+    a.layer[i] = ia::ConvPackLayer{w.data_ptr<float>(), wb.data_ptr(), want_t[i] ? wt.data_ptr() : nullptr, (int)N,
+                                   (int)C, (int)KH, (int)KW};
+    wbs.push_back(wb);
+    wts.push_back(wt);
+  }
+  IA_HIP_CHECK3(ia::conv_pack_weights(a, ia_stream()));
+  py::list lb, lt;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    lb.append(wbs[i]);
+    if (want_t[i]) lt.append(wts[i]);
+    else lt.append(py::none());
+  }
+  return py::make_tuple(lb, lt);
 }
 
 // h fp32 [B, NH] = relu(x [B, K] . w [NH, K]^T + b); x, w bf16
@@ -191,6 +219,7 @@ void register_conv(py::module& m) {
         py::arg("mix_expert") = py::none(), py::arg("beta") = py::none(), py::arg("exec_out") = py::none());
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv + bias + ReLU (bf16 MFMA)", py::arg("x"), py::arg("wb"),
         py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0);
+  m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts, one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
         py::arg("relu_out"), py::arg("pad") = 0);

@@ -218,6 +218,42 @@ void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg,
   IA_HIP_CHECK(ia::adam_flat(a, ia_stream()));
 }
 
+// categorical evaluate_actions: (log pi(a), entropy) from raw logits z [B, A] fp32, acts [B] int64
+py::tuple cat_eval_fwd(torch::Tensor z, torch::Tensor acts) {
+  IA_CHECK_GPU_F32(z);
+  IA_CHECK_CONTIG(z);
+  IA_CHECK_CUDA(acts);
+  IA_CHECK_CONTIG(acts);
+  TORCH_CHECK(z.dim() == 2 && acts.scalar_type() == torch::kInt64 && acts.numel() == z.size(0), "cat_eval shapes");
+  TORCH_CHECK(z.size(1) <= 64, "cat_eval: at most 64 actions");
+  auto logp = torch::empty({z.size(0)}, z.options());
+  auto ent = torch::empty({z.size(0)}, z.options());
+  IA_HIP_CHECK(ia::cat_eval_fwd(z.data_ptr<float>(), acts.data_ptr<int64_t>(), (int)z.size(0), (int)z.size(1),
+                                 logp.data_ptr<float>(), ent.data_ptr<float>(), ia_stream()));
+  return py::make_tuple(logp, ent);
+}
+
+torch::Tensor cat_eval_bwd(torch::Tensor z, torch::Tensor acts, c10::optional<torch::Tensor> g_lp,
+                           c10::optional<torch::Tensor> g_ent) {
+  IA_CHECK_GPU_F32(z);
+  IA_CHECK_CONTIG(z);
+  const float* gl = nullptr;
+  const float* ge = nullptr;
+  torch::Tensor glc, gec;
+  if (g_lp.has_value() && g_lp->defined()) {
+    glc = g_lp->contiguous().to(torch::kFloat32);
+    gl = glc.data_ptr<float>();
+  }
+  if (g_ent.has_value() && g_ent->defined()) {
+    gec = g_ent->contiguous().to(torch::kFloat32);
+    ge = gec.data_ptr<float>();
+  }
+  auto dz = torch::empty_like(z);
+  IA_HIP_CHECK(ia::cat_eval_bwd(z.data_ptr<float>(), acts.data_ptr<int64_t>(), (int)z.size(0), (int)z.size(1), gl, ge,
+                                 dz.data_ptr<float>(), ia_stream()));
+  return dz;
+}
+
 // [E, n] int32: row e is a pseudo-random permutation of 0..n-1 keyed by (seed, e).
 torch::Tensor random_permutations(int64_t E, int64_t n, int64_t seed, torch::Device device) {
   TORCH_CHECK(device.is_cuda(), "random_permutations runs on the GPU");
@@ -280,4 +316,6 @@ void register_kernels(py::module& m) {
         py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
         py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"));
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
+  m.def("cat_eval_fwd", &cat_eval_fwd, py::arg("z"), py::arg("acts"));
+  m.def("cat_eval_bwd", &cat_eval_bwd, py::arg("z"), py::arg("acts"), py::arg("g_lp"), py::arg("g_ent"));
 }

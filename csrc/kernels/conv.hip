@@ -375,8 +375,11 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
 
 // Fixed-order sum of the wgrad block partials: 4 independent accumulators (blocks b with
 // b % 4 == j) keep 4 loads in flight per thread, combined in a fixed order at the end.
+// The weight gradient is written in torch's [N][C][KH][KW] layout (GEMM column k = (kh, kw, c),
+// columns past K = KH*KW*C are the zero padding of Kp and dropped), so no permute copy follows.
 __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restrict__ slab, int nblk, int len,
-                                                          float* __restrict__ dW, float* __restrict__ db, int nk) {
+                                                          float* __restrict__ dW, float* __restrict__ db, int nk,
+                                                          ConvGeo g) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -389,8 +392,16 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restric
   }
   for (; b < nblk; ++b) s0 += slab[(size_t)b * len + i];
   const float s = (s0 + s1) + (s2 + s3);
-  if (i < nk) dW[i] = s;
-  else if (db) db[i - nk] = s;
+  if (i < nk) {
+    const int n = i / g.Kp, k = i - n * g.Kp;
+    const int taps = g.KH * g.KW;
+    if (k < taps * g.C) {
+      const int tap = k / g.C, c = k - tap * g.C;
+      dW[((size_t)n * g.C + c) * taps + tap] = s;
+    }
+  } else if (db) {
+    db[i - nk] = s;
+  }
 }
 
 template <typename TIn>
@@ -489,11 +500,40 @@ hipError_t launch_wgrad(const TIn* X, const bf16* dY, const bf16* Y, float* slab
   (void)M;
   const int K = g.Kp;
   const int len = g.N * K + g.N;
-  hipLaunchKernelGGL(conv_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, s, slab, nblk, len, dW, db, g.N * K);
+  hipLaunchKernelGGL(conv_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, s, slab, nblk, len, dW, db, g.N * K, g);
   return hipGetLastError();
 }
 
+// fp32 torch-layout conv weights [N][C][KH][KW] of up to kMaxPack layers -> bf16 [N][KH][KW][C]
+// (forward GEMM operand) and, where requested, bf16 [C][KH][KW][N] (data-gradient operand),
+// all layers in one launch (blockIdx.y = layer).
+__global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a) {
+  const int li = blockIdx.y;
+  const ConvPackLayer& L = a.layer[li];
+  const int taps = L.KH * L.KW;
+  const int total = L.N * L.C * taps;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int n = i / (L.C * taps), rem = i - n * L.C * taps, c = rem / taps, tap = rem - c * taps;
+    const bf16 v = (bf16)L.w[i];
+    static_cast<bf16*>(L.wb)[((size_t)n * taps + tap) * L.C + c] = v;
+    if (L.wt) static_cast<bf16*>(L.wt)[((size_t)c * taps + tap) * L.N + n] = v;
+  }
+}
+
 }  // namespace
+
+hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  if (a.n > kMaxPack) return hipErrorInvalidValue;
+  int most = 0;
+  for (int i = 0; i < a.n; ++i) {
+    const int t = a.layer[i].N * a.layer[i].C * a.layer[i].KH * a.layer[i].KW;
+    most = t > most ? t : most;
+  }
+  const int bx = (most + 255) / 256 < 64 ? (most + 255) / 256 : 64;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(bx, a.n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
 
 bool conv_geo_ok(const ConvGeo& g) {
   const int K = g.KH * g.KW * g.C;

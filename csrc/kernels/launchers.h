@@ -134,6 +134,11 @@ hipError_t gae_launch(const float* rew, const float* val, const float* starts, c
                       int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);
 // E keyed pseudo-random permutations of [0, n) (Feistel + cycle walking), out [E, n] int32
 hipError_t perm_feistel(int E, int n, uint64_t seed, int* out, hipStream_t s);
+// categorical head: log-prob of the taken action + entropy from raw logits [B][A], and the
+// logit gradient for upstream gradients g_lp / g_ent (either may be nullptr = 0)
+hipError_t cat_eval_fwd(const float* z, const int64_t* act, int B, int A, float* logp, float* ent, hipStream_t s);
+hipError_t cat_eval_bwd(const float* z, const int64_t* act, int B, int A, const float* g_lp, const float* g_ent, float* dz,
+                        hipStream_t s);
 
 // ---- pref.hip: Bradley-Terry preference loss over fragment pairs
 hipError_t pref_loss_fwd(const float* r1, const float* r2, const float* prefs, int P, int L, float discount,
@@ -168,6 +173,20 @@ struct ConvGeo {
   int Kp;          // GEMM K = KH*KW*C rounded up to 32; weights [N][Kp] zero-padded
 };
 bool conv_geo_ok(const ConvGeo& g);
+// one-launch weight packing for a conv stack (ops/conv.py): fp32 [N][C][KH][KW] -> bf16
+// [N][KH][KW][C] and optionally bf16 [C][KH][KW][N]
+constexpr int kMaxPack = 8;
+struct ConvPackLayer {
+  const float* w;
+  void* wb;  // bf16
+  void* wt;  // bf16, nullptr: not needed
+  int N, C, KH, KW;
+};
+struct ConvPackArgs {
+  ConvPackLayer layer[kMaxPack];
+  int n;
+};
+hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s);
 void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* m_per_block);
 size_t conv_wgrad_slab_floats(const ConvGeo& g);
 // in_kind: 0 fp32, 1 bf16, 2 uint8 input; weights bf16 [N][KH][KW][C]; Y bf16 [B*OH*OW][N]

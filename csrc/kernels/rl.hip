@@ -149,4 +149,68 @@ hipError_t perm_feistel(int E, int n, uint64_t seed, int* out, hipStream_t s) {
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------- categorical evaluate_actions
+// log pi(a|s) and the entropy of a categorical head from its raw logits [B][A] in one pass
+// (logsumexp, gather, softmax, entropy: ~10 torch kernels), and the matching logit gradient
+// dz_k = g_lp (1[k == a] - p_k) - g_ent p_k (log p_k + H). One thread per row (A <= 64).
+namespace {
+__global__ __launch_bounds__(256) void cat_eval_fwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ act,
+                                                           int B, int A, float* __restrict__ logp, float* __restrict__ ent) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= B) return;
+  const float* zr = z + (size_t)r * A;
+  float mx = -INFINITY;
+  for (int k = 0; k < A; ++k) mx = fmaxf(mx, zr[k]);
+  float se = 0.f;
+  for (int k = 0; k < A; ++k) se += expf(zr[k] - mx);
+  const float lse = mx + logf(se);
+  float h = 0.f;
+  for (int k = 0; k < A; ++k) {
+    const float lp = zr[k] - lse;
+    h -= expf(lp) * lp;
+  }
+  const int a = (int)act[r];
+  logp[r] = (a >= 0 && a < A) ? zr[a] - lse : -INFINITY;
+  ent[r] = h;
+}
+
+__global__ __launch_bounds__(256) void cat_eval_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ act,
+                                                           int B, int A, const float* __restrict__ g_lp,
+                                                           const float* __restrict__ g_ent, float* __restrict__ dz) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= B) return;
+  const float* zr = z + (size_t)r * A;
+  float mx = -INFINITY;
+  for (int k = 0; k < A; ++k) mx = fmaxf(mx, zr[k]);
+  float se = 0.f;
+  for (int k = 0; k < A; ++k) se += expf(zr[k] - mx);
+  const float lse = mx + logf(se);
+  float h = 0.f;
+  for (int k = 0; k < A; ++k) {
+    const float lp = zr[k] - lse;
+    h -= expf(lp) * lp;
+  }
+  const float gl = g_lp ? g_lp[r] : 0.f, ge = g_ent ? g_ent[r] : 0.f;
+  const int a = (int)act[r];
+  for (int k = 0; k < A; ++k) {
+    const float lp = zr[k] - lse, p = expf(lp);
+    dz[(size_t)r * A + k] = gl * ((k == a ? 1.f : 0.f) - p) - ge * p * (lp + h);
+  }
+}
+}  // namespace
+
+hipError_t cat_eval_fwd(const float* z, const int64_t* act, int B, int A, float* logp, float* ent, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cat_eval_fwd_kernel, dim3((B + 255) / 256), dim3(256), 0, s, z, act, B, A, logp, ent);
+  return hipGetLastError();
+}
+
+hipError_t cat_eval_bwd(const float* z, const int64_t* act, int B, int A, const float* g_lp, const float* g_ent, float* dz,
+                        hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cat_eval_bwd_kernel, dim3((B + 255) / 256), dim3(256), 0, s, z, act, B, A, g_lp, g_ent, dz);
+  return hipGetLastError();
+}
+
 }  // namespace ia

@@ -75,10 +75,12 @@ class _ConvStack(torch.autograd.Function):
         ws, bs = params[0::2], params[1::2]
         acts: List[torch.Tensor] = []
         h = x
-        for i, (w, b, s, p) in enumerate(zip(ws, bs, strides, pads)):
-            wb = w.detach().permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+        # every layer's bf16 GEMM weights (and the data-gradient layouts of layers 1..n-1) in ONE launch
+        wbs, wts = C.conv_pack_weights([w.detach().contiguous() for w in ws], [i > 0 for i in range(len(ws))])
+        for i, (wb, b, s, p) in enumerate(zip(wbs, bs, strides, pads)):
             h = C.conv_fwd(h, wb, b.detach().float().contiguous(), int(s), float(in_scale) if i == 0 else 1.0, True, int(p))
             acts.append(h)
+        ctx.wts = wts
         ctx.save_for_backward(x, *ws, *acts)
         ctx.in_scale = float(in_scale)
         ctx.strides = tuple(int(s) for s in strides)
@@ -100,12 +102,11 @@ class _ConvStack(torch.autograd.Function):
             inp = x if i == 0 else acts[i - 1]
             top = i == n - 1  # only the top layer's ReLU mask is still pending on dz
             scale = ctx.in_scale if i == 0 else 1.0
-            dW, db = C.conv_wgrad(inp, dz, acts[i], int(KH), int(KW), int(s), scale, top, p)
-            grads[2 * i] = dW.permute(0, 3, 1, 2).contiguous().to(w.dtype)
+            dW, db = C.conv_wgrad(inp, dz, acts[i], int(KH), int(KW), int(s), scale, top, p)  # [N, C, KH, KW]
+            grads[2 * i] = dW if dW.dtype == w.dtype else dW.to(w.dtype)
             grads[2 * i + 1] = db
             if i > 0:
-                wt = w.detach().permute(1, 2, 3, 0).contiguous().to(torch.bfloat16)
-                dz = C.conv_dgrad(dz, acts[i], wt, acts[i - 1], int(s), top, True, p)
+                dz = C.conv_dgrad(dz, acts[i], ctx.wts[i], acts[i - 1], int(s), top, True, p)
         return (None, None, None, None, None, *grads)
 
 

@@ -133,13 +133,22 @@ class CategoricalDistribution(Distribution):
     def __init__(self, action_dim: int):
         self.action_dim = action_dim
         self.logits: Optional[th.Tensor] = None
+        self.raw_logits: Optional[th.Tensor] = None
 
     def proba_distribution_net(self, latent_dim: int) -> nn.Module:
         return nn.Linear(latent_dim, self.action_dim)
 
     def proba_distribution(self, action_logits: th.Tensor) -> "CategoricalDistribution":
+        self.raw_logits = action_logits
         self.logits = action_logits - action_logits.logsumexp(dim=-1, keepdim=True)
         return self
+
+    def log_prob_entropy(self, actions: th.Tensor) -> Tuple[th.Tensor, th.Tensor]:
+        """``(log_prob(actions), entropy())`` in one fused pass over the raw logits (HIP
+        ``cat_eval`` on the GPU, identical formulas on the CPU)."""
+        from imitation_amd.ops.rl import categorical_eval
+
+        return categorical_eval(self.raw_logits, actions)
 
     @property
     def probs(self) -> th.Tensor:

@@ -145,6 +145,11 @@ class BaseModel(nn.Module):
 
     def extract_features(self, obs, features_extractor: Optional[nn.Module] = None) -> th.Tensor:
         fe = features_extractor if features_extractor is not None else self.features_extractor
+        if (self.normalize_images and isinstance(fe, NatureCNN) and fe.raw_frames_ok(obs)
+                and is_image_space(self.observation_space)):
+            # uint8 frames straight into the conv kernels, /255 folded into the first layer's
+            # operand load: no float copy of the batch (== preprocess_obs then fe)
+            return fe(obs, 1.0 / 255.0)
         preprocessed = preprocess_obs(obs, self.observation_space, normalize_images=self.normalize_images)
         return fe(preprocessed)
 
@@ -521,8 +526,11 @@ class ActorCriticPolicy(BasePolicy):
                 latent_vf = self.mlp_extractor.forward_critic(vf_features)
             distribution = self._get_action_dist_from_latent(latent_pi)
             values = self.value_net(latent_vf)
-        log_prob = distribution.log_prob(actions)
-        entropy = distribution.entropy()
+        if isinstance(distribution, CategoricalDistribution):
+            log_prob, entropy = distribution.log_prob_entropy(actions)
+        else:
+            log_prob = distribution.log_prob(actions)
+            entropy = distribution.entropy()
         return values, log_prob, entropy
 
     def get_distribution(self, obs) -> Distribution:

@@ -64,16 +64,31 @@ class NatureCNN(BaseFeaturesExtractor):
             n_flatten = self.cnn(th.zeros((1,) + chw)).shape[1]
         self.linear = nn.Sequential(nn.Linear(n_flatten, features_dim), nn.ReLU())
 
-    def forward(self, observations: th.Tensor) -> th.Tensor:
+    def forward(self, observations: th.Tensor, in_scale: float = 1.0) -> th.Tensor:
         # conv trunk: NHWC implicit-GEMM MFMA kernels on GPU (ops/conv.py, csrc/kernels/conv.hip),
-        # fp32 reference on CPU; the module keeps SB3's state-dict layout (cnn.{0,2,4}, linear.0)
+        # fp32 reference on CPU; the module keeps SB3's state-dict layout (cnn.{0,2,4}, linear.0).
+        # ``in_scale``: raw uint8 frames with the image normalisation (1/255) folded into the
+        # first layer's operand load (see BaseModel.extract_features)
         from imitation_amd.ops import conv as conv_ops
 
         x = observations if self.channels_last_input else observations.permute(0, 2, 3, 1)
         convs = [m for m in self.cnn if isinstance(m, nn.Conv2d)]
-        y = conv_ops.conv_stack(x, [c.weight for c in convs], [c.bias for c in convs], [c.stride[0] for c in convs])
+        y = conv_ops.conv_stack(x, [c.weight for c in convs], [c.bias for c in convs], [c.stride[0] for c in convs],
+                                in_scale)
         y = y.permute(0, 3, 1, 2).reshape(y.shape[0], -1)  # nn.Flatten order (C, H, W)
         return self.linear(y)
+
+    def raw_frames_ok(self, obs) -> bool:
+        """Whether ``obs`` (un-preprocessed) can go to :meth:`forward` as uint8 with in_scale
+        1/255: channel-last frames on the GPU kernel path."""
+        from imitation_amd.ops import conv as conv_ops
+        from imitation_amd import ops
+
+        if not (isinstance(obs, th.Tensor) and obs.dtype == th.uint8 and obs.is_cuda and obs.dim() == 4
+                and self.channels_last_input and ops.use_kernel(obs)):
+            return False
+        convs = [m for m in self.cnn if isinstance(m, nn.Conv2d)]
+        return conv_ops.supported(tuple(obs.shape), [c.weight for c in convs], [c.stride[0] for c in convs])
 
 
 class CombinedExtractor(BaseFeaturesExtractor):

@@ -138,6 +138,18 @@ def test_nature_cnn_policy_bc_step_on_gpu():
     loss.backward()
     g = [p.grad for p in pol.features_extractor.cnn.parameters()]
     assert all(x is not None and th.isfinite(x).all() and float(x.abs().sum()) > 0 for x in g)
+    # raw uint8 frames (1/255 folded into the first conv's operand load) == the float
+    # preprocessed path, forward and gradients
+    fe = pol.features_extractor
+    assert fe.raw_frames_ok(obs)
+    ws = list(fe.parameters())
+    y_raw = fe(obs, 1.0 / 255.0)
+    g_raw = th.autograd.grad(y_raw.square().sum(), ws)
+    y_f = fe(obs.float() / 255.0)
+    g_f = th.autograd.grad(y_f.square().sum(), ws)
+    th.testing.assert_close(y_raw, y_f, rtol=1e-3, atol=1e-3)
+    for a, b in zip(g_raw, g_f):
+        th.testing.assert_close(a, b, rtol=2e-2, atol=1e-3 * float(b.abs().max()))
 
 
 REWARD_CNN = [((32, 4, 3, 3), 1), ((32, 32, 3, 3), 1)]

@@ -242,3 +242,21 @@ def test_reward_cnn_fused_forward_matches_modules():
         assert th.allclose(out, ref, atol=2e-2, rtol=2e-2), (out - ref).abs().max()
         for x1, x2 in zip(g_fused, g_ref):
             assert (x1 - x2).norm() <= 3e-2 * x2.norm() + 1e-6
+
+
+@gpu
+@pytest.mark.parametrize("B,A", [(32, 6), (1, 2), (1000, 18), (257, 64)])
+def test_categorical_eval_kernel_matches_autograd(B, A):
+    g = th.Generator().manual_seed(B * 100 + A)
+    z = (3 * th.randn(B, A, generator=g)).double()
+    a = th.randint(0, A, (B,), generator=g)
+    w_lp, w_ent = th.randn(B, generator=g).double(), th.randn(B, generator=g).double()
+    zr = z.clone().requires_grad_(True)
+    lp_r, ent_r = rl_ops.categorical_eval_reference(zr.double(), a)
+    ((lp_r * w_lp).sum() + (ent_r * w_ent).sum()).backward()
+    zg = z.float().cuda().requires_grad_(True)
+    lp, ent = rl_ops.categorical_eval(zg, a.cuda())
+    ((lp * w_lp.float().cuda()).sum() + (ent * w_ent.float().cuda()).sum()).backward()
+    th.testing.assert_close(lp.double().cpu(), lp_r.detach(), rtol=1e-5, atol=1e-5)
+    th.testing.assert_close(ent.double().cpu(), ent_r.detach(), rtol=1e-5, atol=1e-5)
+    th.testing.assert_close(zg.grad.double().cpu(), zr.grad, rtol=1e-4, atol=1e-5)

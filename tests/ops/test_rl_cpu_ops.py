@@ -27,3 +27,16 @@ def test_feistel_keyed_and_roughly_uniform():
     assert counts.min() > 20 and counts.max() < 80
     # displacement is not concentrated near the identity
     assert np.mean(np.abs(a[0] - np.arange(4096))) > 1000
+
+
+def test_categorical_eval_reference_matches_distribution():
+    import torch as th
+
+    from imitation_amd.rl.distributions import CategoricalDistribution
+
+    z = th.randn(50, 6)
+    a = th.randint(0, 6, (50,))
+    d = CategoricalDistribution(6).proba_distribution(z)
+    lp, ent = d.log_prob_entropy(a)
+    th.testing.assert_close(lp, d.log_prob(a))
+    th.testing.assert_close(ent, d.entropy())

@@ -1,0 +1,36 @@
+"""BC minibatch steps only (NatureCNN ActorCriticCnnPolicy, B=32, graphed), for a kernel trace."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch as th  # noqa: E402
+
+
+def main():
+    from imitation_amd.algorithms import bc
+    from imitation_amd.engine.dagger import DeviceDemoAggregate, DeviceTransitionsLoader
+    from imitation_amd.envs.vec_env import native_spaces
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+    from imitation_amd.util import logger
+
+    obs_space, act_space = native_spaces("PongNoFrameskip-v4")
+    pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
+    agg = DeviceDemoAggregate("cuda")
+    agg.append(th.randint(0, 255, (4096, 84, 84, 4), dtype=th.uint8, device="cuda"), th.randint(0, 6, (4096,), device="cuda"))
+    bct = bc.BC(observation_space=obs_space, action_space=act_space, rng=np.random.default_rng(0), policy=pol,
+                batch_size=32, device="cuda", custom_logger=logger.configure("/tmp/ia_probe_bc", format_strs=[]))
+    bct.set_demonstrations(DeviceTransitionsLoader(agg, 32, 0))
+    kw = dict(n_batches=100, log_interval=10**9, progress_bar=False)
+    bct.train(**kw)
+    th.cuda.synchronize()
+    t0 = time.perf_counter()
+    bct.train(**kw)
+    th.cuda.synchronize()
+    print(f"BC step B=32: {1e3 * (time.perf_counter() - t0) / 100:.3f} ms/batch", flush=True)
+
+
+if __name__ == "__main__":
+    main()
