@@ -254,6 +254,134 @@ torch::Tensor cat_eval_bwd(torch::Tensor z, torch::Tensor acts, c10::optional<to
   return dz;
 }
 
+// BC loss on a categorical head: metric vector [7] (see rl.hip) from raw logits z [B, A] fp32,
+// acts [B] int64 and (optionally) the flat fp32 parameter buffer for l2_norm
+torch::Tensor bc_cat_loss_fwd(torch::Tensor z, torch::Tensor acts, c10::optional<torch::Tensor> flat, double ent_w,
+                              double l2_w) {
+  IA_CHECK_GPU_F32(z);
+  IA_CHECK_CONTIG(z);
+  IA_CHECK_CUDA(acts);
+  IA_CHECK_CONTIG(acts);
+  TORCH_CHECK(z.dim() == 2 && acts.scalar_type() == torch::kInt64 && acts.numel() == z.size(0), "bc_cat_loss shapes");
+  TORCH_CHECK(z.size(0) > 0 && z.size(1) <= 64, "bc_cat_loss: 1..64 actions, B > 0");
+  const float* fp = nullptr;
+  long n = 0;
+  if (flat.has_value() && flat->defined()) {
+    IA_CHECK_GPU_F32((*flat));
+    IA_CHECK_CONTIG((*flat));
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(flat->data_ptr()) % 16 == 0, "flat parameter buffer must be 16-B aligned");
+    fp = flat->data_ptr<float>();
+    n = (long)flat->numel();
+  }
+  auto out = torch::empty({7}, z.options());
+  auto part = torch::empty({fp ? ia::sumsq_nparts(n) : 1}, z.options());
+  IA_HIP_CHECK(ia::bc_cat_loss_fwd(z.data_ptr<float>(), acts.data_ptr<int64_t>(), (int)z.size(0), (int)z.size(1), fp, n,
+                                   part.data_ptr<float>(), (float)ent_w, (float)l2_w, out.data_ptr<float>(), ia_stream()));
+  return out;
+}
+
+torch::Tensor bc_cat_loss_bwd(torch::Tensor z, torch::Tensor acts, torch::Tensor g, double ent_w) {
+  IA_CHECK_GPU_F32(z);
+  IA_CHECK_CONTIG(z);
+  auto gc = g.contiguous().to(torch::kFloat32);
+  TORCH_CHECK(gc.numel() == 7 && gc.is_cuda(), "bc_cat_loss_bwd: g must be the [7] metric gradient");
+  auto dz = torch::empty_like(z);
+  IA_HIP_CHECK(ia::bc_cat_loss_bwd(z.data_ptr<float>(), acts.data_ptr<int64_t>(), (int)z.size(0), (int)z.size(1),
+                                   gc.data_ptr<float>(), (float)ent_w, dz.data_ptr<float>(), ia_stream()));
+  return dz;
+}
+
+// MCE-IRL soft value iteration: T [S, A, S] fp64, R [S] fp64 -> (V [H, S], Q [H, S, A], pi [H, S, A])
+py::tuple soft_value_iteration(torch::Tensor T, torch::Tensor R, int64_t H, double gamma) {
+  IA_CHECK_CUDA(T);
+  IA_CHECK_CONTIG(T);
+  IA_CHECK_CUDA(R);
+  IA_CHECK_CONTIG(R);
+  TORCH_CHECK(T.scalar_type() == torch::kFloat64 && R.scalar_type() == torch::kFloat64, "fp64 T / R");
+  TORCH_CHECK(T.dim() == 3 && T.size(0) == T.size(2) && R.dim() == 1 && R.size(0) == T.size(0), "T [S, A, S], R [S]");
+  const int S = (int)T.size(0), A = (int)T.size(1);
+  TORCH_CHECK(ia::soft_vi_fits(S, A) && H > 0, "soft_value_iteration: S * (A + 1) doubles must fit LDS");
+  auto V = torch::empty({H, S}, T.options());
+  auto Q = torch::empty({H, S, A}, T.options());
+  auto P = torch::empty({H, S, A}, T.options());
+  IA_HIP_CHECK(ia::soft_value_iteration(T.data_ptr<double>(), R.data_ptr<double>(), S, A, (int)H, gamma,
+                                        V.data_ptr<double>(), Q.data_ptr<double>(), P.data_ptr<double>(), ia_stream()));
+  return py::make_tuple(V, Q, P);
+}
+
+// MCE-IRL occupancy: T [S, A, S], pi [H, S, A], D0 [S] (fp64) -> D [H + 1, S]
+torch::Tensor occupancy_measures(torch::Tensor T, torch::Tensor P, torch::Tensor D0) {
+  for (auto* t : {&T, &P, &D0}) {
+    IA_CHECK_CUDA((*t));
+    IA_CHECK_CONTIG((*t));
+    TORCH_CHECK(t->scalar_type() == torch::kFloat64, "occupancy_measures: fp64 inputs");
+  }
+  TORCH_CHECK(T.dim() == 3 && T.size(0) == T.size(2) && P.dim() == 3 && P.size(1) == T.size(0) && P.size(2) == T.size(1) &&
+                  D0.numel() == T.size(0),
+              "T [S, A, S], pi [H, S, A], D0 [S]");
+  const int S = (int)T.size(0), A = (int)T.size(1), H = (int)P.size(0);
+  TORCH_CHECK(ia::soft_vi_fits(S, A), "occupancy_measures: S * (A + 1) doubles must fit LDS");
+  auto D = torch::empty({H + 1, S}, T.options());
+  IA_HIP_CHECK(ia::occupancy_measures(T.data_ptr<double>(), P.data_ptr<double>(), D0.data_ptr<double>(), S, A, H,
+                                      D.data_ptr<double>(), ia_stream()));
+  return D;
+}
+
+// KDE: q [NQ, d], x [N, d] fp64 -> logsumexp_j log k(|q - x_j| / h) + offset, [NQ]
+torch::Tensor kde_score(torch::Tensor q, torch::Tensor x, double bandwidth, int64_t kind, double offset) {
+  IA_CHECK_CUDA(q);
+  IA_CHECK_CONTIG(q);
+  IA_CHECK_CUDA(x);
+  IA_CHECK_CONTIG(x);
+  TORCH_CHECK(q.scalar_type() == torch::kFloat64 && x.scalar_type() == torch::kFloat64, "kde_score: fp64 inputs");
+  TORCH_CHECK(q.dim() == 2 && x.dim() == 2 && q.size(1) == x.size(1), "kde_score: q [NQ, d], x [N, d]");
+  const int NQ = (int)q.size(0), N = (int)x.size(0), d = (int)q.size(1);
+  TORCH_CHECK(N > 0 && d > 0 && d <= ia::kKdeMaxDim && kind >= 0 && kind <= 5 && bandwidth > 0, "kde_score args");
+  auto out = torch::empty({NQ}, q.options());
+  if (NQ == 0) return out;
+  const int ns = ia::kde_splits(NQ, N);
+  auto pm = torch::empty({(int64_t)ns * NQ}, q.options());
+  auto ps = torch::empty({(int64_t)ns * NQ}, q.options());
+  IA_HIP_CHECK(ia::kde_score(q.data_ptr<double>(), x.data_ptr<double>(), NQ, N, d, 1.0 / bandwidth, (int)kind, offset,
+                             pm.data_ptr<double>(), ps.data_ptr<double>(), out.data_ptr<double>(), ia_stream()));
+  return out;
+}
+
+// rows b (x n_envs + e) of every source [R, ...] -> new [n, ...] tensors, one launch
+std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::Tensor b, c10::optional<torch::Tensor> e,
+                                       int64_t n_envs) {
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= ia::kGatherMax, "gather_rows: 1..8 fields");
+  IA_CHECK_CUDA(b);
+  IA_CHECK_CONTIG(b);
+  TORCH_CHECK(b.scalar_type() == torch::kInt64 && b.dim() == 1, "gather_rows: b int64 [n]");
+  const int64_t n = b.numel();
+  const int64_t* ep = nullptr;
+  if (e.has_value() && e->defined()) {
+    IA_CHECK_CUDA((*e));
+    IA_CHECK_CONTIG((*e));
+    TORCH_CHECK(e->scalar_type() == torch::kInt64 && e->numel() == n && n_envs >= 1, "gather_rows: e int64 [n]");
+    ep = e->data_ptr<int64_t>();
+  }
+  ia::GatherArgs a{};
+  a.k = (int)srcs.size();
+  std::vector<torch::Tensor> outs;
+  for (int i = 0; i < a.k; ++i) {
+    auto& t = srcs[i];
+    IA_CHECK_CUDA(t);
+    IA_CHECK_CONTIG(t);
+    TORCH_CHECK(t.dim() >= 1 && t.device() == b.device(), "gather_rows: sources [R, ...] on b's device");
+    auto sizes = t.sizes().vec();
+    const int64_t rows = sizes[0];
+    TORCH_CHECK(rows % (ep ? n_envs : 1) == 0, "gather_rows: rows must be a multiple of n_envs");
+    sizes[0] = n;
+    auto o = torch::empty(sizes, t.options());
+    a.f[i] = ia::GatherField{t.data_ptr(), o.data_ptr(), rows ? (int64_t)(t.nbytes() / rows) : 0, rows};
+    outs.push_back(o);
+  }
+  IA_HIP_CHECK(ia::gather_rows(a, b.data_ptr<int64_t>(), ep, (int)n_envs, (int)n, ia_stream()));
+  return outs;
+}
+
 // [E, n] int32: row e is a pseudo-random permutation of 0..n-1 keyed by (seed, e).
 torch::Tensor random_permutations(int64_t E, int64_t n, int64_t seed, torch::Device device) {
   TORCH_CHECK(device.is_cuda(), "random_permutations runs on the GPU");
@@ -316,6 +444,13 @@ void register_kernels(py::module& m) {
         py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
         py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"));
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
+  m.def("gather_rows", &gather_rows, py::arg("srcs"), py::arg("b"), py::arg("e") = py::none(), py::arg("n_envs") = 1);
+  m.def("soft_value_iteration", &soft_value_iteration, py::arg("T"), py::arg("R"), py::arg("H"), py::arg("gamma"));
+  m.def("occupancy_measures", &occupancy_measures, py::arg("T"), py::arg("P"), py::arg("D0"));
+  m.def("kde_score", &kde_score, py::arg("q"), py::arg("x"), py::arg("bandwidth"), py::arg("kind"), py::arg("offset"));
+  m.def("bc_cat_loss_fwd", &bc_cat_loss_fwd, py::arg("z"), py::arg("acts"), py::arg("flat"), py::arg("ent_w"),
+        py::arg("l2_w"));
+  m.def("bc_cat_loss_bwd", &bc_cat_loss_bwd, py::arg("z"), py::arg("acts"), py::arg("g"), py::arg("ent_w"));
   m.def("cat_eval_fwd", &cat_eval_fwd, py::arg("z"), py::arg("acts"));
   m.def("cat_eval_bwd", &cat_eval_bwd, py::arg("z"), py::arg("acts"), py::arg("g_lp"), py::arg("g_ent"));
 }

@@ -139,6 +139,43 @@ hipError_t perm_feistel(int E, int n, uint64_t seed, int* out, hipStream_t s);
 hipError_t cat_eval_fwd(const float* z, const int64_t* act, int B, int A, float* logp, float* ent, hipStream_t s);
 hipError_t cat_eval_bwd(const float* z, const int64_t* act, int B, int A, const float* g_lp, const float* g_ent, float* dz,
                         hipStream_t s);
+// BC loss on a categorical head: metrics [neglogp, entropy, ent_loss, prob_true_act, l2_norm,
+// l2_loss, loss] (flat/n: parameter buffer for l2_norm, part: sumsq_nparts(n) floats), and the
+// logit gradient for an upstream gradient g[7] of the metric vector
+int sumsq_nparts(long n);
+hipError_t bc_cat_loss_fwd(const float* z, const int64_t* act, int B, int A, const float* flat, long n, float* part,
+                           float ent_w, float l2_w, float* out, hipStream_t s);
+hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, const float* g, float ent_w, float* dz,
+                           hipStream_t s);
+
+// ---- gather.hip: one-launch multi-field row gather (row r <- source row b[r] * n_envs + e[r],
+// or b[r] when e == nullptr)
+constexpr int kGatherMax = 8;
+struct GatherField {
+  const void* src;
+  void* dst;
+  int64_t row_bytes;
+  int64_t rows;  // source rows: out-of-range indices produce zero rows, never a stray read
+};
+struct GatherArgs {
+  GatherField f[kGatherMax];
+  int k;
+};
+hipError_t gather_rows(const GatherArgs& a, const int64_t* b, const int64_t* e, int n_envs, int n, hipStream_t s);
+
+// ---- tabular.hip: MCE-IRL soft value iteration / occupancy (fp64, one workgroup, LDS-resident
+// vectors: S * (A + 1) doubles <= 150 KB) and KDE log-density scoring (fp64, d <= kKdeMaxDim)
+bool soft_vi_fits(int S, int A);
+hipError_t soft_value_iteration(const double* T, const double* R, int S, int A, int H, double gamma, double* V, double* Q,
+                                double* P, hipStream_t s);
+hipError_t occupancy_measures(const double* T, const double* P, const double* D0, int S, int A, int H, double* D,
+                              hipStream_t s);
+constexpr int kKdeMaxDim = 32;
+int kde_splits(int NQ, int N);
+// kind: 0 gaussian, 1 exponential, 2 tophat, 3 epanechnikov, 4 linear, 5 cosine;
+// pmax / psum: kde_splits(NQ, N) * NQ doubles of scratch; out[i] = logsumexp_j log k + offset
+hipError_t kde_score(const double* q, const double* x, int NQ, int N, int d, double inv_h, int kind, double offset,
+                     double* pmax, double* psum, double* out, hipStream_t s);
 
 // ---- pref.hip: Bradley-Terry preference loss over fragment pairs
 hipError_t pref_loss_fwd(const float* r1, const float* r2, const float* prefs, int P, int L, float discount,

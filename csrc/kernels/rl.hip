@@ -20,6 +20,7 @@
 // seed produce the same order.
 #include <hip/hip_runtime.h>
 
+#include "ia/wave.h"
 #include "launchers.h"
 
 namespace ia {
@@ -210,6 +211,139 @@ hipError_t cat_eval_bwd(const float* z, const int64_t* act, int B, int A, const 
                         hipStream_t s) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(cat_eval_bwd_kernel, dim3((B + 255) / 256), dim3(256), 0, s, z, act, B, A, g_lp, g_ent, dz);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- BC categorical loss
+// BehaviorCloningLossCalculator on a categorical head (reference algorithms/bc.py:100-130)
+// as 2 forward launches + 1 backward launch instead of ~25 elementwise / reduce kernels:
+//   sumsq_partials: fixed-order per-block partial sums of ||theta||^2 over the flat
+//                   parameter buffer (FusedAdam's bucket);
+//   bc_cat_loss_fwd: one block; per-row log pi(a), entropy, pi(a) reduced in a fixed
+//                   order, the partials summed, and the metric vector written:
+//                   [neglogp, entropy, ent_loss, prob_true_act, l2_norm, l2_loss, loss].
+//   bc_cat_loss_bwd: logit gradient for an upstream gradient g[7] of the metric vector:
+//                   per row g_lp = (-g0 - g6)/B + g3 pi(a)/B, g_ent = (g1 - w g2 - w g6)/B,
+//                   dz_k = g_lp (1[k == a] - p_k) - g_ent p_k (log p_k + H).
+namespace {
+constexpr int kLossThreads = 256;
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(kLossThreads) void sumsq_partials_kernel(const float* __restrict__ x, long n,
+                                                                      float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const long n4 = n >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (long i = (long)blockIdx.x * kLossThreads + threadIdx.x; i < n4; i += (long)gridDim.x * kLossThreads) {
+    const float4 v = x4[i];
+    s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+  }
+  if (blockIdx.x == 0)
+    for (long i = (n4 << 2) + threadIdx.x; i < n; i += kLossThreads) s += x[i] * x[i];
+  s = block_sum256(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__device__ __forceinline__ void cat_row(const float* zr, int A, float& lse, float& h) {
+  float mx = -INFINITY;
+  for (int k = 0; k < A; ++k) mx = fmaxf(mx, zr[k]);
+  float se = 0.f;
+  for (int k = 0; k < A; ++k) se += expf(zr[k] - mx);
+  lse = mx + logf(se);
+  h = 0.f;
+  for (int k = 0; k < A; ++k) {
+    const float lp = zr[k] - lse;
+    h -= expf(lp) * lp;
+  }
+}
+
+__global__ __launch_bounds__(kLossThreads) void bc_cat_loss_fwd_kernel(const float* __restrict__ z,
+                                                                       const int64_t* __restrict__ act, int B, int A,
+                                                                       const float* __restrict__ part, int nparts,
+                                                                       float ent_w, float l2_w, float* __restrict__ out) {
+  __shared__ float red[4];
+  float slp = 0.f, sent = 0.f, sp = 0.f;
+  for (int r = threadIdx.x; r < B; r += kLossThreads) {
+    const float* zr = z + (size_t)r * A;
+    float lse, h;
+    cat_row(zr, A, lse, h);
+    const int a = (int)act[r];
+    const float lp = (a >= 0 && a < A) ? zr[a] - lse : -INFINITY;
+    slp += lp;
+    sent += h;
+    sp += expf(lp);
+  }
+  float sq = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += kLossThreads) sq += part[i];
+  slp = block_sum256(slp, red);
+  sent = block_sum256(sent, red);
+  sp = block_sum256(sp, red);
+  sq = block_sum256(sq, red);
+  if (threadIdx.x == 0) {
+    const float inv = 1.f / (float)B;
+    const float neglogp = -slp * inv, ent = sent * inv, ent_loss = -ent_w * ent;
+    const float l2 = 0.5f * sq, l2_loss = l2_w * l2;
+    out[0] = neglogp;
+    out[1] = ent;
+    out[2] = ent_loss;
+    out[3] = sp * inv;
+    out[4] = l2;
+    out[5] = l2_loss;
+    out[6] = neglogp + ent_loss + l2_loss;
+  }
+}
+
+__global__ __launch_bounds__(kLossThreads) void bc_cat_loss_bwd_kernel(const float* __restrict__ z,
+                                                                       const int64_t* __restrict__ act, int B, int A,
+                                                                       const float* __restrict__ g, float ent_w,
+                                                                       float* __restrict__ dz) {
+  const int r = blockIdx.x * kLossThreads + threadIdx.x;
+  if (r >= B) return;
+  const float* zr = z + (size_t)r * A;
+  float lse, h;
+  cat_row(zr, A, lse, h);
+  const int a = (int)act[r];
+  const float inv = 1.f / (float)B;
+  const float pa = (a >= 0 && a < A) ? expf(zr[a] - lse) : 0.f;
+  const float gl = (-g[0] - g[6]) * inv + g[3] * pa * inv;
+  const float ge = (g[1] - ent_w * g[2] - ent_w * g[6]) * inv;
+  for (int k = 0; k < A; ++k) {
+    const float lp = zr[k] - lse, p = expf(lp);
+    dz[(size_t)r * A + k] = gl * ((k == a ? 1.f : 0.f) - p) - ge * p * (lp + h);
+  }
+}
+}  // namespace
+
+int sumsq_nparts(long n) {
+  const long blocks = (n / 4 + kLossThreads * 8 - 1) / (kLossThreads * 8);
+  return (int)(blocks < 1 ? 1 : (blocks > 256 ? 256 : blocks));
+}
+
+hipError_t bc_cat_loss_fwd(const float* z, const int64_t* act, int B, int A, const float* flat, long n, float* part,
+                           float ent_w, float l2_w, float* out, hipStream_t s) {
+  int np = 0;
+  if (flat && n > 0) {
+    np = sumsq_nparts(n);
+    hipLaunchKernelGGL(sumsq_partials_kernel, dim3(np), dim3(kLossThreads), 0, s, flat, n, part);
+  }
+  hipLaunchKernelGGL(bc_cat_loss_fwd_kernel, dim3(1), dim3(kLossThreads), 0, s, z, act, B, A, part, np, ent_w, l2_w, out);
+  return hipGetLastError();
+}
+
+hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, const float* g, float ent_w, float* dz,
+                           hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bc_cat_loss_bwd_kernel, dim3((B + kLossThreads - 1) / kLossThreads), dim3(kLossThreads), 0, s, z,
+                     act, B, A, g, ent_w, dz);
   return hipGetLastError();
 }
 

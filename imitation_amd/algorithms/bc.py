@@ -91,6 +91,9 @@ class BehaviorCloningLossCalculator:
     def __call__(self, policy: ActorCriticPolicy, obs, acts) -> BCTrainingMetrics:
         tensor_obs = types.map_maybe_dict(util.safe_to_tensor, types.maybe_unwrap_dictobs(obs))
         acts = util.safe_to_tensor(acts)
+        fused = self._fused_categorical(policy, tensor_obs, acts)
+        if fused is not None:
+            return fused
         _, log_prob, entropy = policy.evaluate_actions(tensor_obs, acts)
         prob_true_act = th.exp(log_prob).mean()
         log_prob = log_prob.mean()
@@ -110,6 +113,26 @@ class BehaviorCloningLossCalculator:
         loss = neglogp + ent_loss + l2_loss
         return BCTrainingMetrics(neglogp=neglogp, entropy=entropy, ent_loss=ent_loss, prob_true_act=prob_true_act,
                                  l2_norm=l2_norm, l2_loss=l2_loss, loss=loss)
+
+    def _fused_categorical(self, policy, obs, acts) -> Optional[BCTrainingMetrics]:
+        """Discrete-action policies on the GPU with their parameters in one flat bucket
+        (FusedAdam): the head's logits feed one fused loss op (``ops.rl.bc_categorical_loss``:
+        2 launches forward, 1 backward) and the value head is not evaluated (BC never uses
+        it). Same metrics and loss as the generic path."""
+        from imitation_amd.ops import rl as rl_ops
+        from imitation_amd.ops import use_kernel
+        from imitation_amd.rl.distributions import CategoricalDistribution
+
+        if (self.l2_weight != 0.0 or not isinstance(policy, ActorCriticPolicy) or not isinstance(obs, th.Tensor)
+                or not use_kernel(obs) or not isinstance(policy.action_dist, CategoricalDistribution)):
+            return None
+        params = list(policy.parameters())
+        flat = rl_ops.flat_param_view(params)
+        if flat is None:
+            return None
+        dist = policy.get_distribution(obs)
+        m = rl_ops.bc_categorical_loss(dist.raw_logits, acts, params, self.ent_weight, self.l2_weight, flat)
+        return BCTrainingMetrics(**{k: m[i] for i, k in enumerate(rl_ops.BC_METRICS)})
 
 
 def enumerate_batches(batch_it: Iterable[types.TransitionMapping]) -> Iterable[Tuple[Tuple[int, int, int], types.TransitionMapping]]:
@@ -233,9 +256,14 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
             return None
         g = getattr(self, "_graph_step", None)
         if g is None or g.optimizer is not self.optimizer:
+            fused_buckets = isinstance(self.optimizer, optim_ops.FusedAdam)
+
             def step(obs, acts):
                 metrics = self.loss_calculator(self.policy, obs, acts)
-                metrics.loss.backward()
+                if fused_buckets:  # buckets are zero here: the graph runs from zero_grad / a step
+                    self.optimizer.backward_into_buckets(metrics.loss)
+                else:
+                    metrics.loss.backward()
                 self.optimizer.step()
                 return metrics
 

@@ -72,6 +72,9 @@ def _log_kernel_norm(kernel: str, h: float, d: int) -> float:
     return -factor - d * math.log(h)
 
 
+_KDE_KINDS = {"gaussian": 0, "exponential": 1, "tophat": 2, "epanechnikov": 3, "linear": 4, "cosine": 5}
+
+
 class DeviceKDE:
     """Exact kernel density estimate held on the device; batched ``score_samples``."""
 
@@ -92,6 +95,14 @@ class DeviceKDE:
         q = th.as_tensor(np.asarray(X, dtype=np.float64), device=self.device)
         N, d = self.data.shape
         h = self.bandwidth
+        from imitation_amd import ops
+
+        if self.device.type == "cuda" and ops.fused_enabled() and 0 < d <= 32 and N > 0:
+            # one fused fp64 pass: exact distances + online logsumexp (csrc/kernels/tabular.hip)
+            offset = -math.log(N) + _log_kernel_norm(self.kernel, h, d)
+            out = ops.native().kde_score(q.reshape(-1, d).contiguous(), self.data.contiguous(), h,
+                                         _KDE_KINDS[self.kernel], offset)
+            return out.cpu().numpy()
         out = []
         for s in range(0, q.shape[0], self.chunk):
             qc = q[s : s + self.chunk]

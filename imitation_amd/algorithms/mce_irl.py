@@ -9,10 +9,11 @@
 * :class:`MCEIRL` -- gradient ``E_π[∇r] - E_D[∇r]`` through ``dot(D_π - D_demo, r)``
   (``:264-560``), stopping on L∞ occupancy error or gradient norm.
 
-MI355X: both recursions run as batched tensor ops on the
-training device (``T`` is ``[S, A, S']``: one batched mat-vec per step for the
-backup, one mat-mat per step for the occupancy propagation); ``device="cpu"``
-reproduces the numpy reference bit-for-bit in float64.
+MI355X: on the GPU each recursion is ONE fp64 HIP launch
+(``csrc/kernels/tabular.hip``: a single workgroup loops over the horizon with the running
+vector and the step's ``[S, A]`` table in LDS, ``T`` streamed from L2) instead of ~6
+launches per timestep; larger tables and the CPU run the same recursions as batched
+torch ops (``T`` is ``[S, A, S']``), which reproduce the numpy reference in float64.
 """
 
 from __future__ import annotations
@@ -39,6 +40,14 @@ def _dev(device):
     return th.device(device)
 
 
+def _use_tabular_kernel(dev: th.device, S: int, A: int) -> bool:
+    """The one-workgroup HIP recursions (csrc/kernels/tabular.hip) apply on the GPU when the
+    running vector and one step's [S, A] table fit LDS (S * (A + 1) doubles <= 150 KB)."""
+    from imitation_amd import ops
+
+    return dev.type == "cuda" and ops.fused_enabled() and S * (A + 1) * 8 <= 150 * 1024
+
+
 def mce_partition_fh(env, *, reward: Optional[np.ndarray] = None, discount: float = 1.0, device=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """Soft value iteration over a finite horizon; returns ``(V [H,S], Q [H,S,A], pi [H,S,A])``."""
     horizon = env.horizon
@@ -50,6 +59,11 @@ def mce_partition_fh(env, *, reward: Optional[np.ndarray] = None, discount: floa
         reward = env.reward_matrix
     R = th.as_tensor(np.asarray(reward), dtype=th.float64, device=dev)
     S, A = env.state_dim, env.action_dim
+    if _use_tabular_kernel(dev, S, A) and R.dim() == 1:
+        from imitation_amd.ops import native
+
+        V, Q, pi = native().soft_value_iteration(T.contiguous(), R.contiguous(), int(horizon), float(discount))
+        return V.cpu().numpy(), Q.cpu().numpy(), pi.cpu().numpy()
     Q = th.zeros((horizon, S, A), dtype=th.float64, device=dev)
     V = th.full((horizon, S), -np.inf, dtype=th.float64, device=dev)
     broad_R = R[:, None]
@@ -76,11 +90,17 @@ def mce_occupancy_measures(env, *, reward: Optional[np.ndarray] = None, pi: Opti
     T = th.as_tensor(env.transition_matrix, dtype=th.float64, device=dev)
     P = th.as_tensor(pi, dtype=th.float64, device=dev)
     S = env.state_dim
-    D = th.zeros((horizon + 1, S), dtype=th.float64, device=dev)
-    D[0] = th.as_tensor(env.initial_state_dist, dtype=th.float64, device=dev)
-    for t in range(horizon):
-        # sum_a (D_t * pi_t[:, a]) @ T[:, a, :]
-        D[t + 1] = th.einsum("s,sa,sap->p", D[t], P[t], T)
+    D0 = th.as_tensor(env.initial_state_dist, dtype=th.float64, device=dev)
+    if _use_tabular_kernel(dev, S, env.action_dim) and P.shape[0] >= horizon:
+        from imitation_amd.ops import native
+
+        D = native().occupancy_measures(T.contiguous(), P[:horizon].contiguous(), D0.contiguous())
+    else:
+        D = th.zeros((horizon + 1, S), dtype=th.float64, device=dev)
+        D[0] = D0
+        for t in range(horizon):
+            # sum_a (D_t * pi_t[:, a]) @ T[:, a, :]
+            D[t + 1] = th.einsum("s,sa,sap->p", D[t], P[t], T)
     Dn = D.cpu().numpy()
     Dcum = rollout.discounted_sum(Dn, discount)
     assert isinstance(Dcum, np.ndarray)

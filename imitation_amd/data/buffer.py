@@ -153,8 +153,36 @@ class ReplayBuffer:
         return self._buffer.size()
 
 
+def hbm_capacity(bytes_per_sample: int, *, fraction: float = 0.5, device=None, reserve_bytes: int = 4 << 30,
+                 free_bytes: Optional[int] = None) -> int:
+    """Rows a device-resident ring can hold in ``fraction`` of the device's currently free
+    memory (an MI355X has 288 GB of HBM3E: at the default half of it a Pong frame store
+    holds ~5M 84x84x4 transitions), keeping ``reserve_bytes`` back for activations and the
+    allocator. ``free_bytes`` overrides the query (tests, planning on the host)."""
+    if bytes_per_sample <= 0:
+        raise ValueError("bytes_per_sample must be positive")
+    if free_bytes is None:
+        dev = th.device(device if device is not None else "cuda")
+        if dev.type != "cuda":
+            raise ValueError("hbm_capacity sizes device buffers; pass free_bytes for a host plan")
+        free_bytes, _ = th.cuda.mem_get_info(dev)
+    usable = max(0, int(free_bytes * fraction) - reserve_bytes)
+    return max(1, usable // int(bytes_per_sample))
+
+
 class DeviceBuffer:
-    """Ring buffer of named device tensors with device-side uniform sampling."""
+    """Ring buffer of named device tensors with device-side uniform sampling (one
+    multi-field gather launch per draw, ``ops.rl.gather_rows``)."""
+
+    @classmethod
+    def sized_to_hbm(cls, sample_shapes: Mapping[str, Tuple[int, ...]], dtypes: Mapping[str, th.dtype], device, *,
+                     fraction: float = 0.5, max_capacity: Optional[int] = None) -> "DeviceBuffer":
+        """A ring whose capacity is :func:`hbm_capacity` of one sample's bytes."""
+        per = sum(int(np.prod(s)) * th.empty((), dtype=dtypes[k]).element_size() for k, s in sample_shapes.items())
+        cap = hbm_capacity(per, fraction=fraction, device=device)
+        if max_capacity is not None:
+            cap = min(cap, max_capacity)
+        return cls(cap, sample_shapes, dtypes, device)
 
     def __init__(self, capacity: int, sample_shapes: Mapping[str, Tuple[int, ...]], dtypes: Mapping[str, th.dtype], device):
         self.capacity = capacity
@@ -183,8 +211,15 @@ class DeviceBuffer:
     def sample(self, n_samples: int, generator: Optional[th.Generator] = None) -> Dict[str, th.Tensor]:
         if self._n_data == 0:
             raise ValueError("Buffer is empty")
+        from imitation_amd.ops.rl import gather_rows
+
         ind = th.randint(0, self._n_data, (n_samples,), device=self.device, generator=generator)
-        return {k: a.index_select(0, ind) for k, a in self._arrays.items()}
+        keys = list(self._arrays)
+        out: Dict[str, th.Tensor] = {}
+        for s in range(0, len(keys), 8):  # <= 8 fields per gather launch
+            ks = keys[s : s + 8]
+            out.update(zip(ks, gather_rows([self._arrays[k] for k in ks], ind)))
+        return out
 
     def size(self) -> int:
         return self._n_data

@@ -205,7 +205,7 @@ class DeviceDemoAggregate:
 
 class DeviceTransitionsLoader:
     """Shuffled, drop-last minibatches straight from a :class:`DeviceDemoAggregate`: one
-    ``perm_feistel`` launch per epoch and two ``index_select`` per batch; yields the batch
+    ``perm_feistel`` launch per epoch and one two-field ``gather_rows`` per batch; yields the batch
     dict BC consumes (``obs`` / ``acts`` device tensors)."""
 
     def __init__(self, agg: DeviceDemoAggregate, batch_size: int, seed: int):
@@ -225,8 +225,8 @@ class DeviceTransitionsLoader:
         perm = rl_ops.random_permutations(1, n, self._seed * 1000003 + self._epoch, self.agg.device)[0].long()
         obs, acts = self.agg.obs, self.agg.acts
         for s in range(0, n - n % self.batch_size, self.batch_size):
-            idx = perm[s : s + self.batch_size]
-            yield {"obs": obs.index_select(0, idx), "acts": acts.index_select(0, idx)}
+            o, a = rl_ops.gather_rows([obs, acts], perm[s : s + self.batch_size])
+            yield {"obs": o, "acts": a}
 
 
 class AsyncDemoWriter:

@@ -95,6 +95,42 @@ class FusedAdam(th.optim.Optimizer):
                 f["grad"].zero_()
                 self._bind_grads(f)
 
+    def backward_into_buckets(self, loss: th.Tensor) -> None:
+        """``loss.backward()`` for buckets that are zero on entry (after ``zero_grad()`` or a
+        ``step()``, which clears what it consumed): the gradients are taken with
+        ``autograd.grad`` and written into the bucket with one copy launch per run of
+        adjacent parameters that received one, instead of one accumulate-add launch per
+        parameter. Parameters without a gradient keep their zero slice."""
+        live = [(f, i) for f in self._flat if f["n"] for i in range(len(f["params"]))]
+        params = [f["params"][i] for f, i in live]
+        grads = th.autograd.grad(loss, params, allow_unused=True)
+        run: List[th.Tensor] = []
+        start = end = 0
+        cur = None
+
+        def flush():
+            if run:
+                dst = cur["grad"][start:end]
+                if len(run) == 1:
+                    dst.copy_(run[0].reshape(-1))
+                else:
+                    th.cat([g.reshape(-1) for g in run], out=dst)
+
+        for (f, i), g in zip(live, grads):
+            off, k, _ = f["views"][i]
+            if g is None or f is not cur or off != end:
+                flush()
+                run, cur, start, end = [], f, off, off
+            if g is not None:
+                run.append(g)
+                end = off + k
+            else:
+                start = end = off + k
+        flush()
+        for f in self._flat:
+            if f["n"]:
+                self._bind_grads(f)
+
     # ------------------------------------------------------------------ step
     @th.no_grad()
     def step(self, closure=None):

@@ -153,3 +153,83 @@ def categorical_eval(logits: torch.Tensor, actions: torch.Tensor) -> Tuple[torch
             and actions.numel() == logits.shape[0]):
         return _CategoricalEval.apply(logits, actions)
     return categorical_eval_reference(logits, actions)
+
+
+BC_METRICS = ("neglogp", "entropy", "ent_loss", "prob_true_act", "l2_norm", "l2_loss", "loss")
+
+
+def bc_categorical_loss_reference(logits, actions, params, ent_weight: float, l2_weight: float) -> torch.Tensor:
+    """The BC loss metrics of a categorical head as one ``[7]`` vector (order ``BC_METRICS``)."""
+    lp, ent = categorical_eval_reference(logits, actions)
+    l2 = torch.stack([p.square().sum() for p in params]).sum() / 2 if params else logits.new_zeros(())
+    neglogp, entropy = -lp.mean(), ent.mean()
+    ent_loss, l2_loss = -ent_weight * entropy, l2_weight * l2
+    return torch.stack([neglogp, entropy, ent_loss, lp.exp().mean(), l2, l2_loss, neglogp + ent_loss + l2_loss])
+
+
+class _BCCategoricalLoss(torch.autograd.Function):
+    """rl.hip ``bc_cat_loss_*``: the whole BC loss of a categorical head (log-prob, entropy,
+    means, prob_true_act, ||θ||²/2 over the flat parameter bucket, totals) as 2 forward
+    launches and a 1-launch logit gradient. ``||θ||²`` is a logged metric only (the fused
+    path is taken for ``l2_weight == 0``), so no parameter gradient flows from it."""
+
+    @staticmethod
+    def forward(ctx, logits, actions, flat, ent_weight, l2_weight):
+        from imitation_amd.ops import native
+
+        z = logits.contiguous()
+        a = actions.reshape(-1).long().contiguous()
+        out = native().bc_cat_loss_fwd(z, a, flat, float(ent_weight), float(l2_weight))
+        ctx.save_for_backward(z, a)
+        ctx.ent_weight = float(ent_weight)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from imitation_amd.ops import native
+
+        z, a = ctx.saved_tensors
+        return native().bc_cat_loss_bwd(z, a, g, ctx.ent_weight), None, None, None, None
+
+
+def flat_param_view(params) -> "torch.Tensor | None":
+    """A 1-D view over ``params`` when they are adjacent contiguous slices of one buffer in
+    this order (FusedAdam's bucket layout), 16-B aligned; else None."""
+    if not params:
+        return None
+    p0 = params[0]
+    st = p0.untyped_storage()
+    off = base = p0.storage_offset()
+    for p in params:
+        if (p.dtype != torch.float32 or not p.is_contiguous() or p.device != p0.device
+                or p.untyped_storage().data_ptr() != st.data_ptr() or p.storage_offset() != off):
+            return None
+        off += p.numel()
+    view = p0.new_empty(0).set_(st, base, (off - base,), (1,))
+    return view if view.data_ptr() % 16 == 0 else None
+
+
+def bc_categorical_loss(logits, actions, params, ent_weight: float, l2_weight: float,
+                        flat: "torch.Tensor | None" = None) -> torch.Tensor:
+    """BC loss metric vector ``[7]`` (``BC_METRICS`` order); ``loss`` is differentiable
+    w.r.t. the logits. HIP kernels on the GPU when ``l2_weight == 0`` and the parameters
+    form one flat buffer (``flat``), else the reference."""
+    from imitation_amd.ops import use_kernel
+
+    if (use_kernel(logits) and logits.dtype == torch.float32 and logits.dim() == 2 and 0 < logits.shape[1] <= 64
+            and logits.shape[0] > 0 and actions.numel() == logits.shape[0] and l2_weight == 0.0 and flat is not None):
+        return _BCCategoricalLoss.apply(logits, actions, flat.detach(), ent_weight, l2_weight)
+    return bc_categorical_loss_reference(logits, actions, params, ent_weight, l2_weight)
+
+
+def gather_rows(srcs, b: torch.Tensor, e: "torch.Tensor | None" = None, n_envs: int = 1):
+    """``[s[b * n_envs + e] for s in srcs]`` (or ``s[b]``) for row-major sources ``[R, ...]``:
+    one HIP launch for every field on the GPU (csrc/kernels/gather.hip), torch indexing on
+    the CPU. Out-of-range rows come back as zeros on the GPU."""
+    from imitation_amd.ops import native, use_kernel
+
+    srcs = list(srcs)
+    if use_kernel(b) and 0 < len(srcs) <= 8 and all(s.is_cuda and s.is_contiguous() for s in srcs):
+        return native().gather_rows(srcs, b.long().contiguous(), None if e is None else e.long().contiguous(), int(n_envs))
+    flat = b.long() if e is None else b.long() * n_envs + e.long()
+    return [s.index_select(0, flat) for s in srcs]

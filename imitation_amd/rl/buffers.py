@@ -215,15 +215,20 @@ class ReplayBuffer(BaseBuffer):
         return self._get_samples(batch_inds, env=env)
 
     def _get_samples(self, batch_inds: th.Tensor, env=None) -> ReplayBufferSamples:
+        from imitation_amd.ops.rl import gather_rows
+
         env_inds = th.randint(0, self.n_envs, (len(batch_inds),), device=self.device)
-        obs = self.observations[batch_inds, env_inds]
-        next_obs = self.next_observations[batch_inds, env_inds]
+        # every field of the (step, env) rows in one gather launch (csrc/kernels/gather.hip)
+        SN = self.buffer_size * self.n_envs
+        obs, next_obs, acts, d, tmo, rews = gather_rows(
+            [self.observations.view(SN, *self.obs_shape), self.next_observations.view(SN, *self.obs_shape),
+             self.actions.view(SN, self.action_dim), self.dones.view(SN), self.timeouts.view(SN), self.rewards.view(SN)],
+            batch_inds, env_inds, self.n_envs)
         if env is not None and hasattr(env, "normalize_obs"):
             obs = self.to_torch(env.normalize_obs(obs.cpu().numpy()))
             next_obs = self.to_torch(env.normalize_obs(next_obs.cpu().numpy()))
-        acts = self.actions[batch_inds, env_inds]
-        dones = (self.dones[batch_inds, env_inds] * (1 - self.timeouts[batch_inds, env_inds])).reshape(-1, 1)
-        rews = self.rewards[batch_inds, env_inds].reshape(-1, 1)
+        dones = (d * (1 - tmo)).reshape(-1, 1)
+        rews = rews.reshape(-1, 1)
         if env is not None and hasattr(env, "normalize_reward"):
             rews = self.to_torch(env.normalize_reward(rews.cpu().numpy())).float()
         return ReplayBufferSamples(

@@ -195,3 +195,21 @@ def test_mce_irl_reasonable_mdp(hid, discount, rng):
         stats = rollout.rollout_stats(trajs)
         if discount > 0.0:
             assert stats["return_mean"] >= 15
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,A,H,discount", [(5, 3, 10, 1.0), (64, 4, 40, 0.99), (400, 4, 100, 0.9), (1500, 5, 7, 1.0)])
+def test_tabular_kernels_match_cpu(S, A, H, discount):
+    """One-launch soft value iteration / occupancy (csrc/kernels/tabular.hip) == the fp64
+    torch recursions on the CPU."""
+    mdp = tabular.RandomTransitionEnv(n_states=S, n_actions=A, branch_factor=min(S, 3), horizon=H, random_obs=False,
+                                      obs_dim=None, generator_seed=S)
+    V, Q, pi = mce_partition_fh(mdp, discount=discount, device="cuda")
+    Vc, Qc, pic = mce_partition_fh(mdp, discount=discount, device="cpu")
+    np.testing.assert_allclose(V, Vc, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(Q, Qc, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(pi, pic, rtol=1e-11, atol=1e-13)
+    D, Dcum = mce_occupancy_measures(mdp, pi=pic, discount=discount, device="cuda")
+    Dc, Dcumc = mce_occupancy_measures(mdp, pi=pic, discount=discount, device="cpu")
+    np.testing.assert_allclose(D, Dc, rtol=1e-11, atol=1e-14)
+    np.testing.assert_allclose(Dcum, Dcumc, rtol=1e-11, atol=1e-13)

@@ -260,3 +260,45 @@ def test_categorical_eval_kernel_matches_autograd(B, A):
     th.testing.assert_close(lp.double().cpu(), lp_r.detach(), rtol=1e-5, atol=1e-5)
     th.testing.assert_close(ent.double().cpu(), ent_r.detach(), rtol=1e-5, atol=1e-5)
     th.testing.assert_close(zg.grad.double().cpu(), zr.grad, rtol=1e-4, atol=1e-5)
+
+
+@gpu
+@pytest.mark.parametrize("B,A,n", [(32, 6, 1_700_001), (1, 3, 5), (600, 18, 4096)])
+def test_bc_categorical_loss_kernel_matches_reference(B, A, n):
+    g = th.Generator().manual_seed(B + A)
+    z = 2 * th.randn(B, A, generator=g)
+    a = th.randint(0, A, (B,), generator=g)
+    flat = th.randn(n, generator=g) * 0.01
+    params = [flat[: n // 3], flat[n // 3:]]
+    zr = z.double().requires_grad_(True)
+    ref = rl_ops.bc_categorical_loss_reference(zr, a, [p.double() for p in params], 1e-3, 0.0)
+    wg = th.randn(7, generator=g).double()
+    (ref * wg).sum().backward()
+    zg = z.cuda().requires_grad_(True)
+    fc = flat.cuda()
+    got = rl_ops.bc_categorical_loss(zg, a.cuda(), [fc[: n // 3], fc[n // 3:]], 1e-3, 0.0, flat=fc)
+    assert got.grad_fn is not None and "BCCategorical" in type(got.grad_fn).__name__
+    (got * wg.float().cuda()).sum().backward()
+    th.testing.assert_close(got.double().cpu(), ref.detach(), rtol=2e-5, atol=1e-5)
+    th.testing.assert_close(zg.grad.double().cpu(), zr.grad, rtol=1e-4, atol=1e-6)
+
+
+@gpu
+@pytest.mark.parametrize("n_envs", [1, 3])
+def test_gather_rows_kernel_matches_indexing(n_envs):
+    """One-launch multi-field gather (csrc/kernels/gather.hip): 16-B, 4-B and byte rows,
+    (step, env) addressing, out-of-range rows as zeros."""
+    g = th.Generator().manual_seed(n_envs)
+    R = 50 * n_envs
+    srcs = [th.randint(0, 255, (R, 84, 84, 4), generator=g, dtype=th.uint8), th.randn(R, 17, generator=g),
+            th.randint(0, 6, (R,), generator=g), th.randint(0, 255, (R, 3), generator=g, dtype=th.uint8), th.randn(R)]
+    b = th.randint(0, R // n_envs, (77,), generator=g)
+    e = th.randint(0, n_envs, (77,), generator=g) if n_envs > 1 else None
+    got = rl_ops.gather_rows([s.cuda() for s in srcs], b.cuda(), None if e is None else e.cuda(), n_envs)
+    flat = b if e is None else b * n_envs + e
+    for s, o in zip(srcs, got):
+        assert th.equal(o.cpu(), s[flat])
+    bad = th.tensor([0, R // n_envs + 5, -1], device="cuda")
+    o = rl_ops.gather_rows([srcs[1].cuda()], bad, None, 1)[0].cpu() if n_envs == 1 else None
+    if o is not None:
+        assert th.equal(o[0], srcs[1][0]) and float(o[1:].abs().sum()) == 0.0

@@ -40,3 +40,18 @@ def test_categorical_eval_reference_matches_distribution():
     lp, ent = d.log_prob_entropy(a)
     th.testing.assert_close(lp, d.log_prob(a))
     th.testing.assert_close(ent, d.entropy())
+
+
+def test_gather_rows_cpu_and_hbm_capacity():
+    import torch as th
+
+    from imitation_amd.data.buffer import hbm_capacity
+
+    a, b = th.arange(12).reshape(6, 2), th.arange(6.0)
+    got = rl_ops.gather_rows([a, b], th.tensor([1, 0]), th.tensor([1, 2]), 3)
+    assert th.equal(got[0], a[[4, 2]]) and th.equal(got[1], b[[4, 2]])
+    # 288 GB free, half of it minus the 4 GiB reserve, Pong transitions (84*84*4 + 8 bytes)
+    cap = hbm_capacity(84 * 84 * 4 + 8, free_bytes=288 * 10**9)
+    assert cap == (144 * 10**9 - (4 << 30)) // (84 * 84 * 4 + 8) and cap > 4_900_000
+    with pytest.raises(ValueError):
+        hbm_capacity(0, free_bytes=10)
