@@ -1255,6 +1255,8 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
     IA_RC(2, 4, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
   else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)
     IA_RC(4, 8, 3, 3, 1, 64, 32, 0);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
+  else if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)
+    IA_RC(4, 8, 5, 3, 1, 64, 32, 0);  // Walker2d MlpPolicy [64, 64] ReLU (DRLHP seals_walker config)
   else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && a.discrete)
     IA_RC(2, 4, 1, 3, 2, 32, 64, 1);  // CartPole FeedForward32Policy
   else if (g.kt == 2)
