@@ -171,6 +171,55 @@ torch::Tensor cnn_fc(torch::Tensor x, torch::Tensor w, torch::Tensor b) {
   return h;
 }
 
+// Two same-shape unpadded convs (+ bias + ReLU) in one launch: the collector's expert and
+// learner layers. Returns (y1, y2).
+py::tuple conv_fwd_pair(torch::Tensor x1, torch::Tensor x2, torch::Tensor w1, torch::Tensor w2, torch::Tensor b1,
+                        torch::Tensor b2, int64_t stride, double in_scale, bool relu) {
+  for (auto* t : {&x1, &x2, &w1, &w2}) {
+    IA_CHECK_CUDA((*t));
+    IA_CHECK_CONTIG((*t));
+  }
+  IA_CHECK_GPU_F32(b1);
+  IA_CHECK_GPU_F32(b2);
+  TORCH_CHECK(x1.sizes() == x2.sizes() && x1.scalar_type() == x2.scalar_type(), "conv_fwd_pair: inputs differ");
+  TORCH_CHECK(w1.sizes() == w2.sizes() && w1.scalar_type() == torch::kBFloat16 && w2.scalar_type() == torch::kBFloat16 &&
+                  w1.dim() == 4,
+              "conv_fwd_pair: weights must be same-shape bf16 [N, KH, KW, C]");
+  auto g = geo(x1, w1.size(0), w1.size(1), w1.size(2), stride, 0);
+  TORCH_CHECK(w1.size(3) == g.C && g.Kp == g.KH * g.KW * g.C && g.N % 16 == 0 && b1.numel() == g.N && b2.numel() == g.N,
+              "conv_fwd_pair: K = KH*KW*C must be a multiple of 32, N of 16, bias [N]");
+  auto y1 = torch::empty({g.B, g.OH, g.OW, g.N}, x1.options().dtype(torch::kBFloat16));
+  auto y2 = torch::empty_like(y1);
+  ia::ConvPair p{{x1.data_ptr(), x2.data_ptr()}, {w1.data_ptr(), w2.data_ptr()}, {b1.data_ptr<float>(), b2.data_ptr<float>()},
+                 {y1.data_ptr(), y2.data_ptr()}};
+  IA_HIP_CHECK3(ia::conv_fwd_pair(in_kind(x1), p, g, (float)in_scale, relu ? 1 : 0, ia_stream()));
+  return py::make_tuple(y1, y2);
+}
+
+// cnn_fc of two same-shape networks in one launch; returns (h1, h2)
+py::tuple cnn_fc_pair(torch::Tensor x1, torch::Tensor x2, torch::Tensor w1, torch::Tensor w2, torch::Tensor b1,
+                      torch::Tensor b2) {
+  for (auto* t : {&x1, &x2, &w1, &w2}) {
+    IA_CHECK_CUDA((*t));
+    IA_CHECK_CONTIG((*t));
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16, "cnn_fc_pair: x, w must be bf16");
+  }
+  IA_CHECK_GPU_F32(b1);
+  IA_CHECK_GPU_F32(b2);
+  TORCH_CHECK(x1.sizes() == x2.sizes() && w1.sizes() == w2.sizes(), "cnn_fc_pair: shapes differ");
+  const int B = (int)x1.size(0);
+  const int64_t K = x1.numel() / std::max<int64_t>(1, B);
+  TORCH_CHECK(w1.dim() == 2 && w1.size(1) == K, "w must be [NH, K] with K = x.numel() / B");
+  const int NH = (int)w1.size(0);
+  TORCH_CHECK(b1.numel() == NH && b2.numel() == NH && K % 32 == 0 && NH % 16 == 0, "cnn_fc_pair: K % 32, NH % 16");
+  auto h1 = torch::empty({B, NH}, x1.options().dtype(torch::kFloat32));
+  auto h2 = torch::empty_like(h1);
+  ia::CnnFcPair p{{x1.data_ptr(), x2.data_ptr()}, {w1.data_ptr(), w2.data_ptr()}, {b1.data_ptr<float>(), b2.data_ptr<float>()},
+                  {h1.data_ptr<float>(), h2.data_ptr<float>()}};
+  IA_HIP_CHECK3(ia::cnn_fc_pair(p, B, (int)K, NH, ia_stream()));
+  return py::make_tuple(h1, h2);
+}
+
 // Action head + choice (+ beta-mix); see cnn_infer.hip. All outputs are preallocated int64 [B].
 void cnn_head(torch::Tensor h, torch::Tensor w2, torch::Tensor b2, int64_t mode, int64_t seed,
               c10::optional<torch::Tensor> counter, torch::Tensor out, c10::optional<torch::Tensor> rec_out,
@@ -219,6 +268,8 @@ void register_conv(py::module& m) {
         py::arg("mix_expert") = py::none(), py::arg("beta") = py::none(), py::arg("exec_out") = py::none());
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv + bias + ReLU (bf16 MFMA)", py::arg("x"), py::arg("wb"),
         py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0);
+  m.def("conv_fwd_pair", &conv_fwd_pair, "two same-shape convs (expert + learner) in one launch");
+  m.def("cnn_fc_pair", &cnn_fc_pair, "two same-shape cnn_fc layers in one launch");
   m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts, one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),

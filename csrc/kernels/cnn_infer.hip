@@ -4,7 +4,8 @@
 // Linear(3136 -> 512) + ReLU, the action head Linear(512 -> A) and the action choice.
 // Through torch that is ~25 launches per forward (flatten permute, hipBLASLt GEMM,
 // bias/ReLU, logsumexp, argmax / Gumbel sampling, the β-mix), ~250 us for two policies at
-// batch 8 -- more than the three convolutions. Here it is two launches:
+// batch 8 -- more than the three convolutions. Here it is two launches (the FC of the
+// expert and the learner share one, cnn_fc_pair, like their convs share conv_fwd_pair):
 //
 //   cnn_fc    h[B][H] = relu(X[B][K] . W1[H][K]^T + b1): v_mfma_f32_16x16x32_bf16 tiles of
 //             16 rows x 16 hidden units, K split over the 4 waves of a block and summed in
@@ -24,12 +25,12 @@ namespace {
 
 constexpr int kFcWaves = 8;
 
-__global__ __launch_bounds__(64 * kFcWaves) void cnn_fc_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
-                                                              const float* __restrict__ bias, float* __restrict__ H, int B,
-                                                              int K, int NH) {
+__device__ __forceinline__ void cnn_fc_tile(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                            const float* __restrict__ bias, float* __restrict__ H, int B, int K, int NH,
+                                            int bx, int by) {
   __shared__ f32x4 red[kFcWaves][64];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int n0 = bx * 16, m0 = by * 16;
   const int r = l & 15, kq = (l >> 4) * 8;
   const int ksteps = K / 32;
   const int per = (ksteps + kFcWaves - 1) / kFcWaves;
@@ -64,6 +65,19 @@ __global__ __launch_bounds__(64 * kFcWaves) void cnn_fc_kernel(const bf16* __res
     const int row = m0 + 4 * (l >> 4) + i;
     if (row < B) H[(size_t)row * NH + n] = fmaxf(t[i] + bb, 0.f);
   }
+}
+
+__global__ __launch_bounds__(64 * kFcWaves) void cnn_fc_kernel(const bf16* __restrict__ X, const bf16* __restrict__ W,
+                                                              const float* __restrict__ bias, float* __restrict__ H, int B,
+                                                              int K, int NH) {
+  cnn_fc_tile(X, W, bias, H, B, K, NH, blockIdx.x, blockIdx.y);
+}
+
+// expert + learner FC layers in one launch (blockIdx.z = which), as conv_fwd_pair
+__global__ __launch_bounds__(64 * kFcWaves) void cnn_fc_pair_kernel(CnnFcPair p, int B, int K, int NH) {
+  const int z = blockIdx.z;
+  cnn_fc_tile(static_cast<const bf16*>(p.X[z]), static_cast<const bf16*>(p.W[z]), p.bias[z], p.H[z], B, K, NH,
+              blockIdx.x, blockIdx.y);
 }
 
 __device__ __forceinline__ uint64_t hmix(uint64_t x) {
@@ -135,6 +149,13 @@ hipError_t cnn_fc(const void* X, const void* W, const float* bias, float* H, int
   if (K % 32 != 0 || NH % 16 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(cnn_fc_kernel, dim3(NH / 16, (B + 15) / 16), dim3(64 * kFcWaves), 0, s, static_cast<const bf16*>(X),
                      static_cast<const bf16*>(W), bias, H, B, K, NH);
+  return hipGetLastError();
+}
+
+hipError_t cnn_fc_pair(const CnnFcPair& p, int B, int K, int NH, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (K % 32 != 0 || NH % 16 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cnn_fc_pair_kernel, dim3(NH / 16, (B + 15) / 16, 2), dim3(64 * kFcWaves), 0, s, p, B, K, NH);
   return hipGetLastError();
 }
 

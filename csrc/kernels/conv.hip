@@ -103,16 +103,16 @@ __device__ __forceinline__ bf16x8 load8_pad(const TIn* X, const ConvGeo& g, int 
 // RT row tiles (16 output pixels each) per wave share every weight fragment: at large M the
 // per-wave weight re-reads from L2, not the MFMAs, set the forward's time.
 template <typename TIn, int NT, bool PADDED = false, int RT = 1>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X, const bf16* __restrict__ Wb,
-                                                       const float* __restrict__ bias, bf16* __restrict__ Y, ConvGeo g,
-                                                       float in_scale, int relu) {
+__device__ __forceinline__ void conv_fwd_tile(const TIn* __restrict__ X, const bf16* __restrict__ Wb,
+                                              const float* __restrict__ bias, bf16* __restrict__ Y, const ConvGeo& g,
+                                              float in_scale, int relu, int bx, int by) {
   const int l = threadIdx.x & 63;
-  const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * RT;
+  const int m0 = (bx * 4 + (threadIdx.x >> 6)) * 16 * RT;
   const int OHW = g.OH * g.OW;
   const int M = g.B * OHW;
   if (m0 >= M) return;
   const int K = g.Kp;
-  const int n_base = blockIdx.y * 16 * NT;  // split-N grids (small batches): this block's channels
+  const int n_base = by * 16 * NT;  // split-N grids (small batches): this block's channels
   const int rowlen = g.KW * g.C;
   const int r = l & 15, kq = (l >> 4) * 8;
   const size_t xrow = (size_t)g.W * g.C;
@@ -183,6 +183,23 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
       }
     }
   }
+}
+
+template <typename TIn, int NT, bool PADDED = false, int RT = 1>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X, const bf16* __restrict__ Wb,
+                                                       const float* __restrict__ bias, bf16* __restrict__ Y, ConvGeo g,
+                                                       float in_scale, int relu) {
+  conv_fwd_tile<TIn, NT, PADDED, RT>(X, Wb, bias, Y, g, in_scale, relu, blockIdx.x, blockIdx.y);
+}
+
+// Two same-shape convolutions in one launch (blockIdx.z = which): the DAgger collector's
+// expert and learner CNNs step the same frames, so each layer of both is one small-batch
+// split-N grid of twice the blocks instead of two latency-bound launches.
+template <typename TIn>
+__global__ __launch_bounds__(256) void conv_fwd_pair_kernel(ConvPair p, ConvGeo g, float in_scale, int relu) {
+  const int z = blockIdx.z;
+  conv_fwd_tile<TIn, 1>(static_cast<const TIn*>(p.X[z]), static_cast<const bf16*>(p.W[z]), p.bias[z],
+                        static_cast<bf16*>(p.Y[z]), g, in_scale, relu, blockIdx.x, blockIdx.y);
 }
 
 // ------------------------------------------------------------------ data gradient
@@ -532,6 +549,19 @@ hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s) {
   }
   const int bx = (most + 255) / 256 < 64 ? (most + 255) / 256 : 64;
   hipLaunchKernelGGL(conv_pack_kernel, dim3(bx, a.n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t conv_fwd_pair(int in_kind, const ConvPair& p, const ConvGeo& g, float in_scale, int relu, hipStream_t s) {
+  if (!conv_geo_ok(g) || g.P != 0 || g.Kp != g.KH * g.KW * g.C || g.N % 16 != 0) return hipErrorInvalidValue;
+  const int M = g.B * g.OH * g.OW;
+  const dim3 grid((M + 63) / 64, g.N / 16, 2), block(256);
+  if (in_kind == 1)
+    hipLaunchKernelGGL(conv_fwd_pair_kernel<bf16>, grid, block, 0, s, p, g, in_scale, relu);
+  else if (in_kind == 2)
+    hipLaunchKernelGGL(conv_fwd_pair_kernel<uint8_t>, grid, block, 0, s, p, g, in_scale, relu);
+  else
+    hipLaunchKernelGGL(conv_fwd_pair_kernel<float>, grid, block, 0, s, p, g, in_scale, relu);
   return hipGetLastError();
 }
 

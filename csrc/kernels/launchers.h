@@ -103,6 +103,13 @@ hipError_t dagger_env_step(const DaggerEnvArgs& a, hipStream_t s);
 // ---- cnn_infer.hip: NatureCNN actor tail for the DAgger collector
 // h[B][NH] = relu(X[B][K] . W[NH][K]^T + bias), X / W bf16 (K % 32 == 0, NH % 16 == 0)
 hipError_t cnn_fc(const void* X, const void* W, const float* bias, float* H, int B, int K, int NH, hipStream_t s);
+struct CnnFcPair {
+  const void* X[2];
+  const void* W[2];
+  const float* bias[2];
+  float* H[2];
+};
+hipError_t cnn_fc_pair(const CnnFcPair& p, int B, int K, int NH, hipStream_t s);
 struct CnnHeadArgs {
   const float *h, *W2, *b2;  // h [B, NH], W2 [A, NH], b2 [A]
   int B, NH, A;
@@ -224,6 +231,14 @@ struct ConvPackArgs {
   int n;
 };
 hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s);
+// two same-geometry unpadded convs (+ bias + ReLU) in one launch: X/W/bias/Y of set z
+struct ConvPair {
+  const void* X[2];
+  const void* W[2];
+  const float* bias[2];
+  void* Y[2];
+};
+hipError_t conv_fwd_pair(int in_kind, const ConvPair& p, const ConvGeo& g, float in_scale, int relu, hipStream_t s);
 void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* m_per_block);
 size_t conv_wgrad_slab_floats(const ConvGeo& g);
 // in_kind: 0 fp32, 1 bf16, 2 uint8 input; weights bf16 [N][KH][KW][C]; Y bf16 [B*OH*OW][N]

@@ -148,6 +148,16 @@ def test_cnn_actor_matches_policy():
     p = th.softmax(hrow[0] @ pol.action_net.weight.T + pol.action_net.bias, -1)
     freq = counts / counts.sum()
     assert float((freq - p).abs().max()) < 0.02
+    # expert + learner layers sharing one launch each == two separate forwards, bit for bit
+    th.manual_seed(1)
+    pol2 = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
+    actor2 = CnnActor(pol2, obs_space.shape)
+    assert CnnActor.paired(actor, actor2)
+    for Bp in (8, 1, 64):
+        xp = x[:Bp].contiguous()
+        with th.no_grad():
+            h1, h2 = CnnActor.hidden_pair(actor, actor2, xp)
+            assert th.equal(h1, actor.hidden(xp)) and th.equal(h2, actor2.hidden(xp))
 
 
 @gpu
