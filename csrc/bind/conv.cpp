@@ -124,7 +124,7 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, to
 }
 
 // fp32 conv weights [N, C, KH, KW] -> (bf16 [N, KH, KW, C] each, bf16 [C, KH, KW, N] where want_t)
-py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> want_t) {
+py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> want_t, std::vector<bool> t_hwc) {
   TORCH_CHECK(ws.size() == want_t.size() && (int)ws.size() <= ia::kMaxPack, "conv_pack_weights: layer count");
   ia::ConvPackArgs a{};
   a.n = (int)ws.size();
@@ -137,9 +137,12 @@ py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> wan
     const int64_t N = w.size(0), C = w.size(1), KH = w.size(2), KW = w.size(3);
     auto wb = torch::empty({N, KH, KW, C}, w.options().dtype(torch::kBFloat16));
     torch::Tensor wt;
-    if (want_t[i]) wt = torch::empty({C, KH, KW, N}, w.options().dtype(torch::kBFloat16));
+    const bool hwc = i < t_hwc.size() && t_hwc[i];
+    if (want_t[i])
+      wt = hwc ? torch::empty({KH, KW, C, N}, w.options().dtype(torch::kBFloat16))
+               : torch::empty({C, KH, KW, N}, w.options().dtype(torch::kBFloat16));
     a.layer[i] = ia::ConvPackLayer{w.data_ptr<float>(), wb.data_ptr(), want_t[i] ? wt.data_ptr() : nullptr, (int)N,
-                                   (int)C, (int)KH, (int)KW};
+                                   (int)C, (int)KH, (int)KW, hwc ? 1 : 0};
     wbs.push_back(wb);
     wts.push_back(wt);
   }
@@ -169,6 +172,34 @@ torch::Tensor cnn_fc(torch::Tensor x, torch::Tensor w, torch::Tensor b) {
   auto h = torch::empty({B, NH}, x.options().dtype(torch::kFloat32));
   IA_HIP_CHECK3(ia::cnn_fc(x.data_ptr(), w.data_ptr(), b.data_ptr<float>(), h.data_ptr<float>(), B, (int)K, NH, ia_stream()));
   return h;
+}
+
+// Linear + ReLU backward over the NHWC-flattened conv output: (dW fp32 [NH, C*HW] torch (c, h, w)
+// columns, db fp32 [NH], dX bf16 [M, K] or None)
+py::tuple fc_backward(torch::Tensor x, torch::Tensor dh, torch::Tensor h, torch::Tensor wt, int64_t C, bool need_dx) {
+  IA_CHECK_CUDA(x);
+  IA_CHECK_CONTIG(x);
+  IA_CHECK_CUDA(wt);
+  IA_CHECK_CONTIG(wt);
+  IA_CHECK_GPU_F32(h);
+  IA_CHECK_CONTIG(h);
+  auto dhc = dh.contiguous().to(torch::kFloat32);
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && wt.scalar_type() == torch::kBFloat16, "fc_backward: bf16 x / wt");
+  const int M = (int)x.size(0);
+  const int64_t K = x.numel() / std::max<int64_t>(1, M);
+  const int NH = (int)h.size(1);
+  TORCH_CHECK(h.dim() == 2 && h.size(0) == M && dhc.sizes() == h.sizes() && wt.numel() == K * NH && C > 0 && K % C == 0,
+              "fc_backward: shapes");
+  TORCH_CHECK(ia::fc_train_ok(M, (int)K, NH, (int)C, (int)(K / C)), "fc_backward: K % 64, NH % 64");
+  auto dW = torch::empty({NH, K}, h.options());
+  auto db = torch::empty({NH}, h.options());
+  torch::Tensor dx;
+  if (need_dx) dx = torch::empty({M, K}, x.options());
+  auto dzb = torch::empty({M, NH}, x.options());  // bf16 dZ, fc_wgrad -> fc_dgrad
+  IA_HIP_CHECK3(ia::fc_backward(x.data_ptr(), dhc.data_ptr<float>(), h.data_ptr<float>(), wt.data_ptr(),
+                                dW.data_ptr<float>(), db.data_ptr<float>(), need_dx ? dx.data_ptr() : nullptr, dzb.data_ptr(), M,
+                                (int)K, NH, (int)C, (int)(K / C), ia_stream()));
+  return py::make_tuple(dW, db, need_dx ? py::cast(dx) : py::none());
 }
 
 // Two same-shape unpadded convs (+ bias + ReLU) in one launch: the collector's expert and
@@ -270,7 +301,9 @@ void register_conv(py::module& m) {
         py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0);
   m.def("conv_fwd_pair", &conv_fwd_pair, "two same-shape convs (expert + learner) in one launch");
   m.def("cnn_fc_pair", &cnn_fc_pair, "two same-shape cnn_fc layers in one launch");
-  m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts, one launch");
+  m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts, one launch", py::arg("ws"),
+        py::arg("want_t"), py::arg("t_hwc") = std::vector<bool>{});
+  m.def("fc_backward", &fc_backward, "NatureCNN feature-layer backward (dW torch layout, db, dX NHWC bf16)");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
         py::arg("relu_out"), py::arg("pad") = 0);

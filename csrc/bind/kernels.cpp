@@ -256,8 +256,8 @@ torch::Tensor cat_eval_bwd(torch::Tensor z, torch::Tensor acts, c10::optional<to
 
 // BC loss on a categorical head: metric vector [7] (see rl.hip) from raw logits z [B, A] fp32,
 // acts [B] int64 and (optionally) the flat fp32 parameter buffer for l2_norm
-torch::Tensor bc_cat_loss_fwd(torch::Tensor z, torch::Tensor acts, c10::optional<torch::Tensor> flat, double ent_w,
-                              double l2_w) {
+py::tuple bc_cat_loss_fwd(torch::Tensor z, torch::Tensor acts, c10::optional<torch::Tensor> flat, double ent_w,
+                          double l2_w) {
   IA_CHECK_GPU_F32(z);
   IA_CHECK_CONTIG(z);
   IA_CHECK_CUDA(acts);
@@ -274,20 +274,34 @@ torch::Tensor bc_cat_loss_fwd(torch::Tensor z, torch::Tensor acts, c10::optional
     n = (long)flat->numel();
   }
   auto out = torch::empty({7}, z.options());
+  auto loss = torch::empty({}, z.options());
   auto part = torch::empty({fp ? ia::sumsq_nparts(n) : 1}, z.options());
   IA_HIP_CHECK(ia::bc_cat_loss_fwd(z.data_ptr<float>(), acts.data_ptr<int64_t>(), (int)z.size(0), (int)z.size(1), fp, n,
-                                   part.data_ptr<float>(), (float)ent_w, (float)l2_w, out.data_ptr<float>(), ia_stream()));
-  return out;
+                                   part.data_ptr<float>(), (float)ent_w, (float)l2_w, out.data_ptr<float>(),
+                                   loss.data_ptr<float>(), ia_stream()));
+  return py::make_tuple(out, loss);
 }
 
-torch::Tensor bc_cat_loss_bwd(torch::Tensor z, torch::Tensor acts, torch::Tensor g, double ent_w) {
+torch::Tensor bc_cat_loss_bwd(torch::Tensor z, torch::Tensor acts, c10::optional<torch::Tensor> g,
+                              c10::optional<torch::Tensor> g_loss, double ent_w) {
   IA_CHECK_GPU_F32(z);
   IA_CHECK_CONTIG(z);
-  auto gc = g.contiguous().to(torch::kFloat32);
-  TORCH_CHECK(gc.numel() == 7 && gc.is_cuda(), "bc_cat_loss_bwd: g must be the [7] metric gradient");
+  torch::Tensor gc, glc;
+  const float* gp = nullptr;
+  const float* glp = nullptr;
+  if (g.has_value() && g->defined()) {
+    gc = g->contiguous().to(torch::kFloat32);
+    TORCH_CHECK(gc.numel() == 7 && gc.is_cuda(), "bc_cat_loss_bwd: g must be the [7] metric gradient");
+    gp = gc.data_ptr<float>();
+  }
+  if (g_loss.has_value() && g_loss->defined()) {
+    glc = g_loss->contiguous().to(torch::kFloat32);
+    TORCH_CHECK(glc.numel() == 1 && glc.is_cuda(), "bc_cat_loss_bwd: g_loss must be a scalar");
+    glp = glc.data_ptr<float>();
+  }
   auto dz = torch::empty_like(z);
-  IA_HIP_CHECK(ia::bc_cat_loss_bwd(z.data_ptr<float>(), acts.data_ptr<int64_t>(), (int)z.size(0), (int)z.size(1),
-                                   gc.data_ptr<float>(), (float)ent_w, dz.data_ptr<float>(), ia_stream()));
+  IA_HIP_CHECK(ia::bc_cat_loss_bwd(z.data_ptr<float>(), acts.data_ptr<int64_t>(), (int)z.size(0), (int)z.size(1), gp, glp,
+                                   (float)ent_w, dz.data_ptr<float>(), ia_stream()));
   return dz;
 }
 
@@ -450,7 +464,8 @@ void register_kernels(py::module& m) {
   m.def("kde_score", &kde_score, py::arg("q"), py::arg("x"), py::arg("bandwidth"), py::arg("kind"), py::arg("offset"));
   m.def("bc_cat_loss_fwd", &bc_cat_loss_fwd, py::arg("z"), py::arg("acts"), py::arg("flat"), py::arg("ent_w"),
         py::arg("l2_w"));
-  m.def("bc_cat_loss_bwd", &bc_cat_loss_bwd, py::arg("z"), py::arg("acts"), py::arg("g"), py::arg("ent_w"));
+  m.def("bc_cat_loss_bwd", &bc_cat_loss_bwd, py::arg("z"), py::arg("acts"), py::arg("g"), py::arg("g_loss"),
+        py::arg("ent_w"));
   m.def("cat_eval_fwd", &cat_eval_fwd, py::arg("z"), py::arg("acts"));
   m.def("cat_eval_bwd", &cat_eval_bwd, py::arg("z"), py::arg("acts"), py::arg("g_lp"), py::arg("g_ent"));
 }

@@ -1,0 +1,140 @@
+// Backward of the NatureCNN feature layer Linear(C*H*W -> NH) + ReLU on bf16 MFMA tiles, for
+// training steps whose conv trunk runs on conv.hip (ops/conv.py conv_stack_fc; BC / DAgger
+// minibatches, reference bc.py:100-130 through SB3's NatureCNN).
+//
+// The forward is cnn_fc (cnn_infer.hip) on the conv trunk's NHWC bf16 output and the weight
+// packed to (h, w, c) column order, so there is no flatten permute in either direction. At the
+// BC batch (32 rows) the torch form is three fp32 hipBLASLt GEMMs (~30 us, each reading or
+// writing the 6.4 MB fp32 weight), a permute copy each way, ReLU / bias kernels. Here:
+//   fc_wgrad  dW[n][col] = sum_m dZ[m][n] X[m][k(col)],  db[n] = sum_m dZ[m][n],
+//             dZ = dH * [h > 0] formed on the fly. Block = 64 n x 16 torch columns (4 waves
+//             x 16x16); per 32-row step dZ^T and X are staged transposed in LDS so both MFMA
+//             operands read 8 consecutive rows; dW rows are stored contiguously.
+//   fc_dgrad  dX[m][k] = sum_n dZ[m][n] Wt[k][n] (Wt: the weight packed [(h, w, c)][NH], dZ
+//             in bf16 from fc_wgrad), bf16 out in NHWC order = the conv trunk's upstream
+//             gradient. One wave per 16x16 tile, 8 loads in flight per k-batch.
+#include <hip/hip_runtime.h>
+
+#include "ia/mfma.h"
+#include "launchers.h"
+
+namespace ia {
+namespace {
+
+// Block = 64 n x 16 torch columns (4 waves x 16x16, wave w owns n rows 16w..16w+15). The 16
+// columns are consecutive in torch's (c, h, w) order, so every dW row segment is one 64-B
+// store; they are gathered from X through the column -> NHWC index map while staged, once per
+// block for all 4 waves. The blocks of the first column tile also write dZ in bf16 (the
+// data-gradient operand) and db.
+__global__ __launch_bounds__(256) void fc_wgrad_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
+                                                       const float* __restrict__ Hout, float* __restrict__ dW,
+                                                       float* __restrict__ db, bf16* __restrict__ dZb, int M, int K, int NH,
+                                                       int C, int HW) {
+  __shared__ __attribute__((aligned(16))) bf16 zs[64][40];  // dZ^T chunk [n][m] (+8 pad)
+  __shared__ __attribute__((aligned(16))) bf16 xs[16][40];  // X^T chunk [col][m]
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int col0 = blockIdx.x * 16, n0 = blockIdx.y * 64;
+  const bool first = blockIdx.x == 0;
+  // this thread's 2 staged (column, row) elements of X: column -> NHWC offset
+  const int xc = tid & 15, xm = tid >> 4;  // 16 columns x 16 rows per pass, 2 passes
+  const int xcol = col0 + xc, xch = xcol / HW;
+  const int koff = (xcol - xch * HW) * C + xch;
+  f32x4 acc = zero4();
+  for (int m0 = 0; m0 < M; m0 += 32) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {  // dZ^T: 64 n x 32 m, coalesced along n
+      const int i = tid + 256 * e, nn = i & 63, mm = i >> 6;
+      const int m = m0 + mm;
+      float z = 0.f;
+      if (m < M) {
+        const size_t o = (size_t)m * NH + n0 + nn;
+        z = Hout[o] > 0.f ? dH[o] : 0.f;
+        if (first) dZb[o] = (bf16)z;
+      }
+      zs[nn][mm] = (bf16)z;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {  // X^T: 16 columns x 32 m
+      const int mm = xm + 16 * e, m = m0 + mm;
+      xs[xc][mm] = m < M ? X[(size_t)m * K + koff] : (bf16)0.f;
+    }
+    __syncthreads();
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&zs[w * 16 + (l & 15)][(l >> 4) * 8]);
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(&xs[l & 15][(l >> 4) * 8]);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    __syncthreads();
+  }
+  const int col = col0 + (l & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dW[(size_t)(n0 + w * 16 + 4 * (l >> 4) + i) * K + col] = acc[i];
+  if (first && tid < 64) {  // bias gradient, fixed row order
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) {
+      const size_t o = (size_t)m * NH + n0 + tid;
+      s += Hout[o] > 0.f ? dH[o] : 0.f;
+    }
+    db[n0 + tid] = s;
+  }
+}
+
+// One wave = 16 rows x 16 NHWC columns; the n loop is issued 4 k-steps (8 loads) at a time
+// so the L2 round trips overlap (the wave reads 16 KB of Wt).
+__global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
+                                                       bf16* __restrict__ dX, int M, int K, int NH) {
+  const int l = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int ktiles = K / 16;
+  const int mt = wave / ktiles, kt = wave - mt * ktiles;
+  const int m0 = mt * 16, k0 = kt * 16;
+  if (m0 >= M) return;
+  const int m = m0 + (l & 15);
+  const bool mv = m < M;
+  const int nq = (l >> 4) * 8;
+  const bf16* ar = dZb + (size_t)(mv ? m : 0) * NH + nq;
+  const bf16* br = Wt + (size_t)(k0 + (l & 15)) * NH + nq;
+  f32x4 acc = zero4();
+  for (int n0 = 0; n0 < NH; n0 += 128) {
+    bf16x8 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = n0 + 32 * u < NH;
+      a[u] = ok ? *reinterpret_cast<const bf16x8*>(ar + n0 + 32 * u) : bf16x8{};
+      b[u] = ok ? *reinterpret_cast<const bf16x8*>(br + n0 + 32 * u) : bf16x8{};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!mv) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[u][j] = (bf16)0.f;
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc, 0, 0, 0);
+    }
+  }
+  const int k = k0 + (l & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + 4 * (l >> 4) + i;
+    if (row < M) dX[(size_t)row * K + k] = (bf16)acc[i];
+  }
+}
+
+}  // namespace
+
+bool fc_train_ok(int M, int K, int NH, int C, int HW) {
+  return M > 0 && NH > 0 && NH % 64 == 0 && K % 64 == 0 && C > 0 && HW > 0 && K == C * HW;
+}
+
+hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const void* Wt, float* dW, float* db, void* dX,
+                       void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s) {
+  if (!fc_train_ok(M, K, NH, C, HW)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / 16, NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout, dW, db,
+                     static_cast<bf16*>(dZb), M, K, NH, C, HW);
+  if (dX) {
+    const int waves = ((M + 15) / 16) * (K / 16);
+    hipLaunchKernelGGL(fc_dgrad_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, static_cast<const bf16*>(dZb),
+                       static_cast<const bf16*>(Wt), static_cast<bf16*>(dX), M, K, NH);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace ia

@@ -522,18 +522,50 @@ hipError_t launch_wgrad(const TIn* X, const bf16* dY, const bf16* Y, float* slab
 }
 
 // fp32 torch-layout conv weights [N][C][KH][KW] of up to kMaxPack layers -> bf16 [N][KH][KW][C]
-// (forward GEMM operand) and, where requested, bf16 [C][KH][KW][N] (data-gradient operand),
-// all layers in one launch (blockIdx.y = layer).
-__global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a) {
-  const int li = blockIdx.y;
-  const ConvPackLayer& L = a.layer[li];
-  const int taps = L.KH * L.KW;
-  const int total = L.N * L.C * taps;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-    const int n = i / (L.C * taps), rem = i - n * L.C * taps, c = rem / taps, tap = rem - c * taps;
-    const bf16 v = (bf16)L.w[i];
-    static_cast<bf16*>(L.wb)[((size_t)n * taps + tap) * L.C + c] = v;
-    if (L.wt) static_cast<bf16*>(L.wt)[((size_t)c * taps + tap) * L.N + n] = v;
+// (forward GEMM operand) and, where requested, the data-gradient operand: bf16 [C][KH][KW][N]
+// (a 2-D transpose of the source viewed [N][C*KH*KW]) or, t_hwc, [KH][KW][C][N] (a 2-D
+// transpose of the packed [N][KH*KW*C]). Both passes are 32x32 LDS-tile transposes with
+// coalesced reads and writes (blockIdx.z = layer): the NatureCNN FC weight (6.4 MB) included.
+__global__ __launch_bounds__(256) void conv_pack_wb_kernel(ConvPackArgs a) {
+  __shared__ float t[32][33];
+  const ConvPackLayer& L = a.layer[blockIdx.z];
+  const int n = blockIdx.y;
+  const int taps = L.KH * L.KW, C = L.C;
+  const int tt = (taps + 31) / 32, nc = (C + 31) / 32;
+  if (n >= L.N || (int)blockIdx.x >= tt * nc) return;
+  const int c0 = ((int)blockIdx.x / tt) * 32, p0 = ((int)blockIdx.x % tt) * 32;
+  const float* src = L.w + (size_t)n * C * taps;
+  for (int i = threadIdx.x; i < 1024; i += 256) {  // src [c][tap], coalesced along tap
+    const int r = i >> 5, q = i & 31, c = c0 + r, p = p0 + q;
+    t[r][q] = (c < C && p < taps) ? src[(size_t)c * taps + p] : 0.f;
+  }
+  __syncthreads();
+  bf16* dst = static_cast<bf16*>(L.wb) + (size_t)n * taps * C;
+  for (int i = threadIdx.x; i < 1024; i += 256) {  // dst [tap][c], coalesced along c
+    const int r = i >> 5, q = i & 31, p = p0 + r, c = c0 + q;
+    if (p < taps && c < C) dst[(size_t)p * C + c] = (bf16)t[q][r];
+  }
+}
+
+__global__ __launch_bounds__(256) void conv_pack_wt_kernel(ConvPackArgs a) {
+  __shared__ float t[32][33];
+  const ConvPackLayer& L = a.layer[blockIdx.z];
+  if (!L.wt) return;
+  const int K = L.C * L.KH * L.KW, N = L.N;
+  const int k0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  if (k0 >= K || n0 >= N) return;
+  const bf16* wb = static_cast<const bf16*>(L.wb);
+  for (int i = threadIdx.x; i < 1024; i += 256) {  // [n][k] rows, coalesced along k
+    const int r = i >> 5, q = i & 31, nn = n0 + r, k = k0 + q;
+    float v = 0.f;
+    if (nn < N && k < K) v = L.t_hwc ? (float)wb[(size_t)nn * K + k] : L.w[(size_t)nn * K + k];
+    t[r][q] = v;
+  }
+  __syncthreads();
+  bf16* dst = static_cast<bf16*>(L.wt);
+  for (int i = threadIdx.x; i < 1024; i += 256) {  // [k][n], coalesced along n
+    const int r = i >> 5, q = i & 31, k = k0 + r, nn = n0 + q;
+    if (k < K && nn < N) dst[(size_t)k * N + nn] = (bf16)t[q][r];
   }
 }
 
@@ -542,13 +574,20 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a) {
 hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
   if (a.n > kMaxPack) return hipErrorInvalidValue;
-  int most = 0;
+  int max_n = 0, max_tiles = 0, max_k = 0;
+  bool any_t = false;
   for (int i = 0; i < a.n; ++i) {
-    const int t = a.layer[i].N * a.layer[i].C * a.layer[i].KH * a.layer[i].KW;
-    most = t > most ? t : most;
+    const ConvPackLayer& L = a.layer[i];
+    const int taps = L.KH * L.KW;
+    max_n = L.N > max_n ? L.N : max_n;
+    const int tiles = ((taps + 31) / 32) * ((L.C + 31) / 32);
+    max_tiles = tiles > max_tiles ? tiles : max_tiles;
+    max_k = L.C * taps > max_k ? L.C * taps : max_k;
+    any_t = any_t || L.wt != nullptr;
   }
-  const int bx = (most + 255) / 256 < 64 ? (most + 255) / 256 : 64;
-  hipLaunchKernelGGL(conv_pack_kernel, dim3(bx, a.n), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(conv_pack_wb_kernel, dim3(max_tiles, max_n, a.n), dim3(256), 0, s, a);
+  if (any_t)  // after the wb pass: the t_hwc transposes read the packed weights
+    hipLaunchKernelGGL(conv_pack_wt_kernel, dim3((max_k + 31) / 32, (max_n + 31) / 32, a.n), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

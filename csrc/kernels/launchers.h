@@ -103,6 +103,12 @@ hipError_t dagger_env_step(const DaggerEnvArgs& a, hipStream_t s);
 // ---- cnn_infer.hip: NatureCNN actor tail for the DAgger collector
 // h[B][NH] = relu(X[B][K] . W[NH][K]^T + bias), X / W bf16 (K % 32 == 0, NH % 16 == 0)
 hipError_t cnn_fc(const void* X, const void* W, const float* bias, float* H, int B, int K, int NH, hipStream_t s);
+// NatureCNN feature-layer backward (cnn_fc.hip): X bf16 [M][K] (NHWC-flattened conv output,
+// K = C * HW), dH / Hout fp32 [M][NH], Wt bf16 [K][NH]; dW fp32 [NH][K] in torch's (c, h, w)
+// column order, db fp32 [NH], dX bf16 [M][K] (nullptr: not needed)
+bool fc_train_ok(int M, int K, int NH, int C, int HW);
+hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const void* Wt, float* dW, float* db, void* dX,
+                       void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s);  // dZb: bf16 [M][NH] scratch
 struct CnnFcPair {
   const void* X[2];
   const void* W[2];
@@ -151,9 +157,9 @@ hipError_t cat_eval_bwd(const float* z, const int64_t* act, int B, int A, const 
 // logit gradient for an upstream gradient g[7] of the metric vector
 int sumsq_nparts(long n);
 hipError_t bc_cat_loss_fwd(const float* z, const int64_t* act, int B, int A, const float* flat, long n, float* part,
-                           float ent_w, float l2_w, float* out, hipStream_t s);
-hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, const float* g, float ent_w, float* dz,
-                           hipStream_t s);
+                           float ent_w, float l2_w, float* out, float* loss_out, hipStream_t s);
+hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, const float* g, const float* g_loss,
+                           float ent_w, float* dz, hipStream_t s);
 
 // ---- gather.hip: one-launch multi-field row gather (row r <- source row b[r] * n_envs + e[r],
 // or b[r] when e == nullptr)
@@ -225,6 +231,7 @@ struct ConvPackLayer {
   void* wb;  // bf16
   void* wt;  // bf16, nullptr: not needed
   int N, C, KH, KW;
+  int t_hwc;  // wt layout: 0 [C][KH][KW][N] (conv dgrad), 1 [KH][KW][C][N] (NHWC-flattened FC)
 };
 struct ConvPackArgs {
   ConvPackLayer layer[kMaxPack];

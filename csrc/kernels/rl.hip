@@ -222,7 +222,8 @@ hipError_t cat_eval_bwd(const float* z, const int64_t* act, int B, int A, const 
 //   bc_cat_loss_fwd: one block; per-row log pi(a), entropy, pi(a) reduced in a fixed
 //                   order, the partials summed, and the metric vector written:
 //                   [neglogp, entropy, ent_loss, prob_true_act, l2_norm, l2_loss, loss].
-//   bc_cat_loss_bwd: logit gradient for an upstream gradient g[7] of the metric vector:
+//   bc_cat_loss_bwd: logit gradient for an upstream gradient g[7] of the metric vector (and /
+//                   or g_loss of the separately returned loss, added to g[6]):
 //                   per row g_lp = (-g0 - g6)/B + g3 pi(a)/B, g_ent = (g1 - w g2 - w g6)/B,
 //                   dz_k = g_lp (1[k == a] - p_k) - g_ent p_k (log p_k + H).
 namespace {
@@ -269,7 +270,8 @@ __device__ __forceinline__ void cat_row(const float* zr, int A, float& lse, floa
 __global__ __launch_bounds__(kLossThreads) void bc_cat_loss_fwd_kernel(const float* __restrict__ z,
                                                                        const int64_t* __restrict__ act, int B, int A,
                                                                        const float* __restrict__ part, int nparts,
-                                                                       float ent_w, float l2_w, float* __restrict__ out) {
+                                                                       float ent_w, float l2_w, float* __restrict__ out,
+                                                                       float* __restrict__ loss_out) {
   __shared__ float red[4];
   float slp = 0.f, sent = 0.f, sp = 0.f;
   for (int r = threadIdx.x; r < B; r += kLossThreads) {
@@ -299,12 +301,14 @@ __global__ __launch_bounds__(kLossThreads) void bc_cat_loss_fwd_kernel(const flo
     out[4] = l2;
     out[5] = l2_loss;
     out[6] = neglogp + ent_loss + l2_loss;
+    if (loss_out) loss_out[0] = out[6];
   }
 }
 
 __global__ __launch_bounds__(kLossThreads) void bc_cat_loss_bwd_kernel(const float* __restrict__ z,
                                                                        const int64_t* __restrict__ act, int B, int A,
-                                                                       const float* __restrict__ g, float ent_w,
+                                                                       const float* __restrict__ g,
+                                                                       const float* __restrict__ g_loss, float ent_w,
                                                                        float* __restrict__ dz) {
   const int r = blockIdx.x * kLossThreads + threadIdx.x;
   if (r >= B) return;
@@ -314,8 +318,11 @@ __global__ __launch_bounds__(kLossThreads) void bc_cat_loss_bwd_kernel(const flo
   const int a = (int)act[r];
   const float inv = 1.f / (float)B;
   const float pa = (a >= 0 && a < A) ? expf(zr[a] - lse) : 0.f;
-  const float gl = (-g[0] - g[6]) * inv + g[3] * pa * inv;
-  const float ge = (g[1] - ent_w * g[2] - ent_w * g[6]) * inv;
+  // upstream: the metric vector's gradient g[7] and / or the separate loss output's g_loss
+  const float g6 = (g ? g[6] : 0.f) + (g_loss ? g_loss[0] : 0.f);
+  const float g0 = g ? g[0] : 0.f, g1 = g ? g[1] : 0.f, g2 = g ? g[2] : 0.f, g3 = g ? g[3] : 0.f;
+  const float gl = (-g0 - g6) * inv + g3 * pa * inv;
+  const float ge = (g1 - ent_w * g2 - ent_w * g6) * inv;
   for (int k = 0; k < A; ++k) {
     const float lp = zr[k] - lse, p = expf(lp);
     dz[(size_t)r * A + k] = gl * ((k == a ? 1.f : 0.f) - p) - ge * p * (lp + h);
@@ -329,21 +336,22 @@ int sumsq_nparts(long n) {
 }
 
 hipError_t bc_cat_loss_fwd(const float* z, const int64_t* act, int B, int A, const float* flat, long n, float* part,
-                           float ent_w, float l2_w, float* out, hipStream_t s) {
+                           float ent_w, float l2_w, float* out, float* loss_out, hipStream_t s) {
   int np = 0;
   if (flat && n > 0) {
     np = sumsq_nparts(n);
     hipLaunchKernelGGL(sumsq_partials_kernel, dim3(np), dim3(kLossThreads), 0, s, flat, n, part);
   }
-  hipLaunchKernelGGL(bc_cat_loss_fwd_kernel, dim3(1), dim3(kLossThreads), 0, s, z, act, B, A, part, np, ent_w, l2_w, out);
+  hipLaunchKernelGGL(bc_cat_loss_fwd_kernel, dim3(1), dim3(kLossThreads), 0, s, z, act, B, A, part, np, ent_w, l2_w, out,
+                     loss_out);
   return hipGetLastError();
 }
 
-hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, const float* g, float ent_w, float* dz,
-                           hipStream_t s) {
+hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, const float* g, const float* g_loss,
+                           float ent_w, float* dz, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(bc_cat_loss_bwd_kernel, dim3((B + kLossThreads - 1) / kLossThreads), dim3(kLossThreads), 0, s, z,
-                     act, B, A, g, ent_w, dz);
+                     act, B, A, g, g_loss, ent_w, dz);
   return hipGetLastError();
 }
 

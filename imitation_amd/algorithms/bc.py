@@ -131,8 +131,10 @@ class BehaviorCloningLossCalculator:
         if flat is None:
             return None
         dist = policy.get_distribution(obs)
-        m = rl_ops.bc_categorical_loss(dist.raw_logits, acts, params, self.ent_weight, self.l2_weight, flat)
-        return BCTrainingMetrics(**{k: m[i] for i, k in enumerate(rl_ops.BC_METRICS)})
+        m, loss = rl_ops.bc_categorical_loss(dist.raw_logits, acts, params, self.ent_weight, self.l2_weight, flat)
+        fields = {k: m[i] for i, k in enumerate(rl_ops.BC_METRICS)}
+        fields["loss"] = loss
+        return BCTrainingMetrics(**fields)
 
 
 def enumerate_batches(batch_it: Iterable[types.TransitionMapping]) -> Iterable[Tuple[Tuple[int, int, int], types.TransitionMapping]]:

@@ -90,24 +90,114 @@ class _ConvStack(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        grads = _stack_backward(ctx, saved[0], saved[1 : 1 + n], saved[1 + n :], gy.contiguous().to(torch.bfloat16))
+        return (None, None, None, None, None, *grads)
+
+
+def _stack_backward(ctx, x, ws, acts, dz) -> List[Optional[torch.Tensor]]:
+    """Conv-stack backward from the top layer's (pre-ReLU-mask) upstream gradient ``dz``
+    (bf16 NHWC): per layer one weight-gradient kernel and, below the top, one data-gradient
+    kernel that applies the next-lower layer's ReLU mask."""
+    C = ops.native()
+    n = len(ws)
+    grads: List[Optional[torch.Tensor]] = [None] * (2 * n)
+    for i in range(n - 1, -1, -1):
+        w, s, p = ws[i], ctx.strides[i], ctx.pads[i]
+        N, Cin, KH, KW = w.shape
+        inp = x if i == 0 else acts[i - 1]
+        top = i == n - 1  # only the top layer's ReLU mask is still pending on dz
+        scale = ctx.in_scale if i == 0 else 1.0
+        dW, db = C.conv_wgrad(inp, dz, acts[i], int(KH), int(KW), int(s), scale, top, p)  # [N, C, KH, KW]
+        grads[2 * i] = dW if dW.dtype == w.dtype else dW.to(w.dtype)
+        grads[2 * i + 1] = db
+        if i > 0:
+            dz = C.conv_dgrad(dz, acts[i], ctx.wts[i], acts[i - 1], int(s), top, True, p)
+    return grads
+
+
+class _ConvStackFC(torch.autograd.Function):
+    """Conv stack + flatten + Linear + ReLU (SB3 NatureCNN's whole feature extractor) as one
+    autograd node: all weights packed in ONE launch (the FC weight to (h, w, c) columns and
+    its transposed data-gradient layout), the FC forward on the conv output's NHWC bf16
+    (``cnn_fc``), its backward as 2 launches (``fc_backward``: dW in torch's column order +
+    db, and dX in NHWC = the trunk's upstream gradient) -- no flatten permutes, no fp32
+    hipBLASLt GEMMs over the 6.4 MB weight."""
+
+    @staticmethod
+    def forward(ctx, x, in_scale, strides, *params):
+        C = ops.native()
+        ws, bs = params[0:-2:2], params[1:-2:2]
+        fc_w, fc_b = params[-2], params[-1]
+        n = len(ws)
+        acts: List[torch.Tensor] = []
+        # trunk shape -> the FC weight viewed as a [NH, C3, H3, W3] "conv" for the packer
+        h = x
+        B = x.shape[0]
+        wsrc = [w.detach().contiguous() for w in ws]
+        Hh, Ww, Cc = x.shape[1], x.shape[2], x.shape[3]
+        for w, s in zip(ws, strides):
+            Hh, Ww, Cc = (Hh - w.shape[2]) // int(s) + 1, (Ww - w.shape[3]) // int(s) + 1, w.shape[0]
+        NH = fc_w.shape[0]
+        wsrc.append(fc_w.detach().contiguous().view(NH, Cc, Hh, Ww))
+        wbs, wts = C.conv_pack_weights(wsrc, [i > 0 for i in range(n)] + [True], [False] * n + [True])
+        for i, (wb, b, s) in enumerate(zip(wbs[:n], bs, strides)):
+            h = C.conv_fwd(h, wb, b.detach().float().contiguous(), int(s), float(in_scale) if i == 0 else 1.0, True, 0)
+            acts.append(h)
+        xf = h.reshape(B, -1)
+        out = C.cnn_fc(xf, wbs[n].view(NH, -1), fc_b.detach().float().contiguous())
+        ctx.wts = wts[:n]
+        ctx.wt_fc = wts[n]
+        ctx.c3 = int(Cc)
+        ctx.save_for_backward(x, *ws, *acts, out)
+        ctx.in_scale = float(in_scale)
+        ctx.strides = tuple(int(s) for s in strides)
+        ctx.pads = (0,) * n
+        ctx.n = n
+        return out
+
+    @staticmethod
+    def backward(ctx, dh):
         C = ops.native()
         n = ctx.n
         saved = ctx.saved_tensors
-        x, ws, acts = saved[0], saved[1 : 1 + n], saved[1 + n :]
-        grads = [None] * (2 * n)
-        dz = gy.contiguous().to(torch.bfloat16)
-        for i in range(n - 1, -1, -1):
-            w, s, p = ws[i], ctx.strides[i], ctx.pads[i]
-            N, Cin, KH, KW = w.shape
-            inp = x if i == 0 else acts[i - 1]
-            top = i == n - 1  # only the top layer's ReLU mask is still pending on dz
-            scale = ctx.in_scale if i == 0 else 1.0
-            dW, db = C.conv_wgrad(inp, dz, acts[i], int(KH), int(KW), int(s), scale, top, p)  # [N, C, KH, KW]
-            grads[2 * i] = dW if dW.dtype == w.dtype else dW.to(w.dtype)
-            grads[2 * i + 1] = db
-            if i > 0:
-                dz = C.conv_dgrad(dz, acts[i], ctx.wts[i], acts[i - 1], int(s), top, True, p)
-        return (None, None, None, None, None, *grads)
+        x, ws, acts, out = saved[0], saved[1 : 1 + n], saved[1 + n : 1 + 2 * n], saved[1 + 2 * n]
+        top = acts[-1]
+        dW, db, dx = C.fc_backward(top.reshape(top.shape[0], -1), dh, out, ctx.wt_fc, ctx.c3, True)
+        grads = _stack_backward(ctx, x, ws, acts, dx.view(top.shape))
+        return (None, None, None, *grads, dW, db)
+
+
+def fc_supported(x_shape, weights: Sequence[torch.Tensor], strides: Sequence[int], fc_out: int) -> bool:
+    """Whether :func:`conv_stack_fc` covers this trunk: a valid-padding conv stack the kernels
+    take without channel padding, and an FC with K = C3*H3*W3 % 64 == 0, NH % 64 == 0."""
+    if not supported(x_shape, weights, strides):
+        return False
+    _, H, W, C = x_shape
+    w0 = weights[0]
+    if (w0.shape[1] * w0.shape[2] * w0.shape[3]) % 32 != 0:
+        return False  # first layer would take the tap-checked, channel-padded path
+    for w, s in zip(weights, strides):
+        H, W, C = (H - w.shape[2]) // int(s) + 1, (W - w.shape[3]) // int(s) + 1, w.shape[0]
+    return (C * H * W) % 64 == 0 and fc_out % 64 == 0
+
+
+def conv_stack_fc(x_nhwc: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor],
+                  strides: Sequence[int], fc_weight: torch.Tensor, fc_bias: torch.Tensor,
+                  in_scale: float = 1.0) -> torch.Tensor:
+    """``relu(linear(flatten_chw(conv_stack(x))))`` -- NatureCNN's feature extractor -- as one
+    autograd node on the HIP kernels (:class:`_ConvStackFC`); the fp32 reference elsewhere.
+    Flatten order is torch's (C, H, W), as ``nn.Flatten`` after NCHW convs."""
+    if not ops.use_kernel(x_nhwc) or not fc_supported(tuple(x_nhwc.shape), weights, strides, fc_weight.shape[0]):
+        y = conv_stack_reference(x_nhwc, weights, biases, strides, in_scale)
+        y = y.permute(0, 3, 1, 2).reshape(y.shape[0], -1)
+        return F.relu(F.linear(y, fc_weight, fc_bias))
+    params = []
+    for w, b in zip(weights, biases):
+        params += [w, b]
+    return _ConvStackFC.apply(x_nhwc.contiguous(), float(in_scale), tuple(int(s) for s in strides), *params, fc_weight,
+                              fc_bias)
 
 
 def conv_stack(x_nhwc: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor],

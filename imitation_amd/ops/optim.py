@@ -37,6 +37,7 @@ class FusedAdam(th.optim.Optimizer):
                         decoupled_weight_decay=decoupled_weight_decay, capturable=True)
         super().__init__(params, defaults)
         self._flat: List[Dict[str, Any]] = []
+        self._seeds: Dict[Any, th.Tensor] = {}
         for group in self.param_groups:
             self._flat.append(self._pack_group(group))
 
@@ -103,7 +104,11 @@ class FusedAdam(th.optim.Optimizer):
         parameter. Parameters without a gradient keep their zero slice."""
         live = [(f, i) for f in self._flat if f["n"] for i in range(len(f["params"]))]
         params = [f["params"][i] for f, i in live]
-        grads = th.autograd.grad(loss, params, allow_unused=True)
+        # a persistent unit seed: no fill launch per step (and graph-capturable)
+        seed = self._seeds.get((loss.device, loss.dtype, tuple(loss.shape)))
+        if seed is None:
+            seed = self._seeds[(loss.device, loss.dtype, tuple(loss.shape))] = th.ones_like(loss)
+        grads = th.autograd.grad(loss, params, grad_outputs=seed, allow_unused=True)
         run: List[th.Tensor] = []
         start = end = 0
         cur = None

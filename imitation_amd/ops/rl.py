@@ -179,17 +179,18 @@ class _BCCategoricalLoss(torch.autograd.Function):
 
         z = logits.contiguous()
         a = actions.reshape(-1).long().contiguous()
-        out = native().bc_cat_loss_fwd(z, a, flat, float(ent_weight), float(l2_weight))
+        out, loss = native().bc_cat_loss_fwd(z, a, flat, float(ent_weight), float(l2_weight))
         ctx.save_for_backward(z, a)
         ctx.ent_weight = float(ent_weight)
-        return out
+        ctx.set_materialize_grads(False)
+        return out, loss
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, g_loss):
         from imitation_amd.ops import native
 
         z, a = ctx.saved_tensors
-        return native().bc_cat_loss_bwd(z, a, g, ctx.ent_weight), None, None, None, None
+        return native().bc_cat_loss_bwd(z, a, g, g_loss, ctx.ent_weight), None, None, None, None
 
 
 def flat_param_view(params) -> "torch.Tensor | None":
@@ -210,16 +211,18 @@ def flat_param_view(params) -> "torch.Tensor | None":
 
 
 def bc_categorical_loss(logits, actions, params, ent_weight: float, l2_weight: float,
-                        flat: "torch.Tensor | None" = None) -> torch.Tensor:
-    """BC loss metric vector ``[7]`` (``BC_METRICS`` order); ``loss`` is differentiable
-    w.r.t. the logits. HIP kernels on the GPU when ``l2_weight == 0`` and the parameters
-    form one flat buffer (``flat``), else the reference."""
+                        flat: "torch.Tensor | None" = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``(metrics [7], loss)``: the BC metric vector (``BC_METRICS`` order) and the loss as
+    its own scalar, both differentiable w.r.t. the logits (backpropagating ``loss`` alone
+    needs no zero-filled vector gradient). HIP kernels on the GPU when ``l2_weight == 0`` and
+    the parameters form one flat buffer (``flat``), else the reference."""
     from imitation_amd.ops import use_kernel
 
     if (use_kernel(logits) and logits.dtype == torch.float32 and logits.dim() == 2 and 0 < logits.shape[1] <= 64
             and logits.shape[0] > 0 and actions.numel() == logits.shape[0] and l2_weight == 0.0 and flat is not None):
         return _BCCategoricalLoss.apply(logits, actions, flat.detach(), ent_weight, l2_weight)
-    return bc_categorical_loss_reference(logits, actions, params, ent_weight, l2_weight)
+    m = bc_categorical_loss_reference(logits, actions, params, ent_weight, l2_weight)
+    return m, m[6]
 
 
 def gather_rows(srcs, b: torch.Tensor, e: "torch.Tensor | None" = None, n_envs: int = 1):

@@ -132,16 +132,25 @@ class SquashedDiagGaussianDistribution(DiagGaussianDistribution):
 class CategoricalDistribution(Distribution):
     def __init__(self, action_dim: int):
         self.action_dim = action_dim
-        self.logits: Optional[th.Tensor] = None
         self.raw_logits: Optional[th.Tensor] = None
+        self._logits: Optional[th.Tensor] = None
 
     def proba_distribution_net(self, latent_dim: int) -> nn.Module:
         return nn.Linear(latent_dim, self.action_dim)
 
     def proba_distribution(self, action_logits: th.Tensor) -> "CategoricalDistribution":
         self.raw_logits = action_logits
-        self.logits = action_logits - action_logits.logsumexp(dim=-1, keepdim=True)
+        self._logits = None
         return self
+
+    @property
+    def logits(self) -> Optional[th.Tensor]:
+        """Normalised log-probabilities, computed on first use (the fused BC / evaluation
+        paths read only ``raw_logits`` and never pay for the logsumexp)."""
+        if self._logits is None and self.raw_logits is not None:
+            z = self.raw_logits
+            self._logits = z - z.logsumexp(dim=-1, keepdim=True)
+        return self._logits
 
     def log_prob_entropy(self, actions: th.Tensor) -> Tuple[th.Tensor, th.Tensor]:
         """``(log_prob(actions), entropy())`` in one fused pass over the raw logits (HIP

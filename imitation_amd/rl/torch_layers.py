@@ -73,6 +73,13 @@ class NatureCNN(BaseFeaturesExtractor):
 
         x = observations if self.channels_last_input else observations.permute(0, 2, 3, 1)
         convs = [m for m in self.cnn if isinstance(m, nn.Conv2d)]
+        lin = self.linear[0]
+        if (x.is_cuda and isinstance(self.linear[-1], nn.ReLU) and len(self.linear) == 2
+                and conv_ops.fc_supported(tuple(x.shape), [c.weight for c in convs], [c.stride[0] for c in convs],
+                                          lin.out_features)):
+            # whole extractor (convs + flatten + Linear + ReLU) as one kernel-backed node
+            return conv_ops.conv_stack_fc(x, [c.weight for c in convs], [c.bias for c in convs],
+                                          [c.stride[0] for c in convs], lin.weight, lin.bias, in_scale)
         y = conv_ops.conv_stack(x, [c.weight for c in convs], [c.bias for c in convs], [c.stride[0] for c in convs],
                                 in_scale)
         y = y.permute(0, 3, 1, 2).reshape(y.shape[0], -1)  # nn.Flatten order (C, H, W)

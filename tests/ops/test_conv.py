@@ -182,3 +182,61 @@ def test_same_padding_stack_matches_reference(cin, B, H, W):
     for g, r in zip(grads, ref_grads):
         cos = float((g * r).sum() / (g.norm() * r.norm() + 1e-12))
         assert cos > 0.99, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [32, 1, 70])
+def test_conv_stack_fc_matches_reference(B):
+    """NatureCNN extractor as one node (convs + NHWC FC on cnn_fc / fc_backward) vs the fp32
+    torch modules: output and every parameter gradient to bf16-operand accuracy, uint8 input
+    with the 1/255 folded in."""
+    from imitation_amd.ops import conv as conv_ops
+
+    g = th.Generator().manual_seed(B)
+    convs = [th.nn.Conv2d(4, 32, 8, 4), th.nn.Conv2d(32, 64, 4, 2), th.nn.Conv2d(64, 64, 3, 1)]
+    fc = th.nn.Linear(3136, 512)
+    mods = th.nn.ModuleList(convs + [fc]).cuda()
+    x = th.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=th.uint8).cuda()
+    ws, bs, st = [c.weight for c in convs], [c.bias for c in convs], [4, 2, 1]
+    assert conv_ops.fc_supported(tuple(x.shape), ws, st, 512)
+    wg = th.randn(B, 512, generator=g).cuda()
+    y = conv_ops.conv_stack_fc(x, ws, bs, st, fc.weight, fc.bias, 1.0 / 255.0)
+    gk = th.autograd.grad((y * wg).sum(), list(mods.parameters()))
+    yr = x.float().permute(0, 3, 1, 2) / 255.0
+    for c in convs:
+        yr = th.relu(c(yr))
+    yr = th.relu(fc(yr.reshape(B, -1)))
+    gr = th.autograd.grad((yr * wg).sum(), list(mods.parameters()))
+    assert float((y - yr).norm() / yr.norm()) < 1e-2
+    for a, b in zip(gk, gr):  # cosine: ReLU masks flipped by bf16 dominate the difference (see above)
+        assert a.shape == b.shape
+        cos = float((a * b).sum() / (a.norm() * b.norm() + 1e-12))
+        assert cos > 0.98, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [32, 1, 70])
+def test_fc_backward_kernel_exact_wrt_bf16_operands(M):
+    """fc_backward (csrc/kernels/cnn_fc.hip) against fp64 math on the same bf16 operands:
+    dW in torch's (c, h, w) column order, db, dX in NHWC order."""
+    from imitation_amd import ops
+
+    C = ops.native()
+    g = th.Generator().manual_seed(M)
+    C3, H3, W3, NH = 64, 7, 7, 512
+    K = C3 * H3 * W3
+    x = th.randn(M, H3, W3, C3, generator=g).to(th.bfloat16)
+    w = th.randn(NH, C3, H3, W3, generator=g) * 0.02
+    h = th.relu(th.randn(M, NH, generator=g))
+    dh = th.randn(M, NH, generator=g)
+    _, wts = C.conv_pack_weights([w.cuda()], [True], [True])
+    dW, db, dx = C.fc_backward(x.cuda().reshape(M, -1), dh.cuda(), h.cuda(), wts[0], C3, True)
+    dz = (dh * (h > 0)).to(th.bfloat16).double()
+    xd = x.double()
+    dW_ref = dz.T @ xd.reshape(M, -1)                                     # NHWC columns
+    dW_ref = dW_ref.view(NH, H3, W3, C3).permute(0, 3, 1, 2).reshape(NH, K)  # -> torch (c, h, w)
+    th.testing.assert_close(dW.cpu().double(), dW_ref, rtol=1e-4, atol=1e-4)
+    th.testing.assert_close(db.cpu().double(), (dh * (h > 0)).double().sum(0), rtol=1e-5, atol=1e-5)
+    wb = w.to(th.bfloat16).double().permute(0, 2, 3, 1).reshape(NH, K)     # (h, w, c) columns
+    dx_ref = dz @ wb
+    assert float((dx.cpu().double() - dx_ref).norm() / dx_ref.norm()) < 5e-3

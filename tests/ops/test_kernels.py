@@ -276,11 +276,18 @@ def test_bc_categorical_loss_kernel_matches_reference(B, A, n):
     (ref * wg).sum().backward()
     zg = z.cuda().requires_grad_(True)
     fc = flat.cuda()
-    got = rl_ops.bc_categorical_loss(zg, a.cuda(), [fc[: n // 3], fc[n // 3:]], 1e-3, 0.0, flat=fc)
+    got, loss = rl_ops.bc_categorical_loss(zg, a.cuda(), [fc[: n // 3], fc[n // 3:]], 1e-3, 0.0, flat=fc)
     assert got.grad_fn is not None and "BCCategorical" in type(got.grad_fn).__name__
-    (got * wg.float().cuda()).sum().backward()
+    (got * wg.float().cuda()).sum().backward(retain_graph=True)
     th.testing.assert_close(got.double().cpu(), ref.detach(), rtol=2e-5, atol=1e-5)
     th.testing.assert_close(zg.grad.double().cpu(), zr.grad, rtol=1e-4, atol=1e-6)
+    # the separate loss output alone (what BC backpropagates)
+    th.testing.assert_close(float(loss), float(got[6]))
+    zg.grad = None
+    loss.backward()
+    zr2 = z.double().requires_grad_(True)
+    rl_ops.bc_categorical_loss_reference(zr2, a, [p.double() for p in params], 1e-3, 0.0)[6].backward()
+    th.testing.assert_close(zg.grad.double().cpu(), zr2.grad, rtol=1e-4, atol=1e-7)
 
 
 @gpu
