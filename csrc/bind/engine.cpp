@@ -212,6 +212,7 @@ void ppo_update(py::dict d) {
   a.mb_index = ival(d, "mb_index", 0);
   a.prof = tptr<unsigned long long>(d, "prof", true);
   a.rc_gmax = ival(d, "rc_gmax", 0);
+  a.rc_cw = ival(d, "rc_cw", 0);
   TORCH_CHECK(a.D <= 64, "obs dim <= 64");
   ia::PPORcGeo geo;
   size_t rc_lds = 0;
@@ -240,6 +241,7 @@ std::string ppo_path(py::dict d) {
   a.rows = ival(d, "rows");
   a.log_std_off = ival(d, "log_std_off", -1);
   a.rc_gmax = ival(d, "rc_gmax", 0);
+  a.rc_cw = ival(d, "rc_cw", 0);
   ia::PPORcGeo geo;
   size_t lds = 0;
   if (ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, lds))

@@ -159,7 +159,8 @@ struct PPOArgs {
   int mode;  // 0: full persistent update; 1: one minibatch -> grads only; 2: apply clip+Adam from grads
   int mb_index;  // minibatch index for mode 1 (epoch * n_mb + mb)
   unsigned long long* prof;  // optional [10] cycle counters per phase
-  int rc_gmax;   // mode 0 fast path: max cooperating workgroups per minibatch (0 = default 8)
+  int rc_gmax;   // mode 0 fast path: max cooperating workgroups per minibatch (0 = default 16)
+  int rc_cw;     // mode 0 fast path: rows per chunk override (0 = 64 for <= 32-wide nets, 32 otherwise)
 };
 
 // Geometry + workspace of the register-chained PPO kernel (ppo_rc.hip), planned on the host.

@@ -1117,12 +1117,13 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   const int KT = g.kt;
   // workgroup split: chunks of cw rows (64 for narrow nets, 32 for 64-wide ones: LDS)
   int cw = KT == 2 ? 64 : 32;
+  if (a.rc_cw == 16 || a.rc_cw == 32 || (a.rc_cw == 64 && KT == 2)) cw = a.rc_cw;
   if (a.batch < cw) cw = a.batch;
   if (a.batch % cw != 0) {
     cw = 16;
   }
   const int chunks = a.batch / cw;
-  const int gmax = a.rc_gmax > 0 ? (a.rc_gmax < kMaxRcGroups ? a.rc_gmax : kMaxRcGroups) : 8;
+  const int gmax = a.rc_gmax > 0 ? (a.rc_gmax < kMaxRcGroups ? a.rc_gmax : kMaxRcGroups) : kMaxRcGroups;
   int G = 1;
   for (int c = gmax; c >= 1; --c)
     if (chunks % c == 0) {

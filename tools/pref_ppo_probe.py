@@ -1,5 +1,6 @@
-"""DRLHP agent PPO update (MlpPolicy 64x64 ReLU, batch 128, 20 epochs, 8192 rows) per PPO
-kernel geometry: rc_gmax = cooperating workgroups per minibatch."""
+"""Device-engine PPO update per kernel geometry (rc_gmax = cooperating workgroups per
+minibatch): the DRLHP agent (MlpPolicy 64x64 ReLU, batch 128, 20 epochs, 8192 rows) or, with
+RECIPE=airl_hopper, the AIRL-Hopper generator (batch 512)."""
 import os
 import sys
 import time
@@ -12,11 +13,13 @@ import torch as th  # noqa: E402
 def main():
     from imitation_amd import models
 
-    b = models.build("preference_walker2d", device=th.device("cuda"), seed=0)
-    ag = b.trainer.trajectory_generator
+    recipe = os.environ.get("RECIPE", "preference_walker2d")
+    b = models.build(recipe, device=th.device("cuda"), seed=0)
+    ag = b.trainer.trajectory_generator if recipe == "preference_walker2d" else b.trainer
     ag._rollout()
-    for g in [int(x) for x in os.environ.get("GMAX", "1,2,4,8").split(",")]:
+    for g in [int(x) for x in os.environ.get("GMAX", "1,2,4,8,16").split(",")]:
         ag._ppo_static["rc_gmax"] = g
+        ag._ppo_static["rc_cw"] = int(os.environ.get("RC_CW", "0"))
         path = ag._C.engine_ppo_path(ag._ppo_static)
         ag._ppo_update()
         th.cuda.synchronize()
