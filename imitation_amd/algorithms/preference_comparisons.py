@@ -762,7 +762,24 @@ class BasicRewardTrainer(RewardTrainer):
                s_all.dtype, a_all.dtype, gt is not None, s_all.device)
         g = getattr(self, "_mb_graph", None)
         if g is None or g.key != key or g.capacity < P:
+            # capacity doubling, capped by what fits in half of the free HBM (an MI355X holds
+            # tens of millions of Walker fragment pairs): the store never overshoots into OOM
             cap = 1 << max(0, (P - 1).bit_length())
+            if s_all.is_cuda:
+                from imitation_amd.data.buffer import hbm_capacity
+
+                per_pair = 2 * L * sum(t[:1].numel() * t.element_size() for t in (s_all, a_all, ns_all, d_all)) + 4
+                if g is not None:  # the old store is released before the new one is allocated
+                    per_free = g.capacity * per_pair
+                else:
+                    per_free = 0
+                fits = hbm_capacity(per_pair, fraction=0.5, device=s_all.device,
+                                    free_bytes=th.cuda.mem_get_info(s_all.device)[0] + per_free)
+                if fits < P:
+                    raise MemoryError(f"{P} preference pairs need {P * per_pair / 2**30:.1f} GiB; "
+                                      f"half the free HBM holds {fits}")
+                cap = max(P, min(cap, fits))
+            self._mb_graph = g = None
             g = _MinibatchGraph(self, key, cap, s_all, a_all, ns_all, d_all, gt is not None, L, B)
             self._mb_graph = g
         g.load(s_all, a_all, ns_all, d_all, prefs_all, gt, P)
