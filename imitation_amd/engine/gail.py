@@ -836,15 +836,26 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         buffer by ``g_idx``); returns the last minibatch's statistics sums (device)."""
         import torch.nn.functional as F
 
+        from imitation_amd.ops import optim as optim_ops
+        from imitation_amd.ops.rl import gather_rows
+
         ga = self._gen_dev._arrays
-        gen = {k: ga[k].index_select(0, g_idx) for k in ("obs", "acts", "next_obs", "dones")}
+        keys = ("obs", "acts", "next_obs", "dones")
+        gen = dict(zip(keys, gather_rows([ga[k] for k in keys], g_idx)))  # one launch
         ex = {"obs": e_obs, "acts": e_acts, "next_obs": e_next, "dones": e_dones}
+        # a single minibatch per update (the tuned configs): its gradients go straight into
+        # FusedAdam's (zeroed) bucket, no accumulate-add per parameter
+        into_buckets = (isinstance(self._disc_opt, optim_ops.FusedAdam)
+                        and self.demo_minibatch_size == self.demo_batch_size)
         for batch in self._make_disc_train_batches(gen_samples=gen, expert_samples=ex):
             logits = self.logits_expert_is_high(batch["state"], batch["action"], batch["next_state"], batch["done"],
                                                 batch["log_policy_act_prob"])
             loss = F.binary_cross_entropy_with_logits(logits, batch["labels_expert_is_one"].float())
             loss = loss * (self.demo_minibatch_size / self.demo_batch_size)
-            loss.backward()
+            if into_buckets:
+                self._disc_opt.backward_into_buckets(loss)
+            else:
+                loss.backward()
         self._disc_opt.step()
         return common.train_stats_vec(logits, batch["labels_expert_is_one"], loss)
 
@@ -854,6 +865,11 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         if self._gen_dev.size() == 0:
             raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
         if getattr(self, "_disc_graph", None) is None:
+            # torch Adam's capturable step is ~30 multi-tensor launches; the flat-bucket
+            # FusedAdam (same hyper-parameters and state) is one
+            from imitation_amd.ops import optim as optim_ops
+
+            self._disc_opt = optim_ops.to_fused(self._disc_opt)
             self._disc_graph = graphs.GraphedTrainStep(self._generic_disc_fn, self._disc_opt)
         ex = self._next_expert_batch()
         g_idx = th.randint(0, self._gen_dev.size(), (self.demo_batch_size,), device=self._dev)

@@ -226,3 +226,24 @@ def fused_for(optimizer_cls, device) -> Optional[type]:
     if optimizer_cls is th.optim.AdamW:
         return FusedAdamW
     return None
+
+
+def to_fused(optimizer: th.optim.Optimizer) -> th.optim.Optimizer:
+    """Swap a single-group ``th.optim.Adam`` / ``AdamW`` on a GPU for its fused equivalent over
+    the same parameters, hyper-parameters and (torch-layout) state; anything else is
+    returned unchanged. Call before any graph or kernel descriptor captured the parameters'
+    storage (the fused optimiser re-points them into its flat bucket)."""
+    if len(optimizer.param_groups) != 1:
+        return optimizer
+    g = optimizer.param_groups[0]
+    params = list(g["params"])
+    if not params or g.get("amsgrad", False) or g.get("differentiable", False):
+        return optimizer
+    cls = fused_for(type(optimizer), params[0].device)
+    if cls is None:
+        return optimizer
+    new = cls(params, lr=g["lr"], betas=g["betas"], eps=g["eps"], weight_decay=g["weight_decay"],
+              maximize=g.get("maximize", False))
+    if optimizer.state:
+        new.load_state_dict(optimizer.state_dict())
+    return new
