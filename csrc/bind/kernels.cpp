@@ -396,6 +396,29 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
   return outs;
 }
 
+// RunningNorm: (optionally) merge x's moments into mean / var / count in place, and return
+// the normalised x (or None with want_y = false)
+py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, torch::Tensor count, double eps,
+                        bool update, bool want_y) {
+  IA_CHECK_GPU_F32(x);
+  IA_CHECK_CONTIG(x);
+  IA_CHECK_GPU_F32(mean);
+  IA_CHECK_GPU_F32(var);
+  IA_CHECK_CONTIG(mean);
+  IA_CHECK_CONTIG(var);
+  IA_CHECK_CUDA(count);
+  TORCH_CHECK(count.scalar_type() == torch::kInt32 && count.numel() == 1, "running_norm: int32 scalar count");
+  TORCH_CHECK(x.dim() == 2 && mean.numel() == x.size(1) && var.numel() == x.size(1), "running_norm: x [B, D]");
+  const int B = (int)x.size(0), D = (int)x.size(1);
+  TORCH_CHECK(ia::running_norm_ok(B, D), "running_norm: B * D <= 2^20, D <= 256");
+  torch::Tensor y;
+  if (want_y) y = torch::empty_like(x);
+  IA_HIP_CHECK(ia::running_norm(x.data_ptr<float>(), B, D, mean.data_ptr<float>(), var.data_ptr<float>(),
+                                count.data_ptr<int>(), (float)eps, update ? 1 : 0, want_y ? y.data_ptr<float>() : nullptr,
+                                ia_stream()));
+  return want_y ? py::cast(y) : py::none();
+}
+
 // [E, n] int32: row e is a pseudo-random permutation of 0..n-1 keyed by (seed, e).
 torch::Tensor random_permutations(int64_t E, int64_t n, int64_t seed, torch::Device device) {
   TORCH_CHECK(device.is_cuda(), "random_permutations runs on the GPU");
@@ -458,6 +481,8 @@ void register_kernels(py::module& m) {
         py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
         py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"));
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
+  m.def("running_norm", &running_norm, py::arg("x"), py::arg("mean"), py::arg("var"), py::arg("count"), py::arg("eps"),
+        py::arg("update"), py::arg("want_y"));
   m.def("gather_rows", &gather_rows, py::arg("srcs"), py::arg("b"), py::arg("e") = py::none(), py::arg("n_envs") = 1);
   m.def("soft_value_iteration", &soft_value_iteration, py::arg("T"), py::arg("R"), py::arg("H"), py::arg("gamma"));
   m.def("occupancy_measures", &occupancy_measures, py::arg("T"), py::arg("P"), py::arg("D0"));
