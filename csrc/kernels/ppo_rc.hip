@@ -1254,6 +1254,7 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   hipLaunchKernelGGL((ppo_rc_kernel<KT, KI, S0, NL, ACT, HW, CW, DT>), grid, block, lds_launch, s, a, g)
   if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete)
     IA_RC(2, 4, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
+
   else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)
     IA_RC(4, 8, 3, 3, 1, 64, 32, 0);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
   else if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)

@@ -25,7 +25,7 @@ def main():
     from imitation_amd.util.networks import RunningNorm
     from imitation_amd.util.util import make_vec_env
 
-    for W in (1, 2, 4, 8):
+    for W in [int(w) for w in os.environ.get("WS", "1,2,4,8").split(",")]:
         rng = np.random.default_rng(0)
         venv = make_vec_env("seals/HalfCheetah-v1", rng=rng, n_envs=8 * W)
         demo_env = make_vec_env("seals/HalfCheetah-v1", rng=np.random.default_rng(7), n_envs=4)
@@ -35,6 +35,7 @@ def main():
         rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
         tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, venv=venv, gen_algo=gen, reward_net=rn,
                         n_disc_updates_per_round=1, custom_logger=logger.configure("/tmp/ia_probe", format_strs=[]))
+        tr._ppo_static["rc_cw"] = int(os.environ.get("RC_CW", "0"))
         path = tr._C.engine_ppo_path(tr._ppo_static)
         tr._rollout()
         for _ in range(2):
