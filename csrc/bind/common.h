@@ -22,3 +22,4 @@ void register_kernels(py::module& m);
 void register_engine(py::module& m);
 void register_disc(py::module& m);
 void register_conv(py::module& m);
+void register_comm(py::module& m);

@@ -9,4 +9,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_engine(m);
   register_disc(m);
   register_conv(m);
+  register_comm(m);
 }

@@ -264,4 +264,28 @@ hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y,
 hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
                       int relu_out, int relu_in, hipStream_t s);
 
+// ---- comm.hip: one-shot all-reduce over IPC-mapped peer staging regions (small DP buckets)
+constexpr int kOneShotMaxRanks = 8;
+constexpr int kOneShotMaxBlocks = 64;
+struct OneShotArgs {
+  char* base[kOneShotMaxRanks];  // every rank's region as mapped in this process (base[rank] local)
+  const float* in;               // 16-B aligned
+  float* out;                    // 16-B aligned, may alias in
+  int n, rank, world;
+  float scale;                   // applied to this rank's contribution before the sum
+  size_t stage_bytes;
+  long long timeout_ticks;       // wall-clock ticks before a block gives up (NaN output + error word)
+};
+size_t oneshot_region_bytes(size_t stage_bytes);
+size_t oneshot_handle_bytes();
+int oneshot_blocks(int n);
+hipError_t oneshot_alloc(size_t stage_bytes, void** ptr, void* handle);  // zeroed uncached region + IPC handle
+hipError_t oneshot_open(const void* handle, void** ptr);
+hipError_t oneshot_close(void* ptr);
+hipError_t oneshot_free(void* ptr);
+hipError_t oneshot_read_error(void* local, int* err);
+hipError_t oneshot_clear_error(void* local);
+long long oneshot_ticks_per_second();
+hipError_t oneshot_allreduce(const OneShotArgs& a, hipStream_t s);
+
 }  // namespace ia

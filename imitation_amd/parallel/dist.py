@@ -16,6 +16,9 @@ adds the collectives the MI355X build needs, at the hook points listed there:
   preference fragments): counts first, then one padded ``all_gather_into_tensor``.
 * :func:`broadcast_module` -- initial parameters/buffers from rank 0.
 * :func:`allreduce_scalars` -- eval statistics.
+* small fp32 buckets (gradients, moment sums; <= 256 KiB) go through the one-shot
+  IPC all-reduce kernel of :mod:`imitation_amd.parallel.oneshot` when it is available
+  (one xGMI hop instead of RCCL's 2(W-1)-hop ring), everything else through RCCL.
 """
 
 from __future__ import annotations
@@ -73,12 +76,26 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> Tuple[int, 
     if backend == "nccl":
         kwargs["device_id"] = torch.device("cuda", local_rank())
     tdist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kwargs)
+    from imitation_amd.parallel import oneshot
+
+    oneshot.get()  # collective set-up of the small-bucket path at a point every rank reaches
     return rank(), world_size()
 
 
 def shutdown() -> None:
     if is_initialized():
+        from imitation_amd.parallel import oneshot
+
+        oneshot.reset()
         tdist.destroy_process_group()
+
+
+def _oneshot_for(t: torch.Tensor):
+    """The one-shot communicator if it can reduce ``t`` (fp32, contiguous, on this GPU, small)."""
+    from imitation_amd.parallel import oneshot
+
+    c = oneshot._COMM
+    return c if c is not None and c.fits(t) else None
 
 
 def barrier() -> None:
@@ -183,6 +200,10 @@ class GradBucket:
         if self.flat is None or world_size() <= 1:
             return
         self.bind()
+        c = _oneshot_for(self.flat)
+        if c is not None:
+            c.allreduce_(self.flat, 1.0 / world_size())
+            return
         self.flat.mul_(1.0 / world_size())
         buf = _comm_device(self.flat)
         tdist.all_reduce(buf)
@@ -237,6 +258,10 @@ def allreduce_sum_(t: torch.Tensor) -> None:
     """Sum all-reduce of ``t`` in place (one collective; no-op on one rank)."""
     if world_size() <= 1:
         return
+    c = _oneshot_for(t)
+    if c is not None:
+        c.allreduce_(t)
+        return
     buf = _comm_device(t)
     tdist.all_reduce(buf)
     if buf is not t:
@@ -246,6 +271,10 @@ def allreduce_sum_(t: torch.Tensor) -> None:
 def allreduce_grads_flat(flat: torch.Tensor) -> None:
     """Mean all-reduce of one flat gradient vector in place (one collective)."""
     if world_size() <= 1:
+        return
+    c = _oneshot_for(flat)
+    if c is not None:
+        c.allreduce_(flat, 1.0 / world_size())
         return
     flat.mul_(1.0 / world_size())
     buf = _comm_device(flat)

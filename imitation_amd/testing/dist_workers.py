@@ -215,3 +215,102 @@ def dagger_dp_worker(rank, world, scratch, seed):
     return dict(params=[p.detach().numpy().copy() for p in tr.policy.parameters()], round_num=tr.round_num,
                 n_demos=len(tr._all_demos), local_files=local_files, scratch=str(tr.scratch_dir),
                 last=tr.last_train_timesteps, local=tr.last_train_timesteps_local)
+
+
+def oneshot_worker(rank, world, sizes, scale, seed):
+    """One-shot all-reduce (``parallel/oneshot.py``) on ``cuda:0`` shared by the ranks:
+    rank-seeded buckets reduced eagerly and from a captured HIP graph, plus the latency
+    of a small bucket. Returns this rank's results for the parent to check."""
+    import time
+
+    from imitation_amd.parallel import oneshot
+
+    c = oneshot.get()
+    assert c is not None, "one-shot path not set up"
+    dev = c.device
+    out = {"eager": [], "graph": []}
+    for n in sizes:
+        x = th.as_tensor(np.random.default_rng(seed * 100 + rank * 7 + n).normal(size=n).astype(np.float32), device=dev)
+        c.allreduce_(x, scale)
+        out["eager"].append(x.cpu().numpy())
+    # graph-captured launch: the generation counter lives on the device, so replays stay in step
+    buf = th.zeros(sizes[-1], device=dev)
+    side = th.cuda.Stream(device=dev)
+    side.wait_stream(th.cuda.current_stream(dev))
+    g = th.cuda.CUDAGraph()
+    with th.cuda.stream(side):
+        with th.cuda.graph(g, stream=side):
+            c.allreduce_(buf, scale)
+    th.cuda.current_stream(dev).wait_stream(side)
+    for rep in range(3):
+        buf.copy_(th.as_tensor(np.random.default_rng(seed * 100 + rank * 7 + 1000 + rep).normal(size=buf.numel()).astype(np.float32)))
+        g.replay()
+        out["graph"].append(buf.cpu().numpy())
+    small = th.ones(1024, device=dev)
+    for _ in range(20):
+        c.allreduce_(small)
+    th.cuda.synchronize(dev)
+    from imitation_amd.parallel import dist as pdist
+
+    pdist.barrier()
+    iters = 200
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        c.allreduce_(small, 1.0 / world)
+    th.cuda.synchronize(dev)
+    out["us_per_call_4KB"] = (time.perf_counter() - t0) / iters * 1e6
+    out["error"] = c.error()
+    return out
+
+
+def oneshot_timeout_worker(rank, world, timeout_s):
+    """Rank 0 reduces while rank 1 never joins: the bounded wait must give up, write NaN and
+    raise the error word instead of hanging the GPU."""
+    from imitation_amd.parallel import oneshot
+
+    c = oneshot.get()
+    assert c is not None
+    res = {}
+    if rank == 0:
+        c.timeout_s = timeout_s
+        x = th.ones(4096 + 3, device=c.device)
+        c.allreduce_(x)
+        th.cuda.synchronize(c.device)
+        res = {"all_nan": bool(th.isnan(x).all().item()), "error": c.error()}
+    from imitation_amd.parallel import dist as pdist
+
+    pdist.barrier()
+    return res
+
+
+def gail_round_worker(rank, world, seed):
+    """One fused-discriminator DeviceGAIL round on ``cuda:0`` shared by the ranks (gloo group);
+    returns the reward-net and policy parameters and how many one-shot all-reduces ran."""
+    from imitation_amd.data import rollout
+    from imitation_amd.engine.gail import DeviceGAIL
+    from imitation_amd.parallel import oneshot
+    from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
+    from imitation_amd.rewards.reward_nets import BasicRewardNet, NormalizedRewardNet
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.util import logger
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    th.manual_seed(seed + rank)
+    np.random.seed(seed + rank)
+    rng = np.random.default_rng(seed + rank)
+    venv = make_vec_env("seals/HalfCheetah-v1", rng=rng, n_envs=4)
+    demo_env = make_vec_env("seals/HalfCheetah-v1", rng=np.random.default_rng(7), n_envs=4)
+    demo_env.action_space.seed(11 + rank)  # random-policy demos: reproducible across runs
+    demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(512), rng=rng))
+    gen = PPO(FeedForward32Policy, venv, n_steps=32, batch_size=64, n_epochs=2, device="cuda", seed=seed,
+              ent_coef=0.01, policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+    rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
+    tr = DeviceGAIL(demonstrations=demos, demo_batch_size=128, venv=venv, gen_algo=gen, reward_net=rn,
+                    n_disc_updates_per_round=2, custom_logger=logger.configure(f"/tmp/ia_dp_round_{rank}", format_strs=[]))
+    tr.train(tr.gen_train_timesteps)
+    th.cuda.synchronize()
+    c = oneshot._COMM
+    return {"reward": [p.detach().cpu().numpy().copy() for p in rn.parameters()],
+            "policy": [p.detach().cpu().numpy().copy() for p in gen.policy.parameters()],
+            "oneshot_calls": 0 if c is None else c.calls}
