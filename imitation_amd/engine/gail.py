@@ -825,7 +825,10 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         device demo sampler, and no per-step tensorboard summaries (a host sync)."""
         from imitation_amd.utils import graphs
 
-        return (not self._fused_disc and pdist.world_size() == 1 and self._disc_bucket is None
+        # under DP the gradient mean and the normaliser moments go through the one-shot
+        # all-reduce kernel, which a graph can hold (RCCL / gloo collectives cannot)
+        single = pdist.world_size() == 1 and self._disc_bucket is None
+        return (not self._fused_disc and (single or pdist.oneshot_active())
                 and graphs.graphs_enabled(self._dev, "IMITATION_AMD_DISC_GRAPH")
                 and graphs.supports_capture(self._disc_opt) and not self._init_tensorboard
                 and isinstance(self._endless_expert_iterator, common._DeviceDemoSampler))
@@ -856,6 +859,8 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 self._disc_opt.backward_into_buckets(loss)
             else:
                 loss.backward()
+        if pdist.world_size() > 1:  # mean over ranks of the flat bucket(s): one-shot, in-graph
+            pdist.FlatGradBucket(self._disc_opt).allreduce()
         self._disc_opt.step()
         return common.train_stats_vec(logits, batch["labels_expert_is_one"], loss)
 

@@ -146,6 +146,44 @@ def allreduce_moments(batch: torch.Tensor):
     return mean.to(batch.dtype).reshape(shape), var.to(batch.dtype).reshape(shape), int(count.item())
 
 
+def allreduce_moments_device(batch: torch.Tensor):
+    """Capture-safe variant of :func:`allreduce_moments` on the one-shot path: every rank
+    puts its (count, mean, centred M2) in its own row of a zero ``[world, 2F + 1]`` fp32
+    message, one sum all-reduce hands every rank all rows exactly (adding zeros is exact),
+    and the rows are Chan-merged on the device in rank order -- no host sync, the count
+    comes back as an int32 device tensor. None when the one-shot path cannot take it."""
+    if world_size() <= 1 or not batch.is_cuda:
+        return None
+    from imitation_amd.parallel import oneshot
+
+    c = oneshot._COMM
+    b = batch.reshape(batch.shape[0], -1).float()
+    f = b.shape[1]
+    if c is None or world_size() * (2 * f + 1) * 4 > c.stage_bytes or b.device != c.device:
+        return None
+    mean_r = b.mean(0)
+    m2_r = (b - mean_r).square().sum(0)
+    msg = torch.zeros(world_size(), 2 * f + 1, dtype=torch.float32, device=b.device)
+    # device-side fills / copies only (a Python-scalar setitem is a host->device copy,
+    # which a capturing stream refuses)
+    msg[rank()].copy_(torch.cat([b.new_full((1,), float(b.shape[0])), mean_r, m2_r]))
+    c.allreduce_(msg)
+    n_r = msg[:, :1]
+    n = n_r.sum()
+    mean = (n_r * msg[:, 1 : 1 + f]).sum(0) / n
+    m2 = msg[:, 1 + f :].sum(0) + (n_r * (msg[:, 1 : 1 + f] - mean).square()).sum(0)
+    shape = batch.shape[1:]
+    return (mean.to(batch.dtype).reshape(shape), (m2 / n).to(batch.dtype).reshape(shape),
+            n.round().to(torch.int32))
+
+
+def oneshot_active() -> bool:
+    """True when small fp32 collectives run on the (graph-capturable) one-shot kernel."""
+    from imitation_amd.parallel import oneshot
+
+    return world_size() > 1 and oneshot._COMM is not None
+
+
 def allreduce_scalars(values: Sequence[float], op: str = "sum", device=None) -> List[float]:
     if not is_initialized():
         return list(values)

@@ -314,3 +314,42 @@ def gail_round_worker(rank, world, seed):
     return {"reward": [p.detach().cpu().numpy().copy() for p in rn.parameters()],
             "policy": [p.detach().cpu().numpy().copy() for p in gen.policy.parameters()],
             "oneshot_calls": 0 if c is None else c.calls}
+
+
+def airl_round_worker(rank, world, seed):
+    """One DeviceAIRL round (shaped reward net, generic autograd discriminator update) on
+    ``cuda:0`` shared by the ranks; reports whether the update ran as a HIP-graph replay."""
+    from imitation_amd.data import rollout
+    from imitation_amd.engine.airl import DeviceAIRL
+    from imitation_amd.parallel import oneshot
+    from imitation_amd.policies.base import NormalizeFeaturesExtractor
+    from imitation_amd.rewards.reward_nets import BasicShapedRewardNet, NormalizedRewardNet
+    from imitation_amd.rl.policies import ActorCriticPolicy
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.util import logger
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    th.manual_seed(seed + rank)
+    np.random.seed(seed + rank)
+    rng = np.random.default_rng(seed + rank)
+    venv = make_vec_env("seals/Hopper-v1", rng=rng, n_envs=4)
+    demo_env = make_vec_env("seals/Hopper-v1", rng=np.random.default_rng(7), n_envs=4)
+    demo_env.action_space.seed(7 + rank)
+    demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
+    gen = PPO(ActorCriticPolicy, venv, n_steps=64, batch_size=64, n_epochs=2, device="cuda", seed=seed,
+              policy_kwargs=dict(net_arch=dict(pi=[64, 64], vf=[64, 64]), activation_fn=th.nn.ReLU,
+                                 features_extractor_class=NormalizeFeaturesExtractor))
+    rn = NormalizedRewardNet(BasicShapedRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm),
+                             RunningNorm)
+    tr = DeviceAIRL(demonstrations=demos, demo_batch_size=256, venv=venv, gen_algo=gen, reward_net=rn,
+                    n_disc_updates_per_round=3, custom_logger=logger.configure(f"/tmp/ia_dp_airl_{rank}", format_strs=[]))
+    graphed = tr._graphed_disc_ok()
+    tr.train(tr.gen_train_timesteps)
+    th.cuda.synchronize()
+    c = oneshot._COMM
+    g = getattr(tr, "_disc_graph", None)
+    return {"reward": [p.detach().cpu().numpy().copy() for p in rn.parameters()],
+            "norm": [b.detach().cpu().numpy().copy() for b in rn.buffers()],
+            "graphed": graphed, "replays": 0 if g is None else g.n_replays,
+            "oneshot_calls": 0 if c is None else c.calls}

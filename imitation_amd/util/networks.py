@@ -64,7 +64,8 @@ def _global_batch_moments(batch: th.Tensor):
 
     n = batch.shape[0]
     if pdist.norm_sync_active():
-        return pdist.allreduce_moments(batch)
+        out = pdist.allreduce_moments_device(batch)  # one-shot path: no host sync, capturable
+        return out if out is not None else pdist.allreduce_moments(batch)
     return th.mean(batch, dim=0), th.var(batch, dim=0, unbiased=False), n
 
 

@@ -63,3 +63,24 @@ def test_gail_round_oneshot_equals_gloo(monkeypatch):
             np.testing.assert_array_equal(a, b)
         for a, b in zip(one[0][key], ref[0][key]):
             np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_airl_dp_discriminator_graphed_on_oneshot(monkeypatch):
+    """Under DP the generic (AIRL) discriminator update is a HIP-graph replay holding the
+    one-shot gradient mean and normaliser moments; replicas stay bit-identical and track the
+    eager gloo path (fp64 moments there, fp32 Chan merge here)."""
+    monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", "1")
+    one = run_ranks(W.airl_round_worker, 2, 3, timeout=300)
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", "0")
+    ref = run_ranks(W.airl_round_worker, 2, 3, timeout=300)
+    assert one[0]["graphed"] and one[0]["replays"] >= 2 and one[0]["oneshot_calls"] > 0
+    assert not ref[0]["graphed"]
+    for key in ("reward", "norm"):
+        for a, b in zip(one[0][key], one[1][key]):
+            np.testing.assert_array_equal(a, b)
+    for a, b in zip(one[0]["norm"], ref[0]["norm"]):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    for a, b in zip(one[0]["reward"], ref[0]["reward"]):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=5e-3)
