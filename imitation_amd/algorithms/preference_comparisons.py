@@ -646,6 +646,16 @@ class BasicRewardTrainer(RewardTrainer):
                 pdist.allreduce_grads(self._preference_model.parameters())
         self.optim.step()
 
+    def _dp_graph_ok(self) -> bool:
+        """Under DP the graphed minibatch holds its gradient mean (and the RunningNorm
+        moments) only on the capturable one-shot all-reduce: FusedAdam's flat buckets must
+        fit its staging slot (RCCL / gloo collectives cannot be captured)."""
+        if not (pdist.oneshot_active() and isinstance(self.optim, optim_ops.FusedAdam)):
+            return False
+        from imitation_amd.parallel import oneshot
+
+        return all(oneshot._COMM.fits(f) for f in self.optim.flat_grads)
+
     def _shuffle_seed(self) -> int:
         """Seed of this epoch set's minibatch order; rank 0's under DP, so every replica walks
         the (identical, all-gathered) dataset in the same order."""
@@ -704,8 +714,8 @@ class BasicRewardTrainer(RewardTrainer):
         world, rank = pdist.world_size(), pdist.rank()
         G = B * world
         graph = None
-        if (dev.type == "cuda" and self.minibatch_size == self.batch_size and self.regularizer is None and world == 1
-                and os.environ.get("IMITATION_AMD_PREF_GRAPH", "1") != "0"):
+        if (dev.type == "cuda" and self.minibatch_size == self.batch_size and self.regularizer is None
+                and (world == 1 or self._dp_graph_ok()) and os.environ.get("IMITATION_AMD_PREF_GRAPH", "1") != "0"):
             graph = self._minibatch_graph(s_all, a_all, ns_all, d_all, prefs_all, gt, P, L, B)
         epoch_num = 0
         with self.logger.accumulate_means("reward"):
@@ -908,7 +918,7 @@ class _MinibatchGraph:
             gp = pref_ops.bradley_terry_probs_reference(g[:, 0], g[:, 1], pm.discount_factor, pm.threshold, pm.noise_prob)
             rec.append(th.nn.functional.binary_cross_entropy(gp, prefs))
         (loss * (n / tr.batch_size)).backward()
-        tr.optim.step()
+        tr._optimizer_step()  # under DP: the one-shot gradient mean, captured with the step
         return th.stack(rec)
 
     def run(self, idx: th.Tensor) -> th.Tensor:

@@ -16,7 +16,7 @@ adds the collectives the MI355X build needs, at the hook points listed there:
   preference fragments): counts first, then one padded ``all_gather_into_tensor``.
 * :func:`broadcast_module` -- initial parameters/buffers from rank 0.
 * :func:`allreduce_scalars` -- eval statistics.
-* small fp32 buckets (gradients, moment sums; <= 256 KiB) go through the one-shot
+* small fp32 buckets (gradients, moment sums; <= 1 MiB) go through the one-shot
   IPC all-reduce kernel of :mod:`imitation_amd.parallel.oneshot` when it is available
   (one xGMI hop instead of RCCL's 2(W-1)-hop ring), everything else through RCCL.
 """

@@ -15,7 +15,7 @@ Selection (``IMITATION_AMD_ONESHOT``):
 * ``1`` -- also on under gloo with ranks sharing one GPU (the one-card rehearsal path);
 * ``0`` -- off (every collective goes to torch.distributed).
 
-Buckets larger than ``IMITATION_AMD_ONESHOT_MAX_BYTES`` (default 256 KiB) keep RCCL, whose
+Buckets larger than ``IMITATION_AMD_ONESHOT_MAX_BYTES`` (default 1 MiB) keep RCCL, whose
 pipelined ring wins once the message is bandwidth bound.
 """
 
@@ -153,9 +153,18 @@ def get() -> Optional[OneShotComm]:
 
     C = _native.load()
     dev = torch.device("cuda", torch.cuda.current_device())
-    stage = int(os.environ.get("IMITATION_AMD_ONESHOT_MAX_BYTES", str(256 * 1024)))
+    stage = int(os.environ.get("IMITATION_AMD_ONESHOT_MAX_BYTES", str(1024 * 1024)))
     stage = max(16, (stage + 15) // 16 * 16)
     timeout = float(os.environ.get("IMITATION_AMD_ONESHOT_TIMEOUT_S", "60"))
+    # every pair of distinct devices must be peer-accessible (xGMI); ranks on one card
+    # (the rehearsal path) share the device and need no peer mapping
+    devs = [None] * world
+    tdist.all_gather_object(devs, dev.index)
+    peer_ok = all(d == dev.index or torch.cuda.can_device_access_peer(dev.index, d) for d in devs)
+    if not _agree(peer_ok, dev):
+        if mode not in ("auto",):
+            raise RuntimeError("one-shot all-reduce: devices are not peer-accessible")
+        return None
     comm = None
     try:
         comm = OneShotComm(C, tdist.get_rank(), world, dev, stage, timeout)

@@ -155,8 +155,9 @@ def _pref_dataset(P: int, L: int, seed: int):
     return ds
 
 
-def pref_reward_dp_worker(rank, world, P, L, mb, epochs, seed):
-    """BasicRewardTrainer on a replicated preference dataset; returns the trained parameters."""
+def pref_reward_dp_worker(rank, world, P, L, mb, epochs, seed, device="cpu", report=False):
+    """BasicRewardTrainer on a replicated preference dataset; returns the trained parameters
+    (and with ``report`` whether the minibatch ran as a HIP-graph replay)."""
     import torch as th
 
     from imitation_amd.algorithms import preference_comparisons as pc
@@ -166,7 +167,7 @@ def pref_reward_dp_worker(rank, world, P, L, mb, epochs, seed):
     from imitation_amd.util.networks import RunningNorm
 
     th.manual_seed(seed)
-    net = BasicRewardNet(spaces.Box(-1, 1, (5,)), spaces.Box(-1, 1, (2,)), normalize_input_layer=RunningNorm)
+    net = BasicRewardNet(spaces.Box(-1, 1, (5,)), spaces.Box(-1, 1, (2,)), normalize_input_layer=RunningNorm).to(device)
     tr = pc.BasicRewardTrainer(pc.PreferenceModel(net), pc.CrossEntropyRewardLoss(), rng=np.random.default_rng(seed),
                                batch_size=mb, epochs=epochs, lr=1e-2,
                                custom_logger=logger.configure(f"/tmp/ia_pref_dp_{rank}", format_strs=[]))
@@ -174,8 +175,11 @@ def pref_reward_dp_worker(rank, world, P, L, mb, epochs, seed):
     assert tr._fast_path_ok(ds)
     tr.train(ds)
     norm = net.mlp.normalize_input if hasattr(net.mlp, "normalize_input") else None
-    out = [p.detach().numpy().copy() for p in net.parameters()]
-    out += [b.detach().numpy().copy() for b in net.buffers()]
+    out = [p.detach().cpu().numpy().copy() for p in net.parameters()]
+    out += [b.detach().cpu().numpy().copy() for b in net.buffers()]
+    if report:
+        g = getattr(tr, "_mb_graph", None)
+        return out, (0 if g is None else len(g.graphs))
     return out
 
 
