@@ -188,7 +188,9 @@ struct PPORcGeo {
   float* rowd;             // [K][G*nch][64][4] old_logp, normalised advantage, return
   float* mom;              // [K][128] per-minibatch obs mean / var
   float* slab;             // [2][G][n_items][256] per-workgroup gradient partials (G > 1)
-  unsigned* sync;          // [0] arrival counter, [1] timeout flag (zeroed per launch)
+  float* red;              // [2][n_items][256] reduced gradients (two-level exchange)
+  int xchg2;               // two-level exchange: item id reduced by workgroup id % G, then shared
+  unsigned* sync;          // [0] arrival counter, [1] timeout flag, [2] second-level arrivals (zeroed per launch)
 };
 
 }  // namespace ia

@@ -40,6 +40,7 @@
 //
 // barriers / minibatch: [fwd+loss+bwd chain] B1 [dW items] (exchange) [|g|^2] B2 [clip, Adam] B3
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "ia/engine.h"
 #include "ia/wave.h"
@@ -109,6 +110,18 @@ __device__ __forceinline__ void wait_vm4(f4& a, f4& b, f4& c, f4& d) {
 __device__ __forceinline__ void wait_vm8(f4 (&v)[8]) {
   asm volatile("s_waitcnt vmcnt(0)"
                : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])::"memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_n(f4 (&v)[N]) {
+  if constexpr (N == 8) {
+    wait_vm8(v);
+  } else if constexpr (N == 4) {
+    wait_vm4(v[0], v[1], v[2], v[3]);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i])::"memory");
+  }
 }
 __device__ __forceinline__ unsigned ld_sc1u(unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -526,6 +539,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   if (tid < 16) sprof[tid] = 0;
   unsigned* arrive = g.sync;
   unsigned* tflag = g.sync + 1;
+  unsigned* arrive2 = g.sync + 2;
   __syncthreads();
 
   for (int k = 0; k < K; ++k) {
@@ -932,7 +946,65 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       }
       __syncthreads();
       const unsigned long long e2 = a.prof ? clock64() : 0;
-      if (G == 2) exchange_sum<2, KI>(slab, n_items, w, lane, gg);
+      if (g.xchg2) {
+        // Two-level exchange (large G): workgroup grp sums ONLY the items of its wave slots
+        // it with it % G == grp (ids kWaves*it .. kWaves*it + 7: one item per wave, so the
+        // waves reduce in parallel) over the G partials -- group order, the same additions as
+        // the one-level sum -- and publishes them; after a second arrival every workgroup
+        // reads the n_items reduced tiles once: per-workgroup loads ~2 x n_items KB instead
+        // of G x n_items KB.
+        float* red = g.red + (size_t)(k & 1) * n_items * 256;
+        const size_t gs = (size_t)n_items * 256;
+#pragma unroll
+        for (int it = 0; it < KI; ++it) {
+          const int id = w + it * kWaves;
+          if (id >= n_items || it % G != grp) continue;
+          const float* p = slab + (size_t)id * 256 + lane * 4;
+          f4 sacc = {0.f, 0.f, 0.f, 0.f};
+          for (int gi0 = 0; gi0 < G; gi0 += 8) {  // 8 loads in flight, one wait per batch
+            f4 v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = ld_sc1_x4(p + (size_t)(gi0 + e < G ? gi0 + e : 0) * gs);
+            wait_vm8(v);
+            if (gi0 == 0) sacc = v[0];
+            else sacc += v[0];
+#pragma unroll
+            for (int e = 1; e < 8; ++e)
+              if (gi0 + e < G) sacc += v[e];
+          }
+          st_sc1_x4(red + (size_t)id * 256 + lane * 4, sacc);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          atomicAdd(arrive2, 1u);
+          const unsigned target = (unsigned)G * (unsigned)(k + 1);
+          unsigned spins = 0;
+          while (ld_sc1u(arrive2) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22) || ld_sc1u(tflag) != 0u) {
+              atomicOr(tflag, 1u);
+              break;
+            }
+          }
+        }
+        __syncthreads();
+        f4 v[KI];
+#pragma unroll
+        for (int it = 0; it < KI; ++it) {
+          const int id = w + it * kWaves;
+          v[it] = ld_sc1_x4(red + (size_t)(id < n_items ? id : w) * 256 + lane * 4);
+        }
+        wait_vm_n<KI>(v);  // results tied to the wait (inline-asm loads are invisible to the compiler)
+#pragma unroll
+        for (int it = 0; it < KI; ++it) {
+          if (w + it * kWaves >= n_items) continue;
+          gg[it][0] = v[it].x;
+          gg[it][1] = v[it].y;
+          gg[it][2] = v[it].z;
+          gg[it][3] = v[it].w;
+        }
+      } else       if (G == 2) exchange_sum<2, KI>(slab, n_items, w, lane, gg);
       else if (G == 4) exchange_sum<4, KI>(slab, n_items, w, lane, gg);
       else if (G == 8) exchange_sum<8, KI>(slab, n_items, w, lane, gg);
       else
@@ -1220,7 +1292,7 @@ size_t ppo_rc_workspace_floats(const PPOArgs& a) {
   if (!ppo_rc_plan(a, g, lds)) return 0;
   const size_t K = (size_t)a.n_epochs * (a.rows / a.batch);
   const size_t slots = K * g.G * g.nch;
-  return slots * 64 * (g.dp + 16 + 4) + K * 128 + 2 * (size_t)g.G * g.n_items * 256 + 64;
+  return slots * 64 * (g.dp + 16 + 4) + K * 128 + 2 * (size_t)(g.G + 1) * g.n_items * 256 + 64;
 }
 
 hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
@@ -1234,7 +1306,12 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   g.rowd = g.acts + slots * 64 * 16;
   g.mom = g.rowd + slots * 64 * 4;
   g.slab = g.mom + K * 128;
-  g.sync = reinterpret_cast<unsigned*>(g.slab + 2 * (size_t)g.G * g.n_items * 256);
+  g.red = g.slab + 2 * (size_t)g.G * g.n_items * 256;
+  g.sync = reinterpret_cast<unsigned*>(g.red + 2 * (size_t)g.n_items * 256);
+  {  // two-level exchange from 16 cooperating workgroups (IMITATION_AMD_PPO_XCHG2=0/1 forces it)
+    const char* ev = getenv("IMITATION_AMD_PPO_XCHG2");
+    g.xchg2 = ev ? (ev[0] == '1' && g.G > 1) : (g.G >= 16);
+  }
   if (K == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(g.sync, 0, 64 * sizeof(unsigned), s);
   if (e != hipSuccess) return e;
@@ -1254,6 +1331,8 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   hipLaunchKernelGGL((ppo_rc_kernel<KT, KI, S0, NL, ACT, HW, CW, DT>), grid, block, lds_launch, s, a, g)
   if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete)
     IA_RC(2, 4, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
+  else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 32 && !a.discrete)
+    IA_RC(2, 4, 5, 3, 2, 32, 32, 0);  // the same, 32-row chunks (16 workgroups at the 8-rank DP minibatch)
 
   else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)
     IA_RC(4, 8, 3, 3, 1, 64, 32, 0);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)

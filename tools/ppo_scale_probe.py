@@ -41,21 +41,55 @@ def main():
         for _ in range(2):
             tr._ppo_update()
         th.cuda.synchronize()
-        n = 5
-        t0 = time.perf_counter()
-        for _ in range(n):
+        # one-level vs two-level partial exchange: bitwise-equal update from one state, then timing
+        pol = gen.policy
+        norm = tr.pol_norm
+        def snap():
+            t = [q.detach().clone() for q in pol.parameters()] + [tr.exp_avg.clone(), tr.exp_avg_sq.clone(), tr.adam_step.clone()]
+            if norm is not None:
+                t += [norm.running_mean.clone(), norm.running_var.clone(), norm.count.clone(), tr.norm_count.clone()]
+            return t, tr._perm_round
+        def restore(st):
+            t, pr = st
+            dst = list(pol.parameters()) + [tr.exp_avg, tr.exp_avg_sq, tr.adam_step]
+            if norm is not None:
+                dst += [norm.running_mean, norm.running_var, norm.count, tr.norm_count]
+            with th.no_grad():
+                for d, v in zip(dst, t):
+                    d.copy_(v)
+            tr._perm_round = pr
+        s0 = snap()
+        res = {}
+        for mode in ("0", "1"):
+            os.environ["IMITATION_AMD_PPO_XCHG2"] = mode
+            restore(s0)
             tr._ppo_update()
-        th.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / n
-        print(f"W={W} path={path} rows={tr.T * tr.N} batch={64 * W}: ppo update {1e3 * dt:.3f} ms", flush=True)
-        prof = th.zeros(16, dtype=th.int64, device="cuda")
-        tr._ppo_static["prof"] = prof
-        tr._ppo_update()
-        th.cuda.synchronize()
-        p = prof.cpu().numpy().astype(np.float64) / tr._last_ppo_info[1]
-        print(f"    cycles/minibatch (workgroup 0): chunk {p[0]:.0f} exchange+|g|^2 {p[1]:.0f} clip+adam {p[2]:.0f} | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f}"
-              f" | exchange: publish {p[13]:.0f} arrival {p[14]:.0f} loads {p[15]:.0f}", flush=True)
-        tr._ppo_static.pop("prof")
+            th.cuda.synchronize()
+            res[mode] = [q.detach().clone() for q in pol.parameters()]
+        same = all(th.equal(a, b) for a, b in zip(res["0"], res["1"]))
+        for mode in ("0", "1"):
+            os.environ["IMITATION_AMD_PPO_XCHG2"] = mode
+            n = 5
+            t0 = time.perf_counter()
+            for _ in range(n):
+                tr._ppo_update()
+            th.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / n
+            print(f"W={W} path={path} rows={tr.T * tr.N} batch={64 * W} xchg2={mode}: ppo update {1e3 * dt:.3f} ms"
+                  f" (two-level bitwise equal: {same})", flush=True)
+        os.environ.pop("IMITATION_AMD_PPO_XCHG2")
+        for mode in ("0", "1"):
+            os.environ["IMITATION_AMD_PPO_XCHG2"] = mode
+            prof = th.zeros(16, dtype=th.int64, device="cuda")
+            tr._ppo_static["prof"] = prof
+            tr._ppo_update()
+            th.cuda.synchronize()
+            p = prof.cpu().numpy().astype(np.float64) / tr._last_ppo_info[1]
+            print(f"    xchg2={mode} cycles/minibatch (workgroup 0): chunk {p[0]:.0f} exchange+|g|^2 {p[1]:.0f} clip+adam {p[2]:.0f}"
+                  f" | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f} | exchange: publish {p[13]:.0f} arrival {p[14]:.0f} loads {p[15]:.0f}",
+                  flush=True)
+            tr._ppo_static.pop("prof")
+        os.environ.pop("IMITATION_AMD_PPO_XCHG2")
 
 
 if __name__ == "__main__":
