@@ -357,3 +357,15 @@ def airl_round_worker(rank, world, seed):
             "norm": [b.detach().cpu().numpy().copy() for b in rn.buffers()],
             "graphed": graphed, "replays": 0 if g is None else g.n_replays,
             "oneshot_calls": 0 if c is None else c.calls}
+
+
+def oneshot_cpu_worker(rank, world):
+    """On a CPU gloo group the one-shot path stays off (no device to map) and every
+    collective keeps torch.distributed semantics."""
+    from imitation_amd.parallel import dist as pdist
+    from imitation_amd.parallel import oneshot
+
+    t = th.full((5,), float(rank + 1))
+    pdist.allreduce_sum_(t)
+    return {"comm": oneshot.get() is not None, "active": pdist.oneshot_active(),
+            "moments_device": pdist.allreduce_moments_device(th.ones(3, 2)) is not None, "sum": t.tolist()}

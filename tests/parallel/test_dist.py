@@ -121,3 +121,12 @@ def test_dagger_data_parallel(tmp_path):
     assert a["last"] == b["last"] == a["local"] + b["local"]
     for p, q in zip(a["params"], b["params"]):
         np.testing.assert_array_equal(p, q)
+
+
+@pytest.mark.parametrize("mode", ["auto", "1", "0"])
+def test_oneshot_off_without_gpu(mode, monkeypatch):
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", mode)
+    out = run_ranks(W.oneshot_cpu_worker, 2)
+    for o in out:
+        assert not o["comm"] and not o["active"] and not o["moments_device"]
+        assert o["sum"] == [3.0] * 5
