@@ -155,7 +155,7 @@ def get() -> Optional[OneShotComm]:
     dev = torch.device("cuda", torch.cuda.current_device())
     stage = int(os.environ.get("IMITATION_AMD_ONESHOT_MAX_BYTES", str(1024 * 1024)))
     stage = max(16, (stage + 15) // 16 * 16)
-    timeout = float(os.environ.get("IMITATION_AMD_ONESHOT_TIMEOUT_S", "60"))
+    timeout = float(os.environ.get("IMITATION_AMD_ONESHOT_TIMEOUT_S", "600"))  # = the process-group timeout
     # every pair of distinct devices must be peer-accessible (xGMI); ranks on one card
     # (the rehearsal path) share the device and need no peer mapping
     devs = [None] * world
