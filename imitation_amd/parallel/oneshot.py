@@ -160,7 +160,10 @@ def get() -> Optional[OneShotComm]:
     # (the rehearsal path) share the device and need no peer mapping
     devs = [None] * world
     tdist.all_gather_object(devs, dev.index)
-    peer_ok = all(d == dev.index or torch.cuda.can_device_access_peer(dev.index, d) for d in devs)
+    try:
+        peer_ok = all(d == dev.index or torch.cuda.can_device_access_peer(dev.index, d) for d in devs)
+    except Exception:  # a local query: never skip the agreement collective below
+        peer_ok = False
     if not _agree(peer_ok, dev):
         if mode not in ("auto",):
             raise RuntimeError("one-shot all-reduce: devices are not peer-accessible")
