@@ -413,9 +413,13 @@ py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, 
   TORCH_CHECK(ia::running_norm_ok(B, D), "running_norm: B * D <= 2^20, D <= 256");
   torch::Tensor y;
   if (want_y) y = torch::empty_like(x);
+  // block partials of the multi-workgroup path (caching allocator: graph-capture safe)
+  const size_t wsn = update ? ia::running_norm_ws_floats(B, D) : 0;
+  torch::Tensor ws;
+  if (wsn) ws = torch::empty({(int64_t)wsn}, x.options());
   IA_HIP_CHECK(ia::running_norm(x.data_ptr<float>(), B, D, mean.data_ptr<float>(), var.data_ptr<float>(),
                                 count.data_ptr<int>(), (float)eps, update ? 1 : 0, want_y ? y.data_ptr<float>() : nullptr,
-                                ia_stream()));
+                                wsn ? ws.data_ptr<float>() : nullptr, ia_stream()));
   return want_y ? py::cast(y) : py::none();
 }
 

@@ -164,8 +164,10 @@ hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, con
 // ---- norm.hip: RunningNorm update (batch moments + Chan merge + count) and normalise, one
 // workgroup (B * D <= 2^20, D <= 256); y == nullptr: statistics only
 bool running_norm_ok(int B, int D);
+// ws: running_norm_ws_floats(B, D) floats (multi-workgroup path for large B; nullptr -> one workgroup)
+size_t running_norm_ws_floats(int B, int D);
 hipError_t running_norm(const float* x, int B, int D, float* mean, float* var, int* count, float eps, int update, float* y,
-                        hipStream_t s);
+                        float* ws, hipStream_t s);
 
 // ---- gather.hip: one-launch multi-field row gather (row r <- source row b[r] * n_envs + e[r],
 // or b[r] when e == nullptr)

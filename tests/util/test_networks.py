@@ -83,7 +83,7 @@ def test_build_cnn_fused_plan():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,D", [(4096, 17), (1, 3), (7, 256), (300, 65)])
+@pytest.mark.parametrize("B,D", [(4096, 17), (1, 3), (7, 256), (300, 65), (40000, 5)])
 def test_running_norm_fused_kernel_matches_torch(B, D):
     """RunningNorm update + normalise in one HIP launch == the torch statistics path."""
     import torch as th
