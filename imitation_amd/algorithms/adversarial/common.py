@@ -309,7 +309,9 @@ class AdversarialTrainer(base.DemonstrationAlgorithm[types.Transitions]):
         from imitation_amd.rl.sac import SACPolicy
 
         if isinstance(self.policy, ActorCriticPolicy):
-            _, log_policy_act_prob_th, _ = self.policy.evaluate_actions(obs_th, acts_th)
+            # evaluate_actions' log-prob without its value head and entropy (one fused MLP
+            # pass fewer per discriminator minibatch; same normaliser update, same numbers)
+            log_policy_act_prob_th = self.policy.get_distribution(obs_th).log_prob(acts_th)
         elif isinstance(self.policy, SACPolicy):
             actor = self.policy.actor
             mean_actions, log_std, _ = actor.get_action_dist_params(obs_th)
@@ -347,7 +349,13 @@ class AdversarialTrainer(base.DemonstrationAlgorithm[types.Transitions]):
         ex = {k: to_dev(expert_samples[k]) for k in ("obs", "acts", "next_obs", "dones")}
         ge = {k: to_dev(gen_samples[k]) for k in ("obs", "acts", "next_obs", "dones")}
         mb = self.demo_minibatch_size
-        labels = th.cat([th.ones(mb, dtype=th.int64, device=dev), th.zeros(mb, dtype=th.int64, device=dev)])
+        # constant [1]*mb + [0]*mb labels, built once per (mb, device): no fill / cat launches
+        # per minibatch (nor inside a captured discriminator step)
+        cache = self.__dict__.setdefault("_disc_labels", {})
+        labels = cache.get((mb, dev))
+        if labels is None:
+            labels = cache[(mb, dev)] = th.cat([th.ones(mb, dtype=th.int64, device=dev),
+                                                th.zeros(mb, dtype=th.int64, device=dev)])
         for start in range(0, batch_size, mb):
             end = start + mb
             obs = th.cat([ex["obs"][start:end], ge["obs"][start:end].to(ex["obs"].dtype)])
