@@ -369,3 +369,33 @@ def oneshot_cpu_worker(rank, world):
     pdist.allreduce_sum_(t)
     return {"comm": oneshot.get() is not None, "active": pdist.oneshot_active(),
             "moments_device": pdist.allreduce_moments_device(th.ones(3, 2)) is not None, "sum": t.tolist()}
+
+
+def oneshot_stress_worker(rank, world, iters, seed):
+    """Uneven arrival: every rank runs a random amount of GPU work (and host sleep) before each
+    one-shot reduction of a fresh rank-dependent bucket of random size; returns the max error
+    of every reduction against the closed-form sum (checked over every word)."""
+    import time
+
+    from imitation_amd.parallel import oneshot
+
+    c = oneshot.get()
+    assert c is not None
+    dev = c.device
+    rng = np.random.default_rng(seed)  # same size sequence on every rank
+    local = np.random.default_rng(seed * 31 + rank)  # rank-local load pattern
+    a = th.randn(512, 512, device=dev)
+    errs = []
+    for it in range(iters):
+        n = int(rng.integers(1, 70000))
+        for _ in range(int(local.integers(0, 6))):
+            a = th.tanh(a @ a * 1e-3)
+        if local.random() < 0.2:
+            time.sleep(float(local.random()) * 2e-3)
+        base = th.arange(n, device=dev, dtype=th.float32) % 97
+        x = base * float(rank + 1) + float(it)
+        c.allreduce_(x)
+        exp = base * float(world * (world + 1) / 2) + float(it * world)
+        errs.append((x - exp).abs().max())
+    th.cuda.synchronize(dev)
+    return {"max_err": float(th.stack(errs).max()), "error": c.error()}

@@ -102,3 +102,12 @@ def test_preference_reward_dp_graphed_on_oneshot(monkeypatch):
     for i, (a, b) in enumerate(zip(one[0][0], ref[0][0])):
         if i != 5:  # output bias: rounding noise normalised by Adam (see test_dist.py)
             np.testing.assert_allclose(a, b, rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+def test_oneshot_uneven_arrival_stress(oneshot_env):
+    """200 reductions of random sizes with random per-rank GPU / host delays before each:
+    every word exact (small-integer sums are exact in fp32), no timeout."""
+    out = run_ranks(W.oneshot_stress_worker, 4, 200, 11, timeout=300)
+    for o in out:
+        assert o["error"] == 0 and o["max_err"] == 0.0, o
