@@ -38,6 +38,7 @@ from torch.utils import data as data_th
 from imitation_amd.algorithms import base
 from imitation_amd.data import rollout, types, wrappers
 from imitation_amd.data.types import AnyPath, TrajectoryPair, TrajectoryWithRew, TrajectoryWithRewPair, Transitions
+from imitation_amd.ops import rl as rl_ops
 from imitation_amd.ops import optim as optim_ops
 from imitation_amd.ops import preference as pref_ops
 from imitation_amd.parallel import dist as pdist
@@ -907,14 +908,16 @@ class _MinibatchGraph:
         pm = tr._preference_model
         n, L = idx.shape[0], self.L
         rows = (idx[:, None] * (2 * L) + self.span).reshape(-1)
-        rews = pm.model(self.s.index_select(0, rows), self.a.index_select(0, rows), self.ns.index_select(0, rows),
-                        self.d.index_select(0, rows)).view(n, 2, L)
-        prefs = self.prefs.index_select(0, idx)
+        # the four transition fields in ONE gather launch, preferences (+ ground truth) in another
+        s_, a_, ns_, d_ = rl_ops.gather_rows([self.s, self.a, self.ns, self.d], rows)
+        rews = pm.model(s_, a_, ns_, d_).view(n, 2, L)
+        per_pair = rl_ops.gather_rows([self.prefs] + ([self.gt] if self.gt is not None else []), idx)
+        prefs = per_pair[0]
         loss, probs = pref_ops.bradley_terry(rews[:, 0], rews[:, 1], prefs, pm.discount_factor, pm.threshold,
                                              pm.noise_prob)
         rec = [loss.detach(), ((probs.detach() > 0.5) == (prefs > 0.5)).float().mean()]
         if self.gt is not None:
-            g = self.gt.index_select(0, idx)
+            g = per_pair[1]
             gp = pref_ops.bradley_terry_probs_reference(g[:, 0], g[:, 1], pm.discount_factor, pm.threshold, pm.noise_prob)
             rec.append(th.nn.functional.binary_cross_entropy(gp, prefs))
         (loss * (n / tr.batch_size)).backward()
