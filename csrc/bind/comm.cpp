@@ -63,7 +63,7 @@ void register_comm(py::module& m) {
   m.def("oneshot_close", [](int64_t p) { IA_HIP_CHECK(ia::oneshot_close(reinterpret_cast<void*>((uintptr_t)p))); });
   m.def("oneshot_free", [](int64_t p) { IA_HIP_CHECK(ia::oneshot_free(reinterpret_cast<void*>((uintptr_t)p))); });
   m.def("oneshot_region_bytes", [](int64_t s) { return (int64_t)ia::oneshot_region_bytes((size_t)s); });
-  m.def("oneshot_blocks", [](int64_t n) { return ia::oneshot_blocks((int)n); });
+  m.def("oneshot_blocks", [](int64_t n, int64_t stage) { return ia::oneshot_blocks((int)n, (size_t)stage); });
   m.def("oneshot_allreduce", &oneshot_allreduce, "one-shot sum all-reduce of in*scale over the mapped ranks into out");
   m.def("oneshot_error", &oneshot_error, "error word of a local region (1: a block timed out)");
   m.def("oneshot_clear_error",

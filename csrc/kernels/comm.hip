@@ -14,11 +14,16 @@
 //                then one system-scope acquire per block
 //   4. reduce  : read slot `parity` of ranks 0..W-1 in rank order, sum, store
 //
-// Blocks are independent (block b owns a fixed slice and its own flag row / generation
-// counter), so no inter-block synchronisation is needed and partial residency cannot
-// deadlock.  Two staging parities make a start-barrier sufficient: a peer can be at most
-// one generation ahead (it needs this rank's flag for gen+1, written only after this rank
-// finished reading gen), and gen+1 stages into the other parity.  The generation counter
+// Blocks are independent (block b owns a FIXED slice of the staging region -- vectors
+// [b * per, (b + 1) * per) with per = stage_vectors / kOneShotMaxBlocks, whatever the
+// bucket size -- and its own flag row / generation counter), so no inter-block
+// synchronisation is needed and partial residency cannot deadlock.  Two staging parities
+// make a start-barrier sufficient: a peer's block b can be at most one generation ahead of
+// this rank's block b (it needs this rank's block-b flag for gen+1, written only after this
+// block finished reading gen), and gen+1 stages into the other parity.  Because the slice
+// of block b never depends on the call's size, a block only ever reads staging bytes that
+// peers' block b writes: calls that launch fewer blocks leave the higher blocks' counters
+// behind without letting two blocks with different parities share bytes.  The generation counter
 // lives in device memory, so the launch is graph-capture safe.  Summation order is rank
 // order on every rank -> results are bitwise identical across ranks.
 //
@@ -39,6 +44,14 @@ constexpr size_t kCntOff = 4096;    // [kOneShotMaxBlocks] uint32 generation cou
 constexpr size_t kErrOff = 4096 + 512;
 constexpr size_t kDataOff = 8192;   // 2 x stage_bytes staging slots
 constexpr int kThreads = 256;
+
+// vectors per block slice: the staging region split into kOneShotMaxBlocks fixed slices
+// (at least one 256-thread pass each)
+__host__ __device__ __forceinline__ int oneshot_block_vectors(size_t stage_bytes) {
+  const size_t sv = stage_bytes / 16;
+  const size_t per = (sv + kOneShotMaxBlocks - 1) / kOneShotMaxBlocks;
+  return per < (size_t)kThreads ? kThreads : (int)per;
+}
 
 __device__ __forceinline__ void store_release_sys(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -63,11 +76,12 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(OneShotArgs
   const unsigned gen = s_gen;
   const size_t par = (gen & 1u) ? a.stage_bytes : 0;
 
-  // slice of float4 vectors owned by this block (the n % 4 tail belongs to the last block)
+  // fixed slice of float4 vectors owned by this block (the n % 4 tail belongs to the block
+  // whose slice holds vector nv)
   const int nv = a.n >> 2;
-  const int per = (nv + gridDim.x - 1) / gridDim.x;
+  const int per = oneshot_block_vectors(a.stage_bytes);
   const int v0 = min(nv, b * per), v1 = min(nv, v0 + per);
-  const bool tail_owner = b == (int)gridDim.x - 1;
+  const bool tail_owner = b == nv / per;
   const int tail0 = nv << 2;
 
   // 1. stage
@@ -142,10 +156,11 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(OneShotArgs
 
 size_t oneshot_region_bytes(size_t stage_bytes) { return kDataOff + 2 * stage_bytes; }
 
-int oneshot_blocks(int n) {
+int oneshot_blocks(int n, size_t stage_bytes) {
   const int nv = (n + 3) >> 2;
-  int blocks = (nv + kThreads - 1) / kThreads;
-  return blocks < 1 ? 1 : (blocks > kOneShotMaxBlocks ? kOneShotMaxBlocks : blocks);
+  const int per = oneshot_block_vectors(stage_bytes);
+  const int blocks = (nv + per - 1) / per;
+  return blocks < 1 ? 1 : blocks;  // <= kOneShotMaxBlocks since n * 4 <= stage_bytes
 }
 
 hipError_t oneshot_alloc(size_t stage_bytes, void** ptr, void* handle) {
@@ -195,7 +210,7 @@ hipError_t oneshot_allreduce(const OneShotArgs& a, hipStream_t s) {
   if ((size_t)a.n * sizeof(float) > a.stage_bytes) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out)) & 15) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(oneshot_blocks(a.n)), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(oneshot_blocks(a.n, a.stage_bytes)), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -280,7 +280,7 @@ struct OneShotArgs {
 };
 size_t oneshot_region_bytes(size_t stage_bytes);
 size_t oneshot_handle_bytes();
-int oneshot_blocks(int n);
+int oneshot_blocks(int n, size_t stage_bytes);
 hipError_t oneshot_alloc(size_t stage_bytes, void** ptr, void* handle);  // zeroed uncached region + IPC handle
 hipError_t oneshot_open(const void* handle, void** ptr);
 hipError_t oneshot_close(void* ptr);

@@ -288,6 +288,7 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         compute_rollout_stats = RolloutStatsComputer(log_rollouts_venv, log_rollouts_n_episodes)
 
         def _on_epoch_end(epoch_number: int):
+            pdist.check_comm("BC epoch")
             self._bc_logger.log_epoch(epoch_number + 1)
             if on_epoch_end is not None:
                 on_epoch_end()

@@ -1247,6 +1247,7 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
             with self.logger.accumulate_means("agent"):
                 self.logger.log(f"Training agent for {steps} timesteps")
                 self.trajectory_generator.train(steps=steps)
+            pdist.check_comm("preference iteration")
             self.logger.dump(self._iteration)
             if callback:
                 callback(self._iteration)

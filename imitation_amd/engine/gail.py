@@ -898,6 +898,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                     self._graphed_disc_update(i)
                     steps.append(self._disc_step)
             vals = self._disc_stats_gen[:n].tolist() if n else []  # one host sync per round
+            pdist.check_comm("adversarial round")
             for i in range(n):
                 with self.logger.accumulate_means("disc"):
                     self._record_disc(common.train_stats_from_sums(vals[i], rows), steps[i])
@@ -936,6 +937,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                         self._fused_disc_update(i)
                         steps.append(self._disc_step)
                 vals = self._disc_stats[:n].tolist() if n else []
+            pdist.check_comm("GAIL round")
             if n:
                 for i in range(n):
                     with self.logger.accumulate_means("disc"):
@@ -968,7 +970,11 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         defer = pol_merge and self._pol_defer_buf is not None
         if defer:
             self._ensure_pol_defer(n)
-        serial = pol_merge and not defer  # the disc would write the norm PPO is using
+        # serial when the disc would write the norm PPO is using, or when both would issue
+        # per-step collectives: the non-replicated DP PPO all-reduces every minibatch through
+        # the same one-shot communicator as the disc, and two kernels in flight on it would
+        # pair one rank's PPO gradients with another rank's disc sums
+        serial = (pol_merge and not defer) or (pdist.world_size() > 1 and not self._dp_replicated)
         if not hasattr(self, "_ppo_stats_host"):
             self._ppo_stats_host = th.zeros(self.stats.numel(), pin_memory=True)
         steps: List[int] = []

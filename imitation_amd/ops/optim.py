@@ -180,11 +180,27 @@ class FusedAdam(th.optim.Optimizer):
         g.zero_()
 
     # ------------------------------------------------------------------ checkpoints
+    def state_dict(self) -> Dict[str, Any]:
+        """torch Adam layout that loads into ``th.optim.Adam`` / ``AdamW`` as-is: every
+        parameter gets its OWN scalar ``step`` (the flat group shares one device counter,
+        which torch would otherwise increment once per parameter) and the groups say
+        ``capturable=False`` (torch refuses a capturable step on CPU parameters)."""
+        sd = super().state_dict()
+        for st in sd["state"].values():
+            if "step" in st:
+                st["step"] = th.tensor(float(st["step"]), dtype=th.float32)
+            for k in ("exp_avg", "exp_avg_sq"):
+                if k in st:
+                    st[k] = st[k].detach().clone()
+        sd["param_groups"] = [dict(g, capturable=False) for g in sd["param_groups"]]
+        return sd
+
     def load_state_dict(self, state_dict: Dict[str, Any]) -> None:
         """Load a torch-Adam-layout state and copy it into the flat buffers (the loaded
         tensors would otherwise replace the views)."""
         super().load_state_dict(state_dict)
         for group, f in zip(self.param_groups, self._flat):
+            group["capturable"] = True
             for key in ("lr", "eps", "weight_decay", "maximize"):
                 group.setdefault(key, self.defaults[key])
             group["betas"] = tuple(group["betas"])

@@ -85,6 +85,26 @@ class OneShotComm:
     def error(self) -> int:
         return int(self._C.oneshot_error(self.local))
 
+    def clear_error(self) -> None:
+        self._C.oneshot_clear_error(self.local)
+
+    def check(self, where: str = "") -> None:
+        """Raise if a bounded wait of this communicator timed out (a lost or stalled peer:
+        the kernel wrote NaN into that reduction's output). Called at the once-per-round host
+        syncs of the training loops, so a lost peer stops the run instead of training on NaN."""
+        err = self.error()
+        if err:
+            self.clear_error()
+            raise RuntimeError(f"one-shot all-reduce timed out waiting for a peer{(' (' + where + ')') if where else ''}: "
+                               "its output was poisoned with NaN; aborting the run")
+
+    def block_floats(self) -> int:
+        """Floats per block slice (a bucket of n floats runs ceil(n / block_floats) blocks)."""
+        return 4 * max(256, -(-(self.stage_bytes // 16) // 64))
+
+    def blocks(self, n: int) -> int:
+        return int(self._C.oneshot_blocks(int(n), self.stage_bytes))
+
     def self_test(self) -> bool:
         """Reduce a few rank-dependent buckets (odd sizes, both staging parities, in- and
         out-of-place) and compare with the closed form; agree on the verdict over ranks."""

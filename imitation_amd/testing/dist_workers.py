@@ -281,6 +281,12 @@ def oneshot_timeout_worker(rank, world, timeout_s):
         c.allreduce_(x)
         th.cuda.synchronize(c.device)
         res = {"all_nan": bool(th.isnan(x).all().item()), "error": c.error()}
+        try:  # the training loops' once-per-round check raises and clears the word
+            c.check("test")
+            res["raised"] = False
+        except RuntimeError:
+            res["raised"] = True
+        res["error_after"] = c.error()
     from imitation_amd.parallel import dist as pdist
 
     pdist.barrier()
@@ -399,3 +405,41 @@ def oneshot_stress_worker(rank, world, iters, seed):
         errs.append((x - exp).abs().max())
     th.cuda.synchronize(dev)
     return {"max_err": float(th.stack(errs).max()), "error": c.error()}
+
+
+def oneshot_block_change_worker(rank, world, reps, seed):
+    """Back-to-back one-shot reductions whose block counts change call to call (1, 2, 4, 1
+    blocks), captured in ONE HIP graph and replayed with rank-skewed GPU load in front of each
+    replay; every word of every bucket is checked against the rank-order sum (the
+    staging slice of a block must not depend on the call's size)."""
+    from imitation_amd.parallel import oneshot
+
+    c = oneshot.get()
+    assert c is not None
+    dev = c.device
+    per = c.block_floats()
+    sizes = [per // 2 + 3, per + per // 2, 3 * per + 5, 7]
+    blocks = [c.blocks(n) for n in sizes]
+    bufs = [th.zeros(n, device=dev) for n in sizes]
+    side = th.cuda.Stream(device=dev)
+    side.wait_stream(th.cuda.current_stream(dev))
+    g = th.cuda.CUDAGraph()
+    with th.cuda.stream(side):
+        with th.cuda.graph(g, stream=side):
+            for b in bufs:
+                c.allreduce_(b)
+    th.cuda.current_stream(dev).wait_stream(side)
+    local = np.random.default_rng(seed * 13 + rank)
+    a = th.randn(256, 256, device=dev)
+    bad = 0
+    for rep in range(reps):
+        for i, b in enumerate(bufs):
+            b.copy_(th.arange(b.numel(), device=dev, dtype=th.float32) % 89 * float(rank + 1) + float(rep + i))
+        for _ in range(int(local.integers(0, 4))):
+            a = th.tanh(a @ a * 1e-3)
+        g.replay()
+        for i, b in enumerate(bufs):
+            exp = th.arange(b.numel(), device=dev, dtype=th.float32) % 89 * float(world * (world + 1) / 2) + float((rep + i) * world)
+            bad += int((b != exp).sum().item())
+    th.cuda.synchronize(dev)
+    return {"bad_words": bad, "blocks": blocks, "error": c.error()}

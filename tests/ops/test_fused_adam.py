@@ -58,6 +58,31 @@ def test_fused_adam_state_dict_roundtrip_with_torch_adam():
     assert float(oc.state[next(iter(c.parameters()))]["step"]) == 7.0
 
 
+def test_fused_adam_checkpoint_loads_into_torch_adam():
+    """fused -> torch direction: per-parameter steps, capturable=False; the torch optimizer then
+    continues exactly like the fused one (wrong bias correction if the step were shared)."""
+    a, b, oa, ob = _run("cpu", optim_ops.FusedAdam, th.optim.Adam, lr=1e-2)
+    c, _ = _nets("cpu")
+    c.load_state_dict(a.state_dict())
+    sd = oa.state_dict()
+    assert all(not g["capturable"] for g in sd["param_groups"])
+    steps = [st["step"] for st in sd["state"].values()]
+    assert len({id(s) for s in steps}) == len(steps)
+    oc = th.optim.Adam(c.parameters(), lr=1e-2)
+    oc.load_state_dict(sd)
+    g = th.Generator().manual_seed(5)
+    for _ in range(3):
+        x = th.randn(4, 7, generator=g)
+        for net, opt in ((a, oa), (c, oc)):
+            opt.zero_grad()
+            net(x).sum().backward()
+            opt.step()
+    for p, q in zip(a.parameters(), c.parameters()):
+        th.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+    assert [float(oc.state[p]["step"]) for p in c.parameters()] == [9.0] * 4
+    assert float(oa.state[next(iter(a.parameters()))]["step"]) == 9.0  # the fused counter untouched by state_dict
+
+
 def test_grads_stay_bound_after_module_zero_grad():
     a, _ = _nets("cpu")
     opt = optim_ops.FusedAdam(a.parameters(), lr=1e-2)

@@ -46,6 +46,7 @@ def test_oneshot_allreduce_matches_rank_order_sum(world, oneshot_env):
 def test_oneshot_bounded_wait(oneshot_env):
     out = run_ranks(W.oneshot_timeout_worker, 2, 0.25, timeout=240)
     assert out[0]["all_nan"] and out[0]["error"] == 1
+    assert out[0]["raised"] and out[0]["error_after"] == 0
 
 
 @pytest.mark.gpu
@@ -111,3 +112,13 @@ def test_oneshot_uneven_arrival_stress(oneshot_env):
     out = run_ranks(W.oneshot_stress_worker, 4, 200, 11, timeout=300)
     for o in out:
         assert o["error"] == 0 and o["max_err"] == 0.0, o
+
+
+@pytest.mark.gpu
+def test_oneshot_graph_block_count_changes(oneshot_env):
+    """One graph holding back-to-back reductions of 1, 2, 4 and 1 blocks, replayed under
+    rank-skewed load: every word matches (the staging parity is per fixed block slice)."""
+    out = run_ranks(W.oneshot_block_change_worker, 2, 12, 5, timeout=240)
+    for r in range(2):
+        assert out[r]["blocks"] == [1, 2, 4, 1]
+        assert out[r]["bad_words"] == 0 and out[r]["error"] == 0
