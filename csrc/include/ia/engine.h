@@ -159,13 +159,13 @@ struct PPOArgs {
   int mode;  // 0: full persistent update; 1: one minibatch -> grads only; 2: apply clip+Adam from grads
   int mb_index;  // minibatch index for mode 1 (epoch * n_mb + mb)
   unsigned long long* prof;  // optional [10] cycle counters per phase
-  int rc_gmax;   // mode 0 fast path: max cooperating workgroups per minibatch (0 = default 16)
+  int rc_gmax;   // mode 0 fast path: max cooperating workgroups per minibatch (0 = default kMaxRcGroups)
   int rc_cw;     // mode 0 fast path: rows per chunk override (0 = 64 for <= 32-wide nets, 32 otherwise)
 };
 
 // Geometry + workspace of the register-chained PPO kernel (ppo_rc.hip), planned on the host.
 constexpr int kMaxRcItems = 64;
-constexpr int kMaxRcGroups = 16;
+constexpr int kMaxRcGroups = 64;  // cooperating workgroups per minibatch (one per CU, co-resident)
 struct PPORcGeo {
   int din[2][kWaveMaxLayers], dout[2][kWaveMaxLayers];
   int w_off[2][kWaveMaxLayers], ldw[2][kWaveMaxLayers], b_off[2][kWaveMaxLayers];
@@ -183,6 +183,7 @@ struct PPORcGeo {
   int cw;                  // rows per chunk (one fwd/bwd pass of a workgroup)
   int nch;                 // chunks per workgroup per minibatch
   int G;                   // cooperating workgroups per minibatch (minibatch = G * nch * cw rows)
+  int nw;                  // waves per workgroup (8: <= 32-wide nets, 4: 64-wide nets at 1 wave / SIMD)
   float* xraw;             // [K][G*nch][64][dp] gathered raw observations (one 64-row slot per chunk)
   float* acts;             // [K][G*nch][64][16]
   float* rowd;             // [K][G*nch][64][4] old_logp, normalised advantage, return

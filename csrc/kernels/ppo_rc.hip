@@ -53,8 +53,6 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) float lf;
 typedef __attribute__((address_space(3))) f4 lf4;
 
-constexpr int kThreads = 512;
-constexpr int kWaves = 8;
 constexpr int kL = kWaveMaxLayers;
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
@@ -113,7 +111,11 @@ __device__ __forceinline__ void wait_vm8(f4 (&v)[8]) {
 }
 template <int N>
 __device__ __forceinline__ void wait_vm_n(f4 (&v)[N]) {
-  if constexpr (N == 8) {
+  if constexpr (N == 16) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]),
+                   "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])::"memory");
+  } else if constexpr (N == 8) {
     wait_vm8(v);
   } else if constexpr (N == 4) {
     wait_vm4(v[0], v[1], v[2], v[3]);
@@ -277,36 +279,63 @@ __device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int ro
 // Sum of the G workgroups' partials of this wave's items, in group order, 8 sc1 loads in
 // flight per lane and ONE wait per batch of IB = 8 / G items (a load round trip is ~1.2K
 // cycles; a wait per item and 4 groups made the loads the exchange's dominant cost).
+// ids[s]: item id of owned slot s (-1: empty slot).
 template <int GT, int KI>
-__device__ __forceinline__ void exchange_sum(const float* slab, int n_items, int w, int lane, float (&gg)[KI][4]) {
-  constexpr int IB0 = 8 / GT;
+__device__ __forceinline__ void exchange_sum(const float* slab, int n_items, const int (&ids)[KI], int lane, f4 (&xg)[KI]) {
+  constexpr int IB0 = 16 / GT;
   constexpr int IB = IB0 < KI ? IB0 : KI;
 #pragma unroll
   for (int i0 = 0; i0 < KI; i0 += IB) {
-    f4 v[8];
+    f4 v[16];
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int it = i0 + i;
-      const int id = w + it * kWaves;
-      const bool ok = it < KI && id < n_items;
+      const int id = it < KI && ids[it] >= 0 ? ids[it] : 0;
 #pragma unroll
-      for (int gi = 0; gi < GT; ++gi) v[i * GT + gi] = ld_sc1_x4(slab + ((size_t)gi * n_items + (ok ? id : w)) * 256 + lane * 4);
+      for (int gi = 0; gi < GT; ++gi) v[i * GT + gi] = ld_sc1_x4(slab + ((size_t)gi * n_items + id) * 256 + lane * 4);
     }
 #pragma unroll
-    for (int e = IB * GT; e < 8; ++e) v[e] = v[0];
-    wait_vm8(v);
+    for (int e = IB * GT; e < 16; ++e) v[e] = v[0];
+    wait_vm_n<16>(v);
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int it = i0 + i;
-      if (it >= KI || w + it * kWaves >= n_items) continue;
+      if (it >= KI || ids[it] < 0) continue;
       f4 sacc = v[i * GT];
 #pragma unroll
       for (int gi = 1; gi < GT; ++gi) sacc += v[i * GT + gi];
-      gg[it][0] = sacc.x;
-      gg[it][1] = sacc.y;
-      gg[it][2] = sacc.z;
-      gg[it][3] = sacc.w;
+      xg[it] = sacc;
     }
+  }
+}
+
+// First level of the two-level exchange for G = GT workgroups: this wave sums the G
+// partials of its slots sl = grp + r * GT (group order) and publishes them. All of those
+// loads (<= KI + GT - 1) are issued back to back before ONE wait; slot ids are computed by
+// slot_id (register arrays indexed by the run-time grp would go to scratch).
+template <int GT, int KI, typename SlotId>
+__device__ __forceinline__ void reduce_slots(const float* slab, float* red, size_t gs, int grp, int lane, const SlotId& slot_id) {
+  constexpr int RM = (KI + GT - 1) / GT;
+  f4 v[RM * GT];
+  int rid[RM];
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int sl = grp + r * GT;
+    rid[r] = sl < KI ? slot_id(sl) : -1;
+    const int id = rid[r] >= 0 ? rid[r] : 0;
+#pragma unroll
+    for (int gi = 0; gi < GT; ++gi) v[r * GT + gi] = ld_sc1_x4(slab + (size_t)gi * gs + (size_t)id * 256 + lane * 4);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int e = 0; e < RM * GT; ++e) asm volatile("" : "+v"(v[e])::"memory");  // results tied to the wait
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    if (rid[r] < 0) continue;
+    f4 sacc = v[r * GT];
+#pragma unroll
+    for (int gi = 1; gi < GT; ++gi) sacc += v[r * GT + gi];
+    st_sc1_x4(red + (size_t)rid[r] * 256 + lane * 4, sacc);
   }
 }
 
@@ -315,40 +344,31 @@ __device__ __forceinline__ void exchange_sum(const float* slab, int n_items, int
 // 16-byte LDS load; the N accumulation chains are interleaved step by step.
 template <int N, int CWT>
 __device__ __forceinline__ void dw_tiles(const lf* L, const int* izo, const int* iho, int cw, f4* acc) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) acc[i] = {0.f, 0.f, 0.f, 0.f};
   const int ng = (CWT > 0 ? CWT : cw) >> 4;
+  // acc holds the running sums on entry (accumulated into). Items in groups of 4: four independent accumulation chains keep the MFMA pipe busy,
+  // and only the group's operands (8 x f4) are live instead of all N items'
 #pragma unroll
-  for (int gi = 0; gi < (CWT > 0 ? CWT / 16 : 4); ++gi) {
-    if (CWT == 0 && gi >= ng) break;
-    f4 z[N], h[N];
+  for (int i0 = 0; i0 < N; i0 += 4) {
+    constexpr int GS = 4;
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      z[i] = *(const lf4*)(L + izo[i] + 4 * gi);
-      h[i] = *(const lf4*)(L + iho[i] + 4 * gi);
+    for (int gi = 0; gi < (CWT > 0 ? CWT / 16 : 4); ++gi) {
+      if (CWT == 0 && gi >= ng) break;
+      f4 z[GS], h[GS];
+#pragma unroll
+      for (int i = 0; i < GS; ++i) {
+        if (i0 + i >= N) continue;
+        z[i] = *(const lf4*)(L + izo[i0 + i] + 4 * gi);
+        h[i] = *(const lf4*)(L + iho[i0 + i] + 4 * gi);
+      }
+#pragma unroll
+      for (int i = 0; i < GS; ++i) {
+        if (i0 + i >= N) continue;
+        acc[i0 + i] = mfma(z[i].x, h[i].x, acc[i0 + i]);
+        acc[i0 + i] = mfma(z[i].y, h[i].y, acc[i0 + i]);
+        acc[i0 + i] = mfma(z[i].z, h[i].z, acc[i0 + i]);
+        acc[i0 + i] = mfma(z[i].w, h[i].w, acc[i0 + i]);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      acc[i] = mfma(z[i].x, h[i].x, acc[i]);
-      acc[i] = mfma(z[i].y, h[i].y, acc[i]);
-      acc[i] = mfma(z[i].z, h[i].z, acc[i]);
-      acc[i] = mfma(z[i].w, h[i].w, acc[i]);
-    }
-  }
-}
-
-template <int KI, int CWT>
-__device__ __forceinline__ void dw_tiles_n(const lf* L, const int* izo, const int* iho, int cw, int n, f4* acc) {
-  switch (n) {
-    case 1: dw_tiles<1, CWT>(L, izo, iho, cw, acc); break;
-    case 2: dw_tiles<(KI >= 2 ? 2 : 1), CWT>(L, izo, iho, cw, acc); break;
-    case 3: dw_tiles<(KI >= 3 ? 3 : 1), CWT>(L, izo, iho, cw, acc); break;
-    case 4: dw_tiles<(KI >= 4 ? 4 : 1), CWT>(L, izo, iho, cw, acc); break;
-    case 5: dw_tiles<(KI >= 5 ? 5 : 1), CWT>(L, izo, iho, cw, acc); break;
-    case 6: dw_tiles<(KI >= 6 ? 6 : 1), CWT>(L, izo, iho, cw, acc); break;
-    case 7: dw_tiles<(KI >= 7 ? 7 : 1), CWT>(L, izo, iho, cw, acc); break;
-    case 8: dw_tiles<(KI >= 8 ? 8 : 1), CWT>(L, izo, iho, cw, acc); break;
-    default: break;
   }
 }
 
@@ -356,15 +376,28 @@ __device__ __forceinline__ void dw_tiles_n(const lf* L, const int* izo, const in
 // activation), HWT (hidden width) fold the per-layer loop bounds, tile counts and the
 // activation switch at compile time; 0 / -1 = read them at run time (generic build).
 // DT: action head (0 Gaussian, 1 categorical, -1 read at run time).
-template <int KT, int KI, int S0T, int NLT, int ACTT, int HWT, int CWT, int DT>
-__global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) {
+// NW: waves per workgroup. 8 (512 threads, 2 waves per SIMD) for the <= 32-wide nets; 4
+// (256 threads, ONE wave per SIMD) for the 64-wide ones, whose owned gradient / Adam state
+// (up to 16 items x 12 floats per lane) and 64-wide activation tiles need more than the 256
+// registers a wave gets at 2 waves / SIMD: at 1 wave / SIMD the wave has the whole 512-entry
+// VGPR + AGPR file, and nothing goes to scratch.
+// KW / KB: weight-tile / bias-vector slots per wave. Wave w owns weight items w + it * NW
+// (it < KW; a 16 x 16 tile, 4 elements per lane) and bias / log_std items n_witems + w + ib * NW
+// (ib < KB; one element per lane), so the owned state is 12 KW + 3 KB floats per lane and
+// every slot's kind is known at compile time.
+template <int KT, int KW, int KB, int S0T, int NLT, int ACTT, int HWT, int CWT, int DT, int NW>
+__global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) {
+  constexpr int KI = KW + KB;
+  constexpr int kThreads = 64 * NW;
+  constexpr int kWaves = NW;
+  constexpr int kHalf = NW / 2;  // row-tile waves per net
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* L = (lf*)lds_raw;
   const int tid = threadIdx.x;
   const int w = rfl(tid >> 6), lane = tid & 63;
   const int r16 = lane & 15, kk = lane >> 4;
-  const int q = w >> 2;   // 0 actor, 1 critic
-  const int gw = w & 3;   // row tile
+  const int q = w / kHalf;  // 0 actor, 1 critic
+  const int gw = w % kHalf;  // row tile
   const int grp = blockIdx.x;
   const int G = g.G, nch = g.nch, cw = CWT > 0 ? CWT : g.cw;
   const int CH = G * nch;
@@ -418,37 +451,49 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     run_c = a.norm_count[0];
   }
   // owned items: gradient / moments registers
-  float gm[KI][4], gv[KI][4], gg[KI][4];
+  const int n_witems = rfl(g.n_witems);
+  float gm[KW][4], gv[KW][4];  // weight tiles: Adam moments
+  f4 gg[KW];                   // and gradient (the dW MFMA chains accumulate into it)
+  float bm[KB], bv[KB], bg[KB];           // bias / log_std vectors
 #pragma unroll
-  for (int it = 0; it < KI; ++it) {
+  for (int it = 0; it < KW; ++it) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) gm[it][j] = gv[it][j] = gg[it][j] = 0.f;
+    for (int j = 0; j < 4; ++j) gm[it][j] = gv[it][j] = 0.f;
+    gg[it] = {0.f, 0.f, 0.f, 0.f};
     const int id = w + it * kWaves;
+    if (id < n_witems) {
+      const int desc = rfl(g.items[id]);
+      const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+      const int din = g.din[iq][il], dout = g.dout[iq][il];
+      const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
+      const int in = 16 * tb + r16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = 16 * ta + 4 * kk + j;
+        if (o < dout && in < din) {
+          gm[it][j] = a.exp_avg[wo + o * din + in];
+          gv[it][j] = a.exp_avg_sq[wo + o * din + in];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int ib = 0; ib < KB; ++ib) {
+    bm[ib] = bv[ib] = bg[ib] = 0.f;
+    const int id = n_witems + w + ib * kWaves;
     if (id < n_items) {
       const int desc = rfl(g.items[id]);
-      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-      if (kind == 0) {
-        const int din = g.din[iq][il], dout = g.dout[iq][il];
-        const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
-        const int in = 16 * tb + r16;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int o = 16 * ta + 4 * kk + j;
-          if (o < dout && in < din) {
-            gm[it][j] = a.exp_avg[wo + o * din + in];
-            gv[it][j] = a.exp_avg_sq[wo + o * din + in];
-          }
-        }
-      } else if (kind == 1) {
+      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3;
+      if (kind == 1) {
         const int dout = g.dout[iq][il];
         const int bo = iq == 0 ? a.pi_b_off[il] : a.vf_b_off[il];
         if (lane < dout) {
-          gm[it][0] = a.exp_avg[bo + lane];
-          gv[it][0] = a.exp_avg_sq[bo + lane];
+          bm[ib] = a.exp_avg[bo + lane];
+          bv[ib] = a.exp_avg_sq[bo + lane];
         }
       } else if (has_ls && lane < A) {
-        gm[it][0] = a.exp_avg[a.log_std_off + lane];
-        gv[it][0] = a.exp_avg_sq[a.log_std_off + lane];
+        bm[ib] = a.exp_avg[a.log_std_off + lane];
+        bv[ib] = a.exp_avg_sq[a.log_std_off + lane];
       }
     }
   }
@@ -467,58 +512,32 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     L[g.nm_off + nc] = run_m;
     L[g.nm_off + 64 + nc] = rsqrtf(run_v + a.norm_eps);
   }
-  // dW item operands (LDS offsets of this lane's dZ / H columns; padding items read zeros)
-  // (weight items are ids [0, n_witems): this wave's are its first nwi slots)
-  const int n_witems = rfl(g.n_witems);
-  const int nwi = n_witems > w ? min(KI, (n_witems - w + kWaves - 1) / kWaves) : 0;
+  // dW item operands: this wave's valid weight slots are its first nwi (ids < n_witems);
+  // the LDS offsets of a slot's dZ / H columns are a wave-uniform base (the descriptor) plus
+  // ONE lane term shared by every slot (all K-major images have the row stride cw + 4)
+  const int nwi = n_witems > w ? min(KW, (n_witems - w + kWaves - 1) / kWaves) : 0;
   const int rq = cw / 4;  // K-major image: row r at (r & 3) * rq + (r >> 2)
-  int izo[KI], iho[KI];
+  const int ldr = rfl(g.ldz[0][0]);
+  const int lterm = r16 * ldr + kk * rq;
+  // bias / log_std slots: kind (1 bias, 2 log_std, -1 empty), partial source, element mask
+  int bkind[KB], b_off[KB], b_addr[KB];
+  float b_okf[KB];  // 1 for lanes holding a real bias / log_std element
 #pragma unroll
-  for (int it = 0; it < KI; ++it) {
-    const int id = w + it * kWaves;
-    izo[it] = iho[it] = g.zero_off;
-    if (id < n_items) {
-      const int desc = rfl(g.items[id]);
-      const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-      if (kind == 0) {
-        const LG y = lg(g, iq, il);
-        izo[it] = y.z + (16 * ta + r16) * y.ldz + kk * rq;
-        iho[it] = y.h + (16 * tb + r16) * y.ldh + kk * rq;
-      }
-    }
-  }
-  // loop-invariant item bookkeeping (kind, bias-partial source, Adam targets), computed once
-  // instead of re-reading the descriptors and layer geometry every minibatch
-  // paddr: LDS address of each owned element; padding elements point at a 64-float trash
-  // row (Adam then runs branch-free: their gradient and moments stay 0)
-  int ikind[KI], ib_off[KI], paddr[KI][4];
-  float ib_okf[KI];  // 1 for lanes holding a real bias / log_std element
-#pragma unroll
-  for (int it = 0; it < KI; ++it) {
-    const int id = w + it * kWaves;
-    ikind[it] = -1;
-    ib_off[it] = 0;
-    ib_okf[it] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) paddr[it][j] = g.trash_off + lane;
+  for (int ib = 0; ib < KB; ++ib) {
+    const int id = n_witems + w + ib * kWaves;
+    bkind[ib] = -1;
+    b_off[ib] = 0;
+    b_okf[ib] = 0.f;
+    b_addr[ib] = g.trash_off + lane;
     if (id >= n_items) continue;
     const int desc = rfl(g.items[id]);
-    const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+    const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3;
     const LG y = lg(g, iq, il);
-    ikind[it] = kind;
-    if (kind == 0) {
-      const int in = 16 * tb + r16;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int o = 16 * ta + 4 * kk + j;
-        if (o < y.dout && in < y.din) paddr[it][j] = y.w + o * y.ldw + in;
-      }
-    } else {
-      ib_off[it] = kind == 1 ? y.db : g.lsp_off;
-      const bool ok = kind == 1 ? (lane < y.dout) : (has_ls && lane < A);
-      ib_okf[it] = ok ? 1.f : 0.f;
-      if (ok) paddr[it][0] = kind == 1 ? y.b + lane : g.ls_off + lane;
-    }
+    bkind[ib] = kind;
+    b_off[ib] = kind == 1 ? y.db : g.lsp_off;
+    const bool ok = kind == 1 ? (lane < y.dout) : (has_ls && lane < A);
+    b_okf[ib] = ok ? 1.f : 0.f;
+    if (ok) b_addr[ib] = kind == 1 ? y.b + lane : g.ls_off + lane;
   }
   float pre_m = 0.f, pre_v = 0.f;  // moments of the next minibatch to merge
   if (norm_lane && K > 1) {
@@ -546,9 +565,9 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     unsigned long long t0 = a.prof ? clock64() : 0;
     const int nb = (k & 1) * 128;  // norm buffer of minibatch k
 #pragma unroll
-    for (int it = 0; it < KI; ++it)
+    for (int it = 0; it < KW; ++it) gg[it] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) gg[it][j] = 0.f;
+    for (int ib = 0; ib < KB; ++ib) bg[ib] = 0.f;
     for (int ch = 0; ch < nch; ++ch) {
       const int u = k * nch + ch;
       Rows nxt;
@@ -603,7 +622,22 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           f4 acc[KT];
 #pragma unroll
           for (int t = 0; t < KT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-          if (l == 0) {
+          if (l == 0 && KT > 2) {  // 64-wide: two tiles' operands at a time (register budget)
+#pragma unroll
+            for (int t0 = 0; t0 < KT; t0 += 2) {
+              float w0[2][16];
+#pragma unroll
+              for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 16; ++s)
+                  if (t0 + t < tout && s < s0) w0[t][s] = L[y.w + (16 * (t0 + t) + r16) * y.ldw + 4 * s + kk];
+#pragma unroll
+              for (int s = 0; s < 16; ++s)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                  if (t0 + t < tout && s < s0) acc[t0 + t] = mfma(w0[t][s], xb[s], acc[t0 + t]);
+            }
+          } else if (l == 0) {
             float w0[KT][16];
 #pragma unroll
             for (int t = 0; t < KT; ++t)
@@ -794,8 +828,8 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
           // W_l^T operands (W[16 tt + 4 kk + j][16 u2 + r16]) read before this layer's
           // image stores, so the loads are not ordered behind them
-          constexpr int KW = KT > 2 ? 1 : KT;  // 64-wide: W^T read per tile below (register budget)
-          float wt[KW][KW][4];
+          constexpr int KWT = KT > 2 ? 1 : KT;  // 64-wide: W^T read per tile below (register budget)
+          float wt[KWT][KWT][4];
           if (KT <= 2 && l > 0) {
 #pragma unroll
             for (int u2 = 0; u2 < KT; ++u2)
@@ -803,7 +837,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
               for (int tt = 0; tt < KT; ++tt)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                  if (u2 < tin && tt < tout) wt[u2 % KW][tt % KW][j] = L[y.w + (16 * tt + 4 * kk + j) * y.ldw + 16 * u2 + r16];
+                  if (u2 < tin && tt < tout) wt[u2 % KWT][tt % KWT][j] = L[y.w + (16 * tt + 4 * kk + j) * y.ldw + 16 * u2 + r16];
           }
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) {
@@ -831,7 +865,7 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
               for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int u2 = 0; u2 < KT; ++u2)
-                  if (u2 < tin && tt < tout) accb[u2] = mfma(wt[u2 % KW][tt % KW][j], dzc[tt][j], accb[u2]);
+                  if (u2 < tin && tt < tout) accb[u2] = mfma(wt[u2 % KWT][tt % KWT][j], dzc[tt][j], accb[u2]);
           } else {
 #pragma unroll
             for (int u2 = 0; u2 < KT; ++u2) {
@@ -888,25 +922,32 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 
       // ---------------- dW / db / dlog_std partials of this chunk for the owned items
       {
-        f4 acc[KI];
-        dw_tiles_n<KI, CWT>(L, izo, iho, cw, nwi, acc);
+        int izo[KW], iho[KW];
 #pragma unroll
-        for (int it = 0; it < KI; ++it) {
-          if (it >= nwi) continue;
-          gg[it][0] += acc[it].x;  // padding entries are exactly 0 (zeroed images)
-          gg[it][1] += acc[it].y;
-          gg[it][2] += acc[it].z;
-          gg[it][3] += acc[it].w;
+        for (int it = 0; it < KW; ++it) {
+          izo[it] = iho[it] = g.zero_off;
+          const int id = w + it * kWaves;
+          if (it < nwi) {
+            const int desc = rfl(g.items[id]);
+            const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+            izo[it] = rfl(g.z_off[iq][il]) + 16 * ta * ldr + lterm;
+            iho[it] = rfl(g.h_off[iq][il]) + 16 * tb * ldr + lterm;
+          }
         }
+        // the chunk's dZ^T H continues each slot's MFMA chain from its running gradient
+        // (padding entries are exactly 0: zeroed images)
+        // (empty slots read the zero row: their MFMAs add zeros to gradients nobody reads,
+        // so every wave runs the same straight-line body)
+        dw_tiles<KW, CWT>(L, izo, iho, cw, gg);
       }
 #pragma unroll
-      for (int it = 0; it < KI; ++it) {
-        if (ikind[it] <= 0) continue;
+      for (int ib = 0; ib < KB; ++ib) {
+        if (bkind[ib] <= 0) continue;
         {  // bias (row-tile partials of dZ) / log_std (partials of the Gaussian term)
-          const int stride = ikind[it] == 1 ? 64 : 16;
-          float gval = 0.f;  // (lanes past the vector read finite neighbours, masked by ib_okf)
-          for (int r = 0; r < RT; ++r) gval += L[ib_off[it] + r * stride + lane];
-          gg[it][0] += gval * ib_okf[it];
+          const int stride = bkind[ib] == 1 ? 64 : 16;
+          float gval = 0.f;  // (lanes past the vector read finite neighbours, masked by b_okf)
+          for (int r = 0; r < RT; ++r) gval += L[b_off[ib] + r * stride + lane];
+          bg[ib] += gval * b_okf[ib];
         }
       }
       if (a.prof && tid == 0) {
@@ -920,13 +961,24 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
 
     // ---------------- cross-workgroup exchange of the partials (G > 1)
     if (G > 1) {
+      // owned slots as one list: weight tiles, then bias / log_std vectors ({g, 0, 0, 0})
+      int ids[KI];
+      f4 xg[KI];
+#pragma unroll
+      for (int it = 0; it < KW; ++it) {
+        ids[it] = it < nwi ? w + it * kWaves : -1;
+        xg[it] = gg[it];
+      }
+#pragma unroll
+      for (int ib = 0; ib < KB; ++ib) {
+        ids[KW + ib] = bkind[ib] >= 0 ? n_witems + w + ib * kWaves : -1;
+        xg[KW + ib] = {bg[ib], 0.f, 0.f, 0.f};
+      }
       float* slab = g.slab + (size_t)(k & 1) * G * n_items * 256;
 #pragma unroll
       for (int it = 0; it < KI; ++it) {
-        const int id = w + it * kWaves;
-        if (id >= n_items) continue;
-        const f4 v = {gg[it][0], gg[it][1], gg[it][2], gg[it][3]};
-        st_sc1_x4(slab + ((size_t)grp * n_items + id) * 256 + lane * 4, v);
+        if (ids[it] < 0) continue;
+        st_sc1_x4(slab + ((size_t)grp * n_items + ids[it]) * 256 + lane * 4, xg[it]);
       }
       const unsigned long long e0 = a.prof ? clock64() : 0;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -947,32 +999,43 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
       __syncthreads();
       const unsigned long long e2 = a.prof ? clock64() : 0;
       if (g.xchg2) {
-        // Two-level exchange (large G): workgroup grp sums ONLY the items of its wave slots
-        // it with it % G == grp (ids kWaves*it .. kWaves*it + 7: one item per wave, so the
-        // waves reduce in parallel) over the G partials -- group order, the same additions as
-        // the one-level sum -- and publishes them; after a second arrival every workgroup
-        // reads the n_items reduced tiles once: per-workgroup loads ~2 x n_items KB instead
-        // of G x n_items KB.
+        // Two-level exchange (large G): slot it of every wave is reduced by workgroup
+        // it % G, so each wave of each workgroup sums ~KI / G of its slots over the G
+        // partials -- group order, the same additions as the one-level sum -- and publishes
+        // them; after a second arrival every workgroup reads the n_items reduced tiles once:
+        // per-workgroup loads ~2 x n_items KB instead of G x n_items KB. The partial loads of
+        // all the wave's reduced slots are issued back to back, 16 in flight per wait.
         float* red = g.red + (size_t)(k & 1) * n_items * 256;
         const size_t gs = (size_t)n_items * 256;
+        const auto slot_id = [&](int sl) -> int {  // item id of owned slot sl (computed: no array lookup)
+          if (sl < KW) return sl < nwi ? w + sl * kWaves : -1;
+          const int id = n_witems + w + (sl - KW) * kWaves;
+          return id < n_items ? id : -1;
+        };
+        if (G == 2) reduce_slots<2, KI>(slab, red, gs, grp, lane, slot_id);
+        else if (G == 4) reduce_slots<4, KI>(slab, red, gs, grp, lane, slot_id);
+        else if (G == 8) reduce_slots<8, KI>(slab, red, gs, grp, lane, slot_id);
+        else if (G == 16) reduce_slots<16, KI>(slab, red, gs, grp, lane, slot_id);
+        else {  // G > 16 (or odd): slot it is reduced by workgroup it % G, 16 loads in flight
 #pragma unroll
-        for (int it = 0; it < KI; ++it) {
-          const int id = w + it * kWaves;
-          if (id >= n_items || it % G != grp) continue;
-          const float* p = slab + (size_t)id * 256 + lane * 4;
-          f4 sacc = {0.f, 0.f, 0.f, 0.f};
-          for (int gi0 = 0; gi0 < G; gi0 += 8) {  // 8 loads in flight, one wait per batch
-            f4 v[8];
+          for (int it = 0; it < KI; ++it) {
+            const int id = ids[it];
+            if (id < 0 || it % G != grp) continue;
+            const float* p = slab + (size_t)id * 256 + lane * 4;
+            f4 sacc = {0.f, 0.f, 0.f, 0.f};
+            for (int gi0 = 0; gi0 < G; gi0 += 16) {
+              f4 v[16];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = ld_sc1_x4(p + (size_t)(gi0 + e < G ? gi0 + e : 0) * gs);
-            wait_vm8(v);
-            if (gi0 == 0) sacc = v[0];
-            else sacc += v[0];
+              for (int e = 0; e < 16; ++e) v[e] = ld_sc1_x4(p + (size_t)(gi0 + e < G ? gi0 + e : 0) * gs);
+              wait_vm_n<16>(v);
+              if (gi0 == 0) sacc = v[0];
+              else sacc += v[0];
 #pragma unroll
-            for (int e = 1; e < 8; ++e)
-              if (gi0 + e < G) sacc += v[e];
+              for (int e = 1; e < 16; ++e)
+                if (gi0 + e < G) sacc += v[e];
+            }
+            st_sc1_x4(red + (size_t)id * 256 + lane * 4, sacc);
           }
-          st_sc1_x4(red + (size_t)id * 256 + lane * 4, sacc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -989,48 +1052,44 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
           }
         }
         __syncthreads();
-        f4 v[KI];
+#pragma unroll
+        for (int it = 0; it < KI; ++it) xg[it] = ld_sc1_x4(red + (size_t)(ids[it] >= 0 ? ids[it] : 0) * 256 + lane * 4);
+        wait_vm_n<KI>(xg);  // results tied to the wait (inline-asm loads are invisible to the compiler)
+      } else if (G == 2) {
+        exchange_sum<2, KI>(slab, n_items, ids, lane, xg);
+      } else if (G == 4) {
+        exchange_sum<4, KI>(slab, n_items, ids, lane, xg);
+      } else if (G == 8) {
+        exchange_sum<8, KI>(slab, n_items, ids, lane, xg);
+      } else {
 #pragma unroll
         for (int it = 0; it < KI; ++it) {
-          const int id = w + it * kWaves;
-          v[it] = ld_sc1_x4(red + (size_t)(id < n_items ? id : w) * 256 + lane * 4);
+          if (ids[it] < 0) continue;
+          f4 sacc = {0.f, 0.f, 0.f, 0.f};
+          const float* p = slab + (size_t)ids[it] * 256 + lane * 4;
+          const size_t gs = (size_t)n_items * 256;
+          for (int gi = 0; gi < G; gi += 4) {  // any count: tail lanes read group 0
+            f4 v0 = ld_sc1_x4(p + (size_t)gi * gs);
+            f4 v1 = ld_sc1_x4(p + (size_t)(gi + 1 < G ? gi + 1 : 0) * gs);
+            f4 v2 = ld_sc1_x4(p + (size_t)(gi + 2 < G ? gi + 2 : 0) * gs);
+            f4 v3 = ld_sc1_x4(p + (size_t)(gi + 3 < G ? gi + 3 : 0) * gs);
+            wait_vm4(v0, v1, v2, v3);
+            sacc += v0;
+            if (gi + 1 < G) sacc += v1;
+            if (gi + 2 < G) sacc += v2;
+            if (gi + 3 < G) sacc += v3;
+          }
+          xg[it] = sacc;
         }
-        wait_vm_n<KI>(v);  // results tied to the wait (inline-asm loads are invisible to the compiler)
-#pragma unroll
-        for (int it = 0; it < KI; ++it) {
-          if (w + it * kWaves >= n_items) continue;
-          gg[it][0] = v[it].x;
-          gg[it][1] = v[it].y;
-          gg[it][2] = v[it].z;
-          gg[it][3] = v[it].w;
-        }
-      } else       if (G == 2) exchange_sum<2, KI>(slab, n_items, w, lane, gg);
-      else if (G == 4) exchange_sum<4, KI>(slab, n_items, w, lane, gg);
-      else if (G == 8) exchange_sum<8, KI>(slab, n_items, w, lane, gg);
-      else
-#pragma unroll
-      for (int it = 0; it < KI; ++it) {
-        const int id = w + it * kWaves;
-        if (id >= n_items) continue;
-        f4 s = {0.f, 0.f, 0.f, 0.f};
-        const float* p = slab + (size_t)id * 256 + lane * 4;
-        const size_t gs = (size_t)n_items * 256;
-        for (int gi = 0; gi < G; gi += 4) {  // G is 1, 2, 4, 8 or 16 .. any count: tail lanes read group 0
-          f4 v0 = ld_sc1_x4(p + (size_t)gi * gs);
-          f4 v1 = ld_sc1_x4(p + (size_t)(gi + 1 < G ? gi + 1 : 0) * gs);
-          f4 v2 = ld_sc1_x4(p + (size_t)(gi + 2 < G ? gi + 2 : 0) * gs);
-          f4 v3 = ld_sc1_x4(p + (size_t)(gi + 3 < G ? gi + 3 : 0) * gs);
-          wait_vm4(v0, v1, v2, v3);
-          s += v0;
-          if (gi + 1 < G) s += v1;
-          if (gi + 2 < G) s += v2;
-          if (gi + 3 < G) s += v3;
-        }
-        gg[it][0] = s.x;
-        gg[it][1] = s.y;
-        gg[it][2] = s.z;
-        gg[it][3] = s.w;
       }
+#pragma unroll
+      for (int it = 0; it < KW; ++it) {
+        if (ids[it] < 0) continue;
+        gg[it] = xg[it];
+      }
+#pragma unroll
+      for (int ib = 0; ib < KB; ++ib)
+        if (ids[KW + ib] >= 0) bg[ib] = xg[KW + ib].x;
       if (a.prof && tid == 0) {
         sprof[13] += e1 - e0;
         sprof[14] += e2 - e1;
@@ -1040,11 +1099,16 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     // entropy term of log_std (d(-ent_coef * H)/d log_std = -ent_coef), once per minibatch; |g|^2
     float ss = 0.f;
 #pragma unroll
-    for (int it = 0; it < KI; ++it) {
-      if (ikind[it] < 0) continue;
-      if (ikind[it] == 2) gg[it][0] -= a.ent_coef * ib_okf[it];
+    for (int it = 0; it < KW; ++it) {
+      if (it >= nwi) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ss += gg[it][j] * gg[it][j];
+    }
+#pragma unroll
+    for (int ib = 0; ib < KB; ++ib) {
+      if (bkind[ib] < 0) continue;
+      if (bkind[ib] == 2) bg[ib] -= a.ent_coef * b_okf[ib];
+      ss += bg[ib] * bg[ib];
     }
     ss = wave_sum(ss);
     if (lane == 0) L[g.red_off + w] = ss;
@@ -1071,21 +1135,50 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
     // torch Adam: p -= step_size * m / (sqrt(v) / sqrt(1 - b2^t) + eps), on v_sqrt / v_rcp
     // (~1 ulp each). All of this wave's parameter reads are issued before any write
     // (the items never alias), so the LDS read latency is paid once, not per element.
-    float pval[KI][4];
+    // Weight element j of slot it lives at W[16 ta + 4 kk + j][16 tb + r16] of its layer
+    // image; padding elements (rows / columns past the layer dims) have gradient and
+    // moments exactly 0, so their update is exactly 0 and they are updated in place.
+    int paddr[KW];
+    int pstr[KW];
 #pragma unroll
-    for (int it = 0; it < KI; ++it)
+    for (int it = 0; it < KW; ++it) {
+      paddr[it] = g.trash_off + lane;
+      pstr[it] = 0;
+      if (it < nwi) {
+        const int desc = rfl(g.items[w + it * kWaves]);
+        const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+        const int ldw = rfl(g.ldw[iq][il]);
+        paddr[it] = rfl(g.w_off[iq][il]) + (16 * ta + 4 * kk) * ldw + 16 * tb + r16;
+        pstr[it] = ldw;
+      }
+    }
+    float pval[KW][4], bval[KB];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pval[it][j] = L[paddr[it][j]];
+    for (int it = 0; it < KW; ++it)
 #pragma unroll
-    for (int it = 0; it < KI; ++it) {
+      for (int j = 0; j < 4; ++j) pval[it][j] = L[paddr[it] + j * pstr[it]];
+#pragma unroll
+    for (int ib = 0; ib < KB; ++ib) bval[ib] = L[b_addr[ib]];
+#pragma unroll
+    for (int it = 0; it < KW; ++it) {
+      if (it >= nwi) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float gval = gg[it][j] * coef;
         gm[it][j] = b1 * gm[it][j] + (1.f - b1) * gval;
         gv[it][j] = b2 * gv[it][j] + (1.f - b2) * gval * gval;
         const float denom = __builtin_amdgcn_sqrtf(gv[it][j]) * inv_bc2s + eps;
-        L[paddr[it][j]] = pval[it][j] - step_size * gm[it][j] * __builtin_amdgcn_rcpf(denom);
+        L[paddr[it] + j * pstr[it]] = pval[it][j] - step_size * gm[it][j] * __builtin_amdgcn_rcpf(denom);
       }
+    }
+#pragma unroll
+    for (int ib = 0; ib < KB; ++ib) {
+      if (bkind[ib] < 0) continue;
+      const float gval = bg[ib] * coef;
+      bm[ib] = b1 * bm[ib] + (1.f - b1) * gval;
+      bv[ib] = b2 * bv[ib] + (1.f - b2) * gval * gval;
+      const float denom = __builtin_amdgcn_sqrtf(bv[ib]) * inv_bc2s + eps;
+      L[b_addr[ib]] = bval[ib] - step_size * bm[ib] * __builtin_amdgcn_rcpf(denom);
     }
     __syncthreads();  // B3: parameters updated
     if (a.prof && tid == 0) {
@@ -1131,34 +1224,30 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   }
   if (has_ls && tid < A) a.params[a.log_std_off + tid] = L[g.ls_off + tid];
 #pragma unroll
-  for (int it = 0; it < KI; ++it) {
-    const int id = w + it * kWaves;
-    if (id >= n_items) continue;
-    const int desc = rfl(g.items[id]);
-    const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-    if (kind == 0) {
-      const int din = g.din[iq][il], dout = g.dout[iq][il];
-      const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
-      const int in = 16 * tb + r16;
+  for (int it = 0; it < KW; ++it) {
+    if (it >= nwi) continue;
+    const int desc = rfl(g.items[w + it * kWaves]);
+    const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+    const int din = g.din[iq][il], dout = g.dout[iq][il];
+    const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
+    const int in = 16 * tb + r16;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int o = 16 * ta + 4 * kk + j;
-        if (o < dout && in < din) {
-          a.exp_avg[wo + o * din + in] = gm[it][j];
-          a.exp_avg_sq[wo + o * din + in] = gv[it][j];
-        }
+    for (int j = 0; j < 4; ++j) {
+      const int o = 16 * ta + 4 * kk + j;
+      if (o < dout && in < din) {
+        a.exp_avg[wo + o * din + in] = gm[it][j];
+        a.exp_avg_sq[wo + o * din + in] = gv[it][j];
       }
-    } else if (kind == 1) {
-      const int dout = g.dout[iq][il];
-      const int bo = iq == 0 ? a.pi_b_off[il] : a.vf_b_off[il];
-      if (lane < dout) {
-        a.exp_avg[bo + lane] = gm[it][0];
-        a.exp_avg_sq[bo + lane] = gv[it][0];
-      }
-    } else if (has_ls && lane < A) {
-      a.exp_avg[a.log_std_off + lane] = gm[it][0];
-      a.exp_avg_sq[a.log_std_off + lane] = gv[it][0];
     }
+  }
+#pragma unroll
+  for (int ib = 0; ib < KB; ++ib) {
+    if (bkind[ib] < 0 || b_okf[ib] == 0.f) continue;
+    const int desc = rfl(g.items[n_witems + w + ib * kWaves]);
+    const int iq = desc & 1, il = (desc >> 1) & 3;
+    const int off = bkind[ib] == 1 ? (iq == 0 ? a.pi_b_off[il] : a.vf_b_off[il]) : a.log_std_off;
+    a.exp_avg[off + lane] = bm[ib];
+    a.exp_avg_sq[off + lane] = bv[ib];
   }
   if (norm_lane && K > 0) {
     a.norm_mean[nc] = run_m;
@@ -1169,7 +1258,11 @@ __global__ __launch_bounds__(kThreads) void ppo_rc_kernel(PPOArgs a, PPORcGeo g)
   if (a.prof && tid < 16) a.prof[tid] += sprof[tid];  // (stats barrier above orders the LDS)
 }
 
-constexpr int items_per_wave(int kt) { return kt == 2 ? 4 : 8; }
+// waves per workgroup (NW) and owned weight / bias slots per wave of each tile width
+// (generic builds; the shape-specialised ones size KW / KB to their exact item counts)
+constexpr int waves_for(int kt) { return kt == 2 ? 8 : 4; }
+constexpr int wslots_for(int kt) { return kt == 2 ? 5 : 16; }
+constexpr int bslots_for(int kt) { return kt == 2 ? 2 : 3; }
 
 }  // namespace
 
@@ -1187,7 +1280,9 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   if (wmax > 64) return false;
   g.kt = wmax <= 32 ? 2 : 4;
   const int KT = g.kt;
-  // workgroup split: chunks of cw rows (64 for narrow nets, 32 for 64-wide ones: LDS)
+  g.nw = waves_for(KT);
+  // workgroup split: chunks of cw rows (64 for narrow nets, 32 for 64-wide ones: LDS, and
+  // the 4-wave workgroup has 2 row-tile waves per net)
   int cw = KT == 2 ? 64 : 32;
   if (a.rc_cw == 16 || a.rc_cw == 32 || (a.rc_cw == 64 && KT == 2)) cw = a.rc_cw;
   if (a.batch < cw) cw = a.batch;
@@ -1281,7 +1376,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     g.items[n++] = 2 << 3;
   }
   g.n_items = n;
-  if ((n + kWaves - 1) / kWaves > items_per_wave(KT)) return false;
+  if ((g.n_witems + g.nw - 1) / g.nw > wslots_for(KT) || (n - g.n_witems + g.nw - 1) / g.nw > bslots_for(KT)) return false;
   g.dp = (a.D + 3) & ~3;
   return true;
 }
@@ -1308,9 +1403,10 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   g.slab = g.mom + K * 128;
   g.red = g.slab + 2 * (size_t)g.G * g.n_items * 256;
   g.sync = reinterpret_cast<unsigned*>(g.red + 2 * (size_t)g.n_items * 256);
-  {  // two-level exchange from 16 cooperating workgroups (IMITATION_AMD_PPO_XCHG2=0/1 forces it)
+  {  // two-level exchange from 4 (64-wide nets) / 16 (<= 32-wide) cooperating workgroups
+     // (IMITATION_AMD_PPO_XCHG2=0/1 forces it; measured: profiles/r3_ppo64_scale.md)
     const char* ev = getenv("IMITATION_AMD_PPO_XCHG2");
-    g.xchg2 = ev ? (ev[0] == '1' && g.G > 1) : (g.G >= 16);
+    g.xchg2 = ev ? (ev[0] == '1' && g.G > 1) : (g.G >= (g.kt == 4 ? 4 : 16));
   }
   if (K == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(g.sync, 0, 64 * sizeof(unsigned), s);
@@ -1319,31 +1415,32 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   const int prep_waves = CH < kPrepWaves ? CH : kPrepWaves;
   hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64 * prep_waves), 0, s, a, g);
   // > 80 KiB of LDS keeps the cooperating workgroups one per CU (the measured condition of
-  // the sc1 hand-off); all G <= 16 of them are co-resident on an otherwise idle GPU
+  // the sc1 hand-off); all G <= kMaxRcGroups (64) of them are co-resident (256 CUs)
   const size_t lds_launch = g.G > 1 && lds < 96 * 1024 ? 96 * 1024 : lds;
   // shape-specialised builds for the headline configs, generic otherwise
   int hw = a.pi_dims[1];
   bool uniform = a.n_pi == 3 && a.n_vf == 3;
   for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
   const int s0 = (a.D + 3) / 4;
-  const dim3 grid(g.G), block(kThreads);
-#define IA_RC(KT, KI, S0, NL, ACT, HW, CW, DT) \
-  hipLaunchKernelGGL((ppo_rc_kernel<KT, KI, S0, NL, ACT, HW, CW, DT>), grid, block, lds_launch, s, a, g)
-  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete)
-    IA_RC(2, 4, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
-  else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 32 && !a.discrete)
-    IA_RC(2, 4, 5, 3, 2, 32, 32, 0);  // the same, 32-row chunks (16 workgroups at the 8-rank DP minibatch)
-
-  else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)
-    IA_RC(4, 8, 3, 3, 1, 64, 32, 0);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
-  else if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete)
-    IA_RC(4, 8, 5, 3, 1, 64, 32, 0);  // Walker2d MlpPolicy [64, 64] ReLU (DRLHP seals_walker config)
-  else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && a.discrete)
-    IA_RC(2, 4, 1, 3, 2, 32, 64, 1);  // CartPole FeedForward32Policy
+  const dim3 grid(g.G), block(64 * g.nw);
+  const int nwslot = (g.n_witems + g.nw - 1) / g.nw, nbslot = (g.n_items - g.n_witems + g.nw - 1) / g.nw;
+#define IA_RC(KT, KW, KB, S0, NL, ACT, HW, CW, DT) \
+  hipLaunchKernelGGL((ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, CW, DT, waves_for(KT)>), grid, block, lds_launch, s, a, g)
+  const auto fits = [&](int kw, int kb) { return nwslot <= kw && nbslot <= kb; };
+  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete && fits(3, 1))
+    IA_RC(2, 3, 1, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
+  else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 32 && !a.discrete && fits(3, 1))
+    IA_RC(2, 3, 1, 5, 3, 2, 32, 32, 0);  // the same, 32-row chunks (16 workgroups at the 8-rank DP minibatch)
+  else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete && fits(12, 2))
+    IA_RC(4, 12, 2, 3, 3, 1, 64, 32, 0);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
+  else if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete && fits(14, 2))
+    IA_RC(4, 14, 2, 5, 3, 1, 64, 32, 0);  // Walker2d MlpPolicy [64, 64] ReLU (DRLHP seals_walker config)
+  else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && a.discrete && fits(2, 1))
+    IA_RC(2, 2, 1, 1, 3, 2, 32, 64, 1);  // CartPole FeedForward32Policy
   else if (g.kt == 2)
-    IA_RC(2, 4, 0, 0, -1, 0, 0, -1);
+    IA_RC(2, wslots_for(2), bslots_for(2), 0, 0, -1, 0, 0, -1);
   else
-    IA_RC(4, 8, 0, 0, -1, 0, 0, -1);
+    IA_RC(4, wslots_for(4), bslots_for(4), 0, 0, -1, 0, 0, -1);
 #undef IA_RC
   return hipGetLastError();
 }

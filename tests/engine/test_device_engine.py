@@ -10,7 +10,7 @@ gpu = pytest.mark.gpu
 
 
 def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epochs=2, seed=0, discrete=False,
-           net_arch=None):
+           net_arch=None, activation=None):
     from imitation_amd.data import rollout
     from imitation_amd.engine.gail import DeviceGAIL
     from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
@@ -34,6 +34,8 @@ def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epoc
     if net_arch is not None:
         pk["net_arch"] = net_arch
         policy_cls = ActorCriticPolicy
+    if activation is not None:
+        pk["activation_fn"] = activation
     gen = PPO(policy_cls, venv, n_steps=n_steps, batch_size=batch, n_epochs=n_epochs, device="cuda", seed=seed,
               ent_coef=0.01, policy_kwargs=pk)
     rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
@@ -104,10 +106,19 @@ def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, nor
     # 64-wide nets (AIRL-Hopper MlpPolicy [64, 64]): 32-row chunks
     ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64]), "rc:g2x1x32:kt4"),
     ("seals/Hopper-v1", 1, 256, 4, dict(pi=[64, 64], vf=[64, 64]), "rc:g4x2x32:kt4"),
+    # the shape-specialised 64-wide ReLU builds (4-wave workgroups, owned state in AGPRs):
+    # AIRL-Hopper (minibatch 512 -> 16 workgroups, two-level exchange) and DRLHP-Walker
+    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g2x1x32:kt4"),
+    ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g16x1x32:kt4"),
+    ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g4x1x32:kt4"),
 ])
 def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_arch, path):
-    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=8 if batch > 64 else 4, n_steps=32, batch=batch, n_epochs=2,
-                               net_arch=net_arch)
+    act = None
+    if net_arch is not None and net_arch.get("act") == "relu":
+        net_arch = {k: v for k, v in net_arch.items() if k != "act"}
+        act = th.nn.ReLU
+    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=8 if batch > 64 else 4, n_steps=64 if batch > 256 else 32,
+                               batch=batch, n_epochs=2, net_arch=net_arch, activation=act)
     tr._ppo_static["allow_rc"] = allow_rc
     tr._ppo_static["rc_gmax"] = gmax
     assert tr._C.engine_ppo_path(tr._ppo_static) == path

@@ -1,8 +1,13 @@
-"""Time the replicated data-parallel PPO update of the GAIL-HalfCheetah bench config on ONE GPU.
+"""Time the replicated data-parallel PPO update of a headline config on ONE GPU.
 
 At world size W every rank runs the register-chained kernel over the all-gathered rows
-(W x 4096) with minibatch W x 64 (G = W cooperating workgroups): emulated here with
-8W envs x 512 steps and batch 64W. Prints ms per PPO update for W = 1, 2, 4, 8.
+(W x rows) with minibatch W x batch (cooperating workgroups): emulated here with W x the
+envs and W x the minibatch. Prints ms per PPO update for W = 1, 2, 4, 8.
+
+CONFIG (env var): ``gail`` (default; HalfCheetah FeedForward32Policy, 4096 rows, mb 64, 5
+epochs), ``airl`` (Hopper MlpPolicy [64, 64] ReLU, 8192 rows, mb 512, 20 epochs -- the tuned
+AIRL config), ``drlhp`` (Walker2d MlpPolicy [64, 64] ReLU, 8192 rows, mb 128, 20 epochs --
+the seals_walker preference-comparisons config).
 """
 import sys
 import time
@@ -25,13 +30,23 @@ def main():
     from imitation_amd.util.networks import RunningNorm
     from imitation_amd.util.util import make_vec_env
 
+    from imitation_amd.rl.policies import ActorCriticPolicy
+
+    cfg = os.environ.get("CONFIG", "gail")
+    env_id, n_steps, mb, epochs = {"gail": ("seals/HalfCheetah-v1", 512, 64, 5), "airl": ("seals/Hopper-v1", 1024, 512, 20),
+                                   "drlhp": ("seals/Walker2d-v1", 1024, 128, 20)}[cfg]
     for W in [int(w) for w in os.environ.get("WS", "1,2,4,8").split(",")]:
         rng = np.random.default_rng(0)
-        venv = make_vec_env("seals/HalfCheetah-v1", rng=rng, n_envs=8 * W)
-        demo_env = make_vec_env("seals/HalfCheetah-v1", rng=np.random.default_rng(7), n_envs=4)
+        venv = make_vec_env(env_id, rng=rng, n_envs=8 * W)
+        demo_env = make_vec_env(env_id, rng=np.random.default_rng(7), n_envs=4)
         demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
-        gen = PPO(FeedForward32Policy, venv, n_steps=512, batch_size=64 * W, n_epochs=5, device="cuda",
-                  policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+        if cfg == "gail":
+            gen = PPO(FeedForward32Policy, venv, n_steps=n_steps, batch_size=mb * W, n_epochs=epochs, device="cuda",
+                      policy_kwargs=dict(features_extractor_class=NormalizeFeaturesExtractor))
+        else:
+            gen = PPO(ActorCriticPolicy, venv, n_steps=n_steps, batch_size=mb * W, n_epochs=epochs, device="cuda",
+                      policy_kwargs=dict(net_arch=dict(pi=[64, 64], vf=[64, 64]), activation_fn=th.nn.ReLU,
+                                         features_extractor_class=NormalizeFeaturesExtractor))
         rn = NormalizedRewardNet(BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm), RunningNorm)
         tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, venv=venv, gen_algo=gen, reward_net=rn,
                         n_disc_updates_per_round=1, custom_logger=logger.configure("/tmp/ia_probe", format_strs=[]))
@@ -75,7 +90,7 @@ def main():
                 tr._ppo_update()
             th.cuda.synchronize()
             dt = (time.perf_counter() - t0) / n
-            print(f"W={W} path={path} rows={tr.T * tr.N} batch={64 * W} xchg2={mode}: ppo update {1e3 * dt:.3f} ms"
+            print(f"{cfg} W={W} path={path} rows={tr.T * tr.N} batch={mb * W} xchg2={mode}: ppo update {1e3 * dt:.3f} ms"
                   f" (two-level bitwise equal: {same})", flush=True)
         os.environ.pop("IMITATION_AMD_PPO_XCHG2")
         for mode in ("0", "1"):
@@ -86,8 +101,9 @@ def main():
             th.cuda.synchronize()
             p = prof.cpu().numpy().astype(np.float64) / tr._last_ppo_info[1]
             print(f"    xchg2={mode} cycles/minibatch (workgroup 0): chunk {p[0]:.0f} exchange+|g|^2 {p[1]:.0f} clip+adam {p[2]:.0f}"
-                  f" | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f} | exchange: publish {p[13]:.0f} arrival {p[14]:.0f} loads {p[15]:.0f}",
-                  flush=True)
+                  f" | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f} | exchange: publish {p[13]:.0f} arrival {p[14]:.0f} loads {p[15]:.0f}"
+                  f" | actor rows {p[3]:.0f} fwd {p[4]:.0f} loss {p[5]:.0f} bwd {p[6]:.0f} | critic rows {p[7]:.0f} fwd {p[8]:.0f}"
+                  f" loss {p[9]:.0f} bwd {p[10]:.0f}", flush=True)
             tr._ppo_static.pop("prof")
         os.environ.pop("IMITATION_AMD_PPO_XCHG2")
 
