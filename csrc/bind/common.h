@@ -21,5 +21,6 @@ void register_envs(py::module& m);
 void register_kernels(py::module& m);
 void register_engine(py::module& m);
 void register_disc(py::module& m);
+void register_airl(py::module& m);
 void register_conv(py::module& m);
 void register_comm(py::module& m);

@@ -77,6 +77,63 @@ hipError_t disc_adam(const DiscAdamArgs& a, hipStream_t s);
 hipError_t pol_norm_merge(float* mean, float* var, int* count, const float* defer, int n_slots, int cols,
                           hipStream_t s);
 
+// ---- airl_disc.hip: fused AIRL discriminator update (gather, norms, fwd/loss/bwd; Adam = disc_adam)
+constexpr int kAirlMaxLayers = 4;
+struct AirlNet {
+  int n_layers;
+  int dims[kAirlMaxLayers + 1];
+  int hidden_act;  // output layer is identity
+  const float* W[kAirlMaxLayers];  // [dout][din] fp32 (nn.Linear layout)
+  const float* b[kAirlMaxLayers];
+  int param_off;                   // offset of this net in a gradient slab row (reward nets)
+  int w_off[kAirlMaxLayers], b_off[kAirlMaxLayers];  // offsets within the net
+};
+struct AirlDiscArgs {
+  int mb;         // rows per side (2 * mb per minibatch, expert first)
+  int D, A;       // obs dim, action dim (Box) / n_actions (Discrete)
+  int aw;         // action width in the base input (A, or n_actions one-hot)
+  int aw_pi;      // stored action width for log pi (A, or 1: the index)
+  int act_discrete;
+  int use_state, use_action, use_next_state, use_done, din_b;
+  const int64_t* e_idx;  // [B] (minibatch k uses [k * mb, (k + 1) * mb))
+  const int64_t* g_idx;
+  const float *e_obs, *e_next_obs, *e_acts;
+  const int64_t* e_acts_i;
+  const bool* e_dones;
+  const float *g_obs, *g_next_obs, *g_acts;
+  const int64_t* g_acts_i;
+  const bool* g_dones;
+  // gathered minibatch
+  float *Xb, *S, *S2, *Act, *Done;
+  float* partials;  // [gather blocks][2][din_b + 2 D]
+  int gather_blocks;
+  double* sums;     // [2][din_b + 2 D] (DP modes)
+  // RunningNorms: b base input, p potential, q policy features (null = none)
+  float *b_mean, *b_var, *p_mean, *p_var, *q_mean, *q_var;
+  int *b_count, *p_count, *q_count;
+  float eps_b, eps_p, eps_q;
+  int merge_b, merge_p, merge_q;  // train mode (update stats)
+  float* nrm;  // [4][256]: (mean[128], rstd[128]) for policy, base, potential(s'), potential(s)
+  AirlNet pol, base, pot;
+  const float* log_std;  // [A] (Gaussian) or null
+  float gamma;           // shaping discount
+  float scale;           // dBCE/dlogit scale (mean over 2 mb rows * mb / B)
+  int n_params;          // base + potential parameters (slab row)
+  float* slab;           // [n_mb * fwd blocks][n_params]
+  float* stats_slab;     // [n_mb * fwd blocks][kDiscStats]
+};
+struct AirlPlan {
+  int ldp, ldr, ld_ht, dmax_pad;
+  int pimg_bytes, rimg_bytes, ht_bytes;
+  int w_off, rimg_off, scratch_off, lds_bytes;
+};
+int airl_gather_blocks(int mb);
+int airl_fwd_blocks(int mb);
+bool airl_plan(const AirlDiscArgs& a, AirlPlan& p);
+hipError_t airl_gather(const AirlDiscArgs& a, int k, hipStream_t s);
+hipError_t airl_norm(const AirlDiscArgs& a, int mode, int n_total, hipStream_t s);
+hipError_t airl_fwd_bwd(const AirlDiscArgs& a, const AirlPlan& p, int k, hipStream_t s);
+
 // ---- dagger.hip: device env step of the DAgger collector (one workgroup per env)
 struct DaggerEnvArgs {
   EnvParams P;

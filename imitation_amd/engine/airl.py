@@ -14,9 +14,13 @@ with respect to :class:`~imitation_amd.engine.gail.DeviceGAIL`:
   wave (``reward_outnorm``) replays the merge in env order: exactly the reference's
   per-step result, with the moments of each step all-reduced in ONE collective per round
   under data parallelism;
-* discriminator logit ``r(s,a,s',d) - log pi(a|s)`` (``airl.py:114-119``): the generic
-  discriminator update (autograd over the fused MLP kernels) -- the fused GAIL
-  discriminator kernels do not apply.
+* discriminator logit ``r(s,a,s',d) - log pi(a|s)`` (``airl.py:114-119``): a fused update
+  (``csrc/kernels/airl_disc.hip``, :class:`AirlDiscPlan`) -- per minibatch one gather, one
+  norm launch (the policy, base and potential RunningNorm merges in the reference's order:
+  potential on s' then on s) and one fwd/loss/bwd launch (policy log-prob, base reward,
+  both potential passes, BCE + statistics, backward of the base and potential MLPs), then
+  one fixed-order Adam launch -- instead of ~60 autograd launches. Configurations outside
+  the kernel's limits keep the generic (graphed autograd) update.
 
 PPO (MlpPolicy [64, 64], minibatch 512 in the tuned Hopper config) runs on the
 cooperating-workgroup register-chained kernel.
@@ -29,8 +33,9 @@ from typing import Any, Dict, Tuple
 import torch as th
 from numpy import prod as np_prod
 
+from imitation_amd.algorithms.adversarial import common
 from imitation_amd.algorithms.adversarial.airl import AIRL
-from imitation_amd.engine.gail import DeviceEngineMixin, _mlp_layers, supports_generator
+from imitation_amd.engine.gail import DeviceEngineMixin, _FlatParams, _mlp_layers, _policy_nets, supports_generator
 from imitation_amd.parallel import dist as pdist
 from imitation_amd.rewards import reward_nets
 from imitation_amd.util import networks
@@ -130,3 +135,161 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
                     shaping_gamma=float(shaped.discount_factor), rew_transform=0, use_state=int(base.use_state),
                     use_action=int(base.use_action), use_next_state=int(base.use_next_state),
                     use_done=int(base.use_done))
+
+    # ------------------------------------------------------------------ fused discriminator (airl_disc.hip)
+    def _fused_disc_check(self) -> Tuple[bool, str]:
+        import os
+
+        if os.environ.get("IMITATION_AMD_AIRL_FUSED", "1") == "0":
+            return False, "disabled (IMITATION_AMD_AIRL_FUSED=0)"
+        if type(self).logits_expert_is_high is not AIRL.logits_expert_is_high:
+            return False, "custom discriminator logits"
+        opt = self._disc_opt
+        if type(opt) is not th.optim.Adam or len(opt.param_groups) != 1:
+            return False, "discriminator optimizer is not a single-group torch.optim.Adam"
+        g = opt.param_groups[0]
+        if any(g.get(k) for k in ("amsgrad", "maximize", "capturable", "differentiable", "decoupled_weight_decay")):
+            return False, "Adam variant not fused"
+        if self._init_tensorboard:
+            return False, "tensorboard summaries need per-step logits"
+        if not isinstance(self._endless_expert_iterator, common._DeviceDemoSampler):
+            return False, "demonstrations are not a flat device transitions set"
+        _, shaped = _split(self._reward_net)
+        try:
+            bnorm, blins, _, bout = _mlp_layers(shaped.base.mlp)
+            pnorm, plins, _, pout = _mlp_layers(shaped.potential._potential_net)
+            qnorm, qlins, _, _ = _policy_nets(self.gen_algo.policy)
+        except ValueError as e:
+            return False, str(e)
+        for norm in (bnorm, pnorm, qnorm):
+            if norm is not None and type(norm) is not networks.RunningNorm:
+                return False, "a normaliser is not RunningNorm"
+        if bout != 0 or pout != 0 or blins[-1].out_features != 1 or plins[-1].out_features != 1:
+            return False, "reward / potential MLP shape"
+        if len(blins) > 4 or len(plins) > 4 or len(qlins) > 4:
+            return False, "MLP deeper than 4 layers"
+        widths = [l.out_features for l in blins + plins + qlins] + [blins[0].in_features, plins[0].in_features,
+                                                                    qlins[0].in_features]
+        if max(widths) > 64 or (self.A if not self.discrete else self.A) > 16:
+            return False, "MLP wider than 64"
+        mlp_params = {id(p) for l in blins + plins for p in (l.weight, l.bias)}
+        if {id(p) for p in self._reward_net.parameters()} != mlp_params:
+            return False, "reward net has parameters outside its MLPs"
+        base = shaped.base
+        din = (base.use_state + base.use_next_state) * self.D + base.use_action * self.A + base.use_done
+        if din + 2 * self.D > 128:
+            return False, "too many input columns"
+        return True, ""
+
+    def _setup_fused_disc(self) -> None:
+        ok, why = self._fused_disc_check()
+        self._fused_disc = ok
+        self._fused_disc_why = why
+        self._overlap_disc = False  # log pi needs the post-PPO policy: the updates follow PPO
+        self._side_stream = None
+        self._pol_defer_buf = None
+        if not ok:
+            return
+        dev = self._dev
+        _, shaped = _split(self._reward_net)
+        base = shaped.base
+        bnorm, blins, bh, _ = _mlp_layers(base.mlp)
+        pnorm, plins, ph, _ = _mlp_layers(shaped.potential._potential_net)
+        qnorm, qlins, _, qh = _policy_nets(self.gen_algo.policy)
+        self._bnorm, self._pnorm = bnorm, pnorm
+        plist = []
+        for l in blins + plins:
+            plist += [l.weight, l.bias]
+        self._rflat = _FlatParams(plist)
+        n = self._rflat.n
+        self._r_m = th.zeros(n, device=dev)
+        self._r_v = th.zeros(n, device=dev)
+        self._adopt_disc_opt_state()
+        ed = self._endless_expert_iterator.data
+        ed["obs"] = ed["obs"].float().contiguous()
+        ed["next_obs"] = ed["next_obs"].float().contiguous()
+        ed["acts"] = (ed["acts"].long() if self.discrete else ed["acts"].float()).reshape(ed["acts"].shape[0], -1)
+        ed["acts"] = ed["acts"].reshape(-1).contiguous() if self.discrete else ed["acts"].contiguous()
+        ed["dones"] = ed["dones"].bool().contiguous()
+        gd = self._gen_dev._arrays
+        B, mb = self.demo_batch_size, self.demo_minibatch_size
+        gblk, fblk = self._C.airl_plan_sizes(mb)
+        din = blins[0].in_features
+        D = self.D
+        ncol = din + 2 * D
+        z = lambda *sh, dt=th.float32: th.zeros(*sh, device=dev, dtype=dt)  # noqa: E731
+        rows = 2 * mb
+        self._disc_ws = dict(Xb=z(rows * din), S=z(rows * D), S2=z(rows * D), Act=z(rows * (1 if self.discrete else self.A)),
+                             Done=z(rows), partials=z(gblk * 2 * ncol), sums=z(2 * ncol, dt=th.float64), nrm=z(4 * 256),
+                             slab=z((B // mb) * fblk * n), stats_slab=z((B // mb) * fblk * 8), grads=z(n))
+        self._disc_stats = z(max(1, self.n_disc_updates_per_round), 8)
+        g = self._disc_opt.param_groups[0]
+        pol = self.gen_algo.policy
+
+        def net(lins, act):
+            return dict(W=[l.weight for l in lins], b=[l.bias for l in lins], hidden_act=int(act))
+
+        def norm_args(prefix, nm):
+            if nm is None:
+                return {f"{prefix}_mean": None, f"{prefix}_var": None, f"{prefix}_count": None, f"eps_{prefix}": 1e-5}
+            return {f"{prefix}_mean": nm.running_mean, f"{prefix}_var": nm.running_var, f"{prefix}_count": nm.count,
+                    f"eps_{prefix}": float(nm.eps)}
+
+        d = dict(batch=B, minibatch=mb, obs_dim=D, act_dim=self.A, act_discrete=int(self.discrete),
+                 use_state=int(base.use_state), use_action=int(base.use_action), use_next_state=int(base.use_next_state),
+                 use_done=int(base.use_done), e_obs=ed["obs"], e_next_obs=ed["next_obs"], e_acts=ed["acts"],
+                 e_dones=ed["dones"], g_obs=gd["obs"], g_next_obs=gd["next_obs"], g_acts=gd["acts"], g_dones=gd["dones"],
+                 pol=net(qlins, qh), base=net(blins, bh), pot=net(plins, ph),
+                 log_std=pol.log_std if self.has_log_std else None, gamma=float(shaped.discount_factor),
+                 params=self._rflat.flat, exp_avg=self._r_m, exp_avg_sq=self._r_v, beta1=float(g["betas"][0]),
+                 beta2=float(g["betas"][1]), eps=float(g["eps"]), weight_decay=float(g.get("weight_decay", 0.0)),
+                 **norm_args("b", bnorm), **norm_args("p", pnorm), **norm_args("q", qnorm), **self._disc_ws)
+        self._disc_plan = self._C.AirlDiscPlan(d)
+        self._disc_stats_host = th.zeros(max(1, self.n_disc_updates_per_round), 8, pin_memory=True)
+
+    def _fused_disc_update(self, slot: int, defer_pol: bool = False, e_idx: th.Tensor = None, g_idx: th.Tensor = None,
+                           apply: bool = True) -> None:
+        """One discriminator optimizer step (== AdversarialTrainer.train_disc with AIRL's logits)
+        on the fused kernels, with no host sync. ``e_idx`` / ``g_idx``: explicit expert / replay
+        rows (tests); ``apply=False`` stops after the gradient reduction (``_disc_ws["grads"]``)."""
+        if self._gen_dev.size() == 0:
+            raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
+        opt = self._disc_opt
+        self._adopt_disc_opt_state()
+        g = opt.param_groups[0]
+        t = float(opt.state[self._rflat.params[0]]["step"]) + 1.0
+        beta1, beta2 = g["betas"]
+        step_size = float(g["lr"]) / (1.0 - beta1**t)
+        bc2_sqrt = (1.0 - beta2**t) ** 0.5
+        B, mb = self.demo_batch_size, self.demo_minibatch_size
+        if e_idx is None:
+            e_idx = self._endless_expert_iterator.next_indices()
+        if g_idx is None:
+            g_idx = th.randint(0, self._gen_dev.size(), (B,), device=self._dev)
+        merge_b = self._bnorm is not None and self._bnorm.training
+        merge_p = self._pnorm is not None and self._pnorm.training
+        merge_q = self.pol_norm is not None and self.pol_norm.training
+        plan = self._disc_plan
+        stats_out = self._disc_stats[slot]
+        if pdist.world_size() == 1 and apply:
+            plan.update(e_idx, g_idx, step_size, bc2_sqrt, merge_b, merge_p, merge_q, stats_out)
+        else:
+            world = pdist.world_size()
+            for k in range(B // mb):
+                plan.gather(k, e_idx, g_idx)
+                if pdist.norm_sync_active():
+                    plan.norm(1, 0, merge_b, merge_p, merge_q)
+                    pdist.allreduce_sum_(self._disc_ws["sums"])
+                    plan.norm(2, 2 * mb * world, merge_b, merge_p, merge_q)
+                else:
+                    plan.norm(0, 0, merge_b, merge_p, merge_q)
+                plan.fwd_bwd(k)
+            plan.adam(1, 0, 0.0, 1.0, stats_out)
+            if world > 1:
+                pdist.allreduce_grads_flat(self._disc_ws["grads"])
+            if not apply:
+                return
+            plan.adam(0, 1, step_size, bc2_sqrt, None)
+        for p in self._rflat.params:
+            opt.state[p]["step"] += 1
+        self._disc_step += 1

@@ -402,6 +402,7 @@ def test_device_airl_graphed_disc_matches_eager():
     (IMITATION_AMD_DISC_GRAPH=0), over rounds where the graph is captured then replayed."""
     def run(graph: bool):
         os.environ["IMITATION_AMD_DISC_GRAPH"] = "1" if graph else "0"
+        os.environ["IMITATION_AMD_AIRL_FUSED"] = "0"  # the generic update (fused: test_device_airl_fused_disc_*)
         try:
             tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=3)
             assert tr._graphed_disc_ok() == graph
@@ -419,6 +420,7 @@ def test_device_airl_graphed_disc_matches_eager():
             return [p.detach().cpu().clone() for p in rn.parameters()], recs
         finally:
             os.environ.pop("IMITATION_AMD_DISC_GRAPH", None)
+            os.environ.pop("IMITATION_AMD_AIRL_FUSED", None)
 
     p_g, rec_g = run(True)
     p_e, rec_e = run(False)
@@ -429,3 +431,97 @@ def test_device_airl_graphed_disc_matches_eager():
         assert a.keys() == b.keys()
         for k in a:
             assert abs(a[k] - b[k]) <= 1e-3 * max(1.0, abs(b[k])), (k, a[k], b[k])
+
+
+def _airl_state(tr, rn):
+    from imitation_amd.engine.airl import _split
+    from imitation_amd.engine.gail import _mlp_layers
+
+    _, shaped = _split(rn)
+    norms = [_mlp_layers(shaped.base.mlp)[0], _mlp_layers(shaped.potential._potential_net)[0], tr.pol_norm]
+    assert all(n is not None for n in norms)
+    return norms
+
+
+@gpu
+@pytest.mark.parametrize("normalize_output", [True, False])
+def test_device_airl_fused_disc_matches_autograd(normalize_output):
+    """airl_disc.hip (gather, norm merges, policy log-prob + shaped reward fwd / BCE / bwd, Adam)
+    vs AdversarialTrainer.train_disc's autograd path on the SAME rows: reward-net gradients
+    within bf16 tolerance, every RunningNorm (policy, base, potential twice) equal, loss and
+    accuracy statistics close; then one full fused step changes the parameters like Adam."""
+    from imitation_amd.util import networks
+
+    tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=5, normalize_output=normalize_output)
+    assert tr._fused_disc, tr._fused_disc_why
+    tr.train(tr.gen_train_timesteps)  # replay ring + non-trivial normaliser / optimizer state
+    th.cuda.synchronize()
+    B = tr.demo_batch_size
+    e_idx = tr._endless_expert_iterator.next_indices().clone()
+    g_idx = th.randint(0, tr._gen_dev.size(), (B,), device="cuda")
+    norms = _airl_state(tr, rn)
+    snap = [(n.running_mean.clone(), n.running_var.clone(), n.count.clone()) for n in norms]
+    p0 = [p.detach().clone() for p in rn.parameters()]
+    m0, v0 = tr._r_m.clone(), tr._r_v.clone()
+    step0 = float(tr._disc_opt.state[tr._rflat.params[0]]["step"])
+    # fused: gradients only
+    with networks.training(tr.reward_train):
+        tr._fused_disc_update(0, e_idx=e_idx, g_idx=g_idx, apply=False)
+    th.cuda.synchronize()
+    g_fused = tr._disc_ws["grads"].clone()
+    st_fused = tr._disc_stats[0].clone()
+    n_fused = [(n.running_mean.clone(), n.running_var.clone(), n.count.clone()) for n in norms]
+    # restore, then the autograd path on the same rows
+    with th.no_grad():
+        for n, (mu, var, c) in zip(norms, snap):
+            n.running_mean.copy_(mu); n.running_var.copy_(var); n.count.copy_(c)
+    ed = tr._endless_expert_iterator.data
+    ex = {k: ed[k].index_select(0, e_idx) for k in ("obs", "acts", "next_obs", "dones")}
+    ga = tr._gen_dev._arrays
+    gs = {k: ga[k].index_select(0, g_idx) for k in ("obs", "acts", "next_obs", "dones")}
+    os.environ["IMITATION_AMD_FUSED"] = "0"  # fp32 PyTorch reference
+    try:
+        with networks.training(tr.reward_train):
+            stats = tr.train_disc(expert_samples=ex, gen_samples=gs)
+    finally:
+        os.environ.pop("IMITATION_AMD_FUSED", None)
+    th.cuda.synchronize()
+    g_ref = th.cat([p.grad.reshape(-1) for p in tr._rflat.params])
+    scale = float(g_ref.abs().max())
+    th.testing.assert_close(g_fused, g_ref, rtol=5e-2, atol=3e-2 * scale)
+    cos = float(th.nn.functional.cosine_similarity(g_fused, g_ref, dim=0))
+    assert cos > 0.995, cos
+    for (mu, var, c), n in zip(n_fused, norms):
+        th.testing.assert_close(mu, n.running_mean, rtol=1e-4, atol=1e-5)
+        th.testing.assert_close(var, n.running_var, rtol=1e-4, atol=1e-5)
+        assert int(c) == int(n.count)
+    fs = tr._disc_stats_dict(st_fused.tolist())
+    assert abs(fs["disc_loss"] - stats["disc_loss"]) < 2e-2 * max(1.0, abs(stats["disc_loss"]))
+    assert abs(fs["disc_acc"] - stats["disc_acc"]) < 0.03
+    # one full fused update from the snapshot: Adam moves every parameter with a gradient
+    with th.no_grad():
+        for p, q in zip(rn.parameters(), p0):
+            p.copy_(q)
+        tr._r_m.copy_(m0); tr._r_v.copy_(v0)
+        for n, (mu, var, c) in zip(norms, snap):
+            n.running_mean.copy_(mu); n.running_var.copy_(var); n.count.copy_(c)
+    for p in tr._rflat.params:
+        tr._disc_opt.state[p]["step"].fill_(step0)
+    with networks.training(tr.reward_train):
+        tr._fused_disc_update(1, e_idx=e_idx, g_idx=g_idx)
+    th.cuda.synchronize()
+    moved = th.cat([(p.detach() - q).reshape(-1) for p, q in zip(rn.parameters(), p0)])
+    assert bool(th.isfinite(moved).all()) and float(moved.abs().max()) > 0
+    assert float(tr._disc_opt.state[tr._rflat.params[0]]["step"]) == step0 + 1
+
+
+@gpu
+def test_device_airl_fused_rounds_train_and_log():
+    tr, venv, gen, rn = _setup_airl(n_envs=8, n_steps=128, batch=256)
+    assert tr._fused_disc and not tr._overlap_disc
+    r0 = [p.detach().clone() for p in rn.parameters()]
+    tr.train(3 * tr.gen_train_timesteps)
+    th.cuda.synchronize()
+    assert all(th.isfinite(p).all() for p in list(gen.policy.parameters()) + list(rn.parameters()))
+    assert any(not th.equal(a, b) for a, b in zip(r0, rn.parameters()))
+    assert tr._disc_step == 3 * tr.n_disc_updates_per_round
