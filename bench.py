@@ -27,8 +27,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
-import subprocess
 import sys
 import time
 
@@ -52,49 +50,14 @@ def parse():
 BASELINE_VALUE = None  # the reference publishes no throughput number
 
 
-def _free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def spawn_ranks(n: int) -> int:
-    """``--gpus N`` without a launcher: start N rank processes (one per GPU, RCCL) and
-    return the worst exit code. Runs before anything touches the GPU (counting devices
-    does not initialise HIP), so the children are fresh processes, not exec'd images.
-    ``IMITATION_AMD_DIST_BACKEND=gloo`` rehearses the multi-rank path with every rank on
-    one device (or on the CPU)."""
-    backend = os.environ.get("IMITATION_AMD_DIST_BACKEND", "nccl")
-    if backend != "gloo":
-        import torch as th
+    """``--gpus N`` without a launcher: N rank processes (one per GPU, RCCL), started before
+    anything touches the GPU (devices counted from sysfs, :mod:`imitation_amd.parallel.launch`);
+    returns the worst exit code. ``IMITATION_AMD_DIST_BACKEND=gloo`` rehearses the
+    multi-rank path with every rank on one device (or on the CPU)."""
+    from imitation_amd.parallel.launch import spawn_ranks as _spawn
 
-        have = th.cuda.device_count()
-        if have < n:
-            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have} "
-                  f"(set IMITATION_AMD_DIST_BACKEND=gloo to rehearse on fewer devices)", file=sys.stderr)
-            return 2
-    port = _free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    pending = list(procs)
-    while pending:
-        for p in list(pending):
-            code = p.poll()
-            if code is None:
-                continue
-            pending.remove(p)
-            if code != 0:
-                rc = rc or code
-                for q in pending:  # one rank died: the others would block in a collective
-                    q.terminate()
-        time.sleep(0.05)
-    for p in procs:
-        p.wait()
-    return rc if rc >= 0 else 1
+    return _spawn(n, __file__, sys.argv[1:], label="bench.py")
 
 
 def main():

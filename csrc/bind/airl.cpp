@@ -174,6 +174,16 @@ class AirlDiscPlan {
   int n_params() const { return a_.n_params; }
   int n_minibatches() const { return n_mb_; }
   int lds_bytes() const { return plan_.lds_bytes; }
+  // phase cycle counters of the fwd/bwd kernel (block 0): int64 GPU tensor [8] or None
+  void set_prof(c10::optional<torch::Tensor> t) {
+    if (!t.has_value() || !t->defined()) {
+      a_.prof = nullptr;
+      return;
+    }
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt64 && t->numel() >= 8, "prof: int64 GPU tensor [8]");
+    prof_ = *t;
+    a_.prof = reinterpret_cast<unsigned long long*>(prof_.data_ptr<int64_t>());
+  }
 
   void gather(int k, torch::Tensor e_idx, torch::Tensor g_idx) {
     check_idx(e_idx);
@@ -225,6 +235,7 @@ class AirlDiscPlan {
                 "indices must be int64 GPU tensors of >= batch entries");
   }
   std::vector<torch::Tensor> held_;
+  torch::Tensor prof_;
   ia::AirlDiscArgs a_{};
   ia::AirlPlan plan_{};
   ia::DiscAdamArgs ad_{};
@@ -244,6 +255,7 @@ void register_airl(py::module& m) {
       .def_property_readonly("n_params", &AirlDiscPlan::n_params)
       .def_property_readonly("n_minibatches", &AirlDiscPlan::n_minibatches)
       .def_property_readonly("lds_bytes", &AirlDiscPlan::lds_bytes)
+      .def("set_prof", &AirlDiscPlan::set_prof)
       .def("gather", &AirlDiscPlan::gather)
       .def("norm", &AirlDiscPlan::norm, py::arg("mode"), py::arg("n_total"), py::arg("merge_b"), py::arg("merge_p"),
            py::arg("merge_q"))

@@ -39,7 +39,7 @@ namespace {
 
 constexpr int kRows = 64;  // rows per block (4 waves x 16)
 constexpr int kNW = 4;
-constexpr int kGatherRows = 64;
+constexpr int kGatherRows = 16;  // 8 rows per thread: >= 256 blocks for a 2 x 2048-row batch
 constexpr int kNormPhases = 8;
 
 // ------------------------------------------------------------------ gather
@@ -85,6 +85,7 @@ __global__ __launch_bounds__(256) void airl_gather_kernel(AirlDiscArgs a, int k)
     else shift = a.p_mean ? a.p_mean[(c - nb) % D] : 0.f;
   }
   float s1 = 0.f, s2 = 0.f;
+#pragma unroll
   for (int rr = ph; rr < kGatherRows; rr += 2) {
     const int r = r0 + rr;
     if (r >= n) break;
@@ -253,14 +254,13 @@ __device__ __forceinline__ float act_apply(int act, float x) { return apply_act(
 
 // Forward of an MLP over the staged input Hs[0] (64 rows); hidden outputs go to Hs[l + 1]
 // (kept for the backward pass), the last layer's (fp32, bias added, identity) outputs to
-// out[row * out_ld + col] for col < dims[L] (<= 16).
-__device__ void mlp_forward(const AirlNet& net, bf16* const* Hs, int ld, bf16* Wimg, float* out, int out_ld) {
+// out[row * out_ld + col] for col < dims[L] (<= 16). Wf[l]: pre-staged weight images.
+// Each wave works on its own 16 rows only, so layers need no barrier between them.
+__device__ void mlp_forward(const AirlNet& net, bf16* const* Hs, int ld, bf16* const* Wf, float* out, int out_ld) {
   const int w = wave_id();
   for (int l = 0; l < net.n_layers; ++l) {
     const int din = net.dims[l], dout = net.dims[l + 1];
-    __syncthreads();
-    stage_weights(Wimg, net.W[l], dout, din, false);
-    __syncthreads();
+    const bf16* Wimg = Wf[l];
     const int K = pad32(din), ldw = ld_for_k(din);
     const bool last = l == net.n_layers - 1;
     const int ntiles = last ? 1 : pad32(dout) / 16;
@@ -280,7 +280,6 @@ __device__ void mlp_forward(const AirlNet& net, bf16* const* Hs, int ld, bf16* W
       }
     }
   }
-  __syncthreads();
 }
 
 __device__ __forceinline__ float wave_colsum(float s) {
@@ -292,7 +291,7 @@ __device__ __forceinline__ float wave_colsum(float s) {
 // Backward of an MLP (identity output, dout = 1) from per-row output gradients dy[64]:
 // dW / db into slab[param offsets] (acc: add to what an earlier pass of this block wrote).
 // Scratch: HT [feature][row] (ld_ht), dZ [row][k] (ld) and dZT [k][row] (ld_ht), x2.
-__device__ void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld, bf16* Wimg, const float* dy, bf16* HT, int ld_ht,
+__device__ void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld, bf16* const* Wt, const float* dy, bf16* HT, int ld_ht,
                              bf16* const* dZ, bf16* const* dZT, float* dbs, int dmax_pad, float* slab, bool acc_mode) {
   const int w = wave_id(), lane = lane_id();
   const int L = net.n_layers;
@@ -321,7 +320,6 @@ __device__ void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld, bf16* 
         HT[i * ld_ht + r] = Hs[l][r * ld + i];
       }
     }
-    if (l > 0) stage_weights(Wimg, net.W[l], dout, din, true);
     __syncthreads();
     // db_l
     float* sb = slab + net.param_off + net.b_off[l];
@@ -359,6 +357,7 @@ __device__ void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld, bf16* 
     {
       const int K = pad32(dout), ldw = ld_for_k(dout);
       const bf16* A = dZ[z] + w * 16 * ld;
+      const bf16* Wimg = Wt[l];
       const int ntiles = pad32(din) / 16;
       for (int nt = 0; nt < ntiles; ++nt) {
         f32x4 accv = mma_16x16(A, ld, Wimg + nt * 16 * ldw, ldw, K, zero4());
@@ -392,15 +391,24 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
   __shared__ float fl[6][kRows];  // log pi, r, Phi(s'), Phi(s), grads
   __shared__ float heads[kRows][17];
   __shared__ float st_w[kNW][kDiscStats];
-  bf16* Wimg = reinterpret_cast<bf16*>(smem + p.w_off);
+  bf16* Wf[3][kAirlMaxLayers];
+  bf16* Wt[3][kAirlMaxLayers];
+  for (int q = 0; q < 3; ++q)
+    for (int l = 0; l < kAirlMaxLayers; ++l) {
+      Wf[q][l] = reinterpret_cast<bf16*>(smem + p.wf_off[q][l]);
+      Wt[q][l] = reinterpret_cast<bf16*>(smem + p.wt_off[q][l]);
+    }
   bf16* Pimg[2] = {reinterpret_cast<bf16*>(smem + p.scratch_off), reinterpret_cast<bf16*>(smem + p.scratch_off + p.pimg_bytes)};
   bf16* Bh[kAirlMaxLayers];
   bf16* Qh[kAirlMaxLayers];
   bf16* Rh[kAirlMaxLayers];
-  for (int l = 0; l < kAirlMaxLayers; ++l) {
-    Bh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)l * p.rimg_bytes);
-    Qh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)(kAirlMaxLayers + l) * p.rimg_bytes);
-    Rh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)(2 * kAirlMaxLayers + l) * p.rimg_bytes);
+  {
+    const int nb = a.base.n_layers, np = a.pot.n_layers;
+    for (int l = 0; l < kAirlMaxLayers; ++l) {
+      Bh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)min(l, nb - 1) * p.rimg_bytes);
+      Qh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)(nb + min(l, np - 1)) * p.rimg_bytes);
+      Rh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)(nb + np + min(l, np - 1)) * p.rimg_bytes);
+    }
   }
   // backward scratch aliases the policy images (the policy pass is over by then)
   char* sc = smem + p.scratch_off;
@@ -413,19 +421,35 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
   const int n = 2 * a.mb;
   const int row0 = blockIdx.x * kRows;
   const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+  // optional phase timestamps (block 0, thread 0): a.prof[0..7]
+  const bool stamp = a.prof != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
+  unsigned long long t_0 = stamp ? clock64() : 0;
   lds_zero(smem, p.lds_bytes);
   __syncthreads();
-
-  // ---- policy forward -> log pi(a|s)
+  // every weight image once, up front (forward [o][i]; transposed [i][o] for the backward of
+  // the reward nets' layers >= 1), all loads in flight together
   {
-    stage_rows(Pimg[0], p.ldp, a.S, a.D, n, row0, a.nrm + 0 * 256);
+    const AirlNet* nets[3] = {&a.pol, &a.base, &a.pot};
+    for (int q = 0; q < 3; ++q)
+      for (int l = 0; l < nets[q]->n_layers; ++l) {
+        stage_weights(Wf[q][l], nets[q]->W[l], nets[q]->dims[l + 1], nets[q]->dims[l], false);
+        if (q > 0 && l > 0) stage_weights(Wt[q][l], nets[q]->W[l], nets[q]->dims[l + 1], nets[q]->dims[l], true);
+      }
+  }
+  stage_rows(Pimg[0], p.ldp, a.S, a.D, n, row0, a.nrm + 0 * 256);
+  stage_rows(Bh[0], p.ldr, a.Xb, a.din_b, n, row0, a.nrm + 1 * 256);
+  stage_rows(Qh[0], p.ldr, a.S2, a.D, n, row0, a.nrm + 2 * 256);
+  stage_rows(Rh[0], p.ldr, a.S, a.D, n, row0, a.nrm + 3 * 256);
+  __syncthreads();
+
+  unsigned long long t_1 = stamp ? clock64() : 0;
+  // ---- policy forward -> log pi(a|s)  (each wave on its own 16 rows)
+  {
     const AirlNet& pn = a.pol;
     // ping-pong: layer l reads Pimg[l & 1], writes Pimg[(l + 1) & 1]
     for (int l = 0; l < pn.n_layers; ++l) {
       const int din = pn.dims[l], dout = pn.dims[l + 1];
-      __syncthreads();
-      stage_weights(Wimg, pn.W[l], dout, din, false);
-      __syncthreads();
+      const bf16* Wimg = Wf[0][l];
       const int K = pad32(din), ldw = ld_for_k(din);
       const bool last = l == pn.n_layers - 1;
       const int ntiles = last ? 1 : pad32(dout) / 16;
@@ -468,14 +492,14 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
     }
   }
 
+  unsigned long long t_2 = stamp ? clock64() : 0;
   // ---- reward nets forward: base r, potential Phi(s'), Phi(s)
-  stage_rows(Bh[0], p.ldr, a.Xb, a.din_b, n, row0, a.nrm + 1 * 256);
-  stage_rows(Qh[0], p.ldr, a.S2, a.D, n, row0, a.nrm + 2 * 256);
-  stage_rows(Rh[0], p.ldr, a.S, a.D, n, row0, a.nrm + 3 * 256);
-  mlp_forward(a.base, Bh, p.ldr, Wimg, &fl[1][0], 1);
-  mlp_forward(a.pot, Qh, p.ldr, Wimg, &fl[2][0], 1);
-  mlp_forward(a.pot, Rh, p.ldr, Wimg, &fl[3][0], 1);
+  mlp_forward(a.base, Bh, p.ldr, Wf[1], &fl[1][0], 1);
+  mlp_forward(a.pot, Qh, p.ldr, Wf[2], &fl[2][0], 1);
+  mlp_forward(a.pot, Rh, p.ldr, Wf[2], &fl[3][0], 1);
+  __syncthreads();
 
+  unsigned long long t_3 = stamp ? clock64() : 0;
   // ---- logit, BCE gradient, statistics (one row per thread of wave 0)
   float st[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (tid < kRows) {
@@ -515,11 +539,23 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
   __syncthreads();
   if (tid < kDiscStats) a.stats_slab[((size_t)k * gridDim.x + blockIdx.x) * kDiscStats + tid] = tid < 6 ? st_w[0][tid] : 0.f;
 
+  unsigned long long t_4 = stamp ? clock64() : 0;
   // ---- backward: base, potential on s' (writes), potential on s (adds)
   float* slab_row = a.slab + ((size_t)k * gridDim.x + blockIdx.x) * a.n_params;
-  mlp_backward(a.base, Bh, p.ldr, Wimg, &fl[4][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
-  mlp_backward(a.pot, Qh, p.ldr, Wimg, &fl[5][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
-  mlp_backward(a.pot, Rh, p.ldr, Wimg, &fl[1][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, true);
+  mlp_backward(a.base, Bh, p.ldr, Wt[1], &fl[4][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
+  mlp_backward(a.pot, Qh, p.ldr, Wt[2], &fl[5][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
+  unsigned long long t_5 = stamp ? clock64() : 0;
+  mlp_backward(a.pot, Rh, p.ldr, Wt[2], &fl[1][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, true);
+  if (stamp) {
+    const unsigned long long t_6 = clock64();
+    a.prof[0] += t_1 - t_0;  // zero + stage
+    a.prof[1] += t_2 - t_1;  // policy fwd + log pi
+    a.prof[2] += t_3 - t_2;  // reward fwds
+    a.prof[3] += t_4 - t_3;  // loss
+    a.prof[4] += t_5 - t_4;  // base bwd + pot(s') bwd
+    a.prof[5] += t_6 - t_5;  // pot(s) bwd
+    a.prof[6] += 1;
+  }
 }
 
 }  // namespace
@@ -552,12 +588,22 @@ bool airl_plan(const AirlDiscArgs& a, AirlPlan& p) {
   p.rimg_bytes = kRows * p.ldr * 2;
   p.ht_bytes = pad32(rmax) * p.ld_ht * 2;
   if (p.ht_bytes < kRows * 32 * 2) p.ht_bytes = kRows * 32 * 2;
-  const int w_bytes = pad32(wmax) * ld_for_k(wmax) * 2;
+  (void)wmax;
   int off = 0;
-  p.w_off = off;
-  off += (w_bytes + 15) & ~15;
+  for (int q = 0; q < 3; ++q)
+    for (int l = 0; l < kAirlMaxLayers; ++l) {
+      p.wf_off[q][l] = p.wt_off[q][l] = 0;
+      if (l >= nets[q]->n_layers) continue;
+      const int din = nets[q]->dims[l], dout = nets[q]->dims[l + 1];
+      p.wf_off[q][l] = off;
+      off += (pad32(dout) * ld_for_k(din) * 2 + 15) & ~15;
+      if (q > 0 && l > 0) {
+        p.wt_off[q][l] = off;
+        off += (pad32(din) * ld_for_k(dout) * 2 + 15) & ~15;
+      }
+    }
   p.rimg_off = off;
-  off += 3 * kAirlMaxLayers * p.rimg_bytes;
+  off += (a.base.n_layers + 2 * a.pot.n_layers) * p.rimg_bytes;
   p.scratch_off = off;
   const int pol_scratch = 2 * p.pimg_bytes;
   const int bwd_scratch = 3 * p.ht_bytes + 2 * p.rimg_bytes + (2 * kNW * p.dmax_pad + 16) * 4;

@@ -148,42 +148,81 @@ __device__ __forceinline__ float reward_input(const RolloutPostArgs& a, float o,
 }  // namespace
 
 // NormalizedRewardNet output normalisation (see OutNormArgs): one wave, sequential in t.
-__global__ __launch_bounds__(64) void reward_outnorm_kernel(OutNormArgs a) {
-  const int lane = threadIdx.x & 63;
-  float mean = a.mean[0], var = a.var[0], cnt = a.count[0];
-  for (int t = 0; t < a.T; ++t) {
-    const float rstd = 1.f / sqrtf(var + a.eps);
-    float s = 0.f;
-    for (int n = lane; n < a.N; n += 64) {
-      const size_t i = (size_t)t * a.N + n;
-      const float x = a.rew_raw[i];
-      a.rewards[i] = (x - mean) * rstd + a.boot[i];
-      s += x;
-    }
-    float bm, bv, bn;
-    if (a.step_stats) {
-      bn = a.step_stats[3 * t];
-      bm = a.step_stats[3 * t + 1];
-      bv = a.step_stats[3 * t + 2];
-    } else {
-      bn = (float)a.N;
-      bm = wave_sum(s) / bn;
-      float q = 0.f;
-      for (int n = lane; n < a.N; n += 64) {
-        const float d = a.rew_raw[(size_t)t * a.N + n] - bm;
-        q += d * d;
-      }
-      bv = wave_sum(q) / bn;
-    }
-    const float delta = bm - mean, tot = cnt + bn;
-    mean += delta * bn / tot;
-    var = (var * cnt + bv * bn + delta * delta * cnt * bn / tot) / tot;
-    cnt = tot;
+// Three phases instead of one serial wave: (A) every step's batch moments in parallel (they
+// do not depend on the running state), (B) the scalar Chan recurrence over the steps by one
+// lane, recording the running (mean, var) each step is normalised with, (C) every reward in
+// parallel. Steps go through LDS in chunks of kOutNormChunk.
+constexpr int kOutNormThreads = 256;
+constexpr int kOutNormChunk = 4096;
+
+__global__ __launch_bounds__(kOutNormThreads) void reward_outnorm_kernel(OutNormArgs a) {
+  __shared__ float sm[kOutNormChunk], sv[kOutNormChunk], sn[kOutNormChunk];
+  __shared__ float state[3];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    state[0] = a.mean[0];
+    state[1] = a.var[0];
+    state[2] = a.count[0];
   }
-  if (lane == 0) {
-    a.mean[0] = mean;
-    a.var[0] = var;
-    a.count[0] = cnt;
+  for (int t0 = 0; t0 < a.T; t0 += kOutNormChunk) {
+    const int nt = min(kOutNormChunk, a.T - t0);
+    // (A) batch moments of each step (over the N envs, or the global ones under DP)
+    for (int j = tid; j < nt; j += kOutNormThreads) {
+      const int t = t0 + j;
+      float bm, bv, bn;
+      if (a.step_stats) {
+        bn = a.step_stats[3 * t];
+        bm = a.step_stats[3 * t + 1];
+        bv = a.step_stats[3 * t + 2];
+      } else {
+        bn = (float)a.N;
+        const float* x = a.rew_raw + (size_t)t * a.N;
+        float s = 0.f;
+        for (int n = 0; n < a.N; ++n) s += x[n];
+        bm = s / bn;
+        float q = 0.f;
+        for (int n = 0; n < a.N; ++n) {
+          const float d = x[n] - bm;
+          q += d * d;
+        }
+        bv = q / bn;
+      }
+      sm[j] = bm;
+      sv[j] = bv;
+      sn[j] = bn;
+    }
+    __syncthreads();
+    // (B) running state before each step (replaces the step's moments in LDS)
+    if (tid == 0) {
+      float mean = state[0], var = state[1], cnt = state[2];
+      for (int j = 0; j < nt; ++j) {
+        const float bm = sm[j], bv = sv[j], bn = sn[j];
+        sm[j] = mean;
+        sv[j] = var;
+        const float delta = bm - mean, tot = cnt + bn;
+        mean += delta * bn / tot;
+        var = (var * cnt + bv * bn + delta * delta * cnt * bn / tot) / tot;
+        cnt = tot;
+      }
+      state[0] = mean;
+      state[1] = var;
+      state[2] = cnt;
+    }
+    __syncthreads();
+    // (C) normalised rewards + TimeLimit bootstrap
+    const int n_el = nt * a.N;
+    for (int e = tid; e < n_el; e += kOutNormThreads) {
+      const int j = e / a.N;
+      const size_t i = (size_t)t0 * a.N + e;
+      const float rstd = 1.f / sqrtf(sv[j] + a.eps);
+      a.rewards[i] = (a.rew_raw[i] - sm[j]) * rstd + a.boot[i];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    a.mean[0] = state[0];
+    a.var[0] = state[1];
+    a.count[0] = state[2];
   }
 }
 constexpr int kPostWaves = 4;  // waves per workgroup sharing one LDS image of the nets
@@ -277,7 +316,7 @@ hipError_t rollout_post_launch(const RolloutPostArgs& a, hipStream_t s) {
 
 hipError_t reward_outnorm_launch(const OutNormArgs& a, hipStream_t s) {
   if (a.T <= 0 || a.N <= 0) return hipSuccess;
-  hipLaunchKernelGGL(reward_outnorm_kernel, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(reward_outnorm_kernel, dim3(1), dim3(kOutNormThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -121,11 +121,14 @@ struct AirlDiscArgs {
   int n_params;          // base + potential parameters (slab row)
   float* slab;           // [n_mb * fwd blocks][n_params]
   float* stats_slab;     // [n_mb * fwd blocks][kDiscStats]
+  unsigned long long* prof;  // optional phase cycle counters (block 0) [8]
 };
 struct AirlPlan {
   int ldp, ldr, ld_ht, dmax_pad;
   int pimg_bytes, rimg_bytes, ht_bytes;
-  int w_off, rimg_off, scratch_off, lds_bytes;
+  int wf_off[3][kAirlMaxLayers];  // pre-staged weight images: 0 policy, 1 base, 2 potential
+  int wt_off[3][kAirlMaxLayers];  // transposed images (reward nets, layers >= 1)
+  int rimg_off, scratch_off, lds_bytes;
 };
 int airl_gather_blocks(int mb);
 int airl_fwd_blocks(int mb);

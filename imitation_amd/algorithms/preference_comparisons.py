@@ -1155,6 +1155,8 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
                  allow_variable_horizon: bool = False, rng: Optional[np.random.Generator] = None,
                  query_schedule: Union[str, Callable[[float], float]] = "hyperbolic") -> None:
         super().__init__(custom_logger=custom_logger, allow_variable_horizon=allow_variable_horizon)
+        if pdist.world_size() > 1:  # every replica starts from rank 0's reward model
+            pdist.broadcast_module(reward_model)
         self._iteration = 0
         self.model = reward_model
         self.rng = rng

@@ -187,27 +187,30 @@ def airl_hopper(device=None, n_envs: int = 8, seed: int = 0, rank: int = 0, env_
 
 def dagger_pong(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "PongNoFrameskip-v4",
                 scratch_dir: Optional[str] = None, expert_policy=None, batch_size: int = 32,
-                log_dir: Optional[str] = None, **overrides) -> Built:
+                log_dir: Optional[str] = None, rank: int = 0, **overrides) -> Built:
     """DAgger on Pong frames (uint8 84x84x4): the learner is an ``ActorCriticCnnPolicy``
-    (NatureCNN extractor); the expert is a random-init CNN policy unless one is given."""
+    (NatureCNN extractor); the expert is a random-init CNN policy unless one is given.
+    ``rank``: data-parallel rank -- its own env seeds and sampling streams; the expert is
+    the same on every rank and the learner is broadcast from rank 0 by BC."""
     from imitation_amd.algorithms import bc, dagger
     from imitation_amd.rl.policies import ActorCriticCnnPolicy
     from imitation_amd.util.util import make_vec_env
 
     dev = _device(device)
-    venv = make_vec_env(env_id, rng=np.random.default_rng(seed), n_envs=n_envs)
+    venv = make_vec_env(env_id, rng=np.random.default_rng(seed + 1000 * rank), n_envs=n_envs)
     lr = lambda _: 1e-3  # noqa: E731
     if expert_policy is None:
         th.manual_seed(seed + 7)
         expert_policy = ActorCriticCnnPolicy(venv.observation_space, venv.action_space, lr).to(dev)
     learner = ActorCriticCnnPolicy(venv.observation_space, venv.action_space, lambda _: th.finfo(th.float32).max).to(dev)
     log = _logger(log_dir)
+    rrng = np.random.default_rng(seed + 1000 * rank)
     bc_trainer = bc.BC(observation_space=venv.observation_space, action_space=venv.action_space,
-                       rng=np.random.default_rng(seed), policy=learner, batch_size=batch_size, device=dev,
+                       rng=rrng, policy=learner, batch_size=batch_size, device=dev,
                        custom_logger=log)
     scratch = scratch_dir or tempfile.mkdtemp(prefix="ia_dagger_pong_")
     trainer = dagger.SimpleDAggerTrainer(venv=venv, scratch_dir=scratch, expert_policy=expert_policy,
-                                         rng=np.random.default_rng(seed), bc_trainer=bc_trainer, custom_logger=log,
+                                         rng=rrng, bc_trainer=bc_trainer, custom_logger=log,
                                          **overrides)
     return Built(trainer, venv, "dagger_pong", env_id, 0, {"expert_policy": expert_policy, "engine": trainer.collector_kind})
 
@@ -215,7 +218,7 @@ def dagger_pong(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "Pong
 def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str = "seals/Walker2d-v1",
                         num_iterations: int = 5, fragment_length: int = 100, total_timesteps: int = 1_000_000,
                         n_steps: Optional[int] = None, log_dir: Optional[str] = None, engine: str = "auto",
-                        **overrides) -> Built:
+                        rank: int = 0, **overrides) -> Built:
     """Preference comparisons on Walker2d with the reference's ``seals_walker`` named config
     (``scripts/config/train_preference_comparisons.py:179-203`` + ``train_defaults``):
     MlpPolicy pi/vf [64, 64] ReLU with the policy ingredient's NormalizeFeaturesExtractor,
@@ -225,7 +228,9 @@ def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str
     fragment length 100, 5 iterations over 1e6 timesteps, hyperbolic query schedule,
     ``initial_comparison_frac`` 0.1 and the library-default ``initial_epoch_multiplier`` 200,
     no exploration (``n_steps`` overrides the rollout length for quick tests). The agent trains and samples on the GPU
-    (:class:`~imitation_amd.engine.preference.DeviceAgentTrainer`) when eligible."""
+    (:class:`~imitation_amd.engine.preference.DeviceAgentTrainer`) when eligible. ``rank``: data-parallel rank -- its
+    own env seeds and fragment / preference sampling streams (the pairs of all ranks are all-gathered); the agent and
+    the reward net start from rank 0's weights (broadcast)."""
     from torch import nn
 
     from imitation_amd.algorithms import preference_comparisons as pc
@@ -237,7 +242,7 @@ def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str
     from imitation_amd.util.util import make_vec_env
 
     dev = _device(device)
-    rng = np.random.default_rng(seed)
+    rng = np.random.default_rng(seed + 1000 * rank)
     venv = make_vec_env(env_id, rng=rng, n_envs=n_envs)
     log = _logger(log_dir)
     reward_net = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm).to(dev)
@@ -247,6 +252,7 @@ def preference_walker2d(device=None, n_envs: int = 8, seed: int = 0, env_id: str
                 policy_kwargs=dict(activation_fn=nn.ReLU, net_arch=dict(pi=[64, 64], vf=[64, 64]),
                                    features_extractor_class=NormalizeFeaturesExtractor,
                                    features_extractor_kwargs=dict(normalize_class=RunningNorm)))
+    _reseed_rank(venv, seed, rank)
     gen_cls = pc.AgentTrainer
     if engine in ("auto", "device"):
         from imitation_amd.engine import preference as device_pref

@@ -443,3 +443,54 @@ def oneshot_block_change_worker(rank, world, reps, seed):
             bad += int((b != exp).sum().item())
     th.cuda.synchronize(dev)
     return {"bad_words": bad, "blocks": blocks, "error": c.error()}
+
+
+def pref_device_iter_worker(rank, world, seed):
+    """Full preference-comparisons iterations (DeviceAgentTrainer agent on ``cuda:0`` shared by
+    the ranks, replicated-DP PPO, all-gathered pairs, DP reward trainer) from the
+    ``preference_walker2d`` recipe at a reduced size; returns what the parent compares:
+    replica parameters (must be bit-identical) and each rank's env state (must differ)."""
+    import torch as th
+
+    from imitation_amd import models
+
+    dev = th.device("cuda", 0)
+    th.manual_seed(seed + rank)
+    np.random.seed(seed + rank)
+    b = models.build("preference_walker2d", device=dev, seed=seed, rank=rank, n_envs=4, n_steps=64,
+                     fragment_length=16, total_timesteps=2 * 4 * 64 * 2, num_iterations=2, engine="device")
+    tr = b.trainer
+    gen = tr.trajectory_generator
+    assert type(gen).__name__ == "DeviceAgentTrainer", type(gen)
+    tr.train(2 * 4 * 64 * 2, total_comparisons=24)
+    th.cuda.synchronize()
+    return {"reward": [p.detach().cpu().numpy().copy() for p in tr.model.parameters()],
+            "policy": [p.detach().cpu().numpy().copy() for p in b.extras["agent"].policy.parameters()],
+            "n_pairs": len(tr.dataset), "env_state": gen.state.detach().cpu().numpy().copy(),
+            "cur_obs": gen.cur_obs.detach().cpu().numpy().copy()}
+
+
+def dagger_device_round_worker(rank, world, seed, scratch):
+    """DAgger rounds with the device collector (Pong-shaped frames rendered on ``cuda:0``,
+    shared by the ranks) from the ``dagger_pong`` recipe: BC replicas must stay bit-identical,
+    each rank's env must follow its own seed."""
+    import os
+
+    import torch as th
+
+    from imitation_amd import models
+
+    dev = th.device("cuda", 0)
+    th.manual_seed(seed + rank)
+    np.random.seed(seed + rank)
+    b = models.build("dagger_pong", device=dev, seed=seed, rank=rank, n_envs=2, batch_size=32,
+                     scratch_dir=os.path.join(scratch, "dagger"))
+    tr = b.trainer
+    assert tr.collector_kind == "device", tr.collector_kind
+    tr.train(256 * world, rollout_round_min_episodes=1, rollout_round_min_timesteps=256,
+             bc_train_kwargs=dict(n_batches=4, progress_bar=False, log_interval=10**9))
+    th.cuda.synchronize()
+    col = tr._device_collector
+    return {"policy": [p.detach().cpu().numpy().copy() for p in tr.policy.parameters()],
+            "env_state": col.state.detach().cpu().numpy().copy(), "round_num": tr.round_num,
+            "local": tr.last_train_timesteps_local}

@@ -122,3 +122,32 @@ def test_oneshot_graph_block_count_changes(oneshot_env):
     for r in range(2):
         assert out[r]["blocks"] == [1, 2, 4, 1]
         assert out[r]["bad_words"] == 0 and out[r]["error"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("oneshot", ["0", "1"])
+def test_preference_device_iterations_dp_replicas(monkeypatch, oneshot):
+    """2-rank PreferenceComparisons iterations with the device agent (one card, gloo group):
+    bit-identical reward model and policy replicas, every rank's env on its own seed."""
+    monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", oneshot)
+    out = run_ranks(W.pref_device_iter_worker, 2, 3, timeout=400)
+    for key in ("reward", "policy"):
+        for a, b in zip(out[0][key], out[1][key]):
+            np.testing.assert_array_equal(a, b)
+    assert out[0]["n_pairs"] == out[1]["n_pairs"] > 0
+    assert not np.array_equal(out[0]["env_state"], out[1]["env_state"])
+    assert not np.array_equal(out[0]["cur_obs"], out[1]["cur_obs"])
+
+
+@pytest.mark.gpu
+def test_dagger_device_collector_dp_replicas(monkeypatch, tmp_path):
+    """2-rank DAgger rounds with the device collector (one card, gloo group): identical BC
+    replicas, per-rank env streams."""
+    monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", "1")
+    out = run_ranks(W.dagger_device_round_worker, 2, 4, str(tmp_path), timeout=400)
+    for a, b in zip(out[0]["policy"], out[1]["policy"]):
+        np.testing.assert_array_equal(a, b)
+    assert out[0]["round_num"] == out[1]["round_num"] >= 1
+    assert not np.array_equal(out[0]["env_state"], out[1]["env_state"])
