@@ -47,7 +47,10 @@ def gather_tb_directories() -> dict:
     tmp_dir = pathlib.Path(tempfile.mkdtemp(dir=root))
     count = 0
     for sd in _gather_sacred_dicts():
-        run_dir = sd.sacred_dir.parent.parent
+        # the run's own log dir (recorded in its config) when it exists, else the directory
+        # above the observer's run dir (the reference layout: <log_dir>/sacred/<id>)
+        log_dir = (sd.config.get("logging") or {}).get("log_dir")
+        run_dir = pathlib.Path(log_dir) if log_dir and pathlib.Path(log_dir).is_dir() else sd.sacred_dir.parent.parent
         for basename in ("log", "rl", "tb", "sb_tb"):
             src = tuple(sacred_util.filter_subdirs(run_dir, lambda p, b=basename: p.name == b))
             if src:
