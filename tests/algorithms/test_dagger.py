@@ -1,13 +1,18 @@
 """DAgger (reference: tests/algorithms/test_dagger.py)."""
 
+import glob
+import math
 import os
 
 import numpy as np
 import pytest
+import torch as th
 
 from imitation_amd.algorithms import bc, dagger
 from imitation_amd.data import rollout
+from imitation_amd.policies.base import RandomPolicy
 from imitation_amd.testing import reward_improvement
+from imitation_amd.util import util
 
 
 def test_beta_schedules():
@@ -82,3 +87,180 @@ def test_mismatched_expert_spaces(tmp_path, cartpole_venv, rng):
     with pytest.raises(ValueError):
         dagger.SimpleDAggerTrainer(venv=cartpole_venv, scratch_dir=tmp_path, expert_policy=bad, rng=rng,
                                    bc_trainer=_bc(cartpole_venv, rng))
+
+
+# --------------------------------------------------------------------------- reference parity
+# (reference tests/algorithms/test_dagger.py: beta schedules :36-68, collector :71-160,
+#  trainer save/reload :474, SimpleDAgger rounds :494, errors :528-583)
+
+
+@pytest.mark.parametrize("num_rampdown_rounds", [1, 2, 3, 10])
+def test_linear_beta_schedule(num_rampdown_rounds):
+    sched = dagger.LinearBetaSchedule(num_rampdown_rounds)
+    for i in range(3 * num_rampdown_rounds + 2):
+        assert sched(i) == pytest.approx(min(1.0, max(0.0, (num_rampdown_rounds - i) / num_rampdown_rounds)))
+
+
+@pytest.mark.parametrize("decay_probability", [0.1, 0.5, 0.9, 1])
+def test_exponential_beta_schedule(decay_probability):
+    sched = dagger.ExponentialBetaSchedule(decay_probability)
+    for i in range(20):
+        assert sched(i) == pytest.approx(decay_probability**i)
+
+
+@pytest.mark.parametrize("decay_probability", [-0.1, 0, 1.1, 2])
+def test_forbidden_decay_probability_on_exp_beta_schedule(decay_probability):
+    with pytest.raises(ValueError):
+        dagger.ExponentialBetaSchedule(decay_probability)
+
+
+def test_beta_schedule_json_roundtrip():
+    for s in (dagger.LinearBetaSchedule(7), dagger.ExponentialBetaSchedule(0.3)):
+        r = dagger._schedule_from_json(s.to_json())
+        assert type(r) is type(s) and all(r(i) == s(i) for i in range(10))
+
+
+def _collector(tmp_path, venv, seed, beta=0.5, robot=None):
+    calls = []
+
+    def get_robot_acts(obs):
+        calls.append(len(obs))
+        return robot(obs) if robot else np.stack([venv.action_space.sample() for _ in range(len(obs))])
+
+    coll = dagger.InteractiveTrajectoryCollector(venv, get_robot_acts=get_robot_acts, beta=beta, save_dir=tmp_path,
+                                                 rng=np.random.default_rng(seed))
+    return coll, calls
+
+
+def test_traj_collector_seed(tmp_path, pendulum_venv):
+    """seed() re-seeds both the beta-mixing stream and the envs: identical collections."""
+    runs = []
+    for k in range(2):
+        coll, calls = _collector(tmp_path / f"s{k}", pendulum_venv, seed=123, robot=lambda o: np.zeros((len(o), 1)))
+        coll.seed(42)
+        obs = coll.reset()
+        seen = [obs]
+        for _ in range(20):
+            obs, _, _, _ = coll.step(np.ones((pendulum_venv.num_envs, 1)))
+            seen.append(obs)
+        runs.append((np.stack(seen), list(calls)))
+    np.testing.assert_array_equal(runs[0][0], runs[1][0])
+    assert runs[0][1] == runs[1][1]
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_traj_collector_beta_extremes(tmp_path, pendulum_venv, beta):
+    """beta = 1: the expert always drives the env (robot never asked); beta = 0: the robot
+    always does. The recorded actions are the expert's either way."""
+    coll, calls = _collector(tmp_path, pendulum_venv, seed=0, beta=beta, robot=lambda o: np.zeros((len(o), 1)))
+    coll.reset()
+    for _ in range(205):  # Pendulum episodes: 200 steps
+        coll.step(np.full((pendulum_venv.num_envs, 1), 0.5))
+    if beta == 1.0:
+        assert sum(calls) == 0
+    else:
+        assert sum(calls) == 205 * pendulum_venv.num_envs
+    from imitation_amd.data import serialize
+
+    files = sorted(glob.glob(str(tmp_path / "*.npz")))
+    assert len(files) == pendulum_venv.num_envs
+    for f in files:
+        np.testing.assert_allclose(serialize.load(f)[0].acts, 0.5)
+
+
+def _pendulum_trainer(tmp_path, venv, expert, seed=0, simple=True, batch_size=32):
+    th.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    bct = bc.BC(observation_space=venv.observation_space, action_space=venv.action_space, rng=rng,
+                batch_size=batch_size, custom_logger=None, device="cpu")
+    if simple:
+        return dagger.SimpleDAggerTrainer(venv=venv, scratch_dir=tmp_path, expert_policy=expert, rng=rng, bc_trainer=bct)
+    return dagger.DAggerTrainer(venv=venv, scratch_dir=tmp_path, rng=rng, bc_trainer=bct)
+
+
+@pytest.mark.parametrize("simple", [True, False])
+def test_trainer_save_reload(tmp_path, pendulum_venv, simple):
+    expert = RandomPolicy(pendulum_venv.observation_space, pendulum_venv.action_space)
+    trainer = _pendulum_trainer(tmp_path / "a", pendulum_venv, expert, seed=1, simple=simple)
+    trainer.round_num = 3
+    trainer.save_trainer()
+    loaded = dagger.reconstruct_trainer(trainer.scratch_dir, venv=pendulum_venv, device="cpu")
+    assert loaded.round_num == 3 and type(loaded) is type(trainer)
+    old, new = trainer.policy.state_dict(), loaded.policy.state_dict()
+    assert old.keys() == new.keys() and all(new[k].equal(old[k]) for k in old)
+    third = _pendulum_trainer(tmp_path / "b", pendulum_venv, expert, seed=2, simple=simple)
+    assert not all(third.policy.state_dict()[k].equal(old[k]) for k in old)
+
+
+@pytest.mark.parametrize("num_episodes", [1, 4])
+def test_simple_dagger_rounds_and_files(tmp_path, pendulum_venv, num_episodes):
+    """Rounds of at least ``rollout_round_min_episodes`` episodes: one round dir each with
+    one demo file per collected episode."""
+    expert = RandomPolicy(pendulum_venv.observation_space, pendulum_venv.action_space)
+    trainer = _pendulum_trainer(tmp_path, pendulum_venv, expert)
+    episode_length, min_eps = 200, 2
+    trainer.train(total_timesteps=episode_length * num_episodes, bc_train_kwargs=dict(n_batches=10),
+                  rollout_round_min_episodes=min_eps, rollout_round_min_timesteps=1)
+    per_round = max(min_eps, pendulum_venv.num_envs)
+    rounds = sorted(glob.glob(os.path.join(str(tmp_path), "demos", "round-*")))
+    assert len(rounds) == math.ceil(num_episodes / per_round)
+    for d in rounds:
+        assert len(glob.glob(os.path.join(d, "*dagger-demo-*.npz"))) == per_round
+
+
+def test_trainer_reproducible(tmp_path, pendulum_venv):
+    expert = RandomPolicy(pendulum_venv.observation_space, pendulum_venv.action_space)
+    params = []
+    for k in range(2):
+        pendulum_venv.seed(7)
+        expert.action_space.seed(7)
+        tr = _pendulum_trainer(tmp_path / str(k), pendulum_venv, expert, seed=3)
+        tr.train(total_timesteps=400, bc_train_kwargs=dict(n_batches=5), rollout_round_min_episodes=1,
+                 rollout_round_min_timesteps=1)
+        params.append([p.detach().clone() for p in tr.policy.parameters()])
+    assert all(th.equal(a, b) for a, b in zip(*params))
+
+
+def test_policy_save_reload(tmp_path, pendulum_venv):
+    expert = RandomPolicy(pendulum_venv.observation_space, pendulum_venv.action_space)
+    tr = _pendulum_trainer(tmp_path, pendulum_venv, expert)
+    path = tmp_path / "policy.pt"
+    util.save_policy(tr.policy, path)
+    pol = bc.reconstruct_policy(str(path))
+    obs = np.stack([pendulum_venv.observation_space.sample() for _ in range(8)]).astype(np.float32)
+    np.testing.assert_allclose(pol.predict(obs, deterministic=True)[0], tr.policy.predict(obs, deterministic=True)[0])
+
+
+@pytest.mark.parametrize("which", ["observation", "action"])
+def test_simple_dagger_space_mismatch_error(tmp_path, pendulum_venv, which):
+    from imitation_amd.envs import spaces
+
+    obs_space = spaces.Box(-1, 1, (5,)) if which == "observation" else pendulum_venv.observation_space
+    act_space = spaces.Box(-1, 1, (4,)) if which == "action" else pendulum_venv.action_space
+    expert = RandomPolicy(obs_space, act_space)
+    with pytest.raises(ValueError, match=f"Mismatched {which}.*"):
+        _pendulum_trainer(tmp_path, pendulum_venv, expert)
+
+
+def test_dagger_not_enough_transitions_error(tmp_path, custom_logger, rng):
+    venv = util.make_vec_env("CartPole-v0", rng=rng)
+    bct = bc.BC(observation_space=venv.observation_space, action_space=venv.action_space, batch_size=100_000,
+                custom_logger=custom_logger, rng=rng)
+    trainer = dagger.DAggerTrainer(venv=venv, scratch_dir=tmp_path, bc_trainer=bct, custom_logger=custom_logger, rng=rng)
+    collector = trainer.create_trajectory_collector()
+    policy = RandomPolicy(venv.observation_space, venv.action_space)
+    rollout.generate_trajectories(policy, collector, rollout.make_min_episodes(1), rng=rng)
+    with pytest.raises(ValueError, match="Not enough transitions.*"):
+        trainer.extend_and_update()
+
+
+def test_trainer_train_arguments(tmp_path, pendulum_venv):
+    """``train`` forwards bc_train_kwargs and stops once ``total_timesteps`` are collected."""
+    expert = RandomPolicy(pendulum_venv.observation_space, pendulum_venv.action_space)
+    tr = _pendulum_trainer(tmp_path, pendulum_venv, expert)
+    tr.train(total_timesteps=200, bc_train_kwargs=dict(n_epochs=1, progress_bar=False),
+             rollout_round_min_episodes=1, rollout_round_min_timesteps=1)
+    assert tr.round_num >= 1
+    with pytest.raises(ValueError):
+        tr.train(total_timesteps=200, bc_train_kwargs=dict(n_epochs=1, n_batches=5),
+                 rollout_round_min_episodes=1, rollout_round_min_timesteps=1)
