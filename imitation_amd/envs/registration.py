@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import functools
 
-from imitation_amd.envs import core, tabular
+from imitation_amd.envs import core, tabular, toy_text  # noqa: F401  (toy_text registers FrozenLake)
 
 _NATIVE_IDS = {
     "CartPole-v0": 200,
