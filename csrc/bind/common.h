@@ -22,5 +22,6 @@ void register_kernels(py::module& m);
 void register_engine(py::module& m);
 void register_disc(py::module& m);
 void register_airl(py::module& m);
+void register_wide(py::module& m);
 void register_conv(py::module& m);
 void register_comm(py::module& m);

@@ -9,6 +9,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_engine(m);
   register_disc(m);
   register_airl(m);
+  register_wide(m);
   register_conv(m);
   register_comm(m);
 }

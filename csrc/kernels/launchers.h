@@ -137,6 +137,31 @@ hipError_t airl_gather(const AirlDiscArgs& a, int k, hipStream_t s);
 hipError_t airl_norm(const AirlDiscArgs& a, int mode, int n_total, hipStream_t s);
 hipError_t airl_fwd_bwd(const AirlDiscArgs& a, const AirlPlan& p, int k, hipStream_t s);
 
+// ---- wlin.hip: wide MLP layers (129..1024) on MFMA, bias / activation fused
+struct WideLinArgs {
+  int M, N, K;           // rows, layer outputs, layer inputs
+  const float* X;        // [M][K] layer input (fwd, dW)
+  const float* W;        // [N][K] nn.Linear weight
+  const float* b;        // [N] or null (fwd)
+  float* Y;              // [M][N] (fwd)
+  int act;               // fwd: activation of Y; dx: activation that produced H
+  const float* dZ;       // [M][N] gradient at this layer's pre-activation output (dx, dW)
+  float* G;              // [M][K] (dx)
+  const float* H;        // [M][K] activation output whose derivative multiplies G, or null
+  const float* scale;    // [K] per-column factor of G (input normaliser rstd) or null
+  float* dW;             // [N][K] (dW)
+  float* db;             // [N] or null (dW)
+  int accumulate;        // dW / db: add into existing values
+  float* ws;             // dW split-M partials: wlin_dw_ws_floats(M, N, K) floats (null if 0)
+  int* cnt;              // dW: wlin_dw_tiles(N, K) zero-initialised tile counters (self-resetting)
+};
+int wlin_dw_tiles(int N, int K);
+int wlin_dw_splits(int M, int N, int K);
+size_t wlin_dw_ws_floats(int M, int N, int K);
+hipError_t wlin_forward(const WideLinArgs& a, hipStream_t s);
+hipError_t wlin_backward_x(const WideLinArgs& a, hipStream_t s);
+hipError_t wlin_backward_w(const WideLinArgs& a, hipStream_t s);
+
 // ---- dagger.hip: device env step of the DAgger collector (one workgroup per env)
 struct DaggerEnvArgs {
   EnvParams P;

@@ -269,7 +269,12 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
                 self.optimizer.step()
                 return metrics
 
-            g = self._graph_step = graphs.GraphedTrainStep(step, self.optimizer)
+            def release():
+                dist = getattr(self.policy, "action_dist", None)
+                if dist is not None and hasattr(dist, "detach_"):
+                    dist.detach_()
+
+            g = self._graph_step = graphs.GraphedTrainStep(step, self.optimizer, release)
         return g
 
     def _zero_grad(self):

@@ -146,7 +146,85 @@ class _TMLPFn(torch.autograd.Function):
 
 
 def kernel_supports(dims: Sequence[int]) -> bool:
+    """The whole-network-in-LDS tiny-MLP kernel (tmlp.hip)."""
     return 1 <= len(dims) - 1 <= 4 and max(dims) <= 128
+
+
+WIDE_MAX = 1024
+
+
+def wide_supports(dims: Sequence[int]) -> bool:
+    """The per-layer wide kernels (wlin.hip): widths up to 1024, any depth."""
+    return 1 <= len(dims) - 1 <= 16 and max(dims) <= WIDE_MAX
+
+
+def fusable(dims: Sequence[int]) -> bool:
+    """Whether :func:`tmlp` runs this MLP on a HIP kernel (tiny or wide path)."""
+    return kernel_supports(dims) or wide_supports(dims)
+
+
+def _act_grad_from_out(code: int, y: torch.Tensor) -> torch.Tensor:
+    if code == 1:
+        return (y > 0).to(y.dtype)
+    if code == 2:
+        return 1.0 - y * y
+    if code == 3:
+        return torch.where(y > 0, torch.ones_like(y), torch.full_like(y, 0.01))
+    if code == 4:
+        return y * (1.0 - y)
+    return torch.ones_like(y)
+
+
+class _WideMLPFn(torch.autograd.Function):
+    """MLPs wider than the tiny-MLP kernel (the fork's [256, 256, 128] multi-agent policy,
+    SAC1024Policy [1024, 1024]): one ``wlin_forward`` launch per layer (GEMM + bias +
+    activation), and per layer in the backward one ``wlin_backward_w`` (dW and db) and one
+    ``wlin_backward_x`` (dX times the previous activation's derivative) -- bf16 MFMA
+    operands, fp32 accumulation (csrc/kernels/wlin.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, hidden_act, out_act, mean, var, eps, *params):
+        from imitation_amd.ops import native
+
+        C = native()
+        ws = [p.contiguous() for p in params[0::2]]
+        bs = [p.contiguous() for p in params[1::2]]
+        h = x.contiguous()
+        rstd = None
+        if mean is not None:
+            rstd = torch.rsqrt(var + eps)
+            h = ((h - mean) * rstd).contiguous()
+        hs = [h]
+        L = len(ws)
+        for l in range(L):
+            h = C.wlin_forward(h, ws[l], bs[l], int(out_act if l == L - 1 else hidden_act))
+            hs.append(h)
+        ctx.cfg = (int(hidden_act), int(out_act), L, rstd is not None)
+        ctx.save_for_backward(*hs, *ws, *([rstd] if rstd is not None else []))
+        return h
+
+    @staticmethod
+    def backward(ctx, dy):
+        from imitation_amd.ops import native
+
+        C = native()
+        hidden_act, out_act, L, has_norm = ctx.cfg
+        saved = ctx.saved_tensors
+        hs, ws = saved[: L + 1], saved[L + 1 : 2 * L + 1]
+        rstd = saved[2 * L + 1] if has_norm else None
+        dz = dy.contiguous()
+        if out_act != 0:
+            dz = (dz * _act_grad_from_out(out_act, hs[L])).contiguous()
+        grads = [None] * (2 * L)
+        dx = None
+        for l in range(L - 1, -1, -1):
+            dW, db = C.wlin_backward_w(dz, hs[l], True)
+            grads[2 * l], grads[2 * l + 1] = dW, db
+            if l > 0:
+                dz = C.wlin_backward_x(dz, ws[l], hs[l], hidden_act, None)
+            elif ctx.needs_input_grad[0]:
+                dx = C.wlin_backward_x(dz, ws[0], None, 0, rstd)
+        return (dx, None, None, None, None, None, *grads)
 
 
 def tmlp(
@@ -161,7 +239,8 @@ def tmlp(
 ) -> torch.Tensor:
     """Fused MLP forward (differentiable w.r.t. ``x`` and every weight / bias).
 
-    GPU fp32 tensors go through the HIP kernel; everything else through
+    GPU fp32 tensors go through a HIP kernel -- the whole-network tiny-MLP kernel for widths
+    <= 128, the per-layer wide kernels up to 1024 -- everything else through
     :func:`tmlp_reference`.
     """
     from imitation_amd.ops import use_kernel
@@ -171,7 +250,7 @@ def tmlp(
         use_kernel(x)
         and x.dtype == torch.float32
         and x.dim() == 2
-        and kernel_supports(dims)
+        and fusable(dims)
         and all(w.dtype == torch.float32 for w in weights)
     ):
         if norm_mean is not None:
@@ -180,7 +259,8 @@ def tmlp(
         params = []
         for w, b in zip(weights, biases):
             params += [w, b]
-        return _TMLPFn.apply(x, hidden_act, out_act, norm_mean, norm_var, norm_eps, *params)
+        fn = _TMLPFn if kernel_supports(dims) else _WideMLPFn
+        return fn.apply(x, hidden_act, out_act, norm_mean, norm_var, norm_eps, *params)
     return tmlp_reference(x, weights, biases, hidden_act, out_act, norm_mean, norm_var, norm_eps)
 
 

@@ -57,6 +57,22 @@ class Distribution:
         actions = self.actions_from_params(*args, **kwargs)
         return actions, self.log_prob(actions)
 
+    def detach_(self) -> "Distribution":
+        """Detach the stored parameters from their autograd graph.
+
+        The policy keeps ONE distribution object that every ``get_distribution`` call
+        re-parametrises, so its tensors keep the last forward's graph -- and through it the
+        parameters' AccumulateGrad nodes -- alive. Graph capture needs those nodes created
+        on the capture stream (``utils.graphs.GraphedTrainStep`` calls this first)."""
+        for k, v in vars(self).items():
+            if isinstance(v, th.Tensor) and v.grad_fn is not None:
+                setattr(self, k, v.detach())
+            elif isinstance(v, list):
+                for d in v:
+                    if isinstance(d, Distribution):
+                        d.detach_()
+        return self
+
 
 class DiagGaussianDistribution(Distribution):
     """Gaussian with diagonal covariance; ``log_std`` is a free parameter."""

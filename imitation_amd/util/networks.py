@@ -30,7 +30,7 @@ import torch as th
 from torch import nn
 
 from imitation_amd import ops
-from imitation_amd.ops.mlp import act_code, kernel_supports
+from imitation_amd.ops.mlp import act_code, fusable
 
 
 @contextlib.contextmanager
@@ -223,7 +223,7 @@ class MLP(nn.Sequential):
         if plan is not False:
             hid = set(acts[:-1])
             dims = [linears[0].in_features] + [l.out_features for l in linears] if linears else []
-            if not linears or len(hid) > 1 or not kernel_supports(dims):
+            if not linears or len(hid) > 1 or not fusable(dims):
                 plan = False
             else:
                 plan = dict(

@@ -21,7 +21,7 @@ callers check this: one fixed minibatch size, no DP gradient bucket).
 from __future__ import annotations
 
 import os
-from typing import Any, Callable, Dict, Tuple
+from typing import Any, Callable, Dict, Optional, Tuple
 
 import torch as th
 
@@ -50,9 +50,15 @@ def supports_capture(optimizer: th.optim.Optimizer) -> bool:
 class GraphedTrainStep:
     """``step(*inputs) -> outputs`` with ``fn`` captured as a HIP graph per input signature."""
 
-    def __init__(self, fn: Callable[..., Any], optimizer: th.optim.Optimizer):
+    def __init__(self, fn: Callable[..., Any], optimizer: th.optim.Optimizer,
+                 release: Optional[Callable[[], None]] = None):
         self.fn = fn
         self.optimizer = optimizer
+        # drops references the caller's objects hold to an earlier autograd graph (e.g. the
+        # policy's distribution object): such a graph keeps the parameters' AccumulateGrad
+        # nodes alive with the stream they were created on, and a backward that meets them
+        # inside the capture synchronises with that stream -- illegal during capture
+        self.release = release
         self._graphs: Dict[Tuple, Tuple[Tuple[th.Tensor, ...], Any, Any]] = {}
         self.n_captures = 0
         self.n_replays = 0
@@ -68,17 +74,24 @@ class GraphedTrainStep:
             self.n_replays += 1
             return out
         make_capturable(self.optimizer)
+        if self.release is not None:
+            self.release()
         static = tuple(t.detach().clone() for t in inputs)
         side = th.cuda.Stream()
         side.wait_stream(th.cuda.current_stream())
         with th.cuda.stream(side):  # warm-up == this step
             self.optimizer.zero_grad(set_to_none=True)
             result = self.fn(*static)
-        th.cuda.current_stream().wait_stream(side)
         self.optimizer.zero_grad(set_to_none=True)
+        if self.release is not None:
+            self.release()
         graph = th.cuda.CUDAGraph()
-        with th.cuda.graph(graph):
+        # capture on the warm-up stream: the autograd nodes the warm-up created (e.g. the
+        # parameters' AccumulateGrad) belong to that stream, and a capture on another stream
+        # would make the engine synchronise with it inside the capture
+        with th.cuda.graph(graph, stream=side):
             out = self.fn(*static)
+        th.cuda.current_stream().wait_stream(side)
         self._graphs[key] = (static, graph, out)
         self.n_captures += 1
         return result

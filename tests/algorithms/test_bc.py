@@ -102,6 +102,7 @@ def test_bc_loss_calculator_values():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env_id", ["CartPole-v1", "PongNoFrameskip-v4"])
+@pytest.mark.filterwarnings("error:The AccumulateGrad node's stream")
 def test_bc_graph_replay_matches_eager(monkeypatch, env_id):
     """The HIP-graph BC step (utils/graphs.GraphedTrainStep) == the eager step: same
     parameters after several batches and the same logged metrics (both with the
@@ -171,3 +172,57 @@ def test_multibc_trains_on_agent_concatenated_batches():
     pred, _ = trainer.policy.predict(obs, deterministic=True)
     assert pred.shape == (N, n_agents)
     assert (pred == acts).mean() > 0.9
+
+
+@pytest.mark.gpu
+@pytest.mark.filterwarnings("error:The AccumulateGrad node's stream")
+def test_multibc_homogeneous_policy_runs_on_wide_kernel():
+    """The fork's MultiBC with its default HomogenousFeedForward32Policy ([256, 256, 128],
+    reference policies/base.py:222-234): the agent-concatenated batch goes through the wide
+    MFMA kernels (wlin.hip), the loss equals the fp32 torch loss on the same concatenation
+    within bf16 tolerance, and a few training steps run on the kernel."""
+    import torch as th
+
+    from imitation_amd import ops
+    from imitation_amd.algorithms import bc
+    from imitation_amd.data import types
+    from imitation_amd.envs import spaces
+    from imitation_amd.ops import mlp as mlp_ops
+    from imitation_amd.util import logger
+
+    rng = np.random.default_rng(0)
+    d, n_agents, N = 12, 4, 1024
+    obs = rng.standard_normal((N, d * n_agents)).astype(np.float32)
+    acts = np.stack([(obs[:, d * i] > 0).astype(np.int64) for i in range(n_agents)], axis=1)
+    obs_over = lambda i, o: o[:, d * i: d * i + d]  # noqa: E731
+    act_over = lambda i, a: a[:, i]  # noqa: E731
+    demos = types.TransitionsMinimal(obs=obs, acts=acts, infos=np.array([{}] * N))
+    th.manual_seed(0)
+    trainer = bc.MultiBC(single_agent_observation_space=spaces.Box(-10, 10, (d,)), single_agent_action_space=spaces.Discrete(2),
+                         observation_overide=obs_over, action_overide=act_over, num_agents=n_agents,
+                         rng=np.random.default_rng(0), demonstrations=demos, batch_size=64, device="cuda",
+                         optimizer_kwargs=dict(lr=1e-3), custom_logger=logger.configure(format_strs=[]))
+    pol = trainer.policy
+    plan = pol._fusion()
+    assert plan, "homogeneous policy heads must be fused"
+    dims = [pol.features_dim] + [l.out_features for l in plan["pi"]]
+    assert dims[1:3] == [256, 256] and not mlp_ops.kernel_supports(dims) and mlp_ops.wide_supports(dims)
+    batch = {"obs": obs[:64], "acts": th.as_tensor(acts[:64])}
+    o_cat, a_cat = trainer._prepare_batch(batch)
+    o_cat, a_cat = o_cat.cuda(), a_cat.cuda()
+    loss_kernel = float(trainer.loss_calculator(pol, o_cat, a_cat).loss.detach())
+    import os
+
+    os.environ["IMITATION_AMD_FUSED"] = "0"
+    try:
+        loss_torch = float(trainer.loss_calculator(pol, o_cat, a_cat).loss.detach())
+    finally:
+        os.environ.pop("IMITATION_AMD_FUSED", None)
+    assert abs(loss_kernel - loss_torch) < 2e-2 * max(1.0, abs(loss_torch))
+    # the metrics (and the policy's distribution object, which training releases) are the
+    # only holders of these eager graphs: nothing may keep one alive into the graph capture
+    p0 = [p.detach().clone() for p in pol.parameters()]
+    trainer.train(n_batches=20, progress_bar=False, log_interval=10**9)
+    th.cuda.synchronize()
+    assert all(th.isfinite(p).all() for p in pol.parameters())
+    assert any(not th.equal(a, b) for a, b in zip(p0, pol.parameters()))

@@ -309,3 +309,72 @@ def test_gather_rows_kernel_matches_indexing(n_envs):
     o = rl_ops.gather_rows([srcs[1].cuda()], bad, None, 1)[0].cpu() if n_envs == 1 else None
     if o is not None:
         assert th.equal(o[0], srcs[1][0]) and float(o[1:].abs().sum()) == 0.0
+
+
+@gpu
+@pytest.mark.parametrize("dims,act,B", [
+    ([20, 256, 256, 128], 2, 96),      # HomogenousFeedForward32Policy trunk, agents folded into B
+    ([17, 256, 256, 6], 1, 1000),
+    ([23, 512, 512, 1], 2, 333),
+    ([17, 1024, 1024, 6], 1, 256),    # SAC1024Policy
+    ([33, 200, 129, 7], 3, 45),       # ragged widths: every tail path
+])
+@pytest.mark.parametrize("norm", [False, True])
+def test_wide_mlp_matches_fp32_linear(dims, act, B, norm):
+    """csrc/kernels/wlin.hip (wide path of ops.tmlp): forward and every gradient vs the fp32
+    F.linear reference with bf16-rounded operands (the kernel's operand precision), and the
+    forward vs plain fp32 within bf16 tolerance."""
+    from imitation_amd import ops
+
+    assert not mlp_ops.kernel_supports(dims) and mlp_ops.wide_supports(dims)
+    dev = th.device("cuda")
+    ws, bs = _mk_mlp(dims, dev)
+    x = th.randn(B, dims[0], device=dev).mul_(2.0).add_(0.5).requires_grad_(True)
+    mean = var = None
+    if norm:
+        mean = th.randn(dims[0], device=dev) * 0.3
+        var = th.rand(dims[0], device=dev) + 0.5
+    y = mlp_ops.tmlp(x, ws, bs, act, 0, mean, var)
+    wr = [w.detach().clone().requires_grad_(True) for w in ws]
+    br = [b.detach().clone().requires_grad_(True) for b in bs]
+    xr = x.detach().clone().requires_grad_(True)
+    yr = mlp_ops.tmlp_reference(xr, wr, br, act, 0, mean, var, emulate_bf16_operands=True)
+    y32 = mlp_ops.tmlp_reference(x.detach(), [w.detach() for w in ws], [b.detach() for b in bs], act, 0, mean, var)
+    scale = yr.abs().max().item() + 1e-3
+    assert (y - yr).abs().max().item() <= 2e-2 * scale
+    assert (y - y32).abs().max().item() <= 6e-2 * scale
+    gy = th.randn_like(y)
+    (y * gy).sum().backward()
+    (yr * gy).sum().backward()
+    for l in range(len(ws)):
+        ref = max(wr[l].grad.abs().max().item(), br[l].grad.abs().max().item()) + 1e-3
+        for a, b in ((ws[l], wr[l]), (bs[l], br[l])):
+            err = (a.grad - b.grad).abs().max().item()
+            assert err <= 3e-2 * ref, (l, err, ref)
+    err = (x.grad - xr.grad).abs().max().item()
+    assert err <= 3e-2 * (xr.grad.abs().max().item() + 1e-3)
+    # deterministic: fixed-order reductions
+    y2 = mlp_ops.tmlp(x.detach(), ws, bs, act, 0, mean, var)
+    assert th.equal(y.detach(), y2)
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 128), (1000, 256, 12), (300, 7, 33), (64, 1024, 1024)])
+def test_wide_dw_split_reduction_deterministic(M, N, K):
+    """wlin_backward_w splits M over blocks (csrc/kernels/wlin.hip wlin_dw_kernel): the last
+    split of every tile sums the partials in split order, so repeated launches (which reuse
+    the self-resetting tile counters) give bit-identical dW / db, equal to the fp32 product
+    of the bf16-rounded operands."""
+    from imitation_amd import _native
+
+    C = _native.load()
+    g = th.Generator(device="cuda").manual_seed(M + N + K)
+    dz = th.randn(M, N, device="cuda", generator=g)
+    x = th.randn(M, K, device="cuda", generator=g)
+    outs = [C.wlin_backward_w(dz, x, True) for _ in range(3)]
+    ref = dz.bfloat16().float().t() @ x.bfloat16().float()
+    scale = ref.abs().max().item()
+    assert (outs[0][0] - ref).abs().max().item() <= 1e-4 * scale * max(1.0, M / 256)
+    th.testing.assert_close(outs[0][1], dz.sum(0), rtol=1e-5, atol=1e-3)
+    for dw, db in outs[1:]:
+        assert th.equal(dw, outs[0][0]) and th.equal(db, outs[0][1])
