@@ -327,8 +327,9 @@ def gail_round_worker(rank, world, seed):
 
 
 def airl_round_worker(rank, world, seed):
-    """One DeviceAIRL round (shaped reward net, generic autograd discriminator update) on
-    ``cuda:0`` shared by the ranks; reports whether the update ran as a HIP-graph replay."""
+    """One DeviceAIRL round (shaped reward net) on ``cuda:0`` shared by the ranks; reports
+    whether the discriminator update ran fused (airl_disc.hip) or as a HIP-graph replay of
+    the generic autograd update (``IMITATION_AMD_AIRL_FUSED=0``)."""
     from imitation_amd.data import rollout
     from imitation_amd.engine.airl import DeviceAIRL
     from imitation_amd.parallel import oneshot
@@ -362,6 +363,7 @@ def airl_round_worker(rank, world, seed):
     return {"reward": [p.detach().cpu().numpy().copy() for p in rn.parameters()],
             "norm": [b.detach().cpu().numpy().copy() for b in rn.buffers()],
             "graphed": graphed, "replays": 0 if g is None else g.n_replays,
+            "fused": bool(getattr(tr, "_fused_disc", False)),
             "oneshot_calls": 0 if c is None else c.calls}
 
 

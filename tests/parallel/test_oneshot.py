@@ -72,12 +72,13 @@ def test_airl_dp_discriminator_graphed_on_oneshot(monkeypatch):
     one-shot gradient mean and normaliser moments; replicas stay bit-identical and track the
     eager gloo path (fp64 moments there, fp32 Chan merge here)."""
     monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("IMITATION_AMD_AIRL_FUSED", "0")
     monkeypatch.setenv("IMITATION_AMD_ONESHOT", "1")
     one = run_ranks(W.airl_round_worker, 2, 3, timeout=300)
     monkeypatch.setenv("IMITATION_AMD_ONESHOT", "0")
     ref = run_ranks(W.airl_round_worker, 2, 3, timeout=300)
     assert one[0]["graphed"] and one[0]["replays"] >= 2 and one[0]["oneshot_calls"] > 0
-    assert not ref[0]["graphed"]
+    assert not ref[0]["graphed"] and not one[0]["fused"]
     for key in ("reward", "norm"):
         for a, b in zip(one[0][key], one[1][key]):
             np.testing.assert_array_equal(a, b)
@@ -85,6 +86,30 @@ def test_airl_dp_discriminator_graphed_on_oneshot(monkeypatch):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
     for a, b in zip(one[0]["reward"], ref[0]["reward"]):
         np.testing.assert_allclose(a, b, rtol=1e-3, atol=5e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("oneshot", ["1", "0"])
+def test_airl_dp_fused_discriminator_replicas(monkeypatch, oneshot):
+    """The fused AIRL discriminator update (airl_disc.hip) under DP: normaliser sums and the
+    flat gradient are all-reduced between its launches (one-shot IPC or gloo), so the
+    replicas stay bit-identical and track the generic eager DP update within the bf16
+    operand tolerance."""
+    monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", oneshot)
+    fused = run_ranks(W.airl_round_worker, 2, 3, timeout=300)
+    monkeypatch.setenv("IMITATION_AMD_AIRL_FUSED", "0")
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", "0")
+    ref = run_ranks(W.airl_round_worker, 2, 3, timeout=300)
+    assert fused[0]["fused"] and fused[1]["fused"] and not ref[0]["fused"]
+    assert (fused[0]["oneshot_calls"] > 0) == (oneshot == "1")
+    for key in ("reward", "norm"):
+        for a, b in zip(fused[0][key], fused[1][key]):
+            np.testing.assert_array_equal(a, b)
+    for a, b in zip(fused[0]["norm"], ref[0]["norm"]):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    for a, b in zip(fused[0]["reward"], ref[0]["reward"]):
+        np.testing.assert_allclose(a, b, rtol=1e-2, atol=1e-2)
 
 
 @pytest.mark.gpu
