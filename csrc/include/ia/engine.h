@@ -192,6 +192,11 @@ struct PPORcGeo {
   float* red;              // [2][n_items][256] reduced gradients (two-level exchange)
   int xchg2;               // two-level exchange: item id reduced by workgroup id % G, then shared
   unsigned* sync;          // [0] arrival counter, [1] timeout flag, [2] second-level arrivals (zeroed per launch)
+  // net split (G == 1): workgroup q runs net q only (actor 0 / critic 1) on its own CU; the
+  // two meet once per minibatch to sum |g|^2 for clip_grad_norm_. Items of net q: weight tiles
+  // [wbase[q], wbase[q] + nwit[q]), bias / log_std vectors [bbase[q], bbase[q] + nbit[q]).
+  int ns;
+  int wbase[2], nwit[2], bbase[2], nbit[2];
 };
 
 }  // namespace ia

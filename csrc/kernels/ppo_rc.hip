@@ -396,9 +396,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   const int tid = threadIdx.x;
   const int w = rfl(tid >> 6), lane = tid & 63;
   const int r16 = lane & 15, kk = lane >> 4;
-  const int q = w / kHalf;  // 0 actor, 1 critic
-  const int gw = w % kHalf;  // row tile
-  const int grp = blockIdx.x;
+  const bool ns = g.ns != 0;  // net split: this workgroup runs net blockIdx.x only
+  const int q = ns ? (int)blockIdx.x : w / kHalf;  // 0 actor, 1 critic
+  const int gw = ns ? w : w % kHalf;               // row tile
+  const int grp = ns ? 0 : (int)blockIdx.x;        // row group
   const int G = g.G, nch = g.nch, cw = CWT > 0 ? CWT : g.cw;
   const int CH = G * nch;
   const int Bg = CH * cw;  // minibatch rows
@@ -450,8 +451,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     run_v = a.norm_var[nc];
     run_c = a.norm_count[0];
   }
-  // owned items: gradient / moments registers
+  // owned items: gradient / moments registers. Weight slot it of this wave is item
+  // wb + w + it * NW (valid below nwq), bias slot ib is item bb + w + ib * NW (valid below nbq).
   const int n_witems = rfl(g.n_witems);
+  const int wb = ns ? rfl(g.wbase[q]) : 0, nwq = ns ? rfl(g.nwit[q]) : n_witems;
+  const int bb = ns ? rfl(g.bbase[q]) : n_witems, nbq = ns ? rfl(g.nbit[q]) : n_items - n_witems;
   float gm[KW][4], gv[KW][4];  // weight tiles: Adam moments
   f4 gg[KW];                   // and gradient (the dW MFMA chains accumulate into it)
   float bm[KB], bv[KB], bg[KB];           // bias / log_std vectors
@@ -460,9 +464,8 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
     for (int j = 0; j < 4; ++j) gm[it][j] = gv[it][j] = 0.f;
     gg[it] = {0.f, 0.f, 0.f, 0.f};
-    const int id = w + it * kWaves;
-    if (id < n_witems) {
-      const int desc = rfl(g.items[id]);
+    if (w + it * kWaves < nwq) {
+      const int desc = rfl(g.items[wb + w + it * kWaves]);
       const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
       const int din = g.din[iq][il], dout = g.dout[iq][il];
       const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
@@ -480,9 +483,8 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
   for (int ib = 0; ib < KB; ++ib) {
     bm[ib] = bv[ib] = bg[ib] = 0.f;
-    const int id = n_witems + w + ib * kWaves;
-    if (id < n_items) {
-      const int desc = rfl(g.items[id]);
+    if (w + ib * kWaves < nbq) {
+      const int desc = rfl(g.items[bb + w + ib * kWaves]);
       const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3;
       if (kind == 1) {
         const int dout = g.dout[iq][il];
@@ -515,7 +517,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // dW item operands: this wave's valid weight slots are its first nwi (ids < n_witems);
   // the LDS offsets of a slot's dZ / H columns are a wave-uniform base (the descriptor) plus
   // ONE lane term shared by every slot (all K-major images have the row stride cw + 4)
-  const int nwi = n_witems > w ? min(KW, (n_witems - w + kWaves - 1) / kWaves) : 0;
+  const int nwi = nwq > w ? min(KW, (nwq - w + kWaves - 1) / kWaves) : 0;
   const int rq = cw / 4;  // K-major image: row r at (r & 3) * rq + (r >> 2)
   const int ldr = rfl(g.ldz[0][0]);
   const int lterm = r16 * ldr + kk * rq;
@@ -524,13 +526,12 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   float b_okf[KB];  // 1 for lanes holding a real bias / log_std element
 #pragma unroll
   for (int ib = 0; ib < KB; ++ib) {
-    const int id = n_witems + w + ib * kWaves;
     bkind[ib] = -1;
     b_off[ib] = 0;
     b_okf[ib] = 0.f;
     b_addr[ib] = g.trash_off + lane;
-    if (id >= n_items) continue;
-    const int desc = rfl(g.items[id]);
+    if (w + ib * kWaves >= nbq) continue;
+    const int desc = rfl(g.items[bb + w + ib * kWaves]);
     const int iq = desc & 1, il = (desc >> 1) & 3, kind = (desc >> 3) & 3;
     const LG y = lg(g, iq, il);
     bkind[ib] = kind;
@@ -601,7 +602,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
           for (int s = 0; s < 16; ++s) xb[s] = s < s0 ? (cur.x[s] - nmv[s]) * nrv[s] : 0.f;
         }
-        if (q == 0) {  // shared layer-0 input image
+        if (q == 0 || ns) {  // shared layer-0 input image (each workgroup its own under net split)
           const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
 #pragma unroll
           for (int s = 0; s < 16; ++s)
@@ -896,9 +897,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) dzc[u2] = nd[u2];
         }
-        if (a.prof && lane == 0 && (w == 0 || w == 4)) {
+        if (a.prof && lane == 0 && gw == 0) {
           const unsigned long long c4 = clock64();
-          const int pb = w == 4 ? 7 : 3;
+          const int pb = q == 1 ? 7 : 3;
           sprof[pb + 0] += c1 - c0;
           sprof[pb + 1] += c2 - c1;
           sprof[pb + 2] += c3 - c2;
@@ -926,9 +927,8 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
         for (int it = 0; it < KW; ++it) {
           izo[it] = iho[it] = g.zero_off;
-          const int id = w + it * kWaves;
           if (it < nwi) {
-            const int desc = rfl(g.items[id]);
+            const int desc = rfl(g.items[wb + w + it * kWaves]);
             const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
             izo[it] = rfl(g.z_off[iq][il]) + 16 * ta * ldr + lterm;
             iho[it] = rfl(g.h_off[iq][il]) + 16 * tb * ldr + lterm;
@@ -966,12 +966,12 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       f4 xg[KI];
 #pragma unroll
       for (int it = 0; it < KW; ++it) {
-        ids[it] = it < nwi ? w + it * kWaves : -1;
+        ids[it] = it < nwi ? wb + w + it * kWaves : -1;
         xg[it] = gg[it];
       }
 #pragma unroll
       for (int ib = 0; ib < KB; ++ib) {
-        ids[KW + ib] = bkind[ib] >= 0 ? n_witems + w + ib * kWaves : -1;
+        ids[KW + ib] = bkind[ib] >= 0 ? bb + w + ib * kWaves : -1;
         xg[KW + ib] = {bg[ib], 0.f, 0.f, 0.f};
       }
       float* slab = g.slab + (size_t)(k & 1) * G * n_items * 256;
@@ -1008,9 +1008,8 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         float* red = g.red + (size_t)(k & 1) * n_items * 256;
         const size_t gs = (size_t)n_items * 256;
         const auto slot_id = [&](int sl) -> int {  // item id of owned slot sl (computed: no array lookup)
-          if (sl < KW) return sl < nwi ? w + sl * kWaves : -1;
-          const int id = n_witems + w + (sl - KW) * kWaves;
-          return id < n_items ? id : -1;
+          if (sl < KW) return sl < nwi ? wb + w + sl * kWaves : -1;
+          return w + (sl - KW) * kWaves < nbq ? bb + w + (sl - KW) * kWaves : -1;
         };
         if (G == 2) reduce_slots<2, KI>(slab, red, gs, grp, lane, slot_id);
         else if (G == 4) reduce_slots<4, KI>(slab, red, gs, grp, lane, slot_id);
@@ -1113,7 +1112,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     ss = wave_sum(ss);
     if (lane == 0) L[g.red_off + w] = ss;
     // Gaussian entropy loss uses log_std before this minibatch's update
-    if (gauss && tid == 0 && grp == 0) {
+    if (gauss && tid == 0 && grp == 0 && q == 0) {
       float sl = 0.f;
       for (int j = 0; j < A; ++j) sl += has_ls ? L[g.ls_off + j] : 0.f;
       st_ent += -(sl + A * (0.5f + c_half_log2pi));
@@ -1125,6 +1124,33 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     float tot = 0.f;
 #pragma unroll
     for (int i = 0; i < kWaves; ++i) tot += L[g.red_off + i];
+    if (ns) {
+      // the other net's |g|^2: ONE tagged 8-B agent-scope atomic each way (minibatch tag in
+      // the high word; MI355X_MICROARCH inter-workgroup visibility: 8-B agent atomics both
+      // sides), polled by the other workgroup; summed actor + critic in both workgroups so
+      // that they apply the identical clip
+      const unsigned long long x0 = a.prof ? clock64() : 0;
+      if (tid == 0) {
+        unsigned long long* xs = reinterpret_cast<unsigned long long*>(g.sync + 8);
+        const unsigned long long tag = (unsigned long long)(unsigned)(k + 1) << 32;
+        __hip_atomic_store(xs + q, tag | __float_as_uint(tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long o = __hip_atomic_load(xs + (1 - q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while ((o >> 32) != (unsigned long long)(unsigned)(k + 1)) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 22) || ld_sc1u(tflag) != 0u) {
+            atomicOr(tflag, 1u);
+            break;
+          }
+          o = __hip_atomic_load(xs + (1 - q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const float other = __uint_as_float((unsigned)(o & 0xffffffffu));
+        L[g.red_off + 48] = q == 0 ? tot + other : other + tot;
+      }
+      __syncthreads();
+      tot = L[g.red_off + 48];
+      if (a.prof && tid == 0) sprof[14] += clock64() - x0;  // (net split: the |g|^2 hand-off)
+    }
     const float coef = fminf(1.f, a.max_grad_norm / (sqrtf(tot) + 1e-6f));
     step += 1.f;
     b1t *= a.beta1;
@@ -1145,7 +1171,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       paddr[it] = g.trash_off + lane;
       pstr[it] = 0;
       if (it < nwi) {
-        const int desc = rfl(g.items[w + it * kWaves]);
+        const int desc = rfl(g.items[wb + w + it * kWaves]);
         const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
         const int ldw = rfl(g.ldw[iq][il]);
         paddr[it] = rfl(g.w_off[iq][il]) + (16 * ta + 4 * kk) * ldw + 16 * tb + r16;
@@ -1201,17 +1227,19 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     float s = 0.f;
     for (int i = 0; i < kWaves; ++i) s += L[g.red_off + 8 + i * 5 + tid];
     if (!(tid == 0 && gauss)) s *= invB;  // per-row sums -> sums of minibatch means
-    if (G > 1) atomicAdd(a.stats + tid, s);
+    if (G > 1 || ns) atomicAdd(a.stats + tid, s);
     else a.stats[tid] += s;
   }
   if (grp != 0) return;  // every workgroup holds the identical model: one writes it back
+  // (net split: each workgroup writes its own net, the actor workgroup the shared state)
+  const bool shared_wb = !ns || q == 0;
 
   // ---- write back: params (from LDS), moments (owners), log_std, normaliser
 #pragma unroll
   for (int qq = 0; qq < 2; ++qq) {
 #pragma unroll
     for (int l = 0; l < kL; ++l) {
-      if (l >= (qq == 0 ? a.n_pi : a.n_vf)) continue;
+      if (l >= (qq == 0 ? a.n_pi : a.n_vf) || (ns && qq != q)) continue;
       const LG y = lg(g, qq, l);
       const int wo = qq == 0 ? a.pi_w_off[l] : a.vf_w_off[l];
       const int bo = qq == 0 ? a.pi_b_off[l] : a.vf_b_off[l];
@@ -1222,11 +1250,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       for (int i = tid; i < y.dout; i += kThreads) a.params[bo + i] = L[y.b + i];
     }
   }
-  if (has_ls && tid < A) a.params[a.log_std_off + tid] = L[g.ls_off + tid];
+  if (shared_wb && has_ls && tid < A) a.params[a.log_std_off + tid] = L[g.ls_off + tid];
 #pragma unroll
   for (int it = 0; it < KW; ++it) {
     if (it >= nwi) continue;
-    const int desc = rfl(g.items[w + it * kWaves]);
+    const int desc = rfl(g.items[wb + w + it * kWaves]);
     const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
     const int din = g.din[iq][il], dout = g.dout[iq][il];
     const int wo = iq == 0 ? a.pi_w_off[il] : a.vf_w_off[il];
@@ -1243,19 +1271,19 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
   for (int ib = 0; ib < KB; ++ib) {
     if (bkind[ib] < 0 || b_okf[ib] == 0.f) continue;
-    const int desc = rfl(g.items[n_witems + w + ib * kWaves]);
+    const int desc = rfl(g.items[bb + w + ib * kWaves]);
     const int iq = desc & 1, il = (desc >> 1) & 3;
     const int off = bkind[ib] == 1 ? (iq == 0 ? a.pi_b_off[il] : a.vf_b_off[il]) : a.log_std_off;
     a.exp_avg[off + lane] = bm[ib];
     a.exp_avg_sq[off + lane] = bv[ib];
   }
-  if (norm_lane && K > 0) {
+  if (shared_wb && norm_lane && K > 0) {
     a.norm_mean[nc] = run_m;
     a.norm_var[nc] = run_v;
     if (nc == 0) a.norm_count[0] = run_c;
   }
-  if (tid == 0) a.adam_step[0] = step;
-  if (a.prof && tid < 16) a.prof[tid] += sprof[tid];  // (stats barrier above orders the LDS)
+  if (shared_wb && tid == 0) a.adam_step[0] = step;
+  if (shared_wb && a.prof && tid < 16) a.prof[tid] += sprof[tid];  // (stats barrier above orders the LDS)
 }
 
 // waves per workgroup (NW) and owned weight / bias slots per wave of each tile width
@@ -1281,6 +1309,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.kt = wmax <= 32 ? 2 : 4;
   const int KT = g.kt;
   g.nw = waves_for(KT);
+  const char* nsev = getenv("IMITATION_AMD_PPO_NETSPLIT");
+  const bool want_ns = KT == 2 && !(nsev && nsev[0] == '0');
   // workgroup split: chunks of cw rows (64 for narrow nets, 32 for 64-wide ones: LDS, and
   // the 4-wave workgroup has 2 row-tile waves per net)
   int cw = KT == 2 ? 64 : 32;
@@ -1300,6 +1330,11 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.cw = cw;
   g.G = G;
   g.nch = chunks / G;
+  // net split for the one-workgroup plan: actor and critic on two CUs, one wave per SIMD
+  // (the 4 row tiles of a 64-row chunk), instead of both nets' 8 waves sharing one CU's
+  // matrix cores; the row-tile waves of a net are exactly the workgroup's waves
+  g.ns = want_ns && G == 1 && cw == 64 ? 1 : 0;
+  if (g.ns) g.nw = 4;
   int off = 0;
   auto take = [&](int n) {
     const int o = off;
@@ -1346,15 +1381,16 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   }
   g.lsp_off = take(4 * 16);
   g.nm_off = take(256);
-  g.red_off = take(8 + 8 * 5);
+  g.red_off = take(8 + 8 * 5 + 4);  // wave |g|^2, wave stats, [48] both nets' |g|^2
   g.trash_off = take(64);
   g.lds_floats = off;
   lds_bytes = (size_t)off * 4;
   if (lds_bytes > 160 * 1024) return false;
   // items: dW tiles first (ids [0, n_witems): a wave's weight items are its first slots),
-  // then biases, then log_std
+  // actor's then critic's; then bias vectors: actor's, log_std (an actor item), critic's
   int n = 0;
   for (int q = 0; q < 2; ++q) {
+    g.wbase[q] = n;
     for (int l = 0; l < nls[q]; ++l) {
       const int to = (g.dout[q][l] + 15) / 16, ti = (g.din[q][l] + 15) / 16;
       for (int ta = 0; ta < to; ++ta)
@@ -1363,20 +1399,28 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
           g.items[n++] = q | (l << 1) | (0 << 3) | (ta << 5) | (tb << 9);
         }
     }
+    g.nwit[q] = n - g.wbase[q];
   }
   g.n_witems = n;
   for (int q = 0; q < 2; ++q) {
+    g.bbase[q] = n;
     for (int l = 0; l < nls[q]; ++l) {
       if (n >= kMaxRcItems) return false;
       g.items[n++] = q | (l << 1) | (1 << 3);
     }
-  }
-  if (!a.discrete && a.log_std_off >= 0) {
-    if (n >= kMaxRcItems) return false;
-    g.items[n++] = 2 << 3;
+    if (q == 0 && !a.discrete && a.log_std_off >= 0) {
+      if (n >= kMaxRcItems) return false;
+      g.items[n++] = 2 << 3;
+    }
+    g.nbit[q] = n - g.bbase[q];
   }
   g.n_items = n;
-  if ((g.n_witems + g.nw - 1) / g.nw > wslots_for(KT) || (n - g.n_witems + g.nw - 1) / g.nw > bslots_for(KT)) return false;
+  int wmx = g.n_witems, bmx = n - g.n_witems;
+  if (g.ns) {
+    wmx = g.nwit[0] > g.nwit[1] ? g.nwit[0] : g.nwit[1];
+    bmx = g.nbit[0] > g.nbit[1] ? g.nbit[0] : g.nbit[1];
+  }
+  if ((wmx + g.nw - 1) / g.nw > wslots_for(KT) || (bmx + g.nw - 1) / g.nw > bslots_for(KT)) return false;
   g.dp = (a.D + 3) & ~3;
   return true;
 }
@@ -1416,18 +1460,33 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64 * prep_waves), 0, s, a, g);
   // > 80 KiB of LDS keeps the cooperating workgroups one per CU (the measured condition of
   // the sc1 hand-off); all G <= kMaxRcGroups (64) of them are co-resident (256 CUs)
-  const size_t lds_launch = g.G > 1 && lds < 96 * 1024 ? 96 * 1024 : lds;
+  // (net split: the two workgroups must not share a CU's matrix cores either)
+  const size_t lds_launch = (g.G > 1 || g.ns) && lds < 96 * 1024 ? 96 * 1024 : lds;
   // shape-specialised builds for the headline configs, generic otherwise
   int hw = a.pi_dims[1];
   bool uniform = a.n_pi == 3 && a.n_vf == 3;
   for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
   const int s0 = (a.D + 3) / 4;
-  const dim3 grid(g.G), block(64 * g.nw);
-  const int nwslot = (g.n_witems + g.nw - 1) / g.nw, nbslot = (g.n_items - g.n_witems + g.nw - 1) / g.nw;
+  const dim3 grid(g.ns ? 2 : g.G), block(64 * g.nw);
+  int wmx = g.n_witems, bmx = g.n_items - g.n_witems;
+  if (g.ns) {
+    wmx = g.nwit[0] > g.nwit[1] ? g.nwit[0] : g.nwit[1];
+    bmx = g.nbit[0] > g.nbit[1] ? g.nbit[0] : g.nbit[1];
+  }
+  const int nwslot = (wmx + g.nw - 1) / g.nw, nbslot = (bmx + g.nw - 1) / g.nw;
 #define IA_RC(KT, KW, KB, S0, NL, ACT, HW, CW, DT) \
   hipLaunchKernelGGL((ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, CW, DT, waves_for(KT)>), grid, block, lds_launch, s, a, g)
+#define IA_RC_NS(KW, KB, S0, NL, ACT, HW, DT) \
+  hipLaunchKernelGGL((ppo_rc_kernel<2, KW, KB, S0, NL, ACT, HW, 64, DT, 4>), grid, block, lds_launch, s, a, g)
   const auto fits = [&](int kw, int kb) { return nwslot <= kw && nbslot <= kb; };
-  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete && fits(3, 1))
+  if (g.ns) {
+    if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && !a.discrete && fits(3, 1))
+      IA_RC_NS(3, 1, 5, 3, 2, 32, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
+    else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && a.discrete && fits(2, 1))
+      IA_RC_NS(2, 1, 1, 3, 2, 32, 1);  // CartPole FeedForward32Policy
+    else
+      IA_RC_NS(wslots_for(2), bslots_for(2), 0, 0, -1, 0, -1);
+  } else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete && fits(3, 1))
     IA_RC(2, 3, 1, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
   else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 32 && !a.discrete && fits(3, 1))
     IA_RC(2, 3, 1, 5, 3, 2, 32, 32, 0);  // the same, 32-row chunks (16 workgroups at the 8-rank DP minibatch)
@@ -1442,6 +1501,7 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   else
     IA_RC(4, wslots_for(4), bslots_for(4), 0, 0, -1, 0, 0, -1);
 #undef IA_RC
+#undef IA_RC_NS
   return hipGetLastError();
 }
 
