@@ -25,3 +25,4 @@ void register_airl(py::module& m);
 void register_wide(py::module& m);
 void register_conv(py::module& m);
 void register_comm(py::module& m);
+void register_pref(py::module& m);

@@ -12,4 +12,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_wide(m);
   register_conv(m);
   register_comm(m);
+  register_pref(m);
 }

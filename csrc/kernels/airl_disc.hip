@@ -31,14 +31,14 @@
 // bitwise reproducible.
 #include <hip/hip_runtime.h>
 
+#include "ia/dmlp.h"
 #include "ia/mfma.h"
 #include "launchers.h"
 
 namespace ia {
 namespace {
 
-constexpr int kRows = 64;  // rows per block (4 waves x 16)
-constexpr int kNW = 4;
+using namespace dmlp;  // kRows / kNW, staging, MLP forward / backward (ia/dmlp.h)
 constexpr int kGatherRows = 16;  // 8 rows per thread: >= 256 blocks for a 2 x 2048-row batch
 constexpr int kNormPhases = 8;
 
@@ -128,17 +128,6 @@ __global__ __launch_bounds__(256) void airl_gather_kernel(AirlDiscArgs a, int k)
 }
 
 // ------------------------------------------------------------------ norms
-__device__ __forceinline__ void chan_merge(float* rmean, float* rvar, int count, int c, float bmean, float bvar, int n) {
-  // RunningNorm.update_stats (networks.py:94-111), same fp32 operation order
-  const float fc = (float)count, fn = (float)n, tot = (float)(count + n);
-  const float delta = bmean - rmean[c];
-  rmean[c] += delta * fn / tot;
-  float v = rvar[c] * fc;
-  v += bvar * fn;
-  v += delta * delta * fc * fn / tot;
-  rvar[c] = v / tot;
-}
-
 __device__ __forceinline__ void put_nrm(float* nrm, int slot, int c, const float* mean, const float* var, float eps) {
   nrm[slot * 256 + c] = mean ? mean[c] : 0.f;
   nrm[slot * 256 + 128 + c] = mean ? rsqrtf(var[c] + eps) : 1.f;
@@ -216,174 +205,6 @@ __global__ __launch_bounds__(128 * kNormPhases) void airl_norm_kernel(AirlDiscAr
     if (a.merge_p && a.p_count) *a.p_count += 2 * n;
     if (a.merge_q && a.q_count) *a.q_count += n;
   }
-}
-
-// ------------------------------------------------------------------ fused forward / loss / backward
-// LDS images are bf16 [row][k] with row stride ld (K-contiguous MFMA operands, mfma.h).
-
-// rows [row0, row0 + 64) of X [B][din] -> image H (normalised with nrm slot: mean, rstd)
-__device__ void stage_rows(bf16* H, int ld, const float* __restrict__ X, int din, int B, int row0, const float* nrm) {
-  const int kp = pad32(din);
-  for (int e = threadIdx.x; e < kRows * kp; e += blockDim.x) {
-    const int r = e / kp, c = e - r * kp;
-    const int gr = row0 + r;
-    float v = 0.f;
-    if (gr < B && c < din) v = (X[(size_t)gr * din + c] - nrm[c]) * nrm[128 + c];
-    H[r * ld + c] = to_bf16(v);
-  }
-}
-
-// weight image: [o][i] (forward B^T operand) or [i][o] (transposed, backward), zero padded
-__device__ void stage_weights(bf16* dst, const float* __restrict__ W, int dout, int din, bool transposed) {
-  if (!transposed) {
-    const int ld = ld_for_k(din), R = pad32(dout), C = pad32(din);
-    for (int e = threadIdx.x; e < R * C; e += blockDim.x) {
-      const int o = e / C, i = e - o * C;
-      dst[o * ld + i] = to_bf16((o < dout && i < din) ? W[o * din + i] : 0.f);
-    }
-  } else {
-    const int ld = ld_for_k(dout), R = pad32(din), C = pad32(dout);
-    for (int e = threadIdx.x; e < R * C; e += blockDim.x) {
-      const int i = e / C, o = e - i * C;
-      dst[i * ld + o] = to_bf16((o < dout && i < din) ? W[o * din + i] : 0.f);
-    }
-  }
-}
-
-__device__ __forceinline__ float act_apply(int act, float x) { return apply_act(act, x); }
-
-// Forward of an MLP over the staged input Hs[0] (64 rows); hidden outputs go to Hs[l + 1]
-// (kept for the backward pass), the last layer's (fp32, bias added, identity) outputs to
-// out[row * out_ld + col] for col < dims[L] (<= 16). Wf[l]: pre-staged weight images.
-// Each wave works on its own 16 rows only, so layers need no barrier between them.
-__device__ void mlp_forward(const AirlNet& net, bf16* const* Hs, int ld, bf16* const* Wf, float* out, int out_ld) {
-  const int w = wave_id();
-  for (int l = 0; l < net.n_layers; ++l) {
-    const int din = net.dims[l], dout = net.dims[l + 1];
-    const bf16* Wimg = Wf[l];
-    const int K = pad32(din), ldw = ld_for_k(din);
-    const bool last = l == net.n_layers - 1;
-    const int ntiles = last ? 1 : pad32(dout) / 16;
-    const bf16* A = Hs[l] + w * 16 * ld;
-    for (int nt = 0; nt < ntiles; ++nt) {
-      f32x4 acc = mma_16x16(A, ld, Wimg + nt * 16 * ldw, ldw, K, zero4());
-      const int col = nt * 16 + acc_col();
-      const float bv = col < dout ? net.b[l][col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = w * 16 + acc_row(i);
-        if (last) {
-          if (col < dout) out[r * out_ld + col] = acc[i] + bv;
-        } else {
-          Hs[l + 1][r * ld + col] = to_bf16(col < dout ? act_apply(net.hidden_act, acc[i] + bv) : 0.f);
-        }
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ float wave_colsum(float s) {
-  s += __shfl_xor(s, 16);
-  s += __shfl_xor(s, 32);
-  return s;
-}
-
-// Backward of an MLP (identity output, dout = 1) from per-row output gradients dy[64]:
-// dW / db into slab[param offsets] (acc: add to what an earlier pass of this block wrote).
-// Scratch: HT [feature][row] (ld_ht), dZ [row][k] (ld) and dZT [k][row] (ld_ht), x2.
-__device__ void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld, bf16* const* Wt, const float* dy, bf16* HT, int ld_ht,
-                             bf16* const* dZ, bf16* const* dZT, float* dbs, int dmax_pad, float* slab, bool acc_mode) {
-  const int w = wave_id(), lane = lane_id();
-  const int L = net.n_layers;
-  // last layer: dZ = dy (identity head, one output column)
-  for (int e = threadIdx.x; e < kRows * 32; e += blockDim.x) {
-    const int r = e >> 5, c = e & 31;
-    const float v = c == 0 ? dy[r] : 0.f;
-    dZ[0][r * ld + c] = to_bf16(v);
-    dZT[0][c * ld_ht + r] = to_bf16(v);
-  }
-  float* dbs_head = dbs + 2 * kNW * dmax_pad;
-  if (threadIdx.x == 0) {  // db of the head: fixed-order sum over rows (fp32)
-    float s = 0.f;
-    for (int r = 0; r < kRows; ++r) s += dy[r];
-    *dbs_head = s;
-  }
-  int z = 0;
-  bool head = true;
-  for (int l = L - 1; l >= 0; --l) {
-    const int din = net.dims[l], dout = net.dims[l + 1];
-    __syncthreads();
-    {  // H^T image of this layer's input
-      const int C = pad32(din);
-      for (int e = threadIdx.x; e < C * kRows; e += blockDim.x) {
-        const int i = e / kRows, r = e - i * kRows;
-        HT[i * ld_ht + r] = Hs[l][r * ld + i];
-      }
-    }
-    __syncthreads();
-    // db_l
-    float* sb = slab + net.param_off + net.b_off[l];
-    for (int c = threadIdx.x; c < dout; c += blockDim.x) {
-      float s;
-      if (head) {
-        s = *dbs_head;
-      } else {
-        s = 0.f;
-        for (int ww = 0; ww < kNW; ++ww) s += dbs[(z * kNW + ww) * dmax_pad + c];
-      }
-      sb[c] = acc_mode ? sb[c] + s : s;
-    }
-    // dW_l = dZ^T . H
-    {
-      float* sw = slab + net.param_off + net.w_off[l];
-      const int mt = pad16(dout) / 16, ntl = pad16(din) / 16;
-      for (int t = w; t < mt * ntl; t += kNW) {
-        const int tm = t / ntl, tn = t - tm * ntl;
-        f32x4 accv = mma_16x16(dZT[z] + tm * 16 * ld_ht, ld_ht, HT + tn * 16 * ld_ht, ld_ht, kRows, zero4());
-        const int in = tn * 16 + acc_col();
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int o = tm * 16 + acc_row(i);
-          if (o < dout && in < din) {
-            float* p = sw + o * din + in;
-            *p = acc_mode ? *p + accv[i] : accv[i];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (l == 0) break;
-    // dZ_{l-1} = (dZ_l . W_l) * act'(H_l)
-    {
-      const int K = pad32(dout), ldw = ld_for_k(dout);
-      const bf16* A = dZ[z] + w * 16 * ld;
-      const bf16* Wimg = Wt[l];
-      const int ntiles = pad32(din) / 16;
-      for (int nt = 0; nt < ntiles; ++nt) {
-        f32x4 accv = mma_16x16(A, ld, Wimg + nt * 16 * ldw, ldw, K, zero4());
-        const int col = nt * 16 + acc_col();
-        float colsum = 0.f;
-        float dzv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = w * 16 + acc_row(i);
-          const float h = from_bf16(Hs[l][r * ld + col]);
-          const float dzval = col < din ? accv[i] * act_grad_from_out(net.hidden_act, h) : 0.f;
-          dzv[i] = dzval;
-          colsum += dzval;
-          dZ[z ^ 1][r * ld + col] = to_bf16(dzval);
-        }
-        const int r0 = w * 16 + acc_row(0);
-        bf16x4 v4 = {to_bf16(dzv[0]), to_bf16(dzv[1]), to_bf16(dzv[2]), to_bf16(dzv[3])};
-        *reinterpret_cast<bf16x4*>(&dZT[z ^ 1][col * ld_ht + r0]) = v4;
-        colsum = wave_colsum(colsum);
-        if (lane < 16) dbs[((z ^ 1) * kNW + w) * dmax_pad + col] = colsum;
-      }
-    }
-    z ^= 1;
-    head = false;
-  }
-  __syncthreads();
 }
 
 __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, AirlPlan p, int k) {

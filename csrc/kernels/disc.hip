@@ -199,7 +199,7 @@ __global__ __launch_bounds__(64 * kAdamPhases) void disc_adam_kernel(DiscAdamArg
   if (do_stats && threadIdx.x < kDiscStats) {
     float t = 0.f;
     for (int q = 0; q < kAdamPhases; ++q) t += sred[q][threadIdx.x];
-    a.stats_out[threadIdx.x] = t;
+    a.stats_out[threadIdx.x] = (a.stats_scale != 0.f ? a.stats_scale : 1.f) * t;
   }
   if (ph == 0 && e < a.n_params) {
     float acc = 0.f;
@@ -218,7 +218,16 @@ __global__ __launch_bounds__(64 * kAdamPhases) void disc_adam_kernel(DiscAdamArg
     g = a.grads[e];
   }
   float p = a.params[e];
-  if (a.weight_decay != 0.f) g += a.weight_decay * p;
+  float step_size = a.step_size, bc2_sqrt = a.bc2_sqrt;
+  if (a.step) {  // bias corrections from the device step counter (torch: lr / bc1, sqrt(bc2))
+    const float t = *a.step;
+    step_size = a.lr / (1.f - powf(a.beta1, t));
+    bc2_sqrt = sqrtf(1.f - powf(a.beta2, t));
+  }
+  if (a.weight_decay != 0.f) {
+    if (a.decoupled) p *= 1.f - a.lr * a.weight_decay;  // AdamW
+    else g += a.weight_decay * p;
+  }
   // torch.optim.Adam (_single_tensor/_multi_tensor, non-capturable): lerp, addcmul,
   // denom = sqrt(v) / sqrt(bc2) + eps, p -= lr / bc1 * m / denom
   float m = a.exp_avg[e];
@@ -226,8 +235,8 @@ __global__ __launch_bounds__(64 * kAdamPhases) void disc_adam_kernel(DiscAdamArg
   float v = a.exp_avg_sq[e] * a.beta2 + (1.f - a.beta2) * g * g;
   a.exp_avg[e] = m;
   a.exp_avg_sq[e] = v;
-  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
-  a.params[e] = p - a.step_size * (m / denom);
+  const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+  a.params[e] = p - step_size * (m / denom);
 }
 
 }  // namespace

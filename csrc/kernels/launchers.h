@@ -67,6 +67,12 @@ struct DiscAdamArgs {
   float* grads;
   float *params, *exp_avg, *exp_avg_sq;
   float beta1, beta2, eps, weight_decay, step_size, bc2_sqrt;
+  // device step counter (already incremented for this step) or null: with it the bias
+  // corrections come from the device (graph-capturable) with learning rate lr
+  const float* step;
+  float lr;
+  int decoupled;      // AdamW: p *= 1 - lr * weight_decay (else L2: g += weight_decay * p)
+  float stats_scale;  // stats_out = scale * sums (0: 1)
 };
 int disc_gather_blocks(int mb);
 hipError_t disc_gather(const DiscGatherArgs& a, hipStream_t s);
@@ -136,6 +142,44 @@ bool airl_plan(const AirlDiscArgs& a, AirlPlan& p);
 hipError_t airl_gather(const AirlDiscArgs& a, int k, hipStream_t s);
 hipError_t airl_norm(const AirlDiscArgs& a, int mode, int n_total, hipStream_t s);
 hipError_t airl_fwd_bwd(const AirlDiscArgs& a, const AirlPlan& p, int k, hipStream_t s);
+
+// ---- pref_rm.hip: fused preference reward-model minibatch (gather, fwd, bwd; Adam = disc_adam)
+struct PrefRmArgs {
+  int n, L, din;          // pairs in the minibatch, fragment length, reward-net input width
+  int ds, da, dns;        // state / action / next-state column widths of the input (0: unused)
+  const float *s_all, *a_all, *ns_all, *d_all;  // dataset rows [pair * 2L + t][*] (fragment 1, then 2)
+  const int64_t* idx;     // [n] pair ids of this minibatch
+  const float* prefs_all;  // [P]
+  const float* gt_all;     // [P][2][L] ground-truth rewards or null
+  AirlNet net;             // reward MLP, scalar identity head; offsets into the flat parameters
+  float *rmean, *rvar;     // input RunningNorm (null: none)
+  int* rcount;
+  float eps;
+  int merge;               // train mode: merge the minibatch moments
+  float* X;                // [2nL][din]
+  float* partials;         // [blocks][2 * din] shifted column sums
+  double* sums;            // [2 * din] (data parallel: all-reduced sums)
+  float* old_mv;           // [256] running mean / var before this minibatch
+  int* old_cnt;            // [1]
+  float* nrm;              // [256] mean / rstd the forward normalised with
+  float* r;                // [2nL] rewards
+  float* slab;             // [blocks][n_params]
+  float* pstats;           // [n][8] per pair: loss, correct, ground-truth loss
+  float discount, threshold, noise, gscale;  // gscale: the trainer's loss factor 1 / batch_size
+  float* step;             // Adam step counter (device), bumped by the gather
+  int n_params;
+};
+struct PrefPlan {
+  int ldr, ld_ht, dmax_pad, rimg_bytes, ht_bytes;
+  int wf_off[kAirlMaxLayers], wt_off[kAirlMaxLayers];
+  int rimg_off, scratch_off, lds_bytes;
+};
+int pref_rm_blocks(int n_pairs, int L);
+bool pref_rm_plan(const PrefRmArgs& a, PrefPlan& p);
+hipError_t pref_rm_gather(const PrefRmArgs& a, hipStream_t s);
+hipError_t pref_rm_sums(const PrefRmArgs& a, hipStream_t s);
+hipError_t pref_rm_fwd(const PrefRmArgs& a, const PrefPlan& p, int mode, int n_total, hipStream_t s);
+hipError_t pref_rm_bwd(const PrefRmArgs& a, const PrefPlan& p, hipStream_t s);
 
 // ---- wlin.hip: wide MLP layers (129..1024) on MFMA, bias / activation fused
 struct WideLinArgs {

@@ -715,8 +715,11 @@ class BasicRewardTrainer(RewardTrainer):
         world, rank = pdist.world_size(), pdist.rank()
         G = B * world
         graph = None
+        from imitation_amd.engine import reward_model
+
         if (dev.type == "cuda" and self.minibatch_size == self.batch_size and self.regularizer is None
-                and (world == 1 or self._dp_graph_ok()) and os.environ.get("IMITATION_AMD_PREF_GRAPH", "1") != "0"):
+                and (world == 1 or self._dp_graph_ok() or reward_model.fused_check(self)[0])
+                and os.environ.get("IMITATION_AMD_PREF_GRAPH", "1") != "0"):
             graph = self._minibatch_graph(s_all, a_all, ns_all, d_all, prefs_all, gt, P, L, B)
         epoch_num = 0
         with self.logger.accumulate_means("reward"):
@@ -892,6 +895,12 @@ class _MinibatchGraph:
         self.gt = th.zeros(capacity, 2, L, device=dev) if has_gt else None
         self.span = th.arange(2 * L, device=dev)
         self.graphs: Dict[int, Tuple[th.Tensor, Any, Any]] = {}  # n -> (idx buffer, graph, metrics out)
+        # the fused four-launch minibatch (engine/reward_model.py) when the reward net and
+        # optimizer qualify; it reads these buffers (dones as float32)
+        from imitation_amd.engine import reward_model
+
+        self.d_f = self.d.float() if self.d.dtype != th.float32 else self.d
+        self.fused = reward_model.maybe_fused(trainer, self, L, B)
 
     def load(self, s_all, a_all, ns_all, d_all, prefs_all, gt, P: int) -> None:
         n = s_all.shape[0]
@@ -899,11 +908,15 @@ class _MinibatchGraph:
         self.a[:n].copy_(a_all)
         self.ns[:n].copy_(ns_all)
         self.d[:n].copy_(d_all)
+        if self.d_f is not self.d:
+            self.d_f[:n].copy_(d_all)
         self.prefs[:P].copy_(prefs_all)
         if gt is not None:
             self.gt[:P].copy_(gt)
 
     def _step(self, idx: th.Tensor) -> th.Tensor:
+        if self.fused is not None:
+            return self.fused.step(idx)
         tr = self.trainer
         pm = tr._preference_model
         n, L = idx.shape[0], self.L
@@ -928,6 +941,8 @@ class _MinibatchGraph:
         """One minibatch step; returns its metrics (a fresh device tensor)."""
         n = int(idx.shape[0])
         opt = self.trainer.optim
+        if self.fused is not None and not self.fused.capturable:  # DP fused step: collectives, eager
+            return self.fused.step(idx).clone()
         if n in self.graphs:
             buf, graph, out = self.graphs[n]
             buf.copy_(idx)
@@ -943,7 +958,7 @@ class _MinibatchGraph:
         side.wait_stream(th.cuda.current_stream())
         with th.cuda.stream(side):  # warm-up == this minibatch's real step
             opt.zero_grad(set_to_none=True)
-            rec = self._step(buf)
+            rec = self._step(buf).clone()  # (the fused step returns a view of its metrics buffer)
         th.cuda.current_stream().wait_stream(side)
         opt.zero_grad(set_to_none=True)
         graph = th.cuda.CUDAGraph()

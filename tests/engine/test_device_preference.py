@@ -134,6 +134,7 @@ def test_reward_training_graph_replay_matches_eager(monkeypatch):
     frags = pc.RandomFragmenter(rng=frag_rng, warning_threshold=0)(trajs, 50, 96)
     prefs = pc.SyntheticGatherer(rng=np.random.default_rng(6))(frags)
     out = []
+    monkeypatch.setenv("IMITATION_AMD_PREF_FUSED", "0")  # the autograd minibatch, graphed vs eager
     for mode in ("0", "1"):
         monkeypatch.setenv("IMITATION_AMD_PREF_GRAPH", mode)
         th.manual_seed(11)
@@ -159,6 +160,124 @@ def test_reward_training_graph_replay_matches_eager(monkeypatch):
     assert set(l0) == set(l1)
     for k in l0:
         assert l1[k] == pytest.approx(l0[k], rel=1e-4, abs=1e-5), k
+
+
+def _pref_data(n_pairs=96, L=50):
+    from imitation_amd.algorithms import preference_comparisons as pc
+
+    tr0, venv, agent, _ = _agent(n_envs=4, n_steps=64)
+    trajs = tr0.sample(4000)
+    frags = pc.RandomFragmenter(rng=np.random.default_rng(5), warning_threshold=0)(trajs, L, n_pairs)
+    prefs = pc.SyntheticGatherer(rng=np.random.default_rng(6))(frags)
+    return venv, frags, prefs
+
+
+def _pref_trainer(venv, batch_size=16, epochs=1, seed=11):
+    from imitation_amd.algorithms import preference_comparisons as pc
+    from imitation_amd.rewards.reward_nets import BasicRewardNet
+    from imitation_amd.util import logger as imit_logger
+    from imitation_amd.util.networks import RunningNorm
+
+    th.manual_seed(seed)
+    rn = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm).to("cuda")
+    log = imit_logger.configure(format_strs=[])
+    trainer = pc.BasicRewardTrainer(pc.PreferenceModel(rn), pc.CrossEntropyRewardLoss(), rng=np.random.default_rng(3),
+                                    batch_size=batch_size, epochs=epochs, custom_logger=log)
+    return trainer, rn, log
+
+
+@gpu
+def test_fused_reward_minibatch_matches_autograd(monkeypatch):
+    """pref_rm.hip (engine/reward_model.py): one minibatch's reduced gradient, RunningNorm merge
+    and loss / accuracy / ground-truth loss equal the fp32 autograd minibatch on the same pairs
+    (bf16 operand tolerance); the data-parallel pieces (sums -> forward from the all-reduced
+    sums -> reduce-only backward) are the path exercised."""
+    from imitation_amd.algorithms import preference_comparisons as pc
+    from imitation_amd.engine.gail import _mlp_layers
+    from imitation_amd.ops import preference as pref_ops
+
+    venv, frags, prefs = _pref_data()
+    trainer, rn, _ = _pref_trainer(venv)
+    ds = pc.PreferenceDataset()
+    ds.push(frags, prefs)
+    trainer.train(ds)
+    store = trainer._mb_graph
+    assert store is not None and store.fused is not None, "fused reward minibatch not selected"
+    plan = store.fused.plan
+    norm, lins, _, _ = _mlp_layers(rn.mlp)
+    snap = [t.detach().clone() for t in (norm.running_mean, norm.running_var, norm.count)]
+    L, n, B = store.L, 8, trainer.batch_size
+    idx = th.arange(3, 3 + 2 * n, 2, device="cuda")
+    plan.gather(idx, True, True)
+    plan.forward(idx, True, n * 2 * L)
+    plan.backward(idx, True)
+    g_fused = plan.grads.clone()
+    m_fused = plan.metrics[:3].clone()
+    after = [t.detach().clone() for t in (norm.running_mean, norm.running_var, norm.count)]
+    with th.no_grad():
+        for t, v in zip((norm.running_mean, norm.running_var, norm.count), snap):
+            t.copy_(v)
+    monkeypatch.setenv("IMITATION_AMD_FUSED", "0")  # plain fp32 torch reference
+    rows = (idx[:, None] * (2 * L) + th.arange(2 * L, device="cuda")).reshape(-1)
+    for p in rn.parameters():
+        p.grad = None
+    rews = rn(store.s[rows], store.a[rows], store.ns[rows], store.d[rows]).view(n, 2, L)
+    pm = trainer._preference_model
+    pr = store.prefs[idx]
+    loss, probs = pref_ops.bradley_terry_reference(rews[:, 0], rews[:, 1], pr, pm.discount_factor, pm.threshold,
+                                                   pm.noise_prob)
+    (loss * (n / B)).backward()
+    for a, b in zip(after, (norm.running_mean, norm.running_var, norm.count)):
+        assert th.allclose(a.float(), b.float(), rtol=1e-5, atol=1e-6)
+    off = 0
+    for lin in lins:
+        # per layer against its largest gradient entry (a bias gradient sums ~800 rows of
+        # mixed sign and may cancel far below its terms; test_kernels.py does the same)
+        scale = max(float(lin.weight.grad.abs().max()), float(lin.bias.grad.abs().max())) + 1e-6
+        for p in (lin.weight, lin.bias):
+            k = p.numel()
+            ref = p.grad.reshape(-1)
+            got = g_fused[off : off + k]
+            off += k
+            # vs plain fp32: bf16 operands in three layers, and every pair's coefficient
+            # y - sigmoid(-diff) inherits the error of diff, a sum of 100 bf16-forward rewards
+            assert float((got - ref).abs().max()) <= 1e-1 * scale, (tuple(p.shape), float((got - ref).abs().max()), scale)
+            assert float((got - ref).norm()) <= 1e-1 * float(ref.norm()) + 1e-3 * scale, tuple(p.shape)
+            if float(ref.norm()) > 1e-2 * scale:  # (the head bias cancels between the fragments: ~0)
+                cos = float(th.dot(got, ref) / (got.norm() * ref.norm() + 1e-12))
+                assert cos >= 0.995, (tuple(p.shape), cos)  # an indexing / sign error is far below this
+    acc = ((probs > 0.5) == (pr > 0.5)).float().mean()
+    assert float(m_fused[0]) == pytest.approx(float(loss), rel=2e-2, abs=1e-4)
+    assert float(m_fused[1]) == pytest.approx(float(acc), abs=1.5 / n)
+
+
+@gpu
+def test_fused_reward_training_tracks_autograd_training(monkeypatch):
+    """A fused-minibatch training run (graphed) and the autograd one from the same init:
+    identical RunningNorm statistics, parameters within the bf16-operand drift of a few
+    AdamW steps, and the logged loss means close."""
+    from imitation_amd.algorithms import preference_comparisons as pc
+
+    venv, frags, prefs = _pref_data()
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("IMITATION_AMD_PREF_FUSED", fused)
+        trainer, rn, log = _pref_trainer(venv, epochs=2)
+        ds = pc.PreferenceDataset()
+        ds.push(frags, prefs)
+        trainer.train(ds)
+        assert (trainer._mb_graph.fused is not None) == (fused == "1")
+        out.append(({k: v.detach().clone() for k, v in rn.state_dict().items()}, dict(log.name_to_value)))
+    (p0, l0), (p1, l1) = out
+    for k in p0:
+        if "running" in k or k.endswith("count"):
+            assert th.allclose(p0[k].float(), p1[k].float(), rtol=1e-5, atol=1e-6), k
+        elif not k.endswith("dense_final.bias"):
+            assert float((p0[k] - p1[k]).abs().max()) < 5e-3, k
+    assert set(l0) == set(l1)
+    for k in l0:
+        if "loss" in k:
+            assert l1[k] == pytest.approx(l0[k], rel=2e-2, abs=1e-3), k
 
 
 @gpu
