@@ -218,7 +218,7 @@ def test_save_trajectories(trajectory, trajectory_rew, use_chdir, tmpdir, use_pi
             if use_rewards:
                 with pytest.raises(ValueError):
                     serialize.save(save_path, [trajectory, trajectory_rew])
-        kw = dict(allow_pickle=True) if use_pickle else {}
+        kw = dict(allow_pickle=True) if use_pickle else {}  # noqa: pickle -- the list this test pickled itself
         if type_safe:
             if use_rewards:
                 loaded = serialize.load_with_rewards(save_path, **kw)
