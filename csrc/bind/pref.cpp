@@ -6,6 +6,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <algorithm>
+
 namespace {
 
 #define IA_HIP_CHECK_P(expr)                                                          \
@@ -171,6 +173,34 @@ class PrefRmPlan {
     ia::PrefRmArgs a = args(idx, false);
     adam_launch(a, 0, 1);
   }
+  // One epoch (single rank) in one call -- capturable as ONE graph that is replayed per
+  // epoch: minibatch mb takes pairs order[*cursor * P + mb * B, ...) (P pairs, batch B; the
+  // last minibatch may be partial), its metrics go to ep[mb * 8 ...]; the epoch end copies
+  // ep to all[*cursor] and advances the device cursor.
+  void epoch(torch::Tensor order, int P, torch::Tensor cursor, torch::Tensor ep, torch::Tensor all, bool merge) {
+    TORCH_CHECK(order.is_cuda() && order.is_contiguous() && order.scalar_type() == torch::kInt64, "order: int64 GPU");
+    TORCH_CHECK(cursor.is_cuda() && cursor.scalar_type() == torch::kInt32 && cursor.numel() == 1, "cursor: int32 GPU [1]");
+    const int n_mb = (P + B_ - 1) / B_;
+    TORCH_CHECK(P > 0 && order.numel() >= P, "order holds fewer than P pairs");
+    TORCH_CHECK(ep.is_cuda() && ep.scalar_type() == torch::kFloat32 && ep.numel() >= (int64_t)n_mb * 8, "ep: float32 [n_mb * 8]");
+    TORCH_CHECK(all.is_cuda() && all.scalar_type() == torch::kFloat32 && all.numel() % ((int64_t)n_mb * 8) == 0,
+                "all: float32 [epochs * n_mb * 8]");
+    for (int mb = 0; mb < n_mb; ++mb) {
+      ia::PrefRmArgs a = a_;
+      a.n = std::min(B_, P - mb * B_);
+      TORCH_CHECK(a.n <= cap_, "minibatch above capacity");
+      a.idx = order.data_ptr<int64_t>() + (int64_t)mb * B_;
+      a.cursor = cursor.data_ptr<int>();
+      a.idx_stride = P;
+      a.merge = merge ? 1 : 0;
+      IA_HIP_CHECK_P(ia::pref_rm_gather(a, ia_stream()));
+      IA_HIP_CHECK_P(ia::pref_rm_fwd(a, plan_, 0, 0, ia_stream()));
+      IA_HIP_CHECK_P(ia::pref_rm_bwd(a, plan_, ia_stream()));
+      adam_launch(a, 1, 1, ep.data_ptr<float>() + (int64_t)mb * 8);
+    }
+    IA_HIP_CHECK_P(ia::pref_rm_epoch_end(ep.data_ptr<float>(), all.data_ptr<float>(), n_mb * 8, cursor.data_ptr<int>(),
+                                         ia_stream()));
+  }
 
  private:
   ia::PrefRmArgs args(const torch::Tensor& idx, bool merge) {
@@ -183,14 +213,14 @@ class PrefRmPlan {
     a.merge = merge ? 1 : 0;
     return a;
   }
-  void adam_launch(const ia::PrefRmArgs& a, int reduce, int do_adam) {
+  void adam_launch(const ia::PrefRmArgs& a, int reduce, int do_adam, float* stats_out = nullptr) {
     ia::DiscAdamArgs d = ad_;
     d.reduce = reduce;
     d.adam = do_adam;
     d.nblk = ia::pref_rm_blocks(a.n, a.L);
     d.stats_nblk = a.n;
     d.stats_scale = 1.f / (float)a.n;
-    d.stats_out = reduce ? metrics_.data_ptr<float>() : nullptr;
+    d.stats_out = reduce ? (stats_out ? stats_out : metrics_.data_ptr<float>()) : nullptr;
     IA_HIP_CHECK_P(ia::disc_adam(d, ia_stream()));
   }
   std::vector<torch::Tensor> held_, ws_;
@@ -215,5 +245,7 @@ void register_pref(py::module& m) {
       .def("gather", &PrefRmPlan::gather, py::arg("idx"), py::arg("merge"), py::arg("sums"))
       .def("forward", &PrefRmPlan::forward, py::arg("idx"), py::arg("merge"), py::arg("n_total"))
       .def("backward", &PrefRmPlan::backward, py::arg("idx"), py::arg("merge"))
-      .def("apply", &PrefRmPlan::apply, py::arg("idx"));
+      .def("apply", &PrefRmPlan::apply, py::arg("idx"))
+      .def("epoch", &PrefRmPlan::epoch, py::arg("order"), py::arg("P"), py::arg("cursor"), py::arg("ep"), py::arg("all"),
+           py::arg("merge"));
 }

@@ -168,6 +168,8 @@ struct PrefRmArgs {
   float discount, threshold, noise, gscale;  // gscale: the trainer's loss factor 1 / batch_size
   float* step;             // Adam step counter (device), bumped by the gather
   int n_params;
+  const int* cursor;       // device epoch cursor or null: pair ids at idx + *cursor * idx_stride
+  int idx_stride;
 };
 struct PrefPlan {
   int ldr, ld_ht, dmax_pad, rimg_bytes, ht_bytes;
@@ -180,6 +182,8 @@ hipError_t pref_rm_gather(const PrefRmArgs& a, hipStream_t s);
 hipError_t pref_rm_sums(const PrefRmArgs& a, hipStream_t s);
 hipError_t pref_rm_fwd(const PrefRmArgs& a, const PrefPlan& p, int mode, int n_total, hipStream_t s);
 hipError_t pref_rm_bwd(const PrefRmArgs& a, const PrefPlan& p, hipStream_t s);
+// epoch end: metrics of the epoch's minibatches [n * 8] -> all[*cursor * n * 8 ...], ++*cursor
+hipError_t pref_rm_epoch_end(const float* metrics, float* all, int n, int* cursor, hipStream_t s);
 
 // ---- wlin.hip: wide MLP layers (129..1024) on MFMA, bias / activation fused
 struct WideLinArgs {

@@ -53,38 +53,59 @@ __device__ __forceinline__ float pref_col(const PrefRmArgs& a, int64_t src, int 
   return a.d_all[src];
 }
 
-// 256 threads = 2 phases x 128 columns; block b covers rows [64 b, 64 b + 64)
+// pair ids of this minibatch (epoch graphs: offset by the device epoch cursor)
+__device__ __forceinline__ const int64_t* pair_ids(const PrefRmArgs& a) {
+  return a.cursor ? a.idx + (int64_t)(*a.cursor) * a.idx_stride : a.idx;
+}
+
+// block b covers rows [64 b, 64 b + 64): the 64 x din tile element-parallel (consecutive
+// threads read consecutive columns of a row, all loads independent), staged in LDS for the
+// shifted column sums (4 row phases x 64 columns, fixed order)
 __global__ __launch_bounds__(256) void pref_gather_kernel(PrefRmArgs a) {
-  __shared__ float red[2][2][128];
-  const int c = threadIdx.x & 127, ph = threadIdx.x >> 7;
-  const int rows = 2 * a.n * a.L, twoL = 2 * a.L;
+  __shared__ float tile[kRows][129];
+  __shared__ float red[4][2][64];
+  const int rows = 2 * a.n * a.L, twoL = 2 * a.L, din = a.din;
   const int r0 = blockIdx.x * kRows;
-  const bool col_ok = c < a.din;
-  const float shift = (col_ok && a.rmean) ? a.rmean[c] : 0.f;
-  float s1 = 0.f, s2 = 0.f;
-  for (int rr = ph; rr < kRows; rr += 2) {
+  const int64_t* idx = pair_ids(a);
+  for (int e = threadIdx.x; e < kRows * din; e += 256) {
+    const int rr = e / din, c = e - rr * din;
     const int r = r0 + rr;
-    if (r >= rows) break;
-    const int i = r / twoL, t = r - i * twoL;
-    const int64_t src = a.idx[i] * (int64_t)twoL + t;
-    if (col_ok) {
-      const float v = pref_col(a, src, c);
-      a.X[(size_t)r * a.din + c] = v;
-      const float dv = v - shift;
-      s1 += dv;
-      s2 += dv * dv;
+    float v = 0.f;
+    if (r < rows) {
+      const int i = r / twoL, t = r - i * twoL;
+      v = pref_col(a, idx[i] * (int64_t)twoL + t, c);
+      a.X[(size_t)r * din + c] = v;
     }
+    tile[rr][c] = v;
   }
   if (a.rmean) {
-    red[ph][0][c] = s1;
-    red[ph][1][c] = s2;
     __syncthreads();
-    if (ph == 0 && col_ok) {
-      float* out = a.partials + (size_t)blockIdx.x * 2 * a.din;
-      out[c] = red[0][0][c] + red[1][0][c];
-      out[a.din + c] = red[0][1][c] + red[1][1][c];
+    const int nv = min(kRows, rows - r0);
+    for (int c0 = 0; c0 < din; c0 += 64) {
+      const int c = c0 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+      float s1 = 0.f, s2 = 0.f;
+      if (c < din) {
+        const float shift = a.rmean[c];
+        for (int rr = ph; rr < nv; rr += 4) {
+          const float dv = tile[rr][c] - shift;
+          s1 += dv;
+          s2 += dv * dv;
+        }
+      }
+      red[ph][0][threadIdx.x & 63] = s1;
+      red[ph][1][threadIdx.x & 63] = s2;
+      __syncthreads();
+      if (ph == 0 && c < din) {
+        float* out = a.partials + (size_t)blockIdx.x * 2 * din;
+        const int j = threadIdx.x & 63;
+        out[c] = (red[0][0][j] + red[1][0][j]) + (red[2][0][j] + red[3][0][j]);
+        out[din + c] = (red[0][1][j] + red[1][1][j]) + (red[2][1][j] + red[3][1][j]);
+      }
+      __syncthreads();
     }
   }
+  const int c = threadIdx.x & 127;
+  const bool col_ok = c < din;
   if (blockIdx.x == 0) {
     if (a.rmean && threadIdx.x < 128 && col_ok) {  // running statistics before this minibatch
       a.old_mv[c] = a.rmean[c];
@@ -148,10 +169,11 @@ __device__ __forceinline__ Imgs carve(char* smem, const PrefPlan& p, int n_layer
 // mode 0: moments from the gather's block sums; 1: from the (all-reduced) sums, n_total rows
 __global__ __launch_bounds__(64 * kNW) void pref_fwd_kernel(PrefRmArgs a, PrefPlan p, int mode, int n_total) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ double dred[2][2][128];
+  __shared__ double dsum[4][128];
+  __shared__ double dtot[256];
   __shared__ float nrm[256];
   __shared__ float out[kRows];
-  const int c = threadIdx.x & 127, ph = threadIdx.x >> 7;
+  const int c = threadIdx.x & 127;
   const int rows = 2 * a.n * a.L;
   const int row0 = blockIdx.x * kRows;
   Imgs m = carve(smem, p, a.net.n_layers);
@@ -159,22 +181,28 @@ __global__ __launch_bounds__(64 * kNW) void pref_fwd_kernel(PrefRmArgs a, PrefPl
   // ---- RunningNorm: batch moments (fixed order), Chan merge into the pre-minibatch snapshot
   if (a.rmean) {
     if (mode == 0) {
-      const int nb = (rows + kRows - 1) / kRows;
-      double s1 = 0.0, s2 = 0.0;
-      if (c < a.din)
-        for (int b = ph; b < nb; b += 2) {
-          s1 += (double)a.partials[(size_t)b * 2 * a.din + c];
-          s2 += (double)a.partials[(size_t)b * 2 * a.din + a.din + c];
-        }
-      dred[ph][0][c] = s1;
-      dred[ph][1][c] = s2;
+      // 2 din sums per gather block: thread (j, phase) with j < 64 a sum index (din <= 32
+      // here: 4 block phases; wider inputs: 2), phases combined in order below
+      const int nb = (rows + kRows - 1) / kRows, ns = 2 * a.din;
+      const int npj = ns <= 64 ? 64 : 128, nph = 256 / npj;
+      const int j = threadIdx.x % npj, q = threadIdx.x / npj;
+      double s = 0.0;
+      if (j < ns)
+        for (int b = q; b < nb; b += nph) s += (double)a.partials[(size_t)b * ns + j];
+      dsum[q][j] = s;
+      __syncthreads();
+      if (threadIdx.x < ns) {
+        double t = 0.0;
+        for (int qq = 0; qq < nph; ++qq) t += dsum[qq][threadIdx.x];
+        dtot[threadIdx.x] = t;
+      }
     }
     __syncthreads();
     if (threadIdx.x < 128) {
       float mean = 0.f, rstd = 1.f;
       if (c < a.din) {
-        const double S1 = mode == 0 ? dred[0][0][c] + dred[1][0][c] : a.sums[c];
-        const double S2 = mode == 0 ? dred[0][1][c] + dred[1][1][c] : a.sums[a.din + c];
+        const double S1 = mode == 0 ? dtot[c] : a.sums[c];
+        const double S2 = mode == 0 ? dtot[a.din + c] : a.sums[a.din + c];
         const int n = mode == 0 ? rows : n_total;
         float rm = a.old_mv[c], rv = a.old_mv[128 + c];
         if (a.merge) {
@@ -245,7 +273,7 @@ __global__ __launch_bounds__(64 * kNW) void pref_bwd_kernel(PrefRmArgs a, PrefPl
     const float* r1 = a.r + (size_t)pi * twoL;
     const float* r2 = r1 + a.L;
     float s = 0.f, sg = 0.f;
-    const int64_t gi = a.idx[pi];
+    const int64_t gi = pair_ids(a)[pi];
     for (int t = lane; t < a.L; t += 64) {
       const float wt = a.discount == 1.f ? 1.f : exp2f(lg * (float)t);
       s += wt * (r2[t] - r1[t]);
@@ -300,7 +328,19 @@ __global__ __launch_bounds__(64 * kNW) void pref_bwd_kernel(PrefRmArgs a, PrefPl
   mlp_backward(net, m.H, p.ldr, m.Wt, dy, m.HT, p.ld_ht, m.dZ, m.dZT, m.dbs, p.dmax_pad, slab_row, false);
 }
 
+__global__ void pref_epoch_end_kernel(const float* __restrict__ metrics, float* __restrict__ all, int n, int* cursor) {
+  const int cur = *cursor;
+  __syncthreads();  // every thread has read the cursor before thread 0 moves it
+  for (int i = threadIdx.x; i < n; i += blockDim.x) all[(size_t)cur * n + i] = metrics[i];
+  if (threadIdx.x == 0) *cursor = cur + 1;
+}
+
 }  // namespace
+
+hipError_t pref_rm_epoch_end(const float* metrics, float* all, int n, int* cursor, hipStream_t s) {
+  hipLaunchKernelGGL(pref_epoch_end_kernel, dim3(1), dim3(256), 0, s, metrics, all, n, cursor);
+  return hipGetLastError();
+}
 
 int pref_rm_blocks(int n_pairs, int L) { return (2 * n_pairs * L + kRows - 1) / kRows; }
 

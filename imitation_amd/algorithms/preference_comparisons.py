@@ -721,6 +721,10 @@ class BasicRewardTrainer(RewardTrainer):
                 and (world == 1 or self._dp_graph_ok() or reward_model.fused_check(self)[0])
                 and os.environ.get("IMITATION_AMD_PREF_GRAPH", "1") != "0"):
             graph = self._minibatch_graph(s_all, a_all, ns_all, d_all, prefs_all, gt, P, L, B)
+        if (graph is not None and graph.fused is not None and graph.fused.capturable
+                and os.environ.get("IMITATION_AMD_PREF_EPOCH_GRAPH", "1") != "0"):
+            with self.logger.accumulate_means("reward"):
+                return self._train_fused_epochs(graph, index_loader, epochs, P, dev)
         epoch_num = 0
         with self.logger.accumulate_means("reward"):
             for epoch_num in range(epochs):
@@ -768,6 +772,41 @@ class BasicRewardTrainer(RewardTrainer):
                         for k, v in zip(names, vals):
                             self.logger.record(k, v)
         return epoch_num
+
+    def _train_fused_epochs(self, store: "_MinibatchGraph", index_loader, epochs: int, P: int, dev) -> int:
+        """All epochs on the fused minibatch kernels with ONE host sync: the epoch orders (the
+        same DataLoader permutations as the minibatch loop) go to the device up front, one
+        epoch -- every minibatch plus the metrics copy -- is captured as a HIP graph reading
+        its pair ids at a device epoch cursor, epoch 0 runs eagerly as the capture's warm-up
+        and the graph is replayed for the others; the logged per-minibatch metrics are read
+        back once at the end."""
+        fm = store.fused
+        B = self.minibatch_size
+        n_mb = -(-P // B)
+        orders = th.stack([th.cat(list(index_loader)) for _ in range(epochs)]).to(dev, non_blocking=True)
+        cursor = th.zeros(1, dtype=th.int32, device=dev)
+        ep = th.zeros(n_mb * 8, device=dev)
+        allm = th.zeros(epochs, n_mb, 8, device=dev)
+        merge = fm.norm is not None and fm.norm.training
+        side = th.cuda.Stream()
+        side.wait_stream(th.cuda.current_stream())
+        with th.cuda.stream(side):  # warm-up == epoch 0
+            fm.plan.epoch(orders, P, cursor, ep, allm, merge)
+        th.cuda.current_stream().wait_stream(side)
+        if epochs > 1:
+            graph = th.cuda.CUDAGraph()
+            with th.cuda.graph(graph):
+                fm.plan.epoch(orders, P, cursor, ep, allm, merge)
+            for _ in range(epochs - 1):
+                graph.replay()
+        vals = allm[:, :, : fm.n_metrics].cpu().tolist()
+        names = ["loss", "accuracy", "gt_reward_loss"]
+        for epoch_num in range(epochs):
+            with self.logger.add_key_prefix(f"epoch-{epoch_num}"), self.logger.add_key_prefix("train"):
+                for rec in vals[epoch_num]:
+                    for k, v in zip(names, rec):
+                        self.logger.record(k, v)
+        return epochs - 1
 
     def _minibatch_graph(self, s_all, a_all, ns_all, d_all, prefs_all, gt, P: int, L: int, B: int) -> "_MinibatchGraph":
         """The persistent HIP-graph of one full minibatch step (re-captured only when the
