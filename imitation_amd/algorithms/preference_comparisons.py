@@ -783,7 +783,7 @@ class BasicRewardTrainer(RewardTrainer):
         fm = store.fused
         B = self.minibatch_size
         n_mb = -(-P // B)
-        orders = th.stack([th.cat(list(index_loader)) for _ in range(epochs)]).to(dev, non_blocking=True)
+        orders = th.stack(_epoch_orders(index_loader, P, epochs)).to(dev, non_blocking=True)
         cursor = th.zeros(1, dtype=th.int32, device=dev)
         ep = th.zeros(n_mb * 8, device=dev)
         allm = th.zeros(epochs, n_mb, 8, device=dev)
@@ -908,6 +908,33 @@ class BasicRewardTrainer(RewardTrainer):
         for name, value in output.metrics.items():
             self.logger.record(name, value.item())
         return output.loss
+
+
+def _epoch_orders(index_loader: data_th.DataLoader, P: int, epochs: int) -> List[th.Tensor]:
+    """The pair order of each of ``epochs`` passes of a shuffling DataLoader over range(P).
+
+    An epoch of that loader draws one int64 from its generator (the iterator's base seed),
+    one ``randperm(P)`` (RandomSampler) and, when the sampler is drained, a second one for its
+    empty remainder; replaying exactly those draws costs ~20 us per epoch instead of ~0.5 ms
+    of DataLoader iteration. The first two epochs are checked against the loader itself (on
+    the restored generator state); any mismatch falls back to iterating it."""
+    g = index_loader.generator
+    def draw(gen: th.Generator) -> th.Tensor:
+        th.empty((), dtype=th.int64).random_(generator=gen)
+        perm = th.randperm(P, generator=gen)
+        th.randperm(P, generator=gen)
+        return perm
+
+    if g is not None and isinstance(index_loader.sampler, data_th.RandomSampler) and not index_loader.sampler.replacement:
+        state = g.get_state()
+        probe = th.Generator()
+        probe.set_state(state)
+        fast = [draw(probe) for _ in range(2)]
+        ref = [th.cat(list(index_loader)) for _ in range(2)]
+        g.set_state(state)
+        if all(th.equal(a, b) for a, b in zip(fast, ref)):
+            return [draw(g) for _ in range(epochs)]
+    return [th.cat(list(index_loader)) for _ in range(epochs)]
 
 
 class _MinibatchGraph:

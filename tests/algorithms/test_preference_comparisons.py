@@ -533,3 +533,20 @@ def test_ensemble_grouped_prediction_matches_members():
         y = st.forward(x, st.gather_params(), st.gather_norm())
         ref = th.stack([m(s, a, s, th.zeros(9)) for m in ens.members])
     th.testing.assert_close(y, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("P,B", [(500, 32), (7, 3), (64, 64), (1, 1)])
+def test_epoch_orders_replay_the_dataloader(P, B):
+    """_epoch_orders (the fused reward training's upfront epoch permutations) equals iterating
+    the shuffling DataLoader epoch by epoch, and leaves its generator in the same state."""
+    import torch as th
+    from torch.utils import data as data_th
+
+    from imitation_amd.algorithms.preference_comparisons import _epoch_orders
+
+    mk = lambda: data_th.DataLoader(range(P), batch_size=B, shuffle=True,  # noqa: E731
+                                    generator=th.Generator().manual_seed(123))
+    fast_loader, ref_loader = mk(), mk()
+    fast = _epoch_orders(fast_loader, P, 6) + [th.cat(list(fast_loader))]
+    ref = [th.cat(list(ref_loader)) for _ in range(7)]
+    assert all(th.equal(a, b) for a, b in zip(fast, ref))

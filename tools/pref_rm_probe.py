@@ -34,8 +34,20 @@ def main(n_pairs=500, L=100, epochs=200):
                                     batch_size=32, epochs=3, custom_logger=imit_logger.configure(format_strs=[]))
     ds = pc.PreferenceDataset()
     ds.push(pairs, prefs)
-    trainer.train(ds, epoch_multiplier=1.0)  # warm: captures, allocations
+    import cProfile
+    import pstats
+
+    prof = cProfile.Profile() if os.environ.get("PROBE_CPROFILE") else None
     th.cuda.synchronize()
+    t0 = time.perf_counter()
+    if prof:
+        prof.enable()
+    trainer.train(ds, epoch_multiplier=epochs / 3)  # cold: packing, store, plan, capture
+    th.cuda.synchronize()
+    if prof:
+        prof.disable()
+        pstats.Stats(prof).sort_stats("cumulative").print_stats(25)
+    print(f"cold call: {time.perf_counter() - t0:.3f} s", flush=True)
     t0 = time.perf_counter()
     trainer.train(ds, epoch_multiplier=epochs / 3)
     th.cuda.synchronize()
