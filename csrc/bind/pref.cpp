@@ -101,6 +101,8 @@ class PrefRmPlan {
     a_.partials = ws_.back().data_ptr<float>();
     sums_ = torch::zeros({2 * a_.din}, fo.dtype(torch::kFloat64));
     a_.sums = sums_.data_ptr<double>();
+    ws_.push_back(torch::zeros({1}, fo.dtype(torch::kInt32)));
+    a_.cnt = reinterpret_cast<unsigned*>(ws_.back().data_ptr<int>());
     ws_.push_back(torch::zeros({256}, fo));
     a_.old_mv = ws_.back().data_ptr<float>();
     ws_.push_back(torch::zeros({1}, fo.dtype(torch::kInt32)));
@@ -146,23 +148,22 @@ class PrefRmPlan {
   torch::Tensor step(torch::Tensor idx, bool merge) {
     ia::PrefRmArgs a = args(idx, merge);
     IA_HIP_CHECK_P(ia::pref_rm_gather(a, ia_stream()));
-    IA_HIP_CHECK_P(ia::pref_rm_fwd(a, plan_, 0, 0, ia_stream()));
+    IA_HIP_CHECK_P(ia::pref_rm_fwd(a, plan_, 0, ia_stream()));
     IA_HIP_CHECK_P(ia::pref_rm_bwd(a, plan_, ia_stream()));
     adam_launch(a, 1, 1);
     return metrics_;
   }
   // data-parallel pieces: gather (+ block sums -> sums()), forward from the all-reduced
   // sums of n_total rows, backward + slab reduction into grads() (all-reduce them), AdamW
-  // sums: also reduce the block sums into sums() (to all-reduce before forward(n_total > 0))
-  void gather(torch::Tensor idx, bool merge, bool sums) {
+  // gather (+ the column sums -> sums(): all-reduce them before forward(n_total > 0))
+  void gather(torch::Tensor idx, bool merge) {
     ia::PrefRmArgs a = args(idx, merge);
     IA_HIP_CHECK_P(ia::pref_rm_gather(a, ia_stream()));
-    if (sums && a.rmean) IA_HIP_CHECK_P(ia::pref_rm_sums(a, ia_stream()));
   }
-  // n_total > 0: moments from sums() over n_total rows; 0: from this rank's block sums
+  // moments from sums() over n_total rows (0: this rank's rows)
   void forward(torch::Tensor idx, bool merge, int n_total) {
     ia::PrefRmArgs a = args(idx, merge);
-    IA_HIP_CHECK_P(ia::pref_rm_fwd(a, plan_, (a.rmean && n_total > 0) ? 1 : 0, n_total, ia_stream()));
+    IA_HIP_CHECK_P(ia::pref_rm_fwd(a, plan_, n_total, ia_stream()));
   }
   void backward(torch::Tensor idx, bool merge) {
     ia::PrefRmArgs a = args(idx, merge);
@@ -194,7 +195,7 @@ class PrefRmPlan {
       a.idx_stride = P;
       a.merge = merge ? 1 : 0;
       IA_HIP_CHECK_P(ia::pref_rm_gather(a, ia_stream()));
-      IA_HIP_CHECK_P(ia::pref_rm_fwd(a, plan_, 0, 0, ia_stream()));
+      IA_HIP_CHECK_P(ia::pref_rm_fwd(a, plan_, 0, ia_stream()));
       IA_HIP_CHECK_P(ia::pref_rm_bwd(a, plan_, ia_stream()));
       adam_launch(a, 1, 1, ep.data_ptr<float>() + (int64_t)mb * 8);
     }
@@ -242,7 +243,7 @@ void register_pref(py::module& m) {
       .def_property_readonly("grads", &PrefRmPlan::grads)
       .def_property_readonly("metrics", &PrefRmPlan::metrics)
       .def("step", &PrefRmPlan::step, py::arg("idx"), py::arg("merge"))
-      .def("gather", &PrefRmPlan::gather, py::arg("idx"), py::arg("merge"), py::arg("sums"))
+      .def("gather", &PrefRmPlan::gather, py::arg("idx"), py::arg("merge"))
       .def("forward", &PrefRmPlan::forward, py::arg("idx"), py::arg("merge"), py::arg("n_total"))
       .def("backward", &PrefRmPlan::backward, py::arg("idx"), py::arg("merge"))
       .def("apply", &PrefRmPlan::apply, py::arg("idx"))

@@ -158,7 +158,8 @@ struct PrefRmArgs {
   int merge;               // train mode: merge the minibatch moments
   float* X;                // [2nL][din]
   float* partials;         // [blocks][2 * din] shifted column sums
-  double* sums;            // [2 * din] (data parallel: all-reduced sums)
+  double* sums;            // [2 * din] their block-order sum (data parallel: then all-reduced)
+  unsigned* cnt;           // [1] zero-initialised gather-block counter (self-resetting)
   float* old_mv;           // [256] running mean / var before this minibatch
   int* old_cnt;            // [1]
   float* nrm;              // [256] mean / rstd the forward normalised with
@@ -179,8 +180,7 @@ struct PrefPlan {
 int pref_rm_blocks(int n_pairs, int L);
 bool pref_rm_plan(const PrefRmArgs& a, PrefPlan& p);
 hipError_t pref_rm_gather(const PrefRmArgs& a, hipStream_t s);
-hipError_t pref_rm_sums(const PrefRmArgs& a, hipStream_t s);
-hipError_t pref_rm_fwd(const PrefRmArgs& a, const PrefPlan& p, int mode, int n_total, hipStream_t s);
+hipError_t pref_rm_fwd(const PrefRmArgs& a, const PrefPlan& p, int n_total, hipStream_t s);
 hipError_t pref_rm_bwd(const PrefRmArgs& a, const PrefPlan& p, hipStream_t s);
 // epoch end: metrics of the epoch's minibatches [n * 8] -> all[*cursor * n * 8 ...], ++*cursor
 hipError_t pref_rm_epoch_end(const float* metrics, float* all, int n, int* cursor, hipStream_t s);

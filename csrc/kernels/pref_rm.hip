@@ -10,11 +10,12 @@
 //
 //   pref_gather   rows of the minibatch's pairs (pair ids idx, 2L rows each: fragment 1 then
 //                 fragment 2) gathered into the reward-net input X; per-block shifted column
-//                 sums for the RunningNorm; block 0 bumps the device Adam step and snapshots
-//                 the running statistics
-//   pref_fwd      every block reduces the column sums (fixed order, fp64), Chan-merges them
-//                 into the snapshot and normalises its 64 rows (block 0 publishes the merged
-//                 statistics); reward-net forward -> r[row]
+//                 sums for the RunningNorm, reduced (fixed order, fp64) by the last block to
+//                 finish; block 0 bumps the device Adam step and snapshots the running
+//                 statistics
+//   pref_fwd      every block Chan-merges the batch moments into the snapshot and normalises
+//                 its 64 rows (block 0 publishes the merged statistics); reward-net forward ->
+//                 r[row]
 //   pref_bwd      per 64-row block: the Bradley-Terry terms of the pairs its rows belong to
 //                 (from r: fragment returns, probability, loss, dloss/ddiff), the per-row
 //                 reward gradient, the forward recomputed and the backward -> one slab row;
@@ -53,6 +54,17 @@ __device__ __forceinline__ float pref_col(const PrefRmArgs& a, int64_t src, int 
   return a.d_all[src];
 }
 
+// sc1 (L1-bypassing, agent-coherent) 4-B accesses for the last-block reduction of the
+// gather's column sums; inline asm so a lane keeps 8 loads in flight before ONE wait
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
 // pair ids of this minibatch (epoch graphs: offset by the device epoch cursor)
 __device__ __forceinline__ const int64_t* pair_ids(const PrefRmArgs& a) {
   return a.cursor ? a.idx + (int64_t)(*a.cursor) * a.idx_stride : a.idx;
@@ -60,10 +72,16 @@ __device__ __forceinline__ const int64_t* pair_ids(const PrefRmArgs& a) {
 
 // block b covers rows [64 b, 64 b + 64): the 64 x din tile element-parallel (consecutive
 // threads read consecutive columns of a row, all loads independent), staged in LDS for the
-// shifted column sums (4 row phases x 64 columns, fixed order)
+// shifted column sums (4 row phases x 64 columns, fixed order). The block sums are handed to
+// the LAST block to finish (MI355X_MICROARCH inter-workgroup visibility, row 1: sc1 stores,
+// every storing wave's vmcnt(0), a barrier, one agent-scope add per block; the block whose add
+// returns nblocks - 1 reads them with sc1 loads), which reduces them in block order (fp64) into
+// sums -- so the forward's blocks read 2 din values instead of re-reducing every block's.
 __global__ __launch_bounds__(256) void pref_gather_kernel(PrefRmArgs a) {
   __shared__ float tile[kRows][129];
   __shared__ float red[4][2][64];
+  __shared__ double dred[4][128];
+  __shared__ int is_last;
   const int rows = 2 * a.n * a.L, twoL = 2 * a.L, din = a.din;
   const int r0 = blockIdx.x * kRows;
   const int64_t* idx = pair_ids(a);
@@ -98,10 +116,41 @@ __global__ __launch_bounds__(256) void pref_gather_kernel(PrefRmArgs a) {
       if (ph == 0 && c < din) {
         float* out = a.partials + (size_t)blockIdx.x * 2 * din;
         const int j = threadIdx.x & 63;
-        out[c] = (red[0][0][j] + red[1][0][j]) + (red[2][0][j] + red[3][0][j]);
-        out[din + c] = (red[0][1][j] + red[1][1][j]) + (red[2][1][j] + red[3][1][j]);
+        st_sc1(out + c, (red[0][0][j] + red[1][0][j]) + (red[2][0][j] + red[3][0][j]));
+        st_sc1(out + din + c, (red[0][1][j] + red[1][1][j]) + (red[2][1][j] + red[3][1][j]));
       }
       __syncthreads();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) is_last = atomicAdd(a.cnt, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (is_last) {
+      // sums[j] = sum over blocks b (in order) of partials[b][j]: 64 sums x 4 block phases
+      // per pass, 8 sc1 loads in flight per lane
+      const int nb = gridDim.x, ns = 2 * din;
+      for (int j0 = 0; j0 < ns; j0 += 64) {
+        const int j = j0 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+        double acc = 0.0;
+        if (j < ns)
+          for (int b0 = q; b0 < nb; b0 += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = ld_sc1(a.partials + (size_t)min(b0 + 4 * u, nb - 1) * ns + j);
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                         :
+                         : "memory");
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (b0 + 4 * u < nb) acc += (double)v[u];
+          }
+        dred[q][threadIdx.x & 63] = acc;
+        __syncthreads();
+        if (q == 0 && j < ns) a.sums[j] = (dred[0][threadIdx.x] + dred[1][threadIdx.x]) + (dred[2][threadIdx.x] + dred[3][threadIdx.x]);
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   const int c = threadIdx.x & 127;
@@ -115,26 +164,6 @@ __global__ __launch_bounds__(256) void pref_gather_kernel(PrefRmArgs a) {
       if (a.rcount) a.old_cnt[0] = *a.rcount;
       if (a.step) *a.step += 1.f;
     }
-  }
-}
-
-// DP: the block sums in fixed order -> sums (fp64), all-reduced by the host before pref_fwd
-__global__ __launch_bounds__(256) void pref_sums_kernel(PrefRmArgs a) {
-  __shared__ double red[2][2][128];
-  const int c = threadIdx.x & 127, ph = threadIdx.x >> 7;
-  const int nb = (2 * a.n * a.L + kRows - 1) / kRows;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < a.din)
-    for (int b = ph; b < nb; b += 2) {
-      s1 += (double)a.partials[(size_t)b * 2 * a.din + c];
-      s2 += (double)a.partials[(size_t)b * 2 * a.din + a.din + c];
-    }
-  red[ph][0][c] = s1;
-  red[ph][1][c] = s2;
-  __syncthreads();
-  if (ph == 0 && c < a.din) {
-    a.sums[c] = red[0][0][c] + red[1][0][c];
-    a.sums[a.din + c] = red[0][1][c] + red[1][1][c];
   }
 }
 
@@ -166,11 +195,9 @@ __device__ __forceinline__ Imgs carve(char* smem, const PrefPlan& p, int n_layer
   return m;
 }
 
-// mode 0: moments from the gather's block sums; 1: from the (all-reduced) sums, n_total rows
-__global__ __launch_bounds__(64 * kNW) void pref_fwd_kernel(PrefRmArgs a, PrefPlan p, int mode, int n_total) {
+// moments from sums (the gather's; under data parallelism all-reduced over n_total rows)
+__global__ __launch_bounds__(64 * kNW) void pref_fwd_kernel(PrefRmArgs a, PrefPlan p, int n_total) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ double dsum[4][128];
-  __shared__ double dtot[256];
   __shared__ float nrm[256];
   __shared__ float out[kRows];
   const int c = threadIdx.x & 127;
@@ -180,30 +207,11 @@ __global__ __launch_bounds__(64 * kNW) void pref_fwd_kernel(PrefRmArgs a, PrefPl
   lds_zero(smem, p.lds_bytes);
   // ---- RunningNorm: batch moments (fixed order), Chan merge into the pre-minibatch snapshot
   if (a.rmean) {
-    if (mode == 0) {
-      // 2 din sums per gather block: thread (j, phase) with j < 64 a sum index (din <= 32
-      // here: 4 block phases; wider inputs: 2), phases combined in order below
-      const int nb = (rows + kRows - 1) / kRows, ns = 2 * a.din;
-      const int npj = ns <= 64 ? 64 : 128, nph = 256 / npj;
-      const int j = threadIdx.x % npj, q = threadIdx.x / npj;
-      double s = 0.0;
-      if (j < ns)
-        for (int b = q; b < nb; b += nph) s += (double)a.partials[(size_t)b * ns + j];
-      dsum[q][j] = s;
-      __syncthreads();
-      if (threadIdx.x < ns) {
-        double t = 0.0;
-        for (int qq = 0; qq < nph; ++qq) t += dsum[qq][threadIdx.x];
-        dtot[threadIdx.x] = t;
-      }
-    }
-    __syncthreads();
     if (threadIdx.x < 128) {
       float mean = 0.f, rstd = 1.f;
       if (c < a.din) {
-        const double S1 = mode == 0 ? dtot[c] : a.sums[c];
-        const double S2 = mode == 0 ? dtot[a.din + c] : a.sums[a.din + c];
-        const int n = mode == 0 ? rows : n_total;
+        const double S1 = a.sums[c], S2 = a.sums[a.din + c];
+        const int n = n_total > 0 ? n_total : rows;
         float rm = a.old_mv[c], rv = a.old_mv[128 + c];
         if (a.merge) {
           const double bm = S1 / n;
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(64 * kNW) void pref_fwd_kernel(PrefRmArgs a, PrefPl
       nrm[c] = mean;
       nrm[128 + c] = rstd;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && a.merge) *a.rcount = a.old_cnt[0] + (mode == 0 ? rows : n_total);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.merge) *a.rcount = a.old_cnt[0] + (n_total > 0 ? n_total : rows);
   } else if (threadIdx.x < 128) {
     nrm[c] = 0.f;
     nrm[128 + c] = 1.f;
@@ -385,13 +393,8 @@ hipError_t pref_rm_gather(const PrefRmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t pref_rm_sums(const PrefRmArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(pref_sums_kernel, dim3(1), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t pref_rm_fwd(const PrefRmArgs& a, const PrefPlan& p, int mode, int n_total, hipStream_t s) {
-  hipLaunchKernelGGL(pref_fwd_kernel, dim3(pref_rm_blocks(a.n, a.L)), dim3(64 * kNW), p.lds_bytes, s, a, p, mode, n_total);
+hipError_t pref_rm_fwd(const PrefRmArgs& a, const PrefPlan& p, int n_total, hipStream_t s) {
+  hipLaunchKernelGGL(pref_fwd_kernel, dim3(pref_rm_blocks(a.n, a.L)), dim3(64 * kNW), p.lds_bytes, s, a, p, n_total);
   return hipGetLastError();
 }
 

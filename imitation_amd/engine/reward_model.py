@@ -114,7 +114,7 @@ class FusedMinibatch:
         if self.world == 1:
             return plan.step(idx, merge)[: self.n_metrics]
         sync = self.norm is not None and pdist.norm_sync_active()
-        plan.gather(idx, merge, sync)
+        plan.gather(idx, merge)
         if sync:
             pdist.allreduce_sum_(plan.sums)
         plan.forward(idx, merge, self.world * 2 * self.L * int(idx.shape[0]) if sync else 0)

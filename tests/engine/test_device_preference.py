@@ -208,7 +208,7 @@ def test_fused_reward_minibatch_matches_autograd(monkeypatch):
     snap = [t.detach().clone() for t in (norm.running_mean, norm.running_var, norm.count)]
     L, n, B = store.L, 8, trainer.batch_size
     idx = th.arange(3, 3 + 2 * n, 2, device="cuda")
-    plan.gather(idx, True, True)
+    plan.gather(idx, True)
     plan.forward(idx, True, n * 2 * L)
     plan.backward(idx, True)
     g_fused = plan.grads.clone()

@@ -24,8 +24,19 @@ def main():
         def w(*a, **k):
             th.cuda.synchronize()
             t0 = time.perf_counter()
+            prof = None
+            if os.environ.get("PROBE_CPROFILE") == label and not calls[label]:
+                import cProfile
+
+                prof = cProfile.Profile()
+                prof.enable()
             r = fn(*a, **k)
             th.cuda.synchronize()
+            if prof is not None:
+                import pstats
+
+                prof.disable()
+                pstats.Stats(prof).sort_stats("cumulative").print_stats(30)
             acc[label] += time.perf_counter() - t0
             calls[label] += 1
             return r
