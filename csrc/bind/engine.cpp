@@ -245,7 +245,8 @@ std::string ppo_path(py::dict d) {
   ia::PPORcGeo geo;
   size_t lds = 0;
   if (ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, lds))
-    return "rc:g" + std::to_string(geo.G) + "x" + std::to_string(geo.nch) + "x" + std::to_string(geo.cw) + ":kt" + std::to_string(geo.kt);
+    return "rc:g" + std::to_string(geo.G) + "x" + std::to_string(geo.nch) + "x" + std::to_string(geo.cw) + ":kt" +
+           std::to_string(geo.kt) + (geo.ns ? ":ns" : "");
   return "lds";
 }
 

@@ -396,10 +396,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   const int tid = threadIdx.x;
   const int w = rfl(tid >> 6), lane = tid & 63;
   const int r16 = lane & 15, kk = lane >> 4;
-  const bool ns = g.ns != 0;  // net split: this workgroup runs net blockIdx.x only
-  const int q = ns ? (int)blockIdx.x : w / kHalf;  // 0 actor, 1 critic
-  const int gw = ns ? w : w % kHalf;               // row tile
-  const int grp = ns ? 0 : (int)blockIdx.x;        // row group
+  const bool ns = g.ns != 0;  // net split: workgroup 2 grp + q runs net q of row group grp
+  const int q = ns ? (int)(blockIdx.x & 1) : w / kHalf;  // 0 actor, 1 critic
+  const int gw = ns ? w : w % kHalf;                     // row tile
+  const int grp = ns ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;  // row group
   const int G = g.G, nch = g.nch, cw = CWT > 0 ? CWT : g.cw;
   const int CH = G * nch;
   const int Bg = CH * cw;  // minibatch rows
@@ -429,7 +429,8 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   for (int qq = 0; qq < 2; ++qq) {
 #pragma unroll
     for (int l = 0; l < kL; ++l) {
-      if (l >= (qq == 0 ? a.n_pi : a.n_vf)) continue;
+      // (net split: the other net's images alias this one's -- only net q is loaded)
+      if (l >= (qq == 0 ? a.n_pi : a.n_vf) || (ns && qq != q)) continue;
       const LG y = lg(g, qq, l);
       const int wo = qq == 0 ? a.pi_w_off[l] : a.vf_w_off[l];
       const int bo = qq == 0 ? a.pi_b_off[l] : a.vf_b_off[l];
@@ -440,7 +441,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       for (int i = tid; i < y.dout; i += kThreads) L[y.b + i] = a.params[bo + i];
     }
   }
-  if (tid < 16) L[g.ls_off + tid] = (has_ls && tid < A) ? a.params[a.log_std_off + tid] : 0.f;
+  if (tid < 16) L[g.ls_off + tid] = (has_ls && tid < A && !(ns && q != 0)) ? a.params[a.log_std_off + tid] : 0.f;
   // normaliser running state (double-buffered per-minibatch mean / rstd)
   // (owned by wave 7, one lane per feature)
   const int nc = tid - (kThreads - 64);
@@ -557,9 +558,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // [11] wave 0 B1 wait, [12] dW items; [13..15] exchange: publish, arrival, loads
   __shared__ unsigned long long sprof[16];
   if (tid < 16) sprof[tid] = 0;
-  unsigned* arrive = g.sync;
+  // arrival counters per net under the net split ([0]/[2] actor, [4]/[6] critic)
+  unsigned* arrive = g.sync + (ns ? 4 * q : 0);
   unsigned* tflag = g.sync + 1;
-  unsigned* arrive2 = g.sync + 2;
+  unsigned* arrive2 = g.sync + (ns ? 4 * q + 2 : 2);
   __syncthreads();
 
   for (int k = 0; k < K; ++k) {
@@ -1291,6 +1293,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 constexpr int waves_for(int kt) { return kt == 2 ? 8 : 4; }
 constexpr int wslots_for(int kt) { return kt == 2 ? 5 : 16; }
 constexpr int bslots_for(int kt) { return kt == 2 ? 2 : 3; }
+// net split (4 waves, one net's items): up to 20 / 32 weight tiles and 8 vectors per net
+constexpr int wslots_ns(int kt) { return kt == 2 ? 5 : 8; }
+constexpr int bslots_ns() { return 2; }
 
 }  // namespace
 
@@ -1310,10 +1315,13 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   const int KT = g.kt;
   g.nw = waves_for(KT);
   const char* nsev = getenv("IMITATION_AMD_PPO_NETSPLIT");
-  const bool want_ns = KT == 2 && !(nsev && nsev[0] == '0');
+  // net split: each workgroup runs ONE net (actor or critic) over 64-row chunks -- its 4
+  // row-tile waves at one wave per SIMD, with half of the dW / Adam items a both-nets
+  // workgroup owns -- and the two nets meet once per minibatch for clip_grad_norm_
+  const bool ns = !(nsev && nsev[0] == '0') && (a.rc_cw == 0 || a.rc_cw == 64) && a.batch % 64 == 0;
   // workgroup split: chunks of cw rows (64 for narrow nets, 32 for 64-wide ones: LDS, and
   // the 4-wave workgroup has 2 row-tile waves per net)
-  int cw = KT == 2 ? 64 : 32;
+  int cw = KT == 2 || ns ? 64 : 32;
   if (a.rc_cw == 16 || a.rc_cw == 32 || (a.rc_cw == 64 && KT == 2)) cw = a.rc_cw;
   if (a.batch < cw) cw = a.batch;
   if (a.batch % cw != 0) {
@@ -1330,10 +1338,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.cw = cw;
   g.G = G;
   g.nch = chunks / G;
-  // net split for the one-workgroup plan: actor and critic on two CUs, one wave per SIMD
-  // (the 4 row tiles of a 64-row chunk), instead of both nets' 8 waves sharing one CU's
-  // matrix cores; the row-tile waves of a net are exactly the workgroup's waves
-  g.ns = want_ns && G == 1 && cw == 64 ? 1 : 0;
+  g.ns = ns && cw == 64 ? 1 : 0;
   if (g.ns) g.nw = 4;
   int off = 0;
   auto take = [&](int n) {
@@ -1341,8 +1346,12 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     off += (n + 3) & ~3;
     return o;
   };
-  // parameter images first (zeroed at kernel start)
+  // parameter images first (zeroed at kernel start); net split: both nets' images start at
+  // the same offset (a workgroup holds one net), the region is the larger of the two
+  const int pbase = off;
+  int pend = off;
   for (int q = 0; q < 2; ++q) {
+    if (g.ns) off = pbase;
     for (int l = 0; l < nls[q]; ++l) {
       const int din = dims[q][l], dout = dims[q][l + 1];
       const bool last = l == nls[q] - 1;
@@ -1357,7 +1366,9 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
       g.w_off[q][l] = take(op * g.ldw[q][l]);
       g.b_off[q][l] = take(op);
     }
+    pend = off > pend ? off : pend;
   }
+  off = pend;
   g.ls_off = take(16);
   g.zero_off = take(64);
   g.param_lds = off;
@@ -1365,7 +1376,10 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   // 16 lanes of one b128 read on distinct banks); layer-0 input shared by both nets
   const int ldr = cw + 4;
   const int h0 = take(((a.D + 15) & ~15) * ldr);
+  const int abase = off;
+  int aend = off;
   for (int q = 0; q < 2; ++q) {
+    if (g.ns) off = abase;
     for (int l = 0; l < nls[q]; ++l) {
       if (l == 0) {
         g.h_off[q][0] = h0;
@@ -1378,7 +1392,9 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
       g.z_off[q][l] = take(((g.dout[q][l] + 15) & ~15) * ldr);
       g.db_off[q][l] = take(4 * 64);
     }
+    aend = off > aend ? off : aend;
   }
+  off = aend;
   g.lsp_off = take(4 * 16);
   g.nm_off = take(256);
   g.red_off = take(8 + 8 * 5 + 4);  // wave |g|^2, wave stats, [48] both nets' |g|^2
@@ -1420,7 +1436,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     wmx = g.nwit[0] > g.nwit[1] ? g.nwit[0] : g.nwit[1];
     bmx = g.nbit[0] > g.nbit[1] ? g.nbit[0] : g.nbit[1];
   }
-  if ((wmx + g.nw - 1) / g.nw > wslots_for(KT) || (bmx + g.nw - 1) / g.nw > bslots_for(KT)) return false;
+  const int wcap = g.ns ? wslots_ns(KT) : wslots_for(KT), bcap = g.ns ? bslots_ns() : bslots_for(KT);
+  if ((wmx + g.nw - 1) / g.nw > wcap || (bmx + g.nw - 1) / g.nw > bcap) return false;
   g.dp = (a.D + 3) & ~3;
   return true;
 }
@@ -1467,7 +1484,7 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   bool uniform = a.n_pi == 3 && a.n_vf == 3;
   for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
   const int s0 = (a.D + 3) / 4;
-  const dim3 grid(g.ns ? 2 : g.G), block(64 * g.nw);
+  const dim3 grid(g.ns ? 2 * g.G : g.G), block(64 * g.nw);
   int wmx = g.n_witems, bmx = g.n_items - g.n_witems;
   if (g.ns) {
     wmx = g.nwit[0] > g.nwit[1] ? g.nwit[0] : g.nwit[1];
@@ -1476,16 +1493,22 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   const int nwslot = (wmx + g.nw - 1) / g.nw, nbslot = (bmx + g.nw - 1) / g.nw;
 #define IA_RC(KT, KW, KB, S0, NL, ACT, HW, CW, DT) \
   hipLaunchKernelGGL((ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, CW, DT, waves_for(KT)>), grid, block, lds_launch, s, a, g)
-#define IA_RC_NS(KW, KB, S0, NL, ACT, HW, DT) \
-  hipLaunchKernelGGL((ppo_rc_kernel<2, KW, KB, S0, NL, ACT, HW, 64, DT, 4>), grid, block, lds_launch, s, a, g)
+#define IA_RC_NS(KT, KW, KB, S0, NL, ACT, HW, DT) \
+  hipLaunchKernelGGL((ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, 64, DT, 4>), grid, block, lds_launch, s, a, g)
   const auto fits = [&](int kw, int kb) { return nwslot <= kw && nbslot <= kb; };
   if (g.ns) {
-    if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && !a.discrete && fits(3, 1))
-      IA_RC_NS(3, 1, 5, 3, 2, 32, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
-    else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && a.discrete && fits(2, 1))
-      IA_RC_NS(2, 1, 1, 3, 2, 32, 1);  // CartPole FeedForward32Policy
+    if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && !a.discrete && fits(3, 1))
+      IA_RC_NS(2, 3, 1, 5, 3, 2, 32, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
+    else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && a.discrete && fits(2, 1))
+      IA_RC_NS(2, 2, 1, 1, 3, 2, 32, 1);  // CartPole FeedForward32Policy
+    else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && !a.discrete && fits(6, 1))
+      IA_RC_NS(4, 6, 1, 3, 3, 1, 64, 0);  // Hopper MlpPolicy [64, 64] ReLU (AIRL config)
+    else if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && g.kt == 4 && !a.discrete && fits(7, 1))
+      IA_RC_NS(4, 7, 1, 5, 3, 1, 64, 0);  // Walker2d MlpPolicy [64, 64] ReLU (DRLHP config)
+    else if (g.kt == 2)
+      IA_RC_NS(2, wslots_ns(2), bslots_ns(), 0, 0, -1, 0, -1);
     else
-      IA_RC_NS(wslots_for(2), bslots_for(2), 0, 0, -1, 0, -1);
+      IA_RC_NS(4, wslots_ns(4), bslots_ns(), 0, 0, -1, 0, -1);
   } else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete && fits(3, 1))
     IA_RC(2, 3, 1, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
   else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 32 && !a.discrete && fits(3, 1))

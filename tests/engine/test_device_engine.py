@@ -94,29 +94,44 @@ def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, nor
 
 @gpu
 @pytest.mark.parametrize("env_id,allow_rc,batch,gmax,net_arch,path", [
-    ("seals/HalfCheetah-v1", 1, 64, 0, None, "rc:g1x1x64:kt2"),
+    # ":ns" = net split: one net per workgroup over 64-row chunks, 2 x G workgroups
+    ("seals/HalfCheetah-v1", 1, 64, 0, None, "rc:g1x1x64:kt2:ns"),
     ("seals/HalfCheetah-v1", 0, 64, 0, None, "lds"),
-    ("seals/CartPole-v0", 1, 64, 0, None, "rc:g1x1x64:kt2"),
+    ("seals/CartPole-v0", 1, 64, 0, None, "rc:g1x1x64:kt2:ns"),
     ("seals/CartPole-v0", 0, 64, 0, None, "lds"),
     # cooperating workgroups (sc1 partial exchange) and multi-chunk workgroups
-    ("seals/HalfCheetah-v1", 1, 128, 0, None, "rc:g2x1x64:kt2"),
-    ("seals/HalfCheetah-v1", 1, 128, 1, None, "rc:g1x2x64:kt2"),
-    ("seals/HalfCheetah-v1", 1, 256, 2, None, "rc:g2x2x64:kt2"),
-    ("seals/CartPole-v0", 1, 256, 0, None, "rc:g4x1x64:kt2"),
-    # 64-wide nets (AIRL-Hopper MlpPolicy [64, 64]): 32-row chunks
-    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64]), "rc:g2x1x32:kt4"),
-    ("seals/Hopper-v1", 1, 256, 4, dict(pi=[64, 64], vf=[64, 64]), "rc:g4x2x32:kt4"),
-    # the shape-specialised 64-wide ReLU builds (4-wave workgroups, owned state in AGPRs):
-    # AIRL-Hopper (minibatch 512 -> 16 workgroups, two-level exchange) and DRLHP-Walker
-    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g2x1x32:kt4"),
-    ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g16x1x32:kt4"),
-    ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g4x1x32:kt4"),
+    ("seals/HalfCheetah-v1", 1, 128, 0, None, "rc:g2x1x64:kt2:ns"),
+    ("seals/HalfCheetah-v1", 1, 128, 1, None, "rc:g1x2x64:kt2:ns"),
+    ("seals/HalfCheetah-v1", 1, 256, 2, None, "rc:g2x2x64:kt2:ns"),
+    ("seals/CartPole-v0", 1, 256, 0, None, "rc:g4x1x64:kt2:ns"),
+    # 64-wide nets (AIRL-Hopper MlpPolicy [64, 64])
+    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64]), "rc:g1x1x64:kt4:ns"),
+    ("seals/Hopper-v1", 1, 256, 4, dict(pi=[64, 64], vf=[64, 64]), "rc:g4x1x64:kt4:ns"),
+    # the shape-specialised 64-wide ReLU builds: AIRL-Hopper (minibatch 512, 8 row groups x
+    # 2 nets, two-level exchange) and DRLHP-Walker
+    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g1x1x64:kt4:ns"),
+    ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g8x1x64:kt4:ns"),
+    ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g2x1x64:kt4:ns"),
+    # both nets per workgroup (IMITATION_AMD_PPO_NETSPLIT=0): 64-row chunks for <= 32-wide
+    # nets, 32-row chunks (2 row-tile waves per net) for 64-wide ones
+    ("seals/HalfCheetah-v1", 1, 64, 0, "nons", "rc:g1x1x64:kt2"),
+    ("seals/HalfCheetah-v1", 1, 256, 2, "nons", "rc:g2x2x64:kt2"),
+    ("seals/CartPole-v0", 1, 256, 0, "nons", "rc:g4x1x64:kt2"),
+    ("seals/Hopper-v1", 1, 256, 4, dict(pi=[64, 64], vf=[64, 64], nons=True), "rc:g4x2x32:kt4"),
+    ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g16x1x32:kt4"),
+    ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g4x1x32:kt4"),
 ])
-def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_arch, path):
+def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_arch, path, monkeypatch):
     act = None
-    if net_arch is not None and net_arch.get("act") == "relu":
-        net_arch = {k: v for k, v in net_arch.items() if k != "act"}
-        act = th.nn.ReLU
+    nons = net_arch == "nons" or (isinstance(net_arch, dict) and net_arch.get("nons"))
+    if net_arch == "nons":
+        net_arch = None
+    if nons:
+        monkeypatch.setenv("IMITATION_AMD_PPO_NETSPLIT", "0")
+    if net_arch is not None:
+        if net_arch.get("act") == "relu":
+            act = th.nn.ReLU
+        net_arch = {k: v for k, v in net_arch.items() if k not in ("act", "nons")}
     tr, venv, gen, rn = _setup(env_id=env_id, n_envs=8 if batch > 64 else 4, n_steps=64 if batch > 256 else 32,
                                batch=batch, n_epochs=2, net_arch=net_arch, activation=act)
     tr._ppo_static["allow_rc"] = allow_rc
