@@ -29,7 +29,7 @@
 #define IA_EXPF(x) __expf(x)
 #define IA_SINF(x) __sinf(x)
 #define IA_COSF(x) __cosf(x)
-#define IA_RCPF(x) __frcp_rn(x)
+#define IA_RCPF(x) __builtin_amdgcn_rcpf(x)  // v_rcp_f32 (1 ulp), not the div_scale/fixup sequence
 #else
 #define IA_RCPF(x) (1.0f / (x))
 #define IA_EXPF(x) expf(x)

@@ -14,7 +14,8 @@
 //                then one system-scope acquire per block
 //   4. reduce  : read slot `parity` of ranks 0..W-1 in rank order, sum, store
 //
-// Blocks are independent (block b owns a FIXED slice of the staging region -- vectors
+// fp32 buckets (gradients) and fp64 ones (normaliser column sums) use the same byte-sized
+// slices. Blocks are independent (block b owns a FIXED slice of the staging region -- vectors
 // [b * per, (b + 1) * per) with per = stage_vectors / kOneShotMaxBlocks, whatever the
 // bucket size -- and its own flag row / generation counter), so no inter-block
 // synchronisation is needed and partial residency cannot deadlock.  Two staging parities
@@ -60,7 +61,18 @@ __device__ __forceinline__ unsigned load_relaxed_sys(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// 16-byte staging vector of T (float4 / double2): the slice geometry is in bytes, so fp32
+// gradients and fp64 normaliser sums share the region and its per-block slices.
+template <typename T>
+struct alignas(16) Vec16 {
+  static constexpr int kN = 16 / sizeof(T);
+  T e[kN];
+};
+
+template <typename T>
 __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(OneShotArgs a) {
+  using V = Vec16<T>;
+  constexpr int EPV = V::kN;
   __shared__ unsigned s_gen;
   __shared__ int s_fail;
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -75,28 +87,29 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(OneShotArgs
   __syncthreads();
   const unsigned gen = s_gen;
   const size_t par = (gen & 1u) ? a.stage_bytes : 0;
+  const T scale = (T)a.scale;
+  const T* in = reinterpret_cast<const T*>(a.in);
+  T* out = reinterpret_cast<T*>(a.out);
 
-  // fixed slice of float4 vectors owned by this block (the n % 4 tail belongs to the block
-  // whose slice holds vector nv)
-  const int nv = a.n >> 2;
+  // fixed slice of 16-byte vectors owned by this block (the n % EPV tail belongs to the
+  // block whose slice holds vector nv)
+  const int nv = a.n / EPV;
   const int per = oneshot_block_vectors(a.stage_bytes);
   const int v0 = min(nv, b * per), v1 = min(nv, v0 + per);
   const bool tail_owner = b == nv / per;
-  const int tail0 = nv << 2;
+  const int tail0 = nv * EPV;
 
   // 1. stage
-  float* st = reinterpret_cast<float*>(me + kDataOff + par);
-  const float4* in4 = reinterpret_cast<const float4*>(a.in);
-  float4* st4 = reinterpret_cast<float4*>(st);
+  T* st = reinterpret_cast<T*>(me + kDataOff + par);
+  const V* in4 = reinterpret_cast<const V*>(in);
+  V* st4 = reinterpret_cast<V*>(st);
   for (int v = v0 + tid; v < v1; v += kThreads) {
-    float4 x = in4[v];
-    x.x *= a.scale;
-    x.y *= a.scale;
-    x.z *= a.scale;
-    x.w *= a.scale;
+    V x = in4[v];
+#pragma unroll
+    for (int i = 0; i < EPV; ++i) x.e[i] *= scale;
     st4[v] = x;
   }
-  if (tail_owner && tid < a.n - tail0) st[tail0 + tid] = a.in[tail0 + tid] * a.scale;
+  if (tail_owner && tid < a.n - tail0) st[tail0 + tid] = in[tail0 + tid] * scale;
   // every storing wave drains its stores before the barrier; the signalling lanes then
   // release at system scope and wait again (the compiler may drop the fence's own wait)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -126,29 +139,32 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(OneShotArgs
   __syncthreads();
 
   if (s_fail) {
-    const float nan = __builtin_nanf("");
-    for (int v = v0 + tid; v < v1; v += kThreads) reinterpret_cast<float4*>(a.out)[v] = make_float4(nan, nan, nan, nan);
-    if (tail_owner && tid < a.n - tail0) a.out[tail0 + tid] = nan;
+    const T nan = (T)__builtin_nanf("");
+    for (int v = v0 + tid; v < v1; v += kThreads) {
+      V x;
+#pragma unroll
+      for (int i = 0; i < EPV; ++i) x.e[i] = nan;
+      reinterpret_cast<V*>(out)[v] = x;
+    }
+    if (tail_owner && tid < a.n - tail0) out[tail0 + tid] = nan;
     if (tid == 0) store_release_sys(reinterpret_cast<unsigned*>(me + kErrOff), 1u);
     return;
   }
 
   // 4. reduce in rank order (identical on every rank)
   for (int v = v0 + tid; v < v1; v += kThreads) {
-    float4 acc = reinterpret_cast<const float4*>(a.base[0] + kDataOff + par)[v];
+    V acc = reinterpret_cast<const V*>(a.base[0] + kDataOff + par)[v];
     for (int r = 1; r < a.world; ++r) {
-      const float4 x = reinterpret_cast<const float4*>(a.base[r] + kDataOff + par)[v];
-      acc.x += x.x;
-      acc.y += x.y;
-      acc.z += x.z;
-      acc.w += x.w;
+      const V x = reinterpret_cast<const V*>(a.base[r] + kDataOff + par)[v];
+#pragma unroll
+      for (int i = 0; i < EPV; ++i) acc.e[i] += x.e[i];
     }
-    reinterpret_cast<float4*>(a.out)[v] = acc;
+    reinterpret_cast<V*>(out)[v] = acc;
   }
   if (tail_owner && tid < a.n - tail0) {
-    float acc = reinterpret_cast<const float*>(a.base[0] + kDataOff + par)[tail0 + tid];
-    for (int r = 1; r < a.world; ++r) acc += reinterpret_cast<const float*>(a.base[r] + kDataOff + par)[tail0 + tid];
-    a.out[tail0 + tid] = acc;
+    T acc = reinterpret_cast<const T*>(a.base[0] + kDataOff + par)[tail0 + tid];
+    for (int r = 1; r < a.world; ++r) acc += reinterpret_cast<const T*>(a.base[r] + kDataOff + par)[tail0 + tid];
+    out[tail0 + tid] = acc;
   }
 }
 
@@ -156,8 +172,9 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(OneShotArgs
 
 size_t oneshot_region_bytes(size_t stage_bytes) { return kDataOff + 2 * stage_bytes; }
 
-int oneshot_blocks(int n, size_t stage_bytes) {
-  const int nv = (n + 3) >> 2;
+int oneshot_blocks(int n, size_t stage_bytes, int elem_bytes) {
+  const int epv = 16 / elem_bytes;
+  const int nv = (n + epv - 1) / epv;
   const int per = oneshot_block_vectors(stage_bytes);
   const int blocks = (nv + per - 1) / per;
   return blocks < 1 ? 1 : blocks;  // <= kOneShotMaxBlocks since n * 4 <= stage_bytes
@@ -207,10 +224,15 @@ long long oneshot_ticks_per_second() {
 
 hipError_t oneshot_allreduce(const OneShotArgs& a, hipStream_t s) {
   if (a.world < 1 || a.world > kOneShotMaxRanks || a.rank < 0 || a.rank >= a.world) return hipErrorInvalidValue;
-  if ((size_t)a.n * sizeof(float) > a.stage_bytes) return hipErrorInvalidValue;
+  const int eb = a.f64 ? 8 : 4;
+  if ((size_t)a.n * eb > a.stage_bytes) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out)) & 15) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(oneshot_blocks(a.n, a.stage_bytes)), dim3(kThreads), 0, s, a);
+  const dim3 g(oneshot_blocks(a.n, a.stage_bytes, eb));
+  if (a.f64)
+    hipLaunchKernelGGL(oneshot_allreduce_kernel<double>, g, dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(oneshot_allreduce_kernel<float>, g, dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

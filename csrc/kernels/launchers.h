@@ -404,16 +404,17 @@ constexpr int kOneShotMaxRanks = 8;
 constexpr int kOneShotMaxBlocks = 64;
 struct OneShotArgs {
   char* base[kOneShotMaxRanks];  // every rank's region as mapped in this process (base[rank] local)
-  const float* in;               // 16-B aligned
-  float* out;                    // 16-B aligned, may alias in
-  int n, rank, world;
-  float scale;                   // applied to this rank's contribution before the sum
+  const void* in;                // 16-B aligned, float (f64 == 0) or double elements
+  void* out;                     // 16-B aligned, may alias in
+  int n, rank, world;            // n: elements
+  int f64;                       // elements are double (normaliser sums) instead of float
+  double scale;                  // applied to this rank's contribution before the sum
   size_t stage_bytes;
   long long timeout_ticks;       // wall-clock ticks before a block gives up (NaN output + error word)
 };
 size_t oneshot_region_bytes(size_t stage_bytes);
 size_t oneshot_handle_bytes();
-int oneshot_blocks(int n, size_t stage_bytes);
+int oneshot_blocks(int n, size_t stage_bytes, int elem_bytes = 4);
 hipError_t oneshot_alloc(size_t stage_bytes, void** ptr, void* handle);  // zeroed uncached region + IPC handle
 hipError_t oneshot_open(const void* handle, void** ptr);
 hipError_t oneshot_close(void* ptr);

@@ -237,7 +237,8 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
   float q = L.q, qd = L.qd;
   for (int sub = 0; sub < p.frame_skip; ++sub) {
     const float qdd = L.gear * a - L.stiff * q - L.damp * qd - 2.0f * __sinf(q);
-    const float st = jl ? stance(q) : 0.f;
+    const float st_all = stance(q);  // every lane (no exec-masked branch around the exp / rcp)
+    const float st = jl ? st_all : 0.f;
     const float th_j = L.thrust * st * fmaxf(-qd, 0.f);
     qd = qd + dt * qdd;
     const float thrust = sum_lanes8(th_j);
@@ -272,10 +273,11 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
         }
       }
     }
-    float qn = q + dt * qd;
-    if (qn > 1.2f) { qn = 1.2f; if (qd > 0) qd = 0.f; }
-    if (qn < -1.2f) { qn = -1.2f; if (qd < 0) qd = 0.f; }
-    q = qn;
+    // joint limit: clamp q and kill the velocity into the stop, as selects (no branches)
+    const float qn = q + dt * qd;
+    const bool hi = qn > 1.2f, lo = qn < -1.2f;
+    qd = (hi && qd > 0.f) || (lo && qd < 0.f) ? 0.f : qd;
+    q = fminf(fmaxf(qn, -1.2f), 1.2f);
   }
   L.q = jl ? q : 0.f;
   L.qd = jl ? qd : 0.f;
@@ -286,12 +288,16 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
 // stores need no scalar base registers, and the five per-env scalars of a step go out
 // as ONE store (lane 0 env reward, 1 done, 2 truncation, 3 finished-episode return,
 // 4 episode start).
+// Typed global (address_space 1): pin()'s asm would otherwise erase the address space and
+// the stores would be FLAT, which count in lgkmcnt too -- every LDS wait of the next actor
+// layer then also waited for the previous step's stores to retire.
+typedef __attribute__((address_space(1))) float gfl;
 struct Cursors {
-  float* obs;
-  float* next_obs;
-  float* act_raw;
-  float* act_env;
-  float* sc;
+  gfl* obs;
+  gfl* next_obs;
+  gfl* act_raw;
+  gfl* act_env;
+  gfl* sc;
   int vec_step, act_step, sc_step;
 };
 
@@ -350,13 +356,13 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   c.vec_step = a.N * D;
   c.act_step = a.N * A;
   c.sc_step = a.N;
-  c.obs = pin(a.obs_buf + (size_t)n * D + (lane < D ? lane : 0));
-  c.next_obs = pin(a.next_obs + (size_t)n * D + (lane < D ? lane : 0));
-  c.act_raw = pin(a.act_raw + (size_t)n * A + (lane < A ? lane : 0));
-  c.act_env = pin(a.act_env + (size_t)n * A + (lane < A ? lane : 0));
+  c.obs = pin((gfl*)(a.obs_buf + (size_t)n * D + (lane < D ? lane : 0)));
+  c.next_obs = pin((gfl*)(a.next_obs + (size_t)n * D + (lane < D ? lane : 0)));
+  c.act_raw = pin((gfl*)(a.act_raw + (size_t)n * A + (lane < A ? lane : 0)));
+  c.act_env = pin((gfl*)(a.act_env + (size_t)n * A + (lane < A ? lane : 0)));
   {
     float* b = lane == 0 ? a.env_rew : lane == 1 ? a.dones : lane == 2 ? a.trunc : lane == 3 ? a.ep_ret_out : a.starts;
-    c.sc = pin(b + n);
+    c.sc = pin((gfl*)(b + n));
   }
 
   float o = lane < D ? a.cur_obs[(size_t)n * D + lane] : 0.f;
@@ -451,10 +457,13 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       const bool trunc = !term && elapsed >= max_steps;
       const bool done = term || trunc;
       if (lane < D) *c.next_obs = o_next;
-      if (lane < 5) {
-        const float v = lane == 0 ? r_env : lane == 1 ? (done ? 1.f : 0.f) : lane == 2 ? (trunc ? 1.f : 0.f)
-                      : lane == 3 ? (done ? ep_ret : 0.f) : start;
-        *c.sc = v;
+      {  // selects, not a nest of exec-masked branches
+        float v = start;
+        v = lane == 3 ? (done ? ep_ret : 0.f) : v;
+        v = lane == 2 ? (trunc ? 1.f : 0.f) : v;
+        v = lane == 1 ? (done ? 1.f : 0.f) : v;
+        v = lane == 0 ? r_env : v;
+        if (lane < 5) *c.sc = v;
       }
       c.obs += c.vec_step;
       c.next_obs += c.vec_step;

@@ -721,7 +721,7 @@ class BasicRewardTrainer(RewardTrainer):
                 and (world == 1 or self._dp_graph_ok() or reward_model.fused_check(self)[0])
                 and os.environ.get("IMITATION_AMD_PREF_GRAPH", "1") != "0"):
             graph = self._minibatch_graph(s_all, a_all, ns_all, d_all, prefs_all, gt, P, L, B)
-        if (graph is not None and graph.fused is not None and graph.fused.capturable
+        if (graph is not None and graph.fused is not None and graph.fused.capturable and world == 1
                 and os.environ.get("IMITATION_AMD_PREF_EPOCH_GRAPH", "1") != "0"):
             with self.logger.accumulate_means("reward"):
                 return self._train_fused_epochs(graph, index_loader, epochs, P, dev)

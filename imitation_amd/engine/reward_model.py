@@ -94,7 +94,9 @@ class FusedMinibatch:
     Data parallel (each rank its slice of the global minibatch, as the autograd fast path):
     the RunningNorm block sums are all-reduced between the gather and the forward when
     normaliser statistics are synchronised, and the reduced gradient before AdamW -- two
-    collectives (RCCL / gloo, fp64 sums), so that step runs eagerly (``capturable`` False)."""
+    collectives. On the one-shot IPC all-reduce (both buffers fit its staging slot) they are
+    capturable and the DP step is graph-replayed like the single-rank one; over RCCL / gloo
+    the step runs eagerly (``capturable`` False)."""
 
     def __init__(self, trainer, store, L: int, capacity: int):
         from imitation_amd.parallel import dist as pdist
@@ -104,7 +106,16 @@ class FusedMinibatch:
         self.plan, self.norm = build_plan(trainer, store, L, capacity)
         self.n_metrics = 3 if store.gt is not None else 2
         self.world = pdist.world_size()
-        self.capturable = self.world == 1
+        self.capturable = self.world == 1 or self._oneshot_ok()
+
+    def _oneshot_ok(self) -> bool:
+        from imitation_amd.parallel import dist as pdist
+
+        if not pdist.oneshot_active():
+            return False
+        from imitation_amd.parallel import oneshot
+
+        return all(oneshot._COMM.fits(t) for t in (self.plan.sums, self.plan.grads))
 
     def step(self, idx: th.Tensor) -> th.Tensor:
         from imitation_amd.parallel import dist as pdist

@@ -91,7 +91,7 @@ def shutdown() -> None:
 
 
 def _oneshot_for(t: torch.Tensor):
-    """The one-shot communicator if it can reduce ``t`` (fp32, contiguous, on this GPU, small)."""
+    """The one-shot communicator if it can reduce ``t`` (fp32 or fp64, contiguous, on this GPU, small)."""
     from imitation_amd.parallel import oneshot
 
     c = oneshot._COMM

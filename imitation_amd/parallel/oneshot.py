@@ -73,8 +73,8 @@ class OneShotComm:
         self.calls = 0
 
     def fits(self, t: torch.Tensor) -> bool:
-        return (t.is_cuda and t.device == self.device and t.dtype == torch.float32 and t.is_contiguous()
-                and t.numel() * 4 <= self.stage_bytes and t.data_ptr() % 16 == 0)
+        return (t.is_cuda and t.device == self.device and t.dtype in (torch.float32, torch.float64) and t.is_contiguous()
+                and t.numel() * t.element_size() <= self.stage_bytes and t.data_ptr() % 16 == 0)
 
     def allreduce_(self, t: torch.Tensor, scale: float = 1.0) -> None:
         """``t <- sum_r scale * t_r`` in place (rank-order sum, identical on all ranks)."""

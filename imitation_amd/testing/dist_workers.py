@@ -237,6 +237,15 @@ def oneshot_worker(rank, world, sizes, scale, seed):
         x = th.as_tensor(np.random.default_rng(seed * 100 + rank * 7 + n).normal(size=n).astype(np.float32), device=dev)
         c.allreduce_(x, scale)
         out["eager"].append(x.cpu().numpy())
+    # fp64 buckets (normaliser column sums) interleaved with fp32 ones: same slices, same
+    # generation counters
+    out["f64"] = []
+    for n in sizes[:4]:
+        x = th.as_tensor(np.random.default_rng(seed * 100 + rank * 7 + n + 5).normal(size=n), device=dev)
+        c.allreduce_(x, scale)
+        y = th.ones(n + 3, device=dev)
+        c.allreduce_(y)
+        out["f64"].append(x.cpu().numpy())
     # graph-captured launch: the generation counter lives on the device, so replays stay in step
     buf = th.zeros(sizes[-1], device=dev)
     side = th.cuda.Stream(device=dev)

@@ -32,6 +32,13 @@ def test_oneshot_allreduce_matches_rank_order_sum(world, oneshot_env):
         assert out[r]["error"] == 0
         for n, got in zip(sizes, out[r]["eager"]):
             np.testing.assert_array_equal(got, _expected(world, n, scale, seed))
+        for n, got in zip(sizes[:4], out[r]["f64"]):  # fp64 elements: rank-order double sum
+            exp = None
+            for q in range(world):
+                x = np.random.default_rng(seed * 100 + q * 7 + n + 5).normal(size=n) * scale
+                exp = x if exp is None else exp + x
+            assert got.dtype == np.float64
+            np.testing.assert_array_equal(got, exp)
         for rep, got in enumerate(out[r]["graph"]):
             n = sizes[-1]
             exp = None
