@@ -399,7 +399,8 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
 // RunningNorm: (optionally) merge x's moments into mean / var / count in place, and return
 // the normalised x (or None with want_y = false)
 py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, torch::Tensor count, double eps,
-                        bool update, bool want_y) {
+                        bool update, bool want_y, c10::optional<torch::Tensor> ema_inv_lr,
+                        c10::optional<torch::Tensor> ema_num_batches, double ema_decay) {
   IA_CHECK_GPU_F32(x);
   IA_CHECK_CONTIG(x);
   IA_CHECK_GPU_F32(mean);
@@ -411,6 +412,19 @@ py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, 
   TORCH_CHECK(x.dim() == 2 && mean.numel() == x.size(1) && var.numel() == x.size(1), "running_norm: x [B, D]");
   const int B = (int)x.size(0), D = (int)x.size(1);
   TORCH_CHECK(ia::running_norm_ok(B, D), "running_norm: B * D <= 2^20, D <= 256");
+  float* inv_lr = nullptr;
+  int* nbat = nullptr;
+  if (ema_inv_lr && ema_inv_lr->defined()) {
+    TORCH_CHECK(ema_num_batches && ema_num_batches->defined(), "running_norm: EMA needs inv_learning_rate and num_batches");
+    IA_CHECK_GPU_F32(*ema_inv_lr);
+    IA_CHECK_CUDA(*ema_num_batches);
+    TORCH_CHECK(ema_inv_lr->numel() == 1 && ema_num_batches->numel() == 1 &&
+                    ema_num_batches->scalar_type() == torch::kInt32,
+                "running_norm: scalar fp32 inv_learning_rate, int32 num_batches");
+    TORCH_CHECK(ema_decay > 0.0 && ema_decay < 1.0, "running_norm: EMA decay in (0, 1)");
+    inv_lr = ema_inv_lr->data_ptr<float>();
+    nbat = ema_num_batches->data_ptr<int>();
+  }
   torch::Tensor y;
   if (want_y) y = torch::empty_like(x);
   // block partials of the multi-workgroup path (caching allocator: graph-capture safe)
@@ -419,7 +433,7 @@ py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, 
   if (wsn) ws = torch::empty({(int64_t)wsn}, x.options());
   IA_HIP_CHECK(ia::running_norm(x.data_ptr<float>(), B, D, mean.data_ptr<float>(), var.data_ptr<float>(),
                                 count.data_ptr<int>(), (float)eps, update ? 1 : 0, want_y ? y.data_ptr<float>() : nullptr,
-                                wsn ? ws.data_ptr<float>() : nullptr, ia_stream()));
+                                wsn ? ws.data_ptr<float>() : nullptr, ia_stream(), inv_lr, nbat, (float)ema_decay));
   return want_y ? py::cast(y) : py::none();
 }
 
@@ -486,7 +500,8 @@ void register_kernels(py::module& m) {
         py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"));
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
   m.def("running_norm", &running_norm, py::arg("x"), py::arg("mean"), py::arg("var"), py::arg("count"), py::arg("eps"),
-        py::arg("update"), py::arg("want_y"));
+        py::arg("update"), py::arg("want_y"), py::arg("ema_inv_lr") = py::none(), py::arg("ema_num_batches") = py::none(),
+        py::arg("ema_decay") = 0.0);
   m.def("gather_rows", &gather_rows, py::arg("srcs"), py::arg("b"), py::arg("e") = py::none(), py::arg("n_envs") = 1);
   m.def("soft_value_iteration", &soft_value_iteration, py::arg("T"), py::arg("R"), py::arg("H"), py::arg("gamma"));
   m.def("occupancy_measures", &occupancy_measures, py::arg("T"), py::arg("P"), py::arg("D0"));

@@ -31,7 +31,7 @@ __device__ inline void chan_merge(float* rmean, float* rvar, int count, int c, f
 // LDS images are bf16 [row][k] with row stride ld (K-contiguous MFMA operands, mfma.h).
 
 // rows [row0, row0 + 64) of X [B][din] -> image H (normalised with nrm slot: mean, rstd)
-__device__ inline void stage_rows(bf16* H, int ld, const float* __restrict__ X, int din, int B, int row0, const float* nrm) {
+__device__ inline void stage_rows(lbf* H, int ld, const float* __restrict__ X, int din, int B, int row0, const float* nrm) {
   const int kp = pad32(din);
   for (int e = threadIdx.x; e < kRows * kp; e += blockDim.x) {
     const int r = e / kp, c = e - r * kp;
@@ -43,7 +43,7 @@ __device__ inline void stage_rows(bf16* H, int ld, const float* __restrict__ X, 
 }
 
 // weight image: [o][i] (forward B^T operand) or [i][o] (transposed, backward), zero padded
-__device__ inline void stage_weights(bf16* dst, const float* __restrict__ W, int dout, int din, bool transposed) {
+__device__ inline void stage_weights(lbf* dst, const float* __restrict__ W, int dout, int din, bool transposed) {
   if (!transposed) {
     const int ld = ld_for_k(din), R = pad32(dout), C = pad32(din);
     for (int e = threadIdx.x; e < R * C; e += blockDim.x) {
@@ -65,15 +65,15 @@ __device__ inline float act_apply(int act, float x) { return apply_act(act, x); 
 // (kept for the backward pass), the last layer's (fp32, bias added, identity) outputs to
 // out[row * out_ld + col] for col < dims[L] (<= 16). Wf[l]: pre-staged weight images.
 // Each wave works on its own 16 rows only, so layers need no barrier between them.
-__device__ inline void mlp_forward(const AirlNet& net, bf16* const* Hs, int ld, bf16* const* Wf, float* out, int out_ld) {
+__device__ inline void mlp_forward(const AirlNet& net, lbf* const* Hs, int ld, lbf* const* Wf, lfl* out, int out_ld) {
   const int w = wave_id();
   for (int l = 0; l < net.n_layers; ++l) {
     const int din = net.dims[l], dout = net.dims[l + 1];
-    const bf16* Wimg = Wf[l];
+    const lbf* Wimg = Wf[l];
     const int K = pad32(din), ldw = ld_for_k(din);
     const bool last = l == net.n_layers - 1;
     const int ntiles = last ? 1 : pad32(dout) / 16;
-    const bf16* A = Hs[l] + w * 16 * ld;
+    const lbf* A = Hs[l] + w * 16 * ld;
     for (int nt = 0; nt < ntiles; ++nt) {
       f32x4 acc = mma_16x16(A, ld, Wimg + nt * 16 * ldw, ldw, K, zero4());
       const int col = nt * 16 + acc_col();
@@ -100,8 +100,8 @@ __device__ inline float wave_colsum(float s) {
 // Backward of an MLP (identity output, dout = 1) from per-row output gradients dy[64]:
 // dW / db into slab[param offsets] (acc: add to what an earlier pass of this block wrote).
 // Scratch: HT [feature][row] (ld_ht), dZ [row][k] (ld) and dZT [k][row] (ld_ht), x2.
-__device__ inline void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld, bf16* const* Wt, const float* dy, bf16* HT, int ld_ht,
-                             bf16* const* dZ, bf16* const* dZT, float* dbs, int dmax_pad, float* slab, bool acc_mode) {
+__device__ inline void mlp_backward(const AirlNet& net, lbf* const* Hs, int ld, lbf* const* Wt, const lfl* dy, lbf* HT, int ld_ht,
+                             lbf* const* dZ, lbf* const* dZT, lfl* dbs, int dmax_pad, float* slab, bool acc_mode) {
   const int w = wave_id(), lane = lane_id();
   const int L = net.n_layers;
   // last layer: dZ = dy (identity head, one output column)
@@ -111,7 +111,7 @@ __device__ inline void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld,
     dZ[0][r * ld + c] = to_bf16(v);
     dZT[0][c * ld_ht + r] = to_bf16(v);
   }
-  float* dbs_head = dbs + 2 * kNW * dmax_pad;
+  lfl* dbs_head = dbs + 2 * kNW * dmax_pad;
   if (threadIdx.x == 0) {  // db of the head: fixed-order sum over rows (fp32)
     float s = 0.f;
     for (int r = 0; r < kRows; ++r) s += dy[r];
@@ -165,8 +165,8 @@ __device__ inline void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld,
     // dZ_{l-1} = (dZ_l . W_l) * act'(H_l)
     {
       const int K = pad32(dout), ldw = ld_for_k(dout);
-      const bf16* A = dZ[z] + w * 16 * ld;
-      const bf16* Wimg = Wt[l];
+      const lbf* A = dZ[z] + w * 16 * ld;
+      const lbf* Wimg = Wt[l];
       const int ntiles = pad32(din) / 16;
       for (int nt = 0; nt < ntiles; ++nt) {
         f32x4 accv = mma_16x16(A, ld, Wimg + nt * 16 * ldw, ldw, K, zero4());
@@ -184,7 +184,7 @@ __device__ inline void mlp_backward(const AirlNet& net, bf16* const* Hs, int ld,
         }
         const int r0 = w * 16 + acc_row(0);
         bf16x4 v4 = {to_bf16(dzv[0]), to_bf16(dzv[1]), to_bf16(dzv[2]), to_bf16(dzv[3])};
-        *reinterpret_cast<bf16x4*>(&dZT[z ^ 1][col * ld_ht + r0]) = v4;
+        *(lbf4*)(&dZT[z ^ 1][col * ld_ht + r0]) = v4;
         colsum = wave_colsum(colsum);
         if (lane < 16) dbs[((z ^ 1) * kNW + w) * dmax_pad + col] = colsum;
       }

@@ -25,6 +25,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// LDS-typed (address_space 3) views: images reached through these compile to ds_read /
+// ds_write. A generic pointer into LDS compiles to FLAT accesses, which count in vmcnt as
+// well as lgkmcnt (every LDS wait then also waits for outstanding global memory ops).
+typedef __attribute__((address_space(3))) bf16 lbf;
+typedef __attribute__((address_space(3))) bf16x8 lbf8;
+typedef __attribute__((address_space(3))) bf16x4 lbf4;
+typedef __attribute__((address_space(3))) float lfl;
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
@@ -43,6 +51,21 @@ __device__ __forceinline__ f32x4 mma_16x16(const bf16* a, int lda, const bf16* b
   for (int k = 0; k < K; k += 32) {
     bf16x8 av = *reinterpret_cast<const bf16x8*>(ap + k);
     bf16x8 bv = *reinterpret_cast<const bf16x8*>(bp + k);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// the same on LDS-typed images (ds_read_b128 operands)
+__device__ __forceinline__ f32x4 mma_16x16(const lbf* a, int lda, const lbf* bt, int ldb, int K, f32x4 acc) {
+  const int l = lane_id();
+  const int r = l & 15;
+  const int kq = (l >> 4) * 8;
+  const lbf* ap = a + r * lda + kq;
+  const lbf* bp = bt + r * ldb + kq;
+  for (int k = 0; k < K; k += 32) {
+    bf16x8 av = *(const lbf8*)(ap + k);
+    bf16x8 bv = *(const lbf8*)(bp + k);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
   }
   return acc;

@@ -212,32 +212,31 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
   __shared__ float fl[6][kRows];  // log pi, r, Phi(s'), Phi(s), grads
   __shared__ float heads[kRows][17];
   __shared__ float st_w[kNW][kDiscStats];
-  bf16* Wf[3][kAirlMaxLayers];
-  bf16* Wt[3][kAirlMaxLayers];
+  lbf* Wf[3][kAirlMaxLayers];
+  lbf* Wt[3][kAirlMaxLayers];
   for (int q = 0; q < 3; ++q)
     for (int l = 0; l < kAirlMaxLayers; ++l) {
-      Wf[q][l] = reinterpret_cast<bf16*>(smem + p.wf_off[q][l]);
-      Wt[q][l] = reinterpret_cast<bf16*>(smem + p.wt_off[q][l]);
+      Wf[q][l] = (lbf*)(smem + p.wf_off[q][l]);
+      Wt[q][l] = (lbf*)(smem + p.wt_off[q][l]);
     }
-  bf16* Pimg[2] = {reinterpret_cast<bf16*>(smem + p.scratch_off), reinterpret_cast<bf16*>(smem + p.scratch_off + p.pimg_bytes)};
-  bf16* Bh[kAirlMaxLayers];
-  bf16* Qh[kAirlMaxLayers];
-  bf16* Rh[kAirlMaxLayers];
+  lbf* Pimg[2] = {(lbf*)(smem + p.scratch_off), (lbf*)(smem + p.scratch_off + p.pimg_bytes)};
+  lbf* Bh[kAirlMaxLayers];
+  lbf* Qh[kAirlMaxLayers];
+  lbf* Rh[kAirlMaxLayers];
   {
     const int nb = a.base.n_layers, np = a.pot.n_layers;
     for (int l = 0; l < kAirlMaxLayers; ++l) {
-      Bh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)min(l, nb - 1) * p.rimg_bytes);
-      Qh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)(nb + min(l, np - 1)) * p.rimg_bytes);
-      Rh[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)(nb + np + min(l, np - 1)) * p.rimg_bytes);
+      Bh[l] = (lbf*)(smem + p.rimg_off + (size_t)min(l, nb - 1) * p.rimg_bytes);
+      Qh[l] = (lbf*)(smem + p.rimg_off + (size_t)(nb + min(l, np - 1)) * p.rimg_bytes);
+      Rh[l] = (lbf*)(smem + p.rimg_off + (size_t)(nb + np + min(l, np - 1)) * p.rimg_bytes);
     }
   }
   // backward scratch aliases the policy images (the policy pass is over by then)
   char* sc = smem + p.scratch_off;
-  bf16* HT = reinterpret_cast<bf16*>(sc);
-  bf16* dZ[2] = {reinterpret_cast<bf16*>(sc + p.ht_bytes), reinterpret_cast<bf16*>(sc + p.ht_bytes + p.rimg_bytes)};
-  bf16* dZT[2] = {reinterpret_cast<bf16*>(sc + p.ht_bytes + 2 * p.rimg_bytes),
-                  reinterpret_cast<bf16*>(sc + p.ht_bytes + 2 * p.rimg_bytes + p.ht_bytes)};
-  float* dbs = reinterpret_cast<float*>(sc + 3 * p.ht_bytes + 2 * p.rimg_bytes);
+  lbf* HT = (lbf*)(sc);
+  lbf* dZ[2] = {(lbf*)(sc + p.ht_bytes), (lbf*)(sc + p.ht_bytes + p.rimg_bytes)};
+  lbf* dZT[2] = {(lbf*)(sc + p.ht_bytes + 2 * p.rimg_bytes), (lbf*)(sc + p.ht_bytes + 2 * p.rimg_bytes + p.ht_bytes)};
+  lfl* dbs = (lfl*)(sc + 3 * p.ht_bytes + 2 * p.rimg_bytes);
 
   const int n = 2 * a.mb;
   const int row0 = blockIdx.x * kRows;
@@ -270,12 +269,12 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
     // ping-pong: layer l reads Pimg[l & 1], writes Pimg[(l + 1) & 1]
     for (int l = 0; l < pn.n_layers; ++l) {
       const int din = pn.dims[l], dout = pn.dims[l + 1];
-      const bf16* Wimg = Wf[0][l];
+      const lbf* Wimg = Wf[0][l];
       const int K = pad32(din), ldw = ld_for_k(din);
       const bool last = l == pn.n_layers - 1;
       const int ntiles = last ? 1 : pad32(dout) / 16;
-      const bf16* A = Pimg[l & 1] + w * 16 * p.ldp;
-      bf16* O = Pimg[(l + 1) & 1];
+      const lbf* A = Pimg[l & 1] + w * 16 * p.ldp;
+      lbf* O = Pimg[(l + 1) & 1];
       for (int nt = 0; nt < ntiles; ++nt) {
         f32x4 acc = mma_16x16(A, p.ldp, Wimg + nt * 16 * ldw, ldw, K, zero4());
         const int col = nt * 16 + acc_col();
@@ -315,9 +314,9 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
 
   unsigned long long t_2 = stamp ? clock64() : 0;
   // ---- reward nets forward: base r, potential Phi(s'), Phi(s)
-  mlp_forward(a.base, Bh, p.ldr, Wf[1], &fl[1][0], 1);
-  mlp_forward(a.pot, Qh, p.ldr, Wf[2], &fl[2][0], 1);
-  mlp_forward(a.pot, Rh, p.ldr, Wf[2], &fl[3][0], 1);
+  mlp_forward(a.base, Bh, p.ldr, Wf[1], (lfl*)&fl[1][0], 1);
+  mlp_forward(a.pot, Qh, p.ldr, Wf[2], (lfl*)&fl[2][0], 1);
+  mlp_forward(a.pot, Rh, p.ldr, Wf[2], (lfl*)&fl[3][0], 1);
   __syncthreads();
 
   unsigned long long t_3 = stamp ? clock64() : 0;
@@ -363,10 +362,10 @@ __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, 
   unsigned long long t_4 = stamp ? clock64() : 0;
   // ---- backward: base, potential on s' (writes), potential on s (adds)
   float* slab_row = a.slab + ((size_t)k * gridDim.x + blockIdx.x) * a.n_params;
-  mlp_backward(a.base, Bh, p.ldr, Wt[1], &fl[4][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
-  mlp_backward(a.pot, Qh, p.ldr, Wt[2], &fl[5][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
+  mlp_backward(a.base, Bh, p.ldr, Wt[1], (const lfl*)&fl[4][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
+  mlp_backward(a.pot, Qh, p.ldr, Wt[2], (const lfl*)&fl[5][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, false);
   unsigned long long t_5 = stamp ? clock64() : 0;
-  mlp_backward(a.pot, Rh, p.ldr, Wt[2], &fl[1][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, true);
+  mlp_backward(a.pot, Rh, p.ldr, Wt[2], (const lfl*)&fl[1][0], HT, p.ld_ht, dZ, dZT, dbs, p.dmax_pad, slab_row, true);
   if (stamp) {
     const unsigned long long t_6 = clock64();
     a.prof[0] += t_1 - t_0;  // zero + stage

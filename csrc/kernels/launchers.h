@@ -263,6 +263,24 @@ struct CnnHeadArgs {
 };
 hipError_t cnn_head(const CnnHeadArgs& a, hipStream_t s);
 
+// ---- bc_head.hip: categorical BC head (logits, loss metrics, dW / db / dh) + ||theta||^2 in
+// one launch (B <= 64, NH % 64 == 0 and <= 512, A <= 18)
+struct BcHeadArgs {
+  const float *h, *W, *b;   // features [B, NH] (16-B aligned), head weight [A, NH] (16-B aligned), bias [A]
+  const int64_t* acts;      // [B]
+  int B, NH, A;
+  float ent_w, l2_w;
+  const float* params;      // flat parameter bucket (16-B aligned), n_params floats
+  long n_params;
+  float *dW, *db, *dh;      // gradient slots (written, not accumulated), dh [B, NH]
+  float* metrics;           // [7]: neglogp, entropy, ent_loss, prob_true_act, l2_norm, l2_loss, loss
+  float* partials;          // [bc_head_sumsq_blocks(n_params)]
+  unsigned* cnt;            // zero-initialised hand-off counter (left zero)
+};
+bool bc_head_ok(int B, int NH, int A);
+int bc_head_sumsq_blocks(long n_params);
+hipError_t bc_head_train(const BcHeadArgs& a, hipStream_t s);
+
 // ---- optim.hip: fused Adam / AdamW over a flat fp32 buffer
 struct AdamArgs {
   float *params, *grads, *exp_avg, *exp_avg_sq;
@@ -299,8 +317,10 @@ hipError_t bc_cat_loss_bwd(const float* z, const int64_t* act, int B, int A, con
 bool running_norm_ok(int B, int D);
 // ws: running_norm_ws_floats(B, D) floats (multi-workgroup path for large B; nullptr -> one workgroup)
 size_t running_norm_ws_floats(int B, int D);
+// ema_inv_lr / ema_num_batches (both or neither): EMANorm's merge with decay ema_decay
 hipError_t running_norm(const float* x, int B, int D, float* mean, float* var, int* count, float eps, int update, float* y,
-                        float* ws, hipStream_t s);
+                        float* ws, hipStream_t s, float* ema_inv_lr = nullptr, int* ema_num_batches = nullptr,
+                        float ema_decay = 0.f);
 
 // ---- gather.hip: one-launch multi-field row gather (row r <- source row b[r] * n_envs + e[r],
 // or b[r] when e == nullptr)

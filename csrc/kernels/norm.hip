@@ -1,4 +1,5 @@
-// RunningNorm (reference util/networks.py:80-134) update + normalise in ONE launch.
+// RunningNorm / EMANorm (reference util/networks.py:80-201) update + normalise in
+// ONE launch (EMANorm: same batch moments, exponential-moving-average merge).
 //
 // In training mode every RunningNorm forward merges the batch moments into the running
 // statistics (Chan et al.) and then normalises: in torch that is mean, var, ~12 elementwise
@@ -16,6 +17,43 @@
 namespace ia {
 namespace {
 
+// EMANorm state (networks.py EMANorm.update_stats): the learning rate of this update is
+// 1 / (inv_lr + decay^num_batches); null -> RunningNorm's Chan merge.
+struct EmaState {
+  float* inv_lr;
+  int* num_batches;
+  float decay;
+};
+
+__device__ __forceinline__ float ema_lr(const EmaState& e) {
+  return 1.f / (e.inv_lr[0] + powf(e.decay, (float)e.num_batches[0]));
+}
+
+// merge one feature's batch moments (mean bm, biased var bv over bc rows) into the running
+// statistics: Chan (RunningNorm) or the exponential moving average (EMANorm)
+__device__ __forceinline__ void merge_stats(float* mean, float* var, int ff, float bm, float bv, float bc, float n_old,
+                                            bool ema, float lr) {
+  const float rm = mean[ff], rv = var[ff];
+  const float delta = bm - rm;
+  if (ema) {
+    mean[ff] = rm + lr * delta;
+    var[ff] = rv + lr * (bv + (1.f - lr) * delta * delta - rv);
+  } else {
+    const float tot = n_old + bc;
+    mean[ff] = rm + delta * bc / tot;
+    var[ff] = (rv * n_old + bv * bc + delta * delta * n_old * bc / tot) / tot;
+  }
+}
+
+// count (+ the EMA's inverse learning rate and batch counter) after every lane merged
+__device__ __forceinline__ void advance_counts(int* count, int B, const EmaState& e, bool ema) {
+  count[0] = count[0] + B;
+  if (ema) {
+    e.inv_lr[0] = e.inv_lr[0] + powf(e.decay, (float)e.num_batches[0]);
+    e.num_batches[0] = e.num_batches[0] + 1;
+  }
+}
+
 // One workgroup. Features are processed 64 (or fewer: Dp = next power of two >= D) at a time
 // with 256 / Dp row groups per feature, so a narrow batch (the reward output norm: D = 1,
 // thousands of rows) still uses all 256 lanes. Two passes over the rows (sum -> mean, then
@@ -23,10 +61,12 @@ namespace {
 __global__ __launch_bounds__(256) void running_norm_kernel(const float* __restrict__ x, int B, int D,
                                                            float* __restrict__ mean, float* __restrict__ var,
                                                            int* __restrict__ count, float eps, int update,
-                                                           float* __restrict__ y) {
+                                                           float* __restrict__ y, EmaState ema_st) {
   __shared__ float red[256];
   __shared__ float s_mean[256], s_rstd[256];
   const int tid = threadIdx.x;
+  const bool ema = ema_st.inv_lr != nullptr;
+  const float lr = (update && ema) ? ema_lr(ema_st) : 0.f;
   int Dp = 1;
   while (Dp < D && Dp < 64) Dp <<= 1;
   const int G = 256 / Dp, f = tid % Dp, g = tid / Dp;
@@ -77,11 +117,7 @@ __global__ __launch_bounds__(256) void running_norm_kernel(const float* __restri
       if (g == 0 && ff < D) {
         float t = 0.f;
         for (int q = 0; q < G; ++q) t += red[q * Dp + f];
-        const float bv = t / (float)B, bc = (float)B;
-        const float rm = mean[ff], rv = var[ff];
-        const float delta = bm - rm, tot = n_old + bc;
-        mean[ff] = rm + delta * bc / tot;
-        var[ff] = (rv * n_old + bv * bc + delta * delta * n_old * bc / tot) / tot;
+        merge_stats(mean, var, ff, bm, t / (float)B, (float)B, n_old, ema, lr);
       }
       __syncthreads();
     }
@@ -92,7 +128,7 @@ __global__ __launch_bounds__(256) void running_norm_kernel(const float* __restri
     s_rstd[ff] = 1.f / sqrtf(var[ff] + eps);
   }
   __syncthreads();
-  if (update && tid == 0) count[0] = count[0] + B;
+  if (update && tid == 0) advance_counts(count, B, ema_st, ema);
   if (!y) return;
   const int total = B * D;
   for (int i = tid; i < total; i += 256) {
@@ -158,11 +194,13 @@ __global__ __launch_bounds__(256) void running_norm_partial_kernel(const float* 
 
 __global__ __launch_bounds__(256) void running_norm_merge_kernel(const float* __restrict__ part, int nb, int rpb, int B,
                                                                  int D, float* __restrict__ mean, float* __restrict__ var,
-                                                                 int* __restrict__ count) {
+                                                                 int* __restrict__ count, EmaState ema_st) {
   // the partials of a feature chunk are staged in LDS by all lanes at once (the serial merge
   // chain then reads LDS, not dependent global loads)
   __shared__ float sp[8192];
   const float n_old = (float)count[0];
+  const bool ema = ema_st.inv_lr != nullptr;
+  const float lr = ema ? ema_lr(ema_st) : 0.f;
   const int fc = min(D, (int)(8192 / (2 * nb)));
   for (int f0 = 0; f0 < D; f0 += fc) {
     const int nf = min(fc, D - f0);
@@ -183,16 +221,11 @@ __global__ __launch_bounds__(256) void running_norm_merge_kernel(const float* __
         m2 += m2b + delta * delta * n * nbf / nn;
         n = nn;
       }
-      const int ff = f0 + k;
-      const float bv = m2 / (float)B, bc = (float)B;
-      const float rm = mean[ff], rv = var[ff];
-      const float delta = m - rm, tot = n_old + bc;
-      mean[ff] = rm + delta * bc / tot;
-      var[ff] = (rv * n_old + bv * bc + delta * delta * n_old * bc / tot) / tot;
+      merge_stats(mean, var, f0 + k, m, m2 / (float)B, (float)B, n_old, ema, lr);
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) count[0] = count[0] + B;
+  if (threadIdx.x == 0) advance_counts(count, B, ema_st, ema);
 }
 
 __global__ __launch_bounds__(256) void running_norm_apply_kernel(const float* __restrict__ x, int B, int D, int rpb,
@@ -223,16 +256,18 @@ size_t running_norm_ws_floats(int B, int D) {
 }
 
 hipError_t running_norm(const float* x, int B, int D, float* mean, float* var, int* count, float eps, int update, float* y,
-                        float* ws, hipStream_t s) {
+                        float* ws, hipStream_t s, float* ema_inv_lr, int* ema_num_batches, float ema_decay) {
   if (!running_norm_ok(B, D)) return hipErrorInvalidValue;
+  if ((ema_inv_lr == nullptr) != (ema_num_batches == nullptr)) return hipErrorInvalidValue;
+  const EmaState ema{ema_inv_lr, ema_num_batches, ema_decay};
   const int nb = running_norm_blocks(B);
   if (nb <= 1 || !update || !ws) {
-    hipLaunchKernelGGL(running_norm_kernel, dim3(1), dim3(256), 0, s, x, B, D, mean, var, count, eps, update, y);
+    hipLaunchKernelGGL(running_norm_kernel, dim3(1), dim3(256), 0, s, x, B, D, mean, var, count, eps, update, y, ema);
     return hipGetLastError();
   }
   const int rpb = (B + nb - 1) / nb;
   hipLaunchKernelGGL(running_norm_partial_kernel, dim3(nb), dim3(256), 0, s, x, B, D, rpb, ws);
-  hipLaunchKernelGGL(running_norm_merge_kernel, dim3(1), dim3(256), 0, s, ws, nb, rpb, B, D, mean, var, count);
+  hipLaunchKernelGGL(running_norm_merge_kernel, dim3(1), dim3(256), 0, s, ws, nb, rpb, B, D, mean, var, count, ema);
   if (y) hipLaunchKernelGGL(running_norm_apply_kernel, dim3(nb), dim3(256), 0, s, x, B, D, rpb, mean, var, eps, y);
   return hipGetLastError();
 }

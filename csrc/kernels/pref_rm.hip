@@ -169,29 +169,29 @@ __global__ __launch_bounds__(256) void pref_gather_kernel(PrefRmArgs a) {
 
 // LDS layout of pref_fwd / pref_bwd (PrefPlan): weight images, row images, backward scratch
 struct Imgs {
-  bf16* Wf[kAirlMaxLayers];
-  bf16* Wt[kAirlMaxLayers];
-  bf16* H[kAirlMaxLayers];
-  bf16* HT;
-  bf16* dZ[2];
-  bf16* dZT[2];
-  float* dbs;
+  lbf* Wf[kAirlMaxLayers];
+  lbf* Wt[kAirlMaxLayers];
+  lbf* H[kAirlMaxLayers];
+  lbf* HT;
+  lbf* dZ[2];
+  lbf* dZT[2];
+  lfl* dbs;
 };
 
 __device__ __forceinline__ Imgs carve(char* smem, const PrefPlan& p, int n_layers) {
   Imgs m;
   for (int l = 0; l < kAirlMaxLayers; ++l) {
-    m.Wf[l] = reinterpret_cast<bf16*>(smem + p.wf_off[l]);
-    m.Wt[l] = reinterpret_cast<bf16*>(smem + p.wt_off[l]);
-    m.H[l] = reinterpret_cast<bf16*>(smem + p.rimg_off + (size_t)min(l, n_layers - 1) * p.rimg_bytes);
+    m.Wf[l] = (lbf*)(smem + p.wf_off[l]);
+    m.Wt[l] = (lbf*)(smem + p.wt_off[l]);
+    m.H[l] = (lbf*)(smem + p.rimg_off + (size_t)min(l, n_layers - 1) * p.rimg_bytes);
   }
   char* sc = smem + p.scratch_off;
-  m.HT = reinterpret_cast<bf16*>(sc);
-  m.dZ[0] = reinterpret_cast<bf16*>(sc + p.ht_bytes);
-  m.dZ[1] = reinterpret_cast<bf16*>(sc + p.ht_bytes + p.rimg_bytes);
-  m.dZT[0] = reinterpret_cast<bf16*>(sc + p.ht_bytes + 2 * p.rimg_bytes);
-  m.dZT[1] = reinterpret_cast<bf16*>(sc + 2 * p.ht_bytes + 2 * p.rimg_bytes);
-  m.dbs = reinterpret_cast<float*>(sc + 3 * p.ht_bytes + 2 * p.rimg_bytes);
+  m.HT = (lbf*)(sc);
+  m.dZ[0] = (lbf*)(sc + p.ht_bytes);
+  m.dZ[1] = (lbf*)(sc + p.ht_bytes + p.rimg_bytes);
+  m.dZT[0] = (lbf*)(sc + p.ht_bytes + 2 * p.rimg_bytes);
+  m.dZT[1] = (lbf*)(sc + 2 * p.ht_bytes + 2 * p.rimg_bytes);
+  m.dbs = (lfl*)(sc + 3 * p.ht_bytes + 2 * p.rimg_bytes);
   return m;
 }
 
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(64 * kNW) void pref_fwd_kernel(PrefRmArgs a, PrefPl
   for (int l = 0; l < a.net.n_layers; ++l) stage_weights(m.Wf[l], a.net.W[l], a.net.dims[l + 1], a.net.dims[l], false);
   stage_rows(m.H[0], p.ldr, a.X, a.din, rows, row0, nrm);
   __syncthreads();
-  mlp_forward(a.net, m.H, p.ldr, m.Wf, out, 1);
+  mlp_forward(a.net, m.H, p.ldr, m.Wf, (lfl*)out, 1);
   __syncthreads();
   if (threadIdx.x < kRows && row0 + (int)threadIdx.x < rows) a.r[row0 + threadIdx.x] = out[threadIdx.x];
 }
@@ -331,9 +331,9 @@ __global__ __launch_bounds__(64 * kNW) void pref_bwd_kernel(PrefRmArgs a, PrefPl
     dy[threadIdx.x] = g;
   }
   __syncthreads();
-  mlp_forward(net, m.H, p.ldr, m.Wf, out, 1);  // hidden images for the backward
+  mlp_forward(net, m.H, p.ldr, m.Wf, (lfl*)out, 1);  // hidden images for the backward
   float* slab_row = a.slab + (size_t)blockIdx.x * a.n_params;
-  mlp_backward(net, m.H, p.ldr, m.Wt, dy, m.HT, p.ld_ht, m.dZ, m.dZT, m.dbs, p.dmax_pad, slab_row, false);
+  mlp_backward(net, m.H, p.ldr, m.Wt, (const lfl*)dy, m.HT, p.ld_ht, m.dZ, m.dZT, m.dbs, p.dmax_pad, slab_row, false);
 }
 
 __global__ void pref_epoch_end_kernel(const float* __restrict__ metrics, float* __restrict__ all, int n, int* cursor) {

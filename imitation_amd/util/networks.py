@@ -144,7 +144,13 @@ class RunningNorm(BaseNorm):
 
 
 class EMANorm(BaseNorm):
-    """Exponentially-weighted running normaliser (``networks.py:137-201``)."""
+    """Exponentially-weighted running normaliser (``networks.py:137-201``).
+
+    On the GPU (2-D fp32 batches, no DP statistics sync) the update and the normalisation run
+    on the RunningNorm kernels (``csrc/kernels/norm.hip``) in their EMA merge mode: the same
+    batch moments, then ``lr = 1 / (inv_lr + decay^num_batches)`` and the moving-average
+    update of mean / var, the count, ``inv_learning_rate`` and ``num_batches`` advanced on the
+    device -- one launch (three for large batches) instead of ~25 elementwise kernels."""
 
     inv_learning_rate: th.Tensor
     num_batches: th.IntTensor
@@ -163,10 +169,27 @@ class EMANorm(BaseNorm):
         self.inv_learning_rate.zero_()
         self.num_batches.zero_()
 
+    def _fused_ok(self, x: th.Tensor) -> bool:
+        return RunningNorm._fused_ok(self, x) and self.num_batches.dtype == th.int32 and self.inv_learning_rate.dtype == th.float32
+
+    def _native(self, x: th.Tensor, update: bool, want_y: bool):
+        from imitation_amd import ops
+
+        return ops.native().running_norm(x.contiguous(), self.running_mean, self.running_var, self.count, float(self.eps),
+                                         update, want_y, self.inv_learning_rate, self.num_batches, float(self.decay))
+
+    def forward(self, x: th.Tensor) -> th.Tensor:
+        if self._fused_ok(x) and not (x.requires_grad and th.is_grad_enabled()):
+            return self._native(x, bool(self.training), True)
+        return super().forward(x)
+
     def update_stats(self, batch: th.Tensor) -> None:
         b_size = batch.shape[0]
         if len(batch.shape) == 1:
             batch = batch.reshape(b_size, 1)
+        if self._fused_ok(batch):
+            self._native(batch.detach(), True, False)
+            return
         self.inv_learning_rate += self.decay**self.num_batches
         learning_rate = 1 / self.inv_learning_rate
         batch_mean, batch_var, b_size = _global_batch_moments(batch)

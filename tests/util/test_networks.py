@@ -117,3 +117,29 @@ def test_running_norm_fused_kernel_matches_torch(B, D):
     a.eval()
     x = th.randn(B, D, generator=g).cuda()
     th.testing.assert_close(a(x), (x - a.running_mean) / th.sqrt(a.running_var + a.eps), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,D,decay", [(4096, 17, 0.99), (1, 3, 0.9), (300, 65, 0.5), (40000, 5, 0.99)])
+def test_ema_norm_fused_kernel_matches_torch(B, D, decay):
+    """EMANorm on the norm kernel's EMA merge mode == the module's torch update (CPU copy)."""
+    import torch as th
+
+    from imitation_amd.util.networks import EMANorm
+
+    g = th.Generator().manual_seed(B + D)
+    a, b = EMANorm(D, decay=decay).cuda(), EMANorm(D, decay=decay)
+    for step in range(4):
+        x = th.randn(B, D, generator=g) * 3 + step
+        xa = x.cuda()
+        assert a._fused_ok(xa)
+        ya = a(xa)
+        yb = b(x)  # CPU: the reference update rule
+        th.testing.assert_close(a.running_mean.cpu(), b.running_mean, rtol=1e-5, atol=1e-5)
+        th.testing.assert_close(a.running_var.cpu(), b.running_var, rtol=1e-4, atol=1e-5)
+        th.testing.assert_close(a.inv_learning_rate.cpu(), b.inv_learning_rate, rtol=1e-6, atol=1e-6)
+        assert int(a.count) == int(b.count) and int(a.num_batches) == int(b.num_batches) == step + 1
+        th.testing.assert_close(ya.cpu(), yb, rtol=1e-4, atol=1e-4)
+    a.eval()
+    x = th.randn(B, D, generator=g).cuda()
+    th.testing.assert_close(a(x), (x - a.running_mean) / th.sqrt(a.running_var + a.eps), rtol=1e-5, atol=1e-5)
