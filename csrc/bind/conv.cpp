@@ -74,7 +74,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor wb, c10::optional<torch::T
 
 // (dW fp32 [N][C][KH][KW] (torch layout), db fp32 [N]); dZ = dy * [y > 0] if relu_out
 py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t KH, int64_t KW, int64_t stride,
-                     double in_scale, bool relu_out, int64_t pad) {
+                     double in_scale, bool relu_out, int64_t pad, c10::optional<torch::Tensor> dW_out,
+                     c10::optional<torch::Tensor> db_out) {
   IA_CHECK_CUDA(x);
   IA_CHECK_CONTIG(x);
   IA_CHECK_CUDA(dy);
@@ -89,8 +90,25 @@ py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t
   }
   auto f32 = x.options().dtype(torch::kFloat32);
   auto slab = torch::empty({(int64_t)ia::conv_wgrad_slab_floats(g)}, f32);
-  auto dW = torch::empty({g.N, g.C, g.KH, g.KW}, f32);  // torch layout, written by the reduction
-  auto db = torch::empty({g.N}, f32);
+  // torch layout, written by the reduction (optionally straight into caller slots, e.g. views
+  // of an optimizer's flat gradient bucket)
+  torch::Tensor dW, db;
+  if (dW_out && dW_out->defined()) {
+    IA_CHECK_GPU_F32(*dW_out);
+    IA_CHECK_CONTIG(*dW_out);
+    TORCH_CHECK(dW_out->numel() == (int64_t)g.N * g.C * g.KH * g.KW, "conv_wgrad: dW_out size");
+    dW = *dW_out;
+  } else {
+    dW = torch::empty({g.N, g.C, g.KH, g.KW}, f32);
+  }
+  if (db_out && db_out->defined()) {
+    IA_CHECK_GPU_F32(*db_out);
+    IA_CHECK_CONTIG(*db_out);
+    TORCH_CHECK(db_out->numel() == g.N, "conv_wgrad: db_out size");
+    db = *db_out;
+  } else {
+    db = torch::empty({g.N}, f32);
+  }
   IA_HIP_CHECK3(ia::conv_wgrad(in_kind(x), x.data_ptr(), dy.data_ptr(), relu_out ? y.data_ptr() : nullptr,
                                slab.data_ptr<float>(), dW.data_ptr<float>(), db.data_ptr<float>(), g, (float)in_scale,
                                relu_out ? 1 : 0, ia_stream()));
@@ -176,7 +194,8 @@ torch::Tensor cnn_fc(torch::Tensor x, torch::Tensor w, torch::Tensor b) {
 
 // Linear + ReLU backward over the NHWC-flattened conv output: (dW fp32 [NH, C*HW] torch (c, h, w)
 // columns, db fp32 [NH], dX bf16 [M, K] or None)
-py::tuple fc_backward(torch::Tensor x, torch::Tensor dh, torch::Tensor h, torch::Tensor wt, int64_t C, bool need_dx) {
+py::tuple fc_backward(torch::Tensor x, torch::Tensor dh, torch::Tensor h, torch::Tensor wt, int64_t C, bool need_dx,
+                      c10::optional<torch::Tensor> dW_out, c10::optional<torch::Tensor> db_out) {
   IA_CHECK_CUDA(x);
   IA_CHECK_CONTIG(x);
   IA_CHECK_CUDA(wt);
@@ -191,8 +210,23 @@ py::tuple fc_backward(torch::Tensor x, torch::Tensor dh, torch::Tensor h, torch:
   TORCH_CHECK(h.dim() == 2 && h.size(0) == M && dhc.sizes() == h.sizes() && wt.numel() == K * NH && C > 0 && K % C == 0,
               "fc_backward: shapes");
   TORCH_CHECK(ia::fc_train_ok(M, (int)K, NH, (int)C, (int)(K / C)), "fc_backward: K % 64, NH % 64");
-  auto dW = torch::empty({NH, K}, h.options());
-  auto db = torch::empty({NH}, h.options());
+  torch::Tensor dW, db;
+  if (dW_out && dW_out->defined()) {
+    IA_CHECK_GPU_F32(*dW_out);
+    IA_CHECK_CONTIG(*dW_out);
+    TORCH_CHECK(dW_out->numel() == (int64_t)NH * K, "fc_backward: dW_out size");
+    dW = *dW_out;
+  } else {
+    dW = torch::empty({NH, K}, h.options());
+  }
+  if (db_out && db_out->defined()) {
+    IA_CHECK_GPU_F32(*db_out);
+    IA_CHECK_CONTIG(*db_out);
+    TORCH_CHECK(db_out->numel() == NH, "fc_backward: db_out size");
+    db = *db_out;
+  } else {
+    db = torch::empty({NH}, h.options());
+  }
   torch::Tensor dx;
   if (need_dx) dx = torch::empty({M, K}, x.options());
   auto dzb = torch::empty({M, NH}, x.options());  // bf16 dZ, fc_wgrad -> fc_dgrad
@@ -303,10 +337,12 @@ void register_conv(py::module& m) {
   m.def("cnn_fc_pair", &cnn_fc_pair, "two same-shape cnn_fc layers in one launch");
   m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts, one launch", py::arg("ws"),
         py::arg("want_t"), py::arg("t_hwc") = std::vector<bool>{});
-  m.def("fc_backward", &fc_backward, "NatureCNN feature-layer backward (dW torch layout, db, dX NHWC bf16)");
+  m.def("fc_backward", &fc_backward, "NatureCNN feature-layer backward (dW torch layout, db, dX NHWC bf16)", py::arg("x"),
+        py::arg("dh"), py::arg("h"), py::arg("wt"), py::arg("C"), py::arg("need_dx"), py::arg("dW_out") = py::none(),
+        py::arg("db_out") = py::none());
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
-        py::arg("relu_out"), py::arg("pad") = 0);
+        py::arg("relu_out"), py::arg("pad") = 0, py::arg("dW_out") = py::none(), py::arg("db_out") = py::none());
   m.def("conv_dgrad", &conv_dgrad, "NHWC conv data gradient with fused ReLU masks", py::arg("dy"), py::arg("y"),
         py::arg("wt"), py::arg("xp"), py::arg("stride"), py::arg("relu_out"), py::arg("relu_in"), py::arg("pad") = 0);
 }

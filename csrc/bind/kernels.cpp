@@ -437,6 +437,50 @@ py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, 
   return want_y ? py::cast(y) : py::none();
 }
 
+// Categorical BC head of a CNN policy, fused (bc_head.hip): metrics [7] (BC_METRICS order)
+// into `metrics`, dW / db into the gradient slots (written), dh [B, NH] returned.
+torch::Tensor bc_head_train(torch::Tensor h, torch::Tensor W, torch::Tensor b, torch::Tensor acts, torch::Tensor params,
+                            torch::Tensor dW, torch::Tensor db, torch::Tensor metrics, torch::Tensor ws, double ent_w,
+                            double l2_w) {
+  for (auto* t : {&h, &W, &b, &params, &dW, &db, &metrics, &ws}) {
+    IA_CHECK_GPU_F32((*t));
+    IA_CHECK_CONTIG((*t));
+  }
+  IA_CHECK_CUDA(acts);
+  TORCH_CHECK(acts.scalar_type() == torch::kInt64 && acts.is_contiguous(), "bc_head_train: int64 actions");
+  TORCH_CHECK(h.dim() == 2 && W.dim() == 2 && W.size(1) == h.size(1) && b.numel() == W.size(0) &&
+                  acts.numel() == h.size(0) && dW.numel() == W.numel() && db.numel() == b.numel() && metrics.numel() >= 7,
+              "bc_head_train: shapes");
+  const int B = (int)h.size(0), NH = (int)h.size(1), A = (int)W.size(0);
+  TORCH_CHECK(ia::bc_head_ok(B, NH, A), "bc_head_train: B <= 64, NH % 64 == 0 and <= 512, A <= 18");
+  const long n = (long)params.numel();
+  const int nb = ia::bc_head_sumsq_blocks(n);
+  TORCH_CHECK(ws.numel() >= nb + 1, "bc_head_train: workspace of bc_head_workspace(n_params) floats");
+  TORCH_CHECK(((uintptr_t)h.data_ptr() | (uintptr_t)W.data_ptr() | (uintptr_t)params.data_ptr()) % 16 == 0,
+              "bc_head_train: h / W / params 16-B aligned");
+  auto dh = torch::empty_like(h);
+  ia::BcHeadArgs a{};
+  a.h = h.data_ptr<float>();
+  a.W = W.data_ptr<float>();
+  a.b = b.data_ptr<float>();
+  a.acts = acts.data_ptr<int64_t>();
+  a.B = B;
+  a.NH = NH;
+  a.A = A;
+  a.ent_w = (float)ent_w;
+  a.l2_w = (float)l2_w;
+  a.params = params.data_ptr<float>();
+  a.n_params = n;
+  a.dW = dW.data_ptr<float>();
+  a.db = db.data_ptr<float>();
+  a.dh = dh.data_ptr<float>();
+  a.metrics = metrics.data_ptr<float>();
+  a.cnt = reinterpret_cast<unsigned*>(ws.data_ptr<float>());  // word 0: counter (zeroed by the caller once)
+  a.partials = ws.data_ptr<float>() + 1;
+  IA_HIP_CHECK(ia::bc_head_train(a, ia_stream()));
+  return dh;
+}
+
 // [E, n] int32: row e is a pseudo-random permutation of 0..n-1 keyed by (seed, e).
 torch::Tensor random_permutations(int64_t E, int64_t n, int64_t seed, torch::Device device) {
   TORCH_CHECK(device.is_cuda(), "random_permutations runs on the GPU");
@@ -510,6 +554,9 @@ void register_kernels(py::module& m) {
         py::arg("l2_w"));
   m.def("bc_cat_loss_bwd", &bc_cat_loss_bwd, py::arg("z"), py::arg("acts"), py::arg("g"), py::arg("g_loss"),
         py::arg("ent_w"));
+  m.def("bc_head_train", &bc_head_train, py::arg("h"), py::arg("W"), py::arg("b"), py::arg("acts"), py::arg("params"),
+        py::arg("dW"), py::arg("db"), py::arg("metrics"), py::arg("ws"), py::arg("ent_w"), py::arg("l2_w"));
+  m.def("bc_head_workspace", [](int64_t n) { return (int64_t)ia::bc_head_sumsq_blocks((long)n) + 1; });
   m.def("cat_eval_fwd", &cat_eval_fwd, py::arg("z"), py::arg("acts"));
   m.def("cat_eval_bwd", &cat_eval_bwd, py::arg("z"), py::arg("acts"), py::arg("g_lp"), py::arg("g_ent"));
 }

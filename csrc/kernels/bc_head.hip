@@ -1,0 +1,274 @@
+// Fused BC training head of a categorical CNN policy (DAgger-Pong's NatureCNN learner).
+//
+// The reference's BC minibatch (src/imitation/algorithms/bc.py:443-510: evaluate_actions,
+// -log_prob.mean(), entropy bonus, ||theta||^2 / 2 metric, loss.backward()) spends, after the
+// conv trunk and the 512-unit feature layer, ~10 small launches on the action head: the head
+// GEMM, the loss forward / backward, the parameter-norm reduction, three GEMM / reduce
+// launches for dW / db / dh and the gradient copies. Here ONE launch does all of it:
+//
+//   head blocks   : NH / 64, block c owns feature columns [64 c, 64 c + 64): W^T staged in
+//                   LDS, the logits of every row (recomputed per block: no grid-wide step
+//                   between the softmax and the gradients), per row the log-softmax, entropy
+//                   and dL/dlogits; its columns of dW = dlog^T h (straight into the optimizer's
+//                   gradient bucket) and dh = dlog W (the feature layer's upstream gradient,
+//                   ReLU mask left to fc_backward); block 0 also db and the loss metrics;
+//   sumsq blocks  : sum of squares of the flat parameter bucket (the logged l2_norm);
+//   last block    : (agent-scope counter) reduces the nS partials in block order and finishes
+//                   l2_norm / l2_loss / loss; resets the counter (graph replays).
+//
+// Every reduction has a fixed order, so the step is bitwise reproducible.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "launchers.h"
+
+namespace ia {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxB = 64;
+constexpr int kMaxNH = 512;
+constexpr int kMaxA = 18;  // the full Atari action set
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// Head blocks: NH / 64 of them, block c owning feature columns [64 c, 64 c + 64). Each
+// recomputes the (tiny) logits of all B rows -- 4 waves x 8 rows, a lane 8 contiguous
+// features, partials reduced through LDS in a fixed order -- so no grid-wide dependency
+// separates the softmax from the gradients; then its columns of dW and dh.
+constexpr int kAPad = 8;  // logits row stride for A <= 8 (wider heads: kMaxA)
+
+__global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, int n_head) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ float red[4];
+  __shared__ int is_last;
+  const int tid = threadIdx.x;
+  const int ap = a.A <= kAPad ? kAPad : kMaxA;
+  if ((int)blockIdx.x < n_head) {
+    float* wt = sm;                  // [NH][ap]  W transposed (feature-major)
+    float* part = wt + a.NH * ap;    // [4 waves][8 rows][ap][64 lanes] logit partials
+    float* lg = part + 4 * 8 * ap * 64;  // [B][ap] logits, then dL/dlogits
+    float* pw = lg + kMaxB * ap;     // [4 row groups][ap][64] dW partials
+    float* rowm = pw + 4 * ap * 64;  // [B][3]
+    for (int e = tid; e < a.A * a.NH; e += kThreads) {
+      const int j = e / a.NH, k = e - j * a.NH;
+      wt[k * ap + j] = a.W[e];
+    }
+    __syncthreads();
+    const int w = tid >> 6, lane = tid & 63;
+    const int kpl = a.NH >> 6;  // contiguous features per lane
+    for (int r0 = 0; r0 < a.B; r0 += 32) {  // 32 rows per pass (B <= 64)
+      // ---- logit partials: wave w rows r0 + w + 4 q (q < 8), lane features [lane kpl, +kpl)
+      for (int q = 0; q < 8; ++q) {
+        const int r = r0 + w + 4 * q;
+        float acc[kMaxA];
+#pragma unroll
+        for (int j = 0; j < kMaxA; ++j) acc[j] = 0.f;
+        if (r < a.B) {
+          const float* hr = a.h + (size_t)r * a.NH + lane * kpl;
+          for (int i = 0; i < kpl; i += 4) {
+            const float4 hv = *reinterpret_cast<const float4*>(hr + i);
+            const float hx[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float* wk = wt + (lane * kpl + i + u) * ap;
+#pragma unroll
+              for (int j = 0; j < kMaxA; ++j)
+                if (j < ap) acc[j] = fmaf(hx[u], wk[j], acc[j]);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kMaxA; ++j)
+          if (j < ap) part[((w * 8 + q) * ap + j) * 64 + lane] = acc[j];
+      }
+      __syncthreads();
+      // ---- reduce: thread -> (row, action) pairs, 64 lane partials in order
+      for (int pr = tid; pr < 32 * ap; pr += kThreads) {
+        const int rl = pr / ap, j = pr - rl * ap;  // rl = w + 4 q
+        const int ww = rl & 3, q = rl >> 2;
+        const float4* src = reinterpret_cast<const float4*>(part + ((ww * 8 + q) * ap + j) * 64);
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const float4 x = src[v];
+          s0 += x.x;
+          s1 += x.y;
+          s2 += x.z;
+          s3 += x.w;
+        }
+        const int r = r0 + rl;
+        if (r < a.B && j < a.A) lg[r * ap + j] = ((s0 + s1) + (s2 + s3)) + a.b[j];
+      }
+      __syncthreads();
+    }
+    // ---- per row: log-softmax, entropy, dL/dlogits (loss = -mean log p(a) - ent_w mean H)
+    const float inv = 1.f / (float)a.B;
+    if (tid < a.B) {
+      float* z = lg + tid * ap;
+      float mx = -INFINITY;
+      for (int j = 0; j < a.A; ++j) mx = fmaxf(mx, z[j]);
+      float se = 0.f;
+      for (int j = 0; j < a.A; ++j) se += expf(z[j] - mx);
+      const float lse = mx + logf(se);
+      float h = 0.f;
+      for (int j = 0; j < a.A; ++j) {
+        const float lp = z[j] - lse;
+        h -= expf(lp) * lp;
+      }
+      const int act = (int)a.acts[tid];
+      const bool ok = act >= 0 && act < a.A;
+      const float lpa = ok ? z[act] - lse : -INFINITY;
+      rowm[tid * 3 + 0] = lpa;
+      rowm[tid * 3 + 1] = h;
+      rowm[tid * 3 + 2] = ok ? expf(lpa) : 0.f;
+      for (int j = 0; j < ap; ++j) {
+        float g = 0.f;
+        if (j < a.A) {
+          const float lp = z[j] - lse, p = expf(lp);
+          g = inv * (p - (j == act ? 1.f : 0.f)) + a.ent_w * inv * p * (lp + h);
+        }
+        z[j] = g;
+      }
+    }
+    __syncthreads();
+    // ---- this block's 64 columns: dh = dlog W (thread: column c, row group rg), dW partials
+    {
+      const int c = tid & 63, rg = tid >> 6;
+      const int k = blockIdx.x * 64 + c;
+      const float* wk = wt + k * ap;
+      float pdw[kMaxA];
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j) pdw[j] = 0.f;
+      const int rpg = (a.B + 3) / 4;
+      for (int r = rg * rpg; r < min(a.B, (rg + 1) * rpg); ++r) {
+        const float hv = a.h[(size_t)r * a.NH + k];
+        const float* g = lg + r * ap;
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < kMaxA; ++j)
+          if (j < ap) {
+            d = fmaf(g[j], wk[j], d);
+            pdw[j] = fmaf(g[j], hv, pdw[j]);
+          }
+        a.dh[(size_t)r * a.NH + k] = d;
+      }
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j)
+        if (j < ap) pw[(rg * ap + j) * 64 + c] = pdw[j];
+      __syncthreads();
+      if (rg == 0)
+        for (int j = 0; j < a.A; ++j)
+          a.dW[(size_t)j * a.NH + k] = (pw[(0 * ap + j) * 64 + c] + pw[(1 * ap + j) * 64 + c]) +
+                                       (pw[(2 * ap + j) * 64 + c] + pw[(3 * ap + j) * 64 + c]);
+    }
+    if (blockIdx.x == 0) {
+      if (tid < a.A) {
+        float s = 0.f;
+        for (int r = 0; r < a.B; ++r) s += lg[r * ap + tid];
+        a.db[tid] = s;
+      }
+      // ---- metrics (l2 terms finished by the last block)
+      float slp = 0.f, sent = 0.f, sp = 0.f;
+      if (tid < a.B) {
+        slp = rowm[tid * 3 + 0];
+        sent = rowm[tid * 3 + 1];
+        sp = rowm[tid * 3 + 2];
+      }
+      slp = block_sum(slp, red);
+      sent = block_sum(sent, red);
+      sp = block_sum(sp, red);
+      if (tid == 0) {
+        const float neglogp = -slp * inv, ent = sent * inv, ent_loss = -a.ent_w * ent;
+        st_sc1(a.metrics + 0, neglogp);
+        st_sc1(a.metrics + 1, ent);
+        st_sc1(a.metrics + 2, ent_loss);
+        st_sc1(a.metrics + 3, sp * inv);
+      }
+    }
+  } else {
+    // ---- ||theta||^2 partial of this block's fixed float4 slice
+    const int nb = gridDim.x - n_head, b = blockIdx.x - n_head;
+    const long n4 = a.n_params >> 2;
+    const long per = (n4 + nb - 1) / nb, i0 = (long)b * per, i1 = min(n4, i0 + per);
+    const float4* x4 = reinterpret_cast<const float4*>(a.params);
+    float s = 0.f;
+    for (long i = i0 + tid; i < i1; i += kThreads) {
+      const float4 v = x4[i];
+      s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+    }
+    if (b == nb - 1)
+      for (long i = (n4 << 2) + tid; i < a.n_params; i += kThreads) s += a.params[i] * a.params[i];
+    s = block_sum(s, red);
+    if (tid == 0) st_sc1(a.partials + b, s);
+  }
+  // ---- hand-off: the last block to finish finishes the l2 terms and the loss
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) is_last = atomicAdd(a.cnt, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!is_last) return;
+  if (tid == 0) {
+    const int nb = gridDim.x - n_head;
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += ld_sc1(a.partials + b);
+    const float l2 = 0.5f * s, l2_loss = a.l2_w * l2;
+    const float neglogp = ld_sc1(a.metrics + 0), ent_loss = ld_sc1(a.metrics + 2);
+    a.metrics[4] = l2;
+    a.metrics[5] = l2_loss;
+    a.metrics[6] = neglogp + ent_loss + l2_loss;
+    __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+}  // namespace
+
+int bc_head_sumsq_blocks(long n_params) {
+  const long blocks = (n_params / 4 + kThreads * 16 - 1) / (kThreads * 16);
+  return (int)(blocks < 1 ? 1 : (blocks > 255 ? 255 : blocks));
+}
+
+size_t bc_head_lds_bytes(int B, int NH, int A) {
+  const int ap = A <= kAPad ? kAPad : kMaxA;
+  (void)B;
+  return (size_t)(NH * ap + 4 * 8 * ap * 64 + kMaxB * ap + 4 * ap * 64 + 3 * kMaxB) * sizeof(float);
+}
+
+bool bc_head_ok(int B, int NH, int A) {
+  return B > 0 && B <= kMaxB && NH > 0 && NH <= kMaxNH && NH % 64 == 0 && A > 0 && A <= kMaxA &&
+         bc_head_lds_bytes(B, NH, A) <= 160 * 1024;
+}
+
+hipError_t bc_head_train(const BcHeadArgs& a, hipStream_t s) {
+  if (!bc_head_ok(a.B, a.NH, a.A)) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(a.h) | reinterpret_cast<uintptr_t>(a.W) | reinterpret_cast<uintptr_t>(a.params)) & 15)
+    return hipErrorInvalidValue;
+  const int nb = bc_head_sumsq_blocks(a.n_params), n_head = a.NH / 64;
+  hipLaunchKernelGGL(bc_head_train_kernel, dim3(n_head + nb), dim3(kThreads), bc_head_lds_bytes(a.B, a.NH, a.A), s, a,
+                     n_head);
+  return hipGetLastError();
+}
+
+}  // namespace ia

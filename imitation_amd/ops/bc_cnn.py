@@ -1,0 +1,149 @@
+"""Fused BC minibatch of a NatureCNN categorical policy (the DAgger-Pong learner).
+
+Reference: ``src/imitation/algorithms/bc.py:443-510`` (``BehaviorCloningLossCalculator``:
+``policy.evaluate_actions`` -> ``-log_prob.mean()``, ``-ent_weight * entropy.mean()``, the
+``||theta||^2 / 2`` metric; ``loss.backward()``; ``optimizer.step()``), with the SB3
+``ActorCriticCnnPolicy`` (``NatureCNN`` features, ``net_arch=[]``, ``action_net`` Linear) of
+the reference's ``cnn_policy`` config.
+
+One step without autograd, every gradient written straight into the ``FusedAdam`` bucket:
+
+* one launch packs every bf16 GEMM layout (conv weights, the FC weight in NHWC column order,
+  their transposed data-gradient images);
+* three conv+ReLU MFMA launches on the uint8 frames (``/255`` folded into the first layer's
+  operand load) and the 512-unit FC+ReLU (``cnn_fc``);
+* ONE head launch (``bc_head.hip``): logits, log-softmax, entropy, the seven BC metrics,
+  ``dL/dlogits``, ``dW`` / ``db`` of ``action_net`` into the bucket, ``dL/dh`` and the
+  ``||theta||^2`` reduction over the whole parameter bucket;
+* the FC backward (dW, db into the bucket; dX in NHWC) and the conv stack backward (weight
+  gradients reduced into the bucket, data gradients with the ReLU masks fused);
+* the optimizer step is the caller's (one ``adam_flat`` launch).
+
+The value head is not evaluated: BC never uses it, and its bucket slice stays zero, as its
+``.grad`` would. Numerics: bf16 MFMA operands with fp32 accumulation in the trunk (as the
+autograd path of ``ops/conv.py``), fp32 head.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional
+
+import torch as th
+from torch import nn
+
+METRICS = ("neglogp", "entropy", "ent_loss", "prob_true_act", "l2_norm", "l2_loss", "loss")
+
+
+def _grad_views(optimizer) -> Optional[Dict[int, th.Tensor]]:
+    from imitation_amd.ops import optim as optim_ops
+
+    if not isinstance(optimizer, optim_ops.FusedAdam) or len(optimizer._flat) != 1 or not optimizer._flat[0]["n"]:
+        return None
+    f = optimizer._flat[0]
+    return {id(p): gv for p, (_, _, gv) in zip(f["params"], f["views"])}
+
+
+class FusedCnnBCStep:
+    """``step(obs_u8, acts) -> metrics [8]`` (``METRICS`` order) with the gradients of every
+    policy parameter in ``optimizer``'s bucket. Build with :meth:`maybe`."""
+
+    def __init__(self, policy, optimizer, ent_weight: float, l2_weight: float):
+        from imitation_amd import ops
+
+        self.C = ops.native()
+        self.policy = policy
+        self.optimizer = optimizer
+        self.ent_weight, self.l2_weight = float(ent_weight), float(l2_weight)
+        fe = policy.features_extractor
+        self.convs: List[nn.Conv2d] = [m for m in fe.cnn if isinstance(m, nn.Conv2d)]
+        self.lin: nn.Linear = fe.linear[0]
+        self.head: nn.Linear = policy.action_net
+        views = _grad_views(optimizer)
+        self.g_conv = [(views[id(c.weight)], views[id(c.bias)]) for c in self.convs]
+        self.g_lin = (views[id(self.lin.weight)], views[id(self.lin.bias)])
+        self.g_head = (views[id(self.head.weight)], views[id(self.head.bias)])
+        self.flat = optimizer._flat[0]["flat"]
+        dev = self.flat.device
+        self.metrics = th.zeros(8, device=dev)
+        self.ws = th.zeros(int(self.C.bc_head_workspace(self.flat.numel())), device=dev)  # word 0: counter
+
+    @staticmethod
+    def maybe(policy, optimizer, obs, ent_weight: float, l2_weight: float) -> Optional["FusedCnnBCStep"]:
+        """The fused step when it reproduces the loss calculator exactly, else None."""
+        import os
+
+        from imitation_amd import ops
+        from imitation_amd.ops import conv as conv_ops
+        from imitation_amd.rl.distributions import CategoricalDistribution
+        from imitation_amd.rl.policies import ActorCriticPolicy
+        from imitation_amd.rl.preprocessing import is_image_space
+        from imitation_amd.rl.torch_layers import NatureCNN
+
+        if os.environ.get("IMITATION_AMD_BC_CNN_FUSED", "1") == "0" or l2_weight != 0.0:
+            return None
+        if not (isinstance(policy, ActorCriticPolicy) and isinstance(obs, th.Tensor) and ops.use_kernel(obs)):
+            return None
+        if not (isinstance(policy.action_dist, CategoricalDistribution) and policy.share_features_extractor
+                and isinstance(policy.features_extractor, NatureCNN) and policy.normalize_images
+                and is_image_space(policy.observation_space)):
+            return None
+        fe = policy.features_extractor
+        if not fe.raw_frames_ok(obs) or len(fe.linear) != 2 or not isinstance(fe.linear[1], nn.ReLU):
+            return None
+        if len(policy.mlp_extractor.policy_net) != 0 or not isinstance(policy.action_net, nn.Linear):
+            return None
+        convs = [m for m in fe.cnn if isinstance(m, nn.Conv2d)]
+        lin = fe.linear[0]
+        if not conv_ops.fc_supported(tuple(obs.shape), [c.weight for c in convs], [c.stride[0] for c in convs],
+                                     lin.out_features):
+            return None
+        B, NH, A = obs.shape[0], lin.out_features, policy.action_net.out_features
+        if not (0 < B <= 64 and NH % 64 == 0 and NH <= 512 and 0 < A <= 18):
+            return None
+        views = _grad_views(optimizer)
+        if views is None or any(id(p) not in views for p in policy.parameters()):
+            return None
+        flat = optimizer._flat[0]["flat"]
+        if any(t.data_ptr() % 16 for t in (flat, policy.action_net.weight)):
+            return None
+        return FusedCnnBCStep(policy, optimizer, ent_weight, l2_weight)
+
+    def __call__(self, obs: th.Tensor, acts: th.Tensor) -> th.Tensor:
+        C = self.C
+        convs, lin, head = self.convs, self.lin, self.head
+        n = len(convs)
+        x = obs.contiguous()
+        B = x.shape[0]
+        H, W = x.shape[1], x.shape[2]
+        for c in convs:
+            H, W = (H - c.kernel_size[0]) // c.stride[0] + 1, (W - c.kernel_size[1]) // c.stride[0] + 1
+        C3, NH = convs[-1].out_channels, lin.out_features
+        with th.no_grad():
+            wsrc = [c.weight.detach() for c in convs] + [lin.weight.detach().view(NH, C3, H, W)]
+            wbs, wts = C.conv_pack_weights(wsrc, [i > 0 for i in range(n)] + [True], [False] * n + [True])
+            hs: List[th.Tensor] = []
+            h = x
+            for i, c in enumerate(convs):
+                h = C.conv_fwd(h, wbs[i], c.bias.detach(), int(c.stride[0]), 1.0 / 255.0 if i == 0 else 1.0, True, 0)
+                hs.append(h)
+            xf = h.reshape(B, -1)
+            out = C.cnn_fc(xf, wbs[n].view(NH, -1), lin.bias.detach())
+            a = acts.reshape(-1).long().contiguous()
+            dh = C.bc_head_train(out, head.weight.detach(), head.bias.detach(), a, self.flat, self.g_head[0], self.g_head[1],
+                                 self.metrics, self.ws, self.ent_weight, self.l2_weight)
+            _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1])
+            dz = dx.view(hs[-1].shape)
+            for i in range(n - 1, -1, -1):
+                c = convs[i]
+                inp = x if i == 0 else hs[i - 1]
+                top = i == n - 1
+                C.conv_wgrad(inp, dz, hs[i], int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0]),
+                             1.0 / 255.0 if i == 0 else 1.0, top, 0, self.g_conv[i][0], self.g_conv[i][1])
+                if i > 0:
+                    dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], int(c.stride[0]), top, True, 0)
+        return self.metrics
+
+
+def metrics_fields(m: th.Tensor) -> Dict[str, Any]:
+    """``BCTrainingMetrics`` keyword arguments from the metric vector."""
+    return {k: m[i] for i, k in enumerate(METRICS)}

@@ -226,3 +226,41 @@ def test_multibc_homogeneous_policy_runs_on_wide_kernel():
     th.cuda.synchronize()
     assert all(th.isfinite(p).all() for p in pol.parameters())
     assert any(not th.equal(a, b) for a, b in zip(p0, pol.parameters()))
+
+
+@pytest.mark.gpu
+def test_fused_cnn_bc_step_matches_autograd():
+    """ops/bc_cnn.FusedCnnBCStep (conv trunk + FC + fused head kernel, gradients straight into
+    the FusedAdam bucket) == the autograd BC loss on the same kernels: metrics and every
+    parameter's gradient."""
+    import torch as th
+
+    from imitation_amd.algorithms import bc as bc_mod
+    from imitation_amd.envs.vec_env import native_spaces
+    from imitation_amd.ops import bc_cnn
+    from imitation_amd.ops import optim as optim_ops
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+
+    obs_space, act_space = native_spaces("PongNoFrameskip-v4")
+    th.manual_seed(0)
+    pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
+    opt = optim_ops.FusedAdam(pol.parameters(), lr=1e-3)
+    g = th.Generator().manual_seed(1)
+    obs = th.randint(0, 256, (32, 84, 84, 4), generator=g, dtype=th.uint8).cuda()
+    acts = th.randint(0, act_space.n, (32,), generator=g).cuda()
+    step = bc_cnn.FusedCnnBCStep.maybe(pol, opt, obs, 1e-3, 0.0)
+    assert step is not None
+    opt.zero_grad()
+    m = step(obs, acts).clone()
+    fused = [p.grad.detach().clone() for p in pol.parameters()]
+    opt.zero_grad()
+    calc = bc_mod.BehaviorCloningLossCalculator(1e-3, 0.0)
+    ref = calc(pol, obs, acts)
+    ref.loss.backward()
+    want = th.stack([ref.neglogp, ref.entropy, ref.ent_loss, ref.prob_true_act, ref.l2_norm, ref.l2_loss, ref.loss]).detach()
+    th.testing.assert_close(m[:7], want, rtol=1e-4, atol=1e-5)
+    for name_p, a in zip(pol.named_parameters(), fused):
+        name, p = name_p
+        b = p.grad if p.grad is not None else th.zeros_like(p)
+        th.testing.assert_close(a, b, rtol=2e-3, atol=2e-5, msg=lambda s: f"{name}: {s}")
+    assert float(fused[-2].abs().sum()) == 0.0  # value head: no gradient
