@@ -193,7 +193,7 @@ py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch:
 // One fused Adam / AdamW step over flat fp32 buffers (ops/optim.py FusedAdam).
 void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg, torch::Tensor exp_avg_sq,
                torch::Tensor step, double lr, double beta1, double beta2, double eps, double weight_decay, bool decoupled,
-               bool maximize, bool zero_grad) {
+               bool maximize, bool zero_grad, c10::optional<torch::Tensor> step_cnt) {
   for (auto* t : {&params, &grads, &exp_avg, &exp_avg_sq}) {
     IA_CHECK_GPU_F32(*t);
     TORCH_CHECK(t->numel() == params.numel(), "flat Adam buffers must have equal sizes");
@@ -215,6 +215,11 @@ void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg,
   a.decoupled = decoupled ? 1 : 0;
   a.maximize = maximize ? 1 : 0;
   a.zero_grad = zero_grad ? 1 : 0;
+  if (step_cnt && step_cnt->defined()) {  // the kernel increments `step` itself
+    IA_CHECK_CUDA(*step_cnt);
+    TORCH_CHECK(step_cnt->scalar_type() == torch::kInt32 && step_cnt->numel() == 1, "step_cnt: int32 scalar (zero)");
+    a.cnt = reinterpret_cast<unsigned*>(step_cnt->data_ptr<int>());
+  }
   IA_HIP_CHECK(ia::adam_flat(a, ia_stream()));
 }
 
@@ -452,7 +457,7 @@ torch::Tensor bc_head_train(torch::Tensor h, torch::Tensor W, torch::Tensor b, t
                   acts.numel() == h.size(0) && dW.numel() == W.numel() && db.numel() == b.numel() && metrics.numel() >= 7,
               "bc_head_train: shapes");
   const int B = (int)h.size(0), NH = (int)h.size(1), A = (int)W.size(0);
-  TORCH_CHECK(ia::bc_head_ok(B, NH, A), "bc_head_train: B <= 64, NH % 64 == 0 and <= 512, A <= 18");
+  TORCH_CHECK(ia::bc_head_ok(B, NH, A), "bc_head_train: B <= 64, NH % 64 == 0 and <= 512, A <= 8");
   const long n = (long)params.numel();
   const int nb = ia::bc_head_sumsq_blocks(n);
   TORCH_CHECK(ws.numel() >= nb + 1, "bc_head_train: workspace of bc_head_workspace(n_params) floats");
@@ -541,7 +546,7 @@ void register_kernels(py::module& m) {
         py::arg("dones"), py::arg("gamma"), py::arg("lam"));
   m.def("adam_flat", &adam_flat, py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"),
         py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
-        py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"));
+        py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"), py::arg("step_cnt") = py::none());
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
   m.def("running_norm", &running_norm, py::arg("x"), py::arg("mean"), py::arg("var"), py::arg("count"), py::arg("eps"),
         py::arg("update"), py::arg("want_y"), py::arg("ema_inv_lr") = py::none(), py::arg("ema_num_batches") = py::none(),

@@ -28,7 +28,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxB = 64;
 constexpr int kMaxNH = 512;
-constexpr int kMaxA = 18;  // the full Atari action set
+constexpr int kMaxA = 8;  // minimal Atari action sets (Pong: 6); wider heads keep the autograd step
 
 __device__ __forceinline__ void st_sc1(float* p, float v) {
   asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
@@ -58,66 +58,65 @@ __device__ float block_sum(float v, float* red) {
 // recomputes the (tiny) logits of all B rows -- 4 waves x 8 rows, a lane 8 contiguous
 // features, partials reduced through LDS in a fixed order -- so no grid-wide dependency
 // separates the softmax from the gradients; then its columns of dW and dh.
-constexpr int kAPad = 8;  // logits row stride for A <= 8 (wider heads: kMaxA)
+constexpr int kAPad = 8;  // logits row stride (A <= kMaxA = 8)
 
 __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, int n_head) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ float red[4];
   __shared__ int is_last;
   const int tid = threadIdx.x;
-  const int ap = a.A <= kAPad ? kAPad : kMaxA;
+  const int ap = kAPad;
   if ((int)blockIdx.x < n_head) {
-    float* wt = sm;                  // [NH][ap]  W transposed (feature-major)
-    float* part = wt + a.NH * ap;    // [4 waves][8 rows][ap][64 lanes] logit partials
-    float* lg = part + 4 * 8 * ap * 64;  // [B][ap] logits, then dL/dlogits
-    float* pw = lg + kMaxB * ap;     // [4 row groups][ap][64] dW partials
-    float* rowm = pw + 4 * ap * 64;  // [B][3]
-    for (int e = tid; e < a.A * a.NH; e += kThreads) {
-      const int j = e / a.NH, k = e - j * a.NH;
-      wt[k * ap + j] = a.W[e];
-    }
+    // LDS images laid out so that the 64 lanes of a wave touch 64 different banks:
+    // W as given ([A][NH], lanes on consecutive features), logit partials [lane][pair] with a
+    // 257-float row stride (pair = row-in-pass x action)
+    constexpr int kPS = 257;
+    float* wt = sm;                   // [ap][NH]
+    float* part = wt + ap * a.NH;     // [64 lanes][kPS]
+    float* lg = part + 64 * kPS;      // [B][ap] logits, then dL/dlogits
+    float* pw = lg + kMaxB * ap;      // [4 row groups][ap][64] dW partials
+    float* rowm = pw + 4 * ap * 64;   // [B][3]
+    const int nh4 = a.NH >> 2;
+    for (int i = tid; i < a.A * nh4; i += kThreads) reinterpret_cast<float4*>(wt)[i] = reinterpret_cast<const float4*>(a.W)[i];
     __syncthreads();
     const int w = tid >> 6, lane = tid & 63;
-    const int kpl = a.NH >> 6;  // contiguous features per lane
+    const int kpl = a.NH >> 6;  // features per lane: k = 64 i + lane
     for (int r0 = 0; r0 < a.B; r0 += 32) {  // 32 rows per pass (B <= 64)
-      // ---- logit partials: wave w rows r0 + w + 4 q (q < 8), lane features [lane kpl, +kpl)
+      // ---- logit partials: wave w rows r0 + w + 4 q (q < 8)
       for (int q = 0; q < 8; ++q) {
         const int r = r0 + w + 4 * q;
         float acc[kMaxA];
 #pragma unroll
         for (int j = 0; j < kMaxA; ++j) acc[j] = 0.f;
         if (r < a.B) {
-          const float* hr = a.h + (size_t)r * a.NH + lane * kpl;
-          for (int i = 0; i < kpl; i += 4) {
-            const float4 hv = *reinterpret_cast<const float4*>(hr + i);
-            const float hx[4] = {hv.x, hv.y, hv.z, hv.w};
+          // all of the row's loads in flight before the first FMA (kpl <= 8)
+          const float* hr = a.h + (size_t)r * a.NH + lane;
+          float hv[kMaxNH / 64];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const float* wk = wt + (lane * kpl + i + u) * ap;
+          for (int i = 0; i < kMaxNH / 64; ++i) hv[i] = i < kpl ? hr[64 * i] : 0.f;
+#pragma unroll
+          for (int i = 0; i < kMaxNH / 64; ++i)
+            if (i < kpl) {
 #pragma unroll
               for (int j = 0; j < kMaxA; ++j)
-                if (j < ap) acc[j] = fmaf(hx[u], wk[j], acc[j]);
+                if (j < a.A) acc[j] = fmaf(hv[i], wt[j * a.NH + 64 * i + lane], acc[j]);
             }
-          }
         }
 #pragma unroll
         for (int j = 0; j < kMaxA; ++j)
-          if (j < ap) part[((w * 8 + q) * ap + j) * 64 + lane] = acc[j];
+          if (j < ap) part[lane * kPS + (w + 4 * q) * ap + j] = acc[j];
       }
       __syncthreads();
-      // ---- reduce: thread -> (row, action) pairs, 64 lane partials in order
+      // ---- reduce: thread -> (row, action) pair, the 64 lane partials in lane order
       for (int pr = tid; pr < 32 * ap; pr += kThreads) {
-        const int rl = pr / ap, j = pr - rl * ap;  // rl = w + 4 q
-        const int ww = rl & 3, q = rl >> 2;
-        const float4* src = reinterpret_cast<const float4*>(part + ((ww * 8 + q) * ap + j) * 64);
+        const int rl = pr / ap, j = pr - rl * ap;
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const float4 x = src[v];
-          s0 += x.x;
-          s1 += x.y;
-          s2 += x.z;
-          s3 += x.w;
+#pragma unroll 4
+        for (int v = 0; v < 64; v += 4) {
+          s0 += part[(v + 0) * kPS + pr];
+          s1 += part[(v + 1) * kPS + pr];
+          s2 += part[(v + 2) * kPS + pr];
+          s3 += part[(v + 3) * kPS + pr];
         }
         const int r = r0 + rl;
         if (r < a.B && j < a.A) lg[r * ap + j] = ((s0 + s1) + (s2 + s3)) + a.b[j];
@@ -158,22 +157,33 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
     {
       const int c = tid & 63, rg = tid >> 6;
       const int k = blockIdx.x * 64 + c;
-      const float* wk = wt + k * ap;
       float pdw[kMaxA];
 #pragma unroll
       for (int j = 0; j < kMaxA; ++j) pdw[j] = 0.f;
-      const int rpg = (a.B + 3) / 4;
-      for (int r = rg * rpg; r < min(a.B, (rg + 1) * rpg); ++r) {
-        const float hv = a.h[(size_t)r * a.NH + k];
-        const float* g = lg + r * ap;
-        float d = 0.f;
+      float wk[kMaxA];
 #pragma unroll
-        for (int j = 0; j < kMaxA; ++j)
-          if (j < ap) {
+      for (int j = 0; j < kMaxA; ++j) wk[j] = j < a.A ? wt[j * a.NH + k] : 0.f;
+      // rows rg, rg + 4, ... (<= 16 per group): all h loads in flight first
+      constexpr int kRpg = kMaxB / 4;
+      float hv[kRpg];
+#pragma unroll
+      for (int u = 0; u < kRpg; ++u) {
+        const int r = rg + 4 * u;
+        hv[u] = r < a.B ? a.h[(size_t)r * a.NH + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kRpg; ++u) {
+        const int r = rg + 4 * u;
+        if (r < a.B) {
+          const float* g = lg + r * ap;
+          float d = 0.f;
+#pragma unroll
+          for (int j = 0; j < kMaxA; ++j) {
             d = fmaf(g[j], wk[j], d);
-            pdw[j] = fmaf(g[j], hv, pdw[j]);
+            pdw[j] = fmaf(g[j], hv[u], pdw[j]);
           }
-        a.dh[(size_t)r * a.NH + k] = d;
+          a.dh[(size_t)r * a.NH + k] = d;
+        }
       }
 #pragma unroll
       for (int j = 0; j < kMaxA; ++j)
@@ -215,9 +225,13 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
     const long per = (n4 + nb - 1) / nb, i0 = (long)b * per, i1 = min(n4, i0 + per);
     const float4* x4 = reinterpret_cast<const float4*>(a.params);
     float s = 0.f;
-    for (long i = i0 + tid; i < i1; i += kThreads) {
-      const float4 v = x4[i];
-      s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+    // 8 independent float4 loads in flight per lane per pass
+    for (long i = i0 + tid; i < i1; i += 8 * kThreads) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = i + u * kThreads < i1 ? x4[i + u * kThreads] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (v[u].x * v[u].x + v[u].y * v[u].y) + (v[u].z * v[u].z + v[u].w * v[u].w);
     }
     if (b == nb - 1)
       for (long i = (n4 << 2) + tid; i < a.n_params; i += kThreads) s += a.params[i] * a.params[i];
@@ -230,10 +244,12 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
   if (tid == 0) is_last = atomicAdd(a.cnt, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!is_last) return;
+  // every partial in flight at once (one sc1 load per thread), then a fixed-order block sum
+  const int nb = gridDim.x - n_head;
+  float s = 0.f;
+  for (int b = tid; b < nb; b += kThreads) s += ld_sc1(a.partials + b);
+  s = block_sum(s, red);
   if (tid == 0) {
-    const int nb = gridDim.x - n_head;
-    float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += ld_sc1(a.partials + b);
     const float l2 = 0.5f * s, l2_loss = a.l2_w * l2;
     const float neglogp = ld_sc1(a.metrics + 0), ent_loss = ld_sc1(a.metrics + 2);
     a.metrics[4] = l2;
@@ -251,9 +267,10 @@ int bc_head_sumsq_blocks(long n_params) {
 }
 
 size_t bc_head_lds_bytes(int B, int NH, int A) {
-  const int ap = A <= kAPad ? kAPad : kMaxA;
+  const int ap = kAPad;
   (void)B;
-  return (size_t)(NH * ap + 4 * 8 * ap * 64 + kMaxB * ap + 4 * ap * 64 + 3 * kMaxB) * sizeof(float);
+  (void)A;
+  return (size_t)(NH * ap + 64 * 257 + kMaxB * ap + 4 * ap * 64 + 3 * kMaxB) * sizeof(float);
 }
 
 bool bc_head_ok(int B, int NH, int A) {

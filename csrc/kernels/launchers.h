@@ -264,7 +264,7 @@ struct CnnHeadArgs {
 hipError_t cnn_head(const CnnHeadArgs& a, hipStream_t s);
 
 // ---- bc_head.hip: categorical BC head (logits, loss metrics, dW / db / dh) + ||theta||^2 in
-// one launch (B <= 64, NH % 64 == 0 and <= 512, A <= 18)
+// one launch (B <= 64, NH % 64 == 0 and <= 512, A <= 8)
 struct BcHeadArgs {
   const float *h, *W, *b;   // features [B, NH] (16-B aligned), head weight [A, NH] (16-B aligned), bias [A]
   const int64_t* acts;      // [B]
@@ -284,7 +284,10 @@ hipError_t bc_head_train(const BcHeadArgs& a, hipStream_t s);
 // ---- optim.hip: fused Adam / AdamW over a flat fp32 buffer
 struct AdamArgs {
   float *params, *grads, *exp_avg, *exp_avg_sq;
-  const float* step;  // device step counter, already incremented for this step
+  float* step;        // device step counter: already incremented for this step, or (cnt != null)
+                      // incremented by the kernel (every block uses *step + 1, the last block to
+                      // finish stores it)
+  unsigned* cnt;      // zeroed hand-off counter for the in-kernel increment (left zero), or null
   int64_t n;
   float lr, beta1, beta2, eps, weight_decay;
   int decoupled;  // AdamW: p *= 1 - lr * wd

@@ -29,7 +29,7 @@ __device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v,
 }
 
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
-  const float t = *a.step;
+  const float t = *a.step + (a.cnt ? 1.f : 0.f);
   const float bc1 = 1.f - powf(a.beta1, t);
   const float bc2_sqrt = sqrtf(1.f - powf(a.beta2, t));
   const float step_size = a.lr / bc1;
@@ -49,6 +49,18 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
     *reinterpret_cast<float4*>(a.exp_avg_sq + i4) = v;
   } else {
     for (int64_t i = i4; i < a.n; ++i) adam_one(a.params[i], a.grads[i], a.exp_avg[i], a.exp_avg_sq[i], a, step_size, bc2_sqrt);
+  }
+  if (a.cnt) {
+    // the step counter advances once every block has read it: the last block to arrive stores
+    // it (vector atomics, agent scope) -- no separate `step += 1` launch per optimizer step
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(a.cnt, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+      __hip_atomic_store(a.step, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

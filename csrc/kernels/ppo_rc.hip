@@ -397,9 +397,14 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   const int w = rfl(tid >> 6), lane = tid & 63;
   const int r16 = lane & 15, kk = lane >> 4;
   const bool ns = g.ns != 0;  // net split: workgroup 2 grp + q runs net q of row group grp
-  const int q = ns ? (int)(blockIdx.x & 1) : w / kHalf;  // 0 actor, 1 critic
-  const int gw = ns ? w : w % kHalf;                     // row tile
-  const int grp = ns ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;  // row group
+  int bid = (int)blockIdx.x;
+  if (g.xcd > 1) {  // XCD-co-located plan: only every xcd-th block works
+    if (bid % g.xcd) return;
+    bid /= g.xcd;
+  }
+  const int q = ns ? (bid & 1) : w / kHalf;  // 0 actor, 1 critic
+  const int gw = ns ? w : w % kHalf;         // row tile
+  const int grp = ns ? (bid >> 1) : bid;     // row group
   const int G = g.G, nch = g.nch, cw = CWT > 0 ? CWT : g.cw;
   const int CH = G * nch;
   const int Bg = CH * cw;  // minibatch rows
@@ -1484,7 +1489,15 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   bool uniform = a.n_pi == 3 && a.n_vf == 3;
   for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
   const int s0 = (a.D + 3) / 4;
-  const dim3 grid(g.ns ? 2 * g.G : g.G), block(64 * g.nw);
+  const int nblk = g.ns ? 2 * g.G : g.G;
+  {  // every cooperating workgroup on one XCD (<= 32 workgroups; IMITATION_AMD_PPO_XCD=0 turns it
+     // off). GAIL emulated W = 2 / 4 / 8: 3.14 / 3.28 / 3.64 -> 2.99 / 2.96 / 3.36 ms per update,
+     // headline round 3.63 -> 3.55 ms (profiles/r3_ppo_xcd.md)
+    const char* ev = getenv("IMITATION_AMD_PPO_XCD");
+    const bool on = ev ? ev[0] == '1' : true;
+    g.xcd = on && nblk > 1 && nblk <= 32 ? 8 : 1;
+  }
+  const dim3 grid(nblk * g.xcd), block(64 * g.nw);
   int wmx = g.n_witems, bmx = g.n_items - g.n_witems;
   if (g.ns) {
     wmx = g.nwit[0] > g.nwit[1] ? g.nwit[0] : g.nwit[1];

@@ -98,7 +98,7 @@ class FusedCnnBCStep:
                                      lin.out_features):
             return None
         B, NH, A = obs.shape[0], lin.out_features, policy.action_net.out_features
-        if not (0 < B <= 64 and NH % 64 == 0 and NH <= 512 and 0 < A <= 18):
+        if not (0 < B <= 64 and NH % 64 == 0 and NH <= 512 and 0 < A <= 8):
             return None
         views = _grad_views(optimizer)
         if views is None or any(id(p) not in views for p in policy.parameters()):
