@@ -73,6 +73,55 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor wb, c10::optional<torch::T
 }
 
 // (dW fp32 [N][C][KH][KW] (torch layout), db fp32 [N]); dZ = dy * [y > 0] if relu_out
+// the wgrad block partials only (reduction deferred to conv_reduce_multi): returns the slab
+torch::Tensor conv_wgrad_partials(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t KH, int64_t KW,
+                                  int64_t stride, double in_scale, bool relu_out, int64_t pad) {
+  IA_CHECK_CUDA(x);
+  IA_CHECK_CONTIG(x);
+  IA_CHECK_CUDA(dy);
+  IA_CHECK_CONTIG(dy);
+  TORCH_CHECK(dy.scalar_type() == torch::kBFloat16, "dy must be bf16 NHWC");
+  auto g = geo(x, dy.size(3), KH, KW, stride, pad);
+  TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.OH && dy.size(2) == g.OW, "dy shape");
+  if (relu_out) {
+    IA_CHECK_CUDA(y);
+    IA_CHECK_CONTIG(y);
+    TORCH_CHECK(y.sizes() == dy.sizes() && y.scalar_type() == torch::kBFloat16, "y must match dy");
+  }
+  auto slab = torch::empty({(int64_t)ia::conv_wgrad_slab_floats(g)}, x.options().dtype(torch::kFloat32));
+  IA_HIP_CHECK3(ia::conv_wgrad(in_kind(x), x.data_ptr(), dy.data_ptr(), relu_out ? y.data_ptr() : nullptr,
+                               slab.data_ptr<float>(), nullptr, nullptr, g, (float)in_scale, relu_out ? 1 : 0, ia_stream()));
+  return slab;
+}
+
+// every layer's deferred reduction (slab of conv_wgrad_partials) into dW [N, C, KH, KW] / db [N]
+// slots, one launch; geometry from the same x / dy / kernel / stride / pad as the partials call
+void conv_reduce_multi(std::vector<torch::Tensor> xs, std::vector<torch::Tensor> dys, std::vector<int64_t> KHs,
+                       std::vector<int64_t> KWs, std::vector<int64_t> strides, std::vector<int64_t> pads,
+                       std::vector<torch::Tensor> slabs, std::vector<torch::Tensor> dWs, std::vector<torch::Tensor> dbs) {
+  const size_t n = xs.size();
+  TORCH_CHECK(n > 0 && n <= (size_t)ia::kMaxPack && dys.size() == n && KHs.size() == n && KWs.size() == n &&
+                  strides.size() == n && pads.size() == n && slabs.size() == n && dWs.size() == n && dbs.size() == n,
+              "conv_reduce_multi: one entry per layer (<= 8)");
+  ia::ConvReduceMulti r{};
+  r.n = (int)n;
+  for (size_t l = 0; l < n; ++l) {
+    auto g = geo(xs[l], dys[l].size(3), KHs[l], KWs[l], strides[l], pads[l]);
+    IA_CHECK_GPU_F32(slabs[l]);
+    IA_CHECK_GPU_F32(dWs[l]);
+    IA_CHECK_GPU_F32(dbs[l]);
+    IA_CHECK_CONTIG(dWs[l]);
+    IA_CHECK_CONTIG(dbs[l]);
+    TORCH_CHECK((size_t)slabs[l].numel() >= ia::conv_wgrad_slab_floats(g), "conv_reduce_multi: slab size");
+    TORCH_CHECK(dWs[l].numel() == (int64_t)g.N * g.C * g.KH * g.KW && dbs[l].numel() == g.N, "conv_reduce_multi: dW / db");
+    r.g[l] = g;
+    r.slab[l] = slabs[l].data_ptr<float>();
+    r.dW[l] = dWs[l].data_ptr<float>();
+    r.db[l] = dbs[l].data_ptr<float>();
+  }
+  IA_HIP_CHECK3(ia::conv_reduce_multi(r, ia_stream()));
+}
+
 py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t KH, int64_t KW, int64_t stride,
                      double in_scale, bool relu_out, int64_t pad, c10::optional<torch::Tensor> dW_out,
                      c10::optional<torch::Tensor> db_out) {
@@ -343,6 +392,10 @@ void register_conv(py::module& m) {
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
         py::arg("relu_out"), py::arg("pad") = 0, py::arg("dW_out") = py::none(), py::arg("db_out") = py::none());
+  m.def("conv_wgrad_partials", &conv_wgrad_partials, "NHWC conv weight-gradient block partials (deferred reduction)",
+        py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
+        py::arg("relu_out"), py::arg("pad") = 0);
+  m.def("conv_reduce_multi", &conv_reduce_multi, "deferred wgrad reductions of several layers, one launch");
   m.def("conv_dgrad", &conv_dgrad, "NHWC conv data gradient with fused ReLU masks", py::arg("dy"), py::arg("y"),
         py::arg("wt"), py::arg("xp"), py::arg("stride"), py::arg("relu_out"), py::arg("relu_in"), py::arg("pad") = 0);
 }

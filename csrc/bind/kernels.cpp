@@ -446,7 +446,7 @@ py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, 
 // into `metrics`, dW / db into the gradient slots (written), dh [B, NH] returned.
 torch::Tensor bc_head_train(torch::Tensor h, torch::Tensor W, torch::Tensor b, torch::Tensor acts, torch::Tensor params,
                             torch::Tensor dW, torch::Tensor db, torch::Tensor metrics, torch::Tensor ws, double ent_w,
-                            double l2_w) {
+                            double l2_w, c10::optional<torch::Tensor> prof) {
   for (auto* t : {&h, &W, &b, &params, &dW, &db, &metrics, &ws}) {
     IA_CHECK_GPU_F32((*t));
     IA_CHECK_CONTIG((*t));
@@ -457,7 +457,7 @@ torch::Tensor bc_head_train(torch::Tensor h, torch::Tensor W, torch::Tensor b, t
                   acts.numel() == h.size(0) && dW.numel() == W.numel() && db.numel() == b.numel() && metrics.numel() >= 7,
               "bc_head_train: shapes");
   const int B = (int)h.size(0), NH = (int)h.size(1), A = (int)W.size(0);
-  TORCH_CHECK(ia::bc_head_ok(B, NH, A), "bc_head_train: B <= 64, NH % 64 == 0 and <= 512, A <= 8");
+  TORCH_CHECK(ia::bc_head_ok(B, NH, A), "bc_head_train: B <= 64, NH 256 or 512, A <= 8");
   const long n = (long)params.numel();
   const int nb = ia::bc_head_sumsq_blocks(n);
   TORCH_CHECK(ws.numel() >= nb + 1, "bc_head_train: workspace of bc_head_workspace(n_params) floats");
@@ -482,6 +482,10 @@ torch::Tensor bc_head_train(torch::Tensor h, torch::Tensor W, torch::Tensor b, t
   a.metrics = metrics.data_ptr<float>();
   a.cnt = reinterpret_cast<unsigned*>(ws.data_ptr<float>());  // word 0: counter (zeroed by the caller once)
   a.partials = ws.data_ptr<float>() + 1;
+  if (prof && prof->defined()) {
+    TORCH_CHECK(prof->is_cuda() && prof->scalar_type() == torch::kInt64 && prof->numel() >= 8, "prof: int64 [8]");
+    a.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
+  }
   IA_HIP_CHECK(ia::bc_head_train(a, ia_stream()));
   return dh;
 }
@@ -560,7 +564,7 @@ void register_kernels(py::module& m) {
   m.def("bc_cat_loss_bwd", &bc_cat_loss_bwd, py::arg("z"), py::arg("acts"), py::arg("g"), py::arg("g_loss"),
         py::arg("ent_w"));
   m.def("bc_head_train", &bc_head_train, py::arg("h"), py::arg("W"), py::arg("b"), py::arg("acts"), py::arg("params"),
-        py::arg("dW"), py::arg("db"), py::arg("metrics"), py::arg("ws"), py::arg("ent_w"), py::arg("l2_w"));
+        py::arg("dW"), py::arg("db"), py::arg("metrics"), py::arg("ws"), py::arg("ent_w"), py::arg("l2_w"), py::arg("prof") = py::none());
   m.def("bc_head_workspace", [](int64_t n) { return (int64_t)ia::bc_head_sumsq_blocks((long)n) + 1; });
   m.def("cat_eval_fwd", &cat_eval_fwd, py::arg("z"), py::arg("acts"));
   m.def("cat_eval_bwd", &cat_eval_bwd, py::arg("z"), py::arg("acts"), py::arg("g_lp"), py::arg("g_ent"));

@@ -60,12 +60,14 @@ __device__ float block_sum(float v, float* red) {
 // separates the softmax from the gradients; then its columns of dW and dh.
 constexpr int kAPad = 8;  // logits row stride (A <= kMaxA = 8)
 
+template <int KPL>  // features per lane (NH / 64), compile-time: the logit loops carry no predicates
 __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, int n_head) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ float red[4];
   __shared__ int is_last;
   const int tid = threadIdx.x;
   const int ap = kAPad;
+  if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[0] = clock64();
   if ((int)blockIdx.x < n_head) {
     // LDS images laid out so that the 64 lanes of a wave touch 64 different banks:
     // W as given ([A][NH], lanes on consecutive features), logit partials [lane][pair] with a
@@ -76,37 +78,42 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
     float* lg = part + 64 * kPS;      // [B][ap] logits, then dL/dlogits
     float* pw = lg + kMaxB * ap;      // [4 row groups][ap][64] dW partials
     float* rowm = pw + 4 * ap * 64;   // [B][3]
-    const int nh4 = a.NH >> 2;
-    for (int i = tid; i < a.A * nh4; i += kThreads) reinterpret_cast<float4*>(wt)[i] = reinterpret_cast<const float4*>(a.W)[i];
-    __syncthreads();
     const int w = tid >> 6, lane = tid & 63;
-    const int kpl = a.NH >> 6;  // features per lane: k = 64 i + lane
+    const int nh4 = a.NH >> 2;
     for (int r0 = 0; r0 < a.B; r0 += 32) {  // 32 rows per pass (B <= 64)
-      // ---- logit partials: wave w rows r0 + w + 4 q (q < 8)
+      // every h value of this wave's 8 rows in flight at once (one memory round trip), issued
+      // before the W staging so both overlap
+      float hv[8][KPL];
+#pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int r = r0 + w + 4 * q;
+        const float* hr = a.h + (size_t)(r < a.B ? r : 0) * a.NH + lane;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) hv[q][i] = r < a.B ? hr[64 * i] : 0.f;
+      }
+      if (r0 == 0) {  // W rows A .. kMaxA - 1 are zero: every logit loop runs all kMaxA actions
+        for (int i = tid; i < kMaxA * nh4; i += kThreads)
+          reinterpret_cast<float4*>(wt)[i] =
+              i < a.A * nh4 ? reinterpret_cast<const float4*>(a.W)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        __syncthreads();
+        if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[1] = clock64();
+      }
+      // ---- logit partials: wave w rows r0 + w + 4 q (q < 8)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
         float acc[kMaxA];
 #pragma unroll
         for (int j = 0; j < kMaxA; ++j) acc[j] = 0.f;
-        if (r < a.B) {
-          // all of the row's loads in flight before the first FMA (kpl <= 8)
-          const float* hr = a.h + (size_t)r * a.NH + lane;
-          float hv[kMaxNH / 64];
 #pragma unroll
-          for (int i = 0; i < kMaxNH / 64; ++i) hv[i] = i < kpl ? hr[64 * i] : 0.f;
+        for (int i = 0; i < KPL; ++i) {
 #pragma unroll
-          for (int i = 0; i < kMaxNH / 64; ++i)
-            if (i < kpl) {
-#pragma unroll
-              for (int j = 0; j < kMaxA; ++j)
-                if (j < a.A) acc[j] = fmaf(hv[i], wt[j * a.NH + 64 * i + lane], acc[j]);
-            }
+          for (int j = 0; j < kMaxA; ++j) acc[j] = fmaf(hv[q][i], wt[j * KPL * 64 + 64 * i + lane], acc[j]);
         }
 #pragma unroll
-        for (int j = 0; j < kMaxA; ++j)
-          if (j < ap) part[lane * kPS + (w + 4 * q) * ap + j] = acc[j];
+        for (int j = 0; j < kMaxA; ++j) part[lane * kPS + (w + 4 * q) * ap + j] = acc[j];
       }
       __syncthreads();
+      if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[2] = clock64();
       // ---- reduce: thread -> (row, action) pair, the 64 lane partials in lane order
       for (int pr = tid; pr < 32 * ap; pr += kThreads) {
         const int rl = pr / ap, j = pr - rl * ap;
@@ -122,37 +129,55 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
         if (r < a.B && j < a.A) lg[r * ap + j] = ((s0 + s1) + (s2 + s3)) + a.b[j];
       }
       __syncthreads();
+      if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[3] = clock64();
     }
     // ---- per row: log-softmax, entropy, dL/dlogits (loss = -mean log p(a) - ent_w mean H)
     const float inv = 1.f / (float)a.B;
     if (tid < a.B) {
+      // one exp per action: p_j = e_j / sum e, log p_j = z_j - lse
       float* z = lg + tid * ap;
+      float zz[kMaxA], e[kMaxA];
       float mx = -INFINITY;
-      for (int j = 0; j < a.A; ++j) mx = fmaxf(mx, z[j]);
-      float se = 0.f;
-      for (int j = 0; j < a.A; ++j) se += expf(z[j] - mx);
-      const float lse = mx + logf(se);
-      float h = 0.f;
-      for (int j = 0; j < a.A; ++j) {
-        const float lp = z[j] - lse;
-        h -= expf(lp) * lp;
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j) {
+        zz[j] = z[j];
+        if (j < a.A) mx = fmaxf(mx, zz[j]);
       }
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j) {
+        e[j] = j < a.A ? expf(zz[j] - mx) : 0.f;
+        se += e[j];
+      }
+      const float lse = mx + logf(se), rse = 1.f / se;
+      float h = 0.f;
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j)
+        if (j < a.A) h -= (e[j] * rse) * (zz[j] - lse);
       const int act = (int)a.acts[tid];
       const bool ok = act >= 0 && act < a.A;
-      const float lpa = ok ? z[act] - lse : -INFINITY;
-      rowm[tid * 3 + 0] = lpa;
+      float lpa = -INFINITY, pa = 0.f;
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j)
+        if (j == act) {
+          lpa = zz[j] - lse;
+          pa = e[j] * rse;
+        }
+      rowm[tid * 3 + 0] = ok ? lpa : -INFINITY;
       rowm[tid * 3 + 1] = h;
-      rowm[tid * 3 + 2] = ok ? expf(lpa) : 0.f;
-      for (int j = 0; j < ap; ++j) {
+      rowm[tid * 3 + 2] = ok ? pa : 0.f;
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j) {
         float g = 0.f;
         if (j < a.A) {
-          const float lp = z[j] - lse, p = expf(lp);
+          const float lp = zz[j] - lse, p = e[j] * rse;
           g = inv * (p - (j == act ? 1.f : 0.f)) + a.ent_w * inv * p * (lp + h);
         }
         z[j] = g;
       }
     }
     __syncthreads();
+    if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[4] = clock64();
     // ---- this block's 64 columns: dh = dlog W (thread: column c, row group rg), dW partials
     {
       const int c = tid & 63, rg = tid >> 6;
@@ -162,7 +187,7 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
       for (int j = 0; j < kMaxA; ++j) pdw[j] = 0.f;
       float wk[kMaxA];
 #pragma unroll
-      for (int j = 0; j < kMaxA; ++j) wk[j] = j < a.A ? wt[j * a.NH + k] : 0.f;
+      for (int j = 0; j < kMaxA; ++j) wk[j] = wt[j * KPL * 64 + k];
       // rows rg, rg + 4, ... (<= 16 per group): all h loads in flight first
       constexpr int kRpg = kMaxB / 4;
       float hv[kRpg];
@@ -189,6 +214,7 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
       for (int j = 0; j < kMaxA; ++j)
         if (j < ap) pw[(rg * ap + j) * 64 + c] = pdw[j];
       __syncthreads();
+      if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[5] = clock64();
       if (rg == 0)
         for (int j = 0; j < a.A; ++j)
           a.dW[(size_t)j * a.NH + k] = (pw[(0 * ap + j) * 64 + c] + pw[(1 * ap + j) * 64 + c]) +
@@ -243,15 +269,22 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
   __syncthreads();
   if (tid == 0) is_last = atomicAdd(a.cnt, 1u) == gridDim.x - 1;
   __syncthreads();
+  if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[6] = clock64();
   if (!is_last) return;
-  // every partial in flight at once (one sc1 load per thread), then a fixed-order block sum
+  // every partial and the two head metrics in flight at once (ONE memory round trip), then a
+  // fixed-order block sum
   const int nb = gridDim.x - n_head;
-  float s = 0.f;
-  for (int b = tid; b < nb; b += kThreads) s += ld_sc1(a.partials + b);
+  float s = 0.f, neglogp = 0.f, ent_loss = 0.f;
+  if (tid < nb) asm volatile("global_load_dword %0, %1, off sc1" : "=v"(s) : "v"(a.partials + tid) : "memory");
+  if (tid == 0) {
+    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(neglogp) : "v"(a.metrics + 0) : "memory");
+    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(ent_loss) : "v"(a.metrics + 2) : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(s), "+v"(neglogp), "+v"(ent_loss) : : "memory");
+  for (int b = tid + kThreads; b < nb; b += kThreads) s += ld_sc1(a.partials + b);
   s = block_sum(s, red);
   if (tid == 0) {
     const float l2 = 0.5f * s, l2_loss = a.l2_w * l2;
-    const float neglogp = ld_sc1(a.metrics + 0), ent_loss = ld_sc1(a.metrics + 2);
     a.metrics[4] = l2;
     a.metrics[5] = l2_loss;
     a.metrics[6] = neglogp + ent_loss + l2_loss;
@@ -274,7 +307,7 @@ size_t bc_head_lds_bytes(int B, int NH, int A) {
 }
 
 bool bc_head_ok(int B, int NH, int A) {
-  return B > 0 && B <= kMaxB && NH > 0 && NH <= kMaxNH && NH % 64 == 0 && A > 0 && A <= kMaxA &&
+  return B > 0 && B <= kMaxB && (NH == 512 || NH == 256) && A > 0 && A <= kMaxA &&
          bc_head_lds_bytes(B, NH, A) <= 160 * 1024;
 }
 
@@ -283,8 +316,12 @@ hipError_t bc_head_train(const BcHeadArgs& a, hipStream_t s) {
   if ((reinterpret_cast<uintptr_t>(a.h) | reinterpret_cast<uintptr_t>(a.W) | reinterpret_cast<uintptr_t>(a.params)) & 15)
     return hipErrorInvalidValue;
   const int nb = bc_head_sumsq_blocks(a.n_params), n_head = a.NH / 64;
-  hipLaunchKernelGGL(bc_head_train_kernel, dim3(n_head + nb), dim3(kThreads), bc_head_lds_bytes(a.B, a.NH, a.A), s, a,
-                     n_head);
+  const dim3 grid(n_head + nb), block(kThreads);
+  const size_t lds = bc_head_lds_bytes(a.B, a.NH, a.A);
+  if (a.NH == 512)
+    hipLaunchKernelGGL(bc_head_train_kernel<8>, grid, block, lds, s, a, n_head);
+  else
+    hipLaunchKernelGGL(bc_head_train_kernel<4>, grid, block, lds, s, a, n_head);
   return hipGetLastError();
 }
 

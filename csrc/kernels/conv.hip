@@ -515,10 +515,45 @@ hipError_t launch_wgrad(const TIn* X, const bf16* dY, const bf16* Y, float* slab
   }
   if (e != hipSuccess) return e;
   (void)M;
+  if (!dW) return hipSuccess;  // reduction deferred to conv_reduce_multi
   const int K = g.Kp;
   const int len = g.N * K + g.N;
   hipLaunchKernelGGL(conv_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, s, slab, nblk, len, dW, db, g.N * K, g);
   return hipGetLastError();
+}
+
+// the deferred reductions of several layers' wgrad slabs in one launch (blockIdx.y = layer)
+__global__ __launch_bounds__(256) void conv_reduce_multi_kernel(ConvReduceMulti r) {
+  const int l = blockIdx.y;
+  const ConvGeo& g = r.g[l];
+  const int nblk = r.nblk[l];
+  const int len = g.N * g.Kp + g.N;
+  if ((int)(blockIdx.x * 256) >= len) return;
+  // (same fixed-order body as conv_reduce_kernel)
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  const float* slab = r.slab[l];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = 0;
+  for (; b + 3 < nblk; b += 4) {
+    s0 += slab[(size_t)b * len + i];
+    s1 += slab[(size_t)(b + 1) * len + i];
+    s2 += slab[(size_t)(b + 2) * len + i];
+    s3 += slab[(size_t)(b + 3) * len + i];
+  }
+  for (; b < nblk; ++b) s0 += slab[(size_t)b * len + i];
+  const float sum = (s0 + s1) + (s2 + s3);
+  const int nk = g.N * g.Kp;
+  if (i < nk) {
+    const int n = i / g.Kp, k = i - n * g.Kp;
+    const int taps = g.KH * g.KW;
+    if (k < taps * g.C) {
+      const int tap = k / g.C, c = k - tap * g.C;
+      r.dW[l][((size_t)n * g.C + c) * taps + tap] = sum;
+    }
+  } else if (r.db[l]) {
+    r.db[l][i - nk] = sum;
+  }
 }
 
 // fp32 torch-layout conv weights [N][C][KH][KW] of up to kMaxPack layers -> bf16 [N][KH][KW][C]
@@ -637,6 +672,21 @@ void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* mpb) {
   b = (chunks + cpb - 1) / cpb;
   *nblk = b;
   *mpb = cpb * CH;
+}
+
+hipError_t conv_reduce_multi(const ConvReduceMulti& r, hipStream_t s) {
+  if (r.n <= 0) return hipSuccess;
+  if (r.n > kMaxPack) return hipErrorInvalidValue;
+  ConvReduceMulti rr = r;
+  int maxlen = 0;
+  for (int l = 0; l < r.n; ++l) {
+    int mpb = 0;
+    conv_wgrad_blocks(r.g[l], &rr.nblk[l], &mpb);
+    const int len = r.g[l].N * r.g[l].Kp + r.g[l].N;
+    maxlen = len > maxlen ? len : maxlen;
+  }
+  hipLaunchKernelGGL(conv_reduce_multi_kernel, dim3((maxlen + 255) / 256, r.n), dim3(256), 0, s, rr);
+  return hipGetLastError();
 }
 
 size_t conv_wgrad_slab_floats(const ConvGeo& g) {

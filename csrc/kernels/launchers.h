@@ -264,7 +264,7 @@ struct CnnHeadArgs {
 hipError_t cnn_head(const CnnHeadArgs& a, hipStream_t s);
 
 // ---- bc_head.hip: categorical BC head (logits, loss metrics, dW / db / dh) + ||theta||^2 in
-// one launch (B <= 64, NH % 64 == 0 and <= 512, A <= 8)
+// one launch (B <= 64, NH 256 or 512, A <= 8)
 struct BcHeadArgs {
   const float *h, *W, *b;   // features [B, NH] (16-B aligned), head weight [A, NH] (16-B aligned), bias [A]
   const int64_t* acts;      // [B]
@@ -276,6 +276,7 @@ struct BcHeadArgs {
   float* metrics;           // [7]: neglogp, entropy, ent_loss, prob_true_act, l2_norm, l2_loss, loss
   float* partials;          // [bc_head_sumsq_blocks(n_params)]
   unsigned* cnt;            // zero-initialised hand-off counter (left zero)
+  long long* prof;          // optional phase clocks of block 0 (tools/bc_head_probe.py)
 };
 bool bc_head_ok(int B, int NH, int A);
 int bc_head_sumsq_blocks(long n_params);
@@ -412,6 +413,17 @@ struct ConvPair {
 hipError_t conv_fwd_pair(int in_kind, const ConvPair& p, const ConvGeo& g, float in_scale, int relu, hipStream_t s);
 void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* m_per_block);
 size_t conv_wgrad_slab_floats(const ConvGeo& g);
+// deferred wgrad reductions (conv_wgrad with dW == nullptr leaves its block partials in slab):
+// every layer's slab -> dW (torch layout) / db in one launch
+struct ConvReduceMulti {
+  int n;
+  ConvGeo g[kMaxPack];
+  const float* slab[kMaxPack];
+  float* dW[kMaxPack];
+  float* db[kMaxPack];
+  int nblk[kMaxPack];  // filled by conv_reduce_multi
+};
+hipError_t conv_reduce_multi(const ConvReduceMulti& r, hipStream_t s);
 // in_kind: 0 fp32, 1 bf16, 2 uint8 input; weights bf16 [N][KH][KW][C]; Y bf16 [B*OH*OW][N]
 hipError_t conv_forward(int in_kind, const void* X, const void* Wb, const float* bias, void* Y, const ConvGeo& g,
                         float in_scale, int relu, hipStream_t s);

@@ -16,7 +16,8 @@ One step without autograd, every gradient written straight into the ``FusedAdam`
   ``dL/dlogits``, ``dW`` / ``db`` of ``action_net`` into the bucket, ``dL/dh`` and the
   ``||theta||^2`` reduction over the whole parameter bucket;
 * the FC backward (dW, db into the bucket; dX in NHWC) and the conv stack backward (weight
-  gradients reduced into the bucket, data gradients with the ReLU masks fused);
+  gradient partials per layer, their fixed-order reductions into the bucket as ONE launch;
+  data gradients with the ReLU masks fused);
 * the optimizer step is the caller's (one ``adam_flat`` launch).
 
 The value head is not evaluated: BC never uses it, and its bucket slice stays zero, as its
@@ -98,7 +99,7 @@ class FusedCnnBCStep:
                                      lin.out_features):
             return None
         B, NH, A = obs.shape[0], lin.out_features, policy.action_net.out_features
-        if not (0 < B <= 64 and NH % 64 == 0 and NH <= 512 and 0 < A <= 8):
+        if not (0 < B <= 64 and NH in (256, 512) and 0 < A <= 8):
             return None
         views = _grad_views(optimizer)
         if views is None or any(id(p) not in views for p in policy.parameters()):
@@ -133,14 +134,19 @@ class FusedCnnBCStep:
                                  self.metrics, self.ws, self.ent_weight, self.l2_weight)
             _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1])
             dz = dx.view(hs[-1].shape)
+            # weight-gradient partials per layer; their reductions in ONE launch at the end
+            red = {k: [] for k in ("x", "dy", "kh", "kw", "s", "p", "slab", "dw", "db")}
             for i in range(n - 1, -1, -1):
                 c = convs[i]
                 inp = x if i == 0 else hs[i - 1]
                 top = i == n - 1
-                C.conv_wgrad(inp, dz, hs[i], int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0]),
-                             1.0 / 255.0 if i == 0 else 1.0, top, 0, self.g_conv[i][0], self.g_conv[i][1])
+                kh, kw, st = int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0])
+                slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
+                for k, v in zip(red, (inp, dz, kh, kw, st, 0, slab, self.g_conv[i][0], self.g_conv[i][1])):
+                    red[k].append(v)
                 if i > 0:
-                    dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], int(c.stride[0]), top, True, 0)
+                    dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], st, top, True, 0)
+            C.conv_reduce_multi(*red.values())
         return self.metrics
 
 
