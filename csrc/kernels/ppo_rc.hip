@@ -1490,12 +1490,18 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
   const int s0 = (a.D + 3) / 4;
   const int nblk = g.ns ? 2 * g.G : g.G;
-  {  // every cooperating workgroup on one XCD (<= 32 workgroups; IMITATION_AMD_PPO_XCD=0 turns it
-     // off). GAIL emulated W = 2 / 4 / 8: 3.14 / 3.28 / 3.64 -> 2.99 / 2.96 / 3.36 ms per update,
+  {  // cooperating workgroups on as few XCDs as possible (IMITATION_AMD_PPO_XCD=0 turns it off;
+     // the "xcd" geometry field is the block stride). GAIL emulated W = 2 / 4 / 8: 3.14 / 3.28 / 3.64 -> 2.99 / 2.96 / 3.36 ms per update,
      // headline round 3.63 -> 3.55 ms (profiles/r3_ppo_xcd.md)
+    // At most 16 workgroups (half an XCD's 32 CUs) per XCD, so concurrent work on the other
+    // stream (the discriminator) never holds a CU a spinning cooperating workgroup waits for:
+    // stride 8 / 4 / 2 for <= 16 / 32 / 64 workgroups (blocks b % stride == 0 work: XCDs {0},
+    // {0, 4}, {0, 2, 4, 6} of the deal). DRLHP emulated W = 8 (32 workgroups): one XCD 27.3 ms,
+    // spread 25.6 ms (profiles/r3_ppo_xcd.md).
     const char* ev = getenv("IMITATION_AMD_PPO_XCD");
     const bool on = ev ? ev[0] == '1' : true;
-    g.xcd = on && nblk > 1 && nblk <= 32 ? 8 : 1;
+    g.xcd = 1;
+    if (on && nblk > 1) g.xcd = nblk <= 16 ? 8 : nblk <= 32 ? 4 : nblk <= 64 ? 2 : 1;
   }
   const dim3 grid(nblk * g.xcd), block(64 * g.nw);
   int wmx = g.n_witems, bmx = g.n_items - g.n_witems;
