@@ -36,8 +36,8 @@ import numpy as np
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--engine", choices=["auto", "device", "host"], default=os.environ.get("IA_BENCH_ENGINE", "auto"))
     p.add_argument("--env", default="HalfCheetah-v4")
     p.add_argument("--eval-episodes", type=int, default=8, help="final eval return (after timing); 0 = skip")
@@ -91,17 +91,17 @@ def main():
     n_steps = trainer.gen_algo.n_steps
     steps_per_round = trainer.gen_train_timesteps
 
-    def one_round():
-        trainer.train(steps_per_round)
-
-    for _ in range(args.warmup):
-        one_round()
+    # W warm-up rounds, then K timed rounds as ONE train() call, as a training run issues them:
+    # the trainer enqueues round r + 1's rollout behind round r's PPO update before it logs
+    # round r, so the device never waits for the host between rounds (one call per round
+    # would end every round with a host round trip)
+    if args.warmup:
+        trainer.train(steps_per_round * args.warmup)
     pdist.barrier()
     if device.type == "cuda":
         th.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_round()
+    trainer.train(steps_per_round * args.steps)
     if device.type == "cuda":
         th.cuda.synchronize()
     pdist.barrier()

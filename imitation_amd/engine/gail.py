@@ -497,6 +497,51 @@ class DeviceGeneratorCore:
         self._host_staged = True
         return ev
 
+def flatten_order(dones: np.ndarray, ep_lens_running: np.ndarray):
+    """Replay order of one round's ``[T, N]`` transitions as BufferingWrapper -> flatten ->
+    FIFO store produces it: finished episodes in completion order ((end step, env) row-major),
+    each in time order, then every env's unfinished tail, by env. Vectorised (no Python loop
+    over steps: this runs on the host between a rollout and its discriminator updates).
+
+    Returns ``(order, fin_t, fin_n, ep_lens, ep_lens_running')``: flat row indices
+    ``t * N + n``, the end step / env of each finished episode, its full length (including the
+    steps carried from earlier rounds, ``ep_lens_running``) and the updated carry."""
+    T, N = dones.shape
+    ep_lens_running = np.asarray(ep_lens_running, dtype=np.int64)
+    fin_t, fin_n = np.nonzero(dones)  # row-major: by end step, then env
+    # episode starts: previous done of the same env + 1 (0 for its first done this round)
+    by_env = np.lexsort((fin_t, fin_n))
+    t_env, n_env = fin_t[by_env], fin_n[by_env]
+    first = np.ones(len(by_env), dtype=bool)
+    first[1:] = n_env[1:] != n_env[:-1]
+    s_env = np.where(first, 0, np.concatenate(([0], t_env[:-1] + 1)))
+    starts = np.empty_like(s_env)
+    starts[by_env] = s_env
+    is_first = np.empty_like(first)
+    is_first[by_env] = first
+    lens = fin_t - starts + 1
+    ep_lens = (lens + np.where(is_first, ep_lens_running[fin_n], 0)).astype(np.int64)
+    # tails: from the last done + 1 (or 0) to T - 1
+    seg_start = np.zeros(N, dtype=np.int64)
+    last = np.ones(len(by_env), dtype=bool)
+    last[:-1] = n_env[:-1] != n_env[1:]
+    seg_start[n_env[last]] = t_env[last] + 1
+    done_any = np.zeros(N, dtype=bool)
+    done_any[n_env] = True
+    running = np.where(done_any, T - seg_start, ep_lens_running + T)
+    tail_n = np.flatnonzero(seg_start < T)
+    tail_s = seg_start[tail_n]
+    # concatenated ranges [s, e] -> row indices, episodes first, then tails
+    seg_s = np.concatenate((starts, tail_s))
+    seg_len = np.concatenate((lens, T - tail_s))
+    seg_env = np.concatenate((fin_n, tail_n))
+    total = int(seg_len.sum())
+    offs = np.repeat(np.cumsum(seg_len) - seg_len, seg_len)
+    t_rows = np.repeat(seg_s, seg_len) + (np.arange(total) - offs)
+    order = t_rows * N + np.repeat(seg_env, seg_len)
+    return order.astype(np.int64), fin_t, fin_n, ep_lens.tolist(), running
+
+
 class DeviceEngineMixin(DeviceGeneratorCore):
     """Device generator rounds (rollout -> GAE -> PPO -> replay store) and the fused
     discriminator update for an :class:`~imitation_amd.algorithms.adversarial.common.AdversarialTrainer`
@@ -534,26 +579,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             dones = self.buf["dones"].to("cpu", non_blocking=False).numpy().astype(bool)  # [T, N] (one sync / round)
             ep_ret_host = None
         T, N = dones.shape
-        finished: List[Tuple[int, int, int, int]] = []  # (end_t, env, start_t, len)
-        partial: List[Tuple[int, int, int]] = []
-        seg_start = np.zeros(N, dtype=np.int64)
-        ep_lens = []
-        for t in range(T):
-            for n in np.flatnonzero(dones[t]):
-                finished.append((t, n, int(seg_start[n]), t - int(seg_start[n]) + 1))
-                ep_lens.append(int(self._ep_lens_running[n] + t - seg_start[n] + 1))
-                self._ep_lens_running[n] = 0
-                seg_start[n] = t + 1
-        for n in range(N):
-            if seg_start[n] < T:
-                partial.append((n, int(seg_start[n]), T - int(seg_start[n])))
-                self._ep_lens_running[n] += T - seg_start[n]
-        order = []
-        for (t, n, s, ln) in finished:
-            order.extend(((np.arange(s, t + 1)) * N + n).tolist())
-        for (n, s, ln) in partial:
-            order.extend(((np.arange(s, T)) * N + n).tolist())
-        order = np.asarray(order, dtype=np.int64)
+        order, fin_t, fin_n, ep_lens, self._ep_lens_running = flatten_order(dones, self._ep_lens_running)
         cap = self._gen_dev.capacity
         keep = th.as_tensor(order[-cap:], device=self._dev)
         rows = T * N
@@ -573,14 +599,14 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             ep_lens = [] if lo > -neg_hi else sorted({int(lo), int(-neg_hi)})
         self._check_fixed_horizon(ep_lens)
         # Monitor-style episode stats for the generator logger
-        if finished:
+        if len(fin_t):
             ep_ret = ep_ret_host if ep_ret_host is not None else self.buf["ep_ret_out"].cpu().numpy()
             algo = self.gen_algo
             if algo.ep_info_buffer is None:
                 import collections
 
                 algo.ep_info_buffer = collections.deque(maxlen=algo._stats_window_size)
-            for (t, n, s, ln), l_full in zip(finished, local_lens):
+            for t, n, l_full in zip(fin_t.tolist(), fin_n.tolist(), local_lens):
                 algo.ep_info_buffer.append({"r": float(ep_ret[t, n]), "l": int(l_full), "t": 0.0})
 
     def _gen_sample(self, batch_size: int) -> Dict[str, th.Tensor]:

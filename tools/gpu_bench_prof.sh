@@ -4,6 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_bench -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log 2>&1 || { echo "prof failed rc=$?"; tail -5 $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log; exit 1; }
 cd $GRAFT_REPO_ROOT && python tools/prof_summary.py $(find gpurun_out/prof_bench -name "*.db" | head -1) 25 > gpurun_out/prof_bench_summary.md
+python tools/prof_timeline.py $(find gpurun_out/prof_bench -name "*.db" | head -1) rollout_chain_kernel 6 > gpurun_out/prof_bench_timeline.md || true
 rm -rf gpurun_out/prof_bench
 tail -1 gpurun_out/prof_bench.log
 head -16 gpurun_out/prof_bench_summary.md
