@@ -73,19 +73,21 @@ def make_step(name, device, rank, args):
         b = models.build(name, device=device, seed=args.seed, rank=rank)
         tr = b.trainer
 
-        def step():
-            tr.train(tr.gen_train_timesteps)
-            return tr.gen_train_timesteps
+        def step(k: int = 1):  # k rounds in one train() call (round r + 1 enqueued behind r)
+            tr.train(k * tr.gen_train_timesteps)
+            return k * tr.gen_train_timesteps
 
+        step.multi = True
         return b, step, "env-steps/s", tr.gen_algo.policy, b.venv
     if name == "airl_hopper":
         b = models.build(name, device=device, seed=args.seed, rank=rank)
         tr = b.trainer
 
-        def step():
-            tr.train(tr.gen_train_timesteps)
-            return tr.gen_train_timesteps
+        def step(k: int = 1):  # k rounds in one train() call (round r + 1 enqueued behind r)
+            tr.train(k * tr.gen_train_timesteps)
+            return k * tr.gen_train_timesteps
 
+        step.multi = True
         return b, step, "env-steps/s", tr.gen_algo.policy, b.venv
     if name == "dagger_pong":
         b = models.build(name, device=device, seed=args.seed, rank=rank)
@@ -119,14 +121,22 @@ def run_config(name, args, device, rank, world):
     from imitation_amd.parallel import dist as pdist
 
     b, step, unit, policy, venv = make_step(name, device, rank, args)
-    for _ in range(args.warmup):
-        step()
+    multi = getattr(step, "multi", False)  # the step runs k rounds in one call (as training does)
+    if multi:
+        if args.warmup:
+            step(args.warmup)
+    else:
+        for _ in range(args.warmup):
+            step()
     pdist.barrier()
     _sync(device)
     t0 = time.perf_counter()
     units = 0
-    for _ in range(args.steps):
-        units += step()
+    if multi:
+        units = step(args.steps)
+    else:
+        for _ in range(args.steps):
+            units += step()
     _sync(device)
     pdist.barrier()
     dt = pdist.allreduce_scalars([time.perf_counter() - t0], op="max")[0]
