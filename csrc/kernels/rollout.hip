@@ -45,11 +45,10 @@ struct Actor {
 };
 
 __host__ __device__ __forceinline__ int split_kh(int din) { return ((din + 1) / 2 + 3) & ~3; }
-__host__ __device__ __forceinline__ int full_lds_floats(const WaveMLP& m) {
-  int f = 0;
-  for (int l = 0; l < m.n_layers; ++l) f += ((m.dims[l] + 3) & ~3) * 64;
-  return f;
-}
+// full form: every layer's image padded to 64 inputs (16 groups of 4), so the forward loop has
+// a compile-time trip count and issues all its LDS loads back to back
+constexpr int kFullGroups = 16;
+__host__ __device__ __forceinline__ int full_lds_floats(const WaveMLP& m) { return m.n_layers * 4 * kFullGroups * 64; }
 
 template <bool SPLIT>
 __device__ void load_actor(const WaveMLP& m, Actor<SPLIT>& r, lf* wlds) {
@@ -62,7 +61,7 @@ __device__ void load_actor(const WaveMLP& m, Actor<SPLIT>& r, lf* wlds) {
   for (int l = 0; l < kWaveMaxLayers; ++l) {
     const bool on = l < m.n_layers;
     const int din = on ? m.dims[l] : 0, dout = on ? m.dims[l + 1] : 0;
-    const int kh = SPLIT ? split_kh(din) : ((din + 3) & ~3);
+    const int kh = SPLIT ? split_kh(din) : 4 * kFullGroups;
     const int k0 = h ? kh : 0;
     r.k0[l] = k0;
     r.ng[l] = kh >> 2;
@@ -128,13 +127,17 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
         }
       } else {
         const lf4* w4 = (const lf4*)r.wt[l] + lane;
-        for (int g = 0; g < r.ng[l]; ++g) {
+        float acc2 = 0.f, acc3 = 0.f;
+#pragma unroll
+        for (int g = 0; g < kFullGroups; ++g) {  // zero-padded past din (weights and inputs)
           const f32v4 v = src[g], w = w4[g * 64];
           acc0 = fmaf(w.x, v.x, acc0);
           acc1 = fmaf(w.y, v.y, acc1);
-          acc0 = fmaf(w.z, v.z, acc0);
-          acc1 = fmaf(w.w, v.w, acc1);
+          acc2 = fmaf(w.z, v.z, acc2);
+          acc3 = fmaf(w.w, v.w, acc3);
         }
+        acc0 += acc2;
+        acc1 += acc3;
       }
       float acc = acc0 + acc1;
       if (SPLIT) acc = add_halves(acc);
