@@ -70,6 +70,14 @@ void register_comm(py::module& m) {
         py::arg("n"), py::arg("stage"), py::arg("elem_bytes") = 4);
   m.def("oneshot_allreduce", &oneshot_allreduce, "one-shot sum all-reduce of in*scale over the mapped ranks into out");
   m.def("oneshot_error", &oneshot_error, "error word of a local region (1: a block timed out)");
+  m.def("oneshot_error_async",
+        [](int64_t local, torch::Tensor pinned) {
+          TORCH_CHECK(!pinned.is_cuda() && pinned.is_pinned() && pinned.scalar_type() == torch::kInt32 && pinned.numel() >= 1,
+                      "oneshot_error_async: pinned int32 host tensor");
+          IA_HIP_CHECK(ia::oneshot_read_error_async(reinterpret_cast<void*>((uintptr_t)local), pinned.data_ptr<int>(),
+                                                    ia_stream()));
+        },
+        "stream-ordered copy of the error word into a pinned host int32 tensor");
   m.def("oneshot_clear_error",
         [](int64_t p) { IA_HIP_CHECK(ia::oneshot_clear_error(reinterpret_cast<void*>((uintptr_t)p))); });
 }

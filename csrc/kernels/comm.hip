@@ -213,6 +213,10 @@ hipError_t oneshot_read_error(void* local, int* err) {
   return e;
 }
 
+hipError_t oneshot_read_error_async(void* local, int* host_pinned, hipStream_t s) {
+  return hipMemcpyAsync(host_pinned, static_cast<char*>(local) + kErrOff, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+}
+
 hipError_t oneshot_clear_error(void* local) { return hipMemset(static_cast<char*>(local) + kErrOff, 0, sizeof(unsigned)); }
 
 long long oneshot_ticks_per_second() {

@@ -455,6 +455,8 @@ hipError_t oneshot_open(const void* handle, void** ptr);
 hipError_t oneshot_close(void* ptr);
 hipError_t oneshot_free(void* ptr);
 hipError_t oneshot_read_error(void* local, int* err);
+// stream-ordered copy of the error word into pinned host memory (no device-wide sync)
+hipError_t oneshot_read_error_async(void* local, int* host_pinned, hipStream_t s);
 hipError_t oneshot_clear_error(void* local);
 long long oneshot_ticks_per_second();
 hipError_t oneshot_allreduce(const OneShotArgs& a, hipStream_t s);

@@ -971,6 +971,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             if callback:
                 callback(r)
             self.logger.dump(self._global_step)
+        pdist.check_comm("GAIL training", blocking=True)
 
     def _launch_rollout(self) -> th.cuda.Event:
         """Enqueue one rollout (chain + post pass) and the async copy of its dones / returns to

@@ -184,17 +184,18 @@ def oneshot_active() -> bool:
     return world_size() > 1 and oneshot._COMM is not None
 
 
-def check_comm(where: str = "") -> None:
-    """Raise if a one-shot reduction since the last check timed out on a lost / stalled peer
-    (its output was poisoned with NaN). Cheap (one 4-byte D2H read); call it at a host sync
-    the loop already has -- once per round / epoch / iteration."""
+def check_comm(where: str = "", blocking: bool = False) -> None:
+    """Raise if a one-shot reduction timed out on a lost / stalled peer (its output was
+    poisoned with NaN). Once per round / epoch / iteration: non-blocking (a stream-ordered
+    4-byte copy, read one check later -- see ``OneShotComm.check``); ``blocking`` at the end
+    of a training call."""
     if world_size() <= 1:
         return
     from imitation_amd.parallel import oneshot
 
     c = oneshot._COMM
     if c is not None:
-        c.check(where)
+        c.check(where, blocking=blocking)
 
 
 def allreduce_scalars(values: Sequence[float], op: str = "sum", device=None) -> List[float]:

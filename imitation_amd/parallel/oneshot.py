@@ -88,11 +88,29 @@ class OneShotComm:
     def clear_error(self) -> None:
         self._C.oneshot_clear_error(self.local)
 
-    def check(self, where: str = "") -> None:
+    def check(self, where: str = "", blocking: bool = False) -> None:
         """Raise if a bounded wait of this communicator timed out (a lost or stalled peer:
-        the kernel wrote NaN into that reduction's output). Called at the once-per-round host
-        syncs of the training loops, so a lost peer stops the run instead of training on NaN."""
-        err = self.error()
+        the kernel wrote NaN into that reduction's output). Called once per round / epoch by
+        the training loops, so a lost peer stops the run instead of training on NaN.
+
+        Non-blocking by default: a stream-ordered copy of the error word into pinned memory
+        is enqueued, and the copy enqueued by the PREVIOUS check is read if it has landed
+        (a synchronous read would wait for every stream -- including a next round the loop
+        has already enqueued -- and serialise the pipelined rounds). ``blocking``: read now."""
+        if blocking:
+            err = self.error()
+        else:
+            err = 0
+            ev = getattr(self, "_err_ev", None)
+            if ev is not None and ev.query():
+                err = int(self._err_host[0])
+            if not hasattr(self, "_err_host"):
+                self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            if ev is None or ev.query():  # one copy in flight at a time
+                with torch.cuda.device(self.device):
+                    self._C.oneshot_error_async(self.local, self._err_host)
+                    self._err_ev = torch.cuda.Event()
+                    self._err_ev.record()
         if err:
             self.clear_error()
             raise RuntimeError(f"one-shot all-reduce timed out waiting for a peer{(' (' + where + ')') if where else ''}: "

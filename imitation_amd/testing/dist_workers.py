@@ -291,7 +291,7 @@ def oneshot_timeout_worker(rank, world, timeout_s):
         th.cuda.synchronize(c.device)
         res = {"all_nan": bool(th.isnan(x).all().item()), "error": c.error()}
         try:  # the training loops' once-per-round check raises and clears the word
-            c.check("test")
+            c.check("test", blocking=True)
             res["raised"] = False
         except RuntimeError:
             res["raised"] = True
