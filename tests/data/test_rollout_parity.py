@@ -1,0 +1,168 @@
+"""Rollout behaviours of the reference's tests/data/test_rollout.py, expressed against this
+package: seeding, unwrapping RolloutInfoWrapper records under obs / reward wrappers, sample-until
+validation, discounted returns, policy type / shape errors and Dict observations (CPU)."""
+
+import numpy as np
+import pytest
+
+from imitation_amd.data import rollout, types, wrappers
+from imitation_amd.envs import core, spaces
+from imitation_amd.envs.vec_env import DummyVecEnv
+from imitation_amd.policies.base import RandomPolicy
+from imitation_amd.util import util
+
+
+class _Counter(core.Env):
+    """obs = step count, reward = step count, episode of fixed length."""
+
+    def __init__(self, length: int = 5):
+        self.length = length
+        self.t = 0
+        self.action_space = spaces.Discrete(2)
+        self.observation_space = spaces.Box(np.array([0.0]), np.array([100.0]), dtype=np.float32)
+
+    def reset(self, *, seed=None, options=None):
+        self.t = 0
+        return np.array([0.0], dtype=np.float32), {}
+
+    def step(self, action):
+        self.t += 1
+        return np.array([float(self.t)], dtype=np.float32), float(self.t), self.t >= self.length, False, {}
+
+
+class _HalveObsRew(core.Wrapper):
+    """Halves observations and rewards on top of the recorded env."""
+
+    def reset(self, **kwargs):
+        obs, info = self.env.reset(**kwargs)
+        return obs / 2, info
+
+    def step(self, action):
+        obs, rew, term, trunc, info = self.env.step(action)
+        return obs / 2, rew / 2, term, trunc, info
+
+
+class _DictEnv(core.Env):
+    def __init__(self):
+        self.action_space = spaces.Discrete(3)
+        self.observation_space = spaces.Dict({"a": spaces.Box(-1.0, 1.0, (2,)), "b": spaces.Discrete(4)})
+        self.t = 0
+
+    def reset(self, *, seed=None, options=None):
+        self.t = 0
+        return {"a": np.zeros(2, np.float32), "b": 0}, {}
+
+    def step(self, action):
+        self.t += 1
+        obs = {"a": np.full(2, self.t / 10, np.float32), "b": int(action)}
+        return obs, 1.0, self.t >= 4, False, {}
+
+
+def _random_policy(venv):
+    return RandomPolicy(venv.observation_space, venv.action_space)
+
+
+def _native(seed, n_envs=2):
+    return util.make_vec_env("CartPole-v1", rng=np.random.default_rng(seed), n_envs=n_envs)
+
+
+def test_same_seed_same_trajectories():
+    def run(seed):
+        venv = _native(0)
+        venv.action_space.seed(seed)
+        return rollout.generate_trajectories(_random_policy(venv), venv, rollout.make_min_episodes(4),
+                                             rng=np.random.default_rng(seed))
+
+    a, b, c = run(3), run(3), run(4)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.obs, y.obs)
+        np.testing.assert_array_equal(x.acts, y.acts)
+    assert any(len(x) != len(y) or not np.array_equal(x.acts, y.acts) for x, y in zip(a, c)) or len(a) != len(c)
+
+
+def test_unwrap_traj_recovers_the_recorded_env():
+    venv = DummyVecEnv([lambda: _HalveObsRew(wrappers.RolloutInfoWrapper(_Counter(5)))])
+    trajs = rollout.generate_trajectories(_random_policy(venv), venv, rollout.make_min_episodes(2),
+                                          rng=np.random.default_rng(0))
+    for t in trajs:
+        np.testing.assert_allclose(t.obs.reshape(-1), np.arange(6) / 2)
+        np.testing.assert_allclose(t.rews, np.arange(1, 6) / 2)
+        u = rollout.unwrap_traj(t)
+        np.testing.assert_allclose(u.obs.reshape(-1), np.arange(6))
+        np.testing.assert_allclose(u.rews, np.arange(1, 6))
+        np.testing.assert_array_equal(u.acts, t.acts)
+
+
+def test_unwrap_traj_needs_infos():
+    traj = types.TrajectoryWithRew(obs=np.zeros((3, 1)), acts=np.zeros(2), infos=None, terminal=True, rews=np.zeros(2))
+    with pytest.raises(ValueError, match="infos"):
+        rollout.unwrap_traj(traj)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(min_timesteps=0), dict(min_timesteps=-3), dict(min_episodes=0),
+                                dict(min_episodes=-1), dict(min_timesteps=-1, min_episodes=2)])
+def test_make_sample_until_validation(kw):
+    with pytest.raises(ValueError):
+        rollout.make_sample_until(**kw)
+
+
+def test_make_sample_until_combines_conditions():
+    t = types.TrajectoryWithRew(obs=np.zeros((4, 1)), acts=np.zeros(3), infos=None, terminal=True, rews=np.zeros(3))
+    both = rollout.make_sample_until(min_timesteps=7, min_episodes=2)
+    assert not both([t])  # 3 steps, 1 episode
+    assert not both([t, t])  # 6 steps
+    assert both([t, t, t])
+    assert rollout.make_sample_until(min_episodes=2)([t, t])
+    assert not rollout.make_sample_until(min_timesteps=4)([t])
+
+
+@pytest.mark.parametrize("gamma", [0.0, 0.5, 0.9, 0.99, 1.0])
+def test_discounted_sum_matches_loop(gamma):
+    arr = np.random.default_rng(1).normal(size=17)
+    want = 0.0
+    for r in arr[::-1]:
+        want = r + gamma * want
+    assert rollout.discounted_sum(arr, gamma) == pytest.approx(want)
+    mat = np.random.default_rng(2).normal(size=(9, 3))
+    got = rollout.discounted_sum(mat, gamma)
+    for j in range(3):
+        assert got[j] == pytest.approx(rollout.discounted_sum(mat[:, j], gamma))
+
+
+def test_generate_trajectories_rejects_non_policies():
+    venv = _native(0)
+    with pytest.raises(TypeError):
+        rollout.generate_trajectories(42, venv, rollout.make_min_episodes(1), rng=np.random.default_rng(0))
+
+
+def test_deterministic_flag_with_a_callable_raises():
+    venv = _native(0)
+    with pytest.raises(ValueError, match="deterministic"):
+        rollout.generate_trajectories(lambda obs, state, start: (np.zeros(len(obs), dtype=int), None), venv,
+                                      rollout.make_min_episodes(1), rng=np.random.default_rng(0),
+                                      deterministic_policy=True)
+
+
+def test_dictionary_observations():
+    venv = DummyVecEnv([lambda: wrappers.RolloutInfoWrapper(_DictEnv()) for _ in range(2)])
+    trajs = rollout.generate_trajectories(_random_policy(venv), venv, rollout.make_min_episodes(3),
+                                          rng=np.random.default_rng(0))
+    assert len(trajs) >= 3
+    for t in trajs:
+        assert isinstance(t.obs, types.DictObs)
+        assert len(t.obs) == len(t.acts) + 1 == 5
+        np.testing.assert_allclose(t.obs.get("a")[:, 0], np.arange(5) / 10, rtol=1e-6)
+        np.testing.assert_array_equal(t.obs.get("b")[1:], t.acts)
+    flat = rollout.flatten_trajectories(trajs)
+    assert isinstance(flat.obs, types.DictObs) and len(flat) == sum(len(t) for t in trajs)
+
+
+def test_rollout_stats_of_known_returns():
+    trajs = [types.TrajectoryWithRew(obs=np.zeros((n + 1, 1)), acts=np.zeros(n), infos=None, terminal=True,
+                                     rews=np.full(n, float(r))) for n, r in ((2, 1.0), (4, 0.5), (3, -1.0))]
+    st = rollout.rollout_stats(trajs)
+    assert st["n_traj"] == 3
+    assert st["return_mean"] == pytest.approx(np.mean([2.0, 2.0, -3.0]))
+    assert st["len_mean"] == pytest.approx(3.0)
+    assert st["return_min"] == pytest.approx(-3.0) and st["return_max"] == pytest.approx(2.0)
