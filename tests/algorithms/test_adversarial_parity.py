@@ -1,0 +1,118 @@
+"""Adversarial-trainer behaviours of the reference's tests/algorithms/test_adversarial.py,
+expressed against this package (CPU): AIRL's stochastic-policy check, disc training errors,
+disc steps over expert batch sizes and demonstration formats, train_gen + train_disc,
+logits with / without the policy log-prob, and the train-stat dictionary."""
+
+import numpy as np
+import pytest
+import torch as th
+
+from imitation_amd.algorithms.adversarial import airl, common, gail
+from imitation_amd.data import rollout, types
+from imitation_amd.rewards import reward_nets
+from imitation_amd.rl.dqn import DQN
+from imitation_amd.rl.ppo import PPO
+from imitation_amd.util import networks, util
+
+KINDS = ["gail", "airl"]
+
+
+@pytest.fixture
+def expert_transitions(cartpole_expert_trajectories):
+    return rollout.flatten_trajectories(cartpole_expert_trajectories[:4])
+
+
+def _make(kind, venv, demos, batch, custom_logger=None, **kw):
+    gen = PPO("MlpPolicy", venv, n_steps=32, batch_size=32, n_epochs=1, seed=0, device="cpu",
+              policy_kwargs=dict(net_arch=[16, 16]))
+    if kind == "gail":
+        rn = reward_nets.BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=networks.RunningNorm)
+        cls = gail.GAIL
+    else:
+        rn = reward_nets.BasicShapedRewardNet(venv.observation_space, venv.action_space,
+                                              normalize_input_layer=networks.RunningNorm)
+        cls = airl.AIRL
+    return cls(demonstrations=demos, demo_batch_size=batch, venv=venv, gen_algo=gen, reward_net=rn,
+               custom_logger=custom_logger, **kw)
+
+
+def test_airl_fails_fast_on_a_deterministic_generator(rng, custom_logger):
+    venv = util.make_vec_env("seals/CartPole-v0", n_envs=1, rng=rng)
+    gen = DQN("MlpPolicy", venv, device="cpu", learning_starts=0)
+    demos = rollout.generate_transitions(None, venv, n_timesteps=20, rng=rng)
+    rn = reward_nets.BasicShapedRewardNet(venv.observation_space, venv.action_space)
+    with pytest.raises(TypeError, match="AIRL needs a stochastic policy"):
+        airl.AIRL(demonstrations=demos, demo_batch_size=20, venv=venv, gen_algo=gen, reward_net=rn,
+                  custom_logger=custom_logger)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_train_disc_without_generator_samples_raises(kind, cartpole_venv, expert_transitions, custom_logger):
+    tr = _make(kind, cartpole_venv, expert_transitions, 32, custom_logger)
+    with pytest.raises(RuntimeError, match="No generator samples"):
+        tr.train_disc()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_train_disc_unequal_sample_counts_raise(kind, cartpole_venv, expert_transitions, custom_logger):
+    n = 32
+    tr = _make(kind, cartpole_venv, expert_transitions, n, custom_logger)
+    expert = types.dataclass_quick_asdict(expert_transitions[:n])
+    gen = types.dataclass_quick_asdict(expert_transitions[: n - 1])
+    with pytest.raises(ValueError, match="n_expert"):
+        tr.train_disc(expert_samples=expert, gen_samples=gen)
+
+
+@pytest.mark.parametrize("kind,batch,as_dicts", [(k, b, d) for k in KINDS for b in (1, 128) for d in (False, True)])
+def test_train_disc_step_over_batch_sizes_and_formats(kind, batch, as_dicts, cartpole_venv, expert_transitions, rng,
+                                                      custom_logger):
+    demos = expert_transitions
+    if as_dicts:  # an iterable of transition-mapping batches instead of a Transitions dataset
+        demos = [types.dataclass_quick_asdict(expert_transitions[i: i + batch])
+                 for i in range(0, len(expert_transitions) - batch + 1, batch)]
+    tr = _make(kind, cartpole_venv, demos, batch, custom_logger)
+    trans = rollout.generate_transitions(tr.gen_algo, cartpole_venv, n_timesteps=batch, truncate=True, rng=rng)
+    stats = tr.train_disc(gen_samples=types.dataclass_quick_asdict(trans))
+    assert np.isfinite(stats["disc_loss"])
+    assert 0.0 <= stats["disc_acc"] <= 1.0
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_train_gen_then_train_disc(kind, cartpole_venv, expert_transitions, custom_logger):
+    tr = _make(kind, cartpole_venv, expert_transitions, 32, custom_logger)
+    tr.train_gen(tr.gen_train_timesteps)
+    stats = tr.train_disc()
+    assert np.isfinite(stats["disc_loss"])
+    assert tr._gen_replay_buffer.size() > 0
+
+
+@pytest.mark.parametrize("kind,n", [(k, n) for k in KINDS for n in (2, 4, 10)])
+def test_logits_with_and_without_policy_log_prob(kind, n, cartpole_venv, expert_transitions, rng, custom_logger):
+    tr = _make(kind, cartpole_venv, expert_transitions, 32, custom_logger)
+    trans = rollout.generate_transitions(None, cartpole_venv, n_timesteps=n, rng=rng)
+    obs, acts, next_obs, dones = tr.reward_train.preprocess(trans.obs, trans.acts, trans.next_obs, trans.dones)
+    lp = th.as_tensor(np.log(0.1 + 0.9 * np.random.default_rng(n).random(len(trans))), dtype=th.float32)
+    tr._reward_net.eval()  # frozen input normalisers: repeated forwards see the same statistics
+    out = tr.logits_expert_is_high(obs, acts, next_obs, dones, lp)
+    assert out.shape == (len(trans),)
+    if kind == "airl":
+        with pytest.raises(TypeError, match="Non-None.*required"):
+            tr.logits_expert_is_high(obs, acts, next_obs, dones, None)
+        # AIRL logit = shaped reward - log pi(a|s)
+        r = tr._reward_net(obs, acts, next_obs, dones)
+        np.testing.assert_allclose(out.detach().numpy(), (r - lp).detach().numpy(), rtol=1e-5, atol=1e-6)
+    else:
+        out_none = tr.logits_expert_is_high(obs, acts, next_obs, dones, None)
+        np.testing.assert_allclose(out.detach().numpy(), out_none.detach().numpy())
+
+
+@pytest.mark.parametrize("n", [0, 1, 10, 40])
+def test_compute_train_stats_are_floats(n):
+    g = np.random.default_rng(n)
+    logits = th.from_numpy(g.standard_normal(n) * 10)
+    labels = th.from_numpy(g.integers(0, 2, size=n))
+    stats = common.compute_train_stats(logits, labels, th.tensor(g.random() * 10))
+    assert stats and all(isinstance(k, str) and isinstance(v, float) for k, v in stats.items())
+    if n:
+        pred_expert = (logits > 0).numpy()
+        assert stats["disc_acc"] == pytest.approx(float(np.mean(pred_expert == (labels.numpy() == 1))))
