@@ -368,7 +368,7 @@ torch::Tensor kde_score(torch::Tensor q, torch::Tensor x, double bandwidth, int6
 
 // rows b (x n_envs + e) of every source [R, ...] -> new [n, ...] tensors, one launch
 std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::Tensor b, c10::optional<torch::Tensor> e,
-                                       int64_t n_envs) {
+                                       int64_t n_envs, c10::optional<std::vector<torch::Tensor>> dst) {
   TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= ia::kGatherMax, "gather_rows: 1..8 fields");
   IA_CHECK_CUDA(b);
   IA_CHECK_CONTIG(b);
@@ -393,7 +393,16 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
     const int64_t rows = sizes[0];
     TORCH_CHECK(rows % (ep ? n_envs : 1) == 0, "gather_rows: rows must be a multiple of n_envs");
     sizes[0] = n;
-    auto o = torch::empty(sizes, t.options());
+    torch::Tensor o;
+    if (dst.has_value()) {  // caller-owned outputs (persistent buffers, e.g. a graph's static inputs)
+      TORCH_CHECK((int)dst->size() == a.k, "gather_rows: one dst per source");
+      o = (*dst)[i];
+      IA_CHECK_CONTIG(o);
+      TORCH_CHECK(o.sizes().vec() == sizes && o.scalar_type() == t.scalar_type() && o.device() == t.device(),
+                  "gather_rows: dst ", i, " shape / dtype / device");
+    } else {
+      o = torch::empty(sizes, t.options());
+    }
     a.f[i] = ia::GatherField{t.data_ptr(), o.data_ptr(), rows ? (int64_t)(t.nbytes() / rows) : 0, rows};
     outs.push_back(o);
   }
@@ -555,7 +564,8 @@ void register_kernels(py::module& m) {
   m.def("running_norm", &running_norm, py::arg("x"), py::arg("mean"), py::arg("var"), py::arg("count"), py::arg("eps"),
         py::arg("update"), py::arg("want_y"), py::arg("ema_inv_lr") = py::none(), py::arg("ema_num_batches") = py::none(),
         py::arg("ema_decay") = 0.0);
-  m.def("gather_rows", &gather_rows, py::arg("srcs"), py::arg("b"), py::arg("e") = py::none(), py::arg("n_envs") = 1);
+  m.def("gather_rows", &gather_rows, py::arg("srcs"), py::arg("b"), py::arg("e") = py::none(), py::arg("n_envs") = 1,
+        py::arg("dst") = py::none());
   m.def("soft_value_iteration", &soft_value_iteration, py::arg("T"), py::arg("R"), py::arg("H"), py::arg("gamma"));
   m.def("occupancy_measures", &occupancy_measures, py::arg("T"), py::arg("P"), py::arg("D0"));
   m.def("kde_score", &kde_score, py::arg("q"), py::arg("x"), py::arg("bandwidth"), py::arg("kind"), py::arg("offset"));

@@ -219,6 +219,19 @@ class DeviceDemoAggregate:
     def __len__(self) -> int:
         return self.n
 
+    def batch_buffers(self, batch_size: int):
+        """Persistent ``[obs, acts]`` minibatch buffers of ``batch_size`` rows (one pair per
+        size, reused by every loader over this aggregate), flagged ``_ia_static``."""
+        bufs = getattr(self, "_batch_bufs", {})
+        self._batch_bufs = bufs
+        if batch_size not in bufs:
+            pair = [th.empty((batch_size,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
+                    for t in (self.obs, self.acts)]
+            for t in pair:
+                t._ia_static = True
+            bufs[batch_size] = pair
+        return bufs[batch_size]
+
 
 class DeviceTransitionsLoader:
     """Shuffled, drop-last minibatches straight from a :class:`DeviceDemoAggregate`: one
@@ -241,8 +254,12 @@ class DeviceTransitionsLoader:
         self._epoch += 1
         perm = rl_ops.random_permutations(1, n, self._seed * 1000003 + self._epoch, self.agg.device)[0].long()
         obs, acts = self.agg.obs, self.agg.acts
+        bufs = self.agg.batch_buffers(self.batch_size)
         for s in range(0, n - n % self.batch_size, self.batch_size):
-            o, a = rl_ops.gather_rows([obs, acts], perm[s : s + self.batch_size])
+            # into the aggregate's persistent batch buffers: a graphed BC step captured on them
+            # reads them in place (utils/graphs.py ``_ia_static``), no per-step input copies;
+            # stream order keeps batch k + 1's gather behind step k's reads
+            o, a = rl_ops.gather_rows([obs, acts], perm[s : s + self.batch_size], dst=bufs)
             yield {"obs": o, "acts": a}
 
 

@@ -225,14 +225,19 @@ def bc_categorical_loss(logits, actions, params, ent_weight: float, l2_weight: f
     return m, m[6]
 
 
-def gather_rows(srcs, b: torch.Tensor, e: "torch.Tensor | None" = None, n_envs: int = 1):
+def gather_rows(srcs, b: torch.Tensor, e: "torch.Tensor | None" = None, n_envs: int = 1, dst=None):
     """``[s[b * n_envs + e] for s in srcs]`` (or ``s[b]``) for row-major sources ``[R, ...]``:
     one HIP launch for every field on the GPU (csrc/kernels/gather.hip), torch indexing on
-    the CPU. Out-of-range rows come back as zeros on the GPU."""
+    the CPU. Out-of-range rows come back as zeros on the GPU. ``dst``: caller-owned outputs."""
     from imitation_amd.ops import native, use_kernel
 
     srcs = list(srcs)
     if use_kernel(b) and 0 < len(srcs) <= 8 and all(s.is_cuda and s.is_contiguous() for s in srcs):
-        return native().gather_rows(srcs, b.long().contiguous(), None if e is None else e.long().contiguous(), int(n_envs))
+        return native().gather_rows(srcs, b.long().contiguous(), None if e is None else e.long().contiguous(), int(n_envs),
+                                    None if dst is None else list(dst))
     flat = b.long() if e is None else b.long() * n_envs + e.long()
+    if dst is not None:
+        for s, o in zip(srcs, dst):
+            torch.index_select(s, 0, flat, out=o)
+        return list(dst)
     return [s.index_select(0, flat) for s in srcs]

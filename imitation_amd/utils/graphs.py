@@ -69,14 +69,17 @@ class GraphedTrainStep:
         if entry is not None:
             static, graph, out = entry
             for s, t in zip(static, inputs):
-                s.copy_(t, non_blocking=True)
+                if s.data_ptr() != t.data_ptr():  # persistent (``_ia_static``) inputs are read in place
+                    s.copy_(t, non_blocking=True)
             graph.replay()
             self.n_replays += 1
             return out
         make_capturable(self.optimizer)
         if self.release is not None:
             self.release()
-        static = tuple(t.detach().clone() for t in inputs)
+        # inputs flagged ``_ia_static`` (persistent producer buffers, e.g. the DAgger loader's
+        # batch buffers) are captured in place: their replays need no input copy
+        static = tuple(t if getattr(t, "_ia_static", False) else t.detach().clone() for t in inputs)
         side = th.cuda.Stream()
         side.wait_stream(th.cuda.current_stream())
         with th.cuda.stream(side):  # warm-up == this step
