@@ -167,6 +167,9 @@ __global__ __launch_bounds__(64 * kPrepWaves) void ppo_rc_prep_kernel(PPOArgs a,
   const int k = blockIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int CH = g.G * g.nch, cw = g.cw, Bg = CH * cw, D = a.D;
+  // the main kernel's arrival counters / flags start at zero (stream order: it runs after
+  // this launch) -- replaces a separate memset launch per update
+  if (k == 0 && threadIdx.x < 64) g.sync[threadIdx.x] = 0u;
   const int n_mb = a.rows / Bg;
   const int e = k / n_mb, mb = k - e * n_mb;
   const bool ok = lane < cw;
@@ -1475,8 +1478,6 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
     g.xchg2 = ev ? (ev[0] == '1' && g.G > 1) : (g.G >= (g.kt == 4 ? 4 : 16));
   }
   if (K == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(g.sync, 0, 64 * sizeof(unsigned), s);
-  if (e != hipSuccess) return e;
   const int CH = g.G * g.nch;
   const int prep_waves = CH < kPrepWaves ? CH : kPrepWaves;
   hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64 * prep_waves), 0, s, a, g);

@@ -37,6 +37,8 @@ should use the host-loop trainers.
 
 from __future__ import annotations
 
+import contextlib
+
 import os
 import time
 from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple
@@ -490,10 +492,16 @@ class DeviceGeneratorCore:
         that marks them ready."""
         if not hasattr(self, "_host_stage"):
             self._host_stage = th.empty(2, self.T, self.N, pin_memory=True)
-        self._host_stage[0].copy_(self.buf["dones"], non_blocking=True)
-        self._host_stage[1].copy_(self.buf["ep_ret_out"], non_blocking=True)
-        ev = th.cuda.Event()
-        ev.record()
+        # on the side stream: the copies stay off the rollout -> GAE -> PPO chain (the host
+        # waits for this event before the next rollout can overwrite the buffers)
+        side = getattr(self, "_side_stream", None)
+        if side is not None:
+            side.wait_stream(th.cuda.current_stream(self._dev))
+        with th.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            self._host_stage[0].copy_(self.buf["dones"], non_blocking=True)
+            self._host_stage[1].copy_(self.buf["ep_ret_out"], non_blocking=True)
+            ev = th.cuda.Event()
+            ev.record()
         self._host_staged = True
         return ev
 
