@@ -1,0 +1,133 @@
+"""Exploration-wrapper and replay-buffer-reward-wrapper behaviours of the reference's
+tests/policies/test_exploration_wrapper.py and test_replay_buffer_wrapper.py, expressed
+against this package (CPU): switching statistics over random_prob / switch_prob, valid
+actions, stateful-policy errors, and SAC training through a relabelling buffer (sizes, ring
+position, reset, relabelled vs stored rewards, argument errors)."""
+
+import numpy as np
+import pytest
+import torch as th
+
+from imitation_amd.policies import exploration_wrapper
+from imitation_amd.policies.replay_buffer_wrapper import ReplayBufferRewardWrapper
+from imitation_amd.rl import buffers
+from imitation_amd.rl.ppo import PPO
+from imitation_amd.rl.sac import SAC
+from imitation_amd.util import util
+
+
+def _zeros(obs, state, start):
+    return np.zeros(len(obs), dtype=int), None
+
+
+def _stateful(obs, state, start):
+    return np.zeros(len(obs), dtype=int), (np.zeros(1),)
+
+
+def _wrap(random_prob, switch_prob, seed=0, policy=_zeros):
+    venv = util.make_vec_env("seals/CartPole-v0", n_envs=1, rng=np.random.default_rng(seed))
+    w = exploration_wrapper.ExplorationWrapper(policy, venv, random_prob=random_prob, switch_prob=switch_prob,
+                                               rng=np.random.default_rng(seed))
+    return w, venv
+
+
+def _is_random(w):
+    return w.current_policy == w._random_policy
+
+
+@pytest.mark.parametrize("random_prob", [0.0, 1.0])
+def test_extreme_random_prob_never_changes_kind(random_prob):
+    w, _ = _wrap(random_prob, 0.5)
+    for _ in range(200):
+        w._switch()
+        assert _is_random(w) == (random_prob == 1.0)
+
+
+def test_half_random_prob_switches_both_ways():
+    w, _ = _wrap(0.5, 0.5, seed=3)
+    kinds = []
+    for _ in range(2000):
+        w._switch()
+        kinds.append(_is_random(w))
+    frac = np.mean(kinds)
+    assert 0.45 < frac < 0.55
+
+
+def test_zero_switch_prob_keeps_the_first_choice():
+    w, venv = _wrap(0.5, 0.0, seed=1)
+    first = w.current_policy
+    obs = np.random.default_rng(0).random((100, 4))
+    for _ in range(50):
+        acts, state = w(obs, None, None)
+        assert state is None and w.current_policy == first
+        assert all(venv.action_space.contains(a) for a in acts)
+
+
+@pytest.mark.parametrize("random_prob,lo,hi", [(1.0, 1.0, 1.0), (0.5, 0.45, 0.55), (0.0, 0.0, 0.0)])
+def test_always_switch_follows_random_prob(random_prob, lo, hi):
+    w, _ = _wrap(random_prob, 1.0, seed=5)
+    kinds = []
+    for _ in range(4000):
+        w(np.zeros((1, 4)), None, None)
+        kinds.append(_is_random(w))
+    assert lo <= np.mean(kinds) <= hi
+
+
+@pytest.mark.parametrize("random_prob", [0.0, 0.5, 1.0])
+def test_actions_are_valid_for_every_mixture(random_prob):
+    w, venv = _wrap(random_prob, 0.5, seed=2)
+    for _ in range(20):
+        acts, _ = w(np.random.default_rng(1).random((64, 4)), None, None)
+        assert acts.shape == (64,) and all(venv.action_space.contains(a) for a in acts)
+
+
+def test_stateful_policies_are_rejected():
+    w, _ = _wrap(0.0, 0.0, policy=_stateful)
+    obs = np.zeros((10, 4))
+    with pytest.raises(ValueError, match="does not support stateful policies"):
+        w(obs, (np.ones_like(obs),), None)
+    with pytest.raises(ValueError, match="does not support stateful policies"):
+        w(obs, None, None)
+
+
+def _zero_reward(state, action, next_state, done):
+    return np.zeros(len(state), dtype=np.float32)
+
+
+def _sac(buffer_size, replay_buffer_class=buffers.ReplayBuffer):
+    venv = util.make_vec_env("Pendulum-v1", n_envs=1, rng=np.random.default_rng(0))
+    return SAC("MlpPolicy", venv, seed=42, buffer_size=buffer_size, learning_starts=5, device="cpu",
+               replay_buffer_class=ReplayBufferRewardWrapper,
+               replay_buffer_kwargs=dict(replay_buffer_class=replay_buffer_class, reward_fn=_zero_reward))
+
+
+def test_only_plain_replay_buffers_can_be_wrapped():
+    class _Other(buffers.ReplayBuffer):
+        pass
+
+    with pytest.raises(AssertionError, match="only ReplayBuffer is supported"):
+        _sac(10, replay_buffer_class=_Other)
+
+
+def test_on_policy_algorithms_take_no_replay_buffer():
+    venv = util.make_vec_env("Pendulum-v1", n_envs=1, rng=np.random.default_rng(0))
+    with pytest.raises(TypeError, match="replay_buffer_class"):
+        PPO("MlpPolicy", venv, replay_buffer_class=ReplayBufferRewardWrapper, device="cpu")
+
+
+def test_sac_trains_through_the_relabelling_buffer():
+    buffer_size, steps = 15, 20
+    algo = _sac(buffer_size)
+    algo.learn(total_timesteps=steps)
+    wrapper = algo.replay_buffer
+    inner = wrapper.replay_buffer
+    assert isinstance(wrapper, ReplayBufferRewardWrapper)
+    assert wrapper.size() == inner.size() == buffer_size
+    assert wrapper.full and wrapper.pos == steps - buffer_size
+    assert th.all(wrapper.sample(steps).rewards == 0.0)  # relabelled by the reward function
+    assert th.all(inner.sample(steps).rewards != 0.0)  # Pendulum's own rewards are stored
+    wrapper.reset()
+    assert wrapper.size() == inner.size() == 0 and wrapper.pos == 0 and not wrapper.full
+    assert isinstance(wrapper.to_torch(np.ones(42)), th.Tensor)
+    with pytest.raises(NotImplementedError, match="_get_samples"):
+        wrapper._get_samples()
