@@ -27,7 +27,7 @@ from imitation_amd.envs import spaces
 from imitation_amd.envs.vec_env import DummyVecEnv, Monitor, VecEnv, VecNormalize
 from imitation_amd.rl import logger as rl_logger
 from imitation_amd.rl import save_util
-from imitation_amd.rl.buffers import ReplayBuffer, RolloutBuffer
+from imitation_amd.rl.buffers import DictRolloutBuffer, ReplayBuffer, RolloutBuffer
 from imitation_amd.rl.callbacks import BaseCallback, CallbackList, ConvertCallback, convert_callback
 from imitation_amd.rl.policies import BasePolicy, get_device, get_schedule_fn, obs_as_tensor
 
@@ -440,7 +440,8 @@ class OnPolicyAlgorithm(BaseAlgorithm):
     def _setup_model(self) -> None:
         self._setup_lr_schedule()
         self.set_random_seed(self.seed)
-        buffer_cls = self.rollout_buffer_class or RolloutBuffer
+        buffer_cls = self.rollout_buffer_class or (DictRolloutBuffer if isinstance(self.observation_space, spaces.Dict)
+                                                   else RolloutBuffer)
         self.rollout_buffer = buffer_cls(self.n_steps, self.observation_space, self.action_space, device=self.device,
                                          gamma=self.gamma, gae_lambda=self.gae_lambda, n_envs=self.n_envs,
                                          **self.rollout_buffer_kwargs)

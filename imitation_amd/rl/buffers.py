@@ -157,6 +157,55 @@ class RolloutBuffer(BaseBuffer):
         )
 
 
+class DictRolloutBuffer(RolloutBuffer):
+    """:class:`RolloutBuffer` for ``spaces.Dict`` observations (SB3 ``DictRolloutBuffer``): one
+    device tensor ``[n_steps, n_envs, *shape]`` per observation key; minibatches carry a dict."""
+
+    def reset(self) -> None:
+        T, N, dev = self.buffer_size, self.n_envs, self.device
+        self.observations = {k: th.zeros((T, N, *shp), dtype=_torch_dtype(self.observation_space.spaces[k]), device=dev)
+                             for k, shp in self.obs_shape.items()}
+        act_dtype = th.int64 if isinstance(self.action_space, (spaces.Discrete, spaces.MultiDiscrete)) else th.float32
+        self.actions = th.zeros((T, N, self.action_dim), dtype=act_dtype, device=dev)
+        for name in ("rewards", "returns", "episode_starts", "values", "log_probs", "advantages"):
+            setattr(self, name, th.zeros((T, N), dtype=th.float32, device=dev))
+        self.generator_ready = False
+        BaseBuffer.reset(self)
+
+    def add(self, obs, action, reward, episode_start, value: th.Tensor, log_prob: th.Tensor) -> None:
+        for k, buf in self.observations.items():
+            buf[self.pos].copy_(_to_t(obs[k], self.device, buf.dtype).reshape(buf[self.pos].shape))
+        if len(log_prob.shape) == 0:
+            log_prob = log_prob.reshape(-1, 1)
+        self.actions[self.pos].copy_(_to_t(action, self.device, self.actions.dtype).reshape((self.n_envs, self.action_dim)))
+        self.rewards[self.pos].copy_(_to_t(reward, self.device, th.float32).reshape(-1))
+        self.episode_starts[self.pos].copy_(_to_t(episode_start, self.device, th.float32).reshape(-1))
+        self.values[self.pos].copy_(value.detach().reshape(-1).float())
+        self.log_probs[self.pos].copy_(log_prob.detach().reshape(-1).float())
+        self.pos += 1
+        if self.pos == self.buffer_size:
+            self.full = True
+
+    def _flat(self):
+        T, N = self.buffer_size, self.n_envs
+        return dict(
+            observations={k: v.reshape(T * N, *v.shape[2:]) for k, v in self.observations.items()},
+            actions=self.actions.reshape(T * N, self.action_dim),
+            values=self.values.reshape(-1),
+            log_probs=self.log_probs.reshape(-1),
+            advantages=self.advantages.reshape(-1),
+            returns=self.returns.reshape(-1),
+        )
+
+    def _get_samples(self, flat, idx: th.Tensor) -> RolloutBufferSamples:
+        acts = flat["actions"][idx]
+        if isinstance(self.action_space, spaces.Discrete):
+            acts = acts.reshape(-1)
+        obs = {k: v[idx] for k, v in flat["observations"].items()}
+        return RolloutBufferSamples(obs, acts, flat["values"][idx], flat["log_probs"][idx], flat["advantages"][idx],
+                                    flat["returns"][idx])
+
+
 class ReplayBuffer(BaseBuffer):
     """Off-policy ring buffer on the device (SB3 ``ReplayBuffer`` semantics incl. timeout handling)."""
 

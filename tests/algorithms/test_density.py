@@ -93,3 +93,54 @@ def test_device_kde_kernel_matches_sklearn(kernel, N, NQ, d):
         assert close.mean() > 0.995, close.mean()
     else:
         assert close.all(), (ours[~close][:5], ref[~close][:5])
+
+
+class _DictObsEnv:
+    """Dict observations ("a": Box(2), "b": Box(3)) with an action-dependent episode length."""
+
+    metadata = {}
+    render_mode = None
+
+    def __init__(self):
+        from imitation_amd.envs import spaces
+
+        self.action_space = spaces.Discrete(3)
+        self.observation_space = spaces.Dict({"a": spaces.Box(-1.0, 1.0, (2,)), "b": spaces.Box(0.0, 1.0, (3,))})
+        self.t = 0
+        self.g = np.random.default_rng(0)
+
+    def _obs(self):
+        return {"a": self.g.uniform(-1, 1, 2).astype(np.float32), "b": self.g.uniform(0, 1, 3).astype(np.float32)}
+
+    def reset(self, *, seed=None, options=None):
+        self.t = 0
+        return self._obs(), {}
+
+    def step(self, action):
+        self.t += 1
+        return self._obs(), 0.0, self.t >= 3 + int(action), False, {}
+
+    def close(self):
+        pass
+
+
+def test_dict_space():
+    """Reference tests/algorithms/test_density_baselines.py:173 -- KDE over Dict observations with a
+    multi-input PPO policy (dict rollout buffer)."""
+    from imitation_amd.data import wrappers
+    from imitation_amd.envs.vec_env import DummyVecEnv
+    from imitation_amd.rl.policies import MultiInputActorCriticPolicy
+    from imitation_amd.rl.ppo import PPO
+
+    venv = DummyVecEnv([lambda: wrappers.RolloutInfoWrapper(_DictObsEnv()) for _ in range(2)])
+    rng = np.random.default_rng(0)
+    algo = PPO(MultiInputActorCriticPolicy, venv, n_steps=10, n_epochs=2, batch_size=10, device="cpu")
+    trajs = rollout.rollout(None, venv, rollout.make_min_episodes(15), rng=rng)
+    d = DensityAlgorithm(demonstrations=trajs, kernel="gaussian", venv=venv, rl_algo=algo, kernel_bandwidth=0.2,
+                         standardise_inputs=True, rng=rng, allow_variable_horizon=True)
+    d.train()
+    d.train_policy(n_timesteps=2)
+    stats = d.test_policy(n_trajectories=2)
+    assert stats["n_traj"] >= 2
+    assert isinstance(algo.rollout_buffer.observations, dict)
+    assert set(algo.rollout_buffer.observations) == {"a", "b"}
