@@ -197,6 +197,7 @@ struct PPORcGeo {
   // [wbase[q], wbase[q] + nwit[q]), bias / log_std vectors [bbase[q], bbase[q] + nbit[q]).
   int ns;
   int wbase[2], nwit[2], bbase[2], nbit[2];
+  int xstash;  // LDS offset of the G x 256-float partial stash (item-split first level, G > 16; -1: none)
   // XCD placement (speed only, never correctness): > 1 launches xcd x the workgroups and only
   // blocks b % xcd == 0 work (logical id b / xcd), so under the observed round-robin dealing of
   // blocks over the 8 XCDs every cooperating workgroup shares one XCD's L2

@@ -97,6 +97,9 @@ __device__ __forceinline__ float max_kk(float v) { return max_halves(max_rows16(
 __device__ __forceinline__ void st_sc1_x4(float* p, f4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
+__device__ __forceinline__ void st_sc1_x1(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 __device__ __forceinline__ f4 ld_sc1_x4(const float* p) {
   f4 v;
   asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
@@ -1025,7 +1028,45 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         else if (G == 4) reduce_slots<4, KI>(slab, red, gs, grp, lane, slot_id);
         else if (G == 8) reduce_slots<8, KI>(slab, red, gs, grp, lane, slot_id);
         else if (G == 16) reduce_slots<16, KI>(slab, red, gs, grp, lane, slot_id);
-        else {  // G > 16 (or odd): slot it is reduced by workgroup it % G, 16 loads in flight
+        else if (g.xstash >= 0) {
+          // G > 16: item j of this net's list (weight tiles, then vectors) is reduced by
+          // workgroup j % G. Its G partials are split over the waves -- ONE load batch per
+          // wave (<= 16 in flight) instead of G / 16 serial batches on one wave -- staged in
+          // the activation images (idle between the last dW item and the next chunk; zeroed
+          // again afterwards) and summed one element per lane in group order: the same additions as the one-level
+          // sum, so the update stays bitwise plan-independent.
+          lf* st = L + g.xstash;
+          const int m = nwq + nbq;
+          for (int j = grp; j < m; j += G) {
+            const int id = j < nwq ? wb + j : bb + (j - nwq);
+            const float* p = slab + (size_t)id * 256 + lane * 4;
+            f4 v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int gi = w + e * kWaves;
+              v[e] = {0.f, 0.f, 0.f, 0.f};
+              if (gi < G) v[e] = ld_sc1_x4(p + (size_t)gi * gs);
+            }
+            wait_vm_n<16>(v);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int gi = w + e * kWaves;
+              if (gi < G) *(lf4*)(st + gi * 256 + lane * 4) = v[e];
+            }
+            __syncthreads();
+            for (int el = tid; el < 256; el += kThreads) {
+              float sacc = st[el];
+#pragma unroll 8
+              for (int gi = 1; gi < G; ++gi) sacc += st[gi * 256 + el];
+              st_sc1_x1(red + (size_t)id * 256 + el, sacc);
+            }
+            __syncthreads();  // the stash is rewritten by the next item
+          }
+          // the images' padding rows / columns are read as zeros (zeroed once at kernel
+          // start, never rewritten): restore them
+          if (grp < m)
+            for (int i = tid; i < G * 64; i += kThreads) *(lf4*)(st + 4 * i) = f4{0.f, 0.f, 0.f, 0.f};
+        } else {  // G > 16 without a stash: slot it is reduced by workgroup it % G, 16 loads in flight
 #pragma unroll
           for (int it = 0; it < KI; ++it) {
             const int id = ids[it];
@@ -1403,6 +1444,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     aend = off > aend ? off : aend;
   }
   off = aend;
+  // the G > 16 first-level stash reuses the activation images (G x 256 floats)
+  g.xstash = G > 16 && aend - h0 >= G * 256 ? h0 : -1;
   g.lsp_off = take(4 * 16);
   g.nm_off = take(256);
   g.red_off = take(8 + 8 * 5 + 4);  // wave |g|^2, wave stats, [48] both nets' |g|^2
