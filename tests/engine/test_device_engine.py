@@ -112,6 +112,9 @@ def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, nor
     ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g1x1x64:kt4:ns"),
     ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g8x1x64:kt4:ns"),
     ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g2x1x64:kt4:ns"),
+    # G > 16 (AIRL's 4- / 8-rank DP minibatch): item-split first level from the LDS stash
+    ("seals/Hopper-v1", 1, 2048, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g32x1x64:kt4:ns"),
+    ("seals/Hopper-v1", 1, 4096, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g64x1x64:kt4:ns"),
     # both nets per workgroup (IMITATION_AMD_PPO_NETSPLIT=0): 64-row chunks for <= 32-wide
     # nets, 32-row chunks (2 row-tile waves per net) for 64-wide ones
     ("seals/HalfCheetah-v1", 1, 64, 0, "nons", "rc:g1x1x64:kt2"),
@@ -132,7 +135,7 @@ def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_a
         if net_arch.get("act") == "relu":
             act = th.nn.ReLU
         net_arch = {k: v for k, v in net_arch.items() if k not in ("act", "nons")}
-    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=8 if batch > 64 else 4, n_steps=64 if batch > 256 else 32,
+    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=max(8, batch // 64) if batch > 64 else 4, n_steps=64 if batch > 256 else 32,
                                batch=batch, n_epochs=2, net_arch=net_arch, activation=act)
     tr._ppo_static["allow_rc"] = allow_rc
     tr._ppo_static["rc_gmax"] = gmax

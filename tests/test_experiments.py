@@ -48,3 +48,22 @@ def test_quickstart_example_fast(monkeypatch, tmp_path):
     spec.loader.exec_module(mod)
     before, after = mod.main(["--fast", "--device", "cpu"])
     assert np.isfinite(before) and np.isfinite(after)
+
+
+def test_quickstart_shell_example_runs_twice(tmp_path):
+    """Reference tests/test_examples.py: the CLI quickstart (RL expert, then GAIL and AIRL from its
+    rollouts) runs to completion, twice in the same directory."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, PYTHONPATH=str(ROOT) + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    (bindir / "python").symlink_to(sys.executable)
+    env["PATH"] = str(bindir) + os.pathsep + env["PATH"]
+    for _ in range(2):
+        r = subprocess.run(["bash", "-e", str(ROOT / "examples" / "quickstart.sh")], cwd=tmp_path, env=env,
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+    assert (tmp_path / "quickstart" / "rl" / "rollouts" / "final.npz").exists()
