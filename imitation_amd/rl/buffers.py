@@ -287,3 +287,97 @@ class ReplayBuffer(BaseBuffer):
             dones=dones,
             rewards=rews,
         )
+
+
+class DictReplayBuffer(ReplayBuffer):
+    """:class:`ReplayBuffer` for ``spaces.Dict`` observations (SB3 ``DictReplayBuffer``): one device
+    ring ``[capacity, n_envs, *shape]`` per key for observations and next observations; a sample
+    gathers every key's rows together with the other fields (<= 8 tensors per gather launch)."""
+
+    def __init__(self, buffer_size: int, observation_space: spaces.Space, action_space: spaces.Space,
+                 device: Union[th.device, str] = "auto", n_envs: int = 1, optimize_memory_usage: bool = False,
+                 handle_timeout_termination: bool = True):
+        assert not optimize_memory_usage, "DictReplayBuffer does not support optimize_memory_usage"
+        BaseBuffer.__init__(self, buffer_size, observation_space, action_space, device, n_envs=n_envs)
+        self.buffer_size = max(buffer_size // n_envs, 1)
+        self.optimize_memory_usage = False
+        self.handle_timeout_termination = handle_timeout_termination
+        S, N, dev = self.buffer_size, self.n_envs, self.device
+
+        def rings():
+            return {k: th.zeros((S, N, *shp), dtype=_torch_dtype(observation_space.spaces[k]), device=dev)
+                    for k, shp in self.obs_shape.items()}
+
+        self.observations = rings()
+        self.next_observations = rings()
+        adt = th.int64 if isinstance(action_space, (spaces.Discrete, spaces.MultiDiscrete)) else th.float32
+        self.actions = th.zeros((S, N, self.action_dim), dtype=adt, device=dev)
+        self.rewards = th.zeros((S, N), dtype=th.float32, device=dev)
+        self.dones = th.zeros((S, N), dtype=th.float32, device=dev)
+        self.timeouts = th.zeros((S, N), dtype=th.float32, device=dev)
+
+    def add(self, obs, next_obs, action, reward, done, infos: List[Dict[str, Any]]) -> None:
+        p = self.pos
+        for k, ring in self.observations.items():
+            ring[p].copy_(_to_t(obs[k], self.device, ring.dtype).reshape(ring[p].shape))
+        for k, ring in self.next_observations.items():
+            ring[p].copy_(_to_t(next_obs[k], self.device, ring.dtype).reshape(ring[p].shape))
+        self.actions[p].copy_(_to_t(action, self.device, self.actions.dtype).reshape((self.n_envs, self.action_dim)))
+        self.rewards[p].copy_(_to_t(reward, self.device, th.float32).reshape(-1).expand(self.n_envs))
+        self.dones[p].copy_(_to_t(done, self.device, th.float32).reshape(-1).expand(self.n_envs))
+        if self.handle_timeout_termination:
+            self.timeouts[p].copy_(
+                th.tensor([float(info.get("TimeLimit.truncated", False)) for info in infos], device=self.device)
+            )
+        self.pos += 1
+        if self.pos == self.buffer_size:
+            self.full = True
+            self.pos = 0
+
+    def extend(self, obs, next_obs, action, reward, done) -> None:
+        """Bulk-append ``n`` single-env transitions (``n_envs == 1``); ``obs`` / ``next_obs`` map keys to ``[n, ...]``."""
+        assert self.n_envs == 1
+        n = len(next(iter(obs.values())))
+        idx = (th.arange(n, device=self.device) + self.pos) % self.buffer_size
+        for src, rings in ((obs, self.observations), (next_obs, self.next_observations)):
+            for k, ring in rings.items():
+                ring[idx, 0] = _to_t(src[k], self.device, ring.dtype).reshape((n, *self.obs_shape[k]))
+        self.actions[idx, 0] = _to_t(action, self.device, self.actions.dtype).reshape((n, self.action_dim))
+        self.rewards[idx, 0] = _to_t(reward, self.device, th.float32).reshape(-1).expand(n)
+        self.dones[idx, 0] = _to_t(done, self.device, th.float32).reshape(-1).expand(n)
+        self.timeouts[idx, 0] = 0.0
+        if self.pos + n >= self.buffer_size:
+            self.full = True
+        self.pos = (self.pos + n) % self.buffer_size
+
+    def _get_samples(self, batch_inds: th.Tensor, env=None) -> ReplayBufferSamples:
+        from imitation_amd.ops.rl import gather_rows
+
+        env_inds = th.randint(0, self.n_envs, (len(batch_inds),), device=self.device)
+        SN = self.buffer_size * self.n_envs
+        keys = list(self.observations)
+        srcs = [self.observations[k].view(SN, *self.obs_shape[k]) for k in keys]
+        srcs += [self.next_observations[k].view(SN, *self.obs_shape[k]) for k in keys]
+        srcs += [self.actions.view(SN, self.action_dim), self.dones.view(SN), self.timeouts.view(SN), self.rewards.view(SN)]
+        out: List[th.Tensor] = []
+        for i in range(0, len(srcs), 8):
+            out += list(gather_rows(srcs[i : i + 8], batch_inds, env_inds, self.n_envs))
+        nk = len(keys)
+        obs = dict(zip(keys, out[:nk]))
+        next_obs = dict(zip(keys, out[nk : 2 * nk]))
+        acts, d, tmo, rews = out[2 * nk :]
+        if env is not None and hasattr(env, "normalize_obs"):
+            obs = {k: self.to_torch(v) for k, v in env.normalize_obs({k: v.cpu().numpy() for k, v in obs.items()}).items()}
+            next_obs = {k: self.to_torch(v) for k, v in
+                        env.normalize_obs({k: v.cpu().numpy() for k, v in next_obs.items()}).items()}
+        rews = rews.reshape(-1, 1)
+        if env is not None and hasattr(env, "normalize_reward"):
+            rews = self.to_torch(env.normalize_reward(rews.cpu().numpy())).float()
+        as_f = lambda t: t.float() if t.dtype != th.uint8 else t  # noqa: E731
+        return ReplayBufferSamples(
+            observations={k: as_f(v) for k, v in obs.items()},
+            actions=acts,
+            next_observations={k: as_f(v) for k, v in next_obs.items()},
+            dones=(d * (1 - tmo)).reshape(-1, 1),
+            rewards=rews,
+        )

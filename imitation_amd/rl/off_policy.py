@@ -14,7 +14,7 @@ import torch as th
 from imitation_amd.envs import spaces
 from imitation_amd.parallel import dist as pdist
 from imitation_amd.rl.base import BaseAlgorithm
-from imitation_amd.rl.buffers import ReplayBuffer
+from imitation_amd.rl.buffers import DictReplayBuffer, ReplayBuffer
 from imitation_amd.rl.callbacks import BaseCallback
 
 
@@ -77,7 +77,7 @@ class OffPolicyAlgorithm(BaseAlgorithm):
         self._setup_lr_schedule()
         self.set_random_seed(self.seed)
         if self.replay_buffer_class is None:
-            self.replay_buffer_class = ReplayBuffer
+            self.replay_buffer_class = DictReplayBuffer if isinstance(self.observation_space, spaces.Dict) else ReplayBuffer
         if self.replay_buffer is None:
             kwargs = dict(self.replay_buffer_kwargs)
             self.replay_buffer = self.replay_buffer_class(self.buffer_size, self.observation_space, self.action_space,
@@ -110,10 +110,17 @@ class OffPolicyAlgorithm(BaseAlgorithm):
             reward_ = self._vec_normalize_env.get_original_reward()
         else:
             self._last_original_obs, new_obs_, reward_ = self._last_obs, new_obs, reward
-        next_obs = np.array(new_obs_, copy=True)
-        for i, done in enumerate(dones):
-            if done and infos[i].get("terminal_observation") is not None:
-                next_obs[i] = infos[i]["terminal_observation"]
+        if isinstance(new_obs_, dict):  # Dict observation spaces: one array per key
+            next_obs = {k: np.array(v, copy=True) for k, v in new_obs_.items()}
+            for i, done in enumerate(dones):
+                if done and infos[i].get("terminal_observation") is not None:
+                    for k in next_obs:
+                        next_obs[k][i] = infos[i]["terminal_observation"][k]
+        else:
+            next_obs = np.array(new_obs_, copy=True)
+            for i, done in enumerate(dones):
+                if done and infos[i].get("terminal_observation") is not None:
+                    next_obs[i] = infos[i]["terminal_observation"]
         replay_buffer.add(self._last_original_obs, next_obs, buffer_action, reward_, dones, infos)
         self._last_obs = new_obs
         if self._vec_normalize_env is not None:

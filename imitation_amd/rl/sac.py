@@ -23,7 +23,8 @@ from imitation_amd.rl.distributions import SquashedDiagGaussianDistribution
 from imitation_amd.rl.off_policy import OffPolicyAlgorithm, polyak_update
 from imitation_amd.rl.policies import BasePolicy, get_schedule_fn
 from imitation_amd.rl.preprocessing import get_action_dim
-from imitation_amd.rl.torch_layers import BaseFeaturesExtractor, FlattenExtractor, NatureCNN, create_mlp, get_actor_critic_arch
+from imitation_amd.rl.torch_layers import (BaseFeaturesExtractor, CombinedExtractor, FlattenExtractor, NatureCNN, create_mlp,
+                                           get_actor_critic_arch)
 
 LOG_STD_MAX = 2
 LOG_STD_MIN = -20
@@ -157,7 +158,7 @@ class SACPolicy(BasePolicy):
 
 
 class SAC(OffPolicyAlgorithm):
-    policy_aliases = {"MlpPolicy": SACPolicy}
+    policy_aliases = {"MlpPolicy": SACPolicy}  # + "MultiInputPolicy" (defined below)
 
     def __init__(self, policy, env, learning_rate=3e-4, buffer_size: int = 1_000_000, learning_starts: int = 100,
                  batch_size: int = 256, tau: float = 0.005, gamma: float = 0.99, train_freq=1, gradient_steps: int = 1,
@@ -262,3 +263,20 @@ class SAC(OffPolicyAlgorithm):
 
     def _excluded_save_params(self):
         return super()._excluded_save_params() | {"actor", "critic", "critic_target", "_actor_bucket", "_critic_bucket", "ent_coef_tensor"}
+
+
+class MultiInputPolicy(SACPolicy):
+    """:class:`SACPolicy` over ``spaces.Dict`` observations (SB3 ``MultiInputPolicy``): the
+    per-key features are concatenated by :class:`CombinedExtractor`."""
+
+    def __init__(self, observation_space, action_space, lr_schedule, net_arch=None, activation_fn: Type[nn.Module] = nn.ReLU,
+                 use_sde: bool = False, log_std_init: float = -3, use_expln: bool = False, clip_mean: float = 2.0,
+                 features_extractor_class: Type[BaseFeaturesExtractor] = CombinedExtractor, features_extractor_kwargs=None,
+                 normalize_images: bool = True, optimizer_class: Type[th.optim.Optimizer] = th.optim.Adam,
+                 optimizer_kwargs=None, n_critics: int = 2, share_features_extractor: bool = False):
+        super().__init__(observation_space, action_space, lr_schedule, net_arch, activation_fn, use_sde, log_std_init,
+                         use_expln, clip_mean, features_extractor_class, features_extractor_kwargs, normalize_images,
+                         optimizer_class, optimizer_kwargs, n_critics, share_features_extractor)
+
+
+SAC.policy_aliases["MultiInputPolicy"] = MultiInputPolicy
