@@ -17,7 +17,7 @@ from imitation_amd.envs import spaces
 from imitation_amd.parallel import dist as pdist
 from imitation_amd.rl.off_policy import OffPolicyAlgorithm, polyak_update
 from imitation_amd.rl.policies import BasePolicy, get_schedule_fn
-from imitation_amd.rl.torch_layers import BaseFeaturesExtractor, FlattenExtractor, NatureCNN, create_mlp
+from imitation_amd.rl.torch_layers import BaseFeaturesExtractor, CombinedExtractor, FlattenExtractor, NatureCNN, create_mlp
 
 
 def get_linear_fn(start: float, end: float, end_fraction: float):
@@ -92,8 +92,15 @@ class CnnPolicy(DQNPolicy):
         super().__init__(*args, features_extractor_class=features_extractor_class, **kwargs)
 
 
+class MultiInputPolicy(DQNPolicy):
+    """Q-network over ``spaces.Dict`` observations (per-key features concatenated)."""
+
+    def __init__(self, *args, features_extractor_class=CombinedExtractor, **kwargs):
+        super().__init__(*args, features_extractor_class=features_extractor_class, **kwargs)
+
+
 class DQN(OffPolicyAlgorithm):
-    policy_aliases = {"MlpPolicy": DQNPolicy, "CnnPolicy": CnnPolicy}
+    policy_aliases = {"MlpPolicy": DQNPolicy, "CnnPolicy": CnnPolicy, "MultiInputPolicy": MultiInputPolicy}
 
     def __init__(self, policy, env, learning_rate=1e-4, buffer_size: int = 1_000_000, learning_starts: int = 100,
                  batch_size: int = 32, tau: float = 1.0, gamma: float = 0.99, train_freq=4, gradient_steps: int = 1,

@@ -77,3 +77,26 @@ def test_ppo_multi_input_policy_uses_a_dict_rollout_buffer():
     assert isinstance(algo.rollout_buffer, DictRolloutBuffer)
     assert {k: tuple(v.shape) for k, v in algo.rollout_buffer.observations.items()} == {"a": (16, 2, 2), "b": (16, 2, 3)}
     assert any(not th.equal(a, b) for a, b in zip(before, algo.policy.parameters()))
+
+
+class _DictDiscreteEnv(_DictEnv):
+    def __init__(self):
+        super().__init__()
+        self.action_space = spaces.Discrete(3)
+
+    def step(self, action):
+        self.t += 1
+        return self._obs(), float(action == 1), self.t >= 5, False, {}
+
+
+def test_dqn_multi_input_policy():
+    from imitation_amd.rl.dqn import DQN
+
+    venv = DummyVecEnv([_DictDiscreteEnv])
+    algo = DQN("MultiInputPolicy", venv, buffer_size=100, learning_starts=8, batch_size=8, train_freq=4, device="cpu", seed=0)
+    before = [p.detach().clone() for p in algo.policy.parameters()]
+    algo.learn(40)
+    assert isinstance(algo.replay_buffer, DictReplayBuffer) and algo.replay_buffer.size() == 40
+    assert any(not th.equal(a, b) for a, b in zip(before, algo.policy.parameters()))
+    acts, _ = algo.predict({"a": np.zeros((1, 2), np.float32), "b": np.zeros((1, 3), np.float32)}, deterministic=True)
+    assert acts.shape == (1,) and 0 <= int(acts[0]) < 3
