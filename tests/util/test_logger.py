@@ -116,3 +116,48 @@ def test_tensorboard_event_file(tmp_path):
     h.close()
     files = list(tmp_path.glob("events.out.tfevents.*"))
     assert files and files[0].stat().st_size > 0
+
+
+def test_free_form_text_levels(tmp_path):
+    """Reference test_free_form: free-form messages reach log.txt at or above the level; inside
+    accumulate_means they still go to the default output."""
+    from imitation_amd.rl import logger as sb_logger
+
+    h = logger.configure(str(tmp_path), ["log"])
+    h.log("info 1")
+    h.info("info 2")
+    h.warn("warn 1")
+    h.error("error 1")
+    h.debug("hidden")
+    h.set_level(level=sb_logger.DEBUG)
+    h.debug("debug 1")
+    with h.accumulate_means("foo"):
+        h.info("info inner")
+    h.debug("debug outer")
+    h.close()
+    with open(osp.join(str(tmp_path), "log.txt")) as f:
+        assert f.readlines() == ["info 1\n", "info 2\n", "warn 1\n", "error 1\n", "debug 1\n", "info inner\n",
+                                 "debug outer\n"]
+
+
+def test_dump_after_close_raises(tmp_path):
+    h = logger.configure(str(tmp_path))
+    h.record("A", 1)
+    with h.accumulate_means("foo"):
+        h.record("B", 2)
+    h.dump()
+    h.close()
+    h.record("foo", 42)
+    with pytest.raises(ValueError, match="closed file"):
+        h.dump()
+
+
+def test_prefix_context_errors(tmp_path):
+    h = logger.configure(str(tmp_path))
+    with pytest.raises(RuntimeError):
+        with h.accumulate_means("foo"), h.add_accumulate_prefix("bar"):
+            pass
+    h2 = logger.configure(str(tmp_path / "b"))
+    with pytest.raises(RuntimeError):
+        with h2.add_key_prefix("bar"):
+            pass
