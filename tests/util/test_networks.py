@@ -143,3 +143,43 @@ def test_ema_norm_fused_kernel_matches_torch(B, D, decay):
     a.eval()
     x = th.randn(B, D, generator=g).cuda()
     th.testing.assert_close(a(x), (x - a.running_mean) / th.sqrt(a.running_var + a.eps), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("batch_size", [1, 8, 64, 500])
+@pytest.mark.parametrize("cls", [networks.RunningNorm, networks.EMANorm])
+def test_norm_statistics_converge(batch_size, cls):
+    """Reference test_parameters_converge: running mean / var approach the data's, count = samples."""
+    mean, var = th.tensor([3.0, 0.0]), th.tensor([6.0, 1.0])
+    norm = cls(2)
+    norm.train()
+    g = th.Generator().manual_seed(42)
+    data = th.randn(2000, 2, generator=g) * var.sqrt() + mean
+    for s in range(0, 2000, batch_size):
+        norm(data[s : s + batch_size])
+    norm.eval()
+    th.testing.assert_close(norm.running_mean, mean, rtol=0.05, atol=0.1 if cls is networks.RunningNorm else 0.5)
+    th.testing.assert_close(norm.running_var, var, rtol=0.1 if cls is networks.RunningNorm else 0.5, atol=0.1)
+    assert int(norm.count) == 2000
+
+
+@pytest.mark.parametrize("kw", [{}, {"dropout_prob": 0.5}, {"normalize_input_layer": networks.RunningNorm},
+                                {"normalize_input_layer": networks.EMANorm}])
+def test_build_mlp_trains_on_a_toy_task(kw):
+    x = th.linspace(-3.14159, 3.14159, 200).reshape(-1, 1)
+    y = th.sin(x)
+    model = networks.build_mlp(in_size=1, hid_sizes=[16, 16], out_size=1, **kw)
+    opt = th.optim.Adam(model.parameters(), lr=1e-2)
+    first = None
+    for _ in range(200):
+        loss = th.nn.functional.mse_loss(model(x).reshape(-1, 1), y)
+        first = float(loss.detach()) if first is None else first
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    if "dropout_prob" not in kw:
+        assert float(loss.detach()) < first
+
+
+def test_build_mlp_rejects_an_invalid_normalization_layer():
+    with pytest.raises(ValueError, match="not a valid normalization layer"):
+        networks.build_mlp(in_size=1, hid_sizes=[16, 16], out_size=1, normalize_input_layer=th.nn.Module)
