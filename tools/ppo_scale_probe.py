@@ -51,6 +51,7 @@ def main():
         tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, venv=venv, gen_algo=gen, reward_net=rn,
                         n_disc_updates_per_round=1, custom_logger=logger.configure("/tmp/ia_probe", format_strs=[]))
         tr._ppo_static["rc_cw"] = int(os.environ.get("RC_CW", "0"))
+        tr._ppo_static["rc_gmax"] = int(os.environ.get("RC_GMAX", "0"))  # cap on cooperating workgroups (0: plan default)
         path = tr._C.engine_ppo_path(tr._ppo_static)
         tr._rollout()
         for _ in range(2):
