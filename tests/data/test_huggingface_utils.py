@@ -34,3 +34,18 @@ def test_sliced_info_dicts(data, trajectory):
     assert list(wrapped.infos[sl]) == list(trajectory.infos[sl])
     for i in range(len(trajectory.infos)):
         assert wrapped.infos[i] == trajectory.infos[i]
+
+
+@given(st.data(), h_strats.trajectories_list)
+@settings(deadline=None, max_examples=10)
+def test_sliced_trajectory_access(data, trajectories):
+    """Reference test_sliced_access: a slice of the dataset sequence yields the same trajectories
+    as the same slice of the list (10 slices per dataset: building the dataset dominates)."""
+    wrapped = _wrap(trajectories)
+    for _ in range(10):
+        sl = data.draw(st.slices(len(trajectories)))
+        idx = list(range(*sl.indices(len(trajectories))))
+        got = list(wrapped[sl])
+        assert len(got) == len(idx)
+        for i, t in zip(idx, got):
+            assert t == trajectories[i]
