@@ -68,3 +68,37 @@ def test_registry():
         r.register("c")
     with pytest.raises(KeyError):
         r.get("zzz")
+
+
+def test_endless_iter_errors():
+
+    with pytest.raises(ValueError, match="no elements"):
+        util.endless_iter([])
+    with pytest.raises(ValueError, match="needs a non-iterator Iterable"):
+        util.endless_iter(x for x in range(5))
+
+def test_first_iter_element_of_a_generator_keeps_every_element():
+
+    with pytest.raises(ValueError, match="had no elements"):
+        util.get_first_iter_element([])
+    seq = [4, 1, 7]
+    first, same = util.get_first_iter_element(seq)
+    assert first == 4 and same is seq
+    gen = (x for x in seq)
+    first, rest = util.get_first_iter_element(gen)
+    assert first == 4 and list(rest) == seq and list(rest) == []
+
+def test_oric_keeps_integral_sums():
+    g = np.random.default_rng(0)
+    for n in range(1, 11):
+        x = g.uniform(1e-3, 1e6, n)
+        x = x - (x.sum() - np.floor(x.sum())) / n
+        r = util.oric(x)
+        assert np.allclose(r.sum(), x.sum()) and np.abs(x - r).max() <= 1.0
+        assert np.allclose(r, np.round(r))
+
+def test_dict_get_nested():
+    from imitation_amd.util import sacred as sacred_util
+
+    assert sacred_util.dict_get_nested({}, "asdf.foo", default=4) == 4
+    assert sacred_util.dict_get_nested({"a": {"b": "c"}}, "a.b") == "c"
