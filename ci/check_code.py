@@ -97,9 +97,37 @@ def check_pickle(errors):
                 errors.append(f"{f}:{node.lineno}: unsafe deserialisation {bad}")
 
 
-def main() -> int:
+def check_test_basenames(errors):
+    """``tests/`` subdirectories are rootdir-relative modules (no ``__init__.py``), so two test
+    files with one basename make pytest's collection fail with "import file mismatch" -- which
+    stops every ``-x`` run before its first test (round-3 GPU step)."""
+    seen: dict = {}
+    for f in sorted((ROOT / "tests").rglob("*.py")):
+        if not f.name.startswith("test_"):
+            continue
+        if f.name in seen:
+            errors.append(f"{f}: test module basename also used by {seen[f.name]} (pytest collection error)")
+        else:
+            seen[f.name] = f
+
+
+def check_collect(errors):
+    """``pytest --collect-only`` over the whole suite reports no collection error (CPU, no GPU)."""
+    import subprocess
+
+    proc = subprocess.run([sys.executable, "-m", "pytest", "--collect-only", "-q", "-p", "no:cacheprovider",
+                           str(ROOT / "tests")], cwd=ROOT, capture_output=True, text=True, timeout=900)
+    tail = proc.stdout.strip().splitlines()[-1:] if proc.stdout.strip() else [proc.stderr.strip()[-400:]]
+    if proc.returncode != 0 or any("error" in line for line in tail):
+        errors.append(f"pytest --collect-only failed (rc {proc.returncode}): {tail}")
+
+
+def main(collect: bool = False) -> int:
     errors: list = []
-    for check in (check_compile, check_gpu_marks, check_native, check_pickle):
+    checks = [check_compile, check_gpu_marks, check_native, check_pickle, check_test_basenames]
+    if collect:
+        checks.append(check_collect)
+    for check in checks:
         check(errors)
     for e in errors:
         print(e)
@@ -108,4 +136,4 @@ def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main(collect="--collect" in sys.argv))
