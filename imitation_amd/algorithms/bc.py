@@ -357,6 +357,9 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         if num_samples_so_far % self.batch_size != 0 and state:
             state["batch_num"] += 1
             process_batch()
+        # the per-epoch checks are non-blocking (they read the previous epoch's error word):
+        # one blocking check makes a timed-out all-reduce in the last epoch raise here
+        pdist.check_comm("BC training", blocking=True)
 
 
 class BC(_BCBase):

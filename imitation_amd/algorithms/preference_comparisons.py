@@ -1330,7 +1330,9 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
             with self.logger.accumulate_means("agent"):
                 self.logger.log(f"Training agent for {steps} timesteps")
                 self.trajectory_generator.train(steps=steps)
-            pdist.check_comm("preference iteration")
+            # the last iteration's collectives are checked blocking: a NaN-poisoned one-shot
+            # all-reduce there must raise, not return NaN weights
+            pdist.check_comm("preference iteration", blocking=i == len(schedule) - 1)
             self.logger.dump(self._iteration)
             if callback:
                 callback(self._iteration)

@@ -236,7 +236,12 @@ class DeviceDemoAggregate:
 class DeviceTransitionsLoader:
     """Shuffled, drop-last minibatches straight from a :class:`DeviceDemoAggregate`: one
     ``perm_feistel`` launch per epoch and one two-field ``gather_rows`` per batch; yields the batch
-    dict BC consumes (``obs`` / ``acts`` device tensors)."""
+    dict BC consumes (``obs`` / ``acts`` device tensors).
+
+    Aliasing contract: every yielded batch is a view of the SAME persistent buffers
+    (:meth:`DeviceDemoAggregate.batch_buffers`), overwritten when the next batch is produced. A
+    consumer must use a batch before advancing the iterator (BC does); one that holds batches
+    (``list(loader)``, prefetching, two live iterators of one batch size) must ``clone()`` them."""
 
     def __init__(self, agg: DeviceDemoAggregate, batch_size: int, seed: int):
         self.agg = agg

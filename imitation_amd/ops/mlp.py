@@ -12,6 +12,7 @@ reference's reward nets and SB3 policy heads
 
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -158,9 +159,32 @@ def wide_supports(dims: Sequence[int]) -> bool:
     return 1 <= len(dims) - 1 <= 16 and max(dims) <= WIDE_MAX
 
 
-def fusable(dims: Sequence[int]) -> bool:
-    """Whether :func:`tmlp` runs this MLP on a HIP kernel (tiny or wide path)."""
-    return kernel_supports(dims) or wide_supports(dims)
+def wide_default() -> bool:
+    """Process default of the bf16-operand wide path (``IMITATION_AMD_WIDE_MLP=1``; off).
+
+    The wide kernels multiply bf16 operands (fp32 accumulation) while the reference runs these
+    networks in fp32, so a generic wide MLP stays on the fp32 path unless the caller opts in --
+    per module (``policy.wide_bf16 = True``, see :func:`set_wide_bf16`) or per process."""
+    return os.environ.get("IMITATION_AMD_WIDE_MLP", "0") == "1"
+
+
+def set_wide_bf16(module: torch.nn.Module, enabled: bool = True) -> torch.nn.Module:
+    """Opt ``module`` (a policy / network using :func:`tmlp`) in or out of the bf16-operand
+    wide-MLP kernels; clears a cached fusion plan."""
+    for m in module.modules():
+        object.__setattr__(m, "wide_bf16", bool(enabled))
+        for cache in ("_ia_fusion", "_ia_plan"):
+            if hasattr(m, cache):
+                object.__setattr__(m, cache, None)
+    return module
+
+
+def fusable(dims: Sequence[int], wide: Optional[bool] = None) -> bool:
+    """Whether :func:`tmlp` runs this MLP on a HIP kernel: the tiny kernel (fp32 MFMA) always,
+    the bf16-operand wide path when ``wide`` (default: :func:`wide_default`)."""
+    if kernel_supports(dims):
+        return True
+    return (wide_default() if wide is None else wide) and wide_supports(dims)
 
 
 def _act_grad_from_out(code: int, y: torch.Tensor) -> torch.Tensor:
@@ -236,12 +260,13 @@ def tmlp(
     norm_mean: Optional[torch.Tensor] = None,
     norm_var: Optional[torch.Tensor] = None,
     norm_eps: float = 1e-5,
+    wide: Optional[bool] = None,
 ) -> torch.Tensor:
     """Fused MLP forward (differentiable w.r.t. ``x`` and every weight / bias).
 
     GPU fp32 tensors go through a HIP kernel -- the whole-network tiny-MLP kernel for widths
-    <= 128, the per-layer wide kernels up to 1024 -- everything else through
-    :func:`tmlp_reference`.
+    <= 128, the per-layer bf16-operand wide kernels up to 1024 when ``wide`` (opt-in, see
+    :func:`wide_default`) -- everything else through :func:`tmlp_reference`.
     """
     from imitation_amd.ops import use_kernel
 
@@ -250,7 +275,7 @@ def tmlp(
         use_kernel(x)
         and x.dtype == torch.float32
         and x.dim() == 2
-        and fusable(dims)
+        and fusable(dims, wide)
         and all(w.dtype == torch.float32 for w in weights)
     ):
         if norm_mean is not None:

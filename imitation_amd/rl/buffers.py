@@ -337,18 +337,29 @@ class DictReplayBuffer(ReplayBuffer):
     def extend(self, obs, next_obs, action, reward, done) -> None:
         """Bulk-append ``n`` single-env transitions (``n_envs == 1``); ``obs`` / ``next_obs`` map keys to ``[n, ...]``."""
         assert self.n_envs == 1
-        n = len(next(iter(obs.values())))
-        idx = (th.arange(n, device=self.device) + self.pos) % self.buffer_size
+        n_all = len(next(iter(obs.values())))
+        # FIFO: only the newest ``buffer_size`` rows survive; scattering more than that would
+        # repeat ring indices, and which duplicate write wins in an index_put is unspecified
+        n = min(n_all, self.buffer_size)
+        skip = n_all - n
+        start = (self.pos + skip) % self.buffer_size
+        idx = (th.arange(n, device=self.device) + start) % self.buffer_size
+
+        def tail(x, dtype, shape):
+            t = _to_t(x, self.device, dtype)
+            t = t.reshape(-1).expand(n_all) if shape is None else t.reshape((n_all, *shape))
+            return t[skip:]
+
         for src, rings in ((obs, self.observations), (next_obs, self.next_observations)):
             for k, ring in rings.items():
-                ring[idx, 0] = _to_t(src[k], self.device, ring.dtype).reshape((n, *self.obs_shape[k]))
-        self.actions[idx, 0] = _to_t(action, self.device, self.actions.dtype).reshape((n, self.action_dim))
-        self.rewards[idx, 0] = _to_t(reward, self.device, th.float32).reshape(-1).expand(n)
-        self.dones[idx, 0] = _to_t(done, self.device, th.float32).reshape(-1).expand(n)
+                ring[idx, 0] = tail(src[k], ring.dtype, self.obs_shape[k])
+        self.actions[idx, 0] = tail(action, self.actions.dtype, (self.action_dim,))
+        self.rewards[idx, 0] = tail(reward, th.float32, None)
+        self.dones[idx, 0] = tail(done, th.float32, None)
         self.timeouts[idx, 0] = 0.0
-        if self.pos + n >= self.buffer_size:
+        if self.pos + n_all >= self.buffer_size:
             self.full = True
-        self.pos = (self.pos + n) % self.buffer_size
+        self.pos = (self.pos + n_all) % self.buffer_size
 
     def _get_samples(self, batch_inds: th.Tensor, env=None) -> ReplayBufferSamples:
         from imitation_amd.ops.rl import gather_rows

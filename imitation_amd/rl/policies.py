@@ -434,13 +434,15 @@ class ActorCriticPolicy(BasePolicy):
                     vf_l = vf[0] + [self.value_net]
                     pi_dims = [self.features_dim] + [l.out_features for l in pi_l]
                     vf_dims = [self.features_dim] + [l.out_features for l in vf_l]
-                    if isinstance(self.action_net, nn.Linear) and fusable(pi_dims) and fusable(vf_dims):
+                    wide = getattr(self, "wide_bf16", None)  # opt-in bf16 wide path (ops/mlp.py)
+                    if isinstance(self.action_net, nn.Linear) and fusable(pi_dims, wide) and fusable(vf_dims, wide):
                         plan = dict(
                             norm=norm,
                             pi=pi_l,
                             pi_act=pi[1] or 0,
                             vf=vf_l,
                             vf_act=vf[1] or 0,
+                            wide=wide,
                         )
         object.__setattr__(self, "_ia_fusion", plan)
         return plan
@@ -465,9 +467,9 @@ class ActorCriticPolicy(BasePolicy):
             mean, var, eps = norm.running_mean, norm.running_var, norm.eps
         head = vals = None
         if want_pi:
-            head = ops.tmlp(x, [l.weight for l in plan["pi"]], [l.bias for l in plan["pi"]], plan["pi_act"], 0, mean, var, eps)
+            head = ops.tmlp(x, [l.weight for l in plan["pi"]], [l.bias for l in plan["pi"]], plan["pi_act"], 0, mean, var, eps, plan["wide"])
         if want_vf:
-            vals = ops.tmlp(x, [l.weight for l in plan["vf"]], [l.bias for l in plan["vf"]], plan["vf_act"], 0, mean, var, eps)
+            vals = ops.tmlp(x, [l.weight for l in plan["vf"]], [l.bias for l in plan["vf"]], plan["vf_act"], 0, mean, var, eps, plan["wide"])
         return head, vals
 
     def _dist_from_head(self, head: th.Tensor) -> Distribution:

@@ -246,7 +246,8 @@ class MLP(nn.Sequential):
         if plan is not False:
             hid = set(acts[:-1])
             dims = [linears[0].in_features] + [l.out_features for l in linears] if linears else []
-            if not linears or len(hid) > 1 or not fusable(dims):
+            wide = getattr(self, "wide_bf16", None)  # opt-in bf16 wide path (ops/mlp.py)
+            if not linears or len(hid) > 1 or not fusable(dims, wide):
                 plan = False
             else:
                 plan = dict(
@@ -256,6 +257,7 @@ class MLP(nn.Sequential):
                     hidden_act=(acts[0] if len(acts) > 1 else 0),
                     out_act=acts[-1],
                     squeeze=squeeze,
+                    wide=wide,
                     has_dropout=any(isinstance(m, nn.Dropout) for m in mods),
                 )
         object.__setattr__(self, "_ia_plan", plan)
@@ -284,6 +286,7 @@ class MLP(nn.Sequential):
                     mean,
                     var,
                     eps,
+                    plan["wide"],
                 )
                 if plan["squeeze"]:
                     y = y.squeeze(1)

@@ -85,7 +85,9 @@ class GraphedTrainStep:
         with th.cuda.stream(side):  # warm-up == this step
             self.optimizer.zero_grad(set_to_none=True)
             result = self.fn(*static)
-        self.optimizer.zero_grad(set_to_none=True)
+            # on the warm-up stream: a fused optimiser's zero_grad launches ``grad.zero_()``
+            # over the bucket, which must stay ordered behind the warm-up's backward + step
+            self.optimizer.zero_grad(set_to_none=True)
         if self.release is not None:
             self.release()
         graph = th.cuda.CUDAGraph()

@@ -202,7 +202,7 @@ def test_multibc_homogeneous_policy_runs_on_wide_kernel():
                          observation_overide=obs_over, action_overide=act_over, num_agents=n_agents,
                          rng=np.random.default_rng(0), demonstrations=demos, batch_size=64, device="cuda",
                          optimizer_kwargs=dict(lr=1e-3), custom_logger=logger.configure(format_strs=[]))
-    pol = trainer.policy
+    pol = mlp_ops.set_wide_bf16(trainer.policy)  # the bf16 wide path is opt-in
     plan = pol._fusion()
     assert plan, "homogeneous policy heads must be fused"
     dims = [pol.features_dim] + [l.out_features for l in plan["pi"]]

@@ -50,7 +50,7 @@ def test_tmlp_forward_backward_matches_fp32(dims, act, B, norm):
     if norm:
         mean = th.randn(dims[0], device=dev) * 0.3
         var = th.rand(dims[0], device=dev) + 0.5
-    y = mlp_ops.tmlp(x, ws, bs, act, 0, mean, var)
+    y = mlp_ops.tmlp(x, ws, bs, act, 0, mean, var, wide=True)
     wr = [w.detach().clone().requires_grad_(True) for w in ws]
     br = [b.detach().clone().requires_grad_(True) for b in bs]
     xr = x.detach().clone().requires_grad_(True)
@@ -354,7 +354,7 @@ def test_wide_mlp_matches_fp32_linear(dims, act, B, norm):
     err = (x.grad - xr.grad).abs().max().item()
     assert err <= 3e-2 * (xr.grad.abs().max().item() + 1e-3)
     # deterministic: fixed-order reductions
-    y2 = mlp_ops.tmlp(x.detach(), ws, bs, act, 0, mean, var)
+    y2 = mlp_ops.tmlp(x.detach(), ws, bs, act, 0, mean, var, wide=True)
     assert th.equal(y.detach(), y2)
 
 

@@ -55,3 +55,24 @@ def test_gather_rows_cpu_and_hbm_capacity():
     assert cap == (144 * 10**9 - (4 << 30)) // (84 * 84 * 4 + 8) and cap > 4_900_000
     with pytest.raises(ValueError):
         hbm_capacity(0, free_bytes=10)
+
+
+def test_wide_mlp_path_is_opt_in(monkeypatch):
+    """The bf16-operand wide kernels (wlin.hip) are opt-in: a generic wide MLP stays on the
+    fp32 path unless the module or the process asks for them (advisor round 3)."""
+    from imitation_amd.ops import mlp as mlp_ops
+    from imitation_amd.util import networks
+
+    dims = [17, 256, 256, 6]
+    monkeypatch.delenv("IMITATION_AMD_WIDE_MLP", raising=False)
+    assert mlp_ops.fusable([17, 64, 64, 6]) and not mlp_ops.fusable(dims)
+    assert mlp_ops.fusable(dims, True) and not mlp_ops.fusable(dims, False)
+    monkeypatch.setenv("IMITATION_AMD_WIDE_MLP", "1")
+    assert mlp_ops.fusable(dims)
+    monkeypatch.delenv("IMITATION_AMD_WIDE_MLP")
+    net = networks.build_mlp(in_size=17, hid_sizes=[256, 256], out_size=6)
+    assert not net._fusion_plan()
+    mlp_ops.set_wide_bf16(net)
+    assert net._fusion_plan() and net._fusion_plan()["wide"] is True
+    mlp_ops.set_wide_bf16(net, False)
+    assert not net._fusion_plan()

@@ -65,6 +65,16 @@ def test_dict_replay_buffer_ring_and_terminal_observations():
               {"a": np.zeros((3, 2), np.float32), "b": np.zeros((3, 3), np.float32)}, np.zeros((3, 1)), np.ones(3),
               np.zeros(3))
     assert rb.pos == 1 and (rb.observations["a"][:, 0, 0] == 9).sum() == 3
+    # more rows than the ring holds: only the newest 4 survive, in FIFO slots
+    rows = np.arange(10, dtype=np.float32)
+    rb.extend({"a": np.repeat(rows[:, None], 2, 1), "b": np.zeros((10, 3), np.float32)},
+              {"a": np.zeros((10, 2), np.float32), "b": np.zeros((10, 3), np.float32)}, np.zeros((10, 1)), rows,
+              np.zeros(10))
+    assert rb.pos == (1 + 10) % 4 and rb.full
+    # slot (pos + j) % 4 holds the j-th oldest survivor: rows 6, 7, 8, 9
+    order = [(rb.pos + j) % 4 for j in range(4)]
+    assert rb.observations["a"][order, 0, 0].tolist() == [6.0, 7.0, 8.0, 9.0]
+    assert rb.rewards[order, 0].tolist() == [6.0, 7.0, 8.0, 9.0]
     with pytest.raises(AssertionError, match="optimize_memory_usage"):
         DictReplayBuffer(4, space, spaces.Box(-1.0, 1.0, (1,)), device="cpu", optimize_memory_usage=True)
 

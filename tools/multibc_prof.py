@@ -25,6 +25,9 @@ def main(n_agents=4, batch=256, steps=200):
                     observation_overide=lambda i, o: o[:, d * i: d * i + d], action_overide=lambda i, a: a[:, i],
                     num_agents=n_agents, rng=np.random.default_rng(0), demonstrations=demos, batch_size=batch, device="cuda",
                     optimizer_kwargs=dict(lr=1e-3), custom_logger=logger.configure(format_strs=[]))
+    from imitation_amd.ops import mlp as mlp_ops
+
+    mlp_ops.set_wide_bf16(tr.policy)  # the benchmarked config opts in to the bf16 wide kernels
     tr.train(n_batches=10, progress_bar=False, log_interval=10**9)
     th.cuda.synchronize()
     t0 = time.perf_counter()
