@@ -50,7 +50,7 @@ def test_tmlp_forward_backward_matches_fp32(dims, act, B, norm):
     if norm:
         mean = th.randn(dims[0], device=dev) * 0.3
         var = th.rand(dims[0], device=dev) + 0.5
-    y = mlp_ops.tmlp(x, ws, bs, act, 0, mean, var, wide=True)
+    y = mlp_ops.tmlp(x, ws, bs, act, 0, mean, var)
     wr = [w.detach().clone().requires_grad_(True) for w in ws]
     br = [b.detach().clone().requires_grad_(True) for b in bs]
     xr = x.detach().clone().requires_grad_(True)
@@ -334,7 +334,7 @@ def test_wide_mlp_matches_fp32_linear(dims, act, B, norm):
     if norm:
         mean = th.randn(dims[0], device=dev) * 0.3
         var = th.rand(dims[0], device=dev) + 0.5
-    y = mlp_ops.tmlp(x, ws, bs, act, 0, mean, var)
+    y = mlp_ops.tmlp(x, ws, bs, act, 0, mean, var, wide=True)
     wr = [w.detach().clone().requires_grad_(True) for w in ws]
     br = [b.detach().clone().requires_grad_(True) for b in bs]
     xr = x.detach().clone().requires_grad_(True)
