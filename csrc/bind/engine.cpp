@@ -213,6 +213,10 @@ void ppo_update(py::dict d) {
   a.prof = tptr<unsigned long long>(d, "prof", true);
   a.rc_gmax = ival(d, "rc_gmax", 0);
   a.rc_cw = ival(d, "rc_cw", 0);
+  a.err = reinterpret_cast<unsigned*>(tptr<int>(d, "err", true));
+  a.spin_limit = (unsigned)ival(d, "spin_limit", 0);
+  a.debug_stall = ival(d, "debug_stall", 0);
+  a.rc_cus = ival(d, "rc_cus", 0);
   TORCH_CHECK(a.D <= 64, "obs dim <= 64");
   ia::PPORcGeo geo;
   size_t rc_lds = 0;
@@ -242,6 +246,7 @@ std::string ppo_path(py::dict d) {
   a.log_std_off = ival(d, "log_std_off", -1);
   a.rc_gmax = ival(d, "rc_gmax", 0);
   a.rc_cw = ival(d, "rc_cw", 0);
+  a.rc_cus = ival(d, "rc_cus", 0);
   ia::PPORcGeo geo;
   size_t lds = 0;
   if (ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, lds))

@@ -161,7 +161,16 @@ struct PPOArgs {
   unsigned long long* prof;  // optional [10] cycle counters per phase
   int rc_gmax;   // mode 0 fast path: max cooperating workgroups per minibatch (0 = default kMaxRcGroups)
   int rc_cw;     // mode 0 fast path: rows per chunk override (0 = 64 for <= 32-wide nets, 32 otherwise)
+  // fail-fast for the cooperating workgroups (mode 0 fast path): a bounded spin that gives up
+  // ORs 1 into *err (persistent, host-checked; may be null) besides the per-launch flag
+  unsigned* err;
+  unsigned spin_limit;  // sleeps before a spin gives up (0 = default 2^22)
+  int debug_stall;      // test knob: the last working workgroup never publishes (forces a timeout)
+  int rc_cus;           // CU count to plan against (0 = query the current device)
 };
+
+// CUs of the current device (cached per device; IMITATION_AMD_PPO_CUS overrides, e.g. tests).
+int device_cu_count();
 
 // Geometry + workspace of the register-chained PPO kernel (ppo_rc.hip), planned on the host.
 constexpr int kMaxRcItems = 64;

@@ -132,6 +132,15 @@ __device__ __forceinline__ unsigned ld_sc1u(unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A bounded spin gave up (a partner workgroup never arrived: not co-resident, stalled, or the
+// debug_stall test knob): raise the per-launch flag -- every other spin of this launch then
+// stops at once -- and the persistent error word the host reads (EngineErrorFlag in Python),
+// which turns the silently partial update into a RuntimeError.
+__device__ __forceinline__ void spin_give_up(const PPOArgs& a, unsigned* tflag) {
+  atomicOr(tflag, 1u);
+  if (a.err) atomicOr(a.err, 1u);
+}
+
 // Geometry of one net layer in the LDS images (all offsets in floats, uniform).
 struct LG {
   int din, dout, w, ldw, b, h, ldh, z, ldz, db;
@@ -573,6 +582,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   unsigned* arrive = g.sync + (ns ? 4 * q : 0);
   unsigned* tflag = g.sync + 1;
   unsigned* arrive2 = g.sync + (ns ? 4 * q + 2 : 2);
+  const unsigned spin_lim = a.spin_limit ? a.spin_limit : (1u << 22);
+  // test knob: the last working workgroup never publishes, so its partners' spins time out
+  const bool stall = a.debug_stall != 0 && bid == (ns ? 2 * G : G) - 1;
   __syncthreads();
 
   for (int k = 0; k < K; ++k) {
@@ -998,13 +1010,13 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       __syncthreads();
       const unsigned long long e1 = a.prof ? clock64() : 0;
       if (tid == 0) {
-        atomicAdd(arrive, 1u);
+        if (!stall) atomicAdd(arrive, 1u);
         const unsigned target = (unsigned)G * (unsigned)(k + 1);
         unsigned spins = 0;
         while (ld_sc1u(arrive) < target) {
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 22) || ld_sc1u(tflag) != 0u) {
-            atomicOr(tflag, 1u);
+          if (++spins > spin_lim || ld_sc1u(tflag) != 0u) {
+            spin_give_up(a, tflag);
             break;
           }
         }
@@ -1090,13 +1102,13 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-          atomicAdd(arrive2, 1u);
+          if (!stall) atomicAdd(arrive2, 1u);
           const unsigned target = (unsigned)G * (unsigned)(k + 1);
           unsigned spins = 0;
           while (ld_sc1u(arrive2) < target) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 22) || ld_sc1u(tflag) != 0u) {
-              atomicOr(tflag, 1u);
+            if (++spins > spin_lim || ld_sc1u(tflag) != 0u) {
+              spin_give_up(a, tflag);
               break;
             }
           }
@@ -1184,13 +1196,13 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       if (tid == 0) {
         unsigned long long* xs = reinterpret_cast<unsigned long long*>(g.sync + 8);
         const unsigned long long tag = (unsigned long long)(unsigned)(k + 1) << 32;
-        __hip_atomic_store(xs + q, tag | __float_as_uint(tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!stall) __hip_atomic_store(xs + q, tag | __float_as_uint(tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long o = __hip_atomic_load(xs + (1 - q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
         while ((o >> 32) != (unsigned long long)(unsigned)(k + 1)) {
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 22) || ld_sc1u(tflag) != 0u) {
-            atomicOr(tflag, 1u);
+          if (++spins > spin_lim || ld_sc1u(tflag) != 0u) {
+            spin_give_up(a, tflag);
             break;
           }
           o = __hip_atomic_load(xs + (1 - q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1348,6 +1360,20 @@ constexpr int bslots_ns() { return 2; }
 
 }  // namespace
 
+int device_cu_count() {
+  const char* ev = getenv("IMITATION_AMD_PPO_CUS");
+  if (ev && atoi(ev) > 0) return atoi(ev);
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 // Host planning: LDS images + parameter items + workgroup split. Returns false if the
 // configuration is outside the fast path (falls back to ppo.hip).
 bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
@@ -1377,7 +1403,16 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     cw = 16;
   }
   const int chunks = a.batch / cw;
-  const int gmax = a.rc_gmax > 0 ? (a.rc_gmax < kMaxRcGroups ? a.rc_gmax : kMaxRcGroups) : kMaxRcGroups;
+  int gmax = a.rc_gmax > 0 ? (a.rc_gmax < kMaxRcGroups ? a.rc_gmax : kMaxRcGroups) : kMaxRcGroups;
+  {  // co-residency: every spinning workgroup must hold a CU of its own (> 80 KiB of LDS: one
+     // per CU) while the rest of the chip stays free for concurrent streams (the discriminator
+     // runs beside the update), so the working blocks are capped at half the device's CUs
+    const int cus = a.rc_cus > 0 ? a.rc_cus : device_cu_count();
+    const int per = (ns && cw == 64) ? 2 : 1;  // net split: two workgroups per row group
+    const int cap = (cus / 2) / per;
+    if (cap < 1) return false;
+    if (gmax > cap) gmax = cap;
+  }
   int G = 1;
   for (int c = gmax; c >= 1; --c)
     if (chunks % c == 0) {
@@ -1546,6 +1581,10 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
     const bool on = ev ? ev[0] == '1' : true;
     g.xcd = 1;
     if (on && nblk > 1) g.xcd = nblk <= 16 ? 8 : nblk <= 32 ? 4 : nblk <= 64 ? 2 : 1;
+    // never a wider stride than the device has XCDs (32 CUs each; a partitioned device has fewer)
+    const int cus = a.rc_cus > 0 ? a.rc_cus : device_cu_count();
+    const int xcds = cus / 32 > 1 ? cus / 32 : 1;
+    while (g.xcd > xcds) g.xcd >>= 1;
   }
   const dim3 grid(nblk * g.xcd), block(64 * g.nw);
   int wmx = g.n_witems, bmx = g.n_items - g.n_witems;
@@ -1554,10 +1593,10 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
     bmx = g.nbit[0] > g.nbit[1] ? g.nbit[0] : g.nbit[1];
   }
   const int nwslot = (wmx + g.nw - 1) / g.nw, nbslot = (bmx + g.nw - 1) / g.nw;
-#define IA_RC(KT, KW, KB, S0, NL, ACT, HW, CW, DT) \
-  hipLaunchKernelGGL((ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, CW, DT, waves_for(KT)>), grid, block, lds_launch, s, a, g)
-#define IA_RC_NS(KT, KW, KB, S0, NL, ACT, HW, DT) \
-  hipLaunchKernelGGL((ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, 64, DT, 4>), grid, block, lds_launch, s, a, g)
+  typedef void (*RcKernel)(PPOArgs, PPORcGeo);
+  RcKernel kern = nullptr;
+#define IA_RC(KT, KW, KB, S0, NL, ACT, HW, CW, DT) kern = ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, CW, DT, waves_for(KT)>
+#define IA_RC_NS(KT, KW, KB, S0, NL, ACT, HW, DT) kern = ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, 64, DT, 4>
   const auto fits = [&](int kw, int kb) { return nwslot <= kw && nbslot <= kb; };
   if (g.ns) {
     if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && !a.discrete && fits(3, 1))
@@ -1588,6 +1627,18 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
     IA_RC(4, wslots_for(4), bslots_for(4), 0, 0, -1, 0, 0, -1);
 #undef IA_RC
 #undef IA_RC_NS
+  if (nblk > 1) {
+    // every working block must be resident at once: check the instance's occupancy at this
+    // LDS size against the device (the plan capped the working blocks at half the CUs)
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), (int)block.x,
+                                                     lds_launch) != hipSuccess)
+      per_cu = 1;
+    if (per_cu > 1 && lds_launch > 80 * 1024) per_cu = 1;  // LDS holds one block per CU (the API can read high)
+    const int cus = a.rc_cus > 0 ? a.rc_cus : device_cu_count();
+    if (per_cu < 1 || (long long)per_cu * cus < (long long)nblk) return hipErrorCooperativeLaunchTooLarge;
+  }
+  hipLaunchKernelGGL(kern, grid, block, lds_launch, s, a, g);
   return hipGetLastError();
 }
 

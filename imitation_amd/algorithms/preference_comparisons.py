@@ -1333,6 +1333,9 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
             # the last iteration's collectives are checked blocking: a NaN-poisoned one-shot
             # all-reduce there must raise, not return NaN weights
             pdist.check_comm("preference iteration", blocking=i == len(schedule) - 1)
+            check = getattr(self.trajectory_generator, "check_errors", None)  # device agent (PPO kernel)
+            if check is not None:
+                check(blocking=i == len(schedule) - 1)
             self.logger.dump(self._iteration)
             if callback:
                 callback(self._iteration)

@@ -273,6 +273,9 @@ class DeviceGeneratorCore:
         self._seed = int(np.random.randint(0, 2**62)) ^ (pdist.rank() * 0x9E3779B97F4A7C15 & ((1 << 62) - 1))
         self._step0 = 0
         self._perm_round = 0
+        from imitation_amd.utils.errflag import DeviceErrorFlag
+
+        self._ppo_err = DeviceErrorFlag(self._dev, "PPO update kernel")
         self._ppo_static = self._ppo_args_static()
         self._ep_lens_running = np.zeros(self.N, dtype=np.int64)
 
@@ -307,7 +310,11 @@ class DeviceGeneratorCore:
                  exp_avg_sq=self.exp_avg_sq, n_params=fp.n, has_norm=int(self.pol_norm is not None),
                  rows=self.T * self.N, batch=int(algo.batch_size), n_epochs=int(algo.n_epochs),
                  ent_coef=float(algo.ent_coef), vf_coef=float(algo.vf_coef), max_grad_norm=float(algo.max_grad_norm),
-                 normalize_advantage=int(algo.normalize_advantage), adam_step=self.adam_step, stats=self.stats)
+                 normalize_advantage=int(algo.normalize_advantage), adam_step=self.adam_step, stats=self.stats,
+                 err=self._ppo_err.word,
+                 # fail-fast knobs of the cooperating-workgroup kernel (tests force a timeout)
+                 spin_limit=int(os.environ.get("IMITATION_AMD_PPO_SPIN", "0")),
+                 debug_stall=int(os.environ.get("IMITATION_AMD_PPO_DEBUG_STALL", "0")))
         opt = algo.policy.optimizer
         g = opt.param_groups[0]
         d.update(beta1=float(g.get("betas", (0.9, 0.999))[0]), beta2=float(g.get("betas", (0.9, 0.999))[1]),
@@ -415,8 +422,14 @@ class DeviceGeneratorCore:
                 self._C.engine_ppo_update(d)
         if self.pol_norm is not None:
             self.pol_norm.count.copy_(self.norm_count.to(self.pol_norm.count.dtype).reshape(()))
+        # reads the error word of an EARLIER update (non-blocking); train() ends blocking
+        self._ppo_err.check("PPO update")
         algo._n_updates += algo.n_epochs
         self._last_ppo_info = (rows, algo.n_epochs * (rows // algo.batch_size))
+
+    def check_errors(self, blocking: bool = False) -> None:
+        """Raise if a cooperating PPO workgroup timed out in any update so far."""
+        self._ppo_err.check("PPO update", blocking=blocking)
 
     def _setup_dp(self) -> None:
         """Data-parallel PPO plan. With the register-chained kernel available for the global
@@ -939,6 +952,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             if callback:
                 callback(r)
             self.logger.dump(self._global_step)
+        self.check_errors(blocking=True)
 
     def train(self, total_timesteps: int, callback=None) -> None:
         """Rounds of device generator training + fused discriminator updates; the
@@ -980,6 +994,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 callback(r)
             self.logger.dump(self._global_step)
         pdist.check_comm("GAIL training", blocking=True)
+        self.check_errors(blocking=True)
 
     def _launch_rollout(self) -> th.cuda.Event:
         """Enqueue one rollout (chain + post pass) and the async copy of its dones / returns to

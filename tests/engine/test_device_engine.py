@@ -543,3 +543,58 @@ def test_device_airl_fused_rounds_train_and_log():
     assert all(th.isfinite(p).all() for p in list(gen.policy.parameters()) + list(rn.parameters()))
     assert any(not th.equal(a, b) for a, b in zip(r0, rn.parameters()))
     assert tr._disc_step == 3 * tr.n_disc_updates_per_round
+
+
+def _plan_dict(batch: int, rows: int, rc_cus: int, width: int = 32, act: int = 2):
+    pi = [17, width, width, 6]
+    vf = [17, width, width, 1]
+    return dict(D=17, A=6, discrete=0, pi_dims=pi, vf_dims=vf, batch=batch, rows=rows, log_std_off=0,
+                rc_gmax=0, rc_cw=0, rc_cus=rc_cus, hidden_act=act)
+
+
+def test_ppo_plan_caps_cooperating_groups_by_device_cus():
+    """ppo_rc_plan (csrc/kernels/ppo_rc.hip) keeps every spinning workgroup co-resident: the
+    working blocks (2 x G under the net split) are capped at half the device's CUs; a device
+    too small for even one actor / critic pair falls back to the single-workgroup LDS kernel.
+    Host-only planning (runs on CPU)."""
+    from imitation_amd import _native
+
+    C = _native.load()
+    # MI355X (256 CUs): the 16-chunk minibatch spreads over 16 row groups x 2 nets
+    assert C.engine_ppo_path(_plan_dict(1024, 4096, 256)) == "rc:g16x1x64:kt2:ns"
+    # a 16-CU device: at most 8 working blocks -> 4 row groups of 4 chunks each
+    assert C.engine_ppo_path(_plan_dict(1024, 4096, 16)) == "rc:g4x4x64:kt2:ns"
+    assert C.engine_ppo_path(_plan_dict(1024, 4096, 8)) == "rc:g2x8x64:kt2:ns"
+    # 2 CUs: the actor / critic pair would be the whole device -> non-cooperative kernel
+    assert C.engine_ppo_path(_plan_dict(64, 4096, 2)) == "lds"
+    # the device query is the default (CPU host: no device -> the MI355X count)
+    d = _plan_dict(64, 4096, 0)
+    assert C.engine_ppo_path(d).startswith("rc:g1x1x64")
+
+
+@gpu
+@pytest.mark.parametrize("batch,path", [(64, "rc:g1x1x64:kt2:ns"), (256, "rc:g4x1x64:kt2:ns")])
+def test_ppo_kernel_timeout_raises(batch, path):
+    """Fail-fast: a cooperating workgroup that never publishes (debug_stall knob)
+    makes its partners' bounded spins give up; the persistent error word turns the partial
+    update into a RuntimeError at the engine's check instead of a silent update."""
+    tr, venv, gen, rn = _setup(n_envs=8, n_steps=64, batch=batch, n_epochs=1)
+    assert tr._C.engine_ppo_path(tr._ppo_static) == path
+    tr._rollout()
+    tr._ppo_update()
+    th.cuda.synchronize()
+    tr.check_errors(blocking=True)  # a healthy update: no error
+    tr._ppo_static["debug_stall"] = 1
+    tr._ppo_static["spin_limit"] = 4096
+    tr._rollout()
+    tr._ppo_update()
+    th.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        tr.check_errors(blocking=True)
+    # the word was cleared: a healthy update afterwards passes again
+    tr._ppo_static["debug_stall"] = 0
+    tr._ppo_static["spin_limit"] = 0
+    tr._rollout()
+    tr._ppo_update()
+    th.cuda.synchronize()
+    tr.check_errors(blocking=True)
