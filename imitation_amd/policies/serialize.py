@@ -91,7 +91,8 @@ def _load_from_hub(algo_name: str, cls: Type) -> PolicyLoaderFn:
 policy_registry.register("random", value=registry.build_loader_fn_require_space(base.RandomPolicy))
 policy_registry.register("zero", value=registry.build_loader_fn_require_space(base.ZeroPolicy))
 
-_ALGOS = {"ppo": "imitation_amd.rl.ppo:PPO", "sac": "imitation_amd.rl.sac:SAC", "dqn": "imitation_amd.rl.dqn:DQN"}
+_ALGOS = {"ppo": "imitation_amd.rl.ppo:PPO", "sac": "imitation_amd.rl.sac:SAC", "dqn": "imitation_amd.rl.dqn:DQN",
+          "td3": "imitation_amd.rl.td3:TD3", "ddpg": "imitation_amd.rl.td3:DDPG"}
 
 
 def _lazy(loader_factory, *args):

@@ -93,6 +93,35 @@ def test_sac_runs_and_saves(tmp_path, rng):
     np.testing.assert_allclose(model.predict(obs, deterministic=True)[0], loaded.predict(obs, deterministic=True)[0], rtol=1e-5)
 
 
+@pytest.mark.parametrize("name", ["TD3", "DDPG"])
+def test_td3_ddpg_run_and_save(tmp_path, rng, name):
+    from imitation_amd.rl import noise, td3
+
+    cls = getattr(td3, name)
+    venv = util.make_vec_env("Pendulum-v1", rng=rng, n_envs=1)
+    an = noise.NormalActionNoise(np.zeros(1), 0.1 * np.ones(1), rng=np.random.default_rng(0))
+    model = cls("MlpPolicy", venv, learning_starts=50, buffer_size=1000, batch_size=32, device="cpu", seed=0,
+                action_noise=an, policy_kwargs=dict(net_arch=[32, 32]))
+    model.learn(200)
+    model.save(tmp_path / f"{name}.zip")
+    loaded = cls.load(tmp_path / f"{name}.zip", env=venv, device="cpu")
+    obs = np.random.rand(5, 3).astype(np.float32)
+    np.testing.assert_allclose(model.predict(obs, deterministic=True)[0], loaded.predict(obs, deterministic=True)[0], rtol=1e-5)
+
+
+def test_ou_noise_is_temporally_correlated_and_resets():
+    from imitation_amd.rl import noise
+
+    ou = noise.OrnsteinUhlenbeckActionNoise(np.zeros(2), 0.3 * np.ones(2), rng=np.random.default_rng(0))
+    xs = np.stack([ou() for _ in range(2000)])
+    assert xs.shape == (2000, 2)
+    assert np.corrcoef(xs[:-1, 0], xs[1:, 0])[0, 1] > 0.9
+    ou.reset()
+    assert np.all(ou.noise_prev == 0)
+    vec = noise.VectorizedActionNoise(noise.NormalActionNoise(np.zeros(3), np.ones(3)), n_envs=4)
+    assert vec().shape == (4, 3)
+
+
 def test_rollout_buffer_generator_covers_all_rows():
     from imitation_amd.envs import spaces
 
