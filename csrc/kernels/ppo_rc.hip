@@ -1346,7 +1346,14 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     if (nc == 0) a.norm_count[0] = run_c;
   }
   if (shared_wb && tid == 0) a.adam_step[0] = step;
-  if (shared_wb && a.prof && tid < 16) a.prof[tid] += sprof[tid];  // (stats barrier above orders the LDS)
+  // (stats barrier above orders the LDS). Net split: the critic workgroup owns the critic
+  // row-tile counters [7..10] (the actor's are zero there), added atomically
+  if (a.prof && tid < 16) {
+    const bool critic_slot = tid >= 7 && tid <= 10;
+    if (!ns) a.prof[tid] += sprof[tid];
+    else if (q == 0 && !critic_slot) a.prof[tid] += sprof[tid];
+    else if (q == 1 && critic_slot) atomicAdd(a.prof + tid, sprof[tid]);
+  }
 }
 
 // waves per workgroup (NW) and owned weight / bias slots per wave of each tile width
