@@ -247,6 +247,7 @@ std::string ppo_path(py::dict d) {
   a.rc_gmax = ival(d, "rc_gmax", 0);
   a.rc_cw = ival(d, "rc_cw", 0);
   a.rc_cus = ival(d, "rc_cus", 0);
+  a.hidden_act = ival(d, "hidden_act", 0);  // selects the shape-specialised instance family
   ia::PPORcGeo geo;
   size_t lds = 0;
   if (ival(d, "allow_rc", 1) && ia::ppo_rc_plan(a, geo, lds))

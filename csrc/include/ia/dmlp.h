@@ -65,7 +65,11 @@ __device__ inline float act_apply(int act, float x) { return apply_act(act, x); 
 // (kept for the backward pass), the last layer's (fp32, bias added, identity) outputs to
 // out[row * out_ld + col] for col < dims[L] (<= 16). Wf[l]: pre-staged weight images.
 // Each wave works on its own 16 rows only, so layers need no barrier between them.
-__device__ inline void mlp_forward(const AirlNet& net, lbf* const* Hs, int ld, lbf* const* Wf, lfl* out, int out_ld) {
+// Hs / Wf (and Wt / dZ / dZT below): anything indexable by layer -- pointer arrays, or
+// accessors that compute the image address (pref_rm.hip: a run-time-indexed array of LDS
+// pointers would live in scratch).
+template <class HA, class WA>
+__device__ inline void mlp_forward(const AirlNet& net, const HA& Hs, int ld, const WA& Wf, lfl* out, int out_ld) {
   const int w = wave_id();
   for (int l = 0; l < net.n_layers; ++l) {
     const int din = net.dims[l], dout = net.dims[l + 1];
@@ -100,8 +104,9 @@ __device__ inline float wave_colsum(float s) {
 // Backward of an MLP (identity output, dout = 1) from per-row output gradients dy[64]:
 // dW / db into slab[param offsets] (acc: add to what an earlier pass of this block wrote).
 // Scratch: HT [feature][row] (ld_ht), dZ [row][k] (ld) and dZT [k][row] (ld_ht), x2.
-__device__ inline void mlp_backward(const AirlNet& net, lbf* const* Hs, int ld, lbf* const* Wt, const lfl* dy, lbf* HT, int ld_ht,
-                             lbf* const* dZ, lbf* const* dZT, lfl* dbs, int dmax_pad, float* slab, bool acc_mode) {
+template <class HA, class WA, class ZA>
+__device__ inline void mlp_backward(const AirlNet& net, const HA& Hs, int ld, const WA& Wt, const lfl* dy, lbf* HT, int ld_ht,
+                             const ZA& dZ, const ZA& dZT, lfl* dbs, int dmax_pad, float* slab, bool acc_mode) {
   const int w = wave_id(), lane = lane_id();
   const int L = net.n_layers;
   // last layer: dZ = dy (identity head, one output column)

@@ -275,16 +275,18 @@ __global__ __launch_bounds__(64 * kPrepWaves) void ppo_rc_prep_kernel(PPOArgs a,
 }
 
 // ---------------------------------------------------------------- main kernel
+template <int S0M>
 struct Rows {  // one chunk's rows for this lane, prefetched a chunk ahead
-  float x[16];  // raw obs: feature 4s + kk of row lane&15 (s < S0)
+  float x[S0M];  // raw obs: feature 4s + kk of row lane&15 (s < S0)
   f4 act;       // actions 4kk..4kk+3 (Gaussian) / act index in .x (discrete)
   f4 rd;        // old_logp, adv_n, return
 };
 
-__device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int row, int kk, int s0, Rows& r) {
+template <int S0M>
+__device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int row, int kk, int s0, Rows<S0M>& r) {
   const float* xr = g.xraw + (slot * 64 + row) * g.dp;
 #pragma unroll
-  for (int s = 0; s < 16; ++s)
+  for (int s = 0; s < S0M; ++s)
     if (s < s0) r.x[s] = xr[4 * s + kk];
   const float* ac = g.acts + (slot * 64 + row) * 16;
   r.act = *reinterpret_cast<const f4*>(ac + 4 * kk);
@@ -427,6 +429,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   const bool rows_wave = gw < RT;
   const int nl = NLT > 0 ? NLT : (q == 0 ? a.n_pi : a.n_vf);
   const int D = a.D, A = a.A;
+  // S0T > 0: exact input k-steps; S0T < 0: at most -S0T (run-time count, register arrays sized
+  // to the bound); 0: generic (<= 16)
+  constexpr int S0M = S0T > 0 ? S0T : (S0T < 0 ? -S0T : 16);
   const int s0 = S0T > 0 ? S0T : (D + 3) / 4;
   const bool gauss = DT >= 0 ? DT == 0 : !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
@@ -566,7 +571,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     pre_m = g.mom[128 + nc];
     pre_v = g.mom[128 + 64 + nc];
   }
-  Rows cur;
+  Rows<S0M> cur;
   const int row = 16 * gw + r16;
   const int rp = (row & 3) * rq + (row >> 2);  // this lane's row in the K-major images
   // chunk unit u = k * nch + ch -> prep slot k * CH + grp * nch + ch
@@ -596,7 +601,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     for (int ib = 0; ib < KB; ++ib) bg[ib] = 0.f;
     for (int ch = 0; ch < nch; ++ch) {
       const int u = k * nch + ch;
-      Rows nxt;
+      Rows<S0M> nxt;
       if (rows_wave && u + 1 < K * nch) load_rows(g, slot_of(u + 1), row, kk, s0, nxt);
       // moments of minibatch k+1 (prefetched one minibatch earlier) -> registers; issue k+2
       float mom_m = 0.f, mom_v = 0.f;
@@ -612,11 +617,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       if (rows_wave) {
         // ---------------- normalised input: B operand of layer 0 (natural K order 4s + kk)
         // (padding features: raw value 0 from the prep kernel, normaliser image entries 0)
-        float xb[16];
+        float xb[S0M];
         {
-          float nmv[16], nrv[16];
+          float nmv[S0M], nrv[S0M];
 #pragma unroll
-          for (int s = 0; s < 16; ++s) {
+          for (int s = 0; s < S0M; ++s) {
             nmv[s] = 0.f;
             nrv[s] = 1.f;
             if (s < s0 && a.has_norm) {
@@ -625,12 +630,12 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
             }
           }
 #pragma unroll
-          for (int s = 0; s < 16; ++s) xb[s] = s < s0 ? (cur.x[s] - nmv[s]) * nrv[s] : 0.f;
+          for (int s = 0; s < S0M; ++s) xb[s] = s < s0 ? (cur.x[s] - nmv[s]) * nrv[s] : 0.f;
         }
         if (q == 0 || ns) {  // shared layer-0 input image (each workgroup its own under net split)
           const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
 #pragma unroll
-          for (int s = 0; s < 16; ++s)
+          for (int s = 0; s < S0M; ++s)
             if (s < s0) L[h0 + (4 * s + kk) * ld0 + rp] = xb[s];
         }
         unsigned long long c1 = a.prof ? clock64() : 0;
@@ -651,27 +656,27 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           if (l == 0 && KT > 2) {  // 64-wide: two tiles' operands at a time (register budget)
 #pragma unroll
             for (int t0 = 0; t0 < KT; t0 += 2) {
-              float w0[2][16];
+              float w0[2][S0M];
 #pragma unroll
               for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 16; ++s)
+                for (int s = 0; s < S0M; ++s)
                   if (t0 + t < tout && s < s0) w0[t][s] = L[y.w + (16 * (t0 + t) + r16) * y.ldw + 4 * s + kk];
 #pragma unroll
-              for (int s = 0; s < 16; ++s)
+              for (int s = 0; s < S0M; ++s)
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
                   if (t0 + t < tout && s < s0) acc[t0 + t] = mfma(w0[t][s], xb[s], acc[t0 + t]);
             }
           } else if (l == 0) {
-            float w0[KT][16];
+            float w0[KT][S0M];
 #pragma unroll
             for (int t = 0; t < KT; ++t)
 #pragma unroll
-              for (int s = 0; s < 16; ++s)
+              for (int s = 0; s < S0M; ++s)
                 if (t < tout && s < s0) w0[t][s] = L[y.w + (16 * t + r16) * y.ldw + 4 * s + kk];
 #pragma unroll
-            for (int s = 0; s < 16; ++s)
+            for (int s = 0; s < S0M; ++s)
 #pragma unroll
               for (int t = 0; t < KT; ++t)
                 if (t < tout && s < s0) acc[t] = mfma(w0[t][s], xb[s], acc[t]);
@@ -1364,8 +1369,54 @@ constexpr int bslots_for(int kt) { return kt == 2 ? 2 : 3; }
 // net split (4 waves, one net's items): up to 20 / 32 weight tiles and 8 vectors per net
 constexpr int wslots_ns(int kt) { return kt == 2 ? 5 : 8; }
 constexpr int bslots_ns() { return 2; }
+// generic both-nets build at 4 waves (<= 32-wide nets): up to 20 weight tiles (3-layer nets with
+// obs dim <= 32), 8 vectors
+constexpr int kNarrow4W = 5;
+constexpr int kNarrow4B = 2;
 
 }  // namespace
+
+// Shape-specialised instances (0 = generic). Shared by the plan (which sizes chunks / waves
+// for the instance that will run) and the launch. Every instance the plan can reach compiles
+// without scratch (tools/kernel_resources.py, profiles/r4_kernel_resources.md).
+enum RcInst : int {
+  RC_GENERIC = 0,
+  RC_NS_CHEETAH32,    // HalfCheetah / Walker2d FeedForward32Policy (tanh), net split
+  RC_NS_CARTPOLE32,   // CartPole FeedForward32Policy, net split
+  RC_NS_HOPPER64R,    // Hopper MlpPolicy [64, 64] ReLU (AIRL config)
+  RC_NS_WALKER64R,    // Walker2d MlpPolicy [64, 64] ReLU (DRLHP config)
+  RC_NS_64_D16,       // any 3-layer [64, 64] net, obs dim <= 16 (SB3 MlpPolicy default: CartPole, Hopper, ...)
+  RC_NS_64_D32,       // any 3-layer [64, 64] net, obs dim <= 32 (HalfCheetah / Walker2d / Ant, ...)
+  RC_CHEETAH32_64,    // both nets per workgroup, 64-row chunks
+  RC_CHEETAH32_32,    // the same, 32-row chunks
+  RC_HOPPER64R_32,
+  RC_WALKER64R_32,
+  RC_CARTPOLE32_64,
+};
+
+static int rc_instance(const PPOArgs& a, int kt, int cw, bool ns) {
+  const int hw = a.pi_dims[1];
+  bool uniform = a.n_pi == 3 && a.n_vf == 3;
+  for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
+  const int s0 = (a.D + 3) / 4;
+  const bool gauss = !a.discrete;
+  const bool act_ok = a.hidden_act == 1 || a.hidden_act == 2;
+  if (ns) {
+    if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && kt == 2 && gauss) return RC_NS_CHEETAH32;
+    if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && kt == 2 && !gauss) return RC_NS_CARTPOLE32;
+    if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && kt == 4 && gauss) return RC_NS_HOPPER64R;
+    if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && kt == 4 && gauss) return RC_NS_WALKER64R;
+    if (uniform && hw == 64 && kt == 4 && act_ok && a.D <= 16) return RC_NS_64_D16;
+    if (uniform && hw == 64 && kt == 4 && act_ok && a.D <= 32) return RC_NS_64_D32;
+    return RC_GENERIC;
+  }
+  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && kt == 2 && cw == 64 && gauss) return RC_CHEETAH32_64;
+  if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && kt == 2 && cw == 32 && gauss) return RC_CHEETAH32_32;
+  if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && kt == 4 && cw == 32 && gauss) return RC_HOPPER64R_32;
+  if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && kt == 4 && cw == 32 && gauss) return RC_WALKER64R_32;
+  if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && kt == 2 && cw == 64 && !gauss) return RC_CARTPOLE32_64;
+  return RC_GENERIC;
+}
 
 int device_cu_count() {
   const char* ev = getenv("IMITATION_AMD_PPO_CUS");
@@ -1409,6 +1460,16 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   if (a.batch % cw != 0) {
     cw = 16;
   }
+  bool narrow4 = false;  // generic both-nets build at one wave per SIMD (4 waves, <= 32-row chunks)
+  if (!(ns && cw == 64) && rc_instance(a, KT, cw, false) == RC_GENERIC) {
+    // the 8-wave generic build has 256 registers per wave and spills: run the 4-wave build
+    // (2 row-tile waves per net, 512 registers each) for <= 32-wide nets; the 64-wide generic
+    // both-nets layout cannot hold its owned items without scratch -> the LDS kernel (ppo.hip)
+    if (KT == 4) return false;
+    narrow4 = true;
+    if (cw > 32) cw = 32;
+    if (a.batch % cw != 0) cw = 16;
+  }
   const int chunks = a.batch / cw;
   int gmax = a.rc_gmax > 0 ? (a.rc_gmax < kMaxRcGroups ? a.rc_gmax : kMaxRcGroups) : kMaxRcGroups;
   {  // co-residency: every spinning workgroup must hold a CU of its own (> 80 KiB of LDS: one
@@ -1430,7 +1491,10 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.G = G;
   g.nch = chunks / G;
   g.ns = ns && cw == 64 ? 1 : 0;
-  if (g.ns) g.nw = 4;
+  if (g.ns || narrow4) g.nw = 4;
+  // the generic 64-wide net-split build needs scratch (8 weight slots + 2 vectors at runtime
+  // shapes): nets outside the specialised [64, 64] families take the LDS kernel
+  if (g.ns && KT == 4 && rc_instance(a, KT, cw, true) == RC_GENERIC) return false;
   int off = 0;
   auto take = [&](int n) {
     const int o = off;
@@ -1529,7 +1593,16 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     wmx = g.nwit[0] > g.nwit[1] ? g.nwit[0] : g.nwit[1];
     bmx = g.nbit[0] > g.nbit[1] ? g.nbit[0] : g.nbit[1];
   }
-  const int wcap = g.ns ? wslots_ns(KT) : wslots_for(KT), bcap = g.ns ? bslots_ns() : bslots_for(KT);
+  int wcap = g.ns ? wslots_ns(KT) : wslots_for(KT), bcap = g.ns ? bslots_ns() : bslots_for(KT);
+  if (narrow4) {
+    wcap = kNarrow4W;
+    bcap = kNarrow4B;
+  }
+  {  // the specialised instances size their slots to the shape they were built for
+    const int inst = rc_instance(a, KT, cw, g.ns != 0);
+    if (inst == RC_NS_64_D16) { wcap = 6; bcap = 1; }
+    if (inst == RC_NS_64_D32) { wcap = 7; bcap = 1; }
+  }
   if ((wmx + g.nw - 1) / g.nw > wcap || (bmx + g.nw - 1) / g.nw > bcap) return false;
   g.dp = (a.D + 3) & ~3;
   return true;
@@ -1563,18 +1636,10 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
     g.xchg2 = ev ? (ev[0] == '1' && g.G > 1) : (g.G >= (g.kt == 4 ? 4 : 16));
   }
   if (K == 0) return hipSuccess;
-  const int CH = g.G * g.nch;
-  const int prep_waves = CH < kPrepWaves ? CH : kPrepWaves;
-  hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64 * prep_waves), 0, s, a, g);
   // > 80 KiB of LDS keeps the cooperating workgroups one per CU (the measured condition of
   // the sc1 hand-off); all G <= kMaxRcGroups (64) of them are co-resident (256 CUs)
   // (net split: the two workgroups must not share a CU's matrix cores either)
   const size_t lds_launch = (g.G > 1 || g.ns) && lds < 96 * 1024 ? 96 * 1024 : lds;
-  // shape-specialised builds for the headline configs, generic otherwise
-  int hw = a.pi_dims[1];
-  bool uniform = a.n_pi == 3 && a.n_vf == 3;
-  for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
-  const int s0 = (a.D + 3) / 4;
   const int nblk = g.ns ? 2 * g.G : g.G;
   {  // cooperating workgroups on as few XCDs as possible (IMITATION_AMD_PPO_XCD=0 turns it off;
      // the "xcd" geometry field is the block stride). GAIL emulated W = 2 / 4 / 8: 3.14 / 3.28 / 3.64 -> 2.99 / 2.96 / 3.36 ms per update,
@@ -1605,33 +1670,40 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
 #define IA_RC(KT, KW, KB, S0, NL, ACT, HW, CW, DT) kern = ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, CW, DT, waves_for(KT)>
 #define IA_RC_NS(KT, KW, KB, S0, NL, ACT, HW, DT) kern = ppo_rc_kernel<KT, KW, KB, S0, NL, ACT, HW, 64, DT, 4>
   const auto fits = [&](int kw, int kb) { return nwslot <= kw && nbslot <= kb; };
-  if (g.ns) {
-    if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && !a.discrete && fits(3, 1))
-      IA_RC_NS(2, 3, 1, 5, 3, 2, 32, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
-    else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && a.discrete && fits(2, 1))
-      IA_RC_NS(2, 2, 1, 1, 3, 2, 32, 1);  // CartPole FeedForward32Policy
-    else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && !a.discrete && fits(6, 1))
-      IA_RC_NS(4, 6, 1, 3, 3, 1, 64, 0);  // Hopper MlpPolicy [64, 64] ReLU (AIRL config)
-    else if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && g.kt == 4 && !a.discrete && fits(7, 1))
-      IA_RC_NS(4, 7, 1, 5, 3, 1, 64, 0);  // Walker2d MlpPolicy [64, 64] ReLU (DRLHP config)
-    else if (g.kt == 2)
+  const bool cat = a.discrete != 0;
+  const int hact = a.hidden_act;
+  switch (rc_instance(a, g.kt, g.cw, g.ns != 0)) {
+    case RC_NS_CHEETAH32: if (fits(3, 1)) IA_RC_NS(2, 3, 1, 5, 3, 2, 32, 0); break;
+    case RC_NS_CARTPOLE32: if (fits(2, 1)) IA_RC_NS(2, 2, 1, 1, 3, 2, 32, 1); break;
+    case RC_NS_HOPPER64R: if (fits(6, 1)) IA_RC_NS(4, 6, 1, 3, 3, 1, 64, 0); break;
+    case RC_NS_WALKER64R: if (fits(7, 1)) IA_RC_NS(4, 7, 1, 5, 3, 1, 64, 0); break;
+    case RC_NS_64_D16:
+      if (hact == 1 && !cat) IA_RC_NS(4, 6, 1, -4, 3, 1, 64, 0);
+      else if (hact == 1) IA_RC_NS(4, 6, 1, -4, 3, 1, 64, 1);
+      else if (!cat) IA_RC_NS(4, 6, 1, -4, 3, 2, 64, 0);
+      else IA_RC_NS(4, 6, 1, -4, 3, 2, 64, 1);
+      break;
+    case RC_NS_64_D32:
+      if (hact == 1 && !cat) IA_RC_NS(4, 7, 1, -8, 3, 1, 64, 0);
+      else if (hact == 1) IA_RC_NS(4, 7, 1, -8, 3, 1, 64, 1);
+      else if (!cat) IA_RC_NS(4, 7, 1, -8, 3, 2, 64, 0);
+      else IA_RC_NS(4, 7, 1, -8, 3, 2, 64, 1);
+      break;
+    case RC_CHEETAH32_64: if (fits(3, 1)) IA_RC(2, 3, 1, 5, 3, 2, 32, 64, 0); break;
+    case RC_CHEETAH32_32: if (fits(3, 1)) IA_RC(2, 3, 1, 5, 3, 2, 32, 32, 0); break;
+    case RC_HOPPER64R_32: if (fits(12, 2)) IA_RC(4, 12, 2, 3, 3, 1, 64, 32, 0); break;
+    case RC_WALKER64R_32: if (fits(14, 2)) IA_RC(4, 14, 2, 5, 3, 1, 64, 32, 0); break;
+    case RC_CARTPOLE32_64: if (fits(2, 1)) IA_RC(2, 2, 1, 1, 3, 2, 32, 64, 1); break;
+    default: break;
+  }
+  if (kern == nullptr) {
+    if (g.ns && g.kt == 2)
       IA_RC_NS(2, wslots_ns(2), bslots_ns(), 0, 0, -1, 0, -1);
+    else if (g.kt == 2 && g.nw == 4)
+      kern = ppo_rc_kernel<2, kNarrow4W, kNarrow4B, 0, 0, -1, 0, 0, -1, 4>;
     else
-      IA_RC_NS(4, wslots_ns(4), bslots_ns(), 0, 0, -1, 0, -1);
-  } else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && !a.discrete && fits(3, 1))
-    IA_RC(2, 3, 1, 5, 3, 2, 32, 64, 0);  // HalfCheetah / Walker2d FeedForward32Policy (tanh)
-  else if (uniform && hw == 32 && s0 == 5 && a.hidden_act == 2 && g.kt == 2 && g.cw == 32 && !a.discrete && fits(3, 1))
-    IA_RC(2, 3, 1, 5, 3, 2, 32, 32, 0);  // the same, 32-row chunks (16 workgroups at the 8-rank DP minibatch)
-  else if (uniform && hw == 64 && s0 == 3 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete && fits(12, 2))
-    IA_RC(4, 12, 2, 3, 3, 1, 64, 32, 0);  // Hopper MlpPolicy [64, 64] ReLU (tuned AIRL config)
-  else if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && g.kt == 4 && g.cw == 32 && !a.discrete && fits(14, 2))
-    IA_RC(4, 14, 2, 5, 3, 1, 64, 32, 0);  // Walker2d MlpPolicy [64, 64] ReLU (DRLHP seals_walker config)
-  else if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && g.kt == 2 && g.cw == 64 && a.discrete && fits(2, 1))
-    IA_RC(2, 2, 1, 1, 3, 2, 32, 64, 1);  // CartPole FeedForward32Policy
-  else if (g.kt == 2)
-    IA_RC(2, wslots_for(2), bslots_for(2), 0, 0, -1, 0, 0, -1);
-  else
-    IA_RC(4, wslots_for(4), bslots_for(4), 0, 0, -1, 0, 0, -1);
+      return hipErrorInvalidValue;  // the plan never selects a spilling generic build
+  }
 #undef IA_RC
 #undef IA_RC_NS
   if (nblk > 1) {
@@ -1645,6 +1717,9 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
     const int cus = a.rc_cus > 0 ? a.rc_cus : device_cu_count();
     if (per_cu < 1 || (long long)per_cu * cus < (long long)nblk) return hipErrorCooperativeLaunchTooLarge;
   }
+  const int CH = g.G * g.nch;
+  const int prep_waves = CH < kPrepWaves ? CH : kPrepWaves;
+  hipLaunchKernelGGL(ppo_rc_prep_kernel, dim3((unsigned)K), dim3(64 * prep_waves), 0, s, a, g);
   hipLaunchKernelGGL(kern, grid, block, lds_launch, s, a, g);
   return hipGetLastError();
 }

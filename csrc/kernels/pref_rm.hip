@@ -167,30 +167,41 @@ __global__ __launch_bounds__(256) void pref_gather_kernel(PrefRmArgs a) {
   }
 }
 
-// LDS layout of pref_fwd / pref_bwd (PrefPlan): weight images, row images, backward scratch
+// LDS layout of pref_fwd / pref_bwd (PrefPlan): weight images, row images, backward scratch.
+// Image addresses are computed per use from the plan (a kernel argument, read with scalar
+// loads): an array of LDS pointers indexed by the run-time layer would be kept in scratch.
+struct WImg {  // forward ([o][i]) or transposed ([i][o]) weight image of layer l
+  char* smem;
+  const int* off;
+  __device__ lbf* operator[](int l) const { return (lbf*)(smem + off[l]); }
+};
+struct HImg {  // row image of layer l's input (the output layer reuses the last slot)
+  char* base;
+  int bytes, last;
+  __device__ lbf* operator[](int l) const { return (lbf*)(base + (size_t)min(l, last) * bytes); }
+};
+struct ZImg {  // double-buffered dZ / dZ^T images
+  char* base;
+  int stride;
+  __device__ lbf* operator[](int z) const { return (lbf*)(base + (size_t)z * stride); }
+};
 struct Imgs {
-  lbf* Wf[kAirlMaxLayers];
-  lbf* Wt[kAirlMaxLayers];
-  lbf* H[kAirlMaxLayers];
+  WImg Wf, Wt;
+  HImg H;
   lbf* HT;
-  lbf* dZ[2];
-  lbf* dZT[2];
+  ZImg dZ, dZT;
   lfl* dbs;
 };
 
 __device__ __forceinline__ Imgs carve(char* smem, const PrefPlan& p, int n_layers) {
   Imgs m;
-  for (int l = 0; l < kAirlMaxLayers; ++l) {
-    m.Wf[l] = (lbf*)(smem + p.wf_off[l]);
-    m.Wt[l] = (lbf*)(smem + p.wt_off[l]);
-    m.H[l] = (lbf*)(smem + p.rimg_off + (size_t)min(l, n_layers - 1) * p.rimg_bytes);
-  }
+  m.Wf = WImg{smem, p.wf_off};
+  m.Wt = WImg{smem, p.wt_off};
+  m.H = HImg{smem + p.rimg_off, p.rimg_bytes, n_layers - 1};
   char* sc = smem + p.scratch_off;
   m.HT = (lbf*)(sc);
-  m.dZ[0] = (lbf*)(sc + p.ht_bytes);
-  m.dZ[1] = (lbf*)(sc + p.ht_bytes + p.rimg_bytes);
-  m.dZT[0] = (lbf*)(sc + p.ht_bytes + 2 * p.rimg_bytes);
-  m.dZT[1] = (lbf*)(sc + 2 * p.ht_bytes + 2 * p.rimg_bytes);
+  m.dZ = ZImg{sc + p.ht_bytes, p.rimg_bytes};
+  m.dZT = ZImg{sc + p.ht_bytes + 2 * p.rimg_bytes, p.ht_bytes};
   m.dbs = (lfl*)(sc + 3 * p.ht_bytes + 2 * p.rimg_bytes);
   return m;
 }

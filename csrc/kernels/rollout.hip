@@ -153,12 +153,13 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
   return h;
 }
 
-// Generic (non-locomotion) envs step on lane 0 out of line, so their code does not
-// share the register budget of the kernel's step loop.
-__device__ __noinline__ float env_step_lane0(const EnvParams& P, float* s, const float* action, int* term, uint64_t* rng) {
+// Generic (non-locomotion) envs step on lane 0, inlined: an out-of-line call needs a stack
+// frame (544 B/lane of scratch in the generic instances), while the inlined switch fits the
+// loop's register budget (<= 222 VGPRs at two waves per SIMD, 0 scratch: tools/kernel_resources.py).
+__device__ __forceinline__ float env_step_lane0(const EnvParams& P, float* s, const float* action, int* term, uint64_t* rng) {
   return env_step(P, s, action, term, *rng);
 }
-__device__ __noinline__ void env_reset_lane0(const EnvParams& P, float* s, float* o, uint64_t* rng) {
+__device__ __forceinline__ void env_reset_lane0(const EnvParams& P, float* s, float* o, uint64_t* rng) {
   env_reset(P, s, *rng);
   env_obs(P, s, o);
 }

@@ -167,13 +167,14 @@ def supports_generator(venv, gen_algo) -> Tuple[bool, str]:
 
 def ppo_path(pol: ActorCriticPolicy, nat, batch: int, rows: int, rc_gmax: int = 0) -> str:
     """Which PPO kernel the engine would run (``"rc:g<G>x<nch>x<cw>:kt<KT>"`` or ``"lds"``)."""
-    norm, pl, vl, _ = _policy_nets(pol)
+    norm, pl, vl, act = _policy_nets(pol)
     discrete = isinstance(nat.action_space, spaces.Discrete)
     D = int(np.prod(nat.observation_space.shape))
     A = int(nat.action_space.n) if discrete else int(np.prod(nat.action_space.shape))
     d = dict(D=D, A=A, discrete=int(discrete), pi_dims=[D] + [l.out_features for l in pl],
              vf_dims=[D] + [l.out_features for l in vl], batch=int(batch), rows=int(rows),
-             log_std_off=0 if (hasattr(pol, "log_std") and not discrete) else -1, rc_gmax=int(rc_gmax))
+             log_std_off=0 if (hasattr(pol, "log_std") and not discrete) else -1, rc_gmax=int(rc_gmax),
+             hidden_act=int(act))
     return ops.native().engine_ppo_path(d)
 
 

@@ -120,9 +120,20 @@ def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, nor
     ("seals/HalfCheetah-v1", 1, 64, 0, "nons", "rc:g1x1x64:kt2"),
     ("seals/HalfCheetah-v1", 1, 256, 2, "nons", "rc:g2x2x64:kt2"),
     ("seals/CartPole-v0", 1, 256, 0, "nons", "rc:g4x1x64:kt2"),
-    ("seals/Hopper-v1", 1, 256, 4, dict(pi=[64, 64], vf=[64, 64], nons=True), "rc:g4x2x32:kt4"),
+    # 64-wide generic both-nets layout would need scratch: the plan hands it to the LDS kernel
+    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], nons=True), "lds"),
     ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g16x1x32:kt4"),
     ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g4x1x32:kt4"),
+    # SB3's default MlpPolicy ([64, 64] Tanh; reference scripts/ingredients/rl.py:58-66) and
+    # other [64, 64] nets on the spill-free family builds (obs dim <= 16 / <= 32, Tanh / ReLU,
+    # Gaussian / categorical heads)
+    ("seals/CartPole-v0", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64]), "rc:g1x1x64:kt4:ns"),
+    ("seals/CartPole-v0", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g2x1x64:kt4:ns"),
+    ("seals/HalfCheetah-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64]), "rc:g1x1x64:kt4:ns"),
+    ("seals/HalfCheetah-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g2x1x64:kt4:ns"),
+    ("Pendulum-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64]), "rc:g1x1x64:kt4:ns"),
+    # minibatch of 32: the generic <= 32-wide both-nets build at one wave per SIMD
+    ("Pendulum-v1", 1, 32, 0, None, "rc:g1x1x32:kt2"),
 ])
 def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_arch, path, monkeypatch):
     act = None
@@ -567,6 +578,17 @@ def test_ppo_plan_caps_cooperating_groups_by_device_cus():
     assert C.engine_ppo_path(_plan_dict(1024, 4096, 8)) == "rc:g2x8x64:kt2:ns"
     # 2 CUs: the actor / critic pair would be the whole device -> non-cooperative kernel
     assert C.engine_ppo_path(_plan_dict(64, 4096, 2)) == "lds"
+    # [64, 64] nets: the spill-free family builds; a non-uniform 64-wide net would need the
+    # generic build (scratch) and takes the LDS kernel instead
+    assert C.engine_ppo_path(_plan_dict(64, 4096, 256, width=64, act=2)) == "rc:g1x1x64:kt4:ns"
+    assert C.engine_ppo_path(_plan_dict(64, 4096, 256, width=64, act=1)) == "rc:g1x1x64:kt4:ns"
+    d = _plan_dict(64, 4096, 256, width=64)
+    d["pi_dims"] = [17, 64, 48, 6]
+    assert C.engine_ppo_path(d) == "lds"
+    # 32-row minibatches of a generic <= 32-wide net: both nets per 4-wave workgroup
+    d = _plan_dict(32, 4096, 256)
+    d["D"], d["pi_dims"], d["vf_dims"] = 3, [3, 32, 32, 1], [3, 32, 32, 1]
+    assert C.engine_ppo_path(d) == "rc:g1x1x32:kt2"
     # the device query is the default (CPU host: no device -> the MI355X count)
     d = _plan_dict(64, 4096, 0)
     assert C.engine_ppo_path(d).startswith("rc:g1x1x64")
