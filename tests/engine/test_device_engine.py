@@ -120,8 +120,9 @@ def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, nor
     ("seals/HalfCheetah-v1", 1, 64, 0, "nons", "rc:g1x1x64:kt2"),
     ("seals/HalfCheetah-v1", 1, 256, 2, "nons", "rc:g2x2x64:kt2"),
     ("seals/CartPole-v0", 1, 256, 0, "nons", "rc:g4x1x64:kt2"),
-    # 64-wide generic both-nets layout would need scratch: the plan hands it to the LDS kernel
-    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], nons=True), "lds"),
+    # [64, 64] Tanh, both nets per workgroup: the family build (obs dim <= 16)
+    ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], nons=True), "rc:g2x1x32:kt4"),
+    ("seals/HalfCheetah-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], nons=True), "rc:g2x1x32:kt4"),
     ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g16x1x32:kt4"),
     ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g4x1x32:kt4"),
     # SB3's default MlpPolicy ([64, 64] Tanh; reference scripts/ingredients/rl.py:58-66) and
