@@ -410,6 +410,45 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
   return outs;
 }
 
+// rows perm[*cursor * n + r] of every source into the caller-owned dst tensors (one launch,
+// no host arguments per minibatch: HIP-graph epochs)
+void gather_rows_cursor(std::vector<torch::Tensor> srcs, torch::Tensor perm, torch::Tensor cursor, int64_t n,
+                        std::vector<torch::Tensor> dst) {
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= ia::kGatherMax && dst.size() == srcs.size(), "gather_rows_cursor: 1..8 fields");
+  IA_CHECK_CUDA(perm);
+  IA_CHECK_CONTIG(perm);
+  IA_CHECK_CUDA(cursor);
+  TORCH_CHECK(perm.scalar_type() == torch::kInt32 && cursor.scalar_type() == torch::kInt32 && cursor.numel() >= 1,
+              "gather_rows_cursor: int32 perm / cursor");
+  ia::GatherArgs a{};
+  a.k = (int)srcs.size();
+  for (int i = 0; i < a.k; ++i) {
+    auto& t = srcs[i];
+    auto& o = dst[i];
+    IA_CHECK_CUDA(t);
+    IA_CHECK_CONTIG(t);
+    IA_CHECK_CONTIG(o);
+    const int64_t rows = t.size(0);
+    auto sizes = t.sizes().vec();
+    sizes[0] = n;
+    TORCH_CHECK(o.sizes().vec() == sizes && o.scalar_type() == t.scalar_type() && o.device() == t.device(),
+                "gather_rows_cursor: dst ", i, " shape / dtype / device");
+    a.f[i] = ia::GatherField{t.data_ptr(), o.data_ptr(), rows ? (int64_t)(t.nbytes() / rows) : 0, rows};
+  }
+  IA_HIP_CHECK(ia::gather_rows_cursor(a, perm.data_ptr<int>(), cursor.data_ptr<int>(), (int)n, ia_stream()));
+}
+
+void append_at_cursor(torch::Tensor src, torch::Tensor all, torch::Tensor cursor) {
+  IA_CHECK_CUDA(src);
+  IA_CHECK_CUDA(all);
+  IA_CHECK_CUDA(cursor);
+  TORCH_CHECK(src.scalar_type() == torch::kFloat32 && all.scalar_type() == torch::kFloat32 && src.is_contiguous() &&
+                  all.is_contiguous() && all.numel() % src.numel() == 0 && cursor.scalar_type() == torch::kInt32,
+              "append_at_cursor: fp32 src [n], all [m, n], int32 cursor");
+  IA_HIP_CHECK(ia::append_at_cursor(src.data_ptr<float>(), all.data_ptr<float>(), (int)src.numel(), cursor.data_ptr<int>(),
+                                    ia_stream()));
+}
+
 // RunningNorm: (optionally) merge x's moments into mean / var / count in place, and return
 // the normalised x (or None with want_y = false)
 py::object running_norm(torch::Tensor x, torch::Tensor mean, torch::Tensor var, torch::Tensor count, double eps,
@@ -564,6 +603,8 @@ void register_kernels(py::module& m) {
   m.def("running_norm", &running_norm, py::arg("x"), py::arg("mean"), py::arg("var"), py::arg("count"), py::arg("eps"),
         py::arg("update"), py::arg("want_y"), py::arg("ema_inv_lr") = py::none(), py::arg("ema_num_batches") = py::none(),
         py::arg("ema_decay") = 0.0);
+  m.def("gather_rows_cursor", &gather_rows_cursor, "rows perm[*cursor * n ..] of every source into dst (graph epochs)");
+  m.def("append_at_cursor", &append_at_cursor, "all[*cursor] = src; ++*cursor");
   m.def("gather_rows", &gather_rows, py::arg("srcs"), py::arg("b"), py::arg("e") = py::none(), py::arg("n_envs") = 1,
         py::arg("dst") = py::none());
   m.def("soft_value_iteration", &soft_value_iteration, py::arg("T"), py::arg("R"), py::arg("H"), py::arg("gamma"));

@@ -44,7 +44,63 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a, const in
   }
 }
 
+// Cursor-driven form for HIP-graph epochs (the BC epoch graph, algorithms/bc.py): row r of the
+// output is source row perm[*cursor * n + r] (int32 permutation, one entry per source row), so
+// a captured sequence of minibatch steps walks an epoch's order without host arguments.
+__global__ __launch_bounds__(256) void gather_rows_cursor_kernel(GatherArgs a, const int* __restrict__ perm,
+                                                                 const int* __restrict__ cursor, int n) {
+  const GatherField& f = a.f[blockIdx.y];
+  const int64_t rb = f.row_bytes;
+  const char* __restrict__ src = static_cast<const char*>(f.src);
+  char* __restrict__ dst = static_cast<char*>(f.dst);
+  const int* __restrict__ b = perm + (int64_t)(*cursor) * n;
+  const int vec = ((rb & 15) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) ? 16
+                  : ((rb & 3) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 3) == 0) ? 4 : 1;
+  const int64_t units = rb / vec;
+  const int64_t total = (int64_t)n * units;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / units, u = i - r * units;
+    const int64_t srow = b[r];
+    const bool ok = srow >= 0 && srow < f.rows;
+    if (vec == 16) {
+      reinterpret_cast<uint4*>(dst + r * rb)[u] = ok ? reinterpret_cast<const uint4*>(src + srow * rb)[u] : make_uint4(0, 0, 0, 0);
+    } else if (vec == 4) {
+      reinterpret_cast<uint32_t*>(dst + r * rb)[u] = ok ? reinterpret_cast<const uint32_t*>(src + srow * rb)[u] : 0u;
+    } else {
+      dst[r * rb + u] = ok ? src[srow * rb + u] : (char)0;
+    }
+  }
+}
+
+// all[*cursor][0 .. n) = src[0 .. n), then ++*cursor (one block): per-step metrics of a graphed
+// epoch land in their own row, the cursor names the next minibatch
+__global__ void append_at_cursor_kernel(const float* __restrict__ src, float* __restrict__ all, int n, int* cursor) {
+  const int cur = *cursor;
+  __syncthreads();  // every thread has read the cursor before thread 0 moves it
+  for (int i = threadIdx.x; i < n; i += blockDim.x) all[(size_t)cur * n + i] = src[i];
+  if (threadIdx.x == 0) *cursor = cur + 1;
+}
+
 }  // namespace
+
+hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* cursor, int n, hipStream_t s) {
+  if (n <= 0 || a.k <= 0) return hipSuccess;
+  if (a.k > kGatherMax) return hipErrorInvalidValue;
+  int64_t most = 0;
+  for (int i = 0; i < a.k; ++i) {
+    const int64_t units = a.f[i].row_bytes / ((a.f[i].row_bytes & 15) == 0 ? 16 : 1);
+    most = units * n > most ? units * n : most;
+  }
+  int64_t bx = (most + 255) / 256;
+  bx = bx < 1 ? 1 : (bx > 1024 ? 1024 : bx);
+  hipLaunchKernelGGL(gather_rows_cursor_kernel, dim3((unsigned)bx, a.k), dim3(256), 0, s, a, perm, cursor, n);
+  return hipGetLastError();
+}
+
+hipError_t append_at_cursor(const float* src, float* all, int n, int* cursor, hipStream_t s) {
+  hipLaunchKernelGGL(append_at_cursor_kernel, dim3(1), dim3(64), 0, s, src, all, n, cursor);
+  return hipGetLastError();
+}
 
 hipError_t gather_rows(const GatherArgs& a, const int64_t* b, const int64_t* e, int n_envs, int n, hipStream_t s) {
   if (n <= 0 || a.k <= 0) return hipSuccess;

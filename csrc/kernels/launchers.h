@@ -340,6 +340,10 @@ struct GatherArgs {
   int k;
 };
 hipError_t gather_rows(const GatherArgs& a, const int64_t* b, const int64_t* e, int n_envs, int n, hipStream_t s);
+// rows perm[*cursor * n .. + n) (int32 ids) of every source (graph-captured epochs)
+hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* cursor, int n, hipStream_t s);
+// all[*cursor * n ..] = src[0 .. n), ++*cursor
+hipError_t append_at_cursor(const float* src, float* all, int n, int* cursor, hipStream_t s);
 
 // ---- tabular.hip: MCE-IRL soft value iteration / occupancy (fp64, one workgroup, LDS-resident
 // vectors: S * (A + 1) doubles <= 150 KB) and KDE log-density scoring (fp64, d <= kKdeMaxDim)

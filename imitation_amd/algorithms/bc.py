@@ -291,6 +291,24 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
             g = self._graph_step = graphs.GraphedTrainStep(step, self.optimizer, release)
         return g
 
+    def _epoch_runner(self, graphed, on_batch_end) -> Optional["_DeviceEpochRunner"]:
+        """The graph-epoch runner when the demonstrations are a device aggregate (DAgger's
+        device collector, ``engine/dagger.py``) and every minibatch is the fused NatureCNN
+        step: nothing per minibatch needs the host. Disabled with ``IMITATION_AMD_BC_EPOCH_GRAPH=0``."""
+        import os
+
+        loader = self._demo_data_loader
+        if (graphed is None or on_batch_end is not None or not hasattr(loader, "next_epoch_perm")
+                or self.minibatch_size != self.batch_size or os.environ.get("IMITATION_AMD_BC_EPOCH_GRAPH", "1") == "0"):
+            return None
+        r = getattr(self, "_epoch_run", None)
+        if r is None or r.loader is not loader or r.graphed is not graphed:
+            r = _DeviceEpochRunner(self, loader, graphed)
+            if not r.ok:
+                return None
+            self._epoch_run = r
+        return r
+
     def _zero_grad(self):
         self.optimizer.zero_grad(set_to_none=self._grad_bucket is None)
         if self._grad_bucket is not None:
@@ -334,6 +352,12 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
 
         self._zero_grad()
         graphed = self._graphed_step()
+        runner = self._epoch_runner(graphed, on_batch_end)
+        if runner is not None:
+            # device-resident demonstrations: whole runs of minibatches per HIP-graph replay
+            runner.train(n_epochs, n_minibatches, _on_epoch_end, log_interval, compute_rollout_stats)
+            pdist.check_comm("BC training", blocking=True)
+            return
         num_samples_so_far = 0
         for (batch_num, minibatch_size, num_samples_so_far), batch in batches_with_stats:
             obs, acts = self._prepare_batch(batch)
@@ -360,6 +384,110 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         # the per-epoch checks are non-blocking (they read the previous epoch's error word):
         # one blocking check makes a timed-out all-reduce in the last epoch raise here
         pdist.check_comm("BC training", blocking=True)
+
+
+class _DeviceEpochRunner:
+    """BC epochs over a device demonstration aggregate as HIP-graph replays of ``K`` minibatch
+    steps each: per step ``gather_rows_cursor`` (rows ``perm[cursor * B ..]`` into the
+    aggregate's persistent batch buffers), the fused NatureCNN step (``ops/bc_cnn.py``), the
+    optimizer step and ``append_at_cursor`` (the step's metrics into their row, cursor + 1).
+    Per epoch the host only draws the permutation (one launch) and replays; the reference loop's
+    per-batch observable effects are kept: rollout statistics + logging at every
+    ``log_interval``-th batch (the replays stop at those batches), epoch-end callbacks, the
+    ``n_batches`` cut-off (reference ``bc.py:443-510``). Same batches, kernels and order as the
+    per-minibatch loop, so the result is bitwise the eager-graph path's."""
+
+    K = 16  # minibatch steps per graph replay
+
+    def __init__(self, trainer: "_BCBase", loader, graphed):
+        self.trainer, self.loader, self.graphed = trainer, loader, graphed
+        self.B = trainer.batch_size
+        self.agg = loader.agg
+        self.ok = len(self.agg) >= self.B and self._fused() is not None
+        self._key = None
+
+    def _fused(self):
+        t = self.trainer
+        obs = self.agg.batch_buffers(self.B)[0]
+        f = getattr(self, "_f", None)
+        if f is None:
+            f = bc_cnn.FusedCnnBCStep.maybe(t.policy, t.optimizer, obs, t.loss_calculator.ent_weight,
+                                            t.loss_calculator.l2_weight)
+            self._f = f
+        return f
+
+    def _one_step(self):
+        C = self._f.C
+        bufs = self.agg.batch_buffers(self.B)
+        C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs)
+        self._f(bufs[0], bufs[1])
+        self.trainer.optimizer.step()
+        C.append_at_cursor(self._f.metrics, self.all, self.cursor)
+
+    def _prepare(self, n: int) -> None:
+        """(Re)allocate the static perm / metric buffers and capture the step graphs when the
+        aggregate's storage or the epoch size outgrew them (capacity doubling: O(log) captures)."""
+        dev = self.agg.device
+        cap = max(n, getattr(self, "_cap", 0))
+        key = (self.agg.obs.data_ptr(), self.agg.acts.data_ptr())
+        if self._key == key and n <= getattr(self, "_cap", 0):
+            return
+        if n > getattr(self, "_cap", 0):
+            cap = max(n, 2 * getattr(self, "_cap", 0))
+            self.perm = th.zeros(cap, dtype=th.int32, device=dev)
+            self.all = th.zeros(cap // self.B + 1, 8, device=dev)
+            self.cursor = th.zeros(1, dtype=th.int32, device=dev)
+            self._cap = cap
+        self._key = key
+        self.graphs = {}
+        side = th.cuda.Stream()
+        side.wait_stream(th.cuda.current_stream())
+        for k in (1, self.K):
+            g = th.cuda.CUDAGraph()
+            with th.cuda.graph(g, stream=side):
+                for _ in range(k):
+                    self._one_step()
+            self.graphs[k] = g
+        th.cuda.current_stream().wait_stream(side)
+
+    def _run(self, steps: int) -> None:
+        for _ in range(steps // self.K):
+            self.graphs[self.K].replay()
+        for _ in range(steps % self.K):
+            self.graphs[1].replay()
+
+    def train(self, n_epochs, n_batches, on_epoch_end, log_interval: int, compute_rollout_stats) -> None:
+        t = self.trainer
+        B = self.B
+        batch_num = 0  # minibatches stepped in this call (the reference loop's batch_num)
+        epoch = 0
+        while (n_epochs is None or epoch < n_epochs) and (n_batches is None or batch_num < n_batches):
+            n = len(self.agg)
+            nb = n // B
+            if nb == 0:
+                raise AssertionError(f"Data loader returned no data during epoch {epoch} -- did it reset correctly?")
+            perm = self.loader.next_epoch_perm()
+            self._prepare(n)
+            self.perm[:n].copy_(perm)
+            self.cursor.zero_()
+            steps = nb if n_batches is None else min(nb, n_batches - batch_num)
+            done = 0
+            while done < steps:
+                nxt = -(-(batch_num + done) // log_interval) * log_interval  # next logged batch
+                j = nxt - batch_num  # its index in this epoch
+                if j >= steps:
+                    self._run(steps - done)
+                    break
+                self._run(j + 1 - done)
+                m = BCTrainingMetrics(**bc_cnn.metrics_fields(self.all[j]))
+                t._bc_logger.log_batch(nxt, B, (nxt + 1) * B, m, compute_rollout_stats(t.policy, t.rng))
+                done = j + 1
+            batch_num += steps
+            # the reference's batch iterator reaches an epoch's end callback only when it is
+            # asked for a batch after the epoch's last one
+            if steps == nb and (n_batches is None or batch_num < n_batches):
+                on_epoch_end(epoch)
+            epoch += 1
 
 
 class BC(_BCBase):

@@ -252,12 +252,17 @@ class DeviceTransitionsLoader:
     def __len__(self) -> int:
         return len(self.agg) // self.batch_size
 
-    def __iter__(self):
+    def next_epoch_perm(self) -> th.Tensor:
+        """The int32 row order of the next epoch (advances the epoch counter exactly as iterating
+        does): the BC epoch graph walks it with a device cursor."""
         from imitation_amd.ops import rl as rl_ops
 
-        n = len(self.agg)
         self._epoch += 1
-        perm = rl_ops.random_permutations(1, n, self._seed * 1000003 + self._epoch, self.agg.device)[0].long()
+        return rl_ops.random_permutations(1, len(self.agg), self._seed * 1000003 + self._epoch, self.agg.device)[0]
+
+    def __iter__(self):
+        n = len(self.agg)
+        perm = self.next_epoch_perm().long()
         obs, acts = self.agg.obs, self.agg.acts
         bufs = self.agg.batch_buffers(self.batch_size)
         for s in range(0, n - n % self.batch_size, self.batch_size):

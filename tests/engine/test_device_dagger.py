@@ -180,3 +180,57 @@ def test_device_rollout_stats_match_host_keys(tmp_path):
     tr.train(400, rollout_round_min_episodes=1, rollout_round_min_timesteps=400,
              bc_train_kwargs=dict(n_epochs=1, progress_bar=False, log_interval=10**9))
     assert tr.round_num >= 1
+
+
+@gpu
+@pytest.mark.parametrize("n_epochs,n_batches,log_interval", [(2, None, 3), (None, 11, 4), (None, 7, 500)])
+def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batches, log_interval):
+    """BC over a device demonstration aggregate (DAgger's device collector) with whole runs of
+    minibatches per HIP-graph replay (algorithms/bc.py ``_DeviceEpochRunner``): the same batches,
+    kernels and order as the per-minibatch graphed loop, so the parameters, Adam state and every
+    logged metric are bitwise equal; the epoch-end callbacks and the n_batches cut-off match."""
+    from imitation_amd.algorithms import bc
+    from imitation_amd.engine.dagger import DeviceDemoAggregate, DeviceTransitionsLoader
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+    from imitation_amd.util import logger as ilog
+    from imitation_amd.util.util import make_vec_env
+
+    venv = make_vec_env("PongNoFrameskip-v4", rng=np.random.default_rng(0), n_envs=1)
+    g = th.Generator(device="cuda").manual_seed(5)
+    n_rows = 32 * 9 + 5
+    obs = th.randint(0, 256, (n_rows, 84, 84, 4), generator=g, device="cuda", dtype=th.int64).to(th.uint8)
+    acts = th.randint(0, int(venv.action_space.n), (n_rows,), generator=g, device="cuda")
+    runs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IMITATION_AMD_BC_EPOCH_GRAPH", mode)
+        th.manual_seed(11)
+        pol = ActorCriticCnnPolicy(venv.observation_space, venv.action_space, lambda _: th.finfo(th.float32).max).cuda()
+        agg = DeviceDemoAggregate("cuda")
+        agg.append(obs, acts, gather=False)
+        recorded = []
+        log = ilog.configure(format_strs=[])
+        orig_dump = log.dump
+
+        def dump(step=0, _log=log, _orig=orig_dump, _rec=recorded):
+            _rec.append((step, {k: v for k, v in _log.name_to_value.items() if k.startswith("bc/")}))
+            _orig(step)
+
+        log.dump = dump
+        trainer = bc.BC(observation_space=venv.observation_space, action_space=venv.action_space,
+                        rng=np.random.default_rng(0), policy=pol, batch_size=32, device="cuda", custom_logger=log)
+        trainer.set_demonstrations(DeviceTransitionsLoader(agg, 32, seed=3))
+        ends = []
+        trainer.train(n_epochs=n_epochs, n_batches=n_batches, on_epoch_end=lambda: ends.append(1),
+                      log_interval=log_interval, progress_bar=False)
+        th.cuda.synchronize()
+        used = getattr(trainer, "_epoch_run", None) is not None
+        assert used == (mode == "1")
+        f = trainer.optimizer._flat[0]
+        runs.append(([p.detach().clone() for p in pol.parameters()], f["m"].clone(), f["v"].clone(), recorded, len(ends)))
+    (p0, m0, v0, r0, e0), (p1, m1, v1, r1, e1) = runs
+    assert all(th.equal(a, b) for a, b in zip(p0, p1))
+    assert th.equal(m0, m1) and th.equal(v0, v1)
+    assert e0 == e1
+    assert [s for s, _ in r0] == [s for s, _ in r1] and len(r0) > 0
+    for (_, a), (_, b) in zip(r0, r1):
+        assert a == b
