@@ -178,7 +178,7 @@ constexpr int kMaxRcGroups = 64;  // cooperating workgroups per minibatch (one p
 struct PPORcGeo {
   int din[2][kWaveMaxLayers], dout[2][kWaveMaxLayers];
   int w_off[2][kWaveMaxLayers], ldw[2][kWaveMaxLayers], b_off[2][kWaveMaxLayers];
-  int h_off[2][kWaveMaxLayers], ldh[2][kWaveMaxLayers];
+  int h_off[2][kWaveMaxLayers], ldh[2][kWaveMaxLayers];  // ldh / ldz: floats per image column
   int z_off[2][kWaveMaxLayers], ldz[2][kWaveMaxLayers], db_off[2][kWaveMaxLayers];
   int ls_off, lsp_off, nm_off, red_off, param_lds;
   int zero_off;  // 64 floats of zeros (never written): operand of the padding dW items
@@ -190,6 +190,7 @@ struct PPORcGeo {
   int dp;                  // padded obs row stride of xraw
   int kt;                  // 16-wide tiles per hidden layer (2: width <= 32, 4: width <= 64)
   int cw;                  // rows per chunk (one fwd/bwd pass of a workgroup)
+  int ksteps;              // 32-row K-steps of a dW tile (split-bf16 images padded to >= 32 rows)
   int nch;                 // chunks per workgroup per minibatch
   int G;                   // cooperating workgroups per minibatch (minibatch = G * nch * cw rows)
   int nw;                  // waves per workgroup (8: <= 32-wide nets, 4: 64-wide nets at 1 wave / SIMD)

@@ -144,7 +144,7 @@ enum RcInst : int {
   RC_WALKER64R_32,
   RC_CARTPOLE32_64,
   RC_64_D16,          // both nets per workgroup, 32-row chunks: any 3-layer [64, 64] net, obs dim <= 16
-  RC_64_D32,          // the same, obs dim <= 32, Gaussian head
+  RC_64_D32,          // the same, obs dim <= 32, ReLU + Gaussian head
 };
 
 static int rc_instance(const PPOArgs& a, int kt, int cw, bool ns) {
@@ -169,8 +169,8 @@ static int rc_instance(const PPOArgs& a, int kt, int cw, bool ns) {
   if (uniform && hw == 64 && s0 == 5 && a.hidden_act == 1 && kt == 4 && cw == 32 && gauss) return RC_WALKER64R_32;
   if (uniform && hw == 32 && s0 == 1 && a.hidden_act == 2 && kt == 2 && cw == 64 && !gauss) return RC_CARTPOLE32_64;
   if (uniform && hw == 64 && kt == 4 && cw == 32 && act_ok && a.D <= 16) return RC_64_D16;
-  // (Gaussian heads only: the categorical build of this size needs scratch)
-  if (uniform && hw == 64 && kt == 4 && cw == 32 && act_ok && a.D <= 32 && gauss) return RC_64_D32;
+  // (ReLU + Gaussian head only: the Tanh and categorical builds of this size need scratch)
+  if (uniform && hw == 64 && kt == 4 && cw == 32 && a.hidden_act == 1 && a.D <= 32 && gauss) return RC_64_D32;
   return RC_GENERIC;
 }
 
@@ -283,9 +283,13 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.ls_off = take(16);
   g.zero_off = take(64);
   g.param_lds = off;
-  // activation images, K-major: [column (16-padded)][cw rows + 4] (the +4 keeps the
-  // 16 lanes of one b128 read on distinct banks); layer-0 input shared by both nets
-  const int ldr = cw + 4;
+  // activation / dZ images for the dW MFMAs, K-major split-bf16 (ppo_rc_kernel.h img_store):
+  // per 16-padded column cs floats = hi rows [0, rows_pad) + lo rows at bf16 offset cs (the +12
+  // keeps the 16 columns of one ds_read_b128 group on distinct banks); layer-0 input shared by
+  // both nets
+  const int rows_pad = cw > 32 ? cw : 32;
+  const int ldr = rows_pad + 12;
+  g.ksteps = rows_pad / 32;
   const int h0 = take(((a.D + 15) & ~15) * ldr);
   const int abase = off;
   int aend = off;
@@ -397,7 +401,12 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   // > 80 KiB of LDS keeps the cooperating workgroups one per CU (the measured condition of
   // the sc1 hand-off); all G <= kMaxRcGroups (64) of them are co-resident (256 CUs)
   // (net split: the two workgroups must not share a CU's matrix cores either)
-  const size_t lds_launch = (g.G > 1 || g.ns) && lds < 96 * 1024 ? 96 * 1024 : lds;
+  size_t lds_launch = (g.G > 1 || g.ns) && lds < 96 * 1024 ? 96 * 1024 : lds;
+  {  // IMITATION_AMD_PPO_LDS_EXCL=1: claim the whole 160 KiB of LDS, so no workgroup of a concurrent
+     // stream (the discriminator) can share a cooperating workgroup's CU and SIMDs
+    const char* ev = getenv("IMITATION_AMD_PPO_LDS_EXCL");
+    if (ev && ev[0] == '1' && (g.G > 1 || g.ns)) lds_launch = 160 * 1024;
+  }
   const int nblk = g.ns ? 2 * g.G : g.G;
   {  // cooperating workgroups on as few XCDs as possible (IMITATION_AMD_PPO_XCD=0 turns it off;
      // the "xcd" geometry field is the block stride). GAIL emulated W = 2 / 4 / 8: 3.14 / 3.28 / 3.64 -> 2.99 / 2.96 / 3.36 ms per update,
@@ -459,8 +468,7 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
       else IA_RC(4, 12, 2, -4, 3, 2, 64, 32, 1);
       break;
     case RC_64_D32:
-      if (hact == 1) IA_RC(4, 14, 2, -8, 3, 1, 64, 32, 0);
-      else IA_RC(4, 14, 2, -8, 3, 2, 64, 32, 0);
+      IA_RC(4, 14, 2, -8, 3, 1, 64, 32, 0);
       break;
     default: break;
   }

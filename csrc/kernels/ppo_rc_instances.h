@@ -41,7 +41,6 @@
 
 #define IA_RC_GROUP_F(X) \
   X(4,14,2,5,3,1,64,32,0,4) \
-  X(4,14,2,-8,3,1,64,32,0,4) \
-  X(4,14,2,-8,3,2,64,32,0,4)
+  X(4,14,2,-8,3,1,64,32,0,4)
 
 #define IA_RC_INSTANCES(X) IA_RC_GROUP_A(X) IA_RC_GROUP_B(X) IA_RC_GROUP_C(X) IA_RC_GROUP_D(X) IA_RC_GROUP_E(X) IA_RC_GROUP_F(X)

@@ -56,6 +56,10 @@ namespace rc {
 
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) bf16 lbf;
+typedef __attribute__((address_space(3))) bf16x8 lbf8;
 typedef __attribute__((address_space(3))) float lf;
 typedef __attribute__((address_space(3))) f4 lf4;
 
@@ -248,37 +252,55 @@ __device__ __forceinline__ void reduce_slots(const float* slab, float* red, size
   }
 }
 
-// dW tiles of this wave's N weight items over one chunk (K = cw rows): acc[i] = dZ^T H for
-// item i. Operand columns are K-major (see header), so each lane reads 4 MFMA steps per
-// 16-byte LDS load; the N accumulation chains are interleaved step by step.
-template <int N, int CWT>
-__device__ __forceinline__ void dw_tiles(const lf* L, const int* izo, const int* iho, int cw, f4* acc) {
-  const int ng = (CWT > 0 ? CWT : cw) >> 4;
-  // acc holds the running sums on entry (accumulated into). Items in groups of 4: four independent accumulation chains keep the MFMA pipe busy,
-  // and only the group's operands (8 x f4) are live instead of all N items'
+// dW tiles of this wave's N weight items over one chunk (K = rows): acc[i] += dZ^T H for item i
+// on v_mfma_f32_16x16x32_bf16 with the split-bf16 ("bf16x3") product: every image value is
+// stored as hi = bf16(v) and lo = bf16(v - hi), and dZ^T H = hi.hi + hi.lo + lo.hi (the lo.lo term
+// is ~2^-16 of the product: near-fp32 accuracy at 3 bf16 MFMAs per 32 rows instead of eight
+// 16x16x4 fp32 ones). Images are K-major (rows contiguous): column c of an image has its hi rows
+// at bf16 index 2 c cs + r and its lo rows at 2 c cs + cs + r (cs floats per column, chosen so
+// the 16 columns a ds_read_b128 group touches hit distinct banks). Lane (r16, kk) reads rows
+// 8 kk .. 8 kk + 7 (+ 32 per K-step) of column r16 of the item's dZ (A, M = out) and H (B,
+// N = in) tiles; the accumulator layout is the fp32 kernel's (C[out 4 kk + j][in r16]), so the
+// exchange and Adam code is unchanged. izo / iho: bf16 offsets of the lane's first element.
+__device__ __forceinline__ f4 mfma_bf16(bf16x8 a, bf16x8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+
+template <int N>
+__device__ __forceinline__ void dw_tiles(const lf* L, const int* izo, const int* iho, int cs, int ksteps, f4* acc) {
+  const lbf* Lb = (const lbf*)L;
+  // items in groups of GS: independent accumulation chains keep the MFMA pipe busy while only
+  // the group's operands (4 x bf16x8 per item) are live (2 per group for the largest slot counts)
+  constexpr int GS = N >= 12 ? 2 : 4;
 #pragma unroll
-  for (int i0 = 0; i0 < N; i0 += 4) {
-    constexpr int GS = 4;
-#pragma unroll
-    for (int gi = 0; gi < (CWT > 0 ? CWT / 16 : 4); ++gi) {
-      if (CWT == 0 && gi >= ng) break;
-      f4 z[GS], h[GS];
+  for (int i0 = 0; i0 < N; i0 += GS) {
+    for (int ks = 0; ks < ksteps; ++ks) {
+      bf16x8 zh[GS], zl[GS], hh[GS], hl[GS];
 #pragma unroll
       for (int i = 0; i < GS; ++i) {
         if (i0 + i >= N) continue;
-        z[i] = *(const lf4*)(L + izo[i0 + i] + 4 * gi);
-        h[i] = *(const lf4*)(L + iho[i0 + i] + 4 * gi);
+        const lbf* zp = Lb + izo[i0 + i] + 32 * ks;
+        const lbf* hp = Lb + iho[i0 + i] + 32 * ks;
+        zh[i] = *(const lbf8*)zp;
+        zl[i] = *(const lbf8*)(zp + cs);
+        hh[i] = *(const lbf8*)hp;
+        hl[i] = *(const lbf8*)(hp + cs);
       }
 #pragma unroll
       for (int i = 0; i < GS; ++i) {
         if (i0 + i >= N) continue;
-        acc[i0 + i] = mfma(z[i].x, h[i].x, acc[i0 + i]);
-        acc[i0 + i] = mfma(z[i].y, h[i].y, acc[i0 + i]);
-        acc[i0 + i] = mfma(z[i].z, h[i].z, acc[i0 + i]);
-        acc[i0 + i] = mfma(z[i].w, h[i].w, acc[i0 + i]);
+        acc[i0 + i] = mfma_bf16(zh[i], hh[i], acc[i0 + i]);
+        acc[i0 + i] = mfma_bf16(zh[i], hl[i], acc[i0 + i]);
+        acc[i0 + i] = mfma_bf16(zl[i], hh[i], acc[i0 + i]);
       }
     }
   }
+}
+
+// one value into a split-bf16 K-major image: hi at [col][row], lo one half-column (cs bf16) on
+__device__ __forceinline__ void img_store(lf* L, int off, int cs, int col, int row, float v) {
+  lbf* p = (lbf*)(L + off) + (2 * col * cs + row);
+  const bf16 h = (bf16)v;
+  p[0] = h;
+  p[cs] = (bf16)(v - (float)h);
 }
 
 // Shape specialisation: S0T (16-wide input k-steps / 4), NLT (layers per net), ACTT (hidden
@@ -436,9 +458,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // the LDS offsets of a slot's dZ / H columns are a wave-uniform base (the descriptor) plus
   // ONE lane term shared by every slot (all K-major images have the row stride cw + 4)
   const int nwi = nwq > w ? min(KW, (nwq - w + kWaves - 1) / kWaves) : 0;
-  const int rq = cw / 4;  // K-major image: row r at (r & 3) * rq + (r >> 2)
-  const int ldr = rfl(g.ldz[0][0]);
-  const int lterm = r16 * ldr + kk * rq;
+  const int cs = rfl(g.ldz[0][0]);  // floats per column of the split-bf16 K-major images
+  const int ksteps = rfl(g.ksteps);  // 32-row K-steps of a dW tile
+  const int lterm = r16 * 2 * cs + 8 * kk;  // bf16 offset of this lane's first dW operand
   // bias / log_std slots: kind (1 bias, 2 log_std, -1 empty), partial source, element mask
   int bkind[KB], b_off[KB], b_addr[KB];
   float b_okf[KB];  // 1 for lanes holding a real bias / log_std element
@@ -465,7 +487,6 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   }
   Rows<S0M> cur;
   const int row = 16 * gw + r16;
-  const int rp = (row & 3) * rq + (row >> 2);  // this lane's row in the K-major images
   // chunk unit u = k * nch + ch -> prep slot k * CH + grp * nch + ch
   auto slot_of = [&](int u) -> size_t { return (size_t)(u / nch) * CH + (size_t)grp * nch + (u % nch); };
   if (rows_wave && K > 0) load_rows(g, slot_of(0), row, kk, s0, cur);
@@ -528,7 +549,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
 #pragma unroll
           for (int s = 0; s < S0M; ++s)
-            if (s < s0) L[h0 + (4 * s + kk) * ld0 + rp] = xb[s];
+            if (s < s0) img_store(L, h0, ld0, 4 * s + kk, row, xb[s]);
         }
         unsigned long long c1 = a.prof ? clock64() : 0;
         // ---------------- forward (registers)
@@ -627,11 +648,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
                 hreg[l][t] = v;
                 // input image of layer l + 1 (for its dW)
                 const LG yn = lg(g, q, l + 1);
-                lf* hp = L + yn.h + o0 * yn.ldh + rp;
-                hp[0] = v.x;
-                hp[yn.ldh] = v.y;
-                hp[2 * yn.ldh] = v.z;
-                hp[3 * yn.ldh] = v.w;
+                img_store(L, yn.h, yn.ldh, o0, row, v.x);
+                img_store(L, yn.h, yn.ldh, o0 + 1, row, v.y);
+                img_store(L, yn.h, yn.ldh, o0 + 2, row, v.z);
+                img_store(L, yn.h, yn.ldh, o0 + 3, row, v.w);
               }
             } else if (t == 0) {
               head = v;
@@ -765,11 +785,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) {
             if (u2 >= tout) continue;
-            lf* zp = L + y.z + (16 * u2 + 4 * kk) * y.ldz + rp;
-            zp[0] = dzc[u2].x;
-            zp[y.ldz] = dzc[u2].y;
-            zp[2 * y.ldz] = dzc[u2].z;
-            zp[3 * y.ldz] = dzc[u2].w;
+            const int zc = 16 * u2 + 4 * kk;
+            img_store(L, y.z, y.ldz, zc, row, dzc[u2].x);
+            img_store(L, y.z, y.ldz, zc + 1, row, dzc[u2].y);
+            img_store(L, y.z, y.ldz, zc + 2, row, dzc[u2].z);
+            img_store(L, y.z, y.ldz, zc + 3, row, dzc[u2].w);
             const float s0v = sum16(dzc[u2].x), s1v = sum16(dzc[u2].y), s2v = sum16(dzc[u2].z), s3v = sum16(dzc[u2].w);
             if (r16 == 0) {
               const f4 sv = {s0v, s1v, s2v, s3v};
@@ -848,19 +868,19 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         int izo[KW], iho[KW];
 #pragma unroll
         for (int it = 0; it < KW; ++it) {
-          izo[it] = iho[it] = g.zero_off;
+          izo[it] = iho[it] = 2 * g.zero_off;  // (bf16 units: the zero row)
           if (it < nwi) {
             const int desc = rfl(g.items[wb + w + it * kWaves]);
             const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-            izo[it] = rfl(g.z_off[iq][il]) + 16 * ta * ldr + lterm;
-            iho[it] = rfl(g.h_off[iq][il]) + 16 * tb * ldr + lterm;
+            izo[it] = 2 * rfl(g.z_off[iq][il]) + 16 * ta * 2 * cs + lterm;
+            iho[it] = 2 * rfl(g.h_off[iq][il]) + 16 * tb * 2 * cs + lterm;
           }
         }
         // the chunk's dZ^T H continues each slot's MFMA chain from its running gradient
         // (padding entries are exactly 0: zeroed images)
         // (empty slots read the zero row: their MFMAs add zeros to gradients nobody reads,
         // so every wave runs the same straight-line body)
-        dw_tiles<KW, CWT>(L, izo, iho, cw, gg);
+        dw_tiles<KW>(L, izo, iho, cs, ksteps, gg);
       }
 #pragma unroll
       for (int ib = 0; ib < KB; ++ib) {

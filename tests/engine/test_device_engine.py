@@ -122,7 +122,7 @@ def _torch_ppo_reference(gen, obs, acts, old_logp, adv, ret, perm, clip, lr, nor
     ("seals/CartPole-v0", 1, 256, 0, "nons", "rc:g4x1x64:kt2"),
     # [64, 64] Tanh, both nets per workgroup: the family build (obs dim <= 16)
     ("seals/Hopper-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], nons=True), "rc:g2x1x32:kt4"),
-    ("seals/HalfCheetah-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], nons=True), "rc:g2x1x32:kt4"),
+    ("seals/HalfCheetah-v1", 1, 64, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g2x1x32:kt4"),
     ("seals/Hopper-v1", 1, 512, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g16x1x32:kt4"),
     ("seals/Walker2d-v1", 1, 128, 0, dict(pi=[64, 64], vf=[64, 64], act="relu", nons=True), "rc:g4x1x32:kt4"),
     # SB3's default MlpPolicy ([64, 64] Tanh; reference scripts/ingredients/rl.py:58-66) and
