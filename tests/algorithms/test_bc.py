@@ -264,3 +264,59 @@ def test_fused_cnn_bc_step_matches_autograd():
         b = p.grad if p.grad is not None else th.zeros_like(p)
         th.testing.assert_close(a, b, rtol=2e-3, atol=2e-5, msg=lambda s: f"{name}: {s}")
     assert float(fused[-2].abs().sum()) == 0.0  # value head: no gradient
+
+
+def test_multibc_column_map_probe():
+    """MultiBC overrides that select columns are recognised (and folded into the device gather);
+    anything else (arithmetic, row-dependent selection) is not."""
+    from imitation_amd.algorithms.bc import _column_map
+
+    assert _column_map(lambda i, o: o[:, 3 * i: 3 * i + 3], 1, 12, th.float32) == ([3, 4, 5], False)
+    assert _column_map(lambda i, a: a[:, i], 2, 4, th.int64) == ([2], True)
+    assert _column_map(lambda i, o: o[:, [5, 1]], 0, 8, th.float32) == ([5, 1], False)
+    assert _column_map(lambda i, o: o[:, :3] * 2.0, 0, 8, th.float32) is None
+    assert _column_map(lambda i, o: o[:, :3] - o[:, 3:6], 0, 8, th.float32) is None
+    assert _column_map(lambda i, o: o.flip(0)[:, :2], 0, 8, th.float32) is None
+    assert _column_map(lambda i, o: (_ for _ in ()).throw(ValueError("no")), 0, 8, th.float32) is None
+
+
+@pytest.mark.gpu
+def test_multibc_device_agent_gather_matches_cat_of_overrides():
+    """The device agent-gather loader (one gather launch per batch) yields exactly the
+    agent-concatenation the reference builds with observation_overide / action_overide + th.cat,
+    for the rows of its permutation; training on it runs as graph replays."""
+    from imitation_amd.algorithms import bc
+    from imitation_amd.data import types
+    from imitation_amd.envs import spaces
+    from imitation_amd.ops import rl as rl_ops
+    from imitation_amd.util import logger
+
+    rng = np.random.default_rng(0)
+    d, n_agents, N, B = 12, 4, 1024, 64
+    obs = rng.standard_normal((N, d * n_agents)).astype(np.float32)
+    acts = np.stack([(obs[:, d * i] > 0).astype(np.int64) for i in range(n_agents)], axis=1)
+    obs_over = lambda i, o: o[:, d * i: d * i + d]  # noqa: E731
+    act_over = lambda i, a: a[:, i]  # noqa: E731
+    demos = types.TransitionsMinimal(obs=obs, acts=acts, infos=np.array([{}] * N))
+    trainer = bc.MultiBC(single_agent_observation_space=spaces.Box(-10, 10, (d,)), single_agent_action_space=spaces.Discrete(2),
+                         observation_overide=obs_over, action_overide=act_over, num_agents=n_agents,
+                         rng=np.random.default_rng(0), demonstrations=demos, batch_size=B, device="cuda",
+                         optimizer_kwargs=dict(lr=1e-3), custom_logger=logger.configure(format_strs=[]))
+    p0 = [p.detach().clone() for p in trainer.policy.parameters()]
+    trainer.train(n_batches=20, progress_bar=False, log_interval=10**9)
+    th.cuda.synchronize()
+    loader = trainer._demo_data_loader
+    assert isinstance(loader, bc._AgentGatherLoader)
+    assert trainer._graph_step.n_replays >= 18
+    assert any(not th.equal(a, b) for a, b in zip(p0, trainer.policy.parameters()))
+    # one more epoch by hand: batch b holds the overrides' concatenation of rows perm[b*B:(b+1)*B]
+    ep = loader._epoch + 1
+    perm = rl_ops.random_permutations(1, N, loader._seed * 1000003 + ep, "cuda")[0].long().cpu()
+    it = iter(loader)
+    for b in range(3):
+        got = next(it)
+        rows = perm[b * B:(b + 1) * B]
+        o_all, a_all = th.as_tensor(obs)[rows], th.as_tensor(acts)[rows]
+        want_o = th.cat([obs_over(i, o_all) for i in range(n_agents)])
+        want_a = th.cat([act_over(i, a_all) for i in range(n_agents)])
+        assert th.equal(got["obs"].cpu(), want_o) and th.equal(got["acts"].cpu(), want_a)
