@@ -185,8 +185,14 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         ok, why = self._fused_disc_check()
         self._fused_disc = ok
         self._fused_disc_why = why
-        self._overlap_disc = False  # log pi needs the post-PPO policy: the updates follow PPO
-        self._side_stream = None
+        # log pi needs the post-PPO policy: the updates follow PPO on the main stream, but the round
+        # is pipelined like GAIL's (_overlapped_round: PPO stats copied async, the updates and the
+        # next rollout enqueued before the host reads anything); IMITATION_AMD_DISC_OVERLAP=0: serial
+        import os
+
+        self._overlap_disc = os.environ.get("IMITATION_AMD_DISC_OVERLAP", "1") != "0"
+        self._disc_on_main = True
+        self._side_stream = th.cuda.Stream(device=self._dev) if self._overlap_disc else None  # staging copies
         self._pol_defer_buf = None
         if not ok:
             return

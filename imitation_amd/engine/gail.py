@@ -1016,7 +1016,10 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         disc stats are in ``_disc_stats_host`` when this returns."""
         algo: PPO = self.gen_algo
         main = th.cuda.current_stream(self._dev)
-        side = self._side_stream
+        # AIRL (_disc_on_main): log pi needs the post-PPO policy, so the updates queue behind PPO
+        # on the main stream -- the round is still pipelined: nothing waits on the host between
+        # PPO, the updates and the next rollout
+        side = main if getattr(self, "_disc_on_main", False) else self._side_stream
         pol_merge = self.pol_norm is not None and self.pol_norm.training
         defer = pol_merge and self._pol_defer_buf is not None
         if defer:

@@ -621,3 +621,27 @@ def test_ppo_kernel_timeout_raises(batch, path):
     tr._ppo_update()
     th.cuda.synchronize()
     tr.check_errors(blocking=True)
+
+
+@gpu
+def test_airl_pipelined_rounds_are_bitwise_the_serial_order(monkeypatch):
+    """AIRL rounds pipelined on the main stream (engine/gail.py ``_overlapped_round`` with
+    ``_disc_on_main``: PPO statistics copied asynchronously, the discriminator updates and the next
+    rollout enqueued before the host reads anything) give bit-identical parameters, Adam moments
+    and normalisers to the serial loop (IMITATION_AMD_DISC_OVERLAP=0)."""
+    runs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IMITATION_AMD_DISC_OVERLAP", mode)
+        tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=3)
+        assert tr._fused_disc, tr._fused_disc_why
+        assert tr._overlap_disc == (mode == "1")
+        tr.n_disc_updates_per_round = 3
+        tr.train(3 * tr.gen_train_timesteps)
+        th.cuda.synchronize()
+        vals = [p.detach().cpu().clone() for p in list(gen.policy.parameters()) + list(rn.parameters())]
+        vals += [t.detach().cpu().clone() for t in (tr._r_m, tr._r_v, tr.exp_avg, tr.exp_avg_sq)]
+        vals += [n.running_mean.cpu().clone() for n in _airl_state(tr, rn)]
+        runs.append(vals)
+        assert tr._disc_step == 9
+    bad = [i for i, (a, b) in enumerate(zip(*runs)) if not th.equal(a, b)]
+    assert not bad, bad
