@@ -191,6 +191,8 @@ struct PPORcGeo {
   int kt;                  // 16-wide tiles per hidden layer (2: width <= 32, 4: width <= 64)
   int cw;                  // rows per chunk (one fwd/bwd pass of a workgroup)
   int ksteps;              // 32-row K-steps of a dW tile (split-bf16 images padded to >= 32 rows)
+  int bf3;                 // split-bf16 forward / dX weight images (ppo_rc_kernel.h bf3_tile)
+  int wf_off[2][kWaveMaxLayers], wt_off[2][kWaveMaxLayers];  // their offsets (floats; hi then lo)
   int nch;                 // chunks per workgroup per minibatch
   int G;                   // cooperating workgroups per minibatch (minibatch = G * nch * cw rows)
   int nw;                  // waves per workgroup (8: <= 32-wide nets, 4: 64-wide nets at 1 wave / SIMD)

@@ -251,6 +251,11 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   // the generic 64-wide net-split build needs scratch (8 weight slots + 2 vectors at runtime
   // shapes): nets outside the specialised [64, 64] families take the LDS kernel
   if (g.ns && KT == 4 && rc_instance(a, KT, cw, true) == RC_GENERIC) return false;
+  {  // the 32-wide specialised builds run the split-bf16 forward / dX (kernel: BF3)
+    const int inst = rc_instance(a, KT, cw, g.ns != 0);
+    g.bf3 = (inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32 || inst == RC_CHEETAH32_64 || inst == RC_CHEETAH32_32 ||
+             inst == RC_CARTPOLE32_64) ? 1 : 0;
+  }
   int off = 0;
   auto take = [&](int n) {
     const int o = off;
@@ -276,6 +281,10 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
       g.ldw[q][l] = (l == 0 ? ((din + 15) & ~15) : ip) + 4;
       g.w_off[q][l] = take(op * g.ldw[q][l]);
       g.b_off[q][l] = take(op);
+      if (g.bf3) {  // split-bf16 weight images (hi + lo): forward [op][pos(in)], transposed [32][pos(out)]
+        g.wf_off[q][l] = take(op * kBf3Ld);
+        g.wt_off[q][l] = l > 0 ? take(32 * kBf3Ld) : 0;
+      }
     }
     pend = off > pend ? off : pend;
   }

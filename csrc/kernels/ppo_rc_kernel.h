@@ -303,6 +303,51 @@ __device__ __forceinline__ void img_store(lf* L, int off, int cs, int col, int r
   p[cs] = (bf16)(v - (float)h);
 }
 
+// ---- split-bf16 forward / input-gradient path (BF3: <= 32-wide nets, obs dim <= 32)
+// The fp32 16x16x4 chains (8 MFMAs of 32 cycles per 32-wide K) become v_mfma_f32_16x16x32_bf16
+// triples (hi.hi + hi.lo + lo.hi: 3 x 16 cycles, ~2^-16 relative product error) over bf16 hi / lo
+// weight images kept next to the fp32 master (updated by the Adam owners). The B operand of a
+// lane is its own 8 activations (C layout of the previous layer: features 4 kk + j of tiles 0 / 1)
+// in the K order pos(f) below; the weight images store column f at pos(f), so no data moves
+// between lanes. Layer 0's input is lane kk's features 4 s + kk (s < 8) at position 8 kk + s.
+constexpr int kBf3Ld = 40;  // bf16 per weight-image row (32 + 8: the 16 rows of a b128 group on distinct banks)
+__device__ __forceinline__ int bf3_pos_in0(int f) { return 8 * (f & 3) + (f >> 2); }
+__device__ __forceinline__ int bf3_pos_h(int f) { return 8 * ((f >> 2) & 3) + 4 * (f >> 4) + (f & 3); }
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bf16 h = (bf16)v[j];
+    hi[j] = h;
+    lo[j] = (bf16)(v[j] - (float)h);
+  }
+}
+
+// acc (C[16 x 16]) = A_tile . B with A rows at `a` (hi image; lo image `lo_off` bf16 further)
+__device__ __forceinline__ f4 bf3_tile(const lbf* a, int lo_off, bf16x8 bh, bf16x8 bl) {
+  const bf16x8 ah = *(const lbf8*)a;
+  const bf16x8 al = *(const lbf8*)(a + lo_off);
+  f4 acc = mfma_bf16(ah, bh, f4{0.f, 0.f, 0.f, 0.f});
+  acc = mfma_bf16(ah, bl, acc);
+  return mfma_bf16(al, bh, acc);
+}
+
+// element (o, i) of layer l's weight into its split-bf16 images: forward image Wf [o][pos(i)]
+// (rows: 16-padded dout), transposed image Wt [i][pos(o)] (32 rows; layers >= 1 only)
+__device__ __forceinline__ void bf3_store_w(lf* L, const PPORcGeo& g, int q, int l, int o, int i, float v) {
+  const bf16 h = (bf16)v;
+  const bf16 lo = (bf16)(v - (float)h);
+  const int rows = (g.dout[q][l] + 15) & ~15;
+  lbf* wf = (lbf*)(L + g.wf_off[q][l]) + o * kBf3Ld + (l == 0 ? bf3_pos_in0(i) : bf3_pos_h(i));
+  wf[0] = h;
+  wf[rows * kBf3Ld] = lo;
+  if (l > 0) {
+    lbf* wt = (lbf*)(L + g.wt_off[q][l]) + i * kBf3Ld + bf3_pos_h(o);
+    wt[0] = h;
+    wt[32 * kBf3Ld] = lo;
+  }
+}
+
 // Shape specialisation: S0T (16-wide input k-steps / 4), NLT (layers per net), ACTT (hidden
 // activation), HWT (hidden width) fold the per-layer loop bounds, tile counts and the
 // activation switch at compile time; 0 / -1 = read them at run time (generic build).
@@ -347,6 +392,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // to the bound); 0: generic (<= 16)
   constexpr int S0M = S0T > 0 ? S0T : (S0T < 0 ? -S0T : 16);
   const int s0 = S0T > 0 ? S0T : (D + 3) / 4;
+  // split-bf16 forward / dX (see bf3_tile): the 32-wide specialised builds (the plan sets g.bf3
+  // for exactly these and allocates the bf16 weight images)
+  constexpr bool BF3 = KT == 2 && HWT == 32 && NLT == 3 && S0T > 0 && S0T <= 8;
   const bool gauss = DT >= 0 ? DT == 0 : !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
   float am[4];  // action-slot masks of this lane group (Gaussian head)
@@ -376,6 +424,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       for (int i = tid; i < y.dout * y.din; i += kThreads) {
         const int o = i / y.din, c = i - o * y.din;
         L[y.w + o * y.ldw + c] = a.params[wo + i];
+        if constexpr (BF3) bf3_store_w(L, g, qq, l, o, c, a.params[wo + i]);
       }
       for (int i = tid; i < y.dout; i += kThreads) L[y.b + i] = a.params[bo + i];
     }
@@ -566,7 +615,23 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           f4 acc[KT];
 #pragma unroll
           for (int t = 0; t < KT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-          if (l == 0 && KT > 2) {  // 64-wide: two tiles' operands at a time (register budget)
+          if constexpr (BF3) {
+            // B operand: this lane's 8 inputs (layer 0: features 4 s + kk; hidden: the C layout
+            // of the previous layer's two tiles), split into bf16 hi / lo
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              if (l == 0) v[j] = j < S0M ? xb[j < S0M ? j : 0] : 0.f;
+              else v[j] = hreg[l > 0 ? l - 1 : 0][j >> 2][j & 3];
+            }
+            bf16x8 bh, bl;
+            split8(v, bh, bl);
+            const int rows = (y.dout + 15) & ~15;
+            const lbf* wf = (const lbf*)(L + rfl(g.wf_off[q][l])) + r16 * kBf3Ld + 8 * kk;
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+              if (t < tout) acc[t] = bf3_tile(wf + 16 * t * kBf3Ld, rows * kBf3Ld, bh, bl);
+          } else if (l == 0 && KT > 2) {  // 64-wide: two tiles' operands at a time (register budget)
 #pragma unroll
             for (int t0 = 0; t0 < KT; t0 += 2) {
               float w0[2][S0M];
@@ -773,7 +838,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           // image stores, so the loads are not ordered behind them
           constexpr int KWT = KT > 2 ? 1 : KT;  // 64-wide: W^T read per tile below (register budget)
           float wt[KWT][KWT][4];
-          if (KT <= 2 && l > 0) {
+          if (!BF3 && KT <= 2 && l > 0) {
 #pragma unroll
             for (int u2 = 0; u2 < KT; ++u2)
 #pragma unroll
@@ -801,7 +866,19 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           f4 accb[KT];
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) accb[u2] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (KT <= 2) {
+          if constexpr (BF3) {
+            // B operand: this lane's dZ of the layer's output tiles (head: tile 0 only, the rest
+            // zero); A: the transposed split-bf16 image [in][pos(out)]
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (j >> 2) < tout ? dzc[j >> 2][j & 3] : 0.f;
+            bf16x8 bh, bl;
+            split8(v, bh, bl);
+            const lbf* wt_img = (const lbf*)(L + rfl(g.wt_off[q][l])) + r16 * kBf3Ld + 8 * kk;
+#pragma unroll
+            for (int u2 = 0; u2 < KT; ++u2)
+              if (u2 < tin) accb[u2] = bf3_tile(wt_img + 16 * u2 * kBf3Ld, 32 * kBf3Ld, bh, bl);
+          } else if constexpr (KT <= 2) {
 #pragma unroll
             for (int tt = 0; tt < KT; ++tt)
 #pragma unroll
@@ -1174,7 +1251,15 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         gm[it][j] = b1 * gm[it][j] + (1.f - b1) * gval;
         gv[it][j] = b2 * gv[it][j] + (1.f - b2) * gval * gval;
         const float denom = __builtin_amdgcn_sqrtf(gv[it][j]) * inv_bc2s + eps;
-        L[paddr[it] + j * pstr[it]] = pval[it][j] - step_size * gm[it][j] * __builtin_amdgcn_rcpf(denom);
+        const float nv = pval[it][j] - step_size * gm[it][j] * __builtin_amdgcn_rcpf(denom);
+        L[paddr[it] + j * pstr[it]] = nv;
+        pval[it][j] = nv;
+      }
+      if constexpr (BF3) {  // the split-bf16 images of the updated elements (padding stays 0)
+        const int desc = rfl(g.items[wb + w + it * kWaves]);
+        const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf3_store_w(L, g, iq, il, 16 * ta + 4 * kk + j, 16 * tb + r16, pval[it][j]);
       }
     }
 #pragma unroll
