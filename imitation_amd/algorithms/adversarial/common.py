@@ -109,13 +109,23 @@ class _DeviceDemoSampler:
         }
         self._gen = th.Generator(device=self.device)
         self._gen.manual_seed(int(seed if seed is not None else np.random.randint(0, 2**31 - 1)) + 104729 * pdist.rank())
+        # epoch orders: one keyed Feistel permutation launch per epoch (ops.rl.random_permutations)
+        # instead of torch.randperm's device radix sort (~10 launches); key = (base, epoch count)
+        self._base = int(self._gen.initial_seed())
+        self._epochs = 0
         self._perm = None
         self._pos = 0
 
     def next_indices(self) -> th.Tensor:
         """Row indices of the next batch (a contiguous slice of the epoch permutation)."""
         if self._perm is None or self._pos + self.batch_size > self.n:
-            self._perm = th.randperm(self.n, device=self.device, generator=self._gen)
+            self._epochs += 1
+            if self.device.type == "cuda":
+                from imitation_amd.ops import rl as rl_ops
+
+                self._perm = rl_ops.random_permutations(1, self.n, self._base * 1000003 + self._epochs, self.device)[0].long()
+            else:
+                self._perm = th.randperm(self.n, device=self.device, generator=self._gen)
             self._pos = 0
         idx = self._perm[self._pos : self._pos + self.batch_size]
         self._pos += self.batch_size

@@ -244,7 +244,7 @@ def adversarial_state(trainer) -> Dict[str, Any]:
     sampler = trainer._endless_expert_iterator
     if isinstance(sampler, common._DeviceDemoSampler):
         st["demo_sampler"] = {"perm": None if sampler._perm is None else _to_cpu(sampler._perm), "pos": int(sampler._pos),
-                              "gen": sampler._gen.get_state()}
+                              "gen": sampler._gen.get_state(), "base": int(sampler._base), "epochs": int(sampler._epochs)}
     if hasattr(trainer, "engine_state"):
         st["engine"] = trainer.engine_state()
     return st
@@ -268,6 +268,8 @@ def load_adversarial_state(trainer, st: Dict[str, Any]) -> None:
         sampler._perm = None if ds["perm"] is None else ds["perm"].to(sampler.device)
         sampler._pos = ds["pos"]
         sampler._gen.set_state(ds["gen"])
+        sampler._base = int(ds.get("base", sampler._base))
+        sampler._epochs = int(ds.get("epochs", 0))
     if "engine" in st and hasattr(trainer, "load_engine_state"):
         trainer.load_engine_state(st["engine"])
     determinism.restore_rng_state(st["rng"])
