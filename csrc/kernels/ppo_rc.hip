@@ -1,6 +1,8 @@
 // Register-chained PPO update: host planning, the parallel prep kernel and the launch of the
 // shape-specialised kernel instance (kernel template: ppo_rc_kernel.h; instances compiled in
 // ppo_rc_inst*.hip, declared extern below).
+#include <stdio.h>
+
 #include "ppo_rc_kernel.h"
 #include "ppo_rc_instances.h"
 
@@ -190,16 +192,23 @@ int device_cu_count() {
 
 // Host planning: LDS images + parameter items + workgroup split. Returns false if the
 // configuration is outside the fast path (falls back to ppo.hip).
+// IMITATION_AMD_PPO_PLAN_DEBUG=1: which check rejected a plan (stderr)
+static bool plan_reject(int site) {
+  const char* ev = getenv("IMITATION_AMD_PPO_PLAN_DEBUG");
+  if (ev && ev[0] == '1') fprintf(stderr, "ppo_rc_plan: rejected at check %d\n", site);
+  return false;
+}
+
 bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g = PPORcGeo{};
-  if (a.batch % 16 != 0 || a.batch <= 0 || a.rows % a.batch != 0 || a.D > 64 || a.A > 16) return false;
-  if (a.n_pi < 1 || a.n_vf < 1 || a.n_pi > kL || a.n_vf > kL) return false;
+  if (a.batch % 16 != 0 || a.batch <= 0 || a.rows % a.batch != 0 || a.D > 64 || a.A > 16) return plan_reject(1);
+  if (a.n_pi < 1 || a.n_vf < 1 || a.n_pi > kL || a.n_vf > kL) return plan_reject(2);
   const int* dims[2] = {a.pi_dims, a.vf_dims};
   const int nls[2] = {a.n_pi, a.n_vf};
   int wmax = 0;
   for (int q = 0; q < 2; ++q)
     for (int l = 0; l + 1 < nls[q]; ++l) wmax = dims[q][l + 1] > wmax ? dims[q][l + 1] : wmax;
-  if (wmax > 64) return false;
+  if (wmax > 64) return plan_reject(3);
   g.kt = wmax <= 32 ? 2 : 4;
   const int KT = g.kt;
   g.nw = waves_for(KT);
@@ -221,7 +230,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     // the 8-wave generic build has 256 registers per wave and spills: run the 4-wave build
     // (2 row-tile waves per net, 512 registers each) for <= 32-wide nets; 64-wide nets outside
     // the [64, 64] family builds cannot hold their owned items without scratch -> the LDS kernel
-    if (KT == 4) return false;
+    if (KT == 4) return plan_reject(4);
     narrow4 = true;
     if (cw > 32) cw = 32;
     if (a.batch % cw != 0) cw = 16;
@@ -234,7 +243,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     const int cus = a.rc_cus > 0 ? a.rc_cus : device_cu_count();
     const int per = (ns && cw == 64) ? 2 : 1;  // net split: two workgroups per row group
     const int cap = (cus / 2) / per;
-    if (cap < 1) return false;
+    if (cap < 1) return plan_reject(5);
     if (gmax > cap) gmax = cap;
   }
   int G = 1;
@@ -250,11 +259,10 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   if (g.ns || narrow4) g.nw = 4;
   // the generic 64-wide net-split build needs scratch (8 weight slots + 2 vectors at runtime
   // shapes): nets outside the specialised [64, 64] families take the LDS kernel
-  if (g.ns && KT == 4 && rc_instance(a, KT, cw, true) == RC_GENERIC) return false;
-  {  // the 32-wide specialised builds run the split-bf16 forward / dX (kernel: BF3)
+  if (g.ns && KT == 4 && rc_instance(a, KT, cw, true) == RC_GENERIC) return plan_reject(6);
+  {  // the 32-wide specialised net-split builds run the split-bf16 forward / dX (kernel: BF3)
     const int inst = rc_instance(a, KT, cw, g.ns != 0);
-    g.bf3 = (inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32 || inst == RC_CHEETAH32_64 || inst == RC_CHEETAH32_32 ||
-             inst == RC_CARTPOLE32_64) ? 1 : 0;
+    g.bf3 = (inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32) ? 1 : 0;
   }
   int off = 0;
   auto take = [&](int n) {
@@ -271,9 +279,9 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     for (int l = 0; l < nls[q]; ++l) {
       const int din = dims[q][l], dout = dims[q][l + 1];
       const bool last = l == nls[q] - 1;
-      if (!last && dout > 16 * KT) return false;
-      if (last && dout > 16) return false;
-      if (l > 0 && din > 16 * KT) return false;
+      if (!last && dout > 16 * KT) return plan_reject(7);
+      if (last && dout > 16) return plan_reject(8);
+      if (l > 0 && din > 16 * KT) return plan_reject(9);
       g.din[q][l] = din;
       g.dout[q][l] = dout;
       const int ip = l == 0 ? ((din + 3) & ~3) : ((din + 15) & ~15);
@@ -293,11 +301,11 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.zero_off = take(64);
   g.param_lds = off;
   // activation / dZ images for the dW MFMAs, K-major split-bf16 (ppo_rc_kernel.h img_store):
-  // per 16-padded column cs floats = hi rows [0, rows_pad) + lo rows at bf16 offset cs (the +12
-  // keeps the 16 columns of one ds_read_b128 group on distinct banks); layer-0 input shared by
-  // both nets
+  // per 16-padded column cs floats = hi rows [0, rows_pad) + lo rows at bf16 offset cs (the +4
+  // keeps the 16 columns of one ds_read_b128 group on distinct banks: 68 / 36 dwords per column);
+  // layer-0 input shared by both nets
   const int rows_pad = cw > 32 ? cw : 32;
-  const int ldr = rows_pad + 12;
+  const int ldr = rows_pad + 4;
   g.ksteps = rows_pad / 32;
   const int h0 = take(((a.D + 15) & ~15) * ldr);
   const int abase = off;
@@ -327,7 +335,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.trash_off = take(64);
   g.lds_floats = off;
   lds_bytes = (size_t)off * 4;
-  if (lds_bytes > 160 * 1024) return false;
+  if (getenv("IMITATION_AMD_PPO_PLAN_DEBUG")) fprintf(stderr, "ppo_rc_plan: %zu B of LDS\n", lds_bytes);
+  if (lds_bytes > 160 * 1024) return plan_reject(10);
   // items: dW tiles first (ids [0, n_witems): a wave's weight items are its first slots),
   // actor's then critic's; then bias vectors: actor's, log_std (an actor item), critic's
   int n = 0;
@@ -337,7 +346,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
       const int to = (g.dout[q][l] + 15) / 16, ti = (g.din[q][l] + 15) / 16;
       for (int ta = 0; ta < to; ++ta)
         for (int tb = 0; tb < ti; ++tb) {
-          if (n >= kMaxRcItems) return false;
+          if (n >= kMaxRcItems) return plan_reject(11);
           g.items[n++] = q | (l << 1) | (0 << 3) | (ta << 5) | (tb << 9);
         }
     }
@@ -347,11 +356,11 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   for (int q = 0; q < 2; ++q) {
     g.bbase[q] = n;
     for (int l = 0; l < nls[q]; ++l) {
-      if (n >= kMaxRcItems) return false;
+      if (n >= kMaxRcItems) return plan_reject(12);
       g.items[n++] = q | (l << 1) | (1 << 3);
     }
     if (q == 0 && !a.discrete && a.log_std_off >= 0) {
-      if (n >= kMaxRcItems) return false;
+      if (n >= kMaxRcItems) return plan_reject(13);
       g.items[n++] = 2 << 3;
     }
     g.nbit[q] = n - g.bbase[q];
@@ -374,7 +383,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
     if (inst == RC_64_D16) { wcap = 12; bcap = 2; }
     if (inst == RC_64_D32) { wcap = 14; bcap = 2; }
   }
-  if ((wmx + g.nw - 1) / g.nw > wcap || (bmx + g.nw - 1) / g.nw > bcap) return false;
+  if ((wmx + g.nw - 1) / g.nw > wcap || (bmx + g.nw - 1) / g.nw > bcap) return plan_reject(14);
   g.dp = (a.D + 3) & ~3;
   return true;
 }

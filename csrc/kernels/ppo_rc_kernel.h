@@ -392,9 +392,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // to the bound); 0: generic (<= 16)
   constexpr int S0M = S0T > 0 ? S0T : (S0T < 0 ? -S0T : 16);
   const int s0 = S0T > 0 ? S0T : (D + 3) / 4;
-  // split-bf16 forward / dX (see bf3_tile): the 32-wide specialised builds (the plan sets g.bf3
-  // for exactly these and allocates the bf16 weight images)
-  constexpr bool BF3 = KT == 2 && HWT == 32 && NLT == 3 && S0T > 0 && S0T <= 8;
+  // split-bf16 forward / dX (see bf3_tile): the 32-wide specialised net-split builds (the plan
+  // sets g.bf3 for exactly these and allocates the bf16 weight images)
+  // (net-split builds only: with both nets in one workgroup the extra images exceed the LDS)
+  constexpr bool BF3 = KT == 2 && HWT == 32 && NLT == 3 && S0T > 0 && S0T <= 8 && NW == 4 && CWT == 64;
   const bool gauss = DT >= 0 ? DT == 0 : !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
   float am[4];  // action-slot masks of this lane group (Gaussian head)
