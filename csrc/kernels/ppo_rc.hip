@@ -262,7 +262,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   if (g.ns && KT == 4 && rc_instance(a, KT, cw, true) == RC_GENERIC) return plan_reject(6);
   {  // the 32-wide specialised net-split builds run the split-bf16 forward / dX (kernel: BF3)
     const int inst = rc_instance(a, KT, cw, g.ns != 0);
-    g.bf3 = (inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32) ? 1 : 0;
+    g.bf3 = (inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32 || inst == RC_NS_HOPPER64R || inst == RC_NS_WALKER64R ||
+             inst == RC_NS_64_D16 || inst == RC_NS_64_D32) ? 1 : 0;
   }
   int off = 0;
   auto take = [&](int n) {
@@ -287,11 +288,13 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
       const int ip = l == 0 ? ((din + 3) & ~3) : ((din + 15) & ~15);
       const int op = (dout + 15) & ~15;
       g.ldw[q][l] = (l == 0 ? ((din + 15) & ~15) : ip) + 4;
-      g.w_off[q][l] = take(op * g.ldw[q][l]);
+      // (BF3: the fp32 masters live in the Adam owners' registers -- no fp32 weight image)
+      g.w_off[q][l] = take(g.bf3 ? 0 : op * g.ldw[q][l]);
       g.b_off[q][l] = take(op);
-      if (g.bf3) {  // split-bf16 weight images (hi + lo): forward [op][pos(in)], transposed [32][pos(out)]
-        g.wf_off[q][l] = take(op * kBf3Ld);
-        g.wt_off[q][l] = l > 0 ? take(32 * kBf3Ld) : 0;
+      if (g.bf3) {  // split-bf16 weight images (hi + lo): forward [op][pos(in)], transposed [din][pos(out)]
+        const int kin = l == 0 ? 32 : 16 * KT, kout = last ? 32 : 16 * KT;
+        g.wf_off[q][l] = take(op * bf3_ld(kin));
+        g.wt_off[q][l] = l > 0 ? take(((din + 15) & ~15) * bf3_ld(kout)) : 0;
       }
     }
     pend = off > pend ? off : pend;

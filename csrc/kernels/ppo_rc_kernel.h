@@ -303,16 +303,18 @@ __device__ __forceinline__ void img_store(lf* L, int off, int cs, int col, int r
   p[cs] = (bf16)(v - (float)h);
 }
 
-// ---- split-bf16 forward / input-gradient path (BF3: <= 32-wide nets, obs dim <= 32)
-// The fp32 16x16x4 chains (8 MFMAs of 32 cycles per 32-wide K) become v_mfma_f32_16x16x32_bf16
+// ---- split-bf16 forward / input-gradient path (BF3: 32- and 64-wide 3-layer nets, obs dim <= 32)
+// The fp32 16x16x4 chains (8 MFMAs of 32 cycles per 32 of K) become v_mfma_f32_16x16x32_bf16
 // triples (hi.hi + hi.lo + lo.hi: 3 x 16 cycles, ~2^-16 relative product error) over bf16 hi / lo
-// weight images kept next to the fp32 master (updated by the Adam owners). The B operand of a
-// lane is its own 8 activations (C layout of the previous layer: features 4 kk + j of tiles 0 / 1)
-// in the K order pos(f) below; the weight images store column f at pos(f), so no data moves
-// between lanes. Layer 0's input is lane kk's features 4 s + kk (s < 8) at position 8 kk + s.
-constexpr int kBf3Ld = 40;  // bf16 per weight-image row (32 + 8: the 16 rows of a b128 group on distinct banks)
+// weight images; the fp32 master weights live in the Adam owners' registers, which rewrite the
+// images after every step. The B operand of a lane is its own 8 activations per 32 of K (C layout
+// of the previous layer: features 16 t + 4 kk + j of tiles 2 s, 2 s + 1 in K-step s) in the K
+// order pos_h(f); the weight images store column f at that position, so no data moves between
+// lanes. Layer 0's input is lane kk's features 4 s + kk (s < 8) at position 8 kk + s (pos_in0).
+// Image rows hold K + 8 bf16 (the 16 rows of a b128 group on distinct banks).
+__host__ __device__ __forceinline__ int bf3_ld(int k) { return k + 8; }
 __device__ __forceinline__ int bf3_pos_in0(int f) { return 8 * (f & 3) + (f >> 2); }
-__device__ __forceinline__ int bf3_pos_h(int f) { return 8 * ((f >> 2) & 3) + 4 * (f >> 4) + (f & 3); }
+__device__ __forceinline__ int bf3_pos_h(int f) { return 32 * (f >> 5) + 8 * ((f >> 2) & 3) + 4 * ((f >> 4) & 1) + (f & 3); }
 
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
 #pragma unroll
@@ -323,28 +325,33 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& 
   }
 }
 
-// acc (C[16 x 16]) = A_tile . B with A rows at `a` (hi image; lo image `lo_off` bf16 further)
-__device__ __forceinline__ f4 bf3_tile(const lbf* a, int lo_off, bf16x8 bh, bf16x8 bl) {
+// acc += A_tile(32 of K) . B with A's row of this lane at `a` (hi image; lo image `lo_off` bf16 on)
+__device__ __forceinline__ f4 bf3_tile(const lbf* a, int lo_off, bf16x8 bh, bf16x8 bl, f4 acc) {
   const bf16x8 ah = *(const lbf8*)a;
   const bf16x8 al = *(const lbf8*)(a + lo_off);
-  f4 acc = mfma_bf16(ah, bh, f4{0.f, 0.f, 0.f, 0.f});
+  acc = mfma_bf16(ah, bh, acc);
   acc = mfma_bf16(ah, bl, acc);
   return mfma_bf16(al, bh, acc);
 }
 
-// element (o, i) of layer l's weight into its split-bf16 images: forward image Wf [o][pos(i)]
-// (rows: 16-padded dout), transposed image Wt [i][pos(o)] (32 rows; layers >= 1 only)
-__device__ __forceinline__ void bf3_store_w(lf* L, const PPORcGeo& g, int q, int l, int o, int i, float v) {
+// Geometry of layer l's images: forward Wf [16-padded dout rows][pos(in)] (K = 32 for layer 0,
+// 16 KT for hidden inputs), transposed Wt [16-padded din rows][pos_h(out)] (layers >= 1; K = 32 for
+// the head's <= 16 outputs, 16 KT otherwise); lo image right after hi.
+template <int KT>
+__device__ __forceinline__ void bf3_store_w(lf* L, const PPORcGeo& g, int q, int l, int o, int i, float v, int nl) {
   const bf16 h = (bf16)v;
   const bf16 lo = (bf16)(v - (float)h);
+  const int kin = l == 0 ? 32 : 16 * KT;
   const int rows = (g.dout[q][l] + 15) & ~15;
-  lbf* wf = (lbf*)(L + g.wf_off[q][l]) + o * kBf3Ld + (l == 0 ? bf3_pos_in0(i) : bf3_pos_h(i));
+  lbf* wf = (lbf*)(L + g.wf_off[q][l]) + o * bf3_ld(kin) + (l == 0 ? bf3_pos_in0(i) : bf3_pos_h(i));
   wf[0] = h;
-  wf[rows * kBf3Ld] = lo;
+  wf[rows * bf3_ld(kin)] = lo;
   if (l > 0) {
-    lbf* wt = (lbf*)(L + g.wt_off[q][l]) + i * kBf3Ld + bf3_pos_h(o);
+    const int kout = l == nl - 1 ? 32 : 16 * KT;
+    const int trows = (g.din[q][l] + 15) & ~15;
+    lbf* wt = (lbf*)(L + g.wt_off[q][l]) + i * bf3_ld(kout) + bf3_pos_h(o);
     wt[0] = h;
-    wt[32 * kBf3Ld] = lo;
+    wt[trows * bf3_ld(kout)] = lo;
   }
 }
 
@@ -392,10 +399,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // to the bound); 0: generic (<= 16)
   constexpr int S0M = S0T > 0 ? S0T : (S0T < 0 ? -S0T : 16);
   const int s0 = S0T > 0 ? S0T : (D + 3) / 4;
-  // split-bf16 forward / dX (see bf3_tile): the 32-wide specialised net-split builds (the plan
-  // sets g.bf3 for exactly these and allocates the bf16 weight images)
-  // (net-split builds only: with both nets in one workgroup the extra images exceed the LDS)
-  constexpr bool BF3 = KT == 2 && HWT == 32 && NLT == 3 && S0T > 0 && S0T <= 8 && NW == 4 && CWT == 64;
+  // split-bf16 forward / dX (see bf3_tile): the specialised 3-layer net-split builds with obs dim
+  // <= 32 (the plan sets g.bf3 for exactly these and allocates the bf16 weight images; with both
+  // nets in one workgroup the images would exceed the LDS)
+  constexpr bool BF3 = (HWT == 16 * KT) && NLT == 3 && S0T != 0 && S0M <= 8 && NW == 4 && CWT == 64;
   const bool gauss = DT >= 0 ? DT == 0 : !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
   float am[4];  // action-slot masks of this lane group (Gaussian head)
@@ -424,8 +431,8 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       const int bo = qq == 0 ? a.pi_b_off[l] : a.vf_b_off[l];
       for (int i = tid; i < y.dout * y.din; i += kThreads) {
         const int o = i / y.din, c = i - o * y.din;
-        L[y.w + o * y.ldw + c] = a.params[wo + i];
-        if constexpr (BF3) bf3_store_w(L, g, qq, l, o, c, a.params[wo + i]);
+        if constexpr (BF3) bf3_store_w<KT>(L, g, qq, l, o, c, a.params[wo + i], qq == 0 ? a.n_pi : a.n_vf);
+        else L[y.w + o * y.ldw + c] = a.params[wo + i];
       }
       for (int i = tid; i < y.dout; i += kThreads) L[y.b + i] = a.params[bo + i];
     }
@@ -448,6 +455,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   const int bb = ns ? rfl(g.bbase[q]) : n_witems, nbq = ns ? rfl(g.nbit[q]) : n_items - n_witems;
   float gm[KW][4], gv[KW][4];  // weight tiles: Adam moments
   f4 gg[KW];                   // and gradient (the dW MFMA chains accumulate into it)
+  float wmst[BF3 ? KW : 1][4];  // BF3: the fp32 master weights of the owned tiles (no fp32 LDS image)
   float bm[KB], bv[KB], bg[KB];           // bias / log_std vectors
 #pragma unroll
   for (int it = 0; it < KW; ++it) {
@@ -463,9 +471,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int o = 16 * ta + 4 * kk + j;
+        if constexpr (BF3) wmst[it][j] = 0.f;
         if (o < dout && in < din) {
           gm[it][j] = a.exp_avg[wo + o * din + in];
           gv[it][j] = a.exp_avg_sq[wo + o * din + in];
+          if constexpr (BF3) wmst[it][j] = a.params[wo + o * din + in];
         }
       }
     }
@@ -617,21 +627,28 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
           for (int t = 0; t < KT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (BF3) {
-            // B operand: this lane's 8 inputs (layer 0: features 4 s + kk; hidden: the C layout
-            // of the previous layer's two tiles), split into bf16 hi / lo
-            float v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              if (l == 0) v[j] = j < S0M ? xb[j < S0M ? j : 0] : 0.f;
-              else v[j] = hreg[l > 0 ? l - 1 : 0][j >> 2][j & 3];
-            }
-            bf16x8 bh, bl;
-            split8(v, bh, bl);
+            // B operand per 32 of K: this lane's 8 inputs (layer 0: features 4 s + kk; hidden: the
+            // C layout of the previous layer's tiles 2 s, 2 s + 1), split into bf16 hi / lo
+            constexpr int KS = KT / 2;
+            const int ks_l = l == 0 ? 1 : KS;
+            const int kin = l == 0 ? 32 : 16 * KT;
             const int rows = (y.dout + 15) & ~15;
-            const lbf* wf = (const lbf*)(L + rfl(g.wf_off[q][l])) + r16 * kBf3Ld + 8 * kk;
+            const lbf* wf = (const lbf*)(L + rfl(g.wf_off[q][l])) + r16 * bf3_ld(kin) + 8 * kk;
 #pragma unroll
-            for (int t = 0; t < KT; ++t)
-              if (t < tout) acc[t] = bf3_tile(wf + 16 * t * kBf3Ld, rows * kBf3Ld, bh, bl);
+            for (int ks = 0; ks < KS; ++ks) {
+              if (ks >= ks_l) continue;
+              float v[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                if (l == 0) v[j] = j < S0M ? xb[j < S0M ? j : 0] : 0.f;
+                else v[j] = hreg[l > 0 ? l - 1 : 0][2 * ks + (j >> 2)][j & 3];
+              }
+              bf16x8 bh, bl;
+              split8(v, bh, bl);
+#pragma unroll
+              for (int t = 0; t < KT; ++t)
+                if (t < tout) acc[t] = bf3_tile(wf + 16 * t * bf3_ld(kin) + 32 * ks, rows * bf3_ld(kin), bh, bl, acc[t]);
+            }
           } else if (l == 0 && KT > 2) {  // 64-wide: two tiles' operands at a time (register budget)
 #pragma unroll
             for (int t0 = 0; t0 < KT; t0 += 2) {
@@ -868,17 +885,26 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
           for (int u2 = 0; u2 < KT; ++u2) accb[u2] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (BF3) {
-            // B operand: this lane's dZ of the layer's output tiles (head: tile 0 only, the rest
-            // zero); A: the transposed split-bf16 image [in][pos(out)]
-            float v[8];
+            // B operand per 32 of K: this lane's dZ of output tiles 2 s, 2 s + 1 (head: tile 0 and
+            // zeros); A: the transposed split-bf16 image [in][pos_h(out)]
+            constexpr int KS = KT / 2;
+            const bool head = l == nl - 1;
+            const int ks_l = head ? 1 : KS;
+            const int kout = head ? 32 : 16 * KT;
+            const int trows = (y.din + 15) & ~15;
+            const lbf* wt_img = (const lbf*)(L + rfl(g.wt_off[q][l])) + r16 * bf3_ld(kout) + 8 * kk;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (j >> 2) < tout ? dzc[j >> 2][j & 3] : 0.f;
-            bf16x8 bh, bl;
-            split8(v, bh, bl);
-            const lbf* wt_img = (const lbf*)(L + rfl(g.wt_off[q][l])) + r16 * kBf3Ld + 8 * kk;
+            for (int ks = 0; ks < KS; ++ks) {
+              if (ks >= ks_l) continue;
+              float v[8];
 #pragma unroll
-            for (int u2 = 0; u2 < KT; ++u2)
-              if (u2 < tin) accb[u2] = bf3_tile(wt_img + 16 * u2 * kBf3Ld, 32 * kBf3Ld, bh, bl);
+              for (int j = 0; j < 8; ++j) v[j] = (2 * ks + (j >> 2)) < tout ? dzc[2 * ks + (j >> 2)][j & 3] : 0.f;
+              bf16x8 bh, bl;
+              split8(v, bh, bl);
+#pragma unroll
+              for (int u2 = 0; u2 < KT; ++u2)
+                if (u2 < tin) accb[u2] = bf3_tile(wt_img + 16 * u2 * bf3_ld(kout) + 32 * ks, trows * bf3_ld(kout), bh, bl, accb[u2]);
+            }
           } else if constexpr (KT <= 2) {
 #pragma unroll
             for (int tt = 0; tt < KT; ++tt)
@@ -1240,7 +1266,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
     for (int it = 0; it < KW; ++it)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pval[it][j] = L[paddr[it] + j * pstr[it]];
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (BF3) pval[it][j] = wmst[it][j];
+        else pval[it][j] = L[paddr[it] + j * pstr[it]];
+      }
 #pragma unroll
     for (int ib = 0; ib < KB; ++ib) bval[ib] = L[b_addr[ib]];
 #pragma unroll
@@ -1253,14 +1282,15 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         gv[it][j] = b2 * gv[it][j] + (1.f - b2) * gval * gval;
         const float denom = __builtin_amdgcn_sqrtf(gv[it][j]) * inv_bc2s + eps;
         const float nv = pval[it][j] - step_size * gm[it][j] * __builtin_amdgcn_rcpf(denom);
-        L[paddr[it] + j * pstr[it]] = nv;
-        pval[it][j] = nv;
+        if constexpr (BF3) wmst[it][j] = nv;
+        else L[paddr[it] + j * pstr[it]] = nv;
       }
       if constexpr (BF3) {  // the split-bf16 images of the updated elements (padding stays 0)
         const int desc = rfl(g.items[wb + w + it * kWaves]);
         const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+        const int nlq = iq == 0 ? a.n_pi : a.n_vf;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bf3_store_w(L, g, iq, il, 16 * ta + 4 * kk + j, 16 * tb + r16, pval[it][j]);
+        for (int j = 0; j < 4; ++j) bf3_store_w<KT>(L, g, iq, il, 16 * ta + 4 * kk + j, 16 * tb + r16, wmst[it][j], nlq);
       }
     }
 #pragma unroll
@@ -1309,10 +1339,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       const LG y = lg(g, qq, l);
       const int wo = qq == 0 ? a.pi_w_off[l] : a.vf_w_off[l];
       const int bo = qq == 0 ? a.pi_b_off[l] : a.vf_b_off[l];
-      for (int i = tid; i < y.dout * y.din; i += kThreads) {
-        const int o = i / y.din, c = i - o * y.din;
-        a.params[wo + i] = L[y.w + o * y.ldw + c];
-      }
+      if constexpr (!BF3)
+        for (int i = tid; i < y.dout * y.din; i += kThreads) {
+          const int o = i / y.din, c = i - o * y.din;
+          a.params[wo + i] = L[y.w + o * y.ldw + c];
+        }
       for (int i = tid; i < y.dout; i += kThreads) a.params[bo + i] = L[y.b + i];
     }
   }
@@ -1331,6 +1362,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       if (o < dout && in < din) {
         a.exp_avg[wo + o * din + in] = gm[it][j];
         a.exp_avg_sq[wo + o * din + in] = gv[it][j];
+        if constexpr (BF3) a.params[wo + o * din + in] = wmst[it][j];  // the owners hold the masters
       }
     }
   }
