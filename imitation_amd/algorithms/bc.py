@@ -298,6 +298,7 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         import os
 
         loader = self._demo_data_loader
+        loader = getattr(loader, "data_loader", loader)  # (make_data_loader's batch-size-checking wrapper)
         if (graphed is None or on_batch_end is not None or not hasattr(loader, "next_epoch_perm")
                 or self.minibatch_size != self.batch_size or os.environ.get("IMITATION_AMD_BC_EPOCH_GRAPH", "1") == "0"):
             return None
