@@ -253,10 +253,16 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         """HIP-graph minibatch step when it has the eager loop's semantics: GPU policy, no
         gradient accumulation (minibatch == batch), no DP gradient bucket, an optimiser with
         a capturable mode. Disabled with ``IMITATION_AMD_BC_GRAPH=0``."""
-        if (self.minibatch_size != self.batch_size or self._grad_bucket is not None
-                or not graphs.graphs_enabled(self.policy.device, "IMITATION_AMD_BC_GRAPH")
+        if (self.minibatch_size != self.batch_size or not graphs.graphs_enabled(self.policy.device, "IMITATION_AMD_BC_GRAPH")
                 or not graphs.supports_capture(self.optimizer)):
             return None
+        if self._grad_bucket is not None:
+            # data parallel: the fused NatureCNN step (when it applies) as two graphs around the
+            # bucket all-reduce; other policies keep the eager DP loop
+            g = getattr(self, "_dp_step", None)
+            if g is None or g.optimizer is not self.optimizer:
+                g = self._dp_step = _DPFusedStep(self)
+            return g
         g = getattr(self, "_graph_step", None)
         if g is None or g.optimizer is not self.optimizer:
             fused_buckets = isinstance(self.optimizer, optim_ops.FusedAdam)
@@ -299,7 +305,7 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
 
         loader = self._demo_data_loader
         loader = getattr(loader, "data_loader", loader)  # (make_data_loader's batch-size-checking wrapper)
-        if (graphed is None or on_batch_end is not None or not hasattr(loader, "next_epoch_perm")
+        if (graphed is None or self._grad_bucket is not None or on_batch_end is not None or not hasattr(loader, "next_epoch_perm")
                 or self.minibatch_size != self.batch_size or os.environ.get("IMITATION_AMD_BC_EPOCH_GRAPH", "1") == "0"):
             return None
         r = getattr(self, "_epoch_run", None)
@@ -363,13 +369,15 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         for (batch_num, minibatch_size, num_samples_so_far), batch in batches_with_stats:
             obs, acts = self._prepare_batch(batch)
             if graphed is not None and isinstance(obs, th.Tensor) and minibatch_size == self.batch_size:
-                # whole minibatch step (fwd + bwd + optimizer) as one HIP-graph replay
+                # whole minibatch step (fwd + bwd + optimizer) as one HIP-graph replay (data
+                # parallel: two replays around the bucket all-reduce)
                 metrics = graphed(obs, acts)
-                batch_num = batch_num * self.minibatch_size // self.batch_size
-                state.update(batch_num=batch_num, minibatch_size=minibatch_size, num_samples_so_far=num_samples_so_far,
-                             metrics=metrics)
-                process_batch(stepped=True)
-                continue
+                if metrics is not None:
+                    batch_num = batch_num * self.minibatch_size // self.batch_size
+                    state.update(batch_num=batch_num, minibatch_size=minibatch_size, num_samples_so_far=num_samples_so_far,
+                                 metrics=metrics)
+                    process_batch(stepped=True)
+                    continue
             if graphed is not None and graphed.n_captures:
                 self._zero_grad()  # p.grad still holds the last replay's gradients
             metrics = self.loss_calculator(self.policy, obs, acts)
@@ -385,6 +393,54 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         # the per-epoch checks are non-blocking (they read the previous epoch's error word):
         # one blocking check makes a timed-out all-reduce in the last epoch raise here
         pdist.check_comm("BC training", blocking=True)
+
+
+class _DPFusedStep:
+    """Data-parallel BC minibatch on the fused NatureCNN step (``ops/bc_cnn.py``): graph G1 (the
+    autograd-free forward / backward writing the local minibatch-mean gradients into the FusedAdam
+    bucket), the bucket all-reduce (mean over ranks: reference ``bc.py:464-466`` hook point; RCCL,
+    or gloo on one-card rehearsals), graph G2 (the optimizer step). Falls back to the eager DP loop
+    (returns None from :meth:`__call__`) when the fused step does not apply to the batch."""
+
+    def __init__(self, trainer: "_BCBase"):
+        self.trainer = trainer
+        self.optimizer = trainer.optimizer
+        self._fused: Dict[Any, Any] = {}
+        self._graphs: Dict[Any, Any] = {}
+        self.n_captures = 0
+        self.n_replays = 0
+
+    def __call__(self, obs: th.Tensor, acts: th.Tensor):
+        t = self.trainer
+        key = (tuple(obs.shape), obs.dtype)
+        if key not in self._fused:
+            self._fused[key] = bc_cnn.FusedCnnBCStep.maybe(t.policy, t.optimizer, obs, t.loss_calculator.ent_weight,
+                                                           t.loss_calculator.l2_weight)
+        f = self._fused[key]
+        if f is None:
+            return None
+        entry = self._graphs.get(key)
+        if entry is None:
+            static = tuple(x if getattr(x, "_ia_static", False) else x.detach().clone() for x in (obs, acts))
+            side = th.cuda.Stream()
+            side.wait_stream(th.cuda.current_stream())
+            g1, g2 = th.cuda.CUDAGraph(), th.cuda.CUDAGraph()
+            with th.cuda.graph(g1, stream=side):
+                f(*static)
+            with th.cuda.graph(g2, stream=side):
+                t.optimizer.step()
+            th.cuda.current_stream().wait_stream(side)
+            entry = self._graphs[key] = (static, g1, g2)
+            self.n_captures += 1
+        static, g1, g2 = entry
+        for sx, x in zip(static, (obs, acts)):
+            if sx.data_ptr() != x.data_ptr():
+                sx.copy_(x, non_blocking=True)
+        g1.replay()
+        t._grad_bucket.allreduce()
+        g2.replay()
+        self.n_replays += 1
+        return BCTrainingMetrics(**bc_cnn.metrics_fields(f.metrics))
 
 
 class _DeviceEpochRunner:

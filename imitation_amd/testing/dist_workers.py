@@ -502,6 +502,7 @@ def dagger_device_round_worker(rank, world, seed, scratch):
              bc_train_kwargs=dict(n_batches=4, progress_bar=False, log_interval=10**9))
     th.cuda.synchronize()
     col = tr._device_collector
+    dp_step = getattr(tr.bc_trainer, "_dp_step", None)
     return {"policy": [p.detach().cpu().numpy().copy() for p in tr.policy.parameters()],
             "env_state": col.state.detach().cpu().numpy().copy(), "round_num": tr.round_num,
-            "local": tr.last_train_timesteps_local}
+            "local": tr.last_train_timesteps_local, "dp_fused_replays": dp_step.n_replays if dp_step else 0}

@@ -183,3 +183,22 @@ def test_dagger_device_collector_dp_replicas(monkeypatch, tmp_path):
         np.testing.assert_array_equal(a, b)
     assert out[0]["round_num"] == out[1]["round_num"] >= 1
     assert not np.array_equal(out[0]["env_state"], out[1]["env_state"])
+
+
+@pytest.mark.gpu
+def test_dagger_dp_fused_bc_step_matches_eager_dp(monkeypatch, tmp_path):
+    """Data-parallel BC on the fused NatureCNN step (algorithms/bc.py ``_DPFusedStep``: graph of the
+    autograd-free fwd / bwd into the bucket, bucket all-reduce, graph of the optimizer step): the
+    replicas stay bit-identical and match the eager autograd DP loop within bf16 tolerance."""
+    monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("IMITATION_AMD_ONESHOT", "1")
+    fused = run_ranks(W.dagger_device_round_worker, 2, 4, str(tmp_path / "f"), timeout=400)
+    assert all(o["dp_fused_replays"] >= 4 for o in fused)
+    for a, b in zip(fused[0]["policy"], fused[1]["policy"]):
+        np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("IMITATION_AMD_BC_CNN_FUSED", "0")
+    eager = run_ranks(W.dagger_device_round_worker, 2, 4, str(tmp_path / "e"), timeout=400)
+    assert all(o["dp_fused_replays"] == 0 for o in eager)
+    for a, b in zip(fused[0]["policy"], eager[0]["policy"]):
+        scale = max(1e-3, float(np.abs(b).max()))
+        assert float(np.abs(a - b).max()) <= 2e-2 * scale
