@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/engine/test_device_engine.py tests/engine/test_device_dagger.py tests/algorithms/test_bc.py -m gpu -k "timeout_raises or ppo_kernel_matches or epoch_graph or pipelined or agent_gather" > gpurun_out/r4a_new.log 2>&1 || { echo "new tests failed"; tail -40 gpurun_out/r4a_new.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/engine/test_device_engine.py tests/engine/test_device_dagger.py tests/algorithms/test_bc.py tests/parallel/test_oneshot.py -m gpu -k "timeout_raises or ppo_kernel_matches or epoch_graph or pipelined or agent_gather or dp_fused_bc" > gpurun_out/r4a_new.log 2>&1 || { echo "new tests failed"; tail -40 gpurun_out/r4a_new.log; exit 1; }
 tail -1 gpurun_out/r4a_new.log
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/r4a_gpu.log 2>&1 || { echo "gpu suite failed"; tail -40 gpurun_out/r4a_gpu.log; exit 1; }
 tail -1 gpurun_out/r4a_gpu.log
