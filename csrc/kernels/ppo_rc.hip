@@ -263,7 +263,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   {  // the 32-wide specialised net-split builds run the split-bf16 forward / dX (kernel: BF3)
     const int inst = rc_instance(a, KT, cw, g.ns != 0);
     g.bf3 = (inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32 || inst == RC_NS_HOPPER64R || inst == RC_NS_WALKER64R ||
-             inst == RC_NS_64_D16 || inst == RC_NS_64_D32) ? 1 : 0;
+             inst == RC_NS_64_D16 || inst == RC_NS_64_D32 || inst == RC_CHEETAH32_64 || inst == RC_CARTPOLE32_64) ? 1 : 0;
   }
   int off = 0;
   auto take = [&](int n) {

@@ -399,10 +399,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // to the bound); 0: generic (<= 16)
   constexpr int S0M = S0T > 0 ? S0T : (S0T < 0 ? -S0T : 16);
   const int s0 = S0T > 0 ? S0T : (D + 3) / 4;
-  // split-bf16 forward / dX (see bf3_tile): the specialised 3-layer net-split builds with obs dim
-  // <= 32 (the plan sets g.bf3 for exactly these and allocates the bf16 weight images; with both
-  // nets in one workgroup the images would exceed the LDS)
-  constexpr bool BF3 = (HWT == 16 * KT) && NLT == 3 && S0T != 0 && S0M <= 8 && NW == 4 && CWT == 64;
+  // split-bf16 forward / dX (see bf3_tile): the specialised 3-layer builds with obs dim <= 32 and
+  // 64-row chunks -- net split, and both 32-wide nets in one 8-wave workgroup (the plan sets g.bf3
+  // for exactly these and allocates the bf16 weight images)
+  constexpr bool BF3 = (HWT == 16 * KT) && NLT == 3 && S0T != 0 && S0M <= 8 && CWT == 64 && (NW == 4 || KT == 2);
   const bool gauss = DT >= 0 ? DT == 0 : !a.discrete;
   const bool has_ls = gauss && a.log_std_off >= 0;
   float am[4];  // action-slot masks of this lane group (Gaussian head)
