@@ -381,8 +381,8 @@ class ActiveSelectionFragmenter(Fragmenter):
         return self._uncertainty_on
 
     def raise_uncertainty_on_not_supported(self) -> NoReturn:
-        raise ValueError(f"{self.uncertainty_on} not supported. `uncertainty_on` should be from `logit`, "
-                         "`probability`, or `label`")
+        raise ValueError(f"""{self.uncertainty_on} not supported.
+            `uncertainty_on` should be from `logit`, `probability`, or `label`""")
 
     def __call__(self, trajectories, fragment_length: int, num_pairs: int) -> Sequence[TrajectoryWithRewPair]:
         fragment_pairs = self.base_fragmenter(trajectories=trajectories, fragment_length=fragment_length,

@@ -550,3 +550,70 @@ def test_epoch_orders_replay_the_dataloader(P, B):
     fast = _epoch_orders(fast_loader, P, 6) + [th.cat(list(fast_loader))]
     ref = [th.cat(list(ref_loader)) for _ in range(7)]
     assert all(th.equal(a, b) for a, b in zip(fast, ref))
+
+
+def test_trajectory_dataset_not_static(cartpole_expert_trajectories, rng, num_steps: int = 400):
+    """TrajectoryDataset.sample() does not always return the same trajectories
+    (reference ``test_trajectory_dataset_not_static``)."""
+    import math
+
+    dataset = pc.TrajectoryDataset(cartpole_expert_trajectories, rng)
+    flakiness_prob = 1 / len(cartpole_expert_trajectories)
+    max_samples = math.ceil(math.log(1e-6) / math.log(flakiness_prob))
+    sample = dataset.sample(num_steps)
+
+    def same(a, b):
+        return len(a) == len(b) and all(np.array_equal(x.obs, y.obs) and np.array_equal(x.acts, y.acts) for x, y in zip(a, b))
+
+    assert not all(same(sample, dataset.sample(num_steps)) for _ in range(max_samples))
+
+
+def test_agent_trainer_populates_buffer(agent_trainer):
+    agent_trainer.train(steps=1)
+    assert agent_trainer.buffering_wrapper.n_transitions > 0
+
+
+class _FakeImageEnv(core.Env):
+    """Channels-last uint8 frames, 10-step episodes (SB3's FakeImageEnv, which the reference uses)."""
+
+    def __init__(self):
+        self.observation_space = spaces.Box(low=0, high=255, shape=(12, 16, 3), dtype=np.uint8)
+        self.action_space = spaces.Discrete(2)
+        self._rng = np.random.default_rng(0)
+        self._t = 0
+
+    def _obs(self):
+        return self._rng.integers(0, 256, self.observation_space.shape, dtype=np.uint8)
+
+    def step(self, action):
+        self._t += 1
+        return self._obs(), 0.0, self._t >= 10, False, {}
+
+    def reset(self, *, seed=None, options=None):
+        self._t = 0
+        return self._obs(), {}
+
+
+def test_agent_trainer_sample_image_observations(rng):
+    """AgentTrainer.sample() in an image env returns observations in the env's own layout even
+    if the RL algorithm transposes image channels (reference test of the same name)."""
+    venv = DummyVecEnv([_FakeImageEnv])
+    reward_net = reward_nets.BasicRewardNet(venv.observation_space, venv.action_space)
+    agent = PPO("MlpPolicy", venv, n_epochs=1, batch_size=2, n_steps=10, device="cpu")
+    agent_trainer = pc.AgentTrainer(agent, reward_net, venv, exploration_frac=0.5, rng=rng)
+    trajectories = agent_trainer.sample(2)
+    assert len(trajectories) > 0
+    assert all(t.obs.shape[1:] == venv.observation_space.shape for t in trajectories)
+
+
+def test_active_fragmenter_uncertainty_on_not_supported_error(venv, random_fragmenter):
+    ensemble = pc.PreferenceModel(testing_reward_nets.make_ensemble(venv.observation_space, venv.action_space))
+    with pytest.raises(ValueError, match=r".* not supported\.\n\s+`uncertainty_on` should be from .*"):
+        pc.ActiveSelectionFragmenter(preference_model=ensemble, base_fragmenter=random_fragmenter,
+                                     fragment_sample_factor=2, uncertainty_on="uncertainty_on")
+
+
+def test_active_selection_raises_error_when_initialized_without_an_ensemble(preference_model, random_fragmenter):
+    with pytest.raises(ValueError, match=r"PreferenceModel not wrapped over an ensemble.*"):
+        pc.ActiveSelectionFragmenter(preference_model=preference_model, base_fragmenter=random_fragmenter,
+                                     fragment_sample_factor=2, uncertainty_on="logit")
