@@ -355,6 +355,42 @@ __device__ __forceinline__ void bf3_store_w(lf* L, const PPORcGeo& g, int q, int
   }
 }
 
+// An Adam owner's 4 updated elements W[16 ta + 4 kk + j][16 tb + r16] (j < 4) into the images:
+// forward image rows o = 16 ta + 4 kk + j at one column pos(in) (4 b16 stores per half), the
+// transposed image row in at the 4 consecutive positions pos_h(16 ta + 4 kk + j) (one b64 store
+// per half). Layer offsets / row counts are wave-uniform.
+template <int KT>
+__device__ __forceinline__ void bf3_store_tile(lf* L, const PPORcGeo& g, int q, int l, int ta, int tb, int r16, int kk,
+                                               int nl, const float (&v)[4]) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) bf16x4 lbf4;
+  bf16x4 h4, l4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16 h = (bf16)v[j];
+    h4[j] = h;
+    l4[j] = (bf16)(v[j] - (float)h);
+  }
+  const int i = 16 * tb + r16;
+  const int kin = l == 0 ? 32 : 16 * KT;
+  const int ldi = bf3_ld(kin);
+  const int rows = (rfl(g.dout[q][l]) + 15) & ~15;
+  lbf* wf = (lbf*)(L + rfl(g.wf_off[q][l])) + (16 * ta + 4 * kk) * ldi + (l == 0 ? bf3_pos_in0(i) : bf3_pos_h(i));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    wf[j * ldi] = h4[j];
+    wf[j * ldi + rows * ldi] = l4[j];
+  }
+  if (l > 0) {
+    const int kout = l == nl - 1 ? 32 : 16 * KT;
+    const int ldo = bf3_ld(kout);
+    const int trows = (rfl(g.din[q][l]) + 15) & ~15;
+    lbf* wt = (lbf*)(L + rfl(g.wt_off[q][l])) + i * ldo + 32 * (ta >> 1) + 8 * kk + 4 * (ta & 1);
+    *(lbf4*)wt = h4;
+    *(lbf4*)(wt + trows * ldo) = l4;
+  }
+}
+
 // Shape specialisation: S0T (16-wide input k-steps / 4), NLT (layers per net), ACTT (hidden
 // activation), HWT (hidden width) fold the per-layer loop bounds, tile counts and the
 // activation switch at compile time; 0 / -1 = read them at run time (generic build).
@@ -1288,9 +1324,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       if constexpr (BF3) {  // the split-bf16 images of the updated elements (padding stays 0)
         const int desc = rfl(g.items[wb + w + it * kWaves]);
         const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-        const int nlq = iq == 0 ? a.n_pi : a.n_vf;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bf3_store_w<KT>(L, g, iq, il, 16 * ta + 4 * kk + j, 16 * tb + r16, wmst[it][j], nlq);
+        bf3_store_tile<KT>(L, g, iq, il, ta, tb, r16, kk, iq == 0 ? a.n_pi : a.n_vf, wmst[it]);
       }
     }
 #pragma unroll
