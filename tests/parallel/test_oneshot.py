@@ -199,6 +199,7 @@ def test_dagger_dp_fused_bc_step_matches_eager_dp(monkeypatch, tmp_path):
     monkeypatch.setenv("IMITATION_AMD_BC_CNN_FUSED", "0")
     eager = run_ranks(W.dagger_device_round_worker, 2, 4, str(tmp_path / "e"), timeout=400)
     assert all(o["dp_fused_replays"] == 0 for o in eager)
+    # (bf16 trunk vs fp32 autograd: an Adam step moves an element by up to ~lr whatever its
+    # gradient's size, so near-zero-gradient elements may differ by a few lr = 1e-3)
     for a, b in zip(fused[0]["policy"], eager[0]["policy"]):
-        scale = max(1e-3, float(np.abs(b).max()))
-        assert float(np.abs(a - b).max()) <= 2e-2 * scale
+        assert float(np.abs(a - b).max()) <= 2e-2 * float(np.abs(b).max()) + 4e-3
