@@ -116,3 +116,33 @@ def test_compute_train_stats_are_floats(n):
     if n:
         pred_expert = (logits > 0).numpy()
         assert stats["disc_acc"] == pytest.approx(float(np.mean(pred_expert == (labels.numpy() == 1))))
+
+
+@pytest.mark.gpu
+def test_regression_gail_with_sac(pendulum_expert_trajectories, pendulum_venv):
+    """GAIL with a SAC learner on the GPU trains without crashing (reference
+    ``test_regression_gail_with_sac``, upstream issue #655)."""
+    from imitation_amd.algorithms.adversarial import gail
+    from imitation_amd.rewards import reward_nets
+    from imitation_amd.rl import sac
+
+    learner = sac.SAC(env=pendulum_venv, policy=sac.SACPolicy, device="cuda")
+    reward_net = reward_nets.BasicRewardNet(pendulum_venv.observation_space, pendulum_venv.action_space)
+    gail_trainer = gail.GAIL(demonstrations=pendulum_expert_trajectories, demo_batch_size=1024, venv=pendulum_venv,
+                             gen_algo=learner, reward_net=reward_net)
+    gail_trainer.train(8)
+
+
+def test_gail_with_sac_cpu(pendulum_expert_trajectories, pendulum_venv):
+    """The same composition on the CPU (SAC generator, GAIL discriminator rounds)."""
+    from imitation_amd.algorithms.adversarial import gail
+    from imitation_amd.rewards import reward_nets
+    from imitation_amd.rl import sac
+
+    learner = sac.SAC(env=pendulum_venv, policy=sac.SACPolicy, device="cpu", learning_starts=4, batch_size=32,
+                      policy_kwargs=dict(net_arch=[32, 32]))
+    reward_net = reward_nets.BasicRewardNet(pendulum_venv.observation_space, pendulum_venv.action_space)
+    gail_trainer = gail.GAIL(demonstrations=pendulum_expert_trajectories, demo_batch_size=64, venv=pendulum_venv,
+                             gen_algo=learner, reward_net=reward_net, gen_train_timesteps=16)
+    gail_trainer.train(32)
+    assert gail_trainer._disc_step > 0
