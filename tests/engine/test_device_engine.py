@@ -548,7 +548,8 @@ def test_device_airl_fused_disc_matches_autograd(normalize_output):
 @gpu
 def test_device_airl_fused_rounds_train_and_log():
     tr, venv, gen, rn = _setup_airl(n_envs=8, n_steps=128, batch=256)
-    assert tr._fused_disc and not tr._overlap_disc
+    # pipelined rounds with the discriminator updates behind PPO on the main stream
+    assert tr._fused_disc and tr._overlap_disc and tr._disc_on_main
     r0 = [p.detach().clone() for p in rn.parameters()]
     tr.train(3 * tr.gen_train_timesteps)
     th.cuda.synchronize()
