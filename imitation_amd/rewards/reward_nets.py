@@ -263,8 +263,17 @@ class NormalizedRewardNet(PredictProcessedWrapper):
         self.normalize_output_layer = normalize_output_layer(1)
 
     def predict_processed(self, state, action, next_state, done, update_stats: bool = True, **kwargs) -> np.ndarray:
-        rew = self.predict_processed_th(state, action, next_state, done, update_stats=update_stats, **kwargs)
-        out = rew.detach().cpu().numpy().flatten()
+        """Host API: the base's ``predict_processed`` (extra kwargs forwarded, so a wrapped
+        wrapper's own processing runs), then normalise; ``predict_processed_th`` is the
+        device-resident variant used by the fused reward paths (reference reward_nets.py:637)."""
+        with networks.evaluating(self):
+            rew_th = th.as_tensor(np.asarray(self.base.predict_processed(state, action, next_state, done, **kwargs)),
+                                  device=self.device).float().reshape(-1)
+            with th.no_grad():
+                out = self.normalize_output_layer(rew_th).detach().cpu().numpy().flatten()
+        if update_stats:
+            with th.no_grad():
+                self.normalize_output_layer.update_stats(rew_th)
         assert out.shape == np.shape(state)[:1]
         return out
 

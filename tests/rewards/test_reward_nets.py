@@ -123,3 +123,101 @@ def test_cnn_reward_net_shapes():
         assert out.shape == (5,)
     with pytest.raises(ValueError):
         reward_nets.CnnRewardNet(OBS, ACT)
+
+
+def _potential(x):
+    return th.zeros(x.shape[0], device=x.device)
+
+
+def _frozen_lake_venv(rng):
+    from imitation_amd.util import util
+
+    return util.make_vec_env("FrozenLake-v1", n_envs=1, rng=rng)
+
+
+def test_strip_wrappers_basic(rng):
+    """Reference ``test_strip_wrappers_basic``: a matching outer wrapper is removed, a
+    non-matching one is a no-op."""
+    from imitation_amd.rewards import serialize as rserialize
+    from imitation_amd.util import networks
+
+    venv = _frozen_lake_venv(rng)
+    net = reward_nets.NormalizedRewardNet(reward_nets.BasicRewardNet(venv.observation_space, venv.action_space),
+                                          networks.RunningNorm)
+    net = rserialize._strip_wrappers(net, wrapper_types=[reward_nets.NormalizedRewardNet])
+    assert isinstance(net, reward_nets.BasicRewardNet)
+    net = rserialize._strip_wrappers(net, wrapper_types=[reward_nets.ShapedRewardNet])
+    assert isinstance(net, reward_nets.BasicRewardNet)
+
+
+def test_strip_wrappers_complex(rng):
+    """Wrappers are stripped outside-in only: the wrong order removes nothing."""
+    from imitation_amd.rewards import serialize as rserialize
+    from imitation_amd.util import networks
+
+    venv = _frozen_lake_venv(rng)
+    net = reward_nets.BasicRewardNet(venv.observation_space, venv.action_space)
+    net = reward_nets.ShapedRewardNet(net, _potential, discount_factor=0.99)
+    net = reward_nets.NormalizedRewardNet(net, networks.RunningNorm)
+    net = rserialize._strip_wrappers(net, wrapper_types=[reward_nets.ShapedRewardNet, reward_nets.NormalizedRewardNet])
+    assert isinstance(net, reward_nets.NormalizedRewardNet) and isinstance(net.base, reward_nets.ShapedRewardNet)
+    net = rserialize._strip_wrappers(net, wrapper_types=[reward_nets.NormalizedRewardNet, reward_nets.ShapedRewardNet])
+    assert isinstance(net, reward_nets.BasicRewardNet)
+
+
+def test_strip_wrappers_image(rng):
+    """The same on a CNN reward net over Atari-shaped frames."""
+    from imitation_amd.rewards import serialize as rserialize
+    from imitation_amd.util import networks, util
+
+    venv = util.make_vec_env("PongNoFrameskip-v4", n_envs=1, rng=rng)
+    net = reward_nets.CnnRewardNet(venv.observation_space, venv.action_space)
+    net = reward_nets.ShapedRewardNet(net, _potential, discount_factor=0.99)
+    net = reward_nets.NormalizedRewardNet(net, networks.RunningNorm)
+    net = rserialize._strip_wrappers(net, wrapper_types=[reward_nets.NormalizedRewardNet, reward_nets.ShapedRewardNet])
+    assert isinstance(net, reward_nets.CnnRewardNet)
+
+
+def test_predict_processed_wrappers_pass_on_kwargs():
+    """``NormalizedRewardNet`` / ``AddSTDRewardWrapper``-style wrappers forward extra keyword
+    arguments of ``predict_processed`` to the base (reference test of the same name)."""
+    from unittest import mock
+
+    from imitation_amd.envs import spaces
+    from imitation_amd.testing import reward_nets as testing_reward_nets
+
+    obs_space, act_space = spaces.Box(-1, 1, (2,)), spaces.Box(-1, 1, (1,))
+    base = testing_reward_nets.MockRewardNet(obs_space, act_space)
+    base.predict_processed = mock.Mock(return_value=np.zeros((10,)))
+    from imitation_amd.util import networks
+
+    wrapped = reward_nets.NormalizedRewardNet(base, networks.RunningNorm)  # the reference's concrete wrapper
+    args = (np.zeros((10, 2)), np.zeros((10, 1)), np.zeros((10, 2)), np.zeros(10, dtype=bool))
+    wrapped.predict_processed(*args, foobar=42)
+    base.predict_processed.assert_called_once_with(*args, foobar=42)
+
+
+def test_predict_processed_wrappers_pass_method_calls_to_base():
+    """forward / predict_th / predict / predict_processed / preprocess and the device / dtype
+    properties of a PredictProcessedWrapper go to the wrapped net."""
+    from unittest import mock
+
+    from imitation_amd.envs import spaces
+    from imitation_amd.testing import reward_nets as testing_reward_nets
+
+    obs_space, act_space = spaces.Box(-1, 1, (2,)), spaces.Box(-1, 1, (1,))
+    from imitation_amd.util import networks
+
+    base = testing_reward_nets.MockRewardNet(obs_space, act_space)
+    wrapper = reward_nets.NormalizedRewardNet(base, networks.RunningNorm)
+    np_args = (np.zeros((10, 2), np.float32), np.zeros((10, 1), np.float32), np.zeros((10, 2), np.float32),
+               np.zeros(10, dtype=bool))
+    th_args = tuple(th.as_tensor(a) for a in np_args)
+    for attr, call_with, ret in [("forward", th_args, th.zeros(10)), ("predict_th", np_args, th.zeros(10)),
+                                 ("predict", np_args, np.zeros(10)), ("predict_processed", np_args, np.zeros(10)),
+                                 ("preprocess", np_args, th_args)]:
+        m = mock.MagicMock(return_value=ret)
+        object.__setattr__(base, attr, m)
+        getattr(wrapper, attr)(*call_with)
+        m.assert_called_once_with(*call_with)
+    assert wrapper.device == base.device and wrapper.dtype == base.dtype
