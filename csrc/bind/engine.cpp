@@ -211,6 +211,7 @@ void ppo_update(py::dict d) {
   a.mode = ival(d, "mode", 0);
   a.mb_index = ival(d, "mb_index", 0);
   a.prof = tptr<unsigned long long>(d, "prof", true);
+  if (a.prof) TORCH_CHECK(py::cast<torch::Tensor>(d["prof"]).numel() >= 20, "prof: 20 int64 cycle counters (ppo_rc_kernel.h)");
   a.rc_gmax = ival(d, "rc_gmax", 0);
   a.rc_cw = ival(d, "rc_cw", 0);
   a.err = reinterpret_cast<unsigned*>(tptr<int>(d, "err", true));

@@ -304,8 +304,8 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   g.zero_off = take(64);
   g.param_lds = off;
   // activation / dZ images for the dW MFMAs, K-major split-bf16 (ppo_rc_kernel.h img_store):
-  // per 16-padded column cs floats = hi rows [0, rows_pad) + lo rows at bf16 offset cs (the +4
-  // keeps the 16 columns of one ds_read_b128 group on distinct banks: 68 / 36 dwords per column);
+  // per 16-padded column cs floats = hi rows [0, rows_pad) + lo rows [rows_pad, 2 rows_pad) in
+  // bf16 (ppo_rc_kernel.h img_lo: 16-byte aligned halves, 68 / 36 dwords per column);
   // layer-0 input shared by both nets
   const int rows_pad = cw > 32 ? cw : 32;
   const int ldr = rows_pad + 4;

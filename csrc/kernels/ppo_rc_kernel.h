@@ -257,15 +257,22 @@ __device__ __forceinline__ void reduce_slots(const float* slab, float* red, size
 // stored as hi = bf16(v) and lo = bf16(v - hi), and dZ^T H = hi.hi + hi.lo + lo.hi (the lo.lo term
 // is ~2^-16 of the product: near-fp32 accuracy at 3 bf16 MFMAs per 32 rows instead of eight
 // 16x16x4 fp32 ones). Images are K-major (rows contiguous): column c of an image has its hi rows
-// at bf16 index 2 c cs + r and its lo rows at 2 c cs + cs + r (cs floats per column, chosen so
-// the 16 columns a ds_read_b128 group touches hit distinct banks). Lane (r16, kk) reads rows
+// at bf16 index 2 c cs + r and its lo rows at 2 c cs + img_lo(cs) + r (cs floats per column).
+// Lane (r16, kk) reads rows
 // 8 kk .. 8 kk + 7 (+ 32 per K-step) of column r16 of the item's dZ (A, M = out) and H (B,
 // N = in) tiles; the accumulator layout is the fp32 kernel's (C[out 4 kk + j][in r16]), so the
-// exchange and Adam code is unchanged. izo / iho: bf16 offsets of the lane's first element.
+// exchange and Adam code is unchanged. izo / iho: bf16 offsets of the lane's first element;
+// lo: bf16 offset of the lo half (img_lo).
+// A column of a K-major split-bf16 image is 2 cs bf16 (cs = rows_pad + 4 floats): hi rows at
+// [0, rows_pad), lo rows at [rows_pad, 2 rows_pad), 8 bf16 of padding. The lo half starts at a
+// 16-byte boundary (a ds_read_b128 off its natural alignment stalls ~60 cycles) and the column
+// stride of rows_pad / 4 + 1 (odd) 16-byte slots spreads a read group's 16 columns over the banks.
+__device__ __forceinline__ int img_lo(int cs) { return cs - 4; }
+
 __device__ __forceinline__ f4 mfma_bf16(bf16x8 a, bf16x8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 
 template <int N>
-__device__ __forceinline__ void dw_tiles(const lf* L, const int* izo, const int* iho, int cs, int ksteps, f4* acc) {
+__device__ __forceinline__ void dw_tiles(const lf* L, const int* izo, const int* iho, int lo, int ksteps, f4* acc) {
   const lbf* Lb = (const lbf*)L;
   // items in groups of GS: independent accumulation chains keep the MFMA pipe busy while only
   // the group's operands (4 x bf16x8 per item) are live (2 per group for the largest slot counts)
@@ -280,9 +287,9 @@ __device__ __forceinline__ void dw_tiles(const lf* L, const int* izo, const int*
         const lbf* zp = Lb + izo[i0 + i] + 32 * ks;
         const lbf* hp = Lb + iho[i0 + i] + 32 * ks;
         zh[i] = *(const lbf8*)zp;
-        zl[i] = *(const lbf8*)(zp + cs);
+        zl[i] = *(const lbf8*)(zp + lo);
         hh[i] = *(const lbf8*)hp;
-        hl[i] = *(const lbf8*)(hp + cs);
+        hl[i] = *(const lbf8*)(hp + lo);
       }
 #pragma unroll
       for (int i = 0; i < GS; ++i) {
@@ -300,7 +307,7 @@ __device__ __forceinline__ void img_store(lf* L, int off, int cs, int col, int r
   lbf* p = (lbf*)(L + off) + (2 * col * cs + row);
   const bf16 h = (bf16)v;
   p[0] = h;
-  p[cs] = (bf16)(v - (float)h);
+  p[img_lo(cs)] = (bf16)(v - (float)h);
 }
 
 // ---- split-bf16 forward / input-gradient path (BF3: 32- and 64-wide 3-layer nets, obs dim <= 32)
@@ -358,10 +365,13 @@ __device__ __forceinline__ void bf3_store_w(lf* L, const PPORcGeo& g, int q, int
 // An Adam owner's 4 updated elements W[16 ta + 4 kk + j][16 tb + r16] (j < 4) into the images:
 // forward image rows o = 16 ta + 4 kk + j at one column pos(in) (4 b16 stores per half), the
 // transposed image row in at the 4 consecutive positions pos_h(16 ta + 4 kk + j) (one b64 store
-// per half). Layer offsets / row counts are wave-uniform.
+// per half). kind (0 input layer, 1 hidden, 2 head), the image bases wf / wt (bf16, with the
+// wave-uniform parts of pos) and lo-half offsets are the slot's hoisted uniforms; only the lane
+// terms are formed here: pos_in0(16 tb + r16) = 4 tb + 8 (r16 & 3) + (r16 >> 2), pos_h(16 tb +
+// r16) = 32 (tb >> 1) + 4 (tb & 1) + 8 (r16 >> 2) + (r16 & 3).
 template <int KT>
-__device__ __forceinline__ void bf3_store_tile(lf* L, const PPORcGeo& g, int q, int l, int ta, int tb, int r16, int kk,
-                                               int nl, const float (&v)[4]) {
+__device__ __forceinline__ void bf3_store_tile(lf* L, int kind, int wf, int wfl, int wt, int wtl, int r16, int kk,
+                                               const float (&v)[4]) {
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) bf16x4 lbf4;
   bf16x4 h4, l4;
@@ -371,23 +381,19 @@ __device__ __forceinline__ void bf3_store_tile(lf* L, const PPORcGeo& g, int q, 
     h4[j] = h;
     l4[j] = (bf16)(v[j] - (float)h);
   }
-  const int i = 16 * tb + r16;
-  const int kin = l == 0 ? 32 : 16 * KT;
-  const int ldi = bf3_ld(kin);
-  const int rows = (rfl(g.dout[q][l]) + 15) & ~15;
-  lbf* wf = (lbf*)(L + rfl(g.wf_off[q][l])) + (16 * ta + 4 * kk) * ldi + (l == 0 ? bf3_pos_in0(i) : bf3_pos_h(i));
+  lbf* Lb = (lbf*)L;
+  const int ldi = kind == 0 ? bf3_ld(32) : bf3_ld(16 * KT);
+  lbf* pf = Lb + wf + 4 * kk * ldi + (kind == 0 ? 8 * (r16 & 3) + (r16 >> 2) : 8 * (r16 >> 2) + (r16 & 3));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    wf[j * ldi] = h4[j];
-    wf[j * ldi + rows * ldi] = l4[j];
+    pf[j * ldi] = h4[j];
+    pf[j * ldi + wfl] = l4[j];
   }
-  if (l > 0) {
-    const int kout = l == nl - 1 ? 32 : 16 * KT;
-    const int ldo = bf3_ld(kout);
-    const int trows = (rfl(g.din[q][l]) + 15) & ~15;
-    lbf* wt = (lbf*)(L + rfl(g.wt_off[q][l])) + i * ldo + 32 * (ta >> 1) + 8 * kk + 4 * (ta & 1);
-    *(lbf4*)wt = h4;
-    *(lbf4*)(wt + trows * ldo) = l4;
+  if (kind != 0) {
+    const int ldo = kind == 2 ? bf3_ld(32) : bf3_ld(16 * KT);
+    lbf* pt = Lb + wt + r16 * ldo + 8 * kk;
+    *(lbf4*)pt = h4;
+    *(lbf4*)(pt + wtl) = l4;
   }
 }
 
@@ -554,9 +560,85 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // the LDS offsets of a slot's dZ / H columns are a wave-uniform base (the descriptor) plus
   // ONE lane term shared by every slot (all K-major images have the row stride cw + 4)
   const int nwi = nwq > w ? min(KW, (nwq - w + kWaves - 1) / kWaves) : 0;
-  const int cs = rfl(g.ldz[0][0]);  // floats per column of the split-bf16 K-major images
-  const int ksteps = rfl(g.ksteps);  // 32-row K-steps of a dW tile
+  // floats per column of the split-bf16 K-major images (ppo_rc_plan: max(cw, 32) + 4) and the
+  // 32-row K-steps of a dW tile: compile-time under a fixed chunk width (offsets fold into the
+  // ds_read immediates)
+  constexpr int kRowsPad = CWT > 32 ? CWT : 32;
+  const int cs = CWT > 0 ? kRowsPad + 4 : rfl(g.ldz[0][0]);
+  const int ksteps = CWT > 0 ? kRowsPad / 32 : rfl(g.ksteps);
   const int lterm = r16 * 2 * cs + 8 * kk;  // bf16 offset of this lane's first dW operand
+  // Per-slot wave-uniform LDS bases: the descriptor and layer tables are kernel-argument arrays,
+  // so each dynamically indexed use is a dependent scalar-load chain. The 4-wave builds with at
+  // most 8 weight slots resolve them once (HOIST); the 8-wave ones (256 VGPRs, no AGPRs) and the
+  // 12 / 14-slot ones (full register file) re-resolve them per use.
+  // slot_dw: the slot's dZ / H operand bases (bf16; + lterm per lane).
+  // slot_img (BF3, Adam's image stores): forward image base (+ the lane term of the layer kind:
+  // 0 input layer, 1 hidden, 2 head) and its lo-half offset; transposed image base / lo offset.
+  constexpr bool HOIST = NW == 4 && KW <= 8;
+  auto slot_dw = [&](int it, int& zu, int& hu) {
+    const int desc = rfl(g.items[wb + w + it * kWaves]);
+    const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+    zu = 2 * rfl(g.z_off[iq][il]) + 16 * ta * 2 * cs;
+    hu = 2 * rfl(g.h_off[iq][il]) + 16 * tb * 2 * cs;
+  };
+  auto slot_img = [&](int it, int& kd, int& wf, int& wl, int& wt, int& tl) {
+    const int desc = rfl(g.items[wb + w + it * kWaves]);
+    const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
+    const int nlq = iq == 0 ? a.n_pi : a.n_vf;
+    const int ldi = bf3_ld(il == 0 ? 32 : 16 * KT);
+    wf = rfl(2 * g.wf_off[iq][il] + 16 * ta * ldi + (il == 0 ? 4 * tb : 32 * (tb >> 1) + 4 * (tb & 1)));
+    wl = rfl(((g.dout[iq][il] + 15) & ~15) * ldi);
+    kd = il == 0 ? 0 : (il == nlq - 1 ? 2 : 1);
+    wt = tl = 0;
+    if (il > 0) {
+      const int ldo = bf3_ld(il == nlq - 1 ? 32 : 16 * KT);
+      wt = rfl(2 * g.wt_off[iq][il] + 16 * tb * ldo + 32 * (ta >> 1) + 4 * (ta & 1));
+      tl = rfl(((g.din[iq][il] + 15) & ~15) * ldo);
+    }
+  };
+  // this wave's net geometry per layer (fwd / bwd chains, loss), resolved once for the fully
+  // specialised HOIST builds (GHOIST); the rest index the argument tables per use
+  constexpr bool GHOIST = HOIST && NLT > 0;
+  LG yq[GHOIST ? kL : 1];
+  int wfq[GHOIST && BF3 ? kL : 1], wtq[GHOIST && BF3 ? kL : 1];
+#pragma unroll
+  for (int l = 0; l < kL; ++l) {
+    if (!GHOIST || l >= nl) continue;
+    yq[GHOIST ? l : 0] = lg(g, q, l);
+    if constexpr (BF3) {
+      wfq[GHOIST ? l : 0] = rfl(g.wf_off[q][l]);
+      wtq[GHOIST ? l : 0] = rfl(g.wt_off[q][l]);
+    }
+  }
+  auto LY = [&](int l) -> LG {
+    if constexpr (GHOIST) return yq[GHOIST ? l : 0];
+    else return lg(g, q, l);
+  };
+  auto WF = [&](int l) -> int {
+    if constexpr (GHOIST && BF3) return wfq[GHOIST ? l : 0];
+    else return rfl(g.wf_off[q][l]);
+  };
+  auto WT = [&](int l) -> int {
+    if constexpr (GHOIST && BF3) return wtq[GHOIST ? l : 0];
+    else return rfl(g.wt_off[q][l]);
+  };
+  constexpr int KH = HOIST ? KW : 1, KHB = HOIST && BF3 ? KW : 1;
+  int izu[KH], ihu[KH];
+  int bwf[KHB], bwt[KHB], bpk[KHB];  // bpk: kind | lo offsets << 2 / << 17 (each < 2^15)
+#pragma unroll
+  for (int it = 0; it < KH; ++it) {
+    izu[it] = ihu[it] = 0;
+    if (HOIST && it < nwi) slot_dw(it, izu[it], ihu[it]);
+  }
+#pragma unroll
+  for (int it = 0; it < KHB; ++it) {
+    bwf[it] = bwt[it] = bpk[it] = 0;
+    if (HOIST && BF3 && it < nwi) {
+      int kd, wl, tl;
+      slot_img(it, kd, bwf[it], wl, bwt[it], tl);
+      bpk[it] = kd | (wl << 2) | (tl << 17);
+    }
+  }
   // bias / log_std slots: kind (1 bias, 2 log_std, -1 empty), partial source, element mask
   int bkind[KB], b_off[KB], b_addr[KB];
   float b_okf[KB];  // 1 for lanes holding a real bias / log_std element
@@ -589,9 +671,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // cycle counters (a.prof): accumulated in LDS by one lane, so that they hold no registers
   // across the minibatch loop. [0..2] chunk, exchange + |g|^2, clip + Adam (wave 0);
   // [3..6] / [7..10] actor / critic row tile 0: rows/x, forward, loss, backward chain;
-  // [11] wave 0 B1 wait, [12] dW items; [13..15] exchange: publish, arrival, loads
-  __shared__ unsigned long long sprof[16];
-  if (tid < 16) sprof[tid] = 0;
+  // [11] wave 0 B1 wait, [12] dW items; [13..15] exchange: publish, arrival, loads;
+  // [16] net-split |g|^2 hand-off, [17] Adam on the owned items (wave 0), [18] B3 wait
+  __shared__ unsigned long long sprof[20];
+  if (tid < 20) sprof[tid] = 0;
   // arrival counters per net under the net split ([0]/[2] actor, [4]/[6] critic)
   unsigned* arrive = g.sync + (ns ? 4 * q : 0);
   unsigned* tflag = g.sync + 1;
@@ -600,6 +683,45 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // test knob: the last working workgroup never publishes, so its partners' spins time out
   const bool stall = a.debug_stall != 0 && bid == (ns ? 2 * G : G) - 1;
   __syncthreads();
+
+  // normalised input of this lane's row (cur) with normaliser buffer nbuf -> xo, and the
+  // layer-0 input image for dW (padding features: raw value 0 from the prep kernel, normaliser
+  // image entries 0)
+  auto norm_rows = [&](int nbuf, float (&xo)[S0M]) {
+    float nmv[S0M], nrv[S0M];
+#pragma unroll
+    for (int s = 0; s < S0M; ++s) {
+      nmv[s] = 0.f;
+      nrv[s] = 1.f;
+      if (s < s0 && a.has_norm) {
+        nmv[s] = L[g.nm_off + nbuf + 4 * s + kk];
+        nrv[s] = L[g.nm_off + nbuf + 64 + 4 * s + kk];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S0M; ++s) xo[s] = s < s0 ? (cur.x[s] - nmv[s]) * nrv[s] : 0.f;
+    if (q == 0 || ns) {  // shared layer-0 input image (each workgroup its own under net split)
+      const int h0 = rfl(g.h_off[0][0]);
+#pragma unroll
+      for (int s = 0; s < S0M; ++s)
+        if (s < s0) img_store(L, h0, cs, 4 * s + kk, row, xo[s]);
+    }
+  };
+  // pre_rows: under the exchange (G > 1) or the net split, chunk 0 of minibatch k+1 is
+  // normalised while this workgroup waits for its partners (arrival / |g|^2 hand-off): its
+  // rows are in cur since the last chunk, its normaliser buffer was merged after this
+  // minibatch's B1, and every dW read of the layer-0 image is behind the barrier before it
+  // (32-wide builds: measured slower for the 64-wide ones, whose owned state then moves to
+  // AGPRs around Adam; and the 12 / 14-slot builds' register file is full)
+  constexpr bool PREC = KT == 2 && KW <= 8;
+  const bool pre = PREC && (ns || G > 1);
+  float xpre[PREC ? S0M : 1];
+#pragma unroll
+  for (int s = 0; s < (PREC ? S0M : 1); ++s) xpre[s] = 0.f;
+  auto pre_rows = [&](int k) {
+    if constexpr (PREC)
+      if (pre && rows_wave && k + 1 < K) norm_rows(((k + 1) & 1) * 128, xpre);
+  };
 
   for (int k = 0; k < K; ++k) {
     unsigned long long t0 = a.prof ? clock64() : 0;
@@ -625,9 +747,17 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       unsigned long long c0 = a.prof ? clock64() : 0;
       if (rows_wave) {
         // ---------------- normalised input: B operand of layer 0 (natural K order 4s + kk)
-        // (padding features: raw value 0 from the prep kernel, normaliser image entries 0)
+        // (chunk 0 of minibatch k > 0 under the exchange / net split: done in minibatch k-1's
+        // waiting window, see pre_rows)
         float xb[S0M];
-        {
+        if constexpr (PREC) {
+          if (pre && ch == 0 && k > 0) {
+#pragma unroll
+            for (int s = 0; s < S0M; ++s) xb[s] = xpre[s];
+          } else {
+            norm_rows(nb, xb);
+          }
+        } else {  // (the same as norm_rows, inline: the full-register-file builds stay spill-free)
           float nmv[S0M], nrv[S0M];
 #pragma unroll
           for (int s = 0; s < S0M; ++s) {
@@ -640,12 +770,12 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           }
 #pragma unroll
           for (int s = 0; s < S0M; ++s) xb[s] = s < s0 ? (cur.x[s] - nmv[s]) * nrv[s] : 0.f;
-        }
-        if (q == 0 || ns) {  // shared layer-0 input image (each workgroup its own under net split)
-          const int h0 = rfl(g.h_off[0][0]), ld0 = rfl(g.ldh[0][0]);
+          if (q == 0 || ns) {
+            const int h0 = rfl(g.h_off[0][0]);
 #pragma unroll
-          for (int s = 0; s < S0M; ++s)
-            if (s < s0) img_store(L, h0, ld0, 4 * s + kk, row, xb[s]);
+            for (int s = 0; s < S0M; ++s)
+              if (s < s0) img_store(L, h0, cs, 4 * s + kk, row, xb[s]);
+          }
         }
         unsigned long long c1 = a.prof ? clock64() : 0;
         // ---------------- forward (registers)
@@ -654,7 +784,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
         for (int l = 0; l < kL; ++l) {
           if (l >= nl) continue;
-          const LG y = lg(g, q, l);
+          const LG y = LY(l);
           const bool last = l == nl - 1;
           const int tout = last ? 1 : (HWT > 0 ? HWT / 16 : ((y.dout + 15) >> 4));  // head: dout <= 16
           // all of the layer's weight operands are read first, then the output tiles'
@@ -669,7 +799,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
             const int ks_l = l == 0 ? 1 : KS;
             const int kin = l == 0 ? 32 : 16 * KT;
             const int rows = (y.dout + 15) & ~15;
-            const lbf* wf = (const lbf*)(L + rfl(g.wf_off[q][l])) + r16 * bf3_ld(kin) + 8 * kk;
+            const lbf* wf = (const lbf*)(L + WF(l)) + r16 * bf3_ld(kin) + 8 * kk;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
               if (ks >= ks_l) continue;
@@ -766,11 +896,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
               if (l < kL - 1) {
                 hreg[l][t] = v;
                 // input image of layer l + 1 (for its dW)
-                const LG yn = lg(g, q, l + 1);
-                img_store(L, yn.h, yn.ldh, o0, row, v.x);
-                img_store(L, yn.h, yn.ldh, o0 + 1, row, v.y);
-                img_store(L, yn.h, yn.ldh, o0 + 2, row, v.z);
-                img_store(L, yn.h, yn.ldh, o0 + 3, row, v.w);
+                const LG yn = LY(l + 1);
+                img_store(L, yn.h, cs, o0, row, v.x);
+                img_store(L, yn.h, cs, o0 + 1, row, v.y);
+                img_store(L, yn.h, cs, o0 + 2, row, v.z);
+                img_store(L, yn.h, cs, o0 + 3, row, v.w);
               }
             } else if (t == 0) {
               head = v;
@@ -780,7 +910,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         unsigned long long c2 = a.prof ? clock64() : 0;
         // ---------------- loss -> dZ of the head (C layout, tile 0)
         f4 dz = {0.f, 0.f, 0.f, 0.f};
-        const LG yh = lg(g, q, nl - 1);
+        const LG yh = LY(nl - 1);
         if (q == 0) {
           const float ao[4] = {cur.act.x, cur.act.y, cur.act.z, cur.act.w};
           const float hv[4] = {head.x, head.y, head.z, head.w};
@@ -885,7 +1015,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
 #pragma unroll
         for (int l = kL - 1; l >= 0; --l) {
           if (l >= nl) continue;
-          const LG y = lg(g, q, l);
+          const LG y = LY(l);
           const int tout = l == nl - 1 ? 1 : (HWT > 0 ? HWT / 16 : ((y.dout + 15) >> 4));
           const int tin = HWT > 0 ? HWT / 16 : ((y.din + 15) >> 4);
           // W_l^T operands (W[16 tt + 4 kk + j][16 u2 + r16]) read before this layer's
@@ -905,10 +1035,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           for (int u2 = 0; u2 < KT; ++u2) {
             if (u2 >= tout) continue;
             const int zc = 16 * u2 + 4 * kk;
-            img_store(L, y.z, y.ldz, zc, row, dzc[u2].x);
-            img_store(L, y.z, y.ldz, zc + 1, row, dzc[u2].y);
-            img_store(L, y.z, y.ldz, zc + 2, row, dzc[u2].z);
-            img_store(L, y.z, y.ldz, zc + 3, row, dzc[u2].w);
+            img_store(L, y.z, cs, zc, row, dzc[u2].x);
+            img_store(L, y.z, cs, zc + 1, row, dzc[u2].y);
+            img_store(L, y.z, cs, zc + 2, row, dzc[u2].z);
+            img_store(L, y.z, cs, zc + 3, row, dzc[u2].w);
             const float s0v = sum16(dzc[u2].x), s1v = sum16(dzc[u2].y), s2v = sum16(dzc[u2].z), s3v = sum16(dzc[u2].w);
             if (r16 == 0) {
               const f4 sv = {s0v, s1v, s2v, s3v};
@@ -928,7 +1058,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
             const int ks_l = head ? 1 : KS;
             const int kout = head ? 32 : 16 * KT;
             const int trows = (y.din + 15) & ~15;
-            const lbf* wt_img = (const lbf*)(L + rfl(g.wt_off[q][l])) + r16 * bf3_ld(kout) + 8 * kk;
+            const lbf* wt_img = (const lbf*)(L + WT(l)) + r16 * bf3_ld(kout) + 8 * kk;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
               if (ks >= ks_l) continue;
@@ -1010,17 +1140,22 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         for (int it = 0; it < KW; ++it) {
           izo[it] = iho[it] = 2 * g.zero_off;  // (bf16 units: the zero row)
           if (it < nwi) {
-            const int desc = rfl(g.items[wb + w + it * kWaves]);
-            const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-            izo[it] = 2 * rfl(g.z_off[iq][il]) + 16 * ta * 2 * cs + lterm;
-            iho[it] = 2 * rfl(g.h_off[iq][il]) + 16 * tb * 2 * cs + lterm;
+            int zu, hu;
+            if constexpr (HOIST) {
+              zu = izu[it];
+              hu = ihu[it];
+            } else {
+              slot_dw(it, zu, hu);
+            }
+            izo[it] = zu + lterm;
+            iho[it] = hu + lterm;
           }
         }
         // the chunk's dZ^T H continues each slot's MFMA chain from its running gradient
         // (padding entries are exactly 0: zeroed images)
         // (empty slots read the zero row: their MFMAs add zeros to gradients nobody reads,
         // so every wave runs the same straight-line body)
-        dw_tiles<KW>(L, izo, iho, cs, ksteps, gg);
+        dw_tiles<KW>(L, izo, iho, img_lo(cs), ksteps, gg);
       }
 #pragma unroll
       for (int ib = 0; ib < KB; ++ib) {
@@ -1066,8 +1201,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       const unsigned long long e1 = a.prof ? clock64() : 0;
+      if (tid == 0 && !stall) atomicAdd(arrive, 1u);
+      pre_rows(k);
       if (tid == 0) {
-        if (!stall) atomicAdd(arrive, 1u);
         const unsigned target = (unsigned)G * (unsigned)(k + 1);
         unsigned spins = 0;
         while (ld_sc1u(arrive) < target) {
@@ -1250,10 +1386,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       // sides), polled by the other workgroup; summed actor + critic in both workgroups so
       // that they apply the identical clip
       const unsigned long long x0 = a.prof ? clock64() : 0;
+      unsigned long long* xs = reinterpret_cast<unsigned long long*>(g.sync + 8);
+      const unsigned long long tag = (unsigned long long)(unsigned)(k + 1) << 32;
+      if (tid == 0 && !stall) __hip_atomic_store(xs + q, tag | __float_as_uint(tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (G == 1) pre_rows(k);  // (G > 1: done in the arrival wait)
       if (tid == 0) {
-        unsigned long long* xs = reinterpret_cast<unsigned long long*>(g.sync + 8);
-        const unsigned long long tag = (unsigned long long)(unsigned)(k + 1) << 32;
-        if (!stall) __hip_atomic_store(xs + q, tag | __float_as_uint(tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long o = __hip_atomic_load(xs + (1 - q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
         while ((o >> 32) != (unsigned long long)(unsigned)(k + 1)) {
@@ -1269,8 +1406,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       }
       __syncthreads();
       tot = L[g.red_off + 48];
-      if (a.prof && tid == 0) sprof[14] += clock64() - x0;  // (net split: the |g|^2 hand-off)
+      if (a.prof && tid == 0) sprof[16] += clock64() - x0;  // (net split: the |g|^2 hand-off)
     }
+    // (stamps straight into LDS: no live registers; not in the full-register-file builds)
+    constexpr bool kProfAdam = KW <= 8;
+    if (kProfAdam && a.prof && tid == 0) sprof[17] -= clock64();
     const float coef = fminf(1.f, a.max_grad_norm / (sqrtf(tot) + 1e-6f));
     step += 1.f;
     b1t *= a.beta1;
@@ -1322,9 +1462,13 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         else L[paddr[it] + j * pstr[it]] = nv;
       }
       if constexpr (BF3) {  // the split-bf16 images of the updated elements (padding stays 0)
-        const int desc = rfl(g.items[wb + w + it * kWaves]);
-        const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-        bf3_store_tile<KT>(L, g, iq, il, ta, tb, r16, kk, iq == 0 ? a.n_pi : a.n_vf, wmst[it]);
+        if constexpr (HOIST) {
+          bf3_store_tile<KT>(L, bpk[it] & 3, bwf[it], (bpk[it] >> 2) & 0x7fff, bwt[it], bpk[it] >> 17, r16, kk, wmst[it]);
+        } else {
+          int kd, wf, wl, wt, tl;
+          slot_img(it, kd, wf, wl, wt, tl);
+          bf3_store_tile<KT>(L, kd, wf, wl, wt, tl, r16, kk, wmst[it]);
+        }
       }
     }
 #pragma unroll
@@ -1336,12 +1480,18 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       const float denom = __builtin_amdgcn_sqrtf(bv[ib]) * inv_bc2s + eps;
       L[b_addr[ib]] = bval[ib] - step_size * bm[ib] * __builtin_amdgcn_rcpf(denom);
     }
+    if (kProfAdam && a.prof && tid == 0) {
+      const unsigned long long a1 = clock64();
+      sprof[17] += a1;
+      sprof[18] -= a1;
+    }
     __syncthreads();  // B3: parameters updated
     if (a.prof && tid == 0) {
       const unsigned long long t3 = clock64();
       sprof[0] += t1 - t0;
       sprof[1] += t2 - t1;
       sprof[2] += t3 - t2;
+      if (kProfAdam) sprof[18] += t3;
     }
   }
 
@@ -1417,7 +1567,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   if (shared_wb && tid == 0) a.adam_step[0] = step;
   // (stats barrier above orders the LDS). Net split: the critic workgroup owns the critic
   // row-tile counters [7..10] (the actor's are zero there), added atomically
-  if (a.prof && tid < 16) {
+  if (a.prof && tid < 20) {
     const bool critic_slot = tid >= 7 && tid <= 10;
     if (!ns) a.prof[tid] += sprof[tid];
     else if (q == 0 && !critic_slot) a.prof[tid] += sprof[tid];

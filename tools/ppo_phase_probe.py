@@ -36,7 +36,7 @@ def main():
         tr._rollout()
     th.cuda.synchronize()
     print(f"rollout {1e3 * (time.perf_counter() - t0) / n:.3f} ms (unchanged kernel: box-speed reference)", flush=True)
-    prof = th.zeros(16, dtype=th.int64, device="cuda")
+    prof = th.zeros(20, dtype=th.int64, device="cuda")
     tr._ppo_static["prof"] = prof
     tr._ppo_update()
     th.cuda.synchronize()

@@ -96,7 +96,7 @@ def main():
         os.environ.pop("IMITATION_AMD_PPO_XCHG2")
         for mode in ("0", "1"):
             os.environ["IMITATION_AMD_PPO_XCHG2"] = mode
-            prof = th.zeros(16, dtype=th.int64, device="cuda")
+            prof = th.zeros(20, dtype=th.int64, device="cuda")
             tr._ppo_static["prof"] = prof
             tr._ppo_update()
             th.cuda.synchronize()
@@ -104,7 +104,7 @@ def main():
             print(f"    xchg2={mode} cycles/minibatch (workgroup 0): chunk {p[0]:.0f} exchange+|g|^2 {p[1]:.0f} clip+adam {p[2]:.0f}"
                   f" | wave0 B1 wait {p[11]:.0f} dW {p[12]:.0f} | exchange: publish {p[13]:.0f} arrival {p[14]:.0f} loads {p[15]:.0f}"
                   f" | actor rows {p[3]:.0f} fwd {p[4]:.0f} loss {p[5]:.0f} bwd {p[6]:.0f} | critic rows {p[7]:.0f} fwd {p[8]:.0f}"
-                  f" loss {p[9]:.0f} bwd {p[10]:.0f}", flush=True)
+                  f" loss {p[9]:.0f} bwd {p[10]:.0f} | net-split |g|^2 hand-off {p[16]:.0f} adam {p[17]:.0f} B3 {p[18]:.0f}", flush=True)
             tr._ppo_static.pop("prof")
         os.environ.pop("IMITATION_AMD_PPO_XCHG2")
 
