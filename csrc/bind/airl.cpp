@@ -218,6 +218,41 @@ class AirlDiscPlan {
     }
     IA_HIP_CHECK_A(ia::disc_adam(a, ia_stream()));
   }
+  // Split update (single rank): stage(i) runs update i's gathers and norm merges -- the only
+  // part of an update that touches the running norms, none of it depends on the disc weights --
+  // into per-(update, minibatch) workspaces; apply(i) then runs the fwd/bwd passes and the Adam
+  // step from them. All stages of a round followed by all applies are the same launches on the
+  // same data as update() x n (bitwise), but the policy norm (q, merged as a side effect of the
+  // log pi pass, as the reference's training-mode evaluate_actions does) is final after the
+  // stages: the next rollout's step chain can run concurrently with the applies.
+  void stage(int slot, torch::Tensor e_idx, torch::Tensor g_idx, bool merge_b, bool merge_p, bool merge_q) {
+    TORCH_CHECK(slot >= 0 && slot < n_slots_, "stage: slot ", slot, " outside the reserved ", n_slots_);
+    for (int k = 0; k < n_mb_; ++k) {
+      ia::AirlDiscArgs a = slot_args(slot, k);
+      check_idx(e_idx);
+      check_idx(g_idx);
+      a.e_idx = e_idx.data_ptr<int64_t>();
+      a.g_idx = g_idx.data_ptr<int64_t>();
+      IA_HIP_CHECK_A(ia::airl_gather(a, k, ia_stream()));
+      a.merge_b = merge_b;
+      a.merge_p = merge_p;
+      a.merge_q = merge_q;
+      IA_HIP_CHECK_A(ia::airl_norm(a, 0, 0, ia_stream()));
+    }
+  }
+  // stage / apply workspaces for n updates per round (grow only when no apply is pending)
+  void reserve(int n) {
+    if (n <= n_slots_) return;
+    auto opts = torch::TensorOptions().dtype(torch::kFloat32).device(held_.front().device());
+    slots_ = torch::zeros({(int64_t)n * n_mb_ * slot_floats()}, opts);
+    n_slots_ = n;
+  }
+  void apply(int slot, double step_size, double bc2_sqrt, c10::optional<torch::Tensor> stats_out) {
+    TORCH_CHECK(slot >= 0 && slot < n_slots_, "apply: slot ", slot, " was not staged");
+    for (int k = 0; k < n_mb_; ++k) IA_HIP_CHECK_A(ia::airl_fwd_bwd(slot_args(slot, k), plan_, k, ia_stream()));
+    adam(1, 1, step_size, bc2_sqrt, stats_out);
+  }
+
   // whole single-rank update: 3 launches per minibatch + Adam
   void update(torch::Tensor e_idx, torch::Tensor g_idx, double step_size, double bc2_sqrt, bool merge_b, bool merge_p,
               bool merge_q, c10::optional<torch::Tensor> stats_out) {
@@ -234,7 +269,29 @@ class AirlDiscPlan {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kInt64 && t.numel() >= B_,
                 "indices must be int64 GPU tensors of >= batch entries");
   }
+  // per-(slot, minibatch) copies of the gathered rows (Xb, S, S2, Act, Done) and of the
+  // normaliser rows (nrm) for stage / apply; grown on demand
+  int64_t slot_floats() const {
+    const int64_t n = 2 * mb_;
+    const int64_t f = n * (a_.din_b + 2 * a_.D + a_.aw_pi + 1) + 4 * 256;
+    return (f + 63) & ~int64_t(63);
+  }
+
+  ia::AirlDiscArgs slot_args(int slot, int k) const {
+    ia::AirlDiscArgs a = a_;
+    const int64_t n = 2 * mb_;
+    float* base = slots_.data_ptr<float>() + ((int64_t)slot * n_mb_ + k) * slot_floats();
+    a.Xb = base;
+    a.S = a.Xb + n * a_.din_b;
+    a.S2 = a.S + n * a_.D;
+    a.Act = a.S2 + n * a_.D;
+    a.Done = a.Act + n * a_.aw_pi;
+    a.nrm = a.Done + n;
+    return a;
+  }
   std::vector<torch::Tensor> held_;
+  torch::Tensor slots_;
+  int n_slots_ = 0;
   torch::Tensor prof_;
   ia::AirlDiscArgs a_{};
   ia::AirlPlan plan_{};
@@ -261,6 +318,11 @@ void register_airl(py::module& m) {
            py::arg("merge_q"))
       .def("fwd_bwd", &AirlDiscPlan::fwd_bwd)
       .def("adam", &AirlDiscPlan::adam, py::arg("reduce"), py::arg("do_adam"), py::arg("step_size"), py::arg("bc2_sqrt"),
+           py::arg("stats_out") = py::none())
+      .def("reserve", &AirlDiscPlan::reserve)
+      .def("stage", &AirlDiscPlan::stage, py::arg("slot"), py::arg("e_idx"), py::arg("g_idx"), py::arg("merge_b"),
+           py::arg("merge_p"), py::arg("merge_q"))
+      .def("apply", &AirlDiscPlan::apply, py::arg("slot"), py::arg("step_size"), py::arg("bc2_sqrt"),
            py::arg("stats_out") = py::none())
       .def("update", &AirlDiscPlan::update, py::arg("e_idx"), py::arg("g_idx"), py::arg("step_size"), py::arg("bc2_sqrt"),
            py::arg("merge_b"), py::arg("merge_p"), py::arg("merge_q"), py::arg("stats_out") = py::none());

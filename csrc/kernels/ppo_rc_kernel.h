@@ -124,7 +124,14 @@ __device__ __forceinline__ void wait_vm8(f4 (&v)[8]) {
 }
 template <int N>
 __device__ __forceinline__ void wait_vm_n(f4 (&v)[N]) {
-  if constexpr (N == 16) {
+  if constexpr (N == 32) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]),
+                   "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])::"memory");
+    asm volatile(""
+                 : "+v"(v[16]), "+v"(v[17]), "+v"(v[18]), "+v"(v[19]), "+v"(v[20]), "+v"(v[21]), "+v"(v[22]), "+v"(v[23]),
+                   "+v"(v[24]), "+v"(v[25]), "+v"(v[26]), "+v"(v[27]), "+v"(v[28]), "+v"(v[29]), "+v"(v[30]), "+v"(v[31])::"memory");
+  } else if constexpr (N == 16) {
     asm volatile("s_waitcnt vmcnt(0)"
                  : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]),
                    "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])::"memory");
@@ -193,13 +200,13 @@ __device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int ro
 // flight per lane and ONE wait per batch of IB = 8 / G items (a load round trip is ~1.2K
 // cycles; a wait per item and 4 groups made the loads the exchange's dominant cost).
 // ids[s]: item id of owned slot s (-1: empty slot).
-template <int GT, int KI>
+template <int GT, int KI, int NF = 16>
 __device__ __forceinline__ void exchange_sum(const float* slab, int n_items, const int (&ids)[KI], int lane, f4 (&xg)[KI]) {
-  constexpr int IB0 = 16 / GT;
+  constexpr int IB0 = NF / GT;
   constexpr int IB = IB0 < KI ? IB0 : KI;
 #pragma unroll
   for (int i0 = 0; i0 < KI; i0 += IB) {
-    f4 v[16];
+    f4 v[NF];
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int it = i0 + i;
@@ -208,8 +215,8 @@ __device__ __forceinline__ void exchange_sum(const float* slab, int n_items, con
       for (int gi = 0; gi < GT; ++gi) v[i * GT + gi] = ld_sc1_x4(slab + ((size_t)gi * n_items + id) * 256 + lane * 4);
     }
 #pragma unroll
-    for (int e = IB * GT; e < 16; ++e) v[e] = v[0];
-    wait_vm_n<16>(v);
+    for (int e = IB * GT; e < NF; ++e) v[e] = v[0];
+    wait_vm_n<NF>(v);
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int it = i0 + i;
@@ -711,10 +718,11 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   // normalised while this workgroup waits for its partners (arrival / |g|^2 hand-off): its
   // rows are in cur since the last chunk, its normaliser buffer was merged after this
   // minibatch's B1, and every dW read of the layer-0 image is behind the barrier before it
-  // (32-wide builds: measured slower for the 64-wide ones, whose owned state then moves to
-  // AGPRs around Adam; and the 12 / 14-slot builds' register file is full)
-  constexpr bool PREC = KT == 2 && KW <= 8;
-  const bool pre = PREC && (ns || G > 1);
+  // (not the 12 / 14-slot builds: their register file is full; not with the G > 16 partial
+  // stash, which borrows the activation images -- the layer-0 input image included -- during
+  // the exchange)
+  constexpr bool PREC = KW <= 8;
+  const bool pre = PREC && (ns || G > 1) && g.xstash < 0;
   float xpre[PREC ? S0M : 1];
 #pragma unroll
   for (int s = 0; s < (PREC ? S0M : 1); ++s) xpre[s] = 0.f;
@@ -1192,6 +1200,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         xg[KW + ib] = {bg[ib], 0.f, 0.f, 0.f};
       }
       float* slab = g.slab + (size_t)(k & 1) * G * n_items * 256;
+      // (one-level at G = 8: the 32-wide 4-wave builds keep all of a wave's 8 x KI partials
+      // -- 32 loads -- in flight behind ONE wait; their spare AGPRs hold the rest of the state)
+      constexpr int XNF = (KT == 2 && NW == 4 && KI <= 4) ? 32 : 16;
 #pragma unroll
       for (int it = 0; it < KI; ++it) {
         if (ids[it] < 0) continue;
@@ -1315,7 +1326,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       } else if (G == 4) {
         exchange_sum<4, KI>(slab, n_items, ids, lane, xg);
       } else if (G == 8) {
-        exchange_sum<8, KI>(slab, n_items, ids, lane, xg);
+        exchange_sum<8, KI, XNF>(slab, n_items, ids, lane, xg);
       } else {
 #pragma unroll
         for (int it = 0; it < KI; ++it) {

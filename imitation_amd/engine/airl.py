@@ -28,7 +28,8 @@ cooperating-workgroup register-chained kernel.
 
 from __future__ import annotations
 
-from typing import Any, Dict, Tuple
+import os
+from typing import Any, Dict, List, Tuple
 
 import torch as th
 from numpy import prod as np_prod
@@ -188,12 +189,11 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         # log pi needs the post-PPO policy: the updates follow PPO on the main stream, but the round
         # is pipelined like GAIL's (_overlapped_round: PPO stats copied async, the updates and the
         # next rollout enqueued before the host reads anything); IMITATION_AMD_DISC_OVERLAP=0: serial
-        import os
-
         self._overlap_disc = os.environ.get("IMITATION_AMD_DISC_OVERLAP", "1") != "0"
         self._disc_on_main = True
         self._side_stream = th.cuda.Stream(device=self._dev) if self._overlap_disc else None  # staging copies
         self._pol_defer_buf = None
+        self._disc_split = False
         if not ok:
             return
         dev = self._dev
@@ -252,6 +252,50 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
                  **norm_args("b", bnorm), **norm_args("p", pnorm), **norm_args("q", qnorm), **self._disc_ws)
         self._disc_plan = self._C.AirlDiscPlan(d)
         self._disc_stats_host = th.zeros(max(1, self.n_disc_updates_per_round), 8, pin_memory=True)
+        # split rounds (single rank): the updates' gathers + norm merges are staged on the main
+        # stream right after PPO, then the next rollout's step chain runs concurrently with the
+        # fwd/bwd + Adam applies on the side stream (see _overlapped_round)
+        self._disc_split = (self._overlap_disc and pdist.world_size() == 1
+                            and os.environ.get("IMITATION_AMD_AIRL_SPLIT", "1") != "0")
+        if self._disc_split:
+            self._disc_plan.reserve(max(1, self.n_disc_updates_per_round))
+
+    def _stage_disc_updates(self, n: int) -> List[Tuple[float, float]]:
+        """The gathers and RunningNorm merges (policy, base, potential) of the round's ``n``
+        updates, in update order (``AirlDiscPlan.stage``): everything of an update that the
+        norms see, none of it dependent on the discriminator weights. Returns each update's
+        Adam (step_size, sqrt(1 - beta2^t))."""
+        if self._gen_dev.size() == 0:
+            raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
+        # (grows only here: the previous round's applies were waited for on the host)
+        self._disc_plan.reserve(max(1, n))
+        opt = self._disc_opt
+        self._adopt_disc_opt_state()
+        g = opt.param_groups[0]
+        beta1, beta2 = g["betas"]
+        t0 = float(opt.state[self._rflat.params[0]]["step"])
+        B = self.demo_batch_size
+        merge_b = self._bnorm is not None and self._bnorm.training
+        merge_p = self._pnorm is not None and self._pnorm.training
+        merge_q = self.pol_norm is not None and self.pol_norm.training
+        scal = []
+        for i in range(n):
+            e_idx = self._endless_expert_iterator.next_indices()
+            g_idx = th.randint(0, self._gen_dev.size(), (B,), device=self._dev)
+            self._disc_plan.stage(i, e_idx, g_idx, merge_b, merge_p, merge_q)
+            t = t0 + i + 1.0
+            scal.append((float(g["lr"]) / (1.0 - beta1**t), (1.0 - beta2**t) ** 0.5))
+        return scal
+
+    def _apply_disc_updates(self, scal: List[Tuple[float, float]], steps: List[int]) -> None:
+        """The fwd/bwd passes and Adam steps of the staged updates (``AirlDiscPlan.apply``)."""
+        opt = self._disc_opt
+        for i, (step_size, bc2_sqrt) in enumerate(scal):
+            self._disc_plan.apply(i, step_size, bc2_sqrt, self._disc_stats[i])
+            for p in self._rflat.params:
+                opt.state[p]["step"] += 1
+            self._disc_step += 1
+            steps.append(self._disc_step)
 
     def _fused_disc_update(self, slot: int, defer_pol: bool = False, e_idx: th.Tensor = None, g_idx: th.Tensor = None,
                            apply: bool = True) -> None:

@@ -1033,6 +1033,12 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             self._ppo_stats_host = th.zeros(self.stats.numel(), pin_memory=True)
         steps: List[int] = []
         nxt = None
+        # AIRL split rounds: the updates' gathers + norm merges (the only part the next rollout's
+        # step chain depends on, through the policy RunningNorm) are staged on the main stream;
+        # the fwd/bwd + Adam applies run on the side stream concurrently with that chain, and
+        # the rollout's reward pass waits for them
+        # (single rank only; the policy-norm merges are on the main stream, ahead of the chain)
+        split = getattr(self, "_disc_split", False) and n > 0
         with self.logger.accumulate_means("gen"):
             if algo._total_timesteps < algo.num_timesteps + self.T * self.N:
                 algo._total_timesteps = algo.num_timesteps + self.T * self.N
@@ -1044,6 +1050,8 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             ppo_done = th.cuda.Event()
             ppo_done.record(main)
             ready.synchronize()
+            if split:
+                return self._split_round(n, ppo_done, launch_next, steps)
             if serial:
                 side.wait_stream(main)
             else:
@@ -1065,6 +1073,41 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 nxt = self._launch_rollout()
             ppo_done.synchronize()
             self._log_gen(self._ppo_stats_host)
+        disc_done.synchronize()
+        return steps, nxt
+
+    def _split_round(self, n: int, ppo_done: th.cuda.Event, launch_next: bool,
+                     steps: List[int]) -> Tuple[List[int], Optional[th.cuda.Event]]:
+        """Rest of an AIRL split round after PPO (see _overlapped_round): stage the updates on
+        the main stream, apply them on the side stream while the next rollout's step chain runs,
+        then the rollout's reward pass behind the applies."""
+        main = th.cuda.current_stream(self._dev)
+        side = self._side_stream
+        self._store_generator_samples()
+        with networks.training(self.reward_train):
+            scal = self._stage_disc_updates(n)
+        staged = th.cuda.Event()
+        staged.record(main)
+        side.wait_event(staged)
+        with th.cuda.stream(side):
+            self._apply_disc_updates(scal, steps)
+            self._disc_stats_host[:n].copy_(self._disc_stats[:n], non_blocking=True)
+            disc_done = th.cuda.Event()
+            disc_done.record(side)
+        self._global_step += 1
+        nxt = None
+        if launch_next:
+            self._launch_chain()
+            main.wait_event(disc_done)
+            reward = not self.debug_use_ground_truth
+            self._launch_post(reward)
+            if reward:
+                self._post_rollout_rewards()
+            nxt = self._stage_rollout_to_host()
+        else:
+            main.wait_event(disc_done)
+        ppo_done.synchronize()
+        self._log_gen(self._ppo_stats_host)
         disc_done.synchronize()
         return steps, nxt
 

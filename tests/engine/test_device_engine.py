@@ -203,6 +203,50 @@ def test_ppo_kernel_matches_torch_reference(env_id, allow_rc, batch, gmax, net_a
 
 
 @gpu
+@pytest.mark.parametrize("env_id,batch,n_envs,n_steps,net_arch,path", [
+    # 32-wide GAIL plan at 8 cooperating row groups (the emulated W=8 minibatch)
+    ("seals/HalfCheetah-v1", 512, 16, 64, None, "rc:g8x1x64:kt2:ns"),
+    # 64-wide plans past 16 groups: the first exchange level goes through the LDS partial
+    # stash, which borrows the activation images
+    ("seals/Hopper-v1", 2048, 32, 64, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g32x1x64:kt4:ns"),
+    ("seals/Hopper-v1", 4096, 64, 64, dict(pi=[64, 64], vf=[64, 64], act="relu"), "rc:g64x1x64:kt4:ns"),
+])
+def test_ppo_exchange_levels_are_bitwise_equal(env_id, batch, n_envs, n_steps, net_arch, path, monkeypatch):
+    """The one-level (every workgroup sums all G partials) and two-level (reduce-then-share,
+    with the LDS stash past 16 groups) partial exchanges add the same numbers in the same group
+    order: the updates must be bitwise equal (a clobbered image or a mis-ordered sum breaks it)."""
+    act = None
+    if net_arch is not None:
+        if net_arch.get("act") == "relu":
+            act = th.nn.ReLU
+        net_arch = {k: v for k, v in net_arch.items() if k != "act"}
+    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=n_envs, n_steps=n_steps, batch=batch, n_epochs=2,
+                               net_arch=net_arch, activation=act)
+    assert tr._C.engine_ppo_path(tr._ppo_static) == path
+    tr._rollout()
+    pol = gen.policy
+    norm = tr.pol_norm
+    dst = list(pol.parameters()) + [tr.exp_avg, tr.exp_avg_sq, tr.adam_step]
+    if norm is not None:
+        dst += [norm.running_mean, norm.running_var, norm.count, tr.norm_count]
+    s0 = [t.detach().clone() for t in dst]
+    pr = tr._perm_round
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IMITATION_AMD_PPO_XCHG2", mode)
+        with th.no_grad():
+            for d, v in zip(dst, s0):
+                d.copy_(v)
+        tr._perm_round = pr
+        tr._ppo_update()
+        th.cuda.synchronize()
+        res[mode] = [t.detach().clone() for t in dst]
+    for a, b in zip(res["0"], res["1"]):
+        assert th.equal(a, b)
+    tr.check_errors(blocking=True)
+
+
+@gpu
 def test_device_gail_rounds_run_and_learn_something():
     tr, venv, gen, rn = _setup(n_envs=8, n_steps=64, batch=64, n_epochs=2)
     before = [p.detach().clone() for p in gen.policy.parameters()]
@@ -645,13 +689,17 @@ def test_airl_pipelined_rounds_are_bitwise_the_serial_order(monkeypatch):
     """AIRL rounds pipelined on the main stream (engine/gail.py ``_overlapped_round`` with
     ``_disc_on_main``: PPO statistics copied asynchronously, the discriminator updates and the next
     rollout enqueued before the host reads anything) give bit-identical parameters, Adam moments
-    and normalisers to the serial loop (IMITATION_AMD_DISC_OVERLAP=0)."""
+    and normalisers to the serial loop (IMITATION_AMD_DISC_OVERLAP=0) -- also as split rounds
+    (the updates' gathers + norm merges staged on the main stream, their fwd/bwd + Adam applied
+    on the side stream concurrently with the next rollout's step chain)."""
     runs = []
-    for mode in ("0", "1"):
+    for mode, split in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("IMITATION_AMD_DISC_OVERLAP", mode)
+        monkeypatch.setenv("IMITATION_AMD_AIRL_SPLIT", split)
         tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=3)
         assert tr._fused_disc, tr._fused_disc_why
         assert tr._overlap_disc == (mode == "1")
+        assert tr._disc_split == (split == "1")
         tr.n_disc_updates_per_round = 3
         tr.train(3 * tr.gen_train_timesteps)
         th.cuda.synchronize()
@@ -660,5 +708,6 @@ def test_airl_pipelined_rounds_are_bitwise_the_serial_order(monkeypatch):
         vals += [n.running_mean.cpu().clone() for n in _airl_state(tr, rn)]
         runs.append(vals)
         assert tr._disc_step == 9
-    bad = [i for i, (a, b) in enumerate(zip(*runs)) if not th.equal(a, b)]
-    assert not bad, bad
+    for other in runs[1:]:
+        bad = [i for i, (a, b) in enumerate(zip(runs[0], other)) if not th.equal(a, b)]
+        assert not bad, bad

@@ -18,3 +18,5 @@ IMITATION_AMD_PPO_LDS_EXCL=1 timeout -k 10 300 python bench.py > gpurun_out/r4q_
 tail -1 gpurun_out/r4q_bench_excl.log
 timeout -k 10 300 python bench.py > gpurun_out/r4q_bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/r4q_bench.log; exit 1; }
 tail -1 gpurun_out/r4q_bench.log
+timeout -k 10 200 python -u tools/wlin_roofline.py > gpurun_out/r4q_wlin.md 2> gpurun_out/r4q_wlin.err || { echo "wlin roofline failed"; tail -20 gpurun_out/r4q_wlin.err; exit 1; }
+cat gpurun_out/r4q_wlin.md
