@@ -130,8 +130,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
-            # rollout + PPO run exact fp32 (MFMA f32), the discriminator bf16 MFMA operands
-            "dtype": "mixed (fp32 policy/PPO, bf16 discriminator)",
+            # fp32 master weights / accumulation; PPO MFMA products split-bf16 x3, discriminator bf16 operands
+            "dtype": "mixed (fp32 master weights and accumulation; PPO products as split-bf16 x3 ~fp32, discriminator bf16)",
             "final_eval_return": eval_return,
             "per_rank_ms_per_step": per_rank,
             "data": "synthetic (native HalfCheetah-v4-shaped env, random-policy demos, random-init nets)",

@@ -168,6 +168,60 @@ def test_traj_collector_beta_extremes(tmp_path, pendulum_venv, beta):
         np.testing.assert_allclose(serialize.load(f)[0].acts, 0.5)
 
 
+def test_traj_collector(tmp_path, pendulum_venv):
+    """beta = 0.5 mixing (reference test_traj_collector): the robot is asked for about half of
+    the steps, episodes end every 200 steps and every finished episode is saved with the
+    expert's (here all-zero) actions."""
+    n_env = pendulum_venv.num_envs
+    coll, calls = _collector(tmp_path, pendulum_venv, seed=0, beta=0.5,
+                             robot=lambda o: np.stack([pendulum_venv.action_space.sample() for _ in range(len(o))]))
+    coll.reset()
+    zero = np.zeros((n_env,) + pendulum_venv.action_space.shape, dtype=pendulum_venv.action_space.dtype)
+    obs, rews, dones, infos = coll.step(zero)
+    assert np.all(rews != 0)
+    assert not np.any(dones)
+    assert all(isinstance(i, dict) for i in infos)
+    n_episodes = 0
+    for _ in range(1000):  # 5 episodes per env (Pendulum-v1: 200-step episodes)
+        _, _, dones, _ = coll.step(zero)
+        n_episodes += int(np.sum(dones))
+    # the robot is asked with probability 0.5 per step (< 1e-12 chance to leave this band)
+    assert 388 * n_env <= sum(calls) <= 612 * n_env
+    from imitation_amd.data import serialize
+
+    files = glob.glob(os.path.join(tmp_path, "dagger-demo-*.npz"))
+    assert n_episodes == 5 * n_env
+    assert len(files) == n_episodes
+    assert sum(int(np.sum(serialize.load(f)[0].acts != 0)) for f in files) == 0
+
+
+def test_traj_collector_reproducible(tmp_path, pendulum_venv):
+    """Same seeds -> the same saved file names, each holding the same trajectory (reference
+    test_traj_collector_reproducible)."""
+    from imitation_amd.data import serialize
+
+    runs = []
+    with th.random.fork_rng():
+        for k in range(2):
+            save_dir = tmp_path / f"run{k}"
+            pendulum_venv.seed(12345)
+            pendulum_venv.action_space.seed(12345)
+            coll = dagger.InteractiveTrajectoryCollector(
+                venv=pendulum_venv, get_robot_acts=lambda o: np.stack([pendulum_venv.action_space.sample() for _ in range(len(o))]),
+                beta=0.5, save_dir=save_dir, rng=np.random.default_rng(12345))
+            coll.seed(12345)
+            coll.reset()
+            zero = np.zeros((pendulum_venv.num_envs,) + pendulum_venv.action_space.shape, dtype=pendulum_venv.action_space.dtype)
+            for _ in range(250):
+                coll.step(zero)
+            runs.append({os.path.basename(f): serialize.load(f)[0] for f in glob.glob(os.path.join(save_dir, "*.npz"))})
+    assert runs[0].keys() == runs[1].keys() and len(runs[0]) == pendulum_venv.num_envs
+    for name, t0 in runs[0].items():
+        t1 = runs[1][name]
+        np.testing.assert_array_equal(t0.obs, t1.obs)
+        np.testing.assert_array_equal(t0.acts, t1.acts)
+
+
 def _pendulum_trainer(tmp_path, venv, expert, seed=0, simple=True, batch_size=32):
     th.manual_seed(seed)
     rng = np.random.default_rng(seed)

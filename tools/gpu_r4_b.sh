@@ -8,4 +8,4 @@ for split in 0 1; do
   IMITATION_AMD_AIRL_SPLIT=$split timeout -k 10 400 python -u benchmarking/bench_configs.py --configs airl_hopper --steps 3 --warmup 1 --eval-episodes 2 --out gpurun_out/r4b_airl_s$split.jsonl > gpurun_out/r4b_airl_s$split.log 2>&1 || { echo "airl bench failed"; tail -30 gpurun_out/r4b_airl_s$split.log; exit 1; }
   echo "split=$split"; cut -c1-300 gpurun_out/r4b_airl_s$split.jsonl
 done
-VARIANTS="geo3 geo4" WS=1,8 bash tools/gpu_r4_ab.sh
+VARIANTS="geo4 geo5" WS=1,8 bash tools/gpu_r4_ab.sh
