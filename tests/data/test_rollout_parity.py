@@ -166,3 +166,50 @@ def test_rollout_stats_of_known_returns():
     assert st["return_mean"] == pytest.approx(np.mean([2.0, 2.0, -3.0]))
     assert st["len_mean"] == pytest.approx(3.0)
     assert st["return_min"] == pytest.approx(-3.0) and st["return_max"] == pytest.approx(2.0)
+
+
+class _ImageAlgo:
+    """A stand-in for an algorithm trained on the channel-first (VecTransposeImage) view of an
+    image env: rollout only reads its spaces and calls predict."""
+
+    def __new__(cls, obs_space, act_space):
+        from imitation_amd.rl.base import BaseAlgorithm
+
+        algo = object.__new__(type("ImageAlgo", (BaseAlgorithm,), {
+            "predict": lambda self, obs, state=None, episode_start=None, deterministic=False: (
+                np.zeros(len(obs), dtype=np.int64), None)}))
+        algo.observation_space = obs_space
+        algo.action_space = act_space
+        return algo
+
+
+def test_rollout_verbose_error_for_image_environments():
+    """An algorithm trained on the transposed (C, H, W) view rolled out in the raw (H, W, C) env:
+    the error names the likely fix, ``expert.get_env()`` (reference
+    test_rollout_verbose_error_for_image_environments)."""
+    from imitation_amd.envs import spaces
+    from imitation_amd.util.util import make_vec_env
+
+    env = make_vec_env("PongNoFrameskip-v4", rng=np.random.default_rng(0), n_envs=1)
+    h, w, c = env.observation_space.shape
+    expert = _ImageAlgo(spaces.Box(0, 255, (c, h, w), np.uint8), env.action_space)
+    with pytest.raises(ValueError, match=r".*expert\.get_env().*"):
+        rollout.rollout(expert, env, rollout.make_sample_until(min_timesteps=None, min_episodes=2),
+                        rng=np.random.default_rng(0))
+
+
+def test_rollout_normal_error_for_other_shape_mismatch():
+    """Any other observation-space mismatch keeps the plain space-check error (reference
+    test_rollout_normal_error_for_other_shape_mismatch)."""
+    from imitation_amd.envs import spaces
+    from imitation_amd.util.util import make_vec_env
+
+    img = make_vec_env("PongNoFrameskip-v4", rng=np.random.default_rng(0), n_envs=1)
+    h, w, c = img.observation_space.shape
+    expert = _ImageAlgo(spaces.Box(0, 255, (c, h, w), np.uint8), img.action_space)
+    other_image = _ImageAlgo(spaces.Box(0, 255, (c, h + 1, w), np.uint8), img.action_space)
+    unrelated = make_vec_env("seals/CartPole-v0", rng=np.random.default_rng(0), n_envs=1)
+    for algo, bad_env in ((other_image, img), (expert, unrelated)):
+        with pytest.raises(ValueError, match=r"Observation spaces do not match.*"):
+            rollout.rollout(algo, bad_env, rollout.make_sample_until(min_timesteps=None, min_episodes=2),
+                            rng=np.random.default_rng(0))
