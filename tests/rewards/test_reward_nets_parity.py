@@ -324,3 +324,48 @@ def test_training_regression(normalize_input_layer):
         opt.step()
         losses.append(float(loss))
     assert np.mean(losses[-20:]) < 0.1 * np.mean(losses[:20])
+
+
+DESERIALIZATION_TYPES = ["zero", "RewardNet_normalized", "RewardNet_unnormalized", "RewardNet_shaped", "RewardNet_unshaped"]
+
+
+def _saved_reward(env_name, reward_type, tmp_path, is_image):
+    """A saved reward net of the shape the reward type's loader expects (reference
+    _make_env_and_save_reward_net)."""
+    obs_space, act_space = _spaces(env_name)
+    if is_image:
+        net = reward_nets.CnnRewardNet(obs_space, act_space)
+    else:
+        net = reward_nets.BasicRewardNet(obs_space, act_space)
+    if reward_type == "RewardNet_normalized":
+        net = reward_nets.NormalizedRewardNet(net, networks.RunningNorm)
+    elif reward_type == "RewardNet_shaped":
+        pot_cls = reward_nets.BasicPotentialCNN if is_image else reward_nets.BasicPotentialMLP
+        net = reward_nets.ShapedRewardNet(net, pot_cls(obs_space, [8, 8]), discount_factor=0.99)
+    path = tmp_path / "reward.pt"
+    serialize.save_reward_net(net, path)
+    return obs_space, act_space, path
+
+
+def _assert_reward_valid(env_name, reward_type, tmp_path, is_image):
+    obs_space, act_space, path = _saved_reward(env_name, reward_type, tmp_path, is_image)
+    n = 10
+    obs, acts, next_obs, _ = _batch(obs_space, act_space, n=n)
+    fn = serialize.load_reward(reward_type, str(path), None)
+    rew = fn(obs, acts, next_obs, np.arange(n))
+    assert isinstance(rew, np.ndarray)
+    assert rew.shape == (n,)
+    assert np.issubdtype(rew.dtype, np.number)
+
+
+@pytest.mark.parametrize("env_name", ENVS)
+@pytest.mark.parametrize("reward_type", DESERIALIZATION_TYPES)
+def test_reward_valid(env_name, reward_type, tmp_path):
+    """Every registered reward loader returns a numeric [n] array (reference test_reward_valid)."""
+    _assert_reward_valid(env_name, reward_type, tmp_path, is_image=False)
+
+
+@pytest.mark.parametrize("env_name", IMAGE_ENVS)
+@pytest.mark.parametrize("reward_type", DESERIALIZATION_TYPES)
+def test_reward_valid_image(env_name, reward_type, tmp_path):
+    _assert_reward_valid(env_name, reward_type, tmp_path, is_image=True)
