@@ -88,6 +88,12 @@ def parallel(sacred_ex_name: str, run_name: str, num_samples: int, search_space:
     samples = tune.generate_trials(search_space, int(num_samples), rng)
     trials = []
     for s in samples:
+        # (checked per sampled trial, as the reference's trainable does: search-space values
+        # may be samplers that only resolve here)
+        if not isinstance(s.get("named_configs", []), collections.abc.Sequence):
+            raise TypeError("search_space['named_configs'] must resolve to a Sequence")
+        if not isinstance(s.get("config_updates", {}), collections.abc.Mapping):
+            raise TypeError("search_space['config_updates'] must resolve to a Mapping")
         for rep in range(int(repeat)):
             updates = recursive_update(copy.deepcopy(dict(base_config_updates)), s.get("config_updates") or {})
             if repeat > 1:

@@ -175,3 +175,65 @@ def test_analyze_gather_tb(tmp_path):
     assert res["n_tb_dirs"] >= 1
     out = pathlib.Path(res["gather_dir"])
     assert out.is_dir() and any(out.rglob("*"))
+
+
+SCRIPT_MODS = ["analyze", "eval_policy", "parallel", "train_adversarial", "train_imitation",
+               "train_preference_comparisons", "train_rl", "tuning"]
+
+
+@pytest.mark.parametrize("mod_name", SCRIPT_MODS)
+def test_main_console(mod_name, monkeypatch):
+    """Every script's console entry point runs (print_config) -- reference test_main_console."""
+    import importlib
+    import sys
+
+    mod = importlib.import_module(f"imitation_amd.scripts.{mod_name}")
+    monkeypatch.setattr(sys, "argv", ["sacred-pytest-stub", "print_config"])
+    mod.main_console()
+
+
+def test_train_bc_main_with_none_demonstrations_raises_value_error(tmp_path):
+    from imitation_amd.scripts.train_imitation import train_imitation_ex
+
+    with pytest.raises(ValueError, match="n_expert_demos must be specified"):
+        train_imitation_ex.run("bc", named_configs=["fast", "demonstrations.fast", *FAST_ENV],
+                               config_updates=_updates(tmp_path, demonstrations={"n_expert_demos": None}))
+
+
+def test_train_dagger_warmstart(tmp_path):
+    """A DAgger run warm-started from the previous run's latest scratch policy (reference
+    test_train_dagger_warmstart)."""
+    from imitation_amd.scripts.train_imitation import train_imitation_ex
+
+    run = train_imitation_ex.run("dagger", named_configs=["fast", "demonstrations.fast", *FAST_ENV],
+                                 config_updates=_updates(tmp_path))
+    assert run.status == "COMPLETED"
+    policy_path = pathlib.Path(run.config["logging"]["log_dir"]) / "scratch" / "policy-latest.pt"
+    assert policy_path.exists()
+    warm = train_imitation_ex.run("dagger", named_configs=["fast", "demonstrations.fast", *FAST_ENV],
+                                  config_updates=_updates(tmp_path, bc={"agent_path": str(policy_path)}))
+    assert warm.status == "COMPLETED" and isinstance(warm.result, dict)
+
+
+@pytest.mark.parametrize("named_configs", [[], ["reward.normalize_output_running"], ["reward.normalize_output_disable"]])
+def test_train_preference_comparisons_reward_named_config(tmp_path, named_configs):
+    from imitation_amd.scripts.train_preference_comparisons import train_preference_comparisons_ex
+    from imitation_amd.util import networks
+
+    run = train_preference_comparisons_ex.run(named_configs=["fast", "rl.fast", *FAST_ENV, *named_configs],
+                                              config_updates=_updates(tmp_path))
+    expect = None if "reward.normalize_output_disable" in named_configs else networks.RunningNorm
+    assert run.config["reward"]["normalize_output_layer"] is expect
+    assert run.status == "COMPLETED" and isinstance(run.result, dict)
+
+
+def test_parallel_arg_errors(tmp_path):
+    """Bad base / search-space argument types raise (reference test_parallel_arg_errors)."""
+    from imitation_amd.scripts.parallel import parallel_ex
+
+    base = {"base_config_updates": _updates(tmp_path), "local_dir": str(tmp_path / "par")}
+    cases = [({"base_named_configs": {}}, "Sequence"), ({"base_config_updates": ()}, "Mapping"),
+             ({"search_space": {"named_configs": {}}}, "Sequence"), ({"search_space": {"config_updates": ()}}, "Mapping")]
+    for upd, match in cases:
+        with pytest.raises(TypeError, match=match):
+            parallel_ex.run(named_configs=["generate_test_data"], config_updates={**base, **upd})
