@@ -183,3 +183,42 @@ def test_build_mlp_trains_on_a_toy_task(kw):
 def test_build_mlp_rejects_an_invalid_normalization_layer():
     with pytest.raises(ValueError, match="not a valid normalization layer"):
         networks.build_mlp(in_size=1, hid_sizes=[16, 16], out_size=1, normalize_input_layer=th.nn.Module)
+
+
+class _IncrementalEMA(networks.EMANorm):
+    """Oracle: the incremental batch EMA / EMV update ("algorithm 2" of the note the reference's
+    EMANorm cites) -- weight lr_t = 1 / sum_{s <= t} decay^s, mean += lr_t (batch mean - mean),
+    var = (1 - lr_t) var + lr_t E[(x - old mean)^2] - (mean step)^2. EMANorm itself implements the
+    closed form ("algorithm 3"); the two must agree (reference
+    test_ema_norm_algo_2_and_3_are_the_same)."""
+
+    def update_stats(self, batch: th.Tensor) -> None:
+        x = batch.reshape(batch.shape[0], -1) if batch.dim() > 1 else batch.reshape(-1, 1)
+        n = x.shape[0]
+        self.inv_learning_rate += self.decay ** self.num_batches
+        lr = 1.0 / self.inv_learning_rate
+        if int(self.count) == 0:
+            self.running_mean = x.mean(0)
+            self.running_var = x.var(0, unbiased=False) if n > 1 else th.zeros_like(self.running_mean)
+        else:
+            sq = ((x - self.running_mean) ** 2).mean(0)
+            step = lr * (x.mean(0) - self.running_mean)
+            self.running_mean = self.running_mean + step
+            self.running_var = (1 - lr) * self.running_var + lr * sq - step ** 2
+        self.count += n
+        self.num_batches += 1
+
+
+@pytest.mark.parametrize("decay", [0.5, 0.99])
+@pytest.mark.parametrize("input_shape", [(64,), (1, 256), (64, 256)])
+def test_ema_norm_incremental_and_closed_form_agree(decay, input_shape):
+    feats = input_shape[-1] if len(input_shape) == 2 else 1
+    inc, ema = _IncrementalEMA(feats, decay=decay), networks.EMANorm(feats, decay)
+    base = th.randn(input_shape)
+    for i in range(1000):
+        inc.train(), ema.train()
+        inc(base.clone() + i)  # a moving distribution
+        ema(base.clone() + i)
+        inc.eval(), ema.eval()
+        th.testing.assert_close(inc.running_mean, ema.running_mean, rtol=0.05, atol=0.1)
+        th.testing.assert_close(inc.running_var, ema.running_var, rtol=0.05, atol=0.1)
