@@ -320,3 +320,49 @@ def test_multibc_device_agent_gather_matches_cat_of_overrides():
         want_o = th.cat([obs_over(i, o_all) for i in range(n_agents)])
         want_a = th.cat([act_over(i, a_all) for i in range(n_agents)])
         assert th.equal(got["obs"].cpu(), want_o) and th.equal(got["acts"].cpu(), want_a)
+
+
+def test_weight_decay_in_optimizer_raises(cartpole_venv, rng):
+    """weight_decay belongs in l2_weight (reference test_that_weight_decay_in_optimizer_raises_error)."""
+    with pytest.raises(ValueError, match=".*weight_decay.*"):
+        bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+              demonstrations=None, optimizer_kwargs=dict(weight_decay=1e-4), rng=rng, device="cpu")
+
+
+@pytest.mark.parametrize("duration_args", [dict(n_epochs=1, n_batches=10), dict(), dict(n_epochs=None, n_batches=None)])
+def test_wrong_training_duration_raises(cartpole_venv, expert_transitions, rng, duration_args):
+    tr = bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+               demonstrations=expert_transitions, rng=rng, device="cpu")
+    with pytest.raises(ValueError, match="exactly one.*n_epochs"):
+        tr.train(**duration_args)
+
+
+@pytest.mark.parametrize("no_yield_after_iter", [1, 2, 6])
+def test_bc_raises_when_the_data_loader_runs_dry(cartpole_venv, expert_transitions, rng, no_yield_after_iter):
+    """A loader that stops yielding makes train() fail instead of looping without updates
+    (reference test_that_bc_raises_error_when_data_loader_is_empty)."""
+    import dataclasses
+
+    tr = bc.BC(observation_space=cartpole_venv.observation_space, action_space=cartpole_venv.action_space,
+               demonstrations=expert_transitions, rng=rng, device="cpu")
+    one_batch = dataclasses.asdict(expert_transitions[: tr.batch_size])
+
+    class _Dries:
+        def __init__(self):
+            self.iters = 0
+
+        def __iter__(self):
+            if self.iters < no_yield_after_iter:
+                yield one_batch
+            self.iters += 1
+
+    n_batches = 0
+
+    def on_batch_end():
+        nonlocal n_batches
+        n_batches += 1
+
+    tr.set_demonstrations(_Dries())
+    with pytest.raises(AssertionError, match=".*no data.*"):
+        tr.train(n_batches=20, on_batch_end=on_batch_end)
+    assert n_batches == no_yield_after_iter
