@@ -596,6 +596,14 @@ def parse_command_line(argv: Sequence[str], commands: Iterable[str]) -> Tuple[Op
         elif a in ("-n", "--name"):
             opts["name"] = args[i + 1]
             i += 1
+        elif a in ("-C", "--capture"):  # Sacred's output-capture mode (accepted; stdout is tee'd anyway)
+            opts["capture"] = args[i + 1]
+            i += 1
+        elif a.startswith("--") and not seen_with:
+            # any other Sacred run option (--name=run0, --capture=sys, --unobserved, ...): an
+            # option, never a config update
+            key, _, val = a[2:].partition("=")
+            opts[key] = val if _ else True
         elif a == "with":
             seen_with = True
         elif command is None and not seen_with and a in commands:
