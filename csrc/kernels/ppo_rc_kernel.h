@@ -1200,9 +1200,6 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         xg[KW + ib] = {bg[ib], 0.f, 0.f, 0.f};
       }
       float* slab = g.slab + (size_t)(k & 1) * G * n_items * 256;
-      // (one-level at G = 8: the 32-wide 4-wave builds keep all of a wave's 8 x KI partials
-      // -- 32 loads -- in flight behind ONE wait; their spare AGPRs hold the rest of the state)
-      constexpr int XNF = (KT == 2 && NW == 4 && KI <= 4) ? 32 : 16;
 #pragma unroll
       for (int it = 0; it < KI; ++it) {
         if (ids[it] < 0) continue;
@@ -1326,7 +1323,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
       } else if (G == 4) {
         exchange_sum<4, KI>(slab, n_items, ids, lane, xg);
       } else if (G == 8) {
-        exchange_sum<8, KI, XNF>(slab, n_items, ids, lane, xg);
+        exchange_sum<8, KI>(slab, n_items, ids, lane, xg);
       } else {
 #pragma unroll
         for (int it = 0; it < KI; ++it) {
