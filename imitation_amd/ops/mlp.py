@@ -247,7 +247,15 @@ class _WideMLPFn(torch.autograd.Function):
             if l > 0:
                 dz = C.wlin_backward_x(dz, ws[l], hs[l], hidden_act, None)
             elif ctx.needs_input_grad[0]:
-                dx = C.wlin_backward_x(dz, ws[0], None, 0, rstd)
+                if ws[0].shape[1] <= 64:
+                    # a narrow input (e.g. SAC's critic input obs + action, 17 -> 1024): the
+                    # output has too few 32-column tiles to fill the device, and with no
+                    # activation derivative to fuse this is a plain GEMM (hipBLASLt / rocBLAS)
+                    dx = dz @ ws[0]
+                    if rstd is not None:
+                        dx = dx * rstd
+                else:
+                    dx = C.wlin_backward_x(dz, ws[0], None, 0, rstd)
         return (dx, None, None, None, None, None, *grads)
 
 
