@@ -10,7 +10,8 @@ cp $SO /tmp/orig.so
 for v in ${VARIANTS:-pre head fix}; do
   cp ab/$v.so $SO
   for c in gail airl drlhp; do
-    CONFIG=$c WS=1 timeout -k 10 200 python -u tools/ppo_scale_probe.py > gpurun_out/ab_${v}_$c.log 2>&1 || { echo "$v $c probe failed"; tail -20 gpurun_out/ab_${v}_$c.log; cp /tmp/orig.so $SO; exit 1; }
+    ws=${WS:-1}; [ $c = drlhp ] && ws=1
+    CONFIG=$c WS=$ws timeout -k 10 200 python -u tools/ppo_scale_probe.py > gpurun_out/ab_${v}_$c.log 2>&1 || { echo "$v $c probe failed"; tail -20 gpurun_out/ab_${v}_$c.log; cp /tmp/orig.so $SO; exit 1; }
     echo "== $v"; grep -v Warn gpurun_out/ab_${v}_$c.log | grep -v amdgpu.ids
   done
   timeout -k 10 200 python -u bench.py > gpurun_out/ab_${v}_bench.log 2>&1 || { echo "$v bench failed"; tail -20 gpurun_out/ab_${v}_bench.log; cp /tmp/orig.so $SO; exit 1; }
