@@ -335,10 +335,10 @@ py::tuple cnn_fc_pair(torch::Tensor x1, torch::Tensor x2, torch::Tensor w1, torc
 }
 
 // Action head + choice (+ beta-mix); see cnn_infer.hip. All outputs are preallocated int64 [B].
-void cnn_head(torch::Tensor h, torch::Tensor w2, torch::Tensor b2, int64_t mode, int64_t seed,
-              c10::optional<torch::Tensor> counter, torch::Tensor out, c10::optional<torch::Tensor> rec_out,
-              c10::optional<torch::Tensor> mix_expert, c10::optional<torch::Tensor> beta,
-              c10::optional<torch::Tensor> exec_out) {
+ia::CnnHeadArgs head_args(torch::Tensor h, torch::Tensor w2, torch::Tensor b2, int64_t mode, int64_t seed,
+                          c10::optional<torch::Tensor> counter, torch::Tensor out, c10::optional<torch::Tensor> rec_out,
+                          c10::optional<torch::Tensor> mix_expert, c10::optional<torch::Tensor> beta,
+                          c10::optional<torch::Tensor> exec_out) {
   IA_CHECK_GPU_F32(h);
   IA_CHECK_GPU_F32(w2);
   IA_CHECK_GPU_F32(b2);
@@ -370,7 +370,28 @@ void cnn_head(torch::Tensor h, torch::Tensor w2, torch::Tensor b2, int64_t mode,
     IA_CHECK_GPU_F32(*beta);
     a.beta = beta->data_ptr<float>();
   }
+  return a;
+}
+
+void cnn_head(torch::Tensor h, torch::Tensor w2, torch::Tensor b2, int64_t mode, int64_t seed,
+              c10::optional<torch::Tensor> counter, torch::Tensor out, c10::optional<torch::Tensor> rec_out,
+              c10::optional<torch::Tensor> mix_expert, c10::optional<torch::Tensor> beta,
+              c10::optional<torch::Tensor> exec_out) {
+  const ia::CnnHeadArgs a = head_args(h, w2, b2, mode, seed, counter, out, rec_out, mix_expert, beta, exec_out);
   IA_HIP_CHECK3(ia::cnn_head(a, ia_stream()));
+}
+
+// DAgger's expert argmax (-> out_e, rec_out_e) and learner Gumbel sample (-> out_l, and
+// exec_out = u > beta ? learner : expert) in one launch: the same results as the two cnn_head
+// calls (expert, then learner with mix_expert = out_e).
+void cnn_head_pair(torch::Tensor h_e, torch::Tensor w_e, torch::Tensor b_e, torch::Tensor out_e,
+                   c10::optional<torch::Tensor> rec_out_e, torch::Tensor h_l, torch::Tensor w_l, torch::Tensor b_l,
+                   int64_t seed, torch::Tensor counter, torch::Tensor out_l, torch::Tensor beta, torch::Tensor exec_out) {
+  const ia::CnnHeadArgs e = head_args(h_e, w_e, b_e, 0, 0, c10::nullopt, out_e, rec_out_e, c10::nullopt, c10::nullopt,
+                                      c10::nullopt);
+  const ia::CnnHeadArgs r = head_args(h_l, w_l, b_l, 1, seed, counter, out_l, c10::nullopt, out_e, beta, exec_out);
+  TORCH_CHECK(e.B == r.B && e.NH == r.NH, "cnn_head_pair: the two heads' batch / hidden sizes differ");
+  IA_HIP_CHECK3(ia::cnn_head_pair(e, r, ia_stream()));
 }
 
 }  // namespace
@@ -380,6 +401,9 @@ void register_conv(py::module& m) {
   m.def("cnn_head", &cnn_head, "actor head + argmax / Gumbel sample (+ beta mix)", py::arg("h"), py::arg("w2"),
         py::arg("b2"), py::arg("mode"), py::arg("seed"), py::arg("counter"), py::arg("out"), py::arg("rec_out") = py::none(),
         py::arg("mix_expert") = py::none(), py::arg("beta") = py::none(), py::arg("exec_out") = py::none());
+  m.def("cnn_head_pair", &cnn_head_pair, "expert argmax + learner sample + beta mix in one launch", py::arg("h_e"),
+        py::arg("w_e"), py::arg("b_e"), py::arg("out_e"), py::arg("rec_out_e"), py::arg("h_l"), py::arg("w_l"), py::arg("b_l"),
+        py::arg("seed"), py::arg("counter"), py::arg("out_l"), py::arg("beta"), py::arg("exec_out"));
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv + bias + ReLU (bf16 MFMA)", py::arg("x"), py::arg("wb"),
         py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0);
   m.def("conv_fwd_pair", &conv_fwd_pair, "two same-shape convs (expert + learner) in one launch");

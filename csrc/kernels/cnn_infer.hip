@@ -98,6 +98,67 @@ constexpr int kMaxHeadActions = 64;
 // at once (independent loads in flight), then A wave reductions.
 constexpr int kHeadRegA = 16;
 
+// Row b's choice under head a (argmax, or Gumbel-max with the launch counter ctr): the same
+// accumulation order as cnn_head_kernel.
+__device__ __forceinline__ int head_row(const CnnHeadArgs& a, int b, uint64_t ctr, int l) {
+  const float* hb = a.h + (size_t)b * a.NH;
+  int best = 0;
+  float best_v = -INFINITY;
+  for (int a0 = 0; a0 < a.A; a0 += kHeadRegA) {
+    float acc[kHeadRegA];
+#pragma unroll
+    for (int q = 0; q < kHeadRegA; ++q) acc[q] = 0.f;
+    for (int j = l; j < a.NH; j += 64) {
+      const float hv = hb[j];
+#pragma unroll
+      for (int q = 0; q < kHeadRegA; ++q)
+        if (a0 + q < a.A) acc[q] += hv * a.W2[(size_t)(a0 + q) * a.NH + j];
+    }
+#pragma unroll
+    for (int q = 0; q < kHeadRegA; ++q) {
+      if (a0 + q >= a.A) break;
+      float p = acc[q];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+      float v = p + a.b2[a0 + q];
+      if (a.mode == 1) v += -logf(-logf(hash_uniform(a.seed, ctr, b, a0 + q)));
+      if (v > best_v) {  // first maximum, like torch.argmax
+        best_v = v;
+        best = a0 + q;
+      }
+    }
+  }
+  return best;
+}
+
+// DAgger's per-step pair in ONE launch (one wave per row): the expert's argmax (e: its action
+// and record slot) and the learner's sample (r), mixed as the learner's exec_out does with the
+// expert's action of the same row -- no cross-wave dependency, so no second launch.
+__global__ __launch_bounds__(1024) void cnn_head_pair_kernel(CnnHeadArgs e, CnnHeadArgs r) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t ctr_e = e.counter ? *e.counter : 0ull;
+  const uint64_t ctr_r = r.counter ? *r.counter : 0ull;
+  for (int b = w; b < e.B; b += nw) {
+    const int be = head_row(e, b, ctr_e, l);
+    const int br = head_row(r, b, ctr_r, l);
+    if (l == 0) {
+      e.out[b] = be;
+      if (e.rec_out) e.rec_out[b] = be;
+      r.out[b] = br;
+      if (r.rec_out) r.rec_out[b] = br;
+      if (r.exec_out) {
+        const float u = hash_uniform(r.seed ^ 0x5DEECE66Dull, ctr_r, b, kMaxHeadActions);
+        r.exec_out[b] = (u > *r.beta) ? (int64_t)br : (int64_t)be;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (e.counter) *e.counter = ctr_e + 1;
+    if (r.counter) *r.counter = ctr_r + 1;
+  }
+}
+
 __global__ __launch_bounds__(1024) void cnn_head_kernel(CnnHeadArgs a) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint64_t ctr = a.counter ? *a.counter : 0ull;
@@ -156,6 +217,16 @@ hipError_t cnn_fc_pair(const CnnFcPair& p, int B, int K, int NH, hipStream_t s) 
   if (B <= 0) return hipSuccess;
   if (K % 32 != 0 || NH % 16 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(cnn_fc_pair_kernel, dim3(NH / 16, (B + 15) / 16, 2), dim3(64 * kFcWaves), 0, s, p, B, K, NH);
+  return hipGetLastError();
+}
+
+hipError_t cnn_head_pair(const CnnHeadArgs& e, const CnnHeadArgs& r, hipStream_t s) {
+  if (e.B <= 0) return hipSuccess;
+  if (e.B != r.B || e.NH != r.NH || e.A <= 0 || e.A > kMaxHeadActions || r.A <= 0 || r.A > kMaxHeadActions)
+    return hipErrorInvalidValue;
+  if (r.exec_out && !r.beta) return hipErrorInvalidValue;
+  const int waves = e.B < 16 ? e.B : 16;
+  hipLaunchKernelGGL(cnn_head_pair_kernel, dim3(1), dim3(64 * waves), 0, s, e, r);
   return hipGetLastError();
 }
 

@@ -262,6 +262,8 @@ struct CnnHeadArgs {
   int64_t* exec_out;         // optional: executed action (u > beta ? own : expert)
 };
 hipError_t cnn_head(const CnnHeadArgs& a, hipStream_t s);
+// expert head (e) + learner head (r, its exec_out mixed with e's action of the same row), one launch
+hipError_t cnn_head_pair(const CnnHeadArgs& e, const CnnHeadArgs& r, hipStream_t s);
 
 // ---- bc_head.hip: categorical BC head (logits, loss metrics, dW / db / dh) + ||theta||^2 in
 // one launch (B <= 64, NH 256 or 512, A <= 8)

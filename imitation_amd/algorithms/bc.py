@@ -425,9 +425,9 @@ class _DPFusedStep:
             side = th.cuda.Stream()
             side.wait_stream(th.cuda.current_stream())
             g1, g2 = th.cuda.CUDAGraph(), th.cuda.CUDAGraph()
-            with th.cuda.graph(g1, stream=side):
+            with graphs.capture(g1, stream=side):
                 f(*static)
-            with th.cuda.graph(g2, stream=side):
+            with graphs.capture(g2, stream=side):
                 t.optimizer.step()
             th.cuda.current_stream().wait_stream(side)
             entry = self._graphs[key] = (static, g1, g2)
@@ -501,7 +501,7 @@ class _DeviceEpochRunner:
         side.wait_stream(th.cuda.current_stream())
         for k in (1, self.K):
             g = th.cuda.CUDAGraph()
-            with th.cuda.graph(g, stream=side):
+            with graphs.capture(g, stream=side):
                 for _ in range(k):
                     self._one_step()
             self.graphs[k] = g

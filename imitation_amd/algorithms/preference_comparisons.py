@@ -31,6 +31,8 @@ from typing import Any, Callable, Dict, List, Mapping, NamedTuple, NoReturn, Opt
 
 import numpy as np
 import torch as th
+
+from imitation_amd.utils import graphs
 from scipy import special
 from torch import nn
 from torch.utils import data as data_th
@@ -795,7 +797,7 @@ class BasicRewardTrainer(RewardTrainer):
         th.cuda.current_stream().wait_stream(side)
         if epochs > 1:
             graph = th.cuda.CUDAGraph()
-            with th.cuda.graph(graph):
+            with graphs.capture(graph):
                 fm.plan.epoch(orders, P, cursor, ep, allm, merge)
             for _ in range(epochs - 1):
                 graph.replay()
@@ -1028,7 +1030,7 @@ class _MinibatchGraph:
         th.cuda.current_stream().wait_stream(side)
         opt.zero_grad(set_to_none=True)
         graph = th.cuda.CUDAGraph()
-        with th.cuda.graph(graph):
+        with graphs.capture(graph):
             out = self._step(buf)
         self.graphs[n] = (buf, graph, out)
         return rec

@@ -33,6 +33,8 @@ from typing import Callable, Dict, List, Mapping, Optional, Sequence, Tuple
 import numpy as np
 import torch as th
 
+from imitation_amd.utils import graphs
+
 from imitation_amd import ops
 from imitation_amd.ops import rl as rl_ops
 from imitation_amd.data import types
@@ -405,10 +407,15 @@ class DeviceDAggerCollector:
             h_e, h_l = CnnActor.hidden_pair(ea, la, self.obs)
         else:
             h_e, h_l = ea.hidden(self.obs), la.hidden(self.obs)
-        C.cnn_head(h_e, self.expert.action_net.weight, self.expert.action_net.bias, 0, 0, None, self._a_exp,
-                   rec_out=b["acts"][k])
-        C.cnn_head(h_l, self.learner.action_net.weight, self.learner.action_net.bias, 1, self._head_seed, self._head_ctr,
-                   self._a_rob, mix_expert=self._a_exp, beta=self._beta, exec_out=self._a_exec)
+        if self._pair:  # both heads + the beta mix in one launch (csrc/kernels/cnn_infer.hip)
+            C.cnn_head_pair(h_e, self.expert.action_net.weight, self.expert.action_net.bias, self._a_exp, b["acts"][k],
+                            h_l, self.learner.action_net.weight, self.learner.action_net.bias, self._head_seed,
+                            self._head_ctr, self._a_rob, self._beta, self._a_exec)
+        else:
+            C.cnn_head(h_e, self.expert.action_net.weight, self.expert.action_net.bias, 0, 0, None, self._a_exp,
+                       rec_out=b["acts"][k])
+            C.cnn_head(h_l, self.learner.action_net.weight, self.learner.action_net.bias, 1, self._head_seed,
+                       self._head_ctr, self._a_rob, mix_expert=self._a_exp, beta=self._beta, exec_out=self._a_exec)
         d = self._env_args(0, k, self._a_exec, b)
         d["obs_rec"] = b["obs"][k]
         C.dagger_env_step(d)
@@ -441,7 +448,7 @@ class DeviceDAggerCollector:
             g = th.cuda.CUDAGraph()
             try:
                 # capture only: nothing in this block executes until replay()
-                with th.cuda.graph(g):
+                with graphs.capture(g):
                     for k in range(self.chunk):
                         self._step(k, b)
                 b["graph"] = g

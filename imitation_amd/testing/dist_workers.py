@@ -5,6 +5,8 @@ from __future__ import annotations
 import numpy as np
 import torch as th
 
+from imitation_amd.utils import graphs
+
 
 def moments_worker(rank, world, data):
     from imitation_amd.parallel import dist as pdist
@@ -252,7 +254,7 @@ def oneshot_worker(rank, world, sizes, scale, seed):
     side.wait_stream(th.cuda.current_stream(dev))
     g = th.cuda.CUDAGraph()
     with th.cuda.stream(side):
-        with th.cuda.graph(g, stream=side):
+        with graphs.capture(g, stream=side):
             c.allreduce_(buf, scale)
     th.cuda.current_stream(dev).wait_stream(side)
     for rep in range(3):
@@ -436,7 +438,7 @@ def oneshot_block_change_worker(rank, world, reps, seed):
     side.wait_stream(th.cuda.current_stream(dev))
     g = th.cuda.CUDAGraph()
     with th.cuda.stream(side):
-        with th.cuda.graph(g, stream=side):
+        with graphs.capture(g, stream=side):
             for b in bufs:
                 c.allreduce_(b)
     th.cuda.current_stream(dev).wait_stream(side)

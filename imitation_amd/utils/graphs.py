@@ -20,10 +20,29 @@ callers check this: one fixed minibatch size, no DP gradient bucket).
 
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 from typing import Any, Callable, Dict, Optional, Tuple
 
 import torch as th
+
+
+@contextlib.contextmanager
+def capture(graph: "th.cuda.CUDAGraph", **kwargs):
+    """``th.cuda.graph(graph, **kwargs)`` with Python's garbage collector held off for the
+    capture: a collection inside it can run finalisers that free pinned host memory or
+    destroy events (a synchronising call -- illegal while a stream is capturing), which
+    aborts the process depending on when the collector happens to run."""
+    gc.collect()
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        with th.cuda.graph(graph, **kwargs):
+            yield
+    finally:
+        if enabled:
+            gc.enable()
 
 
 def graphs_enabled(device: th.device, knob: str) -> bool:
@@ -94,7 +113,7 @@ class GraphedTrainStep:
         # capture on the warm-up stream: the autograd nodes the warm-up created (e.g. the
         # parameters' AccumulateGrad) belong to that stream, and a capture on another stream
         # would make the engine synchronise with it inside the capture
-        with th.cuda.graph(graph, stream=side):
+        with capture(graph, stream=side):
             out = self.fn(*static)
         th.cuda.current_stream().wait_stream(side)
         self._graphs[key] = (static, graph, out)

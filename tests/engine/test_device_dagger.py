@@ -158,6 +158,25 @@ def test_cnn_actor_matches_policy():
         with th.no_grad():
             h1, h2 = CnnActor.hidden_pair(actor, actor2, xp)
             assert th.equal(h1, actor.hidden(xp)) and th.equal(h2, actor2.hidden(xp))
+    # both heads + the beta mix in one launch == the expert call then the learner call
+    for Bp, beta in ((8, 0.5), (64, 0.3), (1, 1.0)):
+        he, hl = h[:Bp].contiguous(), actor2.hidden(x[:Bp].contiguous())
+        bt = th.full((1,), beta, device="cuda")
+        outs = []
+        for paired in (False, True):
+            ctr = th.full((1,), 7, dtype=th.int64, device="cuda")
+            a_exp, rec, a_rob, a_exec = (th.full((Bp,), -1, dtype=th.int64, device="cuda") for _ in range(4))
+            if paired:
+                C.cnn_head_pair(he, pol.action_net.weight, pol.action_net.bias, a_exp, rec, hl, pol2.action_net.weight,
+                                pol2.action_net.bias, 99, ctr, a_rob, bt, a_exec)
+            else:
+                C.cnn_head(he, pol.action_net.weight, pol.action_net.bias, 0, 0, None, a_exp, rec_out=rec)
+                C.cnn_head(hl, pol2.action_net.weight, pol2.action_net.bias, 1, 99, ctr, a_rob, mix_expert=a_exp, beta=bt,
+                           exec_out=a_exec)
+            outs.append((a_exp, rec, a_rob, a_exec, ctr))
+        for t0, t1 in zip(*outs):
+            assert th.equal(t0, t1)
+        assert int(outs[1][4].item()) == 8
 
 
 @gpu
