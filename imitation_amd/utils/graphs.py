@@ -33,8 +33,8 @@ def capture(graph: "th.cuda.CUDAGraph", **kwargs):
     """``th.cuda.graph(graph, **kwargs)`` with Python's garbage collector held off for the
     capture: a collection inside it can run finalisers that free pinned host memory or
     destroy events (a synchronising call -- illegal while a stream is capturing), which
-    aborts the process depending on when the collector happens to run."""
-    gc.collect()
+    aborts the process depending on when the collector happens to run. (No collection
+    here: a full gc.collect() per capture costs ~100 ms on a large heap.)"""
     enabled = gc.isenabled()
     gc.disable()
     try:
