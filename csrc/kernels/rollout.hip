@@ -105,15 +105,18 @@ __device__ __forceinline__ T pin(T x) {
 // lane j < dout of the last layer (both halves in split form), the actor output j.
 // The split form always runs 4 groups of 4 inputs (zero weights pad the short layers):
 // 4 extra FMAs on the 17-input layer instead of uniform branches around every group.
-template <bool SPLIT, int HACT>
+// NLT > 0: the layer count at compile time (the per-layer guards and the last-layer test fold
+// away instead of costing exec-mask juggling on every layer of every step).
+template <bool SPLIT, int HACT, int NLT = -1>
 __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
   const int lane = threadIdx.x;
   const int j = SPLIT ? (lane & 31) : lane;
   const lf4* x4 = (const lf4*)xb;
   float h = 0.f;
+  const int nl = NLT > 0 ? NLT : r.n_layers;
 #pragma unroll
   for (int l = 0; l < kWaveMaxLayers; ++l) {
-    if (l < r.n_layers) {
+    if (l < nl) {
       const lf4* src = x4 + (r.k0[l] >> 2);
       float acc0 = r.bias[l], acc1 = 0.f;
       if (SPLIT) {
@@ -141,7 +144,7 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
       }
       float acc = acc0 + acc1;
       if (SPLIT) acc = add_halves(acc);
-      const bool last = l == r.n_layers - 1;
+      const bool last = l == nl - 1;
       h = j < r.dout[l] ? (last ? acc : hidden_act<HACT>(r.hidden_act, acc)) : 0.f;
       if (!last) {
         wave_sync();  // every lane has read this layer's input
@@ -305,7 +308,7 @@ struct Cursors {
   int vec_step, act_step, sc_step;
 };
 
-template <bool SPLIT, int ENV, int HACT>
+template <bool SPLIT, int ENV, int HACT, int NLT = -1>
 __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       // ---- actor
       xb[lane] = lane < D ? (o - nmean) * nrstd : 0.f;
       wave_sync();
-      const float head = actor_forward<SPLIT, HACT>(ar, xb);
+      const float head = actor_forward<SPLIT, HACT, NLT>(ar, xb);
       float a_raw, a_env;
       if (discrete) {
         const float g = lane < a.n_actions ? head + *nz : -INFINITY;
@@ -537,7 +540,17 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   const int env = a.P.kind != ENV_LOCO ? CE_GENERIC : (p.nq_root == 3 && p.nv_root == 3) ? CE_LOCO3 : CE_LOCO;
   const int act = a.pi.n_layers > 1 ? a.pi.hidden_act : ACT_IDENTITY;
   const dim3 g(a.N), b(64);
-  if (split && env == CE_LOCO3 && act == ACT_TANH)
+  // (planar locomotion with the usual two hidden layers + head: the depth is compile-time too)
+  const bool nl3 = a.pi.n_layers == 3;
+  if (split && env == CE_LOCO3 && act == ACT_TANH && nl3)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3>), g, b, lds, s, a);
+  else if (split && env == CE_LOCO3 && act == ACT_RELU && nl3)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_RELU, 3>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_TANH && nl3)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_TANH, 3>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_RELU && nl3)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_RELU, 3>), g, b, lds, s, a);
+  else if (split && env == CE_LOCO3 && act == ACT_TANH)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH>), g, b, lds, s, a);
   else if (split && env == CE_LOCO3 && act == ACT_RELU)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_RELU>), g, b, lds, s, a);
