@@ -106,8 +106,10 @@ __device__ __forceinline__ T pin(T x) {
 // The split form always runs 4 groups of 4 inputs (zero weights pad the short layers):
 // 4 extra FMAs on the 17-input layer instead of uniform branches around every group.
 // NLT > 0: the layer count at compile time (the per-layer guards and the last-layer test fold
-// away instead of costing exec-mask juggling on every layer of every step).
-template <bool SPLIT, int HACT, int NLT = -1>
+// away instead of costing exec-mask juggling on every layer of every step). HW > 0: every
+// hidden layer is HW wide (32 split form, 64 full form), so no lane is past its layer's width
+// and the activation runs unmasked.
+template <bool SPLIT, int HACT, int NLT = -1, int HW = -1>
 __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
   const int lane = threadIdx.x;
   const int j = SPLIT ? (lane & 31) : lane;
@@ -145,7 +147,8 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
       float acc = acc0 + acc1;
       if (SPLIT) acc = add_halves(acc);
       const bool last = l == nl - 1;
-      h = j < r.dout[l] ? (last ? acc : hidden_act<HACT>(r.hidden_act, acc)) : 0.f;
+      const bool full = HW > 0 && !last;  // (HW == 32 split / 64 full: every lane is a unit)
+      h = (full || j < r.dout[l]) ? (last ? acc : hidden_act<HACT>(r.hidden_act, acc)) : 0.f;
       if (!last) {
         wave_sync();  // every lane has read this layer's input
         if (lane < (SPLIT ? 32 : 64)) xb[lane] = h;
@@ -308,7 +311,7 @@ struct Cursors {
   int vec_step, act_step, sc_step;
 };
 
-template <bool SPLIT, int ENV, int HACT, int NLT = -1>
+template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1>
 __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       // ---- actor
       xb[lane] = lane < D ? (o - nmean) * nrstd : 0.f;
       wave_sync();
-      const float head = actor_forward<SPLIT, HACT, NLT>(ar, xb);
+      const float head = actor_forward<SPLIT, HACT, NLT, HW>(ar, xb);
       float a_raw, a_env;
       if (discrete) {
         const float g = lane < a.n_actions ? head + *nz : -INFINITY;
@@ -540,9 +543,19 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   const int env = a.P.kind != ENV_LOCO ? CE_GENERIC : (p.nq_root == 3 && p.nv_root == 3) ? CE_LOCO3 : CE_LOCO;
   const int act = a.pi.n_layers > 1 ? a.pi.hidden_act : ACT_IDENTITY;
   const dim3 g(a.N), b(64);
-  // (planar locomotion with the usual two hidden layers + head: the depth is compile-time too)
+  // (planar locomotion with the usual two uniform hidden layers -- [32, 32] split form, [64, 64]
+  // full form -- + head: depth and width are compile-time too)
   const bool nl3 = a.pi.n_layers == 3;
-  if (split && env == CE_LOCO3 && act == ACT_TANH && nl3)
+  const int hw = nl3 && a.pi.dims[1] == a.pi.dims[2] ? a.pi.dims[1] : 0;
+  if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32>), g, b, lds, s, a);
+  else if (split && env == CE_LOCO3 && act == ACT_RELU && hw == 32)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_RELU, 3, 32>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_TANH && hw == 64)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_TANH, 3, 64>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_RELU && hw == 64)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_RELU, 3, 64>), g, b, lds, s, a);
+  else if (split && env == CE_LOCO3 && act == ACT_TANH && nl3)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3>), g, b, lds, s, a);
   else if (split && env == CE_LOCO3 && act == ACT_RELU && nl3)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_RELU, 3>), g, b, lds, s, a);
