@@ -151,7 +151,13 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
       h = (full || j < r.dout[l]) ? (last ? acc : hidden_act<HACT>(r.hidden_act, acc)) : 0.f;
       if (!last) {
         wave_sync();  // every lane has read this layer's input
-        if (lane < (SPLIT ? 32 : 64)) xb[lane] = h;
+        // split form: lanes 32..63 hold copies of 0..31, and the next layer reads xb[0 .. 32)
+        // only (its last 16 weights are zero), so the write needs no mask
+        if (SPLIT && HW <= 0) {
+          if (lane < 32) xb[lane] = h;
+        } else {
+          xb[lane] = h;
+        }
         wave_sync();
       }
     }
@@ -325,11 +331,11 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   const int lane = threadIdx.x;
   const EnvParams& P = a.P;
   const int D = P.obs_dim;
-  const bool discrete = a.n_actions > 0;
+  constexpr bool loco = ENV != CE_GENERIC;
+  const bool discrete = !loco && a.n_actions > 0;  // locomotion envs are continuous (host check)
   const int A = discrete ? 1 : P.act_dim;
   const int AW = discrete ? a.n_actions : P.act_dim;  // noise values per step
   const int S = state_size(P);
-  constexpr bool loco = ENV != CE_GENERIC;
 
   Actor<SPLIT> ar;
   load_actor<SPLIT>(a.pi, ar, wlds);
@@ -535,7 +541,7 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   for (int l = 0; l <= a.pi.n_layers; ++l)
     if (a.pi.dims[l] > 64 || a.pi.dims[l] < 1) return hipErrorInvalidValue;
   if (a.pi.dims[0] != a.P.obs_dim) return hipErrorInvalidValue;
-  if (a.n_actions > 64 || (a.P.kind == ENV_LOCO && a.P.loco.nj > 8)) return hipErrorInvalidValue;
+  if (a.n_actions > 64 || (a.P.kind == ENV_LOCO && (a.P.loco.nj > 8 || a.n_actions > 0))) return hipErrorInvalidValue;
   const size_t lds = rollout_lds_bytes(a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const bool split = rollout_split_form(a.pi);
