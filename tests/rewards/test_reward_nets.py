@@ -221,3 +221,42 @@ def test_predict_processed_wrappers_pass_method_calls_to_base():
         getattr(wrapper, attr)(*call_with)
         m.assert_called_once_with(*call_with)
     assert wrapper.device == base.device and wrapper.dtype == base.dtype
+
+
+def test_load_reward_passes_along_alpha_to_add_std_predict_processed(tmp_path):
+    """Keyword arguments of load_reward reach AddSTDRewardWrapper.predict_processed: the
+    loaded reward function is mean + alpha * std of the members (reference
+    test_reward_nets.py:838)."""
+    ens = testing_reward_nets.make_ensemble(OBS, ACT, 2)
+    net = reward_nets.AddSTDRewardWrapper(ens, default_alpha=0.0)
+    path = tmp_path / "net.pt"
+    serialize.save_reward_net(net, path)
+    b = _batch()
+    mean, var = ens.predict_reward_moments(*b)
+    for alpha in (-0.5, 0.0, 2.0):
+        out = serialize.load_reward("RewardNet_std_added", str(path), None, alpha=alpha)(*b)
+        np.testing.assert_allclose(out, mean + alpha * np.sqrt(var), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("wrapper", ["normalized", "std_added"])
+def test_predict_processed_wrappers_pass_method_calls_to_base(wrapper):
+    """A PredictProcessedWrapper forwards forward / predict_th / predict / preprocess to its
+    base and exposes the base's device and dtype (reference test_reward_nets.py:808)."""
+    from unittest import mock
+
+    if wrapper == "normalized":
+        w = reward_nets.NormalizedRewardNet(reward_nets.BasicRewardNet(OBS, ACT), networks.RunningNorm)
+    else:
+        w = reward_nets.AddSTDRewardWrapper(testing_reward_nets.make_ensemble(OBS, ACT, 2))
+    base = mock.create_autospec(testing_reward_nets.MockRewardNet)
+    base.device = th.device("cpu")
+    base.dtype = th.float32
+    w._base = base
+    np_b = _batch()
+    th_b = tuple(th.as_tensor(x) for x in np_b)
+    for attr, args, ret in [("forward", th_b, th.zeros(10)), ("predict_th", np_b, th.zeros(10)),
+                            ("predict", np_b, np.zeros(10)), ("preprocess", np_b, th_b)]:
+        setattr(base, attr, mock.MagicMock(return_value=ret))
+        getattr(w, attr)(*args)
+        getattr(base, attr).assert_called_once_with(*args)
+    assert w.device is base.device and w.dtype is base.dtype

@@ -237,3 +237,106 @@ def test_parallel_arg_errors(tmp_path):
     for upd, match in cases:
         with pytest.raises(TypeError, match=match):
             parallel_ex.run(named_configs=["generate_test_data"], config_updates={**base, **upd})
+
+
+@pytest.mark.parametrize("env_name", ["seals_cartpole", "mountain_car", "seals_mountain_car"])
+def test_train_preference_comparisons_envs_no_crash(tmp_path, env_name):
+    """The env named configs of train_preference_comparisons run end to end (reference
+    test_scripts.py:171)."""
+    from imitation_amd.scripts.train_preference_comparisons import train_preference_comparisons_ex
+
+    run = train_preference_comparisons_ex.run(named_configs=[env_name, "fast", "rl.fast", *FAST_ENV],
+                                              config_updates=_updates(tmp_path))
+    assert run.status == "COMPLETED" and isinstance(run.result, dict)
+
+
+def test_train_rl_sac(tmp_path):
+    """rl.sac after rl.fast on Pendulum (reference test_scripts.py:486)."""
+    from imitation_amd.rl.sac import SAC
+    from imitation_amd.scripts.train_rl import train_rl_ex
+
+    run = train_rl_ex.run(named_configs=["pendulum", "environment.fast", "rl.fast", "fast", "rl.sac", "policy.sac"],
+                          config_updates=_updates(tmp_path))
+    assert run.config["rl"]["rl_cls"] is SAC
+    assert run.status == "COMPLETED" and isinstance(run.result, dict)
+
+
+@pytest.mark.parametrize("config", [
+    {"reward_type": "zero", "reward_path": "foobar"},
+    {"explore_kwargs": {"switch_prob": 1.0, "random_prob": 0.1}},
+    {"rollout_save_path": "{log_dir}/rollouts.npz"},
+])
+def test_eval_policy_configs(tmp_path, config):
+    """eval_policy's reward wrapping, exploration and rollout saving (reference
+    test_scripts.py:518): a wrapped reward makes return_mean differ from the monitor's."""
+    from imitation_amd.scripts.eval_policy import eval_policy_ex
+
+    run = eval_policy_ex.run(named_configs=["environment.fast", "fast"], config_updates=_updates(tmp_path, **config))
+    assert run.status == "COMPLETED"
+    stats = run.result
+    assert "return_mean" in stats and "monitor_return_mean" in stats
+    if "reward_type" in config:
+        assert stats["return_mean"] != stats["monitor_return_mean"]
+    else:
+        assert stats["return_mean"] == stats["monitor_return_mean"]
+    if "rollout_save_path" in config:
+        assert next((tmp_path / "out").rglob("rollouts.npz")).exists()
+
+
+def test_converted_trajectories_equal_original(tmp_path):
+    """convert_trajs turns a legacy npz file into the current format with equal trajectories
+    (reference test_scripts.py:1070)."""
+    import shutil
+
+    from imitation_amd.data import serialize
+    from imitation_amd.scripts import convert_trajs
+    from tests.conftest import TESTDATA
+
+    src = tmp_path / "final.npz"
+    shutil.copy(os.path.join(TESTDATA, "expert_models", "cartpole_0", "rollouts", "final.npz"), src)
+    old = serialize.load(src)
+    converted = serialize.load(convert_trajs.update_traj_file_in_place(src))
+    assert len(old) == len(converted)
+    for a, b in zip(old, converted):
+        assert a == b
+
+
+def test_convert_trajs_from_current_format_is_idempotent(tmp_path):
+    """Converting a file that is already in the current format leaves it unchanged (reference
+    test_scripts.py:1085)."""
+    import filecmp
+    import shutil
+
+    from imitation_amd.scripts import convert_trajs
+    from tests.conftest import TESTDATA
+
+    src = tmp_path / "final.npz"
+    shutil.copy(os.path.join(TESTDATA, "expert_models", "cartpole_0", "rollouts", "final.npz"), src)
+    current = convert_trajs.update_traj_file_in_place(src)
+    orig = current.with_suffix(".orig")
+    shutil.copytree(current, orig)
+    again = convert_trajs.update_traj_file_in_place(current)
+    cmp = filecmp.dircmp(again, orig)
+    assert cmp.diff_files == [] and cmp.left_only == [] and cmp.right_only == [], "convert_trajs not idempotent"
+
+
+def test_parallel_train_adversarial_custom_env(tmp_path):
+    """A parallel sweep of train_adversarial on Pendulum with demonstrations from a train_rl run, two
+    repeats of a one-choice search space (reference test_scripts.py:912)."""
+    from imitation_amd.scripts import tune
+    from imitation_amd.scripts.parallel import parallel_ex
+    from imitation_amd.scripts.train_rl import train_rl_ex
+
+    rl_dir = tmp_path / "rl"
+    train_rl_ex.run(named_configs=["pendulum", "environment.fast", "rl.fast", "fast"],
+                    config_updates={"logging": {"log_dir": str(rl_dir)}})
+    demo_path = rl_dir / "rollouts" / "final.npz"
+    assert demo_path.exists()
+    run = parallel_ex.run(config_updates={
+        "sacred_ex_name": "train_adversarial", "repeat": 2, "local_dir": str(tmp_path / "par"),
+        "base_named_configs": ["pendulum", "environment.fast", "demonstrations.fast", "rl.fast", "fast"],
+        "base_config_updates": _updates(tmp_path, demonstrations={"source": "local", "path": str(demo_path),
+                                                                         "n_expert_demos": 1}),
+        "search_space": {"command_name": tune.choice(["gail"])}})
+    assert run.status == "COMPLETED"
+    assert len(run.result) == 2 and all(r["status"] == "COMPLETED" for r in run.result)
