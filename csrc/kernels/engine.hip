@@ -44,15 +44,25 @@ __device__ lf* load_mlp(const WaveMLP& m, LdsMLP& out, lf* lds) {
 #pragma unroll
   for (int l = 0; l <= kWaveMaxLayers; ++l) out.dims[l] = l <= m.n_layers ? m.dims[l] : 0;
   const int lane = threadIdx.x & 63;
+  // every thread of the workgroup takes part: element e of the zero-padded [64][dp] weight
+  // matrix goes to thread e % blockDim.x, so consecutive threads read consecutive inputs of
+  // one unit (coalesced) and 4 loads are in flight per thread before their LDS stores
+  const int tid = threadIdx.x, nth = blockDim.x;
 #pragma unroll
   for (int l = 0; l < kWaveMaxLayers; ++l) {
     if (l < m.n_layers) {
       const int din = m.dims[l], dout = m.dims[l + 1], dp = ceil8(din);
+      const float* W = m.W[l];
       out.WT[l] = lds;
-      for (int k = 0; k < dp; ++k) lds[wt_index(k, lane)] = (lane < dout && k < din) ? m.W[l][lane * din + k] : 0.f;
-      lds += dp * kW;
+      const int n_el = dp * kW;
+#pragma unroll 4
+      for (int e = tid; e < n_el; e += nth) {
+        const int j = e / dp, k = e - j * dp;
+        lds[wt_index(k, j)] = (j < dout && k < din) ? W[j * din + k] : 0.f;
+      }
+      lds += n_el;
       out.b[l] = lds;
-      lds[lane] = lane < dout ? m.b[l][lane] : 0.f;
+      if (tid < kW) lds[tid] = tid < dout ? m.b[l][tid] : 0.f;
       lds += kW;
     } else {
       out.WT[l] = nullptr;
@@ -63,8 +73,10 @@ __device__ lf* load_mlp(const WaveMLP& m, LdsMLP& out, lf* lds) {
     out.mean = lds;
     out.rstd = lds + kW;
     const int d0 = m.dims[0];
-    lds[lane] = lane < d0 ? m.norm_mean[lane] : 0.f;
-    lds[kW + lane] = lane < d0 ? rsqrtf(m.norm_var[lane] + m.norm_eps) : 1.f;
+    if (tid < kW) {
+      lds[tid] = tid < d0 ? m.norm_mean[tid] : 0.f;
+      lds[kW + tid] = tid < d0 ? rsqrtf(m.norm_var[tid] + m.norm_eps) : 1.f;
+    }
     lds += 2 * kW;
   } else {
     out.mean = nullptr;
@@ -75,21 +87,23 @@ __device__ lf* load_mlp(const WaveMLP& m, LdsMLP& out, lf* lds) {
 
 // acc_j += sum_k W[j][k] * x_k, x_k = readlane(h, k) (k uniform), 8 inputs per step:
 // both 16-byte weight fetches are issued before the FMA chain.
+// Two interleaved FMA chains (even / odd inputs) halve the dependent-FMA depth.
 __device__ __forceinline__ float layer_dot(const lf* WT, int din, float h, float acc) {
   const lf4* w4 = (const lf4*)WT + (threadIdx.x & 63);
   const int dp = ceil8(din);
+  float acc1 = 0.f;
   for (int k = 0; k < dp; k += 8) {
     const f32v4 w0 = w4[(k >> 2) * kW], w1 = w4[((k >> 2) + 1) * kW];
     acc = fmaf(w0.x, bcast(h, k + 0), acc);
-    acc = fmaf(w0.y, bcast(h, k + 1), acc);
+    acc1 = fmaf(w0.y, bcast(h, k + 1), acc1);
     acc = fmaf(w0.z, bcast(h, k + 2), acc);
-    acc = fmaf(w0.w, bcast(h, k + 3), acc);
+    acc1 = fmaf(w0.w, bcast(h, k + 3), acc1);
     acc = fmaf(w1.x, bcast(h, k + 4), acc);
-    acc = fmaf(w1.y, bcast(h, k + 5), acc);
+    acc1 = fmaf(w1.y, bcast(h, k + 5), acc1);
     acc = fmaf(w1.z, bcast(h, k + 6), acc);
-    acc = fmaf(w1.w, bcast(h, k + 7), acc);
+    acc1 = fmaf(w1.w, bcast(h, k + 7), acc1);
   }
-  return acc;
+  return acc + acc1;
 }
 
 // Lane j of x holds input feature j (j < dims[0]); returns lane j = output unit j.
@@ -225,7 +239,7 @@ __global__ __launch_bounds__(kOutNormThreads) void reward_outnorm_kernel(OutNorm
     a.count[0] = state[2];
   }
 }
-constexpr int kPostWaves = 4;  // waves per workgroup sharing one LDS image of the nets
+constexpr int kPostWaves = 8;  // waves per workgroup sharing one LDS image of the nets
 
 __global__ __launch_bounds__(64 * kPostWaves) void rollout_post_kernel(RolloutPostArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
@@ -308,8 +322,13 @@ hipError_t rollout_post_launch(const RolloutPostArgs& a, hipStream_t s) {
   if (a.D > kEngineMaxObs || a.A > kWaveMaxDim) return hipErrorInvalidValue;
   const size_t lds = rollout_post_lds_bytes(a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const int rows_per_wave = 2;
-  const int grid = (rows + kPostWaves * rows_per_wave - 1) / (kPostWaves * rows_per_wave);
+  // one transition per wave (the per-row chain of 3-4 small MLPs is latency bound, so the
+  // rows go wide: 4096 rows = 512 workgroups, two per CU at this kernel's LDS / VGPR use); the
+  // N bootstrap rows are second rows of the first N waves (one value net each).
+  // Measured (one MI355X): GAIL HalfCheetah (4104 rows, 3 nets) 78 -> 27 us, AIRL Hopper
+  // (8200 rows, 4 nets) 304 -> 104 us, against 4-wave workgroups of 2 rows per wave that
+  // loaded the weights wave by wave with strided reads (profiles/r4_rollout_breakdown.md).
+  const int grid = (a.T * a.N + kPostWaves - 1) / kPostWaves;
   hipLaunchKernelGGL(rollout_post_kernel, dim3(grid), dim3(64 * kPostWaves), lds, s, a);
   return hipGetLastError();
 }
