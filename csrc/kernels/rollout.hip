@@ -241,7 +241,11 @@ __device__ float loco_obs(const LocoParams& p, const LocoRegs& L, lf* sb) {
 
 // ia::loco_step (envs.h) with the joint loops spread over lanes; a_in = action of joint
 // lane j. Returns the step reward (uniform).
-template <int ENV>
+// FS > 0: frame_skip at compile time. The substeps are then unrolled, so the root-state
+// chain (stance -> thrust / lift lane sums -> root velocities) of one substep overlaps the
+// joint chain (sin -> qdd -> qd -> q) of the next instead of each substep ending at the loop
+// back-edge.
+template <int ENV, int FS = -1>
 __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
   const int lane = threadIdx.x;
   const bool jl = lane < p.nj;
@@ -251,7 +255,7 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
   const float x_before = L.rq[0];
   const float dt = L.dt;
   float q = L.q, qd = L.qd;
-  for (int sub = 0; sub < p.frame_skip; ++sub) {
+  const auto substep = [&]() {
     const float qdd = L.gear * a - L.stiff * q - L.damp * qd - 2.0f * __sinf(q);
     const float st_all = stance(q);  // every lane (no exec-masked branch around the exp / rcp)
     const float st = jl ? st_all : 0.f;
@@ -294,6 +298,12 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
     const bool hi = qn > 1.2f, lo = qn < -1.2f;
     qd = (hi && qd > 0.f) || (lo && qd < 0.f) ? 0.f : qd;
     q = fminf(fmaxf(qn, -1.2f), 1.2f);
+  };
+  if constexpr (FS > 0) {
+#pragma unroll
+    for (int sub = 0; sub < FS; ++sub) substep();
+  } else {
+    for (int sub = 0; sub < p.frame_skip; ++sub) substep();
   }
   L.q = jl ? q : 0.f;
   L.qd = jl ? qd : 0.f;
@@ -317,7 +327,7 @@ struct Cursors {
   int vec_step, act_step, sc_step;
 };
 
-template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1>
+template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1, int FS = -1>
 __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
@@ -454,7 +464,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       float r_env;
       float o_next;
       if (loco) {
-        r_env = loco_step_regs<ENV>(P.loco, L, a_env);
+        r_env = loco_step_regs<ENV, FS>(P.loco, L, a_env);
         o_next = loco_obs<ENV>(P.loco, L, sb);
       } else {
         if (lane < A) act[lane] = a_env;
@@ -553,7 +563,18 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   // full form -- + head: depth and width are compile-time too)
   const bool nl3 = a.pi.n_layers == 3;
   const int hw = nl3 && a.pi.dims[1] == a.pi.dims[2] ? a.pi.dims[1] : 0;
-  if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32)
+  // (+ the frame skip of the benchmark recipes: HalfCheetah 5 with the [32, 32] tanh actor,
+  // Hopper / Walker 4 with the [64, 64] ReLU one)
+  const int fs = env == CE_LOCO3 ? p.frame_skip : 0;
+  if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5>), g, b, lds, s, a);
+  else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 4)
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 4>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_RELU && hw == 64 && fs == 4)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_RELU, 3, 64, 4>), g, b, lds, s, a);
+  else if (!split && env == CE_LOCO3 && act == ACT_RELU && hw == 64 && fs == 5)
+    hipLaunchKernelGGL((rollout_chain_kernel<false, CE_LOCO3, ACT_RELU, 3, 64, 5>), g, b, lds, s, a);
+  else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32>), g, b, lds, s, a);
   else if (split && env == CE_LOCO3 && act == ACT_RELU && hw == 32)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_RELU, 3, 32>), g, b, lds, s, a);
