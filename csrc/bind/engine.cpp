@@ -151,7 +151,9 @@ void reward_outnorm(py::dict d) {
   a.rewards = tptr<float>(d, "rewards");
   a.mean = tptr<float>(d, "mean");
   a.var = tptr<float>(d, "var");
-  a.count = tptr<float>(d, "count");
+  a.count_i = tptr<int>(d, "count_i", true);
+  if (a.count_i) TORCH_CHECK(py::cast<torch::Tensor>(d["count_i"]).scalar_type() == torch::kInt32, "count_i: int32");
+  a.count = tptr<float>(d, "count", a.count_i != nullptr);
   a.eps = (float)fval(d, "eps", 1e-5);
   a.step_stats = tptr<const float>(d, "step_stats", true);
   IA_HIP_CHECK2(ia::reward_outnorm_launch(a, ia_stream()));
@@ -187,6 +189,9 @@ void ppo_update(py::dict d) {
   a.norm_mean = tptr<float>(d, "norm_mean", true);
   a.norm_var = tptr<float>(d, "norm_var", true);
   a.norm_count = tptr<float>(d, "norm_count", true);
+  a.norm_count_i = tptr<int>(d, "norm_count_i", true);
+  if (a.norm_count_i)
+    TORCH_CHECK(py::cast<torch::Tensor>(d["norm_count_i"]).scalar_type() == torch::kInt32, "norm_count_i: int32");
   a.norm_eps = (float)fval(d, "norm_eps", 1e-5);
   a.obs = tptr<const float>(d, "obs");
   a.acts = tptr<const float>(d, "acts");
@@ -208,6 +213,7 @@ void ppo_update(py::dict d) {
   a.normalize_advantage = ival(d, "normalize_advantage", 1);
   a.adam_step = tptr<float>(d, "adam_step");
   a.stats = tptr<float>(d, "stats");
+  a.zero_stats = ival(d, "zero_stats", 0);
   a.mode = ival(d, "mode", 0);
   a.mb_index = ival(d, "mb_index", 0);
   a.prof = tptr<unsigned long long>(d, "prof", true);

@@ -114,6 +114,7 @@ struct OutNormArgs {
   float* mean;   // [1] running state, updated in place
   float* var;    // [1]
   float* count;  // [1] (float)
+  int* count_i;  // optional: the module's int32 count, read / written instead of count
   float eps;
   const float* step_stats;  // [T][3] or nullptr
 };
@@ -139,6 +140,7 @@ struct PPOArgs {
   float* norm_mean;
   float* norm_var;
   float* norm_count;  // float counter (exact up to 2^24)
+  int* norm_count_i;  // optional: the module's int32 counter, read / written instead of norm_count
   float norm_eps;
   int has_norm;
   // data: flat rollout [rows]
@@ -156,6 +158,7 @@ struct PPOArgs {
   float* adam_step;  // running step count (float)
   // diagnostics [5]: entropy_loss, pg_loss, value_loss, clip_fraction, approx_kl (sums over minibatches)
   float* stats;
+  int zero_stats;  // mode 0 fast path: the prep launch zeroes stats (no separate memset)
   int mode;  // 0: full persistent update; 1: one minibatch -> grads only; 2: apply clip+Adam from grads
   int mb_index;  // minibatch index for mode 1 (epoch * n_mb + mb)
   unsigned long long* prof;  // optional [10] cycle counters per phase

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kOutNormThreads) void reward_outnorm_kernel(OutNorm
   if (tid == 0) {
     state[0] = a.mean[0];
     state[1] = a.var[0];
-    state[2] = a.count[0];
+    state[2] = a.count_i ? (float)a.count_i[0] : a.count[0];
   }
   for (int t0 = 0; t0 < a.T; t0 += kOutNormChunk) {
     const int nt = min(kOutNormChunk, a.T - t0);
@@ -236,7 +236,8 @@ __global__ __launch_bounds__(kOutNormThreads) void reward_outnorm_kernel(OutNorm
   if (tid == 0) {
     a.mean[0] = state[0];
     a.var[0] = state[1];
-    a.count[0] = state[2];
+    if (a.count_i) a.count_i[0] = (int)state[2];
+    else a.count[0] = state[2];
   }
 }
 constexpr int kPostWaves = 8;  // waves per workgroup sharing one LDS image of the nets

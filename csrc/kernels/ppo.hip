@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kThreads) void ppo_kernel(PPOArgs a) {
       bf.norm[c] = a.norm_mean[c];
       bf.norm[64 + c] = a.norm_var[c];
     }
-    if (threadIdx.x == 0) bf.norm[128] = a.norm_count[0];
+    if (threadIdx.x == 0) bf.norm[128] = a.norm_count_i ? (float)a.norm_count_i[0] : a.norm_count[0];
   }
 
   const int n_mb = a.rows / a.batch;
@@ -747,7 +747,10 @@ __global__ __launch_bounds__(kThreads) void ppo_kernel(PPOArgs a) {
       a.norm_mean[c] = bf.norm[c];
       a.norm_var[c] = bf.norm[64 + c];
     }
-    if (threadIdx.x == 0) a.norm_count[0] = bf.norm[128];
+    if (threadIdx.x == 0) {
+      if (a.norm_count_i) a.norm_count_i[0] = (int)bf.norm[128];
+      else a.norm_count[0] = bf.norm[128];
+    }
   }
   if (a.prof && threadIdx.x == 0) {
 #pragma unroll

@@ -33,6 +33,7 @@ __global__ __launch_bounds__(64 * kPrepWaves) void ppo_rc_prep_kernel(PPOArgs a,
   // the main kernel's arrival counters / flags start at zero (stream order: it runs after
   // this launch) -- replaces a separate memset launch per update
   if (k == 0 && threadIdx.x < 64) g.sync[threadIdx.x] = 0u;
+  if (k == 0 && a.zero_stats && threadIdx.x < 5) a.stats[threadIdx.x] = 0.f;  // (and the stats)
   const int n_mb = a.rows / Bg;
   const int e = k / n_mb, mb = k - e * n_mb;
   const bool ok = lane < cw;

@@ -495,7 +495,7 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   if (norm_lane) {
     run_m = a.norm_mean[nc];
     run_v = a.norm_var[nc];
-    run_c = a.norm_count[0];
+    run_c = a.norm_count_i ? (float)a.norm_count_i[0] : a.norm_count[0];
   }
   // owned items: gradient / moments registers. Weight slot it of this wave is item
   // wb + w + it * NW (valid below nwq), bias slot ib is item bb + w + ib * NW (valid below nbq).
@@ -1570,7 +1570,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
   if (shared_wb && norm_lane && K > 0) {
     a.norm_mean[nc] = run_m;
     a.norm_var[nc] = run_v;
-    if (nc == 0) a.norm_count[0] = run_c;
+    if (nc == 0) {
+      if (a.norm_count_i) a.norm_count_i[0] = (int)run_c;  // (an exact integer below 2^24)
+      else a.norm_count[0] = run_c;
+    }
   }
   if (shared_wb && tid == 0) a.adam_step[0] = step;
   // (stats barrier above orders the LDS). Net split: the critic workgroup owns the critic

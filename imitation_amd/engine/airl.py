@@ -110,12 +110,17 @@ class OutputNormMixin:
             mean = msg[:, 1] / cnt
             var = (msg[:, 2] / cnt - mean * mean).clamp_min(0.0)
             step_stats = th.stack([cnt, mean, var], 1).float().contiguous()
-        self._onorm_count.copy_(out_norm.count.reshape(1))
+        # an int32 module count is read / written by the kernel itself (no copies around it)
+        direct = out_norm.count.dtype == th.int32
+        if not direct:
+            self._onorm_count.copy_(out_norm.count.reshape(1))
         self._C.engine_reward_outnorm(dict(T=self.T, N=self.N, rew_raw=self._rew_raw, boot=self._boot,
                                            rewards=self.buf["rewards"], mean=out_norm.running_mean,
                                            var=out_norm.running_var, count=self._onorm_count,
+                                           count_i=out_norm.count if direct else None,
                                            eps=float(out_norm.eps), step_stats=step_stats))
-        out_norm.count.copy_(self._onorm_count.to(out_norm.count.dtype).reshape(()))
+        if not direct:
+            out_norm.count.copy_(self._onorm_count.to(out_norm.count.dtype).reshape(()))
 
 
 class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):

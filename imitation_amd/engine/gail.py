@@ -323,7 +323,8 @@ class DeviceGeneratorCore:
         if self.pol_norm is not None:
             d.update(norm_mean=self.pol_norm.running_mean, norm_var=self.pol_norm.running_var, norm_count=self.norm_count,
                      norm_eps=float(self.pol_norm.eps))
-        if not self._C.engine_ppo_path(d).startswith("rc"):
+        self._ppo_is_rc = self._C.engine_ppo_path(d).startswith("rc")
+        if not self._ppo_is_rc:
             lds = self._C.engine_ppo_lds(d) if d["batch"] <= 64 else 1 << 30
             if lds > 150 * 1024:
                 raise ValueError(f"PPO engine needs {lds} B of LDS (> 150 KiB)")
@@ -380,7 +381,13 @@ class DeviceGeneratorCore:
     def _ppo_update(self) -> None:
         algo: PPO = self.gen_algo
         rows = self.T * self.N
-        if self.pol_norm is not None:
+        world = pdist.world_size()
+        # single-rank fast path: the kernel reads / writes the module's int32 count itself and
+        # its prep launch zeroes the stats (three small launches fewer between the rollout
+        # and the update)
+        direct = (world == 1 and getattr(self, "_ppo_is_rc", False)
+                  and (self.pol_norm is None or self.pol_norm.count.dtype == th.int32))
+        if self.pol_norm is not None and not direct:
             # the policy normaliser may also have been updated outside the engine (the
             # discriminator's log-prob pass runs the policy in training mode, as the
             # reference does): the kernel continues from the module's own count
@@ -397,8 +404,10 @@ class DeviceGeneratorCore:
         ret = ret.reshape(rows).contiguous()
         d = dict(self._ppo_static)
         d.update(clip_range=clip, lr=lr)
-        self.stats.zero_()
-        world = pdist.world_size()
+        if direct:
+            d.update(zero_stats=1, norm_count_i=self.pol_norm.count if self.pol_norm is not None else None)
+        else:
+            self.stats.zero_()
         if world == 1:
             perm = self._epoch_perms(rows, self._seed)
             d.update(obs=obs, acts=acts, old_logp=old_logp, adv=adv, returns=ret, perm=perm, mode=0)
@@ -421,7 +430,7 @@ class DeviceGeneratorCore:
                 pdist.allreduce_grads_flat(self.grads)
                 d["mode"] = 2
                 self._C.engine_ppo_update(d)
-        if self.pol_norm is not None:
+        if self.pol_norm is not None and not direct:
             self.pol_norm.count.copy_(self.norm_count.to(self.pol_norm.count.dtype).reshape(()))
         # reads the error word of an EARLIER update (non-blocking); train() ends blocking
         self._ppo_err.check("PPO update")
@@ -1119,6 +1128,8 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         :mod:`imitation_amd.utils.checkpoint`); parameters live in the policy modules."""
         st: Dict[str, Any] = {k: getattr(self, k).detach().cpu().clone() for k in self._ENGINE_TENSORS}
         if self.norm_count is not None:
+            if self.pol_norm is not None:  # (the single-rank update keeps the module's count only)
+                self.norm_count.copy_(self.pol_norm.count.reshape(1))
             st["norm_count"] = self.norm_count.cpu().clone()
         st.update(step0=int(self._step0), seed=int(self._seed), perm_round=int(self._perm_round), ep_lens_running=th.as_tensor(self._ep_lens_running),
                   gen_dev={k: v.cpu().clone() for k, v in self._gen_dev._arrays.items()},

@@ -320,6 +320,8 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
     def engine_state(self) -> Dict[str, Any]:
         st: Dict[str, Any] = {k: getattr(self, k).detach().cpu().clone() for k in self._ENGINE_TENSORS}
         if self.norm_count is not None:
+            if self.pol_norm is not None:  # (the single-rank update keeps the module's count only)
+                self.norm_count.copy_(self.pol_norm.count.reshape(1))
             st["norm_count"] = self.norm_count.cpu().clone()
         st.update(step0=int(self._step0), seed=int(self._seed), explore_random=bool(self._explore_random))
         return st
