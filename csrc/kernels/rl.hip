@@ -27,6 +27,7 @@ namespace ia {
 namespace {
 
 constexpr int kGaeWaves = 4;
+constexpr int kGaeRegSteps = 16;  // register fast path: T <= 64 * 16
 
 __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* __restrict__ rew,
                                                                   const float* __restrict__ val,
@@ -42,6 +43,62 @@ __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* _
   const int t0 = lane * L;
   const int t1 = t0 + L < T ? t0 + L : T;
   const float gl = gamma * lam;
+  if (L <= kGaeRegSteps) {
+    // chunks of <= 16 steps (T <= 1024): every load of the chunk is issued up front into
+    // registers (one memory latency instead of one per step and pass); steps past the chunk
+    // are identity maps (delta 0, c 1), so the fold and the replay are bitwise the loop's
+    float dl[kGaeRegSteps], cl[kGaeRegSteps], vl[kGaeRegSteps];
+#pragma unroll
+    for (int i = 0; i < kGaeRegSteps; ++i) {
+      const int t = t0 + i;
+      dl[i] = 0.f;
+      cl[i] = 1.f;
+      vl[i] = 0.f;
+      if (t < t1) {
+        const size_t o = (size_t)t * N + n;
+        float nv, nnt;
+        if (t + 1 < T) {
+          nv = val[o + N];
+          nnt = 1.f - starts[o + N];
+        } else {
+          nv = last_val[n];
+          nnt = 1.f - dones[n];
+        }
+        vl[i] = val[o];
+        dl[i] = rew[o] + gamma * nv * nnt - vl[i];
+        cl[i] = gl * nnt;
+      }
+    }
+    float C = 1.f, D = 0.f;
+#pragma unroll
+    for (int i = kGaeRegSteps - 1; i >= 0; --i) {
+      D = dl[i] + cl[i] * D;
+      C = cl[i] * C;
+    }
+    float SC = C, SD = D;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const float oc = __shfl_down(SC, k, 64);
+      const float od = __shfl_down(SD, k, 64);
+      if (lane + k < 64) {
+        SD = SD + SC * od;
+        SC = SC * oc;
+      }
+    }
+    float a = __shfl_down(SD, 1, 64);
+    if (lane == 63) a = 0.f;
+#pragma unroll
+    for (int i = kGaeRegSteps - 1; i >= 0; --i) {
+      const int t = t0 + i;
+      a = dl[i] + cl[i] * a;
+      if (t < t1) {
+        const size_t o = (size_t)t * N + n;
+        adv[o] = a;
+        ret[o] = a + vl[i];
+      }
+    }
+    return;
+  }
   // fold this lane's chunk: a(t0) = D + C * a(t1)
   float C = 1.f, D = 0.f;
   for (int t = t1 - 1; t >= t0; --t) {
