@@ -612,7 +612,10 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         T, N = dones.shape
         order, fin_t, fin_n, ep_lens, self._ep_lens_running = flatten_order(dones, self._ep_lens_running)
         cap = self._gen_dev.capacity
-        keep = th.as_tensor(order[-cap:], device=self._dev)
+        # pinned + non-blocking: a pageable H2D copy would block the host until the stream
+        # reaches it (in an AIRL split round: until the PPO kernel ends, which left the round's
+        # staging and the next step chain to be enqueued behind the GPU instead of ahead of it)
+        keep = th.from_numpy(np.ascontiguousarray(order[-cap:])).pin_memory().to(self._dev, non_blocking=True)
         rows = T * N
         acts = self.buf["act_env"].reshape(rows, -1)
         if self.discrete:
@@ -1097,6 +1100,10 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             scal = self._stage_disc_updates(n)
         staged = th.cuda.Event()
         staged.record(main)
+        # the next step chain is enqueued before the applies (host order only: it depends on
+        # the staging, not on the applies), so a slow host never delays its start
+        if launch_next:
+            self._launch_chain()
         side.wait_event(staged)
         with th.cuda.stream(side):
             self._apply_disc_updates(scal, steps)
@@ -1106,7 +1113,6 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         self._global_step += 1
         nxt = None
         if launch_next:
-            self._launch_chain()
             main.wait_event(disc_done)
             reward = not self.debug_use_ground_truth
             self._launch_post(reward)
