@@ -711,3 +711,42 @@ def test_airl_pipelined_rounds_are_bitwise_the_serial_order(monkeypatch):
     for other in runs[1:]:
         bad = [i for i, (a, b) in enumerate(zip(runs[0], other)) if not th.equal(a, b)]
         assert not bad, bad
+
+
+@gpu
+@pytest.mark.parametrize("T,N,count0,int_count", [(1024, 8, 0, False), (1024, 8, 0, True), (300, 3, 5000, True),
+                                                   (64, 4, 17, False)])
+def test_reward_outnorm_scan_matches_serial_reference(T, N, count0, int_count):
+    """reward_outnorm_kernel's wave-level scan of Chan merges (several steps per lane for
+    T > 64) against the per-step serial update in float64: the running (mean, var) each step
+    is normalised with, the final state, and the int32 count path."""
+    from imitation_amd import _native
+
+    C = _native.load()
+    dev = th.device("cuda", 0)
+    rng = np.random.default_rng(T + N)
+    raw = (rng.normal(size=(T, N)) * 3.0 + 1.5).astype(np.float32)
+    boot = (rng.random((T, N)) < 0.05).astype(np.float32) * 0.7
+    m0, v0 = (0.4, 2.0) if count0 else (0.0, 1.0)
+    mean = th.tensor([m0], dtype=th.float32, device=dev)
+    var = th.tensor([v0], dtype=th.float32, device=dev)
+    cnt_f = th.tensor([float(count0)], dtype=th.float32, device=dev)
+    cnt_i = th.tensor(count0, dtype=th.int32, device=dev)
+    rewards = th.empty(T, N, dtype=th.float32, device=dev)
+    C.engine_reward_outnorm(dict(T=T, N=N, rew_raw=th.from_numpy(raw).to(dev), boot=th.from_numpy(boot).to(dev),
+                                 rewards=rewards, mean=mean, var=var, count=cnt_f,
+                                 count_i=cnt_i if int_count else None, eps=1e-8, step_stats=None))
+    th.cuda.synchronize()
+    # serial float64 reference (RunningNorm.update_stats per step, then normalise)
+    m, v, c = float(m0), float(v0), float(count0)
+    expect = np.empty((T, N))
+    for t in range(T):
+        expect[t] = (raw[t] - m) / np.sqrt(v + 1e-8) + boot[t]
+        bm, bv, bn = raw[t].astype(np.float64).mean(), raw[t].astype(np.float64).var(), float(N)
+        d, tot = bm - m, c + bn
+        m, v, c = m + d * bn / tot, (v * c + bv * bn + d * d * c * bn / tot) / tot, tot
+    np.testing.assert_allclose(rewards.cpu().numpy(), expect, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(mean.item(), m, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(var.item(), v, rtol=1e-4)
+    got_c = cnt_i.item() if int_count else cnt_f.item()
+    assert got_c == count0 + T * N
