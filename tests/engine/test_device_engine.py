@@ -750,3 +750,23 @@ def test_reward_outnorm_scan_matches_serial_reference(T, N, count0, int_count):
     np.testing.assert_allclose(var.item(), v, rtol=1e-4)
     got_c = cnt_i.item() if int_count else cnt_f.item()
     assert got_c == count0 + T * N
+
+
+@gpu
+@pytest.mark.parametrize("T,N", [(1024, 8), (512, 3), (100, 5), (2048, 2)])
+def test_gae_scan_register_and_loop_paths_match_reference(T, N):
+    """GAE kernel: the register path (chunks of <= 16 steps, T <= 1024) and the loop path
+    (T = 2048) against the plain PyTorch recurrence, with episode starts and a final done."""
+    from imitation_amd.ops import rl as rl_ops
+
+    g = th.Generator().manual_seed(T * 7 + N)
+    rew = th.randn(T, N, generator=g)
+    val = th.randn(T, N, generator=g)
+    starts = (th.rand(T, N, generator=g) < 0.02).float()
+    last_val = th.randn(N, generator=g)
+    dones = (th.rand(N, generator=g) < 0.5).float()
+    ref_a, ref_r = rl_ops.gae_reference(rew.double(), val.double(), starts.double(), last_val.double(), dones.double(),
+                                        0.99, 0.95)
+    adv, ret = rl_ops.gae(*(x.cuda() for x in (rew, val, starts, last_val, dones)), 0.99, 0.95)
+    np.testing.assert_allclose(adv.cpu().numpy(), ref_a.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(ret.cpu().numpy(), ref_r.numpy(), rtol=1e-4, atol=1e-4)
