@@ -77,6 +77,7 @@ void rollout(py::dict d) {
   TORCH_CHECK(a.pi.dims[0] == a.P.obs_dim, "actor input dim != obs dim");
   TORCH_CHECK(a.pi.dims[a.pi.n_layers] == (a.n_actions > 0 ? a.n_actions : a.P.act_dim), "actor head width");
   a.explore_mode = tptr<const int>(d, "explore_mode", true);
+  a.deterministic = ival(d, "deterministic", 0);
   TORCH_CHECK(a.P.obs_dim <= ia::kEngineMaxObs, "obs dim too large for the device rollout");
   a.obs_buf = tptr<float>(d, "obs_buf");
   a.act_raw = tptr<float>(d, "act_raw");

@@ -172,7 +172,7 @@ py::tuple tmlp_backward_grouped(torch::Tensor x, torch::Tensor dy, std::vector<t
 }
 
 py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch::Tensor last_val, torch::Tensor dones,
-              double gamma, double lam) {
+              double gamma, double lam, c10::optional<torch::Tensor> moments) {
   IA_CHECK_GPU_F32(rew);
   IA_CHECK_GPU_F32(val);
   IA_CHECK_GPU_F32(starts);
@@ -184,9 +184,15 @@ py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch:
   TORCH_CHECK(last_val.numel() == N && dones.numel() == N, "bootstrap shape mismatch");
   auto adv = torch::empty_like(rew);
   auto ret = torch::empty_like(rew);
+  float* mom = nullptr;
+  if (moments && moments->defined()) {
+    IA_CHECK_GPU_F32(*moments);
+    TORCH_CHECK(moments->is_contiguous() && moments->numel() >= 4 * (int64_t)N, "moments must hold [N][4] floats");
+    mom = moments->data_ptr<float>();
+  }
   IA_HIP_CHECK(ia::gae_launch(rew.data_ptr<float>(), val.data_ptr<float>(), starts.data_ptr<float>(),
                               last_val.data_ptr<float>(), dones.data_ptr<float>(), T, N, (float)gamma, (float)lam,
-                              adv.data_ptr<float>(), ret.data_ptr<float>(), ia_stream()));
+                              adv.data_ptr<float>(), ret.data_ptr<float>(), ia_stream(), mom));
   return py::make_tuple(adv, ret);
 }
 
@@ -595,7 +601,7 @@ void register_kernels(py::module& m) {
         py::arg("hidden_act"), py::arg("out_act"), py::arg("norm_mean") = py::none(), py::arg("norm_var") = py::none(),
         py::arg("norm_eps") = 1e-5, py::arg("need_dx") = false);
   m.def("gae", &gae, py::arg("rewards"), py::arg("values"), py::arg("episode_starts"), py::arg("last_values"),
-        py::arg("dones"), py::arg("gamma"), py::arg("lam"));
+        py::arg("dones"), py::arg("gamma"), py::arg("lam"), py::arg("moments") = py::none());
   m.def("adam_flat", &adam_flat, py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"),
         py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
         py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"), py::arg("step_cnt") = py::none());

@@ -1,6 +1,8 @@
 // imitation_amd._C — module definition.
 #include "common.h"
 
+void register_io(py::module& m);  // io.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "imitation_amd native runtime + HIP/CDNA4 kernels (gfx950)";
   m.attr("arch") = "gfx950";
@@ -13,4 +15,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
   register_comm(m);
   register_pref(m);
+  register_io(m);
 }

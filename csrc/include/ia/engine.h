@@ -55,6 +55,9 @@ struct RolloutArgs {
   // optional ExplorationWrapper schedule: explore_mode[t] != 0 -> every env takes a uniform
   // random action at step t (Box.sample / Discrete.sample) instead of the policy's
   const int* explore_mode;  // [T] or nullptr
+  // deterministic actions (evaluation, SB3 predict(deterministic=True)): the Gaussian mean /
+  // the categorical argmax -- the sampling noise is zero
+  int deterministic;
   // outputs, [T][N] (+ trailing feature dim)
   float* obs_buf;
   float* act_raw;   // sampled (unclipped) action, PPO buffer

@@ -301,7 +301,8 @@ hipError_t adam_flat(const AdamArgs& a, hipStream_t s);
 
 // ---- rl.hip: GAE scan over [T, N]
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
-                      int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s);
+                      int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s,
+                      float* mom = nullptr);  // optional [N][4] return / advantage moments
 // E keyed pseudo-random permutations of [0, n) (Feistel + cycle walking), out [E, n] int32
 hipError_t perm_feistel(int E, int n, uint64_t seed, int* out, hipStream_t s);
 // categorical head: log-prob of the taken action + entropy from raw logits [B][A], and the

@@ -150,7 +150,24 @@ enum RcInst : int {
   RC_64_D32,          // the same, obs dim <= 32, ReLU + Gaussian head
 };
 
+static bool rc_inst_is_bf3(int inst) {
+  return inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32 || inst == RC_NS_HOPPER64R || inst == RC_NS_WALKER64R ||
+         inst == RC_NS_64_D16 || inst == RC_NS_64_D32 || inst == RC_CHEETAH32_64 || inst == RC_CARTPOLE32_64;
+}
+
+static int rc_instance_raw(const PPOArgs& a, int kt, int cw, bool ns);
+
+// IMITATION_AMD_PPO_BF3=0: exact-fp32 PPO products. The split-bf16 instances are not selected
+// (the plan then takes a generic fp32 register-chained build, or the LDS kernel where no
+// scratch-free generic build exists -- slower, bit-for-bit the fp32 formulation)
 static int rc_instance(const PPOArgs& a, int kt, int cw, bool ns) {
+  const int inst = rc_instance_raw(a, kt, cw, ns);
+  const char* ev = getenv("IMITATION_AMD_PPO_BF3");
+  if (ev && ev[0] == '0' && rc_inst_is_bf3(inst)) return RC_GENERIC;
+  return inst;
+}
+
+static int rc_instance_raw(const PPOArgs& a, int kt, int cw, bool ns) {
   const int hw = a.pi_dims[1];
   bool uniform = a.n_pi == 3 && a.n_vf == 3;
   for (int l = 1; l < 3 && uniform; ++l) uniform = a.pi_dims[l] == hw && a.vf_dims[l] == hw;
@@ -263,8 +280,7 @@ bool ppo_rc_plan(const PPOArgs& a, PPORcGeo& g, size_t& lds_bytes) {
   if (g.ns && KT == 4 && rc_instance(a, KT, cw, true) == RC_GENERIC) return plan_reject(6);
   {  // the 32-wide specialised net-split builds run the split-bf16 forward / dX (kernel: BF3)
     const int inst = rc_instance(a, KT, cw, g.ns != 0);
-    g.bf3 = (inst == RC_NS_CHEETAH32 || inst == RC_NS_CARTPOLE32 || inst == RC_NS_HOPPER64R || inst == RC_NS_WALKER64R ||
-             inst == RC_NS_64_D16 || inst == RC_NS_64_D32 || inst == RC_CHEETAH32_64 || inst == RC_CARTPOLE32_64) ? 1 : 0;
+    g.bf3 = rc_inst_is_bf3(inst) ? 1 : 0;
   }
   int off = 0;
   auto take = [&](int n) {

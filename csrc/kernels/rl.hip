@@ -27,6 +27,22 @@ namespace ia {
 namespace {
 
 constexpr int kGaeWaves = 4;
+
+// Per-env sums (sum R, sum R^2, sum A, sum A^2) of the returns R and advantages A = R - V:
+// the moments of SB3's train/explained_variance = 1 - Var(R - V) / Var(R), combined on the
+// host from the [N][4] partials (no extra pass over the rollout, no atomics).
+__device__ __forceinline__ void store_moments(float* mom, int n, int lane, float m0, float m1, float m2, float m3) {
+  m0 = wave_sum(m0);
+  m1 = wave_sum(m1);
+  m2 = wave_sum(m2);
+  m3 = wave_sum(m3);
+  if (lane == 0) {
+    mom[4 * n + 0] = m0;
+    mom[4 * n + 1] = m1;
+    mom[4 * n + 2] = m2;
+    mom[4 * n + 3] = m3;
+  }
+}
 constexpr int kGaeRegSteps = 16;  // register fast path: T <= 64 * 16
 
 __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* __restrict__ rew,
@@ -35,7 +51,7 @@ __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* _
                                                                   const float* __restrict__ last_val,
                                                                   const float* __restrict__ dones, int T, int N,
                                                                   float gamma, float lam, float* __restrict__ adv,
-                                                                  float* __restrict__ ret) {
+                                                                  float* __restrict__ ret, float* __restrict__ mom) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * kGaeWaves + (threadIdx.x >> 6);
   if (n >= N) return;  // whole wave exits together
@@ -87,16 +103,23 @@ __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* _
     }
     float a = __shfl_down(SD, 1, 64);
     if (lane == 63) a = 0.f;
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
 #pragma unroll
     for (int i = kGaeRegSteps - 1; i >= 0; --i) {
       const int t = t0 + i;
       a = dl[i] + cl[i] * a;
       if (t < t1) {
         const size_t o = (size_t)t * N + n;
+        const float r = a + vl[i];
         adv[o] = a;
-        ret[o] = a + vl[i];
+        ret[o] = r;
+        m0 += r;
+        m1 += r * r;
+        m2 += a;
+        m3 += a * a;
       }
     }
+    if (mom) store_moments(mom, n, lane, m0, m1, m2, m3);
     return;
   }
   // fold this lane's chunk: a(t0) = D + C * a(t1)
@@ -130,6 +153,7 @@ __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* _
   // carry into this chunk = a(t1) = suffix value of lane + 1 (zero past the end)
   float a = __shfl_down(SD, 1, 64);
   if (lane == 63) a = 0.f;
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
   for (int t = t1 - 1; t >= t0; --t) {
     const size_t o = (size_t)t * N + n;
     float nv, nnt;
@@ -145,7 +169,12 @@ __global__ __launch_bounds__(64 * kGaeWaves) void gae_scan_kernel(const float* _
     a = delta + gl * nnt * a;
     adv[o] = a;
     ret[o] = a + v;
+    m0 += a + v;
+    m1 += (a + v) * (a + v);
+    m2 += a;
+    m3 += a * a;
   }
+  if (mom) store_moments(mom, n, lane, m0, m1, m2, m3);
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -190,11 +219,11 @@ __global__ __launch_bounds__(256) void perm_feistel_kernel(int n, int half_bits,
 }  // namespace
 
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,
-                      int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s) {
+                      int T, int N, float gamma, float lam, float* adv, float* ret, hipStream_t s, float* mom) {
   if (T <= 0 || N <= 0) return hipSuccess;
   const int nblk = (N + kGaeWaves - 1) / kGaeWaves;
   hipLaunchKernelGGL(gae_scan_kernel, dim3(nblk), dim3(64 * kGaeWaves), 0, s, rew, val, starts, last_val, dones, T, N,
-                     gamma, lam, adv, ret);
+                     gamma, lam, adv, ret, mom);
   return hipGetLastError();
 }
 

@@ -409,7 +409,9 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       const uint64_t key = hash3(a.seed, (uint64_t)n, (uint64_t)(a.step0 + t0 + tr));
       uint64_t s = key ^ (kLaneTweak * (uint64_t)(k + 1));
       float v;
-      if (discrete) {  // Gumbel-max: argmax(logits + G) ~ Categorical(softmax(logits))
+      if (a.deterministic) {  // mean / argmax(logits)
+        v = 0.f;
+      } else if (discrete) {  // Gumbel-max: argmax(logits + G) ~ Categorical(softmax(logits))
         const float u = fmaxf(uniform01(s), 1e-12f);
         v = -logf(-logf(u));
       } else {

@@ -409,6 +409,7 @@ class _DPFusedStep:
         self._graphs: Dict[Any, Any] = {}
         self.n_captures = 0
         self.n_replays = 0
+        self._warm: set = set()
 
     def __call__(self, obs: th.Tensor, acts: th.Tensor):
         t = self.trainer
@@ -420,6 +421,15 @@ class _DPFusedStep:
         if f is None:
             return None
         entry = self._graphs.get(key)
+        if entry is None and key not in self._warm:
+            # first call for this shape: one eager step, so that lazily created library /
+            # allocator state is never first made inside a capture (as GraphedTrainStep does)
+            self._warm.add(key)
+            f(obs, acts)
+            t._grad_bucket.allreduce()
+            t.optimizer.step()
+            self.n_replays += 1
+            return BCTrainingMetrics(**bc_cnn.metrics_fields(f.metrics))
         if entry is None:
             static = tuple(x if getattr(x, "_ia_static", False) else x.detach().clone() for x in (obs, acts))
             side = th.cuda.Stream()
@@ -496,6 +506,9 @@ class _DeviceEpochRunner:
             self.cursor = th.zeros(1, dtype=th.int32, device=dev)
             self._cap = cap
         self._key = key
+        self.graphs = None  # captured by the next _run, after the eager warm-up step
+
+    def _capture(self) -> None:
         self.graphs = {}
         side = th.cuda.Stream()
         side.wait_stream(th.cuda.current_stream())
@@ -508,6 +521,14 @@ class _DeviceEpochRunner:
         th.cuda.current_stream().wait_stream(side)
 
     def _run(self, steps: int) -> None:
+        if steps > 0 and not getattr(self, "_warm", False):
+            # the first step runs eagerly (same kernels, so the same result): lazily created
+            # library / allocator state is never first made inside a capture
+            self._one_step()
+            self._warm = True
+            steps -= 1
+        if steps > 0 and self.graphs is None:
+            self._capture()
         for _ in range(steps // self.K):
             self.graphs[self.K].replay()
         for _ in range(steps % self.K):
@@ -623,10 +644,21 @@ class MultiBC(_BCBase):
         return obs, acts
 
 
-def _column_map(fn, i: int, ncols: int, dtype) -> Optional[Tuple[List[int], bool]]:
+def _column_map(fn, i: int, ncols: int, dtype, one_d: bool = False) -> Optional[Tuple[List[int], bool]]:
     """If ``fn(i, x)`` selects columns of a 2-D ``x`` (same selection for every row), the
     selected column ids and whether the result is 1-D; else None. Probed on a tiny host tensor
-    whose entries encode (row, column)."""
+    whose entries encode (row, column). ``one_d``: ``x`` is 1-D (``[B]`` actions); only the
+    identity selection ``fn(i, x) == x`` is folded then. The probe is a candidate only: the
+    caller confirms it on real rows (:func:`_confirm_column_map`)."""
+    if one_d:
+        probe = th.tensor([0, 1], dtype=dtype)
+        try:
+            out = fn(i, probe)
+        except Exception:  # noqa: BLE001 -- arbitrary user callable
+            return None
+        if not isinstance(out, th.Tensor) or out.shape != probe.shape or not th.equal(out.to(dtype), probe):
+            return None
+        return [0], True
     probe = (th.arange(ncols, dtype=th.int64)[None, :] + th.tensor([[0], [ncols]])).to(dtype)
     try:
         out = fn(i, probe)
@@ -641,6 +673,20 @@ def _column_map(fn, i: int, ncols: int, dtype) -> Optional[Tuple[List[int], bool
     if any(c < 0 or c >= ncols for c in cols):
         return None
     return cols, out.dim() == 1
+
+
+def _confirm_column_map(fn, i: int, rows: th.Tensor, m: Tuple[List[int], bool]) -> bool:
+    """``fn(i, rows)`` equals the gather the column map ``m`` implies, values and shape, on real
+    demonstration rows (a probe alone accepts e.g. agent-dependent in-range shifts)."""
+    cols, is_1d = m
+    want = rows if rows.dim() == 1 else rows[:, cols]
+    if is_1d and want.dim() == 2:
+        want = want.reshape(-1)
+    try:
+        out = fn(i, rows.clone())
+    except Exception:  # noqa: BLE001
+        return False
+    return isinstance(out, th.Tensor) and out.shape == want.shape and th.equal(out.to(want.dtype), want)
 
 
 class _AgentGatherLoader:
@@ -674,12 +720,19 @@ class _AgentGatherLoader:
         if obs.ndim != 2 or acts.ndim not in (1, 2) or len(obs) < batch_size:
             return None
         acts2 = acts.reshape(len(acts), -1)
+        adt = th.int64 if np.issubdtype(acts.dtype, np.integer) else th.float32
         om = [_column_map(obs_fn, i, obs.shape[1], th.float32) for i in range(n_agents)]
-        am = [_column_map(act_fn, i, acts2.shape[1], th.int64 if np.issubdtype(acts.dtype, np.integer) else th.float32)
-              for i in range(n_agents)]
+        am = [_column_map(act_fn, i, acts2.shape[1], adt, one_d=acts.ndim == 1) for i in range(n_agents)]
         if any(m is None for m in om + am) or len({len(m[0]) for m in om}) != 1 or len({(len(m[0]), m[1]) for m in am}) != 1:
             return None
         if any(m[1] for m in om):
+            return None
+        # confirm every candidate map on real rows (the host loader is the fallback)
+        k = min(len(obs), 64)
+        o_rows = th.from_numpy(np.array(obs[:k], dtype=np.float32))
+        a_rows = th.from_numpy(np.array(acts[:k])).to(adt)
+        if not all(_confirm_column_map(obs_fn, i, o_rows, om[i]) and _confirm_column_map(act_fn, i, a_rows, am[i])
+                   for i in range(n_agents)):
             return None
         o = th.as_tensor(obs, device=device).float()
         a = th.as_tensor(acts2, device=device)

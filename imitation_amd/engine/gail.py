@@ -270,7 +270,11 @@ class DeviceGeneratorCore:
                         rewards=z(T, N), env_rew=z(T, N), starts=z(T, N), dones=z(T, N), trunc=z(T, N), boot=z(T, N),
                         next_obs=z(T, N, D), ep_ret_out=z(T, N), last_values=z(N))
         self._boot = self.buf["boot"]
-        self.stats = z(5)
+        # PPO statistics sums (kernel output) followed by the GAE pass's [N][4] return /
+        # advantage moments (train/explained_variance): ONE device buffer, one D2H copy per round
+        self._log_dev = z(5 + 4 * N)
+        self.stats = self._log_dev[:5]
+        self._ev_mom = self._log_dev[5:].view(N, 4)
         self._seed = int(np.random.randint(0, 2**62)) ^ (pdist.rank() * 0x9E3779B97F4A7C15 & ((1 << 62) - 1))
         self._step0 = 0
         self._perm_round = 0
@@ -396,7 +400,9 @@ class DeviceGeneratorCore:
         lr = float(algo.lr_schedule(algo._current_progress_remaining))
         clip = float(algo.clip_range(algo._current_progress_remaining))
         adv, ret = rl_ops.gae(self.buf["rewards"], self.buf["values"], self.buf["starts"], self.buf["last_values"],
-                              self.cur_start, float(algo.gamma), float(algo.gae_lambda))
+                              self.cur_start, float(algo.gamma), float(algo.gae_lambda), moments=self._ev_mom)
+        self._last_clip_range = clip
+        self._last_lr = lr
         obs = self.buf["obs_buf"].reshape(rows, self.D)
         acts = self.buf["act_raw"].reshape(rows, -1)
         old_logp = self.buf["logp"].reshape(rows)
@@ -436,6 +442,74 @@ class DeviceGeneratorCore:
         self._ppo_err.check("PPO update")
         algo._n_updates += algo.n_epochs
         self._last_ppo_info = (rows, algo.n_epochs * (rows // algo.batch_size))
+        self._stage_ppo_logs()
+
+    def _stage_ppo_logs(self) -> None:
+        """Async D2H copy (stream order: right behind the update) of the update's statistics, the
+        explained-variance moments and log_std into pinned memory; :meth:`_ppo_log_values` reads
+        them after the copy event -- no blocking read of device tensors at logging time (the next
+        round may already be enqueued behind the update)."""
+        if getattr(self, "_ppo_log_host", None) is None:
+            self._ppo_log_host = th.zeros(self._log_dev.numel(), pin_memory=True)
+            self._ppo_std_host = th.zeros(self.A, pin_memory=True) if self.has_log_std else None
+        self._ppo_log_host.copy_(self._log_dev, non_blocking=True)
+        if self._ppo_std_host is not None:
+            self._ppo_std_host.copy_(self.gen_algo.policy.log_std.detach().reshape(-1), non_blocking=True)
+        self._ppo_log_event = th.cuda.Event()
+        self._ppo_log_event.record()
+
+    def _record_round_metrics(self) -> None:
+        """The host PPO's per-round records (``rl/ppo.py`` ``train`` + ``rl/base.py``
+        ``_dump_logs``) for one device round."""
+        algo = self.gen_algo
+        lg = self.logger
+        vals = self._ppo_log_values()
+        self._fail_if_nonfinite({k: v for k, v in vals.items() if k != "train/explained_variance"}, "PPO update")
+        for k, v in vals.items():
+            lg.record(k, v)
+        lg.record("train/n_updates", algo._n_updates, exclude="tensorboard")
+        now = time.perf_counter()
+        t_prev, n_prev = getattr(self, "_fps_mark", (None, None))
+        if t_prev is not None and now > t_prev and algo.num_timesteps > n_prev:
+            dt = now - t_prev
+            lg.record("time/fps", int((algo.num_timesteps - n_prev) / dt))
+            lg.record("time/time_elapsed", int(dt), exclude="tensorboard")
+        self._fps_mark = (now, algo.num_timesteps)
+        lg.record("time/iterations", 1, exclude="tensorboard")
+        lg.record("time/total_timesteps", algo.num_timesteps, exclude="tensorboard")
+        if algo.ep_info_buffer:
+            lg.record("rollout/ep_rew_mean", float(np.mean([e["r"] for e in algo.ep_info_buffer])))
+            lg.record("rollout/ep_len_mean", float(np.mean([e["l"] for e in algo.ep_info_buffer])))
+
+    def _fail_if_nonfinite(self, values: Mapping[str, float], what: str) -> None:
+        """Fail fast (the reference raises on broken invariants, e.g.
+        ``algorithms/base.py:77-110``): the round's statistics are already on the host, so this
+        costs no device sync. A NaN / Inf loss means the weights it came from are poisoned."""
+        bad = [k for k, v in values.items() if not np.isfinite(v)]
+        if bad:
+            from imitation_amd.utils.watchdog import NonFiniteError
+
+            rnd = getattr(self, "_global_step", None)
+            raise NonFiniteError(f"non-finite {what} statistics{'' if rnd is None else f' in round {rnd}'}: "
+                                 f"{', '.join(bad)}")
+
+    def _ppo_log_values(self) -> Dict[str, float]:
+        """SB3 ``PPO.train`` metrics of the latest update (reference keys, ``rl/ppo.py``): means of
+        the per-minibatch sums, ``train/loss`` from those means (SB3 logs the last minibatch's),
+        explained variance of the round's values vs GAE returns, std of the Gaussian head."""
+        self._ppo_log_event.synchronize()
+        algo: PPO = self.gen_algo
+        h = self._ppo_log_host.numpy()
+        rows, n_mb = self._last_ppo_info
+        s = h[:5] / max(1, n_mb)
+        out = {"train/entropy_loss": float(s[0]), "train/policy_gradient_loss": float(s[1]),
+               "train/value_loss": float(s[2]), "train/clip_fraction": float(s[3]), "train/approx_kl": float(s[4]),
+               "train/loss": float(s[1] + algo.ent_coef * s[0] + algo.vf_coef * s[2]),
+               "train/explained_variance": rl_ops.explained_variance_from_moments(h[5:], rows),
+               "train/clip_range": float(self._last_clip_range), "train/learning_rate": float(self._last_lr)}
+        if self._ppo_std_host is not None:
+            out["train/std"] = float(np.exp(self._ppo_std_host.numpy()).mean())
+        return out
 
     def check_errors(self, blocking: bool = False) -> None:
         """Raise if a cooperating PPO workgroup timed out in any update so far."""
@@ -505,6 +579,65 @@ class DeviceGeneratorCore:
         norm.running_var.copy_(rv / tot)
         self.norm_count.add_(cnt)
 
+    def device_evaluate(self, n_eval_episodes: int = 10, deterministic: bool = True, n_envs: Optional[int] = None,
+                        seed: int = 0) -> Tuple[List[float], List[int]]:
+        """``evaluate_policy(policy, venv, n_eval_episodes, deterministic, return_episode_rewards=True)``
+        on the GPU (reference ``stable_baselines3.common.evaluation.evaluate_policy``, the metric
+        of ``scripts/ingredients/policy_evaluation.py``): a separate block of ``n_envs`` native
+        envs (default: the training count) reset from ``seed`` and stepped by the rollout chain
+        kernel with the current policy (mean / argmax actions when ``deterministic``), one
+        ``max_episode_steps`` launch per episode slot -- no host round trip per step. Env ``i``
+        contributes its first ``(n_eval_episodes + i) // n_envs`` episodes, as SB3 counts them;
+        returns (episode returns, episode lengths) in completion order. The training envs, the
+        policy and every normaliser are untouched."""
+        from imitation_amd.envs.vec_env import NativeVecEnv
+
+        dev = self._dev
+        n = int(n_envs or self.N)
+        targets = np.array([(n_eval_episodes + i) // n for i in range(n)], dtype=np.int64)
+        n_chunks = int(targets.max(initial=0))
+        if n_chunks == 0:
+            return [], []
+        ev = NativeVecEnv(self._native.env_id, n, seed=int(seed), max_episode_steps=self.max_steps)
+        obs0 = ev.reset()
+        st = ev.get_state()
+        T = self.max_steps  # every env finishes >= 1 episode per launch (TimeLimit)
+        Aw = 1 if self.discrete else self.A
+        z = lambda *s: th.zeros(*s, device=dev)  # noqa: E731
+        scratch = dict(obs_buf=z(T, n, self.D), act_raw=z(T, n, Aw), act_env=z(T, n, Aw), env_rew=z(T, n),
+                       starts=z(T, n), trunc=z(T, n), next_obs=z(T, n, self.D))
+        dones = z(n_chunks, T, n)
+        rets = z(n_chunks, T, n)
+        pol = self.gen_algo.policy
+        args = dict(env=self._native.env_id, max_steps=self.max_steps, T=T, N=n, seed=int(seed) * 0x2545F4914F6CDD1D & ((1 << 62) - 1),
+                    state=th.as_tensor(st["state"], device=dev).float().contiguous(),
+                    rng=th.as_tensor(st["rng"].astype(np.int64), device=dev).contiguous(),
+                    elapsed=th.as_tensor(st["elapsed"].astype(np.int32), device=dev).contiguous(), ep_ret=z(n),
+                    cur_obs=th.as_tensor(np.asarray(obs0, np.float32), device=dev).reshape(n, self.D).contiguous(),
+                    cur_start=th.ones(n, device=dev),
+                    pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
+                    log_std=pol.log_std.detach() if self.has_log_std else None, act_low=self.act_low,
+                    act_high=self.act_high, n_actions=self.A if self.discrete else 0, deterministic=int(deterministic),
+                    **scratch)
+        for c in range(n_chunks):
+            args.update(step0=c * T, dones=dones[c], ep_ret_out=rets[c])
+            self._C.engine_rollout(args)
+        d = dones.reshape(n_chunks * T, n).cpu().numpy() > 0.5
+        r = rets.reshape(n_chunks * T, n).cpu().numpy()
+        ts, es = np.nonzero(d)  # row-major: completion step, then env
+        ep_rewards: List[float] = []
+        ep_lengths: List[int] = []
+        last = np.full(n, -1, dtype=np.int64)
+        count = np.zeros(n, dtype=np.int64)
+        for t, e in zip(ts.tolist(), es.tolist()):
+            length = t - last[e]
+            last[e] = t
+            if count[e] < targets[e]:
+                ep_rewards.append(float(r[t, e]))
+                ep_lengths.append(int(length))
+                count[e] += 1
+        return ep_rewards, ep_lengths
+
     def sync_env_to_host(self) -> None:
         """Copy the device env state back into the native host env (e.g. before host-side evaluation)."""
         self._native.set_state({"state": self.state.cpu().numpy(), "rng": self.env_rng.cpu().numpy(),
@@ -513,8 +646,9 @@ class DeviceGeneratorCore:
     def _stage_rollout_to_host(self):
         """Async D2H copy of (dones, episode returns) into pinned buffers; returns the event
         that marks them ready."""
+        wrapped = not self.debug_use_ground_truth
         if not hasattr(self, "_host_stage"):
-            self._host_stage = th.empty(2, self.T, self.N, pin_memory=True)
+            self._host_stage = th.empty(4 if wrapped else 2, self.T, self.N, pin_memory=True)
         # on the side stream: the copies stay off the rollout -> GAE -> PPO chain (the host
         # waits for this event before the next rollout can overwrite the buffers)
         side = getattr(self, "_side_stream", None)
@@ -523,6 +657,9 @@ class DeviceGeneratorCore:
         with th.cuda.stream(side) if side is not None else contextlib.nullcontext():
             self._host_stage[0].copy_(self.buf["dones"], non_blocking=True)
             self._host_stage[1].copy_(self.buf["ep_ret_out"], non_blocking=True)
+            if wrapped:  # learned reward = rewards - TimeLimit bootstrap (RewardVecEnvWrapper's rews)
+                self._host_stage[2].copy_(self.buf["rewards"], non_blocking=True)
+                self._host_stage[3].copy_(self._boot, non_blocking=True)
             ev = th.cuda.Event()
             ev.record()
         self._host_staged = True
@@ -602,14 +739,18 @@ class DeviceEngineMixin(DeviceGeneratorCore):
 
     def _store_generator_samples(self) -> None:
         """Replay-buffer content identical to BufferingWrapper -> flatten -> FIFO store."""
+        wrapped_rew = None
         if getattr(self, "_host_staged", False):
             dones = self._host_stage[0].numpy().astype(bool)
             ep_ret_host = self._host_stage[1].numpy()
+            if self._host_stage.shape[0] == 4:
+                wrapped_rew = self._host_stage[2].numpy() - self._host_stage[3].numpy()
             self._host_staged = False
         else:
             dones = self.buf["dones"].to("cpu", non_blocking=False).numpy().astype(bool)  # [T, N] (one sync / round)
             ep_ret_host = None
         T, N = dones.shape
+        self._track_wrapped_returns(dones, wrapped_rew)
         order, fin_t, fin_n, ep_lens, self._ep_lens_running = flatten_order(dones, self._ep_lens_running)
         cap = self._gen_dev.capacity
         # pinned + non-blocking: a pageable H2D copy would block the host until the stream
@@ -643,6 +784,40 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             for t, n, l_full in zip(fin_t.tolist(), fin_n.tolist(), local_lens):
                 algo.ep_info_buffer.append({"r": float(ep_ret[t, n]), "l": int(l_full), "t": 0.0})
 
+    def _track_wrapped_returns(self, dones: np.ndarray, rew: Optional[np.ndarray]) -> None:
+        """``RewardVecEnvWrapper`` episode bookkeeping (reference ``rewards/reward_wrapper.py:15-37,
+        92-133``): per-env running sums of the learned reward, a deque of the last 100 finished
+        episodes' sums; ``rollout/ep_rew_wrapped_mean`` is its mean at the START of the rollout
+        (``WrappedRewardCallback._on_rollout_start``), i.e. before this round's episodes."""
+        import collections
+
+        if getattr(self, "_wrapped_eps", None) is None:
+            self._wrapped_eps = collections.deque(maxlen=100)
+            self._wrapped_cum = np.zeros(dones.shape[1], dtype=np.float64)
+        eps = self._wrapped_eps
+        self._wrapped_mean_at_start = (sum(eps) / len(eps)) if eps else None
+        if rew is None:
+            return
+        T, N = dones.shape
+        cs = np.cumsum(rew.astype(np.float64), axis=0)  # [T, N] running sums within the round
+        fin_t, fin_n = np.nonzero(dones)  # completion order: step, then env (the wrapper's loop)
+        prev = np.full(N, -1, dtype=np.int64)
+        vals = np.empty(len(fin_t), dtype=np.float64)
+        for n in range(N):  # per env: segment sums between consecutive dones (+ the carry)
+            sel = np.flatnonzero(fin_n == n)
+            if not len(sel):
+                continue
+            t = fin_t[sel]
+            before = np.concatenate(([0.0], cs[t[:-1], n]))
+            v = cs[t, n] - before
+            v[0] += self._wrapped_cum[n]
+            vals[sel] = v
+            prev[n] = t[-1]
+        eps.extend(vals.tolist())
+        last = np.where(prev >= 0, cs[T - 1] - np.where(prev >= 0, cs[np.maximum(prev, 0), np.arange(N)], 0.0),
+                        self._wrapped_cum + cs[T - 1])
+        self._wrapped_cum = last
+
     def _gen_sample(self, batch_size: int) -> Dict[str, th.Tensor]:
         if self._gen_dev.size() == 0:
             raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
@@ -670,21 +845,17 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             self._log_gen()
 
     def _log_gen(self, stats: Optional[th.Tensor] = None) -> None:
-        """Record the PPO update's statistics (``stats``: an already-fetched host copy)."""
-        algo = self.gen_algo
-        src = self.stats if stats is None else stats
-        s = (src / max(1, self._last_ppo_info[1])).tolist()
-        lg = self.logger
-        lg.record("train/entropy_loss", s[0])
-        lg.record("train/policy_gradient_loss", s[1])
-        lg.record("train/value_loss", s[2])
-        lg.record("train/clip_fraction", s[3])
-        lg.record("train/approx_kl", s[4])
-        lg.record("train/n_updates", algo._n_updates)
-        lg.record("time/total_timesteps", algo.num_timesteps)
-        if algo.ep_info_buffer:
-            lg.record("rollout/ep_rew_mean", float(np.mean([e["r"] for e in algo.ep_info_buffer])))
-            lg.record("rollout/ep_len_mean", float(np.mean([e["l"] for e in algo.ep_info_buffer])))
+        """Record one generator round with the host trainer's key set: SB3 ``PPO.train`` metrics
+        (:meth:`_ppo_log_values`), ``OnPolicyAlgorithm._dump_logs`` (``time/*``, Monitor
+        ``rollout/ep_*_mean``) and the reward wrapper's ``rollout/ep_rew_wrapped_mean``
+        (reference ``adversarial/common.py:234-240, 414-419``). ``time/fps``: env steps per
+        second of wall time since the previous round's record (the round's sustained rate; the
+        reference's per-round ``learn`` call gives the same quantity). ``stats`` is unused (kept
+        for callers that pass the old host copy)."""
+        self._record_round_metrics()
+        wm = getattr(self, "_wrapped_mean_at_start", None)
+        if wm is not None:
+            self.logger.record("rollout/ep_rew_wrapped_mean", float(wm))
 
     # ------------------------------------------------------------------ fused discriminator update
     def _fused_disc_check(self) -> Tuple[bool, str]:
@@ -959,6 +1130,8 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                     steps.append(self._disc_step)
             vals = self._disc_stats_gen[:n].tolist() if n else []  # one host sync per round
             pdist.check_comm("adversarial round")
+            self._fail_if_nonfinite({f"update {i} sum {j}": float(v) for i in range(n) for j, v in enumerate(vals[i])},
+                                    "discriminator")
             for i in range(n):
                 with self.logger.accumulate_means("disc"):
                     self._record_disc(common.train_stats_from_sums(vals[i], rows), steps[i])
@@ -966,6 +1139,14 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 callback(r)
             self.logger.dump(self._global_step)
         self.check_errors(blocking=True)
+
+    #: Keep the round pipeline when ``train`` is given a callback: round ``r + 1``'s rollout
+    #: (chain + reward pass) is already enqueued when ``callback(r)`` runs. The callback sees
+    #: round ``r``'s final weights and may read (e.g. checkpoint) any state; it must not mutate
+    #: the env state, the policy or the reward net in place (the in-flight rollout reads them).
+    #: The CLI's checkpoint callback (reference ``scripts/train_adversarial.py:156-160``) only
+    #: saves. False: every callback runs with the device idle, as a host-loop trainer would.
+    pipeline_callbacks = True
 
     def train(self, total_timesteps: int, callback=None) -> None:
         """Rounds of device generator training + fused discriminator updates; the
@@ -984,11 +1165,13 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             self._disc_stats_host = th.zeros(n, 8, pin_memory=True)
         overlap = self._overlap_disc and n > 0 and self.gen_train_timesteps == self.T * self.N
         nxt = None
+        self._fps_mark = (time.perf_counter(), self.gen_algo.num_timesteps)
         for r in range(n_rounds):
             if overlap:
-                # without a callback nothing observes the state between rounds, so the next
-                # rollout is enqueued before this round's logging
-                steps, nxt = self._overlapped_round(n, nxt, launch_next=callback is None and r + 1 < n_rounds)
+                # the next rollout is enqueued before this round's logging and callback (see
+                # pipeline_callbacks), so the device never waits for the host between rounds
+                launch = r + 1 < n_rounds and (callback is None or self.pipeline_callbacks)
+                steps, nxt = self._overlapped_round(n, nxt, launch_next=launch)
                 vals = self._disc_stats_host[:n].tolist()
             else:
                 self.train_gen(self.gen_train_timesteps)
@@ -1000,6 +1183,8 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 vals = self._disc_stats[:n].tolist() if n else []
             pdist.check_comm("GAIL round")
             if n:
+                self._fail_if_nonfinite({f"update {i} sum {j}": float(v) for i in range(n) for j, v in enumerate(vals[i][:6])},
+                                        "discriminator")
                 for i in range(n):
                     with self.logger.accumulate_means("disc"):
                         self._record_disc(self._disc_stats_dict(vals[i]), steps[i])
@@ -1041,8 +1226,6 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         # the same one-shot communicator as the disc, and two kernels in flight on it would
         # pair one rank's PPO gradients with another rank's disc sums
         serial = (pol_merge and not defer) or (pdist.world_size() > 1 and not self._dp_replicated)
-        if not hasattr(self, "_ppo_stats_host"):
-            self._ppo_stats_host = th.zeros(self.stats.numel(), pin_memory=True)
         steps: List[int] = []
         nxt = None
         # AIRL split rounds: the updates' gathers + norm merges (the only part the next rollout's
@@ -1058,7 +1241,6 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 ready = self._launch_rollout()
             algo.num_timesteps += self.T * self.N
             self._ppo_update()
-            self._ppo_stats_host.copy_(self.stats, non_blocking=True)
             ppo_done = th.cuda.Event()
             ppo_done.record(main)
             ready.synchronize()
@@ -1084,7 +1266,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             if launch_next:
                 nxt = self._launch_rollout()
             ppo_done.synchronize()
-            self._log_gen(self._ppo_stats_host)
+            self._log_gen()
         disc_done.synchronize()
         return steps, nxt
 
@@ -1122,7 +1304,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         else:
             main.wait_event(disc_done)
         ppo_done.synchronize()
-        self._log_gen(self._ppo_stats_host)
+        self._log_gen()
         disc_done.synchronize()
         return steps, nxt
 
@@ -1137,6 +1319,9 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             if self.pol_norm is not None:  # (the single-rank update keeps the module's count only)
                 self.norm_count.copy_(self.pol_norm.count.reshape(1))
             st["norm_count"] = self.norm_count.cpu().clone()
+        if getattr(self, "_wrapped_eps", None) is not None:
+            st["wrapped_eps"] = th.tensor(list(self._wrapped_eps), dtype=th.float64)
+            st["wrapped_cum"] = th.as_tensor(self._wrapped_cum, dtype=th.float64)
         st.update(step0=int(self._step0), seed=int(self._seed), perm_round=int(self._perm_round), ep_lens_running=th.as_tensor(self._ep_lens_running),
                   gen_dev={k: v.cpu().clone() for k, v in self._gen_dev._arrays.items()},
                   gen_dev_idx=int(self._gen_dev._idx), gen_dev_n=int(self._gen_dev._n_data))
@@ -1153,6 +1338,11 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         self._step0, self._seed = st["step0"], st["seed"]
         self._perm_round = int(st.get("perm_round", 0))
         self._ep_lens_running = st["ep_lens_running"].numpy().copy()
+        if "wrapped_eps" in st:
+            import collections
+
+            self._wrapped_eps = collections.deque(st["wrapped_eps"].tolist(), maxlen=100)
+            self._wrapped_cum = st["wrapped_cum"].numpy().copy()
         self._gen_dev._idx, self._gen_dev._n_data = st["gen_dev_idx"], st["gen_dev_n"]
         self.sync_env_to_host()
 

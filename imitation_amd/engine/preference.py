@@ -33,6 +33,7 @@ BufferingWrapper's (obs incl. terminal obs, clipped env actions, env rewards,
 from __future__ import annotations
 
 import math
+import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -271,6 +272,7 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
         n_rounds = max(1, math.ceil(steps / per_round))
         target = algo.num_timesteps + n_rounds * per_round
         algo._total_timesteps = max(algo._total_timesteps or 0, target)
+        self._fps_mark = (time.perf_counter(), algo.num_timesteps)
         for _ in range(n_rounds):
             self._rollout()
             ready = self._stage()
@@ -282,15 +284,8 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
 
     def _log_round(self) -> None:
         algo = self.gen_algo
-        s = (self.stats / max(1, self._last_ppo_info[1])).tolist()
         lg = self.logger
-        lg.record("train/entropy_loss", s[0])
-        lg.record("train/policy_gradient_loss", s[1])
-        lg.record("train/value_loss", s[2])
-        lg.record("train/clip_fraction", s[3])
-        lg.record("train/approx_kl", s[4])
-        lg.record("train/n_updates", algo._n_updates)
-        lg.record("time/total_timesteps", algo.num_timesteps)
+        self._record_round_metrics()
         ep = self.reward_venv_wrapper.episode_rewards
         if len(ep):
             lg.record("rollout/ep_rew_wrapped_mean", float(np.mean(ep)))

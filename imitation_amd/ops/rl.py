@@ -9,7 +9,7 @@ orders without a sort (keyed Feistel bijections).
 
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 
@@ -32,7 +32,11 @@ def gae_reference(rewards, values, episode_starts, last_values, dones, gamma: fl
     return adv, adv + values
 
 
-def gae(rewards, values, episode_starts, last_values, dones, gamma: float, lam: float) -> Tuple[torch.Tensor, torch.Tensor]:
+def gae(rewards, values, episode_starts, last_values, dones, gamma: float, lam: float,
+        moments: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """GAE(γ, λ) advantages and returns. ``moments`` (optional ``[N, 4]`` fp32): per-env sums
+    (ΣR, ΣR², ΣA, ΣA²) of the returns R and advantages A = R - V, for
+    :func:`explained_variance_from_moments` (written by the same kernel pass)."""
     from imitation_amd.ops import native, use_kernel
 
     if use_kernel(rewards) and rewards.dtype == torch.float32:
@@ -45,8 +49,23 @@ def gae(rewards, values, episode_starts, last_values, dones, gamma: float, lam: 
             dones.contiguous().float(),
             float(gamma),
             float(lam),
+            moments,
         )
-    return gae_reference(rewards, values, episode_starts, last_values, dones, gamma, lam)
+    adv, ret = gae_reference(rewards, values, episode_starts, last_values, dones, gamma, lam)
+    if moments is not None:
+        moments.view(-1, 4).copy_(torch.stack([ret.sum(0), ret.square().sum(0), adv.sum(0), adv.square().sum(0)], 1))
+    return adv, ret
+
+
+def explained_variance_from_moments(moments, rows: int) -> float:
+    """SB3 ``explained_variance(values, returns)`` = 1 - Var(R - V) / Var(R) (population
+    variances) from the per-env moment sums of :func:`gae`; NaN when Var(R) == 0."""
+    import numpy as np
+
+    m = np.asarray(moments, dtype=np.float64).reshape(-1, 4).sum(0)
+    var_r = m[1] / rows - (m[0] / rows) ** 2
+    var_a = m[3] / rows - (m[2] / rows) ** 2
+    return float("nan") if var_r == 0 else float(1.0 - var_a / var_r)
 
 
 _M64 = (1 << 64) - 1

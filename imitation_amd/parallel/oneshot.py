@@ -124,30 +124,70 @@ class OneShotComm:
         return int(self._C.oneshot_blocks(int(n), self.stage_bytes))
 
     def self_test(self) -> bool:
-        """Reduce a few rank-dependent buckets (odd sizes, both staging parities, in- and
-        out-of-place) and compare with the closed form; agree on the verdict over ranks."""
-        ok = True
-        saved, self.timeout_s = self.timeout_s, min(self.timeout_s, 5.0)  # a broken mapping fails fast
+        return self.self_test_report()[0]
+
+    def self_test_report(self):
+        """Start-up check before any gradient goes through this communicator: ``(ok, reason)``,
+        agreed over ranks (every rank returns the same verdict).
+
+        1. closed form: rank-dependent buckets (odd sizes, both staging parities) against
+           ``sum_r``, with the device error word clear;
+        2. cross-check against the process group (RCCL): the same rank-distinct buckets reduced
+           by ``torch.distributed.all_reduce``. Exactly representable values (small integers +
+           halves) make every summation order exact, so the two must be BITWISE equal; a second,
+           non-dyadic bucket must agree to rounding (a wrong row / rank mapping shows as O(1)
+           differences).
+        The bounded waits use a 5 s timeout here, so a broken peer mapping fails fast (the kernel
+        then poisons its output and sets the error word)."""
+        reasons = []
+        saved, self.timeout_s = self.timeout_s, min(self.timeout_s, 5.0)
         try:
+            # (every rank runs every step whatever it found so far: the collective sequence
+            # must stay identical on all ranks until the verdict is agreed)
+            w = self.world
             for n in (1, 5, 1027, min(self.stage_bytes // 4, 16384 + 3)):
                 for rep in range(2):
                     x = torch.arange(n, dtype=torch.float32, device=self.device) * (self.rank + 1) + rep
                     self.allreduce_(x)
-                    w = self.world
                     exp = torch.arange(n, dtype=torch.float32, device=self.device) * (w * (w + 1) / 2) + rep * w
-                    ok = ok and bool(torch.allclose(x, exp, rtol=1e-6, atol=1e-3)) and self.error() == 0
-                    if not ok:
-                        break
-                if not ok:
-                    break
+                    if not bool(torch.allclose(x, exp, rtol=1e-6, atol=1e-3)) and not reasons:
+                        reasons.append(f"closed-form mismatch at n={n}")
+            n = min(self.stage_bytes // 4, 4099)
+            g = torch.Generator().manual_seed(1234 + self.rank)
+            exact = (torch.randint(-512, 512, (n,), generator=g).float() + 0.5 * (self.rank % 2)).to(self.device)
+            fuzzy = torch.randn(n, generator=g).to(self.device)
+            for name, t in (("exact", exact), ("fuzzy", fuzzy)):
+                mine = t.clone()
+                self.allreduce_(mine)
+                ref = self._reference_allreduce(t)
+                if name == "exact" and not torch.equal(mine, ref):
+                    reasons.append("not bitwise equal to the process-group all-reduce on exactly representable data")
+                if name == "fuzzy" and not bool(torch.allclose(mine, ref, rtol=1e-5, atol=1e-5 * w)):
+                    reasons.append("differs from the process-group all-reduce beyond rounding")
+        except Exception as e:  # noqa: BLE001 -- any failure disables the path
+            reasons.append(f"raised {e!r}")
         finally:
             self.timeout_s = saved
-        torch.cuda.synchronize(self.device)
-        ok = ok and self.error() == 0
-        return _agree(ok, self.device)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        try:
+            if self.error() != 0:
+                reasons.append("a bounded peer wait timed out (error word set)")
+        except Exception as e:  # noqa: BLE001
+            reasons.append(f"error word unreadable: {e!r}")
+        ok = _agree(not reasons, self.device)
+        if not ok and not reasons:
+            reasons.append("failed on another rank")
+        return ok, "; ".join(reasons)
+
+    def _reference_allreduce(self, t: torch.Tensor) -> torch.Tensor:
+        ref = t.clone() if tdist.get_backend() == "nccl" else t.detach().cpu().clone()
+        tdist.all_reduce(ref)
+        return ref.to(self.device)
 
     def close(self) -> None:
-        torch.cuda.synchronize(self.device)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         for p in self._opened:
             self._C.oneshot_close(p)
         self._opened = []
@@ -209,19 +249,38 @@ def get() -> Optional[OneShotComm]:
     comm = None
     try:
         comm = OneShotComm(C, tdist.get_rank(), world, dev, stage, timeout)
-        ok = comm.self_test()
-    except Exception:  # IPC unavailable on this node: keep torch.distributed
-        ok = False
+    except Exception as e:  # IPC unavailable on this node: keep torch.distributed
         if mode not in ("auto",):
             raise
-    if not ok:
-        if comm is not None:
-            comm.close()
-        if mode not in ("auto",):
-            raise RuntimeError("one-shot all-reduce self-test failed")
+        _disable(f"set-up failed: {e!r}")
         return None
-    _COMM = comm
+    _COMM = adopt(comm, mode)
     return _COMM
+
+
+DISABLED_REASON: Optional[str] = None
+
+
+def _disable(reason: str) -> None:
+    global DISABLED_REASON
+    DISABLED_REASON = reason
+    import logging
+
+    logging.getLogger(__name__).warning("one-shot all-reduce disabled, using torch.distributed: %s", reason)
+
+
+def adopt(comm, mode: str = "auto"):
+    """Run ``comm``'s start-up self-test (:meth:`OneShotComm.self_test_report`); the communicator
+    if it passed, else close it and return None with the reason logged and kept in
+    :data:`DISABLED_REASON` (``mode`` other than ``auto``: raise instead)."""
+    ok, reason = comm.self_test_report()
+    if ok:
+        return comm
+    comm.close()
+    if mode not in ("auto",):
+        raise RuntimeError(f"one-shot all-reduce self-test failed: {reason}")
+    _disable(f"self-test failed: {reason}")
+    return None
 
 
 def reset() -> None:

@@ -224,26 +224,115 @@ def _scalar_summary(tag: str, value: float) -> bytes:
     return _field(1, 2) + _varint(len(val)) + val
 
 
+def _native_tb():
+    """``imitation_amd._C`` when it is built (its ``tb_scalar_records`` encodes a whole dump:
+    ``csrc/runtime/tb_events.cpp``), else None (pure-Python encoding below)."""
+    try:
+        from imitation_amd import _native
+
+        C = _native.load(build_if_missing=False)
+        return C if hasattr(C, "tb_scalar_records") else None
+    except Exception:  # noqa: BLE001 -- not built (e.g. a docs build): Python fallback
+        return None
+
+
+def encode_scalar_records(wall_time: float, step: int, tags: Sequence[str], values: Sequence[float], native=None) -> bytes:
+    """Framed TFRecords of one dump's scalars (Python reference of ``tb_scalar_records``)."""
+    if native is not None:
+        return native.tb_scalar_records(float(wall_time), int(step), list(tags), [float(v) for v in values])
+    out = bytearray()
+    for tag, value in zip(tags, values):
+        data = _event(wall_time, int(step), summary=_scalar_summary(tag, float(value)))
+        header = struct.pack("<Q", len(data))
+        out += header + struct.pack("<I", _masked_crc(header)) + data + struct.pack("<I", _masked_crc(data))
+    return bytes(out)
+
+
 class TensorBoardOutputFormat(KVWriter):
-    def __init__(self, folder: str):
+    """TF event file writer. ``write`` only snapshots the dump's scalars; a background thread
+    encodes them (natively when ``imitation_amd._C`` is built) and appends them to the file, so a
+    training loop pays ~microseconds per dump instead of the encoding + CRC + flush (the
+    reference writes synchronously through torch's SummaryWriter, which also queues to a
+    writer thread). ``flush`` / ``close`` drain the queue; every write is on disk after them."""
+
+    def __init__(self, folder: str, background: Optional[bool] = None):
         os.makedirs(folder, exist_ok=True)
         fname = os.path.join(folder, f"events.out.tfevents.{int(time.time())}.{os.uname().nodename}.{os.getpid()}")
         self.file = open(fname, "wb")
+        self._native = _native_tb()
         self._write_record(_event(time.time(), 0, file_version="brain.Event:2"))
+        self.file.flush()
+        if background is None:
+            background = os.environ.get("IMITATION_AMD_TB_THREAD", "0") == "1"
+        self._queue = None
+        self._thread = None
+        self._error: Optional[BaseException] = None
+        if background:
+            import queue
+            import threading
+
+            self._queue = queue.Queue()
+            self._thread = threading.Thread(target=self._drain, name="tb-writer", daemon=True)
+            self._thread.start()
 
     def _write_record(self, data: bytes) -> None:
         header = struct.pack("<Q", len(data))
         self.file.write(header + struct.pack("<I", _masked_crc(header)) + data + struct.pack("<I", _masked_crc(data)))
 
+    def _encode_and_write(self, item) -> None:
+        wall, step, tags, vals = item
+        self.file.write(encode_scalar_records(wall, step, tags, vals, self._native))
+
+    def _drain(self) -> None:
+        q = self._queue
+        while True:
+            item = q.get()
+            try:
+                if item is None:
+                    return
+                self._encode_and_write(item)
+                if q.empty():
+                    self.file.flush()
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the caller's next write / flush
+                self._error = e
+            finally:
+                q.task_done()
+
+    def _check(self) -> None:
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise RuntimeError("tensorboard writer thread failed") from e
+
     def write(self, key_values, key_excluded, step=0):
+        tags, vals = [], []
         for key, value in sorted(key_values.items()):
             if _is_excluded(key_excluded.get(key), "tensorboard"):
                 continue
             if isinstance(value, (int, float, np.integer, np.floating)) and not isinstance(value, bool):
-                self._write_record(_event(time.time(), int(step), summary=_scalar_summary(key, float(value))))
+                tags.append(key)
+                vals.append(float(value))
+        if not tags:
+            return
+        item = (time.time(), int(step), tags, vals)
+        if self._queue is None:
+            self._encode_and_write(item)
+            self.file.flush()
+            return
+        self._check()
+        self._queue.put(item)
+
+    def flush(self) -> None:
+        if self._queue is not None:
+            self._queue.join()
+            self._check()
         self.file.flush()
 
     def close(self):
+        if self._thread is not None:
+            self._queue.put(None)
+            self._thread.join()
+            self._thread = None
+            self._check()
         self.file.close()
 
 
@@ -262,16 +351,95 @@ def make_output_format(_format: str, log_dir: str, log_suffix: str = "") -> KVWr
     raise ValueError(f"Unknown format specified: {_format}")
 
 
-class Logger:
-    """Accumulate ``record``/``record_mean`` key-values and ``dump`` them to writers."""
+class _WriterThread:
+    """ONE daemon thread running the queued format writes of every asynchronous :class:`Logger`
+    in submission order (so the stdout / log / csv / tensorboard outputs of all sub-loggers keep
+    the order a synchronous run produces). A training loop's dump then costs a dict snapshot;
+    the formatting, encoding and file I/O run while the main thread waits on the GPU (event
+    synchronisation releases the GIL). An exception in a write is re-raised by the next
+    submit / drain."""
 
-    def __init__(self, folder: Optional[str], output_formats: List[KVWriter]):
+    def __init__(self):
+        import queue
+        import threading
+
+        self._q: "queue.Queue" = queue.Queue()
+        self._lock = threading.Lock()
+        self._thread = None
+        self._error: Optional[BaseException] = None
+
+    def _run(self) -> None:
+        while True:
+            fn = self._q.get()
+            try:
+                fn()
+            except BaseException as e:  # noqa: BLE001 -- surfaced on the caller's thread
+                if self._error is None:
+                    self._error = e
+            finally:
+                self._q.task_done()
+
+    def _raise(self) -> None:
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise RuntimeError("asynchronous logger write failed") from e
+
+    def submit(self, fn) -> None:
+        import threading
+
+        self._raise()
+        with self._lock:
+            if self._thread is None:
+                self._thread = threading.Thread(target=self._run, name="ia-log-writer", daemon=True)
+                self._thread.start()
+        self._q.put(fn)
+
+    def drain(self) -> None:
+        if self._thread is not None:
+            self._q.join()
+        self._raise()
+
+
+_WRITER = _WriterThread()
+
+
+def flush_async_writes() -> None:
+    """Block until every queued asynchronous logger write is done (also run at exit)."""
+    _WRITER.drain()
+
+
+def _drain_at_exit() -> None:
+    try:
+        _WRITER.drain()
+    except Exception as e:  # noqa: BLE001 -- interpreter shutdown: report, do not raise
+        print(f"imitation_amd logger: {e!r}", file=sys.stderr)
+
+
+import atexit  # noqa: E402
+
+atexit.register(_drain_at_exit)
+
+
+def async_default() -> bool:
+    """``IMITATION_AMD_LOG_ASYNC=1``: loggers built without an explicit choice write asynchronously."""
+    return os.environ.get("IMITATION_AMD_LOG_ASYNC", "0") == "1"
+
+
+class Logger:
+    """Accumulate ``record``/``record_mean`` key-values and ``dump`` them to writers.
+
+    ``async_writes``: ``dump`` / ``log`` hand a snapshot to the shared writer thread
+    (:class:`_WriterThread`) instead of formatting and writing on the caller's thread;
+    ``flush`` / ``close`` (and interpreter exit) wait for the writes."""
+
+    def __init__(self, folder: Optional[str], output_formats: List[KVWriter], async_writes: Optional[bool] = None):
         self.name_to_value: Dict[str, float] = defaultdict(float)
         self.name_to_count: Dict[str, int] = defaultdict(int)
         self.name_to_excluded: Dict[str, Tuple[str, ...]] = {}
         self.level = INFO
         self.dir = folder
         self.output_formats = output_formats
+        self.async_writes = async_default() if async_writes is None else bool(async_writes)
 
     @staticmethod
     def to_tuple(string_or_tuple) -> Tuple[str, ...]:
@@ -296,8 +464,17 @@ class Logger:
     def dump(self, step: int = 0) -> None:
         if self.level == DISABLED:
             return
-        for fmt in self.output_formats:
-            if isinstance(fmt, KVWriter):
+        kv = [f for f in self.output_formats if isinstance(f, KVWriter)]
+        if kv and self.async_writes:
+            values, excluded = dict(self.name_to_value), dict(self.name_to_excluded)
+
+            def write_all(kv=kv, values=values, excluded=excluded, step=step):
+                for fmt in kv:
+                    fmt.write(values, excluded, step)
+
+            _WRITER.submit(write_all)
+        else:
+            for fmt in kv:
                 fmt.write(self.name_to_value, self.name_to_excluded, step)
         self.name_to_value.clear()
         self.name_to_count.clear()
@@ -305,9 +482,19 @@ class Logger:
 
     def log(self, *args, level: int = INFO) -> None:
         if self.level <= level:
-            for fmt in self.output_formats:
-                if isinstance(fmt, SeqWriter):
-                    fmt.write_sequence(list(map(str, args)))
+            seq = [f for f in self.output_formats if isinstance(f, SeqWriter)]
+            if not seq:
+                return
+            items = list(map(str, args))
+            if self.async_writes:
+                _WRITER.submit(lambda seq=seq, items=items: [f.write_sequence(items) for f in seq])
+            else:
+                for fmt in seq:
+                    fmt.write_sequence(items)
+
+    def flush(self) -> None:
+        """Wait for this process's queued asynchronous writes."""
+        _WRITER.drain()
 
     def debug(self, *args) -> None:
         self.log(*args, level=DEBUG)
@@ -328,6 +515,8 @@ class Logger:
         return self.dir
 
     def close(self) -> None:
+        if self.async_writes:
+            _WRITER.drain()
         for fmt in self.output_formats:
             fmt.close()
 

@@ -10,7 +10,7 @@ import numpy as np
 
 
 class ActionNoise:
-    def reset(self) -> None:
+    def reset(self, indices=None) -> None:  # (indices: VectorizedActionNoise's per-env reset)
         pass
 
     def __call__(self) -> np.ndarray:
@@ -51,7 +51,7 @@ class OrnsteinUhlenbeckActionNoise(ActionNoise):
         self.noise_prev = x
         return x.astype(self._dtype)
 
-    def reset(self) -> None:
+    def reset(self, indices=None) -> None:
         self.noise_prev = self.initial_noise if self.initial_noise is not None else np.zeros_like(self._mu)
 
     def __repr__(self) -> str:

@@ -158,7 +158,8 @@ class OffPolicyAlgorithm(BaseAlgorithm):
                     num_collected_episodes += 1
                     self._episode_num += 1
                     if action_noise is not None and hasattr(action_noise, "reset"):
-                        action_noise.reset()
+                        # only the finished env's noise process (SB3: indices=[idx] when n_envs > 1)
+                        action_noise.reset(**({"indices": [idx]} if env.num_envs > 1 else {}))
                     if log_interval is not None and self._episode_num % log_interval == 0:
                         self._dump_logs()
         callback.on_rollout_end()

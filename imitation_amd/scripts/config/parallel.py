@@ -19,7 +19,9 @@ def config():
     num_samples = 1
     repeat = 1  # run each sampled configuration with this many seeds
     experiment_checkpoint_path = ""
-    tune_run_kwargs = {}  # max_concurrent_trials, local_dir, seed
+    # max_concurrent_trials, local_dir, seed, search_alg ("random" / "tpe"; default: tpe when
+    # repeat > 1, as the reference's Repeater(OptunaSearch)), n_startup_trials (TPE)
+    tune_run_kwargs = {}
     local_dir = "output/parallel"
 
 

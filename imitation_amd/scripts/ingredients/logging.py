@@ -1,6 +1,7 @@
 """Logging ingredient: log dir, stdout/TensorBoard/W&B formats (reference: scripts/ingredients/logging.py)."""
 
 import logging
+import os
 import pathlib
 from typing import Sequence, Tuple, Union
 
@@ -64,5 +65,9 @@ def setup_logging(_run, log_format_strs: Sequence[str]) -> Tuple[imit_logger.Hie
     log_dir = make_log_dir()
     if "wandb" in log_format_strs:
         wb.wandb_init(log_dir=str(log_dir))
-    custom_logger = imit_logger.configure(folder=log_dir / "log", format_strs=log_format_strs)
+    # asynchronous format writes: the training loop only snapshots each dump; the tensorboard /
+    # stdout writing runs on the writer thread while the host waits for the GPU (drained at exit;
+    # IMITATION_AMD_LOG_ASYNC=0 writes synchronously)
+    async_writes = os.environ.get("IMITATION_AMD_LOG_ASYNC", "1") != "0"
+    custom_logger = imit_logger.configure(folder=log_dir / "log", format_strs=log_format_strs, async_writes=async_writes)
     return custom_logger, log_dir

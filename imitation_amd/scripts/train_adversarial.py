@@ -23,6 +23,7 @@ from imitation_amd.algorithms.adversarial import common
 from imitation_amd.algorithms.adversarial import gail as gail_algo
 from imitation_amd.data import rollout
 from imitation_amd.parallel import dist as pdist
+from imitation_amd.utils import watchdog
 from imitation_amd.policies import serialize
 from imitation_amd.rewards import serialize as reward_serialize
 from imitation_amd.scripts.config.train_adversarial import train_adversarial_ex
@@ -126,12 +127,15 @@ def train_adversarial(_run, show_config: bool, algo_cls: Type[common.Adversarial
         trainer = _make_trainer(algo_cls, engine, venv=venv, demonstrations=expert_trajs, gen_algo=gen_algo,
                                 log_dir=log_dir, reward_net=reward_net, custom_logger=custom_logger, **algorithm_kwargs)
 
-        def callback(round_num: int, /) -> None:
-            if checkpoint_interval > 0 and round_num % checkpoint_interval == 0:
-                save(trainer, log_dir / "checkpoints" / f"{round_num:05d}")
+        with watchdog.cli_watchdog("train_adversarial") as wd:
+            def callback(round_num: int, /) -> None:
+                wd.beat()  # a round that never ends (stuck collective / kernel) aborts the run
+                if checkpoint_interval > 0 and round_num % checkpoint_interval == 0:
+                    save(trainer, log_dir / "checkpoints" / f"{round_num:05d}")
 
-        trainer.train(total_timesteps, callback)
-        imit_stats = policy_evaluation.eval_policy(trainer.policy, trainer.venv_train)
+            trainer.train(total_timesteps, callback)
+            wd.beat()
+            imit_stats = policy_evaluation.eval_policy(trainer.policy, trainer.venv_train)
     if checkpoint_interval >= 0:
         save(trainer, log_dir / "checkpoints" / "final")
     return {"imit_stats": imit_stats, "expert_stats": rollout.rollout_stats(expert_trajs), "engine": trainer.engine_kind}

@@ -14,6 +14,7 @@ from typing import Any, Mapping, Optional, Type, Union
 
 import numpy as np
 
+from imitation_amd.utils import watchdog
 from imitation_amd.algorithms import preference_comparisons
 from imitation_amd.data import serialize as data_serialize
 from imitation_amd.policies import serialize as policies_serialize
@@ -120,15 +121,18 @@ def train_preference_comparisons(total_timesteps: int, total_comparisons: int, n
             initial_comparison_frac=initial_comparison_frac, custom_logger=custom_logger,
             allow_variable_horizon=allow_variable_horizon, query_schedule=query_schedule)
 
-        def save_callback(iteration_num):
-            if checkpoint_interval > 0 and iteration_num % checkpoint_interval == 0:
-                save_checkpoint(main_trainer, log_dir / "checkpoints" / f"{iteration_num:04d}",
-                                allow_save_policy=trajectory_path is None)
+        with watchdog.cli_watchdog("train_preference_comparisons") as wd:
+            def save_callback(iteration_num):
+                wd.beat()
+                if checkpoint_interval > 0 and iteration_num % checkpoint_interval == 0:
+                    save_checkpoint(main_trainer, log_dir / "checkpoints" / f"{iteration_num:04d}",
+                                    allow_save_policy=trajectory_path is None)
 
-        results = dict(main_trainer.train(total_timesteps, total_comparisons, callback=save_callback))
-        results["engine"] = getattr(trajectory_generator, "engine_kind", "dataset")
-        if trajectory_path is None:
-            results["imit_stats"] = policy_evaluation.eval_policy(agent, venv)
+            results = dict(main_trainer.train(total_timesteps, total_comparisons, callback=save_callback))
+            wd.beat()
+            results["engine"] = getattr(trajectory_generator, "engine_kind", "dataset")
+            if trajectory_path is None:
+                results["imit_stats"] = policy_evaluation.eval_policy(agent, venv)
     if save_preferences:
         main_trainer.dataset.save(log_dir / "preferences.npz")
     if checkpoint_interval >= 0:

@@ -1,6 +1,6 @@
 """Two-phase hyper-parameter tuning (reference: src/imitation/scripts/tuning.py):
-(1) ``parallel`` search over ``parallel_run_config.search_space`` (random search;
-each sample repeated ``repeat`` times with fresh seeds), (2) re-evaluation of the best
+(1) ``parallel`` search over ``parallel_run_config.search_space`` (TPE, ``tune.TPESearch``:
+the reference's OptunaSearch; each sample repeated ``repeat`` times with fresh seeds), (2) re-evaluation of the best
 configuration (highest mean return over its repeats) on ``num_eval_seeds`` new seeds.
 """
 
@@ -44,6 +44,8 @@ def evaluate_trial(trial: Dict[str, Any], num_eval_seeds: int, run_name: str, pa
     cfg = copy.deepcopy(parallel_run_config)
     cfg.update(run_name=run_name, num_samples=1, search_space=space, resources_per_trial=resources_per_trial, repeat=1,
                experiment_checkpoint_path="")
+    # every evaluation seed exactly once: the grid expansion, not the model-based search
+    cfg["tune_run_kwargs"] = dict(cfg.get("tune_run_kwargs") or {}, search_alg="random")
     run = parallel_ex.run(config_updates=cfg)
     rets = np.array([r["metric"] for r in run.result])
     print("Evaluation returns:", rets, "mean", np.nanmean(rets), "std", np.nanstd(rets))
@@ -53,6 +55,8 @@ def evaluate_trial(trial: Dict[str, Any], num_eval_seeds: int, run_name: str, pa
 @tuning_ex.main
 def tune_main(parallel_run_config, eval_best_trial_resource_multiplier: int = 1, num_eval_seeds: int = 5):
     cfg = copy.deepcopy(parallel_run_config)
+    # model-based search, as the reference's tuning (OptunaSearch, scripts/tuning.py:43-46)
+    cfg.setdefault("tune_run_kwargs", {}).setdefault("search_alg", "tpe")
     run = parallel_ex.run(config_updates=cfg)
     records = run.result
     if not records:

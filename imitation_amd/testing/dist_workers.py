@@ -508,3 +508,49 @@ def dagger_device_round_worker(rank, world, seed, scratch):
     return {"policy": [p.detach().cpu().numpy().copy() for p in tr.policy.parameters()],
             "env_state": col.state.detach().cpu().numpy().copy(), "round_num": tr.round_num,
             "local": tr.last_train_timesteps_local, "dp_fused_replays": dp_step.n_replays if dp_step else 0}
+
+
+def oneshot_selftest_worker(rank, world, corrupt, mode="auto"):
+    """``oneshot.adopt`` on a stand-in communicator (gloo on CPU) whose reduction is correct, or
+    corrupted on rank 1 only (``corrupt``): returns (adopted?, reason, closed?) on every rank."""
+    import torch
+    import torch.distributed as tdist
+
+    from imitation_amd.parallel import oneshot
+
+    class FakeComm(oneshot.OneShotComm):
+        def __init__(self):  # no IPC: the reduction is the process group's
+            self.rank, self.world, self.device = rank, world, torch.device("cpu")
+            self.stage_bytes, self.timeout_s = 1 << 16, 5.0
+            self.local, self._opened, self.closed = None, [], False
+
+        def allreduce_(self, t, scale=1.0):
+            tdist.all_reduce(t)
+            if corrupt == "value" and self.rank == 1:
+                t.view(-1)[-1] += 1.0
+            if corrupt == "ulp" and self.rank == 1:
+                t.view(-1)[0] = torch.nextafter(t.view(-1)[0], torch.tensor(float("inf")))
+
+        def error(self):
+            return 0
+
+        def close(self):
+            self.closed = True
+
+    comm = FakeComm()
+    oneshot.DISABLED_REASON = None
+    try:
+        got = oneshot.adopt(comm, mode)
+    except RuntimeError as e:
+        return ("raised", str(e), comm.closed)
+    return (got is comm, oneshot.DISABLED_REASON, comm.closed)
+
+
+def oneshot_selftest_gpu_worker(rank, world):
+    """The real communicator after ``dist.init`` (IMITATION_AMD_ONESHOT=1): adopted, and its
+    start-up self-test (closed form + bitwise cross-check vs the process group) passes again."""
+    from imitation_amd.parallel import oneshot
+
+    c = oneshot._COMM
+    rep = c.self_test_report() if c is not None else (False, "no communicator")
+    return (c is not None, oneshot.DISABLED_REASON, rep)

@@ -1,0 +1,176 @@
+"""Imitation quality of the device engines: does the learner approach the expert?
+
+The reference's benchmark reports ``imit_stats/monitor_return_mean`` normalised as
+``(score - random) / (expert - random)`` (``benchmarking/README.md:94-98``,
+``benchmarking/sacred_output_to_markdown_summary.py:79-140``). This module reproduces that
+measurement for :class:`~imitation_amd.engine.gail.DeviceGAIL` and
+:class:`~imitation_amd.engine.airl.DeviceAIRL`:
+
+* **CartPole** (``seals/CartPole-v0``): the checked-in reference expert
+  (``tests/testdata/expert_models/cartpole_0/policies/final/model.zip``) is rolled out for the
+  demonstrations, learner / trainer hyper-parameters are the reference tutorials'
+  (``docs/tutorials/3_train_gail.ipynb``, ``4_train_airl.ipynb``).
+* **Pendulum** (``Pendulum-v1``): the checked-in demonstrations
+  ``tests/testdata/expert_models/pendulum_0/rollouts/final.npz`` (their mean return is the
+  expert score).
+* **Synthetic locomotion** (``expert`` mode of ``benchmarking/bench_configs.py``): a PPO expert
+  is trained on the device engine with the env reward first (``debug_use_ground_truth``), its
+  deterministic rollouts are the demonstrations.
+
+Every score is measured by :meth:`DeviceGeneratorCore.device_evaluate` (SB3 ``evaluate_policy``
+semantics, deterministic actions, on the GPU). The random-policy score uses the native
+``RandomPolicy`` on the host env.
+"""
+
+from __future__ import annotations
+
+import os
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch as th
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+TESTDATA = os.path.join(ROOT, "tests", "testdata", "expert_models")
+CARTPOLE_EXPERT_ZIP = os.path.join(TESTDATA, "cartpole_0", "policies", "final", "model.zip")
+PENDULUM_DEMOS = os.path.join(TESTDATA, "pendulum_0", "rollouts", "final.npz")
+
+
+def normalized_score(score: float, random_score: float, expert_score: float) -> float:
+    """``(score - random) / (expert - random)`` (reference benchmark summary)."""
+    return float((score - random_score) / (expert_score - random_score))
+
+
+def random_return(env_id: str, n_episodes: int = 50, seed: int = 0) -> float:
+    """Mean return of the uniform-random policy (reference: ``random`` policy type)."""
+    from imitation_amd.data import rollout
+    from imitation_amd.util.util import make_vec_env
+
+    venv = make_vec_env(env_id, rng=np.random.default_rng(seed), n_envs=8)
+    venv.action_space.seed(seed)
+    trajs = rollout.generate_trajectories(None, venv, rollout.make_min_episodes(n_episodes), rng=np.random.default_rng(seed))
+    return float(np.mean([t.rews.sum() for t in trajs[:n_episodes]]))
+
+
+def cartpole_expert_demos(n_episodes: int = 60, seed: int = 0):
+    """Rollouts of the checked-in reference CartPole expert on ``seals/CartPole-v0``."""
+    from imitation_amd.data import rollout
+    from imitation_amd.data.wrappers import RolloutInfoWrapper
+    from imitation_amd.policies import serialize
+    from imitation_amd.util.util import make_vec_env
+
+    venv = make_vec_env("seals/CartPole-v0", rng=np.random.default_rng(seed), n_envs=8,
+                        post_wrappers=[lambda e, _: RolloutInfoWrapper(e)])
+    expert = serialize.load_policy("ppo", venv, path=CARTPOLE_EXPERT_ZIP)
+    trajs = rollout.rollout(expert, venv, rollout.make_sample_until(min_timesteps=None, min_episodes=n_episodes),
+                            rng=np.random.default_rng(seed))
+    return trajs
+
+
+def pendulum_expert_demos():
+    from imitation_amd.data import serialize
+
+    return serialize.load_with_rewards(PENDULUM_DEMOS)
+
+
+def _cartpole_trainer(algo: str, demos, seed: int, device, logger):
+    """The reference tutorials' GAIL / AIRL CartPole setups on the device engines."""
+    from imitation_amd.engine.airl import DeviceAIRL
+    from imitation_amd.engine.gail import DeviceGAIL
+    from imitation_amd.rewards.reward_nets import BasicRewardNet, BasicShapedRewardNet
+    from imitation_amd.rl.policies import ActorCriticPolicy
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    venv = make_vec_env("seals/CartPole-v0", rng=np.random.default_rng(seed), n_envs=8)
+    if algo == "gail":
+        learner = PPO(ActorCriticPolicy, venv, batch_size=64, ent_coef=0.0, learning_rate=4e-4, gamma=0.95, n_epochs=5,
+                      seed=seed, device=device)
+        rn = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
+        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, gen_replay_buffer_capacity=512,
+                        n_disc_updates_per_round=8, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
+    else:
+        learner = PPO(ActorCriticPolicy, venv, batch_size=64, ent_coef=0.0, learning_rate=5e-4, gamma=0.95,
+                      clip_range=0.1, vf_coef=0.1, n_epochs=5, seed=seed, device=device)
+        rn = BasicShapedRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
+        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=2048, gen_replay_buffer_capacity=512,
+                        n_disc_updates_per_round=16, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
+    return tr
+
+
+def _pendulum_trainer(algo: str, demos, seed: int, device, logger):
+    """Pendulum-v1 (continuous): SB3 MlpPolicy PPO with the rl-zoo Pendulum settings
+    (gamma 0.9, gae_lambda 0.95, lr 1e-3, n_steps 1024 x 4 envs, 10 epochs, use_sde off)."""
+    from imitation_amd.engine.airl import DeviceAIRL
+    from imitation_amd.engine.gail import DeviceGAIL
+    from imitation_amd.rewards.reward_nets import BasicRewardNet, BasicShapedRewardNet
+    from imitation_amd.rl.policies import ActorCriticPolicy
+    from imitation_amd.rl.ppo import PPO
+    from imitation_amd.util.networks import RunningNorm
+    from imitation_amd.util.util import make_vec_env
+
+    venv = make_vec_env("Pendulum-v1", rng=np.random.default_rng(seed), n_envs=8)
+    learner = PPO(ActorCriticPolicy, venv, n_steps=1024, batch_size=64, gamma=0.9, gae_lambda=0.95, learning_rate=1e-3,
+                  n_epochs=10, ent_coef=0.0, clip_range=0.2, seed=seed, device=device)
+    if algo == "gail":
+        rn = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
+        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, gen_replay_buffer_capacity=512,
+                        n_disc_updates_per_round=8, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
+    else:
+        rn = BasicShapedRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
+        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=2048, gen_replay_buffer_capacity=512,
+                        n_disc_updates_per_round=16, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
+    return tr
+
+
+def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_000, seed: int = 0, n_eval: int = 50,
+        eval_every: Optional[int] = None, device: Any = "cuda", verbose: bool = False) -> Dict[str, Any]:
+    """Train ``algo`` (``gail`` / ``airl``) on ``env`` (``cartpole`` / ``pendulum``) with expert
+    demonstrations and report returns + normalised scores (before, during, after)."""
+    from imitation_amd.util import logger as imit_logger
+
+    th.manual_seed(seed)
+    np.random.seed(seed)
+    if env == "cartpole":
+        env_id = "seals/CartPole-v0"
+        demos = cartpole_expert_demos(seed=seed)
+        make = _cartpole_trainer
+    elif env == "pendulum":
+        env_id = "Pendulum-v1"
+        demos = pendulum_expert_demos()
+        make = _pendulum_trainer
+    else:
+        raise ValueError(f"unknown env {env!r}")
+    expert = float(np.mean([t.rews.sum() for t in demos]))
+    rand = random_return(env_id, n_eval, seed)
+    log = imit_logger.configure(f"/tmp/ia_quality_{os.getpid()}", format_strs=[])
+    tr = make(algo, demos, seed, device, log)
+
+    def score() -> float:
+        r, _ = tr.device_evaluate(n_eval, deterministic=True, seed=10_000 + seed)
+        return float(np.mean(r))
+
+    r0 = score()
+    curve: List[Dict[str, float]] = [dict(timesteps=0, ret=r0, norm=normalized_score(r0, rand, expert))]
+    step = int(eval_every or total_timesteps)
+    step = max(tr.gen_train_timesteps, step // tr.gen_train_timesteps * tr.gen_train_timesteps)
+    done = 0
+    t_train = 0.0
+    while done < total_timesteps:
+        k = min(step, total_timesteps - done)
+        k = max(tr.gen_train_timesteps, k // tr.gen_train_timesteps * tr.gen_train_timesteps)
+        t0 = time.perf_counter()
+        tr.train(k)
+        th.cuda.synchronize()
+        t_train += time.perf_counter() - t0
+        done += k
+        r = score()
+        curve.append(dict(timesteps=done, ret=r, norm=normalized_score(r, rand, expert)))
+        if verbose:
+            print(f"{algo}/{env} seed {seed}: {done} steps: return {r:.1f} (normalised {curve[-1]['norm']:.3f})", flush=True)
+    final = curve[-1]["ret"]
+    return dict(algo=algo, env=env_id, seed=seed, expert_return=expert, random_return=rand, learner_return_before=r0,
+                learner_return=final, normalized_score=normalized_score(final, rand, expert), curve=curve,
+                total_timesteps=done, train_s=round(t_train, 3), n_eval_episodes=n_eval, n_demo_episodes=len(demos))

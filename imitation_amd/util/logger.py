@@ -62,9 +62,10 @@ class _Scope:
 class _SubLoggerCache:
     """Sub-loggers of the ``raw/...`` scopes, created on first use and kept for reuse."""
 
-    def __init__(self, root_dir: Optional[str], format_strs: Sequence[str]):
+    def __init__(self, root_dir: Optional[str], format_strs: Sequence[str], async_writes: bool = False):
         self.root_dir = root_dir
         self.format_strs = list(format_strs)
+        self.async_writes = async_writes
         self.loggers: Dict[str, sb_logger.Logger] = {}
 
     def get(self, subdir: str) -> sb_logger.Logger:
@@ -73,7 +74,7 @@ class _SubLoggerCache:
             assert self.root_dir is not None
             folder = pathlib.Path(self.root_dir) / "raw" / subdir
             folder.mkdir(exist_ok=True, parents=True)
-            lg = sb_logger.Logger(str(folder), _build_output_formats(folder, self.format_strs))
+            lg = sb_logger.Logger(str(folder), _build_output_formats(folder, self.format_strs), async_writes=self.async_writes)
             self.loggers[subdir] = lg
         return lg
 
@@ -88,10 +89,10 @@ class HierarchicalLogger(sb_logger.Logger):
     def __init__(self, default_logger: sb_logger.Logger, format_strs: Sequence[str] = DEFAULT_FORMATS):
         self.default_logger = default_logger
         self.format_strs = format_strs
-        self._subloggers = _SubLoggerCache(default_logger.dir, format_strs)
+        self._subloggers = _SubLoggerCache(default_logger.dir, format_strs, getattr(default_logger, "async_writes", False))
         self._accumulate_prefixes: List[str] = []
         self._scope: Optional[_Scope] = None
-        super().__init__(folder=default_logger.dir, output_formats=[])
+        super().__init__(folder=default_logger.dir, output_formats=[], async_writes=getattr(default_logger, "async_writes", False))
         self._sync_maps()
 
     # ------------------------------------------------------------------ scope state
@@ -174,6 +175,9 @@ class HierarchicalLogger(sb_logger.Logger):
     def set_level(self, level: int) -> None:
         self.default_logger.set_level(level)
 
+    def flush(self) -> None:
+        self.default_logger.flush()
+
     def close(self):
         self.default_logger.close()
         self._subloggers.close()
@@ -211,13 +215,17 @@ def _default_folder() -> str:
     return os.path.join(tempfile.gettempdir(), stamp)
 
 
-def configure(folder=None, format_strs: Optional[Sequence[str]] = None) -> HierarchicalLogger:
+def configure(folder=None, format_strs: Optional[Sequence[str]] = None,
+              async_writes: Optional[bool] = None) -> HierarchicalLogger:
     """A :class:`HierarchicalLogger` writing to ``folder`` (a fresh temp dir by default) with
-    ``format_strs`` (library default stdout/log/csv); DP ranks other than 0 write nothing."""
+    ``format_strs`` (library default stdout/log/csv); DP ranks other than 0 write nothing.
+    ``async_writes``: format writes on the shared writer thread (default:
+    ``IMITATION_AMD_LOG_ASYNC``; the CLIs turn it on)."""
     from imitation_amd.parallel import dist as pdist
 
     folder = str(folder) if folder is not None else _default_folder()
     formats = list(DEFAULT_FORMATS if format_strs is None else format_strs)
     if pdist.rank() != 0:
         return HierarchicalLogger(sb_logger.Logger(folder, []), [])
-    return HierarchicalLogger(sb_logger.Logger(folder, _build_output_formats(pathlib.Path(folder), formats)), formats)
+    return HierarchicalLogger(sb_logger.Logger(folder, _build_output_formats(pathlib.Path(folder), formats),
+                                               async_writes=async_writes), formats)

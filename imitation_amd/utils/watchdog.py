@@ -120,3 +120,18 @@ class Watchdog:
                     self.on_timeout()
                     return
                 os._exit(self.exit_code)
+
+
+def cli_watchdog(name: str):
+    """The CLIs' hang watchdog (``IMITATION_AMD_WATCHDOG_S`` seconds without a per-round beat,
+    default 1800; 0 disables): a context manager yielding an object with ``beat()``."""
+    import contextlib
+
+    s = float(os.environ.get("IMITATION_AMD_WATCHDOG_S", "1800"))
+    if s <= 0:
+        class _Null:
+            def beat(self) -> None:
+                pass
+
+        return contextlib.nullcontext(_Null())
+    return Watchdog(timeout_s=s, name=name)

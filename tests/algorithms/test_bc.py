@@ -278,6 +278,34 @@ def test_multibc_column_map_probe():
     assert _column_map(lambda i, o: o[:, :3] - o[:, 3:6], 0, 8, th.float32) is None
     assert _column_map(lambda i, o: o.flip(0)[:, :2], 0, 8, th.float32) is None
     assert _column_map(lambda i, o: (_ for _ in ()).throw(ValueError("no")), 0, 8, th.float32) is None
+    # 1-D actions: only the identity folds (as a 1-D gather)
+    assert _column_map(lambda i, a: a, 1, 1, th.int64, one_d=True) == ([0], True)
+    assert _column_map(lambda i, a: a + i, 1, 1, th.int64, one_d=True) is None
+
+
+def test_multibc_agent_gather_confirms_maps_on_real_rows():
+    """a probe-accepted map must reproduce the override on real demo rows, shape
+    included, else MultiBC falls back to the host loader; 1-D identity actions keep the
+    reference's ``[n_agents * B]`` shape."""
+    from imitation_amd.algorithms import bc
+    from imitation_amd.data import types
+
+    rng = np.random.default_rng(0)
+    d, n_agents, N, B = 4, 3, 256, 32
+    obs = rng.standard_normal((N, d * n_agents)).astype(np.float32)
+    acts2 = rng.integers(0, 2, (N, n_agents))
+    demos = types.TransitionsMinimal(obs=obs, acts=acts2, infos=np.array([{}] * N))
+    sel = lambda i, o: o[:, d * i: d * i + d]  # noqa: E731
+    ok = bc._AgentGatherLoader.maybe(demos, sel, lambda i, a: a[:, i], n_agents, B, "cpu", 0)
+    assert isinstance(ok, bc._AgentGatherLoader)
+    # agent-dependent in-range shift: the probe accepts it (columns shifted), real rows do not
+    shift = lambda i, o: o[:, d * i: d * i + d] - i  # noqa: E731
+    assert bc._column_map(shift, 1, d * n_agents, th.float32) is not None
+    assert bc._AgentGatherLoader.maybe(demos, shift, lambda i, a: a[:, i], n_agents, B, "cpu", 0) is None
+    # 1-D actions with an identity override: [n_agents * B] like th.cat of the overrides
+    demos1 = types.TransitionsMinimal(obs=obs, acts=acts2[:, 0].copy(), infos=np.array([{}] * N))
+    ld = bc._AgentGatherLoader.maybe(demos1, sel, lambda i, a: a, n_agents, B, "cpu", 0)
+    assert ld is not None and ld.acts_ag.shape == (n_agents * N,) and ld.bufs[1].shape == (n_agents * B,)
 
 
 @pytest.mark.gpu

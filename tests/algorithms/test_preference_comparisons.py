@@ -123,6 +123,7 @@ def test_preference_comparisons_raises(agent_trainer, reward_net, random_fragmen
 
 @pytest.mark.parametrize("schedule", ["constant", "hyperbolic", "inverse_quadratic", lambda t: 1 / (1 + t ** 3)])
 def test_trainer_no_crash(agent_trainer, reward_net, random_fragmenter, custom_logger, schedule, rng):
+    th.manual_seed(0)  # the accuracy of 10 tiny comparisons depends on the global torch stream (xdist order)
     main = pc.PreferenceComparisons(agent_trainer, reward_net, num_iterations=2, transition_oversampling=2,
                                     fragment_length=2, fragmenter=random_fragmenter, custom_logger=custom_logger,
                                     query_schedule=schedule, initial_epoch_multiplier=2, rng=rng)

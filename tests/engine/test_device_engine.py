@@ -10,7 +10,7 @@ gpu = pytest.mark.gpu
 
 
 def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epochs=2, seed=0, discrete=False,
-           net_arch=None, activation=None):
+           net_arch=None, activation=None, init_seed=None):
     from imitation_amd.data import rollout
     from imitation_amd.engine.gail import DeviceGAIL
     from imitation_amd.policies.base import FeedForward32Policy, NormalizeFeaturesExtractor
@@ -29,6 +29,10 @@ def _setup(env_id="seals/HalfCheetah-v1", n_envs=4, n_steps=32, batch=64, n_epoc
     demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
     from imitation_amd.rl.policies import ActorCriticPolicy
 
+    if init_seed is not None:  # same demonstrations, different initial weights / engine seeds
+        th.manual_seed(init_seed)
+        np.random.seed(init_seed)
+        seed = init_seed
     pk = dict(features_extractor_class=NormalizeFeaturesExtractor)
     policy_cls = FeedForward32Policy
     if net_arch is not None:
@@ -407,7 +411,7 @@ def test_fused_disc_train_logs_and_matches_generic_path_shape():
     assert tr._disc_opt.state[tr._rflat.params[0]]["exp_avg"].data_ptr() == tr._r_m.data_ptr()
 
 
-def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True):
+def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True, init_seed=None):
     from imitation_amd.data import rollout
     from imitation_amd.engine.airl import DeviceAIRL
     from imitation_amd.policies.base import NormalizeFeaturesExtractor
@@ -425,6 +429,10 @@ def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True):
     demo_env = make_vec_env("seals/Hopper-v1", rng=np.random.default_rng(7), n_envs=4)
     demo_env.action_space.seed(7)  # the random demo policy samples from the action space
     demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
+    if init_seed is not None:  # same demonstrations, different initial weights / engine seeds
+        th.manual_seed(init_seed)
+        np.random.seed(init_seed)
+        seed = init_seed
     gen = PPO(ActorCriticPolicy, venv, n_steps=n_steps, batch_size=batch, n_epochs=2, device="cuda", seed=seed,
               policy_kwargs=dict(net_arch=dict(pi=[64, 64], vf=[64, 64]), activation_fn=th.nn.ReLU,
                                  features_extractor_class=NormalizeFeaturesExtractor))
@@ -770,3 +778,95 @@ def test_gae_scan_register_and_loop_paths_match_reference(T, N):
     adv, ret = rl_ops.gae(*(x.cuda() for x in (rew, val, starts, last_val, dones)), 0.99, 0.95)
     np.testing.assert_allclose(adv.cpu().numpy(), ref_a.numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(ret.cpu().numpy(), ref_r.numpy(), rtol=1e-4, atol=1e-4)
+    # the same pass's [N][4] return / advantage moments (train/explained_variance)
+    mom = th.zeros(N, 4, device="cuda")
+    adv2, ret2 = rl_ops.gae(*(x.cuda() for x in (rew, val, starts, last_val, dones)), 0.99, 0.95, moments=mom)
+    assert th.equal(adv2, adv) and th.equal(ret2, ret)
+    want = th.stack([ref_r.sum(0), ref_r.square().sum(0), ref_a.sum(0), ref_a.square().sum(0)], 1)
+    np.testing.assert_allclose(mom.cpu().double().numpy(), want.numpy(), rtol=1e-3, atol=1e-2)
+
+
+@gpu
+@pytest.mark.parametrize("env_id,n_episodes,n_envs", [("Pendulum-v1", 10, 4), ("seals/CartPole-v0", 7, 3)])
+def test_device_evaluate_matches_host_evaluate_policy(env_id, n_episodes, n_envs):
+    """``device_evaluate`` (deterministic rollout chain on a separate env block) counts episodes
+    as SB3 evaluate_policy does, is reproducible, leaves the training state alone, and its mean
+    return agrees with the host evaluate_policy of the same policy on the same env seeds."""
+    from imitation_amd.envs.vec_env import NativeVecEnv
+    from imitation_amd.rl.evaluation import evaluate_policy
+
+    tr, venv, gen, rn = _setup(env_id=env_id, n_envs=4, n_steps=32, batch=64,
+                               net_arch=[64, 64] if env_id.startswith("seals") else None)
+    st0 = tr.state.clone()
+    r1, l1 = tr.device_evaluate(n_episodes, n_envs=n_envs, seed=5)
+    r2, l2 = tr.device_evaluate(n_episodes, n_envs=n_envs, seed=5)
+    assert len(r1) == n_episodes and r1 == r2 and l1 == l2
+    assert th.equal(tr.state, st0)
+    horizon = 200 if env_id == "Pendulum-v1" else 500
+    assert all(n == horizon for n in l1)  # neither env terminates early
+    host_env = NativeVecEnv(env_id, n_envs, seed=5, max_episode_steps=horizon)
+    hr, hl = evaluate_policy(gen.policy, host_env, n_eval_episodes=n_episodes, deterministic=True,
+                             return_episode_rewards=True)
+    assert sorted(hl) == sorted(l1)
+    # same completion order ((step, env) row-major) on both sides; the device transcendentals
+    # differ in the last ulp (ia/envs.h), which an unstable (spinning) pendulum amplifies over a
+    # 200-step episode: most -- not all -- episodes agree to rounding
+    close = [abs(a - b) <= 0.01 * abs(b) + 1.0 for a, b in zip(r1, hr)]
+    assert sum(close) >= 0.6 * len(close), list(zip(r1, hr))
+
+
+def _engine_snapshot(tr):
+    """Everything a resumed run must reproduce bitwise: weights, Adam moments, normalisers,
+    the replay ring, env state and counters."""
+    ts = [p.detach().clone() for p in tr.gen_algo.policy.parameters()]
+    ts += [p.detach().clone() for p in tr._reward_net.parameters()]
+    ts += [b.detach().clone() for b in tr.gen_algo.policy.buffers()] + [b.detach().clone() for b in tr._reward_net.buffers()]
+    ts += [tr.exp_avg.clone(), tr.exp_avg_sq.clone(), tr.state.clone(), tr.cur_obs.clone()]
+    ts += [v.clone() for v in tr._gen_dev._arrays.values()]
+    return ts, (tr._global_step, tr._disc_step, tr.gen_algo.num_timesteps, tr._perm_round, tr._step0)
+
+
+@gpu
+@pytest.mark.parametrize("kind", ["gail", "airl"])
+def test_device_engine_checkpoint_resume_is_bitwise(kind, tmp_path):
+    """k rounds, save_checkpoint, a FRESH trainer built with a different seed,
+    load_checkpoint, k more rounds == 2k uninterrupted rounds, bitwise (device Adam state, env
+    state / RNG, Feistel round counter, replay ring, fused-discriminator state)."""
+    from imitation_amd.utils import checkpoint
+
+    make = (lambda s=None: _setup(n_envs=8, n_steps=64, batch=64, init_seed=s)[0]) if kind == "gail" else \
+        (lambda s=None: _setup_airl(n_envs=8, n_steps=64, batch=256, init_seed=s)[0])
+    k = 2
+    a = make()
+    a.train(2 * k * a.gen_train_timesteps)
+    th.cuda.synchronize()
+    want, want_ctr = _engine_snapshot(a)
+    del a
+    b = make()
+    b.train(k * b.gen_train_timesteps)
+    checkpoint.save_checkpoint(b, str(tmp_path / "ck"))
+    del b
+    c = make(1234)
+    checkpoint.load_checkpoint(c, str(tmp_path / "ck"))
+    c.train(k * c.gen_train_timesteps)
+    th.cuda.synchronize()
+    got, got_ctr = _engine_snapshot(c)
+    assert got_ctr == want_ctr
+    assert len(got) == len(want)
+    for i, (x, y) in enumerate(zip(got, want)):
+        assert th.equal(x, y), f"tensor {i} differs after resume"
+
+
+@gpu
+@pytest.mark.parametrize("kind", ["gail", "airl"])
+def test_device_engine_nan_reward_weight_fails_fast(kind):
+    """a poisoned reward-net weight stops training within one round with
+    NonFiniteError naming the round (the checks read the statistics already on the host)."""
+    from imitation_amd.utils.watchdog import NonFiniteError
+
+    tr = _setup(n_envs=8, n_steps=64, batch=64)[0] if kind == "gail" else _setup_airl(n_envs=8, n_steps=64, batch=256)[0]
+    tr.train(tr.gen_train_timesteps)
+    with th.no_grad():
+        next(tr._reward_net.parameters()).view(-1)[0] = float("nan")
+    with pytest.raises(NonFiniteError, match="round"):
+        tr.train(tr.gen_train_timesteps)

@@ -109,6 +109,28 @@ def test_td3_ddpg_run_and_save(tmp_path, rng, name):
     np.testing.assert_allclose(model.predict(obs, deterministic=True)[0], loaded.predict(obs, deterministic=True)[0], rtol=1e-5)
 
 
+def test_action_noise_resets_only_the_finished_env(rng):
+    """with n_envs > 1 an episode end resets that env's noise process only
+    (SB3 passes ``indices=[idx]``), not every env's Ornstein-Uhlenbeck state."""
+    from imitation_amd.rl import noise, td3
+
+    class Recording(noise.VectorizedActionNoise):
+        calls = []
+
+        def reset(self, indices=None):
+            self.calls.append(None if indices is None else list(indices))
+            super().reset(indices)
+
+    venv = util.make_vec_env("Pendulum-v1", rng=rng, n_envs=2)
+    base = noise.OrnsteinUhlenbeckActionNoise(np.zeros(1), 0.1 * np.ones(1), rng=np.random.default_rng(0))
+    an = Recording(base, n_envs=2)
+    model = td3.TD3("MlpPolicy", venv, learning_starts=50, buffer_size=1000, batch_size=32, device="cpu", seed=0,
+                    action_noise=an, policy_kwargs=dict(net_arch=[16]))
+    model.learn(2 * 210)  # every env finishes one 200-step episode
+    assert Recording.calls and all(c is not None and len(c) == 1 for c in Recording.calls)
+    assert sorted(c[0] for c in Recording.calls) == [0, 1]
+
+
 def test_ou_noise_is_temporally_correlated_and_resets():
     from imitation_amd.rl import noise
 

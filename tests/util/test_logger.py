@@ -118,6 +118,77 @@ def test_tensorboard_event_file(tmp_path):
     assert files and files[0].stat().st_size > 0
 
 
+def _read_tfrecords(path):
+    """(tag, step, value) of every scalar Event in a TF event file, checking each record's
+    masked CRC32C with the pure-Python implementation."""
+    import struct
+
+    from imitation_amd.rl import logger as sb_logger
+
+    out = []
+    data = path.read_bytes()
+    i = 0
+    while i < len(data):
+        (n,) = struct.unpack_from("<Q", data, i)
+        hdr = data[i:i + 8]
+        assert struct.unpack_from("<I", data, i + 8)[0] == sb_logger._masked_crc(hdr)
+        ev = data[i + 12:i + 12 + n]
+        assert struct.unpack_from("<I", data, i + 12 + n)[0] == sb_logger._masked_crc(ev)
+        i += 16 + n
+        if b"brain.Event" in ev:
+            continue
+        # Event: 0x09 <f64 wall> 0x10 <varint step> 0x2a <len> summary
+        j = 9
+        step, shift = 0, 0
+        j += 1
+        while True:
+            b = ev[j]
+            step |= (b & 0x7F) << shift
+            j += 1
+            shift += 7
+            if b < 0x80:
+                break
+        summ = ev[j + 2:]
+        val = summ[2:]
+        tlen = val[1]
+        tag = val[2:2 + tlen].decode()
+        (v,) = struct.unpack_from("<f", val, 2 + tlen + 1)
+        out.append((tag, step, v))
+    return out
+
+
+def test_tensorboard_native_encoder_matches_python():
+    """``_C.tb_scalar_records`` (csrc/runtime/tb_events.cpp) is byte-identical to the Python
+    protobuf + CRC32C encoder, incl. multi-byte varints (long tags, large steps)."""
+    from imitation_amd import _native
+    from imitation_amd.rl import logger as sb_logger
+
+    C = _native.load(build_if_missing=False)
+    for b in (b"", b"a", b"123456789", bytes(range(256)) * 3):
+        assert C.crc32c(b) == sb_logger._crc32c(b)
+        assert C.masked_crc32c(b) == sb_logger._masked_crc(b)
+    assert C.crc32c(b"123456789") == 0xE3069283  # CRC-32C check value
+    tags = ["x", "mean/gen/train/value_loss", "t" * 200]
+    vals = [1.5, -3.25e-7, 12345.0]
+    for step in (0, 3, 300, 2**40 + 7):
+        assert C.tb_scalar_records(1.25e9, step, tags, vals) == sb_logger.encode_scalar_records(1.25e9, step, tags, vals)
+
+
+@pytest.mark.parametrize("background", [True, False])
+def test_tensorboard_writer_thread_round_trip(tmp_path, background, monkeypatch):
+    """Dumps queued to the writer thread are all on disk, in order, after flush / close."""
+    monkeypatch.setenv("IMITATION_AMD_TB_THREAD", "1" if background else "0")
+    h = logger.configure(str(tmp_path), ["tensorboard"])
+    for s in range(50):
+        h.record("a", float(s))
+        h.record("b", 2.0 * s)
+        h.dump(step=s)
+    h.close()
+    files = list(tmp_path.glob("events.out.tfevents.*"))
+    recs = _read_tfrecords(files[0])
+    assert recs == [(k, s, v) for s in range(50) for k, v in (("a", float(s)), ("b", 2.0 * s))]
+
+
 def test_free_form_text_levels(tmp_path):
     """Reference test_free_form: free-form messages reach log.txt at or above the level; inside
     accumulate_means they still go to the default output."""

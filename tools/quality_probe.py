@@ -1,0 +1,29 @@
+"""Normalised imitation scores of the device engines (imitation_amd/testing/imitation_quality.py).
+
+Usage: python tools/quality_probe.py [algo:env:steps[:seed] ...]  (default: the four CartPole /
+Pendulum GAIL / AIRL runs). One JSON line per run on stdout (and appended to $OUT if set)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from imitation_amd.testing import imitation_quality as iq
+
+    specs = sys.argv[1:] or ["gail:cartpole:200000", "airl:cartpole:200000", "gail:pendulum:500000", "airl:pendulum:500000"]
+    for spec in specs:
+        parts = spec.split(":")
+        algo, env, steps = parts[0], parts[1], int(parts[2])
+        seed = int(parts[3]) if len(parts) > 3 else 0
+        res = iq.run(algo, env, total_timesteps=steps, seed=seed, eval_every=max(steps // 5, 1), verbose=True)
+        line = json.dumps(res)
+        print(line, flush=True)
+        if os.environ.get("OUT"):
+            with open(os.environ["OUT"], "a") as f:
+                f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
