@@ -240,6 +240,38 @@ class AirlDiscPlan {
       IA_HIP_CHECK_A(ia::airl_norm(a, 0, 0, ia_stream()));
     }
   }
+  // Split update under data parallelism: the staging of update `slot`, minibatch k, in the two
+  // halves around the normaliser all-reduce -- mode 1: gather + local moments into `sums` (the
+  // caller all-reduces them), mode 2: the merges from the all-reduced sums (n_total rows) into
+  // the slot's normaliser rows. apply_grads(slot) runs the slot's fwd/bwd passes and the gradient
+  // / stats reduction only (the caller all-reduces `grads`, then adam(0, 1, ...)). Same launches,
+  // same data as the non-split DP update (bitwise).
+  void stage_part(int slot, int k, torch::Tensor e_idx, torch::Tensor g_idx, int mode, int n_total, bool merge_b,
+                  bool merge_p, bool merge_q) {
+    TORCH_CHECK(slot >= 0 && slot < n_slots_, "stage_part: slot ", slot, " outside the reserved ", n_slots_);
+    TORCH_CHECK(k >= 0 && k < n_mb_, "stage_part: minibatch ", k);
+    TORCH_CHECK(mode == 1 || mode == 2, "stage_part: mode 1 (gather + moments) or 2 (merges)");
+    TORCH_CHECK(a_.sums != nullptr, "stage_part needs the sums buffer");
+    ia::AirlDiscArgs a = slot_args(slot, k);
+    a.merge_b = merge_b;
+    a.merge_p = merge_p;
+    a.merge_q = merge_q;
+    if (mode == 1) {
+      check_idx(e_idx);
+      check_idx(g_idx);
+      a.e_idx = e_idx.data_ptr<int64_t>();
+      a.g_idx = g_idx.data_ptr<int64_t>();
+      IA_HIP_CHECK_A(ia::airl_gather(a, k, ia_stream()));
+      IA_HIP_CHECK_A(ia::airl_norm(a, 1, 0, ia_stream()));
+    } else {
+      IA_HIP_CHECK_A(ia::airl_norm(a, 2, n_total, ia_stream()));
+    }
+  }
+  void apply_grads(int slot, c10::optional<torch::Tensor> stats_out) {
+    TORCH_CHECK(slot >= 0 && slot < n_slots_, "apply_grads: slot ", slot, " was not staged");
+    for (int k = 0; k < n_mb_; ++k) IA_HIP_CHECK_A(ia::airl_fwd_bwd(slot_args(slot, k), plan_, k, ia_stream()));
+    adam(1, 0, 0.0, 1.0, stats_out);
+  }
   // stage / apply workspaces for n updates per round (grow only when no apply is pending)
   void reserve(int n) {
     if (n <= n_slots_) return;
@@ -320,6 +352,9 @@ void register_airl(py::module& m) {
       .def("adam", &AirlDiscPlan::adam, py::arg("reduce"), py::arg("do_adam"), py::arg("step_size"), py::arg("bc2_sqrt"),
            py::arg("stats_out") = py::none())
       .def("reserve", &AirlDiscPlan::reserve)
+      .def("stage_part", &AirlDiscPlan::stage_part, py::arg("slot"), py::arg("k"), py::arg("e_idx"), py::arg("g_idx"),
+           py::arg("mode"), py::arg("n_total"), py::arg("merge_b"), py::arg("merge_p"), py::arg("merge_q"))
+      .def("apply_grads", &AirlDiscPlan::apply_grads, py::arg("slot"), py::arg("stats_out") = py::none())
       .def("stage", &AirlDiscPlan::stage, py::arg("slot"), py::arg("e_idx"), py::arg("g_idx"), py::arg("merge_b"),
            py::arg("merge_p"), py::arg("merge_q"))
       .def("apply", &AirlDiscPlan::apply, py::arg("slot"), py::arg("step_size"), py::arg("bc2_sqrt"),

@@ -32,6 +32,8 @@ import os
 from typing import Any, Dict, List, Tuple
 
 import torch as th
+
+from imitation_amd.utils import profiling
 from numpy import prod as np_prod
 
 from imitation_amd.algorithms.adversarial import common
@@ -96,6 +98,7 @@ class OutputNormMixin:
             self._onorm_count = th.zeros(1, device=self._dev)
         return {"rew_raw": self._rew_raw}
 
+    @profiling.traced("rollout/reward_outnorm")
     def _post_rollout_rewards(self) -> None:
         out_norm = self._output_norm()
         if out_norm is None:
@@ -260,11 +263,14 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         # split rounds (single rank): the updates' gathers + norm merges are staged on the main
         # stream right after PPO, then the next rollout's step chain runs concurrently with the
         # fwd/bwd + Adam applies on the side stream (see _overlapped_round)
-        self._disc_split = (self._overlap_disc and pdist.world_size() == 1
-                            and os.environ.get("IMITATION_AMD_AIRL_SPLIT", "1") != "0")
+        # (data parallel too: the staging's normaliser all-reduces run on the main stream, the
+        # applies' gradient all-reduces on the side stream, where nothing else uses the
+        # communicator while they run -- the next step chain has no collectives)
+        self._disc_split = (self._overlap_disc and os.environ.get("IMITATION_AMD_AIRL_SPLIT", "1") != "0")
         if self._disc_split:
             self._disc_plan.reserve(max(1, self.n_disc_updates_per_round))
 
+    @profiling.traced("disc/stage")
     def _stage_disc_updates(self, n: int) -> List[Tuple[float, float]]:
         """The gathers and RunningNorm merges (policy, base, potential) of the round's ``n``
         updates, in update order (``AirlDiscPlan.stage``): everything of an update that the
@@ -284,24 +290,40 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         merge_p = self._pnorm is not None and self._pnorm.training
         merge_q = self.pol_norm is not None and self.pol_norm.training
         scal = []
+        world = pdist.world_size()
         for i in range(n):
             e_idx = self._endless_expert_iterator.next_indices()
             g_idx = th.randint(0, self._gen_dev.size(), (B,), device=self._dev)
-            self._disc_plan.stage(i, e_idx, g_idx, merge_b, merge_p, merge_q)
+            if world == 1 or not pdist.norm_sync_active():
+                self._disc_plan.stage(i, e_idx, g_idx, merge_b, merge_p, merge_q)
+            else:  # the DP update's order: gather, moments, all-reduce, merges -- per minibatch
+                mb = self.demo_minibatch_size
+                for k in range(B // mb):
+                    self._disc_plan.stage_part(i, k, e_idx, g_idx, 1, 0, merge_b, merge_p, merge_q)
+                    pdist.allreduce_sum_(self._disc_ws["sums"])
+                    self._disc_plan.stage_part(i, k, e_idx, g_idx, 2, 2 * mb * world, merge_b, merge_p, merge_q)
             t = t0 + i + 1.0
             scal.append((float(g["lr"]) / (1.0 - beta1**t), (1.0 - beta2**t) ** 0.5))
         return scal
 
+    @profiling.traced("disc/apply")
     def _apply_disc_updates(self, scal: List[Tuple[float, float]], steps: List[int]) -> None:
         """The fwd/bwd passes and Adam steps of the staged updates (``AirlDiscPlan.apply``)."""
         opt = self._disc_opt
+        world = pdist.world_size()
         for i, (step_size, bc2_sqrt) in enumerate(scal):
-            self._disc_plan.apply(i, step_size, bc2_sqrt, self._disc_stats[i])
+            if world == 1:
+                self._disc_plan.apply(i, step_size, bc2_sqrt, self._disc_stats[i])
+            else:  # mean gradient over ranks between the reduction and Adam (one-shot, in stream order)
+                self._disc_plan.apply_grads(i, self._disc_stats[i])
+                pdist.allreduce_grads_flat(self._disc_ws["grads"])
+                self._disc_plan.adam(0, 1, step_size, bc2_sqrt, None)
             for p in self._rflat.params:
                 opt.state[p]["step"] += 1
             self._disc_step += 1
             steps.append(self._disc_step)
 
+    @profiling.traced("disc/update")
     def _fused_disc_update(self, slot: int, defer_pol: bool = False, e_idx: th.Tensor = None, g_idx: th.Tensor = None,
                            apply: bool = True) -> None:
         """One discriminator optimizer step (== AdversarialTrainer.train_disc with AIRL's logits)

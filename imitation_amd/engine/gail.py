@@ -61,6 +61,7 @@ from imitation_amd.rewards import reward_nets
 from imitation_amd.rl.policies import ActorCriticPolicy
 from imitation_amd.rl.ppo import PPO
 from imitation_amd.util import networks
+from imitation_amd.utils import profiling
 
 
 def _unwrap_native(venv) -> Optional[NativeVecEnv]:
@@ -337,6 +338,7 @@ class DeviceGeneratorCore:
     # ------------------------------------------------------------------ one generator round
     _CHAIN_OUT = ("obs_buf", "act_raw", "act_env", "env_rew", "starts", "dones", "trunc", "next_obs", "ep_ret_out")
 
+    @profiling.traced("rollout/chain")
     def _launch_chain(self, explore_mode: Optional[th.Tensor] = None) -> None:
         """The serial part of a rollout (rollout.hip): T steps of actor sampling + env
         physics per env, nothing else on the step chain."""
@@ -352,6 +354,7 @@ class DeviceGeneratorCore:
         self._C.engine_rollout(args)
         self._step0 += self.T
 
+    @profiling.traced("rollout/reward_pass")
     def _launch_post(self, reward: bool) -> None:
         """The parallel part (engine.hip): V(s), log-probs, TimeLimit bootstrap and the learned
         reward of all T x N transitions, V of the final observations."""
@@ -382,6 +385,7 @@ class DeviceGeneratorCore:
     def _rollout_extra_bufs(self) -> Dict[str, Any]:
         return {}
 
+    @profiling.traced("ppo/update")
     def _ppo_update(self) -> None:
         algo: PPO = self.gen_algo
         rows = self.T * self.N
@@ -579,6 +583,7 @@ class DeviceGeneratorCore:
         norm.running_var.copy_(rv / tot)
         self.norm_count.add_(cnt)
 
+    @profiling.traced("eval/device")
     def device_evaluate(self, n_eval_episodes: int = 10, deterministic: bool = True, n_envs: Optional[int] = None,
                         seed: int = 0) -> Tuple[List[float], List[int]]:
         """``evaluate_policy(policy, venv, n_eval_episodes, deterministic, return_episode_rewards=True)``
@@ -737,6 +742,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
              "dones": th.bool}, self._dev)
         self._setup_fused_disc()
 
+    @profiling.traced("host/replay_store")
     def _store_generator_samples(self) -> None:
         """Replay-buffer content identical to BufferingWrapper -> flatten -> FIFO store."""
         wrapped_rew = None
@@ -844,6 +850,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 self._global_step += 1
             self._log_gen()
 
+    @profiling.traced("host/log_gen")
     def _log_gen(self, stats: Optional[th.Tensor] = None) -> None:
         """Record one generator round with the host trainer's key set: SB3 ``PPO.train`` metrics
         (:meth:`_ppo_log_values`), ``OnPolicyAlgorithm._dump_logs`` (``time/*``, Monitor
@@ -983,6 +990,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 v.zero_()
             opt.state[p] = {"step": step, "exp_avg": m, "exp_avg_sq": v}
 
+    @profiling.traced("disc/update")
     def _fused_disc_update(self, slot: int, defer_pol: bool = False) -> None:
         """One discriminator optimizer step (== AdversarialTrainer.train_disc) with no host sync.
         ``defer_pol``: record the policy-norm merges in slots ``slot * n_minibatches + k`` of
@@ -1033,6 +1041,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         return common.train_stats_from_sums(
             [v[0] / rows * (mb / B), v[1] / rows, float(mb), v[2], v[3], v[4], v[5] / rows], float(rows))
 
+    @profiling.traced("host/log_disc")
     def _record_disc(self, stats: Mapping[str, float], disc_step: int) -> None:
         self.logger.record("global_step", self._global_step)
         for k, v in stats.items():
@@ -1166,6 +1175,8 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         overlap = self._overlap_disc and n > 0 and self.gen_train_timesteps == self.T * self.N
         nxt = None
         self._fps_mark = (time.perf_counter(), self.gen_algo.num_timesteps)
+        timer = profiling.StepTimer(roctx=False)
+        timer.n0 = self.gen_algo.num_timesteps
         for r in range(n_rounds):
             if overlap:
                 # the next rollout is enqueued before this round's logging and callback (see
@@ -1193,6 +1204,18 @@ class DeviceEngineMixin(DeviceGeneratorCore):
             self.logger.dump(self._global_step)
         pdist.check_comm("GAIL training", blocking=True)
         self.check_errors(blocking=True)
+        self._report_throughput(timer)
+
+    def _report_throughput(self, timer: "profiling.StepTimer") -> None:
+        """Per-rank and whole-node env-steps/s of this ``train`` call: host wall
+        time of the call (its rounds are pipelined, so this is the sustained rate), one small
+        all-reduce under DP. Recorded as ``perf/*`` and kept in ``last_train_perf``."""
+        timer.add_env_steps(self.gen_algo.num_timesteps - timer.n0)
+        rep = timer.report()
+        self.last_train_perf = rep
+        for k in ("rank_env_steps_per_s", "node_env_steps_per_s", "elapsed_s", "world_size"):
+            self.logger.record(f"perf/{k}", rep[k])
+        self.logger.dump(self._global_step)
 
     def _launch_rollout(self) -> th.cuda.Event:
         """Enqueue one rollout (chain + post pass) and the async copy of its dones / returns to

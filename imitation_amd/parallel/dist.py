@@ -34,6 +34,12 @@ import torch.distributed as tdist
 _NORM_SYNC = True
 
 
+def _traced(name):
+    from imitation_amd.utils import profiling
+
+    return profiling.traced(name)
+
+
 def is_initialized() -> bool:
     return tdist.is_available() and tdist.is_initialized()
 
@@ -130,6 +136,7 @@ def _comm_device(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+@_traced("comm/allreduce_moments")
 def allreduce_moments(batch: torch.Tensor):
     """Global (mean, biased var, count) of ``batch`` rows across all ranks, one message."""
     b = batch.reshape(batch.shape[0], -1).double()
@@ -306,6 +313,7 @@ def allreduce_grads(params: Iterable[torch.nn.Parameter]) -> None:
         off += n
 
 
+@_traced("comm/allreduce_sum")
 def allreduce_sum_(t: torch.Tensor) -> None:
     """Sum all-reduce of ``t`` in place (one collective; no-op on one rank)."""
     if world_size() <= 1:
@@ -320,6 +328,7 @@ def allreduce_sum_(t: torch.Tensor) -> None:
         t.copy_(buf)
 
 
+@_traced("comm/allreduce_grads")
 def allreduce_grads_flat(flat: torch.Tensor) -> None:
     """Mean all-reduce of one flat gradient vector in place (one collective)."""
     if world_size() <= 1:
@@ -378,6 +387,7 @@ def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts).to(x.device)
 
 
+@_traced("comm/all_gather")
 def all_gather_flat(out: torch.Tensor, x: torch.Tensor) -> None:
     """Equal-size all-gather of ``x`` into ``out`` (``[world * n, ...]``, rank order), one collective."""
     if world_size() <= 1:

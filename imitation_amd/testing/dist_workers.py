@@ -337,7 +337,7 @@ def gail_round_worker(rank, world, seed):
             "oneshot_calls": 0 if c is None else c.calls}
 
 
-def airl_round_worker(rank, world, seed):
+def airl_round_worker(rank, world, seed, rounds=1):
     """One DeviceAIRL round (shaped reward net) on ``cuda:0`` shared by the ranks; reports
     whether the discriminator update ran fused (airl_disc.hip) or as a HIP-graph replay of
     the generic autograd update (``IMITATION_AMD_AIRL_FUSED=0``)."""
@@ -367,11 +367,13 @@ def airl_round_worker(rank, world, seed):
     tr = DeviceAIRL(demonstrations=demos, demo_batch_size=256, venv=venv, gen_algo=gen, reward_net=rn,
                     n_disc_updates_per_round=3, custom_logger=logger.configure(f"/tmp/ia_dp_airl_{rank}", format_strs=[]))
     graphed = tr._graphed_disc_ok()
-    tr.train(tr.gen_train_timesteps)
+    tr.train(rounds * tr.gen_train_timesteps)
     th.cuda.synchronize()
     c = oneshot._COMM
     g = getattr(tr, "_disc_graph", None)
     return {"reward": [p.detach().cpu().numpy().copy() for p in rn.parameters()],
+            "policy": [p.detach().cpu().numpy().copy() for p in gen.policy.parameters()],
+            "split": bool(getattr(tr, "_disc_split", False)),
             "norm": [b.detach().cpu().numpy().copy() for b in rn.buffers()],
             "graphed": graphed, "replays": 0 if g is None else g.n_replays,
             "fused": bool(getattr(tr, "_fused_disc", False)),

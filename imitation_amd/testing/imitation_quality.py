@@ -74,7 +74,7 @@ def pendulum_expert_demos():
     return serialize.load_with_rewards(PENDULUM_DEMOS)
 
 
-def _cartpole_trainer(algo: str, demos, seed: int, device, logger):
+def _cartpole_trainer(algo: str, demos, seed: int, device, logger, cap: int = 512):
     """The reference tutorials' GAIL / AIRL CartPole setups on the device engines."""
     from imitation_amd.engine.airl import DeviceAIRL
     from imitation_amd.engine.gail import DeviceGAIL
@@ -89,18 +89,18 @@ def _cartpole_trainer(algo: str, demos, seed: int, device, logger):
         learner = PPO(ActorCriticPolicy, venv, batch_size=64, ent_coef=0.0, learning_rate=4e-4, gamma=0.95, n_epochs=5,
                       seed=seed, device=device)
         rn = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
-        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, gen_replay_buffer_capacity=512,
+        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, gen_replay_buffer_capacity=cap,
                         n_disc_updates_per_round=8, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
     else:
         learner = PPO(ActorCriticPolicy, venv, batch_size=64, ent_coef=0.0, learning_rate=5e-4, gamma=0.95,
                       clip_range=0.1, vf_coef=0.1, n_epochs=5, seed=seed, device=device)
         rn = BasicShapedRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
-        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=2048, gen_replay_buffer_capacity=512,
+        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=2048, gen_replay_buffer_capacity=cap,
                         n_disc_updates_per_round=16, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
     return tr
 
 
-def _pendulum_trainer(algo: str, demos, seed: int, device, logger):
+def _pendulum_trainer(algo: str, demos, seed: int, device, logger, cap: int = 512):
     """Pendulum-v1 (continuous): SB3 MlpPolicy PPO with the rl-zoo Pendulum settings
     (gamma 0.9, gae_lambda 0.95, lr 1e-3, n_steps 1024 x 4 envs, 10 epochs, use_sde off)."""
     from imitation_amd.engine.airl import DeviceAIRL
@@ -116,17 +116,17 @@ def _pendulum_trainer(algo: str, demos, seed: int, device, logger):
                   n_epochs=10, ent_coef=0.0, clip_range=0.2, seed=seed, device=device)
     if algo == "gail":
         rn = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
-        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, gen_replay_buffer_capacity=512,
+        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, gen_replay_buffer_capacity=cap,
                         n_disc_updates_per_round=8, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
     else:
         rn = BasicShapedRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
-        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=2048, gen_replay_buffer_capacity=512,
+        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=2048, gen_replay_buffer_capacity=cap,
                         n_disc_updates_per_round=16, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
     return tr
 
 
 def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_000, seed: int = 0, n_eval: int = 50,
-        eval_every: Optional[int] = None, device: Any = "cuda", verbose: bool = False) -> Dict[str, Any]:
+        eval_every: Optional[int] = None, device: Any = "cuda", verbose: bool = False, cap: int = 512) -> Dict[str, Any]:
     """Train ``algo`` (``gail`` / ``airl``) on ``env`` (``cartpole`` / ``pendulum``) with expert
     demonstrations and report returns + normalised scores (before, during, after)."""
     from imitation_amd.util import logger as imit_logger
@@ -146,13 +146,17 @@ def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_00
     expert = float(np.mean([t.rews.sum() for t in demos]))
     rand = random_return(env_id, n_eval, seed)
     log = imit_logger.configure(f"/tmp/ia_quality_{os.getpid()}", format_strs=[])
-    tr = make(algo, demos, seed, device, log)
+    tr = make(algo, demos, seed, device, log, cap=cap)
+
+    last: Dict[str, List[float]] = {}
 
     def score() -> float:
         r, _ = tr.device_evaluate(n_eval, deterministic=True, seed=10_000 + seed)
+        last["returns"] = list(r)
         return float(np.mean(r))
 
     r0 = score()
+    returns_before = last["returns"]
     curve: List[Dict[str, float]] = [dict(timesteps=0, ret=r0, norm=normalized_score(r0, rand, expert))]
     step = int(eval_every or total_timesteps)
     step = max(tr.gen_train_timesteps, step // tr.gen_train_timesteps * tr.gen_train_timesteps)
@@ -173,4 +177,5 @@ def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_00
     final = curve[-1]["ret"]
     return dict(algo=algo, env=env_id, seed=seed, expert_return=expert, random_return=rand, learner_return_before=r0,
                 learner_return=final, normalized_score=normalized_score(final, rand, expert), curve=curve,
-                total_timesteps=done, train_s=round(t_train, 3), n_eval_episodes=n_eval, n_demo_episodes=len(demos))
+                total_timesteps=done, train_s=round(t_train, 3), n_eval_episodes=n_eval, n_demo_episodes=len(demos),
+                returns_before=returns_before, returns_after=last["returns"])

@@ -89,6 +89,32 @@ def range(name: str) -> Iterator[None]:  # noqa: A001 - mirrors roctx naming
         lib.roctxRangePop()
 
 
+def traced(name: str):
+    """Decorator: run the function inside ``range(name)`` when ROCTX ranges are on (disabled:
+    one flag test per call). The device engines mark their phases with it -- rollout chain,
+    reward pass, PPO update, discriminator updates, replay store, collectives, host logging --
+    so a ``rocprofv3 --marker-trace`` timeline attributes the host gaps to phases."""
+    import functools
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapper(*args, **kwargs):
+            if not _enabled:
+                return fn(*args, **kwargs)
+            lib = _load_roctx()
+            if lib is None:
+                return fn(*args, **kwargs)
+            lib.roctxRangePushA(name.encode())
+            try:
+                return fn(*args, **kwargs)
+            finally:
+                lib.roctxRangePop()
+
+        return wrapper
+
+    return deco
+
+
 class StepTimer:
     """Per-phase wall clock + env-step throughput, per rank and whole node.
 

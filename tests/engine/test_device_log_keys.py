@@ -35,6 +35,7 @@ class _FakeRound:
 
     _record_round_metrics = DeviceGeneratorCore._record_round_metrics
     _ppo_log_values = DeviceGeneratorCore._ppo_log_values
+    _fail_if_nonfinite = DeviceGeneratorCore._fail_if_nonfinite
     _track_wrapped_returns = DeviceEngineMixin._track_wrapped_returns
     _log_gen = DeviceEngineMixin._log_gen
 
@@ -137,3 +138,16 @@ def test_explained_variance_from_gae_moments():
     y, yp = ret.numpy().ravel(), val.numpy().ravel()
     want = 1 - np.var(y - yp) / np.var(y)
     assert np.isclose(rl_ops.explained_variance_from_moments(mom.numpy(), T * N), want, rtol=1e-4)
+
+
+def test_nonfinite_round_statistics_raise():
+    """Fail-fast on the host copy of a round's statistics (no device sync)."""
+    import pytest
+
+    from imitation_amd.utils.watchdog import NonFiniteError
+
+    fake = _FakeRound(None)
+    fake._global_step = 7
+    fake._fail_if_nonfinite({"train/loss": 1.0}, "PPO update")
+    with pytest.raises(NonFiniteError, match="round 7.*train/value_loss"):
+        fake._fail_if_nonfinite({"train/loss": 1.0, "train/value_loss": float("nan")}, "PPO update")

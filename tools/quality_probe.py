@@ -1,6 +1,6 @@
 """Normalised imitation scores of the device engines (imitation_amd/testing/imitation_quality.py).
 
-Usage: python tools/quality_probe.py [algo:env:steps[:seed] ...]  (default: the four CartPole /
+Usage: python tools/quality_probe.py [algo:env:steps[:seed[:replay capacity]] ...]  (default: the four CartPole /
 Pendulum GAIL / AIRL runs). One JSON line per run on stdout (and appended to $OUT if set)."""
 import json
 import os
@@ -17,7 +17,8 @@ def main():
         parts = spec.split(":")
         algo, env, steps = parts[0], parts[1], int(parts[2])
         seed = int(parts[3]) if len(parts) > 3 else 0
-        res = iq.run(algo, env, total_timesteps=steps, seed=seed, eval_every=max(steps // 5, 1), verbose=True)
+        cap = int(parts[4]) if len(parts) > 4 else 512
+        res = iq.run(algo, env, total_timesteps=steps, seed=seed, eval_every=max(steps // 10, 1), verbose=True, cap=cap)
         line = json.dumps(res)
         print(line, flush=True)
         if os.environ.get("OUT"):
