@@ -583,6 +583,58 @@ class DeviceGeneratorCore:
         norm.running_var.copy_(rv / tot)
         self.norm_count.add_(cnt)
 
+    def _eval_block(self, n: int, seed: int, deterministic: bool, reward: bool):
+        """A fresh block of ``n`` native envs (reset from ``seed``) and the scratch buffers of one
+        ``max_episode_steps`` launch of the rollout chain (+ the reward pass when ``reward``)."""
+        from imitation_amd.envs.vec_env import NativeVecEnv
+
+        dev = self._dev
+        ev = NativeVecEnv(self._native.env_id, n, seed=int(seed), max_episode_steps=self.max_steps)
+        obs0 = ev.reset()
+        st = ev.get_state()
+        T = self.max_steps  # every env finishes >= 1 episode per launch (TimeLimit)
+        Aw = 1 if self.discrete else self.A
+        z = lambda *s: th.zeros(*s, device=dev)  # noqa: E731
+        bufs = dict(obs_buf=z(T, n, self.D), act_raw=z(T, n, Aw), act_env=z(T, n, Aw), env_rew=z(T, n),
+                    starts=z(T, n), trunc=z(T, n), next_obs=z(T, n, self.D))
+        if reward:
+            bufs.update(values=z(T, n), logp=z(T, n), boot=z(T, n), rewards=z(T, n), last_values=z(n))
+        pol = self.gen_algo.policy
+        args = dict(env=self._native.env_id, max_steps=self.max_steps, T=T, N=n,
+                    seed=int(seed) * 0x2545F4914F6CDD1D & ((1 << 62) - 1),
+                    state=th.as_tensor(st["state"], device=dev).float().contiguous(),
+                    rng=th.as_tensor(st["rng"].astype(np.int64), device=dev).contiguous(),
+                    elapsed=th.as_tensor(st["elapsed"].astype(np.int32), device=dev).contiguous(), ep_ret=z(n),
+                    cur_obs=th.as_tensor(np.asarray(obs0, np.float32), device=dev).reshape(n, self.D).contiguous(),
+                    cur_start=th.ones(n, device=dev),
+                    pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
+                    log_std=pol.log_std.detach() if self.has_log_std else None, act_low=self.act_low,
+                    act_high=self.act_high, n_actions=self.A if self.discrete else 0, deterministic=int(deterministic))
+        return T, bufs, args
+
+    def _eval_learned_reward(self, T: int, n: int, bufs: Dict[str, th.Tensor], args: Dict[str, Any],
+                             dones: th.Tensor, out: th.Tensor) -> None:
+        """The learned reward of one eval launch (the reward pass of training rollouts, written
+        without the TimeLimit bootstrap) into ``out`` [T, n]."""
+        algo: PPO = self.gen_algo
+        pol = algo.policy
+        d = dict(T=T, N=n, D=self.D, A=1 if self.discrete else self.A, n_actions=self.A if self.discrete else 0,
+                 gamma=float(algo.gamma), cur_obs=args["cur_obs"],
+                 pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
+                 vf=self._wave_mlp(self.vf_layers, self.hidden_act, 0, self.pol_norm),
+                 log_std=pol.log_std.detach() if self.has_log_std else None, rew_enabled=1, dones=dones)
+        d.update({k: bufs[k] for k in ("obs_buf", "act_raw", "act_env", "next_obs", "trunc", "env_rew", "values",
+                                       "logp", "boot", "rewards", "last_values")})
+        d.update(self._reward_spec())
+        self._C.engine_rollout_post(d)
+        out.copy_(bufs["rewards"] - bufs["boot"])
+
+    def _eval_supports_learned_reward(self) -> bool:
+        """AIRL's output normalisation runs in a separate pass over the training buffers; its
+        evaluation-time rewards come from the host path."""
+        out_norm = getattr(self, "_output_norm", None)
+        return out_norm is None or out_norm() is None
+
     @profiling.traced("eval/device")
     def device_evaluate(self, n_eval_episodes: int = 10, deterministic: bool = True, n_envs: Optional[int] = None,
                         seed: int = 0) -> Tuple[List[float], List[int]]:
@@ -595,37 +647,16 @@ class DeviceGeneratorCore:
         contributes its first ``(n_eval_episodes + i) // n_envs`` episodes, as SB3 counts them;
         returns (episode returns, episode lengths) in completion order. The training envs, the
         policy and every normaliser are untouched."""
-        from imitation_amd.envs.vec_env import NativeVecEnv
-
-        dev = self._dev
         n = int(n_envs or self.N)
         targets = np.array([(n_eval_episodes + i) // n for i in range(n)], dtype=np.int64)
         n_chunks = int(targets.max(initial=0))
         if n_chunks == 0:
             return [], []
-        ev = NativeVecEnv(self._native.env_id, n, seed=int(seed), max_episode_steps=self.max_steps)
-        obs0 = ev.reset()
-        st = ev.get_state()
-        T = self.max_steps  # every env finishes >= 1 episode per launch (TimeLimit)
-        Aw = 1 if self.discrete else self.A
-        z = lambda *s: th.zeros(*s, device=dev)  # noqa: E731
-        scratch = dict(obs_buf=z(T, n, self.D), act_raw=z(T, n, Aw), act_env=z(T, n, Aw), env_rew=z(T, n),
-                       starts=z(T, n), trunc=z(T, n), next_obs=z(T, n, self.D))
-        dones = z(n_chunks, T, n)
-        rets = z(n_chunks, T, n)
-        pol = self.gen_algo.policy
-        args = dict(env=self._native.env_id, max_steps=self.max_steps, T=T, N=n, seed=int(seed) * 0x2545F4914F6CDD1D & ((1 << 62) - 1),
-                    state=th.as_tensor(st["state"], device=dev).float().contiguous(),
-                    rng=th.as_tensor(st["rng"].astype(np.int64), device=dev).contiguous(),
-                    elapsed=th.as_tensor(st["elapsed"].astype(np.int32), device=dev).contiguous(), ep_ret=z(n),
-                    cur_obs=th.as_tensor(np.asarray(obs0, np.float32), device=dev).reshape(n, self.D).contiguous(),
-                    cur_start=th.ones(n, device=dev),
-                    pi=self._wave_mlp(self.pi_layers, self.hidden_act, 0, self.pol_norm),
-                    log_std=pol.log_std.detach() if self.has_log_std else None, act_low=self.act_low,
-                    act_high=self.act_high, n_actions=self.A if self.discrete else 0, deterministic=int(deterministic),
-                    **scratch)
+        T, bufs, args = self._eval_block(n, seed, deterministic, reward=False)
+        dones = th.zeros(n_chunks, T, n, device=self._dev)
+        rets = th.zeros(n_chunks, T, n, device=self._dev)
         for c in range(n_chunks):
-            args.update(step0=c * T, dones=dones[c], ep_ret_out=rets[c])
+            args.update(bufs, step0=c * T, dones=dones[c], ep_ret_out=rets[c])
             self._C.engine_rollout(args)
         d = dones.reshape(n_chunks * T, n).cpu().numpy() > 0.5
         r = rets.reshape(n_chunks * T, n).cpu().numpy()
@@ -642,6 +673,70 @@ class DeviceGeneratorCore:
                 ep_lengths.append(int(length))
                 count[e] += 1
         return ep_rewards, ep_lengths
+
+    @profiling.traced("eval/device_stats")
+    def device_rollout_stats(self, n_episodes: int, deterministic: bool = False, seed: Optional[int] = None,
+                             n_envs: Optional[int] = None) -> Optional[Dict[str, float]]:
+        """``rollout_stats(generate_trajectories(policy, venv_train, make_min_episodes(n)))`` -- the
+        CLI's final ``imit_stats`` (reference ``scripts/ingredients/policy_evaluation.py``) -- on the
+        GPU: stochastic actions by default (``generate_trajectories``' default), the same
+        unbiased stopping (once >= ``n`` episodes are done, every env finishes its episode in
+        flight and stops), ``return_*`` from the learned reward the training rollouts see and
+        ``monitor_return_*`` / ``len_*`` from the env. A fresh env block reset from ``seed``
+        (default: derived from the engine seed); the training state is untouched. Returns None
+        where the learned reward is not available on this path (AIRL with output normalisation)."""
+        if not self._eval_supports_learned_reward():
+            return None
+        n = int(n_envs or self.N)
+        seed = int(self._seed % (1 << 31)) + 7 if seed is None else int(seed)
+        T, bufs, args = self._eval_block(n, seed, deterministic, reward=not self.debug_use_ground_truth)
+        dl, rl, wl = [], [], []
+        count = 0
+        c = 0
+        finishing = False
+        while True:  # launches until >= n episodes, then one more so every in-flight episode ends
+            dones, rets = th.zeros(T, n, device=self._dev), th.zeros(T, n, device=self._dev)
+            args.update(bufs, step0=c * T, dones=dones, ep_ret_out=rets)
+            self._C.engine_rollout(args)
+            if self.debug_use_ground_truth:
+                w = bufs["env_rew"].clone()
+            else:
+                w = th.zeros(T, n, device=self._dev)
+                self._eval_learned_reward(T, n, bufs, args, dones, w)
+            dl.append(dones)
+            rl.append(rets)
+            wl.append(w)
+            c += 1
+            if finishing:
+                break
+            count += int(dones.sum().item())
+            finishing = count >= n_episodes
+        d = th.cat(dl).cpu().numpy() > 0.5
+        r = th.cat(rl).cpu().numpy()
+        wr = th.cat(wl).double().cpu().numpy()
+        cs = np.cumsum(wr, axis=0)
+        active = np.ones(n, dtype=bool)
+        start = np.zeros(n, dtype=np.int64)
+        rets, lens, mon = [], [], []
+        for t in range(d.shape[0]):
+            fin = np.flatnonzero(d[t] & active)
+            for e in fin.tolist():
+                ln = t - start[e] + 1
+                rets.append(float(cs[t, e] - (cs[start[e] - 1, e] if start[e] > 0 else 0.0)))
+                lens.append(int(ln))
+                mon.append(float(r[t, e]))
+            for e in np.flatnonzero(d[t]).tolist():
+                start[e] = t + 1
+            if len(rets) >= n_episodes:
+                active &= ~d[t]
+            if not active.any():
+                break
+        out: Dict[str, float] = {"n_traj": len(rets)}
+        for name, vals in (("return", np.asarray(rets)), ("len", np.asarray(lens)), ("monitor_return", np.asarray(mon))):
+            for stat in ("min", "mean", "std", "max"):
+                out[f"{name}_{stat}"] = getattr(np, stat)(vals).item()
+        out["monitor_return_len"] = len(mon)
+        return out
 
     def sync_env_to_host(self) -> None:
         """Copy the device env state back into the native host env (e.g. before host-side evaluation)."""

@@ -572,6 +572,14 @@ def _parse_value(text: str):
         return text
 
 
+#: Sacred's run options (``sacred/commandline_options.py``) accepted before ``with``.
+SACRED_RUN_OPTIONS = frozenset({
+    "name", "capture", "unobserved", "force", "comment", "loglevel", "id", "debug", "pdb", "beat_interval",
+    "queue", "priority", "enforce_clean", "print_config", "help", "file_storage", "mongo_db", "sql", "s3",
+    "tiny_db", "sacred_only", "config", "option",
+})
+
+
 def parse_command_line(argv: Sequence[str], commands: Iterable[str]) -> Tuple[Optional[str], List[str], Dict, Dict]:
     commands = set(commands)
     command = None
@@ -600,9 +608,13 @@ def parse_command_line(argv: Sequence[str], commands: Iterable[str]) -> Tuple[Op
             opts["capture"] = args[i + 1]
             i += 1
         elif a.startswith("--") and not seen_with:
-            # any other Sacred run option (--name=run0, --capture=sys, --unobserved, ...): an
-            # option, never a config update
+            # another Sacred run option (--name=run0, --capture=sys, --unobserved, ...): an option,
+            # never a config update; anything else is an error, as Sacred rejects unknown flags
+            # (a typo such as --print-config must not be ignored silently)
             key, _, val = a[2:].partition("=")
+            if key not in SACRED_RUN_OPTIONS:
+                raise ValueError(f"unknown command-line option {a!r} (known: "
+                                 f"{', '.join('--' + o for o in sorted(SACRED_RUN_OPTIONS))})")
             opts[key] = val if _ else True
         elif a == "with":
             seen_with = True

@@ -33,3 +33,17 @@ def eval_policy(rl_algo, venv, n_episodes_eval: int, _rnd: np.random.Generator) 
         train_env = venv
     trajs = rollout.generate_trajectories(rl_algo, train_env, sample_until=sample_until, rng=_rnd)
     return rollout.rollout_stats(trajs)
+
+
+@policy_evaluation_ingredient.capture
+def eval_trainer(trainer, venv, n_episodes_eval: int, _rnd: np.random.Generator) -> Mapping[str, float]:
+    """:func:`eval_policy` of ``trainer.policy`` on ``venv``, run on the GPU by a device engine
+    (``device_rollout_stats``: the same ``rollout_stats`` keys and stopping rule, stochastic actions,
+    learned-reward returns; no host round trip per env step) when it offers it for this
+    configuration, else on the host."""
+    dev = getattr(trainer, "device_rollout_stats", None)
+    if dev is not None:
+        stats = dev(n_episodes_eval)
+        if stats is not None:
+            return stats
+    return eval_policy(trainer.policy, venv)

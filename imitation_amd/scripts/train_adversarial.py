@@ -135,7 +135,7 @@ def train_adversarial(_run, show_config: bool, algo_cls: Type[common.Adversarial
 
             trainer.train(total_timesteps, callback)
             wd.beat()
-            imit_stats = policy_evaluation.eval_policy(trainer.policy, trainer.venv_train)
+            imit_stats = policy_evaluation.eval_trainer(trainer, trainer.venv_train)
     if checkpoint_interval >= 0:
         save(trainer, log_dir / "checkpoints" / "final")
     return {"imit_stats": imit_stats, "expert_stats": rollout.rollout_stats(expert_trajs), "engine": trainer.engine_kind}

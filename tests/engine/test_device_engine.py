@@ -870,3 +870,25 @@ def test_device_engine_nan_reward_weight_fails_fast(kind):
         next(tr._reward_net.parameters()).view(-1)[0] = float("nan")
     with pytest.raises(NonFiniteError, match="round"):
         tr.train(tr.gen_train_timesteps)
+
+
+@gpu
+def test_device_rollout_stats_match_host_rollout_stats():
+    """The CLI's final imit_stats on the GPU (``device_rollout_stats``): the host
+    ``rollout_stats(generate_trajectories(...))`` key set, unbiased stopping (>= n episodes, every
+    env finishes its episode in flight), learned-reward returns that agree with the host reward
+    wrapper's in distribution (stochastic policy, independent streams: means within a few %)."""
+    from imitation_amd.data import rollout as rollout_mod
+
+    tr, venv, gen, rn = _setup(env_id="Pendulum-v1", n_envs=4, n_steps=32, batch=64)
+    tr.train(2 * tr.gen_train_timesteps)
+    dev = tr.device_rollout_stats(40)
+    tr.sync_env_to_host()
+    trajs = rollout_mod.generate_trajectories(gen.policy, tr.venv_train, rollout_mod.make_min_episodes(40),
+                                              rng=np.random.default_rng(0))
+    host = rollout_mod.rollout_stats(trajs)
+    assert set(dev) == set(host), set(dev) ^ set(host)
+    assert dev["n_traj"] >= 40 and dev["n_traj"] % 4 == 0  # fixed horizon: every env stops together
+    assert dev["len_min"] == dev["len_max"] == 200
+    for k in ("return_mean", "monitor_return_mean"):
+        assert abs(dev[k] - host[k]) <= 0.15 * abs(host[k]) + 1.0, (k, dev[k], host[k])

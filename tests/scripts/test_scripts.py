@@ -289,3 +289,17 @@ def test_convert_trajs(tmp_path):
     shutil.copy(os.path.join(TESTDATA, "expert_models", "cartpole_0", "rollouts", "final.npz"), src)
     out = convert_trajs.update_traj_file_in_place(src)
     assert out == tmp_path / "final" and len(serialize.load(out)) == len(serialize.load(src))
+
+
+def test_unknown_option_before_with_raises():
+    """an unknown ``--option`` (e.g. the typo ``--print-config``) fails like Sacred
+    instead of being ignored; Sacred's run options are still accepted."""
+    import pytest
+
+    from imitation_amd.scripts.config_engine import parse_command_line
+
+    cmd, named, upd, opts = parse_command_line(["--name=run0", "--capture=sys", "--unobserved", "gail", "with", "x=1"],
+                                               ["gail"])
+    assert cmd == "gail" and upd == {"x": 1} and opts == {"name": "run0", "capture": "sys", "unobserved": True}
+    with pytest.raises(ValueError, match="print-config"):
+        parse_command_line(["--print-config", "gail"], ["gail"])
