@@ -69,8 +69,9 @@ def make_step(name, device, rank, args):
             return 50 * tr.minibatch_size if hasattr(tr, "minibatch_size") else 50 * 32
 
         return b, step, "samples/s", tr.policy, b.venv
+    demos = getattr(args, "_demos", {}).get(name)
     if name == "gail_halfcheetah":
-        b = models.build(name, device=device, seed=args.seed, rank=rank)
+        b = models.build(name, device=device, seed=args.seed, rank=rank, demonstrations=demos)
         tr = b.trainer
 
         def step(k: int = 1):  # k rounds in one train() call (round r + 1 enqueued behind r)
@@ -80,7 +81,7 @@ def make_step(name, device, rank, args):
         step.multi = True
         return b, step, "env-steps/s", tr.gen_algo.policy, b.venv
     if name == "airl_hopper":
-        b = models.build(name, device=device, seed=args.seed, rank=rank)
+        b = models.build(name, device=device, seed=args.seed, rank=rank, demonstrations=demos)
         tr = b.trainer
 
         def step(k: int = 1):  # k rounds in one train() call (round r + 1 enqueued behind r)
@@ -117,9 +118,41 @@ def make_step(name, device, rank, args):
     raise KeyError(name)
 
 
+EXPERT_CONFIGS = ("gail_halfcheetah", "airl_hopper")
+
+
+def make_expert(name, args, device):
+    """Expert mode (``--expert-steps``): a PPO expert trained on the env reward by the device
+    engine with the config's own generator (``debug_use_ground_truth``), its stochastic rollouts
+    as the demonstrations (``DeviceGeneratorCore.device_demonstrations``); returns (demos,
+    R_expert of its deterministic evaluation, expert training seconds)."""
+    import torch as th
+
+    from imitation_amd import models
+
+    t0 = time.perf_counter()
+    ex = models.build(name, device=device, seed=args.seed + 100, debug_use_ground_truth=True)
+    ex.trainer.train(max(ex.trainer.gen_train_timesteps, args.expert_steps))
+    _sync(device)
+    t_ex = time.perf_counter() - t0
+    r, _ = ex.trainer.device_evaluate(args.eval_episodes_expert, deterministic=True, seed=10_000 + args.seed)
+    demos = ex.trainer.device_demonstrations(args.expert_demo_steps, deterministic=False, seed=20_000 + args.seed)
+    del ex
+    th.cuda.empty_cache()
+    return demos, float(np.mean(r)), t_ex
+
+
 def run_config(name, args, device, rank, world):
     from imitation_amd.parallel import dist as pdist
 
+    expert = None
+    if args.expert_steps > 0 and name in EXPERT_CONFIGS:
+        if world > 1:
+            raise SystemExit("--expert-steps is a single-rank mode")
+        demos, r_expert, t_ex = make_expert(name, args, device)
+        args._demos = {name: demos}
+        expert = dict(expert_return=round(r_expert, 3), expert_steps=args.expert_steps, expert_train_s=round(t_ex, 3),
+                      n_demo_transitions=len(demos.acts))
     b, step, unit, policy, venv = make_step(name, device, rank, args)
     multi = getattr(step, "multi", False)  # the step runs k rounds in one call (as training does)
     if multi:
@@ -141,17 +174,32 @@ def run_config(name, args, device, rank, world):
     pdist.barrier()
     dt = pdist.allreduce_scalars([time.perf_counter() - t0], op="max")[0]
     total = units * world
+    if expert is not None:  # imitation budget (untimed), then the normalised score
+        from imitation_amd.testing import imitation_quality as iq
+
+        done = (args.warmup + args.steps) * b.trainer.gen_train_timesteps
+        if args.imit_steps > done:
+            b.trainer.train((args.imit_steps - done) // b.trainer.gen_train_timesteps * b.trainer.gen_train_timesteps)
+        r, _ = b.trainer.device_evaluate(args.eval_episodes_expert, deterministic=True, seed=10_000 + args.seed)
+        rand = iq.random_return(b.env_id, args.eval_episodes_expert, args.seed)
+        expert.update(learner_return=round(float(np.mean(r)), 3), random_return=round(rand, 3),
+                      imit_steps=max(args.imit_steps, done),
+                      normalized_score=round(iq.normalized_score(float(np.mean(r)), rand, expert["expert_return"]), 4))
     if hasattr(b.trainer, "sync_env_to_host"):
         b.trainer.sync_env_to_host()
     ret = _eval(policy, venv, args.eval_episodes)
     if ret is not None:
         ret = pdist.allreduce_scalars([ret], op="sum")[0] / world
-    return {
+    out = {
         "config": name, "env": b.env_id, "value": round(total / dt, 2), "unit": unit, "n_gpus": world if device.type == "cuda" else 0,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
         "final_eval_return": None if ret is None else round(float(ret), 3), "engine": b.extras.get("engine", "host"),
         "device": str(device), "data": "synthetic env + synthetic demos, random-init weights",
     }
+    if expert is not None:
+        out.update(expert, data="synthetic env; demonstrations = rollouts of a device-PPO expert trained on the env "
+                                "reward; random-init learner")
+    return out
 
 
 def main():
@@ -165,6 +213,12 @@ def main():
     p.add_argument("--dagger-round-steps", type=int, default=2048)
     p.add_argument("--pref-comparisons", type=int, default=5000)
     p.add_argument("--out", default=None, help="append JSON lines to this file (rank 0)")
+    p.add_argument("--expert-steps", type=int, default=0,
+                   help="expert mode (gail_halfcheetah / airl_hopper): train a PPO expert on the env reward for this "
+                        "many steps, imitate its rollouts, report the normalised score")
+    p.add_argument("--expert-demo-steps", type=int, default=50_000)
+    p.add_argument("--imit-steps", type=int, default=5_000_000, help="expert mode: learner env steps before scoring")
+    p.add_argument("--eval-episodes-expert", type=int, default=50)
     p.add_argument("--gpus", type=int, default=1,
                    help="data-parallel ranks, one per GPU (self-spawned without a launcher; weak scaling)")
     args = p.parse_args()

@@ -224,10 +224,6 @@ void ppo_update(py::dict d) {
   a.err = reinterpret_cast<unsigned*>(tptr<int>(d, "err", true));
   a.spin_limit = (unsigned)ival(d, "spin_limit", 0);
   a.debug_stall = ival(d, "debug_stall", 0);
-  {
-    const char* ev = getenv("IMITATION_AMD_PPO_XMASK");
-    a.xmask_off = ev && ev[0] == '0' ? 1 : 0;
-  }
   a.rc_cus = ival(d, "rc_cus", 0);
   TORCH_CHECK(a.D <= 64, "obs dim <= 64");
   ia::PPORcGeo geo;

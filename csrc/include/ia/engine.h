@@ -173,7 +173,6 @@ struct PPOArgs {
   unsigned spin_limit;  // sleeps before a spin gives up (0 = default 2^22)
   int debug_stall;      // test knob: the last working workgroup never publishes (forces a timeout)
   int rc_cus;           // CU count to plan against (0 = query the current device)
-  int xmask_off;        // A/B knob (IMITATION_AMD_PPO_XMASK=0): exchange padding lanes too
 };
 
 // CUs of the current device (cached per device; IMITATION_AMD_PPO_CUS overrides, e.g. tests).

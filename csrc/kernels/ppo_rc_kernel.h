@@ -200,26 +200,8 @@ __device__ __forceinline__ void load_rows(const PPORcGeo& g, size_t slot, int ro
 // flight per lane and ONE wait per batch of IB = 8 / G items (a load round trip is ~1.2K
 // cycles; a wait per item and 4 groups made the loads the exchange's dominant cost).
 // ids[s]: item id of owned slot s (-1: empty slot).
-// xmask: bit it set where this lane's 16 B of slot it hold any real (non-padding) element. The
-// partials of padding lanes are exactly 0 (zeroed images) and are neither published nor loaded
-// (a masked lane reads 0): the exchange reads are served at the cross-XCD rate (sc1 producer
-// stores drop the line from L2), so their bytes -- ~half padding for narrow nets -- are its cost.
-__device__ __forceinline__ bool xbit(unsigned m, int i) { return (m >> i) & 1u; }
-
-// Masked sc1 loads without branches: a raw buffer resource over the exchange region, and a
-// masked lane's offset pushed past num_records -- the buffer unit returns 0 for it and issues
-// no memory access (a branch around an inline-asm load per slot cost registers and scratch).
-typedef __amdgpu_buffer_rsrc_t brsrc;
-__device__ __forceinline__ brsrc xrsrc(const float* base, size_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ f4 ld_sc1_x4_b(brsrc r, unsigned off_bytes, bool on) {
-  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, on ? off_bytes : 0x7ffffff0u, 0, 16));
-}
-
 template <int GT, int KI, int NF = 16>
-__device__ __forceinline__ void exchange_sum(brsrc xr, unsigned slab_off, int n_items, const int (&ids)[KI], int lane,
-                                             f4 (&xg)[KI], unsigned xmask) {
+__device__ __forceinline__ void exchange_sum(const float* slab, int n_items, const int (&ids)[KI], int lane, f4 (&xg)[KI]) {
   constexpr int IB0 = NF / GT;
   constexpr int IB = IB0 < KI ? IB0 : KI;
 #pragma unroll
@@ -229,11 +211,12 @@ __device__ __forceinline__ void exchange_sum(brsrc xr, unsigned slab_off, int n_
     for (int i = 0; i < IB; ++i) {
       const int it = i0 + i;
       const int id = it < KI && ids[it] >= 0 ? ids[it] : 0;
-      const bool on = it < KI && xbit(xmask, it);
 #pragma unroll
-      for (int gi = 0; gi < GT; ++gi)
-        v[i * GT + gi] = ld_sc1_x4_b(xr, slab_off + (unsigned)(((gi * n_items + id) * 256 + lane * 4) * 4), on);
+      for (int gi = 0; gi < GT; ++gi) v[i * GT + gi] = ld_sc1_x4(slab + ((size_t)gi * n_items + id) * 256 + lane * 4);
     }
+#pragma unroll
+    for (int e = IB * GT; e < NF; ++e) v[e] = v[0];
+    wait_vm_n<NF>(v);
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int it = i0 + i;
@@ -251,25 +234,24 @@ __device__ __forceinline__ void exchange_sum(brsrc xr, unsigned slab_off, int n_
 // loads (<= KI + GT - 1) are issued back to back before ONE wait; slot ids are computed by
 // slot_id (register arrays indexed by the run-time grp would go to scratch).
 template <int GT, int KI, typename SlotId>
-__device__ __forceinline__ void reduce_slots(brsrc xr, unsigned slab_off, float* red, size_t gs, int grp, int lane,
-                                             const SlotId& slot_id, unsigned xmask) {
+__device__ __forceinline__ void reduce_slots(const float* slab, float* red, size_t gs, int grp, int lane, const SlotId& slot_id) {
   constexpr int RM = (KI + GT - 1) / GT;
   f4 v[RM * GT];
   int rid[RM];
-  bool on[RM];
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int sl = grp + r * GT;
     rid[r] = sl < KI ? slot_id(sl) : -1;
-    on[r] = sl < KI && xbit(xmask, sl);
     const int id = rid[r] >= 0 ? rid[r] : 0;
 #pragma unroll
-    for (int gi = 0; gi < GT; ++gi)
-      v[r * GT + gi] = ld_sc1_x4_b(xr, slab_off + (unsigned)((gi * gs + (size_t)id * 256 + lane * 4) * 4), on[r]);
+    for (int gi = 0; gi < GT; ++gi) v[r * GT + gi] = ld_sc1_x4(slab + (size_t)gi * gs + (size_t)id * 256 + lane * 4);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int e = 0; e < RM * GT; ++e) asm volatile("" : "+v"(v[e])::"memory");  // results tied to the wait
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
-    if (rid[r] < 0 || !on[r]) continue;
+    if (rid[r] < 0) continue;
     f4 sacc = v[r * GT];
 #pragma unroll
     for (int gi = 1; gi < GT; ++gi) sacc += v[r * GT + gi];
@@ -683,21 +665,6 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
     b_okf[ib] = ok ? 1.f : 0.f;
     if (ok) b_addr[ib] = kind == 1 ? y.b + lane : g.ls_off + lane;
   }
-  // exchange lane masks (xbit): weight slot it -- any of this lane's rows 16 ta + 4 kk + j
-  // (j < 4) below dout and its column 16 tb + r16 below din; vector slots -- a real element
-  unsigned xmask = 0u;
-#pragma unroll
-  for (int it = 0; it < KW; ++it) {
-    if (it >= nwi) continue;
-    const int desc = rfl(g.items[wb + w + it * kWaves]);
-    const int iq = desc & 1, il = (desc >> 1) & 3, ta = (desc >> 5) & 15, tb = (desc >> 9) & 15;
-    const int dout_u = rfl(g.dout[iq][il]), din_u = rfl(g.din[iq][il]);
-    if (16 * ta + 4 * kk < dout_u && 16 * tb + r16 < din_u) xmask |= 1u << it;
-  }
-#pragma unroll
-  for (int ib = 0; ib < KB; ++ib)
-    if (bkind[ib] >= 0 && b_okf[ib] != 0.f) xmask |= 1u << (KW + ib);
-  if (a.xmask_off) xmask = 0xffffffffu;  // A/B knob: exchange every lane (the unmasked form)
   float pre_m = 0.f, pre_v = 0.f;  // moments of the next minibatch to merge
   if (norm_lane && K > 1) {
     pre_m = g.mom[128 + nc];
@@ -1233,13 +1200,9 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         xg[KW + ib] = {bg[ib], 0.f, 0.f, 0.f};
       }
       float* slab = g.slab + (size_t)(k & 1) * G * n_items * 256;
-      // one buffer resource over both slab halves and both reduction halves (g.slab .. g.red + 2 n_items KB)
-      const brsrc xr = xrsrc(g.slab, (size_t)(2 * G + 2) * n_items * 256 * sizeof(float));
-      const unsigned slab_off = (unsigned)((size_t)(k & 1) * G * n_items * 256 * sizeof(float));
-      const unsigned red_off = (unsigned)(((size_t)2 * G * n_items * 256 + (size_t)(k & 1) * n_items * 256) * sizeof(float));
 #pragma unroll
       for (int it = 0; it < KI; ++it) {
-        if (ids[it] < 0 || !xbit(xmask, it)) continue;
+        if (ids[it] < 0) continue;
         st_sc1_x4(slab + ((size_t)grp * n_items + ids[it]) * 256 + lane * 4, xg[it]);
       }
       const unsigned long long e0 = a.prof ? clock64() : 0;
@@ -1274,10 +1237,10 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
           if (sl < KW) return sl < nwi ? wb + w + sl * kWaves : -1;
           return w + (sl - KW) * kWaves < nbq ? bb + w + (sl - KW) * kWaves : -1;
         };
-        if (G == 2) reduce_slots<2, KI>(xr, slab_off, red, gs, grp, lane, slot_id, xmask);
-        else if (G == 4) reduce_slots<4, KI>(xr, slab_off, red, gs, grp, lane, slot_id, xmask);
-        else if (G == 8) reduce_slots<8, KI>(xr, slab_off, red, gs, grp, lane, slot_id, xmask);
-        else if (G == 16) reduce_slots<16, KI>(xr, slab_off, red, gs, grp, lane, slot_id, xmask);
+        if (G == 2) reduce_slots<2, KI>(slab, red, gs, grp, lane, slot_id);
+        else if (G == 4) reduce_slots<4, KI>(slab, red, gs, grp, lane, slot_id);
+        else if (G == 8) reduce_slots<8, KI>(slab, red, gs, grp, lane, slot_id);
+        else if (G == 16) reduce_slots<16, KI>(slab, red, gs, grp, lane, slot_id);
         else if (g.xstash >= 0) {
           // G > 16: item j of this net's list (weight tiles, then vectors) is reduced by
           // workgroup j % G. Its G partials are split over the waves -- ONE load batch per
@@ -1353,23 +1316,19 @@ __global__ __launch_bounds__(64 * NW) void ppo_rc_kernel(PPOArgs a, PPORcGeo g) 
         }
         __syncthreads();
 #pragma unroll
-        for (int it = 0; it < KI; ++it)
-          xg[it] = ld_sc1_x4_b(xr, red_off + (unsigned)(((ids[it] >= 0 ? ids[it] : 0) * 256 + lane * 4) * 4), xbit(xmask, it));
+        for (int it = 0; it < KI; ++it) xg[it] = ld_sc1_x4(red + (size_t)(ids[it] >= 0 ? ids[it] : 0) * 256 + lane * 4);
+        wait_vm_n<KI>(xg);  // results tied to the wait (inline-asm loads are invisible to the compiler)
       } else if (G == 2) {
-        exchange_sum<2, KI>(xr, slab_off, n_items, ids, lane, xg, xmask);
+        exchange_sum<2, KI>(slab, n_items, ids, lane, xg);
       } else if (G == 4) {
-        exchange_sum<4, KI>(xr, slab_off, n_items, ids, lane, xg, xmask);
+        exchange_sum<4, KI>(slab, n_items, ids, lane, xg);
       } else if (G == 8) {
-        exchange_sum<8, KI>(xr, slab_off, n_items, ids, lane, xg, xmask);
+        exchange_sum<8, KI>(slab, n_items, ids, lane, xg);
       } else {
 #pragma unroll
         for (int it = 0; it < KI; ++it) {
           if (ids[it] < 0) continue;
           f4 sacc = {0.f, 0.f, 0.f, 0.f};
-          if (!xbit(xmask, it)) {  // padding lane: never published (exactly 0)
-            xg[it] = sacc;
-            continue;
-          }
           const float* p = slab + (size_t)ids[it] * 256 + lane * 4;
           const size_t gs = (size_t)n_items * 256;
           for (int gi = 0; gi < G; gi += 4) {  // any count: tail lanes read group 0

@@ -456,11 +456,19 @@ class DeviceGeneratorCore:
         if getattr(self, "_ppo_log_host", None) is None:
             self._ppo_log_host = th.zeros(self._log_dev.numel(), pin_memory=True)
             self._ppo_std_host = th.zeros(self.A, pin_memory=True) if self.has_log_std else None
-        self._ppo_log_host.copy_(self._log_dev, non_blocking=True)
-        if self._ppo_std_host is not None:
-            self._ppo_std_host.copy_(self.gen_algo.policy.log_std.detach().reshape(-1), non_blocking=True)
-        self._ppo_log_event = th.cuda.Event()
-        self._ppo_log_event.record()
+        # on a stream of their own: the copies stay off the update -> next rollout chain, and off
+        # the side stream the discriminator updates (enqueued after this) run on concurrently
+        # with the update. The next round's update, which rewrites these buffers, is enqueued
+        # only after the host has waited for this event.
+        if getattr(self, "_log_stream", None) is None:
+            self._log_stream = th.cuda.Stream(device=self._dev)
+        self._log_stream.wait_stream(th.cuda.current_stream(self._dev))
+        with th.cuda.stream(self._log_stream):
+            self._ppo_log_host.copy_(self._log_dev, non_blocking=True)
+            if self._ppo_std_host is not None:
+                self._ppo_std_host.copy_(self.gen_algo.policy.log_std.detach().reshape(-1), non_blocking=True)
+            self._ppo_log_event = th.cuda.Event()
+            self._ppo_log_event.record()
 
     def _record_round_metrics(self) -> None:
         """The host PPO's per-round records (``rl/ppo.py`` ``train`` + ``rl/base.py``
@@ -673,6 +681,53 @@ class DeviceGeneratorCore:
                 ep_lengths.append(int(length))
                 count[e] += 1
         return ep_rewards, ep_lengths
+
+    def device_demonstrations(self, min_timesteps: int, deterministic: bool = False, seed: int = 0,
+                              n_envs: Optional[int] = None) -> types.Transitions:
+        """Rollouts of the current policy as flat demonstration transitions (``rollout.rollout`` +
+        ``flatten_trajectories`` of whole episodes, the way the reference's experts are rolled out
+        for the benchmarks) from a fresh env block on the GPU: launches of ``max_episode_steps``
+        until ``min_timesteps`` transitions of finished episodes are collected; episodes in
+        completion order (per launch: by env), each in time order; ``dones`` marks true
+        terminations only (a TimeLimit cut is not terminal)."""
+        n = int(n_envs or self.N)
+        T, bufs, args = self._eval_block(n, seed, deterministic, reward=False)
+        parts: Dict[str, List[np.ndarray]] = {k: [] for k in ("obs", "acts", "next_obs", "dones")}
+        carry = [dict(obs=[], acts=[], next_obs=[]) for _ in range(n)]  # episodes spanning launches
+        got, c = 0, 0
+        while got < min_timesteps:
+            dones = th.zeros(T, n, device=self._dev)
+            args.update(bufs, step0=c * T, dones=dones, ep_ret_out=th.zeros(T, n, device=self._dev))
+            self._C.engine_rollout(args)
+            c += 1
+            d = dones.cpu().numpy() > 0.5
+            obs, nxt = bufs["obs_buf"].cpu().numpy(), bufs["next_obs"].cpu().numpy()
+            acts = bufs["act_env"].cpu().numpy()
+            trunc = bufs["trunc"].cpu().numpy() > 0.5
+            for e in range(n):
+                cur = carry[e]
+                t0 = 0
+                for t in np.flatnonzero(d[:, e]).tolist() + [None]:
+                    t1 = T if t is None else t + 1
+                    cur["obs"].append(obs[t0:t1, e])
+                    cur["acts"].append(acts[t0:t1, e])
+                    cur["next_obs"].append(nxt[t0:t1, e])
+                    if t is not None:
+                        length = sum(len(x) for x in cur["acts"])
+                        for k in ("obs", "acts", "next_obs"):
+                            parts[k].append(np.concatenate(cur[k]))
+                            cur[k] = []
+                        dn = np.zeros(length, dtype=bool)
+                        dn[-1] = not trunc[t, e]
+                        parts["dones"].append(dn)
+                        got += length
+                    t0 = t1
+        acts = np.concatenate(parts["acts"])
+        if self.discrete:
+            acts = acts.reshape(-1).astype(np.int64)
+        return types.Transitions(obs=np.concatenate(parts["obs"]).astype(np.float32), acts=acts,
+                                 next_obs=np.concatenate(parts["next_obs"]).astype(np.float32),
+                                 dones=np.concatenate(parts["dones"]), infos=np.array([{}] * len(acts)))
 
     @profiling.traced("eval/device_stats")
     def device_rollout_stats(self, n_episodes: int, deterministic: bool = False, seed: Optional[int] = None,

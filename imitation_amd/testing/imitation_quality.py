@@ -179,3 +179,65 @@ def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_00
                 learner_return=final, normalized_score=normalized_score(final, rand, expert), curve=curve,
                 total_timesteps=done, train_s=round(t_train, 3), n_eval_episodes=n_eval, n_demo_episodes=len(demos),
                 returns_before=returns_before, returns_after=last["returns"])
+
+
+LOCOMOTION = {"halfcheetah": ("seals/HalfCheetah-v1", "gail_halfcheetah"),
+              "hopper": ("seals/Hopper-v1", "airl_hopper")}
+
+
+def run_locomotion(algo: str = "gail", env: str = "halfcheetah", expert_timesteps: int = 5_000_000,
+                   total_timesteps: int = 5_000_000, n_demo_timesteps: int = 50_000, seed: int = 0, n_eval: int = 50,
+                   eval_every: Optional[int] = None, device: Any = "cuda", verbose: bool = False) -> Dict[str, Any]:
+    """Expert mode of the benchmark configs on the synthetic MuJoCo-shaped envs (no MuJoCo /
+    HF experts here): (1) a PPO expert is trained on the env reward by the device engine with the
+    recipe's own generator config (``debug_use_ground_truth``), (2) its stochastic rollouts are
+    the demonstrations (as the reference rolls out its experts), (3) the recipe's GAIL
+    (``gail_halfcheetah``) or AIRL (``airl_hopper``) learner imitates them; normalised score as
+    in :func:`run`, R_expert = the expert's deterministic evaluation."""
+    from imitation_amd import models
+
+    env_id, _ = LOCOMOTION[env]
+    recipe = "gail_halfcheetah" if algo == "gail" else "airl_hopper"
+    th.manual_seed(seed)
+    np.random.seed(seed)
+    t0 = time.perf_counter()
+    ex = models.build(recipe, device=device, seed=seed + 100, env_id=env_id, debug_use_ground_truth=True)
+    ex.trainer.train(max(ex.trainer.gen_train_timesteps, expert_timesteps))
+    th.cuda.synchronize()
+    t_expert = time.perf_counter() - t0
+    r_exp, _ = ex.trainer.device_evaluate(n_eval, deterministic=True, seed=10_000 + seed)
+    expert = float(np.mean(r_exp))
+    demos = ex.trainer.device_demonstrations(n_demo_timesteps, deterministic=False, seed=20_000 + seed)
+    demo_return = None
+    del ex
+    rand = random_return(env_id, n_eval, seed)
+    b = models.build(recipe, device=device, seed=seed, env_id=env_id, demonstrations=demos)
+    tr = b.trainer
+    last: Dict[str, List[float]] = {}
+
+    def score() -> float:
+        r, _ = tr.device_evaluate(n_eval, deterministic=True, seed=10_000 + seed)
+        last["returns"] = list(r)
+        return float(np.mean(r))
+
+    r0 = score()
+    returns_before = last["returns"]
+    curve: List[Dict[str, float]] = [dict(timesteps=0, ret=r0, norm=normalized_score(r0, rand, expert))]
+    step = max(tr.gen_train_timesteps, int(eval_every or total_timesteps) // tr.gen_train_timesteps * tr.gen_train_timesteps)
+    done, t_train = 0, 0.0
+    while done < total_timesteps:
+        k = max(tr.gen_train_timesteps, min(step, total_timesteps - done) // tr.gen_train_timesteps * tr.gen_train_timesteps)
+        t1 = time.perf_counter()
+        tr.train(k)
+        th.cuda.synchronize()
+        t_train += time.perf_counter() - t1
+        done += k
+        r = score()
+        curve.append(dict(timesteps=done, ret=r, norm=normalized_score(r, rand, expert)))
+        if verbose:
+            print(f"{algo}/{env} seed {seed}: {done} steps: return {r:.1f} (normalised {curve[-1]['norm']:.3f})", flush=True)
+    return dict(algo=algo, env=env_id, mode="expert", seed=seed, expert_return=expert, expert_timesteps=expert_timesteps,
+                expert_train_s=round(t_expert, 3), random_return=rand, learner_return_before=r0,
+                learner_return=curve[-1]["ret"], normalized_score=curve[-1]["norm"], curve=curve, total_timesteps=done,
+                train_s=round(t_train, 3), n_eval_episodes=n_eval, n_demo_transitions=len(demos.acts),
+                demo_return=demo_return, returns_before=returns_before, returns_after=last["returns"])

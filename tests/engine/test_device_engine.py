@@ -866,8 +866,8 @@ def test_device_engine_nan_reward_weight_fails_fast(kind):
 
     tr = _setup(n_envs=8, n_steps=64, batch=64)[0] if kind == "gail" else _setup_airl(n_envs=8, n_steps=64, batch=256)[0]
     tr.train(tr.gen_train_timesteps)
-    with th.no_grad():
-        next(tr._reward_net.parameters()).view(-1)[0] = float("nan")
+    with th.no_grad():  # the output bias: a poisoned hidden weight is masked by ReLU (fmax(NaN, 0) = 0)
+        list(tr._reward_net.parameters())[-1].view(-1)[0] = float("nan")
     with pytest.raises(NonFiniteError, match="round"):
         tr.train(tr.gen_train_timesteps)
 

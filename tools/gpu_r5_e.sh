@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-timeout -k 10 600 $T tests/engine/test_device_engine.py > gpurun_out/r5_e_engine.log 2>&1 &&
+timeout -k 10 600 $T tests/engine/test_device_engine.py -k "${ENGINE_K:-nan_reward or rollout_stats}" > gpurun_out/r5_e_engine.log 2>&1 &&
 timeout -k 10 300 $T tests/engine/test_imitation_quality.py > gpurun_out/r5_e_quality.log 2>&1 &&
 timeout -k 10 500 $T tests/parallel/test_oneshot.py > gpurun_out/r5_e_oneshot.log 2>&1 &&
 for X in 1 0; do

@@ -15,6 +15,17 @@ def main():
     specs = sys.argv[1:] or ["gail:cartpole:200000", "airl:cartpole:200000", "gail:pendulum:500000", "airl:pendulum:500000"]
     for spec in specs:
         parts = spec.split(":")
+        if parts[1] in iq.LOCOMOTION:  # algo:env:expert_steps:imit_steps[:seed]
+            algo, env, esteps, steps = parts[0], parts[1], int(parts[2]), int(parts[3])
+            seed = int(parts[4]) if len(parts) > 4 else 0
+            res = iq.run_locomotion(algo, env, expert_timesteps=esteps, total_timesteps=steps, seed=seed,
+                                    eval_every=max(steps // 10, 1), verbose=True)
+            line = json.dumps(res)
+            print(line, flush=True)
+            if os.environ.get("OUT"):
+                with open(os.environ["OUT"], "a") as f:
+                    f.write(line + "\n")
+            continue
         algo, env, steps = parts[0], parts[1], int(parts[2])
         seed = int(parts[3]) if len(parts) > 3 else 0
         cap = int(parts[4]) if len(parts) > 4 else 512
