@@ -225,7 +225,12 @@ class AirlDiscPlan {
   // same data as update() x n (bitwise), but the policy norm (q, merged as a side effect of the
   // log pi pass, as the reference's training-mode evaluate_actions does) is final after the
   // stages: the next rollout's step chain can run concurrently with the applies.
-  void stage(int slot, torch::Tensor e_idx, torch::Tensor g_idx, bool merge_b, bool merge_p, bool merge_q) {
+  //
+  // defer_q: the policy-norm merges are left to q_merge(n) (one launch after PPO for the round's
+  // n staged updates); the stages then leave the policy norm untouched and can run concurrently
+  // with the PPO update that reads it.
+  void stage(int slot, torch::Tensor e_idx, torch::Tensor g_idx, bool merge_b, bool merge_p, bool merge_q,
+             bool defer_q) {
     TORCH_CHECK(slot >= 0 && slot < n_slots_, "stage: slot ", slot, " outside the reserved ", n_slots_);
     for (int k = 0; k < n_mb_; ++k) {
       ia::AirlDiscArgs a = slot_args(slot, k);
@@ -237,8 +242,17 @@ class AirlDiscPlan {
       a.merge_b = merge_b;
       a.merge_p = merge_p;
       a.merge_q = merge_q;
+      if (!(defer_q && merge_q && a.q_mean)) a.q_defer = nullptr;
       IA_HIP_CHECK_A(ia::airl_norm(a, 0, 0, ia_stream()));
     }
+  }
+  // the deferred policy-norm merges of staged updates [0, n), in update order
+  void q_merge(int n) {
+    TORCH_CHECK(n >= 0 && n <= n_slots_, "q_merge: ", n, " updates, ", n_slots_, " staged");
+    TORCH_CHECK(a_.q_mean != nullptr && a_.q_count != nullptr, "q_merge: no policy norm");
+    if (n == 0) return;
+    ia::AirlDiscArgs a = slot_args(0, 0);
+    IA_HIP_CHECK_A(ia::airl_q_merge(a, n * n_mb_, (long long)slot_floats(), 2 * mb_, ia_stream()));
   }
   // Split update under data parallelism: the staging of update `slot`, minibatch k, in the two
   // halves around the normaliser all-reduce -- mode 1: gather + local moments into `sums` (the
@@ -256,6 +270,7 @@ class AirlDiscPlan {
     a.merge_b = merge_b;
     a.merge_p = merge_p;
     a.merge_q = merge_q;
+    a.q_defer = nullptr;
     if (mode == 1) {
       check_idx(e_idx);
       check_idx(g_idx);
@@ -305,7 +320,7 @@ class AirlDiscPlan {
   // normaliser rows (nrm) for stage / apply; grown on demand
   int64_t slot_floats() const {
     const int64_t n = 2 * mb_;
-    const int64_t f = n * (a_.din_b + 2 * a_.D + a_.aw_pi + 1) + 4 * 256;
+    const int64_t f = n * (a_.din_b + 2 * a_.D + a_.aw_pi + 1) + 5 * 256;  // nrm rows + q_defer
     return (f + 63) & ~int64_t(63);
   }
 
@@ -319,6 +334,7 @@ class AirlDiscPlan {
     a.Act = a.S2 + n * a_.D;
     a.Done = a.Act + n * a_.aw_pi;
     a.nrm = a.Done + n;
+    a.q_defer = a.nrm + 4 * 256;
     return a;
   }
   std::vector<torch::Tensor> held_;
@@ -356,7 +372,8 @@ void register_airl(py::module& m) {
            py::arg("mode"), py::arg("n_total"), py::arg("merge_b"), py::arg("merge_p"), py::arg("merge_q"))
       .def("apply_grads", &AirlDiscPlan::apply_grads, py::arg("slot"), py::arg("stats_out") = py::none())
       .def("stage", &AirlDiscPlan::stage, py::arg("slot"), py::arg("e_idx"), py::arg("g_idx"), py::arg("merge_b"),
-           py::arg("merge_p"), py::arg("merge_q"))
+           py::arg("merge_p"), py::arg("merge_q"), py::arg("defer_q") = false)
+      .def("q_merge", &AirlDiscPlan::q_merge, py::arg("n"))
       .def("apply", &AirlDiscPlan::apply, py::arg("slot"), py::arg("step_size"), py::arg("bc2_sqrt"),
            py::arg("stats_out") = py::none())
       .def("update", &AirlDiscPlan::update, py::arg("e_idx"), py::arg("g_idx"), py::arg("step_size"), py::arg("bc2_sqrt"),

@@ -194,17 +194,41 @@ __global__ __launch_bounds__(128 * kNormPhases) void airl_norm_kernel(AirlDiscAr
       put_nrm(a.nrm, 2, c, a.p_mean, a.p_var, a.eps_p);
       if (a.merge_p && a.p_mean) chan_merge(a.p_mean, a.p_var, pc + n, c, bm[nb + D + c], bv[nb + D + c], n);
       put_nrm(a.nrm, 3, c, a.p_mean, a.p_var, a.eps_p);
-      // policy features norm: moments of s
-      if (a.merge_q && a.q_mean) chan_merge(a.q_mean, a.q_var, qc, c, bm[nb + D + c], bv[nb + D + c], n);
-      put_nrm(a.nrm, 0, c, a.q_mean, a.q_var, a.eps_q);
+      // policy features norm: moments of s (deferred: kept for airl_q_merge, which writes row 0)
+      const bool defer = a.merge_q && a.q_mean && a.q_defer;
+      if (defer) {
+        a.q_defer[c] = bm[nb + D + c];
+        a.q_defer[128 + c] = bv[nb + D + c];
+      } else {
+        if (a.merge_q && a.q_mean) chan_merge(a.q_mean, a.q_var, qc, c, bm[nb + D + c], bv[nb + D + c], n);
+        put_nrm(a.nrm, 0, c, a.q_mean, a.q_var, a.eps_q);
+      }
     }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     if (a.merge_b && a.b_count) *a.b_count += n;
     if (a.merge_p && a.p_count) *a.p_count += 2 * n;
-    if (a.merge_q && a.q_count) *a.q_count += n;
+    if (a.merge_q && a.q_count && !a.q_defer) *a.q_count += n;
   }
+}
+
+// The policy-norm merges airl_norm deferred, in staging order: the same chan_merge sequence on
+// the same moments as merging in airl_norm (bitwise), so the staging itself (gathers, base and
+// potential merges) can run while PPO still uses the policy norm. One thread per column.
+__global__ __launch_bounds__(128) void airl_q_merge_kernel(AirlDiscArgs a, int count, long long stride, int n) {
+  const int c = threadIdx.x;
+  const int qc = *a.q_count;
+  __syncthreads();
+  if (c < a.D) {
+    for (int j = 0; j < count; ++j) {
+      float* nrm = a.nrm + (size_t)j * stride;
+      const float* dq = a.q_defer + (size_t)j * stride;
+      chan_merge(a.q_mean, a.q_var, qc + j * n, c, dq[c], dq[128 + c], n);
+      put_nrm(nrm, 0, c, a.q_mean, a.q_var, a.eps_q);
+    }
+  }
+  if (c == 0) *a.q_count = qc + count * n;
 }
 
 __global__ __launch_bounds__(64 * kNW) void airl_fwd_bwd_kernel(AirlDiscArgs a, AirlPlan p, int k) {
@@ -440,6 +464,12 @@ hipError_t airl_gather(const AirlDiscArgs& a, int k, hipStream_t s) {
 
 hipError_t airl_norm(const AirlDiscArgs& a, int mode, int n_total, hipStream_t s) {
   hipLaunchKernelGGL(airl_norm_kernel, dim3(1), dim3(128 * kNormPhases), 0, s, a, mode, n_total);
+  return hipGetLastError();
+}
+
+hipError_t airl_q_merge(const AirlDiscArgs& a, int count, long long stride, int n, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(airl_q_merge_kernel, dim3(1), dim3(128), 0, s, a, count, stride, n);
   return hipGetLastError();
 }
 

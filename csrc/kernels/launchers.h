@@ -120,6 +120,7 @@ struct AirlDiscArgs {
   float eps_b, eps_p, eps_q;
   int merge_b, merge_p, merge_q;  // train mode (update stats)
   float* nrm;  // [4][256]: (mean[128], rstd[128]) for policy, base, potential(s'), potential(s)
+  float* q_defer;  // merge_q deferred: the s moments (mean[128], var[128]) for airl_q_merge, else null
   AirlNet pol, base, pot;
   const float* log_std;  // [A] (Gaussian) or null
   float gamma;           // shaping discount
@@ -141,6 +142,9 @@ int airl_fwd_blocks(int mb);
 bool airl_plan(const AirlDiscArgs& a, AirlPlan& p);
 hipError_t airl_gather(const AirlDiscArgs& a, int k, hipStream_t s);
 hipError_t airl_norm(const AirlDiscArgs& a, int mode, int n_total, hipStream_t s);
+// policy-norm merges deferred by airl_norm (q_defer) for `count` staged minibatches whose nrm /
+// q_defer rows are `stride` floats apart, in staging order; n rows per minibatch
+hipError_t airl_q_merge(const AirlDiscArgs& a, int count, long long stride, int n, hipStream_t s);
 hipError_t airl_fwd_bwd(const AirlDiscArgs& a, const AirlPlan& p, int k, hipStream_t s);
 
 // ---- pref_rm.hip: fused preference reward-model minibatch (gather, fwd, bwd; Adam = disc_adam)

@@ -271,11 +271,15 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
             self._disc_plan.reserve(max(1, self.n_disc_updates_per_round))
 
     @profiling.traced("disc/stage")
-    def _stage_disc_updates(self, n: int) -> List[Tuple[float, float]]:
+    def _stage_disc_updates(self, n: int, defer_q: bool = False) -> List[Tuple[float, float]]:
         """The gathers and RunningNorm merges (policy, base, potential) of the round's ``n``
         updates, in update order (``AirlDiscPlan.stage``): everything of an update that the
         norms see, none of it dependent on the discriminator weights. Returns each update's
-        Adam (step_size, sqrt(1 - beta2^t))."""
+        Adam (step_size, sqrt(1 - beta2^t)).
+
+        ``defer_q`` (single rank): leave the policy-norm merges to ``_merge_deferred_q`` (one
+        launch after PPO), so the staging can run on the side stream during the PPO update;
+        ``self._q_deferred`` says whether there is anything to merge."""
         if self._gen_dev.size() == 0:
             raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
         # (grows only here: the previous round's applies were waited for on the host)
@@ -291,11 +295,17 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         merge_q = self.pol_norm is not None and self.pol_norm.training
         scal = []
         world = pdist.world_size()
+        defer_q = defer_q and merge_q and (world == 1 or not pdist.norm_sync_active())
+        self._q_deferred = defer_q
+        cur = th.cuda.current_stream(self._dev)
         for i in range(n):
             e_idx = self._endless_expert_iterator.next_indices()
+            # the epoch permutation may come from another stream's pool: keep its block alive
+            # for this stream's reads
+            e_idx.record_stream(cur)
             g_idx = th.randint(0, self._gen_dev.size(), (B,), device=self._dev)
             if world == 1 or not pdist.norm_sync_active():
-                self._disc_plan.stage(i, e_idx, g_idx, merge_b, merge_p, merge_q)
+                self._disc_plan.stage(i, e_idx, g_idx, merge_b, merge_p, merge_q, defer_q)
             else:  # the DP update's order: gather, moments, all-reduce, merges -- per minibatch
                 mb = self.demo_minibatch_size
                 for k in range(B // mb):
@@ -305,6 +315,12 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
             t = t0 + i + 1.0
             scal.append((float(g["lr"]) / (1.0 - beta1**t), (1.0 - beta2**t) ** 0.5))
         return scal
+
+    def _merge_deferred_q(self, n: int) -> None:
+        """The policy-norm merges ``_stage_disc_updates(n, defer_q=True)`` left (update order)."""
+        if getattr(self, "_q_deferred", False):
+            self._disc_plan.q_merge(n)
+            self._q_deferred = False
 
     @profiling.traced("disc/apply")
     def _apply_disc_updates(self, scal: List[Tuple[float, float]], steps: List[int]) -> None:

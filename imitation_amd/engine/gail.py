@@ -1443,6 +1443,13 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         disc_done.synchronize()
         return steps, nxt
 
+    def _stage_during_ppo(self) -> bool:
+        """Split-round staging on the side stream, concurrent with PPO (single rank; the DP
+        staging's normaliser all-reduces stay on the main stream). IMITATION_AMD_AIRL_EARLY_STAGE=0:
+        stage behind PPO on the main stream."""
+        return (pdist.world_size() == 1 and getattr(self, "_host_staged", False)
+                and os.environ.get("IMITATION_AMD_AIRL_EARLY_STAGE", "1") != "0")
+
     def _split_round(self, n: int, ppo_done: th.cuda.Event, launch_next: bool,
                      steps: List[int]) -> Tuple[List[int], Optional[th.cuda.Event]]:
         """Rest of an AIRL split round after PPO (see _overlapped_round): stage the updates on
@@ -1450,9 +1457,24 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         then the rollout's reward pass behind the applies."""
         main = th.cuda.current_stream(self._dev)
         side = self._side_stream
-        self._store_generator_samples()
-        with networks.training(self.reward_train):
-            scal = self._stage_disc_updates(n)
+        if self._stage_during_ppo():
+            # replay store, gathers and base / potential merges on the side stream while PPO
+            # runs (none of it touches the policy norm or the policy); then the policy-norm
+            # merges, one launch, behind PPO on the main stream. The side stream is already
+            # ordered after the rollout (_stage_rollout_to_host).
+            with th.cuda.stream(side):
+                self._store_generator_samples()
+                with networks.training(self.reward_train):
+                    scal = self._stage_disc_updates(n, defer_q=True)
+                side_staged = th.cuda.Event()
+                side_staged.record(side)
+            main.wait_event(side_staged)
+            self._merge_deferred_q(n)
+            self._early_staged_rounds = getattr(self, "_early_staged_rounds", 0) + 1
+        else:
+            self._store_generator_samples()
+            with networks.training(self.reward_train):
+                scal = self._stage_disc_updates(n)
         staged = th.cuda.Event()
         staged.record(main)
         # the next step chain is enqueued before the applies (host order only: it depends on

@@ -699,11 +699,13 @@ def test_airl_pipelined_rounds_are_bitwise_the_serial_order(monkeypatch):
     rollout enqueued before the host reads anything) give bit-identical parameters, Adam moments
     and normalisers to the serial loop (IMITATION_AMD_DISC_OVERLAP=0) -- also as split rounds
     (the updates' gathers + norm merges staged on the main stream, their fwd/bwd + Adam applied
-    on the side stream concurrently with the next rollout's step chain)."""
+    on the side stream concurrently with the next rollout's step chain) -- also with the staging
+    on the side stream during PPO and the policy-norm merges deferred to one launch after it."""
     runs = []
-    for mode, split in (("0", "0"), ("1", "0"), ("1", "1")):
+    for mode, split, early in (("0", "0", "0"), ("1", "0", "0"), ("1", "1", "0"), ("1", "1", "1")):
         monkeypatch.setenv("IMITATION_AMD_DISC_OVERLAP", mode)
         monkeypatch.setenv("IMITATION_AMD_AIRL_SPLIT", split)
+        monkeypatch.setenv("IMITATION_AMD_AIRL_EARLY_STAGE", early)
         tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=3)
         assert tr._fused_disc, tr._fused_disc_why
         assert tr._overlap_disc == (mode == "1")
@@ -716,6 +718,7 @@ def test_airl_pipelined_rounds_are_bitwise_the_serial_order(monkeypatch):
         vals += [n.running_mean.cpu().clone() for n in _airl_state(tr, rn)]
         runs.append(vals)
         assert tr._disc_step == 9
+        assert (getattr(tr, "_early_staged_rounds", 0) > 0) == (early == "1" and split == "1")
     for other in runs[1:]:
         bad = [i for i, (a, b) in enumerate(zip(runs[0], other)) if not th.equal(a, b)]
         assert not bad, bad
