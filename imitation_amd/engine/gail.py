@@ -211,6 +211,29 @@ class DeviceGeneratorCore:
     Subclasses set ``gen_algo``, ``_reward_net`` and ``debug_use_ground_truth`` and call
     :meth:`_init_generator`."""
 
+    # ------------------------------------------------------------------ stream ordering
+    def _dev_event(self, stream: Optional[th.cuda.Stream] = None):
+        """An event recorded on ``stream`` (default: the current one) for GPU -> GPU ordering
+        and host waits on completion: device-scope release (``_C.DeviceEvent``,
+        csrc/bind/events.cpp), so the markers between the round's critical kernels do not write
+        back the L2s. Pinned D2H copies the host reads keep torch (system-scope) events.
+        IMITATION_AMD_DEVICE_EVENTS=0: torch events everywhere."""
+        if os.environ.get("IMITATION_AMD_DEVICE_EVENTS", "1") != "0" and hasattr(self._C, "DeviceEvent"):
+            ev = self._C.DeviceEvent(True)
+            ev.record(stream.cuda_stream if stream is not None else None)
+            return ev
+        ev = th.cuda.Event()
+        ev.record(stream)
+        return ev
+
+    @staticmethod
+    def _wait_ev(stream: th.cuda.Stream, ev) -> None:
+        """``stream`` waits for ``ev`` (a torch event or a ``_dev_event``)."""
+        if isinstance(ev, th.cuda.Event):
+            stream.wait_event(ev)
+        else:
+            ev.wait(stream.cuda_stream)
+
     def _init_generator(self, venv) -> None:
         self._native = _unwrap_native(venv)
         self._C = ops.native()
@@ -442,11 +465,14 @@ class DeviceGeneratorCore:
                 self._C.engine_ppo_update(d)
         if self.pol_norm is not None and not direct:
             self.pol_norm.count.copy_(self.norm_count.to(self.pol_norm.count.dtype).reshape(()))
-        # reads the error word of an EARLIER update (non-blocking); train() ends blocking
-        self._ppo_err.check("PPO update")
+        # one marker behind the update: the round's host wait and the log copies' stream order
+        self._ppo_done = self._dev_event()
         algo._n_updates += algo.n_epochs
         self._last_ppo_info = (rows, algo.n_epochs * (rows // algo.batch_size))
         self._stage_ppo_logs()
+        # reads the error word of an EARLIER update (non-blocking; its copy on the log stream,
+        # off the update -> next chain path); train() ends blocking
+        self._ppo_err.check("PPO update", stream=self._log_stream)
 
     def _stage_ppo_logs(self) -> None:
         """Async D2H copy (stream order: right behind the update) of the update's statistics, the
@@ -462,7 +488,11 @@ class DeviceGeneratorCore:
         # only after the host has waited for this event.
         if getattr(self, "_log_stream", None) is None:
             self._log_stream = th.cuda.Stream(device=self._dev)
-        self._log_stream.wait_stream(th.cuda.current_stream(self._dev))
+        done = getattr(self, "_ppo_done", None)
+        if done is not None:
+            self._wait_ev(self._log_stream, done)
+        else:
+            self._log_stream.wait_stream(th.cuda.current_stream(self._dev))
         with th.cuda.stream(self._log_stream):
             self._ppo_log_host.copy_(self._log_dev, non_blocking=True)
             if self._ppo_std_host is not None:
@@ -808,7 +838,7 @@ class DeviceGeneratorCore:
         # waits for this event before the next rollout can overwrite the buffers)
         side = getattr(self, "_side_stream", None)
         if side is not None:
-            side.wait_stream(th.cuda.current_stream(self._dev))
+            self._wait_ev(side, self._dev_event())
         with th.cuda.stream(side) if side is not None else contextlib.nullcontext():
             self._host_stage[0].copy_(self.buf["dones"], non_blocking=True)
             self._host_stage[1].copy_(self.buf["ep_ret_out"], non_blocking=True)
@@ -1414,13 +1444,12 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 ready = self._launch_rollout()
             algo.num_timesteps += self.T * self.N
             self._ppo_update()
-            ppo_done = th.cuda.Event()
-            ppo_done.record(main)
+            ppo_done = self._ppo_done
             ready.synchronize()
             if split:
                 return self._split_round(n, ppo_done, launch_next, steps)
             if serial:
-                side.wait_stream(main)
+                self._wait_ev(side, ppo_done)
             else:
                 side.wait_event(ready)
             with th.cuda.stream(side):
@@ -1429,10 +1458,11 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                     for i in range(n):
                         self._fused_disc_update(i, defer_pol=defer)
                         steps.append(self._disc_step)
+                disc_dev = self._dev_event(side)
                 self._disc_stats_host[:n].copy_(self._disc_stats[:n], non_blocking=True)
                 disc_done = th.cuda.Event()
                 disc_done.record(side)
-            main.wait_event(disc_done)
+            self._wait_ev(main, disc_dev)
             if defer:
                 self._disc_plan.pol_norm_merge(n * self._disc_plan.n_minibatches)
             self._global_step += 1
@@ -1466,38 +1496,37 @@ class DeviceEngineMixin(DeviceGeneratorCore):
                 self._store_generator_samples()
                 with networks.training(self.reward_train):
                     scal = self._stage_disc_updates(n, defer_q=True)
-                side_staged = th.cuda.Event()
-                side_staged.record(side)
-            main.wait_event(side_staged)
+                side_staged = self._dev_event(side)
+            self._wait_ev(main, side_staged)
             self._merge_deferred_q(n)
             self._early_staged_rounds = getattr(self, "_early_staged_rounds", 0) + 1
         else:
             self._store_generator_samples()
             with networks.training(self.reward_train):
                 scal = self._stage_disc_updates(n)
-        staged = th.cuda.Event()
-        staged.record(main)
+        staged = self._dev_event(main)
         # the next step chain is enqueued before the applies (host order only: it depends on
         # the staging, not on the applies), so a slow host never delays its start
         if launch_next:
             self._launch_chain()
-        side.wait_event(staged)
+        self._wait_ev(side, staged)
         with th.cuda.stream(side):
             self._apply_disc_updates(scal, steps)
+            disc_dev = self._dev_event(side)
             self._disc_stats_host[:n].copy_(self._disc_stats[:n], non_blocking=True)
             disc_done = th.cuda.Event()
             disc_done.record(side)
         self._global_step += 1
         nxt = None
         if launch_next:
-            main.wait_event(disc_done)
+            self._wait_ev(main, disc_dev)
             reward = not self.debug_use_ground_truth
             self._launch_post(reward)
             if reward:
                 self._post_rollout_rewards()
             nxt = self._stage_rollout_to_host()
         else:
-            main.wait_event(disc_done)
+            self._wait_ev(main, disc_dev)
         ppo_done.synchronize()
         self._log_gen()
         disc_done.synchronize()

@@ -13,6 +13,7 @@ training call). Reference behaviour mirrored: broken invariants raise
 
 from __future__ import annotations
 
+import contextlib
 from typing import Optional
 
 import torch as th
@@ -31,7 +32,9 @@ class DeviceErrorFlag:
     def clear(self) -> None:
         self.word.zero_()
 
-    def check(self, where: str = "", blocking: bool = False) -> None:
+    def check(self, where: str = "", blocking: bool = False, stream: Optional[th.cuda.Stream] = None) -> None:
+        """``stream``: enqueue the copy there (already ordered after the kernels that set the
+        word) instead of on the current stream."""
         if blocking:
             err = int(self.word.item())
         else:
@@ -41,7 +44,8 @@ class DeviceErrorFlag:
             if self._host is None:
                 self._host = th.zeros(1, dtype=th.int32, pin_memory=True)
             if self._ev is None or self._ev.query():  # one copy in flight at a time
-                with th.cuda.device(self.device):
+                with th.cuda.device(self.device), (th.cuda.stream(stream) if stream is not None
+                                                   else contextlib.nullcontext()):
                     self._host.copy_(self.word, non_blocking=True)
                     self._ev = th.cuda.Event()
                     self._ev.record()

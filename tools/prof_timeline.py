@@ -12,7 +12,9 @@ def main():
     c = sqlite3.connect(db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
     name_col = "name" if "name" in cols else "kernel_name"
-    rows = sorted(c.execute(f"select {name_col}, start, end from kernels").fetchall(), key=lambda r: r[1])
+    qcol = "queue_id" if "queue_id" in cols else "0"
+    rows = sorted(c.execute(f"select {name_col}, start, end, {qcol} from kernels").fetchall(), key=lambda r: r[1])
+    qids = {q: i for i, q in enumerate(sorted({r[3] for r in rows}))}
     idx = [i for i, r in enumerate(rows) if marker in r[0]]
     if len(idx) <= nth:
         print("not enough marker dispatches", len(idx))
@@ -21,12 +23,12 @@ def main():
     t0 = rows[a][1]
     prev_end = rows[a - 1][2] if a > 0 else t0
     print(f"round between dispatch {a} and {b}: {(rows[b][1] - t0) / 1e3:.1f} us")
-    print("| start us | dur us | gap us | kernel |\n|---|---|---|---|")
+    print("| start us | dur us | gap us | queue | kernel |\n|---|---|---|---|---|")
     busy_end = prev_end
-    for n, s, e in rows[a:b + 1]:
+    for n, s, e, q in rows[a:b + 1]:
         gap = (s - busy_end) / 1e3
         short = n if len(n) < 80 else n[:77] + "..."
-        print(f"| {(s - t0) / 1e3:.1f} | {(e - s) / 1e3:.1f} | {gap:.1f} | `{short}` |")
+        print(f"| {(s - t0) / 1e3:.1f} | {(e - s) / 1e3:.1f} | {gap:.1f} | q{qids[q]} | `{short}` |")
         busy_end = max(busy_end, e)
 
 
