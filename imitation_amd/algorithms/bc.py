@@ -147,12 +147,31 @@ def enumerate_batches(batch_it: Iterable[types.TransitionMapping]) -> Iterable[T
         yield (num_batches, batch_size, num_samples_so_far), batch
 
 
+class _Done:
+    def __init__(self, value):
+        self.value = value
+
+    def result(self):
+        return self.value
+
+
 @dataclasses.dataclass(frozen=True)
 class RolloutStatsComputer:
     """Computes statistics about rollouts (for logging during BC)."""
 
     venv: Optional[Any]
     n_episodes: int
+
+    def start(self, policy, rng: np.random.Generator):
+        """The statistics of ``policy`` as it is now, possibly still being computed when this
+        returns (a device venv runs them on a worker thread and a side stream while training
+        goes on): an object whose ``result()`` gives them. IMITATION_AMD_BC_ASYNC_STATS=0: in line."""
+        import os
+
+        if (self.venv is not None and self.n_episodes > 0 and hasattr(self.venv, "start_rollout_stats")
+                and os.environ.get("IMITATION_AMD_BC_ASYNC_STATS", "1") != "0"):
+            return self.venv.start_rollout_stats(policy, self.n_episodes)
+        return _Done(self(policy, rng))
 
     def __call__(self, policy, rng: np.random.Generator) -> Mapping[str, float]:
         if self.venv is not None and self.n_episodes > 0 and hasattr(self.venv, "device_rollout_stats"):
@@ -309,6 +328,11 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
                 or self.minibatch_size != self.batch_size or os.environ.get("IMITATION_AMD_BC_EPOCH_GRAPH", "1") == "0"):
             return None
         r = getattr(self, "_epoch_run", None)
+        if r is not None and r.graphed is graphed and r.loader is not loader and getattr(loader, "agg", None) is r.agg:
+            # a new loader over the same aggregate (DAgger: one per round): the captured step
+            # graphs read the aggregate, the runner's perm / cursor buffers and the policy, not
+            # the loader -- keep them (a recapture per round cost ~15 ms on DAgger-Pong)
+            r.loader = loader
         if r is None or r.loader is not loader or r.graphed is not graphed:
             r = _DeviceEpochRunner(self, loader, graphed)
             if not r.ok:
@@ -550,6 +574,10 @@ class _DeviceEpochRunner:
             self.cursor.zero_()
             steps = nb if n_batches is None else min(nb, n_batches - batch_num)
             done = 0
+            # a logged batch's rollout statistics run beside the following minibatches (worker
+            # thread + side stream, on a snapshot of the policy as of that batch); its log_batch
+            # is written when they are in -- before the next logged batch and the epoch's end
+            pending = None
             while done < steps:
                 nxt = -(-(batch_num + done) // log_interval) * log_interval  # next logged batch
                 j = nxt - batch_num  # its index in this epoch
@@ -557,9 +585,19 @@ class _DeviceEpochRunner:
                     self._run(steps - done)
                     break
                 self._run(j + 1 - done)
+                if pending is not None:
+                    pending[0].result()
+                    pending[1]()
                 m = BCTrainingMetrics(**bc_cnn.metrics_fields(self.all[j]))
-                t._bc_logger.log_batch(nxt, B, (nxt + 1) * B, m, compute_rollout_stats(t.policy, t.rng))
+                if self.graphs is None and done < steps:
+                    # capture the step graphs now: no capture may run while the statistics'
+                    # worker thread is stepping the envs
+                    self._capture()
+                fut = compute_rollout_stats.start(t.policy, t.rng)
+                pending = (fut, (lambda f=fut, nb_=nxt, mm=m: t._bc_logger.log_batch(nb_, B, (nb_ + 1) * B, mm, f.result())))
                 done = j + 1
+            if pending is not None:
+                pending[1]()
             batch_num += steps
             # the reference's batch iterator reaches an epoch's end callback only when it is
             # asked for a batch after the epoch's last one

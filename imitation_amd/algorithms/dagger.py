@@ -27,6 +27,7 @@ from __future__ import annotations
 import abc
 import json
 import logging
+import os
 import pathlib
 import uuid
 from typing import Any, Callable, Dict, List, Mapping, Optional, Sequence, Tuple, Union
@@ -457,6 +458,10 @@ class SimpleDAggerTrainer(DAggerTrainer):
             if ok:
                 self._device_collector = dagger_engine.DeviceDAggerCollector(self.venv, self.expert_policy,
                                                                              self.bc_trainer.policy, self.rng)
+                # the round's frames land on the host in the writer thread (before its files are
+                # written) or at the end of train(), not on the collect -> BC path
+                self._device_collector.async_frames = os.environ.get("IMITATION_AMD_DAGGER_ASYNC_FRAMES", "1") != "0"
+                self._landings: List[Any] = []
                 self._device_agg = dagger_engine.DeviceDemoAggregate(self.bc_trainer.policy.device)
                 self._device_counts: Dict[int, int] = {}
                 # demo files are persisted in the background (flushed by save_trainer /
@@ -501,6 +506,9 @@ class SimpleDAggerTrainer(DAggerTrainer):
         if self._device_collector is not None:
             col = self._device_collector
             trajs = col.collect(beta, min_timesteps=min_timesteps, min_episodes=min_episodes)
+            if col.last_landing is not None:
+                self._landings.append(col.last_landing)
+                self._writer.submit(col.last_landing.land)  # (the writer is FIFO: before the files)
             for k, traj in enumerate(trajs):  # reference-format demo files, off the critical path
                 self._writer.submit(self._store.write, traj, k, self.round_num, np.random.default_rng(self.rng.integers(2**63)))
             self._device_append(trajs, self.round_num, col.last_obs, col.last_acts)
@@ -529,10 +537,18 @@ class SimpleDAggerTrainer(DAggerTrainer):
         seed = int(self.rng.integers(0, 2**31 - 1)) + 7919 * pdist.rank()
         self.bc_trainer.set_demonstrations(dagger_engine.DeviceTransitionsLoader(self._device_agg, self.batch_size, seed))
 
+    def land_frames(self) -> None:
+        """Block until the host observation arrays of every collected trajectory are filled
+        (device collector: the frames' D2H copies run asynchronously)."""
+        pending = getattr(self, "_landings", None)
+        while pending:
+            pending.pop(0).land()
+
     def flush_demos(self) -> None:
         """Block until every collected demonstration is on disk (device collector only)."""
         if self._writer is not None:
             self._writer.flush()
+        self.land_frames()
 
     def save_trainer(self) -> Tuple[pathlib.Path, pathlib.Path]:
         if self._writer is not None:
@@ -563,5 +579,6 @@ class SimpleDAggerTrainer(DAggerTrainer):
             lg.record("dagger/round_timestep_count", n_steps)
             self.extend_and_update(bc_train_kwargs)
             rounds += 1
+        self.land_frames()  # the trajectories handed out are complete when train() returns
         self.last_train_timesteps = collected  # all ranks
         self.last_train_timesteps_local = local

@@ -275,6 +275,35 @@ class DeviceTransitionsLoader:
             yield {"obs": o, "acts": a}
 
 
+class FrameLanding:
+    """A round's frames on their way to the host: a D2H copy into pinned staging on a side
+    stream (off the collector -> BC path), and :meth:`land` -- run by the demo writer thread
+    before it writes the round's files, and by the trainer before ``train`` returns -- waits for
+    it and fills the pageable array the round's trajectories view. Until then those host
+    observation arrays are not filled in."""
+
+    def __init__(self, dst: np.ndarray, src: th.Tensor, stream: th.cuda.Stream):
+        self.dst = dst
+        self._pinned = th.empty(tuple(src.shape), dtype=src.dtype, pin_memory=True)
+        stream.wait_stream(th.cuda.current_stream(src.device))
+        with th.cuda.stream(stream):
+            self._pinned.copy_(src, non_blocking=True)
+            self._ev = th.cuda.Event()
+            self._ev.record()
+        src.record_stream(stream)  # (allocated on the main stream; read here)
+        self._lock = threading.Lock()
+        self._landed = False
+
+    def land(self) -> None:
+        with self._lock:
+            if self._landed:
+                return
+            self._ev.synchronize()
+            np.copyto(self.dst, self._pinned.numpy())
+            self._pinned = None
+            self._landed = True
+
+
 class AsyncDemoWriter:
     """Background thread that writes demo files (``fn(trajectory, index)``) in order; the
     collector hands trajectories over and goes on. ``flush()`` waits for the queue."""
@@ -325,6 +354,41 @@ class DeviceStatsVenv:
         if policy is not self.collector.learner:
             raise ValueError("device rollout stats evaluate the collector's learner policy")
         return self.collector.rollout_stats(n_episodes)
+
+    def start_rollout_stats(self, policy, n_episodes: int) -> "StatsFuture":
+        """:meth:`device_rollout_stats` of the learner as it is NOW, run on a side stream by a
+        worker thread while the caller goes on training it (``StatsFuture.result()``)."""
+        if policy is not self.collector.learner:
+            raise ValueError("device rollout stats evaluate the collector's learner policy")
+        return self.collector.start_rollout_stats(n_episodes)
+
+
+class StatsFuture:
+    """A learner rollout-statistics run in flight (:meth:`DeviceDAggerCollector.start_rollout_stats`)."""
+
+    def __init__(self, fn: Callable[[], Mapping[str, float]], finish: Callable[[], None]):
+        self._out: Optional[Mapping[str, float]] = None
+        self._err: Optional[BaseException] = None
+        self._finish = finish
+        self._t = threading.Thread(target=self._run, args=(fn,), daemon=True)
+        self._t.start()
+        self._resolved = False
+
+    def _run(self, fn) -> None:
+        try:
+            self._out = fn()
+        except BaseException as e:  # re-raised by result()
+            self._err = e
+
+    def result(self) -> Mapping[str, float]:
+        if not self._resolved:
+            self._t.join()
+            self._resolved = True
+            if self._err is None:
+                self._finish()
+        if self._err is not None:
+            raise self._err
+        return self._out
 
 
 class DeviceDAggerCollector:
@@ -390,6 +454,11 @@ class DeviceDAggerCollector:
         self.last_obs: Optional[th.Tensor] = None
         self.last_acts: Optional[th.Tensor] = None
         self.steps_collected = 0
+        # frames to the host asynchronously (FrameLanding; the owner must land() them) -- set by
+        # owners that do: SimpleDAggerTrainer; IMITATION_AMD_DAGGER_ASYNC_FRAMES=0 disables
+        self.async_frames = False
+        self.last_landing: Optional[FrameLanding] = None
+        self._copy_stream: Optional[th.cuda.Stream] = None
 
     # -------------------------------------------------------------- device steps
     def _env_args(self, mode: int, k: int = 0, actions: Optional[th.Tensor] = None, b: Optional[Dict] = None) -> Dict:
@@ -553,7 +622,13 @@ class DeviceDAggerCollector:
             with_term.index_copy_(0, th.as_tensor(pos_term, device=dev),
                                   flat(term_all).index_select(0, th.as_tensor(ends, device=dev)))
         h_obs = np.empty(tuple(with_term.shape), dtype=np.uint8 if with_term.dtype == th.uint8 else np.float32)
-        th.from_numpy(h_obs).copy_(with_term)
+        self.last_landing = None
+        if self.async_frames and len(finished):
+            if self._copy_stream is None:
+                self._copy_stream = th.cuda.Stream(device=dev)
+            self.last_landing = FrameLanding(h_obs, with_term, self._copy_stream)
+        else:
+            th.from_numpy(h_obs).copy_(with_term)
         h_acts = self.last_acts.cpu().numpy()
         h_rew = flat(rew_all).index_select(0, ridx).float().cpu().numpy()
         trajs: List[types.TrajectoryWithRew] = []
@@ -567,6 +642,70 @@ class DeviceDAggerCollector:
         return trajs
 
     # -------------------------------------------------------------- rollout stats
+    _ENV_TENSORS = ("state", "env_rng", "elapsed", "ep_ret", "obs")
+
+    def _stats_twin(self) -> "DeviceDAggerCollector":
+        """A collector over a frozen copy of the learner (same expert, same host env, the
+        learner head's sampling seed) whose env state is copied in before a statistics run and
+        back after it, so that running the statistics on it is the same as running them here."""
+        twin = getattr(self, "_twin", None)
+        if twin is None:
+            try:  # a fresh module of the same architecture (no training-side attributes)
+                snap = type(self.learner)(**self.learner._get_constructor_parameters()).to(self.device)
+                snap.load_state_dict(self.learner.state_dict())
+            except Exception:  # noqa: BLE001 -- any other policy class: a deep copy
+                import copy
+
+                snap = copy.deepcopy(self.learner)
+            snap.eval()
+            for p in snap.parameters():
+                p.requires_grad_(False)
+            twin = DeviceDAggerCollector(self.venv, self.expert, snap, self.rng, chunk=self.chunk, use_graph=self.use_graph)
+            if self.cnn:
+                twin._head_seed = self._head_seed
+            # its chunk graphs are captured here, on the calling thread (the worker thread only
+            # replays them: no capture may overlap another thread's work): one eager + captured
+            # chunk per buffer set, on throw-away env state (overwritten by every start)
+            twin.reset()
+            for b in twin._sets:
+                twin._run_chunk(b)
+            th.cuda.synchronize(self.device)
+            self._twin = twin
+            self._twin_stream = th.cuda.Stream(device=self.device)
+        return twin
+
+    def start_rollout_stats(self, n_episodes: int) -> StatsFuture:
+        """:meth:`rollout_stats` of the learner's current weights, on a worker thread and a side
+        stream: the weights, the env state and the head's sampling counter are copied into the
+        twin (main stream order), the twin runs the statistics, and ``result()`` copies the env
+        state and counter back -- the same env / RNG sequence as the in-line call. Until
+        ``result()`` returns, the caller must not step this collector's envs."""
+        twin = self._stats_twin()
+        main = th.cuda.current_stream(self.device)
+        with th.no_grad():
+            for d, s_ in zip(twin.learner.parameters(), self.learner.parameters()):
+                d.copy_(s_)
+            for name in self._ENV_TENSORS:
+                getattr(twin, name).copy_(getattr(self, name))
+            if self.cnn:
+                twin._head_ctr.copy_(self._head_ctr)
+        stream = self._twin_stream
+        stream.wait_stream(main)
+
+        def run():
+            with th.cuda.device(self.device), th.cuda.stream(stream):
+                return twin.rollout_stats(n_episodes)
+
+        def finish():
+            main.wait_stream(stream)
+            with th.no_grad():
+                for name in self._ENV_TENSORS:
+                    getattr(self, name).copy_(getattr(twin, name))
+                if self.cnn:
+                    self._head_ctr.copy_(twin._head_ctr)
+
+        return StatsFuture(run, finish)
+
     def rollout_stats(self, n_episodes: int) -> Mapping[str, float]:
         """BC's rollout statistics (``RolloutStatsComputer``: ``generate_trajectories`` of the
         learner alone with ``make_min_episodes(n_episodes)``, then ``rollout_stats``) on the

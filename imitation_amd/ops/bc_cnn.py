@@ -134,20 +134,47 @@ class FusedCnnBCStep:
                                  self.metrics, self.ws, self.ent_weight, self.l2_weight)
             _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1])
             dz = dx.view(hs[-1].shape)
-            # weight-gradient partials per layer; their reductions in ONE launch at the end
+            # weight-gradient partials per layer; their reductions in ONE launch at the end. Each
+            # layer's wgrad runs on a stream of its own, beside the data-gradient chain it does not
+            # feed (in a captured graph: parallel branches), joined before the reduction
             red = {k: [] for k in ("x", "dy", "kh", "kw", "s", "p", "slab", "dw", "db")}
+            main = th.cuda.current_stream(x.device)
+            sides = self._side_streams(x.device)
             for i in range(n - 1, -1, -1):
                 c = convs[i]
                 inp = x if i == 0 else hs[i - 1]
                 top = i == n - 1
                 kh, kw, st = int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0])
-                slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
+                if sides:
+                    sd = sides[i]
+                    sd.wait_stream(main)
+                    for t in (inp, dz, hs[i]):
+                        t.record_stream(sd)
+                    with th.cuda.stream(sd):
+                        slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
+                    slab.record_stream(main)
+                else:
+                    slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
                 for k, v in zip(red, (inp, dz, kh, kw, st, 0, slab, self.g_conv[i][0], self.g_conv[i][1])):
                     red[k].append(v)
                 if i > 0:
                     dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], st, top, True, 0)
+            for sd in sides:
+                main.wait_stream(sd)
             C.conv_reduce_multi(*red.values())
         return self.metrics
+
+    def _side_streams(self, device) -> List[th.cuda.Stream]:
+        """One stream per conv layer for its weight-gradient partials (IMITATION_AMD_BC_CNN_STREAMS=0:
+        everything on the current stream)."""
+        import os
+
+        if os.environ.get("IMITATION_AMD_BC_CNN_STREAMS", "1") == "0":
+            return []
+        ss = getattr(self, "_sides", None)
+        if ss is None:
+            ss = self._sides = [th.cuda.Stream(device=device) for _ in self.convs]
+        return ss
 
 
 def metrics_fields(m: th.Tensor) -> Dict[str, Any]:

@@ -253,3 +253,42 @@ def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batc
     assert [s for s, _ in r0] == [s for s, _ in r1] and len(r0) > 0
     for (_, a), (_, b) in zip(r0, r1):
         assert a == b
+
+
+@gpu
+def test_async_rollout_stats_and_frame_landing_are_bitwise_the_inline_path(tmp_path, monkeypatch):
+    """DAgger-Pong rounds with BC's rollout statistics on the collector's twin (worker thread +
+    side stream, beside the BC epoch) and the frames' D2H in flight (``FrameLanding``) give the
+    same learner weights, logged statistics, aggregate rows and host trajectories as the in-line
+    statistics and blocking copies: the twin starts from and hands back the env state and the
+    head's sampling counter."""
+    runs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IMITATION_AMD_BC_ASYNC_STATS", mode)
+        monkeypatch.setenv("IMITATION_AMD_DAGGER_ASYNC_FRAMES", mode)
+        tr, venv, expert, learner = _pong_trainer(tmp_path / mode)
+        logged = []
+        orig = tr.bc_trainer._bc_logger.log_batch
+
+        def log_batch(batch_num, batch_size, num_samples, metrics, stats, _orig=orig):
+            logged.append((batch_num, dict(stats)))
+            return _orig(batch_num, batch_size, num_samples, metrics, stats)
+
+        tr.bc_trainer._bc_logger.log_batch = log_batch
+        tr.train(2000, rollout_round_min_episodes=1, rollout_round_min_timesteps=400,
+                 bc_train_kwargs=dict(n_epochs=1, progress_bar=False, log_interval=10**9, log_rollouts_n_episodes=3))
+        th.cuda.synchronize()
+        col = tr._device_collector
+        assert (getattr(col, "_twin", None) is not None) == (mode == "1")
+        assert tr.round_num >= 2 and len(logged) == tr.round_num
+        runs.append(dict(params=[p.detach().cpu().clone() for p in learner.parameters()], logged=logged,
+                         agg=tr._device_agg.obs[: len(tr._device_agg)].cpu().clone(),
+                         trajs=[(t.obs.copy(), t.acts.copy()) for t in tr._all_demos]))
+    a, b = runs
+    assert all(th.equal(x, y) for x, y in zip(a["params"], b["params"]))
+    assert a["logged"] == b["logged"]
+    assert th.equal(a["agg"], b["agg"])
+    assert len(a["trajs"]) == len(b["trajs"])
+    for (o1, a1), (o2, a2) in zip(a["trajs"], b["trajs"]):
+        np.testing.assert_array_equal(o1, o2)
+        np.testing.assert_array_equal(a1, a2)
