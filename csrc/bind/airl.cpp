@@ -246,13 +246,14 @@ class AirlDiscPlan {
       IA_HIP_CHECK_A(ia::airl_norm(a, 0, 0, ia_stream()));
     }
   }
-  // the deferred policy-norm merges of staged updates [0, n), in update order
-  void q_merge(int n) {
+  // the deferred policy-norm merges of staged updates [0, n), in update order; rows: rows per
+  // minibatch merge (0: 2 mb; data parallel with synced norms: 2 mb x world)
+  void q_merge(int n, int rows) {
     TORCH_CHECK(n >= 0 && n <= n_slots_, "q_merge: ", n, " updates, ", n_slots_, " staged");
     TORCH_CHECK(a_.q_mean != nullptr && a_.q_count != nullptr, "q_merge: no policy norm");
     if (n == 0) return;
     ia::AirlDiscArgs a = slot_args(0, 0);
-    IA_HIP_CHECK_A(ia::airl_q_merge(a, n * n_mb_, (long long)slot_floats(), 2 * mb_, ia_stream()));
+    IA_HIP_CHECK_A(ia::airl_q_merge(a, n * n_mb_, (long long)slot_floats(), rows > 0 ? rows : 2 * mb_, ia_stream()));
   }
   // Split update under data parallelism: the staging of update `slot`, minibatch k, in the two
   // halves around the normaliser all-reduce -- mode 1: gather + local moments into `sums` (the
@@ -261,7 +262,7 @@ class AirlDiscPlan {
   // / stats reduction only (the caller all-reduces `grads`, then adam(0, 1, ...)). Same launches,
   // same data as the non-split DP update (bitwise).
   void stage_part(int slot, int k, torch::Tensor e_idx, torch::Tensor g_idx, int mode, int n_total, bool merge_b,
-                  bool merge_p, bool merge_q) {
+                  bool merge_p, bool merge_q, bool defer_q) {
     TORCH_CHECK(slot >= 0 && slot < n_slots_, "stage_part: slot ", slot, " outside the reserved ", n_slots_);
     TORCH_CHECK(k >= 0 && k < n_mb_, "stage_part: minibatch ", k);
     TORCH_CHECK(mode == 1 || mode == 2, "stage_part: mode 1 (gather + moments) or 2 (merges)");
@@ -270,7 +271,7 @@ class AirlDiscPlan {
     a.merge_b = merge_b;
     a.merge_p = merge_p;
     a.merge_q = merge_q;
-    a.q_defer = nullptr;
+    if (!(defer_q && merge_q && a.q_mean) || mode == 1) a.q_defer = nullptr;
     if (mode == 1) {
       check_idx(e_idx);
       check_idx(g_idx);
@@ -369,11 +370,12 @@ void register_airl(py::module& m) {
            py::arg("stats_out") = py::none())
       .def("reserve", &AirlDiscPlan::reserve)
       .def("stage_part", &AirlDiscPlan::stage_part, py::arg("slot"), py::arg("k"), py::arg("e_idx"), py::arg("g_idx"),
-           py::arg("mode"), py::arg("n_total"), py::arg("merge_b"), py::arg("merge_p"), py::arg("merge_q"))
+           py::arg("mode"), py::arg("n_total"), py::arg("merge_b"), py::arg("merge_p"), py::arg("merge_q"),
+           py::arg("defer_q") = false)
       .def("apply_grads", &AirlDiscPlan::apply_grads, py::arg("slot"), py::arg("stats_out") = py::none())
       .def("stage", &AirlDiscPlan::stage, py::arg("slot"), py::arg("e_idx"), py::arg("g_idx"), py::arg("merge_b"),
            py::arg("merge_p"), py::arg("merge_q"), py::arg("defer_q") = false)
-      .def("q_merge", &AirlDiscPlan::q_merge, py::arg("n"))
+      .def("q_merge", &AirlDiscPlan::q_merge, py::arg("n"), py::arg("rows") = 0)
       .def("apply", &AirlDiscPlan::apply, py::arg("slot"), py::arg("step_size"), py::arg("bc2_sqrt"),
            py::arg("stats_out") = py::none())
       .def("update", &AirlDiscPlan::update, py::arg("e_idx"), py::arg("g_idx"), py::arg("step_size"), py::arg("bc2_sqrt"),

@@ -277,9 +277,10 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         norms see, none of it dependent on the discriminator weights. Returns each update's
         Adam (step_size, sqrt(1 - beta2^t)).
 
-        ``defer_q`` (single rank): leave the policy-norm merges to ``_merge_deferred_q`` (one
-        launch after PPO), so the staging can run on the side stream during the PPO update;
-        ``self._q_deferred`` says whether there is anything to merge."""
+        ``defer_q``: leave the policy-norm merges to ``_merge_deferred_q`` (one launch after
+        PPO), so the staging can run on the side stream during the PPO update (under DP its
+        normaliser all-reduces then run there too); ``self._q_deferred`` says whether there is
+        anything to merge."""
         if self._gen_dev.size() == 0:
             raise RuntimeError("No generator samples for training. Call `train_gen()` first.")
         # (grows only here: the previous round's applies were waited for on the host)
@@ -295,8 +296,10 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         merge_q = self.pol_norm is not None and self.pol_norm.training
         scal = []
         world = pdist.world_size()
-        defer_q = defer_q and merge_q and (world == 1 or not pdist.norm_sync_active())
+        defer_q = defer_q and merge_q
         self._q_deferred = defer_q
+        synced = world > 1 and pdist.norm_sync_active()
+        self._q_defer_rows = 2 * self.demo_minibatch_size * (world if synced else 1)
         cur = th.cuda.current_stream(self._dev)
         for i in range(n):
             e_idx = self._endless_expert_iterator.next_indices()
@@ -311,7 +314,7 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
                 for k in range(B // mb):
                     self._disc_plan.stage_part(i, k, e_idx, g_idx, 1, 0, merge_b, merge_p, merge_q)
                     pdist.allreduce_sum_(self._disc_ws["sums"])
-                    self._disc_plan.stage_part(i, k, e_idx, g_idx, 2, 2 * mb * world, merge_b, merge_p, merge_q)
+                    self._disc_plan.stage_part(i, k, e_idx, g_idx, 2, 2 * mb * world, merge_b, merge_p, merge_q, defer_q)
             t = t0 + i + 1.0
             scal.append((float(g["lr"]) / (1.0 - beta1**t), (1.0 - beta2**t) ** 0.5))
         return scal
@@ -319,7 +322,7 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
     def _merge_deferred_q(self, n: int) -> None:
         """The policy-norm merges ``_stage_disc_updates(n, defer_q=True)`` left (update order)."""
         if getattr(self, "_q_deferred", False):
-            self._disc_plan.q_merge(n)
+            self._disc_plan.q_merge(n, self._q_defer_rows)
             self._q_deferred = False
 
     @profiling.traced("disc/apply")

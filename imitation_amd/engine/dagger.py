@@ -28,6 +28,7 @@ from __future__ import annotations
 import os
 import queue
 import threading
+import time
 from typing import Callable, Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
@@ -298,9 +299,16 @@ class FrameLanding:
         with self._lock:
             if self._landed:
                 return
-            self._ev.synchronize()
+            # (polled under the capture lock: a HIP call from this thread must not fall inside
+            # a capture on the training thread)
+            while True:
+                with graphs.CAPTURE_LOCK:
+                    if self._ev.query():
+                        break
+                time.sleep(2e-4)
             np.copyto(self.dst, self._pinned.numpy())
-            self._pinned = None
+            with graphs.CAPTURE_LOCK:  # (the host allocator's free may query events)
+                self._pinned = None
             self._landed = True
 
 
@@ -376,7 +384,8 @@ class StatsFuture:
 
     def _run(self, fn) -> None:
         try:
-            self._out = fn()
+            with graphs.CAPTURE_LOCK:  # (no capture on the training thread while this runs)
+                self._out = fn()
         except BaseException as e:  # re-raised by result()
             self._err = e
 

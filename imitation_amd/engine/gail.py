@@ -1474,10 +1474,11 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         return steps, nxt
 
     def _stage_during_ppo(self) -> bool:
-        """Split-round staging on the side stream, concurrent with PPO (single rank; the DP
-        staging's normaliser all-reduces stay on the main stream). IMITATION_AMD_AIRL_EARLY_STAGE=0:
-        stage behind PPO on the main stream."""
-        return (pdist.world_size() == 1 and getattr(self, "_host_staged", False)
+        """Split-round staging on the side stream, concurrent with PPO. Under data parallelism
+        only with the replicated PPO update, which issues no collective: the staging's normaliser
+        all-reduces are then the only users of the communicator while they run.
+        IMITATION_AMD_AIRL_EARLY_STAGE=0: stage behind PPO on the main stream."""
+        return ((pdist.world_size() == 1 or self._dp_replicated) and getattr(self, "_host_staged", False)
                 and os.environ.get("IMITATION_AMD_AIRL_EARLY_STAGE", "1") != "0")
 
     def _split_round(self, n: int, ppo_done: th.cuda.Event, launch_next: bool,

@@ -165,11 +165,13 @@ class FusedCnnBCStep:
         return self.metrics
 
     def _side_streams(self, device) -> List[th.cuda.Stream]:
-        """One stream per conv layer for its weight-gradient partials (IMITATION_AMD_BC_CNN_STREAMS=0:
-        everything on the current stream)."""
+        """One stream per conv layer for its weight-gradient partials -- opt-in
+        (IMITATION_AMD_BC_CNN_STREAMS=1): a HIP-graph replay of the multi-stream capture crashed
+        the process once in a GPU test run (round 5), so by default everything stays on the
+        current stream."""
         import os
 
-        if os.environ.get("IMITATION_AMD_BC_CNN_STREAMS", "1") == "0":
+        if os.environ.get("IMITATION_AMD_BC_CNN_STREAMS", "0") != "1":
             return []
         ss = getattr(self, "_sides", None)
         if ss is None:

@@ -23,9 +23,16 @@ from __future__ import annotations
 import contextlib
 import gc
 import os
+import threading
 from typing import Any, Callable, Dict, Optional, Tuple
 
 import torch as th
+
+
+# Held for the whole of every capture: worker threads that make HIP calls (event queries /
+# synchronisations, their own launches) take it around those calls, so that none lands inside
+# a capture -- in the default (global) capture mode such a call from ANY thread invalidates it.
+CAPTURE_LOCK = threading.RLock()
 
 
 @contextlib.contextmanager
@@ -34,11 +41,12 @@ def capture(graph: "th.cuda.CUDAGraph", **kwargs):
     capture: a collection inside it can run finalisers that free pinned host memory or
     destroy events (a synchronising call -- illegal while a stream is capturing), which
     aborts the process depending on when the collector happens to run. (No collection
-    here: a full gc.collect() per capture costs ~100 ms on a large heap.)"""
+    here: a full gc.collect() per capture costs ~100 ms on a large heap.) Holds
+    :data:`CAPTURE_LOCK`."""
     enabled = gc.isenabled()
     gc.disable()
     try:
-        with th.cuda.graph(graph, **kwargs):
+        with CAPTURE_LOCK, th.cuda.graph(graph, **kwargs):
             yield
     finally:
         if enabled:
