@@ -7,8 +7,8 @@
 // BC batch (32 rows) the torch form is three fp32 hipBLASLt GEMMs (~30 us, each reading or
 // writing the 6.4 MB fp32 weight), a permute copy each way, ReLU / bias kernels. Here:
 //   fc_wgrad  dW[n][col] = sum_m dZ[m][n] X[m][k(col)],  db[n] = sum_m dZ[m][n],
-//             dZ = dH * [h > 0] formed on the fly. Block = 64 n x 16 torch columns (4 waves
-//             x 16x16); per 32-row step dZ^T and X are staged transposed in LDS so both MFMA
+//             dZ = dH * [h > 0] formed on the fly. Block = 64 n x 64 torch columns (4 waves
+//             x 4 16x16 tiles); per 32-row step dZ^T and X are staged transposed in LDS so both MFMA
 //             operands read 8 consecutive rows; dW rows are stored contiguously.
 //   fc_dgrad  dX[m][k] = sum_n dZ[m][n] Wt[k][n] (Wt: the weight packed [(h, w, c)][NH], dZ
 //             in bf16 from fc_wgrad), bf16 out in NHWC order = the conv trunk's upstream
@@ -21,25 +21,31 @@
 namespace ia {
 namespace {
 
-// Block = 64 n x 16 torch columns (4 waves x 16x16, wave w owns n rows 16w..16w+15). The 16
-// columns are consecutive in torch's (c, h, w) order, so every dW row segment is one 64-B
-// store; they are gathered from X through the column -> NHWC index map while staged, once per
-// block for all 4 waves. The blocks of the first column tile also write dZ in bf16 (the
-// data-gradient operand) and db.
+// Block = 64 n x 64 torch columns (4 waves, wave w owns n rows 16w..16w+15 and four 16x16
+// column tiles). The 64 columns are consecutive in torch's (c, h, w) order, so every dW row
+// segment is one 256-B run; they are gathered from X through the column -> NHWC index map while
+// staged, once per block for all 4 waves. 4 column tiles per block (was 1): the dZ staging --
+// every block re-reads the 64 x M slab of dH / H -- drops 4x (~26 -> ~6 MB of L2 reads per
+// step at NatureCNN / batch 32). The blocks of the first column tile also write dZ in bf16 (the
+// data-gradient operand) and db. Same MFMA per dW element as before (bitwise).
+constexpr int kFcCT = 4;  // 16-column tiles per block
+
 __global__ __launch_bounds__(256) void fc_wgrad_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
                                                        const float* __restrict__ Hout, float* __restrict__ dW,
                                                        float* __restrict__ db, bf16* __restrict__ dZb, int M, int K, int NH,
                                                        int C, int HW) {
-  __shared__ __attribute__((aligned(16))) bf16 zs[64][40];  // dZ^T chunk [n][m] (+8 pad)
-  __shared__ __attribute__((aligned(16))) bf16 xs[16][40];  // X^T chunk [col][m]
+  __shared__ __attribute__((aligned(16))) bf16 zs[64][40];            // dZ^T chunk [n][m] (+8 pad)
+  __shared__ __attribute__((aligned(16))) bf16 xs[16 * kFcCT][40];    // X^T chunk [col][m]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  const int col0 = blockIdx.x * 16, n0 = blockIdx.y * 64;
+  const int col0 = blockIdx.x * 16 * kFcCT, n0 = blockIdx.y * 64;
   const bool first = blockIdx.x == 0;
-  // this thread's 2 staged (column, row) elements of X: column -> NHWC offset
-  const int xc = tid & 15, xm = tid >> 4;  // 16 columns x 16 rows per pass, 2 passes
+  // this thread's staged (column, row) elements of X: 64 columns x 4 rows per pass, 8 passes
+  const int xc = tid & 63, xm = tid >> 6;
   const int xcol = col0 + xc, xch = xcol / HW;
   const int koff = (xcol - xch * HW) * C + xch;
-  f32x4 acc = zero4();
+  f32x4 acc[kFcCT];
+#pragma unroll
+  for (int t = 0; t < kFcCT; ++t) acc[t] = zero4();
   for (int m0 = 0; m0 < M; m0 += 32) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {  // dZ^T: 64 n x 32 m, coalesced along n
@@ -54,19 +60,25 @@ __global__ __launch_bounds__(256) void fc_wgrad_kernel(const bf16* __restrict__ 
       zs[nn][mm] = (bf16)z;
     }
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {  // X^T: 16 columns x 32 m
-      const int mm = xm + 16 * e, m = m0 + mm;
+    for (int e = 0; e < 8; ++e) {  // X^T: 64 columns x 32 m
+      const int mm = xm + 4 * e, m = m0 + mm;
       xs[xc][mm] = m < M ? X[(size_t)m * K + koff] : (bf16)0.f;
     }
     __syncthreads();
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(&zs[w * 16 + (l & 15)][(l >> 4) * 8]);
-    const bf16x8 b = *reinterpret_cast<const bf16x8*>(&xs[l & 15][(l >> 4) * 8]);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < kFcCT; ++t) {
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(&xs[16 * t + (l & 15)][(l >> 4) * 8]);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t], 0, 0, 0);
+    }
     __syncthreads();
   }
-  const int col = col0 + (l & 15);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dW[(size_t)(n0 + w * 16 + 4 * (l >> 4) + i) * K + col] = acc[i];
+  for (int t = 0; t < kFcCT; ++t) {
+    const int col = col0 + 16 * t + (l & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dW[(size_t)(n0 + w * 16 + 4 * (l >> 4) + i) * K + col] = acc[t][i];
+  }
   if (first && tid < 64) {  // bias gradient, fixed row order
     float s = 0.f;
     for (int m = 0; m < M; ++m) {
@@ -127,7 +139,7 @@ bool fc_train_ok(int M, int K, int NH, int C, int HW) {
 hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const void* Wt, float* dW, float* db, void* dX,
                        void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s) {
   if (!fc_train_ok(M, K, NH, C, HW)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / 16, NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout, dW, db,
+  hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / (16 * kFcCT), NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout, dW, db,
                      static_cast<bf16*>(dZb), M, K, NH, C, HW);
   if (dX) {
     const int waves = ((M + 15) / 16) * (K / 16);

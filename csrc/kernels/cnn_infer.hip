@@ -94,26 +94,51 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t ctr, int b
 
 constexpr int kMaxHeadActions = 64;
 
-// One wave per batch row: every lane owns NH/64 hidden units and accumulates all A logits
-// at once (independent loads in flight), then A wave reductions.
-constexpr int kHeadRegA = 16;
+// One wave per batch row: every lane owns NH/64 hidden units and accumulates all A logits,
+// then A wave reductions. For NH <= 64 * kHeadJ (NatureCNN: 512) every load of the row -- the
+// lane's hidden values and the A x NH/64 weights -- is issued before the first FMA (one memory
+// latency per row instead of one per 64 hidden units); the FMAs keep the j-ascending order of
+// the general loop, so both paths give the same bits.
+constexpr int kHeadRegA = 8;
+constexpr int kHeadJ = 8;
 
-// Row b's choice under head a (argmax, or Gumbel-max with the launch counter ctr): the same
-// accumulation order as cnn_head_kernel.
+__device__ __forceinline__ void head_logits(const CnnHeadArgs& a, const float* hb, int a0, int l, float (&acc)[kHeadRegA]) {
+#pragma unroll
+  for (int q = 0; q < kHeadRegA; ++q) acc[q] = 0.f;
+  if (a.NH <= 64 * kHeadJ) {
+    float hv[kHeadJ], wv[kHeadRegA][kHeadJ];
+#pragma unroll
+    for (int jj = 0; jj < kHeadJ; ++jj) {
+      const int j = l + 64 * jj;
+      hv[jj] = j < a.NH ? hb[j] : 0.f;
+#pragma unroll
+      for (int q = 0; q < kHeadRegA; ++q) wv[q][jj] = (j < a.NH && a0 + q < a.A) ? a.W2[(size_t)(a0 + q) * a.NH + j] : 0.f;
+    }
+#pragma unroll
+    for (int jj = 0; jj < kHeadJ; ++jj) {
+      if (l + 64 * jj >= a.NH) break;
+#pragma unroll
+      for (int q = 0; q < kHeadRegA; ++q)
+        if (a0 + q < a.A) acc[q] += hv[jj] * wv[q][jj];
+    }
+    return;
+  }
+  for (int j = l; j < a.NH; j += 64) {
+    const float hv = hb[j];
+#pragma unroll
+    for (int q = 0; q < kHeadRegA; ++q)
+      if (a0 + q < a.A) acc[q] += hv * a.W2[(size_t)(a0 + q) * a.NH + j];
+  }
+}
+
+// Row b's choice under head a (argmax, or Gumbel-max with the launch counter ctr).
 __device__ __forceinline__ int head_row(const CnnHeadArgs& a, int b, uint64_t ctr, int l) {
   const float* hb = a.h + (size_t)b * a.NH;
   int best = 0;
   float best_v = -INFINITY;
   for (int a0 = 0; a0 < a.A; a0 += kHeadRegA) {
     float acc[kHeadRegA];
-#pragma unroll
-    for (int q = 0; q < kHeadRegA; ++q) acc[q] = 0.f;
-    for (int j = l; j < a.NH; j += 64) {
-      const float hv = hb[j];
-#pragma unroll
-      for (int q = 0; q < kHeadRegA; ++q)
-        if (a0 + q < a.A) acc[q] += hv * a.W2[(size_t)(a0 + q) * a.NH + j];
-    }
+    head_logits(a, hb, a0, l, acc);
 #pragma unroll
     for (int q = 0; q < kHeadRegA; ++q) {
       if (a0 + q >= a.A) break;
@@ -131,17 +156,26 @@ __device__ __forceinline__ int head_row(const CnnHeadArgs& a, int b, uint64_t ct
   return best;
 }
 
-// DAgger's per-step pair in ONE launch (one wave per row): the expert's argmax (e: its action
-// and record slot) and the learner's sample (r), mixed as the learner's exec_out does with the
-// expert's action of the same row -- no cross-wave dependency, so no second launch.
+// DAgger's per-step pair in ONE launch: the expert's argmax (e: its action and record slot) and
+// the learner's sample (r), mixed as the learner's exec_out does with the expert's action of
+// the same row. The two heads' rows run on different waves (2 B row tasks), their choices meet
+// in LDS (B <= kHeadPairMaxB; larger batches loop both heads per wave).
+constexpr int kHeadPairMaxB = 256;
+
 __global__ __launch_bounds__(1024) void cnn_head_pair_kernel(CnnHeadArgs e, CnnHeadArgs r) {
+  __shared__ int choice[2][kHeadPairMaxB];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint64_t ctr_e = e.counter ? *e.counter : 0ull;
   const uint64_t ctr_r = r.counter ? *r.counter : 0ull;
-  for (int b = w; b < e.B; b += nw) {
-    const int be = head_row(e, b, ctr_e, l);
-    const int br = head_row(r, b, ctr_r, l);
-    if (l == 0) {
+  if (e.B <= kHeadPairMaxB) {
+    for (int t = w; t < 2 * e.B; t += nw) {
+      const int h = t & 1, b = t >> 1;
+      const int c = h == 0 ? head_row(e, b, ctr_e, l) : head_row(r, b, ctr_r, l);
+      if (l == 0) choice[h][b] = c;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < e.B; b += blockDim.x) {
+      const int be = choice[0][b], br = choice[1][b];
       e.out[b] = be;
       if (e.rec_out) e.rec_out[b] = be;
       r.out[b] = br;
@@ -149,6 +183,21 @@ __global__ __launch_bounds__(1024) void cnn_head_pair_kernel(CnnHeadArgs e, CnnH
       if (r.exec_out) {
         const float u = hash_uniform(r.seed ^ 0x5DEECE66Dull, ctr_r, b, kMaxHeadActions);
         r.exec_out[b] = (u > *r.beta) ? (int64_t)br : (int64_t)be;
+      }
+    }
+  } else {
+    for (int b = w; b < e.B; b += nw) {
+      const int be = head_row(e, b, ctr_e, l);
+      const int br = head_row(r, b, ctr_r, l);
+      if (l == 0) {
+        e.out[b] = be;
+        if (e.rec_out) e.rec_out[b] = be;
+        r.out[b] = br;
+        if (r.rec_out) r.rec_out[b] = br;
+        if (r.exec_out) {
+          const float u = hash_uniform(r.seed ^ 0x5DEECE66Dull, ctr_r, b, kMaxHeadActions);
+          r.exec_out[b] = (u > *r.beta) ? (int64_t)br : (int64_t)be;
+        }
       }
     }
   }
@@ -163,33 +212,7 @@ __global__ __launch_bounds__(1024) void cnn_head_kernel(CnnHeadArgs a) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint64_t ctr = a.counter ? *a.counter : 0ull;
   for (int b = w; b < a.B; b += nw) {
-    const float* hb = a.h + (size_t)b * a.NH;
-    int best = 0;
-    float best_v = -INFINITY;
-    for (int a0 = 0; a0 < a.A; a0 += kHeadRegA) {
-      float acc[kHeadRegA];
-#pragma unroll
-      for (int q = 0; q < kHeadRegA; ++q) acc[q] = 0.f;
-      for (int j = l; j < a.NH; j += 64) {
-        const float hv = hb[j];
-#pragma unroll
-        for (int q = 0; q < kHeadRegA; ++q)
-          if (a0 + q < a.A) acc[q] += hv * a.W2[(size_t)(a0 + q) * a.NH + j];
-      }
-#pragma unroll
-      for (int q = 0; q < kHeadRegA; ++q) {
-        if (a0 + q >= a.A) break;
-        float p = acc[q];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
-        float v = p + a.b2[a0 + q];
-        if (a.mode == 1) v += -logf(-logf(hash_uniform(a.seed, ctr, b, a0 + q)));
-        if (v > best_v) {  // first maximum, like torch.argmax
-          best_v = v;
-          best = a0 + q;
-        }
-      }
-    }
+    const int best = head_row(a, b, ctr, l);
     if (l == 0) {
       a.out[b] = best;
       if (a.rec_out) a.rec_out[b] = best;
@@ -225,7 +248,7 @@ hipError_t cnn_head_pair(const CnnHeadArgs& e, const CnnHeadArgs& r, hipStream_t
   if (e.B != r.B || e.NH != r.NH || e.A <= 0 || e.A > kMaxHeadActions || r.A <= 0 || r.A > kMaxHeadActions)
     return hipErrorInvalidValue;
   if (r.exec_out && !r.beta) return hipErrorInvalidValue;
-  const int waves = e.B < 16 ? e.B : 16;
+  const int waves = 2 * e.B < 16 ? 2 * e.B : 16;
   hipLaunchKernelGGL(cnn_head_pair_kernel, dim3(1), dim3(64 * waves), 0, s, e, r);
   return hipGetLastError();
 }

@@ -290,6 +290,102 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(const bf16* __restrict_
   }
 }
 
+// Small-batch data gradient (one 16-pixel tile per wave, N = 32 NN output channels): the same
+// tap order and MFMA sequence per accumulator as conv_dgrad_kernel<CT, 1> (bitwise), but the
+// loads of the next kDgDepth taps are in flight while a tap's MFMAs run. At BC batch sizes the
+// grid is < 1 wave per CU and the kernel time is one wave's dependent chain of per-tap load
+// round trips (NatureCNN conv3: 9 taps x 2 channel halves ~ 18 us); with 3 taps in flight it
+// is about a third of that.
+constexpr int kDgDepth = 3;
+
+template <int CT, int NN>
+struct DgTap {
+  bool any, valid;
+  bf16x8 a[NN];
+  bf16x8 b[NN][CT];
+};
+
+template <int CT, int NN>
+__global__ __launch_bounds__(256) void conv_dgrad_pf_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
+                                                            const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
+                                                            bf16* __restrict__ dZp, ConvGeo g, int relu_out, int relu_in) {
+  const int l = threadIdx.x & 63;
+  const int ph = blockIdx.y / g.S, pw = blockIdx.y - ph * g.S;
+  const int Hc = (g.H - ph + g.S - 1) / g.S, Wc = (g.W - pw + g.S - 1) / g.S;
+  const int HWc = Hc * Wc;
+  const int P = g.B * HWc;
+  const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  if (p0 >= P) return;
+  const int Kp = g.KH * g.KW * g.N;
+  const int r = l & 15, kq = (l >> 4) * 8;
+  auto pix_of = [&](int q, int& b, int& ih, int& iw) {
+    b = q / HWc;
+    const int rem = q - b * HWc, i = rem / Wc, j = rem - i * Wc;
+    ih = ph + g.S * i;
+    iw = pw + g.S * j;
+  };
+  int pb, pih, piw;
+  const bool pv = p0 + r < P;
+  pix_of(pv ? p0 + r : P - 1, pb, pih, piw);
+  f32x4 acc[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) acc[t] = zero4();
+  const bf16* wr = Wt + (size_t)r * Kp + kq;
+  const int nkw = (g.KW - pw + g.S - 1) / g.S;
+  const int ntap = ((g.KH - ph + g.S - 1) / g.S) * nkw;
+  auto load_tap = [&](int tp, DgTap<CT, NN>& st) {
+    const int kh = ph + g.S * (tp / nkw), kw = pw + g.S * (tp - (tp / nkw) * nkw);
+    const int th = pih + g.P - kh, tw = piw + g.P - kw;
+    const int oh = th / g.S, ow = tw / g.S;
+    st.valid = pv && th >= 0 && oh < g.OH && tw >= 0 && ow < g.OW;
+    st.any = __ballot(st.valid) != 0ull;
+    const size_t dzoff = st.valid ? ((size_t)(pb * g.OH + oh) * g.OW + ow) * g.N + kq : 0;
+    const int kbase = (kh * g.KW + kw) * g.N;
+#pragma unroll
+    for (int nn = 0; nn < NN; ++nn) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) st.b[nn][t] = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * Kp + kbase + 32 * nn);
+      st.a[nn] = st.valid ? load_dz8(dY, Y, dzoff + 32 * nn, relu_out) : zero8();
+    }
+  };
+  auto run_tap = [&](const DgTap<CT, NN>& st) {
+    if (!st.any) return;  // (the tap misses every pixel of the wave's tile: no MFMA, as before)
+#pragma unroll
+    for (int nn = 0; nn < NN; ++nn)
+#pragma unroll
+      for (int t = 0; t < CT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(st.a[nn], st.b[nn][t], acc[t], 0, 0, 0);
+  };
+  DgTap<CT, NN> ring[kDgDepth];
+#pragma unroll
+  for (int d = 0; d < kDgDepth; ++d)
+    if (d < ntap) load_tap(d, ring[d]);
+  for (int tp = 0; tp < ntap; tp += kDgDepth) {
+#pragma unroll
+    for (int d = 0; d < kDgDepth; ++d) {
+      if (tp + d < ntap) {
+        run_tap(ring[d]);
+        if (tp + d + kDgDepth < ntap) load_tap(tp + d + kDgDepth, ring[d]);
+      }
+    }
+  }
+  const int col = l & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = p0 + 4 * (l >> 4) + i;
+    if (q >= P) continue;
+    int bb, hh, ww;
+    pix_of(q, bb, hh, ww);
+    const size_t row = ((size_t)bb * g.H + hh) * g.W + ww;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int c = t * 16 + col;
+      float v = acc[t][i];
+      if (relu_in && !((float)Xp[row * g.C + c] > 0.f)) v = 0.f;
+      dZp[row * g.C + c] = (bf16)v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient (partials)
 // 512 threads; wave w owns output tiles t = w + 8 i (t = nt * KT + kt), TPW >= ceil(NT*KT/8).
 // Each block reduces a contiguous m range in chunks of CH rows staged transposed in LDS
@@ -321,23 +417,38 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
 #pragma unroll
   for (int i = 0; i < TPW; ++i) acc[i] = zero4();
   float bsum = 0.f;  // bias partial of channel tid (tid < N)
+  const int n_items = (K / 8) * CH;
   for (int c0 = mb; c0 < me; c0 += CH) {
-    // im2col fragments (k-group kg, row ml), transposed
-    for (int it = tid; it < (K / 8) * CH; it += 512) {
-      const int ml = it % CH, kg = it / CH;
-      const int m = c0 + ml;
-      bf16x8 v = zero8();
-      if (m < me) {
-        const int b = m / OHW, pix = m - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
-        if (tap_checked) {
-          v = load8_pad(X, g, b, oh, ow, kg * 8, true, in_scale);
-        } else {
-          const int k = kg * 8, kh = k / rowlen, off = k - kh * rowlen;
-          v = load8(X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C + kh * xrow + off, in_scale);
+    // im2col fragments (k-group kg, row ml), transposed; kWgBatch fragments per thread are
+    // loaded before any is stored, so their round trips overlap (small-batch chunks: one batch)
+    constexpr int kWgBatch = 8;
+    for (int base = tid; base < n_items; base += 512 * kWgBatch) {
+      bf16x8 v[kWgBatch];
+#pragma unroll
+      for (int u = 0; u < kWgBatch; ++u) {
+        const int it = base + 512 * u;
+        v[u] = zero8();
+        if (it >= n_items) continue;
+        const int ml = it % CH, kg = it / CH;
+        const int m = c0 + ml;
+        if (m < me) {
+          const int b = m / OHW, pix = m - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
+          if (tap_checked) {
+            v[u] = load8_pad(X, g, b, oh, ow, kg * 8, true, in_scale);
+          } else {
+            const int k = kg * 8, kh = k / rowlen, off = k - kh * rowlen;
+            v[u] = load8(X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C + kh * xrow + off, in_scale);
+          }
         }
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) At[(size_t)(kg * 8 + j) * LD + ml] = v[j];
+      for (int u = 0; u < kWgBatch; ++u) {
+        const int it = base + 512 * u;
+        if (it >= n_items) continue;
+        const int ml = it % CH, kg = it / CH;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) At[(size_t)(kg * 8 + j) * LD + ml] = v[u][j];
+      }
     }
     // dZ fragments (8 channels ng, row ml): dY * [Y > 0] when relu_out, transposed
     for (int it = tid; it < (N / 8) * CH; it += 512) {
@@ -734,8 +845,14 @@ hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void*
   const bf16* wt = static_cast<const bf16*>(Wt);
   const bf16* xp = static_cast<const bf16*>(Xp);
   bf16* dz = static_cast<bf16*>(dZp);
-#define IA_DG(CT)                                                                                                     \
-  if (big) hipLaunchKernelGGL((conv_dgrad_kernel<CT, 4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); \
+  // small batches, N = 32 / 64: the prefetching form (same MFMA sequence)
+  const int nn = g.N / 32;
+  static const bool pf_off = getenv("IMITATION_AMD_CONV_DGRAD_PF") != nullptr;  // (A/B knob: the old loop)
+  const bool pf = !big && (nn == 1 || nn == 2) && !pf_off;
+#define IA_DG(CT)                                                                                                         \
+  if (big) hipLaunchKernelGGL((conv_dgrad_kernel<CT, 4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in);     \
+  else if (pf && nn == 2) hipLaunchKernelGGL((conv_dgrad_pf_kernel<CT, 2>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); \
+  else if (pf) hipLaunchKernelGGL((conv_dgrad_pf_kernel<CT, 1>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); \
   else hipLaunchKernelGGL((conv_dgrad_kernel<CT, 1>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in)
   switch (g.C / 16) {
     case 1: IA_DG(1); break;
