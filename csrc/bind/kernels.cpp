@@ -199,7 +199,9 @@ py::tuple gae(torch::Tensor rew, torch::Tensor val, torch::Tensor starts, torch:
 // One fused Adam / AdamW step over flat fp32 buffers (ops/optim.py FusedAdam).
 void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg, torch::Tensor exp_avg_sq,
                torch::Tensor step, double lr, double beta1, double beta2, double eps, double weight_decay, bool decoupled,
-               bool maximize, bool zero_grad, c10::optional<torch::Tensor> step_cnt) {
+               bool maximize, bool zero_grad, c10::optional<torch::Tensor> step_cnt,
+               c10::optional<torch::Tensor> append_src, c10::optional<torch::Tensor> append_all,
+               c10::optional<torch::Tensor> append_cursor) {
   for (auto* t : {&params, &grads, &exp_avg, &exp_avg_sq}) {
     IA_CHECK_GPU_F32(*t);
     TORCH_CHECK(t->numel() == params.numel(), "flat Adam buffers must have equal sizes");
@@ -225,6 +227,22 @@ void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg,
     IA_CHECK_CUDA(*step_cnt);
     TORCH_CHECK(step_cnt->scalar_type() == torch::kInt32 && step_cnt->numel() == 1, "step_cnt: int32 scalar (zero)");
     a.cnt = reinterpret_cast<unsigned*>(step_cnt->data_ptr<int>());
+  }
+  if (append_cursor && append_cursor->defined()) {  // + the graphed epoch's metrics append
+    TORCH_CHECK(append_src && append_src->defined() && append_all && append_all->defined(), "append: src, all, cursor");
+    const auto& src = *append_src;
+    const auto& all = *append_all;
+    const auto& cur = *append_cursor;
+    IA_CHECK_CUDA(src);
+    IA_CHECK_CUDA(all);
+    IA_CHECK_CUDA(cur);
+    TORCH_CHECK(src.scalar_type() == torch::kFloat32 && all.scalar_type() == torch::kFloat32 && src.is_contiguous() &&
+                    all.is_contiguous() && all.numel() % src.numel() == 0 && cur.scalar_type() == torch::kInt32,
+                "append: fp32 src [n], all [m, n], int32 cursor");
+    a.app_src = src.data_ptr<float>();
+    a.app_all = all.data_ptr<float>();
+    a.app_cursor = cur.data_ptr<int>();
+    a.app_n = (int)src.numel();
   }
   IA_HIP_CHECK(ia::adam_flat(a, ia_stream()));
 }
@@ -419,7 +437,7 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
 // rows perm[*cursor * n + r] of every source into the caller-owned dst tensors (one launch,
 // no host arguments per minibatch: HIP-graph epochs)
 void gather_rows_cursor(std::vector<torch::Tensor> srcs, torch::Tensor perm, torch::Tensor cursor, int64_t n,
-                        std::vector<torch::Tensor> dst) {
+                        std::vector<torch::Tensor> dst, c10::optional<torch::Tensor> inc) {
   TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= ia::kGatherMax && dst.size() == srcs.size(), "gather_rows_cursor: 1..8 fields");
   IA_CHECK_CUDA(perm);
   IA_CHECK_CONTIG(perm);
@@ -441,7 +459,13 @@ void gather_rows_cursor(std::vector<torch::Tensor> srcs, torch::Tensor perm, tor
                 "gather_rows_cursor: dst ", i, " shape / dtype / device");
     a.f[i] = ia::GatherField{t.data_ptr(), o.data_ptr(), rows ? (int64_t)(t.nbytes() / rows) : 0, rows};
   }
-  IA_HIP_CHECK(ia::gather_rows_cursor(a, perm.data_ptr<int>(), cursor.data_ptr<int>(), (int)n, ia_stream()));
+  float* incp = nullptr;
+  if (inc && inc->defined()) {
+    IA_CHECK_GPU_F32(*inc);
+    TORCH_CHECK(inc->numel() == 1, "gather_rows_cursor: inc must be a 1-element fp32 tensor");
+    incp = inc->data_ptr<float>();
+  }
+  IA_HIP_CHECK(ia::gather_rows_cursor(a, perm.data_ptr<int>(), cursor.data_ptr<int>(), (int)n, ia_stream(), incp));
 }
 
 void append_at_cursor(torch::Tensor src, torch::Tensor all, torch::Tensor cursor) {
@@ -604,12 +628,14 @@ void register_kernels(py::module& m) {
         py::arg("dones"), py::arg("gamma"), py::arg("lam"), py::arg("moments") = py::none());
   m.def("adam_flat", &adam_flat, py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"),
         py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
-        py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"), py::arg("step_cnt") = py::none());
+        py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"), py::arg("step_cnt") = py::none(),
+        py::arg("append_src") = py::none(), py::arg("append_all") = py::none(), py::arg("append_cursor") = py::none());
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
   m.def("running_norm", &running_norm, py::arg("x"), py::arg("mean"), py::arg("var"), py::arg("count"), py::arg("eps"),
         py::arg("update"), py::arg("want_y"), py::arg("ema_inv_lr") = py::none(), py::arg("ema_num_batches") = py::none(),
         py::arg("ema_decay") = 0.0);
-  m.def("gather_rows_cursor", &gather_rows_cursor, "rows perm[*cursor * n ..] of every source into dst (graph epochs)");
+  m.def("gather_rows_cursor", &gather_rows_cursor, "rows perm[*cursor * n ..] of every source into dst (graph epochs)",
+        py::arg("srcs"), py::arg("perm"), py::arg("cursor"), py::arg("n"), py::arg("dst"), py::arg("inc") = py::none());
   m.def("append_at_cursor", &append_at_cursor, "all[*cursor] = src; ++*cursor");
   m.def("gather_rows", &gather_rows, py::arg("srcs"), py::arg("b"), py::arg("e") = py::none(), py::arg("n_envs") = 1,
         py::arg("dst") = py::none());

@@ -48,7 +48,8 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a, const in
 // output is source row perm[*cursor * n + r] (int32 permutation, one entry per source row), so
 // a captured sequence of minibatch steps walks an epoch's order without host arguments.
 __global__ __launch_bounds__(256) void gather_rows_cursor_kernel(GatherArgs a, const int* __restrict__ perm,
-                                                                 const int* __restrict__ cursor, int n) {
+                                                                 const int* __restrict__ cursor, int n, float* inc) {
+  if (inc && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *inc += 1.f;  // (nothing else here reads it)
   const GatherField& f = a.f[blockIdx.y];
   const int64_t rb = f.row_bytes;
   const char* __restrict__ src = static_cast<const char*>(f.src);
@@ -83,7 +84,7 @@ __global__ void append_at_cursor_kernel(const float* __restrict__ src, float* __
 
 }  // namespace
 
-hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* cursor, int n, hipStream_t s) {
+hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* cursor, int n, hipStream_t s, float* inc) {
   if (n <= 0 || a.k <= 0) return hipSuccess;
   if (a.k > kGatherMax) return hipErrorInvalidValue;
   int64_t most = 0;
@@ -93,7 +94,7 @@ hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* c
   }
   int64_t bx = (most + 255) / 256;
   bx = bx < 1 ? 1 : (bx > 1024 ? 1024 : bx);
-  hipLaunchKernelGGL(gather_rows_cursor_kernel, dim3((unsigned)bx, a.k), dim3(256), 0, s, a, perm, cursor, n);
+  hipLaunchKernelGGL(gather_rows_cursor_kernel, dim3((unsigned)bx, a.k), dim3(256), 0, s, a, perm, cursor, n, inc);
   return hipGetLastError();
 }
 

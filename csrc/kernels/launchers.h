@@ -300,6 +300,12 @@ struct AdamArgs {
   int decoupled;  // AdamW: p *= 1 - lr * wd
   int maximize;
   int zero_grad;  // clear the gradient after reading it
+  // optional, block 0 after its update: app_all[*app_cursor][0 .. app_n) = app_src, ++*app_cursor
+  // (a graphed BC epoch's per-step metrics row; saves the append launch)
+  const float* app_src;
+  float* app_all;
+  int* app_cursor;
+  int app_n;
 };
 hipError_t adam_flat(const AdamArgs& a, hipStream_t s);
 
@@ -348,7 +354,8 @@ struct GatherArgs {
 };
 hipError_t gather_rows(const GatherArgs& a, const int64_t* b, const int64_t* e, int n_envs, int n, hipStream_t s);
 // rows perm[*cursor * n .. + n) (int32 ids) of every source (graph-captured epochs)
-hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* cursor, int n, hipStream_t s);
+hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* cursor, int n, hipStream_t s,
+                              float* inc = nullptr);  // inc: ++*inc by one thread (an optimizer's step counter)
 // all[*cursor * n ..] = src[0 .. n), ++*cursor
 hipError_t append_at_cursor(const float* src, float* all, int n, int* cursor, hipStream_t s);
 

@@ -50,6 +50,13 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
   } else {
     for (int64_t i = i4; i < a.n; ++i) adam_one(a.params[i], a.grads[i], a.exp_avg[i], a.exp_avg_sq[i], a, step_size, bc2_sqrt);
   }
+  if (a.app_cursor && blockIdx.x == 0) {
+    __shared__ int cur;
+    if (threadIdx.x == 0) cur = *a.app_cursor;
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.app_n; i += blockDim.x) a.app_all[(size_t)cur * a.app_n + i] = a.app_src[i];
+    if (threadIdx.x == 0) *a.app_cursor = cur + 1;
+  }
   if (a.cnt) {
     // the step counter advances once every block has read it: the last block to arrive stores
     // it (vector atomics, agent scope) -- no separate `step += 1` launch per optimizer step

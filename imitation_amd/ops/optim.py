@@ -139,8 +139,25 @@ class FusedAdam(th.optim.Optimizer):
                 self._bind_grads(f)
 
     # ------------------------------------------------------------------ step
+    def graph_epoch_step_ok(self) -> bool:
+        """Whether :meth:`step` can take ``step_incremented`` / ``append`` (one flat GPU group on
+        the kernel path): the graphed BC epoch then folds the step-counter add into its gather
+        launch and its metrics append into the Adam launch."""
+        from imitation_amd import ops
+
+        live = [f for f in self._flat if f["n"]]
+        return len(live) == 1 and live[0]["flat"].is_cuda and ops.use_kernel(live[0]["flat"])
+
+    def step_counter(self) -> th.Tensor:
+        """The device step counter of the (single) flat group."""
+        return next(f for f in self._flat if f["n"])["step"]
+
     @th.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, step_incremented: bool = False, append=None):
+        """``step_incremented``: the step counter was already advanced for this step (by the
+        caller's own launch). ``append``: ``(src, all, cursor)`` -- after the update, block 0 of
+        the Adam launch copies ``src`` into row ``*cursor`` of ``all`` and advances the cursor.
+        Both need :meth:`graph_epoch_step_ok`."""
         loss = None
         if closure is not None:
             with th.enable_grad():
@@ -156,14 +173,17 @@ class FusedAdam(th.optim.Optimizer):
                 # small buckets: the kernel advances the device step counter itself (no separate
                 # add launch); large ones keep the add -- the one-counter hand-off costs ~12 ns per
                 # arriving block (1,640 blocks for NatureCNN's 1.7M parameters: 11 -> 25 us)
-                small = f["flat"].numel() <= 64 * 1024
-                if not small:
+                small = f["flat"].numel() <= 64 * 1024 and not step_incremented
+                if not small and not step_incremented:
                     f["step"].add_(1.0)
+                app = append if append is not None else (None, None, None)
                 ops.native().adam_flat(f["flat"], f["grad"], f["m"], f["v"], f["step"], float(group["lr"]), float(b1),
                                        float(b2), float(group["eps"]), float(group["weight_decay"]),
                                        bool(group["decoupled_weight_decay"]), bool(group["maximize"]), True,
-                                       f["cnt"] if small else None)
+                                       f["cnt"] if small else None, app[0], app[1], app[2])
             else:
+                if step_incremented or append is not None:
+                    raise ValueError("step_incremented / append need the kernel path (graph_epoch_step_ok)")
                 f["step"].add_(1.0)
                 self._step_reference(group, f)
         return loss
