@@ -100,9 +100,13 @@ def _cartpole_trainer(algo: str, demos, seed: int, device, logger, cap: int = 51
     return tr
 
 
-def _pendulum_trainer(algo: str, demos, seed: int, device, logger, cap: int = 512):
+def _pendulum_trainer(algo: str, demos, seed: int, device, logger, cap: int = 512, n_disc: Optional[int] = None,
+                      demo_batch: Optional[int] = None, normalize_output: bool = False):
     """Pendulum-v1 (continuous): SB3 MlpPolicy PPO with the rl-zoo Pendulum settings
-    (gamma 0.9, gae_lambda 0.95, lr 1e-3, n_steps 1024 x 4 envs, 10 epochs, use_sde off)."""
+    (gamma 0.9, gae_lambda 0.95, lr 1e-3, n_steps 1024 x 4 envs, 10 epochs, use_sde off).
+    ``n_disc`` / ``demo_batch`` override the tutorial's discriminator schedule;
+    ``normalize_output`` wraps the reward net in ``NormalizedRewardNet`` (the reference scripts'
+    default ``normalize_output_layer=RunningNorm``)."""
     from imitation_amd.engine.airl import DeviceAIRL
     from imitation_amd.engine.gail import DeviceGAIL
     from imitation_amd.rewards.reward_nets import BasicRewardNet, BasicShapedRewardNet
@@ -114,19 +118,28 @@ def _pendulum_trainer(algo: str, demos, seed: int, device, logger, cap: int = 51
     venv = make_vec_env("Pendulum-v1", rng=np.random.default_rng(seed), n_envs=8)
     learner = PPO(ActorCriticPolicy, venv, n_steps=1024, batch_size=64, gamma=0.9, gae_lambda=0.95, learning_rate=1e-3,
                   n_epochs=10, ent_coef=0.0, clip_range=0.2, seed=seed, device=device)
+    from imitation_amd.rewards.reward_nets import NormalizedRewardNet
+
     if algo == "gail":
         rn = BasicRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
-        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=1024, gen_replay_buffer_capacity=cap,
-                        n_disc_updates_per_round=8, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
+        if normalize_output:
+            rn = NormalizedRewardNet(rn, RunningNorm)
+        tr = DeviceGAIL(demonstrations=demos, demo_batch_size=demo_batch or 1024, gen_replay_buffer_capacity=cap,
+                        n_disc_updates_per_round=n_disc or 8, venv=venv, gen_algo=learner, reward_net=rn,
+                        custom_logger=logger)
     else:
         rn = BasicShapedRewardNet(venv.observation_space, venv.action_space, normalize_input_layer=RunningNorm)
-        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=2048, gen_replay_buffer_capacity=cap,
-                        n_disc_updates_per_round=16, venv=venv, gen_algo=learner, reward_net=rn, custom_logger=logger)
+        if normalize_output:
+            rn = NormalizedRewardNet(rn, RunningNorm)
+        tr = DeviceAIRL(demonstrations=demos, demo_batch_size=demo_batch or 2048, gen_replay_buffer_capacity=cap,
+                        n_disc_updates_per_round=n_disc or 16, venv=venv, gen_algo=learner, reward_net=rn,
+                        custom_logger=logger)
     return tr
 
 
 def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_000, seed: int = 0, n_eval: int = 50,
-        eval_every: Optional[int] = None, device: Any = "cuda", verbose: bool = False, cap: int = 512) -> Dict[str, Any]:
+        eval_every: Optional[int] = None, device: Any = "cuda", verbose: bool = False, cap: int = 512,
+        trainer_kwargs: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
     """Train ``algo`` (``gail`` / ``airl``) on ``env`` (``cartpole`` / ``pendulum``) with expert
     demonstrations and report returns + normalised scores (before, during, after)."""
     from imitation_amd.util import logger as imit_logger
@@ -146,7 +159,7 @@ def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_00
     expert = float(np.mean([t.rews.sum() for t in demos]))
     rand = random_return(env_id, n_eval, seed)
     log = imit_logger.configure(f"/tmp/ia_quality_{os.getpid()}", format_strs=[])
-    tr = make(algo, demos, seed, device, log, cap=cap)
+    tr = make(algo, demos, seed, device, log, cap=cap, **(trainer_kwargs or {}))
 
     last: Dict[str, List[float]] = {}
 

@@ -1,6 +1,6 @@
 """Normalised imitation scores of the device engines (imitation_amd/testing/imitation_quality.py).
 
-Usage: python tools/quality_probe.py [algo:env:steps[:seed[:replay capacity]] ...]  (default: the four CartPole /
+Usage: python tools/quality_probe.py [algo:env:steps[:seed[:replay capacity[:n_disc[:demo_batch[:norm_out]]]]] ...]  (default: the four CartPole /
 Pendulum GAIL / AIRL runs). One JSON line per run on stdout (and appended to $OUT if set)."""
 import json
 import os
@@ -29,7 +29,16 @@ def main():
         algo, env, steps = parts[0], parts[1], int(parts[2])
         seed = int(parts[3]) if len(parts) > 3 else 0
         cap = int(parts[4]) if len(parts) > 4 else 512
-        res = iq.run(algo, env, total_timesteps=steps, seed=seed, eval_every=max(steps // 10, 1), verbose=True, cap=cap)
+        kw = {}
+        if len(parts) > 5 and parts[5]:  # Pendulum: n_disc[:demo_batch[:normalize_output]]
+            kw["n_disc"] = int(parts[5])
+        if len(parts) > 6 and parts[6]:
+            kw["demo_batch"] = int(parts[6])
+        if len(parts) > 7 and parts[7]:
+            kw["normalize_output"] = parts[7] == "1"
+        res = iq.run(algo, env, total_timesteps=steps, seed=seed, eval_every=max(steps // 10, 1), verbose=True, cap=cap,
+                     trainer_kwargs=kw or None)
+        res["trainer_kwargs"] = kw
         line = json.dumps(res)
         print(line, flush=True)
         if os.environ.get("OUT"):
