@@ -323,6 +323,19 @@ class Fragmenter(abc.ABC):
         """Sample ``num_pairs`` fragment pairs of length ``fragment_length``."""
 
 
+def _fragment(traj: TrajectoryWithRew, start: int, end: int, terminal: bool) -> TrajectoryWithRew:
+    """``traj[start:end]`` as a TrajectoryWithRew without re-running the dataclass validation:
+    slices of a validated trajectory with ``0 <= start < end <= len(traj)`` are valid by
+    construction (obs one longer than acts / rews / infos)."""
+    frag = object.__new__(TrajectoryWithRew)
+    object.__setattr__(frag, "obs", traj.obs[start: end + 1])
+    object.__setattr__(frag, "acts", traj.acts[start:end])
+    object.__setattr__(frag, "infos", traj.infos[start:end] if traj.infos is not None else None)
+    object.__setattr__(frag, "terminal", terminal)
+    object.__setattr__(frag, "rews", traj.rews[start:end])
+    return frag
+
+
 class RandomFragmenter(Fragmenter):
     """Fragments sampled uniformly (trajectories weighted by length), with replacement."""
 
@@ -351,14 +364,18 @@ class RandomFragmenter(Fragmenter):
                              "are likely to appear multiple times.")
         fragments = []
         p = weights / weights.sum()
+        # ``rng.choice(len, p=p)`` draws exactly this: one ``random()`` double searched in the
+        # normalised CDF (numpy Generator.choice) -- same index, same RNG stream, without
+        # choice's per-call validation and cumsum (~17 of the ~28 us per fragment; DRLHP samples
+        # ~2K fragments per iteration)
+        cdf = p.cumsum()
+        cdf /= cdf[-1]
         for _ in range(2 * num_pairs):
-            traj = trajectories[int(self.rng.choice(len(trajectories), p=p))]
+            traj = trajectories[int(cdf.searchsorted(self.rng.random(), side="right"))]
             n = len(traj)
             start = int(self.rng.integers(0, n - fragment_length, endpoint=True))
             end = start + fragment_length
-            fragments.append(TrajectoryWithRew(obs=traj.obs[start: end + 1], acts=traj.acts[start:end],
-                                               infos=traj.infos[start:end] if traj.infos is not None else None,
-                                               rews=traj.rews[start:end], terminal=(end == n) and traj.terminal))
+            fragments.append(_fragment(traj, start, end, (end == n) and traj.terminal))
         it = iter(fragments)
         return list(zip(it, it))
 

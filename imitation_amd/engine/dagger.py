@@ -26,6 +26,7 @@ disk before BC re-reads everything. Here one round is:
 from __future__ import annotations
 
 import os
+import collections
 import queue
 import threading
 import time
@@ -467,6 +468,7 @@ class DeviceDAggerCollector:
         # owners that do: SimpleDAggerTrainer; IMITATION_AMD_DAGGER_ASYNC_FRAMES=0 disables
         self.async_frames = False
         self.last_landing: Optional[FrameLanding] = None
+        self.timing: Dict[str, float] = collections.defaultdict(float)  # host seconds per collect() section
         self._copy_stream: Optional[th.cuda.Stream] = None
 
     # -------------------------------------------------------------- device steps
@@ -573,6 +575,8 @@ class DeviceDAggerCollector:
     def collect(self, beta: float, *, min_timesteps: int, min_episodes: int) -> List[types.TrajectoryWithRew]:
         """One round with the reference's ``generate_trajectories`` stopping rule."""
         dev, N, K = self.device, self.N, self.chunk
+        tm = self.timing
+        t_a = time.perf_counter()
         self._beta.fill_(float(beta))
         if self.cnn:
             for actor in self._actors:
@@ -610,6 +614,8 @@ class DeviceDAggerCollector:
                 break
         t_base = i * K  # chunks whose steps count (the speculative next one is discarded)
         self.steps_collected = t_base * N
+        t_b = time.perf_counter()
+        tm["loop"] += t_b - t_a
         obs_all, term_all, acts_all, rew_all = (self._rec[k] for k in ("obs", "term_obs", "acts", "rew"))  # [T, N, ...]
         # flat row indices (t * N + n) of every finished episode, in finishing order
         rows = np.concatenate([np.arange(s, e + 1) * N + n for (n, s, e) in finished]) if finished else np.zeros(0, np.int64)
@@ -638,8 +644,12 @@ class DeviceDAggerCollector:
             self.last_landing = FrameLanding(h_obs, with_term, self._copy_stream)
         else:
             th.from_numpy(h_obs).copy_(with_term)
+        t_c = time.perf_counter()
+        tm["tail_gather"] += t_c - t_b
         h_acts = self.last_acts.cpu().numpy()
         h_rew = flat(rew_all).index_select(0, ridx).float().cpu().numpy()
+        t_d = time.perf_counter()
+        tm["tail_d2h_sync"] += t_d - t_c
         trajs: List[types.TrajectoryWithRew] = []
         off = 0
         for j, (n, s, e) in enumerate(finished):
@@ -647,7 +657,10 @@ class DeviceDAggerCollector:
             trajs.append(types.TrajectoryWithRew(obs=h_obs[obs_off[j] : obs_off[j + 1]], acts=h_acts[off : off + L],
                                                  infos=None, terminal=True, rews=h_rew[off : off + L]))
             off += L
+        t_e = time.perf_counter()
         self.sync_env_to_host()
+        tm["tail_trajs"] += t_e - t_d
+        tm["sync_env"] += time.perf_counter() - t_e
         return trajs
 
     # -------------------------------------------------------------- rollout stats

@@ -618,3 +618,26 @@ def test_active_selection_raises_error_when_initialized_without_an_ensemble(pref
     with pytest.raises(ValueError, match=r"PreferenceModel not wrapped over an ensemble.*"):
         pc.ActiveSelectionFragmenter(preference_model=preference_model, base_fragmenter=random_fragmenter,
                                      fragment_sample_factor=2, uncertainty_on="logit")
+
+
+def test_random_fragmenter_draws_as_rng_choice():
+    """The fragmenter's inverse-CDF draw consumes the RNG exactly as ``rng.choice(n, p=p)`` (the
+    reference's call): same fragments, same order, validated-slice contents and terminal flags."""
+    from imitation_amd.algorithms.preference_comparisons import RandomFragmenter
+
+    rng = np.random.default_rng(0)
+    trajs = [
+        types.TrajectoryWithRew(obs=rng.standard_normal((L + 1, 3)).astype(np.float32),
+                                acts=rng.standard_normal((L, 2)).astype(np.float32), infos=None,
+                                terminal=bool(i % 2), rews=rng.standard_normal(L).astype(np.float32))
+        for i, L in enumerate(rng.integers(50, 400, size=40))
+    ]
+    frags = [f for pair in RandomFragmenter(np.random.default_rng(7), warning_threshold=0)(trajs, 50, 300) for f in pair]
+    ref_rng = np.random.default_rng(7)
+    weights = np.array([len(t) for t in trajs], dtype=np.float64)
+    for f in frags:
+        t = trajs[int(ref_rng.choice(len(trajs), p=weights / weights.sum()))]
+        s = int(ref_rng.integers(0, len(t) - 50, endpoint=True))
+        want = types.TrajectoryWithRew(obs=t.obs[s:s + 51], acts=t.acts[s:s + 50], infos=None, rews=t.rews[s:s + 50],
+                                       terminal=(s + 50 == len(t)) and t.terminal)
+        assert f == want and f.terminal == want.terminal and len(f) == 50

@@ -61,6 +61,8 @@ def main():
         round_()
     th.cuda.synchronize()
     acc.clear()
+    if getattr(tr, "_device_collector", None) is not None:
+        tr._device_collector.timing.clear()
     pr = cProfile.Profile() if args.profile else None
     t0 = time.perf_counter()
     n_steps = 0
@@ -82,6 +84,9 @@ def main():
     acc["demo_flush_after"] = (time.perf_counter() - t2) * args.rounds
     out = dict(rounds=args.rounds, ms_per_round=1e3 * wall / args.rounds, env_steps_per_s=n_steps / wall,
                phases_ms_per_round={k: 1e3 * v / args.rounds for k, v in acc.items()}, per_round=per_round)
+    col = getattr(tr, "_device_collector", None)
+    if col is not None:
+        out["collect_sections_ms_per_round"] = {k: round(1e3 * v / args.rounds, 2) for k, v in col.timing.items()}
     print(json.dumps(out), flush=True)
     if pr:
         s = io.StringIO()
