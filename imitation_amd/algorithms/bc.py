@@ -592,24 +592,34 @@ class _DeviceEpochRunner:
             # thread + side stream, on a snapshot of the policy as of that batch); its log_batch
             # is written when they are in -- before the next logged batch and the epoch's end
             pending = None
-            while done < steps:
-                nxt = -(-(batch_num + done) // log_interval) * log_interval  # next logged batch
-                j = nxt - batch_num  # its index in this epoch
-                if j >= steps:
-                    self._run(steps - done)
-                    break
-                self._run(j + 1 - done)
-                if pending is not None:
-                    pending[0].result()
-                    pending[1]()
-                m = BCTrainingMetrics(**bc_cnn.metrics_fields(self.all[j]))
-                if self.graphs is None and done < steps:
-                    # capture the step graphs now: no capture may run while the statistics'
-                    # worker thread is stepping the envs
-                    self._capture()
-                fut = compute_rollout_stats.start(t.policy, t.rng)
-                pending = (fut, (lambda f=fut, nb_=nxt, mm=m: t._bc_logger.log_batch(nb_, B, (nb_ + 1) * B, mm, f.result())))
-                done = j + 1
+            try:
+                while done < steps:
+                    nxt = -(-(batch_num + done) // log_interval) * log_interval  # next logged batch
+                    j = nxt - batch_num  # its index in this epoch
+                    if j >= steps:
+                        self._run(steps - done)
+                        break
+                    self._run(j + 1 - done)
+                    if pending is not None:
+                        p_, pending = pending, None
+                        p_[0].result()
+                        p_[1]()
+                    m = BCTrainingMetrics(**bc_cnn.metrics_fields(self.all[j]))
+                    if self.graphs is None and done < steps:
+                        # capture the step graphs now: no capture may run while the statistics'
+                        # worker thread is stepping the envs
+                        self._capture()
+                    fut = compute_rollout_stats.start(t.policy, t.rng)
+                    pending = (fut, (lambda f=fut, nb_=nxt, mm=m: t._bc_logger.log_batch(nb_, B, (nb_ + 1) * B, mm,
+                                                                                        f.result())))
+                    done = j + 1
+            except BaseException:
+                if pending is not None:  # hand the envs back before unwinding
+                    try:
+                        pending[0].result()
+                    except BaseException:  # noqa: BLE001 -- the original error wins
+                        pass
+                raise
             if pending is not None:
                 pending[1]()
             batch_num += steps

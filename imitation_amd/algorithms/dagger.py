@@ -558,6 +558,13 @@ class SimpleDAggerTrainer(DAggerTrainer):
     def train(self, total_timesteps: int, *, rollout_round_min_episodes: int = 3, rollout_round_min_timesteps: int = 500,
               bc_train_kwargs: Optional[dict] = None) -> None:
         """Run rounds until ``total_timesteps`` env steps (all ranks) have been collected."""
+        try:
+            self._train_rounds(total_timesteps, rollout_round_min_episodes, rollout_round_min_timesteps, bc_train_kwargs)
+        finally:
+            self.land_frames()  # the trajectories handed out are complete when train() returns (or raises)
+
+    def _train_rounds(self, total_timesteps: int, rollout_round_min_episodes: int, rollout_round_min_timesteps: int,
+                      bc_train_kwargs: Optional[dict]) -> None:
         collected = 0
         local = 0
         rounds = 0
@@ -579,6 +586,5 @@ class SimpleDAggerTrainer(DAggerTrainer):
             lg.record("dagger/round_timestep_count", n_steps)
             self.extend_and_update(bc_train_kwargs)
             rounds += 1
-        self.land_frames()  # the trajectories handed out are complete when train() returns
         self.last_train_timesteps = collected  # all ranks
         self.last_train_timesteps_local = local
