@@ -336,6 +336,32 @@ def _fragment(traj: TrajectoryWithRew, start: int, end: int, terminal: bool) -> 
     return frag
 
 
+def _batched_discounted_sums(fragment_pairs, gamma: float) -> Optional[Tuple[np.ndarray, np.ndarray]]:
+    """``rollout.discounted_sum`` (numpy ``polyval``'s Horner loop, in the rewards' dtype) of every
+    fragment at once, when they all have the same length and 1-D rewards of one dtype: the same
+    operations per fragment, so the same bits, without ~2K Python Horner loops (DRLHP labels ~2K
+    fragments per iteration; the per-fragment loop cost ~50 ms). None when not applicable."""
+    if not fragment_pairs:
+        return None
+    frags = [f for pair in fragment_pairs for f in pair]
+    L = len(frags[0].rews)
+    dt = frags[0].rews.dtype
+    if L == 0 or any(f.rews.ndim != 1 or len(f.rews) != L or f.rews.dtype != dt for f in frags):
+        return None
+    c = np.stack([f.rews for f in frags])  # [2P, L]
+    if c.dtype.char in "?bBhHiIlLqQpP":
+        c = c + 0.0
+    if gamma == 1.0:
+        out = c.sum(axis=1)
+    else:
+        acc = c[:, -1] + gamma * 0
+        for i in range(2, L + 1):
+            acc = c[:, -i] + acc * gamma
+        out = acc
+    out = np.asarray(out, dtype=np.float32)
+    return out[0::2].copy(), out[1::2].copy()
+
+
 class RandomFragmenter(Fragmenter):
     """Fragments sampled uniformly (trajectories weighted by length), with replacement."""
 
@@ -473,6 +499,9 @@ class SyntheticGatherer(PreferenceGatherer):
         return model_probs
 
     def _reward_sums(self, fragment_pairs) -> Tuple[np.ndarray, np.ndarray]:
+        fast = _batched_discounted_sums(fragment_pairs, self.discount_factor)
+        if fast is not None:
+            return fast
         r1, r2 = zip(*[(rollout.discounted_sum(f1.rews, self.discount_factor),
                         rollout.discounted_sum(f2.rews, self.discount_factor)) for f1, f2 in fragment_pairs])
         return np.array(r1, dtype=np.float32), np.array(r2, dtype=np.float32)

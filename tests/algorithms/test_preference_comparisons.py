@@ -641,3 +641,24 @@ def test_random_fragmenter_draws_as_rng_choice():
         want = types.TrajectoryWithRew(obs=t.obs[s:s + 51], acts=t.acts[s:s + 50], infos=None, rews=t.rews[s:s + 50],
                                        terminal=(s + 50 == len(t)) and t.terminal)
         assert f == want and f.terminal == want.terminal and len(f) == 50
+
+
+@pytest.mark.parametrize("gamma", [1.0, 0.99, 0.9])
+def test_synthetic_gatherer_batched_returns_are_bitwise_the_per_fragment_sums(gamma):
+    """The batched Horner evaluation over equal-length fragments == ``rollout.discounted_sum``
+    (numpy ``polyval``) fragment by fragment, bit for bit; mixed lengths take the per-fragment path."""
+    from imitation_amd.algorithms.preference_comparisons import _batched_discounted_sums
+    from imitation_amd.data import rollout
+
+    rng = np.random.default_rng(3)
+
+    def frag(L):
+        return types.TrajectoryWithRew(obs=np.zeros((L + 1, 2), np.float32), acts=np.zeros((L, 1), np.float32), infos=None,
+                                       terminal=False, rews=(rng.standard_normal(L) * 7).astype(np.float32))
+
+    pairs = [(frag(40), frag(40)) for _ in range(64)]
+    r1, r2 = _batched_discounted_sums(pairs, gamma)
+    want1 = np.array([rollout.discounted_sum(a.rews, gamma) for a, _ in pairs], np.float32)
+    want2 = np.array([rollout.discounted_sum(b.rews, gamma) for _, b in pairs], np.float32)
+    assert np.array_equal(r1, want1) and np.array_equal(r2, want2)
+    assert _batched_discounted_sums([(frag(40), frag(41))], gamma) is None
