@@ -71,10 +71,11 @@ class _Timed:
         import torch as th
 
         th.cuda.synchronize()
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         out = self.fn(*a, **k)
         th.cuda.synchronize()
         self.acc[self.key] += time.perf_counter() - t0
+        self.acc[self.key + "_thread_cpu"] += time.thread_time() - c0  # (wall >> cpu: waiting, e.g. for the GIL)
         return out
 
     def __getattr__(self, name):
