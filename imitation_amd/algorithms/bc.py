@@ -547,16 +547,32 @@ class _DeviceEpochRunner:
         self.graphs = None  # captured by the next _run, after the eager warm-up step
 
     def _capture(self) -> None:
+        """The 1- and K-step graphs. IMITATION_AMD_BC_GRAPH_PAIR=1 captures two instances of each and
+        alternates them (an A/B knob: a relaunch of an exec whose previous launch is still running
+        waits for it on the host; round 5 measured the pair SLOWER on DAgger-Pong, 176-186 vs
+        146-164 ms per round, `profiles/r5_dagger.md`)."""
         self.graphs = {}
         side = th.cuda.Stream()
         side.wait_stream(th.cuda.current_stream())
+        import os
+
+        copies = 2 if os.environ.get("IMITATION_AMD_BC_GRAPH_PAIR", "0") == "1" else 1
         for k in (1, self.K):
-            g = th.cuda.CUDAGraph()
-            with graphs.capture(g, stream=side):
-                for _ in range(k):
-                    self._one_step()
-            self.graphs[k] = g
+            gs = []
+            for _ in range(copies):
+                g = th.cuda.CUDAGraph()
+                with graphs.capture(g, stream=side):
+                    for _ in range(k):
+                        self._one_step()
+                gs.append(g)
+            self.graphs[k] = gs
         th.cuda.current_stream().wait_stream(side)
+        self._turn = 0
+
+    def _replay(self, k: int) -> None:
+        gs = self.graphs[k]
+        gs[self._turn % len(gs)].replay()
+        self._turn += 1
 
     def _run(self, steps: int) -> None:
         if steps > 0 and not getattr(self, "_warm", False):
@@ -568,9 +584,9 @@ class _DeviceEpochRunner:
         if steps > 0 and self.graphs is None:
             self._capture()
         for _ in range(steps // self.K):
-            self.graphs[self.K].replay()
+            self._replay(self.K)
         for _ in range(steps % self.K):
-            self.graphs[1].replay()
+            self._replay(1)
 
     def train(self, n_epochs, n_batches, on_epoch_end, log_interval: int, compute_rollout_stats) -> None:
         t = self.trainer
