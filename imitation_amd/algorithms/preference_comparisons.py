@@ -842,11 +842,22 @@ class BasicRewardTrainer(RewardTrainer):
             fm.plan.epoch(orders, P, cursor, ep, allm, merge)
         th.cuda.current_stream().wait_stream(side)
         if epochs > 1:
-            graph = th.cuda.CUDAGraph()
-            with graphs.capture(graph):
-                fm.plan.epoch(orders, P, cursor, ep, allm, merge)
-            for _ in range(epochs - 1):
-                graph.replay()
+            import os
+
+            # a few epochs (the per-iteration schedule) launch eagerly: one C++ call per epoch
+            # issues its n_mb x 4 kernels faster than the device runs them, and a capture would
+            # cost a device sync + cache flush + instantiate every iteration (the dataset grows,
+            # so the graph cannot be kept); long schedules (the initial x200 epochs) replay a graph
+            min_ep = int(os.environ.get("IMITATION_AMD_PREF_EPOCH_GRAPH_MIN", "8"))
+            if epochs - 1 < min_ep:
+                for _ in range(epochs - 1):
+                    fm.plan.epoch(orders, P, cursor, ep, allm, merge)
+            else:
+                graph = th.cuda.CUDAGraph()
+                with graphs.capture(graph):
+                    fm.plan.epoch(orders, P, cursor, ep, allm, merge)
+                for _ in range(epochs - 1):
+                    graph.replay()
         vals = allm[:, :, : fm.n_metrics].cpu().tolist()
         names = ["loss", "accuracy", "gt_reward_loss"]
         for epoch_num in range(epochs):
