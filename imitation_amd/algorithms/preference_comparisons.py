@@ -49,6 +49,7 @@ from imitation_amd.regularization import regularizers
 from imitation_amd.rewards import reward_function, reward_nets, reward_wrapper
 from imitation_amd.rl.base import check_for_correct_spaces
 from imitation_amd.util import logger as imit_logger
+from imitation_amd.utils import profiling
 from imitation_amd.util import networks, util
 
 try:  # progress bars are optional
@@ -1365,11 +1366,13 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
         for i, num_pairs in enumerate(schedule):
             num_steps = math.ceil(self.transition_oversampling * 2 * num_pairs * self.fragment_length)
             self.logger.log(f"Collecting {2 * num_pairs} fragments ({num_steps} transitions)")
-            trajectories = self.trajectory_generator.sample(num_steps)
+            with profiling.range("pref/sample"):
+                trajectories = self.trajectory_generator.sample(num_steps)
             self._check_fixed_horizon(len(t) for t in trajectories if t.terminal)
             self.logger.log("Creating fragment pairs")
-            fragments = self.fragmenter(trajectories, self.fragment_length, num_pairs)
-            with self.logger.accumulate_means("preferences"):
+            with profiling.range("pref/fragment"):
+                fragments = self.fragmenter(trajectories, self.fragment_length, num_pairs)
+            with self.logger.accumulate_means("preferences"), profiling.range("pref/gather"):
                 self.logger.log("Gathering preferences")
                 preferences = self.preference_gatherer(fragments)
             if pdist.world_size() > 1:
@@ -1379,7 +1382,8 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
             self.dataset.push(fragments, preferences)
             self.logger.log(f"Dataset now contains {len(self.dataset)} comparisons")
             epoch_multiplier = self.initial_epoch_multiplier if i == 0 else 1.0
-            self.reward_trainer.train(self.dataset, epoch_multiplier=epoch_multiplier)
+            with profiling.range("pref/reward_train"):
+                self.reward_trainer.train(self.dataset, epoch_multiplier=epoch_multiplier)
             base_key = self.logger.get_accumulate_prefixes() + "reward/final/train"
             assert f"{base_key}/loss" in self.logger.name_to_value
             assert f"{base_key}/accuracy" in self.logger.name_to_value
@@ -1388,7 +1392,8 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
             steps = timesteps_per_iteration + (extra_timesteps if i == self.num_iterations - 1 else 0)
             with self.logger.accumulate_means("agent"):
                 self.logger.log(f"Training agent for {steps} timesteps")
-                self.trajectory_generator.train(steps=steps)
+                with profiling.range("pref/agent_train"):
+                    self.trajectory_generator.train(steps=steps)
             # the last iteration's collectives are checked blocking: a NaN-poisoned one-shot
             # all-reduce there must raise, not return NaN weights
             pdist.check_comm("preference iteration", blocking=i == len(schedule) - 1)
