@@ -488,7 +488,7 @@ class _DeviceEpochRunner:
     ``n_batches`` cut-off (reference ``bc.py:443-510``). Same batches, kernels and order as the
     per-minibatch loop, so the result is bitwise the eager-graph path's."""
 
-    K = 16  # minibatch steps per graph replay
+    K = 16  # default largest graph (minibatch steps per replay); IMITATION_AMD_BC_GRAPH_K overrides
 
     def __init__(self, trainer: "_BCBase", loader, graphed):
         self.trainer, self.loader, self.graphed = trainer, loader, graphed
@@ -501,6 +501,11 @@ class _DeviceEpochRunner:
         opt = trainer.optimizer
         self._fold = (hasattr(opt, "graph_epoch_step_ok") and opt.graph_epoch_step_ok()
                       and os.environ.get("IMITATION_AMD_BC_FOLD_LAUNCHES", "1") != "0")
+        kmax = max(1, int(os.environ.get("IMITATION_AMD_BC_GRAPH_K", self.K)))
+        # graph sizes: the largest, then powers of two below it. A run of n steps replays the
+        # largest as often as it fits and each smaller one at most once, so the remainder is
+        # never a chain of relaunches of one exec (each would wait on the host for the last)
+        self._sizes = [kmax] + [1 << i for i in range(kmax.bit_length() - 1, -1, -1) if (1 << i) < kmax]
 
     def _fused(self):
         t = self.trainer
@@ -547,7 +552,7 @@ class _DeviceEpochRunner:
         self.graphs = None  # captured by the next _run, after the eager warm-up step
 
     def _capture(self) -> None:
-        """The 1- and K-step graphs. IMITATION_AMD_BC_GRAPH_PAIR=1 captures two instances of each and
+        """The step graphs of every size in ``_sizes``. IMITATION_AMD_BC_GRAPH_PAIR=1 captures two instances of each and
         alternates them (an A/B knob: a relaunch of an exec whose previous launch is still running
         waits for it on the host; round 5 measured the pair SLOWER on DAgger-Pong, 176-186 vs
         146-164 ms per round, `profiles/r5_dagger.md`)."""
@@ -557,7 +562,7 @@ class _DeviceEpochRunner:
         import os
 
         copies = 2 if os.environ.get("IMITATION_AMD_BC_GRAPH_PAIR", "0") == "1" else 1
-        for k in (1, self.K):
+        for k in self._sizes:
             gs = []
             for _ in range(copies):
                 g = th.cuda.CUDAGraph()
@@ -583,10 +588,10 @@ class _DeviceEpochRunner:
             steps -= 1
         if steps > 0 and self.graphs is None:
             self._capture()
-        for _ in range(steps // self.K):
-            self._replay(self.K)
-        for _ in range(steps % self.K):
-            self._replay(1)
+        for k in self._sizes:
+            while steps >= k:
+                self._replay(k)
+                steps -= k
 
     def train(self, n_epochs, n_batches, on_epoch_end, log_interval: int, compute_rollout_stats) -> None:
         t = self.trainer

@@ -202,12 +202,14 @@ def test_device_rollout_stats_match_host_keys(tmp_path):
 
 
 @gpu
-@pytest.mark.parametrize("n_epochs,n_batches,log_interval", [(2, None, 3), (None, 11, 4), (None, 7, 500)])
-def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batches, log_interval):
+@pytest.mark.parametrize("n_epochs,n_batches,log_interval,kmax",
+                         [(2, None, 3, "16"), (None, 11, 4, "5"), (None, 7, 500, "16"), (3, None, 500, "3")])
+def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batches, log_interval, kmax):
     """BC over a device demonstration aggregate (DAgger's device collector) with whole runs of
-    minibatches per HIP-graph replay (algorithms/bc.py ``_DeviceEpochRunner``): the same batches,
-    kernels and order as the per-minibatch graphed loop, so the parameters, Adam state and every
-    logged metric are bitwise equal; the epoch-end callbacks and the n_batches cut-off match."""
+    minibatches per HIP-graph replay (algorithms/bc.py ``_DeviceEpochRunner``, graph sizes kmax then
+    powers of two below it): the same batches, kernels and order as the per-minibatch graphed loop,
+    so the parameters, Adam state and every logged metric are bitwise equal; the epoch-end
+    callbacks and the n_batches cut-off match."""
     from imitation_amd.algorithms import bc
     from imitation_amd.engine.dagger import DeviceDemoAggregate, DeviceTransitionsLoader
     from imitation_amd.rl.policies import ActorCriticCnnPolicy
@@ -220,6 +222,7 @@ def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batc
     obs = th.randint(0, 256, (n_rows, 84, 84, 4), generator=g, device="cuda", dtype=th.int64).to(th.uint8)
     acts = th.randint(0, int(venv.action_space.n), (n_rows,), generator=g, device="cuda")
     runs = []
+    monkeypatch.setenv("IMITATION_AMD_BC_GRAPH_K", kmax)
     for mode in ("0", "1"):
         monkeypatch.setenv("IMITATION_AMD_BC_EPOCH_GRAPH", mode)
         th.manual_seed(11)

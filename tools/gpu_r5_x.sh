@@ -12,7 +12,7 @@ run() {  # name, round range, nth, command...
   rm -rf /tmp/r5_x_$name
   return $rc
 }
-run gail ppo/update 8 python3 bench.py --steps 20 --warmup 3 &&
+run gail ppo/update 12 python3 bench.py --steps 30 --warmup 3 &&
 run airl ppo/update 4 python3 benchmarking/bench_configs.py --configs airl_hopper --steps 6 --warmup 2 &&
 run drlhp pref/agent_train 1 python3 benchmarking/bench_configs.py --configs preference_walker2d --steps 2 --warmup 1 &&
 run dagger dagger/collect 2 python3 benchmarking/bench_configs.py --configs dagger_pong --steps 3 --warmup 1

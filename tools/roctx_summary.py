@@ -18,7 +18,9 @@ def main():
     c = sqlite3.connect(args.db)
     rcols = [r[1] for r in c.execute("pragma table_info(regions)")]
     cat = "category" if "category" in rcols else "''"
-    regions = c.execute(f"select name, start, end, {cat} from regions").fetchall()
+    # a ROCTX range's region name is the API (roctxThreadRangeA...), its text is extdata's message
+    msg = "coalesce(json_extract(extdata, '$.message'), name)" if "extdata" in rcols else "name"
+    regions = c.execute(f"select {msg}, start, end, {cat} from regions").fetchall()
     markers = [r for r in regions if not str(r[0]).startswith("hip") and not str(r[0]).startswith("__hip")]
     print(f"{len(markers)} ROCTX ranges, categories {collections.Counter(r[3] for r in markers).most_common(4)}\n")
     agg = collections.defaultdict(lambda: [0, 0.0])
