@@ -33,6 +33,7 @@ BufferingWrapper's (obs incl. terminal obs, clipped env actions, env rewards,
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -273,13 +274,27 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
         target = algo.num_timesteps + n_rounds * per_round
         algo._total_timesteps = max(algo._total_timesteps or 0, target)
         self._fps_mark = (time.perf_counter(), algo.num_timesteps)
+        logged = True
+        defer = os.environ.get("IMITATION_AMD_PREF_DEFER_LOG", "1") != "0"
         for _ in range(n_rounds):
             self._rollout()
             ready = self._stage()
+            if not logged:
+                # the previous round's records (its PPO statistics wait for its update) are
+                # written only now, with this round's rollout already queued behind that update:
+                # the GPU does not idle while the host logs. Same values, steps and order as
+                # logging at the end of each round (the PPO statistics are staged copies; the
+                # wrapped-return deque does not change until this round's _accumulate).
+                self._log_round()
             algo.num_timesteps += per_round
             self._ppo_update()  # PPO kernel runs while the host cuts the episodes
             ready.synchronize()
             self._accumulate(track_wrapped=True)
+            logged = False
+            if not defer:
+                self._log_round()
+                logged = True
+        if not logged:
             self._log_round()
 
     def _log_round(self) -> None:

@@ -316,3 +316,33 @@ def test_device_agent_scores_ensembles_in_one_grouped_launch():
     np.testing.assert_allclose(got, want, rtol=3e-2, atol=3e-2 * float(np.abs(want).max()))
     tr.train(T * N)
     assert all(th.isfinite(p).all() for p in agent.policy.parameters())
+
+
+@gpu
+def test_device_agent_deferred_round_logs_match_per_round_logs(monkeypatch):
+    """The agent writes round r's records after queueing round r + 1's rollout
+    (IMITATION_AMD_PREF_DEFER_LOG, default on): the same dumps (steps, keys, values apart from the
+    wall-clock keys) as logging at the end of each round, and the same final parameters."""
+    runs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IMITATION_AMD_PREF_DEFER_LOG", mode)
+        tr, venv, agent, rn = _agent(seed=3)
+        dumps = []
+        orig = tr.logger.dump
+
+        def dump(step=0, _lg=tr.logger, _orig=orig, _rec=dumps):
+            _rec.append((step, {k: v for k, v in _lg.name_to_value.items() if not k.startswith("time/")}))
+            _orig(step)
+
+        tr.logger.dump = dump
+        tr.train(4 * tr.T * tr.N)
+        th.cuda.synchronize()
+        runs.append((dumps, [p.detach().clone() for p in agent.policy.parameters()]))
+    (d0, p0), (d1, p1) = runs
+    assert len(d0) == len(d1) == 4
+    assert [s for s, _ in d0] == [s for s, _ in d1]
+    for (_, a), (_, b) in zip(d0, d1):
+        assert a.keys() == b.keys() and "train/value_loss" in a
+        for k in a:
+            assert a[k] == b[k] or (np.isnan(a[k]) and np.isnan(b[k])), k
+    assert all(th.equal(x, y) for x, y in zip(p0, p1))

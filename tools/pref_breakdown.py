@@ -47,6 +47,18 @@ def main():
     timed(tr.dataset, "push", "dataset_push")
     tr.fragmenter = _Timed(tr.fragmenter, acc, "fragment")
     tr.preference_gatherer = _Timed(tr.preference_gatherer, acc, "gather_prefs")
+    import gc
+
+    gc_t = {"start": 0.0}
+
+    def gc_cb(phase, info):  # Python's cyclic collector pauses (generation 2 grows with the dataset)
+        if phase == "start":
+            gc_t["start"] = time.perf_counter()
+        else:
+            acc[f"gc_gen{info['generation']}"] += time.perf_counter() - gc_t["start"]
+            acc[f"gc_gen{info['generation']}_n"] += 1e-3  # (reported x 1e3 / iters: collections per iter)
+
+    gc.callbacks.append(gc_cb)
     it = tr.train_iter(b.extras["total_timesteps"], total_comparisons=args.comparisons)
     next(it)  # warm-up: the initial iteration
     th.cuda.synchronize()
@@ -59,7 +71,8 @@ def main():
     out = dict(iters=args.iters, ms_per_iter=1e3 * wall / args.iters,
                env_steps_per_s=args.iters * b.env_steps_per_round / wall,
                phases_ms_per_iter={k: round(1e3 * v / args.iters, 2) for k, v in acc.items()})
-    out["phases_ms_per_iter"]["other"] = round(out["ms_per_iter"] - sum(out["phases_ms_per_iter"].values()), 2)
+    main = [v for k, v in out["phases_ms_per_iter"].items() if not (k.startswith("gc_") or k.endswith("_thread_cpu"))]
+    out["phases_ms_per_iter"]["other"] = round(out["ms_per_iter"] - sum(main), 2)
     print(json.dumps(out), flush=True)
 
 
