@@ -31,6 +31,7 @@ import numpy as np
 import torch as th
 from torch.nn import functional as F
 
+from imitation_amd.utils import gcfreeze
 from imitation_amd.algorithms import base
 from imitation_amd.data import buffer, rollout, types, wrappers
 from imitation_amd.envs import spaces
@@ -295,6 +296,7 @@ class AdversarialTrainer(base.DemonstrationAlgorithm[types.Transitions]):
         gen_samples = rollout.flatten_trajectories_with_rew(gen_trajs)
         self._gen_replay_buffer.store(gen_samples)
 
+    @gcfreeze.during
     def train(self, total_timesteps: int, callback: Optional[Callable[[int], None]] = None) -> None:
         """Alternate generator and discriminator training for ``total_timesteps // gen_train_timesteps`` rounds."""
         n_rounds = total_timesteps // self.gen_train_timesteps

@@ -35,7 +35,7 @@ from imitation_amd.policies import base as policy_base
 from imitation_amd.rl import torch_layers
 from imitation_amd.rl.policies import ActorCriticPolicy, get_device
 from imitation_amd.util import logger as imit_logger
-from imitation_amd.utils import graphs
+from imitation_amd.utils import gcfreeze, graphs
 from imitation_amd.util import util
 
 
@@ -345,6 +345,7 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
         if self._grad_bucket is not None:
             self._grad_bucket.zero()
 
+    @gcfreeze.during
     def train(self, *, n_epochs: Optional[int] = None, n_batches: Optional[int] = None,
               on_epoch_end: Optional[Callable[[], None]] = None, on_batch_end: Optional[Callable[[], None]] = None,
               log_interval: int = 500, log_rollouts_venv=None, log_rollouts_n_episodes: int = 5,

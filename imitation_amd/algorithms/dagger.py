@@ -35,7 +35,7 @@ from typing import Any, Callable, Dict, List, Mapping, Optional, Sequence, Tuple
 import numpy as np
 import torch as th
 
-from imitation_amd.utils import profiling
+from imitation_amd.utils import gcfreeze, profiling
 
 from imitation_amd.algorithms import base, bc
 from imitation_amd.data import rollout, serialize, types
@@ -557,6 +557,7 @@ class SimpleDAggerTrainer(DAggerTrainer):
             self._writer.flush()  # every demo file of the finished rounds is on disk
         return super().save_trainer()
 
+    @gcfreeze.during
     def train(self, total_timesteps: int, *, rollout_round_min_episodes: int = 3, rollout_round_min_timesteps: int = 500,
               bc_train_kwargs: Optional[dict] = None) -> None:
         """Run rounds until ``total_timesteps`` env steps (all ranks) have been collected."""

@@ -49,7 +49,7 @@ from imitation_amd.regularization import regularizers
 from imitation_amd.rewards import reward_function, reward_nets, reward_wrapper
 from imitation_amd.rl.base import check_for_correct_spaces
 from imitation_amd.util import logger as imit_logger
-from imitation_amd.utils import profiling
+from imitation_amd.utils import gcfreeze, profiling
 from imitation_amd.util import networks, util
 
 try:  # progress bars are optional
@@ -1353,7 +1353,12 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
     def train_iter(self, total_timesteps: int, total_comparisons: int,
                    callback: Optional[Callable[[int], None]] = None):
         """:meth:`train` as a generator: yields ``{"reward_loss", "reward_accuracy"}`` after each
-        iteration (for per-iteration timing / external control)."""
+        iteration (for per-iteration timing / external control). The heap from before the loop
+        is kept out of the garbage collector's full passes meanwhile (``utils/gcfreeze.py``)."""
+        with gcfreeze.frozen_heap():
+            yield from self._train_iter(total_timesteps, total_comparisons, callback)
+
+    def _train_iter(self, total_timesteps: int, total_comparisons: int, callback: Optional[Callable[[int], None]]):
         initial_comparisons = int(total_comparisons * self.initial_comparison_frac)
         total_comparisons -= initial_comparisons
         probs = np.vectorize(self.query_schedule)(np.linspace(0, 1, self.num_iterations))

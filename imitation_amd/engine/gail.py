@@ -61,7 +61,7 @@ from imitation_amd.rewards import reward_nets
 from imitation_amd.rl.policies import ActorCriticPolicy
 from imitation_amd.rl.ppo import PPO
 from imitation_amd.util import networks
-from imitation_amd.utils import profiling
+from imitation_amd.utils import gcfreeze, profiling
 
 
 def _unwrap_native(venv) -> Optional[NativeVecEnv]:
@@ -1337,6 +1337,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
     #: saves. False: every callback runs with the device idle, as a host-loop trainer would.
     pipeline_callbacks = True
 
+    @gcfreeze.during
     def train(self, total_timesteps: int, callback=None) -> None:
         """Rounds of device generator training + fused discriminator updates; the
         discriminator statistics of a round are fetched with one host sync and logged
