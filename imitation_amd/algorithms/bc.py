@@ -544,7 +544,9 @@ class _DeviceEpochRunner:
         if self._key == key and n <= getattr(self, "_cap", 0):
             return
         if n > getattr(self, "_cap", 0):
-            cap = max(n, 2 * getattr(self, "_cap", 0))
+            # room for every row the aggregate's storage can hold: a growing aggregate then
+            # recaptures only when its storage moves
+            cap = max(n, 2 * getattr(self, "_cap", 0), self.agg.obs.shape[0])
             self.perm = th.zeros(cap, dtype=th.int32, device=dev)
             self.all = th.zeros(cap // self.B + 1, 8, device=dev)
             self.cursor = th.zeros(1, dtype=th.int32, device=dev)
@@ -558,7 +560,9 @@ class _DeviceEpochRunner:
         waits for it on the host; round 5 measured the pair SLOWER on DAgger-Pong, 176-186 vs
         146-164 ms per round, `profiles/r5_dagger.md`)."""
         self.graphs = {}
-        side = th.cuda.Stream()
+        side = getattr(self, "_capture_stream", None)
+        if side is None:  # (creating a stream costs ~1 ms of host time)
+            side = self._capture_stream = th.cuda.Stream()
         side.wait_stream(th.cuda.current_stream())
         import os
 

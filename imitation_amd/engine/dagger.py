@@ -209,6 +209,12 @@ class DeviceDemoAggregate:
         need = self.n + k
         if self.obs is None or need > self.obs.shape[0]:
             cap = max(need, 2 * (0 if self.obs is None else self.obs.shape[0]), 1024)
+            if self.obs is None and self.device.type == "cuda":
+                # HBM is plentiful: start with room for a whole DAgger run (up to 64K rows or
+                # 2 GiB, e.g. 64K Pong frames = 1.8 GB), so the storage -- and the BC epoch
+                # graphs captured on it -- never move in a typical run
+                row = obs[0].numel() * obs.element_size() + acts[0].numel() * acts.element_size()
+                cap = max(cap, min(1 << 16, (2 << 30) // max(1, row)))
             new_obs = th.empty((cap,) + tuple(obs.shape[1:]), dtype=obs.dtype, device=self.device)
             new_acts = th.empty((cap,) + tuple(acts.shape[1:]), dtype=acts.dtype, device=self.device)
             if self.n:

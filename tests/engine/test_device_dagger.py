@@ -295,3 +295,41 @@ def test_async_rollout_stats_and_frame_landing_are_bitwise_the_inline_path(tmp_p
     for (o1, a1), (o2, a2) in zip(a["trajs"], b["trajs"]):
         np.testing.assert_array_equal(o1, o2)
         np.testing.assert_array_equal(a1, a2)
+
+
+@gpu
+def test_growing_aggregate_keeps_its_storage_and_bc_graphs():
+    """A Pong-frame aggregate on the GPU starts with room for 64K rows, so DAgger rounds append
+    without moving it, and the BC epoch runner captures its step graphs once for the whole run."""
+    from imitation_amd.algorithms import bc
+    from imitation_amd.engine.dagger import DeviceDemoAggregate, DeviceTransitionsLoader
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+    from imitation_amd.util import logger as ilog
+    from imitation_amd.util.util import make_vec_env
+
+    venv = make_vec_env("PongNoFrameskip-v4", rng=np.random.default_rng(0), n_envs=1)
+    g = th.Generator(device="cuda").manual_seed(1)
+
+    def rows(n):
+        return (th.randint(0, 256, (n, 84, 84, 4), generator=g, device="cuda", dtype=th.int64).to(th.uint8),
+                th.randint(0, int(venv.action_space.n), (n,), generator=g, device="cuda"))
+
+    agg = DeviceDemoAggregate("cuda")
+    agg.append(*rows(100), gather=False)
+    assert agg.obs.shape[0] == 1 << 16
+    ptr = agg.obs.data_ptr()
+    pol = ActorCriticCnnPolicy(venv.observation_space, venv.action_space, lambda _: 1e-3).cuda()
+    trainer = bc.BC(observation_space=venv.observation_space, action_space=venv.action_space,
+                    rng=np.random.default_rng(0), policy=pol, batch_size=32, device="cuda",
+                    custom_logger=ilog.configure(format_strs=[]))
+    captured = []
+    for k in range(3):
+        if k:
+            agg.append(*rows(150), gather=False)
+        trainer.set_demonstrations(DeviceTransitionsLoader(agg, 32, seed=k))
+        trainer.train(n_epochs=1, log_interval=10**9, progress_bar=False)
+        run = trainer._epoch_run
+        captured.append(run.graphs)
+    th.cuda.synchronize()
+    assert agg.obs.data_ptr() == ptr and len(agg) == 400
+    assert captured[1] is not None and captured[1] is captured[2]  # no recapture as the aggregate grows
