@@ -577,12 +577,27 @@ class _DeviceEpochRunner:
                 gs.append(g)
             self.graphs[k] = gs
         th.cuda.current_stream().wait_stream(side)
-        self._turn = 0
+        self._turn = {}  # per graph size: the next instance to launch
+        self._done_ev = {}
+        self._wait_prev = os.environ.get("IMITATION_AMD_BC_GRAPH_WAIT", "0") == "1"
 
     def _replay(self, k: int) -> None:
         gs = self.graphs[k]
-        gs[self._turn % len(gs)].replay()
-        self._turn += 1
+        i = self._turn.get(k, 0) % len(gs)
+        if self._wait_prev:
+            # a relaunch of an exec whose previous launch still runs blocks inside
+            # hipGraphLaunch -- and holds up the statistics thread's launches meanwhile (1.5-3 ms
+            # per launch in the round-5 API trace). Wait for that launch on its event instead,
+            # outside the runtime; with two instances the other one keeps the GPU busy.
+            ev = self._done_ev.get((k, i))
+            if ev is not None:
+                ev.synchronize()
+        gs[i].replay()
+        if self._wait_prev:
+            ev = th.cuda.Event()
+            ev.record()
+            self._done_ev[(k, i)] = ev
+        self._turn[k] = i + 1
 
     def _run(self, steps: int) -> None:
         if steps > 0 and not getattr(self, "_warm", False):
