@@ -15,6 +15,9 @@
 //             gradient. One wave per 16x16 tile, 8 loads in flight per k-batch.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+#include <cstdlib>
+
 #include "ia/mfma.h"
 #include "launchers.h"
 
@@ -89,6 +92,90 @@ __global__ __launch_bounds__(256) void fc_wgrad_kernel(const bf16* __restrict__ 
   }
 }
 
+// Channel-aligned variant: a block owns kChG whole channels, i.e. the contiguous torch columns
+// [c0 * HW, (c0 + kChG) * HW), for 64 n rows. Its X operand is then kChG consecutive NHWC
+// channels per (row, position): one 16-B load each. The 64-consecutive-column blocks above load
+// X element by element, every element from a different 128-B line (NHWC stride C): at NatureCNN
+// / batch 32 that is ~100 MB of L2 line traffic per step against ~13 MB here. 8 waves: wave w
+// owns n rows 16 (w & 3) .. + 15 and the column tiles of parity w >> 2. Same MFMA per dW element
+// (same operands, same 32-row m chunks), so dW is bitwise the other kernel's.
+constexpr int kChG = 8;          // channels per block
+constexpr int kChMaxCols = 416;  // kChG * HW bound: 26 tiles of 16 columns
+constexpr int kChTilesW = 13;    // tiles per wave (parity split)
+constexpr int kChXIt = 4;        // X loads per thread per 32-row chunk: ceil(32 * 52 / 512)
+
+__global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
+                                                          const float* __restrict__ Hout, float* __restrict__ dW,
+                                                          float* __restrict__ db, bf16* __restrict__ dZb, int M, int K,
+                                                          int NH, int C, int HW) {
+  __shared__ __attribute__((aligned(16))) bf16 zs[64][40];          // dZ^T chunk [n][m] (+8 pad)
+  __shared__ __attribute__((aligned(16))) bf16 xs[kChMaxCols][40];  // X^T chunk [column][m]
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wn = w & 3, par = w >> 2;
+  const int c0 = blockIdx.x * kChG, n0 = blockIdx.y * 64;
+  const int ncols = kChG * HW, ntiles = (ncols + 15) / 16, nx = 32 * HW;
+  const bool first = blockIdx.x == 0;
+  f32x4 acc[kChTilesW];
+#pragma unroll
+  for (int j = 0; j < kChTilesW; ++j) acc[j] = zero4();
+  for (int m0 = 0; m0 < M; m0 += 32) {
+    bf16x8 xv[kChXIt];
+#pragma unroll
+    for (int e = 0; e < kChXIt; ++e) {  // all of this thread's X loads in flight first
+      const int i = tid + 512 * e, mm = i / HW, hw = i - mm * HW, m = m0 + mm;
+      xv[e] = (i < nx && m < M) ? *reinterpret_cast<const bf16x8*>(X + (size_t)m * K + (size_t)hw * C + c0) : bf16x8{};
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {  // dZ^T: 64 n x 32 m, coalesced along n
+      const int i = tid + 512 * e, nn = i & 63, mm = i >> 6;
+      const int m = m0 + mm;
+      float z = 0.f;
+      if (m < M) {
+        const size_t o = (size_t)m * NH + n0 + nn;
+        z = Hout[o] > 0.f ? dH[o] : 0.f;
+        if (first) dZb[o] = (bf16)z;
+      }
+      zs[nn][mm] = (bf16)z;
+    }
+#pragma unroll
+    for (int e = 0; e < kChXIt; ++e) {
+      const int i = tid + 512 * e, mm = i / HW, hw = i - mm * HW;
+      if (i < nx) {
+#pragma unroll
+        for (int g = 0; g < kChG; ++g) xs[g * HW + hw][mm] = xv[e][g];
+      }
+    }
+    __syncthreads();
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&zs[wn * 16 + (l & 15)][(l >> 4) * 8]);
+#pragma unroll
+    for (int j = 0; j < kChTilesW; ++j) {
+      const int t = par + 2 * j;
+      if (t < ntiles) {  // (wave-uniform) the last tile's columns past ncols are computed, never stored
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&xs[16 * t + (l & 15)][(l >> 4) * 8]);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  float* dWb = dW + (size_t)c0 * HW;
+#pragma unroll
+  for (int j = 0; j < kChTilesW; ++j) {
+    const int col = 16 * (par + 2 * j) + (l & 15);
+    if (col < ncols) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dWb[(size_t)(n0 + wn * 16 + 4 * (l >> 4) + i) * K + col] = acc[j][i];
+    }
+  }
+  if (first && tid < 64) {  // bias gradient, fixed row order
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) {
+      const size_t o = (size_t)m * NH + n0 + tid;
+      s += Hout[o] > 0.f ? dH[o] : 0.f;
+    }
+    db[n0 + tid] = s;
+  }
+}
+
 // One wave = 16 rows x 16 NHWC columns; the n loop is issued 4 k-steps (8 loads) at a time
 // so the L2 round trips overlap (the wave reads 16 KB of Wt).
 __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
@@ -139,8 +226,15 @@ bool fc_train_ok(int M, int K, int NH, int C, int HW) {
 hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const void* Wt, float* dW, float* db, void* dX,
                        void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s) {
   if (!fc_train_ok(M, K, NH, C, HW)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / (16 * kFcCT), NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout, dW, db,
-                     static_cast<bf16*>(dZb), M, K, NH, C, HW);
+  const char* ch_env = getenv("IMITATION_AMD_FC_WGRAD_CH");  // "0": the 64-column blocks (A/B knob, read per call)
+  const bool ch_off = ch_env != nullptr && ch_env[0] == '0';
+  const bool ch = !ch_off && C % kChG == 0 && kChG * HW <= kChMaxCols && reinterpret_cast<uintptr_t>(X) % 16 == 0;
+  if (ch)
+    hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(C / kChG, NH / 64), dim3(512), 0, s, static_cast<const bf16*>(X), dH, Hout, dW,
+                       db, static_cast<bf16*>(dZb), M, K, NH, C, HW);
+  else
+    hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / (16 * kFcCT), NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout,
+                       dW, db, static_cast<bf16*>(dZb), M, K, NH, C, HW);
   if (dX) {
     const int waves = ((M + 15) / 16) * (K / 16);
     hipLaunchKernelGGL(fc_dgrad_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, static_cast<const bf16*>(dZb),

@@ -240,3 +240,26 @@ def test_fc_backward_kernel_exact_wrt_bf16_operands(M):
     wb = w.to(th.bfloat16).double().permute(0, 2, 3, 1).reshape(NH, K)     # (h, w, c) columns
     dx_ref = dz @ wb
     assert float((dx.cpu().double() - dx_ref).norm() / dx_ref.norm()) < 5e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [32, 70])
+def test_fc_wgrad_channel_blocks_bitwise_the_column_blocks(monkeypatch, M):
+    """The channel-aligned fc_wgrad blocks (16-B NHWC operand loads) give bitwise the dW / db /
+    dZ of the 64-consecutive-column blocks (same MFMA operands per element)."""
+    from imitation_amd import ops
+
+    C = ops.native()
+    g = th.Generator().manual_seed(7 + M)
+    C3, H3, W3, NH = 64, 7, 7, 512
+    x = th.randn(M, H3, W3, C3, generator=g).to(th.bfloat16).cuda().reshape(M, -1)
+    w = (th.randn(NH, C3, H3, W3, generator=g) * 0.02).cuda()
+    h = th.relu(th.randn(M, NH, generator=g)).cuda()
+    dh = th.randn(M, NH, generator=g).cuda()
+    _, wts = C.conv_pack_weights([w], [True], [True])
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IMITATION_AMD_FC_WGRAD_CH", mode)
+        out.append([t.clone() for t in C.fc_backward(x, dh, h, wts[0], C3, True)])
+    for a, b in zip(*out):
+        assert th.equal(a, b)
