@@ -515,6 +515,34 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
   if (tid < N) out[(size_t)N * K + tid] = bsum;
 }
 
+// The 4 fixed-order accumulators of a slab column (accumulator j: blocks b = j mod 4 in order,
+// the tail blocks into s0). 16 loads are issued before their adds: the slabs of a BC step have
+// ~50 blocks, and 4 loads per round trip made the sum a chain of ~13 L2 round trips.
+__device__ __forceinline__ void slab_sum4(const float* __restrict__ slab, int nblk, int len, int i, float& s0, float& s1,
+                                          float& s2, float& s3) {
+  s0 = s1 = s2 = s3 = 0.f;
+  int b = 0;
+  for (; b + 15 < nblk; b += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = slab[(size_t)(b + u) * len + i];
+#pragma unroll
+    for (int u = 0; u < 16; u += 4) {
+      s0 += v[u];
+      s1 += v[u + 1];
+      s2 += v[u + 2];
+      s3 += v[u + 3];
+    }
+  }
+  for (; b + 3 < nblk; b += 4) {
+    s0 += slab[(size_t)b * len + i];
+    s1 += slab[(size_t)(b + 1) * len + i];
+    s2 += slab[(size_t)(b + 2) * len + i];
+    s3 += slab[(size_t)(b + 3) * len + i];
+  }
+  for (; b < nblk; ++b) s0 += slab[(size_t)b * len + i];
+}
+
 // Fixed-order sum of the wgrad block partials: 4 independent accumulators (blocks b with
 // b % 4 == j) keep 4 loads in flight per thread, combined in a fixed order at the end.
 // The weight gradient is written in torch's [N][C][KH][KW] layout (GEMM column k = (kh, kw, c),
@@ -524,15 +552,8 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restric
                                                           ConvGeo g) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int b = 0;
-  for (; b + 3 < nblk; b += 4) {
-    s0 += slab[(size_t)b * len + i];
-    s1 += slab[(size_t)(b + 1) * len + i];
-    s2 += slab[(size_t)(b + 2) * len + i];
-    s3 += slab[(size_t)(b + 3) * len + i];
-  }
-  for (; b < nblk; ++b) s0 += slab[(size_t)b * len + i];
+  float s0, s1, s2, s3;
+  slab_sum4(slab, nblk, len, i, s0, s1, s2, s3);
   const float s = (s0 + s1) + (s2 + s3);
   if (i < nk) {
     const int n = i / g.Kp, k = i - n * g.Kp;
@@ -658,15 +679,8 @@ __global__ __launch_bounds__(256) void conv_reduce_multi_kernel(ConvReduceMulti 
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
   const float* slab = r.slab[l];
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int b = 0;
-  for (; b + 3 < nblk; b += 4) {
-    s0 += slab[(size_t)b * len + i];
-    s1 += slab[(size_t)(b + 1) * len + i];
-    s2 += slab[(size_t)(b + 2) * len + i];
-    s3 += slab[(size_t)(b + 3) * len + i];
-  }
-  for (; b < nblk; ++b) s0 += slab[(size_t)b * len + i];
+  float s0, s1, s2, s3;
+  slab_sum4(slab, nblk, len, i, s0, s1, s2, s3);
   const float sum = (s0 + s1) + (s2 + s3);
   const int nk = g.N * g.Kp;
   if (i < nk) {
