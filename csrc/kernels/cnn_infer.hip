@@ -39,25 +39,15 @@ __device__ __forceinline__ void cnn_fc_tile(const bf16* __restrict__ X, const bf
   const bf16* xr = X + (size_t)(m < B ? m : 0) * K + kq;
   const bf16* wr = W + (size_t)(n0 + r) * K + kq;
   f32x4 acc = zero4();
-  // 8 k-steps of operand loads in flight before their MFMAs (same MFMA order: bitwise)
-  constexpr int KB = 8;
-  for (int sb = s0; sb < s1; sb += KB) {
-    bf16x8 a[KB], b[KB];
+#pragma unroll 4
+  for (int s = s0; s < s1; ++s) {
+    bf16x8 a = *reinterpret_cast<const bf16x8*>(xr + s * 32);
+    if (m >= B) {
 #pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      if (sb + u >= s1) break;
-      a[u] = *reinterpret_cast<const bf16x8*>(xr + (sb + u) * 32);
-      b[u] = *reinterpret_cast<const bf16x8*>(wr + (sb + u) * 32);
+      for (int j = 0; j < 8; ++j) a[j] = (bf16)0.f;
     }
-#pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      if (sb + u >= s1) break;
-      if (m >= B) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[u][j] = (bf16)0.f;
-      }
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc, 0, 0, 0);
-    }
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(wr + s * 32);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
   }
   red[w][l] = acc;
   __syncthreads();
