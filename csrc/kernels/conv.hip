@@ -432,35 +432,48 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
   for (int i = 0; i < TPW; ++i) acc[i] = zero4();
   float bsum = 0.f;  // bias partial of channel tid (tid < N)
   const int n_items = (K / 8) * CH;
-  constexpr int kWgBatch = 8;
-  // im2col fragment it = (k-group kg, row ml) of the chunk at c0
-  auto load_a = [&](int c0, int it) -> bf16x8 {
-    const int ml = it % CH, kg = it / CH;
-    const int m = c0 + ml;
-    if (it >= n_items || m >= me) return zero8();
-    const int b = m / OHW, pix = m - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
-    if (tap_checked) return load8_pad(X, g, b, oh, ow, kg * 8, true, in_scale);
-    const int k = kg * 8, kh = k / rowlen, off = k - kh * rowlen;
-    return load8(X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C + kh * xrow + off, in_scale);
-  };
-  auto store_a = [&](int it, const bf16x8& v) {
-    if (it >= n_items) return;
-    const int ml = it % CH, kg = it / CH;
+  for (int c0 = mb; c0 < me; c0 += CH) {
+    // im2col fragments (k-group kg, row ml), transposed; kWgBatch fragments per thread are
+    // loaded before any is stored, so their round trips overlap (small-batch chunks: one batch)
+    constexpr int kWgBatch = 8;
+    for (int base = tid; base < n_items; base += 512 * kWgBatch) {
+      bf16x8 v[kWgBatch];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) At[(size_t)(kg * 8 + j) * LD + ml] = v[j];
-  };
-  // dZ fragment it = (8 channels ng, row ml): dY * [Y > 0] when relu_out, transposed
-  auto load_z = [&](int c0, int it) -> bf16x8 {
-    const int ml = it % CH, ng = it / CH;
-    const int m = c0 + ml;
-    return m < me ? load_dz8(dY, Y, (size_t)m * N + ng * 8, relu_out) : zero8();
-  };
-  auto store_z = [&](int it, const bf16x8& z) {
-    const int ml = it % CH, ng = it / CH;
+      for (int u = 0; u < kWgBatch; ++u) {
+        const int it = base + 512 * u;
+        v[u] = zero8();
+        if (it >= n_items) continue;
+        const int ml = it % CH, kg = it / CH;
+        const int m = c0 + ml;
+        if (m < me) {
+          const int b = m / OHW, pix = m - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
+          if (tap_checked) {
+            v[u] = load8_pad(X, g, b, oh, ow, kg * 8, true, in_scale);
+          } else {
+            const int k = kg * 8, kh = k / rowlen, off = k - kh * rowlen;
+            v[u] = load8(X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C + kh * xrow + off, in_scale);
+          }
+        }
+      }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Zt[(ng * 8 + j) * LD + ml] = z[j];
-  };
-  auto compute = [&]() {
+      for (int u = 0; u < kWgBatch; ++u) {
+        const int it = base + 512 * u;
+        if (it >= n_items) continue;
+        const int ml = it % CH, kg = it / CH;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) At[(size_t)(kg * 8 + j) * LD + ml] = v[u][j];
+      }
+    }
+    // dZ fragments (8 channels ng, row ml): dY * [Y > 0] when relu_out, transposed
+    for (int it = tid; it < (N / 8) * CH; it += 512) {
+      const int ml = it % CH, ng = it / CH;
+      const int m = c0 + ml;
+      bf16x8 z = zero8();
+      if (m < me) z = load_dz8(dY, Y, (size_t)m * N + ng * 8, relu_out);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Zt[(ng * 8 + j) * LD + ml] = z[j];
+    }
+    __syncthreads();
     if (tid < N) {
       const bf16x8* zr = reinterpret_cast<const bf16x8*>(Zt + tid * LD);
 #pragma unroll
@@ -485,43 +498,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
         }
       }
     }
-  };
-  if (CH == 32 && n_items <= 512 * kWgBatch && (N / 8) * CH <= 512) {
-    // small-batch chunks fit one load batch per thread: the next chunk's loads are in flight
-    // while this chunk's MFMAs run (register double buffer; same LDS contents and MFMA order)
-    bf16x8 v[kWgBatch], zv = zero8();
-    const bool zt = tid < (N / 8) * CH;
-#pragma unroll
-    for (int u = 0; u < kWgBatch; ++u) v[u] = load_a(mb, tid + 512 * u);
-    if (zt) zv = load_z(mb, tid);
-    for (int c0 = mb; c0 < me; c0 += CH) {
-#pragma unroll
-      for (int u = 0; u < kWgBatch; ++u) store_a(tid + 512 * u, v[u]);
-      if (zt) store_z(tid, zv);
-      __syncthreads();
-      if (c0 + CH < me) {
-#pragma unroll
-        for (int u = 0; u < kWgBatch; ++u) v[u] = load_a(c0 + CH, tid + 512 * u);
-        if (zt) zv = load_z(c0 + CH, tid);
-      }
-      compute();
-      __syncthreads();
-    }
-  } else {
-    for (int c0 = mb; c0 < me; c0 += CH) {
-      // kWgBatch fragments per thread are loaded before any is stored, so their round trips overlap
-      for (int base = tid; base < n_items; base += 512 * kWgBatch) {
-        bf16x8 v[kWgBatch];
-#pragma unroll
-        for (int u = 0; u < kWgBatch; ++u) v[u] = load_a(c0, base + 512 * u);
-#pragma unroll
-        for (int u = 0; u < kWgBatch; ++u) store_a(base + 512 * u, v[u]);
-      }
-      for (int it = tid; it < (N / 8) * CH; it += 512) store_z(it, load_z(c0, it));
-      __syncthreads();
-      compute();
-      __syncthreads();
-    }
+    __syncthreads();
   }
   // partial dW [N][K] then db [N] of this block
   float* out = slab + (size_t)blockIdx.x * ((size_t)N * K + N);
