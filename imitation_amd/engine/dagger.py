@@ -699,7 +699,11 @@ class DeviceDAggerCollector:
                 twin._run_chunk(b)
             th.cuda.synchronize(self.device)
             self._twin = twin
-            self._twin_stream = th.cuda.Stream(device=self.device)
+            # the statistics chain is the one the epoch's end waits for (round 5, call AI: ~33 ms per
+            # round in StatsFuture.result): its launches get the high-priority queue by default
+            # (IMITATION_AMD_DAGGER_STATS_PRIORITY=0: a normal stream)
+            hi = os.environ.get("IMITATION_AMD_DAGGER_STATS_PRIORITY", "1") != "0"
+            self._twin_stream = th.cuda.Stream(device=self.device, priority=-1 if hi else 0)
         return twin
 
     def start_rollout_stats(self, n_episodes: int) -> StatsFuture:
