@@ -699,10 +699,10 @@ class DeviceDAggerCollector:
                 twin._run_chunk(b)
             th.cuda.synchronize(self.device)
             self._twin = twin
-            # the statistics chain is the one the epoch's end waits for (round 5, call AI: ~33 ms per
-            # round in StatsFuture.result): its launches get the high-priority queue by default
-            # (IMITATION_AMD_DAGGER_STATS_PRIORITY=0: a normal stream)
-            hi = os.environ.get("IMITATION_AMD_DAGGER_STATS_PRIORITY", "1") != "0"
+            # the epoch's end waits ~33 ms per round for the statistics chain (round 5, call AI), but
+            # a high-priority stream for it measured much slower (call AJ: 17.1-18.3K vs 23.8-28.4K
+            # env-steps/s): opt-in only (IMITATION_AMD_DAGGER_STATS_PRIORITY=1)
+            hi = os.environ.get("IMITATION_AMD_DAGGER_STATS_PRIORITY", "0") == "1"
             self._twin_stream = th.cuda.Stream(device=self.device, priority=-1 if hi else 0)
         return twin
 
