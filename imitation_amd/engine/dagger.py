@@ -489,6 +489,13 @@ class DeviceDAggerCollector:
     def _step_cnn(self, k: int, b: Dict) -> None:
         C = self._C
         ea, la = self._actors
+        if getattr(self, "_learner_only", False):
+            # statistics twin: the learner alone acts (BC's RolloutStatsComputer runs the policy
+            # without the expert), no expert forward and no frame / label records
+            C.cnn_head(la.hidden(self.obs), self.learner.action_net.weight, self.learner.action_net.bias, 1,
+                       self._head_seed, self._head_ctr, self._a_rob)
+            C.dagger_env_step(self._env_args(0, k, self._a_rob, b))
+            return
         if self._pair:
             h_e, h_l = CnnActor.hidden_pair(ea, la, self.obs)
         else:
@@ -691,6 +698,8 @@ class DeviceDAggerCollector:
             twin = DeviceDAggerCollector(self.venv, self.expert, snap, self.rng, chunk=self.chunk, use_graph=self.use_graph)
             if self.cnn:
                 twin._head_seed = self._head_seed
+                # (IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY=0: the paired expert + learner step with beta 0)
+                twin._learner_only = os.environ.get("IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY", "1") != "0"
             # its chunk graphs are captured here, on the calling thread (the worker thread only
             # replays them: no capture may overlap another thread's work): one eager + captured
             # chunk per buffer set, on throw-away env state (overwritten by every start)
