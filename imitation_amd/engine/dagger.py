@@ -698,8 +698,9 @@ class DeviceDAggerCollector:
             twin = DeviceDAggerCollector(self.venv, self.expert, snap, self.rng, chunk=self.chunk, use_graph=self.use_graph)
             if self.cnn:
                 twin._head_seed = self._head_seed
-                # (IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY=0: the paired expert + learner step with beta 0)
-                twin._learner_only = os.environ.get("IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY", "1") != "0"
+                # IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY=1: the learner-alone step (no expert forward);
+                # measured no faster than the paired step with beta 0 (round 5, call AO), so opt-in
+                twin._learner_only = os.environ.get("IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY", "0") == "1"
             # its chunk graphs are captured here, on the calling thread (the worker thread only
             # replays them: no capture may overlap another thread's work): one eager + captured
             # chunk per buffer set, on throw-away env state (overwritten by every start)
