@@ -38,6 +38,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 CONFIGS = ["bc_cartpole", "gail_halfcheetah", "airl_hopper", "dagger_pong", "preference_walker2d"]
+# timed steps when --steps is not given: the ms-scale GAIL / AIRL rounds are noisy over 3 rounds
+# (AIRL 6.7-7.8 ms over 3 vs 6.36-6.44 ms over 10, round 5), the 100-500 ms rounds are not
+DEFAULT_STEPS = {"gail_halfcheetah": 20, "airl_hopper": 10}
 
 
 def _sync(device):
@@ -145,6 +148,8 @@ def make_expert(name, args, device):
 def run_config(name, args, device, rank, world):
     from imitation_amd.parallel import dist as pdist
 
+    steps = args.steps if args.steps is not None else DEFAULT_STEPS.get(name, 3)
+
     expert = None
     if args.expert_steps > 0 and name in EXPERT_CONFIGS:
         if world > 1:
@@ -166,9 +171,9 @@ def run_config(name, args, device, rank, world):
     t0 = time.perf_counter()
     units = 0
     if multi:
-        units = step(args.steps)
+        units = step(steps)
     else:
-        for _ in range(args.steps):
+        for _ in range(steps):
             units += step()
     _sync(device)
     pdist.barrier()
@@ -177,7 +182,7 @@ def run_config(name, args, device, rank, world):
     if expert is not None:  # imitation budget (untimed), then the normalised score
         from imitation_amd.testing import imitation_quality as iq
 
-        done = (args.warmup + args.steps) * b.trainer.gen_train_timesteps
+        done = (args.warmup + steps) * b.trainer.gen_train_timesteps
         if args.imit_steps > done:
             b.trainer.train((args.imit_steps - done) // b.trainer.gen_train_timesteps * b.trainer.gen_train_timesteps)
         r, _ = b.trainer.device_evaluate(args.eval_episodes_expert, deterministic=True, seed=10_000 + args.seed)
@@ -192,7 +197,7 @@ def run_config(name, args, device, rank, world):
         ret = pdist.allreduce_scalars([ret], op="sum")[0] / world
     out = {
         "config": name, "env": b.env_id, "value": round(total / dt, 2), "unit": unit, "n_gpus": world if device.type == "cuda" else 0,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "steps": steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / steps, 3),
         "final_eval_return": None if ret is None else round(float(ret), 3), "engine": b.extras.get("engine", "host"),
         "device": str(device), "data": "synthetic env + synthetic demos, random-init weights",
     }
@@ -205,7 +210,7 @@ def run_config(name, args, device, rank, world):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--configs", default="all")
-    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default: 20 GAIL, 10 AIRL, 3 others)")
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--eval-episodes", type=int, default=5)
     p.add_argument("--seed", type=int, default=0)
