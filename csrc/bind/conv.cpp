@@ -244,7 +244,7 @@ torch::Tensor cnn_fc(torch::Tensor x, torch::Tensor w, torch::Tensor b) {
 // Linear + ReLU backward over the NHWC-flattened conv output: (dW fp32 [NH, C*HW] torch (c, h, w)
 // columns, db fp32 [NH], dX bf16 [M, K] or None)
 py::tuple fc_backward(torch::Tensor x, torch::Tensor dh, torch::Tensor h, torch::Tensor wt, int64_t C, bool need_dx,
-                      c10::optional<torch::Tensor> dW_out, c10::optional<torch::Tensor> db_out) {
+                      c10::optional<torch::Tensor> dW_out, c10::optional<torch::Tensor> db_out, bool mask_dx) {
   IA_CHECK_CUDA(x);
   IA_CHECK_CONTIG(x);
   IA_CHECK_CUDA(wt);
@@ -281,7 +281,7 @@ py::tuple fc_backward(torch::Tensor x, torch::Tensor dh, torch::Tensor h, torch:
   auto dzb = torch::empty({M, NH}, x.options());  // bf16 dZ, fc_wgrad -> fc_dgrad
   IA_HIP_CHECK3(ia::fc_backward(x.data_ptr(), dhc.data_ptr<float>(), h.data_ptr<float>(), wt.data_ptr(),
                                 dW.data_ptr<float>(), db.data_ptr<float>(), need_dx ? dx.data_ptr() : nullptr, dzb.data_ptr(), M,
-                                (int)K, NH, (int)C, (int)(K / C), ia_stream()));
+                                (int)K, NH, (int)C, (int)(K / C), ia_stream(), mask_dx));
   return py::make_tuple(dW, db, need_dx ? py::cast(dx) : py::none());
 }
 
@@ -412,7 +412,7 @@ void register_conv(py::module& m) {
         py::arg("want_t"), py::arg("t_hwc") = std::vector<bool>{});
   m.def("fc_backward", &fc_backward, "NatureCNN feature-layer backward (dW torch layout, db, dX NHWC bf16)", py::arg("x"),
         py::arg("dh"), py::arg("h"), py::arg("wt"), py::arg("C"), py::arg("need_dx"), py::arg("dW_out") = py::none(),
-        py::arg("db_out") = py::none());
+        py::arg("db_out") = py::none(), py::arg("mask_dx") = false);
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight/bias gradient (deterministic block reduction)", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
         py::arg("relu_out"), py::arg("pad") = 0, py::arg("dW_out") = py::none(), py::arg("db_out") = py::none());

@@ -189,7 +189,8 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
 // One wave = 16 rows x 16 NHWC columns; the n loop is issued 4 k-steps (8 loads) at a time
 // so the L2 round trips overlap (the wave reads 16 KB of Wt).
 __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
-                                                       bf16* __restrict__ dX, int M, int K, int NH) {
+                                                       bf16* __restrict__ dX, int M, int K, int NH,
+                                                       const bf16* __restrict__ Xm) {
   const int l = threadIdx.x & 63;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int ktiles = K / 16;
@@ -223,7 +224,11 @@ __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = m0 + 4 * (l >> 4) + i;
-    if (row < M) dX[(size_t)row * K + k] = (bf16)acc[i];
+    if (row < M) {
+      float v = acc[i];
+      if (Xm && !((float)Xm[(size_t)row * K + k] > 0.f)) v = 0.f;  // top-layer ReLU mask (same select as load_dz8)
+      dX[(size_t)row * K + k] = (bf16)v;
+    }
   }
 }
 
@@ -234,7 +239,7 @@ bool fc_train_ok(int M, int K, int NH, int C, int HW) {
 }
 
 hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const void* Wt, float* dW, float* db, void* dX,
-                       void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s) {
+                       void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s, bool mask_dx) {
   if (!fc_train_ok(M, K, NH, C, HW)) return hipErrorInvalidValue;
   const char* ch_env = getenv("IMITATION_AMD_FC_WGRAD_CH");  // "0": the 64-column blocks (A/B knob, read per call)
   const bool ch_off = ch_env != nullptr && ch_env[0] == '0';
@@ -248,7 +253,8 @@ hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const 
   if (dX) {
     const int waves = ((M + 15) / 16) * (K / 16);
     hipLaunchKernelGGL(fc_dgrad_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, static_cast<const bf16*>(dZb),
-                       static_cast<const bf16*>(Wt), static_cast<bf16*>(dX), M, K, NH);
+                       static_cast<const bf16*>(Wt), static_cast<bf16*>(dX), M, K, NH,
+                       mask_dx ? static_cast<const bf16*>(X) : nullptr);
   }
   return hipGetLastError();
 }

@@ -244,8 +244,10 @@ hipError_t cnn_fc(const void* X, const void* W, const float* bias, float* H, int
 // K = C * HW), dH / Hout fp32 [M][NH], Wt bf16 [K][NH]; dW fp32 [NH][K] in torch's (c, h, w)
 // column order, db fp32 [NH], dX bf16 [M][K] (nullptr: not needed)
 bool fc_train_ok(int M, int K, int NH, int C, int HW);
+// dZb: bf16 [M][NH] scratch; mask_dx: dX = 0 where X <= 0 (X is the post-ReLU conv output, so the conv
+// trunk's top-layer ReLU mask is applied once here instead of in every dZ load downstream)
 hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const void* Wt, float* dW, float* db, void* dX,
-                       void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s);  // dZb: bf16 [M][NH] scratch
+                       void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s, bool mask_dx = false);
 struct CnnFcPair {
   const void* X[2];
   const void* W[2];

@@ -67,6 +67,9 @@ class FusedCnnBCStep:
         dev = self.flat.device
         self.metrics = th.zeros(8, device=dev)
         self.ws = th.zeros(int(self.C.bc_head_workspace(self.flat.numel())), device=dev)  # word 0: counter
+        import os
+
+        self._mask_dx = os.environ.get("IMITATION_AMD_BC_MASK_DX", "1") != "0"
 
     @staticmethod
     def maybe(policy, optimizer, obs, ent_weight: float, l2_weight: float) -> Optional["FusedCnnBCStep"]:
@@ -132,7 +135,11 @@ class FusedCnnBCStep:
             a = acts.reshape(-1).long().contiguous()
             dh = C.bc_head_train(out, head.weight.detach(), head.bias.detach(), a, self.flat, self.g_head[0], self.g_head[1],
                                  self.metrics, self.ws, self.ent_weight, self.l2_weight)
-            _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1])
+            # the top conv's ReLU mask is applied once, in the FC's dX store (xf is that conv's
+            # post-ReLU output): its dgrad / wgrad then read a masked dZ (same values; round 5
+            # PMC: those kernels are VALU-issue bound). IMITATION_AMD_BC_MASK_DX=0: mask per load
+            pre = self._mask_dx
+            _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1], mask_dx=pre)
             dz = dx.view(hs[-1].shape)
             # weight-gradient partials per layer; their reductions in ONE launch at the end. Each
             # layer's wgrad runs on a stream of its own, beside the data-gradient chain it does not
@@ -143,7 +150,7 @@ class FusedCnnBCStep:
             for i in range(n - 1, -1, -1):
                 c = convs[i]
                 inp = x if i == 0 else hs[i - 1]
-                top = i == n - 1
+                top = i == n - 1 and not pre  # (relu_out: mask dZ in the loads)
                 kh, kw, st = int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0])
                 if sides:
                     sd = sides[i]
