@@ -69,7 +69,7 @@ class FusedCnnBCStep:
         self.ws = th.zeros(int(self.C.bc_head_workspace(self.flat.numel())), device=dev)  # word 0: counter
         import os
 
-        self._mask_dx = os.environ.get("IMITATION_AMD_BC_MASK_DX", "1") != "0"
+        self._mask_dx = os.environ.get("IMITATION_AMD_BC_MASK_DX", "0") == "1"
 
     @staticmethod
     def maybe(policy, optimizer, obs, ent_weight: float, l2_weight: float) -> Optional["FusedCnnBCStep"]:
@@ -135,9 +135,9 @@ class FusedCnnBCStep:
             a = acts.reshape(-1).long().contiguous()
             dh = C.bc_head_train(out, head.weight.detach(), head.bias.detach(), a, self.flat, self.g_head[0], self.g_head[1],
                                  self.metrics, self.ws, self.ent_weight, self.l2_weight)
-            # the top conv's ReLU mask is applied once, in the FC's dX store (xf is that conv's
-            # post-ReLU output): its dgrad / wgrad then read a masked dZ (same values; round 5
-            # PMC: those kernels are VALU-issue bound). IMITATION_AMD_BC_MASK_DX=0: mask per load
+            # IMITATION_AMD_BC_MASK_DX=1: the top conv's ReLU mask is applied once, in the FC's dX
+            # store (xf is that conv's post-ReLU output), and its dgrad / wgrad read a masked dZ
+            # (same values; round 5 PMC: those kernels are VALU-issue bound). Opt-in until measured
             pre = self._mask_dx
             _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1], mask_dx=pre)
             dz = dx.view(hs[-1].shape)
