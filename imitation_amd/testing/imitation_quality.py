@@ -197,6 +197,75 @@ def run(algo: str = "gail", env: str = "cartpole", total_timesteps: int = 200_00
 LOCOMOTION = {"halfcheetah": ("seals/HalfCheetah-v1", "gail_halfcheetah"),
               "hopper": ("seals/Hopper-v1", "airl_hopper")}
 
+_EXPERT_CACHE_VERSION = 1
+
+
+def expert_demonstrations(recipe: str, env_id: str, seed: int = 0, expert_timesteps: int = 5_000_000,
+                          n_demo_timesteps: int = 50_000, n_eval: int = 50, device: Any = "cuda", rank: int = 0,
+                          world: int = 1, n_envs: int = 8, cache_dir: Optional[str] = None) -> Dict[str, Any]:
+    """Expert mode of :func:`run_locomotion` as a reusable (and cached) step: train the recipe's
+    generator on the env reward (``debug_use_ground_truth``) for ``expert_timesteps`` per rank,
+    score it (``n_eval`` deterministic ``device_evaluate`` episodes), roll out
+    ``n_demo_timesteps`` stochastic demonstration transitions and score the uniform-random
+    policy on the same env. Returns ``dict(demos, expert_return, random_return, expert_train_s,
+    cached)``.
+
+    ``cache_dir``: the result is stored there as ``expert_<key>.npz`` (atomic rename), keyed by
+    every argument that changes it (recipe, env, seed, budgets, rank -- the demonstrations' seed
+    --, envs per rank), and reused on the next call. ``bench.py`` fills the cache from a child
+    process (:func:`main`, one GPU, no process group) so the measuring process never hosts the
+    expert run. Under data parallelism every rank must call this together: whether the cache is
+    used is agreed over the process group (a cache miss trains the expert data-parallel in
+    process, so a lone rank training would wait for the others forever)."""
+    import hashlib
+    import json
+
+    from imitation_amd import models
+    from imitation_amd.data import types
+    from imitation_amd.parallel import dist as pdist
+
+    key = dict(v=_EXPERT_CACHE_VERSION, recipe=recipe, env=env_id, seed=seed, expert_timesteps=expert_timesteps,
+               n_demo=n_demo_timesteps, n_eval=n_eval, rank=rank, n_envs=n_envs)
+    path = None
+    loaded = None
+    if cache_dir:
+        digest = hashlib.sha256(json.dumps(key, sort_keys=True).encode()).hexdigest()[:16]
+        path = os.path.join(cache_dir, f"expert_{digest}.npz")
+        if os.path.exists(path):
+            try:
+                with np.load(path, allow_pickle=False) as z:
+                    loaded = {k: z[k] for k in z.files}
+            except (OSError, ValueError):  # torn / foreign file: retrain
+                loaded = None
+    have = 1.0 if loaded is not None else 0.0
+    if world > 1:
+        have = pdist.allreduce_scalars([have], op="min")[0]
+    if have > 0.5:
+        demos = types.Transitions(obs=loaded["obs"], acts=loaded["acts"], next_obs=loaded["next_obs"],
+                                  dones=loaded["dones"], infos=np.array([{}] * len(loaded["acts"])))
+        return dict(demos=demos, expert_return=float(loaded["expert_return"]),
+                    random_return=float(loaded["random_return"]), expert_train_s=float(loaded["expert_train_s"]),
+                    cached=True)
+    t0 = time.perf_counter()
+    ex = models.build(recipe, device=device, seed=seed + 100, n_envs=n_envs, env_id=env_id,
+                      debug_use_ground_truth=True)
+    ex.trainer.train(max(ex.trainer.gen_train_timesteps, expert_timesteps))
+    if th.cuda.is_available():
+        th.cuda.synchronize()
+    t_expert = time.perf_counter() - t0
+    r_exp, _ = ex.trainer.device_evaluate(n_eval, deterministic=True, seed=10_000 + seed)
+    expert = float(np.mean(r_exp))
+    demos = ex.trainer.device_demonstrations(n_demo_timesteps, deterministic=False, seed=20_000 + seed + 97 * rank)
+    del ex
+    rand = random_return(env_id, n_eval, seed)
+    if path is not None:
+        os.makedirs(cache_dir, exist_ok=True)
+        tmp = f"{path}.{os.getpid()}.tmp.npz"
+        np.savez(tmp, obs=demos.obs, acts=demos.acts, next_obs=demos.next_obs, dones=demos.dones,
+                 expert_return=np.float64(expert), random_return=np.float64(rand), expert_train_s=np.float64(t_expert))
+        os.replace(tmp, path)
+    return dict(demos=demos, expert_return=expert, random_return=rand, expert_train_s=t_expert, cached=False)
+
 
 def run_locomotion(algo: str = "gail", env: str = "halfcheetah", expert_timesteps: int = 5_000_000,
                    total_timesteps: int = 5_000_000, n_demo_timesteps: int = 50_000, seed: int = 0, n_eval: int = 50,
@@ -254,3 +323,40 @@ def run_locomotion(algo: str = "gail", env: str = "halfcheetah", expert_timestep
                 learner_return=curve[-1]["ret"], normalized_score=curve[-1]["norm"], curve=curve, total_timesteps=done,
                 train_s=round(t_train, 3), n_eval_episodes=n_eval, n_demo_transitions=len(demos.acts),
                 demo_return=demo_return, returns_before=returns_before, returns_after=last["returns"])
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    """``python -m imitation_amd.testing.imitation_quality expert ...``: fill the expert cache of
+    :func:`expert_demonstrations` in a process of its own (``bench.py`` runs this before it touches
+    the GPU, so its timed process starts as clean as a cached run). Single GPU, no process group."""
+    import argparse
+
+    p = argparse.ArgumentParser(prog="imitation_quality")
+    p.add_argument("cmd", choices=["expert"])
+    p.add_argument("--recipe", default="gail_halfcheetah")
+    p.add_argument("--env", default="HalfCheetah-v4")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--expert-steps", type=int, default=5_000_000)
+    p.add_argument("--n-demo", type=int, default=50_000)
+    p.add_argument("--n-eval", type=int, default=50)
+    p.add_argument("--rank", type=int, default=0)
+    p.add_argument("--n-envs", type=int, default=8)
+    p.add_argument("--device", default="cuda")
+    p.add_argument("--cache-dir", required=True)
+    a = p.parse_args(argv)
+    dev = th.device(a.device)
+    if dev.type == "cuda":
+        th.cuda.set_device(dev)
+    th.manual_seed(a.seed)
+    np.random.seed(a.seed)
+    r = expert_demonstrations(a.recipe, a.env, seed=a.seed, expert_timesteps=a.expert_steps, n_demo_timesteps=a.n_demo,
+                              n_eval=a.n_eval, device=dev, rank=a.rank, world=1, n_envs=a.n_envs, cache_dir=a.cache_dir)
+    print(f"expert {a.recipe}/{a.env} rank {a.rank}: return {r['expert_return']:.1f} (random {r['random_return']:.1f}), "
+          f"{len(r['demos'].acts)} demo transitions, cached={r['cached']}, train {r['expert_train_s']:.2f} s", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    import sys
+
+    sys.exit(main())
