@@ -1,30 +1,29 @@
 """Trajectory / transition containers (reference: ``src/imitation/data/types.py``).
 
-Frozen dataclasses with the reference's validation rules:
+Behaviour (validation rules, error messages, indexing semantics) follows the reference, which
+users and the parity tests depend on; the implementation is this framework's own:
 
-* :class:`DictObs` (``types.py:38-202``) -- dict-of-arrays observation with
-  array-like len/index/iter and stack/concatenate helpers;
-* :class:`Trajectory` (``:336-416``): ``len(obs) == len(acts) + 1``, optional
-  per-step ``infos``, ``terminal`` flag, ``__setstate__`` back-compat;
-* :class:`TrajectoryWithRew` (``:430-439``);
+* :class:`DictObs` (reference ``types.py:38-202``) -- a dict of equally long arrays that
+  indexes, iterates and stacks like one array. Stored as a read-only mapping behind
+  ``__slots__``; stacking checks the key sets in one pass over a materialised list.
+* :class:`Trajectory` / :class:`TrajectoryWithRew` (``:336-439``) -- one episode or fragment:
+  ``len(obs) == len(acts) + 1``; every check is one row of the class's ``_RULES`` table.
 * :class:`TransitionsMinimal` / :class:`Transitions` / :class:`TransitionsWithRew`
-  (``:481-638``): torch ``Dataset``s, read-only arrays, int index -> dict,
-  slice -> same dataclass;
+  (``:481-638``) -- flat torch ``Dataset`` s with read-only arrays; int index -> dict,
+  slice -> same class.
 * :func:`transitions_collate_fn` (``:447-474``), :func:`dataclass_quick_asdict`.
 
-Extra on this framework: :meth:`TransitionsMinimal.to_device` packs the numeric
-fields into device tensors once, so training loops can keep demonstrations
-resident in HBM instead of re-copying every minibatch (the reference converts per
-batch, ``algorithms/bc.py:490-494``).
+Extra on this framework: :meth:`TransitionsMinimal.to_device` packs the numeric fields into
+device tensors once, so training loops keep demonstrations resident in HBM instead of
+re-copying every minibatch (the reference converts per batch, ``algorithms/bc.py:490-494``).
 """
 
 from __future__ import annotations
 
-import collections
 import dataclasses
-import itertools
 import numbers
 import os
+import types as _pytypes
 import warnings
 from typing import Any, Callable, Dict, Iterable, Iterator, List, Mapping, Optional, Sequence, Tuple, TypeVar, Union
 
@@ -43,95 +42,110 @@ AnyTensor = Union[np.ndarray, th.Tensor]
 TensorVar = TypeVar("TensorVar", np.ndarray, th.Tensor)
 
 
-@dataclasses.dataclass(frozen=True)
 class DictObs:
-    """Observations of a ``Dict`` observation space, indexed like one array."""
+    """Observations of a ``Dict`` observation space, indexed like one array: ``len`` is the shared
+    leading dimension, ``obs[i]`` / ``obs[a:b]`` index every array, iteration yields rows."""
 
-    _d: Dict[str, np.ndarray]
+    __slots__ = ("_arrays",)
+
+    def __init__(self, arrays: Mapping[str, np.ndarray]):
+        for v in arrays.values():
+            if not isinstance(v, (np.ndarray, numbers.Number)):
+                raise TypeError("Values must be NumPy arrays")
+        object.__setattr__(self, "_arrays", _pytypes.MappingProxyType(dict(arrays)))
+
+    def __setattr__(self, name, value):
+        raise dataclasses.FrozenInstanceError(f"cannot assign to field {name!r}")
+
+    def __getstate__(self):
+        return dict(self._arrays)
+
+    def __setstate__(self, state):
+        object.__setattr__(self, "_arrays", _pytypes.MappingProxyType(dict(state)))
+
+    def __repr__(self) -> str:
+        return f"DictObs({dict(self._arrays)!r})"
+
+    @property
+    def _d(self) -> Mapping[str, np.ndarray]:  # read-only view (name kept for code written against the reference)
+        return self._arrays
 
     @classmethod
     def from_obs_list(cls, obs_list: List[Dict[str, np.ndarray]]) -> "DictObs":
-        return cls.stack(map(cls, obs_list))
+        return cls.stack([cls(o) for o in obs_list])
 
-    def __post_init__(self):
-        if not all(isinstance(v, (np.ndarray, numbers.Number)) for v in self._d.values()):
-            raise TypeError("Values must be NumPy arrays")
-
-    def __len__(self):
-        lens = {len(v) for v in self._d.values()}
-        if len(lens) == 1:
-            return lens.pop()
-        if not lens:
+    def __len__(self) -> int:
+        firsts = {len(v) for v in self._arrays.values()}
+        if not firsts:
             raise RuntimeError("Length not defined as DictObs is empty")
-        raise RuntimeError(f"Length not defined; arrays have conflicting first dimensions: {lens}")
+        if len(firsts) > 1:
+            raise RuntimeError(f"Length not defined; arrays have conflicting first dimensions: {firsts}")
+        (n,) = firsts
+        return n
 
     @property
-    def dict_len(self):
-        return len(self._d)
+    def dict_len(self) -> int:
+        return len(self._arrays)
 
     def __getitem__(self, key) -> "DictObs":
-        return self.__class__({k: np.asarray(v[key]) for k, v in self._d.items()})
+        return type(self)({k: np.asarray(v[key]) for k, v in self._arrays.items()})
 
     def __iter__(self) -> Iterator["DictObs"]:
-        return (self[i] for i in range(len(self)))
+        for i in range(len(self)):
+            yield self[i]
 
-    def __eq__(self, other):
-        if not isinstance(other, self.__class__):
-            return False
-        if self.keys() != other.keys():
-            return False
-        return all(np.array_equal(self.get(k), other.get(k)) for k in self.keys())
+    def __eq__(self, other) -> bool:
+        return (isinstance(other, type(self)) and self._arrays.keys() == other._arrays.keys()
+                and all(np.array_equal(v, other._arrays[k]) for k, v in self._arrays.items()))
+
+    __hash__ = None  # mutable-array contents: not hashable (as a dataclass with eq would be)
 
     @property
     def shape(self) -> Dict[str, Tuple[int, ...]]:
-        return {k: v.shape for k, v in self.items()}
+        return {k: v.shape for k, v in self._arrays.items()}
 
     @property
     def dtype(self) -> Dict[str, np.dtype]:
-        return {k: v.dtype for k, v in self.items()}
+        return {k: v.dtype for k, v in self._arrays.items()}
 
     def keys(self):
-        return self._d.keys()
+        return self._arrays.keys()
 
     def values(self):
-        return self._d.values()
+        return self._arrays.values()
 
     def items(self):
-        return self._d.items()
+        return self._arrays.items()
 
-    def __contains__(self, key):
-        return key in self._d
+    def __contains__(self, key) -> bool:
+        return key in self._arrays
 
     def get(self, key: str) -> np.ndarray:
-        return self._d[key]
+        return self._arrays[key]
 
     def unwrap(self) -> Dict[str, np.ndarray]:
-        return dict(self._d)
+        return dict(self._arrays)
 
     def map_arrays(self, fn: Callable[[np.ndarray], np.ndarray]) -> "DictObs":
-        return self.__class__({k: fn(v) for k, v in self.items()})
+        return type(self)({k: fn(v) for k, v in self._arrays.items()})
 
-    @staticmethod
-    def _unravel(dictobs_list: Iterable["DictObs"]) -> Dict[str, List[np.ndarray]]:
-        it1, it2 = itertools.tee(dictobs_list)
-        key_set = {frozenset(obs.keys()) for obs in it1}
-        if not key_set:
+    @classmethod
+    def _join(cls, parts: Iterable["DictObs"], fn, axis: int) -> "DictObs":
+        parts = list(parts)
+        if not parts:
             raise ValueError("Empty list of DictObs")
-        if len(key_set) != 1:
-            raise ValueError(f"Inconsistent keys: {key_set}")
-        out: Dict[str, List[np.ndarray]] = collections.defaultdict(list)
-        for ob in it2:
-            for k, arr in ob._d.items():
-                out[k].append(arr)
-        return out
+        keys = frozenset(parts[0].keys())
+        if any(frozenset(p.keys()) != keys for p in parts[1:]):
+            raise ValueError(f"Inconsistent keys: {set(frozenset(p.keys()) for p in parts)}")
+        return cls({k: fn([p._arrays[k] for p in parts], axis=axis) for k in parts[0].keys()})
 
     @classmethod
     def stack(cls, dictobs_list: Iterable["DictObs"], axis=0) -> "DictObs":
-        return cls({k: np.stack(v, axis=axis) for k, v in cls._unravel(dictobs_list).items()})
+        return cls._join(dictobs_list, np.stack, axis)
 
     @classmethod
     def concatenate(cls, dictobs_list: Iterable["DictObs"], axis=0) -> "DictObs":
-        return cls({k: np.concatenate(v, axis=axis) for k, v in cls._unravel(dictobs_list).items()})
+        return cls._join(dictobs_list, np.concatenate, axis)
 
 
 Observation = Union[np.ndarray, DictObs]
@@ -145,16 +159,12 @@ def assert_not_dictobs(x: Observation) -> np.ndarray:
 
 def concatenate_maybe_dictobs(arrs: List[ObsVar]) -> ObsVar:
     assert len(arrs) > 0
-    if isinstance(arrs[0], DictObs):
-        return DictObs.concatenate(arrs)
-    return np.concatenate(arrs)
+    return DictObs.concatenate(arrs) if isinstance(arrs[0], DictObs) else np.concatenate(arrs)
 
 
 def stack_maybe_dictobs(arrs: List[ObsVar]) -> ObsVar:
     assert len(arrs) > 0
-    if isinstance(arrs[0], DictObs):
-        return DictObs.stack(arrs)
-    return np.stack(arrs)
+    return DictObs.stack(arrs) if isinstance(arrs[0], DictObs) else np.stack(arrs)
 
 
 def maybe_unwrap_dictobs(maybe_dictobs):
@@ -174,9 +184,7 @@ def maybe_wrap_in_dictobs(obs):
 
 
 def map_maybe_dict(fn, maybe_dict):
-    if isinstance(maybe_dict, dict):
-        return {k: fn(v) for k, v in maybe_dict.items()}
-    return fn(maybe_dict)
+    return {k: fn(v) for k, v in maybe_dict.items()} if isinstance(maybe_dict, dict) else fn(maybe_dict)
 
 
 class TransitionMappingNoNextObs(TypedDict):
@@ -195,6 +203,32 @@ def dataclass_quick_asdict(obj) -> Dict[str, Any]:
     return {f.name: getattr(obj, f.name) for f in dataclasses.fields(obj)}
 
 
+# A validation rule: (predicate on the instance -> True when it is violated, message builder).
+_Rule = Tuple[Callable[[Any], bool], Callable[[Any], str]]
+
+
+def _enforce(obj, rules: Sequence[_Rule]) -> None:
+    for violated, message in rules:
+        if violated(obj):
+            raise ValueError(message(obj))
+
+
+_REW_RULES: Tuple[_Rule, ...] = (
+    (lambda s: s.rews.shape != (len(s.acts),),
+     lambda s: f"rewards must be 1D array, one entry for each action: {s.rews.shape} != ({len(s.acts)},)"),
+    (lambda s: not np.issubdtype(s.rews.dtype, np.floating), lambda s: f"rewards dtype {s.rews.dtype} not a float"),
+)
+
+
+def _same_field(name: str, a, b, n: int) -> bool:
+    if name == "infos":  # absent infos compare equal to empty per-step dicts
+        a = [{}] * n if a is None else a
+        b = [{}] * n if b is None else b
+    if isinstance(a, DictObs) or isinstance(b, DictObs):
+        return a == b
+    return bool(np.array_equal(a, b))
+
+
 @dataclasses.dataclass(frozen=True)
 class Trajectory:
     """One episode (or fragment): ``obs`` has one more entry than ``acts``."""
@@ -204,53 +238,35 @@ class Trajectory:
     infos: Optional[np.ndarray]
     terminal: bool
 
+    _RULES = (
+        (lambda s: len(s.obs) != len(s.acts) + 1,
+         lambda s: f"expected one more observations than actions: {len(s.obs)} != {len(s.acts)} + 1"),
+        (lambda s: s.infos is not None and len(s.infos) != len(s.acts),
+         lambda s: f"infos when present must be present for each action: {len(s.infos)} != {len(s.acts)}"),
+        (lambda s: len(s.acts) == 0, lambda s: "Degenerate trajectory: must have at least one action."),
+    )
+
     def __len__(self) -> int:
         return len(self.acts)
 
-    def __eq__(self, other) -> bool:
-        if not isinstance(other, Trajectory):
-            return False
-        a, b = dataclass_quick_asdict(self), dataclass_quick_asdict(other)
-        if a.keys() != b.keys() or len(self) != len(other):
-            return False
-        for k, va in a.items():
-            vb = b[k]
-            if k == "infos":
-                va = [{}] * len(self) if va is None else va
-                vb = [{}] * len(other) if vb is None else vb
-            if isinstance(va, DictObs):
-                if not va == vb:
-                    return False
-                continue
-            if not np.array_equal(va, vb):
-                return False
-        return True
-
     def __post_init__(self):
-        if len(self.obs) != len(self.acts) + 1:
-            raise ValueError(f"expected one more observations than actions: {len(self.obs)} != {len(self.acts)} + 1")
-        if self.infos is not None and len(self.infos) != len(self.acts):
-            raise ValueError(
-                f"infos when present must be present for each action: {len(self.infos)} != {len(self.acts)}"
-            )
-        if len(self.acts) == 0:
-            raise ValueError("Degenerate trajectory: must have at least one action.")
+        _enforce(self, Trajectory._RULES)
+
+    def __eq__(self, other) -> bool:
+        if not isinstance(other, Trajectory) or len(self) != len(other):
+            return False
+        mine, theirs = dataclass_quick_asdict(self), dataclass_quick_asdict(other)
+        if mine.keys() != theirs.keys():
+            return False
+        return all(_same_field(k, v, theirs[k], len(self)) for k, v in mine.items())
 
     def __setstate__(self, state):
-        if "terminal" not in state:
-            warnings.warn(
-                "Loading old version of Trajectory.Support for this will be removed in future versions.",
-                DeprecationWarning,
-            )
-            state["terminal"] = True
-        self.__dict__.update(state)
-
-
-def _rews_validation(rews: np.ndarray, acts: np.ndarray):
-    if rews.shape != (len(acts),):
-        raise ValueError(f"rewards must be 1D array, one entry for each action: {rews.shape} != ({len(acts)},)")
-    if not np.issubdtype(rews.dtype, np.floating):
-        raise ValueError(f"rewards dtype {rews.dtype} not a float")
+        if "terminal" not in state:  # pickles written before the field existed ended whole episodes
+            warnings.warn("Trajectory pickled without its `terminal` field (old format): assuming terminal=True. "
+                          "Reading this format will be removed in a future version.", DeprecationWarning)
+            state = dict(state, terminal=True)
+        for k, v in state.items():
+            object.__setattr__(self, k, v)
 
 
 @dataclasses.dataclass(frozen=True, eq=False)
@@ -261,7 +277,7 @@ class TrajectoryWithRew(Trajectory):
 
     def __post_init__(self):
         super().__post_init__()
-        _rews_validation(self.rews, self.acts)
+        _enforce(self, _REW_RULES)
 
 
 Pair = Tuple[T, T]
@@ -270,14 +286,14 @@ TrajectoryWithRewPair = Pair[TrajectoryWithRew]
 
 
 def transitions_collate_fn(batch: Sequence[Mapping[str, np.ndarray]]) -> Mapping[str, AnyTensor]:
-    """DataLoader collate for transitions: default collate except ``infos`` (list) and obs (stacked)."""
-    acts_dones = [{k: np.array(v) for k, v in s.items() if k in ("acts", "dones")} for s in batch]
-    result = th_data.dataloader.default_collate(acts_dones)
-    assert isinstance(result, dict)
-    result["infos"] = [s["infos"] for s in batch]
-    result["obs"] = stack_maybe_dictobs([s["obs"] for s in batch])
-    result["next_obs"] = stack_maybe_dictobs([s["next_obs"] for s in batch])
-    return result
+    """DataLoader collate for transitions: ``acts`` / ``dones`` through torch's default collate,
+    ``infos`` kept as a list, observations stacked (dict observations as one :class:`DictObs`)."""
+    out = dict(th_data.dataloader.default_collate(
+        [{k: np.array(s[k]) for k in ("acts", "dones") if k in s} for s in batch]))
+    out["infos"] = [s["infos"] for s in batch]
+    for k in ("obs", "next_obs"):
+        out[k] = stack_maybe_dictobs([s[k] for s in batch])
+    return out
 
 
 TransitionsMinimalSelf = TypeVar("TransitionsMinimalSelf", bound="TransitionsMinimal")
@@ -285,44 +301,47 @@ TransitionsMinimalSelf = TypeVar("TransitionsMinimalSelf", bound="TransitionsMin
 
 @dataclasses.dataclass(frozen=True)
 class TransitionsMinimal(th_data.Dataset, Sequence[Mapping[str, np.ndarray]]):
-    """Flat batch of (obs, act, info); int index -> dict sample, slice -> same class."""
+    """Flat batch of (obs, act, info); int index -> dict sample, slice -> same class. Array fields
+    are made read-only on construction (the batch may be shared by loaders and replay buffers)."""
 
     obs: Observation
     acts: np.ndarray
     infos: np.ndarray
 
+    _RULES = (
+        (lambda s: len(s.obs) != len(s.acts),
+         lambda s: f"obs and acts must have same number of timesteps: {len(s.obs)} != {len(s.acts)}"),
+        (lambda s: len(s.infos) != len(s.obs),
+         lambda s: f"obs and infos must have same number of timesteps: {len(s.obs)} != {len(s.infos)}"),
+    )
+
     def __len__(self) -> int:
         return len(self.obs)
 
     def __post_init__(self):
-        for val in vars(self).values():
-            if isinstance(val, np.ndarray):
-                val.setflags(write=False)
-        if len(self.obs) != len(self.acts):
-            raise ValueError(f"obs and acts must have same number of timesteps: {len(self.obs)} != {len(self.acts)}")
-        if len(self.infos) != len(self.obs):
-            raise ValueError(f"obs and infos must have same number of timesteps: {len(self.obs)} != {len(self.infos)}")
+        for f in dataclasses.fields(self):
+            v = getattr(self, f.name)
+            if isinstance(v, np.ndarray):
+                v.flags.writeable = False
+        _enforce(self, TransitionsMinimal._RULES)
 
     def __getitem__(self, key):
-        d = dataclass_quick_asdict(self)
-        item = {k: v[key] for k, v in d.items()}
+        fields = dataclass_quick_asdict(self)
         if isinstance(key, slice):
-            return dataclasses.replace(self, **item)
+            return dataclasses.replace(self, **{k: v[key] for k, v in fields.items()})
         assert isinstance(key, (int, np.integer))
-        return item
+        return {k: v[key] for k, v in fields.items()}
 
     def to_device(self, device, dtype=th.float32) -> Dict[str, th.Tensor]:
-        """All numeric fields as contiguous device tensors (one H2D copy each)."""
+        """All numeric fields as contiguous device tensors (one H2D copy each); floats and bools
+        become ``dtype``, integers keep their type."""
         out: Dict[str, th.Tensor] = {}
         for f in dataclasses.fields(self):
             v = getattr(self, f.name)
             if f.name == "infos" or isinstance(v, DictObs):
                 continue
-            arr = np.asarray(v)
-            t = th.as_tensor(np.ascontiguousarray(arr))
-            if t.dtype == th.bool:
-                t = t.to(dtype)
-            elif t.is_floating_point():
+            t = th.as_tensor(np.ascontiguousarray(np.asarray(v)))
+            if t.dtype == th.bool or t.is_floating_point():
                 t = t.to(dtype)
             out[f.name] = t.to(device, non_blocking=True)
         return out
@@ -335,18 +354,19 @@ class Transitions(TransitionsMinimal):
     next_obs: Observation
     dones: np.ndarray
 
+    _RULES = (
+        (lambda s: s.obs.shape != s.next_obs.shape,
+         lambda s: f"obs and next_obs must have same shape: {s.obs.shape} != {s.next_obs.shape}"),
+        (lambda s: s.obs.dtype != s.next_obs.dtype,
+         lambda s: f"obs and next_obs must have the same dtype: {s.obs.dtype} != {s.next_obs.dtype}"),
+        (lambda s: s.dones.shape != (len(s.acts),),
+         lambda s: f"dones must be 1D array, one entry for each timestep: {s.dones.shape} != ({len(s.acts)},)"),
+        (lambda s: s.dones.dtype != bool, lambda s: f"dones must be boolean, not {s.dones.dtype}"),
+    )
+
     def __post_init__(self):
         super().__post_init__()
-        if self.obs.shape != self.next_obs.shape:
-            raise ValueError(f"obs and next_obs must have same shape: {self.obs.shape} != {self.next_obs.shape}")
-        if self.obs.dtype != self.next_obs.dtype:
-            raise ValueError(f"obs and next_obs must have the same dtype: {self.obs.dtype} != {self.next_obs.dtype}")
-        if self.dones.shape != (len(self.acts),):
-            raise ValueError(
-                f"dones must be 1D array, one entry for each timestep: {self.dones.shape} != ({len(self.acts)},)"
-            )
-        if self.dones.dtype != bool:
-            raise ValueError(f"dones must be boolean, not {self.dones.dtype}")
+        _enforce(self, Transitions._RULES)
 
 
 @dataclasses.dataclass(frozen=True)
@@ -357,4 +377,4 @@ class TransitionsWithRew(Transitions):
 
     def __post_init__(self):
         super().__post_init__()
-        _rews_validation(self.rews, self.acts)
+        _enforce(self, _REW_RULES)
