@@ -555,49 +555,24 @@ class _DeviceEpochRunner:
         self.graphs = None  # captured by the next _run, after the eager warm-up step
 
     def _capture(self) -> None:
-        """The step graphs of every size in ``_sizes``. IMITATION_AMD_BC_GRAPH_PAIR=1 captures two instances of each and
-        alternates them (an A/B knob: a relaunch of an exec whose previous launch is still running
-        waits for it on the host; round 5 measured the pair SLOWER on DAgger-Pong, 176-186 vs
-        146-164 ms per round, `profiles/r5_dagger.md`)."""
+        """The step graphs of every size in ``_sizes``, captured once (alternating two instances per
+        size, or waiting on the previous launch's event before a relaunch, measured slower on
+        DAgger-Pong in round 5, ``profiles/r5_dagger.md``)."""
         self.graphs = {}
         side = getattr(self, "_capture_stream", None)
         if side is None:  # (creating a stream costs ~1 ms of host time)
             side = self._capture_stream = th.cuda.Stream()
         side.wait_stream(th.cuda.current_stream())
-        import os
-
-        copies = 2 if os.environ.get("IMITATION_AMD_BC_GRAPH_PAIR", "0") == "1" else 1
         for k in self._sizes:
-            gs = []
-            for _ in range(copies):
-                g = th.cuda.CUDAGraph()
-                with graphs.capture(g, stream=side):
-                    for _ in range(k):
-                        self._one_step()
-                gs.append(g)
-            self.graphs[k] = gs
+            g = th.cuda.CUDAGraph()
+            with graphs.capture(g, stream=side):
+                for _ in range(k):
+                    self._one_step()
+            self.graphs[k] = g
         th.cuda.current_stream().wait_stream(side)
-        self._turn = {}  # per graph size: the next instance to launch
-        self._done_ev = {}
-        self._wait_prev = os.environ.get("IMITATION_AMD_BC_GRAPH_WAIT", "0") == "1"
 
     def _replay(self, k: int) -> None:
-        gs = self.graphs[k]
-        i = self._turn.get(k, 0) % len(gs)
-        if self._wait_prev:
-            # a relaunch of an exec whose previous launch still runs blocks inside
-            # hipGraphLaunch -- and holds up the statistics thread's launches meanwhile (1.5-3 ms
-            # per launch in the round-5 API trace). Wait for that launch on its event instead,
-            # outside the runtime; with two instances the other one keeps the GPU busy.
-            ev = self._done_ev.get((k, i))
-            if ev is not None:
-                ev.synchronize()
-        gs[i].replay()
-        if self._wait_prev:
-            ev = th.cuda.Event()
-            ev.record()
-            self._done_ev[(k, i)] = ev
-        self._turn[k] = i + 1
+        self.graphs[k].replay()
 
     def _run(self, steps: int) -> None:
         if steps > 0 and not getattr(self, "_warm", False):

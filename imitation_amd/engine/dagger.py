@@ -489,13 +489,6 @@ class DeviceDAggerCollector:
     def _step_cnn(self, k: int, b: Dict) -> None:
         C = self._C
         ea, la = self._actors
-        if getattr(self, "_learner_only", False):
-            # statistics twin: the learner alone acts (BC's RolloutStatsComputer runs the policy
-            # without the expert), no expert forward and no frame / label records
-            C.cnn_head(la.hidden(self.obs), self.learner.action_net.weight, self.learner.action_net.bias, 1,
-                       self._head_seed, self._head_ctr, self._a_rob)
-            C.dagger_env_step(self._env_args(0, k, self._a_rob, b))
-            return
         if self._pair:
             h_e, h_l = CnnActor.hidden_pair(ea, la, self.obs)
         else:
@@ -698,9 +691,6 @@ class DeviceDAggerCollector:
             twin = DeviceDAggerCollector(self.venv, self.expert, snap, self.rng, chunk=self.chunk, use_graph=self.use_graph)
             if self.cnn:
                 twin._head_seed = self._head_seed
-                # IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY=1: the learner-alone step (no expert forward);
-                # measured no faster than the paired step with beta 0 (round 5, call AO), so opt-in
-                twin._learner_only = os.environ.get("IMITATION_AMD_DAGGER_TWIN_LEARNER_ONLY", "0") == "1"
             # its chunk graphs are captured here, on the calling thread (the worker thread only
             # replays them: no capture may overlap another thread's work): one eager + captured
             # chunk per buffer set, on throw-away env state (overwritten by every start)
@@ -709,11 +699,8 @@ class DeviceDAggerCollector:
                 twin._run_chunk(b)
             th.cuda.synchronize(self.device)
             self._twin = twin
-            # the epoch's end waits ~33 ms per round for the statistics chain (round 5, call AI), but
-            # a high-priority stream for it measured much slower (call AJ: 17.1-18.3K vs 23.8-28.4K
-            # env-steps/s): opt-in only (IMITATION_AMD_DAGGER_STATS_PRIORITY=1)
-            hi = os.environ.get("IMITATION_AMD_DAGGER_STATS_PRIORITY", "0") == "1"
-            self._twin_stream = th.cuda.Stream(device=self.device, priority=-1 if hi else 0)
+            # (a high-priority stream for the statistics chain measured much slower, round 5 call AJ)
+            self._twin_stream = th.cuda.Stream(device=self.device)
         return twin
 
     def start_rollout_stats(self, n_episodes: int) -> StatsFuture:

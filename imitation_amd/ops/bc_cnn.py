@@ -67,9 +67,6 @@ class FusedCnnBCStep:
         dev = self.flat.device
         self.metrics = th.zeros(8, device=dev)
         self.ws = th.zeros(int(self.C.bc_head_workspace(self.flat.numel())), device=dev)  # word 0: counter
-        import os
-
-        self._mask_dx = os.environ.get("IMITATION_AMD_BC_MASK_DX", "0") == "1"
 
     @staticmethod
     def maybe(policy, optimizer, obs, ent_weight: float, l2_weight: float) -> Optional["FusedCnnBCStep"]:
@@ -135,55 +132,22 @@ class FusedCnnBCStep:
             a = acts.reshape(-1).long().contiguous()
             dh = C.bc_head_train(out, head.weight.detach(), head.bias.detach(), a, self.flat, self.g_head[0], self.g_head[1],
                                  self.metrics, self.ws, self.ent_weight, self.l2_weight)
-            # IMITATION_AMD_BC_MASK_DX=1: the top conv's ReLU mask is applied once, in the FC's dX
-            # store (xf is that conv's post-ReLU output), and its dgrad / wgrad read a masked dZ
-            # (same values; round 5 PMC: those kernels are VALU-issue bound). Opt-in until measured
-            pre = self._mask_dx
-            _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1], mask_dx=pre)
+            _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1])
             dz = dx.view(hs[-1].shape)
-            # weight-gradient partials per layer; their reductions in ONE launch at the end. Each
-            # layer's wgrad runs on a stream of its own, beside the data-gradient chain it does not
-            # feed (in a captured graph: parallel branches), joined before the reduction
+            # weight-gradient partials per layer; their fixed-order reductions in ONE launch at the end
             red = {k: [] for k in ("x", "dy", "kh", "kw", "s", "p", "slab", "dw", "db")}
-            main = th.cuda.current_stream(x.device)
-            sides = self._side_streams(x.device)
             for i in range(n - 1, -1, -1):
                 c = convs[i]
                 inp = x if i == 0 else hs[i - 1]
-                top = i == n - 1 and not pre  # (relu_out: mask dZ in the loads)
+                top = i == n - 1  # relu_out: the top conv's ReLU mask is applied to dZ in the loads
                 kh, kw, st = int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0])
-                if sides:
-                    sd = sides[i]
-                    sd.wait_stream(main)
-                    for t in (inp, dz, hs[i]):
-                        t.record_stream(sd)
-                    with th.cuda.stream(sd):
-                        slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
-                    slab.record_stream(main)
-                else:
-                    slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
+                slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
                 for k, v in zip(red, (inp, dz, kh, kw, st, 0, slab, self.g_conv[i][0], self.g_conv[i][1])):
                     red[k].append(v)
                 if i > 0:
                     dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], st, top, True, 0)
-            for sd in sides:
-                main.wait_stream(sd)
             C.conv_reduce_multi(*red.values())
         return self.metrics
-
-    def _side_streams(self, device) -> List[th.cuda.Stream]:
-        """One stream per conv layer for its weight-gradient partials -- opt-in
-        (IMITATION_AMD_BC_CNN_STREAMS=1): a HIP-graph replay of the multi-stream capture crashed
-        the process once in a GPU test run (round 5), so by default everything stays on the
-        current stream."""
-        import os
-
-        if os.environ.get("IMITATION_AMD_BC_CNN_STREAMS", "0") != "1":
-            return []
-        ss = getattr(self, "_sides", None)
-        if ss is None:
-            ss = self._sides = [th.cuda.Stream(device=device) for _ in self.convs]
-        return ss
 
 
 def metrics_fields(m: th.Tensor) -> Dict[str, Any]:

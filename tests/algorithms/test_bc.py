@@ -394,34 +394,3 @@ def test_bc_raises_when_the_data_loader_runs_dry(cartpole_venv, expert_transitio
     with pytest.raises(AssertionError, match=".*no data.*"):
         tr.train(n_batches=20, on_batch_end=on_batch_end)
     assert n_batches == no_yield_after_iter
-
-
-@pytest.mark.gpu
-def test_fused_cnn_bc_step_masked_dx_is_bitwise_the_per_load_mask(monkeypatch):
-    """The top conv's ReLU mask applied once in the FC's dX store (IMITATION_AMD_BC_MASK_DX=1)
-    gives bitwise the metrics and gradients of masking every dZ load (=0)."""
-    import torch as th
-
-    from imitation_amd.envs.vec_env import native_spaces
-    from imitation_amd.ops import bc_cnn
-    from imitation_amd.ops import optim as optim_ops
-    from imitation_amd.rl.policies import ActorCriticCnnPolicy
-
-    obs_space, act_space = native_spaces("PongNoFrameskip-v4")
-    g = th.Generator().manual_seed(3)
-    obs = th.randint(0, 256, (32, 84, 84, 4), generator=g, dtype=th.uint8).cuda()
-    acts = th.randint(0, act_space.n, (32,), generator=g).cuda()
-    out = []
-    for mode in ("0", "1"):
-        monkeypatch.setenv("IMITATION_AMD_BC_MASK_DX", mode)
-        th.manual_seed(0)
-        pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
-        opt = optim_ops.FusedAdam(pol.parameters(), lr=1e-3)
-        step = bc_cnn.FusedCnnBCStep.maybe(pol, opt, obs, 1e-3, 0.0)
-        assert step is not None and step._mask_dx == (mode == "1")
-        opt.zero_grad()
-        m = step(obs, acts).clone()
-        out.append((m, [p.grad.detach().clone() for p in pol.parameters()]))
-    (m0, g0), (m1, g1) = out
-    assert th.equal(m0, m1)
-    assert all(th.equal(a, b) for a, b in zip(g0, g1))

@@ -202,10 +202,10 @@ def test_device_rollout_stats_match_host_keys(tmp_path):
 
 
 @gpu
-@pytest.mark.parametrize("n_epochs,n_batches,log_interval,kmax,pairwait",
-                         [(2, None, 3, "16", False), (None, 11, 4, "5", False), (None, 7, 500, "16", False),
-                          (3, None, 500, "3", False), (3, None, 4, "2", True)])
-def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batches, log_interval, kmax, pairwait):
+@pytest.mark.parametrize("n_epochs,n_batches,log_interval,kmax",
+                         [(2, None, 3, "16"), (None, 11, 4, "5"), (None, 7, 500, "16"), (3, None, 500, "3"),
+                          (3, None, 4, "2")])
+def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batches, log_interval, kmax):
     """BC over a device demonstration aggregate (DAgger's device collector) with whole runs of
     minibatches per HIP-graph replay (algorithms/bc.py ``_DeviceEpochRunner``, graph sizes kmax then
     powers of two below it): the same batches, kernels and order as the per-minibatch graphed loop,
@@ -224,9 +224,6 @@ def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batc
     acts = th.randint(0, int(venv.action_space.n), (n_rows,), generator=g, device="cuda")
     runs = []
     monkeypatch.setenv("IMITATION_AMD_BC_GRAPH_K", kmax)
-    if pairwait:  # two alternating instances per graph size, each relaunch after its last launch's event
-        monkeypatch.setenv("IMITATION_AMD_BC_GRAPH_PAIR", "1")
-        monkeypatch.setenv("IMITATION_AMD_BC_GRAPH_WAIT", "1")
     for mode in ("0", "1"):
         monkeypatch.setenv("IMITATION_AMD_BC_EPOCH_GRAPH", mode)
         th.manual_seed(11)
