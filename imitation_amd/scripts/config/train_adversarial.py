@@ -25,6 +25,9 @@ def defaults():
     )
     algorithm_specific = {}  # algorithm_specific[<command>] is merged into the config
     checkpoint_interval = 0  # rounds between checkpoints (<0 disables)
+    full_checkpoint_interval = 0  # rounds between FULL trainer checkpoints for exact resume (0 disables)
+    full_checkpoint_keep = 3  # newest full checkpoints kept
+    resume_from = None  # directory of full checkpoints (a previous run's log_dir/full_checkpoints) to resume from
     agent_path = None  # warm-start generator from this model
     engine = "auto"  # "device": whole GAIL / AIRL round on the GPU (engine/{gail,airl}.py); "host": reference loop
 

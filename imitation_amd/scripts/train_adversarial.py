@@ -103,11 +103,55 @@ def _make_trainer(algo_cls, engine: str, **kwargs) -> common.AdversarialTrainer:
     return trainer
 
 
+def train_rounds(trainer, total_timesteps: int, callback, full_checkpoint_interval: int = 0,
+                 resume_from: Optional[str] = None, full_checkpoint_dir: Optional[str] = None,
+                 full_checkpoint_keep: int = 3) -> int:
+    """``trainer.train(total_timesteps, callback)`` with full-state checkpoints for exact resume
+    (the reference snapshots only the reward net and policy,
+    ``src/imitation/scripts/train_adversarial.py:25-35,157``).
+
+    Every ``full_checkpoint_interval`` rounds the whole trainer state (parameters, optimiser
+    moments, normalisers, replay ring, demo sampler, env state, RNG streams, device-engine state)
+    goes to ``full_checkpoint_dir/ckpt-<rounds>`` (:class:`~imitation_amd.utils.checkpoint.CheckpointManager`:
+    atomic, newest ``full_checkpoint_keep`` kept, one directory per DP rank). ``resume_from``
+    restores the newest checkpoint every rank has there and trains only the remaining rounds.
+    The rounds run as ``train()`` calls of at most ``full_checkpoint_interval`` rounds, which is
+    bitwise the single call (the engines drain their pipeline at the end of each call); the
+    callback sees the global round index. Returns the number of rounds restored."""
+    from imitation_amd.utils.checkpoint import CheckpointManager
+
+    per_round = trainer.gen_train_timesteps
+    n_rounds = total_timesteps // per_round
+    if full_checkpoint_interval <= 0 and not resume_from:
+        trainer.train(total_timesteps, callback)
+        return 0
+    assert n_rounds >= 1, "No updates (need at least gen_train_timesteps transitions)"
+    start = 0
+    if resume_from:
+        start = CheckpointManager(resume_from, keep=full_checkpoint_keep).restore_latest(trainer)
+        logger.info(f"Resumed from {resume_from} after {start} rounds")
+    mgr = None
+    if full_checkpoint_interval > 0:
+        mgr = CheckpointManager(full_checkpoint_dir or resume_from, keep=full_checkpoint_keep)
+    seg = full_checkpoint_interval if full_checkpoint_interval > 0 else n_rounds
+    r = start
+    while r < n_rounds:
+        k = min(seg - r % seg, n_rounds - r)
+        trainer.train(k * per_round, None if callback is None else (lambda i, _base=r: callback(_base + i)))
+        r += k
+        if mgr is not None and (r % seg == 0 or r == n_rounds):
+            mgr.save(trainer, r, meta=dict(total_timesteps=total_timesteps, rounds=n_rounds))
+    return start
+
+
 @train_adversarial_ex.capture
 def train_adversarial(_run, show_config: bool, algo_cls: Type[common.AdversarialTrainer],
                       algorithm_kwargs: Mapping[str, Any], total_timesteps: int, checkpoint_interval: int,
-                      agent_path: Optional[str], engine: str = "auto") -> Mapping[str, Mapping[str, float]]:
-    """Checkpoints go to ``{log_dir}/checkpoints/{round|final}/{reward_train,reward_test}.pt`` and ``gen_policy/``."""
+                      agent_path: Optional[str], engine: str = "auto", full_checkpoint_interval: int = 0,
+                      full_checkpoint_keep: int = 3, resume_from: Optional[str] = None) -> Mapping[str, Mapping[str, float]]:
+    """Checkpoints go to ``{log_dir}/checkpoints/{round|final}/{reward_train,reward_test}.pt`` and ``gen_policy/``;
+    full-state checkpoints (``full_checkpoint_interval`` > 0) to ``{log_dir}/full_checkpoints`` and
+    ``resume_from=<dir>`` continues from the newest one (:func:`train_rounds`)."""
     total_timesteps = int(total_timesteps)
     checkpoint_interval = int(checkpoint_interval)
     pdist.init()
@@ -133,7 +177,8 @@ def train_adversarial(_run, show_config: bool, algo_cls: Type[common.Adversarial
                 if checkpoint_interval > 0 and round_num % checkpoint_interval == 0:
                     save(trainer, log_dir / "checkpoints" / f"{round_num:05d}")
 
-            trainer.train(total_timesteps, callback)
+            train_rounds(trainer, total_timesteps, callback, int(full_checkpoint_interval), resume_from,
+                         str(log_dir / "full_checkpoints"), int(full_checkpoint_keep))
             wd.beat()
             imit_stats = policy_evaluation.eval_trainer(trainer, trainer.venv_train)
     if checkpoint_interval >= 0:

@@ -1,0 +1,101 @@
+"""Exact resume from the CLIs (VERDICT r5 missing #2).
+
+Run N rounds with full checkpoints, stop ("kill"), run again with ``resume_from`` for 2N rounds
+in total: the final reward net, generator and evaluation equal those of 2N uninterrupted
+rounds -- exactly on the host loop (CPU) and bitwise on the device engine (GPU). The reference
+only snapshots the reward net / policy (``src/imitation/scripts/train_adversarial.py:25-35,157``),
+so a crashed run restarts from zero there.
+"""
+
+import glob
+import os
+
+import pytest
+import torch as th
+
+FAST_ENV = ["environment.fast", "policy_evaluation.fast"]
+
+
+@pytest.fixture(autouse=True)
+def _chdir(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+
+
+def _final_params(log_root):
+    from imitation_amd.rewards import serialize as reward_serialize
+    from imitation_amd.rl.save_util import load_from_zip_file
+
+    (rew,) = glob.glob(os.path.join(log_root, "**", "checkpoints", "final", "reward_train.pt"), recursive=True)
+    net = reward_serialize.load_reward_net(rew, device="cpu")
+    out = {f"reward.{k}": v.detach().cpu() for k, v in net.state_dict().items()}
+    (zp,) = glob.glob(os.path.join(log_root, "**", "checkpoints", "final", "gen_policy", "model.zip"), recursive=True)
+    _, params, _ = load_from_zip_file(zp, device="cpu")
+
+    def flat(prefix, x):
+        if isinstance(x, th.Tensor):
+            out[prefix] = x.detach().cpu()
+        elif isinstance(x, dict):
+            for n, v in x.items():
+                flat(f"{prefix}.{n}", v)
+        elif isinstance(x, (list, tuple)):
+            for i, v in enumerate(x):
+                flat(f"{prefix}.{i}", v)
+
+    flat("gen", params)  # policy weights and optimizer moments
+    return out
+
+
+def _full_ckpts(log_root):
+    return sorted(glob.glob(os.path.join(log_root, "**", "full_checkpoints", "ckpt-*"), recursive=True))
+
+
+def _adversarial(tmp_path, name, command, named, updates):
+    from imitation_amd.scripts.train_adversarial import train_adversarial_ex
+
+    root = str(tmp_path / name)
+    run = train_adversarial_ex.run(command, named_configs=named,
+                                   config_updates={"logging": {"log_root": root}, "seed": 0, **updates})
+    assert run.status == "COMPLETED"
+    return root, run.result
+
+
+def _check_resume(tmp_path, command, named, updates, per_round, n):
+    full, res_full = _adversarial(tmp_path, "full", command, named, dict(updates, total_timesteps=2 * n * per_round))
+    first, _ = _adversarial(tmp_path, "first", command, named,
+                            dict(updates, total_timesteps=n * per_round, full_checkpoint_interval=2))
+    ck = _full_ckpts(first)
+    assert [os.path.basename(c) for c in ck][-1] == f"ckpt-{n:010d}"
+    resumed, res_resumed = _adversarial(tmp_path, "resumed", command, named,
+                                        dict(updates, total_timesteps=2 * n * per_round, full_checkpoint_interval=2,
+                                             resume_from=os.path.dirname(ck[-1])))
+    a, b = _final_params(full), _final_params(resumed)
+    assert a.keys() == b.keys()
+    for k in a:
+        assert th.equal(a[k], b[k]), f"{k} differs after resume"
+    assert res_full["imit_stats"] == res_resumed["imit_stats"]
+    return res_full
+
+
+@pytest.mark.parametrize("command", ["gail", "airl"])
+def test_train_adversarial_resume_is_exact_on_host(tmp_path, command):
+    named = ["fast", "demonstrations.fast", "rl.fast", *FAST_ENV]
+    # rl.fast: 2 envs x 1 step = 2 env steps per round; 4 rounds, then 4 more after the restart
+    _check_resume(tmp_path, command, named, dict(engine="host"), per_round=2, n=4)
+
+
+def test_full_checkpoints_keep_newest(tmp_path):
+    named = ["fast", "demonstrations.fast", "rl.fast", *FAST_ENV]
+    root, _ = _adversarial(tmp_path, "keep", "gail", named,
+                           dict(engine="host", total_timesteps=2 * 10, full_checkpoint_interval=2, full_checkpoint_keep=2))
+    assert [os.path.basename(c) for c in _full_ckpts(root)] == ["ckpt-0000000008", "ckpt-0000000010"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("command", ["gail", "airl"])
+def test_train_adversarial_resume_is_bitwise_on_device(tmp_path, command):
+    named = ["demonstrations.fast", "policy_evaluation.fast"]
+    updates = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
+                   expert=dict(policy_type="random", loader_kwargs={}),
+                   rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
+                   algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=-1)
+    _check_resume(tmp_path, command, named, updates, per_round=1024, n=4)
