@@ -1299,6 +1299,8 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
         if pdist.world_size() > 1:  # every replica starts from rank 0's reward model
             pdist.broadcast_module(reward_model)
         self._iteration = 0
+        self._completed_iterations = 0  # iterations of the current train() call done (checkpoint state)
+        self._resume_at = 0  # set by a checkpoint restore: the next train() skips this many iterations
         self.model = reward_model
         self.rng = rng
         any_default = None in (preference_gatherer, fragmenter, reward_trainer)
@@ -1368,7 +1370,13 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
         print(f"Query schedule: {schedule}")
         timesteps_per_iteration, extra_timesteps = divmod(total_timesteps, self.num_iterations)
         reward_loss = reward_accuracy = None
+        # resumed from a checkpoint taken after iteration `start` - 1 (utils/checkpoint.py): the
+        # schedule is recomputed identically and the finished iterations are skipped
+        start, self._resume_at = (self._resume_at if self._resume_at < len(schedule) else 0), 0
+        self._completed_iterations = start
         for i, num_pairs in enumerate(schedule):
+            if i < start:
+                continue
             num_steps = math.ceil(self.transition_oversampling * 2 * num_pairs * self.fragment_length)
             self.logger.log(f"Collecting {2 * num_pairs} fragments ({num_steps} transitions)")
             with profiling.range("pref/sample"):
@@ -1406,7 +1414,8 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
             if check is not None:
                 check(blocking=i == len(schedule) - 1)
             self.logger.dump(self._iteration)
+            self._completed_iterations = i + 1
+            self._iteration += 1  # before the callback: a checkpoint taken there resumes at the next iteration
             if callback:
-                callback(self._iteration)
-            self._iteration += 1
+                callback(self._iteration - 1)
             yield {"reward_loss": reward_loss, "reward_accuracy": reward_accuracy}

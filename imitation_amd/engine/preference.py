@@ -336,6 +336,24 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
         st.update(step0=int(self._step0), seed=int(self._seed), explore_random=bool(self._explore_random))
         return st
 
+    def buffer_state(self) -> Dict[str, Any]:
+        """The host-side episode cutter between iterations: finished trajectories not yet
+        sampled, per-env partial segments, the learned-reward episode returns in flight."""
+        from imitation_amd.utils import checkpoint
+
+        return {"finished": [checkpoint.traj_state(t) for t in self._finished],
+                "partial": [[tuple(th.as_tensor(np.ascontiguousarray(x)) for x in seg) for seg in segs]
+                            for segs in self._partial],
+                "n_since_pop": int(self._n_since_pop), "wrapped_ret": th.as_tensor(self._wrapped_ret.copy())}
+
+    def load_buffer_state(self, st: Dict[str, Any]) -> None:
+        from imitation_amd.utils import checkpoint
+
+        self._finished = [checkpoint.traj_load(t) for t in st["finished"]]
+        self._partial = [[tuple(x.numpy() for x in seg) for seg in segs] for segs in st["partial"]]
+        self._n_since_pop = st["n_since_pop"]
+        self._wrapped_ret = st["wrapped_ret"].numpy().copy()
+
     def load_engine_state(self, st: Dict[str, Any]) -> None:
         with th.no_grad():
             for k in self._ENGINE_TENSORS:

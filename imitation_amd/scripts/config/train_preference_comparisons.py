@@ -38,6 +38,9 @@ def train_defaults():
     trajectory_generator_kwargs = {}
     allow_variable_horizon = False
     checkpoint_interval = 0
+    full_checkpoint_interval = 0  # iterations between FULL trainer checkpoints for exact resume (0 disables)
+    full_checkpoint_keep = 3  # newest full checkpoints kept
+    resume_from = None  # directory of full checkpoints (a previous run's log_dir/full_checkpoints) to resume from
     query_schedule = "hyperbolic"
 
 

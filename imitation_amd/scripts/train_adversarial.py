@@ -177,13 +177,16 @@ def train_adversarial(_run, show_config: bool, algo_cls: Type[common.Adversarial
                 if checkpoint_interval > 0 and round_num % checkpoint_interval == 0:
                     save(trainer, log_dir / "checkpoints" / f"{round_num:05d}")
 
-            train_rounds(trainer, total_timesteps, callback, int(full_checkpoint_interval), resume_from,
-                         str(log_dir / "full_checkpoints"), int(full_checkpoint_keep))
+            resumed_rounds = train_rounds(trainer, total_timesteps, callback, int(full_checkpoint_interval),
+                                          resume_from, str(log_dir / "full_checkpoints"), int(full_checkpoint_keep))
             wd.beat()
             imit_stats = policy_evaluation.eval_trainer(trainer, trainer.venv_train)
     if checkpoint_interval >= 0:
         save(trainer, log_dir / "checkpoints" / "final")
-    return {"imit_stats": imit_stats, "expert_stats": rollout.rollout_stats(expert_trajs), "engine": trainer.engine_kind}
+    out = {"imit_stats": imit_stats, "expert_stats": rollout.rollout_stats(expert_trajs), "engine": trainer.engine_kind}
+    if resume_from:
+        out["resumed_rounds"] = resumed_rounds
+    return out
 
 
 @train_adversarial_ex.command

@@ -79,9 +79,13 @@ def train_preference_comparisons(total_timesteps: int, total_comparisons: int, n
                                  active_selection_oversampling: int, uncertainty_on: str,
                                  fragmenter_kwargs: Mapping[str, Any], allow_variable_horizon: bool,
                                  checkpoint_interval: int, query_schedule: Union[str, Any],
-                                 _rnd: np.random.Generator, engine: str = "auto") -> Mapping[str, Any]:
+                                 _rnd: np.random.Generator, engine: str = "auto", full_checkpoint_interval: int = 0,
+                                 full_checkpoint_keep: int = 3, resume_from: Optional[str] = None) -> Mapping[str, Any]:
     """Reward learning from synthetic (or dataset) preferences; returns final reward loss/accuracy
-    and, when an agent is trained, its rollout statistics."""
+    and, when an agent is trained, its rollout statistics. ``full_checkpoint_interval`` > 0 writes
+    the whole trainer state every that many iterations to ``{log_dir}/full_checkpoints``
+    (:class:`~imitation_amd.utils.checkpoint.CheckpointManager`); ``resume_from=<dir>`` restores the
+    newest one and runs only the remaining iterations of the schedule."""
     total_timesteps, total_comparisons, num_iterations = int(total_timesteps), int(total_comparisons), int(num_iterations)
     comparison_queue_size = int(comparison_queue_size) if comparison_queue_size is not None else None
     fragment_length = int(fragment_length)
@@ -121,16 +125,31 @@ def train_preference_comparisons(total_timesteps: int, total_comparisons: int, n
             initial_comparison_frac=initial_comparison_frac, custom_logger=custom_logger,
             allow_variable_horizon=allow_variable_horizon, query_schedule=query_schedule)
 
+        from imitation_amd.utils.checkpoint import CheckpointManager
+
+        full_checkpoint_interval = int(full_checkpoint_interval)
+        resumed = None
+        if resume_from:
+            resumed = CheckpointManager(resume_from, keep=int(full_checkpoint_keep)).restore_latest(main_trainer)
+            logger.info(f"Resumed from {resume_from} after {resumed} iterations")
+        full_mgr = (CheckpointManager(str(log_dir / "full_checkpoints"), keep=int(full_checkpoint_keep))
+                    if full_checkpoint_interval > 0 else None)
+
         with watchdog.cli_watchdog("train_preference_comparisons") as wd:
             def save_callback(iteration_num):
                 wd.beat()
                 if checkpoint_interval > 0 and iteration_num % checkpoint_interval == 0:
                     save_checkpoint(main_trainer, log_dir / "checkpoints" / f"{iteration_num:04d}",
                                     allow_save_policy=trajectory_path is None)
+                done = main_trainer._completed_iterations
+                if full_mgr is not None and done % full_checkpoint_interval == 0:
+                    full_mgr.save(main_trainer, done)
 
             results = dict(main_trainer.train(total_timesteps, total_comparisons, callback=save_callback))
             wd.beat()
             results["engine"] = getattr(trajectory_generator, "engine_kind", "dataset")
+            if resumed is not None:
+                results["resumed_iterations"] = resumed
             if trajectory_path is None:
                 results["imit_stats"] = policy_evaluation.eval_policy(agent, venv)
     if save_preferences:

@@ -275,9 +275,95 @@ def load_adversarial_state(trainer, st: Dict[str, Any]) -> None:
     determinism.restore_rng_state(st["rng"])
 
 
+_PC_RNG_PATHS = ("rng", "fragmenter.rng", "fragmenter.base_fragmenter.rng", "preference_gatherer.rng",
+                 "reward_trainer.rng", "trajectory_generator.rng", "trajectory_generator.exploration_wrapper.rng")
+
+
+def _pc_generators(pc) -> List[Any]:
+    """``(path, np.random.Generator)`` of every component of a preference-comparisons trainer
+    that draws from one (the CLI shares ONE generator among them: it is saved once per path and
+    restored to the same state each time)."""
+    out = []
+    for path in _PC_RNG_PATHS:
+        obj = pc
+        for part in path.split("."):
+            obj = getattr(obj, part, None)
+        if isinstance(obj, np.random.Generator):
+            out.append((path, obj))
+    for i, t in enumerate(getattr(pc.reward_trainer, "member_trainers", ()) or ()):
+        if isinstance(getattr(t, "rng", None), np.random.Generator):
+            out.append((f"reward_trainer.member_trainers.{i}.rng", t.rng))
+    return out
+
+
+def _infos_state(infos):
+    return None if infos is None else {"__json_objects__": json.dumps([_py(e) for e in list(infos)])}
+
+
+def _infos_load(st):
+    return None if st is None else np.array(json.loads(st["__json_objects__"]) or [], dtype=object)
+
+
+def traj_state(t) -> Dict[str, Any]:
+    """A :class:`~imitation_amd.data.types.TrajectoryWithRew` as plain tensors (+ JSON infos)."""
+    from imitation_amd.data import types
+
+    if isinstance(t.obs, types.DictObs):
+        raise TypeError("dict observations cannot be checkpointed here")
+    return {"obs": _to_cpu(np.asarray(t.obs)), "acts": _to_cpu(np.asarray(t.acts)), "rews": _to_cpu(np.asarray(t.rews)),
+            "terminal": bool(t.terminal), "infos": _infos_state(t.infos)}
+
+
+def traj_load(st: Dict[str, Any]):
+    from imitation_amd.data import types
+
+    return types.TrajectoryWithRew(obs=st["obs"].numpy(), acts=st["acts"].numpy(), rews=st["rews"].numpy(),
+                                   terminal=st["terminal"], infos=_infos_load(st["infos"]))
+
+
+def _step_state(step: Dict[str, Any]) -> Dict[str, Any]:
+    return {k: (_infos_state([v])) if k == "infos" else _to_cpu(np.asarray(v)) for k, v in step.items()}
+
+
+def _step_load(st: Dict[str, Any]) -> Dict[str, Any]:
+    return {k: (_infos_load(v)[0] if k == "infos" else v.numpy()) for k, v in st.items()}
+
+
+def buffering_state(bw) -> Dict[str, Any]:
+    """Everything a :class:`~imitation_amd.data.wrappers.BufferingWrapper` carries across
+    ``learn()`` calls: per-env partial trajectories (step dicts), finished trajectories not yet
+    popped, episode counters."""
+    acc = bw._traj_accum
+    return {"partial": None if acc is None else {int(k): [_step_state(d) for d in v]
+                                                  for k, v in acc.partial_trajectories.items()},
+            "finished": [traj_state(t) for t in bw._trajectories], "ep_lens": [int(x) for x in bw._ep_lens],
+            "n_transitions": int(bw.n_transitions), "init_reset": bool(bw._init_reset),
+            "timesteps": None if bw._timesteps is None else th.as_tensor(np.asarray(bw._timesteps, dtype=np.int64))}
+
+
+def load_buffering_state(bw, st: Dict[str, Any]) -> None:
+    from imitation_amd.data import rollout
+
+    if st["partial"] is None:
+        bw._traj_accum = None
+    else:
+        bw._traj_accum = rollout.TrajectoryAccumulator()
+        for k, steps in st["partial"].items():
+            for d in steps:
+                bw._traj_accum.add_step(_step_load(d), key=int(k))
+    bw._trajectories = [traj_load(t) for t in st["finished"]]
+    bw._ep_lens = list(st["ep_lens"])
+    bw.n_transitions = st["n_transitions"]
+    bw._init_reset = st["init_reset"]
+    bw._timesteps = None if st["timesteps"] is None else st["timesteps"].numpy().astype(int)
+    bw._saved_acts = None
+
+
 def preference_state(pc, side_dir: str) -> Dict[str, Any]:
-    """State of :class:`~imitation_amd.algorithms.preference_comparisons.PreferenceComparisons`;
-    the comparison dataset goes to ``side_dir/dataset.npz``."""
+    """State of :class:`~imitation_amd.algorithms.preference_comparisons.PreferenceComparisons`
+    after a whole iteration; the comparison dataset goes to ``side_dir/dataset.npz``. The agent's
+    trajectories in flight (finished ones not yet sampled, per-env partial ones) are part of it:
+    the next iteration samples them. ``completed`` = iterations done (resume skips them)."""
     from imitation_amd.algorithms import preference_comparisons as pcm
 
     rt = pc.reward_trainer
@@ -285,16 +371,27 @@ def preference_state(pc, side_dir: str) -> Dict[str, Any]:
     st: Dict[str, Any] = {
         "format": "imitation_amd.preference_comparisons.v1",
         "iteration": int(pc._iteration),
+        "completed": int(pc._completed_iterations),
         "model": _to_cpu(pc.model.state_dict()),
         "reward_optims": [_to_cpu(t.optim.state_dict()) for t in trainers],
         "rng": determinism.capture_rng_state(),
         "pc_rng": None if pc.rng is None else determinism.generator_state(pc.rng),
+        "component_rngs": {path: determinism.generator_state(g) for path, g in _pc_generators(pc)},
         "dataset_len": len(pc.dataset),
     }
     gen = pc.trajectory_generator
     if isinstance(gen, pcm.AgentTrainer):
         st["agent"] = rl_algo_state(gen.algorithm)
         st["env"] = env_state(gen.venv)
+        st["episode_rewards"] = [float(x) for x in gen.reward_venv_wrapper.episode_rewards]
+        ew = getattr(gen, "exploration_wrapper", None)
+        if ew is not None:
+            st["explore_random"] = bool(ew.current_policy == ew._random_policy)
+        if hasattr(gen, "engine_state"):  # device agent: Adam / env state on the GPU, host-side episode cutter
+            st["agent_engine"] = gen.engine_state()
+            st["agent_buffer"] = gen.buffer_state()
+        else:
+            st["agent_buffer"] = buffering_state(gen.buffering_wrapper)
     if len(pc.dataset):
         pc.dataset.save(os.path.join(side_dir, "dataset.npz"))
     return st
@@ -311,16 +408,34 @@ def load_preference_state(pc, st: Dict[str, Any], side_dir: str) -> None:
     for t, s in zip(trainers, st["reward_optims"]):
         t.optim.load_state_dict(s)
     pc._iteration = st["iteration"]
+    pc._completed_iterations = st.get("completed", st["iteration"])
+    pc._resume_at = pc._completed_iterations  # the next train() continues the interrupted schedule
     gen = pc.trajectory_generator
     if "agent" in st and isinstance(gen, pcm.AgentTrainer):
         env_ok = load_env_state(gen.venv, st.get("env"))
         load_rl_algo_state(gen.algorithm, st["agent"], env_restored=env_ok)
+        if "episode_rewards" in st:
+            er = gen.reward_venv_wrapper.episode_rewards
+            er.clear()
+            er.extend(st["episode_rewards"])
+        ew = getattr(gen, "exploration_wrapper", None)
+        if ew is not None and "explore_random" in st:
+            ew.current_policy = ew._random_policy if st["explore_random"] else ew.wrapped_policy
+        if "agent_engine" in st and hasattr(gen, "load_engine_state"):
+            gen.load_engine_state(st["agent_engine"])
+            gen.load_buffer_state(st["agent_buffer"])
+        elif "agent_buffer" in st:
+            load_buffering_state(gen.buffering_wrapper, st["agent_buffer"])
     if st["dataset_len"]:
         ds = pcm.PreferenceDataset.load(os.path.join(side_dir, "dataset.npz"))
         ds.max_size = pc.dataset.max_size
         pc.dataset = ds
     if pc.rng is not None and st["pc_rng"] is not None:
         determinism.set_generator_state(pc.rng, st["pc_rng"])
+    saved = st.get("component_rngs", {})
+    for path, g in _pc_generators(pc):
+        if path in saved:
+            determinism.set_generator_state(g, saved[path])
     determinism.restore_rng_state(st["rng"])
 
 

@@ -68,6 +68,7 @@ def _check_resume(tmp_path, command, named, updates, per_round, n):
     resumed, res_resumed = _adversarial(tmp_path, "resumed", command, named,
                                         dict(updates, total_timesteps=2 * n * per_round, full_checkpoint_interval=2,
                                              resume_from=os.path.dirname(ck[-1])))
+    assert res_resumed["resumed_rounds"] == n  # restored, not re-run from scratch
     a, b = _final_params(full), _final_params(resumed)
     assert a.keys() == b.keys()
     for k in a:
@@ -99,3 +100,56 @@ def test_train_adversarial_resume_is_bitwise_on_device(tmp_path, command):
                    rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
                    algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=-1)
     _check_resume(tmp_path, command, named, updates, per_round=1024, n=4)
+
+
+def _preference(tmp_path, name, updates):
+    from imitation_amd.scripts.train_preference_comparisons import train_preference_comparisons_ex
+
+    root = str(tmp_path / name)
+    run = train_preference_comparisons_ex.run(named_configs=["fast", "rl.fast", *FAST_ENV],
+                                              config_updates={"logging": {"log_root": root}, "seed": 0, **updates})
+    assert run.status == "COMPLETED"
+    return root, run.result
+
+
+def _pref_final(root):
+    from imitation_amd.rewards import serialize as reward_serialize
+
+    (rew,) = glob.glob(os.path.join(root, "**", "checkpoints", "final", "reward_net.pt"), recursive=True)
+    return {k: v.detach().cpu() for k, v in reward_serialize.load_reward_net(rew, device="cpu").state_dict().items()}
+
+
+def _check_pref_resume(tmp_path, updates, kill_after):
+    import shutil
+
+    full, res_full = _preference(tmp_path, "full", dict(updates, full_checkpoint_interval=1, full_checkpoint_keep=10))
+    ck = [c for c in _full_ckpts(full) if c.endswith(f"ckpt-{kill_after:010d}")]
+    assert len(ck) == 1
+    killed = tmp_path / "killed_run"  # the run "died" after `kill_after` iterations: only that checkpoint exists
+    shutil.copytree(ck[0], killed / os.path.basename(ck[0]))
+    resumed, res_resumed = _preference(tmp_path, "resumed", dict(updates, resume_from=str(killed)))
+    assert res_resumed["resumed_iterations"] == kill_after  # restored, not re-run from scratch
+    a, b = _pref_final(full), _pref_final(resumed)
+    for k in a:
+        assert th.equal(a[k], b[k]), f"{k} differs after resume"
+    assert res_full["reward_loss"] == res_resumed["reward_loss"]
+    assert res_full["reward_accuracy"] == res_resumed["reward_accuracy"]
+    if "imit_stats" in res_full:
+        assert res_full["imit_stats"] == res_resumed["imit_stats"]
+
+
+@pytest.mark.parametrize("kill_after", [1, 2])
+def test_train_preference_comparisons_resume_is_exact_on_host(tmp_path, kill_after):
+    # 3 iterations + the initial one: iterations 0..3; the agent's trajectories in flight (finished
+    # but not sampled, partial episodes) are part of the checkpoint
+    _check_pref_resume(tmp_path, dict(engine="host", num_iterations=3, total_timesteps=60, total_comparisons=8),
+                       kill_after)
+
+
+@pytest.mark.gpu
+def test_train_preference_comparisons_resume_is_bitwise_on_device(tmp_path):
+    updates = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
+                   rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
+                   total_timesteps=4 * 1024, total_comparisons=16, num_iterations=3, fragment_length=20,
+                   reward_trainer_kwargs=dict(epochs=1), checkpoint_interval=-1)
+    _check_pref_resume(tmp_path, updates, 2)
