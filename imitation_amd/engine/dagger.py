@@ -796,6 +796,32 @@ class DeviceDAggerCollector:
                 out[f"{name}_{stat}"] = getattr(np, stat)(vals).item()
         return out
 
+    # -------------------------------------------------------------- checkpoint
+    def engine_state(self) -> Dict[str, Any]:
+        """Env state on the device and the learner head's sampling stream (full-trainer
+        checkpoints, :func:`imitation_amd.utils.checkpoint.dagger_state`). Taken between rounds:
+        nothing is in flight then."""
+        st: Dict[str, Any] = {k: getattr(self, k).detach().cpu().clone() for k in self._ENV_TENSORS}
+        st["steps_collected"] = int(self.steps_collected)
+        if self.cnn:
+            st["head_ctr"] = self._head_ctr.cpu().clone()
+            st["head_seed"] = int(self._head_seed)
+        return st
+
+    def load_engine_state(self, st: Dict[str, Any]) -> None:
+        with th.no_grad():
+            for k in self._ENV_TENSORS:
+                getattr(self, k).copy_(st[k].to(self.device))
+            if self.cnn:
+                self._head_ctr.copy_(st["head_ctr"].to(self.device))
+        self.steps_collected = st["steps_collected"]
+        if self.cnn:
+            self._head_seed = st["head_seed"]
+            twin = getattr(self, "_twin", None)
+            if twin is not None:
+                twin._head_seed = self._head_seed
+        self.sync_env_to_host()
+
     def sync_env_to_host(self) -> None:
         st = {"state": self.state.cpu().numpy(), "rng": self.env_rng.cpu().numpy(),
               "elapsed": self.elapsed.cpu().numpy().astype(np.int64)}

@@ -439,6 +439,73 @@ def load_preference_state(pc, st: Dict[str, Any], side_dir: str) -> None:
     determinism.restore_rng_state(st["rng"])
 
 
+AGGREGATE_FILE = "dagger_aggregate.pt"
+
+
+def dagger_state(tr, side_dir: str) -> Dict[str, Any]:
+    """State of a DAgger trainer between rounds (reference ``dagger.py:521-552`` saves the
+    trainer object; this is the pickle-free full state): the learner and its optimiser moments,
+    the round, the beta schedule's input, every RNG stream, the env state, BC's log counters.
+
+    Demonstrations: the host path re-reads the round files of its scratch dir (as the
+    reference's ``reconstruct_trainer`` does); the device path's aggregate -- its rows in append
+    order, which the BC loader's permutations index -- goes to ``side_dir/dagger_aggregate.pt``,
+    with the device collector's env state and sampling counter."""
+    bct = tr.bc_trainer
+    st: Dict[str, Any] = {
+        "format": "imitation_amd.dagger_full.v1",
+        "round_num": int(tr.round_num),
+        "rng": determinism.generator_state(tr.rng),
+        "bc_rng": determinism.generator_state(bct.rng) if isinstance(getattr(bct, "rng", None), np.random.Generator) else None,
+        "policy": _to_cpu(bct.policy.state_dict()),
+        "optimizer": _to_cpu(bct.optimizer.state_dict()),
+        "bc_log": [int(bct._bc_logger._tensorboard_step), int(bct._bc_logger._current_epoch)],
+        "env": env_state(tr.venv),
+        "global_rng": determinism.capture_rng_state(),
+    }
+    col = getattr(tr, "_device_collector", None)
+    if col is not None:
+        tr.flush_demos()
+        agg = tr._device_agg
+        th.save({"obs": agg.obs[: agg.n].cpu(), "acts": agg.acts[: agg.n].cpu()} if agg.n else {},
+                os.path.join(side_dir, AGGREGATE_FILE))
+        st["device"] = {"n": int(agg.n), "counts": {str(k): int(v) for k, v in tr._device_counts.items()},
+                        "collector": col.engine_state(), "loaded_through": int(tr._store.loaded_through)}
+    return st
+
+
+def load_dagger_state(tr, st: Dict[str, Any], side_dir: str) -> None:
+    if st.get("format") != "imitation_amd.dagger_full.v1":
+        raise ValueError(f"not a DAgger checkpoint: {st.get('format')}")
+    bct = tr.bc_trainer
+    bct.policy.load_state_dict(st["policy"])
+    bct.optimizer.load_state_dict(st["optimizer"])
+    tr.round_num = st["round_num"]
+    determinism.set_generator_state(tr.rng, st["rng"])
+    if st["bc_rng"] is not None and isinstance(getattr(bct, "rng", None), np.random.Generator):
+        determinism.set_generator_state(bct.rng, st["bc_rng"])
+    bct._bc_logger._tensorboard_step, bct._bc_logger._current_epoch = st["bc_log"]
+    load_env_state(tr.venv, st.get("env"))
+    dev = st.get("device")
+    col = getattr(tr, "_device_collector", None)
+    if dev is not None:
+        if col is None:
+            raise ValueError("checkpoint of a device-collector DAgger run; this trainer collects on the host")
+        from imitation_amd.engine import dagger as dagger_engine
+
+        agg = dagger_engine.DeviceDemoAggregate(tr._device_agg.device)
+        if dev["n"]:
+            rows = th.load(os.path.join(side_dir, AGGREGATE_FILE), map_location="cpu", weights_only=True)
+            agg.append(rows["obs"].to(agg.device), rows["acts"].to(agg.device), gather=False)
+        tr._device_agg = agg
+        tr._device_counts = {int(k): v for k, v in dev["counts"].items()}
+        tr._store.loaded_through = dev["loaded_through"]
+        col.load_engine_state(dev["collector"])
+    else:  # host path: the next update re-reads every round's demo files from the scratch dir
+        tr._store.trajectories, tr._store._flat, tr._store.loaded_through = [], None, -1
+    determinism.restore_rng_state(st["global_rng"])
+
+
 def trainer_state(trainer, side_dir: str) -> Dict[str, Any]:
     from imitation_amd.algorithms import preference_comparisons as pcm
     from imitation_amd.algorithms.adversarial import common
@@ -452,7 +519,11 @@ def trainer_state(trainer, side_dir: str) -> Dict[str, Any]:
     if isinstance(trainer, BaseAlgorithm):
         return {"format": "imitation_amd.rl.v1", "algo": rl_algo_state(trainer), "env": env_state(trainer.env),
                 "rng": determinism.capture_rng_state()}
-    raise TypeError(f"no checkpoint support for {type(trainer).__name__} (BC/DAgger: see dagger.save_trainer)")
+    from imitation_amd.algorithms import dagger
+
+    if isinstance(trainer, dagger.DAggerTrainer):
+        return dagger_state(trainer, side_dir)
+    raise TypeError(f"no checkpoint support for {type(trainer).__name__}")
 
 
 def load_trainer_state(trainer, st: Dict[str, Any], side_dir: str) -> None:
@@ -461,6 +532,8 @@ def load_trainer_state(trainer, st: Dict[str, Any], side_dir: str) -> None:
         load_adversarial_state(trainer, st)
     elif fmt == "imitation_amd.preference_comparisons.v1":
         load_preference_state(trainer, st, side_dir)
+    elif fmt == "imitation_amd.dagger_full.v1":
+        load_dagger_state(trainer, st, side_dir)
     elif fmt == "imitation_amd.rl.v1":
         env_ok = load_env_state(trainer.env, st.get("env"))
         load_rl_algo_state(trainer, st["algo"], env_restored=env_ok)
@@ -479,7 +552,7 @@ def save_checkpoint(trainer, path: str, meta: Optional[Dict[str, Any]] = None) -
         st = trainer_state(trainer, tmp)
         th.save(st, os.path.join(tmp, STATE_FILE))
         m = {"format": st["format"]}
-        for k in ("global_step", "disc_step", "iteration"):
+        for k in ("global_step", "disc_step", "iteration", "round_num"):
             if k in st:
                 m[k] = st[k]
         m.update(meta or {})
