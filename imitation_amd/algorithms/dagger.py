@@ -559,15 +559,19 @@ class SimpleDAggerTrainer(DAggerTrainer):
 
     @gcfreeze.during
     def train(self, total_timesteps: int, *, rollout_round_min_episodes: int = 3, rollout_round_min_timesteps: int = 500,
-              bc_train_kwargs: Optional[dict] = None) -> None:
-        """Run rounds until ``total_timesteps`` env steps (all ranks) have been collected."""
+              bc_train_kwargs: Optional[dict] = None,
+              round_callback: Optional[Callable[[int, int], None]] = None) -> None:
+        """Run rounds until ``total_timesteps`` env steps (all ranks) have been collected.
+        ``round_callback(round_num, collected)`` runs after every round (``round_num`` = rounds
+        done, ``collected`` = env steps of this call so far): the CLI's full checkpoints."""
         try:
-            self._train_rounds(total_timesteps, rollout_round_min_episodes, rollout_round_min_timesteps, bc_train_kwargs)
+            self._train_rounds(total_timesteps, rollout_round_min_episodes, rollout_round_min_timesteps, bc_train_kwargs,
+                               round_callback)
         finally:
             self.land_frames()  # the trajectories handed out are complete when train() returns (or raises)
 
     def _train_rounds(self, total_timesteps: int, rollout_round_min_episodes: int, rollout_round_min_timesteps: int,
-                      bc_train_kwargs: Optional[dict]) -> None:
+                      bc_train_kwargs: Optional[dict], round_callback=None) -> None:
         collected = 0
         local = 0
         rounds = 0
@@ -591,5 +595,7 @@ class SimpleDAggerTrainer(DAggerTrainer):
             with profiling.range("dagger/bc_update"):
                 self.extend_and_update(bc_train_kwargs)
             rounds += 1
+            if round_callback is not None:
+                round_callback(self.round_num, collected)
         self.last_train_timesteps = collected  # all ranks
         self.last_train_timesteps_local = local

@@ -16,7 +16,10 @@ train_imitation_ex = Experiment("train_imitation", ingredients=[
 
 @train_imitation_ex.config
 def config():
-    dagger = dict(use_offline_rollouts=False, total_timesteps=1e5, beta_schedule=None)
+    dagger = dict(use_offline_rollouts=False, total_timesteps=1e5, beta_schedule=None,
+                  # rounds between FULL trainer checkpoints ({log_dir}/full_checkpoints; 0 disables), newest kept,
+                  # and a previous run's full_checkpoints dir to resume from (its scratch dir is reused)
+                  full_checkpoint_interval=0, full_checkpoint_keep=3, resume_from=None)
 
 
 @train_imitation_ex.named_config

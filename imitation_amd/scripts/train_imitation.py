@@ -22,6 +22,7 @@ from imitation_amd.scripts.ingredients import demonstrations, environment, exper
 from imitation_amd.scripts.ingredients import logging as logging_ingredient
 from imitation_amd.scripts.ingredients import policy_evaluation
 from imitation_amd.util import util
+from imitation_amd.utils import watchdog
 
 logger = logging.getLogger(__name__)
 
@@ -53,8 +54,30 @@ def bc(bc: Dict[str, Any], _run, _rnd: np.random.Generator) -> Mapping[str, Mapp
 
 @train_imitation_ex.command
 def dagger(bc: Dict[str, Any], dagger: Mapping[str, Any], _run, _rnd: np.random.Generator) -> Mapping[str, Mapping[str, float]]:
-    """DAgger with the expert ingredient's policy as the synthetic teacher."""
+    """DAgger with the expert ingredient's policy as the synthetic teacher.
+
+    ``dagger.full_checkpoint_interval`` > 0 writes the whole trainer state every that many rounds
+    to ``{log_dir}/full_checkpoints`` (:func:`imitation_amd.utils.checkpoint.dagger_state`);
+    ``dagger.resume_from=<dir>`` restores the newest one, reuses that run's scratch dir (the round
+    files the host path re-reads) and collects only the remaining timesteps."""
+    import json
+
+    from imitation_amd.utils.checkpoint import META_FILE, CheckpointManager
+
     custom_logger, log_dir = logging_ingredient.setup_logging()
+    resume_from = dagger.get("resume_from")
+    interval = int(dagger.get("full_checkpoint_interval", 0) or 0)
+    keep = int(dagger.get("full_checkpoint_keep", 3))
+    scratch = osp.join(log_dir, "scratch")
+    resume_meta = None
+    if resume_from:
+        mgr_in = CheckpointManager(resume_from, keep=keep)
+        step = mgr_in.agreed_step()
+        if step is None:
+            raise ValueError(f"resume_from={resume_from!r} holds no full checkpoint")
+        with open(osp.join(mgr_in._rank_dir(step), META_FILE)) as f:
+            resume_meta = json.load(f)
+        scratch = resume_meta["scratch_dir"]
     expert_trajs: Optional[Sequence[types.Trajectory]] = None
     if dagger["use_offline_rollouts"]:
         expert_trajs = demonstrations.get_expert_trajectories()
@@ -65,12 +88,36 @@ def dagger(bc: Dict[str, Any], dagger: Mapping[str, Any], _run, _rnd: np.random.
             kwargs["n_epochs"] = 4
         expert_policy = expert.get_expert_policy(venv)
         dagger_trainer = dagger_algorithm.SimpleDAggerTrainer(
-            venv=venv, scratch_dir=osp.join(log_dir, "scratch"), expert_trajs=expert_trajs, expert_policy=expert_policy,
-            custom_logger=custom_logger, bc_trainer=trainer, beta_schedule=dagger["beta_schedule"], rng=_rnd)
-        dagger_trainer.train(total_timesteps=int(dagger["total_timesteps"]), bc_train_kwargs=kwargs)
+            venv=venv, scratch_dir=scratch, expert_trajs=None if resume_meta else expert_trajs,
+            expert_policy=expert_policy, custom_logger=custom_logger, bc_trainer=trainer,
+            beta_schedule=dagger["beta_schedule"], rng=_rnd)
+        total = int(dagger["total_timesteps"])
+        done = 0
+        if resume_meta is not None:
+            mgr_in.restore_latest(dagger_trainer)
+            done = int(resume_meta["collected"])
+            logger.info(f"Resumed from {resume_from} at round {dagger_trainer.round_num} ({done} timesteps collected)")
+        mgr = CheckpointManager(str(log_dir / "full_checkpoints"), keep=keep) if interval > 0 else None
+
+        def round_callback(round_num: int, collected: int) -> None:
+            if mgr is not None and round_num % interval == 0:
+                mgr.save(dagger_trainer, round_num, meta=dict(collected=done + collected, total_timesteps=total,
+                                                              scratch_dir=str(dagger_trainer.base_scratch_dir)))
+
+        with watchdog.cli_watchdog("train_imitation") as wd:
+            def beat(round_num: int, collected: int) -> None:
+                wd.beat()
+                round_callback(round_num, collected)
+
+            if total - done > 0:
+                dagger_trainer.train(total_timesteps=total - done, bc_train_kwargs=kwargs, round_callback=beat)
+            wd.beat()
         print(f"Model saved to {dagger_trainer.save_trainer()}")
         imit_stats = policy_evaluation.eval_policy(trainer.policy, venv)
-    return _collect_stats(imit_stats, dagger_trainer._all_demos)
+    out = _collect_stats(imit_stats, dagger_trainer._all_demos)
+    if resume_meta is not None:
+        out["resumed_round"] = int(resume_meta["step"])
+    return out
 
 
 @train_imitation_ex.command

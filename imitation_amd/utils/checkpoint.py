@@ -80,18 +80,29 @@ def _unwrap_native(venv):
     return None
 
 
+_PENDING_SEEDS = "__pending_seeds__"
+
+
 def env_state(venv) -> Optional[Dict[str, th.Tensor]]:
+    """Native env state, plus the seeds ``venv.seed()`` queued for the next ``reset()`` (-1 =
+    none): a fresh env built for the restore has its own queued seeds, which would otherwise
+    override the restored RNG at the first reset."""
     nat = _unwrap_native(venv)
     if nat is None:
         return None
-    return {k: th.as_tensor(v) for k, v in nat.get_state().items()}
+    st = {k: th.as_tensor(v) for k, v in nat.get_state().items()}
+    st[_PENDING_SEEDS] = th.tensor([-1 if s is None else int(s) for s in nat._seeds], dtype=th.int64)
+    return st
 
 
 def load_env_state(venv, st: Optional[Dict[str, th.Tensor]]) -> bool:
     nat = _unwrap_native(venv)
     if nat is None or st is None:
         return False
+    st = dict(st)
+    pending = st.pop(_PENDING_SEEDS, None)
     nat.set_state({k: v.numpy() for k, v in st.items()})
+    nat._seeds = [None] * nat.num_envs if pending is None else [None if int(s) < 0 else int(s) for s in pending]
     return True
 
 
@@ -503,6 +514,12 @@ def load_dagger_state(tr, st: Dict[str, Any], side_dir: str) -> None:
         col.load_engine_state(dev["collector"])
     else:  # host path: the next update re-reads every round's demo files from the scratch dir
         tr._store.trajectories, tr._store._flat, tr._store.loaded_through = [], None, -1
+    # demo files of the round that was in progress (and any later one) when the run stopped are
+    # stale: that round is collected again
+    r = tr.round_num
+    while tr._store.round_dir(r).is_dir():
+        shutil.rmtree(tr._store.round_dir(r))
+        r += 1
     determinism.restore_rng_state(st["global_rng"])
 
 

@@ -348,7 +348,9 @@ def test_full_checkpoint_resume_is_exact_on_host(tmp_path, pendulum_venv):
     b.train(1, **kw)
     ck = checkpoint.save_checkpoint(b, str(tmp_path / "ck"))
     assert json.load(open(os.path.join(ck, "meta.json")))["round_num"] == 1
-    c = _pendulum_trainer(tmp_path / "b", pendulum_venv, expert, seed=99)
+    # a fresh env too (its own seeds queued for the first reset): the env state comes from the checkpoint
+    venv2 = util.make_vec_env("Pendulum-v1", rng=np.random.default_rng(42), n_envs=pendulum_venv.num_envs)
+    c = _pendulum_trainer(tmp_path / "b", venv2, expert, seed=99)
     checkpoint.load_checkpoint(c, ck)
     assert c.round_num == 1
     c.train(1, **kw)

@@ -153,3 +153,50 @@ def test_train_preference_comparisons_resume_is_bitwise_on_device(tmp_path):
                    total_timesteps=4 * 1024, total_comparisons=16, num_iterations=3, fragment_length=20,
                    reward_trainer_kwargs=dict(epochs=1), checkpoint_interval=-1)
     _check_pref_resume(tmp_path, updates, 2)
+
+
+def _dagger(tmp_path, name, dagger_cfg):
+    from imitation_amd.scripts.train_imitation import train_imitation_ex
+
+    root = str(tmp_path / name)
+    run = train_imitation_ex.run("dagger", named_configs=["fast", "demonstrations.fast", *FAST_ENV],
+                                 config_updates={"logging": {"log_root": root}, "seed": 0,
+                                                 "bc": {"train_kwargs": {"n_batches": 8}},
+                                                 "dagger": dict(total_timesteps=1500, **dagger_cfg)})
+    assert run.status == "COMPLETED"
+    return root, run.result
+
+
+def _dagger_policy(root):
+    (p,) = glob.glob(os.path.join(root, "**", "scratch", "policy-latest.pt"), recursive=True)
+    out = {}
+
+    def flat(prefix, x):
+        if isinstance(x, th.Tensor):
+            out[prefix] = x.clone()
+        elif isinstance(x, dict):
+            for k, v in x.items():
+                flat(f"{prefix}.{k}", v)
+
+    flat("policy", th.load(p, map_location="cpu", weights_only=True))
+    return out
+
+
+def test_train_imitation_dagger_resume_is_exact_on_host(tmp_path):
+    """3 DAgger rounds (>= 500 steps each) with a full checkpoint per round; a run that "died"
+    after round 1 resumes from it (reusing its scratch dir's round files) and ends where the
+    uninterrupted run did."""
+    import shutil
+
+    full, res_full = _dagger(tmp_path, "full", dict(full_checkpoint_interval=1, full_checkpoint_keep=10))
+    want = _dagger_policy(full)
+    (ck,) = [c for c in _full_ckpts(full) if c.endswith("ckpt-0000000001")]
+    killed = tmp_path / "killed_run"
+    shutil.copytree(ck, killed / os.path.basename(ck))
+    resumed, res_resumed = _dagger(tmp_path, "resumed", dict(resume_from=str(killed)))
+    assert res_resumed["resumed_round"] == 1
+    got = _dagger_policy(full)  # the resumed run trains on in the original run's scratch dir
+    assert want and want.keys() == got.keys()
+    for k in want:
+        assert th.equal(want[k], got[k]), f"{k} differs after resume"
+    assert res_full["imit_stats"] == res_resumed["imit_stats"]
