@@ -80,19 +80,20 @@ def spawn_ranks(n: int) -> int:
     return _spawn(n, __file__, sys.argv[1:], label="bench.py")
 
 
-def fill_expert_cache(args) -> bool:
+def fill_expert_cache(args):
     """Train the expert (or find it cached) in a CHILD process on this rank's GPU, before this
     process touches the GPU: the measuring process then only loads the cached demonstrations, as
     a warm-cache run does (hosting the 5M-step expert run in the same process left the timed
     rounds ~25% slower, ``profiles/r6_bench_quality.md``). The child runs without a process group
-    (one GPU, the same seed on every rank; the demonstrations' seed differs by rank)."""
+    (one GPU, the same seed on every rank; the demonstrations' seed differs by rank). Returns
+    whether the child found the cache filled already (None: no child ran, or it failed)."""
     import subprocess
 
     from imitation_amd.parallel.launch import count_gpus
 
     n = count_gpus()
     if n < 1:
-        return False
+        return None
     rank = int(os.environ.get("RANK", "0"))
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
                                                                "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK")}
@@ -100,18 +101,21 @@ def fill_expert_cache(args) -> bool:
            "--seed", str(args.seed), "--expert-steps", str(args.expert_steps), "--n-eval", str(args.eval_episodes),
            "--rank", str(rank), "--n-envs", str(args.n_envs), "--device", f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % n}",
            "--cache-dir", args.expert_cache]
-    p = subprocess.run(cmd, env=env, cwd=os.path.dirname(os.path.abspath(__file__)), stdout=sys.stderr)
+    p = subprocess.run(cmd, env=env, cwd=os.path.dirname(os.path.abspath(__file__)), stdout=subprocess.PIPE, text=True)
+    sys.stderr.write(p.stdout)
     if p.returncode:
         print(f"bench.py: expert child exited {p.returncode}; the expert trains in this process instead", file=sys.stderr)
-    return p.returncode == 0
+        return None
+    return "cached=True" in p.stdout
 
 
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
+    child_cached = None
     if args.quality_steps > 0 and args.eval_episodes > 0 and args.engine != "host" and args.expert_cache:
-        fill_expert_cache(args)
+        child_cached = fill_expert_cache(args)
     import torch as th
 
     from imitation_amd.parallel import dist as pdist
@@ -190,7 +194,8 @@ def main():
         qual = dict(expert_return=round(ex_r, 3), random_return=round(rnd_r, 3),
                     normalized_score=round(normalized_score(eval_return, rnd_r, ex_r), 4),
                     imitation_env_steps_per_rank=done + rest, expert_env_steps=args.expert_steps,
-                    expert_cached=bool(expert["cached"]), expert_train_s=round(float(expert["expert_train_s"]), 3),
+                    expert_cached=bool(expert["cached"] if child_cached is None else child_cached),
+                    expert_in_child_process=child_cached is not None, expert_train_s=round(float(expert["expert_train_s"]), 3),
                     eval_episodes=args.eval_episodes)
         eval_return = round(eval_return, 3)
     elif args.eval_episodes > 0:  # outside the timed region: mean return of the trained generator

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import dataclasses
 import itertools
+import math
 from typing import Any, Callable, Dict, Iterable, Iterator, List, Mapping, Optional, Tuple, Type, Union
 
 import numpy as np
@@ -205,6 +206,12 @@ class BCLogger:
         vals = {k: v for k, v in training_metrics.__dict__.items()}
         tens = [v.detach().reshape(-1)[0] for v in vals.values() if v is not None]
         host = th.stack(tens).tolist() if tens else []
+        bad = [k for k, x in zip((k for k, v in vals.items() if v is not None), host) if not math.isfinite(x)]
+        if bad:  # the values are on the host already: fail fast instead of logging NaN for the rest of the run
+            from imitation_amd.utils.watchdog import NonFiniteError
+
+            raise NonFiniteError(f"non-finite BC metrics at batch {batch_num} (epoch {self._current_epoch}): "
+                                 f"{', '.join(bad)}")
         it = iter(host)
         for k, v in vals.items():
             self._logger.record(f"bc/{k}", float(next(it)) if v is not None else None)
@@ -588,7 +595,39 @@ class _DeviceEpochRunner:
                 self._replay(k)
                 steps -= k
 
+    def _finite_flag(self, epoch: int, steps: int) -> None:
+        """Fail fast on NaN/Inf BC metrics without a sync per epoch: one reduction over the epoch's
+        metric rows lands in pinned memory asynchronously; it is read one epoch later (long done by
+        then) and at the end of :meth:`train`."""
+        self._check_finite_flag(blocking=False)
+        if not hasattr(self, "_flag_host"):
+            self._flag_host = th.zeros(1, dtype=th.int32, pin_memory=True)
+        self._flag_host.copy_(th.isfinite(self.all[:steps]).all().to(th.int32).reshape(1), non_blocking=True)
+        ev = th.cuda.Event()
+        ev.record()
+        self._flag_pending = (epoch, ev)
+
+    def _check_finite_flag(self, blocking: bool) -> None:
+        pend = getattr(self, "_flag_pending", None)
+        if pend is None:
+            return
+        epoch, ev = pend
+        if not blocking and not ev.query():
+            return
+        ev.synchronize()
+        self._flag_pending = None
+        if not int(self._flag_host[0]):
+            from imitation_amd.utils.watchdog import NonFiniteError
+
+            raise NonFiniteError(f"non-finite BC metrics (loss / entropy / log-prob) in epoch {epoch} of this train() call")
+
     def train(self, n_epochs, n_batches, on_epoch_end, log_interval: int, compute_rollout_stats) -> None:
+        try:
+            self._train(n_epochs, n_batches, on_epoch_end, log_interval, compute_rollout_stats)
+        finally:
+            self._check_finite_flag(blocking=True)
+
+    def _train(self, n_epochs, n_batches, on_epoch_end, log_interval: int, compute_rollout_stats) -> None:
         t = self.trainer
         B = self.B
         batch_num = 0  # minibatches stepped in this call (the reference loop's batch_num)
@@ -638,6 +677,7 @@ class _DeviceEpochRunner:
                 raise
             if pending is not None:
                 pending[1]()
+            self._finite_flag(epoch, steps)
             batch_num += steps
             # the reference's batch iterator reaches an epoch's end callback only when it is
             # asked for a batch after the epoch's last one

@@ -618,7 +618,7 @@ class CrossEntropyRewardLoss(RewardLoss):
             loss, probs = preference_model.loss_and_probs(fragment_pairs, prefs_np)
         else:  # scoring only (ensembles are trained member by member)
             probs, _ = preference_model(fragment_pairs)
-            loss = th.nn.functional.binary_cross_entropy(probs, th.as_tensor(prefs_np, device=probs.device)[:, None]
+            loss = th.nn.functional.binary_cross_entropy(pref_ops._finite_probs(probs), th.as_tensor(prefs_np, device=probs.device)[:, None]
                                                          .expand_as(probs))
         preferences_th = th.as_tensor(prefs_np, device=probs.device)
         metrics = {"accuracy": ((probs.detach() > 0.5) == (preferences_th > 0.5).reshape((-1,) + (1,) * (probs.ndim - 1)))
@@ -1402,6 +1402,10 @@ class PreferenceComparisons(base.BaseImitationAlgorithm):
             assert f"{base_key}/accuracy" in self.logger.name_to_value
             reward_loss = self.logger.name_to_value[f"{base_key}/loss"]
             reward_accuracy = self.logger.name_to_value[f"{base_key}/accuracy"]
+            if not math.isfinite(float(reward_loss)):  # already a host float: fail fast, no extra sync
+                from imitation_amd.utils.watchdog import NonFiniteError
+
+                raise NonFiniteError(f"non-finite reward-model loss in preference iteration {i}: {reward_loss}")
             steps = timesteps_per_iteration + (extra_timesteps if i == self.num_iterations - 1 else 0)
             with self.logger.accumulate_means("agent"):
                 self.logger.log(f"Training agent for {steps} timesteps")

@@ -29,8 +29,18 @@ def bradley_terry_probs_reference(r1: torch.Tensor, r2: torch.Tensor, discount: 
     return noise * 0.5 + (1 - noise) * (1 / (1 + diff.exp()))
 
 
+def _finite_probs(probs: torch.Tensor) -> torch.Tensor:
+    """``F.binary_cross_entropy`` rejects NaN inputs with a RuntimeError on the CPU and a
+    device-side assert on the GPU; a NaN reward model raises ``NonFiniteError`` here instead."""
+    if not bool(torch.isfinite(probs).all()):
+        from imitation_amd.utils.watchdog import NonFiniteError
+
+        raise NonFiniteError("non-finite preference probabilities: the reward model's output is NaN/Inf")
+    return probs
+
+
 def bradley_terry_reference(r1, r2, prefs, discount: float = 1.0, threshold: float = 50.0, noise: float = 0.0):
-    probs = bradley_terry_probs_reference(r1, r2, discount, threshold, noise)
+    probs = _finite_probs(bradley_terry_probs_reference(r1, r2, discount, threshold, noise))
     return F.binary_cross_entropy(probs, prefs), probs
 
 

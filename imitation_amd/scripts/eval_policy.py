@@ -15,6 +15,7 @@ from imitation_amd.policies.exploration_wrapper import ExplorationWrapper
 from imitation_amd.rewards import reward_wrapper
 from imitation_amd.rewards.serialize import load_reward
 from imitation_amd.scripts.config.eval_policy import eval_policy_ex
+from imitation_amd.utils import watchdog
 from imitation_amd.scripts.config_engine import FileStorageObserver
 from imitation_amd.scripts.ingredients import environment, expert
 from imitation_amd.scripts.ingredients import logging as logging_ingredient
@@ -67,7 +68,8 @@ def eval_policy(eval_n_timesteps: Optional[int], eval_n_episodes: Optional[int],
         if explore_kwargs is not None:
             policy = ExplorationWrapper(policy, venv, rng=_rnd, **explore_kwargs)
             logging.info(f"Wrapped policy in ExplorationWrapper with kwargs {explore_kwargs}")
-        trajs = rollout.generate_trajectories(policy, venv, sample_until, rng=_rnd)
+        with watchdog.cli_watchdog("eval_policy"):  # an evaluation that never ends aborts instead of hanging
+            trajs = rollout.generate_trajectories(policy, venv, sample_until, rng=_rnd)
     if rollout_save_path:
         serialize.save(log_dir / rollout_save_path.replace("{log_dir}/", ""), trajs)
     return rollout.rollout_stats(trajs)

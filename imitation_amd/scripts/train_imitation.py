@@ -46,7 +46,10 @@ def bc(bc: Dict[str, Any], _run, _rnd: np.random.Generator) -> Mapping[str, Mapp
         kwargs = dict(log_rollouts_venv=venv, **bc["train_kwargs"])
         if kwargs["n_epochs"] is None and kwargs["n_batches"] is None:
             kwargs["n_batches"] = 50_000
-        trainer.train(**kwargs)
+        with watchdog.cli_watchdog("train_imitation") as wd:
+            if kwargs.get("on_epoch_end") is None:  # (per epoch: the graphed device epochs call nothing per batch)
+                kwargs["on_epoch_end"] = wd.beat
+            trainer.train(**kwargs)
         util.save_policy(trainer.policy, policy_path=osp.join(log_dir, "final.th"))
         imit_stats = policy_evaluation.eval_policy(trainer.policy, venv)
     return _collect_stats(imit_stats, expert_trajs)
@@ -129,7 +132,11 @@ def sqil(sqil: Mapping[str, Any], policy: Mapping[str, Any], rl: Mapping[str, An
     with environment.make_venv() as venv:
         trainer = sqil_algorithm.SQIL(venv=venv, demonstrations=expert_trajs, policy=policy["policy_cls"],
                                       custom_logger=custom_logger, rl_algo_class=rl["rl_cls"], rl_kwargs=rl["rl_kwargs"])
-        trainer.train(total_timesteps=int(sqil["total_timesteps"]), **sqil["train_kwargs"])
+        with watchdog.cli_watchdog("train_imitation") as wd:
+            train_kwargs = dict(sqil["train_kwargs"])
+            if "callback" not in train_kwargs:
+                train_kwargs["callback"] = watchdog.rl_beat_callback(wd)
+            trainer.train(total_timesteps=int(sqil["total_timesteps"]), **train_kwargs)
         util.save_policy(trainer.policy, policy_path=osp.join(log_dir, "final.th"))
         imit_stats = policy_evaluation.eval_policy(trainer.policy, venv)
     return _collect_stats(imit_stats, expert_trajs)

@@ -24,6 +24,7 @@ from imitation_amd.scripts.config_engine import FileStorageObserver
 from imitation_amd.scripts.ingredients import environment
 from imitation_amd.scripts.ingredients import logging as logging_ingredient
 from imitation_amd.scripts.ingredients import policy_evaluation, rl
+from imitation_amd.utils import watchdog
 
 
 @train_rl_ex.main
@@ -55,7 +56,9 @@ def train_rl(*, total_timesteps: int, normalize_reward: bool, normalize_kwargs: 
         callback = callbacks.CallbackList(callback_objs)
         algo = rl.make_rl_algo(venv) if agent_path is None else rl.load_rl_algo_from_path(agent_path=agent_path, venv=venv)
         algo.set_logger(custom_logger)
-        algo.learn(total_timesteps, callback=callback)
+        with watchdog.cli_watchdog("train_rl") as wd:  # a rollout that never ends (stuck env / kernel) aborts the run
+            callback.callbacks.append(watchdog.rl_beat_callback(wd))
+            algo.learn(total_timesteps, callback=callback)
         if rollout_save_final:
             sample_until = rollout.make_sample_until(rollout_save_n_timesteps, rollout_save_n_episodes)
             data_serialize.save(rollout_dir / "final.npz", rollout.rollout(algo, algo.get_env(), sample_until, rng=_rnd))

@@ -135,3 +135,17 @@ def cli_watchdog(name: str):
 
         return contextlib.nullcontext(_Null())
     return Watchdog(timeout_s=s, name=name)
+
+
+def rl_beat_callback(wd):
+    """An RL ``BaseCallback`` beating ``wd`` at every rollout end (``train_rl`` / SQIL ``learn``)."""
+    from imitation_amd.rl.callbacks import BaseCallback
+
+    class _Beat(BaseCallback):
+        def _on_step(self) -> bool:
+            return True
+
+        def _on_rollout_end(self) -> None:
+            wd.beat()
+
+    return _Beat()

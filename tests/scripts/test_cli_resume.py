@@ -200,3 +200,29 @@ def test_train_imitation_dagger_resume_is_exact_on_host(tmp_path):
     for k in want:
         assert th.equal(want[k], got[k]), f"{k} differs after resume"
     assert res_full["imit_stats"] == res_resumed["imit_stats"]
+
+
+def test_every_training_cli_runs_under_the_hang_watchdog(tmp_path, monkeypatch):
+    """train_imitation (bc / dagger / sqil), train_rl and eval_policy run
+    inside ``cli_watchdog`` (train_adversarial / train_preference_comparisons already did)."""
+    from imitation_amd.utils import watchdog
+
+    used = []
+    real = watchdog.cli_watchdog
+
+    def spy(name):
+        used.append(name)
+        return real(name)
+
+    monkeypatch.setattr(watchdog, "cli_watchdog", spy)
+    from imitation_amd.scripts.eval_policy import eval_policy_ex
+    from imitation_amd.scripts.train_imitation import train_imitation_ex
+    from imitation_amd.scripts.train_rl import train_rl_ex
+
+    upd = {"logging": {"log_root": str(tmp_path / "o")}}
+    for cmd in ("bc", "dagger", "sqil"):
+        assert train_imitation_ex.run(cmd, named_configs=["fast", "demonstrations.fast", *FAST_ENV],
+                                      config_updates=upd).status == "COMPLETED"
+    assert train_rl_ex.run(named_configs=["fast", "rl.fast", *FAST_ENV], config_updates=upd).status == "COMPLETED"
+    assert eval_policy_ex.run(named_configs=["fast"], config_updates=upd).status == "COMPLETED"
+    assert used.count("train_imitation") == 3 and "train_rl" in used and "eval_policy" in used

@@ -9,13 +9,16 @@ with the Python threads listed at each point.
 """
 
 import gc
+import os
 import sys
 import threading
 import time
 
-import torch as th
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from imitation_amd import models
+import torch as th  # noqa: E402
+
+from imitation_amd import models  # noqa: E402
 
 
 def timed(tag, demos=None):
