@@ -13,7 +13,10 @@ config                 one timed step                                      throu
 bc_cartpole            ``BC.train(n_batches=50)`` (batch 32)               samples/s
 gail_halfcheetah       one GAIL round (4096 env steps + PPO + 8 disc)      env-steps/s
 airl_hopper            one AIRL round (8192 env steps + PPO + 16 disc)     env-steps/s
-dagger_pong            one DAgger round (>= 2048 env steps + BC epochs)    env-steps/s
+dagger_pong            one DAgger round at the reference's schedule        env-steps/s
+                       (>= 3 episodes and >= 500 env steps per round,
+                       then 4 BC epochs over the aggregate)
+dagger_pong_1epoch     labelled extra: >= 2048 env steps + ONE BC epoch    env-steps/s
 preference_walker2d    one DRLHP iteration (agent steps + pref. training)  env-steps/s
 =====================  ==================================================  =================
 
@@ -94,7 +97,21 @@ def make_step(name, device, rank, args):
         step.multi = True
         return b, step, "env-steps/s", tr.gen_algo.policy, b.venv
     if name == "dagger_pong":
+        # the reference's SimpleDAggerTrainer.train defaults (src/imitation/algorithms/dagger.py:618-697):
+        # rollout_round_min_episodes=3, rollout_round_min_timesteps=500, BC for DEFAULT_N_EPOCHS = 4
+        # epochs per round (dagger.py:326,491-492); one timed step = one round
         b = models.build(name, device=device, seed=args.seed, rank=rank)
+        tr = b.trainer
+
+        def step():
+            tr.train(1, rollout_round_min_episodes=3, rollout_round_min_timesteps=500,
+                     bc_train_kwargs=dict(n_epochs=tr.DEFAULT_N_EPOCHS, log_interval=10**9, progress_bar=False))
+            return tr.last_train_timesteps_local  # this rank's steps (x world below)
+
+        return b, step, "env-steps/s", tr.policy, b.venv
+    if name == "dagger_pong_1epoch":
+        # labelled extra (rounds 2-5's config): >= --dagger-round-steps env steps per round, ONE BC epoch
+        b = models.build("dagger_pong", device=device, seed=args.seed, rank=rank)
         tr = b.trainer
 
         def step():

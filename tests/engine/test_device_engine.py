@@ -411,7 +411,7 @@ def test_fused_disc_train_logs_and_matches_generic_path_shape():
     assert tr._disc_opt.state[tr._rflat.params[0]]["exp_avg"].data_ptr() == tr._r_m.data_ptr()
 
 
-def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True, init_seed=None):
+def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True, init_seed=None, env_id="seals/Hopper-v1"):
     from imitation_amd.data import rollout
     from imitation_amd.engine.airl import DeviceAIRL
     from imitation_amd.policies.base import NormalizeFeaturesExtractor
@@ -425,8 +425,8 @@ def _setup_airl(n_envs=4, n_steps=64, batch=64, seed=0, normalize_output=True, i
     th.manual_seed(seed)
     np.random.seed(seed)
     rng = np.random.default_rng(seed)
-    venv = make_vec_env("seals/Hopper-v1", rng=rng, n_envs=n_envs)
-    demo_env = make_vec_env("seals/Hopper-v1", rng=np.random.default_rng(7), n_envs=4)
+    venv = make_vec_env(env_id, rng=rng, n_envs=n_envs)
+    demo_env = make_vec_env(env_id, rng=np.random.default_rng(7), n_envs=4)
     demo_env.action_space.seed(7)  # the random demo policy samples from the action space
     demos = rollout.flatten_trajectories(rollout.generate_trajectories(None, demo_env, rollout.make_min_timesteps(1024), rng=rng))
     if init_seed is not None:  # same demonstrations, different initial weights / engine seeds
@@ -542,15 +542,21 @@ def _airl_state(tr, rn):
 
 
 @gpu
-@pytest.mark.parametrize("normalize_output", [True, False])
-def test_device_airl_fused_disc_matches_autograd(normalize_output):
+@pytest.mark.parametrize("normalize_output,env_id", [(True, "seals/Hopper-v1"), (False, "seals/Hopper-v1"),
+                                                     (True, "Pendulum-v1"), (False, "Pendulum-v1")])
+def test_device_airl_fused_disc_matches_autograd(normalize_output, env_id):
     """airl_disc.hip (gather, norm merges, policy log-prob + shaped reward fwd / BCE / bwd, Adam)
     vs AdversarialTrainer.train_disc's autograd path on the SAME rows: reward-net gradients
     within bf16 tolerance, every RunningNorm (policy, base, potential twice) equal, loss and
-    accuracy statistics close; then one full fused step changes the parameters like Adam."""
+    accuracy statistics close; then one full fused step changes the parameters like Adam.
+    Pendulum: continuous actions that the env clips to [-2, 2] -- the replay
+    rows hold the clipped env actions, whose diag-Gaussian log-prob enters the logit
+    ``r - log pi(a|s)`` (reference ``airl.py:114-119``, ``common.py:476-519``); the loss /
+    accuracy statistics are functions of those logits, the gradients of their BCE."""
     from imitation_amd.util import networks
 
-    tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=5, normalize_output=normalize_output)
+    tr, venv, gen, rn = _setup_airl(n_envs=4, n_steps=64, batch=64, seed=5, normalize_output=normalize_output,
+                                    env_id=env_id)
     assert tr._fused_disc, tr._fused_disc_why
     tr.train(tr.gen_train_timesteps)  # replay ring + non-trivial normaliser / optimizer state
     th.cuda.synchronize()
@@ -577,6 +583,8 @@ def test_device_airl_fused_disc_matches_autograd(normalize_output):
     ex = {k: ed[k].index_select(0, e_idx) for k in ("obs", "acts", "next_obs", "dones")}
     ga = tr._gen_dev._arrays
     gs = {k: ga[k].index_select(0, g_idx) for k in ("obs", "acts", "next_obs", "dones")}
+    lo, hi = (th.as_tensor(x, device="cuda", dtype=th.float32) for x in (venv.action_space.low, venv.action_space.high))
+    assert bool(((gs["acts"] >= lo) & (gs["acts"] <= hi)).all())  # the replay holds the env's (clipped) actions
     os.environ["IMITATION_AMD_FUSED"] = "0"  # fp32 PyTorch reference
     try:
         with networks.training(tr.reward_train):

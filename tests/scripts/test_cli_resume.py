@@ -98,7 +98,7 @@ def test_train_adversarial_resume_is_bitwise_on_device(tmp_path, command):
     updates = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
                    expert=dict(policy_type="random", loader_kwargs={}),
                    rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
-                   algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=-1)
+                   algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=0)
     _check_resume(tmp_path, command, named, updates, per_round=1024, n=4)
 
 
@@ -151,7 +151,7 @@ def test_train_preference_comparisons_resume_is_bitwise_on_device(tmp_path):
     updates = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
                    rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
                    total_timesteps=4 * 1024, total_comparisons=16, num_iterations=3, fragment_length=20,
-                   reward_trainer_kwargs=dict(epochs=1), checkpoint_interval=-1)
+                   reward_trainer_kwargs=dict(epochs=1), checkpoint_interval=0)
     _check_pref_resume(tmp_path, updates, 2)
 
 
