@@ -30,6 +30,9 @@
 // columns; fragments past K read as zero too.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
+#include "ia/adam.h"
 #include "ia/mfma.h"
 #include "launchers.h"
 
@@ -695,6 +698,69 @@ __global__ __launch_bounds__(256) void conv_reduce_multi_kernel(ConvReduceMulti 
   }
 }
 
+// conv_reduce_multi with the optimizer step fused (ConvReduceAdam, launchers.h): blockIdx.y < n
+// reduces layer y's slab column i exactly as conv_reduce_multi_kernel does and, instead of storing
+// the gradient, applies the Adam element update (ia/adam.h, as adam_flat) to that weight / bias and
+// writes the new weight's bf16 forward / data-gradient images; blockIdx.y == n runs the plain Adam
+// over the tail range (gradients written by earlier launches of the step) and the metrics append.
+__global__ __launch_bounds__(256) void conv_reduce_adam_kernel(ConvReduceAdam a) {
+  const int l = blockIdx.y;
+  float step_size, bc2_sqrt;
+  adam_scalars(*a.step, a.h.lr, a.h.beta1, a.h.beta2, step_size, bc2_sqrt);
+  if (l == a.r.n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < a.tail_n) {
+      const int64_t o = a.tail_off + i;
+      float p = a.params[o], mm = a.m[o], vv = a.v[o];
+      adam_elem(p, a.grads[o], mm, vv, a.h, step_size, bc2_sqrt);
+      a.params[o] = p;
+      a.m[o] = mm;
+      a.v[o] = vv;
+      a.grads[o] = 0.f;
+    }
+    if (a.app_cursor && blockIdx.x == 0) {
+      __shared__ int cur;
+      if (threadIdx.x == 0) cur = *a.app_cursor;
+      __syncthreads();
+      for (int j = threadIdx.x; j < a.app_n; j += blockDim.x) a.app_all[(size_t)cur * a.app_n + j] = a.app_src[j];
+      if (threadIdx.x == 0) *a.app_cursor = cur + 1;
+    }
+    return;
+  }
+  const ConvGeo& g = a.r.g[l];
+  const int nblk = a.r.nblk[l];
+  const int len = g.N * g.Kp + g.N;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  float s0, s1, s2, s3;
+  slab_sum4(a.r.slab[l], nblk, len, i, s0, s1, s2, s3);
+  const float sum = (s0 + s1) + (s2 + s3);
+  const int nk = g.N * g.Kp;
+  int64_t o;
+  int n = 0, tap = 0, c = 0;
+  const int taps = g.KH * g.KW;
+  if (i < nk) {
+    n = i / g.Kp;
+    const int k = i - n * g.Kp;
+    if (k >= taps * g.C) return;  // Kp padding column
+    tap = k / g.C;
+    c = k - tap * g.C;
+    o = a.w_off[l] + ((int64_t)n * g.C + c) * taps + tap;
+  } else {
+    o = a.b_off[l] + (i - nk);
+  }
+  float p = a.params[o], mm = a.m[o], vv = a.v[o];
+  adam_elem(p, sum, mm, vv, a.h, step_size, bc2_sqrt);
+  a.params[o] = p;
+  a.m[o] = mm;
+  a.v[o] = vv;
+  if (i < nk) {
+    const bf16 pb = (bf16)p;
+    static_cast<bf16*>(a.wb[l])[((size_t)n * taps + tap) * g.C + c] = pb;
+    if (a.wt[l]) static_cast<bf16*>(a.wt[l])[((size_t)c * taps + tap) * g.N + n] = pb;
+  }
+}
+
 // fp32 torch-layout conv weights [N][C][KH][KW] of up to kMaxPack layers -> bf16 [N][KH][KW][C]
 // (forward GEMM operand) and, where requested, the data-gradient operand: bf16 [C][KH][KW][N]
 // (a 2-D transpose of the source viewed [N][C*KH*KW]) or, t_hwc, [KH][KW][C][N] (a 2-D
@@ -825,6 +891,23 @@ hipError_t conv_reduce_multi(const ConvReduceMulti& r, hipStream_t s) {
     maxlen = len > maxlen ? len : maxlen;
   }
   hipLaunchKernelGGL(conv_reduce_multi_kernel, dim3((maxlen + 255) / 256, r.n), dim3(256), 0, s, rr);
+  return hipGetLastError();
+}
+
+hipError_t conv_reduce_adam(const ConvReduceAdam& a, hipStream_t s) {
+  if (a.r.n <= 0 || a.r.n > kMaxPack || a.tail_n < 0) return hipErrorInvalidValue;
+  ConvReduceAdam aa = a;
+  int maxlen = 0;
+  for (int l = 0; l < a.r.n; ++l) {
+    int mpb = 0;
+    conv_wgrad_blocks(a.r.g[l], &aa.r.nblk[l], &mpb);
+    const int len = a.r.g[l].N * a.r.g[l].Kp + a.r.g[l].N;
+    maxlen = len > maxlen ? len : maxlen;
+    if (!a.wb[l]) return hipErrorInvalidValue;
+  }
+  const int64_t tail_blocks = (a.tail_n + 255) / 256;
+  const int64_t gx = std::max<int64_t>(std::max<int64_t>((maxlen + 255) / 256, tail_blocks), 1);
+  hipLaunchKernelGGL(conv_reduce_adam_kernel, dim3((unsigned)gx, a.r.n + 1), dim3(256), 0, s, aa);
   return hipGetLastError();
 }
 

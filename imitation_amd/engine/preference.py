@@ -333,7 +333,8 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
             if self.pol_norm is not None:  # (the single-rank update keeps the module's count only)
                 self.norm_count.copy_(self.pol_norm.count.reshape(1))
             st["norm_count"] = self.norm_count.cpu().clone()
-        st.update(step0=int(self._step0), seed=int(self._seed), explore_random=bool(self._explore_random))
+        st.update(step0=int(self._step0), seed=int(self._seed), perm_round=int(self._perm_round),
+                  explore_random=bool(self._explore_random))
         return st
 
     def buffer_state(self) -> Dict[str, Any]:
@@ -361,6 +362,7 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
             if self.norm_count is not None and "norm_count" in st:
                 self.norm_count.copy_(st["norm_count"].to(self._dev))
         self._step0, self._seed = st["step0"], st["seed"]
+        self._perm_round = int(st.get("perm_round", 0))  # the PPO minibatch permutations' round counter
         self._explore_random = st["explore_random"]
         self._reset_accumulator()
         self.sync_env_to_host()

@@ -150,7 +150,7 @@ def test_train_preference_comparisons_resume_is_exact_on_host(tmp_path, kill_aft
 def test_train_preference_comparisons_resume_is_bitwise_on_device(tmp_path):
     updates = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
                    rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
-                   total_timesteps=4 * 1024, total_comparisons=16, num_iterations=3, fragment_length=20,
+                   total_timesteps=4 * 1024, total_comparisons=16, num_iterations=3, fragment_length=4,
                    reward_trainer_kwargs=dict(epochs=1), checkpoint_interval=0)
     _check_pref_resume(tmp_path, updates, 2)
 

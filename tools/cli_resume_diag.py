@@ -1,0 +1,73 @@
+"""Where does a device-engine CLI resume diverge? (train_adversarial, full checkpoints every 2 rounds)
+
+Runs: A = 8 rounds, B = 8 rounds again (run-to-run determinism), C = 4 rounds, D = resume C for 8.
+Compares the full-checkpoint states field by field: A vs B at every step, C vs A at 2 / 4, D vs A
+at 6 / 8. One line per differing field.
+
+    python tools/cli_resume_diag.py [gail|airl]
+"""
+
+import glob
+import os
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch as th  # noqa: E402
+
+
+def run(root, cmd, total, **kw):
+    from imitation_amd.scripts.train_adversarial import train_adversarial_ex
+
+    upd = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
+               expert=dict(policy_type="random", loader_kwargs={}),
+               rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
+               algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=0,
+               full_checkpoint_interval=2, full_checkpoint_keep=10, total_timesteps=total * 1024, seed=0,
+               logging={"log_root": root}, **kw)
+    r = train_adversarial_ex.run(cmd, named_configs=["demonstrations.fast", "policy_evaluation.fast"], config_updates=upd)
+    assert r.status == "COMPLETED"
+    cks = sorted(glob.glob(os.path.join(root, "**", "full_checkpoints", "ckpt-*"), recursive=True))
+    return {int(os.path.basename(c)[5:]): th.load(os.path.join(c, "state.pt"), weights_only=True) for c in cks}, cks
+
+
+def cmp(tag, a, b, path=""):
+    n = 0
+    if isinstance(a, th.Tensor):
+        if not (isinstance(b, th.Tensor) and a.shape == b.shape and th.equal(a, b)):
+            print(f"{tag}: DIFF {path}", flush=True)
+            return 1
+        return 0
+    if isinstance(a, dict):
+        for k in a:
+            n += cmp(tag, a[k], b.get(k) if isinstance(b, dict) else None, f"{path}.{k}")
+        return n
+    if isinstance(a, (list, tuple)):
+        for i, (x, y) in enumerate(zip(a, b)):
+            n += cmp(tag, x, y, f"{path}[{i}]")
+        return n
+    if a != b:
+        print(f"{tag}: DIFF {path} {str(a)[:60]} != {str(b)[:60]}", flush=True)
+        return 1
+    return 0
+
+
+def main():
+    cmd = sys.argv[1] if len(sys.argv) > 1 else "gail"
+    tmp = tempfile.mkdtemp()
+    os.chdir(tmp)
+    A, _ = run(os.path.join(tmp, "A"), cmd, 8)
+    B, _ = run(os.path.join(tmp, "B"), cmd, 8)
+    for s in sorted(A):
+        print(f"A vs B step {s}: {cmp(f'A/B@{s}', A[s], B[s])} differing fields", flush=True)
+    C, ck = run(os.path.join(tmp, "C"), cmd, 4)
+    for s in sorted(C):
+        print(f"C vs A step {s}: {cmp(f'C/A@{s}', C[s], A[s])} differing fields", flush=True)
+    D, _ = run(os.path.join(tmp, "D"), cmd, 8, resume_from=os.path.dirname(ck[-1]))
+    for s in sorted(D):
+        print(f"D vs A step {s}: {cmp(f'D/A@{s}', D[s], A[s])} differing fields", flush=True)
+
+
+if __name__ == "__main__":
+    main()
