@@ -285,135 +285,6 @@ py::tuple fc_backward(torch::Tensor x, torch::Tensor dh, torch::Tensor h, torch:
   return py::make_tuple(dW, db, need_dx ? py::cast(dx) : py::none());
 }
 
-ia::AdamHyper adam_hyper(double lr, double b1, double b2, double eps, double wd, bool decoupled, bool maximize) {
-  return ia::AdamHyper{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd, decoupled ? 1 : 0, maximize ? 1 : 0};
-}
-
-// The BC step's FC backward with the weight's Adam step fused (no dW store): p / m / v are the FC
-// weight's [NH, K] slices of the flat buckets, wb [NH, K] (h, w, c) / wt [K (h, w, c), NH] bf16 the
-// persistent GEMM images (wt is read by the data gradient first, then both are rewritten with the
-// new weights); db_out the bias gradient slot. Returns dX bf16 [M, K] (NHWC) or None.
-py::object fc_backward_adam(torch::Tensor x, torch::Tensor dh, torch::Tensor h, int64_t C, torch::Tensor p, torch::Tensor m,
-                            torch::Tensor v, torch::Tensor step, double lr, double b1, double b2, double eps, double wd,
-                            bool decoupled, bool maximize, torch::Tensor wb, torch::Tensor wt, torch::Tensor db_out,
-                            bool need_dx) {
-  IA_CHECK_CUDA(x);
-  IA_CHECK_CONTIG(x);
-  IA_CHECK_GPU_F32(h);
-  IA_CHECK_CONTIG(h);
-  IA_CHECK_GPU_F32(dh);
-  IA_CHECK_CONTIG(dh);
-  TORCH_CHECK(x.scalar_type() == torch::kBFloat16, "fc_backward_adam: bf16 x");
-  const int M = (int)x.size(0);
-  const int64_t K = x.numel() / std::max<int64_t>(1, M);
-  const int NH = (int)h.size(1);
-  TORCH_CHECK(h.dim() == 2 && h.size(0) == M && dh.sizes() == h.sizes() && C > 0 && K % C == 0, "fc_backward_adam: shapes");
-  TORCH_CHECK(ia::fc_backward_adam_ok(M, (int)K, NH, (int)C, (int)(K / C)), "fc_backward_adam: geometry");
-  for (auto* t : {&p, &m, &v}) {
-    IA_CHECK_GPU_F32(*t);
-    IA_CHECK_CONTIG(*t);
-    TORCH_CHECK(t->numel() == (int64_t)NH * K, "fc_backward_adam: p / m / v must be [NH, K]");
-  }
-  for (auto* t : {&wb, &wt}) {
-    IA_CHECK_CUDA(*t);
-    IA_CHECK_CONTIG(*t);
-    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->numel() == (int64_t)NH * K, "fc_backward_adam: bf16 wb / wt");
-  }
-  IA_CHECK_GPU_F32(step);
-  IA_CHECK_GPU_F32(db_out);
-  TORCH_CHECK(step.numel() == 1 && db_out.numel() == NH && db_out.is_contiguous(), "fc_backward_adam: step / db_out");
-  ia::FcAdamArgs ad{};
-  ad.params = p.data_ptr<float>();
-  ad.m = m.data_ptr<float>();
-  ad.v = v.data_ptr<float>();
-  ad.step = step.data_ptr<float>();
-  ad.h = adam_hyper(lr, b1, b2, eps, wd, decoupled, maximize);
-  ad.wb = wb.data_ptr();
-  ad.wt = wt.data_ptr();
-  torch::Tensor dx;
-  if (need_dx) dx = torch::empty({M, K}, x.options());
-  IA_HIP_CHECK3(ia::fc_backward_adam(x.data_ptr(), dh.data_ptr<float>(), h.data_ptr<float>(), ad, db_out.data_ptr<float>(),
-                                     need_dx ? dx.data_ptr() : nullptr, M, (int)K, NH, (int)C, (int)(K / C), ia_stream()));
-  return need_dx ? py::cast(dx) : py::none();
-}
-
-// The BC step's last launch: conv_reduce_multi with the Adam step fused (ConvReduceAdam): per layer
-// the weight / bias element offsets in the flat buckets (w_offs, b_offs) and the persistent bf16 GEMM
-// images to refresh (wts entries may be None); the tail range gets a plain Adam from its bucket
-// gradients; append (src, all, cursor) optional.
-void conv_reduce_adam(std::vector<torch::Tensor> xs, std::vector<torch::Tensor> dys, std::vector<int64_t> KHs,
-                      std::vector<int64_t> KWs, std::vector<int64_t> strides, std::vector<int64_t> pads,
-                      std::vector<torch::Tensor> slabs, std::vector<int64_t> w_offs, std::vector<int64_t> b_offs,
-                      std::vector<torch::Tensor> wbs, std::vector<c10::optional<torch::Tensor>> wts, torch::Tensor params,
-                      torch::Tensor grads, torch::Tensor m, torch::Tensor v, torch::Tensor step, double lr, double b1,
-                      double b2, double eps, double wd, bool decoupled, bool maximize, int64_t tail_off, int64_t tail_n,
-                      c10::optional<torch::Tensor> app_src, c10::optional<torch::Tensor> app_all,
-                      c10::optional<torch::Tensor> app_cursor) {
-  const size_t n = xs.size();
-  TORCH_CHECK(n > 0 && n <= (size_t)ia::kMaxPack && dys.size() == n && KHs.size() == n && KWs.size() == n &&
-                  strides.size() == n && pads.size() == n && slabs.size() == n && w_offs.size() == n && b_offs.size() == n &&
-                  wbs.size() == n && wts.size() == n,
-              "conv_reduce_adam: one entry per layer (<= 8)");
-  for (auto* t : {&params, &grads, &m, &v}) {
-    IA_CHECK_GPU_F32(*t);
-    IA_CHECK_CONTIG(*t);
-    TORCH_CHECK(t->numel() == params.numel(), "conv_reduce_adam: flat buckets of equal size");
-  }
-  IA_CHECK_GPU_F32(step);
-  TORCH_CHECK(step.numel() == 1, "conv_reduce_adam: step");
-  const int64_t total = params.numel();
-  ia::ConvReduceAdam a{};
-  a.r.n = (int)n;
-  for (size_t l = 0; l < n; ++l) {
-    auto g = geo(xs[l], dys[l].size(3), KHs[l], KWs[l], strides[l], pads[l]);
-    IA_CHECK_GPU_F32(slabs[l]);
-    TORCH_CHECK((size_t)slabs[l].numel() >= ia::conv_wgrad_slab_floats(g), "conv_reduce_adam: slab size");
-    const int64_t nw = (int64_t)g.N * g.C * g.KH * g.KW;
-    TORCH_CHECK(w_offs[l] >= 0 && w_offs[l] + nw <= total && b_offs[l] >= 0 && b_offs[l] + g.N <= total,
-                "conv_reduce_adam: offsets outside the buckets");
-    IA_CHECK_CUDA(wbs[l]);
-    IA_CHECK_CONTIG(wbs[l]);
-    TORCH_CHECK(wbs[l].scalar_type() == torch::kBFloat16 && wbs[l].numel() == nw, "conv_reduce_adam: wb [N, KH, KW, C]");
-    a.r.g[l] = g;
-    a.r.slab[l] = slabs[l].data_ptr<float>();
-    a.w_off[l] = w_offs[l];
-    a.b_off[l] = b_offs[l];
-    a.wb[l] = wbs[l].data_ptr();
-    if (wts[l] && wts[l]->defined()) {
-      IA_CHECK_CUDA(*wts[l]);
-      IA_CHECK_CONTIG(*wts[l]);
-      TORCH_CHECK(wts[l]->scalar_type() == torch::kBFloat16 && wts[l]->numel() == nw, "conv_reduce_adam: wt [C, KH, KW, N]");
-      a.wt[l] = wts[l]->data_ptr();
-    }
-  }
-  TORCH_CHECK(tail_off >= 0 && tail_n >= 0 && tail_off + tail_n <= total, "conv_reduce_adam: tail range");
-  a.params = params.data_ptr<float>();
-  a.grads = grads.data_ptr<float>();
-  a.m = m.data_ptr<float>();
-  a.v = v.data_ptr<float>();
-  a.step = step.data_ptr<float>();
-  a.h = adam_hyper(lr, b1, b2, eps, wd, decoupled, maximize);
-  a.tail_off = tail_off;
-  a.tail_n = tail_n;
-  if (app_cursor && app_cursor->defined()) {
-    TORCH_CHECK(app_src && app_src->defined() && app_all && app_all->defined(), "append: src, all, cursor");
-    const auto& src = *app_src;
-    const auto& all = *app_all;
-    const auto& cur = *app_cursor;
-    IA_CHECK_CUDA(src);
-    IA_CHECK_CUDA(all);
-    IA_CHECK_CUDA(cur);
-    TORCH_CHECK(src.scalar_type() == torch::kFloat32 && all.scalar_type() == torch::kFloat32 && src.is_contiguous() &&
-                    all.is_contiguous() && all.numel() % src.numel() == 0 && cur.scalar_type() == torch::kInt32,
-                "append: fp32 src [n], all [m, n], int32 cursor");
-    a.app_src = src.data_ptr<float>();
-    a.app_all = all.data_ptr<float>();
-    a.app_cursor = cur.data_ptr<int>();
-    a.app_n = (int)src.numel();
-  }
-  IA_HIP_CHECK3(ia::conv_reduce_adam(a, ia_stream()));
-}
-
 // Two same-shape unpadded convs (+ bias + ReLU) in one launch: the collector's expert and
 // learner layers. Returns (y1, y2).
 py::tuple conv_fwd_pair(torch::Tensor x1, torch::Tensor x2, torch::Tensor w1, torch::Tensor w2, torch::Tensor b1,
@@ -549,16 +420,6 @@ void register_conv(py::module& m) {
         py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
         py::arg("relu_out"), py::arg("pad") = 0);
   m.def("conv_reduce_multi", &conv_reduce_multi, "deferred wgrad reductions of several layers, one launch");
-  m.def("fc_backward_adam", &fc_backward_adam, "NatureCNN feature-layer backward with the weight's Adam step fused",
-        py::arg("x"), py::arg("dh"), py::arg("h"), py::arg("C"), py::arg("p"), py::arg("m"), py::arg("v"), py::arg("step"),
-        py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"),
-        py::arg("maximize"), py::arg("wb"), py::arg("wt"), py::arg("db_out"), py::arg("need_dx"));
-  m.def("conv_reduce_adam", &conv_reduce_adam, "deferred wgrad reductions + fused Adam + GEMM images, one launch",
-        py::arg("xs"), py::arg("dys"), py::arg("KHs"), py::arg("KWs"), py::arg("strides"), py::arg("pads"), py::arg("slabs"),
-        py::arg("w_offs"), py::arg("b_offs"), py::arg("wbs"), py::arg("wts"), py::arg("params"), py::arg("grads"),
-        py::arg("m"), py::arg("v"), py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
-        py::arg("weight_decay"), py::arg("decoupled"), py::arg("maximize"), py::arg("tail_off"), py::arg("tail_n"),
-        py::arg("app_src") = py::none(), py::arg("app_all") = py::none(), py::arg("app_cursor") = py::none());
   m.def("conv_dgrad", &conv_dgrad, "NHWC conv data gradient with fused ReLU masks", py::arg("dy"), py::arg("y"),
         py::arg("wt"), py::arg("xp"), py::arg("stride"), py::arg("relu_out"), py::arg("relu_in"), py::arg("pad") = 0);
 }

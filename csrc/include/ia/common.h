@@ -11,13 +11,6 @@ __host__ __device__ __forceinline__ int pad32(int x) { return (x + 31) & ~31; }
 // ds_read_b128 group start on different bank slots.
 __host__ __device__ __forceinline__ int ld_for_k(int k) { return pad32(k) + 8; }
 
-// Adam / AdamW hyper-parameters of one flat parameter group (element update: ia/adam.h)
-struct AdamHyper {
-  float lr, beta1, beta2, eps, weight_decay;
-  int decoupled;  // AdamW: p *= 1 - lr * wd
-  int maximize;
-};
-
 enum Act : int { ACT_IDENTITY = 0, ACT_RELU = 1, ACT_TANH = 2, ACT_LEAKY_RELU = 3, ACT_SIGMOID = 4 };
 
 }  // namespace ia

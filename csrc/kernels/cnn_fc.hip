@@ -18,7 +18,6 @@
 #include <cstdint>
 #include <cstdlib>
 
-#include "ia/adam.h"
 #include "ia/mfma.h"
 #include "launchers.h"
 
@@ -122,11 +121,10 @@ constexpr int kChMaxCols = 416;  // kChG * HW bound: 26 tiles of 16 columns
 constexpr int kChTilesW = 13;    // tiles per wave (parity split)
 constexpr int kChXIt = 4;        // X loads per thread per 32-row chunk: ceil(32 * 52 / 512)
 
-template <bool ADAM>
 __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
                                                           const float* __restrict__ Hout, float* __restrict__ dW,
                                                           float* __restrict__ db, bf16* __restrict__ dZb, int M, int K,
-                                                          int NH, int C, int HW, FcAdamArgs ad) {
+                                                          int NH, int C, int HW) {
   __shared__ __attribute__((aligned(16))) bf16 zs[64][40];          // dZ^T chunk [n][m] (+8 pad)
   __shared__ __attribute__((aligned(16))) bf16 xs[kChMaxCols][40];  // X^T chunk [column][m]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -152,7 +150,7 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
       if (m < M) {
         const size_t o = (size_t)m * NH + n0 + nn;
         z = Hout[o] > 0.f ? dH[o] : 0.f;
-        if (!ADAM && first) dZb[o] = (bf16)z;
+        if (first) dZb[o] = (bf16)z;
       }
       zs[nn][mm] = (bf16)z;
     }
@@ -176,90 +174,23 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
     }
     __syncthreads();
   }
-  if constexpr (!ADAM) {
-    float* dWb = dW + (size_t)c0 * HW;
+  float* dWb = dW + (size_t)c0 * HW;
 #pragma unroll
-    for (int j = 0; j < kChTilesW; ++j) {
-      const int col = 16 * (par + 2 * j) + (l & 15);
-      if (col < ncols) {
+  for (int j = 0; j < kChTilesW; ++j) {
+    const int col = 16 * (par + 2 * j) + (l & 15);
+    if (col < ncols) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dWb[(size_t)(n0 + wn * 16 + 4 * (l >> 4) + i) * K + col] = acc[j][i];
-      }
-    }
-  } else {
-    // The optimizer step of this block's weights, straight from the accumulators (the gradient is
-    // never stored): Adam on (param, m, v) in the flat buckets -- the same element update as
-    // adam_flat (ia/adam.h) -- then the new weights' bf16 GEMM images for the next step: the
-    // forward operand wb [NH][(h, w, c)] and the data-gradient operand wt [(h, w, c)][NH], both
-    // staged through an LDS image [n][hw][channel] so the global stores are whole 16-B runs.
-    extern __shared__ __attribute__((aligned(16))) bf16 img[];  // [64][HW][kChG]
-    float step_size, bc2_sqrt;
-    adam_scalars(*ad.step, ad.h.lr, ad.h.beta1, ad.h.beta2, step_size, bc2_sqrt);
-    float* pb = ad.params + (size_t)c0 * HW;
-    float* mb = ad.m + (size_t)c0 * HW;
-    float* vb = ad.v + (size_t)c0 * HW;
-#pragma unroll
-    for (int j = 0; j < kChTilesW; ++j) {
-      const int col = 16 * (par + 2 * j) + (l & 15);
-      if (col < ncols) {
-        const int cl = col / HW, hw = col - cl * HW;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int nl = wn * 16 + 4 * (l >> 4) + i;
-          const size_t o = (size_t)(n0 + nl) * K + col;
-          float p = pb[o], mm = mb[o], vv = vb[o];
-          adam_elem(p, acc[j][i], mm, vv, ad.h, step_size, bc2_sqrt);
-          pb[o] = p;
-          mb[o] = mm;
-          vb[o] = vv;
-          img[((size_t)nl * HW + hw) * kChG + cl] = (bf16)p;
-        }
-      }
-    }
-    __syncthreads();
-    // wb rows: (n, hw) -> the block's kChG channels, one 16-B store
-    for (int i = tid; i < 64 * HW; i += 512) {
-      const int nl = i / HW, hw = i - nl * HW;
-      *reinterpret_cast<bf16x8*>(static_cast<bf16*>(ad.wb) + (size_t)(n0 + nl) * K + (size_t)hw * C + c0) =
-          *reinterpret_cast<const bf16x8*>(img + (size_t)i * kChG);
-    }
-    // wt rows: (hw, channel) -> 8 consecutive n per 16-B store
-    for (int i = tid; i < HW * kChG * 8; i += 512) {
-      const int q = i & 7, pc = i >> 3, hw = pc / kChG, cl = pc - hw * kChG;
-      bf16x8 v8;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v8[u] = img[((size_t)(8 * q + u) * HW + hw) * kChG + cl];
-      *reinterpret_cast<bf16x8*>(static_cast<bf16*>(ad.wt) + ((size_t)hw * C + c0 + cl) * NH + n0 + 8 * q) = v8;
+      for (int i = 0; i < 4; ++i) dWb[(size_t)(n0 + wn * 16 + 4 * (l >> 4) + i) * K + col] = acc[j][i];
     }
   }
   if (first && tid < 64) db[n0 + tid] = relu_bias_sum(dH, Hout, M, NH, n0 + tid);  // fixed row order
 }
 
-// dZ fragment of 8 consecutive n from the fp32 head gradient: bf16(dH * [Hout > 0]) -- the
-// values fc_wgrad stores as dZb
-__device__ __forceinline__ bf16x8 dz8_from_dh(const float* __restrict__ dH, const float* __restrict__ Hout, size_t o) {
-  const float4 d0 = *reinterpret_cast<const float4*>(dH + o), d1 = *reinterpret_cast<const float4*>(dH + o + 4);
-  const float4 h0 = *reinterpret_cast<const float4*>(Hout + o), h1 = *reinterpret_cast<const float4*>(Hout + o + 4);
-  bf16x8 z;
-  z[0] = (bf16)(h0.x > 0.f ? d0.x : 0.f);
-  z[1] = (bf16)(h0.y > 0.f ? d0.y : 0.f);
-  z[2] = (bf16)(h0.z > 0.f ? d0.z : 0.f);
-  z[3] = (bf16)(h0.w > 0.f ? d0.w : 0.f);
-  z[4] = (bf16)(h1.x > 0.f ? d1.x : 0.f);
-  z[5] = (bf16)(h1.y > 0.f ? d1.y : 0.f);
-  z[6] = (bf16)(h1.z > 0.f ? d1.z : 0.f);
-  z[7] = (bf16)(h1.w > 0.f ? d1.w : 0.f);
-  return z;
-}
-
 // One wave = 16 rows x 16 NHWC columns; the n loop is issued 4 k-steps (8 loads) at a time
-// so the L2 round trips overlap (the wave reads 16 KB of Wt). FROM_DH: dZ is formed from the
-// fp32 dH / Hout on load (the fused BC step runs this BEFORE the weight update overwrites Wt)
-template <bool FROM_DH>
+// so the L2 round trips overlap (the wave reads 16 KB of Wt).
 __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
                                                        bf16* __restrict__ dX, int M, int K, int NH,
-                                                       const bf16* __restrict__ Xm, const float* __restrict__ dH,
-                                                       const float* __restrict__ Hout) {
+                                                       const bf16* __restrict__ Xm) {
   const int l = threadIdx.x & 63;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int ktiles = K / 16;
@@ -277,10 +208,7 @@ __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool ok = n0 + 32 * u < NH;
-      if constexpr (FROM_DH)
-        a[u] = ok ? dz8_from_dh(dH, Hout, (size_t)(mv ? m : 0) * NH + nq + n0 + 32 * u) : bf16x8{};
-      else
-        a[u] = ok ? *reinterpret_cast<const bf16x8*>(ar + n0 + 32 * u) : bf16x8{};
+      a[u] = ok ? *reinterpret_cast<const bf16x8*>(ar + n0 + 32 * u) : bf16x8{};
       b[u] = ok ? *reinterpret_cast<const bf16x8*>(br + n0 + 32 * u) : bf16x8{};
     }
 #pragma unroll
@@ -317,39 +245,17 @@ hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const 
   const bool ch_off = ch_env != nullptr && ch_env[0] == '0';
   const bool ch = !ch_off && C % kChG == 0 && kChG * HW <= kChMaxCols && reinterpret_cast<uintptr_t>(X) % 16 == 0;
   if (ch)
-    hipLaunchKernelGGL(fc_wgrad_ch_kernel<false>, dim3(C / kChG, NH / 64), dim3(512), 0, s, static_cast<const bf16*>(X), dH,
-                       Hout, dW, db, static_cast<bf16*>(dZb), M, K, NH, C, HW, FcAdamArgs{});
+    hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(C / kChG, NH / 64), dim3(512), 0, s, static_cast<const bf16*>(X), dH, Hout, dW,
+                       db, static_cast<bf16*>(dZb), M, K, NH, C, HW);
   else
     hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / (16 * kFcCT), NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout,
                        dW, db, static_cast<bf16*>(dZb), M, K, NH, C, HW);
   if (dX) {
     const int waves = ((M + 15) / 16) * (K / 16);
-    hipLaunchKernelGGL(fc_dgrad_kernel<false>, dim3((waves + 3) / 4), dim3(256), 0, s, static_cast<const bf16*>(dZb),
+    hipLaunchKernelGGL(fc_dgrad_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, static_cast<const bf16*>(dZb),
                        static_cast<const bf16*>(Wt), static_cast<bf16*>(dX), M, K, NH,
-                       mask_dx ? static_cast<const bf16*>(X) : nullptr, nullptr, nullptr);
+                       mask_dx ? static_cast<const bf16*>(X) : nullptr);
   }
-  return hipGetLastError();
-}
-
-bool fc_backward_adam_ok(int M, int K, int NH, int C, int HW) {
-  return fc_train_ok(M, K, NH, C, HW) && C % kChG == 0 && kChG * HW <= kChMaxCols && NH % 64 == 0;
-}
-
-hipError_t fc_backward_adam(const void* X, const float* dH, const float* Hout, const FcAdamArgs& ad, float* db, void* dX,
-                            int M, int K, int NH, int C, int HW, hipStream_t s) {
-  if (!fc_backward_adam_ok(M, K, NH, C, HW) || reinterpret_cast<uintptr_t>(X) % 16 != 0 ||
-      ((reinterpret_cast<uintptr_t>(dH) | reinterpret_cast<uintptr_t>(Hout) | reinterpret_cast<uintptr_t>(ad.wb) |
-        reinterpret_cast<uintptr_t>(ad.wt)) & 15) != 0)
-    return hipErrorInvalidValue;
-  // the data gradient first: it reads the step's weights (wt), which the update below overwrites
-  if (dX) {
-    const int waves = ((M + 15) / 16) * (K / 16);
-    hipLaunchKernelGGL(fc_dgrad_kernel<true>, dim3((waves + 3) / 4), dim3(256), 0, s, nullptr,
-                       static_cast<const bf16*>(ad.wt), static_cast<bf16*>(dX), M, K, NH, nullptr, dH, Hout);
-  }
-  const size_t lds = (size_t)64 * HW * kChG * sizeof(bf16);
-  hipLaunchKernelGGL(fc_wgrad_ch_kernel<true>, dim3(C / kChG, NH / 64), dim3(512), lds, s, static_cast<const bf16*>(X), dH,
-                     Hout, nullptr, db, nullptr, M, K, NH, C, HW, ad);
   return hipGetLastError();
 }
 

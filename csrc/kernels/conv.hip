@@ -30,9 +30,6 @@
 // columns; fragments past K read as zero too.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-
-#include "ia/adam.h"
 #include "ia/mfma.h"
 #include "launchers.h"
 
@@ -403,6 +400,105 @@ __global__ __launch_bounds__(256) void conv_dgrad_pf_kernel(const bf16* __restri
   }
 }
 
+// Small-batch data gradient with the tap loop split over waves: a block is ONE 16-pixel tile and
+// TS x NN waves, wave w = (tap group w / NN, channel half w % NN) accumulating its taps of one
+// 32-channel half of dZ; the TS * NN partial tiles are summed through LDS in wave order. At BC
+// batch sizes the grid of conv_dgrad_pf_kernel is a few hundred waves and each wave's time is its
+// chain of per-tap load round trips (NatureCNN conv3: 9 taps x 2 halves, 19 us); here each wave
+// issues all of its (<= kDgMaxTpg) taps' loads at once and the chain is one round trip deep.
+constexpr int kDgMaxTpg = 4;
+
+template <int CT, int NN>
+__global__ __launch_bounds__(512) void conv_dgrad_split_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
+                                                               const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
+                                                               bf16* __restrict__ dZp, ConvGeo g, int relu_out, int relu_in,
+                                                               int tpg) {
+  __shared__ f32x4 part[8][CT][64];  // [wave][channel tile][lane]
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const int ph = blockIdx.y / g.S, pw = blockIdx.y - ph * g.S;
+  const int Hc = (g.H - ph + g.S - 1) / g.S, Wc = (g.W - pw + g.S - 1) / g.S;
+  const int HWc = Hc * Wc;
+  const int P = g.B * HWc;
+  const int p0 = blockIdx.x * 16;
+  if (p0 >= P) return;  // (block-uniform)
+  const int Kp = g.KH * g.KW * g.N;
+  const int r = l & 15, kq = (l >> 4) * 8;
+  const int q0 = p0 + r;
+  const bool pv = q0 < P;
+  const int qq = pv ? q0 : P - 1;
+  const int pb = qq / HWc;
+  const int rem = qq - pb * HWc, ii = rem / Wc, jj = rem - ii * Wc;
+  const int pih = ph + g.S * ii, piw = pw + g.S * jj;
+  const int nkw = (g.KW - pw + g.S - 1) / g.S;
+  const int ntap = ((g.KH - ph + g.S - 1) / g.S) * nkw;
+  const int tg = w / NN, nn = w - (w / NN) * NN;
+  const int t0 = tg * tpg, t1 = min(ntap, t0 + tpg);
+  const bf16* wr = Wt + (size_t)r * Kp + kq + 32 * nn;
+  f32x4 acc[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) acc[t] = zero4();
+  bf16x8 av[kDgMaxTpg], bv[kDgMaxTpg][CT];
+  bool any[kDgMaxTpg];
+  // every tap's operand loads first (one round trip), then the MFMAs
+#pragma unroll
+  for (int u = 0; u < kDgMaxTpg; ++u) {
+    const int tp = t0 + u;
+    any[u] = false;
+    if (tp < t1) {  // (wave-uniform)
+      const int kh = ph + g.S * (tp / nkw), kw = pw + g.S * (tp - (tp / nkw) * nkw);
+      const int th = pih + g.P - kh, tw = piw + g.P - kw;
+      const int oh = th / g.S, ow = tw / g.S;
+      const bool valid = pv && th >= 0 && oh < g.OH && tw >= 0 && ow < g.OW;
+      any[u] = __ballot(valid) != 0ull;
+      const size_t dzoff = valid ? ((size_t)(pb * g.OH + oh) * g.OW + ow) * g.N + kq + 32 * nn : 0;
+      const int kbase = (kh * g.KW + kw) * g.N;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) bv[u][t] = *reinterpret_cast<const bf16x8*>(wr + (size_t)t * 16 * Kp + kbase);
+      av[u] = valid ? load_dz8(dY, Y, dzoff, relu_out) : zero8();
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kDgMaxTpg; ++u) {
+    if (!any[u]) continue;  // (wave-uniform: past this wave's taps, or a tap missing every pixel)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u], bv[u][t], acc[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < CT; ++t) part[w][t][l] = acc[t];
+  __syncthreads();
+  if (w != 0) return;
+  // fixed wave order (tap groups, then channel halves) for every output element
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    f32x4 s = part[0][t][l];
+    for (int v = 1; v < nw; ++v) {
+      const f32x4 x = part[v][t][l];
+      s[0] += x[0];
+      s[1] += x[1];
+      s[2] += x[2];
+      s[3] += x[3];
+    }
+    acc[t] = s;
+  }
+  const int col = l & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = p0 + 4 * (l >> 4) + i;
+    if (q >= P) continue;
+    const int bb = q / HWc;
+    const int rr = q - bb * HWc, i2 = rr / Wc, j2 = rr - i2 * Wc;
+    const size_t row = ((size_t)bb * g.H + (ph + g.S * i2)) * g.W + (pw + g.S * j2);
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int c = t * 16 + col;
+      float v = acc[t][i];
+      if (relu_in && !((float)Xp[row * g.C + c] > 0.f)) v = 0.f;
+      dZp[row * g.C + c] = (bf16)v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient (partials)
 // 512 threads; wave w owns output tiles t = w + 8 i (t = nt * KT + kt), TPW >= ceil(NT*KT/8).
 // Each block reduces a contiguous m range in chunks of CH rows staged transposed in LDS
@@ -698,69 +794,6 @@ __global__ __launch_bounds__(256) void conv_reduce_multi_kernel(ConvReduceMulti 
   }
 }
 
-// conv_reduce_multi with the optimizer step fused (ConvReduceAdam, launchers.h): blockIdx.y < n
-// reduces layer y's slab column i exactly as conv_reduce_multi_kernel does and, instead of storing
-// the gradient, applies the Adam element update (ia/adam.h, as adam_flat) to that weight / bias and
-// writes the new weight's bf16 forward / data-gradient images; blockIdx.y == n runs the plain Adam
-// over the tail range (gradients written by earlier launches of the step) and the metrics append.
-__global__ __launch_bounds__(256) void conv_reduce_adam_kernel(ConvReduceAdam a) {
-  const int l = blockIdx.y;
-  float step_size, bc2_sqrt;
-  adam_scalars(*a.step, a.h.lr, a.h.beta1, a.h.beta2, step_size, bc2_sqrt);
-  if (l == a.r.n) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < a.tail_n) {
-      const int64_t o = a.tail_off + i;
-      float p = a.params[o], mm = a.m[o], vv = a.v[o];
-      adam_elem(p, a.grads[o], mm, vv, a.h, step_size, bc2_sqrt);
-      a.params[o] = p;
-      a.m[o] = mm;
-      a.v[o] = vv;
-      a.grads[o] = 0.f;
-    }
-    if (a.app_cursor && blockIdx.x == 0) {
-      __shared__ int cur;
-      if (threadIdx.x == 0) cur = *a.app_cursor;
-      __syncthreads();
-      for (int j = threadIdx.x; j < a.app_n; j += blockDim.x) a.app_all[(size_t)cur * a.app_n + j] = a.app_src[j];
-      if (threadIdx.x == 0) *a.app_cursor = cur + 1;
-    }
-    return;
-  }
-  const ConvGeo& g = a.r.g[l];
-  const int nblk = a.r.nblk[l];
-  const int len = g.N * g.Kp + g.N;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= len) return;
-  float s0, s1, s2, s3;
-  slab_sum4(a.r.slab[l], nblk, len, i, s0, s1, s2, s3);
-  const float sum = (s0 + s1) + (s2 + s3);
-  const int nk = g.N * g.Kp;
-  int64_t o;
-  int n = 0, tap = 0, c = 0;
-  const int taps = g.KH * g.KW;
-  if (i < nk) {
-    n = i / g.Kp;
-    const int k = i - n * g.Kp;
-    if (k >= taps * g.C) return;  // Kp padding column
-    tap = k / g.C;
-    c = k - tap * g.C;
-    o = a.w_off[l] + ((int64_t)n * g.C + c) * taps + tap;
-  } else {
-    o = a.b_off[l] + (i - nk);
-  }
-  float p = a.params[o], mm = a.m[o], vv = a.v[o];
-  adam_elem(p, sum, mm, vv, a.h, step_size, bc2_sqrt);
-  a.params[o] = p;
-  a.m[o] = mm;
-  a.v[o] = vv;
-  if (i < nk) {
-    const bf16 pb = (bf16)p;
-    static_cast<bf16*>(a.wb[l])[((size_t)n * taps + tap) * g.C + c] = pb;
-    if (a.wt[l]) static_cast<bf16*>(a.wt[l])[((size_t)c * taps + tap) * g.N + n] = pb;
-  }
-}
-
 // fp32 torch-layout conv weights [N][C][KH][KW] of up to kMaxPack layers -> bf16 [N][KH][KW][C]
 // (forward GEMM operand) and, where requested, the data-gradient operand: bf16 [C][KH][KW][N]
 // (a 2-D transpose of the source viewed [N][C*KH*KW]) or, t_hwc, [KH][KW][C][N] (a 2-D
@@ -894,23 +927,6 @@ hipError_t conv_reduce_multi(const ConvReduceMulti& r, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t conv_reduce_adam(const ConvReduceAdam& a, hipStream_t s) {
-  if (a.r.n <= 0 || a.r.n > kMaxPack || a.tail_n < 0) return hipErrorInvalidValue;
-  ConvReduceAdam aa = a;
-  int maxlen = 0;
-  for (int l = 0; l < a.r.n; ++l) {
-    int mpb = 0;
-    conv_wgrad_blocks(a.r.g[l], &aa.r.nblk[l], &mpb);
-    const int len = a.r.g[l].N * a.r.g[l].Kp + a.r.g[l].N;
-    maxlen = len > maxlen ? len : maxlen;
-    if (!a.wb[l]) return hipErrorInvalidValue;
-  }
-  const int64_t tail_blocks = (a.tail_n + 255) / 256;
-  const int64_t gx = std::max<int64_t>(std::max<int64_t>((maxlen + 255) / 256, tail_blocks), 1);
-  hipLaunchKernelGGL(conv_reduce_adam_kernel, dim3((unsigned)gx, a.r.n + 1), dim3(256), 0, s, aa);
-  return hipGetLastError();
-}
-
 size_t conv_wgrad_slab_floats(const ConvGeo& g) {
   int nblk = 0, mpb = 0;
   conv_wgrad_blocks(g, &nblk, &mpb);
@@ -956,12 +972,24 @@ hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void*
   const bf16* wt = static_cast<const bf16*>(Wt);
   const bf16* xp = static_cast<const bf16*>(Xp);
   bf16* dz = static_cast<bf16*>(dZp);
-  // small batches, N = 32 / 64: the prefetching form (same MFMA sequence)
+  // small batches, N = 32 / 64: the split-tap form (one tile per block, its taps and channel
+  // halves over waves); IMITATION_AMD_CONV_DGRAD_SPLIT=0 the prefetching one-wave-per-tile form,
+  // IMITATION_AMD_CONV_DGRAD_PF=0 the plain loop (A/B knobs, read per call)
   const int nn = g.N / 32;
-  static const bool pf_off = getenv("IMITATION_AMD_CONV_DGRAD_PF") != nullptr;  // (A/B knob: the old loop)
-  const bool pf = !big && (nn == 1 || nn == 2) && !pf_off;
+  const char* pf_env = getenv("IMITATION_AMD_CONV_DGRAD_PF");
+  const char* sp_env = getenv("IMITATION_AMD_CONV_DGRAD_SPLIT");
+  const bool pf = !big && (nn == 1 || nn == 2) && !(pf_env && pf_env[0] == '0');
+  // tap groups of ~3 taps (the largest phase has ceil(KH / S) * ceil(KW / S)), <= 8 waves per block
+  const int ntap_max = ((g.KH + g.S - 1) / g.S) * ((g.KW + g.S - 1) / g.S);
+  int ts = (ntap_max + 2) / 3;
+  if (ts * nn > 8) ts = 8 / nn;
+  const int tpg = (ntap_max + ts - 1) / ts;
+  const bool split = pf && tpg <= kDgMaxTpg && !(sp_env && sp_env[0] == '0');
+  const dim3 sgrid((P + 15) / 16, g.S * g.S), sblock(64 * ts * nn);
 #define IA_DG(CT)                                                                                                         \
   if (big) hipLaunchKernelGGL((conv_dgrad_kernel<CT, 4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in);     \
+  else if (split && nn == 2) hipLaunchKernelGGL((conv_dgrad_split_kernel<CT, 2>), sgrid, sblock, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in, tpg); \
+  else if (split) hipLaunchKernelGGL((conv_dgrad_split_kernel<CT, 1>), sgrid, sblock, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in, tpg); \
   else if (pf && nn == 2) hipLaunchKernelGGL((conv_dgrad_pf_kernel<CT, 2>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); \
   else if (pf) hipLaunchKernelGGL((conv_dgrad_pf_kernel<CT, 1>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in); \
   else hipLaunchKernelGGL((conv_dgrad_kernel<CT, 1>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in)

@@ -290,21 +290,6 @@ bool bc_head_ok(int B, int NH, int A);
 int bc_head_sumsq_blocks(long n_params);
 hipError_t bc_head_train(const BcHeadArgs& a, hipStream_t s);
 
-// ---- the BC step's fused optimizer epilogues (cnn_fc.hip, conv.hip; element update ia/adam.h)
-// NatureCNN feature layer: fc_dgrad (reads wt, dZ formed from dH / Hout), then the weight gradient
-// with the Adam step applied in place of its store -- params / m / v are the FC weight's slices of
-// the flat buckets ([NH][K] torch (c, h, w) columns); wb [NH][K] (h, w, c) and wt [K (h, w, c)][NH]
-// bf16 receive the new weights' GEMM images. db (bias gradient) and dX as fc_backward.
-struct FcAdamArgs {
-  float *params, *m, *v;
-  const float* step;  // device step counter, already advanced for this step
-  AdamHyper h;
-  void *wb, *wt;  // bf16
-};
-bool fc_backward_adam_ok(int M, int K, int NH, int C, int HW);
-hipError_t fc_backward_adam(const void* X, const float* dH, const float* Hout, const FcAdamArgs& ad, float* db, void* dX,
-                            int M, int K, int NH, int C, int HW, hipStream_t s);
-
 // ---- optim.hip: fused Adam / AdamW over a flat fp32 buffer
 struct AdamArgs {
   float *params, *grads, *exp_avg, *exp_avg_sq;
@@ -459,27 +444,6 @@ struct ConvReduceMulti {
   int nblk[kMaxPack];  // filled by conv_reduce_multi
 };
 hipError_t conv_reduce_multi(const ConvReduceMulti& r, hipStream_t s);
-// the BC step's last launch: every layer's deferred wgrad reduction with the Adam step applied in
-// place of the gradient store (weights [N][C][KH][KW] at w_off, biases at b_off of the flat
-// params / m / v buckets), the new weights' bf16 GEMM images (wb [N][KH][KW][C]; wt [C][KH][KW][N]
-// where non-null), plus a plain Adam over grads[tail_off, tail_off + tail_n) -- the parameters
-// whose gradients earlier launches wrote (FC bias, heads) -- zeroing what it consumed, and the
-// graphed epoch's metrics append (app_*; app_cursor null: none)
-struct ConvReduceAdam {
-  ConvReduceMulti r;  // geometry + slabs (dW / db unused)
-  int64_t w_off[kMaxPack], b_off[kMaxPack];
-  void* wb[kMaxPack];
-  void* wt[kMaxPack];
-  float *params, *grads, *m, *v;
-  const float* step;  // device step counter, already advanced for this step
-  AdamHyper h;
-  int64_t tail_off, tail_n;
-  const float* app_src;
-  float* app_all;
-  int* app_cursor;
-  int app_n;
-};
-hipError_t conv_reduce_adam(const ConvReduceAdam& a, hipStream_t s);
 // in_kind: 0 fp32, 1 bf16, 2 uint8 input; weights bf16 [N][KH][KW][C]; Y bf16 [B*OH*OW][N]
 hipError_t conv_forward(int in_kind, const void* X, const void* Wb, const float* bias, void* Y, const ConvGeo& g,
                         float in_scale, int relu, hipStream_t s);

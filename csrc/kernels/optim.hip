@@ -9,7 +9,6 @@
 // slot cleared in the same pass (the next backward accumulates into a zeroed bucket).
 #include <hip/hip_runtime.h>
 
-#include "ia/adam.h"
 #include "launchers.h"
 
 namespace ia {
@@ -17,14 +16,23 @@ namespace {
 
 __device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, const AdamArgs& a, float step_size,
                                          float bc2_sqrt) {
-  adam_elem(p, g, m, v, a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.decoupled, a.maximize, step_size, bc2_sqrt);
+  float gr = a.maximize ? -g : g;
+  if (a.weight_decay != 0.f) {
+    if (a.decoupled) p *= 1.f - a.lr * a.weight_decay;
+    else gr += a.weight_decay * p;
+  }
+  m += (1.f - a.beta1) * (gr - m);
+  v = v * a.beta2 + (1.f - a.beta2) * gr * gr;
+  const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+  p -= step_size * (m / denom);
   if (a.zero_grad) g = 0.f;
 }
 
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
   const float t = *a.step + (a.cnt ? 1.f : 0.f);
-  float step_size, bc2_sqrt;
-  adam_scalars(t, a.lr, a.beta1, a.beta2, step_size, bc2_sqrt);
+  const float bc1 = 1.f - powf(a.beta1, t);
+  const float bc2_sqrt = sqrtf(1.f - powf(a.beta2, t));
+  const float step_size = a.lr / bc1;
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 + 3 < a.n) {
     float4 p = *reinterpret_cast<float4*>(a.params + i4);

@@ -509,9 +509,6 @@ class _DeviceEpochRunner:
         opt = trainer.optimizer
         self._fold = (hasattr(opt, "graph_epoch_step_ok") and opt.graph_epoch_step_ok()
                       and os.environ.get("IMITATION_AMD_BC_FOLD_LAUNCHES", "1") != "0")
-        # IMITATION_AMD_BC_FUSED_ADAM=0: the separate Adam launch + per-step weight packing (A/B knob)
-        self._fused_adam = (self._fold and self.ok and os.environ.get("IMITATION_AMD_BC_FUSED_ADAM", "1") != "0"
-                            and self._f.adam_plan() is not None)
         kmax = max(1, int(os.environ.get("IMITATION_AMD_BC_GRAPH_K", self.K)))
         # graph sizes: the largest, then powers of two below it. A run of n steps replays the
         # largest as often as it fits and each smaller one at most once, so the remainder is
@@ -532,14 +529,6 @@ class _DeviceEpochRunner:
         C = self._f.C
         bufs = self.agg.batch_buffers(self.B)
         opt = self.trainer.optimizer
-        if self._fused_adam:
-            # the optimizer step rides on the step's own kernels (ops/bc_cnn.py step_adam: the FC
-            # weight's Adam in its gradient kernel, the rest in the final reduction, no per-step
-            # weight packing): 14 launches, bitwise the 17-launch step below
-            C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs,
-                                 inc=opt.step_counter())
-            self._f.step_adam(bufs[0], bufs[1], append=(self._f.metrics, self.all, self.cursor))
-            return
         if self._fold:
             # the step counter's add rides on the gather launch, the metrics append on Adam's:
             # 17 launches per step instead of 19 (same arithmetic)
@@ -633,8 +622,6 @@ class _DeviceEpochRunner:
             raise NonFiniteError(f"non-finite BC metrics (loss / entropy / log-prob) in epoch {epoch} of this train() call")
 
     def train(self, n_epochs, n_batches, on_epoch_end, log_interval: int, compute_rollout_stats) -> None:
-        if self._fused_adam:
-            self._f.repack()  # the weights may have changed since the last call (loads, other trainers)
         try:
             self._train(n_epochs, n_batches, on_epoch_end, log_interval, compute_rollout_stats)
         finally:

@@ -107,9 +107,7 @@ class FusedCnnBCStep:
         flat = optimizer._flat[0]["flat"]
         if any(t.data_ptr() % 16 for t in (flat, policy.action_net.weight)):
             return None
-        step = FusedCnnBCStep(policy, optimizer, ent_weight, l2_weight)
-        step._in_hw = (int(obs.shape[1]), int(obs.shape[2]))
-        return step
+        return FusedCnnBCStep(policy, optimizer, ent_weight, l2_weight)
 
     def __call__(self, obs: th.Tensor, acts: th.Tensor) -> th.Tensor:
         C = self.C
@@ -149,118 +147,6 @@ class FusedCnnBCStep:
                 if i > 0:
                     dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], st, top, True, 0)
             C.conv_reduce_multi(*red.values())
-        return self.metrics
-
-
-    # ------------------------------------------------------------------ fused optimizer step
-    def adam_plan(self) -> Optional[Dict[str, Any]]:
-        """The offsets the fused-Adam step needs (None: the layout does not allow it): every conv
-        weight / bias, the FC weight, and ONE contiguous tail range holding every other parameter
-        of the bucket (FC bias, action / value heads), which a plain Adam covers. The FC weight's
-        update runs in its gradient kernel, the rest in the final reduction launch: no separate
-        Adam and no per-step weight packing (the bf16 GEMM images are refreshed by those epilogues)."""
-        plan = getattr(self, "_adam_plan", False)
-        if plan is not False:
-            return plan
-        plan = None
-        opt = self.optimizer
-        f = opt._flat[0]
-        gbase = f["grad"].data_ptr()
-
-        def off(t: th.Tensor) -> int:
-            return (t.data_ptr() - gbase) // 4
-
-        conv = [(off(w), w.numel(), off(b), b.numel()) for w, b in self.g_conv]
-        fw = self.g_lin[0]
-        fcw = (off(fw), fw.numel())
-        covered = sorted([(o, n) for o_w, n_w, o_b, n_b in conv for (o, n) in ((o_w, n_w), (o_b, n_b))] + [fcw])
-        total = f["n"]
-        # the non-covered part must be one contiguous range (the tail): conv params first, then the FC
-        # weight, then everything else in SB3's parameter order
-        pos, gaps = 0, []
-        for o, n in covered:
-            if o > pos:
-                gaps.append((pos, o - pos))
-            pos = max(pos, o + n)
-        if pos < total:
-            gaps.append((pos, total - pos))
-        group = opt.param_groups[0]
-        if len(gaps) <= 1 and not group.get("amsgrad", False) and len(opt.param_groups) == 1:
-            tail = gaps[0] if gaps else (total, 0)
-            plan = dict(conv=conv, fcw=fcw, tail=tail)
-        self._adam_plan = plan
-        return plan
-
-    def repack(self) -> None:
-        """(Re)write the persistent bf16 GEMM images from the current fp32 weights (one launch +
-        copies; at the start of every fused-Adam train() call: the weights may have changed since)."""
-        convs, lin = self.convs, self.lin
-        n = len(convs)
-        C3, NH = convs[-1].out_channels, lin.out_features
-        H, W = self._in_hw
-        for c in convs:
-            H, W = (H - c.kernel_size[0]) // c.stride[0] + 1, (W - c.kernel_size[1]) // c.stride[0] + 1
-        with th.no_grad():
-            wsrc = [c.weight.detach() for c in convs] + [lin.weight.detach().view(NH, C3, H, W)]
-            wbs, wts = self.C.conv_pack_weights(wsrc, [i > 0 for i in range(n)] + [True], [False] * n + [True])
-            if getattr(self, "_img_wb", None) is None:
-                self._img_wb, self._img_wt = list(wbs), list(wts)
-            else:
-                for dst, src in zip(self._img_wb + self._img_wt, list(wbs) + list(wts)):
-                    if dst is not None:
-                        dst.copy_(src)
-
-    def step_adam(self, obs: th.Tensor, acts: th.Tensor, append=None) -> th.Tensor:
-        """One minibatch step INCLUDING the optimizer update (the optimizer's device step counter must
-        already be advanced for it, as the graphed epoch's gather launch does): bitwise the
-        :meth:`__call__` + ``optimizer.step()`` pair (same Adam element update, same bf16 images),
-        in 14 launches instead of 17. ``append``: ``(src, all, cursor)`` metrics append."""
-        C = self.C
-        plan = self.adam_plan()
-        assert plan is not None and getattr(self, "_img_wb", None) is not None, "call repack() first"
-        convs, lin, head = self.convs, self.lin, self.head
-        n = len(convs)
-        x = obs.contiguous()
-        B = x.shape[0]
-        C3, NH = convs[-1].out_channels, lin.out_features
-        opt = self.optimizer
-        f = opt._flat[0]
-        group = opt.param_groups[0]
-        b1, b2 = group["betas"]
-        hyper = (float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
-                 bool(group["decoupled_weight_decay"]), bool(group["maximize"]))
-        wbs, wts = self._img_wb, self._img_wt
-        with th.no_grad():
-            hs: List[th.Tensor] = []
-            h = x
-            for i, c in enumerate(convs):
-                h = C.conv_fwd(h, wbs[i], c.bias.detach(), int(c.stride[0]), 1.0 / 255.0 if i == 0 else 1.0, True, 0)
-                hs.append(h)
-            xf = h.reshape(B, -1)
-            out = C.cnn_fc(xf, wbs[n].view(NH, -1), lin.bias.detach())
-            a = acts.reshape(-1).long().contiguous()
-            dh = C.bc_head_train(out, head.weight.detach(), head.bias.detach(), a, self.flat, self.g_head[0], self.g_head[1],
-                                 self.metrics, self.ws, self.ent_weight, self.l2_weight)
-            o, k = plan["fcw"]
-            dx = C.fc_backward_adam(xf, dh, out, C3, f["flat"][o : o + k], f["m"][o : o + k], f["v"][o : o + k], f["step"],
-                                    *hyper, wbs[n], wts[n], self.g_lin[1], True)
-            dz = dx.view(hs[-1].shape)
-            red = {k_: [] for k_ in ("x", "dy", "kh", "kw", "s", "p", "slab")}
-            for i in range(n - 1, -1, -1):
-                c = convs[i]
-                inp = x if i == 0 else hs[i - 1]
-                top = i == n - 1
-                kh, kw, st = int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0])
-                slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
-                for k_, v in zip(red, (inp, dz, kh, kw, st, 0, slab)):
-                    red[k_].append(v)
-                if i > 0:
-                    dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], st, top, True, 0)
-            order = list(range(n - 1, -1, -1))  # (the reduction lists run top layer first)
-            app = append if append is not None else (None, None, None)
-            C.conv_reduce_adam(*red.values(), [plan["conv"][i][0] for i in order], [plan["conv"][i][2] for i in order],
-                               [wbs[i] for i in order], [wts[i] for i in order], f["flat"], f["grad"], f["m"], f["v"],
-                               f["step"], *hyper, plan["tail"][0], plan["tail"][1], app[0], app[1], app[2])
         return self.metrics
 
 

@@ -42,34 +42,54 @@ def trainers(n=3):
         time.sleep(0.5)  # an idle gap in the kernel trace between instances
 
 
-def split(path):
+def split(path, api_path=None):
+    """Per instance (split at the PPO kernels: 23 per instance), over its 20 timed rounds: GPU busy
+    time vs span (idle = host not keeping the queue full), and per-kernel mean durations; with
+    ``api_path`` (``--hip-trace`` CSV) the slowest HIP API calls of each instance's window."""
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    gaps = sorted(((rows[i + 1][0] - rows[i][1], i) for i in range(len(rows) - 1)), reverse=True)
-    cuts = sorted(i for _, i in gaps[:2])  # the two sleeps between three instances
-    parts = [rows[: cuts[0] + 1], rows[cuts[0] + 1 : cuts[1] + 1], rows[cuts[1] + 1 :]]
-    stats = []
-    for p in parts:
+    ppo = [i for i, r in enumerate(rows) if "ppo_rc_kernel" in r[2]]
+    n_inst = len(ppo) // 23
+    print(f"{len(ppo)} PPO kernels -> {n_inst} instances")
+    windows = []
+    for k in range(n_inst):
+        first_timed = rows[ppo[23 * k + 3]][0]  # rounds 3..22 of the instance are the timed ones
+        last = rows[ppo[23 * k + 22]][1]
+        sel = [r for r in rows if first_timed <= r[0] and r[1] <= last]
+        busy, cur_end = 0, 0
+        for s_, e_, _ in sel:  # union of kernel intervals
+            if e_ <= cur_end:
+                continue
+            busy += e_ - max(s_, cur_end)
+            cur_end = e_
+        span = last - first_timed
+        windows.append((first_timed, last))
+        print(f"instance {k}: span {span / 1e6:.2f} ms, GPU busy {busy / 1e6:.2f} ms, idle {100 * (1 - busy / span):.1f} %, "
+              f"{len(sel)} kernels")
         d = {}
-        for s, e, k in p:
-            d.setdefault(k[:70], []).append(e - s)
-        stats.append(d)
-    keys = sorted(set().union(*stats), key=lambda k: -sum(stats[0].get(k, [0])))
-    print("| kernel | " + " | ".join(f"inst {i} calls / us per call" for i in range(len(stats))) + " |")
-    print("|---|" + "---|" * len(stats))
-    for k in keys[:20]:
-        cells = []
-        for d in stats:
-            v = d.get(k, [])
-            cells.append(f"{len(v)} / {sum(v) / max(1, len(v)) / 1000:.1f}")
-        print(f"| `{k}` | " + " | ".join(cells) + " |")
+        for s_, e_, name in sel:
+            d.setdefault(name[:60], []).append(e_ - s_)
+        top = sorted(d.items(), key=lambda kv: -sum(kv[1]))[:6]
+        print("   " + "; ".join(f"{n}: {len(v)} x {sum(v) / len(v) / 1000:.1f} us" for n, v in top))
+    if api_path:
+        calls = []
+        with open(api_path) as f:
+            for r in csv.DictReader(f):
+                calls.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Function", r.get("Kernel_Name", ""))))
+        for k, (a_, b_) in enumerate(windows):
+            sel = [c for c in calls if a_ <= c[0] <= b_]
+            d = {}
+            for s_, e_, name in sel:
+                d.setdefault(name, []).append(e_ - s_)
+            top = sorted(d.items(), key=lambda kv: -sum(kv[1]))[:8]
+            print(f"instance {k} HIP API: " + "; ".join(f"{n}: {len(v)} x {sum(v) / len(v) / 1000:.1f} us" for n, v in top))
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--split":
-        split(sys.argv[2])
+        split(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
     else:
         trainers()

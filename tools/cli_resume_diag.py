@@ -26,7 +26,22 @@ def run(root, cmd, total, **kw):
                algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=0,
                full_checkpoint_interval=2, full_checkpoint_keep=10, total_timesteps=total * 1024, seed=0,
                logging={"log_root": root}, **kw)
-    r = train_adversarial_ex.run(cmd, named_configs=["demonstrations.fast", "policy_evaluation.fast"], config_updates=upd)
+    from imitation_amd.algorithms.adversarial import common
+
+    seen = {}
+    orig = common.AdversarialTrainer.train
+
+    def spy(self, *a, **k):
+        seen.setdefault("fused", (getattr(self, "_fused_disc", None), getattr(self, "_fused_disc_why", None),
+                                  type(self).__name__))
+        return orig(self, *a, **k)
+
+    common.AdversarialTrainer.train = spy
+    try:
+        r = train_adversarial_ex.run(cmd, named_configs=["demonstrations.fast", "policy_evaluation.fast"], config_updates=upd)
+    finally:
+        common.AdversarialTrainer.train = orig
+    print(f"{root}: trainer {seen.get('fused')}", flush=True)
     assert r.status == "COMPLETED"
     cks = sorted(glob.glob(os.path.join(root, "**", "full_checkpoints", "ckpt-*"), recursive=True))
     return {int(os.path.basename(c)[5:]): th.load(os.path.join(c, "state.pt"), weights_only=True) for c in cks}, cks
@@ -55,6 +70,11 @@ def cmp(tag, a, b, path=""):
 
 def main():
     cmd = sys.argv[1] if len(sys.argv) > 1 else "gail"
+    if "--deterministic" in sys.argv:
+        from imitation_amd.utils import determinism
+
+        determinism.set_deterministic(True)
+        print("torch deterministic algorithms on", flush=True)
     tmp = tempfile.mkdtemp()
     os.chdir(tmp)
     A, _ = run(os.path.join(tmp, "A"), cmd, 8)
