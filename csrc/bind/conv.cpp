@@ -190,6 +190,52 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, to
   return dz;
 }
 
+// One layer's backward in one launch (BC-size batches): (wgrad block partials slab -- reduce with
+// conv_reduce_multi --, dZ of the layer input bf16 [B, H, W, C] = [x > 0] * conv^T(dy * [y > 0]))
+py::tuple conv_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor y, torch::Tensor wt, int64_t stride,
+                             bool relu_out) {
+  for (auto* t : {&x, &dy, &wt}) {
+    IA_CHECK_CUDA((*t));
+    IA_CHECK_CONTIG((*t));
+  }
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && dy.scalar_type() == torch::kBFloat16 &&
+                  wt.scalar_type() == torch::kBFloat16, "conv_backward_pair: bf16 x, dy, wt");
+  TORCH_CHECK(wt.dim() == 4, "wt must be [C, KH, KW, N]");
+  auto g = geo(x, dy.size(3), wt.size(1), wt.size(2), stride, 0);
+  TORCH_CHECK(wt.size(0) == g.C && wt.size(3) == g.N, "wt shape");
+  TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.OH && dy.size(2) == g.OW, "dy shape");
+  if (relu_out) {
+    IA_CHECK_CUDA(y);
+    IA_CHECK_CONTIG(y);
+    TORCH_CHECK(y.sizes() == dy.sizes() && y.scalar_type() == torch::kBFloat16, "y must match dy");
+  }
+  TORCH_CHECK(ia::conv_back_pair_ok(g), "conv_backward_pair: geometry outside the paired kernel");
+  auto slab = torch::empty({(int64_t)ia::conv_wgrad_slab_floats(g)}, x.options().dtype(torch::kFloat32));
+  auto dz = torch::empty({g.B, g.H, g.W, g.C}, x.options());
+  IA_HIP_CHECK3(ia::conv_back_pair(x.data_ptr(), dy.data_ptr(), relu_out ? y.data_ptr() : nullptr, slab.data_ptr<float>(),
+                                   wt.data_ptr(), dz.data_ptr(), g, relu_out ? 1 : 0, 1, ia_stream()));
+  return py::make_tuple(slab, dz);
+}
+
+bool conv_backward_pair_ok(torch::Tensor x, int64_t N, int64_t KH, int64_t KW, int64_t stride) {
+  if (x.dim() != 4 || x.scalar_type() != torch::kBFloat16) return false;
+  ia::ConvGeo g{};
+  g.B = (int)x.size(0);
+  g.H = (int)x.size(1);
+  g.W = (int)x.size(2);
+  g.C = (int)x.size(3);
+  g.KH = (int)KH;
+  g.KW = (int)KW;
+  g.S = (int)stride;
+  g.P = 0;
+  if (g.H < g.KH || g.W < g.KW || g.S <= 0) return false;
+  g.OH = (g.H - g.KH) / g.S + 1;
+  g.OW = (g.W - g.KW) / g.S + 1;
+  g.N = (int)N;
+  g.Kp = (g.KH * g.KW * g.C + 31) & ~31;
+  return ia::conv_back_pair_ok(g);
+}
+
 // fp32 conv weights [N, C, KH, KW] -> (bf16 [N, KH, KW, C] each, bf16 [C, KH, KW, N] where want_t)
 py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> want_t, std::vector<bool> t_hwc) {
   TORCH_CHECK(ws.size() == want_t.size() && (int)ws.size() <= ia::kMaxPack, "conv_pack_weights: layer count");
@@ -420,6 +466,10 @@ void register_conv(py::module& m) {
         py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("in_scale"),
         py::arg("relu_out"), py::arg("pad") = 0);
   m.def("conv_reduce_multi", &conv_reduce_multi, "deferred wgrad reductions of several layers, one launch");
+  m.def("conv_backward_pair", &conv_backward_pair, "one layer's wgrad partials + data gradient in one launch",
+        py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("wt"), py::arg("stride"), py::arg("relu_out"));
+  m.def("conv_backward_pair_ok", &conv_backward_pair_ok, "whether conv_backward_pair takes this layer", py::arg("x"),
+        py::arg("N"), py::arg("KH"), py::arg("KW"), py::arg("stride"));
   m.def("conv_dgrad", &conv_dgrad, "NHWC conv data gradient with fused ReLU masks", py::arg("dy"), py::arg("y"),
         py::arg("wt"), py::arg("xp"), py::arg("stride"), py::arg("relu_out"), py::arg("relu_in"), py::arg("pad") = 0);
 }

@@ -408,19 +408,20 @@ __global__ __launch_bounds__(256) void conv_dgrad_pf_kernel(const bf16* __restri
 // issues all of its (<= kDgMaxTpg) taps' loads at once and the chain is one round trip deep.
 constexpr int kDgMaxTpg = 4;
 
+// the split-tap body for block (bx, by): by = stride phase, bx = 16-pixel tile; part = LDS
+// [8 waves][CT][64 lanes] f32x4; blockDim.x = 512 (8 waves: tap groups x channel halves)
 template <int CT, int NN>
-__global__ __launch_bounds__(512) void conv_dgrad_split_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
-                                                               const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
-                                                               bf16* __restrict__ dZp, ConvGeo g, int relu_out, int relu_in,
-                                                               int tpg) {
-  __shared__ f32x4 part[8][CT][64];  // [wave][channel tile][lane]
+__device__ __forceinline__ void conv_dgrad_split_body(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
+                                                      const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
+                                                      bf16* __restrict__ dZp, const ConvGeo& g, int relu_out, int relu_in,
+                                                      int tpg, int bx, int by, f32x4 (*part)[CT][64]) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nw = blockDim.x >> 6;
-  const int ph = blockIdx.y / g.S, pw = blockIdx.y - ph * g.S;
+  const int ph = by / g.S, pw = by - ph * g.S;
   const int Hc = (g.H - ph + g.S - 1) / g.S, Wc = (g.W - pw + g.S - 1) / g.S;
   const int HWc = Hc * Wc;
   const int P = g.B * HWc;
-  const int p0 = blockIdx.x * 16;
+  const int p0 = bx * 16;
   if (p0 >= P) return;  // (block-uniform)
   const int Kp = g.KH * g.KW * g.N;
   const int r = l & 15, kq = (l >> 4) * 8;
@@ -499,6 +500,26 @@ __global__ __launch_bounds__(512) void conv_dgrad_split_kernel(const bf16* __res
   }
 }
 
+// tap groups of the split-tap data gradient: 8 waves = (8 / NN) tap groups x NN channel halves;
+// 0 when a phase would need more than kDgMaxTpg taps per group (then the prefetching form runs)
+__host__ __device__ __forceinline__ int dgrad_split_tpg(const ConvGeo& g) {
+  const int nn = g.N / 32;
+  if (nn != 1 && nn != 2) return 0;
+  const int ntap_max = ((g.KH + g.S - 1) / g.S) * ((g.KW + g.S - 1) / g.S);
+  const int ts = 8 / nn;
+  const int tpg = (ntap_max + ts - 1) / ts;
+  return tpg <= kDgMaxTpg ? tpg : 0;
+}
+
+template <int CT, int NN>
+__global__ __launch_bounds__(512) void conv_dgrad_split_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ Y,
+                                                               const bf16* __restrict__ Wt, const bf16* __restrict__ Xp,
+                                                               bf16* __restrict__ dZp, ConvGeo g, int relu_out, int relu_in,
+                                                               int tpg) {
+  __shared__ f32x4 part[8][CT][64];  // [wave][channel tile][lane]
+  conv_dgrad_split_body<CT, NN>(dY, Y, Wt, Xp, dZp, g, relu_out, relu_in, tpg, blockIdx.x, blockIdx.y, part);
+}
+
 // ------------------------------------------------------------------ weight gradient (partials)
 // 512 threads; wave w owns output tiles t = w + 8 i (t = nt * KT + kt), TPW >= ceil(NT*KT/8).
 // Each block reduces a contiguous m range in chunks of CH rows staged transposed in LDS
@@ -507,10 +528,9 @@ __global__ __launch_bounds__(512) void conv_dgrad_split_kernel(const bf16* __res
 // chunk. CH = 128 for large M (4x the MFMA work per barrier pair and per load round trip),
 // 32 for the small BC batches, where more blocks matter more.
 template <typename TIn, int NT, int TPW, int CH>
-__global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__ X, const bf16* __restrict__ dY,
-                                                         const bf16* __restrict__ Y, float* __restrict__ slab, ConvGeo g,
-                                                         float in_scale, int relu_out, int m_per_block) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void conv_wgrad_body(const TIn* __restrict__ X, const bf16* __restrict__ dY,
+                                                const bf16* __restrict__ Y, float* __restrict__ slab, const ConvGeo& g,
+                                                float in_scale, int relu_out, int m_per_block, int blk, char* smem) {
   constexpr int LD = CH + 8;
   const int K = g.Kp;
   bf16* At = reinterpret_cast<bf16*>(smem);  // [K][LD]   im2col chunk, m contiguous
@@ -524,7 +544,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
   const bool tap_checked = g.P > 0 || g.Kp != g.KH * g.KW * g.C;
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
-  const int mb = blockIdx.x * m_per_block;
+  const int mb = blk * m_per_block;
   const int me = min(g.B * OHW, mb + m_per_block);
   f32x4 acc[TPW];
 #pragma unroll
@@ -600,7 +620,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
     __syncthreads();
   }
   // partial dW [N][K] then db [N] of this block
-  float* out = slab + (size_t)blockIdx.x * ((size_t)N * K + N);
+  float* out = slab + (size_t)blk * ((size_t)N * K + N);
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
     const int t = w + 8 * i;
@@ -612,6 +632,36 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
     }
   }
   if (tid < N) out[(size_t)N * K + tid] = bsum;
+}
+
+template <typename TIn, int NT, int TPW, int CH>
+__global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__ X, const bf16* __restrict__ dY,
+                                                         const bf16* __restrict__ Y, float* __restrict__ slab, ConvGeo g,
+                                                         float in_scale, int relu_out, int m_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_wgrad_body<TIn, NT, TPW, CH>(X, dY, Y, slab, g, in_scale, relu_out, m_per_block, blockIdx.x, smem);
+}
+
+// One layer's two independent backward products in ONE launch (the BC step's conv2 / conv3): blocks
+// [0, n_wg) are the weight-gradient partials (conv_wgrad_body), the rest the split-tap data
+// gradient (conv_dgrad_split_body, block b -> tile b % dg_gx, phase b / dg_gx). Both read the same
+// dY / Y; neither feeds the other, so the launch's critical path is the longer of the two instead
+// of their sum plus a dispatch.
+template <int NT, int TPW, int CH, int CT, int NN>
+__global__ __launch_bounds__(512) void conv_back_pair_kernel(const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                             const bf16* __restrict__ Y, float* __restrict__ slab,
+                                                             ConvGeo g, int relu_out, int m_per_block, int n_wg,
+                                                             const bf16* __restrict__ Wt, bf16* __restrict__ dZp,
+                                                             int relu_in, int tpg, int dg_gx) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  if (b < n_wg) {
+    conv_wgrad_body<bf16, NT, TPW, CH>(X, dY, Y, slab, g, 1.f, relu_out, m_per_block, b, smem);
+  } else {
+    const int d = b - n_wg;
+    conv_dgrad_split_body<CT, NN>(dY, Y, Wt, X, dZp, g, relu_out, relu_in, tpg, d % dg_gx, d / dg_gx,
+                                  reinterpret_cast<f32x4(*)[CT][64]>(smem));
+  }
 }
 
 // The 4 fixed-order accumulators of a slab column (accumulator j: blocks b = j mod 4 in order,
@@ -960,6 +1010,58 @@ hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y,
   }
 }
 
+bool conv_back_pair_ok(const ConvGeo& g) {
+  if (!conv_geo_ok(g) || g.N % 32 != 0 || g.C % 16 != 0 || g.C > 64 || g.P != 0) return false;
+  const int Hc = (g.H + g.S - 1) / g.S, Wc = (g.W + g.S - 1) / g.S;
+  if (g.B * Hc * Wc >= (1 << 16) || dgrad_split_tpg(g) == 0) return false;  // small batches only
+  if (wgrad_chunk(g) != 32) return false;
+  const int tiles = (g.N / 16) * (g.Kp / 16);
+  return (tiles + 7) / 8 <= 18;
+}
+
+hipError_t conv_back_pair(const void* X, const void* dY, const void* Y, float* slab, const void* Wt, void* dZp,
+                          const ConvGeo& g, int relu_out, int relu_in, hipStream_t s) {
+  if (!conv_back_pair_ok(g)) return hipErrorInvalidValue;
+  int nblk = 0, mpb = 0;
+  conv_wgrad_blocks(g, &nblk, &mpb);
+  const int tpg = dgrad_split_tpg(g);
+  const int Hc = (g.H + g.S - 1) / g.S, Wc = (g.W + g.S - 1) / g.S;
+  const int gx = (g.B * Hc * Wc + 15) / 16;
+  const int n_dg = gx * g.S * g.S;
+  constexpr int CH = 32;
+  const size_t lds_wg = ((size_t)g.Kp + (size_t)g.N) * (CH + 8) * sizeof(bf16);
+  const size_t lds_dg = (size_t)8 * (g.C / 16) * 64 * sizeof(f32x4);
+  const size_t lds = lds_wg > lds_dg ? lds_wg : lds_dg;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const int tpw = ((g.N / 16) * (g.Kp / 16) + 7) / 8;
+  const bf16* x = static_cast<const bf16*>(X);
+  const bf16* dy = static_cast<const bf16*>(dY);
+  const bf16* y = static_cast<const bf16*>(Y);
+  const bf16* wt = static_cast<const bf16*>(Wt);
+  bf16* dz = static_cast<bf16*>(dZp);
+  const dim3 grid(nblk + n_dg), block(512);
+  const int nn = g.N / 32;
+#define IA_BP(NT, TPW, CT, NN)                                                                                           \
+  hipLaunchKernelGGL((conv_back_pair_kernel<NT, TPW, CH, CT, NN>), grid, block, lds, s, x, dy, y, slab, g, relu_out, mpb, \
+                     nblk, wt, dz, relu_in, tpg, gx)
+#define IA_BP_T(NT, CT, NN)         \
+  if (tpw <= 4) IA_BP(NT, 4, CT, NN);      \
+  else if (tpw <= 8) IA_BP(NT, 8, CT, NN); \
+  else if (tpw <= 12) IA_BP(NT, 12, CT, NN); \
+  else IA_BP(NT, 18, CT, NN)
+  // NT = N / 16 (wgrad output tiles), CT = C / 16 (dgrad output tiles), NN = N / 32
+  if (nn == 2 && g.C == 64) { IA_BP_T(4, 4, 2); }
+  else if (nn == 2 && g.C == 32) { IA_BP_T(4, 2, 2); }
+  else if (nn == 2 && g.C == 16) { IA_BP_T(4, 1, 2); }
+  else if (nn == 1 && g.C == 64) { IA_BP_T(2, 4, 1); }
+  else if (nn == 1 && g.C == 32) { IA_BP_T(2, 2, 1); }
+  else if (nn == 1 && g.C == 16) { IA_BP_T(2, 1, 1); }
+  else return hipErrorInvalidValue;
+#undef IA_BP_T
+#undef IA_BP
+  return hipGetLastError();
+}
+
 hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
                       int relu_out, int relu_in, hipStream_t s) {
   if (!conv_geo_ok(g) || g.N % 32 != 0 || g.C % 16 != 0 || g.C > 64) return hipErrorInvalidValue;
@@ -979,13 +1081,9 @@ hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void*
   const char* pf_env = getenv("IMITATION_AMD_CONV_DGRAD_PF");
   const char* sp_env = getenv("IMITATION_AMD_CONV_DGRAD_SPLIT");
   const bool pf = !big && (nn == 1 || nn == 2) && !(pf_env && pf_env[0] == '0');
-  // tap groups of ~3 taps (the largest phase has ceil(KH / S) * ceil(KW / S)), <= 8 waves per block
-  const int ntap_max = ((g.KH + g.S - 1) / g.S) * ((g.KW + g.S - 1) / g.S);
-  int ts = (ntap_max + 2) / 3;
-  if (ts * nn > 8) ts = 8 / nn;
-  const int tpg = (ntap_max + ts - 1) / ts;
-  const bool split = pf && tpg <= kDgMaxTpg && !(sp_env && sp_env[0] == '0');
-  const dim3 sgrid((P + 15) / 16, g.S * g.S), sblock(64 * ts * nn);
+  const int tpg = dgrad_split_tpg(g);  // (8 waves: the same tap grouping as conv_back_pair)
+  const bool split = pf && tpg > 0 && !(sp_env && sp_env[0] == '0');
+  const dim3 sgrid((P + 15) / 16, g.S * g.S), sblock(512);
 #define IA_DG(CT)                                                                                                         \
   if (big) hipLaunchKernelGGL((conv_dgrad_kernel<CT, 4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in);     \
   else if (split && nn == 2) hipLaunchKernelGGL((conv_dgrad_split_kernel<CT, 2>), sgrid, sblock, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in, tpg); \

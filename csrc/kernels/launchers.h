@@ -450,6 +450,11 @@ hipError_t conv_forward(int in_kind, const void* X, const void* Wb, const float*
 // dW fp32 [N][KH][KW][C], db fp32 [N] (may be null); slab of conv_wgrad_slab_floats
 hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y, float* slab, float* dW, float* db,
                       const ConvGeo& g, float in_scale, int relu_out, hipStream_t s);
+// one layer's weight-gradient partials (slab, as conv_wgrad with dW == nullptr; bf16 X) and its data
+// gradient (as conv_dgrad with Xp = X) in ONE launch; small unpadded batches (conv_back_pair_ok)
+bool conv_back_pair_ok(const ConvGeo& g);
+hipError_t conv_back_pair(const void* X, const void* dY, const void* Y, float* slab, const void* Wt, void* dZp,
+                          const ConvGeo& g, int relu_out, int relu_in, hipStream_t s);
 // dZp bf16 [B*H*W][C] = [Xp > 0] * conv^T(dY * [Y > 0]); Wt bf16 [C][KH][KW][N]
 hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
                       int relu_out, int relu_in, hipStream_t s);

@@ -33,6 +33,7 @@ from typing import Any, Dict, List, Tuple
 
 import torch as th
 
+from imitation_amd.utils.streams import shared_stream
 from imitation_amd.utils import profiling
 from numpy import prod as np_prod
 
@@ -199,7 +200,7 @@ class DeviceAIRL(OutputNormMixin, DeviceEngineMixin, AIRL):
         # next rollout enqueued before the host reads anything); IMITATION_AMD_DISC_OVERLAP=0: serial
         self._overlap_disc = os.environ.get("IMITATION_AMD_DISC_OVERLAP", "1") != "0"
         self._disc_on_main = True
-        self._side_stream = th.cuda.Stream(device=self._dev) if self._overlap_disc else None  # staging copies
+        self._side_stream = shared_stream(self._dev, "engine_side") if self._overlap_disc else None  # staging copies
         self._pol_defer_buf = None
         self._disc_split = False
         if not ok:

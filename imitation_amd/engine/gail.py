@@ -47,6 +47,7 @@ import numpy as np
 import torch as th
 from torch import nn
 
+from imitation_amd.utils.streams import shared_stream
 from imitation_amd import ops
 from imitation_amd.algorithms.adversarial import common
 from imitation_amd.algorithms.adversarial.gail import GAIL
@@ -487,7 +488,7 @@ class DeviceGeneratorCore:
         # with the update. The next round's update, which rewrites these buffers, is enqueued
         # only after the host has waited for this event.
         if getattr(self, "_log_stream", None) is None:
-            self._log_stream = th.cuda.Stream(device=self._dev)
+            self._log_stream = shared_stream(self._dev, "engine_log")
         done = getattr(self, "_ppo_done", None)
         if done is not None:
             self._wait_ev(self._log_stream, done)
@@ -1134,7 +1135,7 @@ class DeviceEngineMixin(DeviceGeneratorCore):
         # per minibatch and applied in order after PPO, so the result is bitwise that of
         # the serial order.
         self._overlap_disc = os.environ.get("IMITATION_AMD_DISC_OVERLAP", "1") != "0"
-        self._side_stream = th.cuda.Stream(device=dev) if self._overlap_disc else None
+        self._side_stream = shared_stream(dev, "engine_side") if self._overlap_disc else None
         self._pol_defer_buf = None
         if self._overlap_disc and self.pol_norm is not None and self._disc_plan.pol_cols > 0:
             self._ensure_pol_defer(max(1, self.n_disc_updates_per_round))

@@ -136,18 +136,43 @@ class FusedCnnBCStep:
             dz = dx.view(hs[-1].shape)
             # weight-gradient partials per layer; their fixed-order reductions in ONE launch at the end
             red = {k: [] for k in ("x", "dy", "kh", "kw", "s", "p", "slab", "dw", "db")}
+            pair = self._pairs(x, hs)
             for i in range(n - 1, -1, -1):
                 c = convs[i]
                 inp = x if i == 0 else hs[i - 1]
                 top = i == n - 1  # relu_out: the top conv's ReLU mask is applied to dZ in the loads
                 kh, kw, st = int(c.kernel_size[0]), int(c.kernel_size[1]), int(c.stride[0])
-                slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
+                if i > 0 and pair[i]:
+                    # this layer's weight-gradient partials and data gradient in ONE launch (they
+                    # read the same dZ and neither feeds the other)
+                    slab, dz_next = C.conv_backward_pair(inp, dz, hs[i], wts[i], st, top)
+                else:
+                    slab = C.conv_wgrad_partials(inp, dz, hs[i], kh, kw, st, 1.0 / 255.0 if i == 0 else 1.0, top, 0)
+                    dz_next = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], st, top, True, 0) if i > 0 else None
                 for k, v in zip(red, (inp, dz, kh, kw, st, 0, slab, self.g_conv[i][0], self.g_conv[i][1])):
                     red[k].append(v)
-                if i > 0:
-                    dz = C.conv_dgrad(dz, hs[i], wts[i], hs[i - 1], st, top, True, 0)
+                dz = dz_next
             C.conv_reduce_multi(*red.values())
         return self.metrics
+
+
+    def _pairs(self, x: th.Tensor, hs: List[th.Tensor]) -> List[bool]:
+        """Per conv layer: whether its backward runs as one paired launch (bf16 input, BC-size batch;
+        ``IMITATION_AMD_BC_CONV_PAIR=0`` the separate wgrad / dgrad launches)."""
+        key = (tuple(x.shape), len(hs))
+        cached = getattr(self, "_pair_key", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        import os
+
+        on = os.environ.get("IMITATION_AMD_BC_CONV_PAIR", "1") != "0"
+        out = [False]
+        for i in range(1, len(self.convs)):
+            c = self.convs[i]
+            out.append(on and bool(self.C.conv_backward_pair_ok(hs[i - 1], c.out_channels, int(c.kernel_size[0]),
+                                                                int(c.kernel_size[1]), int(c.stride[0]))))
+        self._pair_key = (key, out)
+        return out
 
 
 def metrics_fields(m: th.Tensor) -> Dict[str, Any]:

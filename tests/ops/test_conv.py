@@ -263,3 +263,63 @@ def test_fc_wgrad_channel_blocks_bitwise_the_column_blocks(monkeypatch, M):
         out.append([t.clone() for t in C.fc_backward(x, dh, h, wts[0], C3, True)])
     for a, b in zip(*out):
         assert th.equal(a, b)
+
+
+def _layer_case(B, C, N, KH, S, H, seed):
+    g = th.Generator().manual_seed(seed)
+    OH = (H - KH) // S + 1
+    x = th.relu(th.randn(B, H, H, C, generator=g)).to(th.bfloat16).cuda()
+    y = th.randn(B, OH, OH, N, generator=g).to(th.bfloat16).cuda()  # signs drive the relu_out mask
+    dy = th.randn(B, OH, OH, N, generator=g).to(th.bfloat16).cuda()
+    w = (th.randn(N, C, KH, KH, generator=g) * 0.05).cuda()
+    return x, y, dy, w
+
+
+# (B, C, N, KH, S, H): NatureCNN conv3 / conv2 at the BC / collector batch sizes
+_BC_LAYERS = [(32, 64, 64, 3, 1, 9), (64, 64, 64, 3, 1, 9), (32, 32, 64, 4, 2, 20), (64, 32, 64, 4, 2, 20),
+              (7, 64, 64, 3, 1, 9)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,N,KH,S,H", _BC_LAYERS)
+def test_conv_dgrad_small_batch_forms_match_fp32_and_pf_is_bitwise_the_plain_loop(monkeypatch, B, C, N, KH, S, H):
+    """the prefetching small-batch data gradient (conv_dgrad_pf_kernel) is bitwise the
+    plain loop (same tap order and MFMA sequence per accumulator); the split-tap form (taps and
+    channel halves over waves, LDS sum) sums in another order and matches the fp32 reference."""
+    from imitation_amd import ops
+
+    Cn = ops.native()
+    x, y, dy, w = _layer_case(B, C, N, KH, S, H, 11 + B + C)
+    _, wts = Cn.conv_pack_weights([w], [True])
+    out = {}
+    for name, pf, split in (("plain", "0", "0"), ("pf", "1", "0"), ("split", "1", "1")):
+        monkeypatch.setenv("IMITATION_AMD_CONV_DGRAD_PF", pf)
+        monkeypatch.setenv("IMITATION_AMD_CONV_DGRAD_SPLIT", split)
+        out[name] = Cn.conv_dgrad(dy, y, wts[0], x, S, True, True, 0).clone()
+    assert th.equal(out["plain"], out["pf"])
+    # fp32 reference: dZ = [x > 0] * conv_transpose(dy * [y > 0]) with the bf16 operands
+    dz = (dy.float() * (y.float() > 0)).permute(0, 3, 1, 2)
+    wb = w.to(th.bfloat16).float()
+    ref = th.nn.functional.conv_transpose2d(dz, wb, stride=S).permute(0, 2, 3, 1)
+    ref = ref * (x.float() > 0)
+    err = float((out["split"].float() - ref).norm() / ref.norm())
+    assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,N,KH,S,H", _BC_LAYERS)
+def test_conv_backward_pair_is_bitwise_the_two_launches(monkeypatch, B, C, N, KH, S, H):
+    """conv_backward_pair (weight-gradient partials + split-tap data gradient in ONE launch) gives
+    bitwise the slab of conv_wgrad_partials and the dZ of conv_dgrad (split form)."""
+    from imitation_amd import ops
+
+    Cn = ops.native()
+    monkeypatch.setenv("IMITATION_AMD_CONV_DGRAD_SPLIT", "1")
+    x, y, dy, w = _layer_case(B, C, N, KH, S, H, 3 + B + C)
+    _, wts = Cn.conv_pack_weights([w], [True])
+    assert Cn.conv_backward_pair_ok(x, N, KH, KH, S)
+    slab, dz = Cn.conv_backward_pair(x, dy, y, wts[0], S, True)
+    slab_ref = Cn.conv_wgrad_partials(x, dy, y, KH, KH, S, 1.0, True, 0)
+    dz_ref = Cn.conv_dgrad(dy, y, wts[0], x, S, True, True, 0)
+    assert th.equal(slab, slab_ref)
+    assert th.equal(dz, dz_ref)

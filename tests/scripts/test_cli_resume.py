@@ -96,7 +96,9 @@ def test_full_checkpoints_keep_newest(tmp_path):
 def test_train_adversarial_resume_is_bitwise_on_device(tmp_path, command):
     named = ["demonstrations.fast", "policy_evaluation.fast"]
     updates = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
-                   expert=dict(policy_type="random", loader_kwargs={}),
+                   # ZeroPolicy demos: a RandomPolicy expert samples from an unseeded action space (as the
+                   # reference's does), so its demonstrations -- and the run -- differ run to run
+                   expert=dict(policy_type="zero", loader_kwargs={}),
                    rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
                    algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=0)
     _check_resume(tmp_path, command, named, updates, per_round=1024, n=4)

@@ -21,7 +21,7 @@ def run(root, cmd, total, **kw):
     from imitation_amd.scripts.train_adversarial import train_adversarial_ex
 
     upd = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
-               expert=dict(policy_type="random", loader_kwargs={}),
+               expert=dict(policy_type="zero", loader_kwargs={}),
                rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
                algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=0,
                full_checkpoint_interval=2, full_checkpoint_keep=10, total_timesteps=total * 1024, seed=0,
@@ -42,6 +42,22 @@ def run(root, cmd, total, **kw):
     finally:
         common.AdversarialTrainer.train = orig
     print(f"{root}: trainer {seen.get('fused')}", flush=True)
+    assert r.status == "COMPLETED"
+    cks = sorted(glob.glob(os.path.join(root, "**", "full_checkpoints", "ckpt-*"), recursive=True))
+    return {int(os.path.basename(c)[5:]): th.load(os.path.join(c, "state.pt"), weights_only=True) for c in cks}, cks
+
+
+def run_pref(root, iters_total=3, **kw):
+    """train_preference_comparisons on the device agent (full checkpoint per iteration)."""
+    from imitation_amd.scripts.train_preference_comparisons import train_preference_comparisons_ex
+
+    upd = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
+               rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
+               total_timesteps=4 * 1024, total_comparisons=16, num_iterations=iters_total, fragment_length=4,
+               reward_trainer_kwargs=dict(epochs=1), checkpoint_interval=0, full_checkpoint_interval=1,
+               full_checkpoint_keep=10, seed=0, logging={"log_root": root}, **kw)
+    r = train_preference_comparisons_ex.run(named_configs=["fast", "rl.fast", "environment.fast", "policy_evaluation.fast"],
+                                            config_updates=upd)
     assert r.status == "COMPLETED"
     cks = sorted(glob.glob(os.path.join(root, "**", "full_checkpoints", "ckpt-*"), recursive=True))
     return {int(os.path.basename(c)[5:]): th.load(os.path.join(c, "state.pt"), weights_only=True) for c in cks}, cks
@@ -77,6 +93,12 @@ def main():
         print("torch deterministic algorithms on", flush=True)
     tmp = tempfile.mkdtemp()
     os.chdir(tmp)
+    if cmd == "pref":
+        A, _ = run_pref(os.path.join(tmp, "A"))
+        B, _ = run_pref(os.path.join(tmp, "B"))
+        for s in sorted(A):
+            print(f"pref A vs B iteration {s}: {cmp(f'A/B@{s}', A[s], B[s])} differing fields", flush=True)
+        return
     A, _ = run(os.path.join(tmp, "A"), cmd, 8)
     B, _ = run(os.path.join(tmp, "B"), cmd, 8)
     for s in sorted(A):
