@@ -49,8 +49,11 @@ class DeviceEvent {
   bool device_scope() const { return device_scope_; }
 
  private:
+  // None: the current stream; an explicit handle as given (0 = the null stream, which is torch's
+  // default stream -- not "the current stream", which inside a `with th.cuda.stream(side)` block is
+  // the side stream)
   static hipStream_t pick(c10::optional<int64_t> stream) {
-    if (stream.has_value() && *stream != 0) return reinterpret_cast<hipStream_t>(*stream);
+    if (stream.has_value()) return reinterpret_cast<hipStream_t>(*stream);
     return ia_stream();
   }
   hipEvent_t ev_ = nullptr;

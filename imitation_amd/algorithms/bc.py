@@ -331,9 +331,11 @@ class _BCBase(algo_base.DemonstrationAlgorithm):
 
         loader = self._demo_data_loader
         loader = getattr(loader, "data_loader", loader)  # (make_data_loader's batch-size-checking wrapper)
-        if (graphed is None or self._grad_bucket is not None or on_batch_end is not None or not hasattr(loader, "next_epoch_perm")
+        if (graphed is None or on_batch_end is not None or not hasattr(loader, "next_epoch_perm")
                 or self.minibatch_size != self.batch_size or os.environ.get("IMITATION_AMD_BC_EPOCH_GRAPH", "1") == "0"):
             return None
+        if self._grad_bucket is not None and _DeviceEpochRunner.dp_comm(self.optimizer) is None:
+            return None  # data parallel without a capturable gradient all-reduce: _DPFusedStep per minibatch
         r = getattr(self, "_epoch_run", None)
         if r is not None and r.graphed is graphed and r.loader is not loader and getattr(loader, "agg", None) is r.agg:
             # a new loader over the same aggregate (DAgger: one per round): the captured step
@@ -509,6 +511,10 @@ class _DeviceEpochRunner:
         opt = trainer.optimizer
         self._fold = (hasattr(opt, "graph_epoch_step_ok") and opt.graph_epoch_step_ok()
                       and os.environ.get("IMITATION_AMD_BC_FOLD_LAUNCHES", "1") != "0")
+        self._world = pdist.world_size()
+        self._comm = _DeviceEpochRunner.dp_comm(opt) if self._world > 1 else None
+        if self._world > 1 and self._comm is None:
+            self.ok = False
         kmax = max(1, int(os.environ.get("IMITATION_AMD_BC_GRAPH_K", self.K)))
         # graph sizes: the largest, then powers of two below it. A run of n steps replays the
         # largest as often as it fits and each smaller one at most once, so the remainder is
@@ -525,10 +531,45 @@ class _DeviceEpochRunner:
             self._f = f
         return f
 
+    @staticmethod
+    def dp_comm(optimizer):
+        """Under data parallelism, the one-shot communicator (``parallel/oneshot.py``: one kernel,
+        capture-safe) when it can reduce the optimizer's single flat gradient bucket in chunks of
+        its staging size; None otherwise (then the per-minibatch ``_DPFusedStep`` runs). Every rank
+        reaches this at the same point (the communicator's creation is collective)."""
+        if pdist.world_size() <= 1:
+            return None
+        from imitation_amd.parallel import oneshot
+
+        comm = oneshot.get()
+        if comm is None or not (hasattr(optimizer, "graph_epoch_step_ok") and optimizer.graph_epoch_step_ok()):
+            return None
+        flat = optimizer.flat_grads[0]
+        return comm if comm.fits(flat[: min(flat.numel(), comm.stage_bytes // 4 // 4 * 4)]) else None
+
+    def _dp_allreduce(self) -> None:
+        """The minibatch-mean gradient over ranks, inside the captured step: the flat bucket in
+        one-shot chunks of the staging size (rank-order sum of grad / world per element: bitwise
+        the eager ``FlatGradBucket.allreduce`` of the same bucket)."""
+        comm = self._comm
+        flat = self.trainer.optimizer.flat_grads[0]
+        step = comm.stage_bytes // 4 // 4 * 4  # floats per chunk, 16-B multiple
+        for o in range(0, flat.numel(), step):
+            comm.allreduce_(flat[o : o + step], 1.0 / self._world)
+
     def _one_step(self):
         C = self._f.C
         bufs = self.agg.batch_buffers(self.B)
         opt = self.trainer.optimizer
+        if self._comm is not None:
+            # data parallel, graph-resident: the bucket all-reduce is a captured one-shot kernel
+            # between the fused step and Adam (reference hook point bc.py:464-466)
+            C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs,
+                                 inc=opt.step_counter())
+            self._f(bufs[0], bufs[1])
+            self._dp_allreduce()
+            opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor))
+            return
         if self._fold:
             # the step counter's add rides on the gather launch, the metrics append on Adam's:
             # 17 launches per step instead of 19 (same arithmetic)

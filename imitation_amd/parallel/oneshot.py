@@ -141,31 +141,41 @@ class OneShotComm:
         then poisons its output and sets the error word)."""
         reasons = []
         saved, self.timeout_s = self.timeout_s, min(self.timeout_s, 5.0)
+        # Every rank issues every process-group collective below whatever happened before it (each
+        # step has its own try): a rank whose one-shot call raised must not skip to the verdict's
+        # MIN all-reduce while the others issue the RCCL cross-check -- mismatched collectives hang
+        # or pair wrongly. (One-shot calls only wait on peers, boundedly.)
+        w = self.world
         try:
-            # (every rank runs every step whatever it found so far: the collective sequence
-            # must stay identical on all ranks until the verdict is agreed)
-            w = self.world
             for n in (1, 5, 1027, min(self.stage_bytes // 4, 16384 + 3)):
                 for rep in range(2):
-                    x = torch.arange(n, dtype=torch.float32, device=self.device) * (self.rank + 1) + rep
-                    self.allreduce_(x)
-                    exp = torch.arange(n, dtype=torch.float32, device=self.device) * (w * (w + 1) / 2) + rep * w
-                    if not bool(torch.allclose(x, exp, rtol=1e-6, atol=1e-3)) and not reasons:
-                        reasons.append(f"closed-form mismatch at n={n}")
+                    try:
+                        x = torch.arange(n, dtype=torch.float32, device=self.device) * (self.rank + 1) + rep
+                        self.allreduce_(x)
+                        exp = torch.arange(n, dtype=torch.float32, device=self.device) * (w * (w + 1) / 2) + rep * w
+                        if not bool(torch.allclose(x, exp, rtol=1e-6, atol=1e-3)) and not reasons:
+                            reasons.append(f"closed-form mismatch at n={n}")
+                    except Exception as e:  # noqa: BLE001 -- any failure disables the path
+                        reasons.append(f"closed form n={n} raised {e!r}")
             n = min(self.stage_bytes // 4, 4099)
             g = torch.Generator().manual_seed(1234 + self.rank)
             exact = (torch.randint(-512, 512, (n,), generator=g).float() + 0.5 * (self.rank % 2)).to(self.device)
             fuzzy = torch.randn(n, generator=g).to(self.device)
             for name, t in (("exact", exact), ("fuzzy", fuzzy)):
-                mine = t.clone()
-                self.allreduce_(mine)
-                ref = self._reference_allreduce(t)
+                mine = None
+                try:
+                    mine = t.clone()
+                    self.allreduce_(mine)
+                except Exception as e:  # noqa: BLE001
+                    reasons.append(f"{name} one-shot call raised {e!r}")
+                    mine = None
+                ref = self._reference_allreduce(t)  # (issued on every rank)
+                if mine is None:
+                    continue
                 if name == "exact" and not torch.equal(mine, ref):
                     reasons.append("not bitwise equal to the process-group all-reduce on exactly representable data")
                 if name == "fuzzy" and not bool(torch.allclose(mine, ref, rtol=1e-5, atol=1e-5 * w)):
                     reasons.append("differs from the process-group all-reduce beyond rounding")
-        except Exception as e:  # noqa: BLE001 -- any failure disables the path
-            reasons.append(f"raised {e!r}")
         finally:
             self.timeout_s = saved
         if self.device.type == "cuda":

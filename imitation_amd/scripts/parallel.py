@@ -244,16 +244,30 @@ def _schedule(ex_name: str, trials: List[Dict[str, Any]], observer_dir: str, run
             for i, (p, si) in list(running.items()):  # a trial process that died without a result
                 if not p.is_alive() and records[i] is None:
                     p.join()
-                    records[i] = {"result": None, "config_updates": trials[i].get("config_updates", {}),
-                                  "named_configs": trials[i].get("named_configs", []), "status": "FAILED",
-                                  "error": f"trial process exited with code {p.exitcode}"}
-                    del running[i]
+                    # its result may still be in flight on the queue: drain before declaring it lost
+                    try:
+                        while True:
+                            j, rj = results.get_nowait()
+                            records[j] = rj
+                            if j in running and j != i:
+                                pj, sj = running.pop(j)
+                                pj.join()
+                                free.append(sj)
+                    except queue_mod.Empty:
+                        pass
+                    if records[i] is None:
+                        records[i] = {"result": None, "config_updates": trials[i].get("config_updates", {}),
+                                      "named_configs": trials[i].get("named_configs", []), "status": "FAILED",
+                                      "error": f"trial process exited with code {p.exitcode}"}
+                    running.pop(i, None)
                     free.append(si)
             continue
-        records[i] = rec
-        p, si = running.pop(i)
-        p.join()
-        free.append(si)
+        records[i] = rec  # (a late real result overwrites a FAILED record)
+        entry = running.pop(i, None)
+        if entry is not None:
+            p, si = entry
+            p.join()
+            free.append(si)
     return [r for r in records if r is not None]
 
 

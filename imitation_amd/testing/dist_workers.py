@@ -556,3 +556,50 @@ def oneshot_selftest_gpu_worker(rank, world):
     c = oneshot._COMM
     rep = c.self_test_report() if c is not None else (False, "no communicator")
     return (c is not None, oneshot.DISABLED_REASON, rep)
+
+
+def bc_dp_epoch_worker(rank, world, mode, n_epochs=2, n_rows=32 * 9 + 5, profile_dir=None):
+    """Data-parallel BC on the fused NatureCNN step over a device aggregate (the DAgger-Pong learner),
+    ``IMITATION_AMD_BC_EPOCH_GRAPH=mode``: "1" the graph-resident epoch runner (16-step graphs with
+    the one-shot gradient all-reduce captured inside), "0" the per-minibatch ``_DPFusedStep``
+    (graph, eager all-reduce, graph). Same frames on every rank, per-rank minibatch orders."""
+    import os
+
+    import torch as th
+
+    os.environ["IMITATION_AMD_BC_EPOCH_GRAPH"] = mode
+    from imitation_amd.algorithms import bc
+    from imitation_amd.engine.dagger import DeviceDemoAggregate, DeviceTransitionsLoader
+    from imitation_amd.envs.vec_env import native_spaces
+    from imitation_amd.rl.policies import ActorCriticCnnPolicy
+    from imitation_amd.util import logger as ilog
+
+    dev = th.device("cuda", 0)
+    obs_space, act_space = native_spaces("PongNoFrameskip-v4")
+    g = th.Generator(device=dev).manual_seed(5)
+    obs = th.randint(0, 256, (n_rows, 84, 84, 4), generator=g, device=dev, dtype=th.int64).to(th.uint8)
+    acts = th.randint(0, int(act_space.n), (n_rows,), generator=g, device=dev)
+    th.manual_seed(11)
+    pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: th.finfo(th.float32).max).to(dev)
+    agg = DeviceDemoAggregate(dev)
+    agg.append(obs, acts, gather=False)
+    log = ilog.configure(format_strs=[])
+    recorded = []
+    orig_dump = log.dump
+
+    def dump(step=0):
+        recorded.append((step, {k: v for k, v in log.name_to_value.items() if k.startswith("bc/")}))
+        orig_dump(step)
+
+    log.dump = dump
+    trainer = bc.BC(observation_space=obs_space, action_space=act_space, rng=np.random.default_rng(rank), policy=pol,
+                    batch_size=32, device=dev, custom_logger=log)
+    trainer.set_demonstrations(DeviceTransitionsLoader(agg, 32, seed=3 + rank))
+    trainer.train(n_epochs=n_epochs, log_interval=4, progress_bar=False)
+    th.cuda.synchronize()
+    run = getattr(trainer, "_epoch_run", None)
+    f = trainer.optimizer._flat[0]
+    return {"params": [p.detach().cpu().numpy().copy() for p in pol.parameters()], "m": f["m"].cpu().numpy().copy(),
+            "v": f["v"].cpu().numpy().copy(), "recorded": recorded,
+            "epoch_runner": run is not None and run._comm is not None,
+            "dp_fused_replays": getattr(getattr(trainer, "_dp_step", None), "n_replays", 0)}
