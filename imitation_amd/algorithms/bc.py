@@ -515,6 +515,10 @@ class _DeviceEpochRunner:
         self._comm = _DeviceEpochRunner.dp_comm(opt) if self._world > 1 else None
         if self._world > 1 and self._comm is None:
             self.ok = False
+        if self._comm is not None:
+            from imitation_amd.utils.streams import shared_stream
+
+            self._dp_side = shared_stream(self.agg.device, "bc_dp_reduce")
         kmax = max(1, int(os.environ.get("IMITATION_AMD_BC_GRAPH_K", self.K)))
         # graph sizes: the largest, then powers of two below it. A run of n steps replays the
         # largest as often as it fits and each smaller one at most once, so the remainder is
@@ -547,15 +551,33 @@ class _DeviceEpochRunner:
         flat = optimizer.flat_grads[0]
         return comm if comm.fits(flat[: min(flat.numel(), comm.stage_bytes // 4 // 4 * 4)]) else None
 
-    def _dp_allreduce(self) -> None:
-        """The minibatch-mean gradient over ranks, inside the captured step: the flat bucket in
-        one-shot chunks of the staging size (rank-order sum of grad / world per element: bitwise
-        the eager ``FlatGradBucket.allreduce`` of the same bucket)."""
-        comm = self._comm
+    def _dp_ranges(self):
+        """(FC range, other ranges) of the flat gradient bucket, each split into one-shot chunks
+        (<= staging size, 16-B multiples): the FC layer's gradients (6.4 of NatureCNN's 6.7 MB) are
+        final right after ``fc_backward``, the conv / head ones only after the conv backward."""
+        r = getattr(self, "_ranges", None)
+        if r is not None:
+            return r
         flat = self.trainer.optimizer.flat_grads[0]
-        step = comm.stage_bytes // 4 // 4 * 4  # floats per chunk, 16-B multiple
-        for o in range(0, flat.numel(), step):
-            comm.allreduce_(flat[o : o + step], 1.0 / self._world)
+        step = self._comm.stage_bytes // 4 // 4 * 4
+        w = self._f.g_lin[0]
+        o = (w.data_ptr() - flat.data_ptr()) // 4
+        lo, hi = o - o % 4, (o + w.numel() + 3) // 4 * 4  # (16-B aligned slices)
+
+        def chunks(a, b):
+            return [flat[i : min(b, i + step)] for i in range(a, b, step)]
+
+        fc = chunks(lo, hi)
+        rest = chunks(0, lo) + chunks(hi, flat.numel())
+        self._ranges = r = (fc, rest)
+        return r
+
+    def _dp_allreduce(self, parts) -> None:
+        """Mean over ranks, inside the captured step: one-shot kernels over ``parts`` (rank-order sum
+        of grad / world per element: bitwise the eager ``FlatGradBucket.allreduce``, whatever the
+        chunking)."""
+        for t in parts:
+            self._comm.allreduce_(t, 1.0 / self._world)
 
     def _one_step(self):
         C = self._f.C
@@ -566,8 +588,21 @@ class _DeviceEpochRunner:
             # between the fused step and Adam (reference hook point bc.py:464-466)
             C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs,
                                  inc=opt.step_counter())
-            self._f(bufs[0], bufs[1])
-            self._dp_allreduce()
+            fc, rest = self._dp_ranges()
+            main = th.cuda.current_stream()
+            side = self._dp_side
+
+            def after_fc():
+                # the FC gradients are final: reduce them on the side stream (in a captured graph: a
+                # parallel branch) while the main stream runs the conv backward
+                side.wait_stream(main)
+                with th.cuda.stream(side):
+                    self._dp_allreduce(fc)
+
+            self._f(bufs[0], bufs[1], after_fc=after_fc)
+            # (the one-shot calls of a rank share one staging region: the rest waits for the FC part)
+            main.wait_stream(side)
+            self._dp_allreduce(rest)
             opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor))
             return
         if self._fold:

@@ -109,7 +109,10 @@ class FusedCnnBCStep:
             return None
         return FusedCnnBCStep(policy, optimizer, ent_weight, l2_weight)
 
-    def __call__(self, obs: th.Tensor, acts: th.Tensor) -> th.Tensor:
+    def __call__(self, obs: th.Tensor, acts: th.Tensor, after_fc=None) -> th.Tensor:
+        """``after_fc``: called (no arguments) once the FC layer's gradients are in the bucket and
+        before the conv backward -- the data-parallel epoch starts the FC bucket's all-reduce there,
+        on a side stream, so it overlaps the conv backward."""
         C = self.C
         convs, lin, head = self.convs, self.lin, self.head
         n = len(convs)
@@ -133,6 +136,8 @@ class FusedCnnBCStep:
             dh = C.bc_head_train(out, head.weight.detach(), head.bias.detach(), a, self.flat, self.g_head[0], self.g_head[1],
                                  self.metrics, self.ws, self.ent_weight, self.l2_weight)
             _, _, dx = C.fc_backward(xf, dh, out, wts[n], C3, True, self.g_lin[0], self.g_lin[1])
+            if after_fc is not None:
+                after_fc()
             dz = dx.view(hs[-1].shape)
             # weight-gradient partials per layer; their fixed-order reductions in ONE launch at the end
             red = {k: [] for k in ("x", "dy", "kh", "kw", "s", "p", "slab", "dw", "db")}
