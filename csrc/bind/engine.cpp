@@ -88,6 +88,12 @@ void rollout(py::dict d) {
   a.trunc = tptr<float>(d, "trunc");
   a.next_obs = tptr<float>(d, "next_obs");
   a.ep_ret_out = tptr<float>(d, "ep_ret_out");
+  if (d.contains("prof") && !d["prof"].is_none()) {
+    auto t = d["prof"].cast<torch::Tensor>();
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kInt64 && t.numel() == (int64_t)a.N * 5,
+                "prof must be a contiguous int64 GPU tensor of N x 5");
+    a.prof = reinterpret_cast<long long*>(t.data_ptr());
+  }
   IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
 }
 

@@ -68,6 +68,10 @@ struct RolloutArgs {
   float* trunc;     // 1 where the episode was cut by the TimeLimit (not terminated)
   float* next_obs;  // terminal obs on done
   float* ep_ret_out;  // episode return where done
+  // optional phase-clock probe (tools/rollout_breakdown.py): [N][5] int64 = core-clock cycles spent
+  // in actor+sampling, env physics, observation, step tail, and the step count; the HalfCheetah
+  // bench configuration only
+  long long* prof;
 };
 
 // Parallel part (engine.hip): per transition V(s), log pi(a|s), the TimeLimit bootstrap

@@ -327,7 +327,15 @@ struct Cursors {
   int vec_step, act_step, sc_step;
 };
 
-template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1, int FS = -1>
+// Phase clock of the breakdown probe: the core clock, read after `dep` is in a register (the
+// volatile asm keeps the stamps in program order and the input ties each to its phase's result).
+__device__ __forceinline__ long long stamp(float dep) {
+  long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep));
+  return t;
+}
+
+template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1, int FS = -1, bool PROF = false>
 __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
@@ -399,6 +407,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   const int chunk = AW > 0 ? max(1, min(a.T, kNoiseFloats / AW)) : a.T;
   const bool has_explore = a.explore_mode != nullptr;
   const int max_steps = a.max_steps;
+  long long ph[4] = {0, 0, 0, 0}, n_prof = 0;
 
   for (int t0 = 0; t0 < a.T; t0 += chunk) {
     const int tc = min(chunk, a.T - t0);
@@ -425,6 +434,8 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
 
     const lf* nz = noise + (lane < AW ? lane : 0);
     for (int tr = 0; tr < tc; ++tr, nz += AW) {
+      long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+      if constexpr (PROF) t0 = stamp(o);
       if (lane < D) *c.obs = o;
       // ---- actor
       xb[lane] = lane < D ? (o - nmean) * nrstd : 0.f;
@@ -465,9 +476,12 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       int term = 0;
       float r_env;
       float o_next;
+      if constexpr (PROF) t1 = stamp(a_env);
       if (loco) {
         r_env = loco_step_regs<ENV, FS>(P.loco, L, a_env);
+        if constexpr (PROF) t2 = stamp(r_env);
         o_next = loco_obs<ENV>(P.loco, L, sb);
+        if constexpr (PROF) t3 = stamp(o_next);
       } else {
         if (lane < A) act[lane] = a_env;
         wave_sync();
@@ -517,7 +531,18 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
         o = o_next;
       }
       start = done ? 1.f : 0.f;
+      if constexpr (PROF) {
+        const long long t4 = stamp(o);
+        ph[0] += t1 - t0;
+        ph[1] += t2 - t1;
+        ph[2] += t3 - t2;
+        ph[3] += t4 - t3;
+        ++n_prof;
+      }
     }
+  }
+  if constexpr (PROF) {
+    if (lane < 5) a.prof[n * 5 + lane] = lane == 4 ? n_prof : lane == 0 ? ph[0] : lane == 1 ? ph[1] : lane == 2 ? ph[2] : ph[3];
   }
   if (loco) loco_store(P.loco, L, st);
   wave_sync();
@@ -568,7 +593,10 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   // (+ the frame skip of the benchmark recipes: HalfCheetah 5 with the [32, 32] tanh actor,
   // Hopper / Walker 4 with the [64, 64] ReLU one)
   const int fs = env == CE_LOCO3 ? p.frame_skip : 0;
-  if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)
+  if (a.prof) {  // the phase-clock probe exists for the HalfCheetah bench configuration only
+    if (!(split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, true>), g, b, lds, s, a);
+  } else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5>), g, b, lds, s, a);
   else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 4)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 4>), g, b, lds, s, a);

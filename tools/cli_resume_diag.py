@@ -98,6 +98,16 @@ def main():
         B, _ = run_pref(os.path.join(tmp, "B"))
         for s in sorted(A):
             print(f"pref A vs B iteration {s}: {cmp(f'A/B@{s}', A[s], B[s])} differing fields", flush=True)
+        import shutil
+
+        _, cks = run_pref(os.path.join(tmp, "C0"))
+        ck2 = [c for c in cks if c.endswith("ckpt-0000000002")][0]
+        killed = os.path.join(tmp, "killed")
+        shutil.copytree(ck2, os.path.join(killed, os.path.basename(ck2)))
+        D, _ = run_pref(os.path.join(tmp, "D"), resume_from=killed)
+        for s in sorted(D):
+            print(f"pref D (resumed after 2) vs A iteration {s}: {cmp(f'D/A@{s}', D[s], A[s])} differing fields",
+                  flush=True)
         return
     A, _ = run(os.path.join(tmp, "A"), cmd, 8)
     B, _ = run(os.path.join(tmp, "B"), cmd, 8)
