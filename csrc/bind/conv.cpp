@@ -166,7 +166,7 @@ py::tuple conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor y, int64_t
 
 // dZp bf16 [B, H, W, C] = [xp > 0] * conv^T(dy * [y > 0]); wt bf16 [C][KH][KW][N]
 torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, torch::Tensor xp, int64_t stride,
-                         bool relu_out, bool relu_in, int64_t pad) {
+                         bool relu_out, bool relu_in, int64_t pad, int64_t form) {
   IA_CHECK_CUDA(dy);
   IA_CHECK_CONTIG(dy);
   IA_CHECK_CUDA(wt);
@@ -186,7 +186,7 @@ torch::Tensor conv_dgrad(torch::Tensor dy, torch::Tensor y, torch::Tensor wt, to
   }
   auto dz = torch::empty({g.B, g.H, g.W, g.C}, xp.options());
   IA_HIP_CHECK3(ia::conv_dgrad(dy.data_ptr(), relu_out ? y.data_ptr() : nullptr, wt.data_ptr(), xp.data_ptr(),
-                               dz.data_ptr(), g, relu_out ? 1 : 0, relu_in ? 1 : 0, ia_stream()));
+                               dz.data_ptr(), g, relu_out ? 1 : 0, relu_in ? 1 : 0, ia_stream(), (int)form));
   return dz;
 }
 
@@ -471,5 +471,6 @@ void register_conv(py::module& m) {
   m.def("conv_backward_pair_ok", &conv_backward_pair_ok, "whether conv_backward_pair takes this layer", py::arg("x"),
         py::arg("N"), py::arg("KH"), py::arg("KW"), py::arg("stride"));
   m.def("conv_dgrad", &conv_dgrad, "NHWC conv data gradient with fused ReLU masks", py::arg("dy"), py::arg("y"),
-        py::arg("wt"), py::arg("xp"), py::arg("stride"), py::arg("relu_out"), py::arg("relu_in"), py::arg("pad") = 0);
+        py::arg("wt"), py::arg("xp"), py::arg("stride"), py::arg("relu_out"), py::arg("relu_in"), py::arg("pad") = 0,
+        py::arg("form") = -1);
 }

@@ -241,9 +241,8 @@ bool fc_train_ok(int M, int K, int NH, int C, int HW) {
 hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const void* Wt, float* dW, float* db, void* dX,
                        void* dZb, int M, int K, int NH, int C, int HW, hipStream_t s, bool mask_dx) {
   if (!fc_train_ok(M, K, NH, C, HW)) return hipErrorInvalidValue;
-  const char* ch_env = getenv("IMITATION_AMD_FC_WGRAD_CH");  // "0": the 64-column blocks (A/B knob, read per call)
-  const bool ch_off = ch_env != nullptr && ch_env[0] == '0';
-  const bool ch = !ch_off && C % kChG == 0 && kChG * HW <= kChMaxCols && reinterpret_cast<uintptr_t>(X) % 16 == 0;
+  // channel-aligned blocks (16-B NHWC loads) when X allows them, else the 64-column blocks
+  const bool ch = C % kChG == 0 && kChG * HW <= kChMaxCols && reinterpret_cast<uintptr_t>(X) % 16 == 0;
   if (ch)
     hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(C / kChG, NH / 64), dim3(512), 0, s, static_cast<const bf16*>(X), dH, Hout, dW,
                        db, static_cast<bf16*>(dZb), M, K, NH, C, HW);

@@ -1063,7 +1063,7 @@ hipError_t conv_back_pair(const void* X, const void* dY, const void* Y, float* s
 }
 
 hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
-                      int relu_out, int relu_in, hipStream_t s) {
+                      int relu_out, int relu_in, hipStream_t s, int form) {
   if (!conv_geo_ok(g) || g.N % 32 != 0 || g.C % 16 != 0 || g.C > 64) return hipErrorInvalidValue;
   const int Hc = (g.H + g.S - 1) / g.S, Wc = (g.W + g.S - 1) / g.S;  // largest phase
   const int P = g.B * Hc * Wc;
@@ -1075,14 +1075,15 @@ hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void*
   const bf16* xp = static_cast<const bf16*>(Xp);
   bf16* dz = static_cast<bf16*>(dZp);
   // small batches, N = 32 / 64: the split-tap form (one tile per block, its taps and channel
-  // halves over waves); IMITATION_AMD_CONV_DGRAD_SPLIT=0 the prefetching one-wave-per-tile form,
-  // IMITATION_AMD_CONV_DGRAD_PF=0 the plain loop (A/B knobs, read per call)
+  // halves over waves), else the prefetching one-wave-per-tile form; `form` forces the
+  // prefetching form or the plain loop (the bitwise / fp32 checks of tests/ops/test_conv.py)
   const int nn = g.N / 32;
-  const char* pf_env = getenv("IMITATION_AMD_CONV_DGRAD_PF");
-  const char* sp_env = getenv("IMITATION_AMD_CONV_DGRAD_SPLIT");
-  const bool pf = !big && (nn == 1 || nn == 2) && !(pf_env && pf_env[0] == '0');
+  const bool small = !big && (nn == 1 || nn == 2);
+  if (form != kDgradAuto && !small) return hipErrorInvalidValue;
+  const bool pf = small && form != kDgradPlain;
   const int tpg = dgrad_split_tpg(g);  // (8 waves: the same tap grouping as conv_back_pair)
-  const bool split = pf && tpg > 0 && !(sp_env && sp_env[0] == '0');
+  if (form == kDgradSplit && tpg <= 0) return hipErrorInvalidValue;
+  const bool split = pf && tpg > 0 && form != kDgradPrefetch;
   const dim3 sgrid((P + 15) / 16, g.S * g.S), sblock(512);
 #define IA_DG(CT)                                                                                                         \
   if (big) hipLaunchKernelGGL((conv_dgrad_kernel<CT, 4>), grid, block, 0, s, dy, y, wt, xp, dz, g, relu_out, relu_in);     \

@@ -456,8 +456,10 @@ bool conv_back_pair_ok(const ConvGeo& g);
 hipError_t conv_back_pair(const void* X, const void* dY, const void* Y, float* slab, const void* Wt, void* dZp,
                           const ConvGeo& g, int relu_out, int relu_in, hipStream_t s);
 // dZp bf16 [B*H*W][C] = [Xp > 0] * conv^T(dY * [Y > 0]); Wt bf16 [C][KH][KW][N]
+// form: kDgradAuto picks by batch; the others force one kernel of the small-batch family (tests)
+enum DgradForm : int { kDgradAuto = -1, kDgradPlain = 0, kDgradPrefetch = 1, kDgradSplit = 2 };
 hipError_t conv_dgrad(const void* dY, const void* Y, const void* Wt, const void* Xp, void* dZp, const ConvGeo& g,
-                      int relu_out, int relu_in, hipStream_t s);
+                      int relu_out, int relu_in, hipStream_t s, int form = kDgradAuto);
 
 // ---- comm.hip: one-shot all-reduce over IPC-mapped peer staging regions (small DP buckets)
 constexpr int kOneShotMaxRanks = 8;

@@ -440,24 +440,17 @@ hipError_t ppo_rc_launch(const PPOArgs& a, float* workspace, hipStream_t s) {
   // the sc1 hand-off); all G <= kMaxRcGroups (64) of them are co-resident (256 CUs)
   // (net split: the two workgroups must not share a CU's matrix cores either)
   size_t lds_launch = (g.G > 1 || g.ns) && lds < 96 * 1024 ? 96 * 1024 : lds;
-  {  // IMITATION_AMD_PPO_LDS_EXCL=1: claim the whole 160 KiB of LDS, so no workgroup of a concurrent
-     // stream (the discriminator) can share a cooperating workgroup's CU and SIMDs
-    const char* ev = getenv("IMITATION_AMD_PPO_LDS_EXCL");
-    if (ev && ev[0] == '1' && (g.G > 1 || g.ns)) lds_launch = 160 * 1024;
-  }
   const int nblk = g.ns ? 2 * g.G : g.G;
-  {  // cooperating workgroups on as few XCDs as possible (IMITATION_AMD_PPO_XCD=0 turns it off;
-     // the "xcd" geometry field is the block stride). GAIL emulated W = 2 / 4 / 8: 3.14 / 3.28 / 3.64 -> 2.99 / 2.96 / 3.36 ms per update,
+  {  // cooperating workgroups on as few XCDs as possible (the "xcd" geometry field is the block
+     // stride). GAIL emulated W = 2 / 4 / 8: 3.14 / 3.28 / 3.64 -> 2.99 / 2.96 / 3.36 ms per update,
      // headline round 3.63 -> 3.55 ms (profiles/r3_ppo_xcd.md)
     // At most 16 workgroups (half an XCD's 32 CUs) per XCD, so concurrent work on the other
     // stream (the discriminator) never holds a CU a spinning cooperating workgroup waits for:
     // stride 8 / 4 / 2 for <= 16 / 32 / 64 workgroups (blocks b % stride == 0 work: XCDs {0},
     // {0, 4}, {0, 2, 4, 6} of the deal). DRLHP emulated W = 8 (32 workgroups): one XCD 27.3 ms,
     // spread 25.6 ms (profiles/r3_ppo_xcd.md).
-    const char* ev = getenv("IMITATION_AMD_PPO_XCD");
-    const bool on = ev ? ev[0] == '1' : true;
     g.xcd = 1;
-    if (on && nblk > 1) g.xcd = nblk <= 16 ? 8 : nblk <= 32 ? 4 : nblk <= 64 ? 2 : 1;
+    if (nblk > 1) g.xcd = nblk <= 16 ? 8 : nblk <= 32 ? 4 : nblk <= 64 ? 2 : 1;
     // never a wider stride than the device has XCDs (32 CUs each; a partitioned device has fewer)
     const int cus = a.rc_cus > 0 ? a.rc_cus : device_cu_count();
     const int xcds = cus / 32 > 1 ? cus / 32 : 1;

@@ -509,8 +509,7 @@ class _DeviceEpochRunner:
         import os
 
         opt = trainer.optimizer
-        self._fold = (hasattr(opt, "graph_epoch_step_ok") and opt.graph_epoch_step_ok()
-                      and os.environ.get("IMITATION_AMD_BC_FOLD_LAUNCHES", "1") != "0")
+        self._fold = hasattr(opt, "graph_epoch_step_ok") and opt.graph_epoch_step_ok()
         self._world = pdist.world_size()
         self._comm = _DeviceEpochRunner.dp_comm(opt) if self._world > 1 else None
         if self._world > 1 and self._comm is None:

@@ -343,8 +343,7 @@ class DeviceGeneratorCore:
                  normalize_advantage=int(algo.normalize_advantage), adam_step=self.adam_step, stats=self.stats,
                  err=self._ppo_err.word,
                  # fail-fast knobs of the cooperating-workgroup kernel (tests force a timeout)
-                 spin_limit=int(os.environ.get("IMITATION_AMD_PPO_SPIN", "0")),
-                 debug_stall=int(os.environ.get("IMITATION_AMD_PPO_DEBUG_STALL", "0")))
+                 spin_limit=0, debug_stall=0)  # (tests set these two in _ppo_static)
         opt = algo.policy.optimizer
         g = opt.param_groups[0]
         d.update(beta1=float(g.get("betas", (0.9, 0.999))[0]), beta2=float(g.get("betas", (0.9, 0.999))[1]),

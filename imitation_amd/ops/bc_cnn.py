@@ -163,18 +163,16 @@ class FusedCnnBCStep:
 
     def _pairs(self, x: th.Tensor, hs: List[th.Tensor]) -> List[bool]:
         """Per conv layer: whether its backward runs as one paired launch (bf16 input, BC-size batch;
-        ``IMITATION_AMD_BC_CONV_PAIR=0`` the separate wgrad / dgrad launches)."""
+        0.159 -> 0.145 ms per batch-32 step against the separate wgrad / dgrad launches,
+        ``profiles/r6_bc_step.md``)."""
         key = (tuple(x.shape), len(hs))
         cached = getattr(self, "_pair_key", None)
         if cached is not None and cached[0] == key:
             return cached[1]
-        import os
-
-        on = os.environ.get("IMITATION_AMD_BC_CONV_PAIR", "1") != "0"
         out = [False]
         for i in range(1, len(self.convs)):
             c = self.convs[i]
-            out.append(on and bool(self.C.conv_backward_pair_ok(hs[i - 1], c.out_channels, int(c.kernel_size[0]),
+            out.append(bool(self.C.conv_backward_pair_ok(hs[i - 1], c.out_channels, int(c.kernel_size[0]),
                                                                 int(c.kernel_size[1]), int(c.stride[0]))))
         self._pair_key = (key, out)
         return out

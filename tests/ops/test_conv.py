@@ -244,7 +244,7 @@ def test_fc_backward_kernel_exact_wrt_bf16_operands(M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M", [32, 70])
-def test_fc_wgrad_channel_blocks_bitwise_the_column_blocks(monkeypatch, M):
+def test_fc_wgrad_channel_blocks_bitwise_the_column_blocks(M):
     """The channel-aligned fc_wgrad blocks (16-B NHWC operand loads) give bitwise the dW / db /
     dZ of the 64-consecutive-column blocks (same MFMA operands per element)."""
     from imitation_amd import ops
@@ -257,10 +257,11 @@ def test_fc_wgrad_channel_blocks_bitwise_the_column_blocks(monkeypatch, M):
     h = th.relu(th.randn(M, NH, generator=g)).cuda()
     dh = th.randn(M, NH, generator=g).cuda()
     _, wts = C.conv_pack_weights([w], [True], [True])
-    out = []
-    for mode in ("0", "1"):
-        monkeypatch.setenv("IMITATION_AMD_FC_WGRAD_CH", mode)
-        out.append([t.clone() for t in C.fc_backward(x, dh, h, wts[0], C3, True)])
+    # an X that is not 16-B aligned takes the 64-column blocks
+    xu = th.empty(x.numel() + 1, dtype=x.dtype, device=x.device)[1:].view_as(x)
+    xu.copy_(x)
+    assert xu.data_ptr() % 16 != 0
+    out = [[t.clone() for t in C.fc_backward(xx, dh, h, wts[0], C3, True)] for xx in (xu, x)]
     for a, b in zip(*out):
         assert th.equal(a, b)
 
@@ -292,10 +293,8 @@ def test_conv_dgrad_small_batch_forms_match_fp32_and_pf_is_bitwise_the_plain_loo
     x, y, dy, w = _layer_case(B, C, N, KH, S, H, 11 + B + C)
     _, wts = Cn.conv_pack_weights([w], [True])
     out = {}
-    for name, pf, split in (("plain", "0", "0"), ("pf", "1", "0"), ("split", "1", "1")):
-        monkeypatch.setenv("IMITATION_AMD_CONV_DGRAD_PF", pf)
-        monkeypatch.setenv("IMITATION_AMD_CONV_DGRAD_SPLIT", split)
-        out[name] = Cn.conv_dgrad(dy, y, wts[0], x, S, True, True, 0).clone()
+    for name, form in (("plain", 0), ("pf", 1), ("split", 2)):
+        out[name] = Cn.conv_dgrad(dy, y, wts[0], x, S, True, True, 0, form).clone()
     assert th.equal(out["plain"], out["pf"])
     # fp32 reference: dZ = [x > 0] * conv_transpose(dy * [y > 0]) with the bf16 operands
     dz = (dy.float() * (y.float() > 0)).permute(0, 3, 1, 2)
@@ -314,12 +313,11 @@ def test_conv_backward_pair_is_bitwise_the_two_launches(monkeypatch, B, C, N, KH
     from imitation_amd import ops
 
     Cn = ops.native()
-    monkeypatch.setenv("IMITATION_AMD_CONV_DGRAD_SPLIT", "1")
     x, y, dy, w = _layer_case(B, C, N, KH, S, H, 3 + B + C)
     _, wts = Cn.conv_pack_weights([w], [True])
     assert Cn.conv_backward_pair_ok(x, N, KH, KH, S)
     slab, dz = Cn.conv_backward_pair(x, dy, y, wts[0], S, True)
     slab_ref = Cn.conv_wgrad_partials(x, dy, y, KH, KH, S, 1.0, True, 0)
-    dz_ref = Cn.conv_dgrad(dy, y, wts[0], x, S, True, True, 0)
+    dz_ref = Cn.conv_dgrad(dy, y, wts[0], x, S, True, True, 0, 2)
     assert th.equal(slab, slab_ref)
     assert th.equal(dz, dz_ref)
