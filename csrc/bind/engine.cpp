@@ -94,6 +94,7 @@ void rollout(py::dict d) {
                 "prof must be a contiguous int64 GPU tensor of N x 5");
     a.prof = reinterpret_cast<long long*>(t.data_ptr());
   }
+  a.lds_actor = ival(d, "lds_actor", 0);
   IA_HIP_CHECK2(ia::rollout_launch(a, ia_stream()));
 }
 

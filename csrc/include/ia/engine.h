@@ -72,6 +72,9 @@ struct RolloutArgs {
   // in actor+sampling, env physics, observation, step tail, and the step count; the HalfCheetah
   // bench configuration only
   long long* prof;
+  // test hook (tests/engine/test_rollout_probe.py): the HalfCheetah configuration with the LDS
+  // split-form actor instead of the row form, to check the two are bitwise equal
+  int lds_actor;
 };
 
 // Parallel part (engine.hip): per transition V(s), log pi(a|s), the TimeLimit bootstrap

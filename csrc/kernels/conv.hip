@@ -847,16 +847,15 @@ __global__ __launch_bounds__(256) void conv_reduce_multi_kernel(ConvReduceMulti 
 // fp32 torch-layout conv weights [N][C][KH][KW] of up to kMaxPack layers -> bf16 [N][KH][KW][C]
 // (forward GEMM operand) and, where requested, the data-gradient operand: bf16 [C][KH][KW][N]
 // (a 2-D transpose of the source viewed [N][C*KH*KW]) or, t_hwc, [KH][KW][C][N] (a 2-D
-// transpose of the packed [N][KH*KW*C]). Both passes are 32x32 LDS-tile transposes with
-// coalesced reads and writes (blockIdx.z = layer): the NatureCNN FC weight (6.4 MB) included.
-__global__ __launch_bounds__(256) void conv_pack_wb_kernel(ConvPackArgs a) {
-  __shared__ float t[32][33];
-  const ConvPackLayer& L = a.layer[blockIdx.z];
-  const int n = blockIdx.y;
+// transpose of the packed [N][KH*KW*C], read straight from the fp32 source: bf16 of the same
+// value). Both passes are 32x32 LDS-tile transposes in ONE launch (the per-step weight refresh
+// of the fused BC step: two launches were ~12.5 us of its ~145): blocks [0, nwb) the forward
+// images (tile, output channel, layer), the rest the transposes (k tile, n tile, layer).
+__device__ __forceinline__ void pack_wb_tile(const ConvPackLayer& L, int tile, int n, float (*t)[33]) {
   const int taps = L.KH * L.KW, C = L.C;
   const int tt = (taps + 31) / 32, nc = (C + 31) / 32;
-  if (n >= L.N || (int)blockIdx.x >= tt * nc) return;
-  const int c0 = ((int)blockIdx.x / tt) * 32, p0 = ((int)blockIdx.x % tt) * 32;
+  if (n >= L.N || tile >= tt * nc) return;
+  const int c0 = (tile / tt) * 32, p0 = (tile % tt) * 32;
   const float* src = L.w + (size_t)n * C * taps;
   for (int i = threadIdx.x; i < 1024; i += 256) {  // src [c][tap], coalesced along tap
     const int r = i >> 5, q = i & 31, c = c0 + r, p = p0 + q;
@@ -870,18 +869,19 @@ __global__ __launch_bounds__(256) void conv_pack_wb_kernel(ConvPackArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void conv_pack_wt_kernel(ConvPackArgs a) {
-  __shared__ float t[32][33];
-  const ConvPackLayer& L = a.layer[blockIdx.z];
+__device__ __forceinline__ void pack_wt_tile(const ConvPackLayer& L, int kt, int nt, float (*t)[33]) {
   if (!L.wt) return;
-  const int K = L.C * L.KH * L.KW, N = L.N;
-  const int k0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  const int taps = L.KH * L.KW, K = L.C * taps, N = L.N;
+  const int k0 = kt * 32, n0 = nt * 32;
   if (k0 >= K || n0 >= N) return;
-  const bf16* wb = static_cast<const bf16*>(L.wb);
-  for (int i = threadIdx.x; i < 1024; i += 256) {  // [n][k] rows, coalesced along k
+  for (int i = threadIdx.x; i < 1024; i += 256) {  // [n][k] rows
     const int r = i >> 5, q = i & 31, nn = n0 + r, k = k0 + q;
     float v = 0.f;
-    if (nn < N && k < K) v = L.t_hwc ? (float)wb[(size_t)nn * K + k] : L.w[(size_t)nn * K + k];
+    if (nn < N && k < K) {
+      // t_hwc: k = tap * C + c of the packed row, i.e. source element [nn][c][tap]
+      const int tap = L.t_hwc ? k / L.C : 0, c = L.t_hwc ? k - tap * L.C : 0;
+      v = L.w[(size_t)nn * K + (L.t_hwc ? (size_t)c * taps + tap : (size_t)k)];
+    }
     t[r][q] = v;
   }
   __syncthreads();
@@ -889,6 +889,22 @@ __global__ __launch_bounds__(256) void conv_pack_wt_kernel(ConvPackArgs a) {
   for (int i = threadIdx.x; i < 1024; i += 256) {  // [k][n], coalesced along n
     const int r = i >> 5, q = i & 31, k = k0 + r, nn = n0 + q;
     if (k < K && nn < N) dst[(size_t)k * N + nn] = (bf16)t[q][r];
+  }
+}
+
+__global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a, int max_tiles, int max_n, int kts, int nts) {
+  __shared__ float t[32][33];
+  const int nwb = max_tiles * max_n * a.n;
+  int b = blockIdx.x;
+  if (b < nwb) {
+    const int l = b / (max_tiles * max_n);
+    b -= l * max_tiles * max_n;
+    pack_wb_tile(a.layer[l], b % max_tiles, b / max_tiles, t);
+  } else {
+    b -= nwb;
+    const int l = b / (kts * nts);
+    b -= l * kts * nts;
+    pack_wt_tile(a.layer[l], b % kts, b / kts, t);
   }
 }
 
@@ -908,9 +924,9 @@ hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s) {
     max_k = L.C * taps > max_k ? L.C * taps : max_k;
     any_t = any_t || L.wt != nullptr;
   }
-  hipLaunchKernelGGL(conv_pack_wb_kernel, dim3(max_tiles, max_n, a.n), dim3(256), 0, s, a);
-  if (any_t)  // after the wb pass: the t_hwc transposes read the packed weights
-    hipLaunchKernelGGL(conv_pack_wt_kernel, dim3((max_k + 31) / 32, (max_n + 31) / 32, a.n), dim3(256), 0, s, a);
+  const int kts = any_t ? (max_k + 31) / 32 : 0, nts = any_t ? (max_n + 31) / 32 : 0;
+  const int blocks = max_tiles * max_n * a.n + kts * nts * a.n;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(blocks), dim3(256), 0, s, a, max_tiles, max_n, kts, nts);
   return hipGetLastError();
 }
 

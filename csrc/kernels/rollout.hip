@@ -14,6 +14,9 @@
 // input is broadcast from a 64-float LDS vector with ds_read_b128 (every lane of a
 // half reads the same address), and the two half sums meet through
 // v_permlane32_swap. Widths up to 64 use the "full" form (lane = unit, whole K).
+// Split form with every hidden layer exactly 32 wide (the locomotion recipes): the "row" form
+// -- no LDS at all, the layer input is a DPP row broadcast of the lane's own register (see
+// nb_lane below).
 // The locomotion model keeps its state in registers: joint j on lane j, the root
 // coordinates uniform in every lane, cross-joint sums by DPP quad/row butterflies.
 // No loop iteration waits on global memory: inputs are LDS, outputs are fire-and-
@@ -50,15 +53,33 @@ __host__ __device__ __forceinline__ int split_kh(int din) { return ((din + 1) / 
 constexpr int kFullGroups = 16;
 __host__ __device__ __forceinline__ int full_lds_floats(const WaveMLP& m) { return m.n_layers * 4 * kFullGroups * 64; }
 
-template <bool SPLIT>
+// Row form (split form, every hidden width 32): the 64 lanes are 4 DPP rows of 16; in layer l
+// row r takes K-half `kh` and block `ub` of 16 units, (kh, ub) = (r & 1, r >> 1) in even layers
+// and (r >> 1, r & 1) in odd ones, so the two K-halves of a unit meet through permlane16_swap
+// (rows 0+1, 2+3) in even layers and permlane32_swap (rows 0+2, 1+3) in odd ones. Either swap
+// leaves unit 16 * b + i in lane i of exactly the rows whose K-half is b in the next layer, so
+// that layer reads input k0 + i as row_newbcast:i of the lane's own register. Same weights,
+// products and summation order per unit as the LDS split form (bitwise the same outputs).
+__device__ __forceinline__ void nb_lane(int l, int lane, int& kh, int& ub) {
+  const int r = lane >> 4;
+  kh = (l & 1) ? (r >> 1) : (r & 1);
+  ub = (l & 1) ? (r & 1) : (r >> 1);
+}
+
+template <bool SPLIT, bool NB = false>
 __device__ void load_actor(const WaveMLP& m, Actor<SPLIT>& r, lf* wlds) {
   const int lane = threadIdx.x;
-  const int h = SPLIT ? (lane >> 5) : 0;
-  const int j = SPLIT ? (lane & 31) : lane;
   r.n_layers = m.n_layers;
   r.hidden_act = m.hidden_act;
 #pragma unroll
   for (int l = 0; l < kWaveMaxLayers; ++l) {
+    int h = SPLIT ? (lane >> 5) : 0;
+    int j = SPLIT ? (lane & 31) : lane;
+    if (NB) {
+      int ub;
+      nb_lane(l, lane, h, ub);
+      j = 16 * ub + (lane & 15);
+    }
     const bool on = l < m.n_layers;
     const int din = on ? m.dims[l] : 0, dout = on ? m.dims[l + 1] : 0;
     const int kh = SPLIT ? split_kh(din) : 4 * kFullGroups;
@@ -165,6 +186,49 @@ __device__ __forceinline__ float actor_forward(const Actor<SPLIT>& r, lf* xb) {
   return h;
 }
 
+// Row form of actor_forward (NLT layers, hidden widths 32): x = this lane's layer-0 input,
+// input k0 + (lane & 15) of its row's K-half (actor_obs_index). Returns the actor output j in
+// lane j < dout of the last layer.
+// acc += x[row lane I] * w as ONE v_fmac_f32_dpp (the compiler keeps a separate v_mov_b32_dpp
+// per broadcast, twice the VALU issue). I == 0 is the layer's first read of x, just written by a
+// VALU op: the DPP read needs two wait states after it.
+template <int I>
+__device__ __forceinline__ float fmac_row_bcast(float acc, float x, float w) {
+  if constexpr (I == 0)
+    asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(x), "v"(w), "i"(I));
+  else
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x), "v"(w), "i"(I));
+  return acc;
+}
+
+template <int I>
+__device__ __forceinline__ void nb_dot(const float* w, float x, float& a0, float& a1) {
+  if constexpr (I < 16) {
+    a0 = fmac_row_bcast<I>(a0, x, w[I]);  // == fmaf(w[I], x_I, a0)
+    a1 = fmac_row_bcast<I + 1>(a1, x, w[I + 1]);
+    nb_dot<I + 2>(w, x, a0, a1);
+  }
+}
+
+template <int HACT, int NLT>
+__device__ __forceinline__ float actor_forward_nb(const Actor<true>& r, float x) {
+  static_assert(NLT > 0, "the row form needs the layer count at compile time");
+#pragma unroll
+  for (int l = 0; l < NLT; ++l) {
+    float acc0 = r.bias[l], acc1 = 0.f;
+    nb_dot<0>(r.w[l], x, acc0, acc1);
+    const float acc = (l & 1) ? add_halves(acc0 + acc1) : add_rows16(acc0 + acc1);
+    x = l == NLT - 1 ? acc : hidden_act<HACT>(r.hidden_act, acc);
+  }
+  return x;
+}
+
+// The observation index whose (normalised) value is lane `lane`'s row-form layer-0 input.
+__device__ __forceinline__ int actor_obs_index(int lane, int obs_dim) {
+  return ((lane >> 4) & 1 ? split_kh(obs_dim) : 0) + (lane & 15);
+}
+
 // Generic (non-locomotion) envs step on lane 0, inlined: an out-of-line call needs a stack
 // frame (544 B/lane of scratch in the generic instances), while the inlined switch fits the
 // loop's register budget (<= 222 VGPRs at two waves per SIMD, 0 scratch: tools/kernel_resources.py).
@@ -216,7 +280,7 @@ __device__ void loco_store(const LocoParams& p, const LocoRegs& L, lf* s) {
 
 // Observation [qpos[obs_skip:], qvel] in lane layout, through the LDS scratch sb.
 template <int ENV>
-__device__ float loco_obs(const LocoParams& p, const LocoRegs& L, lf* sb) {
+__device__ float loco_obs(const LocoParams& p, const LocoRegs& L, lf* sb, int oxi, float& ox) {
   const int lane = threadIdx.x;
   const int nr = ENV == CE_LOCO3 ? 3 : 8;
   const int nqr = ENV == CE_LOCO3 ? 3 : p.nq_root, nvr = ENV == CE_LOCO3 ? 3 : p.nv_root;
@@ -236,6 +300,7 @@ __device__ float loco_obs(const LocoParams& p, const LocoRegs& L, lf* sb) {
   if (lane < nvr) sb[npr + nj + lane] = rvi;
   wave_sync();
   const int D = npr + nj + nvr + nj;
+  ox = sb[oxi];  // (the row-form actor's input layout; past D a zero word of xb, oxi < 0)
   return lane < D ? sb[lane] : 0.f;
 }
 
@@ -335,7 +400,7 @@ __device__ __forceinline__ long long stamp(float dep) {
   return t;
 }
 
-template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1, int FS = -1, bool PROF = false>
+template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1, int FS = -1, bool PROF = false, bool ROW = true>
 __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
@@ -355,10 +420,18 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   const int AW = discrete ? a.n_actions : P.act_dim;  // noise values per step
   const int S = state_size(P);
 
+  // row form: the split form with every hidden layer 32 wide (HW == 32, depth NLT known)
+  constexpr bool NB = ROW && SPLIT && HW == 32 && NLT > 0;
   Actor<SPLIT> ar;
-  load_actor<SPLIT>(a.pi, ar, wlds);
-  const float nmean = pin((a.pi.norm_mean && lane < D) ? a.pi.norm_mean[lane] : 0.f);
-  const float nrstd = pin((a.pi.norm_mean && lane < D) ? rsqrtf(a.pi.norm_var[lane] + a.pi.norm_eps) : 1.f);
+  load_actor<SPLIT, NB>(a.pi, ar, wlds);
+  // lane layout of the observation (stores) and, for the row form, the layer-0 input layout
+  const int oxi = NB ? actor_obs_index(lane, D) : lane;
+  const bool ox_on = oxi < D;
+  // LDS word (relative to sb) of this lane's layer-0 input: past D, a word of xb, which the row
+  // form never writes (0 from the prologue) -- so (ox - 0) * 1 = +0 exactly as the LDS form's 0.f
+  const int oxr = ox_on ? oxi : lane - 64;
+  const float nmean = pin((a.pi.norm_mean && ox_on) ? a.pi.norm_mean[oxi] : 0.f);
+  const float nrstd = pin((a.pi.norm_mean && ox_on) ? rsqrtf(a.pi.norm_var[oxi] + a.pi.norm_eps) : 1.f);
   const float lstd = (!discrete && a.log_std && lane < A) ? a.log_std[lane] : 0.f;
   const float sd = pin(expf(lstd));
   const float lo = pin((!discrete && a.act_low && lane < A) ? a.act_low[lane] : 0.f);
@@ -400,6 +473,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   }
 
   float o = lane < D ? a.cur_obs[(size_t)n * D + lane] : 0.f;
+  float ox = ox_on ? a.cur_obs[(size_t)n * D + oxi] : 0.f;  // (row form: == o otherwise)
   float start = a.cur_start[n];
   uint64_t rng = a.rng[n];
   int elapsed = a.elapsed[n];
@@ -438,9 +512,14 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       if constexpr (PROF) t0 = stamp(o);
       if (lane < D) *c.obs = o;
       // ---- actor
-      xb[lane] = lane < D ? (o - nmean) * nrstd : 0.f;
-      wave_sync();
-      const float head = actor_forward<SPLIT, HACT, NLT, HW>(ar, xb);
+      float head;
+      if constexpr (NB) {
+        head = actor_forward_nb<HACT, NLT>(ar, (ox - nmean) * nrstd);
+      } else {
+        xb[lane] = lane < D ? (o - nmean) * nrstd : 0.f;
+        wave_sync();
+        head = actor_forward<SPLIT, HACT, NLT, HW>(ar, xb);
+      }
       float a_raw, a_env;
       if (discrete) {
         const float g = lane < a.n_actions ? head + *nz : -INFINITY;
@@ -475,12 +554,12 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       // ---- env step + SB3 auto-reset, TimeLimit, Monitor
       int term = 0;
       float r_env;
-      float o_next;
+      float o_next, ox_next;
       if constexpr (PROF) t1 = stamp(a_env);
       if (loco) {
         r_env = loco_step_regs<ENV, FS>(P.loco, L, a_env);
         if constexpr (PROF) t2 = stamp(r_env);
-        o_next = loco_obs<ENV>(P.loco, L, sb);
+        o_next = loco_obs<ENV>(P.loco, L, sb, oxr, ox_next);
         if constexpr (PROF) t3 = stamp(o_next);
       } else {
         if (lane < A) act[lane] = a_env;
@@ -493,6 +572,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
         term = __builtin_amdgcn_readfirstlane(term);
         r_env = bcast(r_env, 0);
         o_next = lane < D ? sb[lane] : 0.f;
+        ox_next = sb[oxr];
       }
       elapsed += 1;
       ep_ret += r_env;
@@ -521,14 +601,16 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
         wave_sync();
         if (loco) {
           loco_load(P.loco, st, L);
-          o = loco_obs<ENV>(P.loco, L, sb);
+          o = loco_obs<ENV>(P.loco, L, sb, oxr, ox);
         } else {
           o = lane < D ? sb[lane] : 0.f;
+          ox = sb[oxr];
         }
         elapsed = 0;
         ep_ret = 0.f;
       } else {
         o = o_next;
+        ox = ox_next;
       }
       start = done ? 1.f : 0.f;
       if constexpr (PROF) {
@@ -593,9 +675,14 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   // (+ the frame skip of the benchmark recipes: HalfCheetah 5 with the [32, 32] tanh actor,
   // Hopper / Walker 4 with the [64, 64] ReLU one)
   const int fs = env == CE_LOCO3 ? p.frame_skip : 0;
-  if (a.prof) {  // the phase-clock probe exists for the HalfCheetah bench configuration only
+  if (a.prof || a.lds_actor) {  // the probe / test instances: the HalfCheetah bench configuration only
     if (!(split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, true>), g, b, lds, s, a);
+    if (a.prof && a.lds_actor)
+      hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, true, false>), g, b, lds, s, a);
+    else if (a.prof)
+      hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, true>), g, b, lds, s, a);
+    else
+      hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, false, false>), g, b, lds, s, a);
   } else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5>), g, b, lds, s, a);
   else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 4)

@@ -507,9 +507,11 @@ def dagger_device_round_worker(rank, world, seed, scratch):
     th.cuda.synchronize()
     col = tr._device_collector
     dp_step = getattr(tr.bc_trainer, "_dp_step", None)
+    run = getattr(tr.bc_trainer, "_epoch_run", None)
     return {"policy": [p.detach().cpu().numpy().copy() for p in tr.policy.parameters()],
             "env_state": col.state.detach().cpu().numpy().copy(), "round_num": tr.round_num,
-            "local": tr.last_train_timesteps_local, "dp_fused_replays": dp_step.n_replays if dp_step else 0}
+            "local": tr.last_train_timesteps_local, "dp_fused_replays": dp_step.n_replays if dp_step else 0,
+            "dp_epoch_runner": run is not None and run._comm is not None}
 
 
 def oneshot_selftest_worker(rank, world, corrupt, mode="auto"):

@@ -241,6 +241,8 @@ def adversarial_state(trainer) -> Dict[str, Any]:
     """State of a GAIL / AIRL trainer (host loop or :class:`~imitation_amd.engine.gail.DeviceGAIL`)."""
     from imitation_amd.algorithms.adversarial import common
 
+    if hasattr(trainer, "sync_env_to_host"):  # device engine: the host env mirrors the device env state
+        trainer.sync_env_to_host()
     st: Dict[str, Any] = {
         "format": "imitation_amd.adversarial.v1",
         "global_step": int(trainer._global_step),
@@ -392,6 +394,8 @@ def preference_state(pc, side_dir: str) -> Dict[str, Any]:
     }
     gen = pc.trajectory_generator
     if isinstance(gen, pcm.AgentTrainer):
+        if hasattr(gen, "sync_env_to_host"):  # device agent: the host env mirrors the device env state
+            gen.sync_env_to_host()
         st["agent"] = rl_algo_state(gen.algorithm)
         st["env"] = env_state(gen.venv)
         st["episode_rewards"] = [float(x) for x in gen.reward_venv_wrapper.episode_rewards]

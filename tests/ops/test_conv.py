@@ -321,3 +321,23 @@ def test_conv_backward_pair_is_bitwise_the_two_launches(monkeypatch, B, C, N, KH
     dz_ref = Cn.conv_dgrad(dy, y, wts[0], x, S, True, True, 0, 2)
     assert th.equal(slab, slab_ref)
     assert th.equal(dz, dz_ref)
+
+
+@pytest.mark.gpu
+def test_conv_pack_weights_layouts_in_one_launch():
+    """conv_pack_weights (forward images and transposes in ONE launch) == the torch permutes of the
+    bf16-rounded weights, for the NatureCNN layers and its FC weight (t_hwc) packed together."""
+    from imitation_amd import ops
+
+    C = ops.native()
+    g = th.Generator().manual_seed(5)
+    shapes = [(32, 4, 8, 8), (64, 32, 4, 4), (64, 64, 3, 3), (512, 64, 7, 7)]
+    ws = [th.randn(*s, generator=g).cuda() for s in shapes]
+    want_t, t_hwc = [False, True, True, True], [False, False, False, True]
+    wbs, wts = C.conv_pack_weights(ws, want_t, t_hwc)
+    for w, wb, wt, t, hwc in zip(ws, wbs, wts, want_t, t_hwc):
+        wr = w.to(th.bfloat16)
+        assert th.equal(wb, wr.permute(0, 2, 3, 1).contiguous())
+        if t:
+            src = wr.permute(0, 2, 3, 1) if hwc else wr
+            assert th.equal(wt.reshape(-1, w.shape[0]), src.reshape(w.shape[0], -1).t().contiguous())

@@ -187,14 +187,22 @@ def test_dagger_device_collector_dp_replicas(monkeypatch, tmp_path):
 
 @pytest.mark.gpu
 def test_dagger_dp_fused_bc_step_matches_eager_dp(monkeypatch, tmp_path):
-    """Data-parallel BC on the fused NatureCNN step (algorithms/bc.py ``_DPFusedStep``: graph of the
-    autograd-free fwd / bwd into the bucket, bucket all-reduce, graph of the optimizer step): the
-    replicas stay bit-identical and match the eager autograd DP loop within bf16 tolerance."""
+    """Data-parallel BC on the fused NatureCNN step -- the graph-resident epoch runner (one-shot
+    all-reduce inside the step graphs) and, with it off, ``_DPFusedStep`` (graph of the fwd / bwd
+    into the bucket, bucket all-reduce, graph of the optimizer step): the replicas stay
+    bit-identical, the two are bitwise equal, and they match the eager autograd DP loop within
+    bf16 tolerance."""
     monkeypatch.setenv("IMITATION_AMD_DIST_BACKEND", "gloo")
     monkeypatch.setenv("IMITATION_AMD_ONESHOT", "1")
     fused = run_ranks(W.dagger_device_round_worker, 2, 4, str(tmp_path / "f"), timeout=400)
-    assert all(o["dp_fused_replays"] >= 4 for o in fused)
+    assert all(o["dp_epoch_runner"] for o in fused)
     for a, b in zip(fused[0]["policy"], fused[1]["policy"]):
+        np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("IMITATION_AMD_BC_EPOCH_GRAPH", "0")
+    per_mb = run_ranks(W.dagger_device_round_worker, 2, 4, str(tmp_path / "m"), timeout=400)
+    monkeypatch.delenv("IMITATION_AMD_BC_EPOCH_GRAPH")
+    assert all(o["dp_fused_replays"] >= 4 for o in per_mb)
+    for a, b in zip(fused[0]["policy"], per_mb[0]["policy"]):
         np.testing.assert_array_equal(a, b)
     monkeypatch.setenv("IMITATION_AMD_BC_CNN_FUSED", "0")
     eager = run_ranks(W.dagger_device_round_worker, 2, 4, str(tmp_path / "e"), timeout=400)

@@ -25,7 +25,8 @@ def run(root, cmd, total, **kw):
                rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
                algorithm_kwargs=dict(demo_batch_size=256, n_disc_updates_per_round=2), checkpoint_interval=0,
                full_checkpoint_interval=2, full_checkpoint_keep=10, total_timesteps=total * 1024, seed=0,
-               logging={"log_root": root}, **kw)
+               logging={"log_root": root})
+    upd.update(kw)
     from imitation_amd.algorithms.adversarial import common
 
     seen = {}
@@ -47,9 +48,41 @@ def run(root, cmd, total, **kw):
     return {int(os.path.basename(c)[5:]): th.load(os.path.join(c, "state.pt"), weights_only=True) for c in cks}, cks
 
 
+def _trace_reward_training():
+    """Print, per reward-model training call, the path taken, the dataset size, the epochs and the
+    optimizer's step counter before / after."""
+    from imitation_amd.algorithms import preference_comparisons as pcm
+
+    if getattr(pcm, "_diag_traced", False):
+        return
+    pcm._diag_traced = True
+    orig_fast, orig_fused = pcm.BasicRewardTrainer._train_fast, pcm.BasicRewardTrainer._train_fused_epochs
+
+    def step_of(self):
+        f = getattr(self.optim, "_flat", None)
+        return float(f[0]["step"]) if f else None
+
+    def fast(self, dataset, epoch_multiplier):
+        s0 = step_of(self)
+        r = orig_fast(self, dataset, epoch_multiplier)
+        print(f"  reward _train_fast: P={len(dataset)} mult={epoch_multiplier} step {s0} -> {step_of(self)} "
+              f"optim={type(self.optim).__name__}", flush=True)
+        return r
+
+    def fused(self, store, index_loader, epochs, P, dev):
+        print(f"  reward fused epochs: P={P} epochs={epochs}", flush=True)
+        return orig_fused(self, store, index_loader, epochs, P, dev)
+
+    pcm.BasicRewardTrainer._train_fast = fast
+    pcm.BasicRewardTrainer._train_fused_epochs = fused
+
+
 def run_pref(root, iters_total=3, **kw):
     """train_preference_comparisons on the device agent (full checkpoint per iteration)."""
     from imitation_amd.scripts.train_preference_comparisons import train_preference_comparisons_ex
+
+    _trace_reward_training()
+    print(f"== run {root} {kw}", flush=True)
 
     upd = dict(environment=dict(gym_id="seals/Hopper-v1", num_vec=8, parallel=False),
                rl=dict(batch_size=1024, rl_kwargs=dict(batch_size=64, n_epochs=1)), engine="device",
@@ -67,7 +100,8 @@ def cmp(tag, a, b, path=""):
     n = 0
     if isinstance(a, th.Tensor):
         if not (isinstance(b, th.Tensor) and a.shape == b.shape and th.equal(a, b)):
-            print(f"{tag}: DIFF {path}", flush=True)
+            extra = f" {a.flatten()[:4].tolist()} != {b.flatten()[:4].tolist()}" if isinstance(b, th.Tensor) and a.numel() <= 4 else ""
+            print(f"{tag}: DIFF {path}{extra}", flush=True)
             return 1
         return 0
     if isinstance(a, dict):
@@ -82,6 +116,36 @@ def cmp(tag, a, b, path=""):
         print(f"{tag}: DIFF {path} {str(a)[:60]} != {str(b)[:60]}", flush=True)
         return 1
     return 0
+
+
+def final_params(root):
+    """The final reward_train.pt state and the generator's policy parameters of a run."""
+    from imitation_amd.rewards import serialize as reward_serialize
+    from imitation_amd.rl.save_util import load_from_zip_file
+
+    (rew,) = glob.glob(os.path.join(root, "**", "checkpoints", "final", "reward_train.pt"), recursive=True)
+    out = {"reward": reward_serialize.load_reward_net(rew, device="cpu").state_dict()}
+    (zp,) = glob.glob(os.path.join(root, "**", "checkpoints", "final", "gen_policy", "model.zip"), recursive=True)
+    out["gen"] = load_from_zip_file(zp, device="cpu")[1]
+    return out
+
+
+def chunk_check(tmp, cmd):
+    """Does chunking train() at the full-checkpoint interval (or the saving itself) change an
+    uninterrupted run? E: one train() call; A: interval 2 with saves; F: interval 2, saves skipped."""
+    from imitation_amd.utils import checkpoint
+
+    run(os.path.join(tmp, "E"), cmd, 8, full_checkpoint_interval=0)
+    run(os.path.join(tmp, "A"), cmd, 8)
+    orig = checkpoint.CheckpointManager.save
+    checkpoint.CheckpointManager.save = lambda self, *a, **k: None
+    try:
+        run(os.path.join(tmp, "F"), cmd, 8)
+    finally:
+        checkpoint.CheckpointManager.save = orig
+    E, A, F = (final_params(os.path.join(tmp, x)) for x in "EAF")
+    print(f"{cmd}: E (one call) vs A (chunks + saves): {cmp('E/A', E, A)} differing fields", flush=True)
+    print(f"{cmd}: E (one call) vs F (chunks, no saves): {cmp('E/F', E, F)} differing fields", flush=True)
 
 
 def main():
@@ -108,6 +172,9 @@ def main():
         for s in sorted(D):
             print(f"pref D (resumed after 2) vs A iteration {s}: {cmp(f'D/A@{s}', D[s], A[s])} differing fields",
                   flush=True)
+        return
+    if "--chunks" in sys.argv:
+        chunk_check(tmp, cmd)
         return
     A, _ = run(os.path.join(tmp, "A"), cmd, 8)
     B, _ = run(os.path.join(tmp, "B"), cmd, 8)

@@ -14,3 +14,6 @@ rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 200 python -u tools/rollout_breakdown.py > gpurun_out/r6h_breakdown.log 2>&1 || exit $?
 timeout -k 10 400 python -u tools/cli_resume_diag.py airl > gpurun_out/r6h_diag_airl.log 2>&1 || exit $?
 timeout -k 10 400 python -u tools/cli_resume_diag.py pref > gpurun_out/r6h_diag_pref.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/ops/test_conv.py > gpurun_out/r6h_conv_tests.log 2>&1
+rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r6h_bcprof -o bc -- python3 $GRAFT_REPO_ROOT/tools/bc_step_probe.py > $GRAFT_REPO_ROOT/gpurun_out/r6h_bcprof.log 2>&1 || exit $?

@@ -4,7 +4,8 @@ Runs the bench trainer (``gail_halfcheetah``) and, for a few rounds, launches th
 phase-clock instance (``prof`` argument, rollout.hip ``PROF = true``): every wave accumulates the
 core-clock cycles of each step phase -- actor + sampling, env physics, observation, step tail.
 Prints cycles / step per phase, their shares, and the chain kernel's time with and without the
-stamps (events around the launch; the stamps' own cost shows as the difference).
+stamps (events around the launch; the stamps' own cost shows as the difference), for the
+production row-form actor and the LDS split form it replaced (``lds_actor``).
 
     python tools/rollout_breakdown.py
 """
@@ -22,14 +23,13 @@ class _Proxy:
     def __init__(self, C):
         self._C = C
         self.prof = None
+        self.lds_actor = 0
 
     def __getattr__(self, k):
         return getattr(self._C, k)
 
     def engine_rollout(self, d):
-        if self.prof is not None:
-            d = dict(d, prof=self.prof)
-        return self._C.engine_rollout(d)
+        return self._C.engine_rollout(dict(d, prof=self.prof, lds_actor=self.lds_actor))
 
 
 def main():
@@ -45,7 +45,15 @@ def main():
     px = _Proxy(eng._C)
     eng._C = px
     N, T = eng.N, eng.T
-    res = {"N": N, "T": T}
+    for form in ("row", "lds"):
+        px.lds_actor = int(form == "lds")
+        measure(eng, px, N, T, form)
+
+
+def measure(eng, px, N, T, form):
+    import torch as th
+
+    res = {"actor_form": form, "N": N, "T": T}
     for mode in ("plain", "stamped", "plain"):
         px.prof = th.zeros(N, 5, dtype=th.int64, device="cuda") if mode == "stamped" else None
         times = []
