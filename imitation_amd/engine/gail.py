@@ -1341,11 +1341,21 @@ class DeviceEngineMixin(DeviceGeneratorCore):
     def train(self, total_timesteps: int, callback=None) -> None:
         """Rounds of device generator training + fused discriminator updates; the
         discriminator statistics of a round are fetched with one host sync and logged
-        per update exactly as the reference's ``train_disc`` does."""
+        per update exactly as the reference's ``train_disc`` does. At the end the host env
+        mirrors the device env state: a host-side evaluation on ``venv_train`` (the reference
+        CLI's final ``eval_policy``, e.g. AIRL with output normalisation) then continues from
+        the training env state, as the reference's does, whether or not a checkpoint or a
+        resume copied it before."""
         if not self._fused_disc:
             if self._graphed_disc_ok():
-                return self._train_graphed_generic(total_timesteps, callback)
-            return super().train(total_timesteps, callback)
+                self._train_graphed_generic(total_timesteps, callback)
+            else:
+                super().train(total_timesteps, callback)
+        else:
+            self._train_fused(total_timesteps, callback)
+        self.sync_env_to_host()
+
+    def _train_fused(self, total_timesteps: int, callback=None) -> None:
         n_rounds = total_timesteps // self.gen_train_timesteps
         assert n_rounds >= 1, (
             f"No updates (need at least {self.gen_train_timesteps} timesteps, have only total_timesteps={total_timesteps})!")

@@ -296,6 +296,7 @@ class DeviceAgentTrainer(OutputNormMixin, DeviceGeneratorCore, AgentTrainer):
                 logged = True
         if not logged:
             self._log_round()
+        self.sync_env_to_host()  # (a host-side evaluation continues from the training env state)
 
     def _log_round(self) -> None:
         algo = self.gen_algo

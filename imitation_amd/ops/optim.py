@@ -215,12 +215,13 @@ class FusedAdam(th.optim.Optimizer):
         which torch would otherwise increment once per parameter) and the groups say
         ``capturable=False`` (torch refuses a capturable step on CPU parameters)."""
         sd = super().state_dict()
-        for st in sd["state"].values():
-            if "step" in st:
-                st["step"] = th.tensor(float(st["step"]), dtype=th.float32)
-            for k in ("exp_avg", "exp_avg_sq"):
-                if k in st:
-                    st[k] = st[k].detach().clone()
+        # (new per-parameter dicts: torch's state_dict hands out the live ``self.state`` dicts, and
+        # writing the snapshots into those would detach them from the flat buffers -- every later
+        # state_dict would then return this one's step and moments)
+        sd["state"] = {i: {k: (th.tensor(float(v), dtype=th.float32) if k == "step" else
+                               v.detach().clone() if k in ("exp_avg", "exp_avg_sq") else v)
+                           for k, v in st.items()}
+                       for i, st in sd["state"].items()}
         sd["param_groups"] = [dict(g, capturable=False) for g in sd["param_groups"]]
         return sd
 

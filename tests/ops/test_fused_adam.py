@@ -58,6 +58,24 @@ def test_fused_adam_state_dict_roundtrip_with_torch_adam():
     assert float(oc.state[next(iter(c.parameters()))]["step"]) == 7.0
 
 
+def test_fused_adam_state_dict_leaves_the_live_state_bound():
+    """Each state_dict is a snapshot of the CURRENT flat step counter and moments: taking one must
+    not detach the optimizer's live state (a second checkpoint after more steps once saved the
+    first checkpoint's step and moments -- a device DRLHP run resumed from it diverged)."""
+    p = th.nn.Parameter(th.randn(4, 3))
+    opt = optim_ops.FusedAdamW([p], lr=1e-3)
+    f = opt._flat[0]
+    for n in (1, 2, 3):
+        p.grad = th.randn_like(p)
+        opt.step()
+        st = opt.state_dict()["state"][0]
+        assert float(st["step"]) == n
+        assert th.equal(st["exp_avg"].reshape(-1), f["m"][:12]) and th.equal(st["exp_avg_sq"].reshape(-1), f["v"][:12])
+        assert opt.state[p]["step"] is f["step"]  # still the live counter
+    st["exp_avg"].add_(1.0)  # the snapshot is a copy
+    assert not th.equal(st["exp_avg"].reshape(-1), f["m"][:12])
+
+
 def test_fused_adam_checkpoint_loads_into_torch_adam():
     """fused -> torch direction: per-parameter steps, capturable=False; the torch optimizer then
     continues exactly like the fused one (wrong bias correction if the step were shared)."""
