@@ -872,40 +872,57 @@ __device__ __forceinline__ void pack_wb_tile(const ConvPackLayer& L, int tile, i
 __device__ __forceinline__ void pack_wt_tile(const ConvPackLayer& L, int kt, int nt, float (*t)[33]) {
   if (!L.wt) return;
   const int taps = L.KH * L.KW, K = L.C * taps, N = L.N;
-  const int k0 = kt * 32, n0 = nt * 32;
-  if (k0 >= K || n0 >= N) return;
-  for (int i = threadIdx.x; i < 1024; i += 256) {  // [n][k] rows
-    const int r = i >> 5, q = i & 31, nn = n0 + r, k = k0 + q;
-    float v = 0.f;
-    if (nn < N && k < K) {
-      // t_hwc: k = tap * C + c of the packed row, i.e. source element [nn][c][tap]
-      const int tap = L.t_hwc ? k / L.C : 0, c = L.t_hwc ? k - tap * L.C : 0;
-      v = L.w[(size_t)nn * K + (L.t_hwc ? (size_t)c * taps + tap : (size_t)k)];
-    }
-    t[r][q] = v;
-  }
-  __syncthreads();
+  const int n0 = nt * 32;
+  if (n0 >= N) return;
   bf16* dst = static_cast<bf16*>(L.wt);
-  for (int i = threadIdx.x; i < 1024; i += 256) {  // [k][n], coalesced along n
-    const int r = i >> 5, q = i & 31, k = k0 + r, nn = n0 + q;
-    if (k < K && nn < N) dst[(size_t)k * N + nn] = (bf16)t[q][r];
+  if (!L.t_hwc) {
+    // [C*KH*KW][N] = the source viewed [N][K], transposed: tiles of 32 k x 32 n
+    const int k0 = kt * 32;
+    if (k0 >= K) return;
+    for (int i = threadIdx.x; i < 1024; i += 256) {  // [n][k] rows, coalesced along k
+      const int r = i >> 5, q = i & 31, nn = n0 + r, k = k0 + q;
+      t[r][q] = (nn < N && k < K) ? L.w[(size_t)nn * K + k] : 0.f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 1024; i += 256) {  // [k][n], coalesced along n
+      const int r = i >> 5, q = i & 31, k = k0 + r, nn = n0 + q;
+      if (k < K && nn < N) dst[(size_t)k * N + nn] = (bf16)t[q][r];
+    }
+  } else {
+    // [KH*KW][C][N]: per channel c a 32 tap x 32 n tile of source rows w[n][c][tap], coalesced
+    // along tap on the read and along n on the write (a k tile of the packed row would read
+    // 32 channels of one tap, one 4-B element per source line)
+    const int ttl = (taps + 31) / 32, c = kt / ttl, p0 = (kt - c * ttl) * 32;
+    if (c >= L.C) return;
+    for (int i = threadIdx.x; i < 1024; i += 256) {  // [n][tap]
+      const int r = i >> 5, q = i & 31, nn = n0 + r, p = p0 + q;
+      t[r][q] = (nn < N && p < taps) ? L.w[((size_t)nn * L.C + c) * taps + p] : 0.f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 1024; i += 256) {  // [tap][c][n]
+      const int r = i >> 5, q = i & 31, p = p0 + r, nn = n0 + q;
+      if (p < taps && nn < N) dst[((size_t)p * L.C + c) * N + nn] = (bf16)t[q][r];
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a, int max_tiles, int max_n, int kts, int nts) {
+// Block ranges of one pack launch: per layer its forward-image tiles (tiles x N) then, after all
+// of those, its transpose tiles (kts x nts) -- exact counts, no idle blocks.
+struct PackPlan {
+  int off[2 * kMaxPack + 1];  // block offsets: [0, n) forward images, [n, 2n) transposes
+  int tiles[kMaxPack], kts[kMaxPack];
+};
+
+__global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a, PackPlan pl) {
   __shared__ float t[32][33];
-  const int nwb = max_tiles * max_n * a.n;
-  int b = blockIdx.x;
-  if (b < nwb) {
-    const int l = b / (max_tiles * max_n);
-    b -= l * max_tiles * max_n;
-    pack_wb_tile(a.layer[l], b % max_tiles, b / max_tiles, t);
-  } else {
-    b -= nwb;
-    const int l = b / (kts * nts);
-    b -= l * kts * nts;
-    pack_wt_tile(a.layer[l], b % kts, b / kts, t);
-  }
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < 2 * a.n && b >= pl.off[j + 1]) ++j;  // (uniform)
+  const int r = b - pl.off[j];
+  if (j < a.n)
+    pack_wb_tile(a.layer[j], r % pl.tiles[j], r / pl.tiles[j], t);
+  else
+    pack_wt_tile(a.layer[j - a.n], r % pl.kts[j - a.n], r / pl.kts[j - a.n], t);
 }
 
 }  // namespace
@@ -913,20 +930,24 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a, int max_
 hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
   if (a.n > kMaxPack) return hipErrorInvalidValue;
-  int max_n = 0, max_tiles = 0, max_k = 0;
-  bool any_t = false;
-  for (int i = 0; i < a.n; ++i) {
+  PackPlan pl{};
+  int total = 0;
+  for (int i = 0; i < a.n; ++i) {  // forward images: (channel x tap) tiles per output channel
     const ConvPackLayer& L = a.layer[i];
     const int taps = L.KH * L.KW;
-    max_n = L.N > max_n ? L.N : max_n;
-    const int tiles = ((taps + 31) / 32) * ((L.C + 31) / 32);
-    max_tiles = tiles > max_tiles ? tiles : max_tiles;
-    max_k = L.C * taps > max_k ? L.C * taps : max_k;
-    any_t = any_t || L.wt != nullptr;
+    pl.tiles[i] = ((taps + 31) / 32) * ((L.C + 31) / 32);
+    pl.off[i] = total;
+    total += pl.tiles[i] * L.N;
   }
-  const int kts = any_t ? (max_k + 31) / 32 : 0, nts = any_t ? (max_n + 31) / 32 : 0;
-  const int blocks = max_tiles * max_n * a.n + kts * nts * a.n;
-  hipLaunchKernelGGL(conv_pack_kernel, dim3(blocks), dim3(256), 0, s, a, max_tiles, max_n, kts, nts);
+  for (int i = 0; i < a.n; ++i) {  // transposes: k tiles (or channel x 32-tap tiles, t_hwc) x n tiles
+    const ConvPackLayer& L = a.layer[i];
+    const int taps = L.KH * L.KW;
+    pl.kts[i] = L.t_hwc ? L.C * ((taps + 31) / 32) : (L.C * taps + 31) / 32;
+    pl.off[a.n + i] = total;
+    if (L.wt) total += pl.kts[i] * ((L.N + 31) / 32);
+  }
+  pl.off[2 * a.n] = total;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(total), dim3(256), 0, s, a, pl);
   return hipGetLastError();
 }
 
