@@ -47,7 +47,7 @@ struct Actor {
   int n_layers, hidden_act;
 };
 
-__host__ __device__ __forceinline__ constexpr int split_kh(int din) { return ((din + 1) / 2 + 3) & ~3; }
+__host__ __device__ __forceinline__ int split_kh(int din) { return ((din + 1) / 2 + 3) & ~3; }
 // full form: every layer's image padded to 64 inputs (16 groups of 4), so the forward loop has
 // a compile-time trip count and issues all its LDS loads back to back
 constexpr int kFullGroups = 16;
@@ -375,58 +375,6 @@ __device__ float loco_step_regs(const LocoParams& p, LocoRegs& L, float a_in) {
   return L.fwd_weight * (L.rq[0] - x_before) * L.inv_dt_total + L.healthy - L.ctrl_cost * ctrl;
 }
 
-// Observation of a planar (CE_LOCO3) model with a compile-time layout, straight from registers:
-// [rq[3 - NPR .. 2], q (NJ joints), rv[0 .. 2], qd (NJ joints)], the joints in lanes 0 .. NJ-1 of
-// row 0. Returns the lane layout o (lane i = obs[i], the stores) and the row-form actor's layer-0
-// input ox (actor_obs_index) -- no LDS round trip on the step chain (loco_obs's write, wait, read).
-// Same values as loco_obs: copies and selects only.
-template <int SHIFT>
-__device__ __forceinline__ float row_shift(float v) {  // lane i <- lane i - SHIFT of its DPP row (0 outside it)
-  if constexpr (SHIFT == 0) return v;
-  else if constexpr (SHIFT > 0 && SHIFT < 16) return dpp<0x110 + SHIFT>(v);  // row_shr
-  else if constexpr (SHIFT < 0 && SHIFT > -16) return dpp<0x100 - SHIFT>(v);  // row_shl
-  else return 0.f;
-}
-
-template <int NPR, int NJ>
-struct ObsLayout {
-  static constexpr int Q0 = NPR, V0 = NPR + NJ, QD0 = V0 + 3, D = QD0 + NJ, KB = split_kh(D);
-  static_assert(D <= 32, "observation wider than two DPP rows");
-};
-
-// obs[B + i] for the lanes of one DPP row (i = lane & 15); q2 / qd2 hold row 0's joints in this row
-template <int NPR, int NJ, int B>
-__device__ __forceinline__ float obs_slot(const LocoRegs& L, float q2, float qd2, int i) {
-  using O = ObsLayout<NPR, NJ>;
-  const int idx = B + i;
-  const float qv = row_shift<O::Q0 - B>(q2);
-  const float qdv = row_shift<O::QD0 - B>(qd2);
-  const float rvv = idx == O::V0 ? L.rv[0] : idx == O::V0 + 1 ? L.rv[1] : L.rv[2];
-  const float rqv = idx + 3 - NPR == 0 ? L.rq[0] : idx + 3 - NPR == 1 ? L.rq[1] : L.rq[2];
-  float v = idx < O::D ? qdv : 0.f;
-  v = idx < O::QD0 ? rvv : v;
-  v = idx < O::V0 ? qv : v;
-  return idx < O::Q0 ? rqv : v;
-}
-
-template <int NPR, int NJ>
-__device__ __forceinline__ float loco_obs_regs(const LocoRegs& L, float& ox) {
-  using O = ObsLayout<NPR, NJ>;
-  const int lane = threadIdx.x, i = lane & 15, r = lane >> 4;
-  // row 0's joints also in row 1 (v_permlane16_swap: [row 0, row 0, row 2, row 2])
-  const auto q2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(L.q), __float_as_uint(L.q), false, false);
-  const auto qd2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(L.qd), __float_as_uint(L.qd), false, false);
-  const float qa = __uint_as_float(q2[0]), qda = __uint_as_float(qd2[0]);
-  const float s0 = obs_slot<NPR, NJ, 0>(L, qa, qda, i);
-  const float s16 = obs_slot<NPR, NJ, 16>(L, qa, qda, i);
-  const float skb = obs_slot<NPR, NJ, O::KB>(L, qa, qda, i);
-  // layer-0 input: row 0 = K-half 0 (obs[i]), row 1 = K-half 1 (obs[KB + i]); rows 2, 3 copy them
-  const float x01 = r == 0 ? s0 : skb;
-  const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(x01), __float_as_uint(x01), false, false);
-  ox = __uint_as_float(x[0]);
-  return r == 0 ? s0 : r == 1 ? s16 : 0.f;
-}
-
 // Per-lane output cursors (VGPRs, advanced by one step per iteration): the per-step
 // stores need no scalar base registers, and the five per-env scalars of a step go out
 // as ONE store (lane 0 env reward, 1 done, 2 truncation, 3 finished-episode return,
@@ -452,10 +400,7 @@ __device__ __forceinline__ long long stamp(float dep) {
   return t;
 }
 
-// OBS = (NPR << 4) | NJ: the observation layout at compile time (row form, CE_LOCO3 only): the
-// observation comes from registers (loco_obs_regs) instead of the LDS scratch
-template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1, int FS = -1, bool PROF = false, bool ROW = true,
-          int OBS = 0>
+template <bool SPLIT, int ENV, int HACT, int NLT = -1, int HW = -1, int FS = -1, bool PROF = false, bool ROW = true>
 __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_raw[];
   lf* xb = (lf*)lds_raw;       // [64] layer input broadcast
@@ -477,8 +422,6 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
 
   // row form: the split form with every hidden layer 32 wide (HW == 32, depth NLT known)
   constexpr bool NB = ROW && SPLIT && HW == 32 && NLT > 0;
-  constexpr bool OBSR = NB && ENV == CE_LOCO3 && OBS != 0;
-  constexpr int NPR = OBS >> 4, NJO = OBS & 15;
   Actor<SPLIT> ar;
   load_actor<SPLIT, NB>(a.pi, ar, wlds);
   // lane layout of the observation (stores) and, for the row form, the layer-0 input layout
@@ -616,8 +559,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
       if (loco) {
         r_env = loco_step_regs<ENV, FS>(P.loco, L, a_env);
         if constexpr (PROF) t2 = stamp(r_env);
-        if constexpr (OBSR) o_next = loco_obs_regs<NPR, NJO>(L, ox_next);
-        else o_next = loco_obs<ENV>(P.loco, L, sb, oxr, ox_next);
+        o_next = loco_obs<ENV>(P.loco, L, sb, oxr, ox_next);
         if constexpr (PROF) t3 = stamp(o_next);
       } else {
         if (lane < A) act[lane] = a_env;
@@ -659,8 +601,7 @@ __global__ __launch_bounds__(64) void rollout_chain_kernel(RolloutArgs a) {
         wave_sync();
         if (loco) {
           loco_load(P.loco, st, L);
-          if constexpr (OBSR) o = loco_obs_regs<NPR, NJO>(L, ox);
-          else o = loco_obs<ENV>(P.loco, L, sb, oxr, ox);
+          o = loco_obs<ENV>(P.loco, L, sb, oxr, ox);
         } else {
           o = lane < D ? sb[lane] : 0.f;
           ox = sb[oxr];
@@ -734,20 +675,15 @@ hipError_t rollout_launch(const RolloutArgs& a, hipStream_t s) {
   // (+ the frame skip of the benchmark recipes: HalfCheetah 5 with the [32, 32] tanh actor,
   // Hopper / Walker 4 with the [64, 64] ReLU one)
   const int fs = env == CE_LOCO3 ? p.frame_skip : 0;
-  // HalfCheetah's observation layout (2 root coordinates, 6 joints) at compile time
-  const bool hc = env == CE_LOCO3 && p.obs_skip == 1 && p.nj == 6;
-  constexpr int kHcObs = (2 << 4) | 6;
   if (a.prof || a.lds_actor) {  // the probe / test instances: the HalfCheetah bench configuration only
-    if (!(split && hc && act == ACT_TANH && hw == 32 && fs == 5)) return hipErrorInvalidValue;
-    if (a.prof && a.lds_actor)  // (the LDS actor reads its input from the LDS observation)
+    if (!(split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)) return hipErrorInvalidValue;
+    if (a.prof && a.lds_actor)
       hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, true, false>), g, b, lds, s, a);
     else if (a.prof)
-      hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, true, true, kHcObs>), g, b, lds, s, a);
+      hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, true>), g, b, lds, s, a);
     else
       hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, false, false>), g, b, lds, s, a);
-  } else if (split && hc && act == ACT_TANH && hw == 32 && fs == 5)
-    hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5, false, true, kHcObs>), g, b, lds, s, a);
-  else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)
+  } else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 5)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 5>), g, b, lds, s, a);
   else if (split && env == CE_LOCO3 && act == ACT_TANH && hw == 32 && fs == 4)
     hipLaunchKernelGGL((rollout_chain_kernel<true, CE_LOCO3, ACT_TANH, 3, 32, 4>), g, b, lds, s, a);
