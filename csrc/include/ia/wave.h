@@ -37,13 +37,6 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-// row_newbcast:I -- lane I of each 16-lane DPP row, in every lane of that row (every source
-// lane is valid, so bound_ctrl only spares the compiler an "old" value per move).
-template <int I>
-__device__ __forceinline__ float row_bcast(float v) {
-  return dpp<0x150 + I>(v);
-}
-
 // Sum over lanes 0..7 (the joint lanes; lanes 8.. must hold 0 in each 16-lane row's
 // upper half for rows != 0 to not matter -- only lane 7 of row 0 is read): two
 // quad_perm butterflies give quad sums, row_shr:4 adds quad 0 into quad 1.
