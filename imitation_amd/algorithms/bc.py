@@ -560,14 +560,19 @@ class _DeviceEpochRunner:
         flat = self.trainer.optimizer.flat_grads[0]
         step = self._comm.stage_bytes // 4 // 4 * 4
         w = self._f.g_lin[0]
-        o = (w.data_ptr() - flat.data_ptr()) // 4
-        lo, hi = o - o % 4, (o + w.numel() + 3) // 4 * 4  # (16-B aligned slices)
+        lo = (w.data_ptr() - flat.data_ptr()) // 4
+        hi = lo + w.numel()
 
         def chunks(a, b):
             return [flat[i : min(b, i + step)] for i in range(a, b, step)]
 
-        fc = chunks(lo, hi)
-        rest = chunks(0, lo) + chunks(hi, flat.numel())
+        if lo % 4 or hi % 4:
+            # the early range must hold the FC weight gradient and nothing else (a neighbour's
+            # gradient is not final yet) and start on a 16-B boundary: else no early reduction
+            fc, rest = [], chunks(0, flat.numel())
+        else:
+            fc = chunks(lo, hi)
+            rest = chunks(0, lo) + chunks(hi, flat.numel())
         self._ranges = r = (fc, rest)
         return r
 

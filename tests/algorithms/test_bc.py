@@ -394,3 +394,32 @@ def test_bc_raises_when_the_data_loader_runs_dry(cartpole_venv, expert_transitio
     with pytest.raises(AssertionError, match=".*no data.*"):
         tr.train(n_batches=20, on_batch_end=on_batch_end)
     assert n_batches == no_yield_after_iter
+
+
+@pytest.mark.parametrize("fc_off,fc_n", [(77984, 1_605_632), (77985, 1_605_632), (77984, 1_605_630)])
+def test_dp_bc_reduction_ranges_cover_the_bucket_once(fc_off, fc_n):
+    """The graph-resident DP BC step reduces the FC weight gradient early (overlapping the conv
+    backward) and the rest after it: the chunks cover the flat bucket exactly once, none exceeds
+    the one-shot staging slot, and the early range is exactly the FC weight -- or, when it does not
+    sit on 16-B boundaries, empty (a neighbour's gradient is not final at that point)."""
+    import types
+
+    flat = th.zeros(fc_off + fc_n + 1000)
+    runner = bc._DeviceEpochRunner.__new__(bc._DeviceEpochRunner)
+    runner.trainer = types.SimpleNamespace(optimizer=types.SimpleNamespace(flat_grads=[flat]))
+    runner._comm = types.SimpleNamespace(stage_bytes=1 << 20)
+    runner._f = types.SimpleNamespace(g_lin=[flat[fc_off : fc_off + fc_n]])
+    fc, rest = runner._dp_ranges()
+    base = flat.data_ptr()
+    spans = sorted(((t.data_ptr() - base) // 4, t.numel()) for t in fc + rest)
+    pos = 0
+    for o, n in spans:
+        assert o == pos and 0 < n <= (1 << 20) // 4
+        pos += n
+    assert pos == flat.numel()
+    aligned = fc_off % 4 == 0 and (fc_off + fc_n) % 4 == 0
+    if aligned:
+        assert (fc[0].data_ptr() - base) // 4 == fc_off and sum(t.numel() for t in fc) == fc_n
+        assert all((t.data_ptr() - base) % 16 == 0 for t in fc)
+    else:
+        assert fc == []
