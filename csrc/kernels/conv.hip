@@ -984,12 +984,13 @@ void conv_wgrad_blocks(const ConvGeo& g, int* nblk, int* mpb) {
   const int chunks = (M + CH - 1) / CH;
   const int K = g.Kp;
   // fp32 partial traffic (nblk x N x K, written then re-read by conv_reduce) vs parallelism:
-  // small layers (BC batches) ~1M partial floats at most (the 256-block cap moved 24 MB per
-  // NatureCNN BC step); large ones (>= 64K rows, e.g. full-resolution reward CNN batches,
-  // where the m loop is the cost) up to 8M floats and 512 blocks -- 2 per CU
+  // small layers (BC batches) ~2M partial floats at most (the 256-block cap moved 24 MB per
+  // NatureCNN BC step; 1M -> 2M: BC step 0.145 -> 0.140 ms, 4M 0.141, profiles/r6_bc_step.md);
+  // large ones (>= 64K rows, e.g. full-resolution reward CNN batches, where the m loop is the
+  // cost) up to 8M floats and 512 blocks -- 2 per CU
   const int len = g.N * K + g.N;
   const bool big = CH > 32;
-  int cap = (big ? (8 << 20) : (1 << 20)) / len;
+  int cap = (big ? (8 << 20) : (2 << 20)) / len;
   const int hi = big ? 512 : 256;
   cap = cap < 16 ? 16 : (cap > hi ? hi : cap);
   int b = chunks < cap ? chunks : cap;
