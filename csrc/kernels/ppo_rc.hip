@@ -16,6 +16,7 @@ IA_RC_INSTANCES(IA_RC_EXTERN)
 // minibatch has more chunks than waves), one lane per row. Minibatch statistics (obs
 // moments, advantage mean / std) are exact two-pass reductions over all its rows.
 constexpr int kPrepWaves = 16;
+constexpr int kPrepBatch = 16;  // obs loads of a row issued back to back (launch bounds: <= 128 VGPRs)
 
 __device__ __forceinline__ int prep_idx(const PPOArgs& a, const PPORcGeo& g, int e, int mb, int c, int lane) {
   const int Bg = g.G * g.nch * g.cw;
@@ -43,24 +44,41 @@ __global__ __launch_bounds__(64 * kPrepWaves) void ppo_rc_prep_kernel(PPOArgs a,
     const int idx = ok ? prep_idx(a, g, e, mb, c, lane) : 0;
     const size_t slot = (size_t)k * CH + c;
     float* xr = g.xraw + (slot * 64 + lane) * g.dp;
-    for (int f = 0; f < g.dp; ++f) {
-      const float v = (ok && f < D) ? a.obs[(size_t)idx * D + f] : 0.f;
-      if (ok) xr[f] = v;
-      if (f < D && a.has_norm) {
-        const float s = wave_sum(v);
-        if (lane == f) fs += s;
+    // batches of kPrepBatch features: all of a batch's loads are issued before its first store
+    // (a store to xraw between two obs loads serialises them -- the buffers may alias as far as
+    // the compiler knows: ~20 dependent L2 round trips per row before)
+    for (int f0 = 0; f0 < g.dp; f0 += kPrepBatch) {
+      float xv[kPrepBatch];
+#pragma unroll
+      for (int i = 0; i < kPrepBatch; ++i) xv[i] = (ok && f0 + i < D) ? a.obs[(size_t)idx * D + f0 + i] : 0.f;
+#pragma unroll
+      for (int i = 0; i < kPrepBatch; ++i) {
+        const int f = f0 + i;
+        if (f < g.dp) {
+          if (ok) xr[f] = xv[i];
+          if (f < D && a.has_norm) {
+            const float s = wave_sum(xv[i]);
+            if (lane == f) fs += s;
+          }
+        }
       }
     }
-    float* ac = g.acts + (slot * 64 + lane) * 16;
+    float av16[16];
+#pragma unroll
     for (int j = 0; j < 16; ++j) {
+      float v = 0.f;
       if (ok) {
-        float v = 0.f;
         if (a.discrete) v = j == 0 ? a.acts[idx] : 0.f;
         else v = j < a.A ? a.acts[(size_t)idx * a.A + j] : 0.f;
-        ac[j] = v;
       }
+      av16[j] = v;
     }
-    as += wave_sum(ok ? a.adv[idx] : 0.f);
+    const float adv = ok ? a.adv[idx] : 0.f;
+    float* ac = g.acts + (slot * 64 + lane) * 16;
+    if (ok)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ac[j] = av16[j];
+    as += wave_sum(adv);
   }
   red[wv][lane] = fs;
   if (lane == 0) red_a[wv] = as;
@@ -82,11 +100,19 @@ __global__ __launch_bounds__(64 * kPrepWaves) void ppo_rc_prep_kernel(PPOArgs a,
   for (int c = wv; c < CH; c += nw) {
     const int idx = ok ? prep_idx(a, g, e, mb, c, lane) : 0;
     if (a.has_norm) {
-      for (int f = 0; f < D; ++f) {
-        const float v = ok ? a.obs[(size_t)idx * D + f] : 0.f;
-        const float d = ok ? v - stat[0][f] : 0.f;
-        const float s = wave_sum(d * d);
-        if (lane == f) fv += s;
+      for (int f0 = 0; f0 < D; f0 += kPrepBatch) {  // (batched loads, as in pass 1)
+        float xv[kPrepBatch];
+#pragma unroll
+        for (int i = 0; i < kPrepBatch; ++i) xv[i] = (ok && f0 + i < D) ? a.obs[(size_t)idx * D + f0 + i] : 0.f;
+#pragma unroll
+        for (int i = 0; i < kPrepBatch; ++i) {
+          const int f = f0 + i;
+          if (f < D) {
+            const float d = ok ? xv[i] - stat[0][f] : 0.f;
+            const float s = wave_sum(d * d);
+            if (lane == f) fv += s;
+          }
+        }
       }
     }
     const float d = ok ? a.adv[idx] - am : 0.f;
