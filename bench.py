@@ -101,7 +101,12 @@ def fill_expert_cache(args):
            "--seed", str(args.seed), "--expert-steps", str(args.expert_steps), "--n-eval", str(args.eval_episodes),
            "--rank", str(rank), "--n-envs", str(args.n_envs), "--device", f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % n}",
            "--cache-dir", args.expert_cache]
-    p = subprocess.run(cmd, env=env, cwd=os.path.dirname(os.path.abspath(__file__)), stdout=subprocess.PIPE, text=True)
+    try:  # (bounded: a stuck child must not hang the bench; ~5 s normally)
+        p = subprocess.run(cmd, env=env, cwd=os.path.dirname(os.path.abspath(__file__)), stdout=subprocess.PIPE,
+                           text=True, timeout=900)
+    except subprocess.TimeoutExpired:
+        print("bench.py: expert child timed out; the expert trains in this process instead", file=sys.stderr)
+        return None
     sys.stderr.write(p.stdout)
     if p.returncode:
         print(f"bench.py: expert child exited {p.returncode}; the expert trains in this process instead", file=sys.stderr)
