@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include "ia/wave.h"
 #include "launchers.h"
 
 namespace ia {
@@ -39,12 +40,8 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return v;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
+// (wave sums: ia::wave_sum, DPP row sums + permlane swaps -- a __shfl_xor butterfly is six
+// ds_bpermute round trips per call, ~18 of them on block 0's metrics path)
 __device__ float block_sum(float v, float* red) {
   v = wave_sum(v);
   const int w = threadIdx.x >> 6;
@@ -98,7 +95,14 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
         __syncthreads();
         if (a.prof && blockIdx.x == 0 && tid == 0) a.prof[1] = clock64();
       }
-      // ---- logit partials: wave w rows r0 + w + 4 q (q < 8)
+      // ---- logit partials: wave w rows r0 + w + 4 q (q < 8). This lane's W columns go to
+      // registers once: read inside the row loop they were re-read from LDS for every row (the
+      // partial stores below may alias them as far as the compiler knows): 8x the LDS reads
+      float wr[KPL][kMaxA];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i)
+#pragma unroll
+        for (int j = 0; j < kMaxA; ++j) wr[i][j] = wt[j * KPL * 64 + 64 * i + lane];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         float acc[kMaxA];
@@ -107,7 +111,7 @@ __global__ __launch_bounds__(kThreads) void bc_head_train_kernel(BcHeadArgs a, i
 #pragma unroll
         for (int i = 0; i < KPL; ++i) {
 #pragma unroll
-          for (int j = 0; j < kMaxA; ++j) acc[j] = fmaf(hv[q][i], wt[j * KPL * 64 + 64 * i + lane], acc[j]);
+          for (int j = 0; j < kMaxA; ++j) acc[j] = fmaf(hv[q][i], wr[i][j], acc[j]);
         }
 #pragma unroll
         for (int j = 0; j < kMaxA; ++j) part[lane * kPS + (w + 4 * q) * ap + j] = acc[j];

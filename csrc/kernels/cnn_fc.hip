@@ -120,18 +120,22 @@ constexpr int kChG = 8;          // channels per block
 constexpr int kChMaxCols = 416;  // kChG * HW bound: 26 tiles of 16 columns
 constexpr int kChTilesW = 13;    // tiles per wave (parity split)
 constexpr int kChXIt = 4;        // X loads per thread per 32-row chunk: ceil(32 * 52 / 512)
+constexpr int kChHwSplit = 4;  // HW position groups per (channel group, n block): 256 blocks at NatureCNN (64 before; BC step -1 us, profiles/r6_bc_step.md)
 
 __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
                                                           const float* __restrict__ Hout, float* __restrict__ dW,
                                                           float* __restrict__ db, bf16* __restrict__ dZb, int M, int K,
-                                                          int NH, int C, int HW) {
+                                                          int NH, int C, int HW, int hws) {
   __shared__ __attribute__((aligned(16))) bf16 zs[64][40];          // dZ^T chunk [n][m] (+8 pad)
   __shared__ __attribute__((aligned(16))) bf16 xs[kChMaxCols][40];  // X^T chunk [column][m]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int wn = w & 3, par = w >> 2;
   const int c0 = blockIdx.x * kChG, n0 = blockIdx.y * 64;
-  const int ncols = kChG * HW, ntiles = (ncols + 15) / 16, nx = 32 * HW;
-  const bool first = blockIdx.x == 0;
+  // blockIdx.z: positions [hw0, hw0 + hwn) of the kChG channels (a block's columns: channel g,
+  // position hw0 + j -> local column g * hwn + j)
+  const int hw0 = blockIdx.z * hws, hwn = HW - hw0 < hws ? HW - hw0 : hws;
+  const int ncols = kChG * hwn, ntiles = (ncols + 15) / 16, nx = 32 * hwn;
+  const bool first = blockIdx.x == 0 && blockIdx.z == 0;
   f32x4 acc[kChTilesW];
 #pragma unroll
   for (int j = 0; j < kChTilesW; ++j) acc[j] = zero4();
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
     bf16x8 xv[kChXIt];
 #pragma unroll
     for (int e = 0; e < kChXIt; ++e) {  // all of this thread's X loads in flight first
-      const int i = tid + 512 * e, mm = i / HW, hw = i - mm * HW, m = m0 + mm;
+      const int i = tid + 512 * e, mm = i / hwn, hw = hw0 + i - mm * hwn, m = m0 + mm;
       xv[e] = (i < nx && m < M) ? *reinterpret_cast<const bf16x8*>(X + (size_t)m * K + (size_t)hw * C + c0) : bf16x8{};
     }
 #pragma unroll
@@ -156,10 +160,10 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
     }
 #pragma unroll
     for (int e = 0; e < kChXIt; ++e) {
-      const int i = tid + 512 * e, mm = i / HW, hw = i - mm * HW;
+      const int i = tid + 512 * e, mm = i / hwn, hl = i - mm * hwn;
       if (i < nx) {
 #pragma unroll
-        for (int g = 0; g < kChG; ++g) xs[g * HW + hw][mm] = xv[e][g];
+        for (int g = 0; g < kChG; ++g) xs[g * hwn + hl][mm] = xv[e][g];
       }
     }
     __syncthreads();
@@ -174,13 +178,14 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
     }
     __syncthreads();
   }
-  float* dWb = dW + (size_t)c0 * HW;
 #pragma unroll
   for (int j = 0; j < kChTilesW; ++j) {
-    const int col = 16 * (par + 2 * j) + (l & 15);
-    if (col < ncols) {
+    const int lc = 16 * (par + 2 * j) + (l & 15);  // local column: channel lc / hwn, position hw0 + lc % hwn
+    if (lc < ncols) {
+      const int g = lc / hwn;
+      const int col = (c0 + g) * HW + hw0 + (lc - g * hwn);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dWb[(size_t)(n0 + wn * 16 + 4 * (l >> 4) + i) * K + col] = acc[j][i];
+      for (int i = 0; i < 4; ++i) dW[(size_t)(n0 + wn * 16 + 4 * (l >> 4) + i) * K + col] = acc[j][i];
     }
   }
   if (first && tid < 64) db[n0 + tid] = relu_bias_sum(dH, Hout, M, NH, n0 + tid);  // fixed row order
@@ -243,9 +248,12 @@ hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const 
   if (!fc_train_ok(M, K, NH, C, HW)) return hipErrorInvalidValue;
   // channel-aligned blocks (16-B NHWC loads) when X allows them, else the 64-column blocks
   const bool ch = C % kChG == 0 && kChG * HW <= kChMaxCols && reinterpret_cast<uintptr_t>(X) % 16 == 0;
+  // each block's positions: a split of the HW positions over gridDim.z (more blocks than the
+  // C / kChG x NH / 64 = 64 of NatureCNN, each with fewer column tiles)
+  const int hws = (HW + kChHwSplit - 1) / kChHwSplit;
   if (ch)
-    hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(C / kChG, NH / 64), dim3(512), 0, s, static_cast<const bf16*>(X), dH, Hout, dW,
-                       db, static_cast<bf16*>(dZb), M, K, NH, C, HW);
+    hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(C / kChG, NH / 64, (HW + hws - 1) / hws), dim3(512), 0, s,
+                       static_cast<const bf16*>(X), dH, Hout, dW, db, static_cast<bf16*>(dZb), M, K, NH, C, HW, hws);
   else
     hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / (16 * kFcCT), NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout,
                        dW, db, static_cast<bf16*>(dZb), M, K, NH, C, HW);

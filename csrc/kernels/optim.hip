@@ -29,10 +29,16 @@ __device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v,
 }
 
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
-  const float t = *a.step + (a.cnt ? 1.f : 0.f);
-  const float bc1 = 1.f - powf(a.beta1, t);
-  const float bc2_sqrt = sqrtf(1.f - powf(a.beta2, t));
-  const float step_size = a.lr / bc1;
+  // the bias corrections once per block (two powf per thread were ~100 VALU each); same values
+  __shared__ float bcs[3];
+  if (threadIdx.x == 0) {
+    const float t0 = *a.step + (a.cnt ? 1.f : 0.f);
+    bcs[0] = t0;
+    bcs[1] = sqrtf(1.f - powf(a.beta2, t0));
+    bcs[2] = a.lr / (1.f - powf(a.beta1, t0));
+  }
+  __syncthreads();
+  const float t = bcs[0], bc2_sqrt = bcs[1], step_size = bcs[2];
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 + 3 < a.n) {
     float4 p = *reinterpret_cast<float4*>(a.params + i4);
