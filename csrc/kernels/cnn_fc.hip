@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void fc_wgrad_kernel(const bf16* __restrict__ 
       if (m < M) {
         const size_t o = (size_t)m * NH + n0 + nn;
         z = Hout[o] > 0.f ? dH[o] : 0.f;
-        if (first) dZb[o] = (bf16)z;
+        if (first && dZb) dZb[o] = (bf16)z;
       }
       zs[nn][mm] = (bf16)z;
     }
@@ -122,20 +122,22 @@ constexpr int kChTilesW = 13;    // tiles per wave (parity split)
 constexpr int kChXIt = 4;        // X loads per thread per 32-row chunk: ceil(32 * 52 / 512)
 constexpr int kChHwSplit = 4;  // HW position groups per (channel group, n block): 256 blocks at NatureCNN (64 before; BC step -1 us, profiles/r6_bc_step.md)
 
-__global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
-                                                          const float* __restrict__ Hout, float* __restrict__ dW,
-                                                          float* __restrict__ db, bf16* __restrict__ dZb, int M, int K,
-                                                          int NH, int C, int HW, int hws) {
+// (bx, by, bz): channel group, n block, position group (the kernel's blockIdx, or decoded from a
+// paired launch's block index)
+__device__ __forceinline__ void fc_wgrad_ch_body(const bf16* __restrict__ X, const float* __restrict__ dH,
+                                                 const float* __restrict__ Hout, float* __restrict__ dW,
+                                                 float* __restrict__ db, bf16* __restrict__ dZb, int M, int K, int NH,
+                                                 int C, int HW, int hws, int bx, int by, int bz) {
   __shared__ __attribute__((aligned(16))) bf16 zs[64][40];          // dZ^T chunk [n][m] (+8 pad)
   __shared__ __attribute__((aligned(16))) bf16 xs[kChMaxCols][40];  // X^T chunk [column][m]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int wn = w & 3, par = w >> 2;
-  const int c0 = blockIdx.x * kChG, n0 = blockIdx.y * 64;
-  // blockIdx.z: positions [hw0, hw0 + hwn) of the kChG channels (a block's columns: channel g,
-  // position hw0 + j -> local column g * hwn + j)
-  const int hw0 = blockIdx.z * hws, hwn = HW - hw0 < hws ? HW - hw0 : hws;
+  const int c0 = bx * kChG, n0 = by * 64;
+  // bz: positions [hw0, hw0 + hwn) of the kChG channels (a block's columns: channel g, position
+  // hw0 + j -> local column g * hwn + j)
+  const int hw0 = bz * hws, hwn = HW - hw0 < hws ? HW - hw0 : hws;
   const int ncols = kChG * hwn, ntiles = (ncols + 15) / 16, nx = 32 * hwn;
-  const bool first = blockIdx.x == 0 && blockIdx.z == 0;
+  const bool first = bx == 0 && bz == 0;
   f32x4 acc[kChTilesW];
 #pragma unroll
   for (int j = 0; j < kChTilesW; ++j) acc[j] = zero4();
@@ -191,13 +193,34 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
   if (first && tid < 64) db[n0 + tid] = relu_bias_sum(dH, Hout, M, NH, n0 + tid);  // fixed row order
 }
 
+__global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
+                                                          const float* __restrict__ Hout, float* __restrict__ dW,
+                                                          float* __restrict__ db, bf16* __restrict__ dZb, int M, int K,
+                                                          int NH, int C, int HW, int hws) {
+  fc_wgrad_ch_body(X, dH, Hout, dW, db, dZb, M, K, NH, C, HW, hws, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
 // One wave = 16 rows x 16 NHWC columns; the n loop is issued 4 k-steps (8 loads) at a time
 // so the L2 round trips overlap (the wave reads 16 KB of Wt).
-__global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
-                                                       bf16* __restrict__ dX, int M, int K, int NH,
-                                                       const bf16* __restrict__ Xm) {
+// FROM_H: the dZ operand formed from dH / Hout (fp32, ReLU mask) as the weight-gradient blocks form
+// it -- bf16 of the same value as their dZb, so no ordering against them (the paired launch)
+__device__ __forceinline__ bf16x8 relu_dz8(const float* __restrict__ dH, const float* __restrict__ Hout, size_t o) {
+  const float4 d0 = *reinterpret_cast<const float4*>(dH + o), d1 = *reinterpret_cast<const float4*>(dH + o + 4);
+  const float4 h0 = *reinterpret_cast<const float4*>(Hout + o), h1 = *reinterpret_cast<const float4*>(Hout + o + 4);
+  bf16x8 v;
+  v[0] = (bf16)(h0.x > 0.f ? d0.x : 0.f); v[1] = (bf16)(h0.y > 0.f ? d0.y : 0.f);
+  v[2] = (bf16)(h0.z > 0.f ? d0.z : 0.f); v[3] = (bf16)(h0.w > 0.f ? d0.w : 0.f);
+  v[4] = (bf16)(h1.x > 0.f ? d1.x : 0.f); v[5] = (bf16)(h1.y > 0.f ? d1.y : 0.f);
+  v[6] = (bf16)(h1.z > 0.f ? d1.z : 0.f); v[7] = (bf16)(h1.w > 0.f ? d1.w : 0.f);
+  return v;
+}
+
+template <bool FROM_H>
+__device__ __forceinline__ void fc_dgrad_body(const bf16* __restrict__ dZb, const float* __restrict__ dH,
+                                              const float* __restrict__ Hout, const bf16* __restrict__ Wt,
+                                              bf16* __restrict__ dX, int M, int K, int NH, const bf16* __restrict__ Xm,
+                                              int wave) {
   const int l = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int ktiles = K / 16;
   const int mt = wave / ktiles, kt = wave - mt * ktiles;
   const int m0 = mt * 16, k0 = kt * 16;
@@ -205,7 +228,8 @@ __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ 
   const int m = m0 + (l & 15);
   const bool mv = m < M;
   const int nq = (l >> 4) * 8;
-  const bf16* ar = dZb + (size_t)(mv ? m : 0) * NH + nq;
+  const size_t ao = (size_t)(mv ? m : 0) * NH + nq;
+  const bf16* ar = FROM_H ? nullptr : dZb + ao;
   const bf16* br = Wt + (size_t)(k0 + (l & 15)) * NH + nq;
   f32x4 acc = zero4();
   for (int n0 = 0; n0 < NH; n0 += 128) {
@@ -213,7 +237,8 @@ __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool ok = n0 + 32 * u < NH;
-      a[u] = ok ? *reinterpret_cast<const bf16x8*>(ar + n0 + 32 * u) : bf16x8{};
+      if constexpr (FROM_H) a[u] = ok ? relu_dz8(dH, Hout, ao + n0 + 32 * u) : bf16x8{};
+      else a[u] = ok ? *reinterpret_cast<const bf16x8*>(ar + n0 + 32 * u) : bf16x8{};
       b[u] = ok ? *reinterpret_cast<const bf16x8*>(br + n0 + 32 * u) : bf16x8{};
     }
 #pragma unroll
@@ -237,6 +262,30 @@ __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
+                                                       bf16* __restrict__ dX, int M, int K, int NH,
+                                                       const bf16* __restrict__ Xm) {
+  fc_dgrad_body<false>(dZb, nullptr, nullptr, Wt, dX, M, K, NH, Xm, blockIdx.x * 4 + (threadIdx.x >> 6));
+}
+
+// The FC backward in ONE launch (BC-size batches): blocks [0, nwb) the channel-aligned weight
+// gradient (decoded (bx, by, bz)), the rest the data gradient, 8 waves = 8 tiles per block. The
+// two read the same dH / Hout and neither feeds the other (the data gradient forms its bf16 dZ
+// operand itself): one launch, and the ~5 us dispatch of the second, fewer per step.
+__global__ __launch_bounds__(512) void fc_back_pair_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
+                                                           const float* __restrict__ Hout, float* __restrict__ dW,
+                                                           float* __restrict__ db, const bf16* __restrict__ Wt,
+                                                           bf16* __restrict__ dX, int M, int K, int NH, int C, int HW,
+                                                           int hws, int gx, int gz, int nwb, const bf16* __restrict__ Xm) {
+  const int b = blockIdx.x;
+  if (b < nwb) {
+    const int bx = b % gx, r = b / gx, bz = r % gz, by = r / gz;
+    fc_wgrad_ch_body(X, dH, Hout, dW, db, nullptr, M, K, NH, C, HW, hws, bx, by, bz);
+  } else {
+    fc_dgrad_body<true>(nullptr, dH, Hout, Wt, dX, M, K, NH, Xm, (b - nwb) * 8 + (threadIdx.x >> 6));
+  }
+}
+
 }  // namespace
 
 bool fc_train_ok(int M, int K, int NH, int C, int HW) {
@@ -251,8 +300,17 @@ hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const 
   // each block's positions: a split of the HW positions over gridDim.z (more blocks than the
   // C / kChG x NH / 64 = 64 of NatureCNN, each with fewer column tiles)
   const int hws = (HW + kChHwSplit - 1) / kChHwSplit;
+  const int gx = C / kChG, gy = NH / 64, gz = (HW + hws - 1) / hws;
+  if (ch && dX && M <= 64) {  // BC-size batches: both halves in one launch
+    const int nwb = gx * gy * gz;
+    const int dblocks = (((M + 15) / 16) * (K / 16) + 7) / 8;
+    hipLaunchKernelGGL(fc_back_pair_kernel, dim3(nwb + dblocks), dim3(512), 0, s, static_cast<const bf16*>(X), dH, Hout,
+                       dW, db, static_cast<const bf16*>(Wt), static_cast<bf16*>(dX), M, K, NH, C, HW, hws, gx, gz, nwb,
+                       mask_dx ? static_cast<const bf16*>(X) : nullptr);
+    return hipGetLastError();
+  }
   if (ch)
-    hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(C / kChG, NH / 64, (HW + hws - 1) / hws), dim3(512), 0, s,
+    hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(gx, gy, gz), dim3(512), 0, s,
                        static_cast<const bf16*>(X), dH, Hout, dW, db, static_cast<bf16*>(dZb), M, K, NH, C, HW, hws);
   else
     hipLaunchKernelGGL(fc_wgrad_kernel, dim3(K / (16 * kFcCT), NH / 64), dim3(256), 0, s, static_cast<const bf16*>(X), dH, Hout,
