@@ -17,6 +17,14 @@ namespace py = pybind11;
 
 inline hipStream_t ia_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+namespace ia {
+struct GatherArgs;
+}
+// (kernels.cpp) the checked GatherArgs of a cursor-indexed row gather; *incp: the step counter or nullptr
+ia::GatherArgs gather_cursor_args(const std::vector<torch::Tensor>& srcs, const torch::Tensor& perm,
+                                  const torch::Tensor& cursor, int64_t n, const std::vector<torch::Tensor>& dst,
+                                  const c10::optional<torch::Tensor>& inc, float** incp);
+
 void register_envs(py::module& m);
 void register_kernels(py::module& m);
 void register_engine(py::module& m);

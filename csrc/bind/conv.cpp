@@ -237,7 +237,9 @@ bool conv_backward_pair_ok(torch::Tensor x, int64_t N, int64_t KH, int64_t KW, i
 }
 
 // fp32 conv weights [N, C, KH, KW] -> (bf16 [N, KH, KW, C] each, bf16 [C, KH, KW, N] where want_t)
-py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> want_t, std::vector<bool> t_hwc) {
+// gather (optional): (srcs, perm, cursor, n, dst, inc) of gather_rows_cursor, run in the same launch
+py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> want_t, std::vector<bool> t_hwc,
+                            py::object gather) {
   TORCH_CHECK(ws.size() == want_t.size() && (int)ws.size() <= ia::kMaxPack, "conv_pack_weights: layer count");
   ia::ConvPackArgs a{};
   a.n = (int)ws.size();
@@ -259,7 +261,22 @@ py::tuple conv_pack_weights(std::vector<torch::Tensor> ws, std::vector<bool> wan
     wbs.push_back(wb);
     wts.push_back(wt);
   }
-  IA_HIP_CHECK3(ia::conv_pack_weights(a, ia_stream()));
+  if (gather.is_none()) {
+    IA_HIP_CHECK3(ia::conv_pack_weights(a, ia_stream()));
+  } else {
+    auto g = gather.cast<py::tuple>();
+    TORCH_CHECK(g.size() == 6, "conv_pack_weights: gather = (srcs, perm, cursor, n, dst, inc)");
+    auto srcs = g[0].cast<std::vector<torch::Tensor>>();
+    auto perm = g[1].cast<torch::Tensor>();
+    auto cursor = g[2].cast<torch::Tensor>();
+    const int64_t n = g[3].cast<int64_t>();
+    auto dst = g[4].cast<std::vector<torch::Tensor>>();
+    c10::optional<torch::Tensor> inc;
+    if (!g[5].is_none()) inc = g[5].cast<torch::Tensor>();
+    float* incp = nullptr;
+    const ia::GatherArgs ga = gather_cursor_args(srcs, perm, cursor, n, dst, inc, &incp);
+    IA_HIP_CHECK3(ia::conv_pack_weights(a, ia_stream(), &ga, perm.data_ptr<int>(), cursor.data_ptr<int>(), (int)n, incp));
+  }
   py::list lb, lt;
   for (size_t i = 0; i < ws.size(); ++i) {
     lb.append(wbs[i]);
@@ -454,8 +471,8 @@ void register_conv(py::module& m) {
         py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0);
   m.def("conv_fwd_pair", &conv_fwd_pair, "two same-shape convs (expert + learner) in one launch");
   m.def("cnn_fc_pair", &cnn_fc_pair, "two same-shape cnn_fc layers in one launch");
-  m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts, one launch", py::arg("ws"),
-        py::arg("want_t"), py::arg("t_hwc") = std::vector<bool>{});
+  m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts (+ a minibatch gather), one launch",
+        py::arg("ws"), py::arg("want_t"), py::arg("t_hwc") = std::vector<bool>{}, py::arg("gather") = py::none());
   m.def("fc_backward", &fc_backward, "NatureCNN feature-layer backward (dW torch layout, db, dX NHWC bf16)", py::arg("x"),
         py::arg("dh"), py::arg("h"), py::arg("wt"), py::arg("C"), py::arg("need_dx"), py::arg("dW_out") = py::none(),
         py::arg("db_out") = py::none(), py::arg("mask_dx") = false);

@@ -434,10 +434,12 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
   return outs;
 }
 
-// rows perm[*cursor * n + r] of every source into the caller-owned dst tensors (one launch,
-// no host arguments per minibatch: HIP-graph epochs)
-void gather_rows_cursor(std::vector<torch::Tensor> srcs, torch::Tensor perm, torch::Tensor cursor, int64_t n,
-                        std::vector<torch::Tensor> dst, c10::optional<torch::Tensor> inc) {
+}  // namespace
+
+// (external: conv.cpp's weight-packing launch carries the same gather)
+ia::GatherArgs gather_cursor_args(const std::vector<torch::Tensor>& srcs, const torch::Tensor& perm,
+                                  const torch::Tensor& cursor, int64_t n, const std::vector<torch::Tensor>& dst,
+                                  const c10::optional<torch::Tensor>& inc, float** incp) {
   TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= ia::kGatherMax && dst.size() == srcs.size(), "gather_rows_cursor: 1..8 fields");
   IA_CHECK_CUDA(perm);
   IA_CHECK_CONTIG(perm);
@@ -459,12 +461,23 @@ void gather_rows_cursor(std::vector<torch::Tensor> srcs, torch::Tensor perm, tor
                 "gather_rows_cursor: dst ", i, " shape / dtype / device");
     a.f[i] = ia::GatherField{t.data_ptr(), o.data_ptr(), rows ? (int64_t)(t.nbytes() / rows) : 0, rows};
   }
-  float* incp = nullptr;
+  *incp = nullptr;
   if (inc && inc->defined()) {
     IA_CHECK_GPU_F32(*inc);
     TORCH_CHECK(inc->numel() == 1, "gather_rows_cursor: inc must be a 1-element fp32 tensor");
-    incp = inc->data_ptr<float>();
+    *incp = inc->data_ptr<float>();
   }
+  return a;
+}
+
+namespace {
+
+// rows perm[*cursor * n + r] of every source into the caller-owned dst tensors (one launch,
+// no host arguments per minibatch: HIP-graph epochs)
+void gather_rows_cursor(std::vector<torch::Tensor> srcs, torch::Tensor perm, torch::Tensor cursor, int64_t n,
+                        std::vector<torch::Tensor> dst, c10::optional<torch::Tensor> inc) {
+  float* incp = nullptr;
+  const ia::GatherArgs a = gather_cursor_args(srcs, perm, cursor, n, dst, inc, &incp);
   IA_HIP_CHECK(ia::gather_rows_cursor(a, perm.data_ptr<int>(), cursor.data_ptr<int>(), (int)n, ia_stream(), incp));
 }
 

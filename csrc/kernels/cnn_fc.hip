@@ -122,8 +122,9 @@ constexpr int kChTilesW = 13;    // tiles per wave (parity split)
 constexpr int kChXIt = 4;        // X loads per thread per 32-row chunk: ceil(32 * 52 / 512)
 constexpr int kChHwSplit = 4;  // HW position groups per (channel group, n block): 256 blocks at NatureCNN (64 before; BC step -1 us, profiles/r6_bc_step.md)
 
-// (bx, by, bz): channel group, n block, position group (the kernel's blockIdx, or decoded from a
-// paired launch's block index)
+// (bx, by, bz): channel group, n block, position group. (A one-launch FC backward -- these blocks
+// plus the data gradient forming its dZ from dH / Hout -- measured slower: 25 us vs 12 + 6 for
+// the two launches, call W, profiles/r6_bc_step.md.)
 __device__ __forceinline__ void fc_wgrad_ch_body(const bf16* __restrict__ X, const float* __restrict__ dH,
                                                  const float* __restrict__ Hout, float* __restrict__ dW,
                                                  float* __restrict__ db, bf16* __restrict__ dZb, int M, int K, int NH,
@@ -202,22 +203,7 @@ __global__ __launch_bounds__(512) void fc_wgrad_ch_kernel(const bf16* __restrict
 
 // One wave = 16 rows x 16 NHWC columns; the n loop is issued 4 k-steps (8 loads) at a time
 // so the L2 round trips overlap (the wave reads 16 KB of Wt).
-// FROM_H: the dZ operand formed from dH / Hout (fp32, ReLU mask) as the weight-gradient blocks form
-// it -- bf16 of the same value as their dZb, so no ordering against them (the paired launch)
-__device__ __forceinline__ bf16x8 relu_dz8(const float* __restrict__ dH, const float* __restrict__ Hout, size_t o) {
-  const float4 d0 = *reinterpret_cast<const float4*>(dH + o), d1 = *reinterpret_cast<const float4*>(dH + o + 4);
-  const float4 h0 = *reinterpret_cast<const float4*>(Hout + o), h1 = *reinterpret_cast<const float4*>(Hout + o + 4);
-  bf16x8 v;
-  v[0] = (bf16)(h0.x > 0.f ? d0.x : 0.f); v[1] = (bf16)(h0.y > 0.f ? d0.y : 0.f);
-  v[2] = (bf16)(h0.z > 0.f ? d0.z : 0.f); v[3] = (bf16)(h0.w > 0.f ? d0.w : 0.f);
-  v[4] = (bf16)(h1.x > 0.f ? d1.x : 0.f); v[5] = (bf16)(h1.y > 0.f ? d1.y : 0.f);
-  v[6] = (bf16)(h1.z > 0.f ? d1.z : 0.f); v[7] = (bf16)(h1.w > 0.f ? d1.w : 0.f);
-  return v;
-}
-
-template <bool FROM_H>
-__device__ __forceinline__ void fc_dgrad_body(const bf16* __restrict__ dZb, const float* __restrict__ dH,
-                                              const float* __restrict__ Hout, const bf16* __restrict__ Wt,
+__device__ __forceinline__ void fc_dgrad_body(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
                                               bf16* __restrict__ dX, int M, int K, int NH, const bf16* __restrict__ Xm,
                                               int wave) {
   const int l = threadIdx.x & 63;
@@ -229,7 +215,7 @@ __device__ __forceinline__ void fc_dgrad_body(const bf16* __restrict__ dZb, cons
   const bool mv = m < M;
   const int nq = (l >> 4) * 8;
   const size_t ao = (size_t)(mv ? m : 0) * NH + nq;
-  const bf16* ar = FROM_H ? nullptr : dZb + ao;
+  const bf16* ar = dZb + ao;
   const bf16* br = Wt + (size_t)(k0 + (l & 15)) * NH + nq;
   f32x4 acc = zero4();
   for (int n0 = 0; n0 < NH; n0 += 128) {
@@ -237,8 +223,7 @@ __device__ __forceinline__ void fc_dgrad_body(const bf16* __restrict__ dZb, cons
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool ok = n0 + 32 * u < NH;
-      if constexpr (FROM_H) a[u] = ok ? relu_dz8(dH, Hout, ao + n0 + 32 * u) : bf16x8{};
-      else a[u] = ok ? *reinterpret_cast<const bf16x8*>(ar + n0 + 32 * u) : bf16x8{};
+      a[u] = ok ? *reinterpret_cast<const bf16x8*>(ar + n0 + 32 * u) : bf16x8{};
       b[u] = ok ? *reinterpret_cast<const bf16x8*>(br + n0 + 32 * u) : bf16x8{};
     }
 #pragma unroll
@@ -265,25 +250,7 @@ __device__ __forceinline__ void fc_dgrad_body(const bf16* __restrict__ dZb, cons
 __global__ __launch_bounds__(256) void fc_dgrad_kernel(const bf16* __restrict__ dZb, const bf16* __restrict__ Wt,
                                                        bf16* __restrict__ dX, int M, int K, int NH,
                                                        const bf16* __restrict__ Xm) {
-  fc_dgrad_body<false>(dZb, nullptr, nullptr, Wt, dX, M, K, NH, Xm, blockIdx.x * 4 + (threadIdx.x >> 6));
-}
-
-// The FC backward in ONE launch (BC-size batches): blocks [0, nwb) the channel-aligned weight
-// gradient (decoded (bx, by, bz)), the rest the data gradient, 8 waves = 8 tiles per block. The
-// two read the same dH / Hout and neither feeds the other (the data gradient forms its bf16 dZ
-// operand itself): one launch, and the ~5 us dispatch of the second, fewer per step.
-__global__ __launch_bounds__(512) void fc_back_pair_kernel(const bf16* __restrict__ X, const float* __restrict__ dH,
-                                                           const float* __restrict__ Hout, float* __restrict__ dW,
-                                                           float* __restrict__ db, const bf16* __restrict__ Wt,
-                                                           bf16* __restrict__ dX, int M, int K, int NH, int C, int HW,
-                                                           int hws, int gx, int gz, int nwb, const bf16* __restrict__ Xm) {
-  const int b = blockIdx.x;
-  if (b < nwb) {
-    const int bx = b % gx, r = b / gx, bz = r % gz, by = r / gz;
-    fc_wgrad_ch_body(X, dH, Hout, dW, db, nullptr, M, K, NH, C, HW, hws, bx, by, bz);
-  } else {
-    fc_dgrad_body<true>(nullptr, dH, Hout, Wt, dX, M, K, NH, Xm, (b - nwb) * 8 + (threadIdx.x >> 6));
-  }
+  fc_dgrad_body(dZb, Wt, dX, M, K, NH, Xm, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
 
 }  // namespace
@@ -301,14 +268,6 @@ hipError_t fc_backward(const void* X, const float* dH, const float* Hout, const 
   // C / kChG x NH / 64 = 64 of NatureCNN, each with fewer column tiles)
   const int hws = (HW + kChHwSplit - 1) / kChHwSplit;
   const int gx = C / kChG, gy = NH / 64, gz = (HW + hws - 1) / hws;
-  if (ch && dX && M <= 64) {  // BC-size batches: both halves in one launch
-    const int nwb = gx * gy * gz;
-    const int dblocks = (((M + 15) / 16) * (K / 16) + 7) / 8;
-    hipLaunchKernelGGL(fc_back_pair_kernel, dim3(nwb + dblocks), dim3(512), 0, s, static_cast<const bf16*>(X), dH, Hout,
-                       dW, db, static_cast<const bf16*>(Wt), static_cast<bf16*>(dX), M, K, NH, C, HW, hws, gx, gz, nwb,
-                       mask_dx ? static_cast<const bf16*>(X) : nullptr);
-    return hipGetLastError();
-  }
   if (ch)
     hipLaunchKernelGGL(fc_wgrad_ch_kernel, dim3(gx, gy, gz), dim3(512), 0, s,
                        static_cast<const bf16*>(X), dH, Hout, dW, db, static_cast<bf16*>(dZb), M, K, NH, C, HW, hws);

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ia/mfma.h"
+#include "gather_body.h"
 #include "launchers.h"
 
 namespace ia {
@@ -906,48 +907,132 @@ __device__ __forceinline__ void pack_wt_tile(const ConvPackLayer& L, int kt, int
   }
 }
 
-// Block ranges of one pack launch: per layer its forward-image tiles (tiles x N) then, after all
-// of those, its transpose tiles (kts x nts) -- exact counts, no idle blocks.
+// Row form (layers whose C x KH*KW fits one LDS image, e.g. all of NatureCNN): one block per
+// output channel n transposes the whole [C][taps] row to [taps][C] (the FC: 3136 elements, 12
+// loads per thread in flight), and the t_hwc transpose runs one block per (channel, 64 n): 64
+// source rows of `taps` floats -> taps rows of 64 bf16. ~1250 blocks for the NatureCNN step
+// instead of ~4400 32x32 tiles (each a load -> barrier -> store round trip). The LDS row stride
+// is odd (taps | 1), so the column-order reads are bank-conflict free.
+constexpr int kPackRowLds = 4224;  // floats: C * stride (forward image) or 64 * stride (t_hwc)
+constexpr int kPackRowIt = 17;     // loads per thread: ceil(4224 / 256)
+
+__device__ __forceinline__ int pack_stride(int taps) { return taps | 1; }
+
+__device__ __forceinline__ void pack_wb_row(const ConvPackLayer& L, int n, float* t) {
+  const int taps = L.KH * L.KW, C = L.C, K = C * taps, st = pack_stride(taps);
+  const float* src = L.w + (size_t)n * K;
+  float v[kPackRowIt];
+#pragma unroll
+  for (int u = 0; u < kPackRowIt; ++u) {  // all loads in flight before the LDS stores
+    const int i = threadIdx.x + 256 * u;
+    v[u] = i < K ? src[i] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kPackRowIt; ++u) {  // src [c][tap] -> t[c * st + tap]
+    const int i = threadIdx.x + 256 * u;
+    if (i < K) {
+      const int c = i / taps;
+      t[c * st + i - c * taps] = v[u];
+    }
+  }
+  __syncthreads();
+  bf16* dst = static_cast<bf16*>(L.wb) + (size_t)n * K;
+  for (int i = threadIdx.x; i < K; i += 256) {  // dst [tap][c], coalesced along c
+    const int p = i / C, c = i - p * C;
+    dst[i] = (bf16)t[c * st + p];
+  }
+}
+
+__device__ __forceinline__ void pack_wt_row(const ConvPackLayer& L, int c, int nt, float* t) {
+  const int taps = L.KH * L.KW, C = L.C, N = L.N, st = pack_stride(taps), n0 = nt * 64;
+  const int cnt = 64 * taps;
+  float v[kPackRowIt];
+#pragma unroll
+  for (int u = 0; u < kPackRowIt; ++u) {  // 64 source rows w[n][c][0..taps)
+    const int i = threadIdx.x + 256 * u;
+    const int nl = i / taps, p = i - nl * taps;
+    v[u] = (i < cnt && n0 + nl < N) ? L.w[((size_t)(n0 + nl) * C + c) * taps + p] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kPackRowIt; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i < cnt) {
+      const int nl = i / taps;
+      t[nl * st + i - nl * taps] = v[u];
+    }
+  }
+  __syncthreads();
+  bf16* dst = static_cast<bf16*>(L.wt);
+  for (int i = threadIdx.x; i < cnt; i += 256) {  // dst [tap][c][n0 .. n0 + 64), coalesced along n
+    const int p = i >> 6, nl = i & 63;
+    if (n0 + nl < N) dst[((size_t)p * C + c) * N + n0 + nl] = (bf16)t[nl * st + p];
+  }
+}
+
+// Block ranges of one pack launch: per layer its forward-image tiles (tiles x N; row form: N)
+// then, after all of those, its transpose tiles (kts x nts) -- exact counts, no idle blocks.
 struct PackPlan {
   int off[2 * kMaxPack + 1];  // block offsets: [0, n) forward images, [n, 2n) transposes
   int tiles[kMaxPack], kts[kMaxPack];
+  int row[kMaxPack];  // forward image in row form; t_hwc transpose in row form
 };
 
-__global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a, PackPlan pl) {
-  __shared__ float t[32][33];
+// Blocks past the packing ranges: the BC step's minibatch gather (gather_body.h), ga.k fields x gx
+// blocks -- independent of the packing, so it rides on this launch instead of a dispatch of its own.
+__global__ __launch_bounds__(256) void conv_pack_kernel(ConvPackArgs a, PackPlan pl, GatherArgs ga, const int* perm,
+                                                        const int* cursor, int gn, float* inc, int gx) {
+  __shared__ float t[kPackRowLds];
   const int b = blockIdx.x;
+  if (b >= pl.off[2 * a.n]) {
+    const int r = b - pl.off[2 * a.n];
+    gather_rows_cursor_block(ga, perm, cursor, gn, inc, r % gx, r / gx, gx);
+    return;
+  }
   int j = 0;
   while (j + 1 < 2 * a.n && b >= pl.off[j + 1]) ++j;  // (uniform)
   const int r = b - pl.off[j];
-  if (j < a.n)
-    pack_wb_tile(a.layer[j], r % pl.tiles[j], r / pl.tiles[j], t);
-  else
-    pack_wt_tile(a.layer[j - a.n], r % pl.kts[j - a.n], r / pl.kts[j - a.n], t);
+  float(*t32)[33] = reinterpret_cast<float(*)[33]>(t);
+  if (j < a.n) {
+    if (pl.row[j]) pack_wb_row(a.layer[j], r, t);
+    else pack_wb_tile(a.layer[j], r % pl.tiles[j], r / pl.tiles[j], t32);
+  } else {
+    const int l = j - a.n;
+    if (pl.row[l] && a.layer[l].t_hwc) pack_wt_row(a.layer[l], r % pl.kts[l], r / pl.kts[l], t);
+    else pack_wt_tile(a.layer[l], r % pl.kts[l], r / pl.kts[l], t32);
+  }
 }
 
 }  // namespace
 
-hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s) {
+hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s, const GatherArgs* ga, const int* perm, const int* cursor,
+                             int gn, float* inc) {
   if (a.n <= 0) return hipSuccess;
   if (a.n > kMaxPack) return hipErrorInvalidValue;
+  const bool gather = ga != nullptr && ga->k > 0 && gn > 0;
+  if (gather && ga->k > kGatherMax) return hipErrorInvalidValue;
   PackPlan pl{};
   int total = 0;
-  for (int i = 0; i < a.n; ++i) {  // forward images: (channel x tap) tiles per output channel
+  for (int i = 0; i < a.n; ++i) {  // forward images: (channel x tap) tiles per output channel, or rows
     const ConvPackLayer& L = a.layer[i];
-    const int taps = L.KH * L.KW;
-    pl.tiles[i] = ((taps + 31) / 32) * ((L.C + 31) / 32);
+    const int taps = L.KH * L.KW, st = taps | 1;
+    pl.row[i] = L.C * st <= kPackRowLds && taps <= 64;  // (t_hwc row form: 64 x st floats)
+    pl.tiles[i] = pl.row[i] ? 1 : ((taps + 31) / 32) * ((L.C + 31) / 32);
     pl.off[i] = total;
     total += pl.tiles[i] * L.N;
   }
   for (int i = 0; i < a.n; ++i) {  // transposes: k tiles (or channel x 32-tap tiles, t_hwc) x n tiles
     const ConvPackLayer& L = a.layer[i];
     const int taps = L.KH * L.KW;
-    pl.kts[i] = L.t_hwc ? L.C * ((taps + 31) / 32) : (L.C * taps + 31) / 32;
+    const bool row = pl.row[i] && L.t_hwc;  // one block per (channel, 64 n)
+    pl.kts[i] = row ? L.C : L.t_hwc ? L.C * ((taps + 31) / 32) : (L.C * taps + 31) / 32;
     pl.off[a.n + i] = total;
-    if (L.wt) total += pl.kts[i] * ((L.N + 31) / 32);
+    if (L.wt) total += pl.kts[i] * (row ? (L.N + 63) / 64 : (L.N + 31) / 32);
   }
   pl.off[2 * a.n] = total;
-  hipLaunchKernelGGL(conv_pack_kernel, dim3(total), dim3(256), 0, s, a, pl);
+  const GatherArgs none{};
+  const int gx = gather ? gather_cursor_blocks(*ga, gn) : 1;
+  const int blocks = total + (gather ? gx * ga->k : 0);
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(blocks), dim3(256), 0, s, a, pl, gather ? *ga : none, perm, cursor, gn, inc, gx);
   return hipGetLastError();
 }
 

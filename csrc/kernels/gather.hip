@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gather_body.h"
 #include "launchers.h"
 
 namespace ia {
@@ -49,28 +50,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GatherArgs a, const in
 // a captured sequence of minibatch steps walks an epoch's order without host arguments.
 __global__ __launch_bounds__(256) void gather_rows_cursor_kernel(GatherArgs a, const int* __restrict__ perm,
                                                                  const int* __restrict__ cursor, int n, float* inc) {
-  if (inc && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *inc += 1.f;  // (nothing else here reads it)
-  const GatherField& f = a.f[blockIdx.y];
-  const int64_t rb = f.row_bytes;
-  const char* __restrict__ src = static_cast<const char*>(f.src);
-  char* __restrict__ dst = static_cast<char*>(f.dst);
-  const int* __restrict__ b = perm + (int64_t)(*cursor) * n;
-  const int vec = ((rb & 15) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) ? 16
-                  : ((rb & 3) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 3) == 0) ? 4 : 1;
-  const int64_t units = rb / vec;
-  const int64_t total = (int64_t)n * units;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / units, u = i - r * units;
-    const int64_t srow = b[r];
-    const bool ok = srow >= 0 && srow < f.rows;
-    if (vec == 16) {
-      reinterpret_cast<uint4*>(dst + r * rb)[u] = ok ? reinterpret_cast<const uint4*>(src + srow * rb)[u] : make_uint4(0, 0, 0, 0);
-    } else if (vec == 4) {
-      reinterpret_cast<uint32_t*>(dst + r * rb)[u] = ok ? reinterpret_cast<const uint32_t*>(src + srow * rb)[u] : 0u;
-    } else {
-      dst[r * rb + u] = ok ? src[srow * rb + u] : (char)0;
-    }
-  }
+  gather_rows_cursor_block(a, perm, cursor, n, inc, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // all[*cursor][0 .. n) = src[0 .. n), then ++*cursor (one block): per-step metrics of a graphed
@@ -87,13 +67,7 @@ __global__ void append_at_cursor_kernel(const float* __restrict__ src, float* __
 hipError_t gather_rows_cursor(const GatherArgs& a, const int* perm, const int* cursor, int n, hipStream_t s, float* inc) {
   if (n <= 0 || a.k <= 0) return hipSuccess;
   if (a.k > kGatherMax) return hipErrorInvalidValue;
-  int64_t most = 0;
-  for (int i = 0; i < a.k; ++i) {
-    const int64_t units = a.f[i].row_bytes / ((a.f[i].row_bytes & 15) == 0 ? 16 : 1);
-    most = units * n > most ? units * n : most;
-  }
-  int64_t bx = (most + 255) / 256;
-  bx = bx < 1 ? 1 : (bx > 1024 ? 1024 : bx);
+  const int bx = gather_cursor_blocks(a, n);
   hipLaunchKernelGGL(gather_rows_cursor_kernel, dim3((unsigned)bx, a.k), dim3(256), 0, s, a, perm, cursor, n, inc);
   return hipGetLastError();
 }

@@ -422,7 +422,10 @@ struct ConvPackArgs {
   ConvPackLayer layer[kMaxPack];
   int n;
 };
-hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s);
+struct GatherArgs;
+// ga (optional): a cursor-indexed row gather (gather_rows_cursor) run in the same launch
+hipError_t conv_pack_weights(const ConvPackArgs& a, hipStream_t s, const GatherArgs* ga = nullptr, const int* perm = nullptr,
+                             const int* cursor = nullptr, int gn = 0, float* inc = nullptr);
 // two same-geometry unpadded convs (+ bias + ReLU) in one launch: X/W/bias/Y of set z
 struct ConvPair {
   const void* X[2];

@@ -490,7 +490,7 @@ class _DPFusedStep:
 class _DeviceEpochRunner:
     """BC epochs over a device demonstration aggregate as HIP-graph replays of ``K`` minibatch
     steps each: per step ``gather_rows_cursor`` (rows ``perm[cursor * B ..]`` into the
-    aggregate's persistent batch buffers), the fused NatureCNN step (``ops/bc_cnn.py``), the
+    aggregate's persistent batch buffers; run inside the step's weight-packing launch), the fused NatureCNN step (``ops/bc_cnn.py``), the
     optimizer step and ``append_at_cursor`` (the step's metrics into their row, cursor + 1).
     Per epoch the host only draws the permutation (one launch) and replays; the reference loop's
     per-batch observable effects are kept: rollout statistics + logging at every
@@ -499,6 +499,9 @@ class _DeviceEpochRunner:
     per-minibatch loop, so the result is bitwise the eager-graph path's."""
 
     K = 16  # default largest graph (minibatch steps per replay); IMITATION_AMD_BC_GRAPH_K overrides
+    # the minibatch gather inside the fused step's weight-packing launch (False: its own launch;
+    # test hook / A/B, bitwise the same)
+    fuse_gather = True
 
     def __init__(self, trainer: "_BCBase", loader, graphed):
         self.trainer, self.loader, self.graphed = trainer, loader, graphed
@@ -587,11 +590,17 @@ class _DeviceEpochRunner:
         C = self._f.C
         bufs = self.agg.batch_buffers(self.B)
         opt = self.trainer.optimizer
+        gather = None
+        if self._comm is not None or self._fold:
+            # the minibatch gather and the step counter's add: inside the weight-packing launch, or
+            # (``fuse_gather`` off, the test hook) a launch of its own -- bitwise the same rows
+            gather = ([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs, opt.step_counter())
+            if not self.fuse_gather:
+                C.gather_rows_cursor(*gather[:5], inc=gather[5])
+                gather = None
         if self._comm is not None:
             # data parallel, graph-resident: the bucket all-reduce is a captured one-shot kernel
             # between the fused step and Adam (reference hook point bc.py:464-466)
-            C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs,
-                                 inc=opt.step_counter())
             fc, rest = self._dp_ranges()
             main = th.cuda.current_stream()
             side = self._dp_side
@@ -603,18 +612,16 @@ class _DeviceEpochRunner:
                 with th.cuda.stream(side):
                     self._dp_allreduce(fc)
 
-            self._f(bufs[0], bufs[1], after_fc=after_fc)
+            self._f(bufs[0], bufs[1], after_fc=after_fc, gather=gather)
             # (the one-shot calls of a rank share one staging region: the rest waits for the FC part)
             main.wait_stream(side)
             self._dp_allreduce(rest)
             opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor))
             return
         if self._fold:
-            # the step counter's add rides on the gather launch, the metrics append on Adam's:
-            # 17 launches per step instead of 19 (same arithmetic)
-            C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs,
-                                 inc=opt.step_counter())
-            self._f(bufs[0], bufs[1])
+            # the gather rides on the weight-packing launch, the metrics append on Adam's: 13 launches
+            # per step (same arithmetic)
+            self._f(bufs[0], bufs[1], gather=gather)
             opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor))
             return
         C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs)

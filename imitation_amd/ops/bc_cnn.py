@@ -109,10 +109,14 @@ class FusedCnnBCStep:
             return None
         return FusedCnnBCStep(policy, optimizer, ent_weight, l2_weight)
 
-    def __call__(self, obs: th.Tensor, acts: th.Tensor, after_fc=None) -> th.Tensor:
+    def __call__(self, obs: th.Tensor, acts: th.Tensor, after_fc=None, gather=None) -> th.Tensor:
         """``after_fc``: called (no arguments) once the FC layer's gradients are in the bucket and
         before the conv backward -- the data-parallel epoch starts the FC bucket's all-reduce there,
-        on a side stream, so it overlaps the conv backward."""
+        on a side stream, so it overlaps the conv backward. ``gather``: ``(srcs, perm, cursor, n,
+        [obs, acts], step_counter)`` of the minibatch's ``gather_rows_cursor``, run inside the
+        weight-packing launch (one dispatch fewer per step); ``obs`` / ``acts`` are its outputs."""
+        if gather is not None and not (obs.is_contiguous() and acts.is_contiguous()):
+            raise ValueError("the fused gather writes obs / acts in place: they must be contiguous")
         C = self.C
         convs, lin, head = self.convs, self.lin, self.head
         n = len(convs)
@@ -124,7 +128,7 @@ class FusedCnnBCStep:
         C3, NH = convs[-1].out_channels, lin.out_features
         with th.no_grad():
             wsrc = [c.weight.detach() for c in convs] + [lin.weight.detach().view(NH, C3, H, W)]
-            wbs, wts = C.conv_pack_weights(wsrc, [i > 0 for i in range(n)] + [True], [False] * n + [True])
+            wbs, wts = C.conv_pack_weights(wsrc, [i > 0 for i in range(n)] + [True], [False] * n + [True], gather)
             hs: List[th.Tensor] = []
             h = x
             for i, c in enumerate(convs):

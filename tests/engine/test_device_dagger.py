@@ -202,15 +202,16 @@ def test_device_rollout_stats_match_host_keys(tmp_path):
 
 
 @gpu
-@pytest.mark.parametrize("n_epochs,n_batches,log_interval,kmax",
-                         [(2, None, 3, "16"), (None, 11, 4, "5"), (None, 7, 500, "16"), (3, None, 500, "3"),
-                          (3, None, 4, "2")])
-def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batches, log_interval, kmax):
+@pytest.mark.parametrize("n_epochs,n_batches,log_interval,kmax,fuse",
+                         [(2, None, 3, "16", True), (None, 11, 4, "5", True), (None, 7, 500, "16", True),
+                          (3, None, 500, "3", True), (3, None, 4, "2", True), (2, None, 3, "16", False)])
+def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batches, log_interval, kmax, fuse):
     """BC over a device demonstration aggregate (DAgger's device collector) with whole runs of
     minibatches per HIP-graph replay (algorithms/bc.py ``_DeviceEpochRunner``, graph sizes kmax then
     powers of two below it): the same batches, kernels and order as the per-minibatch graphed loop,
     so the parameters, Adam state and every logged metric are bitwise equal; the epoch-end
-    callbacks and the n_batches cut-off match."""
+    callbacks and the n_batches cut-off match. ``fuse``: the minibatch gather inside the weight-
+    packing launch (the default) or a launch of its own."""
     from imitation_amd.algorithms import bc
     from imitation_amd.engine.dagger import DeviceDemoAggregate, DeviceTransitionsLoader
     from imitation_amd.rl.policies import ActorCriticCnnPolicy
@@ -224,6 +225,7 @@ def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batc
     acts = th.randint(0, int(venv.action_space.n), (n_rows,), generator=g, device="cuda")
     runs = []
     monkeypatch.setenv("IMITATION_AMD_BC_GRAPH_K", kmax)
+    monkeypatch.setattr(bc._DeviceEpochRunner, "fuse_gather", fuse)
     for mode in ("0", "1"):
         monkeypatch.setenv("IMITATION_AMD_BC_EPOCH_GRAPH", mode)
         th.manual_seed(11)

@@ -326,14 +326,17 @@ def test_conv_backward_pair_is_bitwise_the_two_launches(monkeypatch, B, C, N, KH
 @pytest.mark.gpu
 def test_conv_pack_weights_layouts_in_one_launch():
     """conv_pack_weights (forward images and transposes in ONE launch) == the torch permutes of the
-    bf16-rounded weights, for the NatureCNN layers and its FC weight (t_hwc) packed together."""
+    bf16-rounded weights, for the NatureCNN layers and its FC weight (t_hwc) packed together (row
+    form: one block per output channel / per (channel, 64 n)), and for layers too wide for the row
+    form's LDS image (C x KH*KW > 4224: the 32 x 32 tiles) and an N that is not a multiple of 64."""
     from imitation_amd import ops
 
     C = ops.native()
     g = th.Generator().manual_seed(5)
-    shapes = [(32, 4, 8, 8), (64, 32, 4, 4), (64, 64, 3, 3), (512, 64, 7, 7)]
+    shapes = [(32, 4, 8, 8), (64, 32, 4, 4), (64, 64, 3, 3), (512, 64, 7, 7), (48, 256, 5, 5), (80, 160, 5, 5),
+              (96, 3, 9, 9)]
     ws = [th.randn(*s, generator=g).cuda() for s in shapes]
-    want_t, t_hwc = [False, True, True, True], [False, False, False, True]
+    want_t, t_hwc = [False, True, True, True, True, True, True], [False, False, False, True, False, True, True]
     wbs, wts = C.conv_pack_weights(ws, want_t, t_hwc)
     for w, wb, wt, t, hwc in zip(ws, wbs, wts, want_t, t_hwc):
         wr = w.to(th.bfloat16)

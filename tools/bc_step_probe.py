@@ -1,4 +1,5 @@
-"""BC minibatch steps only (NatureCNN ActorCriticCnnPolicy, B=32, graphed), for a kernel trace."""
+"""BC minibatch steps only (NatureCNN ActorCriticCnnPolicy, B=32, graphed), for a kernel trace.
+``--sep-gather``: the minibatch gather as a launch of its own (A/B of the fused gather)."""
 import os
 import sys
 import time
@@ -16,6 +17,8 @@ def main():
     from imitation_amd.rl.policies import ActorCriticCnnPolicy
     from imitation_amd.util import logger
 
+    if "--sep-gather" in sys.argv:
+        bc._DeviceEpochRunner.fuse_gather = False
     obs_space, act_space = native_spaces("PongNoFrameskip-v4")
     pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
     agg = DeviceDemoAggregate("cuda")
@@ -29,7 +32,8 @@ def main():
     t0 = time.perf_counter()
     bct.train(**kw)
     th.cuda.synchronize()
-    print(f"BC step B=32: {1e3 * (time.perf_counter() - t0) / 100:.3f} ms/batch", flush=True)
+    tag = " (separate gather)" if "--sep-gather" in sys.argv else ""
+    print(f"BC step B=32{tag}: {1e3 * (time.perf_counter() - t0) / 100:.3f} ms/batch", flush=True)
 
 
 if __name__ == "__main__":
