@@ -19,11 +19,19 @@ inline hipStream_t ia_stream() { return c10::hip::getCurrentHIPStream().stream()
 
 namespace ia {
 struct GatherArgs;
+struct ConvReduceMulti;
 }
 // (kernels.cpp) the checked GatherArgs of a cursor-indexed row gather; *incp: the step counter or nullptr
 ia::GatherArgs gather_cursor_args(const std::vector<torch::Tensor>& srcs, const torch::Tensor& perm,
                                   const torch::Tensor& cursor, int64_t n, const std::vector<torch::Tensor>& dst,
                                   const c10::optional<torch::Tensor>& inc, float** incp);
+
+// (conv.cpp) the checked ConvReduceMulti of conv_reduce_multi's arguments
+ia::ConvReduceMulti conv_reduce_args(const std::vector<torch::Tensor>& xs, const std::vector<torch::Tensor>& dys,
+                                     const std::vector<int64_t>& KHs, const std::vector<int64_t>& KWs,
+                                     const std::vector<int64_t>& strides, const std::vector<int64_t>& pads,
+                                     const std::vector<torch::Tensor>& slabs, const std::vector<torch::Tensor>& dWs,
+                                     const std::vector<torch::Tensor>& dbs);
 
 void register_envs(py::module& m);
 void register_kernels(py::module& m);

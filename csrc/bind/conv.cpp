@@ -94,11 +94,16 @@ torch::Tensor conv_wgrad_partials(torch::Tensor x, torch::Tensor dy, torch::Tens
   return slab;
 }
 
+}  // namespace
+
 // every layer's deferred reduction (slab of conv_wgrad_partials) into dW [N, C, KH, KW] / db [N]
-// slots, one launch; geometry from the same x / dy / kernel / stride / pad as the partials call
-void conv_reduce_multi(std::vector<torch::Tensor> xs, std::vector<torch::Tensor> dys, std::vector<int64_t> KHs,
-                       std::vector<int64_t> KWs, std::vector<int64_t> strides, std::vector<int64_t> pads,
-                       std::vector<torch::Tensor> slabs, std::vector<torch::Tensor> dWs, std::vector<torch::Tensor> dbs) {
+// slots; geometry from the same x / dy / kernel / stride / pad as the partials call. (External:
+// the fused Adam launch takes the same reductions, kernels.cpp.)
+ia::ConvReduceMulti conv_reduce_args(const std::vector<torch::Tensor>& xs, const std::vector<torch::Tensor>& dys,
+                                     const std::vector<int64_t>& KHs, const std::vector<int64_t>& KWs,
+                                     const std::vector<int64_t>& strides, const std::vector<int64_t>& pads,
+                                     const std::vector<torch::Tensor>& slabs, const std::vector<torch::Tensor>& dWs,
+                                     const std::vector<torch::Tensor>& dbs) {
   const size_t n = xs.size();
   TORCH_CHECK(n > 0 && n <= (size_t)ia::kMaxPack && dys.size() == n && KHs.size() == n && KWs.size() == n &&
                   strides.size() == n && pads.size() == n && slabs.size() == n && dWs.size() == n && dbs.size() == n,
@@ -110,8 +115,6 @@ void conv_reduce_multi(std::vector<torch::Tensor> xs, std::vector<torch::Tensor>
     IA_CHECK_GPU_F32(slabs[l]);
     IA_CHECK_GPU_F32(dWs[l]);
     IA_CHECK_GPU_F32(dbs[l]);
-    IA_CHECK_CONTIG(dWs[l]);
-    IA_CHECK_CONTIG(dbs[l]);
     TORCH_CHECK((size_t)slabs[l].numel() >= ia::conv_wgrad_slab_floats(g), "conv_reduce_multi: slab size");
     TORCH_CHECK(dWs[l].numel() == (int64_t)g.N * g.C * g.KH * g.KW && dbs[l].numel() == g.N, "conv_reduce_multi: dW / db");
     r.g[l] = g;
@@ -119,6 +122,15 @@ void conv_reduce_multi(std::vector<torch::Tensor> xs, std::vector<torch::Tensor>
     r.dW[l] = dWs[l].data_ptr<float>();
     r.db[l] = dbs[l].data_ptr<float>();
   }
+  return r;
+}
+
+namespace {
+
+void conv_reduce_multi(std::vector<torch::Tensor> xs, std::vector<torch::Tensor> dys, std::vector<int64_t> KHs,
+                       std::vector<int64_t> KWs, std::vector<int64_t> strides, std::vector<int64_t> pads,
+                       std::vector<torch::Tensor> slabs, std::vector<torch::Tensor> dWs, std::vector<torch::Tensor> dbs) {
+  const ia::ConvReduceMulti r = conv_reduce_args(xs, dys, KHs, KWs, strides, pads, slabs, dWs, dbs);
   IA_HIP_CHECK3(ia::conv_reduce_multi(r, ia_stream()));
 }
 

@@ -201,7 +201,7 @@ void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg,
                torch::Tensor step, double lr, double beta1, double beta2, double eps, double weight_decay, bool decoupled,
                bool maximize, bool zero_grad, c10::optional<torch::Tensor> step_cnt,
                c10::optional<torch::Tensor> append_src, c10::optional<torch::Tensor> append_all,
-               c10::optional<torch::Tensor> append_cursor) {
+               c10::optional<torch::Tensor> append_cursor, py::object reduce) {
   for (auto* t : {&params, &grads, &exp_avg, &exp_avg_sq}) {
     IA_CHECK_GPU_F32(*t);
     TORCH_CHECK(t->numel() == params.numel(), "flat Adam buffers must have equal sizes");
@@ -243,6 +243,17 @@ void adam_flat(torch::Tensor params, torch::Tensor grads, torch::Tensor exp_avg,
     a.app_all = all.data_ptr<float>();
     a.app_cursor = cur.data_ptr<int>();
     a.app_n = (int)src.numel();
+  }
+  if (!reduce.is_none()) {  // conv_reduce_multi's arguments: those reductions run in this launch
+    const auto t = reduce.cast<py::tuple>();
+    TORCH_CHECK(t.size() == 9, "reduce: the 9 conv_reduce_multi argument lists");
+    const ia::ConvReduceMulti r = conv_reduce_args(
+        t[0].cast<std::vector<torch::Tensor>>(), t[1].cast<std::vector<torch::Tensor>>(), t[2].cast<std::vector<int64_t>>(),
+        t[3].cast<std::vector<int64_t>>(), t[4].cast<std::vector<int64_t>>(), t[5].cast<std::vector<int64_t>>(),
+        t[6].cast<std::vector<torch::Tensor>>(), t[7].cast<std::vector<torch::Tensor>>(),
+        t[8].cast<std::vector<torch::Tensor>>());
+    IA_HIP_CHECK(ia::adam_flat(a, ia_stream(), &r));
+    return;
   }
   IA_HIP_CHECK(ia::adam_flat(a, ia_stream()));
 }
@@ -642,7 +653,8 @@ void register_kernels(py::module& m) {
   m.def("adam_flat", &adam_flat, py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"),
         py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"),
         py::arg("decoupled"), py::arg("maximize"), py::arg("zero_grad"), py::arg("step_cnt") = py::none(),
-        py::arg("append_src") = py::none(), py::arg("append_all") = py::none(), py::arg("append_cursor") = py::none());
+        py::arg("append_src") = py::none(), py::arg("append_all") = py::none(), py::arg("append_cursor") = py::none(),
+        py::arg("reduce") = py::none());
   m.def("random_permutations", &random_permutations, py::arg("E"), py::arg("n"), py::arg("seed"), py::arg("device"));
   m.def("running_norm", &running_norm, py::arg("x"), py::arg("mean"), py::arg("var"), py::arg("count"), py::arg("eps"),
         py::arg("update"), py::arg("want_y"), py::arg("ema_inv_lr") = py::none(), py::arg("ema_num_batches") = py::none(),

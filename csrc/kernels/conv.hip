@@ -32,6 +32,7 @@
 
 #include "ia/mfma.h"
 #include "gather_body.h"
+#include "wgrad_reduce.h"
 #include "launchers.h"
 
 namespace ia {
@@ -665,34 +666,6 @@ __global__ __launch_bounds__(512) void conv_back_pair_kernel(const bf16* __restr
   }
 }
 
-// The 4 fixed-order accumulators of a slab column (accumulator j: blocks b = j mod 4 in order,
-// the tail blocks into s0). 16 loads are issued before their adds: the slabs of a BC step have
-// ~50 blocks, and 4 loads per round trip made the sum a chain of ~13 L2 round trips.
-__device__ __forceinline__ void slab_sum4(const float* __restrict__ slab, int nblk, int len, int i, float& s0, float& s1,
-                                          float& s2, float& s3) {
-  s0 = s1 = s2 = s3 = 0.f;
-  int b = 0;
-  for (; b + 15 < nblk; b += 16) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = slab[(size_t)(b + u) * len + i];
-#pragma unroll
-    for (int u = 0; u < 16; u += 4) {
-      s0 += v[u];
-      s1 += v[u + 1];
-      s2 += v[u + 2];
-      s3 += v[u + 3];
-    }
-  }
-  for (; b + 3 < nblk; b += 4) {
-    s0 += slab[(size_t)b * len + i];
-    s1 += slab[(size_t)(b + 1) * len + i];
-    s2 += slab[(size_t)(b + 2) * len + i];
-    s3 += slab[(size_t)(b + 3) * len + i];
-  }
-  for (; b < nblk; ++b) s0 += slab[(size_t)b * len + i];
-}
-
 // Fixed-order sum of the wgrad block partials: 4 independent accumulators (blocks b with
 // b % 4 == j) keep 4 loads in flight per thread, combined in a fixed order at the end.
 // The weight gradient is written in torch's [N][C][KH][KW] layout (GEMM column k = (kh, kw, c),
@@ -702,19 +675,11 @@ __global__ __launch_bounds__(256) void conv_reduce_kernel(const float* __restric
                                                           ConvGeo g) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
-  float s0, s1, s2, s3;
-  slab_sum4(slab, nblk, len, i, s0, s1, s2, s3);
-  const float s = (s0 + s1) + (s2 + s3);
-  if (i < nk) {
-    const int n = i / g.Kp, k = i - n * g.Kp;
-    const int taps = g.KH * g.KW;
-    if (k < taps * g.C) {
-      const int tap = k / g.C, c = k - tap * g.C;
-      dW[((size_t)n * g.C + c) * taps + tap] = s;
-    }
-  } else if (db) {
-    db[i - nk] = s;
-  }
+  (void)nk;
+  int wi, bi;
+  const float s = slab_column(slab, nblk, g, i, &wi, &bi);
+  if (wi >= 0) dW[wi] = s;
+  else if (bi >= 0 && db) db[bi] = s;
 }
 
 template <typename TIn>
@@ -822,27 +787,14 @@ hipError_t launch_wgrad(const TIn* X, const bf16* dY, const bf16* Y, float* slab
 __global__ __launch_bounds__(256) void conv_reduce_multi_kernel(ConvReduceMulti r) {
   const int l = blockIdx.y;
   const ConvGeo& g = r.g[l];
-  const int nblk = r.nblk[l];
   const int len = g.N * g.Kp + g.N;
-  if ((int)(blockIdx.x * 256) >= len) return;
-  // (same fixed-order body as conv_reduce_kernel)
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
-  const float* slab = r.slab[l];
-  float s0, s1, s2, s3;
-  slab_sum4(slab, nblk, len, i, s0, s1, s2, s3);
-  const float sum = (s0 + s1) + (s2 + s3);
-  const int nk = g.N * g.Kp;
-  if (i < nk) {
-    const int n = i / g.Kp, k = i - n * g.Kp;
-    const int taps = g.KH * g.KW;
-    if (k < taps * g.C) {
-      const int tap = k / g.C, c = k - tap * g.C;
-      r.dW[l][((size_t)n * g.C + c) * taps + tap] = sum;
-    }
-  } else if (r.db[l]) {
-    r.db[l][i - nk] = sum;
-  }
+  // (same fixed-order sum as conv_reduce_kernel, and as the Adam launch that folds it: optim.hip)
+  int wi, bi;
+  const float s = slab_column(r.slab[l], r.nblk[l], g, i, &wi, &bi);
+  if (wi >= 0) r.dW[l][wi] = s;
+  else if (bi >= 0 && r.db[l]) r.db[l][bi] = s;
 }
 
 // fp32 torch-layout conv weights [N][C][KH][KW] of up to kMaxPack layers -> bf16 [N][KH][KW][C]

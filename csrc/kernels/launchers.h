@@ -309,7 +309,11 @@ struct AdamArgs {
   int* app_cursor;
   int app_n;
 };
-hipError_t adam_flat(const AdamArgs& a, hipStream_t s);
+struct ConvReduceMulti;
+// red (optional): conv layers' deferred weight-gradient reductions whose dW / db slots lie in
+// grads (16-B aligned ranges); their elements are summed from the slabs and updated by blocks of
+// this launch (the BC step's conv_reduce_multi folded into Adam: bitwise the two launches)
+hipError_t adam_flat(const AdamArgs& a, hipStream_t s, const ConvReduceMulti* red = nullptr);
 
 // ---- rl.hip: GAE scan over [T, N]
 hipError_t gae_launch(const float* rew, const float* val, const float* starts, const float* last_val, const float* dones,

@@ -502,6 +502,10 @@ class _DeviceEpochRunner:
     # the minibatch gather inside the fused step's weight-packing launch (False: its own launch;
     # test hook / A/B, bitwise the same)
     fuse_gather = True
+    # the conv weight-gradient reductions inside the Adam launch (False: conv_reduce_multi's own
+    # launch; test hook / A/B, bitwise the same). Not under data parallelism: the all-reduce runs
+    # between them and Adam.
+    fuse_reduce = True
 
     def __init__(self, trainer: "_BCBase", loader, graphed):
         self.trainer, self.loader, self.graphed = trainer, loader, graphed
@@ -619,10 +623,12 @@ class _DeviceEpochRunner:
             opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor))
             return
         if self._fold:
-            # the gather rides on the weight-packing launch, the metrics append on Adam's: 13 launches
-            # per step (same arithmetic)
-            self._f(bufs[0], bufs[1], gather=gather)
-            opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor))
+            # the gather rides on the weight-packing launch, the conv weight-gradient reductions and
+            # the metrics append on Adam's: 12 launches per step (same arithmetic)
+            fold = self.fuse_reduce and self._f.reduce_foldable
+            self._f(bufs[0], bufs[1], gather=gather, defer_reduce=fold)
+            opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor),
+                     reduce=self._f.pending_reduce if fold else None)
             return
         C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs)
         self._f(bufs[0], bufs[1])

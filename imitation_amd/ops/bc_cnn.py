@@ -109,12 +109,15 @@ class FusedCnnBCStep:
             return None
         return FusedCnnBCStep(policy, optimizer, ent_weight, l2_weight)
 
-    def __call__(self, obs: th.Tensor, acts: th.Tensor, after_fc=None, gather=None) -> th.Tensor:
+    def __call__(self, obs: th.Tensor, acts: th.Tensor, after_fc=None, gather=None, defer_reduce: bool = False) -> th.Tensor:
         """``after_fc``: called (no arguments) once the FC layer's gradients are in the bucket and
         before the conv backward -- the data-parallel epoch starts the FC bucket's all-reduce there,
         on a side stream, so it overlaps the conv backward. ``gather``: ``(srcs, perm, cursor, n,
         [obs, acts], step_counter)`` of the minibatch's ``gather_rows_cursor``, run inside the
-        weight-packing launch (one dispatch fewer per step); ``obs`` / ``acts`` are its outputs."""
+        weight-packing launch (one dispatch fewer per step); ``obs`` / ``acts`` are its outputs.
+        ``defer_reduce``: the conv weight-gradient reductions are not launched; their arguments are
+        left in ``self.pending_reduce`` for the optimizer step to run them in its own launch
+        (``FusedAdam.step(reduce=...)``) -- only when :attr:`reduce_foldable`."""
         if gather is not None and not (obs.is_contiguous() and acts.is_contiguous()):
             raise ValueError("the fused gather writes obs / acts in place: they must be contiguous")
         C = self.C
@@ -161,8 +164,18 @@ class FusedCnnBCStep:
                 for k, v in zip(red, (inp, dz, kh, kw, st, 0, slab, self.g_conv[i][0], self.g_conv[i][1])):
                     red[k].append(v)
                 dz = dz_next
-            C.conv_reduce_multi(*red.values())
+            if defer_reduce:
+                self.pending_reduce = tuple(red.values())
+            else:
+                C.conv_reduce_multi(*red.values())
         return self.metrics
+
+    @property
+    def reduce_foldable(self) -> bool:
+        """Whether every conv layer's dW / db slot is a whole number of 16-B quads of the flat
+        gradient buffer (the fused Adam launch's column blocks own exactly those quads)."""
+        base = self.optimizer._flat[0]["grad"].data_ptr()
+        return all((t.data_ptr() - base) % 16 == 0 and t.numel() % 4 == 0 for pair in self.g_conv for t in pair)
 
 
     def _pairs(self, x: th.Tensor, hs: List[th.Tensor]) -> List[bool]:

@@ -153,11 +153,13 @@ class FusedAdam(th.optim.Optimizer):
         return next(f for f in self._flat if f["n"])["step"]
 
     @th.no_grad()
-    def step(self, closure=None, step_incremented: bool = False, append=None):
+    def step(self, closure=None, step_incremented: bool = False, append=None, reduce=None):
         """``step_incremented``: the step counter was already advanced for this step (by the
         caller's own launch). ``append``: ``(src, all, cursor)`` -- after the update, block 0 of
         the Adam launch copies ``src`` into row ``*cursor`` of ``all`` and advances the cursor.
-        Both need :meth:`graph_epoch_step_ok`."""
+        ``reduce``: ``conv_reduce_multi``'s nine argument lists -- those conv weight-gradient
+        reductions run inside the Adam launch, their gradient slots summed from the slabs before
+        their update (bitwise the two launches). All three need :meth:`graph_epoch_step_ok`."""
         loss = None
         if closure is not None:
             with th.enable_grad():
@@ -180,10 +182,10 @@ class FusedAdam(th.optim.Optimizer):
                 ops.native().adam_flat(f["flat"], f["grad"], f["m"], f["v"], f["step"], float(group["lr"]), float(b1),
                                        float(b2), float(group["eps"]), float(group["weight_decay"]),
                                        bool(group["decoupled_weight_decay"]), bool(group["maximize"]), True,
-                                       f["cnt"] if small else None, app[0], app[1], app[2])
+                                       f["cnt"] if small else None, app[0], app[1], app[2], reduce)
             else:
-                if step_incremented or append is not None:
-                    raise ValueError("step_incremented / append need the kernel path (graph_epoch_step_ok)")
+                if step_incremented or append is not None or reduce is not None:
+                    raise ValueError("step_incremented / append / reduce need the kernel path (graph_epoch_step_ok)")
                 f["step"].add_(1.0)
                 self._step_reference(group, f)
         return loss

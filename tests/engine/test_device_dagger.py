@@ -210,8 +210,9 @@ def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batc
     minibatches per HIP-graph replay (algorithms/bc.py ``_DeviceEpochRunner``, graph sizes kmax then
     powers of two below it): the same batches, kernels and order as the per-minibatch graphed loop,
     so the parameters, Adam state and every logged metric are bitwise equal; the epoch-end
-    callbacks and the n_batches cut-off match. ``fuse``: the minibatch gather inside the weight-
-    packing launch (the default) or a launch of its own."""
+    callbacks and the n_batches cut-off match. ``fuse``: the epoch graphs' minibatch gather inside
+    the weight-packing launch and the conv weight-gradient reductions inside the Adam launch (the
+    defaults), or each a launch of its own."""
     from imitation_amd.algorithms import bc
     from imitation_amd.engine.dagger import DeviceDemoAggregate, DeviceTransitionsLoader
     from imitation_amd.rl.policies import ActorCriticCnnPolicy
@@ -226,6 +227,7 @@ def test_bc_epoch_graph_matches_per_minibatch_path(monkeypatch, n_epochs, n_batc
     runs = []
     monkeypatch.setenv("IMITATION_AMD_BC_GRAPH_K", kmax)
     monkeypatch.setattr(bc._DeviceEpochRunner, "fuse_gather", fuse)
+    monkeypatch.setattr(bc._DeviceEpochRunner, "fuse_reduce", fuse)
     for mode in ("0", "1"):
         monkeypatch.setenv("IMITATION_AMD_BC_EPOCH_GRAPH", mode)
         th.manual_seed(11)

@@ -195,3 +195,53 @@ def test_backward_into_buckets_equals_backward():
     for r, p in zip(ref, mods.parameters()):
         th.testing.assert_close(p.grad, r)
     assert float(opt.flat_grads[0][sum(p.numel() for p in net.parameters()):].abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_grad", [True, False])
+def test_adam_flat_with_folded_conv_reductions_is_bitwise_the_two_launches(zero_grad):
+    """adam_flat(reduce=...) (csrc/kernels/optim.hip: the conv layers' slab columns summed and
+    updated by blocks of the Adam launch; the other quads by the elementwise blocks) == the
+    conv_reduce_multi launch then adam_flat: parameters, moments and gradient slots bitwise."""
+    from imitation_amd import ops
+
+    C = ops.native()
+    g = th.Generator().manual_seed(3)
+    # NatureCNN conv2 / conv3 at batch 8, their slots inside a flat buffer with other parameters
+    layers = [(8, 32, 64, 4, 2, 20), (8, 64, 64, 3, 1, 9)]
+    args = {k: [] for k in ("x", "dy", "kh", "kw", "s", "p", "slab")}
+    sizes = []
+    for B, Cin, N, KH, S, H in layers:
+        OH = (H - KH) // S + 1
+        x = th.relu(th.randn(B, H, H, Cin, generator=g)).to(th.bfloat16).cuda()
+        y = th.randn(B, OH, OH, N, generator=g).to(th.bfloat16).cuda()
+        dy = th.randn(B, OH, OH, N, generator=g).to(th.bfloat16).cuda()
+        slab = C.conv_wgrad_partials(x, dy, y, KH, KH, S, 1.0, True, 0)
+        for k, v in zip(args, (x, dy, KH, KH, S, 0, slab)):
+            args[k].append(v)
+        sizes += [N * Cin * KH * KH, N]
+    offs, o = [], 64  # a leading block of other parameters
+    for n in sizes:
+        offs.append(o)
+        o += n
+    n_all = o + 1000
+    p0 = th.randn(n_all, generator=g).cuda()
+    g0 = th.randn(n_all, generator=g).cuda()
+    m0 = th.randn(n_all, generator=g).cuda() * 0.1
+    v0 = th.rand(n_all, generator=g).cuda() * 0.1
+    step = th.full((1,), 3.0, device="cuda")
+    runs = []
+    for fold in (False, True):
+        p, gr, m, v = p0.clone(), g0.clone(), m0.clone(), v0.clone()
+        dws = [gr[offs[2 * i]:offs[2 * i] + sizes[2 * i]] for i in range(len(layers))]
+        dbs = [gr[offs[2 * i + 1]:offs[2 * i + 1] + sizes[2 * i + 1]] for i in range(len(layers))]
+        red = tuple(args.values()) + (dws, dbs)
+        if not fold:
+            C.conv_reduce_multi(*red)
+        C.adam_flat(p, gr, m, v, step, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, False, zero_grad, None, None, None, None,
+                    red if fold else None)
+        th.cuda.synchronize()
+        runs.append((p, gr, m, v))
+    for a, b in zip(*runs):
+        assert th.equal(a, b)
+    assert not th.equal(runs[0][0], p0)

@@ -1,5 +1,6 @@
 """BC minibatch steps only (NatureCNN ActorCriticCnnPolicy, B=32, graphed), for a kernel trace.
-``--sep-gather``: the minibatch gather as a launch of its own (A/B of the fused gather)."""
+``--sep-gather`` / ``--sep-reduce``: the minibatch gather / the conv weight-gradient reductions as a
+launch of their own (A/B of the folded launches)."""
 import os
 import sys
 import time
@@ -19,6 +20,8 @@ def main():
 
     if "--sep-gather" in sys.argv:
         bc._DeviceEpochRunner.fuse_gather = False
+    if "--sep-reduce" in sys.argv:
+        bc._DeviceEpochRunner.fuse_reduce = False
     obs_space, act_space = native_spaces("PongNoFrameskip-v4")
     pol = ActorCriticCnnPolicy(obs_space, act_space, lambda _: 1e-3).cuda()
     agg = DeviceDemoAggregate("cuda")
@@ -32,7 +35,7 @@ def main():
     t0 = time.perf_counter()
     bct.train(**kw)
     th.cuda.synchronize()
-    tag = " (separate gather)" if "--sep-gather" in sys.argv else ""
+    tag = "".join(f" ({a[2:]})" for a in sys.argv[1:] if a.startswith("--sep"))
     print(f"BC step B=32{tag}: {1e3 * (time.perf_counter() - t0) / 100:.3f} ms/batch", flush=True)
 
 
