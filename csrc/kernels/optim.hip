@@ -15,17 +15,21 @@
 namespace ia {
 namespace {
 
+// FMA contraction off, the fused multiply-adds spelled out: the float4 path, the scalar tail and the
+// folded-reduction blocks (one element per thread) then compute bitwise the same update (with
+// contraction left to the compiler, the packed float4 code formed other FMAs than the scalar code).
 __device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, const AdamArgs& a, float step_size,
                                          float bc2_sqrt) {
+#pragma clang fp contract(off)
   float gr = a.maximize ? -g : g;
   if (a.weight_decay != 0.f) {
     if (a.decoupled) p *= 1.f - a.lr * a.weight_decay;
-    else gr += a.weight_decay * p;
+    else gr = __builtin_fmaf(a.weight_decay, p, gr);
   }
-  m += (1.f - a.beta1) * (gr - m);
-  v = v * a.beta2 + (1.f - a.beta2) * gr * gr;
+  m = __builtin_fmaf(1.f - a.beta1, gr - m, m);
+  v = __builtin_fmaf(v, a.beta2, ((1.f - a.beta2) * gr) * gr);
   const float denom = sqrtf(v) / bc2_sqrt + a.eps;
-  p -= step_size * (m / denom);
+  p = __builtin_fmaf(-step_size, m / denom, p);
   if (a.zero_grad) g = 0.f;
 }
 
