@@ -51,7 +51,7 @@ torch::Tensor pad_k(const torch::Tensor& w, int Kp) {
 
 // x NHWC, wb bf16 [N][KH][KW][C] -> y bf16 [B, OH, OW, N]
 torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor wb, c10::optional<torch::Tensor> bias, int64_t stride,
-                       double in_scale, bool relu, int64_t pad) {
+                       double in_scale, bool relu, int64_t pad, bool splitk) {
   IA_CHECK_CUDA(x);
   IA_CHECK_CONTIG(x);
   IA_CHECK_CUDA(wb);
@@ -67,6 +67,11 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor wb, c10::optional<torch::T
     b = bias->data_ptr<float>();
   }
   auto y = torch::empty({g.B, g.OH, g.OW, g.N}, x.options().dtype(torch::kBFloat16));
+  if (splitk && ia::conv_forward_sk_ok(g)) {  // (else the default form)
+    IA_HIP_CHECK3(ia::conv_forward_sk(in_kind(x), x.data_ptr(), wk.data_ptr(), b, y.data_ptr(), g, (float)in_scale,
+                                      relu ? 1 : 0, ia_stream()));
+    return y;
+  }
   IA_HIP_CHECK3(ia::conv_forward(in_kind(x), x.data_ptr(), wk.data_ptr(), b, y.data_ptr(), g, (float)in_scale, relu ? 1 : 0,
                                  ia_stream()));
   return y;
@@ -480,7 +485,8 @@ void register_conv(py::module& m) {
         py::arg("w_e"), py::arg("b_e"), py::arg("out_e"), py::arg("rec_out_e"), py::arg("h_l"), py::arg("w_l"), py::arg("b_l"),
         py::arg("seed"), py::arg("counter"), py::arg("out_l"), py::arg("beta"), py::arg("exec_out"));
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv + bias + ReLU (bf16 MFMA)", py::arg("x"), py::arg("wb"),
-        py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0);
+        py::arg("bias"), py::arg("stride"), py::arg("in_scale") = 1.0, py::arg("relu") = true, py::arg("pad") = 0,
+        py::arg("splitk") = false);
   m.def("conv_fwd_pair", &conv_fwd_pair, "two same-shape convs (expert + learner) in one launch");
   m.def("cnn_fc_pair", &cnn_fc_pair, "two same-shape cnn_fc layers in one launch");
   m.def("conv_pack_weights", &conv_pack_weights, "fp32 conv weights -> bf16 GEMM layouts (+ a minibatch gather), one launch",

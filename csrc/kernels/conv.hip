@@ -208,6 +208,71 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const TIn* __restrict__ X
   conv_fwd_tile<TIn, NT, PADDED, RT>(X, Wb, bias, Y, g, in_scale, relu, blockIdx.x, blockIdx.y);
 }
 
+// Split-K forward for BC-size batches: one 16 x 16 output tile per block of KS waves, wave w taking
+// k-steps [w * per, (w + 1) * per) with all of its operand loads issued at once, the KS partial tiles
+// summed through LDS in wave order. conv_fwd_tile's waves walk the whole K in rounds of 8 k-steps: at
+// batch 32 its few hundred waves each wait on 2-3 dependent load rounds. Different summation order from
+// conv_fwd_tile (not bitwise with it); used where the caller asks for it (the fused BC step).
+constexpr int kSkMaxSteps = 8;
+template <typename TIn, int KS>
+__global__ __launch_bounds__(64 * KS) void conv_fwd_sk_kernel(const TIn* __restrict__ X, const bf16* __restrict__ Wb,
+                                                              const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                              ConvGeo g, float in_scale, int relu) {
+  __shared__ f32x4 part[KS][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int OHW = g.OH * g.OW, M = g.B * OHW;
+  const int m0 = blockIdx.x * 16, n0 = blockIdx.y * 16;
+  const int K = g.Kp, steps = K / 32, per = (steps + KS - 1) / KS;
+  const int s0 = w * per, s1 = min(steps, s0 + per);
+  const int r = l & 15, kq = (l >> 4) * 8;
+  const int m = m0 + r;
+  const bool mv = m < M;
+  const int mm = mv ? m : M - 1;
+  const int b = mm / OHW, pix = mm - b * OHW, oh = pix / g.OW, ow = pix - oh * g.OW;
+  const TIn* xb = X + ((size_t)(b * g.H + oh * g.S) * g.W + (size_t)ow * g.S) * g.C;
+  const int rowlen = g.KW * g.C;
+  const size_t xrow = (size_t)g.W * g.C;
+  const bf16* wr = Wb + (size_t)(n0 + r) * K + kq;
+  bf16x8 av[kSkMaxSteps], bv[kSkMaxSteps];
+#pragma unroll
+  for (int u = 0; u < kSkMaxSteps; ++u) {  // every k-step's operands in flight at once
+    const int st = s0 + u;
+    if (st < s1) {  // (wave-uniform)
+      const int k = st * 32 + kq, kh = k / rowlen, off = k - kh * rowlen;
+      av[u] = load8(xb + kh * xrow + off, in_scale);
+      if (!mv) av[u] = zero8();
+      bv[u] = *reinterpret_cast<const bf16x8*>(wr + st * 32);
+    }
+  }
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int u = 0; u < kSkMaxSteps; ++u)
+    if (s0 + u < s1) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u], bv[u], acc, 0, 0, 0);
+  part[w][l] = acc;
+  __syncthreads();
+  if (w != 0) return;
+  f32x4 sum = part[0][l];
+#pragma unroll
+  for (int v = 1; v < KS; ++v) {
+    const f32x4 x = part[v][l];
+    sum[0] += x[0];
+    sum[1] += x[1];
+    sum[2] += x[2];
+    sum[3] += x[3];
+  }
+  const int n = n0 + (l & 15);
+  const float bb = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + 4 * (l >> 4) + i;
+    if (row < M) {
+      float v = sum[i] + bb;
+      if (relu) v = fmaxf(v, 0.f);
+      Y[(size_t)row * g.N + n] = (bf16)v;
+    }
+  }
+}
+
 // Two same-shape convolutions in one launch (blockIdx.z = which): the DAgger collector's
 // expert and learner CNNs step the same frames, so each layer of both is one small-batch
 // split-N grid of twice the blocks instead of two latency-bound launches.
@@ -1070,6 +1135,35 @@ hipError_t conv_forward(int in_kind, const void* X, const void* Wb, const float*
     case 2: return launch_fwd(static_cast<const uint8_t*>(X), w, bias, y, g, in_scale, relu, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+bool conv_forward_sk_ok(const ConvGeo& g) {
+  const int steps = g.Kp / 32;
+  return conv_geo_ok(g) && g.P == 0 && g.Kp == g.KH * g.KW * g.C && g.Kp % 32 == 0 && g.N % 16 == 0 && steps >= 2 &&
+         steps <= 4 * kSkMaxSteps;
+}
+
+hipError_t conv_forward_sk(int in_kind, const void* X, const void* Wb, const float* bias, void* Y, const ConvGeo& g,
+                           float in_scale, int relu, hipStream_t s) {
+  if (!conv_forward_sk_ok(g)) return hipErrorInvalidValue;
+  const int M = g.B * g.OH * g.OW, steps = g.Kp / 32;
+  const dim3 grid((M + 15) / 16, g.N / 16);
+  const bf16* w = static_cast<const bf16*>(Wb);
+  bf16* y = static_cast<bf16*>(Y);
+  // 2 waves per tile up to 16 k-steps (<= 8 each), else 4
+#define IA_SK(T, KS) \
+  hipLaunchKernelGGL((conv_fwd_sk_kernel<T, KS>), grid, dim3(64 * KS), 0, s, static_cast<const T*>(X), w, bias, y, g, in_scale, relu)
+#define IA_SK_K(T) \
+  if (steps <= 8) IA_SK(T, 2); else IA_SK(T, 4)
+  switch (in_kind) {
+    case 0: IA_SK_K(float); break;
+    case 1: IA_SK_K(bf16); break;
+    case 2: IA_SK_K(uint8_t); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef IA_SK_K
+#undef IA_SK
+  return hipGetLastError();
 }
 
 hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y, float* slab, float* dW, float* db,

@@ -454,6 +454,11 @@ hipError_t conv_reduce_multi(const ConvReduceMulti& r, hipStream_t s);
 // in_kind: 0 fp32, 1 bf16, 2 uint8 input; weights bf16 [N][KH][KW][C]; Y bf16 [B*OH*OW][N]
 hipError_t conv_forward(int in_kind, const void* X, const void* Wb, const float* bias, void* Y, const ConvGeo& g,
                         float in_scale, int relu, hipStream_t s);
+// split-K form (BC-size batches; other summation order than conv_forward): 16 x 16 tiles of 2 or 4
+// waves, each wave's k-steps' loads at once, LDS sum in wave order
+bool conv_forward_sk_ok(const ConvGeo& g);
+hipError_t conv_forward_sk(int in_kind, const void* X, const void* Wb, const float* bias, void* Y, const ConvGeo& g,
+                           float in_scale, int relu, hipStream_t s);
 // dW fp32 [N][KH][KW][C], db fp32 [N] (may be null); slab of conv_wgrad_slab_floats
 hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y, float* slab, float* dW, float* db,
                       const ConvGeo& g, float in_scale, int relu_out, hipStream_t s);

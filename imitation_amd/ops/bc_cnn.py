@@ -109,6 +109,10 @@ class FusedCnnBCStep:
             return None
         return FusedCnnBCStep(policy, optimizer, ent_weight, l2_weight)
 
+    # the convs' forward in the split-K form (conv_forward_sk: 16 x 16 tiles over 2-4 waves, all of a
+    # wave's loads at once); False: the default form (A/B hook)
+    splitk_fwd = True
+
     def __call__(self, obs: th.Tensor, acts: th.Tensor, after_fc=None, gather=None, defer_reduce: bool = False) -> th.Tensor:
         """``after_fc``: called (no arguments) once the FC layer's gradients are in the bucket and
         before the conv backward -- the data-parallel epoch starts the FC bucket's all-reduce there,
@@ -135,7 +139,8 @@ class FusedCnnBCStep:
             hs: List[th.Tensor] = []
             h = x
             for i, c in enumerate(convs):
-                h = C.conv_fwd(h, wbs[i], c.bias.detach(), int(c.stride[0]), 1.0 / 255.0 if i == 0 else 1.0, True, 0)
+                h = C.conv_fwd(h, wbs[i], c.bias.detach(), int(c.stride[0]), 1.0 / 255.0 if i == 0 else 1.0, True, 0,
+                               self.splitk_fwd)
                 hs.append(h)
             xf = h.reshape(B, -1)
             out = C.cnn_fc(xf, wbs[n].view(NH, -1), lin.bias.detach())

@@ -344,3 +344,32 @@ def test_conv_pack_weights_layouts_in_one_launch():
         if t:
             src = wr.permute(0, 2, 3, 1) if hwc else wr
             assert th.equal(wt.reshape(-1, w.shape[0]), src.reshape(w.shape[0], -1).t().contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,N,KH,S,H,dtype", [(32, 4, 32, 8, 4, 84, th.uint8), (32, 32, 64, 4, 2, 20, th.bfloat16),
+                                              (32, 64, 64, 3, 1, 9, th.bfloat16), (7, 64, 64, 3, 1, 9, th.bfloat16),
+                                              (5, 32, 64, 4, 2, 20, th.float32)])
+def test_conv_fwd_splitk_matches_fp32_and_the_default_form(B, C, N, KH, S, H, dtype):
+    """conv_forward_sk (split-K: 16 x 16 tiles over 2-4 waves, LDS sum in wave order) against the fp32
+    conv of the same bf16 operands, and close to the default form (other summation order only)."""
+    import torch.nn.functional as F
+
+    from imitation_amd import ops
+
+    Cn = ops.native()
+    g = th.Generator().manual_seed(B + C + KH)
+    scale = 1.0 / 255.0 if dtype == th.uint8 else 1.0
+    if dtype == th.uint8:
+        x = th.randint(0, 256, (B, H, H, C), generator=g).to(th.uint8)
+    else:
+        x = th.randn(B, H, H, C, generator=g).to(dtype)
+    w = th.randn(N, C, KH, KH, generator=g) * 0.05
+    b = th.randn(N, generator=g) * 0.1
+    wbs, _ = Cn.conv_pack_weights([w.cuda()], [False])
+    y_sk = Cn.conv_fwd(x.cuda(), wbs[0], b.cuda(), S, scale, True, 0, True).float().cpu()
+    y_df = Cn.conv_fwd(x.cuda(), wbs[0], b.cuda(), S, scale, True, 0, False).float().cpu()
+    xr = (x.float() * scale).to(th.bfloat16).float().permute(0, 3, 1, 2)
+    ref = F.relu(F.conv2d(xr, w.to(th.bfloat16).float(), b, stride=S)).permute(0, 2, 3, 1)
+    th.testing.assert_close(y_sk, ref, rtol=1e-2, atol=1e-2)
+    th.testing.assert_close(y_sk, y_df, rtol=1e-2, atol=1e-2)

@@ -1,6 +1,6 @@
 """BC minibatch steps only (NatureCNN ActorCriticCnnPolicy, B=32, graphed), for a kernel trace.
 ``--sep-gather`` / ``--sep-reduce``: the minibatch gather / the conv weight-gradient reductions as a
-launch of their own (A/B of the folded launches)."""
+launch of their own (A/B of the folded launches); ``--sep-fwd``: the default (not split-K) conv forward."""
 import os
 import sys
 import time
@@ -20,6 +20,10 @@ def main():
 
     if "--sep-gather" in sys.argv:
         bc._DeviceEpochRunner.fuse_gather = False
+    if "--sep-fwd" in sys.argv:
+        from imitation_amd.ops import bc_cnn
+
+        bc_cnn.FusedCnnBCStep.splitk_fwd = False
     if "--sep-reduce" in sys.argv:
         bc._DeviceEpochRunner.fuse_reduce = False
     obs_space, act_space = native_spaces("PongNoFrameskip-v4")

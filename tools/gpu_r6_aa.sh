@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 6 call AA: the whole GPU suite + smoke after the BC launch merges (as the driver runs them)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 1050 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/r6aa_gpu_suite.log 2>&1
+rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r6aa_smoke.log 2>&1 || exit $?
