@@ -3,7 +3,10 @@
 aggregate) with per-phase wall clocks (collect / demo save / BC) from patched methods, the
 GPU-busy share from CUDA events, and a cProfile of the timed rounds (top cumulative entries).
 
-Usage: python tools/dagger_breakdown.py [--rounds 4] [--warmup 1] [--profile]"""
+``--reference-schedule``: the reference's ``SimpleDAggerTrainer.train`` defaults instead (>= 3 episodes
+and >= 500 env steps per round, 4 BC epochs; ``bench_configs.py dagger_pong``).
+
+Usage: python tools/dagger_breakdown.py [--rounds 4] [--warmup 1] [--profile] [--reference-schedule]"""
 import argparse
 import collections
 import cProfile
@@ -23,6 +26,7 @@ def main():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--round-steps", type=int, default=2048)
     p.add_argument("--profile", action="store_true")
+    p.add_argument("--reference-schedule", action="store_true")
     args = p.parse_args()
     import torch as th
 
@@ -54,6 +58,10 @@ def main():
         timed(tr._device_collector, "collect", "device_collect")
 
     def round_():
+        if args.reference_schedule:
+            tr.train(1, rollout_round_min_episodes=3, rollout_round_min_timesteps=500,
+                     bc_train_kwargs=dict(n_epochs=tr.DEFAULT_N_EPOCHS, log_interval=10**9, progress_bar=False))
+            return
         tr.train(args.round_steps, rollout_round_min_episodes=1, rollout_round_min_timesteps=args.round_steps,
                  bc_train_kwargs=dict(n_epochs=1, log_interval=10**9, progress_bar=False))
 
