@@ -714,7 +714,9 @@ __global__ __launch_bounds__(512) void conv_wgrad_kernel(const TIn* __restrict__
 // gradient (conv_dgrad_split_body, block b -> tile b % dg_gx, phase b / dg_gx). Both read the same
 // dY / Y; neither feeds the other, so the launch's critical path is the longer of the two instead
 // of their sum plus a dispatch.
-template <int NT, int TPW, int CH, int CT, int NN>
+// RT: 16-pixel data-gradient tiles per block, one after another (LDS partials reused after a
+// barrier; the same per-tile arithmetic, so the same bits whatever RT).
+template <int NT, int TPW, int CH, int CT, int NN, int RT>
 __global__ __launch_bounds__(512) void conv_back_pair_kernel(const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                              const bf16* __restrict__ Y, float* __restrict__ slab,
                                                              ConvGeo g, int relu_out, int m_per_block, int n_wg,
@@ -726,8 +728,13 @@ __global__ __launch_bounds__(512) void conv_back_pair_kernel(const bf16* __restr
     conv_wgrad_body<bf16, NT, TPW, CH>(X, dY, Y, slab, g, 1.f, relu_out, m_per_block, b, smem);
   } else {
     const int d = b - n_wg;
-    conv_dgrad_split_body<CT, NN>(dY, Y, Wt, X, dZp, g, relu_out, relu_in, tpg, d % dg_gx, d / dg_gx,
-                                  reinterpret_cast<f32x4(*)[CT][64]>(smem));
+#pragma unroll 1
+    for (int k = 0; k < RT; ++k) {
+      // (waves 1..7 leave the body after its barrier; wave 0 after the tile's stores)
+      conv_dgrad_split_body<CT, NN>(dY, Y, Wt, X, dZp, g, relu_out, relu_in, tpg, (d % dg_gx) * RT + k, d / dg_gx,
+                                    reinterpret_cast<f32x4(*)[CT][64]>(smem));
+      if (RT > 1) __syncthreads();  // wave 0's reads of the partials before the next tile's writes
+    }
   }
 }
 
@@ -1179,6 +1186,18 @@ hipError_t conv_wgrad(int in_kind, const void* X, const void* dY, const void* Y,
   }
 }
 
+// compute units of the current device (cached; BC-size launch shapes are sized against it)
+static int cu_count() {
+  static int n = 0;
+  if (n <= 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      n = v;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
 bool conv_back_pair_ok(const ConvGeo& g) {
   if (!conv_geo_ok(g) || g.N % 32 != 0 || g.C % 16 != 0 || g.C > 64 || g.P != 0) return false;
   const int Hc = (g.H + g.S - 1) / g.S, Wc = (g.W + g.S - 1) / g.S;
@@ -1195,7 +1214,12 @@ hipError_t conv_back_pair(const void* X, const void* dY, const void* Y, float* s
   conv_wgrad_blocks(g, &nblk, &mpb);
   const int tpg = dgrad_split_tpg(g);
   const int Hc = (g.H + g.S - 1) / g.S, Wc = (g.W + g.S - 1) / g.S;
-  const int gx = (g.B * Hc * Wc + 15) / 16;
+  // The kernel's VGPR budget is the weight-gradient body's (~240: one 512-thread block per CU), so
+  // its short data-gradient blocks run ~one per CU. When the launch would need more than one round
+  // of blocks (conv2 at batch 32: 41 + 800), each data-gradient block takes 4 tiles: 41 + 200.
+  const int tiles16 = (g.B * Hc * Wc + 15) / 16;
+  const int rt = nblk + tiles16 * g.S * g.S > cu_count() ? 4 : 1;
+  const int gx = (tiles16 + rt - 1) / rt;
   const int n_dg = gx * g.S * g.S;
   constexpr int CH = 32;
   const size_t lds_wg = ((size_t)g.Kp + (size_t)g.N) * (CH + 8) * sizeof(bf16);
@@ -1210,9 +1234,15 @@ hipError_t conv_back_pair(const void* X, const void* dY, const void* Y, float* s
   bf16* dz = static_cast<bf16*>(dZp);
   const dim3 grid(nblk + n_dg), block(512);
   const int nn = g.N / 32;
-#define IA_BP(NT, TPW, CT, NN)                                                                                           \
-  hipLaunchKernelGGL((conv_back_pair_kernel<NT, TPW, CH, CT, NN>), grid, block, lds, s, x, dy, y, slab, g, relu_out, mpb, \
-                     nblk, wt, dz, relu_in, tpg, gx)
+#define IA_BP(NT, TPW, CT, NN)                                                                                                 \
+  do {                                                                                                                         \
+    if (rt == 4)                                                                                                               \
+      hipLaunchKernelGGL((conv_back_pair_kernel<NT, TPW, CH, CT, NN, 4>), grid, block, lds, s, x, dy, y, slab, g, relu_out, mpb, \
+                         nblk, wt, dz, relu_in, tpg, gx);                                                                      \
+    else                                                                                                                       \
+      hipLaunchKernelGGL((conv_back_pair_kernel<NT, TPW, CH, CT, NN, 1>), grid, block, lds, s, x, dy, y, slab, g, relu_out, mpb, \
+                         nblk, wt, dz, relu_in, tpg, gx);                                                                      \
+  } while (0)
 #define IA_BP_T(NT, CT, NN)         \
   if (tpw <= 4) IA_BP(NT, 4, CT, NN);      \
   else if (tpw <= 8) IA_BP(NT, 8, CT, NN); \
