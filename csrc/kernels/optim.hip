@@ -40,8 +40,10 @@ struct AdamRed {
   int64_t w_off[kMaxPack], b_off[kMaxPack];  // flat offsets of the dW / db slots
   int64_t lo[2 * kMaxPack], hi[2 * kMaxPack];  // the slot ranges (multiples of 4): the quads the
   int nr;                                      // elementwise blocks skip
-  int nadam;                                   // blocks [0, nadam) elementwise, then the layers'
-  int boff[kMaxPack + 1];                      // column blocks: [nadam + boff[l], nadam + boff[l + 1])
+  int ncol;                                    // blocks [0, ncol) the layers' column blocks
+  int boff[kMaxPack + 1];                      // ([boff[l], boff[l + 1]) of layer l), then the
+                                               // elementwise blocks: their chains of slab loads
+                                               // start first and overlap the elementwise part
 };
 
 template <bool RED>
@@ -56,8 +58,8 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, AdamRed rd) 
   }
   __syncthreads();
   const float t = bcs[0], bc2_sqrt = bcs[1], step_size = bcs[2];
-  if (!RED || (int)blockIdx.x < rd.nadam) {
-    const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (!RED || (int)blockIdx.x >= rd.ncol) {
+    const int64_t i4 = ((int64_t)((int)blockIdx.x - (RED ? rd.ncol : 0)) * 256 + threadIdx.x) * 4;
     bool skip = false;  // a quad of a folded layer: its column block updates it
     if constexpr (RED) {
       for (int j = 0; j < rd.nr; ++j) skip |= i4 >= rd.lo[j] && i4 < rd.hi[j];
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a, AdamRed rd) 
   } else if constexpr (RED) {
     // slab column i of layer l: conv_reduce_multi's fixed-order sum, stored to its gradient slot
     // (or 0 with zero_grad) and that element's Adam update
-    const int rb = (int)blockIdx.x - rd.nadam;
+    const int rb = (int)blockIdx.x;
     int l = 0;
     while (l + 1 < rd.r.n && rb >= rd.boff[l + 1]) ++l;  // (uniform)
     const ConvGeo& g = rd.r.g[l];
@@ -127,7 +129,6 @@ hipError_t adam_flat(const AdamArgs& a, hipStream_t s, const ConvReduceMulti* re
   const int64_t threads = (a.n + 3) / 4;
   const int nadam = (int)((threads + 255) / 256);
   AdamRed rd{};
-  rd.nadam = nadam;
   if (red == nullptr || red->n <= 0) {
     hipLaunchKernelGGL(adam_flat_kernel<false>, dim3((unsigned)nadam), dim3(256), 0, s, a, rd);
     return hipGetLastError();
@@ -155,6 +156,7 @@ hipError_t adam_flat(const AdamArgs& a, hipStream_t s, const ConvReduceMulti* re
     total += (g.N * g.Kp + g.N + 255) / 256;
   }
   rd.boff[red->n] = total;
+  rd.ncol = total;
   hipLaunchKernelGGL(adam_flat_kernel<true>, dim3((unsigned)(nadam + total)), dim3(256), 0, s, a, rd);
   return hipGetLastError();
 }

@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 6 call AL: folded conv reductions first in the Adam launch (order_new) vs after the elementwise blocks (order_old)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/ops/test_fused_adam.py \
+  tests/algorithms/test_bc.py tests/engine/test_device_dagger.py tests/parallel/test_oneshot.py > gpurun_out/r6al_tests.log 2>&1
+rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+SO=imitation_amd/_C.cpython-310-x86_64-linux-gnu.so
+cp $SO /tmp/orig.so
+for v in order_new order_old order_new order_old order_new order_old; do
+  cp ab/$v.so $SO
+  echo "== $v" >> gpurun_out/r6al_bcstep.log
+  timeout -k 10 120 python -u tools/bc_step_probe.py >> gpurun_out/r6al_bcstep.log 2>&1 || { cp /tmp/orig.so $SO; exit 1; }
+done
+cp /tmp/orig.so $SO
+cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r6al_bcprof -o bc -- python3 $R/tools/bc_step_probe.py > $R/gpurun_out/r6al_bcprof.log 2>&1
