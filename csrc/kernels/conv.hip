@@ -951,19 +951,34 @@ __device__ __forceinline__ void pack_wb_row(const ConvPackLayer& L, int n, float
     const int i = threadIdx.x + 256 * u;
     v[u] = i < K ? src[i] : 0.f;
   }
+  // (integer divisions by runtime taps / C are ~40 VALU each: skipped where the layout allows --
+  // odd taps (st == taps: the LDS index is i itself), power-of-two C (a shift))
+  const bool odd = st == taps;
 #pragma unroll
   for (int u = 0; u < kPackRowIt; ++u) {  // src [c][tap] -> t[c * st + tap]
     const int i = threadIdx.x + 256 * u;
     if (i < K) {
-      const int c = i / taps;
-      t[c * st + i - c * taps] = v[u];
+      if (odd) {
+        t[i] = v[u];
+      } else {
+        const int c = i / taps;
+        t[c * st + i - c * taps] = v[u];
+      }
     }
   }
   __syncthreads();
   bf16* dst = static_cast<bf16*>(L.wb) + (size_t)n * K;
-  for (int i = threadIdx.x; i < K; i += 256) {  // dst [tap][c], coalesced along c
-    const int p = i / C, c = i - p * C;
-    dst[i] = (bf16)t[c * st + p];
+  if ((C & (C - 1)) == 0) {
+    const int sh = __builtin_ctz(C);
+    for (int i = threadIdx.x; i < K; i += 256) {  // dst [tap][c], coalesced along c
+      const int p = i >> sh, c = i & (C - 1);
+      dst[i] = (bf16)t[c * st + p];
+    }
+  } else {
+    for (int i = threadIdx.x; i < K; i += 256) {
+      const int p = i / C, c = i - p * C;
+      dst[i] = (bf16)t[c * st + p];
+    }
   }
 }
 
@@ -971,19 +986,19 @@ __device__ __forceinline__ void pack_wt_row(const ConvPackLayer& L, int c, int n
   const int taps = L.KH * L.KW, C = L.C, N = L.N, st = pack_stride(taps), n0 = nt * 64;
   const int cnt = 64 * taps;
   float v[kPackRowIt];
+  const bool odd = st == taps;
+  int nls[kPackRowIt];
 #pragma unroll
   for (int u = 0; u < kPackRowIt; ++u) {  // 64 source rows w[n][c][0..taps)
     const int i = threadIdx.x + 256 * u;
     const int nl = i / taps, p = i - nl * taps;
+    nls[u] = nl;
     v[u] = (i < cnt && n0 + nl < N) ? L.w[((size_t)(n0 + nl) * C + c) * taps + p] : 0.f;
   }
 #pragma unroll
   for (int u = 0; u < kPackRowIt; ++u) {
     const int i = threadIdx.x + 256 * u;
-    if (i < cnt) {
-      const int nl = i / taps;
-      t[nl * st + i - nl * taps] = v[u];
-    }
+    if (i < cnt) t[odd ? i : nls[u] * st + i - nls[u] * taps] = v[u];
   }
   __syncthreads();
   bf16* dst = static_cast<bf16*>(L.wt);

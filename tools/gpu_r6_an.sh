@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 6 call AN: row-form packing without the runtime integer divisions (pack_new) vs before (pack_old)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/ops/test_conv.py \
+  tests/algorithms/test_bc.py tests/engine/test_device_dagger.py tests/parallel/test_oneshot.py > gpurun_out/r6an_tests.log 2>&1
+rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+SO=imitation_amd/_C.cpython-310-x86_64-linux-gnu.so
+cp $SO /tmp/orig.so
+for v in pack_new pack_old pack_new pack_old pack_new pack_old; do
+  cp ab/$v.so $SO
+  echo "== $v" >> gpurun_out/r6an_bcstep.log
+  timeout -k 10 120 python -u tools/bc_step_probe.py >> gpurun_out/r6an_bcstep.log 2>&1 || { cp /tmp/orig.so $SO; exit 1; }
+done
+cp /tmp/orig.so $SO
+cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r6an_bcprof -o bc -- python3 $R/tools/bc_step_probe.py > $R/gpurun_out/r6an_bcprof.log 2>&1
