@@ -627,8 +627,11 @@ class _DeviceEpochRunner:
             # the metrics append on Adam's: 12 launches per step (same arithmetic)
             fold = self.fuse_reduce and self._f.reduce_foldable
             self._f(bufs[0], bufs[1], gather=gather, defer_reduce=fold)
+            # zero_grad off: the fused step writes (not accumulates) every gradient slot Adam reads
+            # with a nonzero value -- conv, FC and head; the value net's slots, which BC never
+            # writes, stay at the zeros of the last zeroing step
             opt.step(step_incremented=True, append=(self._f.metrics, self.all, self.cursor),
-                     reduce=self._f.pending_reduce if fold else None)
+                     reduce=self._f.pending_reduce if fold else None, zero_grad=False)
             return
         C.gather_rows_cursor([self.agg.obs, self.agg.acts], self.perm, self.cursor, self.B, bufs)
         self._f(bufs[0], bufs[1])

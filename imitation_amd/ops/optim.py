@@ -153,13 +153,15 @@ class FusedAdam(th.optim.Optimizer):
         return next(f for f in self._flat if f["n"])["step"]
 
     @th.no_grad()
-    def step(self, closure=None, step_incremented: bool = False, append=None, reduce=None):
+    def step(self, closure=None, step_incremented: bool = False, append=None, reduce=None, zero_grad: bool = True):
         """``step_incremented``: the step counter was already advanced for this step (by the
         caller's own launch). ``append``: ``(src, all, cursor)`` -- after the update, block 0 of
         the Adam launch copies ``src`` into row ``*cursor`` of ``all`` and advances the cursor.
         ``reduce``: ``conv_reduce_multi``'s nine argument lists -- those conv weight-gradient
         reductions run inside the Adam launch, their gradient slots summed from the slabs before
-        their update (bitwise the two launches). All three need :meth:`graph_epoch_step_ok`."""
+        their update (bitwise the two launches). All three need :meth:`graph_epoch_step_ok`.
+        ``zero_grad=False``: the kernel leaves the gradient bucket as it is (one 4-B store per
+        parameter less) -- for callers whose next backward rewrites every slot it reads."""
         loss = None
         if closure is not None:
             with th.enable_grad():
@@ -181,7 +183,7 @@ class FusedAdam(th.optim.Optimizer):
                 app = append if append is not None else (None, None, None)
                 ops.native().adam_flat(f["flat"], f["grad"], f["m"], f["v"], f["step"], float(group["lr"]), float(b1),
                                        float(b2), float(group["eps"]), float(group["weight_decay"]),
-                                       bool(group["decoupled_weight_decay"]), bool(group["maximize"]), True,
+                                       bool(group["decoupled_weight_decay"]), bool(group["maximize"]), bool(zero_grad),
                                        f["cnt"] if small else None, app[0], app[1], app[2], reduce)
             else:
                 if step_incremented or append is not None or reduce is not None:
